@@ -1,0 +1,225 @@
+/*
+ * pinot_amd.h — C-ABI of the MI355X-native segment query hot path.
+ *
+ * This is the drop-in boundary a Pinot server binds (Java FFM / JNI).
+ * Everything above it (QueryContext, PredicateEvaluator, Dictionary, DataTable building,
+ * broker reduce) stays in the host language; everything below it runs as hand-written HIP
+ * on gfx950. Plain pointers and sizes only — no torch, no C++ types.
+ *
+ * Reference interfaces replaced (all paths relative to /root/reference):
+ *
+ *  pa_segment_add_sv_dict_column
+ *      replaces the device-side role of
+ *      pinot-segment-local/.../readers/forward/FixedBitSVForwardIndexReaderV2.java:38 (ctor over the
+ *      PinotDataBuffer) and io/reader/impl/FixedBitIntReader.java:51 (getReader): the caller passes the
+ *      forward-index bytes exactly as written by FixedBitSVForwardIndexWriter (big-endian, MSB-first,
+ *      io/util/PinotDataBitSet.java:80 layout) and the dictionary values
+ *      (segment-spi/.../index/reader/Dictionary.java getLongValue/getDoubleValue).
+ *  pa_segment_add_mv_dict_column
+ *      replaces readers/forward/FixedBitMVForwardIndexReader.java:56 (chunk offsets + row-start bitmap
+ *      + bit-packed values, same bytes).
+ *  pa_segment_add_raw_column
+ *      replaces the raw (no-dictionary) fixed-width forward index readers
+ *      (readers/forward/FixedByteChunkSVForwardIndexReader.java) — values are passed decoded.
+ *  pa_query_* (spec, bind, execute, fetch)
+ *      replaces, for one segment set on one GPU, the per-segment operator chain
+ *        pinot-core/.../operator/filter/ScanBasedFilterOperator.java + dociditerators/SVScanDocIdIterator.java:76
+ *        operator/filter/BitmapBasedFilterOperator.java, AndFilterOperator.java, OrFilterOperator.java,
+ *        NotFilterOperator.java (the filter tree, evaluated in dictId space from
+ *        operator/filter/predicate/{Range,In,Equals,NotIn,NotEquals}PredicateEvaluatorFactory.java ranges / matching-dictId sets),
+ *        operator/query/AggregationOperator.java and operator/query/GroupByOperator.java:84
+ *        (query/aggregation/groupby/DefaultGroupByExecutor.java:140 process(),
+ *         DictionaryBasedGroupKeyGenerator.java:233 raw-key generation,
+ *         aggregation/function/{Count,Sum,Min,Max,DistinctCountHLL}AggregationFunction.java
+ *         aggregateGroupBySV / aggregate),
+ *      and the in-server merge of those partial results
+ *        operator/combine/AggregationCombineOperator.java, GroupByCombineOperator.java:110
+ *      (segments of one GPU accumulate into ONE table-wide key space, so no per-segment merge is needed).
+ *  pa_query_accumulators / layout
+ *      exposes the device accumulators so the cross-GPU merge of partial aggregates runs as an RCCL
+ *      reduce (SUM for COUNT/SUM, MIN, MAX, MAX for HLL registers) — the multi-GPU analogue of
+ *      GroupByCombineOperator's IndexedTable upsert/merge.
+ *
+ * Error convention: functions returning int return 0 on success and a negative PA_E* code on error;
+ * pa_last_error() returns a thread-local message. Functions returning pointers return NULL on error.
+ */
+#ifndef PINOT_AMD_H_
+#define PINOT_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PA_ABI_VERSION 1
+
+/* limits of one query shape */
+#define PA_MAX_LEAVES 16
+#define PA_MAX_OPS 48
+#define PA_MAX_GROUP_BY 8
+#define PA_MAX_AGGS 16
+
+/* error codes */
+#define PA_OK 0
+#define PA_EINVAL (-1)
+#define PA_EHIP (-2)
+#define PA_ENOMEM (-3)
+#define PA_EUNSUPPORTED (-4)
+
+/* stored value types: org.apache.pinot.spi.data.FieldSpec.DataType#getStoredType */
+#define PA_INT 0
+#define PA_LONG 1
+#define PA_FLOAT 2
+#define PA_DOUBLE 3
+#define PA_STRING 4
+#define PA_BYTES 5
+
+/* filter leaf kinds (how a predicate is evaluated on the GPU; resolution into dictId space happens in
+ * the host's PredicateEvaluator exactly as in the reference) */
+#define PA_LEAF_DICT_RANGE 0 /* lo <= dictId < hi   (SortedDictionaryBasedRangePredicateEvaluator, EQ)   */
+#define PA_LEAF_DICT_SET 1   /* bit dictId of lut set (IN / NOT IN / unsorted range matching-dictId set)  */
+#define PA_LEAF_RAW_RANGE 2  /* ilo<=v<=ihi (INT/LONG) or dlo<=v<=dhi (FLOAT/DOUBLE) on a raw column       */
+#define PA_LEAF_MV_DICT_RANGE 3 /* MV column: any value with lo <= dictId < hi (MVScanDocIdIterator)      */
+#define PA_LEAF_MV_DICT_SET 4   /* MV column: any value whose bit is set in lut                            */
+
+/* postfix filter program opcodes; PA_OP_LEAF carries the leaf index in bits 8..15 */
+#define PA_OP_LEAF 0
+#define PA_OP_AND 1
+#define PA_OP_OR 2
+#define PA_OP_NOT 3
+
+/* aggregation types (AggregationFunctionType) */
+#define PA_AGG_COUNT 0
+#define PA_AGG_SUM 1
+#define PA_AGG_MIN 2
+#define PA_AGG_MAX 3
+#define PA_AGG_DISTINCTCOUNTHLL 4
+
+/* ---------------------------------------------------------------- device / errors */
+int pa_abi_version(void);
+int pa_device_count(void);
+int pa_set_device(int device);
+const char* pa_last_error(void);
+
+/* ---------------------------------------------------------------- segments (HBM resident) */
+typedef struct pa_segment pa_segment;
+
+pa_segment* pa_segment_create(int32_t num_docs);
+
+/* fwd_index: FixedBitSVForwardIndexWriter bytes, length must equal ceil(num_docs*num_bits/8)
+ * (FixedBitIntReaderWriter.java:31 precondition). dict_values: int64[cardinality] for INT/LONG,
+ * double[cardinality] for FLOAT/DOUBLE, NULL for STRING/BYTES. dict_hashes (nullable): MurmurHash
+ * (stream-lib 2.9.8 MurmurHash.hash(Object)) of every dictionary value, required only to run
+ * DISTINCTCOUNTHLL on STRING/BYTES dictionaries (numeric ones are hashed on the GPU). */
+int pa_segment_add_sv_dict_column(pa_segment* seg, int32_t column_id, const uint8_t* fwd_index,
+                                  uint64_t fwd_index_bytes, int32_t num_bits_per_value,
+                                  int32_t cardinality, int32_t value_type, const void* dict_values,
+                                  const int32_t* dict_hashes);
+
+/* fwd_index: FixedBitMVForwardIndexReader layout (chunk offsets | row-start bitmap | bit-packed values). */
+int pa_segment_add_mv_dict_column(pa_segment* seg, int32_t column_id, const uint8_t* fwd_index,
+                                  uint64_t fwd_index_bytes, int32_t num_bits_per_value,
+                                  int32_t cardinality, int64_t total_num_values, int32_t value_type,
+                                  const void* dict_values, const int32_t* dict_hashes);
+
+/* values: int32[num_docs] (INT), int64 (LONG), float (FLOAT), double (DOUBLE). */
+int pa_segment_add_raw_column(pa_segment* seg, int32_t column_id, int32_t value_type,
+                              const void* values);
+
+int32_t pa_segment_num_docs(const pa_segment* seg);
+uint64_t pa_segment_device_bytes(const pa_segment* seg);
+void pa_segment_destroy(pa_segment* seg);
+
+/* ---------------------------------------------------------------- query shape */
+typedef struct {
+  int32_t column_id;
+  int32_t kind; /* PA_LEAF_* */
+} pa_leaf_spec;
+
+typedef struct {
+  int32_t type;      /* PA_AGG_* */
+  int32_t column_id; /* ignored for COUNT */
+  int32_t log2m;     /* DISTINCTCOUNTHLL only (CommonConstants.Helix.DEFAULT_HYPERLOGLOG_LOG2M = 8) */
+  int32_t reserved;
+} pa_agg_spec;
+
+typedef struct {
+  int32_t num_leaves;
+  pa_leaf_spec leaves[PA_MAX_LEAVES];
+  int32_t num_ops; /* 0 = match all (MatchAllFilterOperator) */
+  int32_t ops[PA_MAX_OPS];
+  int32_t num_group_by; /* 0 = aggregation-only query */
+  int32_t group_by_columns[PA_MAX_GROUP_BY];
+  int64_t group_by_cardinality[PA_MAX_GROUP_BY]; /* size of the table-wide key space per column */
+  int32_t num_aggs;
+  pa_agg_spec aggs[PA_MAX_AGGS];
+  int32_t flags; /* PA_QF_* */
+  int32_t reserved;
+} pa_query_spec;
+
+#define PA_QF_STAGE_ALL 1  /* stage post-filter columns through LDS even when a filter exists */
+#define PA_QF_FORCE_GLOBAL 2 /* force global-memory accumulators (testing the fallback) */
+
+/* per-(segment, leaf) parameters in that segment's dictId space */
+typedef struct {
+  int32_t lo, hi;       /* DICT_RANGE: lo <= dictId < hi */
+  int32_t negate;       /* result XOR negate */
+  int32_t reserved;
+  const uint32_t* lut;  /* DICT_SET: host bitmap, ceil(cardinality/32) words, bit (id&31) of word id>>5 */
+  int64_t ilo, ihi;     /* RAW_RANGE on INT/LONG, inclusive */
+  double dlo, dhi;      /* RAW_RANGE on FLOAT/DOUBLE, inclusive */
+} pa_leaf_params;
+
+typedef struct pa_query pa_query;
+
+pa_query* pa_query_create(const pa_query_spec* spec, int32_t num_segments);
+
+/* group_remaps[j]: host int32[segment cardinality of group_by_columns[j]] mapping the segment's dictId
+ * to the table-wide key id of that column (NULL = identity). */
+int pa_query_bind_segment(pa_query* q, int32_t index, const pa_segment* seg,
+                          const pa_leaf_params* leaf_params, const int32_t* const* group_remaps);
+
+/* Uploads per-segment parameters, builds the tile schedule and HLL lookup tables, sizes the
+ * accumulators. Must be called once after every segment is bound. */
+int pa_query_prepare(pa_query* q);
+
+/* Number of keys of the table-wide key space (1 for aggregation-only queries). */
+int64_t pa_query_num_keys(const pa_query* q);
+
+/* Zeroes the accumulators and runs the fused scan (filter + group-key + aggregate) over every bound
+ * segment on `stream` (hipStream_t, NULL = default stream). Asynchronous. */
+int pa_query_execute(pa_query* q, void* stream);
+
+/* Accumulator sections, for the cross-GPU RCCL reduce. section kinds: */
+#define PA_ACC_COUNT_U64 0 /* reduce SUM */
+#define PA_ACC_SUM_I64 1   /* reduce SUM */
+#define PA_ACC_SUM_F64 2   /* reduce SUM */
+#define PA_ACC_MIN_I64 3   /* reduce MIN (ordered encoding for floating values) */
+#define PA_ACC_MAX_I64 4   /* reduce MAX */
+#define PA_ACC_HLL_U32 5   /* reduce MAX */
+int32_t pa_query_num_sections(const pa_query* q);
+/* returns device pointer, writes kind and element count */
+void* pa_query_section(const pa_query* q, int32_t section, int32_t* kind, int64_t* num_elements);
+
+/* Compacts the non-empty keys (count > 0) in ascending key order and copies them to the host.
+ * out_keys: int64[capacity]; out_counts: int64[capacity]; out_aggs[i]: double[capacity] for
+ * COUNT/SUM/MIN/MAX (the reference's intermediate type), uint8[capacity << log2m] for HLL registers.
+ * For aggregation-only queries key 0 is always returned (count may be 0).
+ * Returns the number of groups (may exceed capacity: then only `capacity` were written), <0 on error.
+ * Synchronises `stream`. */
+int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out_keys,
+                       int64_t* out_counts, void* const* out_aggs);
+
+/* Kernel statistics of the last execute (for roofline accounting): bytes of forward index staged
+ * (always-read columns), number of docs scanned. */
+int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs,
+                   uint64_t* num_tiles);
+
+void pa_query_destroy(pa_query* q);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PINOT_AMD_H_ */

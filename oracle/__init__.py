@@ -1,0 +1,419 @@
+"""CPU ORACLE — TEST INFRASTRUCTURE ONLY.
+
+Imported solely by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker; the product
+path (pinot_amd) never imports it. Parity is pinned against the reference's own golden results
+(tests/golden/sv_queries.json, transcribed with file:line from pinot-core/src/test/java/org/apache/pinot/queries)
+on the reference's own test input (tests/golden/test_data_sv.npz, converted from
+pinot-core/src/test/resources/data/test_data-sv.avro by tests/golden/make_golden.py).
+
+The per-doc scan lives in pinot_oracle.c (scalar C restatement, see its header for the reference file:line map);
+this module restates the dictionary-based predicate evaluators (value -> set of matching dictIds), drives the
+per-segment scan, and merges segment results by group-key VALUE in segment order
+(GroupByCombineOperator / IndexedTable.upsert semantics: SUM +, MIN min, MAX max, COUNT +, HLL register max).
+"""
+import ctypes
+import os
+import subprocess
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(HERE, "_build")
+LIB = os.path.join(BUILD, "liboracle.so")
+SRC = os.path.join(HERE, "pinot_oracle.c")
+
+_lock = threading.Lock()
+_lib = None
+
+
+def build(force=False):
+    os.makedirs(BUILD, exist_ok=True)
+    if force or not os.path.exists(LIB) or os.path.getmtime(SRC) > os.path.getmtime(LIB):
+        subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-std=c11", "-o", LIB + ".tmp", SRC, "-lm"], check=True)
+        os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+class OCol(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("num_bits", ctypes.c_int32), ("cardinality", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("fwd", ctypes.c_void_p), ("raw", ctypes.c_void_p),
+                ("dict_f64", ctypes.c_void_p), ("dict_hash", ctypes.c_void_p)]
+
+
+class OLeaf(ctypes.Structure):
+    _fields_ = [("col", ctypes.c_int32), ("kind", ctypes.c_int32), ("match", ctypes.c_void_p),
+                ("dlo", ctypes.c_double), ("dhi", ctypes.c_double), ("ilo", ctypes.c_int64), ("ihi", ctypes.c_int64),
+                ("lo_unbounded", ctypes.c_int32), ("hi_unbounded", ctypes.c_int32),
+                ("lo_incl", ctypes.c_int32), ("hi_incl", ctypes.c_int32)]
+
+
+class OQuery(ctypes.Structure):
+    _fields_ = [("num_ops", ctypes.c_int32), ("ops", ctypes.c_void_p), ("num_leaves", ctypes.c_int32),
+                ("leaves", ctypes.c_void_p), ("num_gb", ctypes.c_int32), ("gb_col", ctypes.c_void_p),
+                ("num_groups_limit", ctypes.c_int64), ("num_aggs", ctypes.c_int32), ("agg_type", ctypes.c_void_p),
+                ("agg_col", ctypes.c_void_p), ("agg_log2m", ctypes.c_void_p)]
+
+
+def lib():
+    global _lib
+    with _lock:
+        if _lib is None:
+            _lib = ctypes.CDLL(build())
+            _lib.oracle_read_int.restype = ctypes.c_int32
+            _lib.oracle_read_int.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]
+            _lib.oracle_read_ints.restype = None
+            _lib.oracle_read_ints.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                                              ctypes.c_void_p]
+            _lib.oracle_write_int.restype = None
+            _lib.oracle_write_int.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]
+            _lib.oracle_hash_long.restype = ctypes.c_int32
+            _lib.oracle_hash_long.argtypes = [ctypes.c_int64]
+            _lib.oracle_hash_bytes.restype = ctypes.c_int32
+            _lib.oracle_hash_bytes.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32]
+            _lib.oracle_run_segment.restype = ctypes.c_int64
+            _lib.oracle_run_segment.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(OQuery),
+                                                ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
+    return _lib
+
+
+# ------------------------------------------------------------------ small helpers used by tests
+def read_ints(buf, n, nb, start=0):
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    out = np.zeros(n, dtype=np.int32)
+    lib().oracle_read_ints(buf.ctypes.data, start, n, nb, out.ctypes.data)
+    return out
+
+
+def write_ints(values, nb):
+    values = np.asarray(values, dtype=np.int32)
+    buf = np.zeros((len(values) * nb + 7) // 8 + 1, dtype=np.uint8)
+    for i, v in enumerate(values.tolist()):
+        lib().oracle_write_int(buf.ctypes.data, i, nb, v)
+    return buf[: (len(values) * nb + 7) // 8]
+
+
+def murmur_hash(value, data_type):
+    """MurmurHash.hash(Object) for the boxed dictionary value of a column of `data_type`."""
+    L = lib()
+    if data_type in ("INT", "LONG"):
+        return L.oracle_hash_long(int(value))
+    if data_type == "FLOAT":
+        return L.oracle_hash_long(int(np.array([value], dtype=np.float32).view(np.int32)[0]))
+    if data_type == "DOUBLE":
+        return L.oracle_hash_long(int(np.array([value], dtype=np.float64).view(np.int64)[0]))
+    b = str(value).encode("utf-8")  # String.getBytes() with the UTF-8 platform charset
+    return L.oracle_hash_bytes(b, len(b), -1)
+
+
+# ------------------------------------------------------------------ predicate evaluators (restated)
+def _parse(raw, data_type):
+    if data_type in ("INT", "LONG"):
+        try:
+            return int(str(raw))
+        except ValueError:
+            return int(float(str(raw)))
+    if data_type == "FLOAT":
+        return float(np.float32(float(raw)))
+    if data_type == "DOUBLE":
+        return float(raw)
+    return str(raw)
+
+
+def _dict_match(pred, col):
+    """applySV(dictId) for every dictId of the (sorted) dictionary, as uint8[cardinality]."""
+    from pinot_amd import query as Q  # query model only (data classes)
+    d = col.dictionary
+    card = len(d)
+    m = np.zeros(card, dtype=np.uint8)
+    values = d.tolist()
+    dt = col.data_type
+
+    def index_of(v):
+        lo, hi = 0, card
+        while lo < hi:  # Dictionary.indexOf on a sorted dictionary (binary search)
+            mid = (lo + hi) // 2
+            if values[mid] < v:
+                lo = mid + 1
+            else:
+                hi = mid
+        return lo if lo < card and values[lo] == v else -1
+
+    def insertion_point(v):
+        lo, hi = 0, card
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if values[mid] < v:
+                lo = mid + 1
+            else:
+                hi = mid
+        return lo
+
+    if isinstance(pred, Q.EqPredicate):
+        i = index_of(_parse(pred.value, dt))
+        if i >= 0:
+            m[i] = 1
+    elif isinstance(pred, Q.NotEqPredicate):
+        m[:] = 1
+        i = index_of(_parse(pred.value, dt))
+        if i >= 0:
+            m[i] = 0
+    elif isinstance(pred, Q.InPredicate):
+        for v in pred.values:
+            i = index_of(_parse(v, dt))
+            if i >= 0:
+                m[i] = 1
+    elif isinstance(pred, Q.NotInPredicate):
+        m[:] = 1
+        for v in pred.values:
+            i = index_of(_parse(v, dt))
+            if i >= 0:
+                m[i] = 0
+    elif isinstance(pred, Q.RangePredicate):
+        # SortedDictionaryBasedRangePredicateEvaluator: [startDictId, endDictId)
+        if pred.lower == Q.UNBOUNDED:
+            start = 0
+        else:
+            v = _parse(pred.lower, dt)
+            p = insertion_point(v)
+            start = p + 1 if (p < card and values[p] == v and not pred.lower_inclusive) else p
+        if pred.upper == Q.UNBOUNDED:
+            end = card
+        else:
+            v = _parse(pred.upper, dt)
+            p = insertion_point(v)
+            end = p + 1 if (p < card and values[p] == v and pred.upper_inclusive) else p
+        if end > start:
+            m[start:end] = 1
+    else:
+        raise TypeError(pred)
+    return m
+
+
+def _raw_leaf(pred, col, leaf):
+    from pinot_amd import query as Q
+    dt = col.data_type
+    integral = dt in ("INT", "LONG")
+    leaf.kind = 1
+    leaf.lo_unbounded = leaf.hi_unbounded = 1
+    leaf.lo_incl = leaf.hi_incl = 1
+
+    def setb(which, raw, incl):
+        v = _parse(raw, dt)
+        if which == "lo":
+            leaf.lo_unbounded, leaf.lo_incl = 0, int(incl)
+            if integral:
+                leaf.ilo = v
+            else:
+                leaf.dlo = v
+        else:
+            leaf.hi_unbounded, leaf.hi_incl = 0, int(incl)
+            if integral:
+                leaf.ihi = v
+            else:
+                leaf.dhi = v
+
+    if isinstance(pred, Q.EqPredicate):
+        setb("lo", pred.value, True)
+        setb("hi", pred.value, True)
+    elif isinstance(pred, Q.RangePredicate):
+        if pred.lower != Q.UNBOUNDED:
+            setb("lo", pred.lower, pred.lower_inclusive)
+        if pred.upper != Q.UNBOUNDED:
+            setb("hi", pred.upper, pred.upper_inclusive)
+    else:
+        raise TypeError("raw leaf %r" % (pred,))
+
+
+def _flatten(f, leaves, ops, segment):
+    from pinot_amd import query as Q
+    if isinstance(f, (Q.And, Q.Or)):
+        for i, c in enumerate(f.children):
+            _flatten(c, leaves, ops, segment)
+            if i:
+                ops.append(1 if isinstance(f, Q.And) else 2)
+    elif isinstance(f, Q.Not):
+        _flatten(f.child, leaves, ops, segment)
+        ops.append(3)
+    elif isinstance(f, (Q.NotEqPredicate, Q.InPredicate, Q.NotInPredicate)) and not segment.column(f.column).has_dictionary:
+        # raw: != -> NOT(=); IN -> OR(=...); NOT IN -> NOT(OR(=...))
+        if isinstance(f, Q.NotEqPredicate):
+            _flatten(Q.Not(Q.EqPredicate(f.column, f.value)), leaves, ops, segment)
+        else:
+            ors = Q.Or(tuple(Q.EqPredicate(f.column, v) for v in f.values))
+            _flatten(Q.Not(ors) if isinstance(f, Q.NotInPredicate) else ors, leaves, ops, segment)
+    else:
+        ops.append(0 | (len(leaves) << 8))
+        leaves.append(f)
+
+
+_AGG = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "DISTINCTCOUNTHLL": 4}
+
+
+def run_segment(query, segment):
+    """Per-segment intermediate result: {key tuple (values): [count, per-oracle-agg values]}; () for agg-only."""
+    from pinot_amd import query as Q  # noqa: F401
+    cols_order = sorted(query.columns())
+    cidx = {c: i for i, c in enumerate(cols_order)}
+    ocols = (OCol * max(1, len(cols_order)))()
+    keep = []
+    hll_cols = {a.column for a in query.aggregations if a.function == "DISTINCTCOUNTHLL"}
+    for name, i in cidx.items():
+        col = segment.column(name)
+        oc = ocols[i]
+        if col.has_dictionary:
+            oc.kind = 0
+            oc.num_bits = col.num_bits
+            oc.cardinality = col.cardinality
+            fwd = np.ascontiguousarray(col.fwd_bytes, dtype=np.uint8)
+            keep.append(fwd)
+            oc.fwd = fwd.ctypes.data
+            if col.data_type != "STRING":
+                df = np.ascontiguousarray(col.dictionary, dtype=np.float64)
+                keep.append(df)
+                oc.dict_f64 = df.ctypes.data
+            if name in hll_cols:
+                hh = np.array([murmur_hash(v, col.data_type) for v in col.dictionary.tolist()], dtype=np.int32)
+                keep.append(hh)
+                oc.dict_hash = hh.ctypes.data
+        else:
+            oc.kind = {"INT": 1, "LONG": 2, "FLOAT": 3, "DOUBLE": 4}[col.data_type]
+            raw = np.ascontiguousarray(col.raw_values)
+            keep.append(raw)
+            oc.raw = raw.ctypes.data
+
+    # filter
+    leaves, ops = [], []
+    if query.filter is not None:
+        _flatten(query.filter, leaves, ops, segment)
+    oleaves = (OLeaf * max(1, len(leaves)))()
+    for i, pred in enumerate(leaves):
+        col = segment.column(pred.column)
+        oleaves[i].col = cidx[pred.column]
+        if col.has_dictionary:
+            m = _dict_match(pred, col)
+            keep.append(m)
+            oleaves[i].kind = 0
+            oleaves[i].match = m.ctypes.data
+        else:
+            _raw_leaf(pred, col, oleaves[i])
+    ops_a = np.array(ops or [0], dtype=np.int32)
+
+    # aggregations: one oracle agg per distinct (function, column); AVG uses SUM + count
+    oaggs = []
+    amap = []
+    for a in query.aggregations:
+        fn = "SUM" if a.function == "AVG" else a.function
+        key = (fn, a.column if fn != "COUNT" else None, a.log2m if fn == "DISTINCTCOUNTHLL" else 0)
+        if key not in oaggs:
+            oaggs.append(key)
+        amap.append(oaggs.index(key))
+    at = np.array([_AGG[k[0]] for k in oaggs] or [0], dtype=np.int32)
+    ac = np.array([cidx[k[1]] if k[1] else 0 for k in oaggs] or [0], dtype=np.int32)
+    al = np.array([k[2] for k in oaggs] or [0], dtype=np.int32)
+    gb = np.array([cidx[c] for c in query.group_by] or [0], dtype=np.int32)
+
+    oq = OQuery()
+    oq.num_ops = len(ops)
+    oq.ops = ops_a.ctypes.data
+    oq.num_leaves = len(leaves)
+    oq.leaves = ctypes.cast(oleaves, ctypes.c_void_p)
+    oq.num_gb = len(query.group_by)
+    oq.gb_col = gb.ctypes.data
+    oq.num_groups_limit = query.num_groups_limit
+    oq.num_aggs = len(oaggs)
+    oq.agg_type = at.ctypes.data
+    oq.agg_col = ac.ctypes.data
+    oq.agg_log2m = al.ctypes.data
+
+    if query.group_by:
+        prod = 1
+        for c in query.group_by:
+            prod *= segment.column(c).cardinality
+        cap = max(1, min(prod, segment.num_docs, query.num_groups_limit))
+    else:
+        cap = 1
+    keys = np.zeros(cap, dtype=np.int64)
+    counts = np.zeros(cap, dtype=np.int64)
+    vals = np.zeros(max(1, len(oaggs)) * cap, dtype=np.float64)
+    hll_bufs = [np.zeros(cap << k[2], dtype=np.uint8) if k[0] == "DISTINCTCOUNTHLL" else np.zeros(1, np.uint8)
+                for k in oaggs] or [np.zeros(1, np.uint8)]
+    hll_ptrs = (ctypes.c_void_p * len(hll_bufs))(*[b.ctypes.data for b in hll_bufs])
+    matched = ctypes.c_int64()
+    n = lib().oracle_run_segment(ctypes.cast(ocols, ctypes.c_void_p), segment.num_docs, ctypes.byref(oq), cap,
+                                 keys.ctypes.data, counts.ctypes.data, vals.ctypes.data,
+                                 ctypes.cast(hll_ptrs, ctypes.c_void_p), ctypes.byref(matched))
+    if n < 0:
+        raise MemoryError("oracle allocation failed")
+    n = min(n, cap)
+    out = {}
+    for g in range(n):
+        if query.group_by:
+            rk = int(keys[g])
+            kv = []
+            for c in query.group_by:
+                col = segment.column(c)
+                kv.append(col.dictionary[rk % col.cardinality].item())
+                rk //= col.cardinality
+            key = tuple(kv)
+        else:
+            key = ()
+        row = []
+        for ai, k in enumerate(oaggs):
+            if k[0] == "DISTINCTCOUNTHLL":
+                mm = 1 << k[2]
+                row.append(hll_bufs[ai][g * mm:(g + 1) * mm].copy())
+            else:
+                row.append(float(vals[ai * cap + g]))
+        out[key] = (int(counts[g]), row)
+    return out, oaggs, amap, int(matched.value)
+
+
+def run_query(query, segments):
+    """Server-level intermediate result for a segment set, merged by key value in segment order."""
+    from pinot_amd.engine import AvgPair, IntermediateResult
+    from pinot_amd.hll import HyperLogLog
+    merged = {}
+    oaggs, amap = None, None
+    scanned = 0
+    for seg in segments:
+        res, oaggs, amap, matched = run_segment(query, seg)
+        scanned += matched
+        for key, (cnt, row) in res.items():
+            if key not in merged:
+                merged[key] = [cnt, [r.copy() if isinstance(r, np.ndarray) else r for r in row]]
+                continue
+            acc = merged[key]
+            acc[0] += cnt
+            for ai, k in enumerate(oaggs):
+                if k[0] == "SUM":
+                    acc[1][ai] = acc[1][ai] + row[ai]
+                elif k[0] == "MIN":
+                    acc[1][ai] = min(acc[1][ai], row[ai])
+                elif k[0] == "MAX":
+                    acc[1][ai] = max(acc[1][ai], row[ai])
+                elif k[0] == "DISTINCTCOUNTHLL":
+                    acc[1][ai] = np.maximum(acc[1][ai], row[ai])
+    out = IntermediateResult(list(query.aggregations), list(query.group_by))
+    out.num_total_docs = sum(s.num_docs for s in segments)
+    out.num_docs_scanned = scanned
+    if not query.group_by and () not in merged:
+        merged[()] = [0, [np.zeros(1 << k[2], np.uint8) if k[0] == "DISTINCTCOUNTHLL" else
+                          (0.0 if k[0] in ("SUM", "COUNT") else (np.inf if k[0] == "MIN" else -np.inf)) for k in oaggs]]
+    for key, (cnt, row) in merged.items():
+        vals = []
+        for a, ai in zip(query.aggregations, amap):
+            if a.function == "COUNT":
+                vals.append(cnt)
+            elif a.function == "AVG":
+                vals.append(AvgPair(row[ai], cnt))
+            elif a.function == "DISTINCTCOUNTHLL":
+                vals.append(HyperLogLog(a.log2m, row[ai] if isinstance(row[ai], np.ndarray) else None))
+            else:
+                vals.append(row[ai])
+        if query.group_by:
+            out.groups[key] = vals
+        else:
+            out.row = vals
+    return out

@@ -1,0 +1,129 @@
+"""ctypes binding of include/pinot_amd.h (the C-ABI a Pinot server would bind through FFM/JNI).
+
+There is no CPU fallback: if libpinot_amd.so is missing or a call fails, a PinotAmdError is raised.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpinot_amd.so")
+
+PA_MAX_LEAVES = 16
+PA_MAX_OPS = 48
+PA_MAX_GROUP_BY = 8
+PA_MAX_AGGS = 16
+
+PA_INT, PA_LONG, PA_FLOAT, PA_DOUBLE, PA_STRING, PA_BYTES = range(6)
+PA_LEAF_DICT_RANGE, PA_LEAF_DICT_SET, PA_LEAF_RAW_RANGE, PA_LEAF_MV_DICT_RANGE, PA_LEAF_MV_DICT_SET = range(5)
+PA_OP_LEAF, PA_OP_AND, PA_OP_OR, PA_OP_NOT = range(4)
+PA_AGG_COUNT, PA_AGG_SUM, PA_AGG_MIN, PA_AGG_MAX, PA_AGG_DISTINCTCOUNTHLL = range(5)
+PA_QF_STAGE_ALL = 1
+PA_QF_FORCE_GLOBAL = 2
+PA_ACC_COUNT_U64, PA_ACC_SUM_I64, PA_ACC_SUM_F64, PA_ACC_MIN_I64, PA_ACC_MAX_I64, PA_ACC_HLL_U32 = range(6)
+
+# every symbol declared in include/pinot_amd.h
+EXPORTED = [
+    "pa_abi_version", "pa_device_count", "pa_set_device", "pa_last_error",
+    "pa_segment_create", "pa_segment_add_sv_dict_column", "pa_segment_add_mv_dict_column",
+    "pa_segment_add_raw_column", "pa_segment_num_docs", "pa_segment_device_bytes", "pa_segment_destroy",
+    "pa_query_create", "pa_query_bind_segment", "pa_query_prepare", "pa_query_num_keys",
+    "pa_query_execute", "pa_query_num_sections", "pa_query_section", "pa_query_fetch", "pa_query_stats",
+    "pa_query_destroy",
+]
+
+
+class PinotAmdError(RuntimeError):
+    pass
+
+
+class LeafSpec(ctypes.Structure):
+    _fields_ = [("column_id", ctypes.c_int32), ("kind", ctypes.c_int32)]
+
+
+class AggSpec(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("column_id", ctypes.c_int32), ("log2m", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+class QuerySpec(ctypes.Structure):
+    _fields_ = [
+        ("num_leaves", ctypes.c_int32),
+        ("leaves", LeafSpec * PA_MAX_LEAVES),
+        ("num_ops", ctypes.c_int32),
+        ("ops", ctypes.c_int32 * PA_MAX_OPS),
+        ("num_group_by", ctypes.c_int32),
+        ("group_by_columns", ctypes.c_int32 * PA_MAX_GROUP_BY),
+        ("group_by_cardinality", ctypes.c_int64 * PA_MAX_GROUP_BY),
+        ("num_aggs", ctypes.c_int32),
+        ("aggs", AggSpec * PA_MAX_AGGS),
+        ("flags", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+class LeafParams(ctypes.Structure):
+    _fields_ = [
+        ("lo", ctypes.c_int32), ("hi", ctypes.c_int32), ("negate", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("lut", ctypes.POINTER(ctypes.c_uint32)),
+        ("ilo", ctypes.c_int64), ("ihi", ctypes.c_int64),
+        ("dlo", ctypes.c_double), ("dhi", ctypes.c_double),
+    ]
+
+
+_lib = None
+
+
+def _declare(lib):
+    vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+    sig = {
+        "pa_abi_version": (ctypes.c_int, []),
+        "pa_device_count": (ctypes.c_int, []),
+        "pa_set_device": (ctypes.c_int, [ctypes.c_int]),
+        "pa_last_error": (ctypes.c_char_p, []),
+        "pa_segment_create": (vp, [i32]),
+        "pa_segment_add_sv_dict_column": (ctypes.c_int, [vp, i32, vp, u64, i32, i32, i32, vp, vp]),
+        "pa_segment_add_mv_dict_column": (ctypes.c_int, [vp, i32, vp, u64, i32, i32, i64, i32, vp, vp]),
+        "pa_segment_add_raw_column": (ctypes.c_int, [vp, i32, i32, vp]),
+        "pa_segment_num_docs": (i32, [vp]),
+        "pa_segment_device_bytes": (u64, [vp]),
+        "pa_segment_destroy": (None, [vp]),
+        "pa_query_create": (vp, [ctypes.POINTER(QuerySpec), i32]),
+        "pa_query_bind_segment": (ctypes.c_int, [vp, i32, vp, ctypes.POINTER(LeafParams), vp]),
+        "pa_query_prepare": (ctypes.c_int, [vp]),
+        "pa_query_num_keys": (i64, [vp]),
+        "pa_query_execute": (ctypes.c_int, [vp, vp]),
+        "pa_query_num_sections": (i32, [vp]),
+        "pa_query_section": (vp, [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i64)]),
+        "pa_query_fetch": (i64, [vp, vp, i64, vp, vp, vp]),
+        "pa_query_stats": (ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "pa_query_destroy": (None, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+
+
+def lib():
+    """Loads the in-tree HIP extension; raises if it is missing (no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PinotAmdError("%s is missing: run `python -m pinot_amd.build` (hipcc, gfx950)" % LIB_PATH)
+        _lib = ctypes.CDLL(LIB_PATH)
+        _declare(_lib)
+        if _lib.pa_abi_version() != 1:
+            raise PinotAmdError("ABI version mismatch")
+    return _lib
+
+
+def check(rc, what=""):
+    if rc < 0:
+        raise PinotAmdError("%s failed (%d): %s" % (what, rc, lib().pa_last_error().decode(errors="replace")))
+    return rc
+
+
+def check_ptr(p, what=""):
+    if not p:
+        raise PinotAmdError("%s failed: %s" % (what, lib().pa_last_error().decode(errors="replace")))
+    return p

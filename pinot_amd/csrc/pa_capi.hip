@@ -1,0 +1,813 @@
+// Host side of the C-ABI (include/pinot_amd.h): segment residency, query planning (CNF filter, column
+// slots, staging, accumulator layout, strategy) and result fetch. No CPU fallback: every query runs the
+// HIP kernels; errors surface as negative return codes + pa_last_error().
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "pa_device.h"
+#include "pa_launch.h"
+
+using namespace pa;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define PA_HIP(call)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (call);                                                           \
+    if (e_ != hipSuccess) return fail(PA_EHIP, std::string(#call ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+#define PA_HIP_NULL(call)                                                             \
+  do {                                                                                \
+    hipError_t e_ = (call);                                                           \
+    if (e_ != hipSuccess) { fail(PA_EHIP, std::string(#call ": ") + hipGetErrorString(e_)); return nullptr; } \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+};
+
+int dev_alloc(DevBuf& b, size_t bytes) {
+  b.n = bytes;
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e != hipSuccess) return fail(PA_ENOMEM, std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e));
+  return PA_OK;
+}
+
+void dev_free(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.n = 0;
+}
+
+int64_t wtiles_for(int64_t num_docs) { return (num_docs + kWTileDocs - 1) / kWTileDocs; }
+
+struct Column {
+  int32_t kind = COL_NONE;
+  int32_t vtype = PA_INT;
+  int32_t nbits = 0;
+  int32_t cardinality = 0;
+  int64_t total_values = 0;
+  DevBuf words;   // guard + stream + pad (SV dict)
+  DevBuf raw;     // raw values (SV raw)
+  DevBuf dict;    // int64 or double
+  DevBuf hashes;  // int32 murmur hashes (STRING/BYTES dictionaries)
+  ~Column() {
+    dev_free(words);
+    dev_free(raw);
+    dev_free(dict);
+    dev_free(hashes);
+  }
+};
+
+}  // namespace
+
+struct pa_segment {
+  int32_t num_docs = 0;
+  std::map<int32_t, Column*> cols;
+  uint64_t bytes = 0;
+  ~pa_segment() {
+    for (auto& kv : cols) delete kv.second;
+  }
+};
+
+namespace {
+
+int upload_dict(Column* c, int32_t vtype, int32_t card, const void* dict_values, const int32_t* dict_hashes) {
+  c->vtype = vtype;
+  c->cardinality = card;
+  if (dict_values != nullptr && (vtype == PA_INT || vtype == PA_LONG || vtype == PA_FLOAT || vtype == PA_DOUBLE)) {
+    int rc = dev_alloc(c->dict, (size_t)card * 8);
+    if (rc) return rc;
+    PA_HIP(hipMemcpy(c->dict.p, dict_values, (size_t)card * 8, hipMemcpyHostToDevice));
+  }
+  if (dict_hashes != nullptr) {
+    int rc = dev_alloc(c->hashes, (size_t)card * 4);
+    if (rc) return rc;
+    PA_HIP(hipMemcpy(c->hashes.p, dict_hashes, (size_t)card * 4, hipMemcpyHostToDevice));
+  }
+  return PA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pa_abi_version(void) { return PA_ABI_VERSION; }
+
+int pa_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int pa_set_device(int device) {
+  PA_HIP(hipSetDevice(device));
+  return PA_OK;
+}
+
+const char* pa_last_error(void) { return g_err.c_str(); }
+
+pa_segment* pa_segment_create(int32_t num_docs) {
+  if (num_docs < 0) {
+    fail(PA_EINVAL, "num_docs < 0");
+    return nullptr;
+  }
+  pa_segment* s = new pa_segment();
+  s->num_docs = num_docs;
+  return s;
+}
+
+int pa_segment_add_sv_dict_column(pa_segment* seg, int32_t column_id, const uint8_t* fwd_index,
+                                  uint64_t fwd_index_bytes, int32_t num_bits_per_value, int32_t cardinality,
+                                  int32_t value_type, const void* dict_values, const int32_t* dict_hashes) {
+  if (!seg) return fail(PA_EINVAL, "null segment");
+  if (num_bits_per_value < 1 || num_bits_per_value > 31) return fail(PA_EINVAL, "num_bits_per_value must be 1..31");
+  if (cardinality < 1) return fail(PA_EINVAL, "cardinality < 1");
+  if (value_type < PA_INT || value_type > PA_BYTES) return fail(PA_EINVAL, "bad value_type");
+  const uint64_t need = ((uint64_t)seg->num_docs * (uint64_t)num_bits_per_value + 7) / 8;
+  if (fwd_index_bytes < need) return fail(PA_EINVAL, "forward index shorter than ceil(numDocs*numBits/8)");
+  if (seg->cols.count(column_id)) return fail(PA_EINVAL, "duplicate column id");
+  Column* c = new Column();
+  c->kind = COL_SV_DICT;
+  c->nbits = num_bits_per_value;
+  // guard words | whole wave tiles of 64*nb words | guard words
+  const int64_t stream_words = wtiles_for(seg->num_docs) * 64 * num_bits_per_value;
+  const int64_t total_words = kGuardWords + stream_words + kGuardWords;
+  int rc = dev_alloc(c->words, (size_t)total_words * 4);
+  if (rc) { delete c; return rc; }
+  uint32_t* w = (uint32_t*)c->words.p;
+  if (hipMemset(w, 0, (size_t)total_words * 4) != hipSuccess ||
+      hipMemcpy(w + kGuardWords, fwd_index, need, hipMemcpyHostToDevice) != hipSuccess) {
+    delete c;
+    return fail(PA_EHIP, "forward index upload failed");
+  }
+  if (launch_bswap_words(w + kGuardWords, (int64_t)((need + 3) / 4), nullptr) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    delete c;
+    return fail(PA_EHIP, "bswap kernel failed");
+  }
+  rc = upload_dict(c, value_type, cardinality, dict_values, dict_hashes);
+  if (rc) { delete c; return rc; }
+  seg->bytes += c->words.n + c->dict.n + c->hashes.n;
+  seg->cols[column_id] = c;
+  return PA_OK;
+}
+
+int pa_segment_add_mv_dict_column(pa_segment* seg, int32_t column_id, const uint8_t* fwd_index,
+                                  uint64_t fwd_index_bytes, int32_t num_bits_per_value, int32_t cardinality,
+                                  int64_t total_num_values, int32_t value_type, const void* dict_values,
+                                  const int32_t* dict_hashes) {
+  (void)seg; (void)column_id; (void)fwd_index; (void)fwd_index_bytes; (void)num_bits_per_value;
+  (void)cardinality; (void)total_num_values; (void)value_type; (void)dict_values; (void)dict_hashes;
+  return fail(PA_EUNSUPPORTED, "multi-value columns are not implemented yet");
+}
+
+int pa_segment_add_raw_column(pa_segment* seg, int32_t column_id, int32_t value_type, const void* values) {
+  if (!seg) return fail(PA_EINVAL, "null segment");
+  if (value_type < PA_INT || value_type > PA_DOUBLE) return fail(PA_EINVAL, "raw columns must be INT/LONG/FLOAT/DOUBLE");
+  if (seg->cols.count(column_id)) return fail(PA_EINVAL, "duplicate column id");
+  const size_t esz = (value_type == PA_INT || value_type == PA_FLOAT) ? 4 : 8;
+  Column* c = new Column();
+  c->kind = COL_SV_RAW;
+  c->vtype = value_type;
+  const size_t padded = (size_t)wtiles_for(seg->num_docs) * kWTileDocs;
+  int rc = dev_alloc(c->raw, padded * esz + 16);
+  if (rc) { delete c; return rc; }
+  if (hipMemset(c->raw.p, 0, padded * esz + 16) != hipSuccess ||
+      hipMemcpy(c->raw.p, values, (size_t)seg->num_docs * esz, hipMemcpyHostToDevice) != hipSuccess) {
+    delete c;
+    return fail(PA_EHIP, "raw column upload failed");
+  }
+  seg->bytes += c->raw.n;
+  seg->cols[column_id] = c;
+  return PA_OK;
+}
+
+int32_t pa_segment_num_docs(const pa_segment* seg) { return seg ? seg->num_docs : -1; }
+uint64_t pa_segment_device_bytes(const pa_segment* seg) { return seg ? seg->bytes : 0; }
+void pa_segment_destroy(pa_segment* seg) { delete seg; }
+
+}  // extern "C"
+
+// ====================================================================== queries
+
+namespace {
+
+struct Literal {
+  int leaf;
+  bool neg;
+};
+using Clause = std::vector<Literal>;
+
+struct Node {
+  int op;    // PA_OP_*
+  int leaf;  // for LEAF
+  int a = -1, b = -1;
+};
+
+// Postfix program -> CNF (list of clauses, each a disjunction of possibly negated leaves).
+int to_cnf(const pa_query_spec& spec, std::vector<Clause>& out) {
+  out.clear();
+  if (spec.num_ops == 0) return PA_OK;
+  std::vector<Node> nodes;
+  std::vector<int> st;
+  for (int i = 0; i < spec.num_ops; ++i) {
+    const int op = spec.ops[i] & 0xff;
+    if (op == PA_OP_LEAF) {
+      const int leaf = (spec.ops[i] >> 8) & 0xff;
+      if (leaf >= spec.num_leaves) return fail(PA_EINVAL, "filter program references a missing leaf");
+      nodes.push_back({PA_OP_LEAF, leaf});
+      st.push_back((int)nodes.size() - 1);
+    } else if (op == PA_OP_NOT) {
+      if (st.empty()) return fail(PA_EINVAL, "malformed filter program");
+      Node n{PA_OP_NOT, -1};
+      n.a = st.back();
+      st.pop_back();
+      nodes.push_back(n);
+      st.push_back((int)nodes.size() - 1);
+    } else if (op == PA_OP_AND || op == PA_OP_OR) {
+      if (st.size() < 2) return fail(PA_EINVAL, "malformed filter program");
+      Node n{op, -1};
+      n.b = st.back();
+      st.pop_back();
+      n.a = st.back();
+      st.pop_back();
+      nodes.push_back(n);
+      st.push_back((int)nodes.size() - 1);
+    } else {
+      return fail(PA_EINVAL, "unknown filter opcode");
+    }
+  }
+  if (st.size() != 1) return fail(PA_EINVAL, "malformed filter program");
+  // recursive CNF with negation pushed to the leaves (De Morgan)
+  std::function<int(int, bool, std::vector<Clause>&)> rec = [&](int ni, bool neg, std::vector<Clause>& cl) -> int {
+    const Node& n = nodes[ni];
+    if (n.op == PA_OP_LEAF) {
+      cl = {Clause{Literal{n.leaf, neg}}};
+      return PA_OK;
+    }
+    if (n.op == PA_OP_NOT) return rec(n.a, !neg, cl);
+    const bool is_and = (n.op == PA_OP_AND) != neg;
+    std::vector<Clause> ca, cb;
+    int rc = rec(n.a, neg, ca);
+    if (rc) return rc;
+    rc = rec(n.b, neg, cb);
+    if (rc) return rc;
+    if (is_and) {
+      cl = ca;
+      cl.insert(cl.end(), cb.begin(), cb.end());
+    } else {
+      cl.clear();
+      for (auto& x : ca)
+        for (auto& y : cb) {
+          Clause c = x;
+          c.insert(c.end(), y.begin(), y.end());
+          cl.push_back(c);
+        }
+    }
+    size_t lits = 0;
+    for (auto& c : cl) lits += c.size();
+    if (lits > PA_MAX_LEAVES) return fail(PA_EUNSUPPORTED, "filter expands to more than PA_MAX_LEAVES CNF literals");
+    return PA_OK;
+  };
+  return rec(st.back(), false, out);
+}
+
+struct Section {
+  int32_t kind;
+  void* ptr;
+  int64_t n;
+};
+
+}  // namespace
+
+struct pa_query {
+  pa_query_spec spec;
+  int32_t nseg = 0;
+  std::vector<const pa_segment*> segs;
+  std::vector<std::vector<pa_leaf_params>> leaf_params;
+  std::vector<std::vector<std::vector<uint32_t>>> luts;        // [seg][leaf]
+  std::vector<std::vector<std::vector<int32_t>>> remaps;       // [seg][gb]
+  std::vector<std::vector<char>> has_remap;
+  bool prepared = false;
+
+  // plan
+  std::vector<int32_t> slot_cols;
+  std::vector<Literal> literals;
+  std::vector<int> clause_end;
+  int64_t num_keys = 1;
+  int strategy = STRAT_GLOBAL;
+  int grid = 0;
+  int lds_bytes = 0;
+  uint64_t staged_bytes = 0;
+  uint64_t num_docs = 0;
+  uint64_t num_tiles = 0;
+
+  DevQuery hq;
+  std::vector<DevSeg> hsegs;
+  DevBuf dq, dsegs;
+  std::vector<DevBuf> owned;  // LUTs, remaps, HLL LUTs
+  DevBuf acc;                 // all accumulator sections
+  std::vector<Section> sections;
+  std::vector<int> agg_section;  // agg -> section index (-1 for COUNT)
+
+  ~pa_query() {
+    dev_free(dq);
+    dev_free(dsegs);
+    dev_free(acc);
+    for (auto& b : owned) dev_free(b);
+  }
+};
+
+namespace {
+
+int slot_of(pa_query* q, int32_t col) {
+  for (size_t i = 0; i < q->slot_cols.size(); ++i)
+    if (q->slot_cols[i] == col) return (int)i;
+  if ((int)q->slot_cols.size() >= kMaxSlots) return -1;
+  q->slot_cols.push_back(col);
+  return (int)q->slot_cols.size() - 1;
+}
+
+int upload_owned(pa_query* q, const void* host, size_t bytes, void** dev) {
+  DevBuf b;
+  int rc = dev_alloc(b, bytes);
+  if (rc) return rc;
+  q->owned.push_back(b);
+  if (bytes) PA_HIP(hipMemcpy(b.p, host, bytes, hipMemcpyHostToDevice));
+  *dev = b.p;
+  return PA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+pa_query* pa_query_create(const pa_query_spec* spec, int32_t num_segments) {
+  if (!spec || num_segments < 0) {
+    fail(PA_EINVAL, "bad query spec");
+    return nullptr;
+  }
+  if (spec->num_leaves < 0 || spec->num_leaves > PA_MAX_LEAVES || spec->num_ops < 0 || spec->num_ops > PA_MAX_OPS ||
+      spec->num_group_by < 0 || spec->num_group_by > PA_MAX_GROUP_BY || spec->num_aggs < 0 ||
+      spec->num_aggs > PA_MAX_AGGS) {
+    fail(PA_EINVAL, "query spec counts out of range");
+    return nullptr;
+  }
+  pa_query* q = new pa_query();
+  q->spec = *spec;
+  q->nseg = num_segments;
+  q->segs.assign(num_segments, nullptr);
+  q->leaf_params.resize(num_segments);
+  q->luts.resize(num_segments);
+  q->remaps.resize(num_segments);
+  q->has_remap.resize(num_segments);
+  return q;
+}
+
+int pa_query_bind_segment(pa_query* q, int32_t index, const pa_segment* seg, const pa_leaf_params* leaf_params,
+                          const int32_t* const* group_remaps) {
+  if (!q || !seg || index < 0 || index >= q->nseg) return fail(PA_EINVAL, "bad bind arguments");
+  if (q->prepared) return fail(PA_EINVAL, "query already prepared");
+  const pa_query_spec& s = q->spec;
+  q->segs[index] = seg;
+  q->leaf_params[index].assign(leaf_params, leaf_params + s.num_leaves);
+  q->luts[index].assign(s.num_leaves, {});
+  for (int l = 0; l < s.num_leaves; ++l) {
+    const int kind = s.leaves[l].kind;
+    if (kind == PA_LEAF_DICT_SET) {
+      auto it = seg->cols.find(s.leaves[l].column_id);
+      if (it == seg->cols.end()) return fail(PA_EINVAL, "leaf column missing in segment");
+      if (!leaf_params[l].lut) return fail(PA_EINVAL, "DICT_SET leaf without lut");
+      const size_t words = ((size_t)it->second->cardinality + 31) / 32;
+      q->luts[index][l].assign(leaf_params[l].lut, leaf_params[l].lut + words);
+    }
+  }
+  q->remaps[index].assign(s.num_group_by, {});
+  q->has_remap[index].assign(s.num_group_by, 0);
+  for (int j = 0; j < s.num_group_by; ++j) {
+    if (group_remaps && group_remaps[j]) {
+      auto it = seg->cols.find(s.group_by_columns[j]);
+      if (it == seg->cols.end()) return fail(PA_EINVAL, "group-by column missing in segment");
+      const int32_t card = it->second->cardinality;
+      q->remaps[index][j].assign(group_remaps[j], group_remaps[j] + card);
+      for (int32_t v : q->remaps[index][j])
+        if (v < 0 || v >= s.group_by_cardinality[j]) return fail(PA_EINVAL, "group remap id outside the key space");
+      q->has_remap[index][j] = 1;
+    }
+  }
+  return PA_OK;
+}
+
+int pa_query_prepare(pa_query* q) {
+  if (!q) return fail(PA_EINVAL, "null query");
+  if (q->prepared) return PA_OK;
+  const pa_query_spec& s = q->spec;
+  for (int i = 0; i < q->nseg; ++i)
+    if (!q->segs[i]) return fail(PA_EINVAL, "segment " + std::to_string(i) + " not bound");
+
+  // ---- CNF + slots
+  std::vector<Clause> cnf;
+  int rc = to_cnf(s, cnf);
+  if (rc) return rc;
+  q->literals.clear();
+  q->clause_end.clear();
+  for (auto& c : cnf) {
+    for (size_t i = 0; i < c.size(); ++i) {
+      q->literals.push_back(c[i]);
+      q->clause_end.push_back(i + 1 == c.size());
+    }
+  }
+  std::vector<char> leaf_slot_is_filter(kMaxSlots, 0);
+  std::vector<int> leaf_slot(s.num_leaves, -1);
+  for (int l = 0; l < s.num_leaves; ++l) {
+    const int sl = slot_of(q, s.leaves[l].column_id);
+    if (sl < 0) return fail(PA_EUNSUPPORTED, "too many distinct columns in one query");
+    leaf_slot[l] = sl;
+    leaf_slot_is_filter[sl] = 1;
+    const int k = s.leaves[l].kind;
+    if (k == PA_LEAF_MV_DICT_RANGE || k == PA_LEAF_MV_DICT_SET)
+      return fail(PA_EUNSUPPORTED, "multi-value filter leaves are not implemented yet");
+  }
+  std::vector<int> gb_slot(s.num_group_by);
+  for (int j = 0; j < s.num_group_by; ++j) {
+    gb_slot[j] = slot_of(q, s.group_by_columns[j]);
+    if (gb_slot[j] < 0) return fail(PA_EUNSUPPORTED, "too many distinct columns in one query");
+  }
+  std::vector<int> agg_slot(s.num_aggs, 0);
+  for (int a = 0; a < s.num_aggs; ++a) {
+    const int t = s.aggs[a].type;
+    if (t < PA_AGG_COUNT || t > PA_AGG_DISTINCTCOUNTHLL) return fail(PA_EINVAL, "bad aggregation type");
+    if (t == PA_AGG_COUNT) continue;
+    agg_slot[a] = slot_of(q, s.aggs[a].column_id);
+    if (agg_slot[a] < 0) return fail(PA_EUNSUPPORTED, "too many distinct columns in one query");
+    if (t == PA_AGG_DISTINCTCOUNTHLL && (s.aggs[a].log2m < 4 || s.aggs[a].log2m > 16))
+      return fail(PA_EINVAL, "log2m must be 4..16");
+  }
+  const int nslots = (int)q->slot_cols.size();
+  const bool has_filter = !q->literals.empty();
+  const bool stage_all = !has_filter || (s.flags & PA_QF_STAGE_ALL);
+
+  // ---- key space
+  int64_t K = 1;
+  std::vector<int64_t> stride(s.num_group_by);
+  for (int j = 0; j < s.num_group_by; ++j) {
+    if (s.group_by_cardinality[j] < 1) return fail(PA_EINVAL, "group_by_cardinality < 1");
+    stride[j] = K;
+    if (K > (int64_t(1) << 40) / s.group_by_cardinality[j])
+      return fail(PA_EUNSUPPORTED, "group key space too large for direct addressing (hash fallback not implemented)");
+    K *= s.group_by_cardinality[j];
+  }
+  q->num_keys = K;
+
+  // ---- per-segment descriptors
+  q->hsegs.assign(q->nseg, DevSeg{});
+  std::vector<char> staged(nslots, 0);
+  std::vector<int> agg_src(s.num_aggs, SRC_INT);
+  int64_t first = 0;
+  int image_max = 0;
+  q->staged_bytes = 0;
+  q->num_docs = 0;
+  for (int si = 0; si < q->nseg; ++si) {
+    const pa_segment* seg = q->segs[si];
+    DevSeg& d = q->hsegs[si];
+    std::memset(&d, 0, sizeof(d));
+    d.num_docs = seg->num_docs;
+    d.num_wtiles = (int32_t)wtiles_for(seg->num_docs);
+    d.first_wtile = first;
+    first += d.num_wtiles;
+    q->num_docs += (uint64_t)seg->num_docs;
+    int off = kGuardWords;
+    for (int sl = 0; sl < nslots; ++sl) {
+      auto it = seg->cols.find(q->slot_cols[sl]);
+      if (it == seg->cols.end())
+        return fail(PA_EINVAL, "column " + std::to_string(q->slot_cols[sl]) + " missing in segment " + std::to_string(si));
+      const Column* c = it->second;
+      DevCol& dc = d.cols[sl];
+      dc.kind = c->kind;
+      dc.nbits = c->nbits;
+      dc.vtype = c->vtype;
+      dc.words = c->words.p ? (const uint32_t*)c->words.p + kGuardWords : nullptr;
+      dc.raw = c->raw.p;
+      dc.dict_i64 = (c->vtype == PA_INT || c->vtype == PA_LONG) ? (const int64_t*)c->dict.p : nullptr;
+      dc.dict_f64 = (c->vtype == PA_FLOAT || c->vtype == PA_DOUBLE) ? (const double*)c->dict.p : nullptr;
+      dc.lds_off = -1;
+      if (c->kind == COL_SV_DICT && (leaf_slot_is_filter[sl] || stage_all)) {
+        staged[sl] = 1;
+        dc.lds_off = off;
+        off += 64 * c->nbits + kGuardWords;
+        q->staged_bytes += (uint64_t)d.num_wtiles * 64 * c->nbits * 4;
+      }
+    }
+    d.image_dwords = off;
+    image_max = std::max(image_max, off);
+    // filter literals
+    for (size_t li = 0; li < q->literals.size(); ++li) {
+      const Literal lit = q->literals[li];
+      const pa_leaf_params& p = q->leaf_params[si][lit.leaf];
+      DevLeaf& L = d.leaves[li];
+      L.kind = s.leaves[lit.leaf].kind;
+      L.slot = leaf_slot[lit.leaf];
+      L.negate = (p.negate != 0) != lit.neg;
+      L.clause_end = q->clause_end[li];
+      const DevCol& dc = d.cols[L.slot];
+      if (L.kind == PA_LEAF_DICT_RANGE || L.kind == PA_LEAF_DICT_SET) {
+        if (dc.kind != COL_SV_DICT) return fail(PA_EINVAL, "dictionary leaf on a non-dictionary column");
+      } else if (L.kind == PA_LEAF_RAW_RANGE) {
+        if (dc.kind != COL_SV_RAW) return fail(PA_EINVAL, "raw leaf on a non-raw column");
+      }
+      if (L.kind == PA_LEAF_DICT_RANGE) {
+        L.lo = p.lo;
+        L.span = p.hi > p.lo ? p.hi - p.lo : 0;
+      } else if (L.kind == PA_LEAF_DICT_SET) {
+        const auto& lut = q->luts[si][lit.leaf];
+        void* dp = nullptr;
+        rc = upload_owned(q, lut.data(), lut.size() * 4, &dp);
+        if (rc) return rc;
+        L.lut = (const uint32_t*)dp;
+      } else {
+        L.ilo = p.ilo;
+        L.ihi = p.ihi;
+        L.dlo = p.dlo;
+        L.dhi = p.dhi;
+      }
+    }
+    // group-by remaps
+    for (int j = 0; j < s.num_group_by; ++j) {
+      const DevCol& dc = d.cols[gb_slot[j]];
+      if (dc.kind != COL_SV_DICT) return fail(PA_EUNSUPPORTED, "group-by on non-dictionary columns is not implemented yet");
+      if (q->has_remap[si][j]) {
+        void* dp = nullptr;
+        rc = upload_owned(q, q->remaps[si][j].data(), q->remaps[si][j].size() * 4, &dp);
+        if (rc) return rc;
+        d.remap[j] = (const int32_t*)dp;
+      } else {
+        const Column* c = seg->cols.at(s.group_by_columns[j]);
+        if (c->cardinality > s.group_by_cardinality[j])
+          return fail(PA_EINVAL, "segment cardinality exceeds the key space without a remap");
+      }
+    }
+    // aggregations: value source + HLL lookup tables
+    for (int a = 0; a < s.num_aggs; ++a) {
+      const pa_agg_spec& A = s.aggs[a];
+      if (A.type == PA_AGG_COUNT) continue;
+      const Column* c = seg->cols.at(A.column_id);
+      const int src = (c->vtype == PA_FLOAT || c->vtype == PA_DOUBLE) ? SRC_DOUBLE : SRC_INT;
+      if (A.type != PA_AGG_DISTINCTCOUNTHLL) {
+        if (c->vtype == PA_STRING || c->vtype == PA_BYTES) return fail(PA_EINVAL, "numeric aggregation on a non-numeric column");
+        if (c->kind == COL_SV_DICT && !c->dict.p) return fail(PA_EINVAL, "dictionary values missing");
+      }
+      if (si == 0) agg_src[a] = src;
+      else if (agg_src[a] != src) return fail(PA_EINVAL, "aggregation column type differs across segments");
+      if (A.type == PA_AGG_DISTINCTCOUNTHLL && c->kind == COL_SV_DICT) {
+        DevBuf b;
+        rc = dev_alloc(b, (size_t)c->cardinality * 4);
+        if (rc) return rc;
+        q->owned.push_back(b);
+        hipError_t e;
+        if (c->vtype == PA_STRING || c->vtype == PA_BYTES) {
+          if (!c->hashes.p) return fail(PA_EINVAL, "DISTINCTCOUNTHLL on a STRING/BYTES dictionary needs dict_hashes");
+          e = launch_hll_lut_hashes((const int32_t*)c->hashes.p, c->cardinality, A.log2m, (uint32_t*)b.p, nullptr);
+        } else {
+          e = launch_hll_lut_numeric((const int64_t*)c->dict.p, (const double*)c->dict.p, c->vtype, c->cardinality,
+                                     A.log2m, (uint32_t*)b.p, nullptr);
+        }
+        if (e != hipSuccess) return fail(PA_EHIP, std::string("hll lut: ") + hipGetErrorString(e));
+        d.hll_lut[a] = (const uint32_t*)b.p;
+      }
+    }
+  }
+  q->num_tiles = (uint64_t)first;
+
+  // ---- accumulators (one device block, sections 256-byte aligned)
+  q->sections.clear();
+  q->agg_section.assign(s.num_aggs, -1);
+  std::vector<std::pair<int32_t, int64_t>> sec;  // kind, elements
+  sec.push_back({PA_ACC_COUNT_U64, K});
+  for (int a = 0; a < s.num_aggs; ++a) {
+    const pa_agg_spec& A = s.aggs[a];
+    switch (A.type) {
+      case PA_AGG_COUNT: continue;
+      case PA_AGG_SUM: sec.push_back({agg_src[a] == SRC_INT ? PA_ACC_SUM_I64 : PA_ACC_SUM_F64, K}); break;
+      case PA_AGG_MIN: sec.push_back({PA_ACC_MIN_I64, K}); break;
+      case PA_AGG_MAX: sec.push_back({PA_ACC_MAX_I64, K}); break;
+      case PA_AGG_DISTINCTCOUNTHLL: sec.push_back({PA_ACC_HLL_U32, K << A.log2m}); break;
+    }
+    q->agg_section[a] = (int)sec.size() - 1;
+  }
+  size_t total = 0;
+  std::vector<size_t> offs;
+  for (auto& x : sec) {
+    offs.push_back(total);
+    const size_t es = x.first == PA_ACC_HLL_U32 ? 4 : 8;
+    total += ((size_t)x.second * es + 255) & ~(size_t)255;
+  }
+  rc = dev_alloc(q->acc, total);
+  if (rc) return rc;
+  for (size_t i = 0; i < sec.size(); ++i)
+    q->sections.push_back({sec[i].first, (char*)q->acc.p + offs[i], sec[i].second});
+
+  // ---- strategy + LDS layout
+  size_t lds_acc = ((size_t)K * 4 + 15) & ~(size_t)15;  // u32 counts
+  std::vector<size_t> agg_lds(s.num_aggs, 0);
+  for (int a = 0; a < s.num_aggs; ++a) {
+    const pa_agg_spec& A = s.aggs[a];
+    if (A.type == PA_AGG_COUNT) continue;
+    agg_lds[a] = lds_acc;
+    const size_t bytes = A.type == PA_AGG_DISTINCTCOUNTHLL ? ((size_t)K << A.log2m) * 4 : (size_t)K * 8;
+    lds_acc += (bytes + 15) & ~(size_t)15;
+  }
+  const size_t image_bytes = (size_t)kWavesPerWG * 2 * image_max * 4;
+  const size_t kLdsBudget = 160 * 1024;
+  const bool lds_ok = !(s.flags & PA_QF_FORCE_GLOBAL) && lds_acc <= 64 * 1024 && lds_acc + image_bytes <= kLdsBudget;
+  q->strategy = lds_ok ? STRAT_LDS : STRAT_GLOBAL;
+  q->lds_bytes = (int)((q->strategy == STRAT_LDS ? lds_acc : 0) + image_bytes);
+  if ((size_t)q->lds_bytes > kLdsBudget) return fail(PA_EUNSUPPORTED, "staged columns too wide for one wave-tile image");
+
+  DevQuery& h = q->hq;
+  std::memset(&h, 0, sizeof(h));
+  h.num_segments = q->nseg;
+  h.num_slots = nslots;
+  h.num_leaves = (int32_t)q->literals.size();
+  h.num_gb = s.num_group_by;
+  h.num_aggs = s.num_aggs;
+  h.strategy = q->strategy;
+  h.image_dwords_max = image_max;
+  h.num_staged = 0;
+  for (int sl = 0; sl < nslots; ++sl)
+    if (staged[sl]) h.staged_slots[h.num_staged++] = sl;
+  for (int j = 0; j < s.num_group_by; ++j) {
+    h.gb_slot[j] = gb_slot[j];
+    h.gb_stride[j] = stride[j];
+  }
+  h.num_keys = K;
+  h.total_wtiles = first;
+  h.count = (unsigned long long*)q->sections[0].ptr;
+  h.lds_count_off = 0;
+  h.lds_acc_bytes = q->strategy == STRAT_LDS ? (uint32_t)lds_acc : 0;
+  for (int a = 0; a < s.num_aggs; ++a) {
+    DevAgg& A = h.aggs[a];
+    A.type = s.aggs[a].type;
+    A.slot = agg_slot[a];
+    A.log2m = s.aggs[a].log2m;
+    A.src = agg_src[a];
+    A.lds_off = (int32_t)agg_lds[a];
+    if (q->agg_section[a] >= 0) {
+      void* p = q->sections[q->agg_section[a]].ptr;
+      A.acc_i64 = (int64_t*)p;
+      A.acc_f64 = (double*)p;
+      A.acc_hll = (uint32_t*)p;
+    }
+  }
+
+  // ---- grid: persistent waves, enough workgroups to cover the CUs several times over
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
+  }
+  int wg_per_cu = q->lds_bytes > 0 ? (int)std::min<size_t>(4, kLdsBudget / (size_t)q->lds_bytes) : 4;
+  if (wg_per_cu < 1) wg_per_cu = 1;
+  const int64_t max_wg = (int64_t)cus * wg_per_cu;
+  const int64_t want = (first + kWavesPerWG - 1) / kWavesPerWG;
+  q->grid = (int)std::max<int64_t>(1, std::min(max_wg, want));
+
+  // ---- upload descriptors
+  rc = dev_alloc(q->dq, sizeof(DevQuery));
+  if (rc) return rc;
+  rc = dev_alloc(q->dsegs, sizeof(DevSeg) * std::max(1, q->nseg));
+  if (rc) return rc;
+  PA_HIP(hipMemcpy(q->dq.p, &h, sizeof(DevQuery), hipMemcpyHostToDevice));
+  if (q->nseg) PA_HIP(hipMemcpy(q->dsegs.p, q->hsegs.data(), sizeof(DevSeg) * q->nseg, hipMemcpyHostToDevice));
+  PA_HIP(set_scan_lds_limit(q->strategy, q->lds_bytes));
+  PA_HIP(hipDeviceSynchronize());
+  q->prepared = true;
+  return PA_OK;
+}
+
+int64_t pa_query_num_keys(const pa_query* q) { return q ? q->num_keys : -1; }
+
+int pa_query_execute(pa_query* q, void* stream) {
+  if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
+  hipStream_t st = (hipStream_t)stream;
+  for (const Section& sc : q->sections) {
+    if (sc.kind == PA_ACC_MIN_I64) PA_HIP(launch_fill_i64((int64_t*)sc.ptr, sc.n, INT64_MAX, st));
+    else if (sc.kind == PA_ACC_MAX_I64) PA_HIP(launch_fill_i64((int64_t*)sc.ptr, sc.n, INT64_MIN, st));
+    else PA_HIP(hipMemsetAsync(sc.ptr, 0, (size_t)sc.n * (sc.kind == PA_ACC_HLL_U32 ? 4 : 8), st));
+  }
+  if (q->num_tiles == 0) return PA_OK;
+  PA_HIP(launch_scan(q->strategy, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p, (const DevSeg*)q->dsegs.p, st));
+  return PA_OK;
+}
+
+int32_t pa_query_num_sections(const pa_query* q) { return q ? (int32_t)q->sections.size() : -1; }
+
+void* pa_query_section(const pa_query* q, int32_t section, int32_t* kind, int64_t* num_elements) {
+  if (!q || section < 0 || section >= (int32_t)q->sections.size()) {
+    fail(PA_EINVAL, "bad section");
+    return nullptr;
+  }
+  if (kind) *kind = q->sections[section].kind;
+  if (num_elements) *num_elements = q->sections[section].n;
+  return q->sections[section].ptr;
+}
+
+int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out_keys, int64_t* out_counts,
+                       void* const* out_aggs) {
+  if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
+  hipStream_t st = (hipStream_t)stream;
+  const pa_query_spec& s = q->spec;
+  const int64_t K = q->num_keys;
+  std::vector<uint64_t> cnt(K);
+  PA_HIP(hipMemcpyAsync(cnt.data(), q->sections[0].ptr, (size_t)K * 8, hipMemcpyDeviceToHost, st));
+  PA_HIP(hipStreamSynchronize(st));
+  std::vector<int64_t> keys;
+  if (s.num_group_by == 0) {
+    keys.push_back(0);
+  } else {
+    for (int64_t k = 0; k < K; ++k)
+      if (cnt[k] != 0) keys.push_back(k);
+  }
+  const int64_t n = (int64_t)keys.size();
+  const int64_t m = std::min(n, capacity);
+  if (m <= 0) return n;
+  for (int64_t i = 0; i < m; ++i) {
+    if (out_keys) out_keys[i] = keys[i];
+    if (out_counts) out_counts[i] = (int64_t)cnt[keys[i]];
+  }
+  DevBuf dkeys;
+  int rc = dev_alloc(dkeys, (size_t)m * 8);
+  if (rc) return rc;
+  if (hipMemcpy(dkeys.p, keys.data(), (size_t)m * 8, hipMemcpyHostToDevice) != hipSuccess) {
+    dev_free(dkeys);
+    return fail(PA_EHIP, "key upload failed");
+  }
+  for (int a = 0; a < s.num_aggs; ++a) {
+    if (!out_aggs || !out_aggs[a]) continue;
+    const pa_agg_spec& A = s.aggs[a];
+    double* outd = (double*)out_aggs[a];
+    if (A.type == PA_AGG_COUNT) {
+      for (int64_t i = 0; i < m; ++i) outd[i] = (double)cnt[keys[i]];
+      continue;
+    }
+    const Section& sc = q->sections[q->agg_section[a]];
+    const int64_t per = A.type == PA_AGG_DISTINCTCOUNTHLL ? (int64_t(1) << A.log2m) : 1;
+    const int es = A.type == PA_AGG_DISTINCTCOUNTHLL ? 4 : 8;
+    DevBuf g;
+    rc = dev_alloc(g, (size_t)m * per * es);
+    if (rc) { dev_free(dkeys); return rc; }
+    std::vector<char> host((size_t)m * per * es);
+    hipError_t e = launch_gather(sc.ptr, es, per, (const int64_t*)dkeys.p, m, g.p, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(host.data(), g.p, host.size(), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    dev_free(g);
+    if (e != hipSuccess) { dev_free(dkeys); return fail(PA_EHIP, std::string("fetch: ") + hipGetErrorString(e)); }
+    const int src = q->hq.aggs[a].src;
+    if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
+      uint8_t* o = (uint8_t*)out_aggs[a];
+      const uint32_t* r = (const uint32_t*)host.data();
+      for (int64_t i = 0; i < m * per; ++i) o[i] = (uint8_t)r[i];
+    } else if (A.type == PA_AGG_SUM) {
+      for (int64_t i = 0; i < m; ++i)
+        outd[i] = src == SRC_INT ? (double)((const int64_t*)host.data())[i] : ((const double*)host.data())[i];
+    } else {  // MIN / MAX; empty aggregation-only result -> +/-inf (Min/MaxAggregationFunction DEFAULT_VALUE)
+      for (int64_t i = 0; i < m; ++i) {
+        const int64_t e8 = ((const int64_t*)host.data())[i];
+        if (cnt[keys[i]] == 0) outd[i] = A.type == PA_AGG_MIN ? __builtin_inf() : -__builtin_inf();
+        else outd[i] = src == SRC_INT ? (double)e8 : f64_order_decode(e8);
+      }
+    }
+  }
+  dev_free(dkeys);
+  return n;
+}
+
+int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs, uint64_t* num_tiles) {
+  if (!q) return fail(PA_EINVAL, "null query");
+  if (staged_bytes) *staged_bytes = q->staged_bytes;
+  if (num_docs) *num_docs = q->num_docs;
+  if (num_tiles) *num_tiles = q->num_tiles;
+  return PA_OK;
+}
+
+void pa_query_destroy(pa_query* q) { delete q; }
+
+}  // extern "C"

@@ -1,0 +1,133 @@
+// Device-side descriptors shared by the scan kernels (pa_kernels.hip) and the host layer (pa_capi.hip).
+//
+// Data layout in HBM (see DESIGN.md "Data layout"):
+//  * SV dictionary-encoded forward index: the reference's FixedBitSVForwardIndexWriter bitstream
+//    (PinotDataBitSet.java:80, value i at stream bits [i*nb, (i+1)*nb), MSB-first) with every 32-bit
+//    word byte-swapped once at upload, so word w holds stream bits [32w, 32w+32) with stream bit 32w
+//    in bit 31. Four guard words precede the stream and the stream is zero-padded to a whole number of
+//    2048-doc wave tiles plus four words, so every staged or lazy read is in bounds.
+//  * Dictionaries: int64 (INT/LONG) or double (FLOAT/DOUBLE) arrays indexed by dictId.
+//  * Raw columns: native little-endian arrays of the stored type.
+#pragma once
+#include <stdint.h>
+#include "../../include/pinot_amd.h"
+
+namespace pa {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerWG = 4;
+constexpr int kWGSize = kWave * kWavesPerWG;
+constexpr int kSteps = 32;                    // 64-doc steps per wave tile
+constexpr int kWTileDocs = kWave * kSteps;    // 2048 docs: one wave tile; 64*nb stream words per column
+constexpr int kMaxSlots = 12;                 // distinct columns referenced by one query
+constexpr int kGuardWords = 4;
+
+enum ColKind : int32_t { COL_NONE = 0, COL_SV_DICT = 1, COL_SV_RAW = 2, COL_MV_DICT = 3 };
+enum Strategy : int32_t { STRAT_LDS = 0, STRAT_GLOBAL = 1 };
+enum AccSrc : int32_t { SRC_INT = 0, SRC_DOUBLE = 1 };
+
+struct DevCol {
+  const uint32_t* words;     // SV dict: byte-swapped stream words (points past the guard words)
+  const void* raw;           // SV raw: values
+  const int64_t* dict_i64;   // INT/LONG dictionary
+  const double* dict_f64;    // FLOAT/DOUBLE dictionary
+  int32_t kind;              // ColKind
+  int32_t nbits;
+  int32_t vtype;             // PA_INT..PA_BYTES
+  int32_t lds_off;           // staged: dword offset of the column's region inside a wave image; -1 = lazy
+};
+
+struct DevLeaf {
+  int32_t kind;              // PA_LEAF_*
+  int32_t slot;
+  int32_t lo;                // DICT_RANGE: (uint)(id - lo) < (uint)span
+  int32_t span;
+  int32_t negate;
+  int32_t clause_end;        // 1 if this literal closes a CNF clause
+  const uint32_t* lut;       // DICT_SET bitmap (device)
+  int64_t ilo, ihi;
+  double dlo, dhi;
+};
+
+struct DevSeg {
+  int64_t first_wtile;       // prefix sum of wave tiles over the segment list
+  int32_t num_docs;
+  int32_t num_wtiles;
+  int32_t image_dwords;      // staged image size (dwords) of one wave tile of this segment
+  int32_t pad;
+  DevCol cols[kMaxSlots];
+  DevLeaf leaves[PA_MAX_LEAVES];
+  const int32_t* remap[PA_MAX_GROUP_BY];   // dictId -> table-wide key id (nullptr = identity)
+  const uint32_t* hll_lut[PA_MAX_AGGS];    // dictId -> (register index << 8) | rank
+};
+
+struct DevAgg {
+  int32_t type;              // PA_AGG_*
+  int32_t slot;
+  int32_t log2m;
+  int32_t src;               // AccSrc
+  int64_t* acc_i64;          // SUM(int) / MIN / MAX (ordered encoding for doubles)
+  double* acc_f64;           // SUM(double)
+  uint32_t* acc_hll;         // [num_keys << log2m]
+  int32_t lds_off;           // LDS strategy: byte offset of the WG-private copy
+  int32_t pad;
+};
+
+struct DevQuery {
+  int32_t num_segments;
+  int32_t num_slots;
+  int32_t num_leaves;        // CNF literals (clause-major)
+  int32_t num_gb;
+  int32_t num_aggs;
+  int32_t strategy;
+  int32_t num_staged;
+  int32_t image_dwords_max;  // max over segments
+  int32_t staged_slots[kMaxSlots];
+  int32_t gb_slot[PA_MAX_GROUP_BY];
+  int64_t gb_stride[PA_MAX_GROUP_BY];
+  int64_t num_keys;
+  int64_t total_wtiles;
+  unsigned long long* count; // [num_keys]
+  uint32_t lds_count_off;    // LDS strategy: byte offset of u32 count[num_keys]
+  uint32_t lds_acc_bytes;    // LDS strategy: bytes of the WG-private accumulator block
+  DevAgg aggs[PA_MAX_AGGS];
+};
+
+// Order-preserving int64 image of an IEEE double (an involution): signed int64 order == double order.
+__host__ __device__ inline int64_t f64_order_encode(double d) {
+  int64_t b = __builtin_bit_cast(int64_t, d);
+  return b >= 0 ? b : (b ^ 0x7FFFFFFFFFFFFFFFLL);
+}
+__host__ __device__ inline double f64_order_decode(int64_t e) {
+  int64_t b = e >= 0 ? e : (e ^ 0x7FFFFFFFFFFFFFFFLL);
+  return __builtin_bit_cast(double, b);
+}
+
+// stream-lib 2.9.8 com.clearspring.analytics.hash.MurmurHash#hashLong (Pinot pom.xml:1184 pins 2.9.8).
+__host__ __device__ inline int32_t murmur_hash_long(int64_t data) {
+  const uint32_t m = 0x5bd1e995u;
+  const int r = 24;
+  uint32_t h = 0;
+  uint32_t k = (uint32_t)data * m;
+  k ^= k >> r;
+  h ^= k * m;
+  k = (uint32_t)(data >> 32) * m;
+  k ^= k >> r;
+  h *= m;
+  h ^= k * m;
+  h ^= h >> 13;
+  h *= m;
+  h ^= h >> 15;
+  return (int32_t)h;
+}
+
+// stream-lib HyperLogLog#offerHashed: register index j and rank r for a 32-bit hash.
+__host__ __device__ inline uint32_t hll_slot_rank(int32_t hashed, int32_t log2m) {
+  uint32_t h = (uint32_t)hashed;
+  uint32_t j = h >> (32 - log2m);
+  uint32_t x = (h << log2m) | ((1u << (log2m - 1)) + 1u);
+  uint32_t r = (uint32_t)__builtin_clz(x) + 1u;  // x != 0 by construction
+  return (j << 8) | r;
+}
+
+}  // namespace pa

@@ -1,0 +1,16 @@
+// Host-callable launchers of the kernels in pa_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "pa_device.h"
+
+namespace pa {
+hipError_t launch_bswap_words(uint32_t* w, int64_t n, hipStream_t s);
+hipError_t launch_hll_lut_numeric(const int64_t* di, const double* dd, int32_t vtype, int32_t card, int32_t log2m,
+                                  uint32_t* lut, hipStream_t s);
+hipError_t launch_hll_lut_hashes(const int32_t* hashes, int32_t card, int32_t log2m, uint32_t* lut, hipStream_t s);
+hipError_t launch_fill_i64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
+hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t* keys, int64_t n, void* out,
+                         hipStream_t s);
+hipError_t set_scan_lds_limit(int strategy, int bytes);
+hipError_t launch_scan(int strategy, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs, hipStream_t s);
+}  // namespace pa

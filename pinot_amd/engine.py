@@ -1,0 +1,359 @@
+"""GPU segment residency + query execution through the C-ABI.
+
+Host-side mirror of the Java operator layer that stays in the JVM in a real integration:
+  GpuSegment            ~ ImmutableSegmentLoader handing forward-index PinotDataBuffers to the GPU
+  GpuQueryExecutor      ~ AggregationPlanNode/GroupByPlanNode -> AggregationOperator / GroupByOperator on every
+                          segment + AggregationCombineOperator / GroupByCombineOperator
+                          (pinot-core/.../operator/query/GroupByOperator.java:84,
+                           operator/combine/GroupByCombineOperator.java:110)
+It resolves predicates per segment (predicate.py), builds the table-wide group-key dictionaries (the value-keyed
+merge GroupByCombineOperator performs with IndexedTable.upsert), and decodes the GPU's accumulators into the
+reference's intermediate results: COUNT -> long, SUM/MIN/MAX -> double, AVG -> (sum, count),
+DISTINCTCOUNTHLL -> HyperLogLog.
+"""
+import ctypes
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from . import _lib as L
+from . import predicate as P
+from . import query as Q
+from .hll import HyperLogLog, hash_value
+from .segment import Segment
+
+_VTYPE = {"INT": L.PA_INT, "LONG": L.PA_LONG, "FLOAT": L.PA_FLOAT, "DOUBLE": L.PA_DOUBLE, "STRING": L.PA_STRING}
+
+
+class UnsupportedQuery(L.PinotAmdError):
+    pass
+
+
+def column_ids_for(segment: Segment) -> Dict[str, int]:
+    """Table-level column id assignment (stable across the segments of one table)."""
+    return {name: i for i, name in enumerate(sorted(segment.columns))}
+
+
+class GpuSegment:
+    """HBM-resident forward indexes + dictionaries of one immutable segment (a pa_segment)."""
+
+    def __init__(self, segment: Segment, columns=None, column_ids=None, device=None):
+        lib = L.lib()
+        if device is not None:
+            L.check(lib.pa_set_device(int(device)), "pa_set_device")
+        self.segment = segment
+        self.column_ids = dict(column_ids or column_ids_for(segment))
+        self.handle = L.check_ptr(lib.pa_segment_create(segment.num_docs), "pa_segment_create")
+        self._keep = []
+        for name in (columns if columns is not None else segment.columns):
+            self._add(name)
+
+    def _add(self, name):
+        lib = L.lib()
+        col = self.segment.column(name)
+        cid = self.column_ids[name]
+        vt = _VTYPE[col.data_type]
+        if col.has_dictionary:
+            hashes = None
+            if col.data_type in ("INT", "LONG"):
+                dv = np.ascontiguousarray(col.dictionary, dtype=np.int64)
+            elif col.data_type in ("FLOAT", "DOUBLE"):
+                dv = np.ascontiguousarray(col.dictionary, dtype=np.float64)
+            else:
+                dv = None
+                hashes = np.array([hash_value(v, "STRING") for v in col.dictionary.tolist()], dtype=np.int32)
+            fwd = np.ascontiguousarray(col.fwd_bytes, dtype=np.uint8)
+            L.check(lib.pa_segment_add_sv_dict_column(
+                self.handle, cid, fwd.ctypes.data, fwd.nbytes, col.num_bits, col.cardinality, vt,
+                None if dv is None else dv.ctypes.data, None if hashes is None else hashes.ctypes.data),
+                "pa_segment_add_sv_dict_column(%s)" % name)
+        else:
+            raw = np.ascontiguousarray(col.raw_values)
+            L.check(lib.pa_segment_add_raw_column(self.handle, cid, vt, raw.ctypes.data),
+                    "pa_segment_add_raw_column(%s)" % name)
+
+    @property
+    def device_bytes(self):
+        return int(L.lib().pa_segment_device_bytes(self.handle))
+
+    def close(self):
+        if self.handle:
+            L.lib().pa_segment_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class AvgPair:
+    """AvgAggregationFunction intermediate result (sum, count)."""
+    sum: float
+    count: int
+
+
+@dataclass
+class IntermediateResult:
+    """What the server returns for the segment set (AggregationResultsBlock / GroupByResultsBlock contents)."""
+    aggregations: List[Q.Aggregation]
+    group_by: List[str]
+    groups: Dict[tuple, list] = field(default_factory=dict)   # group-by: key values -> intermediate values
+    row: Optional[list] = None                                # aggregation-only
+    num_docs_scanned: int = 0
+    num_total_docs: int = 0
+    num_groups_limit_reached: bool = False
+
+
+def _flatten_filter(f, leaves, ops):
+    """Filter tree -> leaves + postfix program (PA_OP_*)."""
+    if isinstance(f, (Q.And, Q.Or)):
+        for i, c in enumerate(f.children):
+            _flatten_filter(c, leaves, ops)
+            if i:
+                ops.append(L.PA_OP_AND if isinstance(f, Q.And) else L.PA_OP_OR)
+    elif isinstance(f, Q.Not):
+        _flatten_filter(f.child, leaves, ops)
+        ops.append(L.PA_OP_NOT)
+    else:
+        ops.append(L.PA_OP_LEAF | (len(leaves) << 8))
+        leaves.append(f)
+
+
+class GpuQueryExecutor:
+    def __init__(self, query: Q.Query, gpu_segments: List[GpuSegment], flags=0, enforce_num_groups_limit=True):
+        if not gpu_segments:
+            raise ValueError("no segments")
+        self.query = query
+        self.gsegs = gpu_segments
+        self.segs = [g.segment for g in gpu_segments]
+        self.flags = flags
+        self.enforce_num_groups_limit = enforce_num_groups_limit
+        self.handle = None
+        self._plan()
+
+    # ------------------------------------------------------------------ planning
+    def _plan(self):
+        lib = L.lib()
+        q = self.query
+        ids = self.gsegs[0].column_ids
+        seg0 = self.segs[0]
+        spec = L.QuerySpec()
+
+        # aggregations -> GPU accumulators (AVG = SUM + group count)
+        self.pa_aggs = []
+        self.agg_map = []
+        for a in q.aggregations:
+            if a.function == "COUNT":
+                key = (L.PA_AGG_COUNT, -1, 0)
+            elif a.function in ("SUM", "AVG"):
+                key = (L.PA_AGG_SUM, ids[a.column], 0)
+            elif a.function == "MIN":
+                key = (L.PA_AGG_MIN, ids[a.column], 0)
+            elif a.function == "MAX":
+                key = (L.PA_AGG_MAX, ids[a.column], 0)
+            elif a.function == "DISTINCTCOUNTHLL":
+                key = (L.PA_AGG_DISTINCTCOUNTHLL, ids[a.column], a.log2m)
+            else:
+                raise UnsupportedQuery("aggregation %s" % a.function)
+            if key not in self.pa_aggs:
+                self.pa_aggs.append(key)
+            self.agg_map.append(self.pa_aggs.index(key))
+        if len(self.pa_aggs) > L.PA_MAX_AGGS:
+            raise UnsupportedQuery("too many aggregations")
+        spec.num_aggs = len(self.pa_aggs)
+        for i, (t, cid, log2m) in enumerate(self.pa_aggs):
+            spec.aggs[i].type = t
+            spec.aggs[i].column_id = max(cid, 0)
+            spec.aggs[i].log2m = log2m
+
+        # filter
+        filt = P.expand_raw_in(q.filter, seg0) if q.filter is not None else None
+        leaves, ops = [], []
+        if filt is not None:
+            _flatten_filter(filt, leaves, ops)
+        if len(leaves) > L.PA_MAX_LEAVES or len(ops) > L.PA_MAX_OPS:
+            raise UnsupportedQuery("filter too large")
+        per_seg = []
+        for seg in self.segs:
+            params = []
+            for pred in leaves:
+                col = seg.column(pred.column)
+                params.append(P.dictionary_leaf(pred, col) if col.has_dictionary else P.raw_leaf(pred, col))
+            per_seg.append(params)
+        spec.num_leaves = len(leaves)
+        for li, pred in enumerate(leaves):
+            kinds = {ps[li].kind for ps in per_seg}
+            kind = L.PA_LEAF_DICT_SET if L.PA_LEAF_DICT_SET in kinds else kinds.pop()
+            spec.leaves[li].column_id = ids[pred.column]
+            spec.leaves[li].kind = kind
+        spec.num_ops = len(ops)
+        for i, op in enumerate(ops):
+            spec.ops[i] = op
+
+        # group-by: table-wide dictionaries (value-keyed combine)
+        self.global_dicts = []
+        self.remaps = []  # [seg][gb] -> np.int32 or None
+        spec.num_group_by = len(q.group_by)
+        if spec.num_group_by > L.PA_MAX_GROUP_BY:
+            raise UnsupportedQuery("too many group-by columns")
+        for j, name in enumerate(q.group_by):
+            dicts = [s.column(name).dictionary for s in self.segs]
+            if any(not s.column(name).has_dictionary for s in self.segs):
+                raise UnsupportedQuery("group-by on a no-dictionary column")
+            first = dicts[0]
+            same = all(d is first or (len(d) == len(first) and np.array_equal(d, first)) for d in dicts)
+            gd = first if same else np.unique(np.concatenate(dicts))
+            self.global_dicts.append(gd)
+            spec.group_by_columns[j] = ids[name]
+            spec.group_by_cardinality[j] = len(gd)
+        for seg in self.segs:
+            rm = []
+            for j, name in enumerate(q.group_by):
+                d = seg.column(name).dictionary
+                gd = self.global_dicts[j]
+                if d is gd or (len(d) == len(gd) and np.array_equal(d, gd)):
+                    rm.append(None)
+                else:
+                    rm.append(np.searchsorted(gd, d).astype(np.int32))
+            self.remaps.append(rm)
+        spec.flags = self.flags
+
+        # numGroupsLimit (DictionaryBasedGroupKeyGenerator._globalGroupIdUpperBound): the per-segment first-seen
+        # group cap can only bind when a segment could produce more groups than the limit.
+        self.num_groups_limit_may_bind = False
+        if q.group_by:
+            lim = q.num_groups_limit
+            for seg in self.segs:
+                prod = 1
+                for name in q.group_by:
+                    prod *= seg.column(name).cardinality
+                if min(prod, seg.num_docs) > lim:
+                    self.num_groups_limit_may_bind = True
+            if self.num_groups_limit_may_bind and self.enforce_num_groups_limit:
+                raise UnsupportedQuery("numGroupsLimit=%d may bind for this segment set (first-seen group trimming is "
+                                       "not implemented on the GPU yet); raise OPTION(numGroupsLimit=...)" % lim)
+
+        self.spec = spec
+        self.handle = L.check_ptr(lib.pa_query_create(ctypes.byref(spec), len(self.segs)), "pa_query_create")
+        self._keep = []
+        for si, (g, params) in enumerate(zip(self.gsegs, per_seg)):
+            arr = (L.LeafParams * max(1, len(params)))()
+            for li, p in enumerate(params):
+                lp = arr[li]
+                if isinstance(p, P.DictLeaf):
+                    lp.negate = int(p.negate)
+                    if spec.leaves[li].kind == L.PA_LEAF_DICT_SET:
+                        ids_ = p.ids if p.ids is not None else np.arange(p.lo, p.hi, dtype=np.int32)
+                        lut = P.DictLeaf(L.PA_LEAF_DICT_SET, ids=ids_).lut_words(self.segs[si].column(leaves[li].column).cardinality)
+                        self._keep.append(lut)
+                        lp.lut = lut.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+                    else:
+                        lp.lo, lp.hi = p.lo, p.hi
+                else:
+                    lp.negate = int(p.negate)
+                    lp.ilo = max(min(int(p.ilo), P.LONG_MAX), P.LONG_MIN)
+                    lp.ihi = max(min(int(p.ihi), P.LONG_MAX), P.LONG_MIN)
+                    lp.dlo, lp.dhi = float(p.dlo), float(p.dhi)
+            rms = (ctypes.c_void_p * max(1, len(q.group_by)))()
+            for j, rm in enumerate(self.remaps[si]):
+                if rm is not None:
+                    self._keep.append(rm)
+                    rms[j] = rm.ctypes.data
+            L.check(lib.pa_query_bind_segment(self.handle, si, g.handle, arr, rms), "pa_query_bind_segment")
+        L.check(lib.pa_query_prepare(self.handle), "pa_query_prepare")
+        self.num_keys = int(lib.pa_query_num_keys(self.handle))
+        self.strides = []
+        s = 1
+        for gd in self.global_dicts:
+            self.strides.append(s)
+            s *= len(gd)
+
+    # ------------------------------------------------------------------ execution
+    def execute(self, stream=None):
+        L.check(L.lib().pa_query_execute(self.handle, stream), "pa_query_execute")
+
+    def sections(self):
+        """[(kind, device_ptr, num_elements)] accumulator sections (for the cross-GPU reduce)."""
+        lib = L.lib()
+        out = []
+        for i in range(lib.pa_query_num_sections(self.handle)):
+            kind, n = ctypes.c_int32(), ctypes.c_int64()
+            p = L.check_ptr(lib.pa_query_section(self.handle, i, ctypes.byref(kind), ctypes.byref(n)), "section")
+            out.append((kind.value, p, n.value))
+        return out
+
+    def stats(self):
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        L.check(L.lib().pa_query_stats(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "stats")
+        return {"staged_bytes": a.value, "num_docs": b.value, "num_wave_tiles": c.value}
+
+    def fetch(self, stream=None) -> IntermediateResult:
+        lib = L.lib()
+        q = self.query
+        cap = 1 if not q.group_by else min(self.num_keys, 1 << 16)
+        while True:
+            keys = np.zeros(cap, dtype=np.int64)
+            counts = np.zeros(cap, dtype=np.int64)
+            outs, ptrs = [], (ctypes.c_void_p * max(1, len(self.pa_aggs)))()
+            for i, (t, _, log2m) in enumerate(self.pa_aggs):
+                o = np.zeros(cap << log2m, dtype=np.uint8) if t == L.PA_AGG_DISTINCTCOUNTHLL else np.zeros(cap, dtype=np.float64)
+                outs.append(o)
+                ptrs[i] = o.ctypes.data
+            n = L.check(lib.pa_query_fetch(self.handle, stream, cap, keys.ctypes.data, counts.ctypes.data, ptrs),
+                        "pa_query_fetch")
+            if n <= cap:
+                break
+            cap = n
+        res = IntermediateResult(list(q.aggregations), list(q.group_by))
+        res.num_total_docs = sum(s.num_docs for s in self.segs)
+        res.num_docs_scanned = int(counts[:n].sum())
+        # decode key ids -> values
+        key_cols = []
+        for j, gd in enumerate(self.global_dicts):
+            ids = (keys[:n] // self.strides[j]) % len(gd)
+            key_cols.append(gd[ids])
+        for r in range(n):
+            vals = []
+            for a, pi in zip(q.aggregations, self.agg_map):
+                t, _, log2m = self.pa_aggs[pi]
+                if a.function == "COUNT":
+                    vals.append(int(counts[r]))
+                elif a.function == "AVG":
+                    vals.append(AvgPair(float(outs[pi][r]), int(counts[r])))
+                elif a.function == "DISTINCTCOUNTHLL":
+                    m = 1 << log2m
+                    vals.append(HyperLogLog(log2m, outs[pi][r * m:(r + 1) * m]))
+                else:
+                    vals.append(float(outs[pi][r]))
+            if q.group_by:
+                res.groups[tuple(_py(kc[r]) for kc in key_cols)] = vals
+            else:
+                res.row = vals
+        if q.group_by:
+            res.num_groups_limit_reached = len(res.groups) >= q.num_groups_limit
+        return res
+
+    def run(self, stream=None) -> IntermediateResult:
+        self.execute(stream)
+        return self.fetch(stream)
+
+    def close(self):
+        if self.handle:
+            L.lib().pa_query_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _py(v):
+    if isinstance(v, np.generic):
+        return v.item()
+    return v

@@ -1,0 +1,125 @@
+"""Server trim + broker reduce of intermediate results (the callers either side of the hot path).
+
+  merge_intermediate   ~ GroupByDataTableReducer / AggregationDataTableReducer merging server DataTables
+                         (AggregationFunction.merge: COUNT/SUM +, MIN min, MAX max, AVG pair +, HLL addAll)
+  server_trim          ~ IndexedTable.finish on the server (IndexedTable.java:149): with ORDER BY keep the top
+                         max(limit*5, minServerGroupTrimSize) groups (GroupByUtils.getTableCapacity); without
+                         ORDER BY keep `limit` groups (GroupByCombineOperator.java:63-73)
+  final_result_table   ~ broker: extractFinalResult (AVG sum/count, HLL cardinality), ORDER BY, LIMIT
+"""
+import math
+from functools import cmp_to_key
+
+from . import query as Q
+from .engine import AvgPair, IntermediateResult
+from .hll import HyperLogLog
+
+
+def merge_value(fn, a, b):
+    if fn in ("COUNT", "SUM"):
+        return a + b
+    if fn == "MIN":
+        return min(a, b)
+    if fn == "MAX":
+        return max(a, b)
+    if fn == "AVG":
+        return AvgPair(a.sum + b.sum, a.count + b.count)
+    if fn == "DISTINCTCOUNTHLL":
+        return HyperLogLog(a.log2m, a.registers).add_all(b)
+    raise ValueError(fn)
+
+
+def final_value(fn, v):
+    if fn == "AVG":
+        return v.sum / v.count if v.count else -math.inf
+    if fn == "DISTINCTCOUNTHLL":
+        return v.cardinality()
+    return v
+
+
+def merge_intermediate(results):
+    results = list(results)
+    out = IntermediateResult(results[0].aggregations, results[0].group_by)
+    fns = [a.function for a in out.aggregations]
+    for r in results:
+        out.num_docs_scanned += r.num_docs_scanned
+        out.num_total_docs += r.num_total_docs
+        out.num_groups_limit_reached |= r.num_groups_limit_reached
+        if out.group_by:
+            for k, vals in r.groups.items():
+                if k in out.groups:
+                    out.groups[k] = [merge_value(f, a, b) for f, a, b in zip(fns, out.groups[k], vals)]
+                else:
+                    out.groups[k] = list(vals)
+        elif out.row is None:
+            out.row = list(r.row)
+        else:
+            out.row = [merge_value(f, a, b) for f, a, b in zip(fns, out.row, r.row)]
+    return out
+
+
+def _order_key_fn(query):
+    """Comparator over (key, final values) following ORDER BY; ties broken by group key for determinism."""
+    items = []
+    for ob in query.order_by:
+        if isinstance(ob.expr, Q.Aggregation):
+            idx = None
+            for i, a in enumerate(query.aggregations):
+                if a == ob.expr:
+                    idx = i
+            if idx is None:
+                raise ValueError("ORDER BY aggregation not in select list: %r" % (ob.expr,))
+            items.append(("agg", idx, ob.asc))
+        else:
+            items.append(("key", query.group_by.index(ob.expr), ob.asc))
+
+    def cmp(x, y):
+        for kind, idx, asc in items:
+            a = x[1][idx] if kind == "agg" else x[0][idx]
+            b = y[1][idx] if kind == "agg" else y[0][idx]
+            if a != b:
+                c = -1 if a < b else 1
+                return c if asc else -c
+        return -1 if x[0] < y[0] else (1 if x[0] > y[0] else 0)
+    return cmp_to_key(cmp)
+
+
+def server_trim(res: IntermediateResult, query: Q.Query) -> IntermediateResult:
+    if not query.group_by:
+        return res
+    fns = [a.function for a in query.aggregations]
+    if query.order_by:
+        trim = max(query.limit * 5, query.min_server_group_trim_size)
+    else:
+        trim = query.limit
+    if len(res.groups) <= trim:
+        return res
+    rows = [(k, [final_value(f, v) for f, v in zip(fns, vals)], k) for k, vals in res.groups.items()]
+    if query.order_by:
+        rows.sort(key=_order_key_fn(query))
+    else:
+        rows.sort(key=lambda r: r[0])
+    keep = {r[2] for r in rows[:trim]}
+    out = IntermediateResult(res.aggregations, res.group_by, {k: v for k, v in res.groups.items() if k in keep})
+    out.num_docs_scanned, out.num_total_docs = res.num_docs_scanned, res.num_total_docs
+    out.num_groups_limit_reached = res.num_groups_limit_reached
+    return out
+
+
+def final_result_table(res: IntermediateResult, query: Q.Query):
+    """Broker ResultTable rows: [select group-by columns..., final aggregation values...]."""
+    fns = [a.function for a in query.aggregations]
+    nsel = query.num_select_aggs if query.num_select_aggs >= 0 else len(fns)
+    if not query.group_by:
+        return [[final_value(f, v) for f, v in zip(fns, res.row)][:nsel]]
+    rows = [(k, [final_value(f, v) for f, v in zip(fns, vals)]) for k, vals in res.groups.items()]
+    if query.order_by:
+        rows.sort(key=_order_key_fn(query))
+    else:
+        rows.sort(key=lambda r: r[0])
+    rows = rows[: query.limit]
+    sel = query.select_columns
+    out = []
+    for k, vals in rows:
+        out.append([k[query.group_by.index(c)] for c in sel] + vals[:nsel])
+    return out

@@ -1,0 +1,48 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through the C-ABI)")
+
+
+@pytest.fixture(scope="session")
+def golden_spec():
+    with open(os.path.join(GOLDEN, "sv_queries.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def golden_segment(golden_spec):
+    """The reference's BaseSingleValueQueriesTest segment, rebuilt by our segment creator."""
+    from pinot_amd.segment import create_segment
+    data = np.load(os.path.join(GOLDEN, "test_data_sv.npz"))
+    return create_segment("testTable_126164076_167572854", {k: data[k] for k in data.files}, golden_spec["schema"])
+
+
+def rows_match(got, expected, delta):
+    if len(got) != len(expected):
+        return False
+    for g, e in zip(got, expected):
+        if len(g) != len(e):
+            return False
+        for a, b in zip(g, e):
+            if isinstance(b, str) or isinstance(a, str):
+                if a != b:
+                    return False
+            elif delta:
+                if abs(float(a) - float(b)) > delta:
+                    return False
+            elif float(a) != float(b):
+                return False
+    return True

@@ -1,0 +1,169 @@
+"""Generates the committed golden fixtures from the reference's OWN test input and expected results.
+
+Run here (needs /root/reference; the GPU box never runs this):  python tests/golden/make_golden.py
+
+  test_data_sv.npz   the 11 columns BaseSingleValueQueriesTest.java:95-104 selects from
+                     pinot-core/src/test/resources/data/test_data-sv.avro (30000 rows, no nulls)
+  sv_queries.json    queries + expected broker ResultTables transcribed from
+                     pinot-core/src/test/java/org/apache/pinot/queries/InterSegmentAggregationSingleValueQueriesTest.java
+                     and InterSegmentGroupBySingleValueQueriesTest.java (source file:line in every case).
+                     Those tests run on 2 servers x 2 identical segments (BaseQueriesTest.java:200-230,
+                     BaseSingleValueQueriesTest.java:139), i.e. 4 copies of the segment.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import avro_min  # noqa: E402
+
+AVRO = "/root/reference/pinot-core/src/test/resources/data/test_data-sv.avro"
+SCHEMA = {  # BaseSingleValueQueriesTest.java:95-104
+    "column1": "INT", "column3": "INT", "column5": "STRING", "column6": "INT", "column7": "INT",
+    "column9": "INT", "column11": "STRING", "column12": "STRING", "column17": "INT", "column18": "INT",
+    "daysSinceEpoch": "INT",
+}
+
+AGG = "pinot-core/src/test/java/org/apache/pinot/queries/InterSegmentAggregationSingleValueQueriesTest.java"
+GBY = "pinot-core/src/test/java/org/apache/pinot/queries/InterSegmentGroupBySingleValueQueriesTest.java"
+FILTER = (" WHERE column1 > 100000000 AND column3 BETWEEN 20000000 AND 1000000000 AND column5 = 'gFuH'"
+          " AND (column6 < 500000000 OR column11 NOT IN ('t', 'P')) AND daysSinceEpoch = 126164076")
+GROUP_BY = " GROUP BY column9 ORDER BY v1 DESC, v2 DESC LIMIT 1"
+
+CASES = []
+
+
+def case(source, sql, rows, delta=0.0):
+    CASES.append({"source": source, "sql": sql, "rows": rows, "delta": delta})
+
+
+# ---- InterSegmentAggregationSingleValueQueriesTest
+q = "SELECT COUNT(*) FROM testTable"
+case(AGG + ":47-50", q, [[120000]])
+case(AGG + ":52-54", q + FILTER, [[24516]])
+gb = " GROUP BY column9 ORDER BY COUNT(*) DESC LIMIT 1"
+case(AGG + ":56-59", q + gb, [[64420]])
+case(AGG + ":61-63", q + FILTER + gb, [[17080]])
+q = "SELECT MAX(column1) AS v1, MAX(column3) AS v2 FROM testTable"
+case(AGG + ":89-100", q, [[2146952047.0, 2147419555.0]])
+case(AGG + ":102-105", q + FILTER, [[2146952047.0, 999813884.0]])
+case(AGG + ":107-110", q + GROUP_BY, [[2146952047.0, 2146630496.0]])
+case(AGG + ":112-115", q + FILTER + GROUP_BY, [[2146952047.0, 999813884.0]])
+q = "SELECT MIN(column1) AS v1, MIN(column3) AS v2 FROM testTable"
+gb = " GROUP BY column9 ORDER BY v1, v2 LIMIT 1"
+case(AGG + ":119-130", q, [[240528.0, 17891.0]])
+case(AGG + ":132-135", q + FILTER, [[101116473.0, 20396372.0]])
+case(AGG + ":137-141", q + gb, [[240528.0, 17891.0]])
+case(AGG + ":143-146", q + FILTER + gb, [[101116473.0, 91804599.0]])
+q = "SELECT SUM(column1) AS v1, SUM(column3) AS v2 FROM testTable"
+case(AGG + ":150-158", q, [[129268741751388.0, 129156636756600.0]])
+case(AGG + ":160-163", q + FILTER, [[27503790384288.0, 12429178874916.0]])
+case(AGG + ":165-168", q + GROUP_BY, [[69526727335224.0, 69225631719808.0]])
+case(AGG + ":170-173", q + FILTER + GROUP_BY, [[19058003631876.0, 8606725456500.0]])
+q = "SELECT AVG(column1) AS v1, AVG(column3) AS v2 FROM testTable"
+case(AGG + ":177-185", q, [[1077239514.5949, 1076305306.305]], 1e-5)
+case(AGG + ":187-191", q + FILTER, [[1121871038.68037, 506982332.96280]], 1e-5)
+case(AGG + ":193-197", q + GROUP_BY, [[2142595699.0, 334963174.0]])
+case(AGG + ":199-202", q + FILTER + GROUP_BY, [[2142595699.0, 334963174.0]])
+q = "SELECT DISTINCTCOUNTHLL(column1) AS v1, DISTINCTCOUNTHLL(column3) AS v2 FROM testTable"
+case(AGG + ":261-271", q, [[5977, 23825]])
+case(AGG + ":273-275", q + FILTER, [[1886, 4492]])
+case(AGG + ":277-279", q + GROUP_BY, [[3592, 11889]])
+case(AGG + ":281-283", q + FILTER + GROUP_BY, [[1324, 3197]])
+
+# ---- InterSegmentGroupBySingleValueQueriesTest.groupByOrderByDataProvider
+c11 = [["", 5935285005452.0], ["P", 88832999206836.0], ["gFuH", 63202785888.0], ["o", 18105331533948.0],
+       ["t", 16331923219264.0]]
+case(GBY + ":66-71", "SELECT column11, SUM(column1) FROM testTable GROUP BY column11 ORDER BY column11", c11)
+case(GBY + ":73-77", "SELECT column11, sum(column1) FROM testTable GROUP BY column11 ORDER BY column11 DESC",
+     list(reversed(c11)))
+case(GBY + ":79-84", "SELECT column11, Sum(column1) FROM testTable GROUP BY column11 ORDER BY column11 LIMIT 3",
+     c11[:3])
+two = [["", "HEuxNvH", 3789390396216.0], ["", "KrNxpdycSiwoRohEiTIlLqDHnx", 733802350944.0],
+       ["", "MaztCmmxxgguBUxPti", 1333941430664.0], ["", "dJWwFk", 55470665124.0],
+       ["", "oZgnrlDEtjjVpUoFLol", 22680162504.0], ["P", "HEuxNvH", 21998672845052.0],
+       ["P", "KrNxpdycSiwoRohEiTIlLqDHnx", 18069909216728.0], ["P", "MaztCmmxxgguBUxPti", 27177029040008.0],
+       ["P", "TTltMtFiRqUjvOG", 4462670055540.0], ["P", "XcBNHe", 120021767504.0]]
+case(GBY + ":86-99", "SELECT column11, column12, SUM(column1) FROM testTable GROUP BY column11, column12 "
+     "ORDER BY column11, column12", two)
+case(GBY + ":101-110", "SELECT column11, column12, SUM(column1) FROM testTable GROUP BY column11, column12 "
+     "ORDER BY column11, column12 LIMIT 15",
+     two + [["P", "dJWwFk", 6224665921376.0], ["P", "fykKFqiw", 1574451324140.0], ["P", "gFuH", 860077643636.0],
+            ["P", "oZgnrlDEtjjVpUoFLol", 8345501392852.0], ["gFuH", "HEuxNvH", 29872400856.0]])
+case(GBY + ":112-121", "SELECT column11, column12, SUM(column1) FROM testTable GROUP BY column11, column12 "
+     "ORDER BY column11, column12 DESC",
+     [["", "oZgnrlDEtjjVpUoFLol", 22680162504.0], ["", "dJWwFk", 55470665124.0],
+      ["", "MaztCmmxxgguBUxPti", 1333941430664.0], ["", "KrNxpdycSiwoRohEiTIlLqDHnx", 733802350944.0],
+      ["", "HEuxNvH", 3789390396216.0], ["P", "oZgnrlDEtjjVpUoFLol", 8345501392852.0],
+      ["P", "gFuH", 860077643636.0], ["P", "fykKFqiw", 1574451324140.0], ["P", "dJWwFk", 6224665921376.0],
+      ["P", "XcBNHe", 120021767504.0]])
+case(GBY + ":123-132", "SELECT column11, column12, SUM(column1) FROM testTable GROUP BY column11, column12 "
+     "ORDER BY column11, sum(column1)",
+     [["", "oZgnrlDEtjjVpUoFLol", 22680162504.0], ["", "dJWwFk", 55470665124.0],
+      ["", "KrNxpdycSiwoRohEiTIlLqDHnx", 733802350944.0], ["", "MaztCmmxxgguBUxPti", 1333941430664.0],
+      ["", "HEuxNvH", 3789390396216.0], ["P", "XcBNHe", 120021767504.0], ["P", "gFuH", 860077643636.0],
+      ["P", "fykKFqiw", 1574451324140.0], ["P", "TTltMtFiRqUjvOG", 4462670055540.0],
+      ["P", "dJWwFk", 6224665921376.0]])
+case(GBY + ":134-157", "SELECT column11, column12, SUM(column1) FROM testTable GROUP BY column11, column12 "
+     "ORDER BY SUM(column1) DESC LIMIT 50",
+     [["P", "MaztCmmxxgguBUxPti", 27177029040008.0], ["P", "HEuxNvH", 21998672845052.0],
+      ["P", "KrNxpdycSiwoRohEiTIlLqDHnx", 18069909216728.0], ["P", "oZgnrlDEtjjVpUoFLol", 8345501392852.0],
+      ["o", "MaztCmmxxgguBUxPti", 6905624581072.0], ["P", "dJWwFk", 6224665921376.0],
+      ["o", "HEuxNvH", 5026384681784.0], ["t", "MaztCmmxxgguBUxPti", 4492405624940.0],
+      ["P", "TTltMtFiRqUjvOG", 4462670055540.0], ["t", "HEuxNvH", 4424489490364.0],
+      ["o", "KrNxpdycSiwoRohEiTIlLqDHnx", 4051812250524.0], ["", "HEuxNvH", 3789390396216.0],
+      ["t", "KrNxpdycSiwoRohEiTIlLqDHnx", 3529048341192.0], ["P", "fykKFqiw", 1574451324140.0],
+      ["t", "dJWwFk", 1349058948804.0], ["", "MaztCmmxxgguBUxPti", 1333941430664.0],
+      ["o", "dJWwFk", 1152689463360.0], ["t", "oZgnrlDEtjjVpUoFLol", 1039101333316.0],
+      ["P", "gFuH", 860077643636.0], ["", "KrNxpdycSiwoRohEiTIlLqDHnx", 733802350944.0],
+      ["o", "oZgnrlDEtjjVpUoFLol", 699381633640.0], ["t", "TTltMtFiRqUjvOG", 675238030848.0],
+      ["t", "fykKFqiw", 480973878052.0], ["t", "gFuH", 330331507792.0],
+      ["o", "TTltMtFiRqUjvOG", 203835153352.0], ["P", "XcBNHe", 120021767504.0],
+      ["o", "fykKFqiw", 62975165296.0], ["", "dJWwFk", 55470665124.0],
+      ["gFuH", "HEuxNvH", 29872400856.0], ["gFuH", "MaztCmmxxgguBUxPti", 29170832184.0],
+      ["", "oZgnrlDEtjjVpUoFLol", 22680162504.0], ["t", "XcBNHe", 11276063956.0],
+      ["gFuH", "KrNxpdycSiwoRohEiTIlLqDHnx", 4159552848.0], ["o", "gFuH", 2628604920.0]])
+case(GBY + ":159-167", "SELECT sum(column1), MIN(column6) FROM testTable GROUP BY column11 ORDER BY column11",
+     [[5935285005452.0, 2.96467636E8], [88832999206836.0, 1689277.0], [63202785888.0, 2.96467636E8],
+      [18105331533948.0, 2.96467636E8], [16331923219264.0, 1980174.0]])
+case(GBY + ":169-178", "SELECT column11, column12, SUM(column1) FROM testTable GROUP BY column11, column12 "
+     "ORDER BY SUM  (\tcolumn1) DESC LIMIT 3",
+     [["P", "MaztCmmxxgguBUxPti", 27177029040008.0], ["P", "HEuxNvH", 21998672845052.0],
+      ["P", "KrNxpdycSiwoRohEiTIlLqDHnx", 18069909216728.0]])
+c12min = [["XcBNHe", 329467557.0], ["fykKFqiw", 296467636.0], ["gFuH", 296467636.0], ["HEuxNvH", 6043515.0],
+          ["MaztCmmxxgguBUxPti", 6043515.0], ["dJWwFk", 6043515.0], ["KrNxpdycSiwoRohEiTIlLqDHnx", 1980174.0],
+          ["TTltMtFiRqUjvOG", 1980174.0], ["oZgnrlDEtjjVpUoFLol", 1689277.0]]
+case(GBY + ":180-189", "SELECT column12, MIN(column6) FROM testTable GROUP BY column12 "
+     "ORDER BY Min(column6) DESC, column12", c12min)
+case(GBY + ":191-198", "SELECT column12 FROM testTable GROUP BY column12 ORDER BY Min(column6) DESC, column12",
+     [[r[0]] for r in c12min])
+case(GBY + ":200-204", "SELECT column12 FROM testTable GROUP BY column12 ORDER BY Min(column6) DESC, "
+     "SUM(column1) LIMIT 3", [["XcBNHe"], ["gFuH"], ["fykKFqiw"]])
+case(GBY + ":206-213", "SELECT column12, MIN(column6) FROM testTable GROUP BY column12 "
+     "ORDER BY Min(column6) DESC, SUM(column1) LIMIT 3",
+     [["XcBNHe", 329467557.0], ["gFuH", 296467636.0], ["fykKFqiw", 296467636.0]])
+case(GBY + ":215-225", "select column17, count(*) from testTable group by column17 order by column17 limit 15",
+     [[83386499, 2924], [217787432, 3892], [227908817, 6564], [402773817, 7304], [423049234, 6556],
+      [561673250, 7420], [635942547, 3308], [638936844, 3816], [939479517, 3116], [984091268, 3824],
+      [1230252339, 5620], [1284373442, 7428], [1555255521, 2900], [1618904660, 2744], [1670085862, 3388]])
+
+
+def main():
+    _, recs = avro_min.read_avro(AVRO)
+    cols = {}
+    for name, dt in SCHEMA.items():
+        vals = [r[name] for r in recs]
+        assert all(v is not None for v in vals), name
+        cols[name] = np.array(vals, dtype=np.int32) if dt == "INT" else np.array(vals).astype(str)
+    np.savez_compressed(os.path.join(HERE, "test_data_sv.npz"), **cols)
+    with open(os.path.join(HERE, "sv_queries.json"), "w") as f:
+        json.dump({"schema": SCHEMA, "copies": 4, "servers": 2, "segments_per_server": 2, "cases": CASES},
+                  f, indent=1)
+    print("wrote %d rows, %d cases" % (len(recs), len(CASES)))
+
+
+if __name__ == "__main__":
+    main()
