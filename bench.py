@@ -1,0 +1,230 @@
+"""Headline benchmark: rows/sec scanned + %HBM roofline for filter + GROUP BY SUM (BASELINE.json).
+
+Workload (BASELINE.json configs[1]): the README AdAnalytics query
+  SELECT sum(clicks), sum(impressions) FROM AdAnalyticsTable
+  WHERE daysSinceEpoch BETWEEN 17849 AND 17856 AND accountId IN (123456789)
+  GROUP BY daysSinceEpoch TOP 100
+over 1B rows = 100 synthetic segments x 10M docs PER GPU (weak scaling: N GPUs scan N billion rows; configs[3]).
+Columns are dictionary-encoded fixed-bit forward indexes (daysSinceEpoch INT 512 days = 9 bits, accountId INT
+2^17 accounts = 17 bits, clicks LONG 1024 values = 10 bits, impressions LONG 16384 values = 14 bits), with
+uniformly random dictIds; data is synthetic, generated on the host and resident in HBM before timing.
+
+A step = one execution of the query over the rank's whole segment set: accumulator reset + the fused HIP scan
+kernel + (N>1) the RCCL reduce of partial aggregates to rank 0 + rank 0's fetch/decode of the groups.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "rows/sec scanned + %HBM roofline, filter+GROUP BY SUM at 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+QUERY = ("SELECT sum(clicks), sum(impressions) FROM AdAnalyticsTable WHERE daysSinceEpoch BETWEEN 17849 AND 17856 "
+         "AND accountId IN (123456789) GROUP BY daysSinceEpoch TOP 100")
+COLUMNS = {  # name: (type, cardinality, dictionary values)
+    "daysSinceEpoch": ("INT", 512, lambda: np.arange(17532, 17532 + 512, dtype=np.int64)),
+    "accountId": ("INT", 1 << 17, lambda: 123456789 + (np.arange(1 << 17, dtype=np.int64) - (1 << 16)) * 997),
+    "clicks": ("LONG", 1024, lambda: np.arange(1024, dtype=np.int64)),
+    "impressions": ("LONG", 1 << 14, lambda: np.arange(1 << 14, dtype=np.int64) * 3),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_segment(seed, docs):
+    from pinot_amd.segment import segment_from_dict_ids
+    rng = np.random.default_rng(seed)
+    specs = {}
+    for name, (dt, card, dvals) in COLUMNS.items():
+        nb = int(card - 1).bit_length()
+        nbytes = (docs * nb + 7) // 8
+        # uniform dictIds over [0, 2^nb) == uniformly random bytes, because card == 2^nb
+        specs[name] = (dt, dvals(), np.frombuffer(rng.bytes(nbytes), dtype=np.uint8))
+    return segment_from_dict_ids("AdAnalytics_%d" % seed, docs, specs)
+
+
+def load_traffic(workload, docs, nseg):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), if it matches this shape."""
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % workload)
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        if d.get("docs_per_segment") == docs and d.get("segments") == nseg:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def cpu_baseline(query, host_segments):
+    """Oracle (the scalar C port of the reference's per-doc path) on the host cores, one segment per thread
+    like the reference's combine operator's per-segment tasks."""
+    import oracle
+    from concurrent.futures import ThreadPoolExecutor
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except Exception:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(16, cores, len(host_segments)))
+    oracle.lib()
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        list(ex.map(lambda s: oracle.run_segment(query, s), host_segments))
+    dt = time.perf_counter() - t0
+    rows = sum(s.num_docs for s in host_segments)
+    return {"value": rows / dt, "unit": "rows/s", "cores": cores, "kind": "port",
+            "sample": "%d segments x %d docs (%.2f s wall)" % (len(host_segments), host_segments[0].num_docs, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--segments", type=int, default=100, help="segments per GPU")
+    ap.add_argument("--docs", type=int, default=10_000_000, help="docs per segment")
+    ap.add_argument("--cpu-sample", type=int, default=16, help="segments in the CPU baseline sample (0 = skip)")
+    ap.add_argument("--flags", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+
+    from pinot_amd import parse_sql
+    from pinot_amd.engine import GpuQueryExecutor, GpuSegment
+    from pinot_amd.parallel import DistributedAccumulators, shard_segments
+
+    q = parse_sql(QUERY)
+    total_segments = args.segments * world
+    mine = shard_segments(total_segments, rank, world)
+    t_setup = time.perf_counter()
+    gsegs, host_sample = [], []
+    cids = None
+    for i in mine:
+        seg = make_segment(1000 + i, args.docs)
+        if cids is None:
+            cids = {n: j for j, n in enumerate(sorted(seg.columns))}
+        gsegs.append(GpuSegment(seg, column_ids=cids, device=local))
+        if rank == 0 and len(host_sample) < args.cpu_sample:
+            host_sample.append(seg)
+        else:
+            for c in seg.columns.values():  # HBM holds the forward index now; keep only the dictionaries
+                c.fwd_bytes = None
+    log("rank %d: %d segments (%d rows) resident, %.1f GB HBM, setup %.1f s" % (
+        rank, len(gsegs), sum(g.segment.num_docs for g in gsegs), sum(g.device_bytes for g in gsegs) / 1e9,
+        time.perf_counter() - t_setup))
+
+    ex = GpuQueryExecutor(q, gsegs, flags=args.flags)
+    dacc = DistributedAccumulators(ex, device) if world > 1 else None
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+
+    def step():
+        ex.execute(sptr)
+        if dacc is not None:
+            dacc.reduce(dst=0)
+        if rank == 0:
+            return ex.fetch(sptr)
+        return None
+
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize()
+
+    # kernel-only timing with HIP events on the launch stream (accumulator reset + fused scan)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for a, b in ev:
+        a.record(stream)
+        ex.execute(sptr)
+        b.record(stream)
+    torch.cuda.synchronize()
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    st = ex.stats()
+    rows_per_gpu = st["num_docs"]
+    total_rows = rows_per_gpu * world
+    if rank == 0:
+        algo_bytes = st["staged_bytes"]  # forward-index bytes the filter must read (lazy post-filter reads ~0)
+        achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
+        cpu = cpu_baseline(q, host_sample) if host_sample else None
+        out = {
+            "metric": METRIC,
+            "value": total_rows * args.steps / elapsed,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic",
+            "config": {
+                "workload": "adanalytics_readme_query",
+                "query": QUERY,
+                "rows_per_gpu": rows_per_gpu,
+                "segments_per_gpu": len(gsegs),
+                "docs_per_segment": args.docs,
+                "columns": {k: {"type": v[0], "cardinality": v[1], "bits": int(v[1] - 1).bit_length()}
+                            for k, v in COLUMNS.items()},
+                "parallelism": "segment-sharded dp%d, RCCL reduce of partial aggregates" % world,
+                "groups": len(res.groups) if res is not None else None,
+                "matched_docs_rank0": res.num_docs_scanned if res is not None else None,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": load_traffic("adanalytics", args.docs, len(gsegs)),
+                "kernel_ms": kernel_ms,
+                "algorithmic_bytes_per_launch": algo_bytes,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    ex.close()
+    for g in gsegs:
+        g.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

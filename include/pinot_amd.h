@@ -198,6 +198,12 @@ int pa_query_execute(pa_query* q, void* stream);
 #define PA_ACC_MIN_I64 3   /* reduce MIN (ordered encoding for floating values) */
 #define PA_ACC_MAX_I64 4   /* reduce MAX */
 #define PA_ACC_HLL_U32 5   /* reduce MAX */
+#define PA_ACC_SUM_I64X2 6 /* reduce SUM; [2k] = sum of low 32 bits (unsigned), [2k+1] = sum of high 32 bits */
+/* All sections live in one device block of pa_query_accumulator_bytes() bytes (256-byte aligned sections).
+ * pa_query_set_accumulator_buffer lets the caller own that block (e.g. memory its collective library
+ * registered) instead of the library: call after pa_query_prepare; `bytes` must be >= the size. */
+uint64_t pa_query_accumulator_bytes(const pa_query* q);
+int pa_query_set_accumulator_buffer(pa_query* q, void* device_buffer, uint64_t bytes);
 int32_t pa_query_num_sections(const pa_query* q);
 /* returns device pointer, writes kind and element count */
 void* pa_query_section(const pa_query* q, int32_t section, int32_t* kind, int64_t* num_elements);

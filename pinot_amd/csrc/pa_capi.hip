@@ -65,6 +65,7 @@ struct Column {
   int32_t nbits = 0;
   int32_t cardinality = 0;
   int64_t total_values = 0;
+  bool fits_int32 = false;  // every dictionary value (INT/LONG) fits in int32
   DevBuf words;   // guard + stream + pad (SV dict)
   DevBuf raw;     // raw values (SV raw)
   DevBuf dict;    // int64 or double
@@ -97,6 +98,11 @@ int upload_dict(Column* c, int32_t vtype, int32_t card, const void* dict_values,
     int rc = dev_alloc(c->dict, (size_t)card * 8);
     if (rc) return rc;
     PA_HIP(hipMemcpy(c->dict.p, dict_values, (size_t)card * 8, hipMemcpyHostToDevice));
+    if (vtype == PA_INT || vtype == PA_LONG) {
+      const int64_t* v = (const int64_t*)dict_values;
+      c->fits_int32 = true;
+      for (int32_t i = 0; i < card && c->fits_int32; ++i) c->fits_int32 = v[i] >= INT32_MIN && v[i] <= INT32_MAX;
+    }
   }
   if (dict_hashes != nullptr) {
     int rc = dev_alloc(c->hashes, (size_t)card * 4);
@@ -188,6 +194,7 @@ int pa_segment_add_raw_column(pa_segment* seg, int32_t column_id, int32_t value_
   Column* c = new Column();
   c->kind = COL_SV_RAW;
   c->vtype = value_type;
+  c->fits_int32 = value_type == PA_INT;
   const size_t padded = (size_t)wtiles_for(seg->num_docs) * kWTileDocs;
   int rc = dev_alloc(c->raw, padded * esz + 16);
   if (rc) { delete c; return rc; }
@@ -325,7 +332,8 @@ struct pa_query {
   std::vector<DevSeg> hsegs;
   DevBuf dq, dsegs;
   std::vector<DevBuf> owned;  // LUTs, remaps, HLL LUTs
-  DevBuf acc;                 // all accumulator sections
+  DevBuf acc;                 // all accumulator sections (unless the caller provided the block)
+  void* external_acc = nullptr;
   std::vector<Section> sections;
   std::vector<int> agg_section;  // agg -> section index (-1 for COUNT)
 
@@ -570,13 +578,18 @@ int pa_query_prepare(pa_query* q) {
       const pa_agg_spec& A = s.aggs[a];
       if (A.type == PA_AGG_COUNT) continue;
       const Column* c = seg->cols.at(A.column_id);
-      const int src = (c->vtype == PA_FLOAT || c->vtype == PA_DOUBLE) ? SRC_DOUBLE : SRC_INT;
+      const int src = (c->vtype == PA_FLOAT || c->vtype == PA_DOUBLE) ? SRC_DOUBLE : (c->fits_int32 ? SRC_INT : SRC_LONG);
       if (A.type != PA_AGG_DISTINCTCOUNTHLL) {
         if (c->vtype == PA_STRING || c->vtype == PA_BYTES) return fail(PA_EINVAL, "numeric aggregation on a non-numeric column");
         if (c->kind == COL_SV_DICT && !c->dict.p) return fail(PA_EINVAL, "dictionary values missing");
       }
-      if (si == 0) agg_src[a] = src;
-      else if (agg_src[a] != src) return fail(PA_EINVAL, "aggregation column type differs across segments");
+      if (si == 0) {
+        agg_src[a] = src;
+      } else if (agg_src[a] != src) {
+        if (agg_src[a] == SRC_DOUBLE || src == SRC_DOUBLE)
+          return fail(PA_EINVAL, "aggregation column type differs across segments");
+        agg_src[a] = SRC_LONG;  // widen: some segment has values outside int32
+      }
       if (A.type == PA_AGG_DISTINCTCOUNTHLL && c->kind == COL_SV_DICT) {
         DevBuf b;
         rc = dev_alloc(b, (size_t)c->cardinality * 4);
@@ -606,7 +619,10 @@ int pa_query_prepare(pa_query* q) {
     const pa_agg_spec& A = s.aggs[a];
     switch (A.type) {
       case PA_AGG_COUNT: continue;
-      case PA_AGG_SUM: sec.push_back({agg_src[a] == SRC_INT ? PA_ACC_SUM_I64 : PA_ACC_SUM_F64, K}); break;
+      case PA_AGG_SUM:
+        if (agg_src[a] == SRC_LONG) sec.push_back({PA_ACC_SUM_I64X2, 2 * K});
+        else sec.push_back({agg_src[a] == SRC_INT ? PA_ACC_SUM_I64 : PA_ACC_SUM_F64, K});
+        break;
       case PA_AGG_MIN: sec.push_back({PA_ACC_MIN_I64, K}); break;
       case PA_AGG_MAX: sec.push_back({PA_ACC_MAX_I64, K}); break;
       case PA_AGG_DISTINCTCOUNTHLL: sec.push_back({PA_ACC_HLL_U32, K << A.log2m}); break;
@@ -632,7 +648,8 @@ int pa_query_prepare(pa_query* q) {
     const pa_agg_spec& A = s.aggs[a];
     if (A.type == PA_AGG_COUNT) continue;
     agg_lds[a] = lds_acc;
-    const size_t bytes = A.type == PA_AGG_DISTINCTCOUNTHLL ? ((size_t)K << A.log2m) * 4 : (size_t)K * 8;
+    const size_t bytes = A.type == PA_AGG_DISTINCTCOUNTHLL ? ((size_t)K << A.log2m) * 4
+                         : (size_t)K * 8 * ((A.type == PA_AGG_SUM && agg_src[a] == SRC_LONG) ? 2 : 1);
     lds_acc += (bytes + 15) & ~(size_t)15;
   }
   const size_t image_bytes = (size_t)kWavesPerWG * 2 * image_max * 4;
@@ -718,6 +735,34 @@ int pa_query_execute(pa_query* q, void* stream) {
   return PA_OK;
 }
 
+uint64_t pa_query_accumulator_bytes(const pa_query* q) { return q ? (uint64_t)q->acc.n : 0; }
+
+int pa_query_set_accumulator_buffer(pa_query* q, void* device_buffer, uint64_t bytes) {
+  if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
+  if (!device_buffer || bytes < q->acc.n) return fail(PA_EINVAL, "accumulator buffer too small");
+  if (((uintptr_t)device_buffer & 255) != 0) return fail(PA_EINVAL, "accumulator buffer must be 256-byte aligned");
+  char* old = (char*)(q->external_acc ? q->external_acc : q->acc.p);
+  char* nb = (char*)device_buffer;
+  for (Section& s : q->sections) s.ptr = nb + ((char*)s.ptr - old);
+  DevQuery& h = q->hq;
+  h.count = (unsigned long long*)(nb + ((char*)h.count - old));
+  for (int a = 0; a < h.num_aggs; ++a) {
+    if (q->agg_section[a] < 0) continue;
+    void* p = q->sections[q->agg_section[a]].ptr;
+    h.aggs[a].acc_i64 = (int64_t*)p;
+    h.aggs[a].acc_f64 = (double*)p;
+    h.aggs[a].acc_hll = (uint32_t*)p;
+  }
+  PA_HIP(hipMemcpy(q->dq.p, &h, sizeof(DevQuery), hipMemcpyHostToDevice));
+  if (!q->external_acc) {
+    const size_t n = q->acc.n;
+    dev_free(q->acc);
+    q->acc.n = n;
+  }
+  q->external_acc = device_buffer;
+  return PA_OK;
+}
+
 int32_t pa_query_num_sections(const pa_query* q) { return q ? (int32_t)q->sections.size() : -1; }
 
 void* pa_query_section(const pa_query* q, int32_t section, int32_t* kind, int64_t* num_elements) {
@@ -769,7 +814,9 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
       continue;
     }
     const Section& sc = q->sections[q->agg_section[a]];
-    const int64_t per = A.type == PA_AGG_DISTINCTCOUNTHLL ? (int64_t(1) << A.log2m) : 1;
+    const int src0 = q->hq.aggs[a].src;
+    const int64_t per = A.type == PA_AGG_DISTINCTCOUNTHLL ? (int64_t(1) << A.log2m)
+                        : ((A.type == PA_AGG_SUM && src0 == SRC_LONG) ? 2 : 1);
     const int es = A.type == PA_AGG_DISTINCTCOUNTHLL ? 4 : 8;
     DevBuf g;
     rc = dev_alloc(g, (size_t)m * per * es);
@@ -786,13 +833,20 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
       const uint32_t* r = (const uint32_t*)host.data();
       for (int64_t i = 0; i < m * per; ++i) o[i] = (uint8_t)r[i];
     } else if (A.type == PA_AGG_SUM) {
-      for (int64_t i = 0; i < m; ++i)
-        outd[i] = src == SRC_INT ? (double)((const int64_t*)host.data())[i] : ((const double*)host.data())[i];
+      const int64_t* hv = (const int64_t*)host.data();
+      for (int64_t i = 0; i < m; ++i) {
+        if (src == SRC_LONG) {  // exact 96-bit total, rounded once (the reference's double of the exact sum)
+          const __int128 t = ((__int128)hv[2 * i + 1] << 32) + (__int128)(uint64_t)hv[2 * i];
+          outd[i] = (double)t;
+        } else {
+          outd[i] = src == SRC_INT ? (double)hv[i] : ((const double*)host.data())[i];
+        }
+      }
     } else {  // MIN / MAX; empty aggregation-only result -> +/-inf (Min/MaxAggregationFunction DEFAULT_VALUE)
       for (int64_t i = 0; i < m; ++i) {
         const int64_t e8 = ((const int64_t*)host.data())[i];
         if (cnt[keys[i]] == 0) outd[i] = A.type == PA_AGG_MIN ? __builtin_inf() : -__builtin_inf();
-        else outd[i] = src == SRC_INT ? (double)e8 : f64_order_decode(e8);
+        else outd[i] = src != SRC_DOUBLE ? (double)e8 : f64_order_decode(e8);
       }
     }
   }

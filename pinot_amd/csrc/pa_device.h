@@ -24,7 +24,10 @@ constexpr int kGuardWords = 4;
 
 enum ColKind : int32_t { COL_NONE = 0, COL_SV_DICT = 1, COL_SV_RAW = 2, COL_MV_DICT = 3 };
 enum Strategy : int32_t { STRAT_LDS = 0, STRAT_GLOBAL = 1 };
-enum AccSrc : int32_t { SRC_INT = 0, SRC_DOUBLE = 1 };
+// SUM/MIN/MAX value source. SRC_INT: every value fits int32 (one exact int64 accumulator);
+// SRC_LONG: 64-bit values, SUM kept exactly as a (low 32 bits unsigned, high 32 bits signed) pair of int64
+// sums = a 96-bit total for up to 2^32 docs per key; SRC_DOUBLE: FLOAT/DOUBLE.
+enum AccSrc : int32_t { SRC_INT = 0, SRC_DOUBLE = 1, SRC_LONG = 2 };
 
 struct DevCol {
   const uint32_t* words;     // SV dict: byte-swapped stream words (points past the guard words)
@@ -66,7 +69,7 @@ struct DevAgg {
   int32_t slot;
   int32_t log2m;
   int32_t src;               // AccSrc
-  int64_t* acc_i64;          // SUM(int) / MIN / MAX (ordered encoding for doubles)
+  int64_t* acc_i64;          // SUM(int) [K], SUM(long) [2K: lo, hi], MIN / MAX (ordered encoding for doubles)
   double* acc_f64;           // SUM(double)
   uint32_t* acc_hll;         // [num_keys << log2m]
   int32_t lds_off;           // LDS strategy: byte offset of the WG-private copy

@@ -124,7 +124,7 @@ __device__ __forceinline__ AggValue agg_value(const DevAgg& A, int a, const DevS
     const uint32_t id = decode_dict_id(c, img, doc_local, doc);
     if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
       out.i = seg->hll_lut[a][id];
-    } else if (A.src == SRC_INT) {
+    } else if (A.src != SRC_DOUBLE) {
       out.i = c.dict_i64[id];
     } else {
       out.d = c.dict_f64[id];
@@ -142,7 +142,7 @@ __device__ __forceinline__ AggValue agg_value(const DevAgg& A, int a, const DevS
       // MurmurHash.hash(Object): Integer/Long -> hashLong(value), Float -> hashLong(floatToRawIntBits),
       // Double -> hashLong(doubleToRawLongBits); iv already holds exactly those longs.
       out.i = hll_slot_rank(murmur_hash_long(iv), A.log2m);
-    } else if (A.src == SRC_INT) {
+    } else if (A.src != SRC_DOUBLE) {
       out.i = iv;
     } else {
       out.d = dv;
@@ -234,12 +234,19 @@ __device__ __forceinline__ void accumulate_step(const DevQuery* __restrict__ q, 
           if (A.src == SRC_INT) {
             const int64_t s = wave_sum_i64(in ? v.i : 0);
             if (lane == leader) acc.add_i64(A, k0, s);
+          } else if (A.src == SRC_LONG) {
+            const int64_t lo = wave_sum_i64(in ? (int64_t)(uint32_t)v.i : 0);
+            const int64_t hi = wave_sum_i64(in ? (v.i >> 32) : 0);
+            if (lane == leader) {
+              acc.add_i64(A, 2 * k0, lo);
+              acc.add_i64(A, 2 * k0 + 1, hi);
+            }
           } else {
             const double s = wave_sum_f64(in ? v.d : 0.0);
             if (lane == leader) acc.add_f64(A, k0, s);
           }
         } else {
-          const int64_t e = A.src == SRC_INT ? v.i : f64_order_encode(v.d);
+          const int64_t e = A.src != SRC_DOUBLE ? v.i : f64_order_encode(v.d);
           if (A.type == PA_AGG_MIN) {
             const int64_t r = wave_min_i64(in ? e : INT64_MAX);
             if (lane == leader) acc.min_i64(A, k0, r);
@@ -250,10 +257,16 @@ __device__ __forceinline__ void accumulate_step(const DevQuery* __restrict__ q, 
         }
       } else if (in) {
         if (A.type == PA_AGG_SUM) {
-          if (A.src == SRC_INT) acc.add_i64(A, key, v.i);
-          else acc.add_f64(A, key, v.d);
+          if (A.src == SRC_INT) {
+            acc.add_i64(A, key, v.i);
+          } else if (A.src == SRC_LONG) {
+            acc.add_i64(A, 2 * key, (int64_t)(uint32_t)v.i);
+            acc.add_i64(A, 2 * key + 1, v.i >> 32);
+          } else {
+            acc.add_f64(A, key, v.d);
+          }
         } else {
-          const int64_t e = A.src == SRC_INT ? v.i : f64_order_encode(v.d);
+          const int64_t e = A.src != SRC_DOUBLE ? v.i : f64_order_encode(v.d);
           if (A.type == PA_AGG_MIN) acc.min_i64(A, key, e);
           else acc.max_i64(A, key, e);
         }
@@ -326,7 +339,8 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
       } else {
         int64_t* r = (int64_t*)(lds_acc + A.lds_off);
         const int64_t init = A.type == PA_AGG_MIN ? INT64_MAX : (A.type == PA_AGG_MAX ? INT64_MIN : 0);
-        for (int64_t k = threadIdx.x; k < K; k += kWGSize) r[k] = init;  // SUM(double) 0.0 == all-zero bits
+        const int64_t n = (A.type == PA_AGG_SUM && A.src == SRC_LONG) ? 2 * K : K;
+        for (int64_t k = threadIdx.x; k < n; k += kWGSize) r[k] = init;  // SUM(double) 0.0 == all-zero bits
       }
     }
     __syncthreads();
@@ -366,8 +380,15 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
         const DevAgg& A = q->aggs[a];
         switch (A.type) {
           case PA_AGG_SUM:
-            if (A.src == SRC_INT) atomicAdd((unsigned long long*)A.acc_i64 + k, ((const unsigned long long*)(lds_acc + A.lds_off))[k]);
-            else atomicAdd(A.acc_f64 + k, ((const double*)(lds_acc + A.lds_off))[k]);
+            if (A.src == SRC_INT) {
+              atomicAdd((unsigned long long*)A.acc_i64 + k, ((const unsigned long long*)(lds_acc + A.lds_off))[k]);
+            } else if (A.src == SRC_LONG) {
+              const unsigned long long* r = (const unsigned long long*)(lds_acc + A.lds_off);
+              atomicAdd((unsigned long long*)A.acc_i64 + 2 * k, r[2 * k]);
+              atomicAdd((unsigned long long*)A.acc_i64 + 2 * k + 1, r[2 * k + 1]);
+            } else {
+              atomicAdd(A.acc_f64 + k, ((const double*)(lds_acc + A.lds_off))[k]);
+            }
             break;
           case PA_AGG_MIN: atomicMin((long long*)A.acc_i64 + k, ((const long long*)(lds_acc + A.lds_off))[k]); break;
           case PA_AGG_MAX: atomicMax((long long*)A.acc_i64 + k, ((const long long*)(lds_acc + A.lds_off))[k]); break;

@@ -1,0 +1,69 @@
+"""Multi-GPU segment sharding + cross-GPU merge of partial aggregates.
+
+One process per GPU. Every rank owns a disjoint segment set (segments shard naturally: no data-path exchange) and
+accumulates it into the SAME table-wide key space; the GroupByCombineOperator / AggregationCombineOperator merge of
+partial aggregates across GPUs then becomes one collective per accumulator section over RCCL (xGMI):
+SUM for COUNT/SUM, MIN for MIN, MAX for MAX and for HLL registers (HyperLogLog.addAll == register max).
+"""
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+
+SECTION_OP = {
+    L.PA_ACC_COUNT_U64: dist.ReduceOp.SUM,
+    L.PA_ACC_SUM_I64: dist.ReduceOp.SUM,
+    L.PA_ACC_SUM_I64X2: dist.ReduceOp.SUM,
+    L.PA_ACC_SUM_F64: dist.ReduceOp.SUM,
+    L.PA_ACC_MIN_I64: dist.ReduceOp.MIN,
+    L.PA_ACC_MAX_I64: dist.ReduceOp.MAX,
+    L.PA_ACC_HLL_U32: dist.ReduceOp.MAX,
+}
+SECTION_DTYPE = {
+    L.PA_ACC_COUNT_U64: torch.int64,
+    L.PA_ACC_SUM_I64: torch.int64,
+    L.PA_ACC_SUM_I64X2: torch.int64,
+    L.PA_ACC_SUM_F64: torch.float64,
+    L.PA_ACC_MIN_I64: torch.int64,
+    L.PA_ACC_MAX_I64: torch.int64,
+    L.PA_ACC_HLL_U32: torch.int32,  # registers are < 32: signed max == unsigned max
+}
+
+
+def shard_segments(num_segments, rank, world_size):
+    """Contiguous segment ranges per rank (each GPU owns a segment set)."""
+    per = num_segments // world_size
+    extra = num_segments % world_size
+    start = rank * per + min(rank, extra)
+    return list(range(start, start + per + (1 if rank < extra else 0)))
+
+
+def reduce_sections(views, dst=0, group=None, all_reduce=False):
+    """views: [(section kind, tensor)] -> reduced in place on `dst` (or everywhere)."""
+    for kind, t in views:
+        if all_reduce:
+            dist.all_reduce(t, op=SECTION_OP[kind], group=group)
+        else:
+            dist.reduce(t, dst=dst, op=SECTION_OP[kind], group=group)
+
+
+class DistributedAccumulators:
+    """Moves an executor's accumulators into one torch-owned device block and reduces it across ranks."""
+
+    def __init__(self, executor, device):
+        lib = L.lib()
+        nbytes = int(lib.pa_query_accumulator_bytes(executor.handle))
+        self.buf = torch.zeros(nbytes + 512, dtype=torch.uint8, device=device)
+        base = self.buf.data_ptr()
+        pad = (-base) % 256
+        self.base = base + pad
+        L.check(lib.pa_query_set_accumulator_buffer(executor.handle, self.base, nbytes), "set_accumulator_buffer")
+        self.views = []
+        for kind, ptr, n in executor.sections():
+            off = ptr - self.base + pad
+            dt = SECTION_DTYPE[kind]
+            es = torch.empty(0, dtype=dt).element_size()
+            self.views.append((kind, self.buf[off:off + n * es].view(dt)))
+
+    def reduce(self, dst=0, all_reduce=False):
+        reduce_sections(self.views, dst=dst, all_reduce=all_reduce)

@@ -1,0 +1,297 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle and the reference's golden results.
+
+Bar: bit-exact for COUNT, integer/long SUM (exact int64 accumulation == the reference's double accumulation while
+partial sums stay below 2^53, true for every case here), MIN/MAX, group keys and HLL registers; DOUBLE/FLOAT sums
+within a relative tolerance of 1e-9 (summation order differs from the reference's docId order).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import rows_match
+from pinot_amd import _lib as L
+from pinot_amd import parse_sql
+from pinot_amd.engine import AvgPair, GpuQueryExecutor, GpuSegment
+from pinot_amd.hll import HyperLogLog
+from pinot_amd.reduce import final_result_table, merge_intermediate, server_trim
+from synth import make_segment
+
+pytestmark = pytest.mark.gpu
+
+DOUBLE_REL = 1e-9
+
+
+def _close(a, b, rel):
+    if isinstance(b, HyperLogLog):
+        return isinstance(a, HyperLogLog) and a == b
+    if isinstance(b, AvgPair):
+        return a.count == b.count and _close(a.sum, b.sum, rel)
+    if isinstance(b, int) and not isinstance(b, bool):
+        return a == b
+    a, b = float(a), float(b)
+    if a == b:
+        return True
+    if np.isinf(b) or np.isinf(a):
+        return False
+    return rel > 0 and abs(a - b) <= rel * max(abs(b), 1.0)
+
+
+def assert_same(gpu, ora, rel=0.0):
+    assert gpu.num_docs_scanned == ora.num_docs_scanned
+    if ora.group_by:
+        assert set(gpu.groups) == set(ora.groups), (sorted(set(gpu.groups) ^ set(ora.groups))[:5])
+        for k, vals in ora.groups.items():
+            for a, b in zip(gpu.groups[k], vals):
+                assert _close(a, b, rel), (k, a, b)
+    else:
+        for a, b in zip(gpu.row, ora.row):
+            assert _close(a, b, rel), (a, b)
+
+
+def run_both(sql, segments, gsegs=None, flags=0, rel=0.0):
+    q = parse_sql(sql)
+    own = gsegs is None
+    if own:
+        gsegs = [GpuSegment(s) for s in segments]
+    ex = GpuQueryExecutor(q, gsegs, flags=flags)
+    try:
+        got = ex.run()
+    finally:
+        ex.close()
+        if own:
+            for g in gsegs:
+                g.close()
+    exp = oracle.run_query(q, segments)
+    assert_same(got, exp, rel)
+    return got, exp, ex
+
+
+# ------------------------------------------------------------------ reference golden results on the GPU
+def test_golden_cases_gpu(golden_spec, golden_segment):
+    g = GpuSegment(golden_segment)
+    failures = []
+    try:
+        for case in golden_spec["cases"]:
+            q = parse_sql(case["sql"])
+            ex = GpuQueryExecutor(q, [g, g])  # one server = 2 copies of the segment
+            server = ex.run()
+            ex.close()
+            exp = oracle.run_query(q, [golden_segment] * 2)
+            assert_same(server, exp)
+            got = final_result_table(merge_intermediate([server_trim(server, q)] * 2), q)
+            if not rows_match(got, case["rows"], case["delta"]):
+                failures.append((case["source"], got[:3], case["rows"][:3]))
+    finally:
+        g.close()
+    assert not failures, failures
+
+
+# ------------------------------------------------------------------ randomized parity vs the oracle
+COLS = {"d1": ("INT", 50), "d2": ("STRING", 20), "d3": ("LONG", 3000), "m1": ("INT", 500), "m2": ("LONG", 10000),
+        "f1": ("DOUBLE", 200), "f2": ("FLOAT", 300), "r1": ("DOUBLE", 0), "r2": ("INT", 0), "r3": ("LONG", 0)}
+RAW = ("r1", "r2", "r3")
+
+QUERIES = [
+    "SELECT COUNT(*), SUM(m1), SUM(m2), MIN(m1), MAX(m2) FROM t",
+    "SELECT COUNT(*), SUM(m1) FROM t WHERE d1 BETWEEN {d1a} AND {d1b}",
+    "SELECT COUNT(*), SUM(m2), MIN(d3), MAX(d3) FROM t WHERE d3 > {d3a} AND d2 IN ('s00003_xxx', 's00007_', 's00011_xxxx')",
+    "SELECT d1, COUNT(*), SUM(m1), SUM(m2), MIN(m1), MAX(m1) FROM t GROUP BY d1 ORDER BY d1 LIMIT 100",
+    "SELECT d1, d2, COUNT(*), SUM(m2), AVG(m1) FROM t WHERE d3 <= {d3a} OR d2 NOT IN ('s00001_x', 's00002_xx') "
+    "GROUP BY d1, d2 LIMIT 2000",
+    "SELECT d2, DISTINCTCOUNTHLL(m2), DISTINCTCOUNTHLL(d2), DISTINCTCOUNTHLL(f1) FROM t GROUP BY d2 LIMIT 100",
+    "SELECT DISTINCTCOUNTHLL(d3), DISTINCTCOUNTHLL(m1, 10), DISTINCTCOUNTHLL(r2), DISTINCTCOUNTHLL(r1) FROM t "
+    "WHERE NOT (d1 < {d1a})",
+    "SELECT d1, SUM(f1), MIN(f1), MAX(f2), SUM(r1), MIN(r1), MAX(r3), SUM(r2) FROM t GROUP BY d1 LIMIT 100",
+    "SELECT COUNT(*), SUM(r1), MAX(r2) FROM t WHERE r2 > 100 AND r1 <= 50.5",
+    "SELECT d3, COUNT(*) FROM t WHERE r3 IN (5, 7, 11, -3) OR d1 = {d1a} GROUP BY d3 LIMIT 5000",
+    "SELECT COUNT(*) FROM t WHERE d1 != {d1a} AND NOT (d2 = 's00004_xxxx' OR m1 >= {m1a})",
+    "SELECT d1, d2, d3, COUNT(*), SUM(m1) FROM t WHERE f1 < 0 GROUP BY d1, d2, d3 LIMIT 100000 "
+    "OPTION(numGroupsLimit=1000000)",
+]
+
+
+def _fill(sql, seg):
+    vals = {}
+    for c in ("d1", "d3", "m1"):
+        d = seg.column(c).dictionary
+        vals[c + "a"] = int(d[len(d) // 3])
+        vals[c + "b"] = int(d[(2 * len(d)) // 3])
+    return sql.format(**vals)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("qi", range(len(QUERIES)))
+def test_random_queries(seed, qi):
+    sizes = [(20011, 5000), (8191, 70001), (1, 2049)][seed - 1]
+    segs = [make_segment(seed * 100 + i, n, COLS, no_dict=RAW) for i, n in enumerate(sizes)]
+    sql = _fill(QUERIES[qi], segs[0])
+    rel = DOUBLE_REL if any(c in sql for c in ("f1", "f2", "r1")) else 0.0
+    run_both(sql, segs, rel=rel)
+
+
+@pytest.mark.parametrize("flags", [L.PA_QF_FORCE_GLOBAL, L.PA_QF_STAGE_ALL, L.PA_QF_FORCE_GLOBAL | L.PA_QF_STAGE_ALL])
+def test_strategies_agree(flags):
+    """LDS-privatised vs global accumulators, staged vs lazy post-filter columns: identical results."""
+    segs = [make_segment(11 + i, n, COLS, no_dict=RAW) for i, n in enumerate((30001, 4096))]
+    for sql in QUERIES[:8]:
+        sql = _fill(sql, segs[0])
+        rel = DOUBLE_REL if any(c in sql for c in ("f1", "f2", "r1")) else 0.0
+        run_both(sql, segs, flags=flags, rel=rel)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 2047, 2048, 2049, 4095, 4097, 100003])
+def test_ragged_segment_sizes(n):
+    cols = {"a": ("INT", 37), "b": ("LONG", 1500), "m": ("LONG", 777)}
+    seg = make_segment(n, n, cols)
+    run_both("SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t WHERE b > %d" % int(seg.column("b").dictionary[0]), [seg])
+    run_both("SELECT a, COUNT(*), SUM(m), MAX(b) FROM t GROUP BY a LIMIT 100", [seg])
+
+
+def test_empty_and_no_match():
+    """Zero-doc segment and a filter matching nothing: aggregation-only returns COUNT 0, SUM 0.0,
+    MIN +inf, MAX -inf (Min/MaxAggregationFunction DEFAULT_VALUE) and an empty HLL."""
+    cols = {"a": ("INT", 10), "m": ("LONG", 50)}
+    seg = make_segment(6, 1000, cols)
+    got, _, _ = run_both("SELECT COUNT(*), SUM(m), MIN(m), MAX(m), DISTINCTCOUNTHLL(m) FROM t WHERE a > 2147483000",
+                         [seg])
+    assert got.row[0] == 0 and got.row[1] == 0.0 and got.row[2] == np.inf and got.row[3] == -np.inf
+    assert got.row[4].cardinality() == 0
+    got, _, _ = run_both("SELECT a, COUNT(*) FROM t WHERE a > 2147483000 GROUP BY a", [seg])
+    assert got.groups == {}
+
+
+def test_zero_doc_segment_in_set():
+    from pinot_amd.segment import Segment, build_column
+    cols = {"a": ("INT", 10), "m": ("LONG", 50)}
+    seg = make_segment(7, 5000, cols)
+    z = Segment("empty", 0)
+    for c, (dt, _) in cols.items():
+        col = build_column(c, seg.column(c).dictionary[:1], dt)  # one-value dictionary, no docs
+        col.fwd_bytes = np.zeros(0, dtype=np.uint8)
+        z.columns[c] = col
+    run_both("SELECT a, COUNT(*), SUM(m) FROM t GROUP BY a", [z, seg, z])
+
+
+def test_different_dictionaries_remap():
+    """Segments with different dictionaries: group keys merge by value (GroupByCombineOperator semantics)."""
+    cols = {"k1": ("INT", 40), "k2": ("STRING", 15), "m": ("INT", 100)}
+    segs = [make_segment(s, 7000 + s, cols) for s in (21, 22, 23, 24)]
+    run_both("SELECT k1, k2, COUNT(*), SUM(m), MIN(m), DISTINCTCOUNTHLL(m) FROM t GROUP BY k1, k2 LIMIT 10000", segs)
+
+
+def test_long_sum_beyond_2_53():
+    """Past 2^53 the reference's docId-order double accumulation rounds; the GPU's exact int64 sum converted once
+    is the correctly rounded value. Agreement is then within the reference's own rounding error (n ulps)."""
+    from pinot_amd.segment import create_segment
+    rng = np.random.default_rng(5)
+    n = 50000
+    vals = rng.integers(1 << 60, (1 << 61), size=n, dtype=np.int64)
+    seg = create_segment("big", {"m": vals, "k": rng.integers(0, 4, size=n).astype(np.int32)},
+                         {"m": "LONG", "k": "INT"})
+    run_both("SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t", [seg], rel=1e-12)
+    run_both("SELECT k, SUM(m) FROM t GROUP BY k", [seg], rel=1e-12)
+    exact = int(vals.astype(object).sum())
+    q = parse_sql("SELECT SUM(m) FROM t")
+    g = GpuSegment(seg)
+    ex = GpuQueryExecutor(q, [g])
+    assert ex.run().row[0] == float(exact)
+    ex.close()
+    g.close()
+
+
+def test_high_cardinality_global_fallback():
+    """~1M-key space (LDS cannot hold it): global-memory accumulators."""
+    cols = {"k1": ("INT", 1000), "k2": ("LONG", 1000), "m": ("LONG", 5000)}
+    seg = make_segment(30, 300000, cols)
+    got, exp, ex = run_both("SELECT k1, k2, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t GROUP BY k1, k2 LIMIT 1000000 "
+                            "OPTION(numGroupsLimit=2000000)", [seg])
+    assert len(got.groups) > 100000
+
+
+def test_num_groups_limit_guard():
+    """Until first-seen trimming runs on the GPU, a query whose numGroupsLimit may bind fails loudly."""
+    from pinot_amd.engine import UnsupportedQuery
+    cols = {"k1": ("INT", 1000), "k2": ("LONG", 1000)}
+    seg = make_segment(32, 200000, cols)
+    g = GpuSegment(seg)
+    with pytest.raises(UnsupportedQuery):
+        GpuQueryExecutor(parse_sql("SELECT k1, k2, COUNT(*) FROM t GROUP BY k1, k2"), [g])
+    g.close()
+
+
+@pytest.mark.parametrize("nb", [1, 7, 8, 15, 16, 17, 24, 31])
+def test_bit_widths_through_capi(nb):
+    """Raw C-ABI use: an nb-bit column with no dictionary values (STRING type), DICT_RANGE filter count and a
+    DICT_SET filter, against numpy on the same ids."""
+    from pinot_amd.segment import pack_bits
+    lib = L.lib()
+    n = 50_000 + nb
+    rng = np.random.default_rng(nb)
+    ids = rng.integers(0, 1 << nb, size=n, dtype=np.int64).astype(np.uint32)
+    card = (1 << nb) if nb < 31 else (1 << 31) - 1
+    ids = np.minimum(ids, card - 1)
+    fwd = pack_bits(ids, nb)
+    seg = L.check_ptr(lib.pa_segment_create(n), "create")
+    L.check(lib.pa_segment_add_sv_dict_column(seg, 0, fwd.ctypes.data, fwd.nbytes, nb, card, L.PA_STRING, None, None),
+            "add")
+    lo, hi = int(card // 5), int(card // 2) + 1
+    for kind in (L.PA_LEAF_DICT_RANGE, L.PA_LEAF_DICT_SET):
+        if kind == L.PA_LEAF_DICT_SET and nb > 20:
+            continue
+        spec = L.QuerySpec()
+        spec.num_leaves = 1
+        spec.leaves[0].column_id = 0
+        spec.leaves[0].kind = kind
+        spec.num_ops = 1
+        spec.ops[0] = L.PA_OP_LEAF
+        spec.num_aggs = 1
+        spec.aggs[0].type = L.PA_AGG_COUNT
+        q = L.check_ptr(lib.pa_query_create(ctypes.byref(spec), 1), "qcreate")
+        lp = (L.LeafParams * 1)()
+        lut = None
+        if kind == L.PA_LEAF_DICT_RANGE:
+            lp[0].lo, lp[0].hi = lo, hi
+            expected = int(((ids >= lo) & (ids < hi)).sum())
+        else:
+            sel = np.arange(0, card, 3, dtype=np.int64)
+            lut = np.zeros((card + 31) // 32, dtype=np.uint32)
+            np.bitwise_or.at(lut, sel >> 5, (np.uint32(1) << (sel & 31).astype(np.uint32)))
+            lp[0].lut = lut.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+            expected = int((ids % 3 == 0).sum())
+        L.check(lib.pa_query_bind_segment(q, 0, seg, lp, None), "bind")
+        L.check(lib.pa_query_prepare(q), "prepare")
+        L.check(lib.pa_query_execute(q, None), "execute")
+        keys = np.zeros(1, np.int64)
+        counts = np.zeros(1, np.int64)
+        outs = np.zeros(1, np.float64)
+        ptrs = (ctypes.c_void_p * 1)(outs.ctypes.data)
+        assert L.check(lib.pa_query_fetch(q, None, 1, keys.ctypes.data, counts.ctypes.data, ptrs), "fetch") == 1
+        assert counts[0] == expected
+        lib.pa_query_destroy(q)
+    lib.pa_segment_destroy(seg)
+
+
+def test_large_segment_properties():
+    """A 10M-doc segment (the BASELINE configs' segment size): filter+group-by counts sum to the filter-only count,
+    both equal to the oracle, and the group-by sums are exact."""
+    from pinot_amd.segment import segment_from_dict_ids
+    n = 10_000_000
+    rng = np.random.default_rng(99)
+    specs = {}
+    for name, card in (("day", 512), ("acct", 1 << 17), ("clicks", 1024)):
+        nb = int(card - 1).bit_length()
+        ids = rng.integers(0, card, size=n, dtype=np.int64).astype(np.uint32)
+        from pinot_amd.segment import pack_bits
+        specs[name] = ("LONG" if name == "clicks" else "INT", np.arange(card, dtype=np.int64) * 3 + 17000,
+                       pack_bits(ids, nb))
+    seg = segment_from_dict_ids("big", n, specs)
+    g = GpuSegment(seg)
+    sql_f = "SELECT COUNT(*), SUM(clicks) FROM t WHERE day BETWEEN 17300 AND 17400"
+    sql_g = "SELECT day, COUNT(*), SUM(clicks) FROM t WHERE day BETWEEN 17300 AND 17400 GROUP BY day LIMIT 1000"
+    a, _, _ = run_both(sql_f, [seg], gsegs=[g])
+    b, _, _ = run_both(sql_g, [seg], gsegs=[g])
+    assert sum(v[0] for v in b.groups.values()) == a.row[0]
+    assert sum(v[1] for v in b.groups.values()) == a.row[1]
+    g.close()
