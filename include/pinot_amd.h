@@ -160,6 +160,12 @@ typedef struct {
 
 #define PA_QF_STAGE_ALL 1  /* stage post-filter columns through LDS even when a filter exists */
 #define PA_QF_FORCE_GLOBAL 2 /* force global-memory accumulators (testing the fallback) */
+/* tuning overrides of the tile planner (0 = automatic) */
+#define PA_QF_STEPS16 (1 << 4)        /* 1024-doc wave tiles */
+#define PA_QF_STEPS32 (1 << 5)        /* 2048-doc wave tiles */
+#define PA_QF_RING_SHIFT 8            /* bits 8..11: tile images per wave (2..8) */
+#define PA_QF_WG_SHIFT 12             /* bits 12..13: workgroups per CU (1..3) */
+#define PA_QF_DEBUG_STREAM_ONLY (1 << 16) /* measurement only: stream the tiles, skip decode (results invalid) */
 
 /* per-(segment, leaf) parameters in that segment's dictId space */
 typedef struct {
@@ -221,6 +227,11 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
  * (always-read columns), number of docs scanned. */
 int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs,
                    uint64_t* num_tiles);
+
+/* The kernel plan chosen by pa_query_prepare: accumulator strategy (0 = LDS-privatised, 1 = global), 64-doc
+ * steps per wave tile, DMA instructions per tile, tile images per wave, workgroups per CU, grid, LDS bytes. */
+int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t* dma_slots, int32_t* ring,
+                  int32_t* wg_per_cu, int32_t* grid, int32_t* lds_bytes);
 
 void pa_query_destroy(pa_query* q);
 

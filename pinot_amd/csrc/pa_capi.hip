@@ -323,6 +323,10 @@ struct pa_query {
   int64_t num_keys = 1;
   int strategy = STRAT_GLOBAL;
   int grid = 0;
+  int steps = 32;
+  int dma_slots = 8;
+  int plan_ring = 2;
+  int plan_wg = 1;
   int lds_bytes = 0;
   uint64_t staged_bytes = 0;
   uint64_t num_docs = 0;
@@ -490,20 +494,16 @@ int pa_query_prepare(pa_query* q) {
   q->hsegs.assign(q->nseg, DevSeg{});
   std::vector<char> staged(nslots, 0);
   std::vector<int> agg_src(s.num_aggs, SRC_INT);
-  int64_t first = 0;
-  int image_max = 0;
-  q->staged_bytes = 0;
+  
+  
+  
   q->num_docs = 0;
   for (int si = 0; si < q->nseg; ++si) {
     const pa_segment* seg = q->segs[si];
     DevSeg& d = q->hsegs[si];
     std::memset(&d, 0, sizeof(d));
     d.num_docs = seg->num_docs;
-    d.num_wtiles = (int32_t)wtiles_for(seg->num_docs);
-    d.first_wtile = first;
-    first += d.num_wtiles;
     q->num_docs += (uint64_t)seg->num_docs;
-    int off = kGuardWords;
     for (int sl = 0; sl < nslots; ++sl) {
       auto it = seg->cols.find(q->slot_cols[sl]);
       if (it == seg->cols.end())
@@ -520,13 +520,10 @@ int pa_query_prepare(pa_query* q) {
       dc.lds_off = -1;
       if (c->kind == COL_SV_DICT && (leaf_slot_is_filter[sl] || stage_all)) {
         staged[sl] = 1;
-        dc.lds_off = off;
-        off += 64 * c->nbits + kGuardWords;
-        q->staged_bytes += (uint64_t)d.num_wtiles * 64 * c->nbits * 4;
+        dc.lds_off = 0;  // staged; the region offset depends on the tile size (apply_layout below)
+        d.stage[d.num_staged++] = StageDesc{dc.words, dc.nbits, 0};
       }
     }
-    d.image_dwords = off;
-    image_max = std::max(image_max, off);
     // filter literals
     for (size_t li = 0; li < q->literals.size(); ++li) {
       const Literal lit = q->literals[li];
@@ -537,14 +534,30 @@ int pa_query_prepare(pa_query* q) {
       L.negate = (p.negate != 0) != lit.neg;
       L.clause_end = q->clause_end[li];
       const DevCol& dc = d.cols[L.slot];
+      L.nbits = dc.nbits;
+      L.lds_off = dc.lds_off;
+      L.words = dc.words;
+      L.raw = dc.raw;
+      L.vtype = dc.vtype;
       if (L.kind == PA_LEAF_DICT_RANGE || L.kind == PA_LEAF_DICT_SET) {
         if (dc.kind != COL_SV_DICT) return fail(PA_EINVAL, "dictionary leaf on a non-dictionary column");
       } else if (L.kind == PA_LEAF_RAW_RANGE) {
         if (dc.kind != COL_SV_RAW) return fail(PA_EINVAL, "raw leaf on a non-raw column");
       }
       if (L.kind == PA_LEAF_DICT_RANGE) {
-        L.lo = p.lo;
-        L.span = p.hi > p.lo ? p.hi - p.lo : 0;
+        // kernel form (leaf_bits): MSB-aligned bounds lo' = lo << (32-nb), hi' = span << (32-nb) - 1;
+        // an empty range becomes NOT(full range)
+        const int nb = dc.nbits;
+        int64_t lo = std::max<int64_t>(0, p.lo);
+        int64_t span = (int64_t)p.hi - lo;
+        if (span <= 0) {
+          lo = 0;
+          span = int64_t(1) << nb;
+          L.negate = !L.negate;
+        }
+        if (lo + span > (int64_t(1) << nb)) span = (int64_t(1) << nb) - lo;
+        L.lo = (int32_t)(uint32_t)((uint64_t)lo << (32 - nb));
+        L.span = (int32_t)(uint32_t)(((uint64_t)span << (32 - nb)) - 1);
       } else if (L.kind == PA_LEAF_DICT_SET) {
         const auto& lut = q->luts[si][lit.leaf];
         void* dp = nullptr;
@@ -608,7 +621,7 @@ int pa_query_prepare(pa_query* q) {
       }
     }
   }
-  q->num_tiles = (uint64_t)first;
+  
 
   // ---- accumulators (one device block, sections 256-byte aligned)
   q->sections.clear();
@@ -652,12 +665,98 @@ int pa_query_prepare(pa_query* q) {
                          : (size_t)K * 8 * ((A.type == PA_AGG_SUM && agg_src[a] == SRC_LONG) ? 2 : 1);
     lds_acc += (bytes + 15) & ~(size_t)15;
   }
-  const size_t image_bytes = (size_t)kWavesPerWG * 2 * image_max * 4;
+  // ---- tile geometry: wave tile of 1024 or 2048 docs, D DMA instructions per tile, a ring of R tile images per
+  // wave (R-1 tiles in flight). HBM latency under full load is several microseconds, so the plan maximises the
+  // bytes in flight per CU (~128 KiB sustain the HBM rate) within 160 KiB of LDS, then prefers more waves.
   const size_t kLdsBudget = 160 * 1024;
-  const bool lds_ok = !(s.flags & PA_QF_FORCE_GLOBAL) && lds_acc <= 64 * 1024 && lds_acc + image_bytes <= kLdsBudget;
-  q->strategy = lds_ok ? STRAT_LDS : STRAT_GLOBAL;
-  q->lds_bytes = (int)((q->strategy == STRAT_LDS ? lds_acc : 0) + image_bytes);
-  if ((size_t)q->lds_bytes > kLdsBudget) return fail(PA_EUNSUPPORTED, "staged columns too wide for one wave-tile image");
+  struct Plan {
+    int steps = 0, dma = 0, ring = 0, wg_per_cu = 0, img_dw = 0;
+    size_t lds = 0;
+    double score = -1;
+  };
+  const int force_ring = (s.flags >> PA_QF_RING_SHIFT) & 15;
+  const int force_wg = (s.flags >> PA_QF_WG_SHIFT) & 3;
+  auto plan_for = [&](bool lds_strategy) {
+    Plan best;
+    for (int steps : {32, 16}) {
+      if ((s.flags & PA_QF_STEPS16) && steps != 16) continue;
+      if ((s.flags & PA_QF_STEPS32) && steps != 32) continue;
+      int img_dw = kGuardWords, need = 0;
+      for (int si = 0; si < q->nseg; ++si) {
+        int dw = kGuardWords, n = 0;
+        for (int k = 0; k < q->hsegs[si].num_staged; ++k) {
+          const int nb = q->hsegs[si].stage[k].nbits;
+          dw += 2 * steps * nb + kGuardWords;
+          n += ((steps / 2) * nb + 63) / 64;
+        }
+        img_dw = std::max(img_dw, dw);
+        need = std::max(need, n);
+      }
+      const int dma = scan_dma_slots(need);
+      if (dma < 0) continue;
+      const size_t img_bytes = (size_t)img_dw * 4;
+      const size_t acc_b = lds_strategy ? lds_acc : 0;
+      for (int wg : {3, 2, 1}) {
+        if (force_wg && wg != force_wg) continue;
+        if (!force_wg && wg == 3) continue;
+        const size_t per_wg = kLdsBudget / wg;
+        if (per_wg <= acc_b) continue;
+        int ring = (int)((per_wg - acc_b) / (kWavesPerWG * img_bytes));
+        ring = std::min({ring, 8, 2 + 63 / dma});
+        if (force_ring) {
+          if (force_ring > ring) continue;
+          ring = force_ring;
+        }
+        if (ring < 2) continue;
+        const double inflight = (double)wg * kWavesPerWG * (ring - 1) * img_bytes;
+        const double score = std::min(inflight, 128.0 * 1024) + 4096.0 * wg + (steps == 32 ? 1 : 0);
+        if (score > best.score) {
+          best = Plan{steps, dma, ring, wg, img_dw, acc_b + (size_t)kWavesPerWG * ring * img_bytes, score};
+        }
+      }
+    }
+    return best;
+  };
+  Plan plan;
+  q->strategy = STRAT_GLOBAL;
+  if (!(s.flags & PA_QF_FORCE_GLOBAL) && lds_acc <= 64 * 1024) {
+    plan = plan_for(true);
+    if (plan.score >= 0) q->strategy = STRAT_LDS;
+  }
+  if (q->strategy == STRAT_GLOBAL) plan = plan_for(false);
+  if (plan.score < 0) return fail(PA_EUNSUPPORTED, "staged columns too wide for the LDS tile ring");
+  q->lds_bytes = (int)plan.lds;
+  q->steps = plan.steps;
+  q->dma_slots = plan.dma;
+
+  // ---- apply the layout: tiles per segment, LDS regions, staged bytes
+  int64_t first = 0;
+  q->staged_bytes = 0;
+  void* dummy = nullptr;  // 256 readable bytes: source of the DMA padding instructions
+  {
+    std::vector<char> z(256, 0);
+    rc = upload_owned(q, z.data(), z.size(), &dummy);
+    if (rc) return rc;
+  }
+  for (int si = 0; si < q->nseg; ++si) {
+    DevSeg& d = q->hsegs[si];
+    const int64_t tile_docs = (int64_t)plan.steps * kWave;
+    d.num_wtiles = (int32_t)((d.num_docs + tile_docs - 1) / tile_docs);
+    d.first_wtile = first;
+    first += d.num_wtiles;
+    d.dummy_src = (const uint32_t*)dummy;
+    int off = kGuardWords;
+    for (int k = 0; k < d.num_staged; ++k) {
+      d.stage[k].lds_off = off;
+      for (int sl = 0; sl < nslots; ++sl)
+        if (d.cols[sl].lds_off >= 0 && d.cols[sl].words == d.stage[k].words) d.cols[sl].lds_off = off;
+      q->staged_bytes += (uint64_t)d.num_wtiles * 2 * plan.steps * d.stage[k].nbits * 4;
+      off += 2 * plan.steps * d.stage[k].nbits + kGuardWords;
+    }
+    d.image_dwords = off;
+    for (size_t li = 0; li < q->literals.size(); ++li) d.leaves[li].lds_off = d.cols[d.leaves[li].slot].lds_off;
+  }
+  const int image_max = plan.img_dw;
 
   DevQuery& h = q->hq;
   std::memset(&h, 0, sizeof(h));
@@ -677,6 +776,12 @@ int pa_query_prepare(pa_query* q) {
   }
   h.num_keys = K;
   h.total_wtiles = first;
+  h.ring = plan.ring;
+  h.steps = plan.steps;
+  h.debug_stream_only = (s.flags & PA_QF_DEBUG_STREAM_ONLY) ? 1 : 0;
+  q->plan_ring = plan.ring;
+  q->plan_wg = plan.wg_per_cu;
+  q->num_tiles = (uint64_t)first;
   h.count = (unsigned long long*)q->sections[0].ptr;
   h.lds_count_off = 0;
   h.lds_acc_bytes = q->strategy == STRAT_LDS ? (uint32_t)lds_acc : 0;
@@ -701,7 +806,7 @@ int pa_query_prepare(pa_query* q) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
   }
-  int wg_per_cu = q->lds_bytes > 0 ? (int)std::min<size_t>(4, kLdsBudget / (size_t)q->lds_bytes) : 4;
+  int wg_per_cu = plan.wg_per_cu;
   if (wg_per_cu < 1) wg_per_cu = 1;
   const int64_t max_wg = (int64_t)cus * wg_per_cu;
   const int64_t want = (first + kWavesPerWG - 1) / kWavesPerWG;
@@ -714,7 +819,7 @@ int pa_query_prepare(pa_query* q) {
   if (rc) return rc;
   PA_HIP(hipMemcpy(q->dq.p, &h, sizeof(DevQuery), hipMemcpyHostToDevice));
   if (q->nseg) PA_HIP(hipMemcpy(q->dsegs.p, q->hsegs.data(), sizeof(DevSeg) * q->nseg, hipMemcpyHostToDevice));
-  PA_HIP(set_scan_lds_limit(q->strategy, q->lds_bytes));
+  PA_HIP(set_scan_lds_limit(q->strategy, q->dma_slots, q->steps, q->lds_bytes));
   PA_HIP(hipDeviceSynchronize());
   q->prepared = true;
   return PA_OK;
@@ -731,7 +836,7 @@ int pa_query_execute(pa_query* q, void* stream) {
     else PA_HIP(hipMemsetAsync(sc.ptr, 0, (size_t)sc.n * (sc.kind == PA_ACC_HLL_U32 ? 4 : 8), st));
   }
   if (q->num_tiles == 0) return PA_OK;
-  PA_HIP(launch_scan(q->strategy, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p, (const DevSeg*)q->dsegs.p, st));
+  PA_HIP(launch_scan(q->strategy, q->dma_slots, q->steps, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p, (const DevSeg*)q->dsegs.p, st));
   return PA_OK;
 }
 
@@ -859,6 +964,19 @@ int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs
   if (staged_bytes) *staged_bytes = q->staged_bytes;
   if (num_docs) *num_docs = q->num_docs;
   if (num_tiles) *num_tiles = q->num_tiles;
+  return PA_OK;
+}
+
+int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t* dma_slots, int32_t* ring,
+                  int32_t* wg_per_cu, int32_t* grid, int32_t* lds_bytes) {
+  if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
+  if (strategy) *strategy = q->strategy;
+  if (steps) *steps = q->steps;
+  if (dma_slots) *dma_slots = q->dma_slots;
+  if (ring) *ring = q->plan_ring;
+  if (wg_per_cu) *wg_per_cu = q->plan_wg;
+  if (grid) *grid = q->grid;
+  if (lds_bytes) *lds_bytes = q->lds_bytes;
   return PA_OK;
 }
 

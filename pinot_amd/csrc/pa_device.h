@@ -40,6 +40,8 @@ struct DevCol {
   int32_t lds_off;           // staged: dword offset of the column's region inside a wave image; -1 = lazy
 };
 
+// One CNF literal for one segment. The column fields the leaf reads are copied in, so evaluating a leaf
+// costs one scalar-load round per tile (no dependent leaf -> column descriptor chain).
 struct DevLeaf {
   int32_t kind;              // PA_LEAF_*
   int32_t slot;
@@ -47,9 +49,21 @@ struct DevLeaf {
   int32_t span;
   int32_t negate;
   int32_t clause_end;        // 1 if this literal closes a CNF clause
+  int32_t nbits;             // column copy: bits per dictId
+  int32_t lds_off;           // column copy: staged region offset (dwords) or -1
   const uint32_t* lut;       // DICT_SET bitmap (device)
+  const uint32_t* words;     // column copy: stream words
+  const void* raw;           // column copy: raw values
+  int32_t vtype;             // column copy
+  int32_t pad;
   int64_t ilo, ihi;
   double dlo, dhi;
+};
+
+struct StageDesc {           // one staged column of a segment
+  const uint32_t* words;
+  int32_t nbits;
+  int32_t lds_off;
 };
 
 struct DevSeg {
@@ -57,7 +71,9 @@ struct DevSeg {
   int32_t num_docs;
   int32_t num_wtiles;
   int32_t image_dwords;      // staged image size (dwords) of one wave tile of this segment
-  int32_t pad;
+  int32_t num_staged;
+  const uint32_t* dummy_src;  // any readable device address: source of the DMA padding instructions
+  StageDesc stage[kMaxSlots];
   DevCol cols[kMaxSlots];
   DevLeaf leaves[PA_MAX_LEAVES];
   const int32_t* remap[PA_MAX_GROUP_BY];   // dictId -> table-wide key id (nullptr = identity)
@@ -85,6 +101,10 @@ struct DevQuery {
   int32_t strategy;
   int32_t num_staged;
   int32_t image_dwords_max;  // max over segments
+  int32_t ring;              // wave-tile images per wave (tiles in flight = ring - 1)
+  int32_t steps;             // 64-doc steps per wave tile (16 or 32)
+  int32_t debug_stream_only; // measurement only: skip the decode (PA_QF_DEBUG_STREAM_ONLY)
+  int32_t pad0;
   int32_t staged_slots[kMaxSlots];
   int32_t gb_slot[PA_MAX_GROUP_BY];
   int64_t gb_stride[PA_MAX_GROUP_BY];

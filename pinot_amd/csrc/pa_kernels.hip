@@ -22,6 +22,15 @@ namespace pa {
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
 
+// Every HBM access goes through address-space-1 pointers: global_* instructions instead of flat_*. A flat
+// access may alias LDS, which makes the compiler put vmcnt(0) in front of later LDS reads.
+#define AS1 __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ AS1 T* gp(T* p) { return (AS1 T*)p; }
+template <class T>
+__device__ __forceinline__ const AS1 T* gp(const T* p) { return (const AS1 T*)p; }
+#define RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
 __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ uint32_t nbits_mask(int nb) { return nb >= 32 ? 0xffffffffu : ((1u << nb) - 1u); }
@@ -41,8 +50,8 @@ __device__ __forceinline__ uint32_t decode_lds(const uint32_t* region, int doc_l
 __device__ __forceinline__ uint32_t decode_global(const uint32_t* words, int64_t doc, int nb) {
   const uint64_t e1 = (uint64_t)doc * (uint64_t)nb + (uint64_t)(nb - 1);
   const int64_t we = (int64_t)(e1 >> 5);
-  const uint32_t lo = words[we];
-  const uint32_t hi = words[we - 1];
+  const uint32_t lo = gp(words)[we];
+  const uint32_t hi = gp(words)[we - 1];
   return __builtin_amdgcn_alignbit(hi, lo, (~(uint32_t)e1) & 31u) & nbits_mask(nb);
 }
 
@@ -51,41 +60,55 @@ __device__ __forceinline__ uint32_t decode_dict_id(const DevCol& c, const uint32
   return c.lds_off >= 0 ? decode_lds(img + c.lds_off, doc_local, c.nbits) : decode_global(c.words, doc, c.nbits);
 }
 
-// Issue the LDS-DMA of one wave tile of every staged column of `seg` into the wave image `img`.
-__device__ __forceinline__ void stage_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
-                                           int64_t wt, uint32_t* img, int lane) {
-  for (int si = 0; si < q->num_staged; ++si) {
-    const DevCol& c = seg->cols[q->staged_slots[si]];
-    const int nb = c.nbits;
-    const uint32_t* src = c.words + wt * (int64_t)(64 * nb);
-    uint32_t* dst = img + c.lds_off;
-    const int chunks = 16 * nb;  // 16-byte chunks of this column's wave tile (64*nb words)
-    for (int c0 = 0; c0 < chunks; c0 += 64) {
-      if (c0 + lane < chunks)
-        __builtin_amdgcn_global_load_lds((const void*)(src + 4 * (c0 + lane)), (lds_u32_t*)(dst + 4 * c0), 16, 0, 0);
-    }
-  }
+// s_waitcnt vmcnt(N) with every other counter at its maximum (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14).
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-__device__ __forceinline__ bool eval_leaf(const DevLeaf& L, const DevSeg* __restrict__ seg, const uint32_t* img,
-                                          int doc_local, int64_t doc, bool valid) {
-  const DevCol& c = seg->cols[L.slot];
-  bool m = false;
-  if (L.kind == PA_LEAF_DICT_RANGE) {
-    const uint32_t id = decode_dict_id(c, img, doc_local, doc);
-    m = (id - (uint32_t)L.lo) < (uint32_t)L.span;
-  } else if (L.kind == PA_LEAF_DICT_SET) {
-    const uint32_t id = decode_dict_id(c, img, doc_local, doc);
-    m = (L.lut[id >> 5] >> (id & 31u)) & 1u;
-  } else if (L.kind == PA_LEAF_RAW_RANGE) {
-    switch (c.vtype) {
-      case PA_INT: { const int64_t v = ((const int32_t*)c.raw)[doc]; m = v >= L.ilo && v <= L.ihi; } break;
-      case PA_LONG: { const int64_t v = ((const int64_t*)c.raw)[doc]; m = v >= L.ilo && v <= L.ihi; } break;
-      case PA_FLOAT: { const double v = ((const float*)c.raw)[doc]; m = v >= L.dlo && v <= L.dhi; } break;
-      default: { const double v = ((const double*)c.raw)[doc]; m = v >= L.dlo && v <= L.dhi; } break;
+// Issue the LDS-DMA of one wave tile of every staged column of `seg` into the wave image `img`: exactly D
+// wave instructions (the host guarantees the real count <= D; the rest are 16-byte dummies into the image's
+// guard words), so `vmcnt` counts tiles and a ring of tiles can be in flight behind counted waits.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// One LDS-DMA wave instruction (global_load_lds_dwordx4): lane l copies 16 bytes from its `src` to
+// lds_base + 16*l. Issued as inline asm on purpose: the compiler's waitcnt pass cannot disambiguate LDS-DMA
+// writes from later ds_reads of OTHER ring slots and would put vmcnt(0) in front of every tile's decode,
+// draining the whole ring. Visibility is guaranteed by the explicit counted waits in wait_tile; vm ops the
+// compiler does not know about only make its own vmcnt waits stricter, never wrong.
+__device__ __forceinline__ void dma16(const void* src, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_base));
+}
+
+template <int D, int STEPS>
+__device__ __forceinline__ void stage_tile(const DevSeg* __restrict__ seg, int64_t wt, uint32_t* img, int lane) {
+  const int ns = seg->num_staged;
+  int issued = 0;
+  for (int si = 0; si < ns; ++si) {
+    const StageDesc& c = seg->stage[si];
+    const int nb = c.nbits;
+    const uint32_t* src = c.words + wt * (int64_t)(2 * STEPS * nb);  // 2*STEPS*nb stream words per wave tile
+    const uint32_t dst = lds_addr(img + c.lds_off);
+    const int chunks = (STEPS / 2) * nb;  // 16-byte chunks of this column's wave tile
+    for (int c0 = 0; c0 < chunks; c0 += 64) {
+      if (c0 + lane < chunks) dma16(src + 4 * (c0 + lane), dst + 16 * c0);
+      ++issued;
     }
   }
-  return valid && (m != (L.negate != 0));
+  for (; issued < D; ++issued) {
+    if (lane == 0) dma16(seg->dummy_src, lds_addr(img));
+  }
 }
 
 // ---- wave reductions (all 64 lanes participate) ----
@@ -123,20 +146,20 @@ __device__ __forceinline__ AggValue agg_value(const DevAgg& A, int a, const DevS
   if (c.kind == COL_SV_DICT) {
     const uint32_t id = decode_dict_id(c, img, doc_local, doc);
     if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
-      out.i = seg->hll_lut[a][id];
+      out.i = gp(seg->hll_lut[a])[id];
     } else if (A.src != SRC_DOUBLE) {
-      out.i = c.dict_i64[id];
+      out.i = gp(c.dict_i64)[id];
     } else {
-      out.d = c.dict_f64[id];
+      out.d = gp(c.dict_f64)[id];
     }
   } else {  // raw column
     int64_t iv = 0;
     double dv = 0.0;
     switch (c.vtype) {
-      case PA_INT: iv = ((const int32_t*)c.raw)[doc]; dv = (double)iv; break;
-      case PA_LONG: iv = ((const int64_t*)c.raw)[doc]; dv = (double)iv; break;
-      case PA_FLOAT: { const float f = ((const float*)c.raw)[doc]; dv = f; iv = __builtin_bit_cast(int32_t, f); } break;
-      default: dv = ((const double*)c.raw)[doc]; iv = __builtin_bit_cast(int64_t, dv); break;
+      case PA_INT: iv = gp((const int32_t*)c.raw)[doc]; dv = (double)iv; break;
+      case PA_LONG: iv = gp((const int64_t*)c.raw)[doc]; dv = (double)iv; break;
+      case PA_FLOAT: { const float f = gp((const float*)c.raw)[doc]; dv = f; iv = __builtin_bit_cast(int32_t, f); } break;
+      default: dv = gp((const double*)c.raw)[doc]; iv = __builtin_bit_cast(int64_t, dv); break;
     }
     if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
       // MurmurHash.hash(Object): Integer/Long -> hashLong(value), Float -> hashLong(floatToRawIntBits),
@@ -159,28 +182,28 @@ struct Acc {
 
   __device__ __forceinline__ void add_count(int64_t key, uint32_t n) const {
     if (STRAT == STRAT_LDS) atomicAdd((uint32_t*)(lds + q->lds_count_off) + key, n);
-    else atomicAdd(q->count + key, (unsigned long long)n);
+    else __hip_atomic_fetch_add(gp(q->count) + key, (unsigned long long)n, RLX);
   }
   __device__ __forceinline__ void add_i64(const DevAgg& A, int64_t key, int64_t v) const {
     if (STRAT == STRAT_LDS) atomicAdd((unsigned long long*)(lds + A.lds_off) + key, (unsigned long long)v);
-    else atomicAdd((unsigned long long*)A.acc_i64 + key, (unsigned long long)v);
+    else __hip_atomic_fetch_add(gp((unsigned long long*)A.acc_i64) + key, (unsigned long long)v, RLX);
   }
   __device__ __forceinline__ void add_f64(const DevAgg& A, int64_t key, double v) const {
     if (STRAT == STRAT_LDS) atomicAdd((double*)(lds + A.lds_off) + key, v);
-    else atomicAdd(A.acc_f64 + key, v);
+    else __hip_atomic_fetch_add(gp(A.acc_f64) + key, v, RLX);
   }
   __device__ __forceinline__ void min_i64(const DevAgg& A, int64_t key, int64_t v) const {
     if (STRAT == STRAT_LDS) atomicMin((long long*)(lds + A.lds_off) + key, (long long)v);
-    else atomicMin((long long*)A.acc_i64 + key, (long long)v);
+    else __hip_atomic_fetch_min(gp((long long*)A.acc_i64) + key, (long long)v, RLX);
   }
   __device__ __forceinline__ void max_i64(const DevAgg& A, int64_t key, int64_t v) const {
     if (STRAT == STRAT_LDS) atomicMax((long long*)(lds + A.lds_off) + key, (long long)v);
-    else atomicMax((long long*)A.acc_i64 + key, (long long)v);
+    else __hip_atomic_fetch_max(gp((long long*)A.acc_i64) + key, (long long)v, RLX);
   }
   __device__ __forceinline__ void max_hll(const DevAgg& A, int64_t key, uint32_t jr) const {
     const int64_t idx = (key << A.log2m) + (jr >> 8);
     if (STRAT == STRAT_LDS) atomicMax((uint32_t*)(lds + A.lds_off) + idx, jr & 0xffu);
-    else atomicMax(A.acc_hll + idx, jr & 0xffu);
+    else __hip_atomic_fetch_max(gp(A.acc_hll) + idx, jr & 0xffu, RLX);
   }
 };
 
@@ -198,7 +221,7 @@ __device__ __forceinline__ void accumulate_step(const DevQuery* __restrict__ q, 
     if (mine) {
       id = decode_dict_id(c, img, doc_local, doc);
       const int32_t* rm = seg->remap[j];
-      if (rm != nullptr) id = (uint32_t)rm[id];
+      if (rm != nullptr) id = (uint32_t)gp(rm)[id];
     }
     key += (int64_t)id * q->gb_stride[j];
   }
@@ -275,31 +298,143 @@ __device__ __forceinline__ void accumulate_step(const DevQuery* __restrict__ q, 
   }
 }
 
-template <int STRAT>
+// Match word of one leaf over a whole wave tile: bit i of lane l <=> doc 64*i + l of the tile matches.
+// Leaf parameters are loaded once per tile; the 32 decodes are independent, so the LDS reads pipeline.
+template <int STEPS>
+__device__ __forceinline__ uint32_t leaf_bits(const DevLeaf& L, const uint32_t* img, int64_t doc_base, int lane) {
+  uint32_t bits = 0;
+  if (L.kind == PA_LEAF_DICT_RANGE || L.kind == PA_LEAF_DICT_SET) {
+    const int nb = L.nbits;
+    const uint32_t mask = nbits_mask(nb);
+    const uint32_t e1 = (uint32_t)lane * (uint32_t)nb + (uint32_t)(nb - 1);
+    const uint32_t sh = (~e1) & 31u;
+    const int step = 2 * nb;  // stream words per 64-doc step
+    {
+      const uint32_t* p = img + L.lds_off + (int)(e1 >> 5);
+      if (L.kind == PA_LEAF_DICT_RANGE) {
+        // MSB-aligned decode: the window starts at the word holding the value's first bit (or the word before,
+        // when that bit is bit 0 of a word), so t = alignbit(.) carries the value in its top nb bits with junk
+        // below. With lo' = lo << (32-nb) and hi' = span << (32-nb) - 1 (host-side),
+        //   lo <= v < lo + span  <=>  (t - lo') <= hi'   (unsigned; exact for any junk bits).
+        // Non-matches accumulate as nm = 2*nm + borrow(hi' - (t - lo')): sub, sub_co, addc per 64 docs.
+        const uint32_t lo_t = (uint32_t)L.lo, hi_t = (uint32_t)L.span;  // pre-shifted by the host
+        const uint32_t b0 = (uint32_t)lane * (uint32_t)nb;
+        const uint32_t o = b0 & 31u;
+        const int ws = (int)(b0 >> 5) - (o == 0 ? 1 : 0);
+        const uint32_t shr = (32u - o) & 31u;
+        const uint32_t* pw = img + L.lds_off + ws;
+        // every scalar parameter in SGPRs before the first LDS read: a scalar load between LDS reads forces
+        // lgkmcnt(0) (SMEM returns out of order) and serialises the reads
+        uint32_t pw_off = (uint32_t)(uintptr_t)pw;
+        asm volatile("" : "+v"(pw_off) : "s"(lo_t), "s"(hi_t), "s"(step));
+        pw = (const uint32_t*)(uintptr_t)pw_off;
+        uint32_t w0[STEPS], w1[STEPS];
+#pragma unroll
+        for (int i = 0; i < STEPS; ++i) {
+          w0[i] = pw[i * step];
+          w1[i] = pw[i * step + 1];
+        }
+        uint32_t nm = 0;
+#pragma unroll
+        for (int i = STEPS - 1; i >= 0; --i) {
+          const uint32_t t = __builtin_amdgcn_alignbit(w0[i], w1[i], shr);
+          uint32_t u;
+          // u = t - lo'; borrow = hi' < u (non-match); nm = 2*nm + borrow  (the compiler otherwise rewrites the
+          // carry-add into cndmask + or)
+          asm("v_sub_u32_e64 %[u], %[t], %[lo]\n\t"
+              "v_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
+              "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
+              : [nm] "+v"(nm), [u] "=&v"(u)
+              : [t] "v"(t), [lo] "s"(lo_t), [hi] "s"(hi_t)
+              : "vcc");
+        }
+        bits = STEPS == 32 ? ~nm : (~nm & ((1u << STEPS) - 1u));
+        (void)mask;
+        (void)p;
+      } else {
+        const AS1 uint32_t* lut = gp(L.lut);
+#pragma unroll 8
+        for (int i = 0; i < STEPS; ++i) {
+          const uint32_t id = __builtin_amdgcn_alignbit(p[i * step - 1], p[i * step], sh) & mask;
+          bits |= ((lut[id >> 5] >> (id & 31u)) & 1u) << i;
+        }
+      }
+    }  // filter columns are always staged (pa_query_prepare), so there is no lazy filter-decode path
+  } else {  // PA_LEAF_RAW_RANGE: coalesced loads of the raw values
+    const int64_t d0 = doc_base + lane;
+    switch (L.vtype) {
+      case PA_INT: {
+        const AS1 int32_t* v = gp((const int32_t*)L.raw) + d0;
+#pragma unroll 8
+        for (int i = 0; i < STEPS; ++i) {
+          const int64_t x = v[i * kWave];
+          bits |= (uint32_t)(x >= L.ilo && x <= L.ihi) << i;
+        }
+      } break;
+      case PA_LONG: {
+        const AS1 int64_t* v = gp((const int64_t*)L.raw) + d0;
+#pragma unroll 8
+        for (int i = 0; i < STEPS; ++i) {
+          const int64_t x = v[i * kWave];
+          bits |= (uint32_t)(x >= L.ilo && x <= L.ihi) << i;
+        }
+      } break;
+      case PA_FLOAT: {
+        const AS1 float* v = gp((const float*)L.raw) + d0;
+#pragma unroll 8
+        for (int i = 0; i < STEPS; ++i) {
+          const double x = v[i * kWave];
+          bits |= (uint32_t)(x >= L.dlo && x <= L.dhi) << i;
+        }
+      } break;
+      default: {
+        const AS1 double* v = gp((const double*)L.raw) + d0;
+#pragma unroll 8
+        for (int i = 0; i < STEPS; ++i) {
+          const double x = v[i * kWave];
+          bits |= (uint32_t)(x >= L.dlo && x <= L.dhi) << i;
+        }
+      } break;
+    }
+  }
+  return L.negate ? ~bits : bits;
+}
+
+template <int STRAT, int STEPS>
 __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
                                              int64_t wt, const uint32_t* img, int lane, const Acc<STRAT>& acc) {
-  const int64_t doc_base = wt * kWTileDocs;
-  const int nleaves = q->num_leaves;
-  const int64_t ndocs = seg->num_docs;
-  for (int i = 0; i < kSteps; ++i) {
-    const int doc_local = i * kWave + lane;
-    const int64_t doc = doc_base + doc_local;
-    const bool valid = doc < ndocs;
-    uint64_t m = __ballot(valid);
-    if (m == 0) break;
-    uint64_t clause = 0;
-    for (int li = 0; li < nleaves; ++li) {
-      if (m == 0) break;
-      const DevLeaf& L = seg->leaves[li];
-      clause |= __ballot(eval_leaf(L, seg, img, doc_local, doc, valid));
-      if (L.clause_end) {
-        m &= clause;
-        clause = 0;
-      }
-    }
-    if (m == 0) continue;
-    accumulate_step<STRAT>(q, seg, img, doc_local, doc, m, lane, acc);
+  const int64_t doc_base = wt * (STEPS * kWave);
+  // docs of this tile owned by the lane: 64*i + lane < rem
+  const int64_t rem = (int64_t)seg->num_docs - doc_base;
+  uint32_t valid;
+  if (rem >= (STEPS * kWave)) {
+    valid = 0xffffffffu;
+  } else {
+    const int64_t n = rem > lane ? (rem - lane + kWave - 1) / kWave : 0;  // steps with a valid doc for this lane
+    valid = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
   }
+  uint32_t m = valid;
+  uint32_t clause = 0;
+  const int nleaves = q->num_leaves;
+  for (int li = 0; li < nleaves; ++li) {
+    const DevLeaf& L = seg->leaves[li];
+    clause |= leaf_bits<STEPS>(L, img, doc_base, lane);
+    if (L.clause_end) {
+      m &= clause;
+      clause = 0;
+      if (__ballot(m != 0) == 0) return;  // no doc of the tile can match any more
+    }
+  }
+  if (__ballot(m != 0) == 0) return;
+  for (int i = 0; i < STEPS; ++i) {
+    const uint64_t sm = __ballot((m >> i) & 1u);
+    if (sm == 0) continue;
+    const int doc_local = i * kWave + lane;
+    accumulate_step<STRAT>(q, seg, img, doc_local, doc_base + doc_local, sm, lane, acc);
+  }
+  // Leave no compiler-visible VMEM op pending past a tile with matches (a compiler-understood wait): otherwise the
+  // waitcnt pass guards the next tile's LDS decode with vmcnt(0) on EVERY tile, draining the DMA ring.
+  __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // vmcnt(0)
 }
 
 __device__ __forceinline__ int find_segment(const DevSeg* __restrict__ segs, int nseg, int64_t t) {
@@ -313,17 +448,49 @@ __device__ __forceinline__ int find_segment(const DevSeg* __restrict__ segs, int
   return lo;
 }
 
-template <int STRAT>
+// s_waitcnt vmcnt(N) that also "produces" `token` (the ring slot's LDS offset): every LDS read of the slot is
+// addressed through the token, so it cannot be scheduled above the wait. No "memory" clobber: a clobber would
+// make the compiler re-load every query/segment descriptor field after each wait (dependent SMEM round trips per
+// tile).
+template <int N>
+__device__ __forceinline__ void vm_wait_token(uint32_t& token) {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%1)" : "+s"(token) : "n"(N));
+}
+
+template <int D, int Y>
+__device__ __forceinline__ void vm_wait_tiles(uint32_t& token) {
+  if constexpr (Y * D < 64) vm_wait_token<Y * D>(token);
+  else vm_wait_token<0>(token);
+}
+
+// Wait until the tile with `younger` tiles issued after it has landed; `token` = its slot offset.
+template <int D>
+__device__ __forceinline__ void wait_tile(int younger, uint32_t& token) {
+  switch (younger) {
+    case 0: vm_wait_token<0>(token); break;
+    case 1: vm_wait_tiles<D, 1>(token); break;
+    case 2: vm_wait_tiles<D, 2>(token); break;
+    case 3: vm_wait_tiles<D, 3>(token); break;
+    case 4: vm_wait_tiles<D, 4>(token); break;
+    case 5: vm_wait_tiles<D, 5>(token); break;
+    case 6: vm_wait_tiles<D, 6>(token); break;
+    default: vm_wait_tiles<D, 7>(token); break;
+  }
+}
+
+template <int STRAT, int D, int STEPS>
 __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restrict__ q,
                                                        const DevSeg* __restrict__ segs) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  // wave-uniform by construction; readfirstlane makes the compiler keep the whole tile/segment cursor in SGPRs
+  // (otherwise segment descriptors are read with vector loads whose vmcnt(0) waits drain the DMA ring)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   unsigned char* lds_acc = (unsigned char*)smem;
   const uint32_t acc_dwords = STRAT == STRAT_LDS ? (q->lds_acc_bytes >> 2) : 0u;
   const int img_dw = q->image_dwords_max;
-  uint32_t* img0 = smem + acc_dwords + wave * 2 * img_dw;
-  uint32_t* img1 = img0 + img_dw;
+  uint32_t* ring = smem + acc_dwords + wave * q->ring * img_dw;
   Acc<STRAT> acc{q, lds_acc};
 
   if (STRAT == STRAT_LDS) {
@@ -352,19 +519,45 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
   const int64_t t0 = gw * T / W;
   const int64_t t1 = (gw + 1) * T / W;
   if (t0 < t1) {
-    const DevSeg* seg = segs + find_segment(segs, q->num_segments, t0);
-    stage_tile(q, seg, t0 - seg->first_wtile, img0, lane);
-    for (int64_t t = t0; t < t1; ++t) {
-      const bool odd = ((t - t0) & 1) != 0;
-      uint32_t* img = odd ? img1 : img0;
-      uint32_t* nimg = odd ? img0 : img1;
-      vm_wait_all();  // tile t has landed in `img` (same-wave LDS-DMA: vmcnt covers it)
-      const DevSeg* cur = seg;
-      if (t + 1 < t1) {
-        while (t + 1 >= seg->first_wtile + seg->num_wtiles) ++seg;
-        stage_tile(q, seg, t + 1 - seg->first_wtile, nimg, lane);
+    // Ring of R wave-tile images: tiles t+1 .. t+R-1 stream in (LDS-DMA) while tile t is decoded; each tile is
+    // exactly D DMA instructions, so "tile t landed" is vmcnt(<= (tiles issued after t) * D).
+    const int R = q->ring;
+    int isi = find_segment(segs, q->num_segments, t0);   // issue cursor: segment, its tile range, ring slot
+    int64_t ifirst = segs[isi].first_wtile;
+    int64_t iend = ifirst + segs[isi].num_wtiles;
+    int64_t ti = t0;
+    int islot = 0;
+    auto issue_next = [&]() {
+      while (ti >= iend) {
+        ++isi;
+        ifirst = segs[isi].first_wtile;
+        iend = ifirst + segs[isi].num_wtiles;
       }
-      process_tile<STRAT>(q, cur, t - cur->first_wtile, img, lane, acc);
+      stage_tile<D, STEPS>(segs + isi, ti - ifirst, ring + islot * img_dw, lane);
+      ++ti;
+      islot = islot + 1 == R ? 0 : islot + 1;
+    };
+    for (int k = 0; k < R - 1 && ti < t1; ++k) issue_next();
+
+    int si = find_segment(segs, q->num_segments, t0);
+    int pslot = 0;
+    int64_t t = t0;
+    while (t < t1) {
+      // segment-outer / tile-inner: `seg` is invariant in the inner loop, so its descriptors stay in SGPRs
+      const DevSeg* seg = segs + si;
+      const int64_t seg_first = seg->first_wtile;
+      const int64_t seg_end = min(t1, seg_first + (int64_t)seg->num_wtiles);
+      for (; t < seg_end; ++t) {
+        uint32_t slot_off = (uint32_t)(pslot * img_dw);
+        wait_tile<D>((int)(ti - (t + 1)), slot_off);  // tile t has landed in its slot (same-wave LDS-DMA)
+        if (ti < t1) issue_next();                     // refill the slot tile t-1 used
+        if (!q->debug_stream_only) process_tile<STRAT, STEPS>(q, seg, t - seg_first, ring + slot_off, lane, acc);
+        pslot = pslot + 1 == R ? 0 : pslot + 1;
+      }
+      if (t < t1) {
+        ++si;
+        while (t >= segs[si].first_wtile + segs[si].num_wtiles) ++si;
+      }
     }
   }
 
@@ -375,28 +568,28 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
     for (int64_t k = threadIdx.x; k < K; k += kWGSize) {
       const uint32_t c = cnt[k];
       if (c == 0) continue;
-      atomicAdd(q->count + k, (unsigned long long)c);
+      __hip_atomic_fetch_add(gp(q->count) + k, (unsigned long long)c, RLX);
       for (int a = 0; a < q->num_aggs; ++a) {
         const DevAgg& A = q->aggs[a];
         switch (A.type) {
           case PA_AGG_SUM:
             if (A.src == SRC_INT) {
-              atomicAdd((unsigned long long*)A.acc_i64 + k, ((const unsigned long long*)(lds_acc + A.lds_off))[k]);
+              __hip_atomic_fetch_add(gp((unsigned long long*)A.acc_i64) + k, ((const unsigned long long*)(lds_acc + A.lds_off))[k], RLX);
             } else if (A.src == SRC_LONG) {
               const unsigned long long* r = (const unsigned long long*)(lds_acc + A.lds_off);
-              atomicAdd((unsigned long long*)A.acc_i64 + 2 * k, r[2 * k]);
-              atomicAdd((unsigned long long*)A.acc_i64 + 2 * k + 1, r[2 * k + 1]);
+              __hip_atomic_fetch_add(gp((unsigned long long*)A.acc_i64) + 2 * k, r[2 * k], RLX);
+              __hip_atomic_fetch_add(gp((unsigned long long*)A.acc_i64) + 2 * k + 1, r[2 * k + 1], RLX);
             } else {
-              atomicAdd(A.acc_f64 + k, ((const double*)(lds_acc + A.lds_off))[k]);
+              __hip_atomic_fetch_add(gp(A.acc_f64) + k, ((const double*)(lds_acc + A.lds_off))[k], RLX);
             }
             break;
-          case PA_AGG_MIN: atomicMin((long long*)A.acc_i64 + k, ((const long long*)(lds_acc + A.lds_off))[k]); break;
-          case PA_AGG_MAX: atomicMax((long long*)A.acc_i64 + k, ((const long long*)(lds_acc + A.lds_off))[k]); break;
+          case PA_AGG_MIN: __hip_atomic_fetch_min(gp((long long*)A.acc_i64) + k, ((const long long*)(lds_acc + A.lds_off))[k], RLX); break;
+          case PA_AGG_MAX: __hip_atomic_fetch_max(gp((long long*)A.acc_i64) + k, ((const long long*)(lds_acc + A.lds_off))[k], RLX); break;
           case PA_AGG_DISTINCTCOUNTHLL: {
             const uint32_t* r = (const uint32_t*)(lds_acc + A.lds_off) + (k << A.log2m);
             uint32_t* g = A.acc_hll + (k << A.log2m);
             for (int j = 0; j < (1 << A.log2m); ++j)
-              if (r[j] != 0) atomicMax(g + j, r[j]);
+              if (r[j] != 0) __hip_atomic_fetch_max(gp(g) + j, r[j], RLX);
           } break;
           default: break;
         }
@@ -484,16 +677,33 @@ hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t*
   return hipGetLastError();
 }
 
-hipError_t set_scan_lds_limit(int strategy, int bytes) {
-  if (strategy == STRAT_LDS)
-    return hipFuncSetAttribute((const void*)scan_kernel<STRAT_LDS>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-  return hipFuncSetAttribute((const void*)scan_kernel<STRAT_GLOBAL>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+template <int STRAT, int STEPS>
+static const void* scan_fn(int d) {
+  switch (d) {
+    case 4: return (const void*)scan_kernel<STRAT, 4, STEPS>;
+    case 8: return (const void*)scan_kernel<STRAT, 8, STEPS>;
+    case 16: return (const void*)scan_kernel<STRAT, 16, STEPS>;
+    default: return (const void*)scan_kernel<STRAT, 32, STEPS>;
+  }
 }
 
-hipError_t launch_scan(int strategy, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs, hipStream_t s) {
-  if (strategy == STRAT_LDS) scan_kernel<STRAT_LDS><<<grid, kWGSize, lds_bytes, s>>>(q, segs);
-  else scan_kernel<STRAT_GLOBAL><<<grid, kWGSize, lds_bytes, s>>>(q, segs);
-  return hipGetLastError();
+static const void* scan_fn_any(int strategy, int d, int steps) {
+  if (strategy == STRAT_LDS) return steps == 16 ? scan_fn<STRAT_LDS, 16>(d) : scan_fn<STRAT_LDS, 32>(d);
+  return steps == 16 ? scan_fn<STRAT_GLOBAL, 16>(d) : scan_fn<STRAT_GLOBAL, 32>(d);
+}
+
+int scan_dma_slots(int needed) {
+  return needed <= 4 ? 4 : needed <= 8 ? 8 : needed <= 16 ? 16 : needed <= 32 ? 32 : -1;
+}
+
+hipError_t set_scan_lds_limit(int strategy, int d, int steps, int bytes) {
+  return hipFuncSetAttribute(scan_fn_any(strategy, d, steps), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+hipError_t launch_scan(int strategy, int d, int steps, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs,
+                       hipStream_t s) {
+  void* args[] = {(void*)&q, (void*)&segs};
+  return hipLaunchKernel(scan_fn_any(strategy, d, steps), dim3(grid), dim3(kWGSize), args, (size_t)lds_bytes, s);
 }
 
 }  // namespace pa

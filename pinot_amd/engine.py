@@ -289,7 +289,13 @@ class GpuQueryExecutor:
     def stats(self):
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         L.check(L.lib().pa_query_stats(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "stats")
-        return {"staged_bytes": a.value, "num_docs": b.value, "num_wave_tiles": c.value}
+        out = {"staged_bytes": a.value, "num_docs": b.value, "num_wave_tiles": c.value}
+        vals = [ctypes.c_int32() for _ in range(7)]
+        L.check(L.lib().pa_query_plan(self.handle, *[ctypes.byref(v) for v in vals]), "plan")
+        names = ("strategy", "steps", "dma_slots", "ring", "wg_per_cu", "grid", "lds_bytes")
+        out["plan"] = {n: v.value for n, v in zip(names, vals)}
+        out["plan"]["strategy"] = "lds" if out["plan"]["strategy"] == 0 else "global"
+        return out
 
     def fetch(self, stream=None) -> IntermediateResult:
         lib = L.lib()
