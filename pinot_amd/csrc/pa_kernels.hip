@@ -322,12 +322,13 @@ __device__ __forceinline__ uint32_t leaf_bits(const DevLeaf& L, const uint32_t* 
         const uint32_t o = b0 & 31u;
         const int ws = (int)(b0 >> 5) - (o == 0 ? 1 : 0);
         const uint32_t shr = (32u - o) & 31u;
-        const uint32_t* pw = img + L.lds_off + ws;
         // every scalar parameter in SGPRs before the first LDS read: a scalar load between LDS reads forces
-        // lgkmcnt(0) (SMEM returns out of order) and serialises the reads
-        uint32_t pw_off = (uint32_t)(uintptr_t)pw;
+        // lgkmcnt(0) (SMEM returns out of order) and serialises the reads. The window pointer goes through the asm
+        // as a 32-bit LDS offset and comes back as an address-space-3 pointer (ds_read; a generic pointer rebuilt
+        // from 32 bits would lose the shared aperture and address global memory).
+        uint32_t pw_off = lds_addr(img + L.lds_off + ws);
         asm volatile("" : "+v"(pw_off) : "s"(lo_t), "s"(hi_t), "s"(step));
-        pw = (const uint32_t*)(uintptr_t)pw_off;
+        const lds_u32_t* pw = (const lds_u32_t*)(uintptr_t)pw_off;
         uint32_t w0[STEPS], w1[STEPS];
 #pragma unroll
         for (int i = 0; i < STEPS; ++i) {
