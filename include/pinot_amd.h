@@ -163,8 +163,10 @@ typedef struct {
 /* tuning overrides of the tile planner (0 = automatic) */
 #define PA_QF_STEPS16 (1 << 4)        /* 1024-doc wave tiles */
 #define PA_QF_STEPS32 (1 << 5)        /* 2048-doc wave tiles */
+#define PA_QF_NO_LAZY (1 << 6)        /* evaluate every filter clause on staged tiles (no late materialisation) */
+#define PA_QF_FORCE_LDS (1 << 7)      /* LDS-privatised accumulators even for sparse results (when they fit) */
 #define PA_QF_RING_SHIFT 8            /* bits 8..11: tile images per wave (2..8) */
-#define PA_QF_WG_SHIFT 12             /* bits 12..13: workgroups per CU (1..3) */
+#define PA_QF_WG_SHIFT 12             /* bits 12..14: workgroups per CU (1..4) */
 #define PA_QF_DEBUG_STREAM_ONLY (1 << 16) /* measurement only: stream the tiles, skip decode (results invalid) */
 
 /* per-(segment, leaf) parameters in that segment's dictId space */
@@ -194,8 +196,11 @@ int pa_query_prepare(pa_query* q);
 int64_t pa_query_num_keys(const pa_query* q);
 
 /* Zeroes the accumulators and runs the fused scan (filter + group-key + aggregate) over every bound
- * segment on `stream` (hipStream_t, NULL = default stream). Asynchronous. */
+ * segment on `stream` (hipStream_t, NULL = default stream). Asynchronous. Equivalent to pa_query_reset followed by
+ * pa_query_scan (the two halves exist so a caller can time the scan kernel alone). */
 int pa_query_execute(pa_query* q, void* stream);
+int pa_query_reset(pa_query* q, void* stream);
+int pa_query_scan(pa_query* q, void* stream);
 
 /* Accumulator sections, for the cross-GPU RCCL reduce. section kinds: */
 #define PA_ACC_COUNT_U64 0 /* reduce SUM */
@@ -230,6 +235,8 @@ int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs
 
 /* The kernel plan chosen by pa_query_prepare: accumulator strategy (0 = LDS-privatised, 1 = global), 64-doc
  * steps per wave tile, DMA instructions per tile, tile images per wave, workgroups per CU, grid, LDS bytes. */
+/* Filter literals evaluated on whole staged tiles (the rest only on the docs those matched). */
+int32_t pa_query_num_eager_literals(const pa_query* q);
 int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t* dma_slots, int32_t* ring,
                   int32_t* wg_per_cu, int32_t* grid, int32_t* lds_bytes);
 

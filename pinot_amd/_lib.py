@@ -21,6 +21,8 @@ PA_QF_STAGE_ALL = 1
 PA_QF_FORCE_GLOBAL = 2
 PA_QF_STEPS16 = 1 << 4
 PA_QF_STEPS32 = 1 << 5
+PA_QF_NO_LAZY = 1 << 6
+PA_QF_FORCE_LDS = 1 << 7
 PA_QF_RING_SHIFT = 8
 PA_QF_WG_SHIFT = 12
 PA_QF_DEBUG_STREAM_ONLY = 1 << 16
@@ -33,7 +35,8 @@ EXPORTED = [
     "pa_segment_create", "pa_segment_add_sv_dict_column", "pa_segment_add_mv_dict_column",
     "pa_segment_add_raw_column", "pa_segment_num_docs", "pa_segment_device_bytes", "pa_segment_destroy",
     "pa_query_create", "pa_query_bind_segment", "pa_query_prepare", "pa_query_num_keys",
-    "pa_query_execute", "pa_query_accumulator_bytes", "pa_query_set_accumulator_buffer", "pa_query_num_sections", "pa_query_section", "pa_query_fetch", "pa_query_stats",
+    "pa_query_execute", "pa_query_reset", "pa_query_scan", "pa_query_num_eager_literals",
+    "pa_query_accumulator_bytes", "pa_query_set_accumulator_buffer", "pa_query_num_sections", "pa_query_section", "pa_query_fetch", "pa_query_stats",
     "pa_query_plan", "pa_query_destroy",
 ]
 
@@ -98,6 +101,9 @@ def _declare(lib):
         "pa_query_prepare": (ctypes.c_int, [vp]),
         "pa_query_num_keys": (i64, [vp]),
         "pa_query_execute": (ctypes.c_int, [vp, vp]),
+        "pa_query_reset": (ctypes.c_int, [vp, vp]),
+        "pa_query_scan": (ctypes.c_int, [vp, vp]),
+        "pa_query_num_eager_literals": (i32, [vp]),
         "pa_query_accumulator_bytes": (u64, [vp]),
         "pa_query_set_accumulator_buffer": (ctypes.c_int, [vp, vp, u64]),
         "pa_query_num_sections": (i32, [vp]),

@@ -325,6 +325,7 @@ struct pa_query {
   int grid = 0;
   int steps = 32;
   int dma_slots = 8;
+  int num_eager = 0;
   int plan_ring = 2;
   int plan_wg = 1;
   int lds_bytes = 0;
@@ -357,6 +358,28 @@ int slot_of(pa_query* q, int32_t col) {
   if ((int)q->slot_cols.size() >= kMaxSlots) return -1;
   q->slot_cols.push_back(col);
   return (int)q->slot_cols.size() - 1;
+}
+
+// Estimated fraction of a segment's docs a literal matches: the matching-dictId fraction of the dictionary (dictIds
+// assumed equally frequent), 1/2 for raw-value leaves. Planning input only: results never depend on it.
+double leaf_selectivity(const pa_query* q, int si, int leaf, bool neg_literal) {
+  const pa_query_spec& s = q->spec;
+  const pa_leaf_params& p = q->leaf_params[si][leaf];
+  const int kind = s.leaves[leaf].kind;
+  auto it = q->segs[si]->cols.find(s.leaves[leaf].column_id);
+  if (it == q->segs[si]->cols.end() || (kind != PA_LEAF_DICT_RANGE && kind != PA_LEAF_DICT_SET)) return 0.5;
+  const int64_t card = std::max<int32_t>(1, it->second->cardinality);
+  double sel;
+  if (kind == PA_LEAF_DICT_RANGE) {
+    const int64_t lo = std::max<int64_t>(0, p.lo), hi = std::min<int64_t>(p.hi, card);
+    sel = hi > lo ? (double)(hi - lo) / (double)card : 0.0;
+  } else {
+    const std::vector<uint32_t>& lut = q->luts[si][leaf];
+    int64_t n = 0;
+    for (int64_t id = 0; id < card && (size_t)(id >> 5) < lut.size(); ++id) n += (lut[id >> 5] >> (id & 31)) & 1u;
+    sel = (double)n / (double)card;
+  }
+  return ((p.negate != 0) != neg_literal) ? 1.0 - sel : sel;
 }
 
 int upload_owned(pa_query* q, const void* host, size_t bytes, void** dev) {
@@ -440,25 +463,56 @@ int pa_query_prepare(pa_query* q) {
   std::vector<Clause> cnf;
   int rc = to_cnf(s, cnf);
   if (rc) return rc;
+  for (int l = 0; l < s.num_leaves; ++l) {
+    const int k = s.leaves[l].kind;
+    if (k == PA_LEAF_MV_DICT_RANGE || k == PA_LEAF_MV_DICT_SET)
+      return fail(PA_EUNSUPPORTED, "multi-value filter leaves are not implemented yet");
+  }
+  // Clause order and late materialisation. Clauses are evaluated most selective first (estimated from the
+  // matching-dictId fraction, i.e. assuming dictIds are equally frequent; only speed depends on the estimate).
+  // The leading clauses whose expected survivors per wave tile exceed kLazyDensity run on whole staged tiles
+  // ("eager"); the rest only on surviving docs, from HBM ("lazy") — the reference's AndDocIdIterator likewise
+  // advances later iterators only to candidate docs (operator/dociditerators/AndDocIdIterator.java).
+  const double kLazyDensity = 0.25;
+  std::vector<double> csel(cnf.size(), 1.0);
+  for (size_t c = 0; c < cnf.size(); ++c) {
+    double worst = q->nseg ? 0.0 : 1.0;
+    for (int si = 0; si < q->nseg; ++si) {
+      double sum = 0.0;
+      for (const Literal& lit : cnf[c]) sum += leaf_selectivity(q, si, lit.leaf, lit.neg);
+      worst = std::max(worst, std::min(1.0, sum));
+    }
+    csel[c] = worst;
+  }
+  std::vector<size_t> order(cnf.size());
+  for (size_t c = 0; c < cnf.size(); ++c) order[c] = c;
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return csel[a] < csel[b]; });
+  const bool no_lazy = (s.flags & (PA_QF_STAGE_ALL | PA_QF_NO_LAZY)) != 0;
+  size_t eager_clauses = 0;
+  double density = (double)kWTileDocs;  // expected surviving docs per wave tile
+  while (eager_clauses < cnf.size() && (no_lazy || eager_clauses == 0 || density > kLazyDensity))
+    density *= csel[order[eager_clauses++]];
+  double post_density = density;
+  for (size_t c = eager_clauses; c < cnf.size(); ++c) post_density *= csel[order[c]];
   q->literals.clear();
   q->clause_end.clear();
-  for (auto& c : cnf) {
+  q->num_eager = 0;
+  for (size_t oc = 0; oc < cnf.size(); ++oc) {
+    const Clause& c = cnf[order[oc]];
     for (size_t i = 0; i < c.size(); ++i) {
       q->literals.push_back(c[i]);
       q->clause_end.push_back(i + 1 == c.size());
     }
+    if (oc < eager_clauses) q->num_eager = (int)q->literals.size();
   }
-  std::vector<char> leaf_slot_is_filter(kMaxSlots, 0);
+  std::vector<char> slot_eager(kMaxSlots, 0);
   std::vector<int> leaf_slot(s.num_leaves, -1);
   for (int l = 0; l < s.num_leaves; ++l) {
     const int sl = slot_of(q, s.leaves[l].column_id);
     if (sl < 0) return fail(PA_EUNSUPPORTED, "too many distinct columns in one query");
     leaf_slot[l] = sl;
-    leaf_slot_is_filter[sl] = 1;
-    const int k = s.leaves[l].kind;
-    if (k == PA_LEAF_MV_DICT_RANGE || k == PA_LEAF_MV_DICT_SET)
-      return fail(PA_EUNSUPPORTED, "multi-value filter leaves are not implemented yet");
   }
+  for (int li = 0; li < q->num_eager; ++li) slot_eager[leaf_slot[q->literals[li].leaf]] = 1;
   std::vector<int> gb_slot(s.num_group_by);
   for (int j = 0; j < s.num_group_by; ++j) {
     gb_slot[j] = slot_of(q, s.group_by_columns[j]);
@@ -476,7 +530,15 @@ int pa_query_prepare(pa_query* q) {
   }
   const int nslots = (int)q->slot_cols.size();
   const bool has_filter = !q->literals.empty();
+  // Post-filter columns (group-by keys, aggregated values) are staged with the filter columns when the filter lets
+  // more than kLazyPost docs per wave tile through; below that each surviving doc reads them from HBM.
+  const double kLazyPost = 0.25;
   const bool stage_all = !has_filter || (s.flags & PA_QF_STAGE_ALL);
+  const bool stage_post = stage_all || post_density > kLazyPost;
+  std::vector<char> slot_post(kMaxSlots, 0);
+  for (int j = 0; j < s.num_group_by; ++j) slot_post[gb_slot[j]] = 1;
+  for (int a = 0; a < s.num_aggs; ++a)
+    if (s.aggs[a].type != PA_AGG_COUNT) slot_post[agg_slot[a]] = 1;
 
   // ---- key space
   int64_t K = 1;
@@ -518,7 +580,7 @@ int pa_query_prepare(pa_query* q) {
       dc.dict_i64 = (c->vtype == PA_INT || c->vtype == PA_LONG) ? (const int64_t*)c->dict.p : nullptr;
       dc.dict_f64 = (c->vtype == PA_FLOAT || c->vtype == PA_DOUBLE) ? (const double*)c->dict.p : nullptr;
       dc.lds_off = -1;
-      if (c->kind == COL_SV_DICT && (leaf_slot_is_filter[sl] || stage_all)) {
+      if (c->kind == COL_SV_DICT && (slot_eager[sl] || stage_all || (stage_post && slot_post[sl]))) {
         staged[sl] = 1;
         dc.lds_off = 0;  // staged; the region offset depends on the tile size (apply_layout below)
         d.stage[d.num_staged++] = StageDesc{dc.words, dc.nbits, 0};
@@ -666,8 +728,9 @@ int pa_query_prepare(pa_query* q) {
     lds_acc += (bytes + 15) & ~(size_t)15;
   }
   // ---- tile geometry: wave tile of 1024 or 2048 docs, D DMA instructions per tile, a ring of R tile images per
-  // wave (R-1 tiles in flight). HBM latency under full load is several microseconds, so the plan maximises the
-  // bytes in flight per CU (~128 KiB sustain the HBM rate) within 160 KiB of LDS, then prefers more waves.
+  // wave (R-1 tiles in flight). Measured on MI355X (tools/sweep.py): the decode, not the DMA, is what needs
+  // hiding, so the plan maximises resident waves per CU (workgroups per CU, checked against the occupancy the
+  // compiled kernel really has), then prefers 2048-doc tiles, then bytes in flight (capped at 128 KiB per CU).
   const size_t kLdsBudget = 160 * 1024;
   struct Plan {
     int steps = 0, dma = 0, ring = 0, wg_per_cu = 0, img_dw = 0;
@@ -675,13 +738,14 @@ int pa_query_prepare(pa_query* q) {
     double score = -1;
   };
   const int force_ring = (s.flags >> PA_QF_RING_SHIFT) & 15;
-  const int force_wg = (s.flags >> PA_QF_WG_SHIFT) & 3;
-  auto plan_for = [&](bool lds_strategy) {
+  const int force_wg = (s.flags >> PA_QF_WG_SHIFT) & 7;
+  auto plan_for = [&](int strat) {
+    const bool lds_strategy = strat == STRAT_LDS;
     Plan best;
     for (int steps : {32, 16}) {
       if ((s.flags & PA_QF_STEPS16) && steps != 16) continue;
       if ((s.flags & PA_QF_STEPS32) && steps != 32) continue;
-      int img_dw = kGuardWords, need = 0;
+      int img_dw = kGuardWords, dma = 0;
       for (int si = 0; si < q->nseg; ++si) {
         int dw = kGuardWords, n = 0;
         for (int k = 0; k < q->hsegs[si].num_staged; ++k) {
@@ -690,40 +754,44 @@ int pa_query_prepare(pa_query* q) {
           n += ((steps / 2) * nb + 63) / 64;
         }
         img_dw = std::max(img_dw, dw);
-        need = std::max(need, n);
+        dma = std::max(dma, n);
       }
-      const int dma = scan_dma_slots(need);
-      if (dma < 0) continue;
       const size_t img_bytes = (size_t)img_dw * 4;
       const size_t acc_b = lds_strategy ? lds_acc : 0;
-      for (int wg : {3, 2, 1}) {
+      for (int wg : {4, 3, 2, 1}) {
         if (force_wg && wg != force_wg) continue;
-        if (!force_wg && wg == 3) continue;
         const size_t per_wg = kLdsBudget / wg;
         if (per_wg <= acc_b) continue;
         int ring = (int)((per_wg - acc_b) / (kWavesPerWG * img_bytes));
-        ring = std::min({ring, 8, 2 + 63 / dma});
+        ring = std::min(ring, 8);
         if (force_ring) {
           if (force_ring > ring) continue;
           ring = force_ring;
         }
         if (ring < 2) continue;
+        const size_t lds = acc_b + (size_t)kWavesPerWG * ring * img_bytes;
+        int resident = 0;
+        if (set_scan_lds_limit(strat, steps, (int)kLdsBudget) != hipSuccess ||
+            scan_occupancy(strat, steps, (int)lds, &resident) != hipSuccess)
+          resident = wg;  // no device to ask (planning only): trust the LDS arithmetic
+        if (resident < wg) continue;
         const double inflight = (double)wg * kWavesPerWG * (ring - 1) * img_bytes;
-        const double score = std::min(inflight, 128.0 * 1024) + 4096.0 * wg + (steps == 32 ? 1 : 0);
-        if (score > best.score) {
-          best = Plan{steps, dma, ring, wg, img_dw, acc_b + (size_t)kWavesPerWG * ring * img_bytes, score};
-        }
+        const double score = 1e7 * wg + (steps == 32 ? 1e6 : 0) + std::min(inflight, 128.0 * 1024);
+        if (score > best.score) best = Plan{steps, dma, ring, wg, img_dw, lds, score};
       }
     }
     return best;
   };
+  // LDS-privatised accumulators when many docs are expected to reach them (and the key space fits); otherwise the
+  // LDS goes to tile rings (more resident waves) and the rare survivors update global accumulators directly.
+  const bool dense = !has_filter || post_density >= 1.0;
   Plan plan;
   q->strategy = STRAT_GLOBAL;
-  if (!(s.flags & PA_QF_FORCE_GLOBAL) && lds_acc <= 64 * 1024) {
-    plan = plan_for(true);
+  if (!(s.flags & PA_QF_FORCE_GLOBAL) && lds_acc <= 64 * 1024 && (dense || (s.flags & PA_QF_FORCE_LDS))) {
+    plan = plan_for(STRAT_LDS);
     if (plan.score >= 0) q->strategy = STRAT_LDS;
   }
-  if (q->strategy == STRAT_GLOBAL) plan = plan_for(false);
+  if (q->strategy == STRAT_GLOBAL) plan = plan_for(STRAT_GLOBAL);
   if (plan.score < 0) return fail(PA_EUNSUPPORTED, "staged columns too wide for the LDS tile ring");
   q->lds_bytes = (int)plan.lds;
   q->steps = plan.steps;
@@ -777,6 +845,8 @@ int pa_query_prepare(pa_query* q) {
   h.num_keys = K;
   h.total_wtiles = first;
   h.ring = plan.ring;
+  h.num_eager = q->num_eager;
+  h.dma_per_tile = plan.dma;
   h.steps = plan.steps;
   h.debug_stream_only = (s.flags & PA_QF_DEBUG_STREAM_ONLY) ? 1 : 0;
   q->plan_ring = plan.ring;
@@ -819,7 +889,7 @@ int pa_query_prepare(pa_query* q) {
   if (rc) return rc;
   PA_HIP(hipMemcpy(q->dq.p, &h, sizeof(DevQuery), hipMemcpyHostToDevice));
   if (q->nseg) PA_HIP(hipMemcpy(q->dsegs.p, q->hsegs.data(), sizeof(DevSeg) * q->nseg, hipMemcpyHostToDevice));
-  PA_HIP(set_scan_lds_limit(q->strategy, q->dma_slots, q->steps, q->lds_bytes));
+  PA_HIP(set_scan_lds_limit(q->strategy, q->steps, q->lds_bytes));
   PA_HIP(hipDeviceSynchronize());
   q->prepared = true;
   return PA_OK;
@@ -827,7 +897,7 @@ int pa_query_prepare(pa_query* q) {
 
 int64_t pa_query_num_keys(const pa_query* q) { return q ? q->num_keys : -1; }
 
-int pa_query_execute(pa_query* q, void* stream) {
+int pa_query_reset(pa_query* q, void* stream) {
   if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
   hipStream_t st = (hipStream_t)stream;
   for (const Section& sc : q->sections) {
@@ -835,9 +905,20 @@ int pa_query_execute(pa_query* q, void* stream) {
     else if (sc.kind == PA_ACC_MAX_I64) PA_HIP(launch_fill_i64((int64_t*)sc.ptr, sc.n, INT64_MIN, st));
     else PA_HIP(hipMemsetAsync(sc.ptr, 0, (size_t)sc.n * (sc.kind == PA_ACC_HLL_U32 ? 4 : 8), st));
   }
-  if (q->num_tiles == 0) return PA_OK;
-  PA_HIP(launch_scan(q->strategy, q->dma_slots, q->steps, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p, (const DevSeg*)q->dsegs.p, st));
   return PA_OK;
+}
+
+int pa_query_scan(pa_query* q, void* stream) {
+  if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
+  if (q->num_tiles == 0) return PA_OK;
+  PA_HIP(launch_scan(q->strategy, q->steps, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p,
+                     (const DevSeg*)q->dsegs.p, (hipStream_t)stream));
+  return PA_OK;
+}
+
+int pa_query_execute(pa_query* q, void* stream) {
+  const int rc = pa_query_reset(q, stream);
+  return rc ? rc : pa_query_scan(q, stream);
 }
 
 uint64_t pa_query_accumulator_bytes(const pa_query* q) { return q ? (uint64_t)q->acc.n : 0; }
@@ -979,6 +1060,8 @@ int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t*
   if (lds_bytes) *lds_bytes = q->lds_bytes;
   return PA_OK;
 }
+
+int32_t pa_query_num_eager_literals(const pa_query* q) { return q && q->prepared ? q->num_eager : -1; }
 
 void pa_query_destroy(pa_query* q) { delete q; }
 

@@ -104,7 +104,10 @@ struct DevQuery {
   int32_t ring;              // wave-tile images per wave (tiles in flight = ring - 1)
   int32_t steps;             // 64-doc steps per wave tile (16 or 32)
   int32_t debug_stream_only; // measurement only: skip the decode (PA_QF_DEBUG_STREAM_ONLY)
-  int32_t pad0;
+  int32_t num_eager;         // literals [0, num_eager) are evaluated on whole staged tiles; the rest (whole CNF
+                             // clauses) only on docs the eager clauses matched, straight from HBM
+  int32_t dma_per_tile;      // LDS-DMA wave instructions per wave tile (max over segments)
+  int32_t pad1;
   int32_t staged_slots[kMaxSlots];
   int32_t gb_slot[PA_MAX_GROUP_BY];
   int64_t gb_stride[PA_MAX_GROUP_BY];

@@ -68,8 +68,9 @@ __device__ __forceinline__ void vm_wait() {
 }
 
 // Issue the LDS-DMA of one wave tile of every staged column of `seg` into the wave image `img`: exactly D
-// wave instructions (the host guarantees the real count <= D; the rest are 16-byte dummies into the image's
-// guard words), so `vmcnt` counts tiles and a ring of tiles can be in flight behind counted waits.
+// wave instructions (D = the maximum over the query's segments; a segment needing fewer pads with 16-byte
+// dummies into the image's guard words), so `vmcnt` counts tiles and a ring of tiles can be in flight behind
+// counted waits.
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
@@ -91,8 +92,9 @@ __device__ __forceinline__ void dma16(const void* src, uint32_t lds_base) {
       : "v"(src), "s"(lds_base));
 }
 
-template <int D, int STEPS>
-__device__ __forceinline__ void stage_tile(const DevSeg* __restrict__ seg, int64_t wt, uint32_t* img, int lane) {
+template <int STEPS>
+__device__ __forceinline__ void stage_tile(const DevSeg* __restrict__ seg, int64_t wt, uint32_t* img, int lane,
+                                           const int D) {
   const int ns = seg->num_staged;
   int issued = 0;
   for (int si = 0; si < ns; ++si) {
@@ -401,6 +403,32 @@ __device__ __forceinline__ uint32_t leaf_bits(const DevLeaf& L, const uint32_t* 
   return L.negate ? ~bits : bits;
 }
 
+// One literal on one doc, read straight from HBM: the lazy clauses, evaluated only on docs every eager clause
+// matched (the leap-frog evaluation of the reference's AndDocIdIterator: later iterators only advance to candidate
+// docs). DICT_RANGE bounds are stored MSB-aligned for leaf_bits; lo = lo' >> (32-nb), span = (hi' + 1) >> (32-nb).
+__device__ __forceinline__ bool leaf_match_doc(const DevLeaf& L, int64_t doc) {
+  bool m;
+  if (L.kind == PA_LEAF_DICT_RANGE || L.kind == PA_LEAF_DICT_SET) {
+    const uint32_t id = decode_global(L.words, doc, L.nbits);
+    if (L.kind == PA_LEAF_DICT_RANGE) {
+      const int sh = 32 - L.nbits;
+      const uint32_t lo = (uint32_t)L.lo >> sh;
+      const uint32_t span = (uint32_t)(((uint64_t)(uint32_t)L.span + 1u) >> sh);
+      m = (id - lo) < span;
+    } else {
+      m = (gp(L.lut)[id >> 5] >> (id & 31u)) & 1u;
+    }
+  } else {
+    switch (L.vtype) {
+      case PA_INT: { const int64_t x = gp((const int32_t*)L.raw)[doc]; m = x >= L.ilo && x <= L.ihi; } break;
+      case PA_LONG: { const int64_t x = gp((const int64_t*)L.raw)[doc]; m = x >= L.ilo && x <= L.ihi; } break;
+      case PA_FLOAT: { const double x = gp((const float*)L.raw)[doc]; m = x >= L.dlo && x <= L.dhi; } break;
+      default: { const double x = gp((const double*)L.raw)[doc]; m = x >= L.dlo && x <= L.dhi; } break;
+    }
+  }
+  return m != (L.negate != 0);
+}
+
 template <int STRAT, int STEPS>
 __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
                                              int64_t wt, const uint32_t* img, int lane, const Acc<STRAT>& acc) {
@@ -417,7 +445,8 @@ __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, con
   uint32_t m = valid;
   uint32_t clause = 0;
   const int nleaves = q->num_leaves;
-  for (int li = 0; li < nleaves; ++li) {
+  const int neager = q->num_eager;
+  for (int li = 0; li < neager; ++li) {
     const DevLeaf& L = seg->leaves[li];
     clause |= leaf_bits<STEPS>(L, img, doc_base, lane);
     if (L.clause_end) {
@@ -427,6 +456,26 @@ __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, con
     }
   }
   if (__ballot(m != 0) == 0) return;
+  if (neager < nleaves) {
+    // lazy clauses: only the (rare) docs the eager clauses kept, one 64-doc step at a time
+    for (int i = 0; i < STEPS; ++i) {
+      const uint32_t bit = 1u << i;
+      if (__ballot((m & bit) != 0) == 0) continue;
+      const int64_t doc = doc_base + i * kWave + lane;
+      bool ok = (m & bit) != 0;
+      bool any = false;
+      for (int li = neager; li < nleaves; ++li) {
+        const DevLeaf& L = seg->leaves[li];
+        if (ok && !any) any = leaf_match_doc(L, doc);
+        if (L.clause_end) {
+          ok = ok && any;
+          any = false;
+        }
+      }
+      if (!ok) m &= ~bit;
+    }
+    if (__ballot(m != 0) == 0) return;
+  }
   for (int i = 0; i < STEPS; ++i) {
     const uint64_t sm = __ballot((m >> i) & 1u);
     if (sm == 0) continue;
@@ -459,28 +508,27 @@ __device__ __forceinline__ void vm_wait_token(uint32_t& token) {
   asm volatile("s_waitcnt vmcnt(%1)" : "+s"(token) : "n"(N));
 }
 
-template <int D, int Y>
-__device__ __forceinline__ void vm_wait_tiles(uint32_t& token) {
-  if constexpr (Y * D < 64) vm_wait_token<Y * D>(token);
-  else vm_wait_token<0>(token);
-}
-
-// Wait until the tile with `younger` tiles issued after it has landed; `token` = its slot offset.
-template <int D>
-__device__ __forceinline__ void wait_tile(int younger, uint32_t& token) {
-  switch (younger) {
-    case 0: vm_wait_token<0>(token); break;
-    case 1: vm_wait_tiles<D, 1>(token); break;
-    case 2: vm_wait_tiles<D, 2>(token); break;
-    case 3: vm_wait_tiles<D, 3>(token); break;
-    case 4: vm_wait_tiles<D, 4>(token); break;
-    case 5: vm_wait_tiles<D, 5>(token); break;
-    case 6: vm_wait_tiles<D, 6>(token); break;
-    default: vm_wait_tiles<D, 7>(token); break;
+// vmcnt(n) for a wave-uniform runtime n in [LO, HI]: a 6-deep binary tree of scalar branches down to the immediate.
+template <int LO, int HI>
+__device__ __forceinline__ void vm_wait_n(uint32_t& token, int n) {
+  if constexpr (LO == HI) {
+    vm_wait_token<LO>(token);
+  } else {
+    constexpr int MID = (LO + HI) / 2;
+    if (n <= MID) vm_wait_n<LO, MID>(token, n);
+    else vm_wait_n<MID + 1, HI>(token, n);
   }
 }
 
-template <int STRAT, int D, int STEPS>
+// Wait until the tile with `younger` tiles issued after it has landed (every tile is exactly D DMA instructions,
+// so that is vmcnt(younger * D); above 63 — the counter's width — vmcnt(63) waits for more, never less); `token` =
+// the tile's slot offset.
+__device__ __forceinline__ void wait_tile(int younger, int D, uint32_t& token) {
+  const int n = younger * D;
+  vm_wait_n<0, 63>(token, n < 63 ? n : 63);
+}
+
+template <int STRAT, int STEPS>
 __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restrict__ q,
                                                        const DevSeg* __restrict__ segs) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -523,6 +571,7 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
     // Ring of R wave-tile images: tiles t+1 .. t+R-1 stream in (LDS-DMA) while tile t is decoded; each tile is
     // exactly D DMA instructions, so "tile t landed" is vmcnt(<= (tiles issued after t) * D).
     const int R = q->ring;
+    const int D = q->dma_per_tile;
     int isi = find_segment(segs, q->num_segments, t0);   // issue cursor: segment, its tile range, ring slot
     int64_t ifirst = segs[isi].first_wtile;
     int64_t iend = ifirst + segs[isi].num_wtiles;
@@ -534,7 +583,7 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
         ifirst = segs[isi].first_wtile;
         iend = ifirst + segs[isi].num_wtiles;
       }
-      stage_tile<D, STEPS>(segs + isi, ti - ifirst, ring + islot * img_dw, lane);
+      stage_tile<STEPS>(segs + isi, ti - ifirst, ring + islot * img_dw, lane, D);
       ++ti;
       islot = islot + 1 == R ? 0 : islot + 1;
     };
@@ -550,7 +599,7 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
       const int64_t seg_end = min(t1, seg_first + (int64_t)seg->num_wtiles);
       for (; t < seg_end; ++t) {
         uint32_t slot_off = (uint32_t)(pslot * img_dw);
-        wait_tile<D>((int)(ti - (t + 1)), slot_off);  // tile t has landed in its slot (same-wave LDS-DMA)
+        wait_tile((int)(ti - (t + 1)), D, slot_off);  // tile t has landed in its slot (same-wave LDS-DMA)
         if (ti < t1) issue_next();                     // refill the slot tile t-1 used
         if (!q->debug_stream_only) process_tile<STRAT, STEPS>(q, seg, t - seg_first, ring + slot_off, lane, acc);
         pslot = pslot + 1 == R ? 0 : pslot + 1;
@@ -678,33 +727,24 @@ hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t*
   return hipGetLastError();
 }
 
-template <int STRAT, int STEPS>
-static const void* scan_fn(int d) {
-  switch (d) {
-    case 4: return (const void*)scan_kernel<STRAT, 4, STEPS>;
-    case 8: return (const void*)scan_kernel<STRAT, 8, STEPS>;
-    case 16: return (const void*)scan_kernel<STRAT, 16, STEPS>;
-    default: return (const void*)scan_kernel<STRAT, 32, STEPS>;
-  }
+static const void* scan_fn(int strategy, int steps) {
+  if (strategy == STRAT_LDS) return steps == 16 ? (const void*)scan_kernel<STRAT_LDS, 16> : (const void*)scan_kernel<STRAT_LDS, 32>;
+  return steps == 16 ? (const void*)scan_kernel<STRAT_GLOBAL, 16> : (const void*)scan_kernel<STRAT_GLOBAL, 32>;
 }
 
-static const void* scan_fn_any(int strategy, int d, int steps) {
-  if (strategy == STRAT_LDS) return steps == 16 ? scan_fn<STRAT_LDS, 16>(d) : scan_fn<STRAT_LDS, 32>(d);
-  return steps == 16 ? scan_fn<STRAT_GLOBAL, 16>(d) : scan_fn<STRAT_GLOBAL, 32>(d);
+hipError_t set_scan_lds_limit(int strategy, int steps, int bytes) {
+  return hipFuncSetAttribute(scan_fn(strategy, steps), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
-int scan_dma_slots(int needed) {
-  return needed <= 4 ? 4 : needed <= 8 ? 8 : needed <= 16 ? 16 : needed <= 32 ? 32 : -1;
+hipError_t scan_occupancy(int strategy, int steps, int lds_bytes, int* blocks_per_cu) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, scan_fn(strategy, steps), kWGSize,
+                                                      (size_t)lds_bytes);
 }
 
-hipError_t set_scan_lds_limit(int strategy, int d, int steps, int bytes) {
-  return hipFuncSetAttribute(scan_fn_any(strategy, d, steps), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-}
-
-hipError_t launch_scan(int strategy, int d, int steps, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs,
+hipError_t launch_scan(int strategy, int steps, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs,
                        hipStream_t s) {
   void* args[] = {(void*)&q, (void*)&segs};
-  return hipLaunchKernel(scan_fn_any(strategy, d, steps), dim3(grid), dim3(kWGSize), args, (size_t)lds_bytes, s);
+  return hipLaunchKernel(scan_fn(strategy, steps), dim3(grid), dim3(kWGSize), args, (size_t)lds_bytes, s);
 }
 
 }  // namespace pa

@@ -276,6 +276,12 @@ class GpuQueryExecutor:
     def execute(self, stream=None):
         L.check(L.lib().pa_query_execute(self.handle, stream), "pa_query_execute")
 
+    def reset(self, stream=None):
+        L.check(L.lib().pa_query_reset(self.handle, stream), "pa_query_reset")
+
+    def scan(self, stream=None):
+        L.check(L.lib().pa_query_scan(self.handle, stream), "pa_query_scan")
+
     def sections(self):
         """[(kind, device_ptr, num_elements)] accumulator sections (for the cross-GPU reduce)."""
         lib = L.lib()
@@ -295,6 +301,7 @@ class GpuQueryExecutor:
         names = ("strategy", "steps", "dma_slots", "ring", "wg_per_cu", "grid", "lds_bytes")
         out["plan"] = {n: v.value for n, v in zip(names, vals)}
         out["plan"]["strategy"] = "lds" if out["plan"]["strategy"] == 0 else "global"
+        out["plan"]["eager_literals"] = int(L.lib().pa_query_num_eager_literals(self.handle))
         return out
 
     def fetch(self, stream=None) -> IntermediateResult:

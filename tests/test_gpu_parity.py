@@ -141,6 +141,46 @@ def test_strategies_agree(flags):
         run_both(sql, segs, flags=flags, rel=rel)
 
 
+LAZY_QUERIES = [
+    # the headline shape: a very selective clause leads, the day range is evaluated lazily on its survivors
+    "SELECT day, SUM(clicks), SUM(imps), COUNT(*) FROM t WHERE day BETWEEN {da} AND {db} AND acct IN ({acct}) "
+    "GROUP BY day LIMIT 1000",
+    "SELECT COUNT(*), SUM(clicks), MIN(imps), MAX(day) FROM t WHERE acct = {acct0} AND (day < {da} OR imps > {ia}) "
+    "AND NOT (clicks = {c0})",
+    "SELECT day, COUNT(*), DISTINCTCOUNTHLL(clicks) FROM t WHERE acct IN ({acct}) AND r1 < 0.5 GROUP BY day "
+    "LIMIT 1000",
+    "SELECT COUNT(*), SUM(r1) FROM t WHERE acct NOT IN ({acct}) AND day = {da}",
+]
+
+
+@pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LAZY, L.PA_QF_FORCE_LDS, L.PA_QF_STAGE_ALL,
+                                   (4 << L.PA_QF_WG_SHIFT) | (2 << L.PA_QF_RING_SHIFT) | L.PA_QF_STEPS16])
+def test_lazy_clauses(flags):
+    """Late materialisation: clauses behind a very selective lead clause run only on its survivors, from HBM.
+    Every plan variant must return the oracle's result; the default plan must actually defer clauses."""
+    cols = {"day": ("INT", 512), "acct": ("INT", 50000), "clicks": ("LONG", 1000), "imps": ("LONG", 9000),
+            "r1": ("DOUBLE", 0)}
+    # even seeds: uniform (unskewed) values, so the dictId-fraction estimate holds and the lead clause is lazy-worthy
+    segs = [make_segment(42 + 2 * i, n, cols, no_dict=("r1",)) for i, n in enumerate((300007, 65536, 5000))]
+    d = segs[0].column("day").dictionary
+    a = segs[0].column("acct").dictionary
+    vals = {"da": int(d[100]), "db": int(d[300]), "acct0": int(a[7]), "acct": ", ".join(str(int(v)) for v in a[5:9]),
+            "ia": int(segs[0].column("imps").dictionary[4000]), "c0": int(segs[0].column("clicks").dictionary[3])}
+    gsegs = [GpuSegment(s) for s in segs]
+    try:
+        for sql in LAZY_QUERIES:
+            sql = sql.format(**vals)
+            _, _, ex = run_both(sql, segs, gsegs=gsegs, flags=flags, rel=DOUBLE_REL if "r1" in sql else 0.0)
+        if flags == 0:
+            ex = GpuQueryExecutor(parse_sql(LAZY_QUERIES[0].format(**vals)), gsegs)
+            st = ex.stats()
+            ex.close()
+            assert st["plan"]["eager_literals"] == 1, st
+    finally:
+        for g in gsegs:
+            g.close()
+
+
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 2047, 2048, 2049, 4095, 4097, 100003])
 def test_ragged_segment_sizes(n):
     cols = {"a": ("INT", 37), "b": ("LONG", 1500), "m": ("LONG", 777)}

@@ -40,12 +40,13 @@ def main():
             c.fwd_bytes = None
     q = parse_sql(args.query)
     stream = torch.cuda.current_stream()
-    configs = [("auto", 0)]
-    for steps_flag, steps in ((L.PA_QF_STEPS32, 32), (L.PA_QF_STEPS16, 16)):
-        for ring in (2, 3, 4, 5, 6, 8):
-            for wg in (1, 2, 3):
-                configs.append(("s%d_r%d_wg%d" % (steps, ring, wg),
-                                steps_flag | (ring << L.PA_QF_RING_SHIFT) | (wg << L.PA_QF_WG_SHIFT)))
+    configs = [("auto", 0), ("auto_nolazy", L.PA_QF_NO_LAZY)]
+    for lazy_name, lazy_flag in (("", 0), ("_nolazy", L.PA_QF_NO_LAZY)):
+        for steps_flag, steps in ((L.PA_QF_STEPS32, 32), (L.PA_QF_STEPS16, 16)):
+            for ring in (2, 3, 4):
+                for wg in (2, 3, 4):
+                    configs.append(("s%d_r%d_wg%d%s" % (steps, ring, wg, lazy_name),
+                                    lazy_flag | steps_flag | (ring << L.PA_QF_RING_SHIFT) | (wg << L.PA_QF_WG_SHIFT)))
     ref = None
     for name, flags in configs:
         for dbg in (0, L.PA_QF_DEBUG_STREAM_ONLY):
