@@ -157,16 +157,17 @@ def main():
         res = step()
     torch.cuda.synchronize()
 
-    # scan-kernel-only timing: HIP events recorded on the stream the kernel is launched on, around the fused scan
-    # alone (the accumulator reset is issued before the first event)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    for a, b in ev:
-        ex.reset(sptr)
-        a.record(stream)
+    # scan-kernel-only timing: HIP events on the stream the kernel is launched on, around `steps` back-to-back launches
+    # of the fused scan alone (one accumulator reset before the first event; the scans keep accumulating, which
+    # changes no byte the kernel reads). Per-launch duration = elapsed / steps, the figure rocprofv3 --stats averages.
+    ex.reset(sptr)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(args.steps):
         ex.scan(sptr)
-        b.record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
 
     if world > 1:
         dist.barrier()

@@ -1,0 +1,112 @@
+"""Multi-rank merge of partial aggregates (pinot_amd/parallel.py) on CPU with the gloo backend, world size 2.
+
+Each rank owns a disjoint segment range (shard_segments) and holds its partial accumulators in the library's section
+layout (pa_query_section kinds); reduce_sections must reproduce what one GPU would hold for the whole segment set:
+the cross-server half of GroupByCombineOperator (IndexedTable upsert: COUNT/SUM +, MIN min, MAX max, HLL register max).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pinot_amd import _lib as L
+from pinot_amd.parallel import SECTION_DTYPE, reduce_sections, shard_segments
+
+K = 257  # keys
+LOG2M = 8
+
+
+def f64_order_encode(d):
+    """pa_device.h f64_order_encode: signed int64 order == double order."""
+    b = np.asarray(d, dtype=np.float64).view(np.int64)
+    return np.where(b >= 0, b, b ^ np.int64(0x7FFFFFFFFFFFFFFF))
+
+
+def f64_order_decode(e):
+    e = np.asarray(e, dtype=np.int64)
+    return np.where(e >= 0, e, e ^ np.int64(0x7FFFFFFFFFFFFFFF)).view(np.float64)
+
+
+def partial(rank):
+    """Partial accumulators of one rank's segments (random, seeded by rank)."""
+    rng = np.random.default_rng(100 + rank)
+    count = rng.integers(0, 1000, K).astype(np.int64)
+    vals = rng.integers(-(1 << 62), 1 << 62, K)
+    sum_x2 = np.empty(2 * K, dtype=np.int64)  # PA_ACC_SUM_I64X2: [2k] low-32 unsigned sum, [2k+1] high-32 signed sum
+    sum_x2[0::2] = vals & 0xFFFFFFFF
+    sum_x2[1::2] = vals >> 32
+    dsum = rng.standard_normal(K)
+    dmin = f64_order_encode(rng.standard_normal(K) * 1e6)
+    imax = rng.integers(-(1 << 40), 1 << 40, K).astype(np.int64)
+    hll = rng.integers(0, 26, K << LOG2M).astype(np.int32)
+    return [(L.PA_ACC_COUNT_U64, count), (L.PA_ACC_SUM_I64X2, sum_x2), (L.PA_ACC_SUM_F64, dsum),
+            (L.PA_ACC_MIN_I64, dmin), (L.PA_ACC_MAX_I64, imax), (L.PA_ACC_HLL_U32, hll)], vals
+
+
+def _worker(rank, world, port, all_reduce, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    secs, _ = partial(rank)
+    views = [(k, torch.from_numpy(np.ascontiguousarray(a)).to(SECTION_DTYPE[k])) for k, a in secs]
+    reduce_sections(views, dst=0, all_reduce=all_reduce)
+    if rank == 0 or all_reduce:
+        out[rank] = [t.numpy().copy() for _, t in views]
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("all_reduce", [False, True])
+def test_gloo_reduce_matches_single_gpu_merge(all_reduce):
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), all_reduce, out), nprocs=world, join=True)
+    parts = [partial(r) for r in range(world)]
+    exp_count = sum(p[0][0][1] for p in parts)
+    exp_sum = sum(p[1].astype(object) for p in parts)  # exact big-int totals
+    exp_dsum = sum(p[0][2][1] for p in parts)
+    exp_min = np.minimum.reduce([f64_order_decode(p[0][3][1]) for p in parts])
+    exp_max = np.maximum.reduce([p[0][4][1] for p in parts])
+    exp_hll = np.maximum.reduce([p[0][5][1] for p in parts])
+    for r in (range(world) if all_reduce else [0]):
+        count, sx2, dsum, dmin, imax, hll = out[r]
+        assert np.array_equal(count, exp_count)
+        total = sx2[0::2].astype(object) + (sx2[1::2].astype(object) << 32)  # decode of pa_query_fetch
+        assert all(a == b for a, b in zip(total, exp_sum))
+        assert np.allclose(dsum, exp_dsum, rtol=1e-12, atol=0)
+        assert np.array_equal(f64_order_decode(dmin), exp_min)
+        assert np.array_equal(imax, exp_max)
+        assert np.array_equal(hll, exp_hll)
+
+
+def test_f64_order_encoding_is_monotone():
+    rng = np.random.default_rng(0)
+    d = np.concatenate([rng.standard_normal(1000) * 10.0 ** rng.integers(-300, 300, 1000),
+                        [0.0, -0.0, np.inf, -np.inf, 5e-324, -5e-324]])
+    e = f64_order_encode(d)
+    # sorted by the encoding, the doubles are non-decreasing (-0.0 sorts just below 0.0, as Java's Math.min/max
+    # order them)
+    ds = d[np.argsort(e, kind="stable")]
+    assert np.all(ds[1:] >= ds[:-1])
+    assert f64_order_encode(-0.0) < f64_order_encode(0.0)
+    assert np.array_equal(f64_order_decode(e).view(np.int64), d.view(np.int64))
+
+
+@pytest.mark.parametrize("n,world", [(100, 1), (100, 2), (100, 8), (7, 8), (801, 3)])
+def test_shard_segments_partition(n, world):
+    parts = [shard_segments(n, r, world) for r in range(world)]
+    flat = [i for p in parts for i in p]
+    assert flat == list(range(n))  # disjoint, complete, contiguous
+    assert max(map(len, parts)) - min(map(len, parts)) <= 1
