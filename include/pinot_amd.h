@@ -168,6 +168,7 @@ typedef struct {
 #define PA_QF_RING_SHIFT 8            /* bits 8..11: tile images per wave (2..8) */
 #define PA_QF_WG_SHIFT 12             /* bits 12..14: workgroups per CU (1..4) */
 #define PA_QF_DEBUG_STREAM_ONLY (1 << 16) /* measurement only: stream the tiles, skip decode (results invalid) */
+#define PA_QF_NO_LANE_MAJOR (1 << 17)     /* use the step-major scan kernel even when the lane-major one applies */
 
 /* per-(segment, leaf) parameters in that segment's dictId space */
 typedef struct {
@@ -237,6 +238,8 @@ int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs
  * steps per wave tile, DMA instructions per tile, tile images per wave, workgroups per CU, grid, LDS bytes. */
 /* Filter literals evaluated on whole staged tiles (the rest only on the docs those matched). */
 int32_t pa_query_num_eager_literals(const pa_query* q);
+/* 1 if the lane-major scan kernel was chosen (lane l owns docs [32l, 32l+32) of a tile), 0 step-major, <0 error. */
+int32_t pa_query_lane_major(const pa_query* q);
 int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t* dma_slots, int32_t* ring,
                   int32_t* wg_per_cu, int32_t* grid, int32_t* lds_bytes);
 

@@ -26,6 +26,7 @@ PA_QF_FORCE_LDS = 1 << 7
 PA_QF_RING_SHIFT = 8
 PA_QF_WG_SHIFT = 12
 PA_QF_DEBUG_STREAM_ONLY = 1 << 16
+PA_QF_NO_LANE_MAJOR = 1 << 17
 PA_ACC_COUNT_U64, PA_ACC_SUM_I64, PA_ACC_SUM_F64, PA_ACC_MIN_I64, PA_ACC_MAX_I64, PA_ACC_HLL_U32, \
     PA_ACC_SUM_I64X2 = range(7)
 
@@ -35,7 +36,7 @@ EXPORTED = [
     "pa_segment_create", "pa_segment_add_sv_dict_column", "pa_segment_add_mv_dict_column",
     "pa_segment_add_raw_column", "pa_segment_num_docs", "pa_segment_device_bytes", "pa_segment_destroy",
     "pa_query_create", "pa_query_bind_segment", "pa_query_prepare", "pa_query_num_keys",
-    "pa_query_execute", "pa_query_reset", "pa_query_scan", "pa_query_num_eager_literals",
+    "pa_query_execute", "pa_query_reset", "pa_query_scan", "pa_query_num_eager_literals", "pa_query_lane_major",
     "pa_query_accumulator_bytes", "pa_query_set_accumulator_buffer", "pa_query_num_sections", "pa_query_section", "pa_query_fetch", "pa_query_stats",
     "pa_query_plan", "pa_query_destroy",
 ]
@@ -104,6 +105,7 @@ def _declare(lib):
         "pa_query_reset": (ctypes.c_int, [vp, vp]),
         "pa_query_scan": (ctypes.c_int, [vp, vp]),
         "pa_query_num_eager_literals": (i32, [vp]),
+        "pa_query_lane_major": (i32, [vp]),
         "pa_query_accumulator_bytes": (u64, [vp]),
         "pa_query_set_accumulator_buffer": (ctypes.c_int, [vp, vp, u64]),
         "pa_query_num_sections": (i32, [vp]),

@@ -298,6 +298,8 @@ int to_cnf(const pa_query_spec& spec, std::vector<Clause>& out) {
   return rec(st.back(), false, out);
 }
 
+constexpr size_t kFetchWholeBlockBytes = 1 << 20;
+
 struct Section {
   int32_t kind;
   void* ptr;
@@ -335,7 +337,10 @@ struct pa_query {
 
   DevQuery hq;
   std::vector<DevSeg> hsegs;
-  DevBuf dq, dsegs;
+  DevBuf dq, dsegs, dplans;
+  void* host_acc = nullptr;  // pinned copy of the accumulator block (small-block fetch path)
+  int lane_major = 0;
+  std::vector<LmSegPlan> hplans;
   std::vector<DevBuf> owned;  // LUTs, remaps, HLL LUTs
   DevBuf acc;                 // all accumulator sections (unless the caller provided the block)
   void* external_acc = nullptr;
@@ -345,6 +350,8 @@ struct pa_query {
   ~pa_query() {
     dev_free(dq);
     dev_free(dsegs);
+    dev_free(dplans);
+    if (host_acc) (void)hipHostFree(host_acc);
     dev_free(acc);
     for (auto& b : owned) dev_free(b);
   }
@@ -739,10 +746,20 @@ int pa_query_prepare(pa_query* q) {
   };
   const int force_ring = (s.flags >> PA_QF_RING_SHIFT) & 15;
   const int force_wg = (s.flags >> PA_QF_WG_SHIFT) & 7;
+  // Lane-major kernel: every eager literal is a dictionary leaf on a staged column and the per-segment plan table
+  // has room for the staged columns and eager literals (otherwise the step-major kernel runs the query).
+  bool lm = !(s.flags & (PA_QF_NO_LANE_MAJOR | PA_QF_STEPS16)) && q->num_eager <= kLmEager;
+  for (int li = 0; li < q->num_eager && lm; ++li) {
+    const int k = s.leaves[q->literals[li].leaf].kind;
+    if (k != PA_LEAF_DICT_RANGE && k != PA_LEAF_DICT_SET) lm = false;
+  }
+  for (int si = 0; si < q->nseg && lm; ++si)
+    if (q->hsegs[si].num_staged > kLmStaged) lm = false;
   auto plan_for = [&](int strat) {
     const bool lds_strategy = strat == STRAT_LDS;
     Plan best;
     for (int steps : {32, 16}) {
+      if (lm && steps != 32) continue;
       if ((s.flags & PA_QF_STEPS16) && steps != 16) continue;
       if ((s.flags & PA_QF_STEPS32) && steps != 32) continue;
       int img_dw = kGuardWords, dma = 0;
@@ -771,8 +788,8 @@ int pa_query_prepare(pa_query* q) {
         if (ring < 2) continue;
         const size_t lds = acc_b + (size_t)kWavesPerWG * ring * img_bytes;
         int resident = 0;
-        if (set_scan_lds_limit(strat, steps, (int)kLdsBudget) != hipSuccess ||
-            scan_occupancy(strat, steps, (int)lds, &resident) != hipSuccess)
+        if (set_scan_lds_limit(strat, steps, lm, (int)kLdsBudget) != hipSuccess ||
+            scan_occupancy(strat, steps, lm, (int)lds, &resident) != hipSuccess)
           resident = wg;  // no device to ask (planning only): trust the LDS arithmetic
         if (resident < wg) continue;
         const double inflight = (double)wg * kWavesPerWG * (ring - 1) * img_bytes;
@@ -848,7 +865,9 @@ int pa_query_prepare(pa_query* q) {
   h.num_eager = q->num_eager;
   h.dma_per_tile = plan.dma;
   h.steps = plan.steps;
-  h.debug_stream_only = (s.flags & PA_QF_DEBUG_STREAM_ONLY) ? 1 : 0;
+  h.debug_stream_only = (s.flags & PA_QF_DEBUG_STREAM_ONLY) ? 1 : ((s.flags >> 18) & 7) ? 1 + ((s.flags >> 18) & 7) : 0;
+  h.lane_major = lm ? 1 : 0;
+  q->lane_major = lm ? 1 : 0;
   q->plan_ring = plan.ring;
   q->plan_wg = plan.wg_per_cu;
   q->num_tiles = (uint64_t)first;
@@ -889,7 +908,42 @@ int pa_query_prepare(pa_query* q) {
   if (rc) return rc;
   PA_HIP(hipMemcpy(q->dq.p, &h, sizeof(DevQuery), hipMemcpyHostToDevice));
   if (q->nseg) PA_HIP(hipMemcpy(q->dsegs.p, q->hsegs.data(), sizeof(DevSeg) * q->nseg, hipMemcpyHostToDevice));
-  PA_HIP(set_scan_lds_limit(q->strategy, q->steps, q->lds_bytes));
+  q->hplans.assign(std::max(1, q->nseg), LmSegPlan{});
+  if (lm) {
+    for (int si = 0; si < q->nseg; ++si) {
+      const DevSeg& d = q->hsegs[si];
+      LmSegPlan& P = q->hplans[si];
+      std::memset(&P, 0, sizeof(P));
+      P.nstaged = d.num_staged;
+      P.neager = q->num_eager;
+      P.num_docs = d.num_docs;
+      P.num_wtiles = d.num_wtiles;
+      P.dummy_lo = (uint32_t)(uintptr_t)d.dummy_src;
+      P.dummy_hi = (uint32_t)((uint64_t)(uintptr_t)d.dummy_src >> 32);
+      for (int k = 0; k < d.num_staged; ++k) {
+        P.st[k].lo = (uint32_t)(uintptr_t)d.stage[k].words;
+        P.st[k].hi = (uint32_t)((uint64_t)(uintptr_t)d.stage[k].words >> 32);
+        P.st[k].nbits = d.stage[k].nbits;
+        P.st[k].lds_off = d.stage[k].lds_off;
+      }
+      for (int li = 0; li < q->num_eager; ++li) {
+        const DevLeaf& L = d.leaves[li];
+        if (L.lds_off < 0) return fail(PA_EINVAL, "internal: eager literal on an unstaged column");
+        P.lf[li].kind = L.kind;
+        P.lf[li].nbits = L.nbits;
+        P.lf[li].lds_off = L.lds_off;
+        P.lf[li].lo = (uint32_t)L.lo;
+        P.lf[li].span = (uint32_t)L.span;
+        P.lf[li].flags = (L.negate ? 1 : 0) | (L.clause_end ? 2 : 0);
+        P.lf[li].lut_lo = (uint32_t)(uintptr_t)L.lut;
+        P.lf[li].lut_hi = (uint32_t)((uint64_t)(uintptr_t)L.lut >> 32);
+      }
+    }
+  }
+  rc = dev_alloc(q->dplans, sizeof(LmSegPlan) * q->hplans.size());
+  if (rc) return rc;
+  PA_HIP(hipMemcpy(q->dplans.p, q->hplans.data(), sizeof(LmSegPlan) * q->hplans.size(), hipMemcpyHostToDevice));
+  PA_HIP(set_scan_lds_limit(q->strategy, q->steps, q->lane_major, q->lds_bytes));
   PA_HIP(hipDeviceSynchronize());
   q->prepared = true;
   return PA_OK;
@@ -900,10 +954,11 @@ int64_t pa_query_num_keys(const pa_query* q) { return q ? q->num_keys : -1; }
 int pa_query_reset(pa_query* q, void* stream) {
   if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
   hipStream_t st = (hipStream_t)stream;
+  // one memset of the whole accumulator block, then the MIN/MAX sections to their identities
+  PA_HIP(hipMemsetAsync(q->external_acc ? q->external_acc : q->acc.p, 0, q->acc.n, st));
   for (const Section& sc : q->sections) {
     if (sc.kind == PA_ACC_MIN_I64) PA_HIP(launch_fill_i64((int64_t*)sc.ptr, sc.n, INT64_MAX, st));
     else if (sc.kind == PA_ACC_MAX_I64) PA_HIP(launch_fill_i64((int64_t*)sc.ptr, sc.n, INT64_MIN, st));
-    else PA_HIP(hipMemsetAsync(sc.ptr, 0, (size_t)sc.n * (sc.kind == PA_ACC_HLL_U32 ? 4 : 8), st));
   }
   return PA_OK;
 }
@@ -911,8 +966,8 @@ int pa_query_reset(pa_query* q, void* stream) {
 int pa_query_scan(pa_query* q, void* stream) {
   if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
   if (q->num_tiles == 0) return PA_OK;
-  PA_HIP(launch_scan(q->strategy, q->steps, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p,
-                     (const DevSeg*)q->dsegs.p, (hipStream_t)stream));
+  PA_HIP(launch_scan(q->strategy, q->steps, q->lane_major, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p,
+                     (const DevSeg*)q->dsegs.p, (const LmSegPlan*)q->dplans.p, (hipStream_t)stream));
   return PA_OK;
 }
 
@@ -967,6 +1022,57 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   hipStream_t st = (hipStream_t)stream;
   const pa_query_spec& s = q->spec;
   const int64_t K = q->num_keys;
+  // Small accumulator blocks (the common case: a few thousand keys): ONE device-to-host copy of the whole block into
+  // pinned memory and one synchronisation, then compaction + decode on the host.
+  if (q->acc.n <= kFetchWholeBlockBytes) {
+    if (!q->host_acc) {
+      if (hipHostMalloc(&q->host_acc, std::max<size_t>(q->acc.n, 16), hipHostMallocDefault) != hipSuccess) {
+        q->host_acc = nullptr;
+        return fail(PA_ENOMEM, "hipHostMalloc for the accumulator copy failed");
+      }
+    }
+    char* dbase = (char*)(q->external_acc ? q->external_acc : q->acc.p);
+    PA_HIP(hipMemcpyAsync(q->host_acc, dbase, q->acc.n, hipMemcpyDeviceToHost, st));
+    PA_HIP(hipStreamSynchronize(st));
+    const char* hb = (const char*)q->host_acc;
+    auto hsec = [&](int sec) { return hb + ((char*)q->sections[sec].ptr - dbase); };
+    const uint64_t* hc = (const uint64_t*)hsec(0);
+    int64_t n = 0;
+    for (int64_t k = 0; k < K; ++k) {
+      if (s.num_group_by != 0 && hc[k] == 0) continue;
+      if (n < capacity) {
+        if (out_keys) out_keys[n] = k;
+        if (out_counts) out_counts[n] = (int64_t)hc[k];
+        for (int a = 0; a < s.num_aggs; ++a) {
+          if (!out_aggs || !out_aggs[a]) continue;
+          const pa_agg_spec& A = s.aggs[a];
+          double* outd = (double*)out_aggs[a];
+          if (A.type == PA_AGG_COUNT) {
+            outd[n] = (double)hc[k];
+            continue;
+          }
+          const char* sp = hsec(q->agg_section[a]);
+          const int src = q->hq.aggs[a].src;
+          if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
+            const int64_t per = int64_t(1) << A.log2m;
+            const uint32_t* r = (const uint32_t*)sp + k * per;
+            uint8_t* o = (uint8_t*)out_aggs[a] + n * per;
+            for (int64_t j = 0; j < per; ++j) o[j] = (uint8_t)r[j];
+          } else if (A.type == PA_AGG_SUM) {
+            const int64_t* hv = (const int64_t*)sp;
+            if (src == SRC_LONG) outd[n] = (double)(((__int128)hv[2 * k + 1] << 32) + (__int128)(uint64_t)hv[2 * k]);
+            else outd[n] = src == SRC_INT ? (double)hv[k] : ((const double*)sp)[k];
+          } else {
+            const int64_t e8 = ((const int64_t*)sp)[k];
+            if (hc[k] == 0) outd[n] = A.type == PA_AGG_MIN ? __builtin_inf() : -__builtin_inf();
+            else outd[n] = src != SRC_DOUBLE ? (double)e8 : f64_order_decode(e8);
+          }
+        }
+      }
+      ++n;
+    }
+    return n;
+  }
   std::vector<uint64_t> cnt(K);
   PA_HIP(hipMemcpyAsync(cnt.data(), q->sections[0].ptr, (size_t)K * 8, hipMemcpyDeviceToHost, st));
   PA_HIP(hipStreamSynchronize(st));
@@ -1062,6 +1168,8 @@ int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t*
 }
 
 int32_t pa_query_num_eager_literals(const pa_query* q) { return q && q->prepared ? q->num_eager : -1; }
+
+int32_t pa_query_lane_major(const pa_query* q) { return q && q->prepared ? q->lane_major : -1; }
 
 void pa_query_destroy(pa_query* q) { delete q; }
 

@@ -107,7 +107,7 @@ struct DevQuery {
   int32_t num_eager;         // literals [0, num_eager) are evaluated on whole staged tiles; the rest (whole CNF
                              // clauses) only on docs the eager clauses matched, straight from HBM
   int32_t dma_per_tile;      // LDS-DMA wave instructions per wave tile (max over segments)
-  int32_t pad1;
+  int32_t lane_major;        // 1: scan_lm_kernel (docs 32*lane + i of a tile), 0: scan_kernel (docs 64*i + lane)
   int32_t staged_slots[kMaxSlots];
   int32_t gb_slot[PA_MAX_GROUP_BY];
   int64_t gb_stride[PA_MAX_GROUP_BY];
@@ -118,6 +118,36 @@ struct DevQuery {
   uint32_t lds_acc_bytes;    // LDS strategy: bytes of the WG-private accumulator block
   DevAgg aggs[PA_MAX_AGGS];
 };
+
+// Per-segment table of the lane-major scan kernel (scan_lm_kernel): 64 dwords, loaded at segment entry into ONE
+// VGPR (lane k holds dword k) and read back with v_readlane — the tile loop needs no scalar-memory round trips.
+// Lane-major: lane l of a wave owns docs [32l, 32l+32) of a 2048-doc wave tile, i.e. stream words [l*nb, (l+1)*nb)
+// of every staged nb-bit column, so an eager filter leaf is nb ds_reads + a static unpack per lane.
+constexpr int kLmStaged = 4;
+constexpr int kLmEager = 4;
+struct LmSegPlan {
+  int32_t nstaged;           // dword 0
+  int32_t neager;            // 1: leading eager literals (all DICT_RANGE / DICT_SET on staged columns)
+  int32_t num_docs;          // 2
+  int32_t num_wtiles;        // 3
+  uint32_t dummy_lo, dummy_hi;  // 4,5: readable address for the DMA padding instructions
+  int32_t pad0[2];           // 6,7
+  struct {                   // 8 + 4c
+    uint32_t lo, hi;         // stream words (past the guard words)
+    int32_t nbits;
+    int32_t lds_off;         // dword offset of the region inside the tile image
+  } st[kLmStaged];
+  struct {                   // 24 + 8l
+    int32_t kind;            // PA_LEAF_DICT_RANGE / PA_LEAF_DICT_SET
+    int32_t nbits;
+    int32_t lds_off;
+    uint32_t lo, span;       // DICT_RANGE, MSB-aligned (see DevLeaf)
+    int32_t flags;           // bit 0: negate, bit 1: closes a CNF clause
+    uint32_t lut_lo, lut_hi; // DICT_SET bitmap
+  } lf[kLmEager];
+  int32_t pad1[8];           // 56..63
+};
+static_assert(sizeof(LmSegPlan) == 256, "one dword per lane");
 
 // Order-preserving int64 image of an IEEE double (an involution): signed int64 order == double order.
 __host__ __device__ inline int64_t f64_order_encode(double d) {

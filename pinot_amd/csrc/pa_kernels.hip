@@ -487,6 +487,180 @@ __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, con
   __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // vmcnt(0)
 }
 
+
+// ---------------------------------------------------------------- lane-major tile evaluation (scan_kernel<.., LM=1>)
+//
+// Lane l owns docs [32l, 32l+32) of the wave tile, i.e. the nb consecutive stream words [l*nb, (l+1)*nb) of every
+// staged column: an eager leaf is nb ds_reads at immediate offsets (1x the staged bytes, against 2 dwords per doc in
+// the step-major layout) plus a static unpack (nb is a template parameter: every shift is a constant).
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
+
+// Match word of one DICT_RANGE / DICT_SET leaf: bit i <=> doc 32*lane + i of the tile matches (before negation).
+template <int NB>
+__device__ __forceinline__ uint32_t leaf_lm(int kind, uint32_t region_lds, int lane, uint32_t lo_t, uint32_t hi_t,
+                                            const uint32_t* lut) {
+  const lds_u32_t* p = (const lds_u32_t*)(uintptr_t)(region_lds + (uint32_t)lane * (uint32_t)(NB * 4));
+  uint32_t w[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) w[j] = p[j];
+  // MSB-aligned value of doc i: the nb bits starting at stream bit i*NB of the lane's words, in the top bits of t
+  auto top = [&](int i) -> uint32_t {
+    const int s = i * NB, j = s >> 5, o = s & 31;
+    if (o + NB <= 32) return w[j] << o;
+    return __builtin_amdgcn_alignbit(w[j], w[(j + 1 < NB) ? j + 1 : j], 32 - o);
+  };
+  if (kind == PA_LEAF_DICT_RANGE) {
+    // lo <= v < lo + span  <=>  (t - lo') <= hi' (unsigned), lo' / hi' MSB-aligned by the host (see leaf_bits);
+    // non-matches accumulate as nm = 2*nm + borrow: bit i of nm = doc i does not match
+    uint32_t nm = 0;
+#pragma unroll
+    for (int i = 31; i >= 0; --i) {
+      const uint32_t t = top(i);
+      uint32_t u;
+      asm("v_sub_u32_e64 %[u], %[t], %[lo]\n\t"
+          "v_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
+          "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
+          : [nm] "+v"(nm), [u] "=&v"(u)
+          : [t] "v"(t), [lo] "s"(lo_t), [hi] "s"(hi_t)
+          : "vcc");
+    }
+    return ~nm;
+  }
+  const AS1 uint32_t* lt = gp(lut);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const uint32_t id = top(i) >> (32 - NB);
+    bits |= ((lt[id >> 5] >> (id & 31u)) & 1u) << i;
+  }
+  return bits;
+}
+
+__device__ __forceinline__ uint32_t leaf_lm_any(int nb, int kind, uint32_t region_lds, int lane, uint32_t lo_t,
+                                                uint32_t hi_t, const uint32_t* lut) {
+  switch (nb) {
+#define PA_LM_CASE(N) \
+  case N: return leaf_lm<N>(kind, region_lds, lane, lo_t, hi_t, lut);
+    PA_LM_CASE(1) PA_LM_CASE(2) PA_LM_CASE(3) PA_LM_CASE(4) PA_LM_CASE(5) PA_LM_CASE(6) PA_LM_CASE(7) PA_LM_CASE(8)
+    PA_LM_CASE(9) PA_LM_CASE(10) PA_LM_CASE(11) PA_LM_CASE(12) PA_LM_CASE(13) PA_LM_CASE(14) PA_LM_CASE(15)
+    PA_LM_CASE(16) PA_LM_CASE(17) PA_LM_CASE(18) PA_LM_CASE(19) PA_LM_CASE(20) PA_LM_CASE(21) PA_LM_CASE(22)
+    PA_LM_CASE(23) PA_LM_CASE(24) PA_LM_CASE(25) PA_LM_CASE(26) PA_LM_CASE(27) PA_LM_CASE(28) PA_LM_CASE(29)
+    PA_LM_CASE(30) PA_LM_CASE(31) PA_LM_CASE(32)
+#undef PA_LM_CASE
+    default: return 0;
+  }
+}
+
+// LDS-DMA of one wave tile of every staged column (plan table `ip`), padded to exactly D instructions.
+__device__ __forceinline__ void stage_tile_lm(uint32_t ip, int64_t wt, uint32_t img_lds, int lane, const int D) {
+  const int ns = (int)rl(ip, 0);
+  int issued = 0;
+  for (int c = 0; c < ns; ++c) {
+    const uint64_t words = ((uint64_t)rl(ip, 9 + 4 * c) << 32) | rl(ip, 8 + 4 * c);
+    const int nb = (int)rl(ip, 10 + 4 * c);
+    const uint32_t dst = img_lds + 4u * rl(ip, 11 + 4 * c);
+    const char* src = (const char*)words + wt * (int64_t)(256 * nb) + 16 * lane;  // 256*nb bytes per wave tile
+    const int chunks = 16 * nb;                                                      // 16-byte chunks per wave tile
+    for (int c0 = 0; c0 < chunks; c0 += 64) {
+      if (c0 + lane < chunks) dma16(src + 16 * c0, dst + 16 * c0);
+      ++issued;
+    }
+  }
+  const void* dummy = (const void*)(((uint64_t)rl(ip, 5) << 32) | rl(ip, 4));
+  for (; issued < D; ++issued) {
+    if (lane == 0) dma16(dummy, img_lds);
+  }
+}
+
+template <int STRAT>
+__device__ __forceinline__ void process_tile_lm(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                                uint32_t pp, int64_t wt, const uint32_t* img, uint32_t img_lds,
+                                                int lane, const Acc<STRAT>& acc) {
+  const int64_t doc_base = wt * kWTileDocs;
+  const int64_t rem = (int64_t)(int32_t)rl(pp, 2) - doc_base;
+  uint32_t valid = 0xffffffffu;
+  if (rem < kWTileDocs) {
+    const int64_t n = rem - 32 * lane;  // docs of this lane's 32 that exist
+    valid = n >= 32 ? 0xffffffffu : (n <= 0 ? 0u : ((1u << n) - 1u));
+  }
+  uint32_t m = valid;
+  uint32_t clause = 0;
+  const int neager = (int)rl(pp, 1);
+  for (int l = 0; l < neager; ++l) {
+    const int b = 24 + 8 * l;
+    const int flags = (int)rl(pp, b + 5);
+    const uint32_t* lut = (const uint32_t*)(((uint64_t)rl(pp, b + 7) << 32) | rl(pp, b + 6));
+    uint32_t bits = leaf_lm_any((int)rl(pp, b + 1), (int)rl(pp, b), img_lds + 4u * rl(pp, b + 2), lane,
+                                rl(pp, b + 3), rl(pp, b + 4), lut);
+    if (flags & 1) bits = ~bits;
+    clause |= bits;
+    if (flags & 2) {
+      m &= clause;
+      clause = 0;
+      if (__ballot(m != 0) == 0) return;
+    }
+  }
+  if (__ballot(m != 0) == 0) return;
+  const int nleaves = q->num_leaves;
+  if (neager < nleaves) {
+    for (int i = 0; i < 32; ++i) {
+      const uint32_t bit = 1u << i;
+      if (__ballot((m & bit) != 0) == 0) continue;
+      const int64_t doc = doc_base + 32 * lane + i;
+      bool ok = (m & bit) != 0;
+      bool any = false;
+      for (int li = neager; li < nleaves; ++li) {
+        const DevLeaf& L = seg->leaves[li];
+        if (ok && !any) any = leaf_match_doc(L, doc);
+        if (L.clause_end) {
+          ok = ok && any;
+          any = false;
+        }
+      }
+      if (!ok) m &= ~bit;
+    }
+    if (__ballot(m != 0) == 0) return;
+  }
+  for (int i = 0; i < 32; ++i) {
+    const uint64_t sm = __ballot((m >> i) & 1u);
+    if (sm == 0) continue;
+    const int doc_local = 32 * lane + i;
+    accumulate_step<STRAT>(q, seg, img, doc_local, doc_base + doc_local, sm, lane, acc);
+  }
+  __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // vmcnt(0): see process_tile
+}
+
+// Measurement-only tile bodies (flags bits 18..20): 1 = decode the eager leaves and sink the match word,
+// 2 = the same VALU work with no LDS reads, 3 = the LDS reads with no VALU work.
+__device__ __noinline__ void debug_tile_lm(int dbg, uint32_t pp, uint32_t img_lds, int lane) {
+  uint32_t m = 0;
+  const int b = 24;
+  if (dbg == 2) {
+    m = leaf_lm_any((int)rl(pp, b + 1), (int)rl(pp, b), img_lds + 4u * rl(pp, b + 2), lane, rl(pp, b + 3),
+                    rl(pp, b + 4), nullptr);
+  } else if (dbg == 3) {
+    uint32_t x = (uint32_t)lane;
+    const uint32_t lo = rl(pp, b + 3), hi = rl(pp, b + 4);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const uint32_t t = __builtin_amdgcn_alignbit(x, x + i, i & 31);
+      uint32_t u;
+      asm volatile("v_sub_u32_e64 %[u], %[t], %[lo]\n\t"
+                   "v_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
+                   "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
+                   : [nm] "+v"(m), [u] "=&v"(u)
+                   : [t] "v"(t), [lo] "s"(lo), [hi] "s"(hi)
+                   : "vcc");
+    }
+  } else {
+    const lds_u32_t* p = (const lds_u32_t*)(uintptr_t)(img_lds + 4u * rl(pp, b + 2) + (uint32_t)lane * 68u);
+#pragma unroll
+    for (int j = 0; j < 17; ++j) m ^= p[j];
+  }
+  if (m == 0x9E3779B9u) asm volatile("s_nop 0" ::"v"(m));  // keep m alive
+}
+
 __device__ __forceinline__ int find_segment(const DevSeg* __restrict__ segs, int nseg, int64_t t) {
   int lo = 0, hi = nseg - 1;
   while (lo < hi) {
@@ -528,9 +702,12 @@ __device__ __forceinline__ void wait_tile(int younger, int D, uint32_t& token) {
   vm_wait_n<0, 63>(token, n < 63 ? n : 63);
 }
 
-template <int STRAT, int STEPS>
+// LM = 1: lane-major tiles (STEPS must be 32) driven by the per-segment plan tables `plans`; LM = 0: step-major.
+template <int STRAT, int STEPS, int LM>
 __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restrict__ q,
-                                                       const DevSeg* __restrict__ segs) {
+                                                       const DevSeg* __restrict__ segs,
+                                                       const LmSegPlan* __restrict__ plans) {
+  static_assert(!LM || STEPS == 32, "lane-major tiles are 2048 docs");
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63;
   // wave-uniform by construction; readfirstlane makes the compiler keep the whole tile/segment cursor in SGPRs
@@ -575,15 +752,20 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
     int isi = find_segment(segs, q->num_segments, t0);   // issue cursor: segment, its tile range, ring slot
     int64_t ifirst = segs[isi].first_wtile;
     int64_t iend = ifirst + segs[isi].num_wtiles;
+    // LM: the issue segment's plan table, one dword per lane (its load drains the ring once per segment crossing)
+    uint32_t ip = LM ? ((const uint32_t*)(plans + isi))[lane] : 0u;
     int64_t ti = t0;
     int islot = 0;
+    const uint32_t ring_lds = lds_addr(ring);
     auto issue_next = [&]() {
       while (ti >= iend) {
         ++isi;
         ifirst = segs[isi].first_wtile;
         iend = ifirst + segs[isi].num_wtiles;
+        if (LM) ip = ((const uint32_t*)(plans + isi))[lane];
       }
-      stage_tile<STEPS>(segs + isi, ti - ifirst, ring + islot * img_dw, lane, D);
+      if constexpr (LM) stage_tile_lm(ip, ti - ifirst, ring_lds + 4u * (uint32_t)(islot * img_dw), lane, D);
+      else stage_tile<STEPS>(segs + isi, ti - ifirst, ring + islot * img_dw, lane, D);
       ++ti;
       islot = islot + 1 == R ? 0 : islot + 1;
     };
@@ -597,11 +779,19 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
       const DevSeg* seg = segs + si;
       const int64_t seg_first = seg->first_wtile;
       const int64_t seg_end = min(t1, seg_first + (int64_t)seg->num_wtiles);
+      const uint32_t pp = LM ? ((const uint32_t*)(plans + si))[lane] : 0u;  // process segment's plan table
+      const int dbg = q->debug_stream_only;
+      const bool stream_only = dbg == 1;
       for (; t < seg_end; ++t) {
         uint32_t slot_off = (uint32_t)(pslot * img_dw);
         wait_tile((int)(ti - (t + 1)), D, slot_off);  // tile t has landed in its slot (same-wave LDS-DMA)
         if (ti < t1) issue_next();                     // refill the slot tile t-1 used
-        if (!q->debug_stream_only) process_tile<STRAT, STEPS>(q, seg, t - seg_first, ring + slot_off, lane, acc);
+        if (LM && dbg > 1) {
+          debug_tile_lm(dbg, pp, ring_lds + 4u * slot_off, lane);
+        } else if (!stream_only) {
+          if constexpr (LM) process_tile_lm<STRAT>(q, seg, pp, t - seg_first, ring + slot_off, ring_lds + 4u * slot_off, lane, acc);
+          else process_tile<STRAT, STEPS>(q, seg, t - seg_first, ring + slot_off, lane, acc);
+        }
         pslot = pslot + 1 == R ? 0 : pslot + 1;
       }
       if (t < t1) {
@@ -727,24 +917,25 @@ hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t*
   return hipGetLastError();
 }
 
-static const void* scan_fn(int strategy, int steps) {
-  if (strategy == STRAT_LDS) return steps == 16 ? (const void*)scan_kernel<STRAT_LDS, 16> : (const void*)scan_kernel<STRAT_LDS, 32>;
-  return steps == 16 ? (const void*)scan_kernel<STRAT_GLOBAL, 16> : (const void*)scan_kernel<STRAT_GLOBAL, 32>;
+static const void* scan_fn(int strategy, int steps, int lm) {
+  if (lm) return strategy == STRAT_LDS ? (const void*)scan_kernel<STRAT_LDS, 32, 1> : (const void*)scan_kernel<STRAT_GLOBAL, 32, 1>;
+  if (strategy == STRAT_LDS) return steps == 16 ? (const void*)scan_kernel<STRAT_LDS, 16, 0> : (const void*)scan_kernel<STRAT_LDS, 32, 0>;
+  return steps == 16 ? (const void*)scan_kernel<STRAT_GLOBAL, 16, 0> : (const void*)scan_kernel<STRAT_GLOBAL, 32, 0>;
 }
 
-hipError_t set_scan_lds_limit(int strategy, int steps, int bytes) {
-  return hipFuncSetAttribute(scan_fn(strategy, steps), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+hipError_t set_scan_lds_limit(int strategy, int steps, int lm, int bytes) {
+  return hipFuncSetAttribute(scan_fn(strategy, steps, lm), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
-hipError_t scan_occupancy(int strategy, int steps, int lds_bytes, int* blocks_per_cu) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, scan_fn(strategy, steps), kWGSize,
+hipError_t scan_occupancy(int strategy, int steps, int lm, int lds_bytes, int* blocks_per_cu) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, scan_fn(strategy, steps, lm), kWGSize,
                                                       (size_t)lds_bytes);
 }
 
-hipError_t launch_scan(int strategy, int steps, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs,
-                       hipStream_t s) {
-  void* args[] = {(void*)&q, (void*)&segs};
-  return hipLaunchKernel(scan_fn(strategy, steps), dim3(grid), dim3(kWGSize), args, (size_t)lds_bytes, s);
+hipError_t launch_scan(int strategy, int steps, int lm, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs,
+                       const LmSegPlan* plans, hipStream_t s) {
+  void* args[] = {(void*)&q, (void*)&segs, (void*)&plans};
+  return hipLaunchKernel(scan_fn(strategy, steps, lm), dim3(grid), dim3(kWGSize), args, (size_t)lds_bytes, s);
 }
 
 }  // namespace pa

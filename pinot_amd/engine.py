@@ -302,6 +302,7 @@ class GpuQueryExecutor:
         out["plan"] = {n: v.value for n, v in zip(names, vals)}
         out["plan"]["strategy"] = "lds" if out["plan"]["strategy"] == 0 else "global"
         out["plan"]["eager_literals"] = int(L.lib().pa_query_num_eager_literals(self.handle))
+        out["plan"]["lane_major"] = int(L.lib().pa_query_lane_major(self.handle))
         return out
 
     def fetch(self, stream=None) -> IntermediateResult:

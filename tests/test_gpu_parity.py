@@ -131,9 +131,12 @@ def test_random_queries(seed, qi):
     run_both(sql, segs, rel=rel)
 
 
-@pytest.mark.parametrize("flags", [L.PA_QF_FORCE_GLOBAL, L.PA_QF_STAGE_ALL, L.PA_QF_FORCE_GLOBAL | L.PA_QF_STAGE_ALL])
+@pytest.mark.parametrize("flags", [L.PA_QF_FORCE_GLOBAL, L.PA_QF_STAGE_ALL, L.PA_QF_FORCE_GLOBAL | L.PA_QF_STAGE_ALL,
+                                   L.PA_QF_NO_LANE_MAJOR, L.PA_QF_NO_LANE_MAJOR | L.PA_QF_FORCE_GLOBAL,
+                                   L.PA_QF_NO_LANE_MAJOR | L.PA_QF_STAGE_ALL | L.PA_QF_NO_LAZY])
 def test_strategies_agree(flags):
-    """LDS-privatised vs global accumulators, staged vs lazy post-filter columns: identical results."""
+    """LDS-privatised vs global accumulators, staged vs lazy post-filter columns, lane-major vs step-major tiles:
+    identical results."""
     segs = [make_segment(11 + i, n, COLS, no_dict=RAW) for i, n in enumerate((30001, 4096))]
     for sql in QUERIES[:8]:
         sql = _fill(sql, segs[0])
@@ -154,7 +157,9 @@ LAZY_QUERIES = [
 
 
 @pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LAZY, L.PA_QF_FORCE_LDS, L.PA_QF_STAGE_ALL,
-                                   (4 << L.PA_QF_WG_SHIFT) | (2 << L.PA_QF_RING_SHIFT) | L.PA_QF_STEPS16])
+                                   (4 << L.PA_QF_WG_SHIFT) | (2 << L.PA_QF_RING_SHIFT) | L.PA_QF_STEPS16,
+                                   L.PA_QF_NO_LANE_MAJOR, L.PA_QF_NO_LANE_MAJOR | L.PA_QF_NO_LAZY,
+                                   (2 << L.PA_QF_WG_SHIFT) | (3 << L.PA_QF_RING_SHIFT)])
 def test_lazy_clauses(flags):
     """Late materialisation: clauses behind a very selective lead clause run only on its survivors, from HBM.
     Every plan variant must return the oracle's result; the default plan must actually defer clauses."""
@@ -174,8 +179,10 @@ def test_lazy_clauses(flags):
         if flags == 0:
             ex = GpuQueryExecutor(parse_sql(LAZY_QUERIES[0].format(**vals)), gsegs)
             st = ex.stats()
+            lm = L.lib().pa_query_lane_major(ex.handle)
             ex.close()
             assert st["plan"]["eager_literals"] == 1, st
+            assert lm == 1, "the headline shape must run the lane-major kernel"
     finally:
         for g in gsegs:
             g.close()
@@ -261,10 +268,11 @@ def test_num_groups_limit_guard():
     g.close()
 
 
-@pytest.mark.parametrize("nb", [1, 7, 8, 15, 16, 17, 24, 31])
-def test_bit_widths_through_capi(nb):
-    """Raw C-ABI use: an nb-bit column with no dictionary values (STRING type), DICT_RANGE filter count and a
-    DICT_SET filter, against numpy on the same ids."""
+@pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LANE_MAJOR])
+@pytest.mark.parametrize("nb", list(range(1, 32)))
+def test_bit_widths_through_capi(nb, flags):
+    """Raw C-ABI use: an nb-bit column with no dictionary values (STRING type), DICT_RANGE filter count (plain and
+    negated) and a DICT_SET filter, against numpy on the same ids — every bit width, both tile layouts."""
     from pinot_amd.segment import pack_bits
     lib = L.lib()
     n = 50_000 + nb
@@ -277,10 +285,11 @@ def test_bit_widths_through_capi(nb):
     L.check(lib.pa_segment_add_sv_dict_column(seg, 0, fwd.ctypes.data, fwd.nbytes, nb, card, L.PA_STRING, None, None),
             "add")
     lo, hi = int(card // 5), int(card // 2) + 1
-    for kind in (L.PA_LEAF_DICT_RANGE, L.PA_LEAF_DICT_SET):
+    for kind, negate in ((L.PA_LEAF_DICT_RANGE, 0), (L.PA_LEAF_DICT_RANGE, 1), (L.PA_LEAF_DICT_SET, 0)):
         if kind == L.PA_LEAF_DICT_SET and nb > 20:
             continue
         spec = L.QuerySpec()
+        spec.flags = flags
         spec.num_leaves = 1
         spec.leaves[0].column_id = 0
         spec.leaves[0].kind = kind
@@ -291,9 +300,12 @@ def test_bit_widths_through_capi(nb):
         q = L.check_ptr(lib.pa_query_create(ctypes.byref(spec), 1), "qcreate")
         lp = (L.LeafParams * 1)()
         lut = None
+        lp[0].negate = negate
         if kind == L.PA_LEAF_DICT_RANGE:
             lp[0].lo, lp[0].hi = lo, hi
             expected = int(((ids >= lo) & (ids < hi)).sum())
+            if negate:
+                expected = n - expected
         else:
             sel = np.arange(0, card, 3, dtype=np.int64)
             lut = np.zeros((card + 31) // 32, dtype=np.uint32)
@@ -302,6 +314,7 @@ def test_bit_widths_through_capi(nb):
             expected = int((ids % 3 == 0).sum())
         L.check(lib.pa_query_bind_segment(q, 0, seg, lp, None), "bind")
         L.check(lib.pa_query_prepare(q), "prepare")
+        assert lib.pa_query_lane_major(q) == (0 if flags else 1)
         L.check(lib.pa_query_execute(q, None), "execute")
         keys = np.zeros(1, np.int64)
         counts = np.zeros(1, np.int64)

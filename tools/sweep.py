@@ -24,6 +24,10 @@ def main():
     ap.add_argument("--docs", type=int, default=10_000_000)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--query", default=bench.QUERY)
+    ap.add_argument("--quick", action="store_true", help="only the automatic plans")
+    ap.add_argument("--only", default=None, help="run just this configuration name")
+    ap.add_argument("--debug", action="store_true", help="auto plan + measurement-only tile bodies")
+    ap.add_argument("--mode", choices=("both", "full", "stream"), default="both")
     args = ap.parse_args()
     import torch
     from pinot_amd import parse_sql
@@ -40,16 +44,25 @@ def main():
             c.fwd_bytes = None
     q = parse_sql(args.query)
     stream = torch.cuda.current_stream()
-    configs = [("auto", 0), ("auto_nolazy", L.PA_QF_NO_LAZY)]
+    configs = [("auto", 0), ("auto_nolazy", L.PA_QF_NO_LAZY), ("auto_stepmajor", L.PA_QF_NO_LANE_MAJOR),
+               ("auto_nolazy_stepmajor", L.PA_QF_NO_LAZY | L.PA_QF_NO_LANE_MAJOR),
+               ("dbg_decode_sink", 1 << 18), ("dbg_valu_only", 2 << 18), ("dbg_lds_only", 3 << 18)]
     for lazy_name, lazy_flag in (("", 0), ("_nolazy", L.PA_QF_NO_LAZY)):
         for steps_flag, steps in ((L.PA_QF_STEPS32, 32), (L.PA_QF_STEPS16, 16)):
             for ring in (2, 3, 4):
                 for wg in (2, 3, 4):
                     configs.append(("s%d_r%d_wg%d%s" % (steps, ring, wg, lazy_name),
                                     lazy_flag | steps_flag | (ring << L.PA_QF_RING_SHIFT) | (wg << L.PA_QF_WG_SHIFT)))
+    if args.quick:
+        configs = configs[:4]
+    if args.debug:
+        configs = [configs[0]] + configs[4:]
+    if args.only:
+        configs = [c for c in configs if c[0] == args.only]
+    modes = {"both": (0, L.PA_QF_DEBUG_STREAM_ONLY), "full": (0,), "stream": (L.PA_QF_DEBUG_STREAM_ONLY,)}[args.mode]
     ref = None
     for name, flags in configs:
-        for dbg in (0, L.PA_QF_DEBUG_STREAM_ONLY):
+        for dbg in modes:
             try:
                 ex = GpuQueryExecutor(q, gsegs, flags=flags | dbg)
             except L.PinotAmdError as e:
@@ -58,18 +71,20 @@ def main():
                 break
             ex.execute(stream.cuda_stream)
             torch.cuda.synchronize()
-            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.reps)]
-            for a, b in evs:
-                a.record(stream)
-                ex.execute(stream.cuda_stream)
-                b.record(stream)
+            # back-to-back scans between one event pair (per-launch duration, as in bench.py)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for _ in range(args.reps):
+                ex.scan(stream.cuda_stream)
+            b.record(stream)
             torch.cuda.synchronize()
-            ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+            ms = a.elapsed_time(b) / args.reps
+            ex.execute(stream.cuda_stream)
             st = ex.stats()
             rec = {"config": name, "stream_only": bool(dbg), "plan": st["plan"], "kernel_ms": round(ms, 4),
                    "GBps": round(st["staged_bytes"] / ms / 1e6, 1),
                    "Grows_per_s": round(st["num_docs"] / ms / 1e6, 1)}
-            if not dbg:
+            if not dbg and not (flags >> 18) & 7:
                 res = ex.fetch(stream.cuda_stream)
                 snap = {k: tuple(v) for k, v in res.groups.items()}
                 if ref is None:
