@@ -95,6 +95,10 @@ extern "C" {
 #define PA_AGG_MIN 2
 #define PA_AGG_MAX 3
 #define PA_AGG_DISTINCTCOUNTHLL 4
+#define PA_AGG_COUNT_MV 5 /* COUNTMV: number of values of an MV column (AVGMV = SUM over an MV column / COUNTMV) */
+/* SUM / MIN / MAX / DISTINCTCOUNTHLL over a multi-value column aggregate every value of the doc (SUMMV, MINMV, MAXMV,
+ * DISTINCTCOUNTHLLMV); a multi-value group-by column expands a doc into one key per value (cartesian product over
+ * several MV columns), as DictionaryBasedGroupKeyGenerator.getIntRawKeys does. */
 
 /* ---------------------------------------------------------------- device / errors */
 int pa_abi_version(void);
@@ -211,6 +215,7 @@ int pa_query_scan(pa_query* q, void* stream);
 #define PA_ACC_MAX_I64 4   /* reduce MAX */
 #define PA_ACC_HLL_U32 5   /* reduce MAX */
 #define PA_ACC_SUM_I64X2 6 /* reduce SUM; [2k] = sum of low 32 bits (unsigned), [2k+1] = sum of high 32 bits */
+#define PA_ACC_DOCS_U64 7  /* reduce SUM; one element: docs that passed the filter (numDocsScanned) */
 /* All sections live in one device block of pa_query_accumulator_bytes() bytes (256-byte aligned sections).
  * pa_query_set_accumulator_buffer lets the caller own that block (e.g. memory its collective library
  * registered) instead of the library: call after pa_query_prepare; `bytes` must be >= the size. */
@@ -228,6 +233,10 @@ void* pa_query_section(const pa_query* q, int32_t section, int32_t* kind, int64_
  * Synchronises `stream`. */
 int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out_keys,
                        int64_t* out_counts, void* const* out_aggs);
+
+/* numDocsScanned captured by the last pa_query_fetch (docs that passed the filter; with a multi-value group-by this
+ * differs from the sum of the group counts), <0 on error. */
+int64_t pa_query_matched_docs(const pa_query* q);
 
 /* Kernel statistics of the last execute (for roofline accounting): bytes of forward index staged
  * (always-read columns), number of docs scanned. */

@@ -38,14 +38,16 @@ def build(force=False):
 class OCol(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("num_bits", ctypes.c_int32), ("cardinality", ctypes.c_int32),
                 ("reserved", ctypes.c_int32), ("fwd", ctypes.c_void_p), ("raw", ctypes.c_void_p),
-                ("dict_f64", ctypes.c_void_p), ("dict_hash", ctypes.c_void_p)]
+                ("dict_f64", ctypes.c_void_p), ("dict_hash", ctypes.c_void_p),
+                ("mv_bitmap", ctypes.c_void_p), ("mv_num_values", ctypes.c_int64)]
 
 
 class OLeaf(ctypes.Structure):
     _fields_ = [("col", ctypes.c_int32), ("kind", ctypes.c_int32), ("match", ctypes.c_void_p),
                 ("dlo", ctypes.c_double), ("dhi", ctypes.c_double), ("ilo", ctypes.c_int64), ("ihi", ctypes.c_int64),
                 ("lo_unbounded", ctypes.c_int32), ("hi_unbounded", ctypes.c_int32),
-                ("lo_incl", ctypes.c_int32), ("hi_incl", ctypes.c_int32)]
+                ("lo_incl", ctypes.c_int32), ("hi_incl", ctypes.c_int32),
+                ("exclusive", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class OQuery(ctypes.Structure):
@@ -248,7 +250,13 @@ def _flatten(f, leaves, ops, segment):
         leaves.append(f)
 
 
-_AGG = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "DISTINCTCOUNTHLL": 4}
+_AGG = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "DISTINCTCOUNTHLL": 4, "COUNTMV": 5}
+# query function -> oracle accumulators (the *MV forms read every value of the MV column; AVG = SUM + group count,
+# AVGMV = SUM + COUNTMV over the column)
+_ORACLE_FNS = {"SUM": ("SUM",), "AVG": ("SUM",), "MIN": ("MIN",), "MAX": ("MAX",),
+               "DISTINCTCOUNTHLL": ("DISTINCTCOUNTHLL",), "SUMMV": ("SUM",), "MINMV": ("MIN",), "MAXMV": ("MAX",),
+               "DISTINCTCOUNTHLLMV": ("DISTINCTCOUNTHLL",), "COUNTMV": ("COUNTMV",), "AVGMV": ("SUM", "COUNTMV"),
+               "COUNT": ("COUNT",)}
 
 
 def run_segment(query, segment):
@@ -258,7 +266,7 @@ def run_segment(query, segment):
     cidx = {c: i for i, c in enumerate(cols_order)}
     ocols = (OCol * max(1, len(cols_order)))()
     keep = []
-    hll_cols = {a.column for a in query.aggregations if a.function == "DISTINCTCOUNTHLL"}
+    hll_cols = {a.column for a in query.aggregations if a.function in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV")}
     for name, i in cidx.items():
         col = segment.column(name)
         oc = ocols[i]
@@ -269,6 +277,12 @@ def run_segment(query, segment):
             fwd = np.ascontiguousarray(col.fwd_bytes, dtype=np.uint8)
             keep.append(fwd)
             oc.fwd = fwd.ctypes.data
+            if not col.single_value:  # FixedBitMVForwardIndexReader sections (chunk offsets | bitmap | values)
+                _, _, boff, roff = col.mv_layout(segment.num_docs)
+                oc.kind = 5
+                oc.fwd = fwd.ctypes.data + roff
+                oc.mv_bitmap = fwd.ctypes.data + boff
+                oc.mv_num_values = col.total_num_values
             if col.data_type != "STRING":
                 df = np.ascontiguousarray(col.dictionary, dtype=np.float64)
                 keep.append(df)
@@ -296,19 +310,23 @@ def run_segment(query, segment):
             keep.append(m)
             oleaves[i].kind = 0
             oleaves[i].match = m.ctypes.data
+            # PredicateEvaluator.isExclusive (NOT_EQ, NOT_IN): applyMV requires every value to pass
+            oleaves[i].exclusive = int(isinstance(pred, (Q.NotEqPredicate, Q.NotInPredicate)))
         else:
             _raw_leaf(pred, col, oleaves[i])
     ops_a = np.array(ops or [0], dtype=np.int32)
 
-    # aggregations: one oracle agg per distinct (function, column); AVG uses SUM + count
+    # aggregations: one oracle accumulator per distinct (function, column)
     oaggs = []
     amap = []
     for a in query.aggregations:
-        fn = "SUM" if a.function == "AVG" else a.function
-        key = (fn, a.column if fn != "COUNT" else None, a.log2m if fn == "DISTINCTCOUNTHLL" else 0)
-        if key not in oaggs:
-            oaggs.append(key)
-        amap.append(oaggs.index(key))
+        idx = []
+        for fn in _ORACLE_FNS[a.function]:
+            key = (fn, a.column if fn != "COUNT" else None, a.log2m if fn == "DISTINCTCOUNTHLL" else 0)
+            if key not in oaggs:
+                oaggs.append(key)
+            idx.append(oaggs.index(key))
+        amap.append(idx[0] if len(idx) == 1 else tuple(idx))
     at = np.array([_AGG[k[0]] for k in oaggs] or [0], dtype=np.int32)
     ac = np.array([cidx[k[1]] if k[1] else 0 for k in oaggs] or [0], dtype=np.int32)
     al = np.array([k[2] for k in oaggs] or [0], dtype=np.int32)
@@ -331,7 +349,8 @@ def run_segment(query, segment):
         prod = 1
         for c in query.group_by:
             prod *= segment.column(c).cardinality
-        cap = max(1, min(prod, segment.num_docs, query.num_groups_limit))
+        mv = any(not segment.column(c).single_value for c in query.group_by)
+        cap = max(1, min(prod, query.num_groups_limit) if mv else min(prod, segment.num_docs, query.num_groups_limit))
     else:
         cap = 1
     keys = np.zeros(cap, dtype=np.int64)
@@ -387,7 +406,7 @@ def run_query(query, segments):
             acc = merged[key]
             acc[0] += cnt
             for ai, k in enumerate(oaggs):
-                if k[0] == "SUM":
+                if k[0] in ("SUM", "COUNTMV"):
                     acc[1][ai] = acc[1][ai] + row[ai]
                 elif k[0] == "MIN":
                     acc[1][ai] = min(acc[1][ai], row[ai])
@@ -400,7 +419,8 @@ def run_query(query, segments):
     out.num_docs_scanned = scanned
     if not query.group_by and () not in merged:
         merged[()] = [0, [np.zeros(1 << k[2], np.uint8) if k[0] == "DISTINCTCOUNTHLL" else
-                          (0.0 if k[0] in ("SUM", "COUNT") else (np.inf if k[0] == "MIN" else -np.inf)) for k in oaggs]]
+                          (0.0 if k[0] in ("SUM", "COUNT", "COUNTMV") else (np.inf if k[0] == "MIN" else -np.inf))
+                          for k in oaggs]]
     for key, (cnt, row) in merged.items():
         vals = []
         for a, ai in zip(query.aggregations, amap):
@@ -408,7 +428,11 @@ def run_query(query, segments):
                 vals.append(cnt)
             elif a.function == "AVG":
                 vals.append(AvgPair(row[ai], cnt))
-            elif a.function == "DISTINCTCOUNTHLL":
+            elif a.function == "AVGMV":
+                vals.append(AvgPair(row[ai[0]], int(row[ai[1]])))
+            elif a.function == "COUNTMV":
+                vals.append(int(row[ai]))
+            elif a.function in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV"):
                 vals.append(HyperLogLog(a.log2m, row[ai] if isinstance(row[ai], np.ndarray) else None))
             else:
                 vals.append(row[ai])

@@ -16,6 +16,13 @@
  *  - DISTINCTCOUNTHLL:   stream-lib 2.9.8 MurmurHash.hashLong / hash(byte[]) + HyperLogLog.offerHashed
  *                        (offering every doc's value; register max is idempotent, so this equals the reference's
  *                        dictId-bitmap-then-offer of DistinctCountHLLAggregationFunction.java:176-183)
+ *  - multi-value:        FixedBitMVForwardIndexReader.getDictIdMV in docId order (readers/forward/
+ *                        FixedBitMVForwardIndexReader.java:106-146: start = previous end, end = next set bit of the
+ *                        row-start bitmap, numValues for the last doc), MV leaves via
+ *                        BaseDictionaryBasedPredicateEvaluator.applyMV (:164-179: ANY value for inclusive predicates,
+ *                        ALL values for exclusive ones), MV group keys via DictionaryBasedGroupKeyGenerator.getIntRawKeys
+ *                        (:473-540, cartesian expansion in the reference's order), *MV aggregations
+ *                        (SumMVAggregationFunction.java:42-82 etc.: every value of the doc, for every group key)
  */
 #include <math.h>
 #include <stdint.h>
@@ -121,9 +128,9 @@ static void hll_offer(uint8_t* regs, int32_t log2m, int32_t hashed) {
 }
 
 /* ------------------------------------------------------------------ query */
-enum { OC_DICT = 0, OC_RAW_I32 = 1, OC_RAW_I64 = 2, OC_RAW_F32 = 3, OC_RAW_F64 = 4 };
+enum { OC_DICT = 0, OC_RAW_I32 = 1, OC_RAW_I64 = 2, OC_RAW_F32 = 3, OC_RAW_F64 = 4, OC_MV_DICT = 5 };
 enum { OQ_LEAF = 0, OQ_AND = 1, OQ_OR = 2, OQ_NOT = 3 };
-enum { OA_COUNT = 0, OA_SUM = 1, OA_MIN = 2, OA_MAX = 3, OA_HLL = 4 };
+enum { OA_COUNT = 0, OA_SUM = 1, OA_MIN = 2, OA_MAX = 3, OA_HLL = 4, OA_COUNTMV = 5 };
 
 typedef struct {
   int32_t kind;
@@ -134,6 +141,8 @@ typedef struct {
   const void* raw;          /* raw values */
   const double* dict_f64;   /* dictionary values as double (getDoubleValue) */
   const int32_t* dict_hash; /* MurmurHash.hash(Dictionary.get(dictId)) */
+  const uint8_t* mv_bitmap; /* MV: row-start bitmap section (one bit per value, MSB-first) */
+  int64_t mv_num_values;    /* MV: total number of values */
 } oracle_col;
 
 typedef struct {
@@ -143,6 +152,8 @@ typedef struct {
   double dlo, dhi;          /* raw FLOAT/DOUBLE */
   int64_t ilo, ihi;         /* raw INT/LONG */
   int32_t lo_unbounded, hi_unbounded, lo_incl, hi_incl;
+  int32_t exclusive;        /* NOT_EQ / NOT_IN: an MV doc matches when ALL its values pass applySV */
+  int32_t reserved;
 } oracle_leaf;
 
 typedef struct {
@@ -161,6 +172,29 @@ typedef struct {
 
 static int32_t dict_id(const oracle_col* c, int64_t doc) { return oracle_read_int(c->fwd, doc, c->num_bits); }
 
+/* PinotDataBitSet.getNextSetBitOffset: first set bit at index >= from (MSB-first within each byte), or -1 */
+static int64_t next_set_bit(const uint8_t* bits, int64_t from, int64_t nbits) {
+  for (int64_t i = from; i < nbits; ++i)
+    if (bits[i >> 3] & (0x80 >> (i & 7))) return i;
+  return -1;
+}
+
+/* value range [start, end) of the current doc of every MV column (sequential-docId context of the reader) */
+#define OMAX_COLS 32
+static int64_t g_mv_start[OMAX_COLS], g_mv_end[OMAX_COLS];
+
+static void mv_advance(const oracle_col* cols, int ncols, int64_t doc, int64_t num_docs) {
+  for (int c = 0; c < ncols && c < OMAX_COLS; ++c) {
+    if (cols[c].kind != OC_MV_DICT) continue;
+    const int64_t start = doc == 0 ? 0 : g_mv_end[c];
+    int64_t end = doc == num_docs - 1 ? cols[c].mv_num_values
+                                      : next_set_bit(cols[c].mv_bitmap, start + 1, cols[c].mv_num_values);
+    if (end < 0) end = cols[c].mv_num_values;
+    g_mv_start[c] = start;
+    g_mv_end[c] = end;
+  }
+}
+
 static double raw_double(const oracle_col* c, int64_t doc) {
   switch (c->kind) {
     case OC_RAW_I32: return (double)((const int32_t*)c->raw)[doc];
@@ -172,6 +206,14 @@ static double raw_double(const oracle_col* c, int64_t doc) {
 
 static int leaf_match(const oracle_leaf* L, const oracle_col* cols, int64_t doc) {
   const oracle_col* c = &cols[L->col];
+  if (L->kind == 0 && c->kind == OC_MV_DICT) {
+    for (int64_t v = g_mv_start[L->col]; v < g_mv_end[L->col]; ++v) {
+      const int m = L->match[oracle_read_int(c->fwd, v, c->num_bits)];
+      if (L->exclusive && !m) return 0;
+      if (!L->exclusive && m) return 1;
+    }
+    return L->exclusive ? 1 : 0;
+  }
   if (L->kind == 0) return L->match[dict_id(c, doc)];
   if (c->kind == OC_RAW_I32 || c->kind == OC_RAW_I64) {
     const int64_t v = c->kind == OC_RAW_I32 ? ((const int32_t*)c->raw)[doc] : ((const int64_t*)c->raw)[doc];
@@ -278,55 +320,118 @@ int64_t oracle_run_segment(const oracle_col* cols, int64_t num_docs, const oracl
     if (q->agg_type[a] == OA_HLL) memset(out_hll[a], 0, (size_t)capacity << q->agg_log2m[a]);
   }
   int64_t matched = 0;
+  int ncols = 0;
+  for (int j = 0; j < q->num_gb; ++j) if (q->gb_col[j] + 1 > ncols) ncols = q->gb_col[j] + 1;
+  for (int a = 0; a < q->num_aggs; ++a) if (q->agg_col[a] + 1 > ncols) ncols = q->agg_col[a] + 1;
+  for (int l = 0; l < q->num_leaves; ++l) if (q->leaves[l].col + 1 > ncols) ncols = q->leaves[l].col + 1;
+  int64_t* raw_keys = NULL;
+  int64_t raw_cap = 0;
   for (int64_t doc = 0; doc < num_docs; ++doc) {
+    mv_advance(cols, ncols, doc, num_docs);
     if (!filter_match(q, cols, doc)) continue;
     matched++;
-    int64_t g = 0;
+    /* group keys of this doc: getIntRawKeys (one key for SV-only group-by) */
+    int64_t nkeys = 1;
+    int64_t rawkey = 0;
     if (grouped) {
-      int64_t key = 0;
-      for (int j = q->num_gb - 1; j >= 0; --j) key = key * cols[q->gb_col[j]].cardinality + dict_id(&cols[q->gb_col[j]], doc);
-      const int32_t gid = gmap_get(&map, key, q->num_groups_limit);
-      if (gid < 0) continue; /* group limit reached: the doc is not aggregated */
-      g = gid;
-      if (g >= capacity) continue;
-      if (g + 1 > ngroups) {
-        ngroups = g + 1;
-        out_keys[g] = key;
-        out_counts[g] = 0;
+      int have_array = 0;
+      for (int j = q->num_gb - 1; j >= 0; --j) {
+        const oracle_col* gc = &cols[q->gb_col[j]];
+        const int64_t card = gc->cardinality;
+        if (gc->kind != OC_MV_DICT || g_mv_end[q->gb_col[j]] - g_mv_start[q->gb_col[j]] == 1) {
+          const int32_t id = gc->kind == OC_MV_DICT ? oracle_read_int(gc->fwd, g_mv_start[q->gb_col[j]], gc->num_bits)
+                                                    : dict_id(gc, doc);
+          if (!have_array) rawkey = rawkey * card + id;
+          else for (int64_t k = 0; k < nkeys; ++k) raw_keys[k] = raw_keys[k] * card + id;
+        } else {
+          const int64_t s0 = g_mv_start[q->gb_col[j]], nv = g_mv_end[q->gb_col[j]] - s0;
+          const int64_t cur = have_array ? nkeys : 1;
+          if (cur * nv > raw_cap) {
+            raw_cap = cur * nv * 2;
+            raw_keys = (int64_t*)realloc(raw_keys, sizeof(int64_t) * raw_cap);
+            if (!raw_keys) return -1;
+          }
+          if (!have_array) {
+            for (int64_t v = 0; v < nv; ++v) raw_keys[v] = rawkey * card + oracle_read_int(gc->fwd, s0 + v, gc->num_bits);
+            have_array = 1;
+          } else {
+            /* newRawKeys[v*cur + k] = rawKeys[k] * card + dictId_v, built back to front so it can run in place */
+            for (int64_t v = nv - 1; v >= 0; --v) {
+              const int32_t id = oracle_read_int(gc->fwd, s0 + v, gc->num_bits);
+              for (int64_t k = cur - 1; k >= 0; --k) raw_keys[v * cur + k] = raw_keys[k] * card + id;
+            }
+          }
+          nkeys = cur * nv;
+        }
+      }
+      if (!have_array) {
+        if (raw_cap < 1) {
+          raw_cap = 16;
+          raw_keys = (int64_t*)realloc(raw_keys, sizeof(int64_t) * raw_cap);
+          if (!raw_keys) return -1;
+        }
+        raw_keys[0] = rawkey;
+        nkeys = 1;
       }
     }
-    out_counts[g]++;
-    for (int a = 0; a < q->num_aggs; ++a) {
-      const int t = q->agg_type[a];
-      if (t == OA_COUNT) continue;
-      const oracle_col* c = &cols[q->agg_col[a]];
-      if (t == OA_HLL) {
-        int32_t h;
-        if (c->kind == OC_DICT) {
-          h = c->dict_hash[dict_id(c, doc)];
-        } else if (c->kind == OC_RAW_I32) {
-          h = oracle_hash_long(((const int32_t*)c->raw)[doc]);
-        } else if (c->kind == OC_RAW_I64) {
-          h = oracle_hash_long(((const int64_t*)c->raw)[doc]);
-        } else if (c->kind == OC_RAW_F32) {
-          int32_t bits;
-          memcpy(&bits, (const float*)c->raw + doc, 4);
-          h = oracle_hash_long(bits);
-        } else {
-          int64_t bits;
-          memcpy(&bits, (const double*)c->raw + doc, 8);
-          h = oracle_hash_long(bits);
+    for (int64_t kk = 0; kk < nkeys; ++kk) {
+      int64_t g = 0;
+      if (grouped) {
+        const int64_t key = raw_keys[kk];
+        const int32_t gid = gmap_get(&map, key, q->num_groups_limit);
+        if (gid < 0) continue; /* group limit reached: the doc is not aggregated into this key */
+        g = gid;
+        if (g >= capacity) continue;
+        if (g + 1 > ngroups) {
+          ngroups = g + 1;
+          out_keys[g] = key;
+          out_counts[g] = 0;
         }
-        hll_offer(out_hll[a] + ((size_t)g << q->agg_log2m[a]), q->agg_log2m[a], h);
-        continue;
       }
-      const double v = c->kind == OC_DICT ? c->dict_f64[dict_id(c, doc)] : raw_double(c, doc);
-      double* acc = &out_vals[a * capacity + g];
-      if (t == OA_SUM) *acc += v;
-      else if (t == OA_MIN) { if (v < *acc) *acc = v; }
-      else if (t == OA_MAX) { if (v > *acc) *acc = v; }
+      out_counts[g]++;
+      for (int a = 0; a < q->num_aggs; ++a) {
+        const int t = q->agg_type[a];
+        if (t == OA_COUNT) continue;
+        const oracle_col* c = &cols[q->agg_col[a]];
+        const int mv = c->kind == OC_MV_DICT;
+        const int64_t v0 = mv ? g_mv_start[q->agg_col[a]] : doc;
+        const int64_t v1 = mv ? g_mv_end[q->agg_col[a]] : doc + 1;
+        for (int64_t vi = v0; vi < v1; ++vi) {
+          if (t == OA_COUNTMV) {
+            out_vals[a * capacity + g] += 1.0;
+            continue;
+          }
+          if (t == OA_HLL) {
+            int32_t h;
+            if (c->kind == OC_DICT || mv) {
+              h = c->dict_hash[oracle_read_int(c->fwd, vi, c->num_bits)];
+            } else if (c->kind == OC_RAW_I32) {
+              h = oracle_hash_long(((const int32_t*)c->raw)[vi]);
+            } else if (c->kind == OC_RAW_I64) {
+              h = oracle_hash_long(((const int64_t*)c->raw)[vi]);
+            } else if (c->kind == OC_RAW_F32) {
+              int32_t bits;
+              memcpy(&bits, (const float*)c->raw + vi, 4);
+              h = oracle_hash_long(bits);
+            } else {
+              int64_t bits;
+              memcpy(&bits, (const double*)c->raw + vi, 8);
+              h = oracle_hash_long(bits);
+            }
+            hll_offer(out_hll[a] + ((size_t)g << q->agg_log2m[a]), q->agg_log2m[a], h);
+            continue;
+          }
+          const double v = (c->kind == OC_DICT || mv) ? c->dict_f64[oracle_read_int(c->fwd, vi, c->num_bits)]
+                                                      : raw_double(c, vi);
+          double* acc = &out_vals[a * capacity + g];
+          if (t == OA_SUM) *acc += v;
+          else if (t == OA_MIN) { if (v < *acc) *acc = v; }
+          else if (t == OA_MAX) { if (v > *acc) *acc = v; }
+        }
+      }
     }
   }
+  free(raw_keys);
   if (grouped) {
     free(map.keys);
     free(map.vals);

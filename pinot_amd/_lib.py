@@ -16,7 +16,7 @@ PA_MAX_AGGS = 16
 PA_INT, PA_LONG, PA_FLOAT, PA_DOUBLE, PA_STRING, PA_BYTES = range(6)
 PA_LEAF_DICT_RANGE, PA_LEAF_DICT_SET, PA_LEAF_RAW_RANGE, PA_LEAF_MV_DICT_RANGE, PA_LEAF_MV_DICT_SET = range(5)
 PA_OP_LEAF, PA_OP_AND, PA_OP_OR, PA_OP_NOT = range(4)
-PA_AGG_COUNT, PA_AGG_SUM, PA_AGG_MIN, PA_AGG_MAX, PA_AGG_DISTINCTCOUNTHLL = range(5)
+PA_AGG_COUNT, PA_AGG_SUM, PA_AGG_MIN, PA_AGG_MAX, PA_AGG_DISTINCTCOUNTHLL, PA_AGG_COUNT_MV = range(6)
 PA_QF_STAGE_ALL = 1
 PA_QF_FORCE_GLOBAL = 2
 PA_QF_STEPS16 = 1 << 4
@@ -28,7 +28,7 @@ PA_QF_WG_SHIFT = 12
 PA_QF_DEBUG_STREAM_ONLY = 1 << 16
 PA_QF_NO_LANE_MAJOR = 1 << 17
 PA_ACC_COUNT_U64, PA_ACC_SUM_I64, PA_ACC_SUM_F64, PA_ACC_MIN_I64, PA_ACC_MAX_I64, PA_ACC_HLL_U32, \
-    PA_ACC_SUM_I64X2 = range(7)
+    PA_ACC_SUM_I64X2, PA_ACC_DOCS_U64 = range(8)
 
 # every symbol declared in include/pinot_amd.h
 EXPORTED = [
@@ -37,7 +37,8 @@ EXPORTED = [
     "pa_segment_add_raw_column", "pa_segment_num_docs", "pa_segment_device_bytes", "pa_segment_destroy",
     "pa_query_create", "pa_query_bind_segment", "pa_query_prepare", "pa_query_num_keys",
     "pa_query_execute", "pa_query_reset", "pa_query_scan", "pa_query_num_eager_literals", "pa_query_lane_major",
-    "pa_query_accumulator_bytes", "pa_query_set_accumulator_buffer", "pa_query_num_sections", "pa_query_section", "pa_query_fetch", "pa_query_stats",
+    "pa_query_accumulator_bytes", "pa_query_set_accumulator_buffer", "pa_query_num_sections", "pa_query_section",
+    "pa_query_fetch", "pa_query_matched_docs", "pa_query_stats",
     "pa_query_plan", "pa_query_destroy",
 ]
 
@@ -111,6 +112,7 @@ def _declare(lib):
         "pa_query_num_sections": (i32, [vp]),
         "pa_query_section": (vp, [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i64)]),
         "pa_query_fetch": (i64, [vp, vp, i64, vp, vp, vp]),
+        "pa_query_matched_docs": (i64, [vp]),
         "pa_query_stats": (ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "pa_query_plan": (ctypes.c_int, [vp] + [ctypes.POINTER(i32)] * 7),
         "pa_query_destroy": (None, [vp]),

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cmath>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -70,7 +71,9 @@ struct Column {
   DevBuf raw;     // raw values (SV raw)
   DevBuf dict;    // int64 or double
   DevBuf hashes;  // int32 murmur hashes (STRING/BYTES dictionaries)
+  DevBuf mv_off;  // MV: int32[num_docs + 1] value offset of every doc's first value
   ~Column() {
+    dev_free(mv_off);
     dev_free(words);
     dev_free(raw);
     dev_free(dict);
@@ -181,9 +184,71 @@ int pa_segment_add_mv_dict_column(pa_segment* seg, int32_t column_id, const uint
                                   uint64_t fwd_index_bytes, int32_t num_bits_per_value, int32_t cardinality,
                                   int64_t total_num_values, int32_t value_type, const void* dict_values,
                                   const int32_t* dict_hashes) {
-  (void)seg; (void)column_id; (void)fwd_index; (void)fwd_index_bytes; (void)num_bits_per_value;
-  (void)cardinality; (void)total_num_values; (void)value_type; (void)dict_values; (void)dict_hashes;
-  return fail(PA_EUNSUPPORTED, "multi-value columns are not implemented yet");
+  if (!seg) return fail(PA_EINVAL, "null segment");
+  if (num_bits_per_value < 1 || num_bits_per_value > 31) return fail(PA_EINVAL, "num_bits_per_value must be 1..31");
+  if (cardinality < 1) return fail(PA_EINVAL, "cardinality < 1");
+  if (value_type < PA_INT || value_type > PA_BYTES) return fail(PA_EINVAL, "bad value_type");
+  if (seg->cols.count(column_id)) return fail(PA_EINVAL, "duplicate column id");
+  const int64_t nd = seg->num_docs;
+  if (total_num_values < nd || total_num_values > INT32_MAX)
+    return fail(PA_EINVAL, "total_num_values must be in [num_docs, 2^31) (every MV row holds at least one value)");
+  // FixedBitMVForwardIndexReader.java:66-79 section sizes: chunk offsets | row-start bitmap | bit-packed values
+  int64_t num_chunks = 0, docs_per_chunk = 1;
+  if (nd > 0) {
+    const float avg = (float)(total_num_values / nd);  // Java: int / int, then widened
+    docs_per_chunk = (int64_t)std::ceil((double)(2048.0f / avg));
+    num_chunks = (nd + docs_per_chunk - 1) / docs_per_chunk;
+  }
+  const uint64_t bitmap_bytes = (uint64_t)(total_num_values + 7) / 8;
+  const uint64_t raw_bytes = ((uint64_t)total_num_values * (uint64_t)num_bits_per_value + 7) / 8;
+  const uint64_t header = (uint64_t)num_chunks * 4;
+  if (fwd_index_bytes < header + bitmap_bytes + raw_bytes)
+    return fail(PA_EINVAL, "MV forward index shorter than its chunk-offset, bitmap and value sections");
+  const uint8_t* bitmap = fwd_index + header;
+  const uint8_t* raw = bitmap + bitmap_bytes;
+  // row starts: the set bits of the bitmap, in order (the reader's getNextSetBitOffset walk, done once at load)
+  std::vector<int32_t> off((size_t)nd + 1);
+  int64_t d = 0;
+  for (int64_t v = 0; v < total_num_values; ++v) {
+    if (bitmap[v >> 3] & (0x80 >> (v & 7))) {
+      if (d >= nd) return fail(PA_EINVAL, "MV bitmap has more row starts than documents");
+      off[d++] = (int32_t)v;
+    }
+  }
+  if (d != nd || (nd > 0 && off[0] != 0)) return fail(PA_EINVAL, "MV bitmap row starts do not match num_docs");
+  off[nd] = (int32_t)total_num_values;
+  for (int64_t ch = 0; ch < num_chunks; ++ch) {  // chunk offsets (big-endian int32) must agree with the bitmap
+    const uint8_t* p = fwd_index + 4 * ch;
+    const int64_t co = ((int64_t)p[0] << 24) | ((int64_t)p[1] << 16) | ((int64_t)p[2] << 8) | (int64_t)p[3];
+    if (co != off[ch * docs_per_chunk]) return fail(PA_EINVAL, "MV chunk offsets disagree with the row-start bitmap");
+  }
+  Column* c = new Column();
+  c->kind = COL_MV_DICT;
+  c->nbits = num_bits_per_value;
+  c->total_values = total_num_values;
+  // guard words | value stream padded to whole 64-value steps | guard words (reads stay in bounds)
+  const int64_t stream_words = ((total_num_values + 2047) / 2048) * 64 * num_bits_per_value;
+  const int64_t total_words = kGuardWords + stream_words + kGuardWords;
+  int rc = dev_alloc(c->words, (size_t)total_words * 4);
+  if (!rc) rc = dev_alloc(c->mv_off, off.size() * 4);
+  if (rc) { delete c; return rc; }
+  uint32_t* w = (uint32_t*)c->words.p;
+  if (hipMemset(w, 0, (size_t)total_words * 4) != hipSuccess ||
+      hipMemcpy(w + kGuardWords, raw, raw_bytes, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->mv_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    delete c;
+    return fail(PA_EHIP, "MV forward index upload failed");
+  }
+  if (launch_bswap_words(w + kGuardWords, (int64_t)((raw_bytes + 3) / 4), nullptr) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    delete c;
+    return fail(PA_EHIP, "bswap kernel failed");
+  }
+  rc = upload_dict(c, value_type, cardinality, dict_values, dict_hashes);
+  if (rc) { delete c; return rc; }
+  seg->bytes += c->words.n + c->mv_off.n + c->dict.n + c->hashes.n;
+  seg->cols[column_id] = c;
+  return PA_OK;
 }
 
 int pa_segment_add_raw_column(pa_segment* seg, int32_t column_id, int32_t value_type, const void* values) {
@@ -340,6 +405,8 @@ struct pa_query {
   DevBuf dq, dsegs, dplans;
   void* host_acc = nullptr;  // pinned copy of the accumulator block (small-block fetch path)
   int lane_major = 0;
+  int has_mv = 0;
+  int64_t last_matched = -1;  // numDocsScanned read by the last fetch
   std::vector<LmSegPlan> hplans;
   std::vector<DevBuf> owned;  // LUTs, remaps, HLL LUTs
   DevBuf acc;                 // all accumulator sections (unless the caller provided the block)
@@ -375,6 +442,7 @@ double leaf_selectivity(const pa_query* q, int si, int leaf, bool neg_literal) {
   const int kind = s.leaves[leaf].kind;
   auto it = q->segs[si]->cols.find(s.leaves[leaf].column_id);
   if (it == q->segs[si]->cols.end() || (kind != PA_LEAF_DICT_RANGE && kind != PA_LEAF_DICT_SET)) return 0.5;
+  // (MV leaves: 0.5 — they are always evaluated lazily, after every single-value clause)
   const int64_t card = std::max<int32_t>(1, it->second->cardinality);
   double sel;
   if (kind == PA_LEAF_DICT_RANGE) {
@@ -435,7 +503,7 @@ int pa_query_bind_segment(pa_query* q, int32_t index, const pa_segment* seg, con
   q->luts[index].assign(s.num_leaves, {});
   for (int l = 0; l < s.num_leaves; ++l) {
     const int kind = s.leaves[l].kind;
-    if (kind == PA_LEAF_DICT_SET) {
+    if (kind == PA_LEAF_DICT_SET || kind == PA_LEAF_MV_DICT_SET) {
       auto it = seg->cols.find(s.leaves[l].column_id);
       if (it == seg->cols.end()) return fail(PA_EINVAL, "leaf column missing in segment");
       if (!leaf_params[l].lut) return fail(PA_EINVAL, "DICT_SET leaf without lut");
@@ -470,11 +538,13 @@ int pa_query_prepare(pa_query* q) {
   std::vector<Clause> cnf;
   int rc = to_cnf(s, cnf);
   if (rc) return rc;
-  for (int l = 0; l < s.num_leaves; ++l) {
-    const int k = s.leaves[l].kind;
-    if (k == PA_LEAF_MV_DICT_RANGE || k == PA_LEAF_MV_DICT_SET)
-      return fail(PA_EUNSUPPORTED, "multi-value filter leaves are not implemented yet");
-  }
+  auto is_mv_leaf = [&](int leaf) {
+    const int k = s.leaves[leaf].kind;
+    return k == PA_LEAF_MV_DICT_RANGE || k == PA_LEAF_MV_DICT_SET;
+  };
+  std::vector<char> clause_mv(cnf.size(), 0);  // clauses with an MV literal are evaluated per doc (lazily), last
+  for (size_t c = 0; c < cnf.size(); ++c)
+    for (const Literal& lit : cnf[c]) clause_mv[c] |= is_mv_leaf(lit.leaf);
   // Clause order and late materialisation. Clauses are evaluated most selective first (estimated from the
   // matching-dictId fraction, i.e. assuming dictIds are equally frequent; only speed depends on the estimate).
   // The leading clauses whose expected survivors per wave tile exceed kLazyDensity run on whole staged tiles
@@ -493,11 +563,15 @@ int pa_query_prepare(pa_query* q) {
   }
   std::vector<size_t> order(cnf.size());
   for (size_t c = 0; c < cnf.size(); ++c) order[c] = c;
-  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return csel[a] < csel[b]; });
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+    if (clause_mv[a] != clause_mv[b]) return clause_mv[a] < clause_mv[b];
+    return csel[a] < csel[b];
+  });
   const bool no_lazy = (s.flags & (PA_QF_STAGE_ALL | PA_QF_NO_LAZY)) != 0;
   size_t eager_clauses = 0;
   double density = (double)kWTileDocs;  // expected surviving docs per wave tile
-  while (eager_clauses < cnf.size() && (no_lazy || eager_clauses == 0 || density > kLazyDensity))
+  while (eager_clauses < cnf.size() && !clause_mv[order[eager_clauses]] &&
+         (no_lazy || eager_clauses == 0 || density > kLazyDensity))
     density *= csel[order[eager_clauses++]];
   double post_density = density;
   for (size_t c = eager_clauses; c < cnf.size(); ++c) post_density *= csel[order[c]];
@@ -528,7 +602,7 @@ int pa_query_prepare(pa_query* q) {
   std::vector<int> agg_slot(s.num_aggs, 0);
   for (int a = 0; a < s.num_aggs; ++a) {
     const int t = s.aggs[a].type;
-    if (t < PA_AGG_COUNT || t > PA_AGG_DISTINCTCOUNTHLL) return fail(PA_EINVAL, "bad aggregation type");
+    if (t < PA_AGG_COUNT || t > PA_AGG_COUNT_MV) return fail(PA_EINVAL, "bad aggregation type");
     if (t == PA_AGG_COUNT) continue;
     agg_slot[a] = slot_of(q, s.aggs[a].column_id);
     if (agg_slot[a] < 0) return fail(PA_EUNSUPPORTED, "too many distinct columns in one query");
@@ -584,6 +658,7 @@ int pa_query_prepare(pa_query* q) {
       dc.vtype = c->vtype;
       dc.words = c->words.p ? (const uint32_t*)c->words.p + kGuardWords : nullptr;
       dc.raw = c->raw.p;
+      dc.mv_off = (const int32_t*)c->mv_off.p;
       dc.dict_i64 = (c->vtype == PA_INT || c->vtype == PA_LONG) ? (const int64_t*)c->dict.p : nullptr;
       dc.dict_f64 = (c->vtype == PA_FLOAT || c->vtype == PA_DOUBLE) ? (const double*)c->dict.p : nullptr;
       dc.lds_off = -1;
@@ -608,8 +683,11 @@ int pa_query_prepare(pa_query* q) {
       L.words = dc.words;
       L.raw = dc.raw;
       L.vtype = dc.vtype;
+      L.mv_off = dc.mv_off;
       if (L.kind == PA_LEAF_DICT_RANGE || L.kind == PA_LEAF_DICT_SET) {
         if (dc.kind != COL_SV_DICT) return fail(PA_EINVAL, "dictionary leaf on a non-dictionary column");
+      } else if (L.kind == PA_LEAF_MV_DICT_RANGE || L.kind == PA_LEAF_MV_DICT_SET) {
+        if (dc.kind != COL_MV_DICT) return fail(PA_EINVAL, "multi-value leaf on a single-value column");
       } else if (L.kind == PA_LEAF_RAW_RANGE) {
         if (dc.kind != COL_SV_RAW) return fail(PA_EINVAL, "raw leaf on a non-raw column");
       }
@@ -627,7 +705,12 @@ int pa_query_prepare(pa_query* q) {
         if (lo + span > (int64_t(1) << nb)) span = (int64_t(1) << nb) - lo;
         L.lo = (int32_t)(uint32_t)((uint64_t)lo << (32 - nb));
         L.span = (int32_t)(uint32_t)(((uint64_t)span << (32 - nb)) - 1);
-      } else if (L.kind == PA_LEAF_DICT_SET) {
+      } else if (L.kind == PA_LEAF_MV_DICT_RANGE) {  // plain bounds: lo <= id < lo + span
+        const int64_t card = (int64_t)seg->cols.at(s.leaves[lit.leaf].column_id)->cardinality;
+        const int64_t lo = std::max<int64_t>(0, p.lo), hi = std::min<int64_t>(p.hi, card);
+        L.lo = (int32_t)lo;
+        L.span = (int32_t)std::max<int64_t>(0, hi - lo);
+      } else if (L.kind == PA_LEAF_DICT_SET || L.kind == PA_LEAF_MV_DICT_SET) {
         const auto& lut = q->luts[si][lit.leaf];
         void* dp = nullptr;
         rc = upload_owned(q, lut.data(), lut.size() * 4, &dp);
@@ -643,7 +726,9 @@ int pa_query_prepare(pa_query* q) {
     // group-by remaps
     for (int j = 0; j < s.num_group_by; ++j) {
       const DevCol& dc = d.cols[gb_slot[j]];
-      if (dc.kind != COL_SV_DICT) return fail(PA_EUNSUPPORTED, "group-by on non-dictionary columns is not implemented yet");
+      if (dc.kind != COL_SV_DICT && dc.kind != COL_MV_DICT)
+        return fail(PA_EUNSUPPORTED, "group-by on non-dictionary columns is not implemented yet");
+      if (dc.kind == COL_MV_DICT) q->has_mv = 1;
       if (q->has_remap[si][j]) {
         void* dp = nullptr;
         rc = upload_owned(q, q->remaps[si][j].data(), q->remaps[si][j].size() * 4, &dp);
@@ -660,6 +745,12 @@ int pa_query_prepare(pa_query* q) {
       const pa_agg_spec& A = s.aggs[a];
       if (A.type == PA_AGG_COUNT) continue;
       const Column* c = seg->cols.at(A.column_id);
+      if (c->kind == COL_MV_DICT) q->has_mv = 1;
+      if (A.type == PA_AGG_COUNT_MV) {
+        if (c->kind != COL_MV_DICT) return fail(PA_EINVAL, "COUNT_MV on a single-value column");
+        agg_src[a] = SRC_INT;
+        continue;
+      }
       const int src = (c->vtype == PA_FLOAT || c->vtype == PA_DOUBLE) ? SRC_DOUBLE : (c->fits_int32 ? SRC_INT : SRC_LONG);
       if (A.type != PA_AGG_DISTINCTCOUNTHLL) {
         if (c->vtype == PA_STRING || c->vtype == PA_BYTES) return fail(PA_EINVAL, "numeric aggregation on a non-numeric column");
@@ -672,7 +763,7 @@ int pa_query_prepare(pa_query* q) {
           return fail(PA_EINVAL, "aggregation column type differs across segments");
         agg_src[a] = SRC_LONG;  // widen: some segment has values outside int32
       }
-      if (A.type == PA_AGG_DISTINCTCOUNTHLL && c->kind == COL_SV_DICT) {
+      if (A.type == PA_AGG_DISTINCTCOUNTHLL && (c->kind == COL_SV_DICT || c->kind == COL_MV_DICT)) {
         DevBuf b;
         rc = dev_alloc(b, (size_t)c->cardinality * 4);
         if (rc) return rc;
@@ -708,9 +799,11 @@ int pa_query_prepare(pa_query* q) {
       case PA_AGG_MIN: sec.push_back({PA_ACC_MIN_I64, K}); break;
       case PA_AGG_MAX: sec.push_back({PA_ACC_MAX_I64, K}); break;
       case PA_AGG_DISTINCTCOUNTHLL: sec.push_back({PA_ACC_HLL_U32, K << A.log2m}); break;
+      case PA_AGG_COUNT_MV: sec.push_back({PA_ACC_SUM_I64, K}); break;
     }
     q->agg_section[a] = (int)sec.size() - 1;
   }
+  sec.push_back({PA_ACC_DOCS_U64, 1});  // numDocsScanned (last section)
   size_t total = 0;
   std::vector<size_t> offs;
   for (auto& x : sec) {
@@ -872,6 +965,8 @@ int pa_query_prepare(pa_query* q) {
   q->plan_wg = plan.wg_per_cu;
   q->num_tiles = (uint64_t)first;
   h.count = (unsigned long long*)q->sections[0].ptr;
+  h.matched_docs = (unsigned long long*)q->sections.back().ptr;
+  h.has_mv = q->has_mv;
   h.lds_count_off = 0;
   h.lds_acc_bytes = q->strategy == STRAT_LDS ? (uint32_t)lds_acc : 0;
   for (int a = 0; a < s.num_aggs; ++a) {
@@ -987,6 +1082,7 @@ int pa_query_set_accumulator_buffer(pa_query* q, void* device_buffer, uint64_t b
   for (Section& s : q->sections) s.ptr = nb + ((char*)s.ptr - old);
   DevQuery& h = q->hq;
   h.count = (unsigned long long*)(nb + ((char*)h.count - old));
+  h.matched_docs = (unsigned long long*)(nb + ((char*)h.matched_docs - old));
   for (int a = 0; a < h.num_aggs; ++a) {
     if (q->agg_section[a] < 0) continue;
     void* p = q->sections[q->agg_section[a]].ptr;
@@ -1037,6 +1133,7 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
     const char* hb = (const char*)q->host_acc;
     auto hsec = [&](int sec) { return hb + ((char*)q->sections[sec].ptr - dbase); };
     const uint64_t* hc = (const uint64_t*)hsec(0);
+    q->last_matched = (int64_t)*(const uint64_t*)hsec((int)q->sections.size() - 1);
     int64_t n = 0;
     for (int64_t k = 0; k < K; ++k) {
       if (s.num_group_by != 0 && hc[k] == 0) continue;
@@ -1058,7 +1155,7 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
             const uint32_t* r = (const uint32_t*)sp + k * per;
             uint8_t* o = (uint8_t*)out_aggs[a] + n * per;
             for (int64_t j = 0; j < per; ++j) o[j] = (uint8_t)r[j];
-          } else if (A.type == PA_AGG_SUM) {
+          } else if (A.type == PA_AGG_SUM || A.type == PA_AGG_COUNT_MV) {
             const int64_t* hv = (const int64_t*)sp;
             if (src == SRC_LONG) outd[n] = (double)(((__int128)hv[2 * k + 1] << 32) + (__int128)(uint64_t)hv[2 * k]);
             else outd[n] = src == SRC_INT ? (double)hv[k] : ((const double*)sp)[k];
@@ -1074,8 +1171,11 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
     return n;
   }
   std::vector<uint64_t> cnt(K);
+  uint64_t md = 0;
   PA_HIP(hipMemcpyAsync(cnt.data(), q->sections[0].ptr, (size_t)K * 8, hipMemcpyDeviceToHost, st));
+  PA_HIP(hipMemcpyAsync(&md, q->sections.back().ptr, 8, hipMemcpyDeviceToHost, st));
   PA_HIP(hipStreamSynchronize(st));
+  q->last_matched = (int64_t)md;
   std::vector<int64_t> keys;
   if (s.num_group_by == 0) {
     keys.push_back(0);
@@ -1124,7 +1224,7 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
       uint8_t* o = (uint8_t*)out_aggs[a];
       const uint32_t* r = (const uint32_t*)host.data();
       for (int64_t i = 0; i < m * per; ++i) o[i] = (uint8_t)r[i];
-    } else if (A.type == PA_AGG_SUM) {
+    } else if (A.type == PA_AGG_SUM || A.type == PA_AGG_COUNT_MV) {
       const int64_t* hv = (const int64_t*)host.data();
       for (int64_t i = 0; i < m; ++i) {
         if (src == SRC_LONG) {  // exact 96-bit total, rounded once (the reference's double of the exact sum)
@@ -1170,6 +1270,8 @@ int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t*
 int32_t pa_query_num_eager_literals(const pa_query* q) { return q && q->prepared ? q->num_eager : -1; }
 
 int32_t pa_query_lane_major(const pa_query* q) { return q && q->prepared ? q->lane_major : -1; }
+
+int64_t pa_query_matched_docs(const pa_query* q) { return q && q->prepared ? q->last_matched : -1; }
 
 void pa_query_destroy(pa_query* q) { delete q; }
 

@@ -34,6 +34,7 @@ struct DevCol {
   const void* raw;           // SV raw: values
   const int64_t* dict_i64;   // INT/LONG dictionary
   const double* dict_f64;    // FLOAT/DOUBLE dictionary
+  const int32_t* mv_off;     // MV dict: value offset of every doc's first value [num_docs + 1]
   int32_t kind;              // ColKind
   int32_t nbits;
   int32_t vtype;             // PA_INT..PA_BYTES
@@ -54,6 +55,7 @@ struct DevLeaf {
   const uint32_t* lut;       // DICT_SET bitmap (device)
   const uint32_t* words;     // column copy: stream words
   const void* raw;           // column copy: raw values
+  const int32_t* mv_off;     // column copy: MV value offsets (MV leaves)
   int32_t vtype;             // column copy
   int32_t pad;
   int64_t ilo, ihi;
@@ -108,6 +110,9 @@ struct DevQuery {
                              // clauses) only on docs the eager clauses matched, straight from HBM
   int32_t dma_per_tile;      // LDS-DMA wave instructions per wave tile (max over segments)
   int32_t lane_major;        // 1: scan_lm_kernel (docs 32*lane + i of a tile), 0: scan_kernel (docs 64*i + lane)
+  int32_t has_mv;            // a group-by or aggregation column is multi-value: per-lane key expansion path
+  int32_t pad2;
+  unsigned long long* matched_docs;  // [1]: docs that passed the filter (numDocsScanned)
   int32_t staged_slots[kMaxSlots];
   int32_t gb_slot[PA_MAX_GROUP_BY];
   int64_t gb_stride[PA_MAX_GROUP_BY];

@@ -300,6 +300,97 @@ __device__ __forceinline__ void accumulate_step(const DevQuery* __restrict__ q, 
   }
 }
 
+// Value of an aggregation at value index `vi` of an MV dictionary column (SUMMV / MINMV / MAXMV / DISTINCTCOUNTHLLMV).
+__device__ __forceinline__ AggValue agg_value_mv(const DevAgg& A, int a, const DevSeg* __restrict__ seg,
+                                                 const DevCol& c, int64_t vi) {
+  AggValue out{0, 0.0};
+  const uint32_t id = decode_global(c.words, vi, c.nbits);
+  if (A.type == PA_AGG_DISTINCTCOUNTHLL) out.i = gp(seg->hll_lut[a])[id];
+  else if (A.src != SRC_DOUBLE) out.i = gp(c.dict_i64)[id];
+  else out.d = gp(c.dict_f64)[id];
+  return out;
+}
+
+template <int STRAT>
+__device__ __forceinline__ void update_one(const DevAgg& A, int64_t key, const AggValue& v, const Acc<STRAT>& acc) {
+  if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
+    acc.max_hll(A, key, (uint32_t)v.i);
+  } else if (A.type == PA_AGG_SUM) {
+    if (A.src == SRC_INT) {
+      acc.add_i64(A, key, v.i);
+    } else if (A.src == SRC_LONG) {
+      acc.add_i64(A, 2 * key, (int64_t)(uint32_t)v.i);
+      acc.add_i64(A, 2 * key + 1, v.i >> 32);
+    } else {
+      acc.add_f64(A, key, v.d);
+    }
+  } else {
+    const int64_t e = A.src != SRC_DOUBLE ? v.i : f64_order_encode(v.d);
+    if (A.type == PA_AGG_MIN) acc.min_i64(A, key, e);
+    else acc.max_i64(A, key, e);
+  }
+}
+
+// One matching doc of a query with a multi-value group-by or aggregation column, on its own lane (no wave
+// grouping): the doc expands into the cartesian product of its MV group-by values (DictionaryBasedGroupKeyGenerator
+// .getIntRawKeys; duplicates included, like the reference), and every key receives COUNT += 1 and every aggregation
+// — over all values of an MV aggregation column (aggregateGroupByMV / *MVAggregationFunction).
+template <int STRAT>
+__device__ void accumulate_doc_mv(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                  const uint32_t* img, int doc_local, int64_t doc, const Acc<STRAT>& acc) {
+  int64_t base_key = 0;
+  int nmv = 0;
+  int mv_gb[PA_MAX_GROUP_BY];
+  int32_t mv_s[PA_MAX_GROUP_BY], mv_n[PA_MAX_GROUP_BY];
+  int64_t combos = 1;
+  for (int j = 0; j < q->num_gb; ++j) {
+    const DevCol& c = seg->cols[q->gb_slot[j]];
+    if (c.kind == COL_MV_DICT) {
+      const int32_t s0 = gp(c.mv_off)[doc];
+      mv_gb[nmv] = j;
+      mv_s[nmv] = s0;
+      mv_n[nmv] = gp(c.mv_off)[doc + 1] - s0;
+      combos *= mv_n[nmv];
+      ++nmv;
+    } else {
+      uint32_t id = decode_dict_id(c, img, doc_local, doc);
+      const int32_t* rm = seg->remap[j];
+      if (rm != nullptr) id = (uint32_t)gp(rm)[id];
+      base_key += (int64_t)id * q->gb_stride[j];
+    }
+  }
+  for (int64_t cb = 0; cb < combos; ++cb) {
+    int64_t key = base_key;
+    int64_t rem = cb;
+    for (int t = 0; t < nmv; ++t) {
+      const int j = mv_gb[t];
+      const DevCol& c = seg->cols[q->gb_slot[j]];
+      const int64_t digit = rem % mv_n[t];
+      rem /= mv_n[t];
+      uint32_t id = decode_global(c.words, mv_s[t] + digit, c.nbits);
+      const int32_t* rm = seg->remap[j];
+      if (rm != nullptr) id = (uint32_t)gp(rm)[id];
+      key += (int64_t)id * q->gb_stride[j];
+    }
+    acc.add_count(key, 1u);
+    for (int a = 0; a < q->num_aggs; ++a) {
+      const DevAgg& A = q->aggs[a];
+      if (A.type == PA_AGG_COUNT) continue;
+      const DevCol& c = seg->cols[A.slot];
+      if (c.kind == COL_MV_DICT) {
+        const int32_t v0 = gp(c.mv_off)[doc], v1 = gp(c.mv_off)[doc + 1];
+        if (A.type == PA_AGG_COUNT_MV) {
+          acc.add_i64(A, key, (int64_t)(v1 - v0));
+          continue;
+        }
+        for (int32_t vi = v0; vi < v1; ++vi) update_one<STRAT>(A, key, agg_value_mv(A, a, seg, c, vi), acc);
+      } else {
+        update_one<STRAT>(A, key, agg_value(A, a, seg, img, doc_local, doc), acc);
+      }
+    }
+  }
+}
+
 // Match word of one leaf over a whole wave tile: bit i of lane l <=> doc 64*i + l of the tile matches.
 // Leaf parameters are loaded once per tile; the 32 decodes are independent, so the LDS reads pipeline.
 template <int STEPS>
@@ -408,7 +499,17 @@ __device__ __forceinline__ uint32_t leaf_bits(const DevLeaf& L, const uint32_t* 
 // docs). DICT_RANGE bounds are stored MSB-aligned for leaf_bits; lo = lo' >> (32-nb), span = (hi' + 1) >> (32-nb).
 __device__ __forceinline__ bool leaf_match_doc(const DevLeaf& L, int64_t doc) {
   bool m;
-  if (L.kind == PA_LEAF_DICT_RANGE || L.kind == PA_LEAF_DICT_SET) {
+  if (L.kind == PA_LEAF_MV_DICT_RANGE || L.kind == PA_LEAF_MV_DICT_SET) {
+    // MVScanDocIdIterator + applyMV: ANY value in the leaf's set (exclusive predicates arrive negated, so that is
+    // NOT ANY == ALL values outside the set). Plain (not MSB-aligned) bounds for MV ranges.
+    const int32_t v0 = gp(L.mv_off)[doc], v1 = gp(L.mv_off)[doc + 1];
+    m = false;
+    for (int32_t v = v0; v < v1 && !m; ++v) {
+      const uint32_t id = decode_global(L.words, v, L.nbits);
+      m = L.kind == PA_LEAF_MV_DICT_RANGE ? (id - (uint32_t)L.lo) < (uint32_t)L.span
+                                          : ((gp(L.lut)[id >> 5] >> (id & 31u)) & 1u) != 0;
+    }
+  } else if (L.kind == PA_LEAF_DICT_RANGE || L.kind == PA_LEAF_DICT_SET) {
     const uint32_t id = decode_global(L.words, doc, L.nbits);
     if (L.kind == PA_LEAF_DICT_RANGE) {
       const int sh = 32 - L.nbits;
@@ -431,13 +532,17 @@ __device__ __forceinline__ bool leaf_match_doc(const DevLeaf& L, int64_t doc) {
 
 template <int STRAT, int STEPS>
 __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
-                                             int64_t wt, const uint32_t* img, int lane, const Acc<STRAT>& acc) {
+                                             int64_t wt, const uint32_t* img, int lane, const Acc<STRAT>& acc,
+                                             uint32_t& matched) {
   const int64_t doc_base = wt * (STEPS * kWave);
   // docs of this tile owned by the lane: 64*i + lane < rem
   const int64_t rem = (int64_t)seg->num_docs - doc_base;
+  // bit i <=> step i holds a doc of this segment (only the low STEPS bits: a negated leaf sets the others, and the
+  // matched-doc count must not see them)
+  constexpr uint32_t kFull = STEPS == 32 ? 0xffffffffu : ((1u << STEPS) - 1u);
   uint32_t valid;
   if (rem >= (STEPS * kWave)) {
-    valid = 0xffffffffu;
+    valid = kFull;
   } else {
     const int64_t n = rem > lane ? (rem - lane + kWave - 1) / kWave : 0;  // steps with a valid doc for this lane
     valid = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
@@ -476,11 +581,17 @@ __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, con
     }
     if (__ballot(m != 0) == 0) return;
   }
-  for (int i = 0; i < STEPS; ++i) {
-    const uint64_t sm = __ballot((m >> i) & 1u);
-    if (sm == 0) continue;
-    const int doc_local = i * kWave + lane;
-    accumulate_step<STRAT>(q, seg, img, doc_local, doc_base + doc_local, sm, lane, acc);
+  matched += (uint32_t)__builtin_popcount(m);
+  if (q->has_mv) {
+    for (int i = 0; i < STEPS; ++i)
+      if ((m >> i) & 1u) accumulate_doc_mv<STRAT>(q, seg, img, i * kWave + lane, doc_base + i * kWave + lane, acc);
+  } else {
+    for (int i = 0; i < STEPS; ++i) {
+      const uint64_t sm = __ballot((m >> i) & 1u);
+      if (sm == 0) continue;
+      const int doc_local = i * kWave + lane;
+      accumulate_step<STRAT>(q, seg, img, doc_local, doc_base + doc_local, sm, lane, acc);
+    }
   }
   // Leave no compiler-visible VMEM op pending past a tile with matches (a compiler-understood wait): otherwise the
   // waitcnt pass guards the next tile's LDS decode with vmcnt(0) on EVERY tile, draining the DMA ring.
@@ -576,7 +687,7 @@ __device__ __forceinline__ void stage_tile_lm(uint32_t ip, int64_t wt, uint32_t 
 template <int STRAT>
 __device__ __forceinline__ void process_tile_lm(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
                                                 uint32_t pp, int64_t wt, const uint32_t* img, uint32_t img_lds,
-                                                int lane, const Acc<STRAT>& acc) {
+                                                int lane, const Acc<STRAT>& acc, uint32_t& matched) {
   const int64_t doc_base = wt * kWTileDocs;
   const int64_t rem = (int64_t)(int32_t)rl(pp, 2) - doc_base;
   uint32_t valid = 0xffffffffu;
@@ -622,11 +733,17 @@ __device__ __forceinline__ void process_tile_lm(const DevQuery* __restrict__ q, 
     }
     if (__ballot(m != 0) == 0) return;
   }
-  for (int i = 0; i < 32; ++i) {
-    const uint64_t sm = __ballot((m >> i) & 1u);
-    if (sm == 0) continue;
-    const int doc_local = 32 * lane + i;
-    accumulate_step<STRAT>(q, seg, img, doc_local, doc_base + doc_local, sm, lane, acc);
+  matched += (uint32_t)__builtin_popcount(m);
+  if (q->has_mv) {
+    for (int i = 0; i < 32; ++i)
+      if ((m >> i) & 1u) accumulate_doc_mv<STRAT>(q, seg, img, 32 * lane + i, doc_base + 32 * lane + i, acc);
+  } else {
+    for (int i = 0; i < 32; ++i) {
+      const uint64_t sm = __ballot((m >> i) & 1u);
+      if (sm == 0) continue;
+      const int doc_local = 32 * lane + i;
+      accumulate_step<STRAT>(q, seg, img, doc_local, doc_base + doc_local, sm, lane, acc);
+    }
   }
   __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // vmcnt(0): see process_tile
 }
@@ -731,7 +848,7 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
         for (int64_t k = threadIdx.x; k < (K << A.log2m); k += kWGSize) r[k] = 0;
       } else {
         int64_t* r = (int64_t*)(lds_acc + A.lds_off);
-        const int64_t init = A.type == PA_AGG_MIN ? INT64_MAX : (A.type == PA_AGG_MAX ? INT64_MIN : 0);
+        const int64_t init = A.type == PA_AGG_MIN ? INT64_MAX : (A.type == PA_AGG_MAX ? INT64_MIN : 0);  // SUM, COUNT_MV: 0
         const int64_t n = (A.type == PA_AGG_SUM && A.src == SRC_LONG) ? 2 * K : K;
         for (int64_t k = threadIdx.x; k < n; k += kWGSize) r[k] = init;  // SUM(double) 0.0 == all-zero bits
       }
@@ -739,6 +856,7 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
     __syncthreads();
   }
 
+  uint32_t matched = 0;  // docs of this lane that passed the filter (numDocsScanned)
   const int64_t T = q->total_wtiles;
   const int64_t W = (int64_t)gridDim.x * kWavesPerWG;
   const int64_t gw = (int64_t)blockIdx.x * kWavesPerWG + wave;
@@ -789,8 +907,8 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
         if (LM && dbg > 1) {
           debug_tile_lm(dbg, pp, ring_lds + 4u * slot_off, lane);
         } else if (!stream_only) {
-          if constexpr (LM) process_tile_lm<STRAT>(q, seg, pp, t - seg_first, ring + slot_off, ring_lds + 4u * slot_off, lane, acc);
-          else process_tile<STRAT, STEPS>(q, seg, t - seg_first, ring + slot_off, lane, acc);
+          if constexpr (LM) process_tile_lm<STRAT>(q, seg, pp, t - seg_first, ring + slot_off, ring_lds + 4u * slot_off, lane, acc, matched);
+          else process_tile<STRAT, STEPS>(q, seg, t - seg_first, ring + slot_off, lane, acc, matched);
         }
         pslot = pslot + 1 == R ? 0 : pslot + 1;
       }
@@ -801,6 +919,10 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
     }
   }
 
+  {
+    const int64_t wm = wave_sum_i64((int64_t)matched);
+    if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)wm, RLX);
+  }
   if (STRAT == STRAT_LDS) {
     __syncthreads();
     const int64_t K = q->num_keys;
@@ -822,6 +944,9 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
             } else {
               __hip_atomic_fetch_add(gp(A.acc_f64) + k, ((const double*)(lds_acc + A.lds_off))[k], RLX);
             }
+            break;
+          case PA_AGG_COUNT_MV:
+            __hip_atomic_fetch_add(gp((unsigned long long*)A.acc_i64) + k, ((const unsigned long long*)(lds_acc + A.lds_off))[k], RLX);
             break;
           case PA_AGG_MIN: __hip_atomic_fetch_min(gp((long long*)A.acc_i64) + k, ((const long long*)(lds_acc + A.lds_off))[k], RLX); break;
           case PA_AGG_MAX: __hip_atomic_fetch_max(gp((long long*)A.acc_i64) + k, ((const long long*)(lds_acc + A.lds_off))[k], RLX); break;

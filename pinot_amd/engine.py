@@ -64,10 +64,17 @@ class GpuSegment:
                 dv = None
                 hashes = np.array([hash_value(v, "STRING") for v in col.dictionary.tolist()], dtype=np.int32)
             fwd = np.ascontiguousarray(col.fwd_bytes, dtype=np.uint8)
-            L.check(lib.pa_segment_add_sv_dict_column(
-                self.handle, cid, fwd.ctypes.data, fwd.nbytes, col.num_bits, col.cardinality, vt,
-                None if dv is None else dv.ctypes.data, None if hashes is None else hashes.ctypes.data),
-                "pa_segment_add_sv_dict_column(%s)" % name)
+            if col.single_value:
+                L.check(lib.pa_segment_add_sv_dict_column(
+                    self.handle, cid, fwd.ctypes.data, fwd.nbytes, col.num_bits, col.cardinality, vt,
+                    None if dv is None else dv.ctypes.data, None if hashes is None else hashes.ctypes.data),
+                    "pa_segment_add_sv_dict_column(%s)" % name)
+            else:
+                L.check(lib.pa_segment_add_mv_dict_column(
+                    self.handle, cid, fwd.ctypes.data, fwd.nbytes, col.num_bits, col.cardinality,
+                    col.total_num_values, vt, None if dv is None else dv.ctypes.data,
+                    None if hashes is None else hashes.ctypes.data),
+                    "pa_segment_add_mv_dict_column(%s)" % name)
         else:
             raw = np.ascontiguousarray(col.raw_values)
             L.check(lib.pa_segment_add_raw_column(self.handle, cid, vt, raw.ctypes.data),
@@ -143,25 +150,37 @@ class GpuQueryExecutor:
         seg0 = self.segs[0]
         spec = L.QuerySpec()
 
-        # aggregations -> GPU accumulators (AVG = SUM + group count)
+        # aggregations -> GPU accumulators (AVG = SUM + group count, AVGMV = SUM + COUNT_MV over the MV column; the
+        # *MV forms aggregate every value of a multi-value column)
         self.pa_aggs = []
         self.agg_map = []
-        for a in q.aggregations:
-            if a.function == "COUNT":
-                key = (L.PA_AGG_COUNT, -1, 0)
-            elif a.function in ("SUM", "AVG"):
-                key = (L.PA_AGG_SUM, ids[a.column], 0)
-            elif a.function == "MIN":
-                key = (L.PA_AGG_MIN, ids[a.column], 0)
-            elif a.function == "MAX":
-                key = (L.PA_AGG_MAX, ids[a.column], 0)
-            elif a.function == "DISTINCTCOUNTHLL":
-                key = (L.PA_AGG_DISTINCTCOUNTHLL, ids[a.column], a.log2m)
-            else:
-                raise UnsupportedQuery("aggregation %s" % a.function)
+
+        def acc_index(key):
             if key not in self.pa_aggs:
                 self.pa_aggs.append(key)
-            self.agg_map.append(self.pa_aggs.index(key))
+            return self.pa_aggs.index(key)
+
+        for a in q.aggregations:
+            fn = a.function
+            if fn.endswith("MV") and seg0.column(a.column).single_value:
+                raise UnsupportedQuery("%s on single-value column %s" % (fn, a.column))
+            if fn == "COUNT":
+                self.agg_map.append(acc_index((L.PA_AGG_COUNT, -1, 0)))
+            elif fn == "AVGMV":
+                self.agg_map.append((acc_index((L.PA_AGG_SUM, ids[a.column], 0)),
+                                     acc_index((L.PA_AGG_COUNT_MV, ids[a.column], 0))))
+            elif fn == "COUNTMV":
+                self.agg_map.append(acc_index((L.PA_AGG_COUNT_MV, ids[a.column], 0)))
+            elif fn in ("SUM", "AVG", "SUMMV"):
+                self.agg_map.append(acc_index((L.PA_AGG_SUM, ids[a.column], 0)))
+            elif fn in ("MIN", "MINMV"):
+                self.agg_map.append(acc_index((L.PA_AGG_MIN, ids[a.column], 0)))
+            elif fn in ("MAX", "MAXMV"):
+                self.agg_map.append(acc_index((L.PA_AGG_MAX, ids[a.column], 0)))
+            elif fn in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV"):
+                self.agg_map.append(acc_index((L.PA_AGG_DISTINCTCOUNTHLL, ids[a.column], a.log2m)))
+            else:
+                raise UnsupportedQuery("aggregation %s" % fn)
         if len(self.pa_aggs) > L.PA_MAX_AGGS:
             raise UnsupportedQuery("too many aggregations")
         spec.num_aggs = len(self.pa_aggs)
@@ -188,6 +207,8 @@ class GpuQueryExecutor:
         for li, pred in enumerate(leaves):
             kinds = {ps[li].kind for ps in per_seg}
             kind = L.PA_LEAF_DICT_SET if L.PA_LEAF_DICT_SET in kinds else kinds.pop()
+            if not seg0.column(pred.column).single_value:  # MVScanDocIdIterator: ANY value (ALL for NOT IN / !=)
+                kind = {L.PA_LEAF_DICT_RANGE: L.PA_LEAF_MV_DICT_RANGE, L.PA_LEAF_DICT_SET: L.PA_LEAF_MV_DICT_SET}[kind]
             spec.leaves[li].column_id = ids[pred.column]
             spec.leaves[li].kind = kind
         spec.num_ops = len(ops)
@@ -231,7 +252,8 @@ class GpuQueryExecutor:
                 prod = 1
                 for name in q.group_by:
                     prod *= seg.column(name).cardinality
-                if min(prod, seg.num_docs) > lim:
+                mv = any(not seg.column(name).single_value for name in q.group_by)
+                if (prod if mv else min(prod, seg.num_docs)) > lim:
                     self.num_groups_limit_may_bind = True
             if self.num_groups_limit_may_bind and self.enforce_num_groups_limit:
                 raise UnsupportedQuery("numGroupsLimit=%d may bind for this segment set (first-seen group trimming is "
@@ -246,7 +268,7 @@ class GpuQueryExecutor:
                 lp = arr[li]
                 if isinstance(p, P.DictLeaf):
                     lp.negate = int(p.negate)
-                    if spec.leaves[li].kind == L.PA_LEAF_DICT_SET:
+                    if spec.leaves[li].kind in (L.PA_LEAF_DICT_SET, L.PA_LEAF_MV_DICT_SET):
                         ids_ = p.ids if p.ids is not None else np.arange(p.lo, p.hi, dtype=np.int32)
                         lut = P.DictLeaf(L.PA_LEAF_DICT_SET, ids=ids_).lut_words(self.segs[si].column(leaves[li].column).cardinality)
                         self._keep.append(lut)
@@ -324,7 +346,7 @@ class GpuQueryExecutor:
             cap = n
         res = IntermediateResult(list(q.aggregations), list(q.group_by))
         res.num_total_docs = sum(s.num_docs for s in self.segs)
-        res.num_docs_scanned = int(counts[:n].sum())
+        res.num_docs_scanned = int(lib.pa_query_matched_docs(self.handle))
         # decode key ids -> values
         key_cols = []
         for j, gd in enumerate(self.global_dicts):
@@ -333,12 +355,16 @@ class GpuQueryExecutor:
         for r in range(n):
             vals = []
             for a, pi in zip(q.aggregations, self.agg_map):
-                t, _, log2m = self.pa_aggs[pi]
                 if a.function == "COUNT":
                     vals.append(int(counts[r]))
                 elif a.function == "AVG":
                     vals.append(AvgPair(float(outs[pi][r]), int(counts[r])))
-                elif a.function == "DISTINCTCOUNTHLL":
+                elif a.function == "AVGMV":
+                    vals.append(AvgPair(float(outs[pi[0]][r]), int(outs[pi[1]][r])))
+                elif a.function == "COUNTMV":
+                    vals.append(int(outs[pi][r]))
+                elif a.function in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV"):
+                    log2m = self.pa_aggs[pi][2]
                     m = 1 << log2m
                     vals.append(HyperLogLog(log2m, outs[pi][r * m:(r + 1) * m]))
                 else:

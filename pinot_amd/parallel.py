@@ -18,6 +18,7 @@ SECTION_OP = {
     L.PA_ACC_MIN_I64: dist.ReduceOp.MIN,
     L.PA_ACC_MAX_I64: dist.ReduceOp.MAX,
     L.PA_ACC_HLL_U32: dist.ReduceOp.MAX,
+    L.PA_ACC_DOCS_U64: dist.ReduceOp.SUM,
 }
 SECTION_DTYPE = {
     L.PA_ACC_COUNT_U64: torch.int64,
@@ -27,6 +28,7 @@ SECTION_DTYPE = {
     L.PA_ACC_MIN_I64: torch.int64,
     L.PA_ACC_MAX_I64: torch.int64,
     L.PA_ACC_HLL_U32: torch.int32,  # registers are < 32: signed max == unsigned max
+    L.PA_ACC_DOCS_U64: torch.int64,
 }
 
 

@@ -72,9 +72,20 @@ class Not:
 PREDICATES = (EqPredicate, NotEqPredicate, InPredicate, NotInPredicate, RangePredicate)
 
 
+# AggregationFunctionType names the hot path runs: single-value functions and their multi-value (*MV) forms, which
+# aggregate every value of a multi-value column (SumMVAggregationFunction, CountMVAggregationFunction, ...)
+SUPPORTED_FUNCTIONS = ("SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNTHLL",
+                       "COUNTMV", "SUMMV", "MINMV", "MAXMV", "AVGMV", "DISTINCTCOUNTHLLMV")
+
+
+def base_function(fn):
+    """Merge/extract semantics of a function: the *MV forms behave like their single-value form, COUNTMV like COUNT."""
+    return fn[:-2] if fn.endswith("MV") else fn
+
+
 @dataclass(frozen=True)
 class Aggregation:
-    function: str              # COUNT SUM MIN MAX AVG DISTINCTCOUNTHLL
+    function: str              # COUNT SUM MIN MAX AVG DISTINCTCOUNTHLL and the *MV forms
     column: Optional[str] = None
     log2m: int = DEFAULT_HLL_LOG2M
 
@@ -213,7 +224,7 @@ class _Parser:
         if self.op(","):
             log2m = int(self.literal())
         self.expect_op(")")
-        if fn not in ("SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNTHLL"):
+        if fn not in SUPPORTED_FUNCTIONS:
             raise ValueError("unsupported aggregation %s" % fn)
         return Aggregation(fn, col, log2m)
 

@@ -16,6 +16,7 @@ from .hll import HyperLogLog
 
 
 def merge_value(fn, a, b):
+    fn = Q.base_function(fn)
     if fn in ("COUNT", "SUM"):
         return a + b
     if fn == "MIN":
@@ -30,6 +31,7 @@ def merge_value(fn, a, b):
 
 
 def final_value(fn, v):
+    fn = Q.base_function(fn)
     if fn == "AVG":
         return v.sum / v.count if v.count else -math.inf
     if fn == "DISTINCTCOUNTHLL":

@@ -5,6 +5,9 @@ Mirrors the parts of SegmentIndexCreationDriverImpl the scan path depends on:
   * dictionary-encoded SV forward index: FixedBitSVForwardIndexWriter bytes, i.e. PinotDataBitSet.writeInt
     layout (pinot-segment-local/.../io/util/PinotDataBitSet.java:143) — value i at stream bits
     [i*nb, (i+1)*nb), MSB-first, nb = PinotDataBitSet.getNumBitsPerValue(cardinality - 1) (:61),
+  * dictionary-encoded MV forward index: FixedBitMVForwardIndexWriter bytes
+    (pinot-segment-local/.../creator/impl/fwd/FixedBitMVForwardIndexWriter.java:70-140): big-endian int32 chunk
+    offsets | row-start bitmap (one bit per value, MSB-first) | the dictIds of all rows bit-packed back to back,
   * raw (no-dictionary) SV columns: the decoded fixed-width values.
 """
 from dataclasses import dataclass, field
@@ -58,6 +61,24 @@ class Column:
     fwd_bytes: Optional[np.ndarray] = None    # uint8, FixedBitSVForwardIndexWriter layout
     raw_values: Optional[np.ndarray] = None   # no-dictionary columns
     is_sorted: bool = False
+    single_value: bool = True
+    total_num_values: int = 0                 # MV: values over all docs (FixedBitMVForwardIndexWriter totalNumValues)
+    max_num_multi_values: int = 0             # MV: longest row
+
+    def mv_layout(self, num_docs):
+        """MV forward index sections: (docs per chunk, chunk-offset bytes, bitmap offset, raw-data offset)."""
+        dpc, nchunks = mv_docs_per_chunk(num_docs, self.total_num_values)
+        header = nchunks * 4
+        bitmap = (self.total_num_values + 7) // 8
+        return dpc, header, header, header + bitmap
+
+    def mv_dict_ids(self, num_docs):
+        """Per-doc dictId arrays decoded from the MV forward index bytes (vectorised test helper)."""
+        _, _, boff, roff = self.mv_layout(num_docs)
+        tv = self.total_num_values
+        starts = np.flatnonzero(np.unpackbits(self.fwd_bytes[boff:roff])[:tv])
+        ids = unpack_bits(self.fwd_bytes[roff:], tv, self.num_bits)
+        return np.split(ids, starts[1:])
 
     @property
     def is_numeric(self):
@@ -95,6 +116,50 @@ def _coerce(values, data_type):
     return np.asarray(values, dtype=_NP[data_type])
 
 
+def mv_docs_per_chunk(num_docs, total_num_values):
+    """FixedBitMVForwardIndexWriter.java:72-74: averageValuesPerDoc = totalNumValues / numDocs (int division, widened to
+    float), docsPerChunk = (int) Math.ceil(2048 / averageValuesPerDoc) in float arithmetic; returns (docsPerChunk, numChunks)."""
+    if num_docs == 0:
+        return 1, 0
+    avg = np.float32(total_num_values // num_docs)
+    dpc = int(np.ceil(np.float64(np.float32(2048) / avg)))
+    return dpc, (num_docs + dpc - 1) // dpc
+
+
+def write_mv_forward_index(ids_per_doc, num_bits) -> np.ndarray:
+    """FixedBitMVForwardIndexWriter byte layout for per-doc dictId arrays (every row holds >= 1 value)."""
+    n = len(ids_per_doc)
+    lengths = np.array([len(x) for x in ids_per_doc], dtype=np.int64)
+    if n and lengths.min() < 1:
+        raise ValueError("every multi-value row must hold at least one value (Pinot stores the default null value)")
+    total = int(lengths.sum())
+    dpc, nchunks = mv_docs_per_chunk(n, total)
+    starts = np.concatenate([[0], np.cumsum(lengths)[:-1]]).astype(np.int64) if n else np.zeros(0, np.int64)
+    header = starts[::dpc][:nchunks].astype(">i4").tobytes()
+    bits = np.zeros(((total + 7) // 8) * 8, dtype=np.uint8)
+    bits[starts] = 1
+    bitmap = np.packbits(bits)
+    flat = np.concatenate(ids_per_doc).astype(np.uint32) if n else np.zeros(0, np.uint32)
+    raw = pack_bits(flat, num_bits)
+    return np.concatenate([np.frombuffer(header, dtype=np.uint8), bitmap, raw]).astype(np.uint8)
+
+
+def build_mv_column(name, rows, data_type) -> Column:
+    """Dictionary-encoded multi-value column from per-doc value arrays."""
+    rows = [_coerce(np.atleast_1d(r), data_type) for r in rows]
+    col = Column(name=name, data_type=data_type, single_value=False)
+    flat = np.concatenate(rows) if rows else _coerce([], data_type)
+    dictionary = np.unique(flat)
+    col.dictionary = dictionary
+    col.cardinality = int(len(dictionary))
+    col.num_bits = num_bits_per_value(max(col.cardinality - 1, 0))
+    ids = [np.searchsorted(dictionary, r).astype(np.uint32) for r in rows]
+    col.total_num_values = int(len(flat))
+    col.max_num_multi_values = int(max((len(r) for r in rows), default=0))
+    col.fwd_bytes = write_mv_forward_index(ids, col.num_bits)
+    return col
+
+
 def build_column(name, values, data_type, has_dictionary=True) -> Column:
     values = _coerce(values, data_type)
     col = Column(name=name, data_type=data_type, has_dictionary=has_dictionary)
@@ -113,8 +178,10 @@ def build_column(name, values, data_type, has_dictionary=True) -> Column:
     return col
 
 
-def create_segment(name, data: Dict[str, np.ndarray], schema: Dict[str, str], no_dictionary_columns=()) -> Segment:
-    """Builds an immutable segment from column arrays. schema: column -> data type."""
+def create_segment(name, data: Dict[str, np.ndarray], schema: Dict[str, str], no_dictionary_columns=(),
+                   multi_value_columns=()) -> Segment:
+    """Builds an immutable segment from column arrays. schema: column -> data type; a multi-value column's data is a
+    sequence of per-doc value arrays."""
     n = None
     seg = None
     for col_name, dtype in schema.items():
@@ -124,7 +191,10 @@ def create_segment(name, data: Dict[str, np.ndarray], schema: Dict[str, str], no
             seg = Segment(name=name, num_docs=n)
         elif len(vals) != n:
             raise ValueError("column %s has %d rows, expected %d" % (col_name, len(vals), n))
-        seg.columns[col_name] = build_column(col_name, vals, dtype, col_name not in no_dictionary_columns)
+        if col_name in multi_value_columns:
+            seg.columns[col_name] = build_mv_column(col_name, vals, dtype)
+        else:
+            seg.columns[col_name] = build_column(col_name, vals, dtype, col_name not in no_dictionary_columns)
     if seg is None:
         seg = Segment(name=name, num_docs=0)
     return seg
