@@ -404,6 +404,8 @@ struct pa_query {
   std::vector<DevSeg> hsegs;
   DevBuf dq, dsegs, dplans;
   void* host_acc = nullptr;  // pinned copy of the accumulator block (small-block fetch path)
+  DevBuf fetch_blocks, fetch_stage;  // large-key fetch: per-block counts / compacted rows
+  void* fetch_host = nullptr;        // pinned copy of the compacted rows
   int lane_major = 0;
   int has_mv = 0;
   int64_t last_matched = -1;  // numDocsScanned read by the last fetch
@@ -419,6 +421,9 @@ struct pa_query {
     dev_free(dsegs);
     dev_free(dplans);
     if (host_acc) (void)hipHostFree(host_acc);
+    dev_free(fetch_blocks);
+    dev_free(fetch_stage);
+    if (fetch_host) (void)hipHostFree(fetch_host);
     dev_free(acc);
     for (auto& b : owned) dev_free(b);
   }
@@ -848,11 +853,11 @@ int pa_query_prepare(pa_query* q) {
   }
   for (int si = 0; si < q->nseg && lm; ++si)
     if (q->hsegs[si].num_staged > kLmStaged) lm = false;
-  auto plan_for = [&](int strat) {
+  auto plan_for = [&](int strat, bool use_lm) {
     const bool lds_strategy = strat == STRAT_LDS;
     Plan best;
     for (int steps : {32, 16}) {
-      if (lm && steps != 32) continue;
+      if (use_lm && steps != 32) continue;
       if ((s.flags & PA_QF_STEPS16) && steps != 16) continue;
       if ((s.flags & PA_QF_STEPS32) && steps != 32) continue;
       int img_dw = kGuardWords, dma = 0;
@@ -881,8 +886,8 @@ int pa_query_prepare(pa_query* q) {
         if (ring < 2) continue;
         const size_t lds = acc_b + (size_t)kWavesPerWG * ring * img_bytes;
         int resident = 0;
-        if (set_scan_lds_limit(strat, steps, lm, (int)kLdsBudget) != hipSuccess ||
-            scan_occupancy(strat, steps, lm, (int)lds, &resident) != hipSuccess)
+        if (set_scan_lds_limit(strat, steps, use_lm, (int)kLdsBudget) != hipSuccess ||
+            scan_occupancy(strat, steps, use_lm, (int)lds, &resident) != hipSuccess)
           resident = wg;  // no device to ask (planning only): trust the LDS arithmetic
         if (resident < wg) continue;
         const double inflight = (double)wg * kWavesPerWG * (ring - 1) * img_bytes;
@@ -895,13 +900,28 @@ int pa_query_prepare(pa_query* q) {
   // LDS-privatised accumulators when many docs are expected to reach them (and the key space fits); otherwise the
   // LDS goes to tile rings (more resident waves) and the rare survivors update global accumulators directly.
   const bool dense = !has_filter || post_density >= 1.0;
+  // Tile layout: lane-major when it applies, except for dense queries on global accumulators, whose per-doc atomics
+  // want the most resident waves (measured, tools/bench_configs.py highcard): there the step-major plan wins when it
+  // fits more workgroups per CU.
+  auto plan_pick = [&](int strat) {
+    if (!lm) return plan_for(strat, false);
+    Plan a = plan_for(strat, true);
+    if (strat == STRAT_GLOBAL && dense) {
+      Plan b = plan_for(strat, false);
+      if (b.score >= 0 && b.wg_per_cu > a.wg_per_cu) {
+        lm = false;
+        return b;
+      }
+    }
+    return a;
+  };
   Plan plan;
   q->strategy = STRAT_GLOBAL;
   if (!(s.flags & PA_QF_FORCE_GLOBAL) && lds_acc <= 64 * 1024 && (dense || (s.flags & PA_QF_FORCE_LDS))) {
-    plan = plan_for(STRAT_LDS);
+    plan = plan_pick(STRAT_LDS);
     if (plan.score >= 0) q->strategy = STRAT_LDS;
   }
-  if (q->strategy == STRAT_GLOBAL) plan = plan_for(STRAT_GLOBAL);
+  if (q->strategy == STRAT_GLOBAL) plan = plan_pick(STRAT_GLOBAL);
   if (plan.score < 0) return fail(PA_EUNSUPPORTED, "staged columns too wide for the LDS tile ring");
   q->lds_bytes = (int)plan.lds;
   q->steps = plan.steps;
@@ -1118,6 +1138,51 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   hipStream_t st = (hipStream_t)stream;
   const pa_query_spec& s = q->spec;
   const int64_t K = q->num_keys;
+  const bool grouped = s.num_group_by != 0;
+  char* dbase = (char*)(q->external_acc ? q->external_acc : q->acc.p);
+
+  // Decodes `nrows` host rows into the caller's arrays: row r has key key_of(r), count hc[r] and the aggregation
+  // section rows at sec(section)[r * per]. Rows with a zero count are skipped when `skip_empty`.
+  auto decode = [&](int64_t nrows, const uint64_t* hc, const std::function<const char*(int)>& sec,
+                    const std::function<int64_t(int64_t)>& key_of, bool skip_empty) -> int64_t {
+    int64_t n = 0;
+    for (int64_t r = 0; r < nrows; ++r) {
+      if (skip_empty && hc[r] == 0) continue;
+      if (n < capacity) {
+        if (out_keys) out_keys[n] = key_of(r);
+        if (out_counts) out_counts[n] = (int64_t)hc[r];
+        for (int a = 0; a < s.num_aggs; ++a) {
+          if (!out_aggs || !out_aggs[a]) continue;
+          const pa_agg_spec& A = s.aggs[a];
+          double* outd = (double*)out_aggs[a];
+          if (A.type == PA_AGG_COUNT) {
+            outd[n] = (double)hc[r];
+            continue;
+          }
+          const char* sp = sec(q->agg_section[a]);
+          const int src = q->hq.aggs[a].src;
+          if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
+            const int64_t per = int64_t(1) << A.log2m;
+            const uint32_t* rg = (const uint32_t*)sp + r * per;
+            uint8_t* o = (uint8_t*)out_aggs[a] + n * per;
+            for (int64_t j = 0; j < per; ++j) o[j] = (uint8_t)rg[j];
+          } else if (A.type == PA_AGG_SUM || A.type == PA_AGG_COUNT_MV) {
+            const int64_t* hv = (const int64_t*)sp;
+            // SRC_LONG: exact 96-bit total, rounded once (the reference's double of the exact sum)
+            if (src == SRC_LONG) outd[n] = (double)(((__int128)hv[2 * r + 1] << 32) + (__int128)(uint64_t)hv[2 * r]);
+            else outd[n] = src == SRC_INT ? (double)hv[r] : ((const double*)sp)[r];
+          } else {  // MIN / MAX; empty aggregation-only result -> +/-inf (Min/MaxAggregationFunction DEFAULT_VALUE)
+            const int64_t e8 = ((const int64_t*)sp)[r];
+            if (hc[r] == 0) outd[n] = A.type == PA_AGG_MIN ? __builtin_inf() : -__builtin_inf();
+            else outd[n] = src != SRC_DOUBLE ? (double)e8 : f64_order_decode(e8);
+          }
+        }
+      }
+      ++n;
+    }
+    return n;
+  };
+
   // Small accumulator blocks (the common case: a few thousand keys): ONE device-to-host copy of the whole block into
   // pinned memory and one synchronisation, then compaction + decode on the host.
   if (q->acc.n <= kFetchWholeBlockBytes) {
@@ -1127,123 +1192,80 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
         return fail(PA_ENOMEM, "hipHostMalloc for the accumulator copy failed");
       }
     }
-    char* dbase = (char*)(q->external_acc ? q->external_acc : q->acc.p);
     PA_HIP(hipMemcpyAsync(q->host_acc, dbase, q->acc.n, hipMemcpyDeviceToHost, st));
     PA_HIP(hipStreamSynchronize(st));
     const char* hb = (const char*)q->host_acc;
     auto hsec = [&](int sec) { return hb + ((char*)q->sections[sec].ptr - dbase); };
-    const uint64_t* hc = (const uint64_t*)hsec(0);
     q->last_matched = (int64_t)*(const uint64_t*)hsec((int)q->sections.size() - 1);
-    int64_t n = 0;
-    for (int64_t k = 0; k < K; ++k) {
-      if (s.num_group_by != 0 && hc[k] == 0) continue;
-      if (n < capacity) {
-        if (out_keys) out_keys[n] = k;
-        if (out_counts) out_counts[n] = (int64_t)hc[k];
-        for (int a = 0; a < s.num_aggs; ++a) {
-          if (!out_aggs || !out_aggs[a]) continue;
-          const pa_agg_spec& A = s.aggs[a];
-          double* outd = (double*)out_aggs[a];
-          if (A.type == PA_AGG_COUNT) {
-            outd[n] = (double)hc[k];
-            continue;
-          }
-          const char* sp = hsec(q->agg_section[a]);
-          const int src = q->hq.aggs[a].src;
-          if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
-            const int64_t per = int64_t(1) << A.log2m;
-            const uint32_t* r = (const uint32_t*)sp + k * per;
-            uint8_t* o = (uint8_t*)out_aggs[a] + n * per;
-            for (int64_t j = 0; j < per; ++j) o[j] = (uint8_t)r[j];
-          } else if (A.type == PA_AGG_SUM || A.type == PA_AGG_COUNT_MV) {
-            const int64_t* hv = (const int64_t*)sp;
-            if (src == SRC_LONG) outd[n] = (double)(((__int128)hv[2 * k + 1] << 32) + (__int128)(uint64_t)hv[2 * k]);
-            else outd[n] = src == SRC_INT ? (double)hv[k] : ((const double*)sp)[k];
-          } else {
-            const int64_t e8 = ((const int64_t*)sp)[k];
-            if (hc[k] == 0) outd[n] = A.type == PA_AGG_MIN ? __builtin_inf() : -__builtin_inf();
-            else outd[n] = src != SRC_DOUBLE ? (double)e8 : f64_order_decode(e8);
-          }
-        }
-      }
-      ++n;
-    }
-    return n;
+    return decode(K, (const uint64_t*)hsec(0), hsec, [](int64_t r) { return r; }, grouped);
   }
-  std::vector<uint64_t> cnt(K);
+
+  // Large key spaces: ordered compaction of the non-empty keys on the GPU (count + scan, then key ids and every
+  // section's rows gathered into a staging block), one copy of the compacted rows, decode on the host.
+  const int64_t nb = (K + 2047) / 2048;
+  if ((int64_t)q->fetch_blocks.n < (nb + 1) * 4) {
+    dev_free(q->fetch_blocks);
+    int rc = dev_alloc(q->fetch_blocks, (size_t)(nb + 1) * 4);
+    if (rc) return rc;
+  }
+  const int all = grouped ? 0 : 1;
+  uint32_t total = 0;
   uint64_t md = 0;
-  PA_HIP(hipMemcpyAsync(cnt.data(), q->sections[0].ptr, (size_t)K * 8, hipMemcpyDeviceToHost, st));
+  PA_HIP(launch_compact((const unsigned long long*)q->sections[0].ptr, K, all, (uint32_t*)q->fetch_blocks.p, 0,
+                        nullptr, 0, st));
+  PA_HIP(hipMemcpyAsync(&total, (uint32_t*)q->fetch_blocks.p + nb, 4, hipMemcpyDeviceToHost, st));
   PA_HIP(hipMemcpyAsync(&md, q->sections.back().ptr, 8, hipMemcpyDeviceToHost, st));
   PA_HIP(hipStreamSynchronize(st));
   q->last_matched = (int64_t)md;
-  std::vector<int64_t> keys;
-  if (s.num_group_by == 0) {
-    keys.push_back(0);
-  } else {
-    for (int64_t k = 0; k < K; ++k)
-      if (cnt[k] != 0) keys.push_back(k);
+  const int64_t m = (int64_t)total;
+  const int64_t rows = std::min<int64_t>(m, std::max<int64_t>(capacity, 0));
+  if (rows == 0) return m;
+  // staging: keys | count | one block per aggregation section (rows x per x es), 256-byte aligned pieces
+  CompactDesc d;
+  std::memset(&d, 0, sizeof(d));
+  std::vector<int> secs = {0};
+  for (int a = 0; a < s.num_aggs; ++a)
+    if (q->agg_section[a] >= 0) secs.push_back(q->agg_section[a]);
+  std::vector<size_t> offs;
+  size_t bytes = ((size_t)rows * 8 + 255) & ~(size_t)255;
+  for (int sec : secs) {
+    const Section& sc = q->sections[sec];
+    const int es = sc.kind == PA_ACC_HLL_U32 ? 4 : 8;
+    const int64_t per = sc.n / K;
+    offs.push_back(bytes);
+    bytes += ((size_t)rows * per * es + 255) & ~(size_t)255;
   }
-  const int64_t n = (int64_t)keys.size();
-  const int64_t m = std::min(n, capacity);
-  if (m <= 0) return n;
-  for (int64_t i = 0; i < m; ++i) {
-    if (out_keys) out_keys[i] = keys[i];
-    if (out_counts) out_counts[i] = (int64_t)cnt[keys[i]];
-  }
-  DevBuf dkeys;
-  int rc = dev_alloc(dkeys, (size_t)m * 8);
-  if (rc) return rc;
-  if (hipMemcpy(dkeys.p, keys.data(), (size_t)m * 8, hipMemcpyHostToDevice) != hipSuccess) {
-    dev_free(dkeys);
-    return fail(PA_EHIP, "key upload failed");
-  }
-  for (int a = 0; a < s.num_aggs; ++a) {
-    if (!out_aggs || !out_aggs[a]) continue;
-    const pa_agg_spec& A = s.aggs[a];
-    double* outd = (double*)out_aggs[a];
-    if (A.type == PA_AGG_COUNT) {
-      for (int64_t i = 0; i < m; ++i) outd[i] = (double)cnt[keys[i]];
-      continue;
-    }
-    const Section& sc = q->sections[q->agg_section[a]];
-    const int src0 = q->hq.aggs[a].src;
-    const int64_t per = A.type == PA_AGG_DISTINCTCOUNTHLL ? (int64_t(1) << A.log2m)
-                        : ((A.type == PA_AGG_SUM && src0 == SRC_LONG) ? 2 : 1);
-    const int es = A.type == PA_AGG_DISTINCTCOUNTHLL ? 4 : 8;
-    DevBuf g;
-    rc = dev_alloc(g, (size_t)m * per * es);
-    if (rc) { dev_free(dkeys); return rc; }
-    std::vector<char> host((size_t)m * per * es);
-    hipError_t e = launch_gather(sc.ptr, es, per, (const int64_t*)dkeys.p, m, g.p, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(host.data(), g.p, host.size(), hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    dev_free(g);
-    if (e != hipSuccess) { dev_free(dkeys); return fail(PA_EHIP, std::string("fetch: ") + hipGetErrorString(e)); }
-    const int src = q->hq.aggs[a].src;
-    if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
-      uint8_t* o = (uint8_t*)out_aggs[a];
-      const uint32_t* r = (const uint32_t*)host.data();
-      for (int64_t i = 0; i < m * per; ++i) o[i] = (uint8_t)r[i];
-    } else if (A.type == PA_AGG_SUM || A.type == PA_AGG_COUNT_MV) {
-      const int64_t* hv = (const int64_t*)host.data();
-      for (int64_t i = 0; i < m; ++i) {
-        if (src == SRC_LONG) {  // exact 96-bit total, rounded once (the reference's double of the exact sum)
-          const __int128 t = ((__int128)hv[2 * i + 1] << 32) + (__int128)(uint64_t)hv[2 * i];
-          outd[i] = (double)t;
-        } else {
-          outd[i] = src == SRC_INT ? (double)hv[i] : ((const double*)host.data())[i];
-        }
-      }
-    } else {  // MIN / MAX; empty aggregation-only result -> +/-inf (Min/MaxAggregationFunction DEFAULT_VALUE)
-      for (int64_t i = 0; i < m; ++i) {
-        const int64_t e8 = ((const int64_t*)host.data())[i];
-        if (cnt[keys[i]] == 0) outd[i] = A.type == PA_AGG_MIN ? __builtin_inf() : -__builtin_inf();
-        else outd[i] = src != SRC_DOUBLE ? (double)e8 : f64_order_decode(e8);
-      }
+  if (q->fetch_stage.n < bytes) {
+    dev_free(q->fetch_stage);
+    int rc = dev_alloc(q->fetch_stage, bytes);
+    if (rc) return rc;
+    if (q->fetch_host) (void)hipHostFree(q->fetch_host);
+    if (hipHostMalloc(&q->fetch_host, bytes, hipHostMallocDefault) != hipSuccess) {
+      q->fetch_host = nullptr;
+      return fail(PA_ENOMEM, "hipHostMalloc for the fetch staging failed");
     }
   }
-  dev_free(dkeys);
-  return n;
+  char* dstage = (char*)q->fetch_stage.p;
+  d.nsec = (int32_t)secs.size();
+  d.keys = (int64_t*)dstage;
+  for (size_t i = 0; i < secs.size(); ++i) {
+    const Section& sc = q->sections[secs[i]];
+    d.es[i] = sc.kind == PA_ACC_HLL_U32 ? 4 : 8;
+    d.per[i] = sc.n / K;
+    d.src[i] = sc.ptr;
+    d.dst[i] = dstage + offs[i];
+  }
+  PA_HIP(launch_compact((const unsigned long long*)q->sections[0].ptr, K, all, (uint32_t*)q->fetch_blocks.p, rows,
+                        &d, 1, st));
+  PA_HIP(hipMemcpyAsync(q->fetch_host, dstage, bytes, hipMemcpyDeviceToHost, st));
+  PA_HIP(hipStreamSynchronize(st));
+  const char* hb = (const char*)q->fetch_host;
+  const int64_t* hkeys = (const int64_t*)hb;
+  std::map<int, const char*> hsec;
+  for (size_t i = 0; i < secs.size(); ++i) hsec[secs[i]] = hb + offs[i];
+  decode(rows, (const uint64_t*)hsec[0], [&](int sec) { return hsec[sec]; }, [&](int64_t r) { return hkeys[r]; },
+         false);
+  return m;
 }
 
 int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs, uint64_t* num_tiles) {

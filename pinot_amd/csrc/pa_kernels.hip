@@ -1006,6 +1006,95 @@ __global__ void gather_kernel(const void* src, int esize, int64_t per, const int
   }
 }
 
+
+// ---------------------------------------------------------------- fetch: ordered compaction of non-empty keys
+// Block b covers keys [2048b, 2048b + 2048): thread t owns keys 8t .. 8t+7 of it.
+constexpr int kCompactKeys = 2048;
+
+__device__ __forceinline__ uint32_t block_exclusive_scan_256(uint32_t v, uint32_t* sh, uint32_t* total) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const uint32_t add = t >= o ? sh[t - o] : 0u;
+    __syncthreads();
+    sh[t] += add;
+    __syncthreads();
+  }
+  const uint32_t incl = sh[t];
+  if (total) *total = sh[255];
+  __syncthreads();
+  return incl - v;
+}
+
+__global__ void __launch_bounds__(256) compact_count_kernel(const unsigned long long* count, int64_t K, int all,
+                                                            uint32_t* block_sums) {
+  __shared__ uint32_t sh[256];
+  const int64_t k0 = (int64_t)blockIdx.x * kCompactKeys + 8 * threadIdx.x;
+  uint32_t c = 0;
+  for (int j = 0; j < 8; ++j) c += (k0 + j < K) && (all || count[k0 + j] != 0);
+  uint32_t total;
+  block_exclusive_scan_256(c, sh, &total);
+  if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
+}
+
+// single workgroup: in-place exclusive scan of n block sums; v[n] = total
+__global__ void __launch_bounds__(256) compact_scan_kernel(uint32_t* v, int64_t n) {
+  __shared__ uint32_t sh[256];
+  uint32_t carry = 0;
+  for (int64_t base = 0; base < n; base += 256) {
+    const int64_t i = base + threadIdx.x;
+    const uint32_t x = i < n ? v[i] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan_256(x, sh, &tot);
+    if (i < n) v[i] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) v[n] = carry;
+}
+
+__global__ void __launch_bounds__(256) compact_gather_kernel(const unsigned long long* count, int64_t K, int all,
+                                                             const uint32_t* block_off, int64_t cap,
+                                                             CompactDesc d) {
+  __shared__ uint32_t sh[256];
+  const int64_t k0 = (int64_t)blockIdx.x * kCompactKeys + 8 * threadIdx.x;
+  uint32_t c = 0;
+  for (int j = 0; j < 8; ++j) c += (k0 + j < K) && (all || count[k0 + j] != 0);
+  int64_t pos = (int64_t)block_off[blockIdx.x] + block_exclusive_scan_256(c, sh, nullptr);
+  for (int j = 0; j < 8; ++j) {
+    const int64_t k = k0 + j;
+    if (k >= K || !(all || count[k] != 0)) continue;
+    if (pos < cap) {
+      d.keys[pos] = k;
+      for (int si = 0; si < d.nsec; ++si) {
+        const int64_t per = d.per[si];
+        if (d.es[si] == 8) {
+          const uint64_t* src = (const uint64_t*)d.src[si] + k * per;
+          uint64_t* dst = (uint64_t*)d.dst[si] + pos * per;
+          for (int64_t e = 0; e < per; ++e) dst[e] = src[e];
+        } else {
+          const uint32_t* src = (const uint32_t*)d.src[si] + k * per;
+          uint32_t* dst = (uint32_t*)d.dst[si] + pos * per;
+          for (int64_t e = 0; e < per; ++e) dst[e] = src[e];
+        }
+      }
+    }
+    ++pos;
+  }
+}
+
+hipError_t launch_compact(const unsigned long long* count, int64_t K, int all, uint32_t* block_sums, int64_t cap,
+                          const CompactDesc* d, int phase, hipStream_t s) {
+  const int64_t nb = (K + kCompactKeys - 1) / kCompactKeys;
+  if (phase == 0) {
+    compact_count_kernel<<<(unsigned)nb, 256, 0, s>>>(count, K, all, block_sums);
+    compact_scan_kernel<<<1, 256, 0, s>>>(block_sums, nb);
+  } else {
+    compact_gather_kernel<<<(unsigned)nb, 256, 0, s>>>(count, K, all, block_sums, cap, *d);
+  }
+  return hipGetLastError();
+}
+
 static int grid_for(int64_t n, int block) {
   int64_t g = (n + block - 1) / block;
   if (g < 1) g = 1;

@@ -4,6 +4,19 @@
 #include "pa_device.h"
 
 namespace pa {
+// ordered compaction of the non-empty keys (fetch): phase 0 = per-block counts + scan (block_sums[nb] = total),
+// phase 1 = write key ids + gather every section's rows into d.dst
+constexpr int kMaxCompactSections = PA_MAX_AGGS + 2;
+struct CompactDesc {
+  int32_t nsec;
+  int32_t es[kMaxCompactSections];
+  int64_t per[kMaxCompactSections];
+  const void* src[kMaxCompactSections];
+  void* dst[kMaxCompactSections];
+  int64_t* keys;
+};
+hipError_t launch_compact(const unsigned long long* count, int64_t K, int all, uint32_t* block_sums, int64_t cap,
+                          const CompactDesc* d, int phase, hipStream_t s);
 hipError_t launch_bswap_words(uint32_t* w, int64_t n, hipStream_t s);
 hipError_t launch_hll_lut_numeric(const int64_t* di, const double* dd, int32_t vtype, int32_t card, int32_t log2m,
                                   uint32_t* lut, hipStream_t s);

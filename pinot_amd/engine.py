@@ -327,16 +327,17 @@ class GpuQueryExecutor:
         out["plan"]["lane_major"] = int(L.lib().pa_query_lane_major(self.handle))
         return out
 
-    def fetch(self, stream=None) -> IntermediateResult:
+    def fetch_arrays(self, stream=None):
+        """Non-empty groups in ascending table-wide key order as arrays: (keys int64[n], counts int64[n],
+        [one array per GPU accumulator: float64[n], or uint8[n << log2m] HLL registers]). Synchronises `stream`."""
         lib = L.lib()
-        q = self.query
-        cap = 1 if not q.group_by else min(self.num_keys, 1 << 16)
+        cap = 1 if not self.query.group_by else min(self.num_keys, 1 << 16)
         while True:
-            keys = np.zeros(cap, dtype=np.int64)
-            counts = np.zeros(cap, dtype=np.int64)
+            keys = np.empty(cap, dtype=np.int64)
+            counts = np.empty(cap, dtype=np.int64)
             outs, ptrs = [], (ctypes.c_void_p * max(1, len(self.pa_aggs)))()
             for i, (t, _, log2m) in enumerate(self.pa_aggs):
-                o = np.zeros(cap << log2m, dtype=np.uint8) if t == L.PA_AGG_DISTINCTCOUNTHLL else np.zeros(cap, dtype=np.float64)
+                o = np.empty(cap << log2m, dtype=np.uint8) if t == L.PA_AGG_DISTINCTCOUNTHLL else np.empty(cap, np.float64)
                 outs.append(o)
                 ptrs[i] = o.ctypes.data
             n = L.check(lib.pa_query_fetch(self.handle, stream, cap, keys.ctypes.data, counts.ctypes.data, ptrs),
@@ -344,37 +345,45 @@ class GpuQueryExecutor:
             if n <= cap:
                 break
             cap = n
+        outs = [o[: n << self.pa_aggs[i][2]] if self.pa_aggs[i][0] == L.PA_AGG_DISTINCTCOUNTHLL else o[:n]
+                for i, o in enumerate(outs)]
+        return keys[:n], counts[:n], outs
+
+    def key_values(self, keys):
+        """Table-wide key ids -> one value array per group-by column (DictionaryBasedGroupKeyGenerator.getKeys)."""
+        return [gd[(keys // st) % len(gd)] for gd, st in zip(self.global_dicts, self.strides)]
+
+    def fetch(self, stream=None) -> IntermediateResult:
+        lib = L.lib()
+        q = self.query
+        keys, counts, outs = self.fetch_arrays(stream)
+        n = len(keys)
         res = IntermediateResult(list(q.aggregations), list(q.group_by))
         res.num_total_docs = sum(s.num_docs for s in self.segs)
         res.num_docs_scanned = int(lib.pa_query_matched_docs(self.handle))
-        # decode key ids -> values
-        key_cols = []
-        for j, gd in enumerate(self.global_dicts):
-            ids = (keys[:n] // self.strides[j]) % len(gd)
-            key_cols.append(gd[ids])
-        for r in range(n):
-            vals = []
-            for a, pi in zip(q.aggregations, self.agg_map):
-                if a.function == "COUNT":
-                    vals.append(int(counts[r]))
-                elif a.function == "AVG":
-                    vals.append(AvgPair(float(outs[pi][r]), int(counts[r])))
-                elif a.function == "AVGMV":
-                    vals.append(AvgPair(float(outs[pi[0]][r]), int(outs[pi[1]][r])))
-                elif a.function == "COUNTMV":
-                    vals.append(int(outs[pi][r]))
-                elif a.function in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV"):
-                    log2m = self.pa_aggs[pi][2]
-                    m = 1 << log2m
-                    vals.append(HyperLogLog(log2m, outs[pi][r * m:(r + 1) * m]))
-                else:
-                    vals.append(float(outs[pi][r]))
-            if q.group_by:
-                res.groups[tuple(_py(kc[r]) for kc in key_cols)] = vals
+        key_cols = [kc.tolist() for kc in self.key_values(keys)]
+        cols = []  # one python list per query aggregation
+        for a, pi in zip(q.aggregations, self.agg_map):
+            if a.function == "COUNT":
+                cols.append(counts.tolist())
+            elif a.function == "AVG":
+                cols.append([AvgPair(s_, c_) for s_, c_ in zip(outs[pi].tolist(), counts.tolist())])
+            elif a.function == "AVGMV":
+                cols.append([AvgPair(s_, int(c_)) for s_, c_ in zip(outs[pi[0]].tolist(), outs[pi[1]].tolist())])
+            elif a.function == "COUNTMV":
+                cols.append([int(v) for v in outs[pi].tolist()])
+            elif a.function in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV"):
+                log2m = self.pa_aggs[pi][2]
+                regs = outs[pi].reshape(n, 1 << log2m)
+                cols.append([HyperLogLog(log2m, regs[r]) for r in range(n)])
             else:
-                res.row = vals
+                cols.append(outs[pi].tolist())
+        rows = list(zip(*cols)) if cols else [()] * n
         if q.group_by:
+            res.groups = {tuple(kc[r] for kc in key_cols): list(rows[r]) for r in range(n)}
             res.num_groups_limit_reached = len(res.groups) >= q.num_groups_limit
+        else:
+            res.row = list(rows[0])
         return res
 
     def run(self, stream=None) -> IntermediateResult:

@@ -144,6 +144,31 @@ def write_mv_forward_index(ids_per_doc, num_bits) -> np.ndarray:
     return np.concatenate([np.frombuffer(header, dtype=np.uint8), bitmap, raw]).astype(np.uint8)
 
 
+def mv_column_from_flat(name, lengths, flat_ids, dictionary, data_type) -> Column:
+    """MV column from row lengths + the flat dictId stream (vectorised; synthetic benchmark segments)."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    if len(lengths) and lengths.min() < 1:
+        raise ValueError("every multi-value row must hold at least one value")
+    col = Column(name=name, data_type=data_type, single_value=False)
+    col.dictionary = np.asarray(dictionary)
+    col.cardinality = int(len(dictionary))
+    col.num_bits = num_bits_per_value(max(col.cardinality - 1, 0))
+    n = len(lengths)
+    total = int(lengths.sum())
+    col.total_num_values = total
+    col.max_num_multi_values = int(lengths.max()) if n else 0
+    dpc, nchunks = mv_docs_per_chunk(n, total)
+    starts = np.zeros(n, dtype=np.int64)
+    if n:
+        np.cumsum(lengths[:-1], out=starts[1:])
+    header = starts[::dpc][:nchunks].astype(">i4").tobytes()
+    bits = np.zeros(((total + 7) // 8) * 8, dtype=np.uint8)
+    bits[starts] = 1
+    col.fwd_bytes = np.concatenate([np.frombuffer(header, dtype=np.uint8), np.packbits(bits),
+                                    pack_bits(np.asarray(flat_ids, dtype=np.uint32), col.num_bits)]).astype(np.uint8)
+    return col
+
+
 def build_mv_column(name, rows, data_type) -> Column:
     """Dictionary-encoded multi-value column from per-doc value arrays."""
     rows = [_coerce(np.atleast_1d(r), data_type) for r in rows]

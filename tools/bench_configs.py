@@ -1,0 +1,137 @@
+"""Secondary measurements for BASELINE.json configs[2] and configs[4] (the headline configs[1] line is bench.py).
+
+  highcard : configs[2] — GROUP BY 2 dictionary dims (1024 x 1024 = ~1M groups) with SUM/MIN/MAX over every doc
+             (and over a 10 % filter); the key space does not fit LDS, so accumulators are global
+  star     : configs[4] shape on one GPU — raw DOUBLE SUM + DISTINCTCOUNTHLLMV over a multi-value column, 4-dim
+             GROUP BY
+
+python tools/bench_configs.py [--workload highcard|star|all] [--segments S] [--docs D] [--reps R]
+Prints one JSON line per (workload, plan): scan-kernel ms per launch (HIP events around back-to-back launches on
+the launch stream), rows/s, forward-index bytes staged per launch and GB/s, fetch ms, groups.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def sv_spec(rng, docs, card, dtype="INT", base=0):
+    from pinot_amd.segment import num_bits_per_value, pack_bits
+    nb = num_bits_per_value(card - 1)
+    if card == 1 << nb:  # uniform dictIds over [0, 2^nb) == uniformly random bytes
+        fwd = np.frombuffer(rng.bytes((docs * nb + 7) // 8), dtype=np.uint8)
+    else:
+        fwd = pack_bits(rng.integers(0, card, size=docs).astype(np.uint32), nb)
+    return (dtype, np.arange(card, dtype=np.int64) + base, fwd)
+
+
+def highcard_segment(seed, docs):
+    from pinot_amd.segment import segment_from_dict_ids
+    rng = np.random.default_rng(seed)
+    return segment_from_dict_ids("hc%d" % seed, docs, {
+        "d1": sv_spec(rng, docs, 1024, base=1000), "d2": sv_spec(rng, docs, 1024, base=5000),
+        "m": sv_spec(rng, docs, 1 << 16, "LONG")})
+
+
+def star_segment(seed, docs, avg_mv=3):
+    from pinot_amd.segment import Column, mv_column_from_flat, segment_from_dict_ids
+    rng = np.random.default_rng(seed)
+    seg = segment_from_dict_ids("st%d" % seed, docs, {
+        "d1": sv_spec(rng, docs, 16), "d2": sv_spec(rng, docs, 32), "d3": sv_spec(rng, docs, 64),
+        "d4": sv_spec(rng, docs, 8)})
+    lengths = rng.integers(1, 2 * avg_mv, size=docs)
+    flat = rng.integers(0, 4096, size=int(lengths.sum())).astype(np.uint32)
+    seg.columns["tags"] = mv_column_from_flat("tags", lengths, flat, np.arange(4096, dtype=np.int64) * 11, "INT")
+    r = Column(name="r", data_type="DOUBLE", has_dictionary=False)
+    r.raw_values = rng.normal(100.0, 30.0, size=docs)
+    seg.columns["r"] = r
+    return seg
+
+
+WORKLOADS = {
+    "highcard": (highcard_segment, [
+        ("all_docs", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000 "
+                     "OPTION(numGroupsLimit=2000000)", 0),
+        ("filtered_10pct", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t WHERE m < 6554 GROUP BY d1, d2 "
+                           "LIMIT 2000000 OPTION(numGroupsLimit=2000000)", 0),
+    ]),
+    "star": (star_segment, [
+        ("all_docs", "SELECT d1, d2, d3, d4, SUM(r), DISTINCTCOUNTHLLMV(tags) FROM t GROUP BY d1, d2, d3, d4 "
+                     "LIMIT 1000000 OPTION(numGroupsLimit=1000000)", 0),
+    ]),
+}
+
+
+def run(workload, nseg, docs, reps):
+    import torch
+    from pinot_amd import parse_sql
+    from pinot_amd import _lib as L
+    from pinot_amd.engine import GpuQueryExecutor, GpuSegment
+    make, queries = WORKLOADS[workload]
+    t0 = time.perf_counter()
+    gsegs, cids = [], None
+    for i in range(nseg):
+        seg = make(100 + i, docs)
+        if cids is None:
+            cids = {n: j for j, n in enumerate(sorted(seg.columns))}
+        gsegs.append(GpuSegment(seg, column_ids=cids, device=0))
+        for c in seg.columns.values():  # HBM holds the data now; keep only the dictionaries
+            c.fwd_bytes = None
+            c.raw_values = None
+    log("%s: %d segments x %d docs resident (%.1f GB), %.1f s" % (
+        workload, nseg, docs, sum(g.device_bytes for g in gsegs) / 1e9, time.perf_counter() - t0))
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    for name, sql, flags in queries:
+        for extra, tag in ((0, ""), (L.PA_QF_NO_LANE_MAJOR, "_stepmajor")):
+            ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags | extra)
+            ex.execute(sp)
+            torch.cuda.synchronize()
+            ex.reset(sp)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for _ in range(reps):
+                ex.scan(sp)
+            b.record(stream)
+            torch.cuda.synchronize()
+            ms = a.elapsed_time(b) / reps
+            ex.execute(sp)
+            t1 = time.perf_counter()
+            keys, counts, outs = ex.fetch_arrays(sp)
+            fetch_ms = (time.perf_counter() - t1) * 1e3
+            st = ex.stats()
+            print(json.dumps({"workload": workload, "plan_name": name + tag, "kernel_ms": round(ms, 4),
+                              "rows_per_s": st["num_docs"] / (ms * 1e-3), "staged_bytes": st["staged_bytes"],
+                              "staged_GBps": st["staged_bytes"] / (ms * 1e-3) / 1e9, "fetch_ms": round(fetch_ms, 2),
+                              "groups": int(len(keys)), "matched_docs": int(L.lib().pa_query_matched_docs(ex.handle)),
+                              "plan": st["plan"], "segments": nseg, "docs_per_segment": docs}), flush=True)
+            ex.close()
+    for g in gsegs:
+        g.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="all")
+    ap.add_argument("--segments", type=int, default=20)
+    ap.add_argument("--docs", type=int, default=10_000_000)
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    for w in (WORKLOADS if args.workload == "all" else [args.workload]):
+        run(w, args.segments, args.docs, args.reps)
+
+
+if __name__ == "__main__":
+    main()
