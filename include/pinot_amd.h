@@ -173,6 +173,8 @@ typedef struct {
 #define PA_QF_WG_SHIFT 12             /* bits 12..14: workgroups per CU (1..4) */
 #define PA_QF_DEBUG_STREAM_ONLY (1 << 16) /* measurement only: stream the tiles, skip decode (results invalid) */
 #define PA_QF_NO_LANE_MAJOR (1 << 17)     /* use the step-major scan kernel even when the lane-major one applies */
+/* bits 18..20: measurement-only tile bodies (tools/sweep.py --debug) */
+#define PA_QF_NO_PARTITION (1 << 21)      /* high-cardinality dense GROUP BY: per-doc global atomics, not partitioned */
 
 /* per-(segment, leaf) parameters in that segment's dictId space */
 typedef struct {
@@ -243,7 +245,8 @@ int64_t pa_query_matched_docs(const pa_query* q);
 int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs,
                    uint64_t* num_tiles);
 
-/* The kernel plan chosen by pa_query_prepare: accumulator strategy (0 = LDS-privatised, 1 = global), 64-doc
+/* The kernel plan chosen by pa_query_prepare: accumulator strategy (0 = LDS-privatised, 1 = global atomics,
+ * 2 = partitioned: records partitioned by key range, then aggregated per partition in LDS), 64-doc
  * steps per wave tile, DMA instructions per tile, tile images per wave, workgroups per CU, grid, LDS bytes. */
 /* Filter literals evaluated on whole staged tiles (the rest only on the docs those matched). */
 int32_t pa_query_num_eager_literals(const pa_query* q);

@@ -364,6 +364,8 @@ int to_cnf(const pa_query_spec& spec, std::vector<Clause>& out) {
 }
 
 constexpr size_t kFetchWholeBlockBytes = 1 << 20;
+constexpr size_t kPartLdsBytes = 64 * 1024;  // pass C accumulators of one partition (2 workgroups per CU)
+constexpr int64_t kMaxParts = 4096;          // partition counters of the scan passes: 16 KiB of LDS
 
 struct Section {
   int32_t kind;
@@ -408,6 +410,10 @@ struct pa_query {
   void* fetch_host = nullptr;        // pinned copy of the compacted rows
   int lane_major = 0;
   int has_mv = 0;
+  bool partitioned = false;      // partitioned aggregation (STRAT_PCOUNT / STRAT_PSCATTER passes + part_agg_kernel)
+  int part_P = 0, part_shift = 0, rec_words = 0, part_lds_c = 0;
+  std::vector<int> pay_off, part_agg_lds;
+  DevBuf part_hist, part_base, recs;
   int64_t last_matched = -1;  // numDocsScanned read by the last fetch
   std::vector<LmSegPlan> hplans;
   std::vector<DevBuf> owned;  // LUTs, remaps, HLL LUTs
@@ -420,6 +426,9 @@ struct pa_query {
     dev_free(dq);
     dev_free(dsegs);
     dev_free(dplans);
+    dev_free(part_hist);
+    dev_free(part_base);
+    dev_free(recs);
     if (host_acc) (void)hipHostFree(host_acc);
     dev_free(fetch_blocks);
     dev_free(fetch_stage);
@@ -853,6 +862,7 @@ int pa_query_prepare(pa_query* q) {
   }
   for (int si = 0; si < q->nseg && lm; ++si)
     if (q->hsegs[si].num_staged > kLmStaged) lm = false;
+  size_t part_hist_bytes = 0;  // partitioned aggregation: the per-partition LDS counters of the scan passes
   auto plan_for = [&](int strat, bool use_lm) {
     const bool lds_strategy = strat == STRAT_LDS;
     Plan best;
@@ -872,7 +882,7 @@ int pa_query_prepare(pa_query* q) {
         dma = std::max(dma, n);
       }
       const size_t img_bytes = (size_t)img_dw * 4;
-      const size_t acc_b = lds_strategy ? lds_acc : 0;
+      const size_t acc_b = lds_strategy ? lds_acc : (strat == STRAT_PCOUNT ? part_hist_bytes : 0);
       for (int wg : {4, 3, 2, 1}) {
         if (force_wg && wg != force_wg) continue;
         const size_t per_wg = kLdsBudget / wg;
@@ -906,7 +916,7 @@ int pa_query_prepare(pa_query* q) {
   auto plan_pick = [&](int strat) {
     if (!lm) return plan_for(strat, false);
     Plan a = plan_for(strat, true);
-    if (strat == STRAT_GLOBAL && dense) {
+    if ((strat == STRAT_GLOBAL || strat == STRAT_PCOUNT) && dense) {
       Plan b = plan_for(strat, false);
       if (b.score >= 0 && b.wg_per_cu > a.wg_per_cu) {
         lm = false;
@@ -921,7 +931,59 @@ int pa_query_prepare(pa_query* q) {
     plan = plan_pick(STRAT_LDS);
     if (plan.score >= 0) q->strategy = STRAT_LDS;
   }
-  if (q->strategy == STRAT_GLOBAL) plan = plan_pick(STRAT_GLOBAL);
+  // Partitioned aggregation for dense queries whose key space does not fit LDS (BASELINE configs[2]): two scan passes
+  // (count per (workgroup, partition); write one record per matching doc into its partition) + one LDS aggregation
+  // per partition, instead of ~(1 + aggregations) device-scope atomics per matching doc on random keys.
+  q->partitioned = false;
+  if (q->strategy == STRAT_GLOBAL && dense && !q->has_mv && !(s.flags & (PA_QF_NO_PARTITION | PA_QF_FORCE_GLOBAL)) &&
+      K <= (int64_t(1) << 32) && q->num_docs < (uint64_t(1) << 31)) {
+    bool ok = true;
+    size_t per_key = 4;  // u32 count
+    int words = 1;       // key
+    std::vector<int> pay(s.num_aggs, 0);
+    for (int a = 0; a < s.num_aggs && ok; ++a) {
+      const int t = s.aggs[a].type;
+      if (t == PA_AGG_COUNT) continue;
+      if (t == PA_AGG_DISTINCTCOUNTHLL || t == PA_AGG_COUNT_MV) { ok = false; break; }
+      per_key += (t == PA_AGG_SUM && agg_src[a] == SRC_LONG) ? 16 : 8;
+      // one payload per distinct (column, value source): SUM/MIN/MAX of one column share it
+      int shared = -1;
+      for (int b = 0; b < a; ++b)
+        if (s.aggs[b].type != PA_AGG_COUNT && agg_slot[b] == agg_slot[a] && agg_src[b] == agg_src[a]) shared = pay[b];
+      if (shared >= 0) {
+        pay[a] = shared;
+      } else {
+        pay[a] = words;
+        words += agg_src[a] == SRC_INT ? 1 : 2;
+      }
+    }
+    int64_t kr = 1;
+    while (ok && (size_t)(kr * 2) * per_key <= kPartLdsBytes) kr *= 2;
+    const int64_t P = ok ? (K + kr - 1) / kr : 0;
+    if (ok && kr >= 256 && P >= 2 && P <= kMaxParts) {
+      part_hist_bytes = ((size_t)P * 4 + 15) & ~(size_t)15;
+      Plan pp = plan_pick(STRAT_PCOUNT);
+      if (pp.score >= 0) {
+        plan = pp;
+        q->partitioned = true;
+        q->part_P = (int)P;
+        q->part_shift = __builtin_ctzll((uint64_t)kr);
+        q->rec_words = words;
+        q->pay_off = pay;
+        // pass C LDS layout: u32 count[kr], then every aggregation's accumulators for kr keys (8-byte aligned)
+        size_t off = ((size_t)kr * 4 + 15) & ~(size_t)15;
+        q->part_agg_lds.assign(s.num_aggs, 0);
+        for (int a = 0; a < s.num_aggs; ++a) {
+          const int t = s.aggs[a].type;
+          if (t == PA_AGG_COUNT) continue;
+          q->part_agg_lds[a] = (int)off;
+          off += (size_t)kr * ((t == PA_AGG_SUM && agg_src[a] == SRC_LONG) ? 16 : 8);
+        }
+        q->part_lds_c = (int)off;
+      }
+    }
+  }
+  if (q->strategy == STRAT_GLOBAL && !q->partitioned) plan = plan_pick(STRAT_GLOBAL);
   if (plan.score < 0) return fail(PA_EUNSUPPORTED, "staged columns too wide for the LDS tile ring");
   q->lds_bytes = (int)plan.lds;
   q->steps = plan.steps;
@@ -988,14 +1050,15 @@ int pa_query_prepare(pa_query* q) {
   h.matched_docs = (unsigned long long*)q->sections.back().ptr;
   h.has_mv = q->has_mv;
   h.lds_count_off = 0;
-  h.lds_acc_bytes = q->strategy == STRAT_LDS ? (uint32_t)lds_acc : 0;
+  h.lds_acc_bytes = q->strategy == STRAT_LDS ? (uint32_t)lds_acc : (q->partitioned ? (uint32_t)part_hist_bytes : 0);
   for (int a = 0; a < s.num_aggs; ++a) {
     DevAgg& A = h.aggs[a];
     A.type = s.aggs[a].type;
     A.slot = agg_slot[a];
     A.log2m = s.aggs[a].log2m;
     A.src = agg_src[a];
-    A.lds_off = (int32_t)agg_lds[a];
+    A.lds_off = q->partitioned ? q->part_agg_lds[a] : (int32_t)agg_lds[a];
+    A.pay_off = q->partitioned ? q->pay_off[a] : 0;
     if (q->agg_section[a] >= 0) {
       void* p = q->sections[q->agg_section[a]].ptr;
       A.acc_i64 = (int64_t*)p;
@@ -1015,6 +1078,23 @@ int pa_query_prepare(pa_query* q) {
   const int64_t max_wg = (int64_t)cus * wg_per_cu;
   const int64_t want = (first + kWavesPerWG - 1) / kWavesPerWG;
   q->grid = (int)std::max<int64_t>(1, std::min(max_wg, want));
+  if (q->partitioned) {
+    // records: at most one per doc (every bound doc may match); hist: [grid][P]; base: [P + 1]
+    dev_free(q->part_hist);
+    dev_free(q->part_base);
+    dev_free(q->recs);
+    rc = dev_alloc(q->part_hist, (size_t)q->grid * q->part_P * 4);
+    if (!rc) rc = dev_alloc(q->part_base, (size_t)(q->part_P + 1) * 4);
+    if (!rc) rc = dev_alloc(q->recs, std::max<size_t>(16, (size_t)q->num_docs * q->rec_words * 4));
+    if (rc) return rc;
+    h.part_shift = q->part_shift;
+    h.num_parts = q->part_P;
+    h.rec_words = q->rec_words;
+    h.part_lds_bytes = (uint32_t)q->part_lds_c;
+    h.part_hist = (uint32_t*)q->part_hist.p;
+    h.part_base = (uint32_t*)q->part_base.p;
+    h.recs = (uint32_t*)q->recs.p;
+  }
 
   // ---- upload descriptors
   rc = dev_alloc(q->dq, sizeof(DevQuery));
@@ -1058,7 +1138,13 @@ int pa_query_prepare(pa_query* q) {
   rc = dev_alloc(q->dplans, sizeof(LmSegPlan) * q->hplans.size());
   if (rc) return rc;
   PA_HIP(hipMemcpy(q->dplans.p, q->hplans.data(), sizeof(LmSegPlan) * q->hplans.size(), hipMemcpyHostToDevice));
-  PA_HIP(set_scan_lds_limit(q->strategy, q->steps, q->lane_major, q->lds_bytes));
+  if (q->partitioned) {
+    PA_HIP(set_scan_lds_limit(STRAT_PCOUNT, q->steps, q->lane_major, q->lds_bytes));
+    PA_HIP(set_scan_lds_limit(STRAT_PSCATTER, q->steps, q->lane_major, q->lds_bytes));
+    PA_HIP(set_part_agg_lds_limit(q->part_lds_c));
+  } else {
+    PA_HIP(set_scan_lds_limit(q->strategy, q->steps, q->lane_major, q->lds_bytes));
+  }
   PA_HIP(hipDeviceSynchronize());
   q->prepared = true;
   return PA_OK;
@@ -1081,6 +1167,17 @@ int pa_query_reset(pa_query* q, void* stream) {
 int pa_query_scan(pa_query* q, void* stream) {
   if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
   if (q->num_tiles == 0) return PA_OK;
+  if (q->partitioned) {  // pass A, per-partition offsets, pass B, pass C
+    hipStream_t st = (hipStream_t)stream;
+    const DevQuery* dq = (const DevQuery*)q->dq.p;
+    PA_HIP(launch_scan(STRAT_PCOUNT, q->steps, q->lane_major, q->grid, q->lds_bytes, dq, (const DevSeg*)q->dsegs.p,
+                       (const LmSegPlan*)q->dplans.p, st));
+    PA_HIP(launch_part_offsets((uint32_t*)q->part_hist.p, q->grid, q->part_P, (uint32_t*)q->part_base.p, st));
+    PA_HIP(launch_scan(STRAT_PSCATTER, q->steps, q->lane_major, q->grid, q->lds_bytes, dq, (const DevSeg*)q->dsegs.p,
+                       (const LmSegPlan*)q->dplans.p, st));
+    PA_HIP(launch_part_agg(dq, q->part_P, q->part_lds_c, st));
+    return PA_OK;
+  }
   PA_HIP(launch_scan(q->strategy, q->steps, q->lane_major, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p,
                      (const DevSeg*)q->dsegs.p, (const LmSegPlan*)q->dplans.p, (hipStream_t)stream));
   return PA_OK;
@@ -1279,7 +1376,7 @@ int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs
 int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t* dma_slots, int32_t* ring,
                   int32_t* wg_per_cu, int32_t* grid, int32_t* lds_bytes) {
   if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
-  if (strategy) *strategy = q->strategy;
+  if (strategy) *strategy = q->partitioned ? STRAT_PCOUNT : q->strategy;
   if (steps) *steps = q->steps;
   if (dma_slots) *dma_slots = q->dma_slots;
   if (ring) *ring = q->plan_ring;

@@ -23,7 +23,10 @@ constexpr int kMaxSlots = 12;                 // distinct columns referenced by 
 constexpr int kGuardWords = 4;
 
 enum ColKind : int32_t { COL_NONE = 0, COL_SV_DICT = 1, COL_SV_RAW = 2, COL_MV_DICT = 3 };
-enum Strategy : int32_t { STRAT_LDS = 0, STRAT_GLOBAL = 1 };
+// STRAT_PCOUNT / STRAT_PSCATTER: the two scan passes of partitioned aggregation (high-cardinality dense GROUP BY):
+// pass A counts matching docs per (workgroup, key partition), pass B writes one record (key, values) per matching doc
+// into its partition, then part_agg_kernel aggregates every partition in LDS (no per-doc device-scope atomics).
+enum Strategy : int32_t { STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PCOUNT = 2, STRAT_PSCATTER = 3 };
 // SUM/MIN/MAX value source. SRC_INT: every value fits int32 (one exact int64 accumulator);
 // SRC_LONG: 64-bit values, SUM kept exactly as a (low 32 bits unsigned, high 32 bits signed) pair of int64
 // sums = a 96-bit total for up to 2^32 docs per key; SRC_DOUBLE: FLOAT/DOUBLE.
@@ -90,8 +93,8 @@ struct DevAgg {
   int64_t* acc_i64;          // SUM(int) [K], SUM(long) [2K: lo, hi], MIN / MAX (ordered encoding for doubles)
   double* acc_f64;           // SUM(double)
   uint32_t* acc_hll;         // [num_keys << log2m]
-  int32_t lds_off;           // LDS strategy: byte offset of the WG-private copy
-  int32_t pad;
+  int32_t lds_off;           // LDS strategy / partition aggregation: byte offset of the WG-private copy
+  int32_t pay_off;           // partitioned aggregation: word offset of the value inside a record
 };
 
 struct DevQuery {
@@ -113,6 +116,13 @@ struct DevQuery {
   int32_t has_mv;            // a group-by or aggregation column is multi-value: per-lane key expansion path
   int32_t pad2;
   unsigned long long* matched_docs;  // [1]: docs that passed the filter (numDocsScanned)
+  int32_t part_shift;        // partitioned aggregation: 1 << part_shift table-wide keys per partition
+  int32_t num_parts;
+  int32_t rec_words;         // words per record: key + values
+  uint32_t part_lds_bytes;   // part_agg_kernel: LDS accumulator bytes for one partition
+  uint32_t* part_hist;       // [grid][num_parts]: pass A counts, then (in place) each workgroup's offset in a partition
+  uint32_t* part_base;       // [num_parts + 1]: first record of every partition
+  uint32_t* recs;            // records, partition-major
   int32_t staged_slots[kMaxSlots];
   int32_t gb_slot[PA_MAX_GROUP_BY];
   int64_t gb_stride[PA_MAX_GROUP_BY];

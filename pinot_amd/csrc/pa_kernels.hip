@@ -82,6 +82,8 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // compiler does not know about only make its own vmcnt waits stricter, never wrong.
 __device__ __forceinline__ void dma16(const void* src, uint32_t lds_base) {
   uint32_t keep;
+  // wave-uniform by construction; readfirstlane keeps it in an SGPR even where the compiler computed it with VALU ops
+  lds_base = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_base);
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %2\n\t"
@@ -391,6 +393,56 @@ __device__ void accumulate_doc_mv(const DevQuery* __restrict__ q, const DevSeg* 
   }
 }
 
+// Partitioned aggregation, passes A (STRAT_PCOUNT) and B (STRAT_PSCATTER) for one matching doc: the table-wide key
+// (DictionaryBasedGroupKeyGenerator raw key) picks partition key >> part_shift; pass A counts it in the workgroup's
+// LDS histogram, pass B claims the next slot of the workgroup's range of that partition and writes the record
+// (key, then every aggregation's value: int32, or int64 / double bits as two words).
+template <int STRAT>
+__device__ __forceinline__ void partition_doc(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                              const uint32_t* img, int doc_local, int64_t doc, uint32_t* part_lds) {
+  int64_t key = 0;
+  for (int j = 0; j < q->num_gb; ++j) {
+    const DevCol& c = seg->cols[q->gb_slot[j]];
+    uint32_t id = decode_dict_id(c, img, doc_local, doc);
+    const int32_t* rm = seg->remap[j];
+    if (rm != nullptr) id = (uint32_t)gp(rm)[id];
+    key += (int64_t)id * q->gb_stride[j];
+  }
+  const uint32_t p = (uint32_t)(key >> q->part_shift);
+  if (STRAT == STRAT_PCOUNT) {
+    atomicAdd(part_lds + p, 1u);
+    return;
+  }
+  const uint32_t pos = atomicAdd(part_lds + p, 1u);
+  AS1 uint32_t* r = gp(q->recs) + (size_t)pos * (uint32_t)q->rec_words;
+  if (q->rec_words <= 2) {
+    // the common record (key, one int32 value shared by every aggregation of one column): one 8-byte store
+    uint32_t v = 0;
+    for (int a = 0; a < q->num_aggs; ++a) {
+      const DevAgg& A = q->aggs[a];
+      if (A.type != PA_AGG_COUNT) {
+        v = (uint32_t)agg_value(A, a, seg, img, doc_local, doc).i;
+        break;
+      }
+    }
+    *(AS1 uint64_t*)r = ((uint64_t)v << 32) | (uint32_t)key;
+    return;
+  }
+  r[0] = (uint32_t)key;
+  for (int a = 0; a < q->num_aggs; ++a) {
+    const DevAgg& A = q->aggs[a];
+    if (A.type == PA_AGG_COUNT) continue;
+    const AggValue v = agg_value(A, a, seg, img, doc_local, doc);
+    if (A.src == SRC_INT) {
+      r[A.pay_off] = (uint32_t)v.i;
+    } else {
+      const int64_t b = A.src == SRC_DOUBLE ? __builtin_bit_cast(int64_t, v.d) : v.i;
+      r[A.pay_off] = (uint32_t)b;
+      r[A.pay_off + 1] = (uint32_t)(b >> 32);
+    }
+  }
+}
+
 // Match word of one leaf over a whole wave tile: bit i of lane l <=> doc 64*i + l of the tile matches.
 // Leaf parameters are loaded once per tile; the 32 decodes are independent, so the LDS reads pipeline.
 template <int STEPS>
@@ -582,7 +634,11 @@ __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, con
     if (__ballot(m != 0) == 0) return;
   }
   matched += (uint32_t)__builtin_popcount(m);
-  if (q->has_mv) {
+  if constexpr (STRAT == STRAT_PCOUNT || STRAT == STRAT_PSCATTER) {
+    for (int i = 0; i < STEPS; ++i)
+      if ((m >> i) & 1u)
+        partition_doc<STRAT>(q, seg, img, i * kWave + lane, doc_base + i * kWave + lane, (uint32_t*)acc.lds);
+  } else if (q->has_mv) {
     for (int i = 0; i < STEPS; ++i)
       if ((m >> i) & 1u) accumulate_doc_mv<STRAT>(q, seg, img, i * kWave + lane, doc_base + i * kWave + lane, acc);
   } else {
@@ -734,7 +790,11 @@ __device__ __forceinline__ void process_tile_lm(const DevQuery* __restrict__ q, 
     if (__ballot(m != 0) == 0) return;
   }
   matched += (uint32_t)__builtin_popcount(m);
-  if (q->has_mv) {
+  if constexpr (STRAT == STRAT_PCOUNT || STRAT == STRAT_PSCATTER) {
+    for (int i = 0; i < 32; ++i)
+      if ((m >> i) & 1u)
+        partition_doc<STRAT>(q, seg, img, 32 * lane + i, doc_base + 32 * lane + i, (uint32_t*)acc.lds);
+  } else if (q->has_mv) {
     for (int i = 0; i < 32; ++i)
       if ((m >> i) & 1u) accumulate_doc_mv<STRAT>(q, seg, img, 32 * lane + i, doc_base + 32 * lane + i, acc);
   } else {
@@ -796,6 +856,7 @@ __device__ __forceinline__ int find_segment(const DevSeg* __restrict__ segs, int
 template <int N>
 __device__ __forceinline__ void vm_wait_token(uint32_t& token) {
   static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  token = (uint32_t)__builtin_amdgcn_readfirstlane((int)token);  // wave-uniform (see dma16)
   asm volatile("s_waitcnt vmcnt(%1)" : "+s"(token) : "n"(N));
 }
 
@@ -831,7 +892,7 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
   // (otherwise segment descriptors are read with vector loads whose vmcnt(0) waits drain the DMA ring)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   unsigned char* lds_acc = (unsigned char*)smem;
-  const uint32_t acc_dwords = STRAT == STRAT_LDS ? (q->lds_acc_bytes >> 2) : 0u;
+  const uint32_t acc_dwords = STRAT != STRAT_GLOBAL ? (q->lds_acc_bytes >> 2) : 0u;
   const int img_dw = q->image_dwords_max;
   uint32_t* ring = smem + acc_dwords + wave * q->ring * img_dw;
   Acc<STRAT> acc{q, lds_acc};
@@ -853,6 +914,13 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
         for (int64_t k = threadIdx.x; k < n; k += kWGSize) r[k] = init;  // SUM(double) 0.0 == all-zero bits
       }
     }
+    __syncthreads();
+  } else if (STRAT == STRAT_PCOUNT || STRAT == STRAT_PSCATTER) {
+    // pass A: zeroed per-partition counters; pass B: this workgroup's first slot in every partition
+    uint32_t* pl = (uint32_t*)lds_acc;
+    const int P = q->num_parts;
+    for (int p = threadIdx.x; p < P; p += kWGSize)
+      pl[p] = STRAT == STRAT_PCOUNT ? 0u : q->part_base[p] + q->part_hist[(size_t)blockIdx.x * P + p];
     __syncthreads();
   }
 
@@ -919,9 +987,15 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
     }
   }
 
-  {
+  if (STRAT != STRAT_PSCATTER) {  // (pass B sees the same docs as pass A)
     const int64_t wm = wave_sum_i64((int64_t)matched);
     if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)wm, RLX);
+  }
+  if (STRAT == STRAT_PCOUNT) {
+    __syncthreads();
+    const uint32_t* pl = (const uint32_t*)lds_acc;
+    const int P = q->num_parts;
+    for (int p = threadIdx.x; p < P; p += kWGSize) gp(q->part_hist)[(size_t)blockIdx.x * P + p] = pl[p];
   }
   if (STRAT == STRAT_LDS) {
     __syncthreads();
@@ -1095,6 +1169,120 @@ hipError_t launch_compact(const unsigned long long* count, int64_t K, int all, u
   return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------- partitioned aggregation: offsets + pass C
+// Block p: exclusive scan of the G workgroup counts of partition p (hist[wg][p], in place); total -> totals[p].
+__global__ void __launch_bounds__(256) part_scan_kernel(uint32_t* hist, int G, int P, uint32_t* totals) {
+  __shared__ uint32_t sh[256];
+  const int p = blockIdx.x;
+  uint32_t carry = 0;
+  for (int base = 0; base < G; base += 256) {
+    const int wg = base + threadIdx.x;
+    const uint32_t x = wg < G ? hist[(size_t)wg * P + p] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan_256(x, sh, &tot);
+    if (wg < G) hist[(size_t)wg * P + p] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) totals[p] = carry;
+}
+
+// Pass C, block p: aggregate the records of partition p (keys [p << shift, (p+1) << shift)) in LDS, then add the
+// partition's non-empty keys into the global accumulators (this block owns those keys: plain read-modify-write).
+__global__ void __launch_bounds__(256) part_agg_kernel(const DevQuery* __restrict__ q) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  unsigned char* lds = (unsigned char*)smem;
+  const int p = blockIdx.x;
+  const int64_t KR = int64_t(1) << q->part_shift;
+  const int64_t kbase = (int64_t)p << q->part_shift;
+  const int64_t nk = min(KR, q->num_keys - kbase);
+  uint32_t* cnt = (uint32_t*)lds;
+  for (int64_t k = threadIdx.x; k < KR; k += 256) cnt[k] = 0;
+  for (int a = 0; a < q->num_aggs; ++a) {
+    const DevAgg& A = q->aggs[a];
+    if (A.type == PA_AGG_COUNT) continue;
+    int64_t* r = (int64_t*)(lds + A.lds_off);
+    const int64_t init = A.type == PA_AGG_MIN ? INT64_MAX : (A.type == PA_AGG_MAX ? INT64_MIN : 0);
+    const int64_t n = (A.type == PA_AGG_SUM && A.src == SRC_LONG) ? 2 * KR : KR;
+    for (int64_t k = threadIdx.x; k < n; k += 256) r[k] = init;
+  }
+  __syncthreads();
+  const uint32_t r0 = q->part_base[p], r1 = q->part_base[p + 1];
+  const int W = q->rec_words;
+  for (uint32_t ri = r0 + threadIdx.x; ri < r1; ri += 256) {
+    const AS1 uint32_t* rec = gp(q->recs) + (size_t)ri * (uint32_t)W;
+    const int64_t lk = (int64_t)rec[0] - kbase;
+    atomicAdd(cnt + lk, 1u);
+    for (int a = 0; a < q->num_aggs; ++a) {
+      const DevAgg& A = q->aggs[a];
+      if (A.type == PA_AGG_COUNT) continue;
+      int64_t iv;
+      if (A.src == SRC_INT) iv = (int64_t)(int32_t)rec[A.pay_off];
+      else iv = (int64_t)(((uint64_t)rec[A.pay_off + 1] << 32) | rec[A.pay_off]);
+      if (A.type == PA_AGG_SUM) {
+        if (A.src == SRC_INT) {
+          atomicAdd((unsigned long long*)(lds + A.lds_off) + lk, (unsigned long long)iv);
+        } else if (A.src == SRC_LONG) {
+          atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk, (unsigned long long)(uint32_t)iv);
+          atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk + 1, (unsigned long long)(iv >> 32));
+        } else {
+          atomicAdd((double*)(lds + A.lds_off) + lk, __builtin_bit_cast(double, iv));
+        }
+      } else {
+        const int64_t e = A.src != SRC_DOUBLE ? iv : f64_order_encode(__builtin_bit_cast(double, iv));
+        if (A.type == PA_AGG_MIN) atomicMin((long long*)(lds + A.lds_off) + lk, (long long)e);
+        else atomicMax((long long*)(lds + A.lds_off) + lk, (long long)e);
+      }
+    }
+  }
+  __syncthreads();
+  for (int64_t lk = threadIdx.x; lk < nk; lk += 256) {
+    const uint32_t c = cnt[lk];
+    if (c == 0) continue;
+    const int64_t k = kbase + lk;
+    gp(q->count)[k] += c;
+    for (int a = 0; a < q->num_aggs; ++a) {
+      const DevAgg& A = q->aggs[a];
+      switch (A.type) {
+        case PA_AGG_SUM:
+          if (A.src == SRC_INT) {
+            gp(A.acc_i64)[k] += ((const int64_t*)(lds + A.lds_off))[lk];
+          } else if (A.src == SRC_LONG) {
+            gp(A.acc_i64)[2 * k] += ((const int64_t*)(lds + A.lds_off))[2 * lk];
+            gp(A.acc_i64)[2 * k + 1] += ((const int64_t*)(lds + A.lds_off))[2 * lk + 1];
+          } else {
+            gp(A.acc_f64)[k] += ((const double*)(lds + A.lds_off))[lk];
+          }
+          break;
+        case PA_AGG_MIN: {
+          const int64_t v = ((const int64_t*)(lds + A.lds_off))[lk];
+          if (v < gp(A.acc_i64)[k]) gp(A.acc_i64)[k] = v;
+        } break;
+        case PA_AGG_MAX: {
+          const int64_t v = ((const int64_t*)(lds + A.lds_off))[lk];
+          if (v > gp(A.acc_i64)[k]) gp(A.acc_i64)[k] = v;
+        } break;
+        default: break;
+      }
+    }
+  }
+}
+
+hipError_t launch_part_offsets(uint32_t* hist, int G, int P, uint32_t* part_base, hipStream_t s) {
+  part_scan_kernel<<<P, 256, 0, s>>>(hist, G, P, part_base);
+  compact_scan_kernel<<<1, 256, 0, s>>>(part_base, P);
+  return hipGetLastError();
+}
+
+hipError_t set_part_agg_lds_limit(int lds_bytes) {
+  return hipFuncSetAttribute((const void*)part_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+}
+
+hipError_t launch_part_agg(const DevQuery* q, int P, int lds_bytes, hipStream_t s) {
+  part_agg_kernel<<<P, 256, (size_t)lds_bytes, s>>>(q);
+  return hipGetLastError();
+}
+
 static int grid_for(int64_t n, int block) {
   int64_t g = (n + block - 1) / block;
   if (g < 1) g = 1;
@@ -1131,10 +1319,19 @@ hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t*
   return hipGetLastError();
 }
 
+template <int STRAT>
+static const void* scan_fn_s(int steps, int lm) {
+  if (lm) return (const void*)scan_kernel<STRAT, 32, 1>;
+  return steps == 16 ? (const void*)scan_kernel<STRAT, 16, 0> : (const void*)scan_kernel<STRAT, 32, 0>;
+}
+
 static const void* scan_fn(int strategy, int steps, int lm) {
-  if (lm) return strategy == STRAT_LDS ? (const void*)scan_kernel<STRAT_LDS, 32, 1> : (const void*)scan_kernel<STRAT_GLOBAL, 32, 1>;
-  if (strategy == STRAT_LDS) return steps == 16 ? (const void*)scan_kernel<STRAT_LDS, 16, 0> : (const void*)scan_kernel<STRAT_LDS, 32, 0>;
-  return steps == 16 ? (const void*)scan_kernel<STRAT_GLOBAL, 16, 0> : (const void*)scan_kernel<STRAT_GLOBAL, 32, 0>;
+  switch (strategy) {
+    case STRAT_LDS: return scan_fn_s<STRAT_LDS>(steps, lm);
+    case STRAT_PCOUNT: return scan_fn_s<STRAT_PCOUNT>(steps, lm);
+    case STRAT_PSCATTER: return scan_fn_s<STRAT_PSCATTER>(steps, lm);
+    default: return scan_fn_s<STRAT_GLOBAL>(steps, lm);
+  }
 }
 
 hipError_t set_scan_lds_limit(int strategy, int steps, int lm, int bytes) {

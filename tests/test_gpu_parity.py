@@ -257,6 +257,36 @@ def test_high_cardinality_global_fallback():
     assert len(got.groups) > 100000
 
 
+@pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LANE_MAJOR, L.PA_QF_NO_PARTITION, L.PA_QF_STAGE_ALL])
+def test_partitioned_aggregation(flags):
+    """High-cardinality dense GROUP BY (BASELINE configs[2] shape): records partitioned by key range, aggregated per
+    partition in LDS. INT / LONG (beyond int32) / DOUBLE / FLOAT values, SUM MIN MAX AVG, with and without a filter,
+    several segments with different dictionaries; identical to the oracle and to the per-doc atomic path."""
+    cols = {"k1": ("INT", 700), "k2": ("LONG", 900), "m": ("INT", 5000), "big": ("LONG", 3000), "f": ("DOUBLE", 800),
+            "g": ("FLOAT", 600)}
+    segs = [make_segment(70 + i, n, cols) for i, n in enumerate((120011, 40009))]
+    queries = [
+        "SELECT k1, k2, COUNT(*), SUM(m), MIN(m), MAX(m), AVG(m) FROM t GROUP BY k1, k2 LIMIT 1000000 "
+        "OPTION(numGroupsLimit=2000000)",
+        "SELECT k2, k1, SUM(big), MIN(big), MAX(f), SUM(f), MIN(g) FROM t WHERE m > {m} GROUP BY k2, k1 "
+        "LIMIT 1000000 OPTION(numGroupsLimit=2000000)",
+    ]
+    mv = int(segs[0].column("m").dictionary[len(segs[0].column("m").dictionary) // 4])
+    gsegs = [GpuSegment(sg) for sg in segs]
+    try:
+        for sql in queries:
+            sql = sql.format(m=mv)
+            got, exp, _ = run_both(sql, segs, gsegs=gsegs, flags=flags, rel=DOUBLE_REL)
+            assert len(got.groups) > 50000
+            ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags)
+            strategy = ex.stats()["plan"]["strategy"]
+            ex.close()
+            assert strategy == ("global" if flags & L.PA_QF_NO_PARTITION else "partitioned"), strategy
+    finally:
+        for g in gsegs:
+            g.close()
+
+
 def test_num_groups_limit_guard():
     """Until first-seen trimming runs on the GPU, a query whose numGroupsLimit may bind fails loudly."""
     from pinot_amd.engine import UnsupportedQuery

@@ -72,7 +72,7 @@ WORKLOADS = {
 }
 
 
-def run(workload, nseg, docs, reps):
+def run(workload, nseg, docs, reps, only=None, no_stepmajor=False):
     import torch
     from pinot_amd import parse_sql
     from pinot_amd import _lib as L
@@ -93,7 +93,10 @@ def run(workload, nseg, docs, reps):
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
     for name, sql, flags in queries:
-        for extra, tag in ((0, ""), (L.PA_QF_NO_LANE_MAJOR, "_stepmajor")):
+        if only and name != only:
+            continue
+        variants = ((0, ""),) if no_stepmajor else ((0, ""), (L.PA_QF_NO_LANE_MAJOR, "_stepmajor"))
+        for extra, tag in variants:
             ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags | extra)
             ex.execute(sp)
             torch.cuda.synchronize()
@@ -126,11 +129,13 @@ def main():
     ap.add_argument("--segments", type=int, default=20)
     ap.add_argument("--docs", type=int, default=10_000_000)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--plan", default=None, help="only this plan name (e.g. all_docs)")
+    ap.add_argument("--no-stepmajor", action="store_true", help="skip the forced step-major variants")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
     for w in (WORKLOADS if args.workload == "all" else [args.workload]):
-        run(w, args.segments, args.docs, args.reps)
+        run(w, args.segments, args.docs, args.reps, args.plan, args.no_stepmajor)
 
 
 if __name__ == "__main__":
