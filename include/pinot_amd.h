@@ -173,7 +173,6 @@ typedef struct {
 #define PA_QF_WG_SHIFT 12             /* bits 12..14: workgroups per CU (1..4) */
 #define PA_QF_DEBUG_STREAM_ONLY (1 << 16) /* measurement only: stream the tiles, skip decode (results invalid) */
 #define PA_QF_NO_LANE_MAJOR (1 << 17)     /* use the step-major scan kernel even when the lane-major one applies */
-/* bits 18..20: measurement-only tile bodies (tools/sweep.py --debug) */
 #define PA_QF_NO_PARTITION (1 << 21)      /* high-cardinality dense GROUP BY: per-doc global atomics, not partitioned */
 
 /* per-(segment, leaf) parameters in that segment's dictId space */

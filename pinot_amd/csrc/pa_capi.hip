@@ -1040,7 +1040,7 @@ int pa_query_prepare(pa_query* q) {
   h.num_eager = q->num_eager;
   h.dma_per_tile = plan.dma;
   h.steps = plan.steps;
-  h.debug_stream_only = (s.flags & PA_QF_DEBUG_STREAM_ONLY) ? 1 : ((s.flags >> 18) & 7) ? 1 + ((s.flags >> 18) & 7) : 0;
+  h.debug_stream_only = (s.flags & PA_QF_DEBUG_STREAM_ONLY) ? 1 : 0;
   h.lane_major = lm ? 1 : 0;
   q->lane_major = lm ? 1 : 0;
   q->plan_ring = plan.ring;

@@ -94,6 +94,25 @@ __device__ __forceinline__ void dma16(const void* src, uint32_t lds_base) {
       : "v"(src), "s"(lds_base));
 }
 
+// dma16 for the lanes of `mask` only, with EXEC set and restored inside the asm block (no branch around a partial
+// DMA instruction; the compiler's EXEC tracking is unaffected).
+__device__ __forceinline__ void dma16_masked(const void* src, uint32_t lds_base, uint64_t mask) {
+  uint32_t keep;
+  uint64_t save;
+  lds_base = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_base);
+  asm volatile(
+      "s_mov_b64 %1, exec\n\t"
+      "s_mov_b64 exec, %4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, off\n\t"
+      "s_mov_b32 m0, %0\n\t"
+      "s_mov_b64 exec, %1"
+      : "=&s"(keep), "=&s"(save)
+      : "v"(src), "s"(lds_base), "s"(mask));
+}
+
 template <int STEPS>
 __device__ __forceinline__ void stage_tile(const DevSeg* __restrict__ seg, int64_t wt, uint32_t* img, int lane,
                                            const int D) {
@@ -582,6 +601,54 @@ __device__ __forceinline__ bool leaf_match_doc(const DevLeaf& L, int64_t doc) {
   return m != (L.negate != 0);
 }
 
+// The rare part of a tile (some doc survived the eager clauses): lazy clauses per surviving doc, then aggregation.
+// Returns the docs that matched.
+// LM: doc of bit i of lane l = 32l + i (lane-major tile), else 64i + l.
+template <int STRAT, int STEPS, int LM>
+__device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                                const uint32_t* img, int64_t doc_base, uint32_t m, int lane,
+                                                unsigned char* lds) {
+  const Acc<STRAT> acc{q, lds};
+  auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
+  const int nleaves = q->num_leaves;
+  const int neager = q->num_eager;
+  if (neager < nleaves) {
+    // lazy clauses: only the docs the eager clauses kept, one step at a time, straight from HBM
+    for (int i = 0; i < STEPS; ++i) {
+      const uint32_t bit = 1u << i;
+      if (__ballot((m & bit) != 0) == 0) continue;
+      const int64_t doc = doc_base + local(i);
+      bool ok = (m & bit) != 0;
+      bool any = false;
+      for (int li = neager; li < nleaves; ++li) {
+        const DevLeaf& L = seg->leaves[li];
+        if (ok && !any) any = leaf_match_doc(L, doc);
+        if (L.clause_end) {
+          ok = ok && any;
+          any = false;
+        }
+      }
+      if (!ok) m &= ~bit;
+    }
+    if (__ballot(m != 0) == 0) return 0;
+  }
+  if constexpr (STRAT == STRAT_PCOUNT || STRAT == STRAT_PSCATTER) {
+    for (int i = 0; i < STEPS; ++i)
+      if ((m >> i) & 1u) partition_doc<STRAT>(q, seg, img, local(i), doc_base + local(i), (uint32_t*)lds);
+  } else if (q->has_mv) {
+    for (int i = 0; i < STEPS; ++i)
+      if ((m >> i) & 1u) accumulate_doc_mv<STRAT>(q, seg, img, local(i), doc_base + local(i), acc);
+  } else {
+    for (int i = 0; i < STEPS; ++i) {
+      const uint64_t sm = __ballot((m >> i) & 1u);
+      if (sm == 0) continue;
+      accumulate_step<STRAT>(q, seg, img, local(i), doc_base + local(i), sm, lane, acc);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // vmcnt(0): no compiler-visible load left pending
+  return (uint32_t)__builtin_popcount(m);
+}
+
 template <int STRAT, int STEPS>
 __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
                                              int64_t wt, const uint32_t* img, int lane, const Acc<STRAT>& acc,
@@ -601,7 +668,6 @@ __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, con
   }
   uint32_t m = valid;
   uint32_t clause = 0;
-  const int nleaves = q->num_leaves;
   const int neager = q->num_eager;
   for (int li = 0; li < neager; ++li) {
     const DevLeaf& L = seg->leaves[li];
@@ -613,45 +679,7 @@ __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, con
     }
   }
   if (__ballot(m != 0) == 0) return;
-  if (neager < nleaves) {
-    // lazy clauses: only the (rare) docs the eager clauses kept, one 64-doc step at a time
-    for (int i = 0; i < STEPS; ++i) {
-      const uint32_t bit = 1u << i;
-      if (__ballot((m & bit) != 0) == 0) continue;
-      const int64_t doc = doc_base + i * kWave + lane;
-      bool ok = (m & bit) != 0;
-      bool any = false;
-      for (int li = neager; li < nleaves; ++li) {
-        const DevLeaf& L = seg->leaves[li];
-        if (ok && !any) any = leaf_match_doc(L, doc);
-        if (L.clause_end) {
-          ok = ok && any;
-          any = false;
-        }
-      }
-      if (!ok) m &= ~bit;
-    }
-    if (__ballot(m != 0) == 0) return;
-  }
-  matched += (uint32_t)__builtin_popcount(m);
-  if constexpr (STRAT == STRAT_PCOUNT || STRAT == STRAT_PSCATTER) {
-    for (int i = 0; i < STEPS; ++i)
-      if ((m >> i) & 1u)
-        partition_doc<STRAT>(q, seg, img, i * kWave + lane, doc_base + i * kWave + lane, (uint32_t*)acc.lds);
-  } else if (q->has_mv) {
-    for (int i = 0; i < STEPS; ++i)
-      if ((m >> i) & 1u) accumulate_doc_mv<STRAT>(q, seg, img, i * kWave + lane, doc_base + i * kWave + lane, acc);
-  } else {
-    for (int i = 0; i < STEPS; ++i) {
-      const uint64_t sm = __ballot((m >> i) & 1u);
-      if (sm == 0) continue;
-      const int doc_local = i * kWave + lane;
-      accumulate_step<STRAT>(q, seg, img, doc_local, doc_base + doc_local, sm, lane, acc);
-    }
-  }
-  // Leave no compiler-visible VMEM op pending past a tile with matches (a compiler-understood wait): otherwise the
-  // waitcnt pass guards the next tile's LDS decode with vmcnt(0) on EVERY tile, draining the DMA ring.
-  __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // vmcnt(0)
+  matched += tile_survivors<STRAT, STEPS, 0>(q, seg, img, doc_base, m, lane, acc.lds);
 }
 
 
@@ -668,40 +696,48 @@ template <int NB>
 __device__ __forceinline__ uint32_t leaf_lm(int kind, uint32_t region_lds, int lane, uint32_t lo_t, uint32_t hi_t,
                                             const uint32_t* lut) {
   const lds_u32_t* p = (const lds_u32_t*)(uintptr_t)(region_lds + (uint32_t)lane * (uint32_t)(NB * 4));
-  uint32_t w[NB];
+  // Wide columns are unpacked in two halves of 16 docs, so at most ~NB/2 + 1 stream words are live at once (keeps
+  // the kernel within 128 VGPRs: 4 waves per SIMD).
+  constexpr int H = NB > 16 ? 2 : 1;
+  constexpr int DPH = 32 / H;  // docs per half
+  uint32_t nm = 0, bits = 0;
 #pragma unroll
-  for (int j = 0; j < NB; ++j) w[j] = p[j];
-  // MSB-aligned value of doc i: the nb bits starting at stream bit i*NB of the lane's words, in the top bits of t
-  auto top = [&](int i) -> uint32_t {
-    const int s = i * NB, j = s >> 5, o = s & 31;
-    if (o + NB <= 32) return w[j] << o;
-    return __builtin_amdgcn_alignbit(w[j], w[(j + 1 < NB) ? j + 1 : j], 32 - o);
-  };
-  if (kind == PA_LEAF_DICT_RANGE) {
-    // lo <= v < lo + span  <=>  (t - lo') <= hi' (unsigned), lo' / hi' MSB-aligned by the host (see leaf_bits);
-    // non-matches accumulate as nm = 2*nm + borrow: bit i of nm = doc i does not match
-    uint32_t nm = 0;
+  for (int h = H - 1; h >= 0; --h) {
+    constexpr int WMAX = (DPH * NB + 31) / 32 + 1;
+    const int wlo = (h * DPH * NB) >> 5;  // first stream word of this half (compile-time after unrolling)
+    uint32_t w[WMAX];
 #pragma unroll
-    for (int i = 31; i >= 0; --i) {
-      const uint32_t t = top(i);
-      uint32_t u;
-      asm("v_sub_u32_e64 %[u], %[t], %[lo]\n\t"
-          "v_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
-          "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
-          : [nm] "+v"(nm), [u] "=&v"(u)
-          : [t] "v"(t), [lo] "s"(lo_t), [hi] "s"(hi_t)
-          : "vcc");
+    for (int j = 0; j < WMAX; ++j) w[j] = (wlo + j < NB) ? p[wlo + j] : 0u;
+    // MSB-aligned value of doc i: the NB bits starting at stream bit i*NB, in the top bits of t
+    auto top = [&](int i) -> uint32_t {
+      const int s = i * NB, j = (s >> 5) - wlo, o = s & 31;
+      if (o + NB <= 32) return w[j] << o;
+      return __builtin_amdgcn_alignbit(w[j], w[(j + 1 < WMAX) ? j + 1 : j], 32 - o);
+    };
+    if (kind == PA_LEAF_DICT_RANGE) {
+      // lo <= v < lo + span  <=>  (t - lo') <= hi' (unsigned), lo' / hi' MSB-aligned by the host (see leaf_bits);
+      // non-matches accumulate as nm = 2*nm + borrow: bit i of nm = doc i does not match
+#pragma unroll
+      for (int i = (h + 1) * DPH - 1; i >= h * DPH; --i) {
+        const uint32_t t = top(i);
+        uint32_t u;
+        asm("v_sub_u32_e64 %[u], %[t], %[lo]\n\t"
+            "v_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
+            "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
+            : [nm] "+v"(nm), [u] "=&v"(u)
+            : [t] "v"(t), [lo] "s"(lo_t), [hi] "s"(hi_t)
+            : "vcc");
+      }
+    } else {
+      const AS1 uint32_t* lt = gp(lut);
+#pragma unroll
+      for (int i = h * DPH; i < (h + 1) * DPH; ++i) {
+        const uint32_t id = top(i) >> (32 - NB);
+        bits |= ((lt[id >> 5] >> (id & 31u)) & 1u) << i;
+      }
     }
-    return ~nm;
   }
-  const AS1 uint32_t* lt = gp(lut);
-  uint32_t bits = 0;
-#pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    const uint32_t id = top(i) >> (32 - NB);
-    bits |= ((lt[id >> 5] >> (id & 31u)) & 1u) << i;
-  }
-  return bits;
+  return kind == PA_LEAF_DICT_RANGE ? ~nm : bits;
 }
 
 __device__ __forceinline__ uint32_t leaf_lm_any(int nb, int kind, uint32_t region_lds, int lane, uint32_t lo_t,
@@ -769,73 +805,7 @@ __device__ __forceinline__ void process_tile_lm(const DevQuery* __restrict__ q, 
     }
   }
   if (__ballot(m != 0) == 0) return;
-  const int nleaves = q->num_leaves;
-  if (neager < nleaves) {
-    for (int i = 0; i < 32; ++i) {
-      const uint32_t bit = 1u << i;
-      if (__ballot((m & bit) != 0) == 0) continue;
-      const int64_t doc = doc_base + 32 * lane + i;
-      bool ok = (m & bit) != 0;
-      bool any = false;
-      for (int li = neager; li < nleaves; ++li) {
-        const DevLeaf& L = seg->leaves[li];
-        if (ok && !any) any = leaf_match_doc(L, doc);
-        if (L.clause_end) {
-          ok = ok && any;
-          any = false;
-        }
-      }
-      if (!ok) m &= ~bit;
-    }
-    if (__ballot(m != 0) == 0) return;
-  }
-  matched += (uint32_t)__builtin_popcount(m);
-  if constexpr (STRAT == STRAT_PCOUNT || STRAT == STRAT_PSCATTER) {
-    for (int i = 0; i < 32; ++i)
-      if ((m >> i) & 1u)
-        partition_doc<STRAT>(q, seg, img, 32 * lane + i, doc_base + 32 * lane + i, (uint32_t*)acc.lds);
-  } else if (q->has_mv) {
-    for (int i = 0; i < 32; ++i)
-      if ((m >> i) & 1u) accumulate_doc_mv<STRAT>(q, seg, img, 32 * lane + i, doc_base + 32 * lane + i, acc);
-  } else {
-    for (int i = 0; i < 32; ++i) {
-      const uint64_t sm = __ballot((m >> i) & 1u);
-      if (sm == 0) continue;
-      const int doc_local = 32 * lane + i;
-      accumulate_step<STRAT>(q, seg, img, doc_local, doc_base + doc_local, sm, lane, acc);
-    }
-  }
-  __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // vmcnt(0): see process_tile
-}
-
-// Measurement-only tile bodies (flags bits 18..20): 1 = decode the eager leaves and sink the match word,
-// 2 = the same VALU work with no LDS reads, 3 = the LDS reads with no VALU work.
-__device__ __noinline__ void debug_tile_lm(int dbg, uint32_t pp, uint32_t img_lds, int lane) {
-  uint32_t m = 0;
-  const int b = 24;
-  if (dbg == 2) {
-    m = leaf_lm_any((int)rl(pp, b + 1), (int)rl(pp, b), img_lds + 4u * rl(pp, b + 2), lane, rl(pp, b + 3),
-                    rl(pp, b + 4), nullptr);
-  } else if (dbg == 3) {
-    uint32_t x = (uint32_t)lane;
-    const uint32_t lo = rl(pp, b + 3), hi = rl(pp, b + 4);
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      const uint32_t t = __builtin_amdgcn_alignbit(x, x + i, i & 31);
-      uint32_t u;
-      asm volatile("v_sub_u32_e64 %[u], %[t], %[lo]\n\t"
-                   "v_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
-                   "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
-                   : [nm] "+v"(m), [u] "=&v"(u)
-                   : [t] "v"(t), [lo] "s"(lo), [hi] "s"(hi)
-                   : "vcc");
-    }
-  } else {
-    const lds_u32_t* p = (const lds_u32_t*)(uintptr_t)(img_lds + 4u * rl(pp, b + 2) + (uint32_t)lane * 68u);
-#pragma unroll
-    for (int j = 0; j < 17; ++j) m ^= p[j];
-  }
-  if (m == 0x9E3779B9u) asm volatile("s_nop 0" ::"v"(m));  // keep m alive
+  matched += tile_survivors<STRAT, 32, 1>(q, seg, img, doc_base, m, lane, acc.lds);
 }
 
 __device__ __forceinline__ int find_segment(const DevSeg* __restrict__ segs, int nseg, int64_t t) {
@@ -880,9 +850,43 @@ __device__ __forceinline__ void wait_tile(int younger, int D, uint32_t& token) {
   vm_wait_n<0, 63>(token, n < 63 ? n : 63);
 }
 
+// Issue side of the lane-major steady state, hoisted per segment (see scan_kernel).
+struct LmIssue {
+  const char* base[kLmStaged];  // column stream (wave-uniform: the lane's 16-byte offset is added per DMA)
+  int64_t stride[kLmStaged];    // bytes per wave tile
+  uint32_t off[kLmStaged];      // LDS byte offset of the column region in a tile image
+  int nfull[kLmStaged];         // full 64-lane DMA instructions per tile
+  uint64_t tail[kLmStaged];     // lanes of the last, partial instruction (0 = none)
+  int nst;
+  const void* dummy;
+};
+
+// Wait for the tile in slot `slot_off`, then issue the next tile `ti` (ring slot `islot`): every instruction a full
+// 64-lane DMA except a column's lane-masked tail, padded to exactly D instructions.
+__device__ __forceinline__ void lm_wait_issue(const LmIssue& I, uint32_t& slot_off, int R, int D, int64_t younger,
+                                              uint32_t dst0, int64_t it, uint32_t lane_off) {
+  if (R == 2) vm_wait_token<0>(slot_off);  // the one tile in flight has landed
+  else wait_tile((int)younger, D, slot_off);
+  int issued = 0;
+#pragma unroll
+  for (int c = 0; c < kLmStaged; ++c) {
+    if (c < I.nst) {
+      const char* src = I.base[c] + it * I.stride[c] + lane_off;
+      const uint32_t dst = dst0 + I.off[c];
+      for (int k = 0; k < I.nfull[c]; ++k) dma16(src + 1024 * k, dst + 1024 * k);
+      issued += I.nfull[c];
+      if (I.tail[c]) {
+        dma16_masked(src + 1024 * I.nfull[c], dst + 1024 * I.nfull[c], I.tail[c]);
+        ++issued;
+      }
+    }
+  }
+  for (; issued < D; ++issued) dma16_masked(I.dummy, dst0, 1ull);
+}
+
 // LM = 1: lane-major tiles (STEPS must be 32) driven by the per-segment plan tables `plans`; LM = 0: step-major.
 template <int STRAT, int STEPS, int LM>
-__global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restrict__ q,
+__global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __restrict__ q,
                                                        const DevSeg* __restrict__ segs,
                                                        const LmSegPlan* __restrict__ plans) {
   static_assert(!LM || STEPS == 32, "lane-major tiles are 2048 docs");
@@ -966,15 +970,73 @@ __global__ void __launch_bounds__(kWGSize) scan_kernel(const DevQuery* __restric
       const int64_t seg_first = seg->first_wtile;
       const int64_t seg_end = min(t1, seg_first + (int64_t)seg->num_wtiles);
       const uint32_t pp = LM ? ((const uint32_t*)(plans + si))[lane] : 0u;  // process segment's plan table
-      const int dbg = q->debug_stream_only;
-      const bool stream_only = dbg == 1;
+      const bool stream_only = q->debug_stream_only != 0;
+      if constexpr (LM) {
+        if (!stream_only && isi == si) {
+          // Steady state: the tile to issue lies in this segment too; every per-segment value of the issue side and of
+          // the leaf is hoisted into registers (no segment-crossing checks, no plan-table reads per tile).
+          LmIssue I;
+          I.nst = (int)rl(pp, 0);
+#pragma unroll
+          for (int c = 0; c < kLmStaged; ++c) {
+            const int nb = c < I.nst ? (int)rl(pp, 10 + 4 * c) : 0;
+            I.base[c] = (const char*)(((uint64_t)rl(pp, 9 + 4 * c) << 32) | rl(pp, 8 + 4 * c));
+            I.stride[c] = 256 * (int64_t)nb;  // bytes of one wave tile of an nb-bit column
+            I.off[c] = 4u * rl(pp, 11 + 4 * c);
+            I.nfull[c] = (16 * nb) / 64;
+            const int tail = (16 * nb) % 64;
+            I.tail[c] = tail ? ((1ull << tail) - 1ull) : 0ull;
+          }
+          I.dummy = (const void*)(((uint64_t)rl(pp, 5) << 32) | rl(pp, 4));
+          const int64_t issue_end = min(iend, t1);
+          const bool single_range = (int)rl(pp, 1) == 1 && (int)rl(pp, 24) == PA_LEAF_DICT_RANGE && (rl(pp, 29) & 2u);
+          if (single_range) {
+            // one eager DICT_RANGE literal closing its clause: the hoisted leaf on whole tiles (the ragged last tile of
+            // a segment goes through process_tile_lm)
+            const int nb0 = (int)rl(pp, 25);
+            const uint32_t off0 = 4u * rl(pp, 26), lo0 = rl(pp, 27), hi0 = rl(pp, 28);
+            const bool neg0 = (rl(pp, 29) & 1u) != 0;
+            const int64_t full_tiles = (int64_t)(int32_t)rl(pp, 2) / kWTileDocs;
+            while (t < seg_end && ti < issue_end) {
+              uint32_t slot_off = (uint32_t)(pslot * img_dw);
+              lm_wait_issue(I, slot_off, R, D, ti - (t + 1), ring_lds + 4u * (uint32_t)(islot * img_dw), ti - ifirst,
+                            16u * (uint32_t)lane);
+              ++ti;
+              islot = islot + 1 == R ? 0 : islot + 1;
+              if (t - seg_first < full_tiles) {
+                uint32_t m = leaf_lm_any(nb0, PA_LEAF_DICT_RANGE, ring_lds + 4u * slot_off + off0, lane, lo0, hi0,
+                                         nullptr);
+                if (neg0) m = ~m;
+                if (__ballot(m != 0) != 0)
+                  matched += tile_survivors<STRAT, 32, 1>(q, seg, ring + slot_off, (t - seg_first) * kWTileDocs, m,
+                                                          lane, acc.lds);
+              } else {
+                process_tile_lm<STRAT>(q, seg, pp, t - seg_first, ring + slot_off, ring_lds + 4u * slot_off, lane, acc,
+                                       matched);
+              }
+              pslot = pslot + 1 == R ? 0 : pslot + 1;
+              ++t;
+            }
+          } else {
+            while (t < seg_end && ti < issue_end) {
+              uint32_t slot_off = (uint32_t)(pslot * img_dw);
+              lm_wait_issue(I, slot_off, R, D, ti - (t + 1), ring_lds + 4u * (uint32_t)(islot * img_dw), ti - ifirst,
+                            16u * (uint32_t)lane);
+              ++ti;
+              islot = islot + 1 == R ? 0 : islot + 1;
+              process_tile_lm<STRAT>(q, seg, pp, t - seg_first, ring + slot_off, ring_lds + 4u * slot_off, lane, acc,
+                                     matched);
+              pslot = pslot + 1 == R ? 0 : pslot + 1;
+              ++t;
+            }
+          }
+        }
+      }
       for (; t < seg_end; ++t) {
         uint32_t slot_off = (uint32_t)(pslot * img_dw);
         wait_tile((int)(ti - (t + 1)), D, slot_off);  // tile t has landed in its slot (same-wave LDS-DMA)
         if (ti < t1) issue_next();                     // refill the slot tile t-1 used
-        if (LM && dbg > 1) {
-          debug_tile_lm(dbg, pp, ring_lds + 4u * slot_off, lane);
-        } else if (!stream_only) {
+        if (!stream_only) {
           if constexpr (LM) process_tile_lm<STRAT>(q, seg, pp, t - seg_first, ring + slot_off, ring_lds + 4u * slot_off, lane, acc, matched);
           else process_tile<STRAT, STEPS>(q, seg, t - seg_first, ring + slot_off, lane, acc, matched);
         }

@@ -107,6 +107,156 @@ __global__ void __launch_bounds__(256) read_ldsdma(const uint4* __restrict__ p, 
   if (acc == 0x12345678u) out[0] = acc;
 }
 
+
+// Mimic of scan_kernel<GLOBAL, 32, LM> on one 17-bit column: 4352-B tiles (5 DMA instructions, the last with 16
+// lanes), ring of R, lane-major decode (17 ds_read_b32 + static unpack + 3-op range compare per doc), ballot.
+template <int R, int DECODE>
+__global__ void __launch_bounds__(256) lm17(const uint32_t* __restrict__ words, int64_t ntiles, uint32_t lo,
+                                            uint32_t hi, uint32_t* out) {
+  constexpr int NB = 17;
+  constexpr int TILE_DW = 64 * NB;  // 1088 dwords = 4352 B
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* ring = smem + wave * R * (TILE_DW + 16);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t t0 = gw * ntiles / W, t1 = (gw + 1) * ntiles / W;
+  uint32_t found = 0;
+  int64_t ti = t0;
+  int islot = 0;
+  auto issue = [&](int64_t t) {
+    const char* src = (const char*)(words + t * TILE_DW) + 16 * lane;
+    const uint32_t dst = lds_addr(ring + islot * (TILE_DW + 16));
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      if (k < 4 || lane < 16) dma16(src + 1024 * k, dst + 1024 * k);
+    islot = islot + 1 == R ? 0 : islot + 1;
+  };
+  for (int k = 0; k < R - 1 && ti < t1; ++k) issue(ti++);
+  int pslot = 0;
+  for (int64_t t = t0; t < t1; ++t) {
+    if (ti < t1) { vm_wait<(R - 2) * 5>(); } else { vm_wait<0>(); }
+    if (ti < t1) issue(ti++);
+    if (DECODE) {
+      const __attribute__((address_space(3))) uint32_t* p =
+          (const __attribute__((address_space(3))) uint32_t*)(uintptr_t)(lds_addr(ring + pslot * (TILE_DW + 16)) + lane * NB * 4);
+      uint32_t w[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) w[j] = p[j];
+      uint32_t nm = 0;
+#pragma unroll
+      for (int i = 31; i >= 0; --i) {
+        const int s = i * NB, j = s >> 5, o = s & 31;
+        const uint32_t tt = (o + NB <= 32) ? (w[j] << o) : __builtin_amdgcn_alignbit(w[j], w[(j + 1 < NB) ? j + 1 : j], 32 - o);
+        uint32_t u;
+        asm("v_sub_u32_e64 %[u], %[t], %[lo]\n\t"
+            "v_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
+            "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
+            : [nm] "+v"(nm), [u] "=&v"(u) : [t] "v"(tt), [lo] "s"(lo), [hi] "s"(hi) : "vcc");
+      }
+      const uint32_t m = ~nm;
+      if (__ballot(m != 0) != 0) found += __builtin_popcount(m);
+    }
+    pslot = pslot + 1 == R ? 0 : pslot + 1;
+  }
+  vm_wait<0>();
+  if (found == 0x12345678u) out[0] = found;
+}
+
+
+template <int NB>
+__device__ __forceinline__ uint32_t probe_leaf(uint32_t region_lds, int lane, uint32_t lo, uint32_t hi) {
+  const __attribute__((address_space(3))) uint32_t* p =
+      (const __attribute__((address_space(3))) uint32_t*)(uintptr_t)(region_lds + lane * NB * 4);
+  uint32_t w[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) w[j] = p[j];
+  uint32_t nm = 0;
+#pragma unroll
+  for (int i = 31; i >= 0; --i) {
+    const int s = i * NB, j = s >> 5, o = s & 31;
+    const uint32_t tt = (o + NB <= 32) ? (w[j] << o) : __builtin_amdgcn_alignbit(w[j], w[(j + 1 < NB) ? j + 1 : j], 32 - o);
+    uint32_t u;
+    asm("v_sub_u32_e64 %[u], %[t], %[lo]\n\t"
+        "v_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
+        "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
+        : [nm] "+v"(nm), [u] "=&v"(u) : [t] "v"(tt), [lo] "s"(lo), [hi] "s"(hi) : "vcc");
+  }
+  return ~nm;
+}
+__device__ __forceinline__ uint32_t probe_leaf_any(int nb, uint32_t region_lds, int lane, uint32_t lo, uint32_t hi) {
+  switch (nb) {
+#define PC(N) case N: return probe_leaf<N>(region_lds, lane, lo, hi);
+    PC(1) PC(2) PC(3) PC(4) PC(5) PC(6) PC(7) PC(8) PC(9) PC(10) PC(11) PC(12) PC(13) PC(14) PC(15) PC(16)
+    PC(17) PC(18) PC(19) PC(20) PC(21) PC(22) PC(23) PC(24) PC(25) PC(26) PC(27) PC(28) PC(29) PC(30) PC(31) PC(32)
+#undef PC
+    default: return 0;
+  }
+}
+template <int LO, int HI>
+__device__ __forceinline__ void vm_wait_rt(int n) {
+  if constexpr (LO == HI) {
+    vm_wait<LO>();
+  } else {
+    constexpr int MID = (LO + HI) / 2;
+    if (n <= MID) vm_wait_rt<LO, MID>(n);
+    else vm_wait_rt<MID + 1, HI>(n);
+  }
+}
+// SWITCH: decode through the 32-way runtime dispatch; RTWAIT: vmcnt through the runtime binary tree
+template <int SWITCH, int RTWAIT>
+__global__ void __launch_bounds__(256) lm17x(const uint32_t* __restrict__ words, int64_t ntiles, uint32_t lo,
+                                             uint32_t hi, int nb, int D, uint32_t* out) {
+  constexpr int R = 2;
+  constexpr int TILE_DW = 64 * 17;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* ring = smem + wave * R * (TILE_DW + 16);
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t t0 = gw * ntiles / W, t1 = (gw + 1) * ntiles / W;
+  uint32_t found = 0;
+  int64_t ti = t0;
+  int islot = 0;
+  auto issue = [&](int64_t t) {
+    const char* src = (const char*)(words + t * TILE_DW) + 16 * lane;
+    const uint32_t dst = lds_addr(ring + islot * (TILE_DW + 16));
+    const int chunks = 16 * nb;
+    int issued = 0;
+    for (int c0 = 0; c0 < chunks; c0 += 64) {
+      if (c0 + lane < chunks) dma16(src + 16 * c0, dst + 16 * c0);
+      ++issued;
+    }
+    islot = islot + 1 == R ? 0 : islot + 1;
+  };
+  for (int k = 0; k < R - 1 && ti < t1; ++k) issue(ti++);
+  int pslot = 0;
+  for (int64_t t = t0; t < t1; ++t) {
+    if (RTWAIT) {
+      vm_wait_rt<0, 63>((int)(ti - (t + 1)) * D);
+    } else {
+      if (ti < t1) { vm_wait<5>(); } else { vm_wait<0>(); }
+    }
+    if (ti < t1) issue(ti++);
+    const uint32_t region = lds_addr(ring + pslot * (TILE_DW + 16));
+    const uint32_t m = SWITCH ? probe_leaf_any(nb, region, lane, lo, hi) : probe_leaf<17>(region, lane, lo, hi);
+    if (__ballot(m != 0) != 0) found += __builtin_popcount(m);
+    pslot = pslot + 1 == R ? 0 : pslot + 1;
+  }
+  vm_wait<0>();
+  if (found == 0x12345678u) out[0] = found;
+}
+
+__global__ void fill_random(uint32_t* p, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t x = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+    x ^= x >> 29; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 32;
+    p[i] = (uint32_t)x;
+  }
+}
+
 static float time_kernel(void (*launch)(void*), void* arg, int reps) {
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
@@ -124,6 +274,8 @@ static float time_kernel(void (*launch)(void*), void* arg, int reps) {
 }
 
 struct Args { const uint4* p; int64_t bytes; uint32_t* out; int grid; };
+#define LM17X(SW, RT) [](void* v) { Args* a = (Args*)v; lm17x<SW, RT><<<a->grid, 256, 4 * 2 * (1088 + 16) * 4>>>((const uint32_t*)a->p, a->bytes / 4352, 0x80000000u, 0x7fffu, 17, 5, a->out); }
+#define LM17(R, DEC) [](void* v) { Args* a = (Args*)v; lm17<R, DEC><<<a->grid, 256, 4 * R * (1088 + 16) * 4>>>((const uint32_t*)a->p, a->bytes / 4352, 0x80000000u, 0x7fffu, a->out); }
 static Args g;
 
 #define REG(U) [](void* v) { Args* a = (Args*)v; read_reg<U><<<a->grid, 256>>>(a->p, a->bytes / 16, a->out); }
@@ -139,6 +291,11 @@ int main(int argc, char** argv) {
   void* p;
   CHECK(hipMalloc(&p, bytes));
   CHECK(hipMemset(p, 1, bytes));
+  const bool random = argc > 2 && argv[2][0] == 'r';
+  if (random) {
+    fill_random<<<4096, 256>>>((uint32_t*)p, bytes / 4);
+    CHECK(hipDeviceSynchronize());
+  }
   uint32_t* out;
   CHECK(hipMalloc(&out, 64));
   g = Args{(const uint4*)p, bytes, out, 0};
@@ -155,6 +312,10 @@ int main(int argc, char** argv) {
       {"dec 4K r2 rd16 va8", DMAX(4, 2, 16, 8), 4, 4 * 2 * 4 * 1024}, {"dec 4K r2 rd16 va0", DMAX(4, 2, 16, 0), 4, 4 * 2 * 4 * 1024},
       {"dec 4K r3 rd60 va2", DMAX(4, 3, 60, 2), 4, 4 * 3 * 4 * 1024}, {"dec 4K r3 rd16 va8", DMAX(4, 3, 16, 8), 4, 4 * 3 * 4 * 1024},
       {"dec 4K r2 rd4 va30", DMAX(4, 2, 4, 30), 4, 4 * 2 * 4 * 1024}, {"dec 8K r2 rd32 va8", DMAX(8, 2, 32, 8), 2, 4 * 2 * 8 * 1024},
+      {"lm17 r2 stream", LM17(2, 0), 4, 4 * 2 * 1104 * 4}, {"lm17 r2 decode", LM17(2, 1), 4, 4 * 2 * 1104 * 4},
+      {"lm17 r3 decode wg3", LM17(3, 1), 3, 4 * 3 * 1104 * 4}, {"lm17 r2 decode wg3", LM17(2, 1), 3, 4 * 2 * 1104 * 4},
+      {"lm17x base", LM17X(0, 0), 4, 4 * 2 * 1104 * 4}, {"lm17x switch", LM17X(1, 0), 4, 4 * 2 * 1104 * 4},
+      {"lm17x rtwait", LM17X(0, 1), 4, 4 * 2 * 1104 * 4}, {"lm17x switch+rtwait", LM17X(1, 1), 4, 4 * 2 * 1104 * 4},
   };
   for (auto& v : vs) {
     if (v.lds > 65536) {

@@ -26,7 +26,6 @@ def main():
     ap.add_argument("--query", default=bench.QUERY)
     ap.add_argument("--quick", action="store_true", help="only the automatic plans")
     ap.add_argument("--only", default=None, help="run just this configuration name")
-    ap.add_argument("--debug", action="store_true", help="auto plan + measurement-only tile bodies")
     ap.add_argument("--mode", choices=("both", "full", "stream"), default="both")
     args = ap.parse_args()
     import torch
@@ -45,8 +44,7 @@ def main():
     q = parse_sql(args.query)
     stream = torch.cuda.current_stream()
     configs = [("auto", 0), ("auto_nolazy", L.PA_QF_NO_LAZY), ("auto_stepmajor", L.PA_QF_NO_LANE_MAJOR),
-               ("auto_nolazy_stepmajor", L.PA_QF_NO_LAZY | L.PA_QF_NO_LANE_MAJOR),
-               ("dbg_decode_sink", 1 << 18), ("dbg_valu_only", 2 << 18), ("dbg_lds_only", 3 << 18)]
+               ("auto_nolazy_stepmajor", L.PA_QF_NO_LAZY | L.PA_QF_NO_LANE_MAJOR)]
     for lazy_name, lazy_flag in (("", 0), ("_nolazy", L.PA_QF_NO_LAZY)):
         for steps_flag, steps in ((L.PA_QF_STEPS32, 32), (L.PA_QF_STEPS16, 16)):
             for ring in (2, 3, 4):
@@ -55,8 +53,6 @@ def main():
                                     lazy_flag | steps_flag | (ring << L.PA_QF_RING_SHIFT) | (wg << L.PA_QF_WG_SHIFT)))
     if args.quick:
         configs = configs[:4]
-    if args.debug:
-        configs = [configs[0]] + configs[4:]
     if args.only:
         configs = [c for c in configs if c[0] == args.only]
     modes = {"both": (0, L.PA_QF_DEBUG_STREAM_ONLY), "full": (0,), "stream": (L.PA_QF_DEBUG_STREAM_ONLY,)}[args.mode]
@@ -84,7 +80,7 @@ def main():
             rec = {"config": name, "stream_only": bool(dbg), "plan": st["plan"], "kernel_ms": round(ms, 4),
                    "GBps": round(st["staged_bytes"] / ms / 1e6, 1),
                    "Grows_per_s": round(st["num_docs"] / ms / 1e6, 1)}
-            if not dbg and not (flags >> 18) & 7:
+            if not dbg:
                 res = ex.fetch(stream.cuda_stream)
                 snap = {k: tuple(v) for k, v in res.groups.items()}
                 if ref is None:
