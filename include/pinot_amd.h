@@ -155,7 +155,9 @@ typedef struct {
   int32_t ops[PA_MAX_OPS];
   int32_t num_group_by; /* 0 = aggregation-only query */
   int32_t group_by_columns[PA_MAX_GROUP_BY];
-  int64_t group_by_cardinality[PA_MAX_GROUP_BY]; /* size of the table-wide key space per column */
+  int64_t group_by_cardinality[PA_MAX_GROUP_BY]; /* size of the table-wide key space per column; 0 for a raw
+                                                     (no-dictionary) column, grouped by value
+                                                     (NoDictionarySingle/MultiColumnGroupKeyGenerator) */
   int32_t num_aggs;
   pa_agg_spec aggs[PA_MAX_AGGS];
   int32_t flags; /* PA_QF_* */
@@ -216,7 +218,9 @@ int pa_query_scan(pa_query* q, void* stream);
 #define PA_ACC_MAX_I64 4   /* reduce MAX */
 #define PA_ACC_HLL_U32 5   /* reduce MAX */
 #define PA_ACC_SUM_I64X2 6 /* reduce SUM; [2k] = sum of low 32 bits (unsigned), [2k+1] = sum of high 32 bits */
-#define PA_ACC_DOCS_U64 7  /* reduce SUM; one element: docs that passed the filter (numDocsScanned) */
+#define PA_ACC_DOCS_U64 7  /* reduce SUM; [0] docs that passed the filter (numDocsScanned), [1] group-table overflows */
+#define PA_ACC_KEYS_I64 8  /* hashed key space only: slot -> packed key (INT64_MAX = empty); not element-wise
+                              reducible across GPUs (slots differ): merge fetched groups by key instead */
 /* All sections live in one device block of pa_query_accumulator_bytes() bytes (256-byte aligned sections).
  * pa_query_set_accumulator_buffer lets the caller own that block (e.g. memory its collective library
  * registered) instead of the library: call after pa_query_prepare; `bytes` must be >= the size. */
@@ -238,6 +242,12 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
 /* numDocsScanned captured by the last pa_query_fetch (docs that passed the filter; with a multi-value group-by this
  * differs from the sum of the group counts), <0 on error. */
 int64_t pa_query_matched_docs(const pa_query* q);
+
+/* Group-key layout. Direct (hashed = 0): key = sum_j id_j * prod_{k<j} cardinality_k. Hashed (hashed = 1, chosen when
+ * a group-by column is raw or the product of cardinalities is too large to address): the key packs component j
+ * (a table-wide key id, or the raw value's bits: 32 for INT/FLOAT, 64 for LONG/DOUBLE) at bit shifts[j]. Keys returned
+ * by pa_query_fetch follow this layout. */
+int pa_query_key_layout(const pa_query* q, int32_t* hashed, int32_t* shifts);
 
 /* Kernel statistics of the last execute (for roofline accounting): bytes of forward index staged
  * (always-read columns), number of docs scanned. */

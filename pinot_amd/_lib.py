@@ -29,7 +29,7 @@ PA_QF_DEBUG_STREAM_ONLY = 1 << 16
 PA_QF_NO_LANE_MAJOR = 1 << 17
 PA_QF_NO_PARTITION = 1 << 21
 PA_ACC_COUNT_U64, PA_ACC_SUM_I64, PA_ACC_SUM_F64, PA_ACC_MIN_I64, PA_ACC_MAX_I64, PA_ACC_HLL_U32, \
-    PA_ACC_SUM_I64X2, PA_ACC_DOCS_U64 = range(8)
+    PA_ACC_SUM_I64X2, PA_ACC_DOCS_U64, PA_ACC_KEYS_I64 = range(9)
 
 # every symbol declared in include/pinot_amd.h
 EXPORTED = [
@@ -39,7 +39,7 @@ EXPORTED = [
     "pa_query_create", "pa_query_bind_segment", "pa_query_prepare", "pa_query_num_keys",
     "pa_query_execute", "pa_query_reset", "pa_query_scan", "pa_query_num_eager_literals", "pa_query_lane_major",
     "pa_query_accumulator_bytes", "pa_query_set_accumulator_buffer", "pa_query_num_sections", "pa_query_section",
-    "pa_query_fetch", "pa_query_matched_docs", "pa_query_stats",
+    "pa_query_fetch", "pa_query_matched_docs", "pa_query_key_layout", "pa_query_stats",
     "pa_query_plan", "pa_query_destroy",
 ]
 
@@ -114,6 +114,7 @@ def _declare(lib):
         "pa_query_section": (vp, [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i64)]),
         "pa_query_fetch": (i64, [vp, vp, i64, vp, vp, vp]),
         "pa_query_matched_docs": (i64, [vp]),
+        "pa_query_key_layout": (ctypes.c_int, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "pa_query_stats": (ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "pa_query_plan": (ctypes.c_int, [vp] + [ctypes.POINTER(i32)] * 7),
         "pa_query_destroy": (None, [vp]),

@@ -366,6 +366,8 @@ int to_cnf(const pa_query_spec& spec, std::vector<Clause>& out) {
 constexpr size_t kFetchWholeBlockBytes = 1 << 20;
 constexpr size_t kPartLdsBytes = 64 * 1024;  // pass C accumulators of one partition (2 workgroups per CU)
 constexpr int64_t kMaxParts = 4096;          // partition counters of the scan passes: 16 KiB of LDS
+constexpr int64_t kDirectMaxKeys = int64_t(1) << 27;  // direct-indexed key space limit (beyond: hashed keys)
+constexpr uint64_t kMaxHashSlots = uint64_t(1) << 28;
 
 struct Section {
   int32_t kind;
@@ -410,6 +412,10 @@ struct pa_query {
   void* fetch_host = nullptr;        // pinned copy of the compacted rows
   int lane_major = 0;
   int has_mv = 0;
+  bool hashed = false;           // packed 64-bit keys through a global open-addressing table
+  int64_t ht_slots = 0;
+  int key_shift[PA_MAX_GROUP_BY] = {0};
+  int keys_section = -1;
   bool partitioned = false;      // partitioned aggregation (STRAT_PCOUNT / STRAT_PSCATTER passes + part_agg_kernel)
   int part_P = 0, part_shift = 0, rec_words = 0, part_lds_c = 0;
   std::vector<int> pay_off, part_agg_lds;
@@ -635,15 +641,58 @@ int pa_query_prepare(pa_query* q) {
   for (int a = 0; a < s.num_aggs; ++a)
     if (s.aggs[a].type != PA_AGG_COUNT) slot_post[agg_slot[a]] = 1;
 
-  // ---- key space
+  // ---- key space. Direct: table-wide key id = sum_j id_j * prod_{k<j} card_k (DictionaryBasedGroupKeyGenerator raw
+  // key) indexes the accumulators, when every group-by column has a dictionary and the product fits kDirectMaxKeys.
+  // Hashed: the components (dictionary key ids, raw value bits for no-dictionary columns) are packed side by side into
+  // one 64-bit key, mapped to an accumulator slot by a global open-addressing table (the IntMap / LongMap /
+  // NoDictionary*GroupKeyGenerator holders of the reference).
+  q->hashed = false;
+  std::vector<int> gb_bits(s.num_group_by, 0);
+  std::vector<char> gb_raw(s.num_group_by, 0);
+  bool direct_ok = true;
   int64_t K = 1;
   std::vector<int64_t> stride(s.num_group_by);
   for (int j = 0; j < s.num_group_by; ++j) {
-    if (s.group_by_cardinality[j] < 1) return fail(PA_EINVAL, "group_by_cardinality < 1");
+    auto it = q->segs[0]->cols.find(s.group_by_columns[j]);
+    if (it == q->segs[0]->cols.end()) return fail(PA_EINVAL, "group-by column missing in segment 0");
+    if (it->second->kind == COL_SV_RAW) {
+      gb_raw[j] = 1;
+      const int vt = it->second->vtype;
+      gb_bits[j] = (vt == PA_INT || vt == PA_FLOAT) ? 32 : 64;
+      direct_ok = false;
+      continue;
+    }
+    const int64_t card = s.group_by_cardinality[j];
+    if (card < 1) return fail(PA_EINVAL, "group_by_cardinality < 1 for a dictionary column");
+    gb_bits[j] = std::max(1, 64 - __builtin_clzll((unsigned long long)std::max<int64_t>(card - 1, 1)));
     stride[j] = K;
-    if (K > (int64_t(1) << 40) / s.group_by_cardinality[j])
-      return fail(PA_EUNSUPPORTED, "group key space too large for direct addressing (hash fallback not implemented)");
-    K *= s.group_by_cardinality[j];
+    if (K > kDirectMaxKeys / card) direct_ok = false;
+    else K *= card;
+  }
+  if (!direct_ok) {
+    int total_bits = 0;
+    for (int j = 0; j < s.num_group_by; ++j) {
+      if (total_bits + gb_bits[j] > 64) return fail(PA_EUNSUPPORTED, "packed group key wider than 64 bits");
+      stride[j] = total_bits < 64 ? (int64_t)(uint64_t(1) << total_bits) : 0;
+      q->key_shift[j] = total_bits;
+      total_bits += gb_bits[j];
+    }
+    // slots: twice the keys that can exist (docs, or docs x values for MV group-by), at least 1024, a power of two
+    uint64_t bound = 0;
+    for (int si = 0; si < q->nseg; ++si) {
+      uint64_t n = (uint64_t)q->segs[si]->num_docs;
+      for (int j = 0; j < s.num_group_by; ++j) {
+        auto it = q->segs[si]->cols.find(s.group_by_columns[j]);
+        if (it != q->segs[si]->cols.end() && it->second->kind == COL_MV_DICT)
+          n = std::max<uint64_t>(n, (uint64_t)it->second->total_values) * 2;
+      }
+      bound += n;
+    }
+    uint64_t H = 1024;
+    while (H < 2 * bound && H < kMaxHashSlots) H <<= 1;
+    q->hashed = true;
+    q->ht_slots = (int64_t)H;
+    K = (int64_t)H + 1;  // + the reserved slot of the key INT64_MAX (the table's empty marker)
   }
   q->num_keys = K;
 
@@ -740,8 +789,13 @@ int pa_query_prepare(pa_query* q) {
     // group-by remaps
     for (int j = 0; j < s.num_group_by; ++j) {
       const DevCol& dc = d.cols[gb_slot[j]];
+      if (gb_raw[j]) {
+        if (dc.kind != COL_SV_RAW || dc.vtype != q->segs[0]->cols.at(s.group_by_columns[j])->vtype)
+          return fail(PA_EINVAL, "a raw group-by column must be raw with the same type in every segment");
+        continue;
+      }
       if (dc.kind != COL_SV_DICT && dc.kind != COL_MV_DICT)
-        return fail(PA_EUNSUPPORTED, "group-by on non-dictionary columns is not implemented yet");
+        return fail(PA_EINVAL, "group-by column is dictionary-encoded in segment 0 but not here");
       if (dc.kind == COL_MV_DICT) q->has_mv = 1;
       if (q->has_remap[si][j]) {
         void* dp = nullptr;
@@ -817,7 +871,12 @@ int pa_query_prepare(pa_query* q) {
     }
     q->agg_section[a] = (int)sec.size() - 1;
   }
-  sec.push_back({PA_ACC_DOCS_U64, 1});  // numDocsScanned (last section)
+  q->keys_section = -1;
+  if (q->hashed) {
+    sec.push_back({PA_ACC_KEYS_I64, K});  // slot -> packed key (INT64_MAX = empty)
+    q->keys_section = (int)sec.size() - 1;
+  }
+  sec.push_back({PA_ACC_DOCS_U64, 2});  // [0] numDocsScanned, [1] group-table overflows (last section)
   size_t total = 0;
   std::vector<size_t> offs;
   for (auto& x : sec) {
@@ -927,7 +986,7 @@ int pa_query_prepare(pa_query* q) {
   };
   Plan plan;
   q->strategy = STRAT_GLOBAL;
-  if (!(s.flags & PA_QF_FORCE_GLOBAL) && lds_acc <= 64 * 1024 && (dense || (s.flags & PA_QF_FORCE_LDS))) {
+  if (!(s.flags & PA_QF_FORCE_GLOBAL) && !q->hashed && lds_acc <= 64 * 1024 && (dense || (s.flags & PA_QF_FORCE_LDS))) {
     plan = plan_pick(STRAT_LDS);
     if (plan.score >= 0) q->strategy = STRAT_LDS;
   }
@@ -935,7 +994,8 @@ int pa_query_prepare(pa_query* q) {
   // (count per (workgroup, partition); write one record per matching doc into its partition) + one LDS aggregation
   // per partition, instead of ~(1 + aggregations) device-scope atomics per matching doc on random keys.
   q->partitioned = false;
-  if (q->strategy == STRAT_GLOBAL && dense && !q->has_mv && !(s.flags & (PA_QF_NO_PARTITION | PA_QF_FORCE_GLOBAL)) &&
+  if (q->strategy == STRAT_GLOBAL && dense && !q->has_mv && !q->hashed &&
+      !(s.flags & (PA_QF_NO_PARTITION | PA_QF_FORCE_GLOBAL)) &&
       K <= (int64_t(1) << 32) && q->num_docs < (uint64_t(1) << 31)) {
     bool ok = true;
     size_t per_key = 4;  // u32 count
@@ -1048,6 +1108,11 @@ int pa_query_prepare(pa_query* q) {
   q->num_tiles = (uint64_t)first;
   h.count = (unsigned long long*)q->sections[0].ptr;
   h.matched_docs = (unsigned long long*)q->sections.back().ptr;
+  h.hashed = q->hashed ? 1 : 0;
+  if (q->hashed) {
+    h.ht_mask = q->ht_slots - 1;
+    h.ht_keys = (long long*)q->sections[q->keys_section].ptr;
+  }
   h.has_mv = q->has_mv;
   h.lds_count_off = 0;
   h.lds_acc_bytes = q->strategy == STRAT_LDS ? (uint32_t)lds_acc : (q->partitioned ? (uint32_t)part_hist_bytes : 0);
@@ -1158,7 +1223,7 @@ int pa_query_reset(pa_query* q, void* stream) {
   // one memset of the whole accumulator block, then the MIN/MAX sections to their identities
   PA_HIP(hipMemsetAsync(q->external_acc ? q->external_acc : q->acc.p, 0, q->acc.n, st));
   for (const Section& sc : q->sections) {
-    if (sc.kind == PA_ACC_MIN_I64) PA_HIP(launch_fill_i64((int64_t*)sc.ptr, sc.n, INT64_MAX, st));
+    if (sc.kind == PA_ACC_MIN_I64 || sc.kind == PA_ACC_KEYS_I64) PA_HIP(launch_fill_i64((int64_t*)sc.ptr, sc.n, INT64_MAX, st));
     else if (sc.kind == PA_ACC_MAX_I64) PA_HIP(launch_fill_i64((int64_t*)sc.ptr, sc.n, INT64_MIN, st));
   }
   return PA_OK;
@@ -1200,6 +1265,7 @@ int pa_query_set_accumulator_buffer(pa_query* q, void* device_buffer, uint64_t b
   DevQuery& h = q->hq;
   h.count = (unsigned long long*)(nb + ((char*)h.count - old));
   h.matched_docs = (unsigned long long*)(nb + ((char*)h.matched_docs - old));
+  if (q->hashed) h.ht_keys = (long long*)(nb + ((char*)h.ht_keys - old));
   for (int a = 0; a < h.num_aggs; ++a) {
     if (q->agg_section[a] < 0) continue;
     void* p = q->sections[q->agg_section[a]].ptr;
@@ -1240,10 +1306,14 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
 
   // Decodes `nrows` host rows into the caller's arrays: row r has key key_of(r), count hc[r] and the aggregation
   // section rows at sec(section)[r * per]. Rows with a zero count are skipped when `skip_empty`.
+  // `order` (optional) lists the rows to emit, in output order (hashed key spaces: sorted by packed key).
   auto decode = [&](int64_t nrows, const uint64_t* hc, const std::function<const char*(int)>& sec,
-                    const std::function<int64_t(int64_t)>& key_of, bool skip_empty) -> int64_t {
+                    const std::function<int64_t(int64_t)>& key_of, bool skip_empty,
+                    const std::vector<int64_t>* order) -> int64_t {
     int64_t n = 0;
-    for (int64_t r = 0; r < nrows; ++r) {
+    const int64_t total = order ? (int64_t)order->size() : nrows;
+    for (int64_t oi = 0; oi < total; ++oi) {
+      const int64_t r = order ? (*order)[oi] : oi;
       if (skip_empty && hc[r] == 0) continue;
       if (n < capacity) {
         if (out_keys) out_keys[n] = key_of(r);
@@ -1293,8 +1363,19 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
     PA_HIP(hipStreamSynchronize(st));
     const char* hb = (const char*)q->host_acc;
     auto hsec = [&](int sec) { return hb + ((char*)q->sections[sec].ptr - dbase); };
-    q->last_matched = (int64_t)*(const uint64_t*)hsec((int)q->sections.size() - 1);
-    return decode(K, (const uint64_t*)hsec(0), hsec, [](int64_t r) { return r; }, grouped);
+    const uint64_t* docs = (const uint64_t*)hsec((int)q->sections.size() - 1);
+    q->last_matched = (int64_t)docs[0];
+    if (docs[1]) return fail(PA_EUNSUPPORTED, "group-key table overflow (more distinct groups than slots)");
+    const uint64_t* hc = (const uint64_t*)hsec(0);
+    if (q->hashed) {
+      const int64_t* hk = (const int64_t*)hsec(q->keys_section);
+      std::vector<int64_t> order;
+      for (int64_t r = 0; r < K; ++r)
+        if (hc[r]) order.push_back(r);
+      std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return hk[a] < hk[b]; });
+      return decode(K, hc, hsec, [&](int64_t r) { return hk[r]; }, false, &order);
+    }
+    return decode(K, hc, hsec, [](int64_t r) { return r; }, grouped, nullptr);
   }
 
   // Large key spaces: ordered compaction of the non-empty keys on the GPU (count + scan, then key ids and every
@@ -1307,23 +1388,28 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   }
   const int all = grouped ? 0 : 1;
   uint32_t total = 0;
-  uint64_t md = 0;
+  uint64_t md[2] = {0, 0};
   PA_HIP(launch_compact((const unsigned long long*)q->sections[0].ptr, K, all, (uint32_t*)q->fetch_blocks.p, 0,
                         nullptr, 0, st));
   PA_HIP(hipMemcpyAsync(&total, (uint32_t*)q->fetch_blocks.p + nb, 4, hipMemcpyDeviceToHost, st));
-  PA_HIP(hipMemcpyAsync(&md, q->sections.back().ptr, 8, hipMemcpyDeviceToHost, st));
+  PA_HIP(hipMemcpyAsync(md, q->sections.back().ptr, 16, hipMemcpyDeviceToHost, st));
   PA_HIP(hipStreamSynchronize(st));
-  q->last_matched = (int64_t)md;
+  q->last_matched = (int64_t)md[0];
+  if (md[1]) return fail(PA_EUNSUPPORTED, "group-key table overflow (more distinct groups than slots)");
   const int64_t m = (int64_t)total;
-  const int64_t rows = std::min<int64_t>(m, std::max<int64_t>(capacity, 0));
-  if (rows == 0) return m;
+  const int64_t rows_cap = std::min<int64_t>(m, std::max<int64_t>(capacity, 0));
+  if (rows_cap == 0) return m;
   // staging: keys | count | one block per aggregation section (rows x per x es), 256-byte aligned pieces
   CompactDesc d;
   std::memset(&d, 0, sizeof(d));
   std::vector<int> secs = {0};
   for (int a = 0; a < s.num_aggs; ++a)
     if (q->agg_section[a] >= 0) secs.push_back(q->agg_section[a]);
+  if (q->hashed) secs.push_back(q->keys_section);
+  // hashed key spaces: every non-empty slot is needed to sort by packed key before the capacity cut
+  const int64_t rows_needed = q->hashed ? m : std::min<int64_t>(m, std::max<int64_t>(capacity, 0));
   std::vector<size_t> offs;
+  const int64_t rows = rows_needed;
   size_t bytes = ((size_t)rows * 8 + 255) & ~(size_t)255;
   for (int sec : secs) {
     const Section& sc = q->sections[sec];
@@ -1360,8 +1446,18 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   const int64_t* hkeys = (const int64_t*)hb;
   std::map<int, const char*> hsec;
   for (size_t i = 0; i < secs.size(); ++i) hsec[secs[i]] = hb + offs[i];
+  if (q->hashed) {  // rows are slots: emit them in packed-key order
+    const int64_t* pk = (const int64_t*)hsec[q->keys_section];
+    std::vector<int64_t> order(rows);
+    for (int64_t r = 0; r < rows; ++r) order[r] = r;
+    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return pk[a] < pk[b]; });
+    order.resize(rows_cap);
+    decode(rows, (const uint64_t*)hsec[0], [&](int sec) { return hsec[sec]; }, [&](int64_t r) { return pk[r]; },
+           false, &order);
+    return m;
+  }
   decode(rows, (const uint64_t*)hsec[0], [&](int sec) { return hsec[sec]; }, [&](int64_t r) { return hkeys[r]; },
-         false);
+         false, nullptr);
   return m;
 }
 
@@ -1391,6 +1487,14 @@ int32_t pa_query_num_eager_literals(const pa_query* q) { return q && q->prepared
 int32_t pa_query_lane_major(const pa_query* q) { return q && q->prepared ? q->lane_major : -1; }
 
 int64_t pa_query_matched_docs(const pa_query* q) { return q && q->prepared ? q->last_matched : -1; }
+
+int pa_query_key_layout(const pa_query* q, int32_t* hashed, int32_t* shifts) {
+  if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
+  if (hashed) *hashed = q->hashed ? 1 : 0;
+  if (shifts)
+    for (int j = 0; j < q->spec.num_group_by; ++j) shifts[j] = q->hashed ? q->key_shift[j] : 0;
+  return PA_OK;
+}
 
 void pa_query_destroy(pa_query* q) { delete q; }
 

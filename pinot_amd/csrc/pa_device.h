@@ -115,7 +115,11 @@ struct DevQuery {
   int32_t lane_major;        // 1: scan_lm_kernel (docs 32*lane + i of a tile), 0: scan_kernel (docs 64*i + lane)
   int32_t has_mv;            // a group-by or aggregation column is multi-value: per-lane key expansion path
   int32_t pad2;
-  unsigned long long* matched_docs;  // [1]: docs that passed the filter (numDocsScanned)
+  unsigned long long* matched_docs;  // [0]: docs that passed the filter (numDocsScanned), [1]: group-table overflows
+  int32_t hashed;            // packed keys through the open-addressing table ht_keys (gb_stride = 1 << shift)
+  int32_t pad3;
+  int64_t ht_mask;           // table slots - 1 (power of two); slot ht_mask + 1 is reserved for the key INT64_MAX
+  long long* ht_keys;        // slot -> packed key, INT64_MAX = empty
   int32_t part_shift;        // partitioned aggregation: 1 << part_shift table-wide keys per partition
   int32_t num_parts;
   int32_t rec_words;         // words per record: key + values

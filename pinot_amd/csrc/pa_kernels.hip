@@ -230,24 +230,72 @@ struct Acc {
   }
 };
 
+// Group-key component of one doc for group-by column j: the table-wide key id of a dictionary column (remapped), or
+// the value bits of a raw column (hashed key space: INT/FLOAT 32 bits, LONG/DOUBLE 64 bits).
+__device__ __forceinline__ uint64_t gb_component(const DevCol& c, const int32_t* remap, const uint32_t* img,
+                                                 int doc_local, int64_t doc) {
+  if (c.kind == COL_SV_RAW) {
+    switch (c.vtype) {
+      case PA_INT: return (uint64_t)(uint32_t)gp((const int32_t*)c.raw)[doc];
+      case PA_FLOAT: return (uint64_t)gp((const uint32_t*)c.raw)[doc];
+      default: return (uint64_t)gp((const int64_t*)c.raw)[doc];
+    }
+  }
+  uint32_t id = decode_dict_id(c, img, doc_local, doc);
+  if (remap != nullptr) id = (uint32_t)gp(remap)[id];
+  return id;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+
+// Hashed key space: the accumulator slot of a packed key (linear probing; insert by CAS on the empty marker
+// INT64_MAX, which itself lives in the reserved slot ht_mask + 1). -1 if the table is full (counted as an overflow:
+// the query then fails loudly at fetch).
+__device__ __forceinline__ int64_t key_slot(const DevQuery* __restrict__ q, int64_t key) {
+  if (!q->hashed) return key;
+  const int64_t mask = q->ht_mask;
+  if (key == INT64_MAX) return mask + 1;
+  AS1 long long* keys = gp(q->ht_keys);
+  int64_t h = (int64_t)(mix64((uint64_t)key) & (uint64_t)mask);
+  for (int64_t probe = 0; probe <= mask; ++probe) {
+    long long cur = __hip_atomic_load(keys + h, RLX);
+    if (cur == key) return h;
+    if (cur == INT64_MAX) {
+      long long expected = INT64_MAX;
+      if (__hip_atomic_compare_exchange_strong(keys + h, &expected, (long long)key, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT) ||
+          expected == key)
+        return h;
+    }
+    h = (h + 1) & mask;
+  }
+  __hip_atomic_fetch_add(gp(q->matched_docs) + 1, 1ull, RLX);
+  return -1;
+}
+
 // Accumulate the matched lanes (`matched` = wave mask) of one 64-doc step.
 template <int STRAT>
 __device__ __forceinline__ void accumulate_step(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
                                                 const uint32_t* img, int doc_local, int64_t doc,
                                                 uint64_t matched, int lane, const Acc<STRAT>& acc) {
-  const bool mine = (matched >> lane) & 1ull;
-  // table-wide group key (DictionaryBasedGroupKeyGenerator: rawKey = sum dictId_j * prod_{k<j} card_k)
+  bool mine = (matched >> lane) & 1ull;
+  // table-wide group key (DictionaryBasedGroupKeyGenerator: rawKey = sum dictId_j * prod_{k<j} card_k), or the packed
+  // key's accumulator slot in the hashed key space
   int64_t key = 0;
-  for (int j = 0; j < q->num_gb; ++j) {
-    const DevCol& c = seg->cols[q->gb_slot[j]];
-    uint32_t id = 0;
-    if (mine) {
-      id = decode_dict_id(c, img, doc_local, doc);
-      const int32_t* rm = seg->remap[j];
-      if (rm != nullptr) id = (uint32_t)gp(rm)[id];
-    }
-    key += (int64_t)id * q->gb_stride[j];
+  if (mine) {
+    for (int j = 0; j < q->num_gb; ++j)
+      key += (int64_t)(gb_component(seg->cols[q->gb_slot[j]], seg->remap[j], img, doc_local, doc) * (uint64_t)q->gb_stride[j]);
+    key = key_slot(q, key);
+    if (key < 0) mine = false;
   }
+  matched &= __ballot(mine);
 
   uint64_t pending = matched;
   bool first = true;
@@ -374,10 +422,7 @@ __device__ void accumulate_doc_mv(const DevQuery* __restrict__ q, const DevSeg* 
       combos *= mv_n[nmv];
       ++nmv;
     } else {
-      uint32_t id = decode_dict_id(c, img, doc_local, doc);
-      const int32_t* rm = seg->remap[j];
-      if (rm != nullptr) id = (uint32_t)gp(rm)[id];
-      base_key += (int64_t)id * q->gb_stride[j];
+      base_key += (int64_t)(gb_component(c, seg->remap[j], img, doc_local, doc) * (uint64_t)q->gb_stride[j]);
     }
   }
   for (int64_t cb = 0; cb < combos; ++cb) {
@@ -393,6 +438,8 @@ __device__ void accumulate_doc_mv(const DevQuery* __restrict__ q, const DevSeg* 
       if (rm != nullptr) id = (uint32_t)gp(rm)[id];
       key += (int64_t)id * q->gb_stride[j];
     }
+    key = key_slot(q, key);
+    if (key < 0) continue;
     acc.add_count(key, 1u);
     for (int a = 0; a < q->num_aggs; ++a) {
       const DevAgg& A = q->aggs[a];

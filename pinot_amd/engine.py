@@ -221,10 +221,21 @@ class GpuQueryExecutor:
         spec.num_group_by = len(q.group_by)
         if spec.num_group_by > L.PA_MAX_GROUP_BY:
             raise UnsupportedQuery("too many group-by columns")
+        self.raw_group_by = []
         for j, name in enumerate(q.group_by):
+            has_dict = [s.column(name).has_dictionary for s in self.segs]
+            if not any(has_dict):
+                # raw (no-dictionary) column: grouped by value through the hashed key space
+                # (NoDictionarySingleColumnGroupKeyGenerator / NoDictionaryMultiColumnGroupKeyGenerator)
+                self.global_dicts.append(None)
+                self.raw_group_by.append(seg0.column(name).data_type)
+                spec.group_by_columns[j] = ids[name]
+                spec.group_by_cardinality[j] = 0
+                continue
+            if not all(has_dict):
+                raise UnsupportedQuery("group-by column %s is dictionary-encoded in some segments only" % name)
+            self.raw_group_by.append(None)
             dicts = [s.column(name).dictionary for s in self.segs]
-            if any(not s.column(name).has_dictionary for s in self.segs):
-                raise UnsupportedQuery("group-by on a no-dictionary column")
             first = dicts[0]
             same = all(d is first or (len(d) == len(first) and np.array_equal(d, first)) for d in dicts)
             gd = first if same else np.unique(np.concatenate(dicts))
@@ -236,7 +247,7 @@ class GpuQueryExecutor:
             for j, name in enumerate(q.group_by):
                 d = seg.column(name).dictionary
                 gd = self.global_dicts[j]
-                if d is gd or (len(d) == len(gd) and np.array_equal(d, gd)):
+                if gd is None or d is gd or (len(d) == len(gd) and np.array_equal(d, gd)):
                     rm.append(None)
                 else:
                     rm.append(np.searchsorted(gd, d).astype(np.int32))
@@ -251,7 +262,8 @@ class GpuQueryExecutor:
             for seg in self.segs:
                 prod = 1
                 for name in q.group_by:
-                    prod *= seg.column(name).cardinality
+                    col = seg.column(name)
+                    prod *= col.cardinality if col.has_dictionary else seg.num_docs
                 mv = any(not seg.column(name).single_value for name in q.group_by)
                 if (prod if mv else min(prod, seg.num_docs)) > lim:
                     self.num_groups_limit_may_bind = True
@@ -288,11 +300,15 @@ class GpuQueryExecutor:
             L.check(lib.pa_query_bind_segment(self.handle, si, g.handle, arr, rms), "pa_query_bind_segment")
         L.check(lib.pa_query_prepare(self.handle), "pa_query_prepare")
         self.num_keys = int(lib.pa_query_num_keys(self.handle))
+        hashed, shifts = ctypes.c_int32(), (ctypes.c_int32 * max(1, len(q.group_by)))()
+        L.check(lib.pa_query_key_layout(self.handle, ctypes.byref(hashed), shifts), "pa_query_key_layout")
+        self.hashed = bool(hashed.value)
+        self.key_shifts = list(shifts)[:len(q.group_by)]
         self.strides = []
         s = 1
         for gd in self.global_dicts:
             self.strides.append(s)
-            s *= len(gd)
+            s *= len(gd) if gd is not None else 1
 
     # ------------------------------------------------------------------ execution
     def execute(self, stream=None):
@@ -350,8 +366,30 @@ class GpuQueryExecutor:
         return keys[:n], counts[:n], outs
 
     def key_values(self, keys):
-        """Table-wide key ids -> one value array per group-by column (DictionaryBasedGroupKeyGenerator.getKeys)."""
-        return [gd[(keys // st) % len(gd)] for gd, st in zip(self.global_dicts, self.strides)]
+        """Keys -> one value array per group-by column (DictionaryBasedGroupKeyGenerator.getKeys). Direct key space:
+        key = sum id_j * prod_{k<j} card_k. Hashed (pa_query_key_layout): component j at bit shift_j, a table-wide key
+        id for dictionary columns, the value bits for raw ones (INT/FLOAT 32 bits, LONG/DOUBLE 64)."""
+        if not self.hashed:
+            return [gd[(keys // st) % len(gd)] for gd, st in zip(self.global_dicts, self.strides)]
+        k = np.asarray(keys, dtype=np.int64).view(np.uint64)
+        out = []
+        for gd, raw, sh in zip(self.global_dicts, self.raw_group_by, self.key_shifts):
+            if gd is not None:
+                bits = max(1, int(len(gd) - 1).bit_length())
+            else:
+                bits = 32 if raw in ("INT", "FLOAT") else 64
+            comp = (k >> np.uint64(sh)) & np.uint64((1 << bits) - 1) if bits < 64 else (k >> np.uint64(sh))
+            if gd is not None:
+                out.append(gd[comp.astype(np.int64)])
+            elif raw == "INT":
+                out.append(comp.astype(np.uint32).view(np.int32))
+            elif raw == "FLOAT":
+                out.append(comp.astype(np.uint32).view(np.float32))
+            elif raw == "LONG":
+                out.append(comp.view(np.int64))
+            else:
+                out.append(comp.view(np.float64))
+        return out
 
     def fetch(self, stream=None) -> IntermediateResult:
         lib = L.lib()

@@ -19,6 +19,7 @@ SECTION_OP = {
     L.PA_ACC_MAX_I64: dist.ReduceOp.MAX,
     L.PA_ACC_HLL_U32: dist.ReduceOp.MAX,
     L.PA_ACC_DOCS_U64: dist.ReduceOp.SUM,
+    L.PA_ACC_KEYS_I64: None,  # not element-wise reducible (hashed key spaces)
 }
 SECTION_DTYPE = {
     L.PA_ACC_COUNT_U64: torch.int64,
@@ -29,6 +30,7 @@ SECTION_DTYPE = {
     L.PA_ACC_MAX_I64: torch.int64,
     L.PA_ACC_HLL_U32: torch.int32,  # registers are < 32: signed max == unsigned max
     L.PA_ACC_DOCS_U64: torch.int64,
+    L.PA_ACC_KEYS_I64: torch.int64,
 }
 
 
@@ -49,10 +51,26 @@ def reduce_sections(views, dst=0, group=None, all_reduce=False):
             dist.reduce(t, dst=dst, op=SECTION_OP[kind], group=group)
 
 
+def merge_results_across_ranks(executor, dst=0, group=None):
+    """Key-based merge for hashed key spaces (accumulator slots differ per GPU, so sections cannot be reduced element-
+    wise): every rank fetches its groups and rank `dst` merges them by key value (GroupByCombineOperator / broker
+    reduce semantics, reduce.merge_intermediate). Returns the merged IntermediateResult on `dst`, None elsewhere."""
+    from .reduce import merge_intermediate
+    res = executor.fetch()
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    gathered = [None] * world if rank == dst else None
+    dist.gather_object(res, gathered, dst=dst, group=group)
+    return merge_intermediate(gathered) if rank == dst else None
+
+
 class DistributedAccumulators:
-    """Moves an executor's accumulators into one torch-owned device block and reduces it across ranks."""
+    """Moves an executor's accumulators into one torch-owned device block and reduces it across ranks (direct key
+    spaces: the same key id addresses the same accumulator row on every GPU)."""
 
     def __init__(self, executor, device):
+        if getattr(executor, "hashed", False):
+            raise L.PinotAmdError("hashed key space: merge with merge_results_across_ranks (slots differ per GPU)")
         lib = L.lib()
         nbytes = int(lib.pa_query_accumulator_bytes(executor.handle))
         self.buf = torch.zeros(nbytes + 512, dtype=torch.uint8, device=device)

@@ -287,6 +287,61 @@ def test_partitioned_aggregation(flags):
             g.close()
 
 
+@pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LANE_MAJOR])
+def test_raw_group_by_hashed(flags):
+    """GROUP BY raw (no-dictionary) columns — INT, LONG, DOUBLE, and mixed with dictionary columns — through the hashed
+    key space (NoDictionarySingle/MultiColumnGroupKeyGenerator semantics: groups by value), small and large fetch
+    paths, filters on the same raw columns; identical to the oracle."""
+    cols = {"d1": ("INT", 40), "m": ("LONG", 300), "r2": ("INT", 0), "r3": ("LONG", 0), "r1": ("DOUBLE", 0)}
+    small = [make_segment(80 + i, n, cols, no_dict=("r1", "r2", "r3")) for i, n in enumerate((9001, 3001))]
+    queries = [
+        "SELECT r2, COUNT(*), SUM(m), MAX(m) FROM t GROUP BY r2 LIMIT 100000",
+        "SELECT d1, r2, COUNT(*), MIN(m), SUM(r3) FROM t WHERE r2 > 0 GROUP BY d1, r2 LIMIT 100000",
+        "SELECT r3, COUNT(*), MIN(m), SUM(r2) FROM t WHERE r2 > 0 GROUP BY r3 LIMIT 100000",
+        "SELECT r2, d1, AVG(m), DISTINCTCOUNTHLL(m) FROM t WHERE d1 < {d1} GROUP BY r2, d1 LIMIT 100000",
+        "SELECT r1, COUNT(*) FROM t WHERE r1 > 50 GROUP BY r1 LIMIT 100000",
+    ]
+    d1 = int(small[0].column("d1").dictionary[20])
+    for sql in queries:
+        got, exp, _ = run_both(sql.format(d1=d1), small, flags=flags, rel=DOUBLE_REL)
+        assert got.groups
+    # large fetch path (accumulator block > 1 MiB): many distinct raw values
+    rng = np.random.default_rng(5)
+    from pinot_amd.segment import create_segment
+    n = 200_000
+    big = create_segment("big", {"r": rng.integers(-(1 << 40), 1 << 40, size=n), "m": rng.integers(0, 100, size=n)},
+                         {"r": "LONG", "m": "INT"}, no_dictionary_columns=("r",))
+    got, exp, _ = run_both("SELECT r, COUNT(*), SUM(m) FROM t GROUP BY r LIMIT 1000000 OPTION(numGroupsLimit=1000000)",
+                           [big], flags=flags)
+    assert len(got.groups) > 190_000
+
+
+def test_packed_key_wider_than_64_bits_is_refused():
+    """Packed group keys hold at most 64 bits (a raw LONG/DOUBLE column takes all of them): refused loudly."""
+    cols = {"d1": ("INT", 40), "r3": ("LONG", 0)}
+    seg = make_segment(85, 1000, cols, no_dict=("r3",))
+    g = GpuSegment(seg)
+    with pytest.raises(L.PinotAmdError):
+        GpuQueryExecutor(parse_sql("SELECT d1, r3, COUNT(*) FROM t GROUP BY d1, r3"), [g])
+    g.close()
+
+
+def test_hashed_dictionary_key_space():
+    """A dictionary-only key space too large to address directly (product of cardinalities > 2^27) is hashed."""
+    cols = {"a": ("INT", 900), "b": ("LONG", 800), "c": ("INT", 400), "m": ("LONG", 1000)}
+    segs = [make_segment(90 + i, n, cols) for i, n in enumerate((30011, 7001))]
+    sql = "SELECT a, b, c, COUNT(*), SUM(m), MIN(m) FROM t GROUP BY a, b, c LIMIT 100000 OPTION(numGroupsLimit=1000000)"
+    gsegs = [GpuSegment(sg) for sg in segs]
+    try:
+        got, exp, ex = run_both(sql, segs, gsegs=gsegs)
+        ex = GpuQueryExecutor(parse_sql(sql), gsegs)
+        assert ex.hashed
+        ex.close()
+    finally:
+        for g in gsegs:
+            g.close()
+
+
 def test_num_groups_limit_guard():
     """Until first-seen trimming runs on the GPU, a query whose numGroupsLimit may bind fails loudly."""
     from pinot_amd.engine import UnsupportedQuery

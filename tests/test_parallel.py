@@ -110,3 +110,47 @@ def test_shard_segments_partition(n, world):
     flat = [i for p in parts for i in p]
     assert flat == list(range(n))  # disjoint, complete, contiguous
     assert max(map(len, parts)) - min(map(len, parts)) <= 1
+
+
+class _FakeExecutor:
+    """Stands in for a GpuQueryExecutor on CPU: fetch() returns this rank's partial groups."""
+
+    def __init__(self, rank):
+        from pinot_amd.engine import IntermediateResult
+        from pinot_amd.query import Aggregation
+        self.res = IntermediateResult([Aggregation("COUNT"), Aggregation("SUM", "m"), Aggregation("MAX", "m")], ["k"])
+        rng = np.random.default_rng(rank)
+        for k in rng.choice(50, size=30, replace=False).tolist():
+            self.res.groups[(k,)] = [int(rng.integers(1, 10)), float(rng.integers(0, 100)), float(rng.integers(0, 9))]
+        self.res.num_docs_scanned = 100 + rank
+
+    def fetch(self):
+        return self.res
+
+
+def _merge_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pinot_amd.parallel import merge_results_across_ranks
+    merged = merge_results_across_ranks(_FakeExecutor(rank), dst=0)
+    if rank == 0:
+        out[0] = (merged.groups, merged.num_docs_scanned)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_key_based_merge_for_hashed_key_spaces():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_merge_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    groups, docs = out[0]
+    exp = {}
+    for r in range(world):
+        for k, (c, sm, mx) in _FakeExecutor(r).res.groups.items():
+            if k in exp:
+                exp[k] = [exp[k][0] + c, exp[k][1] + sm, max(exp[k][2], mx)]
+            else:
+                exp[k] = [c, sm, mx]
+    assert groups == exp
+    assert docs == 201
