@@ -161,7 +161,9 @@ typedef struct {
   int32_t num_aggs;
   pa_agg_spec aggs[PA_MAX_AGGS];
   int32_t flags; /* PA_QF_* */
-  int32_t reserved;
+  int32_t num_groups_limit; /* numGroupsLimit (QueryOptionsUtils / InstancePlanMakerImplV2, default 100000); 0 = none.
+                               When some segment can hold that many distinct groups, the reference's first-seen trimming
+                               runs on the GPU (DictionaryBasedGroupKeyGenerator IntGroupIdMap.getGroupId :992-1017) */
 } pa_query_spec;
 
 #define PA_QF_STAGE_ALL 1  /* stage post-filter columns through LDS even when a filter exists */
@@ -218,7 +220,8 @@ int pa_query_scan(pa_query* q, void* stream);
 #define PA_ACC_MAX_I64 4   /* reduce MAX */
 #define PA_ACC_HLL_U32 5   /* reduce MAX */
 #define PA_ACC_SUM_I64X2 6 /* reduce SUM; [2k] = sum of low 32 bits (unsigned), [2k+1] = sum of high 32 bits */
-#define PA_ACC_DOCS_U64 7  /* reduce SUM; [0] docs that passed the filter (numDocsScanned), [1] group-table overflows */
+#define PA_ACC_DOCS_U64 7  /* reduce SUM; [0] docs that passed the filter (numDocsScanned), [1] group-table overflows,
+                              [2] segments whose distinct groups reached numGroupsLimit */
 #define PA_ACC_KEYS_I64 8  /* hashed key space only: slot -> packed key (INT64_MAX = empty); not element-wise
                               reducible across GPUs (slots differ): merge fetched groups by key instead */
 /* All sections live in one device block of pa_query_accumulator_bytes() bytes (256-byte aligned sections).
@@ -242,6 +245,14 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
 /* numDocsScanned captured by the last pa_query_fetch (docs that passed the filter; with a multi-value group-by this
  * differs from the sum of the group counts), <0 on error. */
 int64_t pa_query_matched_docs(const pa_query* q);
+
+/* numGroupsLimit: 1 if the first-seen trimming path runs for this query (some segment can reach the limit), 0 if
+ * not, <0 if not prepared. */
+int32_t pa_query_limit_trimming(const pa_query* q);
+/* Segments whose distinct groups reached numGroupsLimit in the last pa_query_fetch (the reference's
+ * numGroupsLimitReached is this > 0: GroupByOperator.java:112 per segment, GroupByCombineOperator.java:154 OR), <0 on
+ * error. */
+int64_t pa_query_num_groups_limit_reached(const pa_query* q);
 
 /* Group-key layout. Direct (hashed = 0): key = sum_j id_j * prod_{k<j} cardinality_k. Hashed (hashed = 1, chosen when
  * a group-by column is raw or the product of cardinalities is too large to address): the key packs component j

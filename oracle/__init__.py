@@ -423,9 +423,12 @@ def run_query(query, segments):
     merged = {}
     oaggs, amap = None, None
     scanned = 0
+    limit_reached = False
     for seg in segments:
         res, oaggs, amap, matched = run_segment(query, seg)
         scanned += matched
+        # GroupByOperator.java:112: a segment whose group table holds numGroupsLimit groups; OR over segments
+        limit_reached |= bool(query.group_by) and len(res) >= query.num_groups_limit
         for key, (cnt, row) in res.items():
             if key not in merged:
                 merged[key] = [cnt, [r.copy() if isinstance(r, np.ndarray) else r for r in row]]
@@ -444,6 +447,7 @@ def run_query(query, segments):
     out = IntermediateResult(list(query.aggregations), list(query.group_by))
     out.num_total_docs = sum(s.num_docs for s in segments)
     out.num_docs_scanned = scanned
+    out.num_groups_limit_reached = limit_reached
     if not query.group_by and () not in merged:
         merged[()] = [0, [np.zeros(1 << k[2], np.uint8) if k[0] == "DISTINCTCOUNTHLL" else
                           (0.0 if k[0] in ("SUM", "COUNT", "COUNTMV") else (np.inf if k[0] == "MIN" else -np.inf))

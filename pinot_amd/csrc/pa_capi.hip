@@ -66,6 +66,7 @@ struct Column {
   int32_t nbits = 0;
   int32_t cardinality = 0;
   int64_t total_values = 0;
+  int32_t max_values = 1;   // MV: most values in one row
   bool fits_int32 = false;  // every dictionary value (INT/LONG) fits in int32
   DevBuf words;   // guard + stream + pad (SV dict)
   DevBuf raw;     // raw values (SV raw)
@@ -217,6 +218,8 @@ int pa_segment_add_mv_dict_column(pa_segment* seg, int32_t column_id, const uint
   }
   if (d != nd || (nd > 0 && off[0] != 0)) return fail(PA_EINVAL, "MV bitmap row starts do not match num_docs");
   off[nd] = (int32_t)total_num_values;
+  int32_t max_values = 1;
+  for (int64_t i = 0; i < nd; ++i) max_values = std::max(max_values, off[i + 1] - off[i]);
   for (int64_t ch = 0; ch < num_chunks; ++ch) {  // chunk offsets (big-endian int32) must agree with the bitmap
     const uint8_t* p = fwd_index + 4 * ch;
     const int64_t co = ((int64_t)p[0] << 24) | ((int64_t)p[1] << 16) | ((int64_t)p[2] << 8) | (int64_t)p[3];
@@ -226,6 +229,7 @@ int pa_segment_add_mv_dict_column(pa_segment* seg, int32_t column_id, const uint
   c->kind = COL_MV_DICT;
   c->nbits = num_bits_per_value;
   c->total_values = total_num_values;
+  c->max_values = max_values;
   // guard words | value stream padded to whole 64-value steps | guard words (reads stay in bounds)
   const int64_t stream_words = ((total_num_values + 2047) / 2048) * 64 * num_bits_per_value;
   const int64_t total_words = kGuardWords + stream_words + kGuardWords;
@@ -421,6 +425,13 @@ struct pa_query {
   std::vector<int> pay_off, part_agg_lds;
   DevBuf part_hist, part_base, recs;
   int64_t last_matched = -1;  // numDocsScanned read by the last fetch
+  int64_t last_reached = -1;  // segments that reached numGroupsLimit, read by the last fetch
+  // numGroupsLimit first-seen trimming (launch_limit_passes): on when some segment can hold numGroupsLimit groups
+  bool limit_mode = false;
+  LimitDesc limit{};
+  int limit_grid = 0;
+  DevBuf lim_keys, lim_pos, lim_sk, lim_sorted, lim_thresh, lim_temp;
+  size_t lim_temp_bytes = 0;
   std::vector<LmSegPlan> hplans;
   std::vector<DevBuf> owned;  // LUTs, remaps, HLL LUTs
   DevBuf acc;                 // all accumulator sections (unless the caller provided the block)
@@ -435,6 +446,12 @@ struct pa_query {
     dev_free(part_hist);
     dev_free(part_base);
     dev_free(recs);
+    dev_free(lim_keys);
+    dev_free(lim_pos);
+    dev_free(lim_sk);
+    dev_free(lim_sorted);
+    dev_free(lim_thresh);
+    dev_free(lim_temp);
     if (host_acc) (void)hipHostFree(host_acc);
     dev_free(fetch_blocks);
     dev_free(fetch_stage);
@@ -696,6 +713,45 @@ int pa_query_prepare(pa_query* q) {
   }
   q->num_keys = K;
 
+  // ---- numGroupsLimit. The reference caps each segment's group table at numGroupsLimit first-seen groups
+  // (DictionaryBasedGroupKeyGenerator._globalGroupIdUpperBound, NoDictionary*GroupKeyGenerator). It can only bind
+  // when a segment can hold that many distinct keys: min(product of its key cardinalities (a raw column: its docs),
+  // its expanded (doc, key) pairs). Then the first-seen trimming passes run instead of the fused scan.
+  q->limit_mode = false;
+  uint64_t limit_pairs = 0;  // bound on distinct (segment, key) pairs
+  int limit_eb = 0;
+  if (s.num_group_by > 0 && s.num_groups_limit > 0) {
+    auto sat_mul = [](uint64_t a, uint64_t b) { return (b != 0 && a > UINT64_MAX / b) ? UINT64_MAX : a * b; };
+    uint64_t max_exp = 1;
+    for (int si = 0; si < q->nseg; ++si) {
+      const pa_segment* seg = q->segs[si];
+      uint64_t distinct = 1, per_doc = 1;
+      int nmv = 0;
+      int64_t mv_total = 0;
+      for (int j = 0; j < s.num_group_by; ++j) {
+        auto it = seg->cols.find(s.group_by_columns[j]);
+        if (it == seg->cols.end()) return fail(PA_EINVAL, "group-by column missing in segment " + std::to_string(si));
+        const Column* c = it->second;
+        distinct = sat_mul(distinct, c->kind == COL_SV_RAW ? (uint64_t)seg->num_docs : (uint64_t)c->cardinality);
+        if (c->kind == COL_MV_DICT) {
+          per_doc = sat_mul(per_doc, (uint64_t)c->max_values);
+          mv_total = c->total_values;
+          ++nmv;
+        }
+      }
+      const uint64_t pairs = nmv == 1 ? (uint64_t)mv_total : sat_mul((uint64_t)seg->num_docs, per_doc);
+      const uint64_t bound = std::min(distinct, pairs);
+      if (bound >= (uint64_t)s.num_groups_limit) q->limit_mode = true;
+      limit_pairs = std::min<uint64_t>(UINT64_MAX / 4, limit_pairs + bound);
+      max_exp = std::max(max_exp, per_doc);
+    }
+    while (limit_eb < 63 && (uint64_t(1) << limit_eb) < max_exp) ++limit_eb;
+    if (q->limit_mode) {
+      if (limit_eb > 21) return fail(PA_EUNSUPPORTED, "numGroupsLimit trimming: more than 2^21 group keys in one doc");
+      if (q->nseg >= 4095) return fail(PA_EUNSUPPORTED, "numGroupsLimit trimming: more than 4094 segments in one query");
+    }
+  }
+
   // ---- per-segment descriptors
   q->hsegs.assign(q->nseg, DevSeg{});
   std::vector<char> staged(nslots, 0);
@@ -876,7 +932,7 @@ int pa_query_prepare(pa_query* q) {
     sec.push_back({PA_ACC_KEYS_I64, K});  // slot -> packed key (INT64_MAX = empty)
     q->keys_section = (int)sec.size() - 1;
   }
-  sec.push_back({PA_ACC_DOCS_U64, 2});  // [0] numDocsScanned, [1] group-table overflows (last section)
+  sec.push_back({PA_ACC_DOCS_U64, 3});  // [0] numDocsScanned, [1] group-table overflows, [2] limit reached (last)
   size_t total = 0;
   std::vector<size_t> offs;
   for (auto& x : sec) {
@@ -986,7 +1042,8 @@ int pa_query_prepare(pa_query* q) {
   };
   Plan plan;
   q->strategy = STRAT_GLOBAL;
-  if (!(s.flags & PA_QF_FORCE_GLOBAL) && !q->hashed && lds_acc <= 64 * 1024 && (dense || (s.flags & PA_QF_FORCE_LDS))) {
+  if (!(s.flags & PA_QF_FORCE_GLOBAL) && !q->limit_mode && !q->hashed && lds_acc <= 64 * 1024 &&
+      (dense || (s.flags & PA_QF_FORCE_LDS))) {
     plan = plan_pick(STRAT_LDS);
     if (plan.score >= 0) q->strategy = STRAT_LDS;
   }
@@ -994,7 +1051,7 @@ int pa_query_prepare(pa_query* q) {
   // (count per (workgroup, partition); write one record per matching doc into its partition) + one LDS aggregation
   // per partition, instead of ~(1 + aggregations) device-scope atomics per matching doc on random keys.
   q->partitioned = false;
-  if (q->strategy == STRAT_GLOBAL && dense && !q->has_mv && !q->hashed &&
+  if (q->strategy == STRAT_GLOBAL && dense && !q->has_mv && !q->hashed && !q->limit_mode &&
       !(s.flags & (PA_QF_NO_PARTITION | PA_QF_FORCE_GLOBAL)) &&
       K <= (int64_t(1) << 32) && q->num_docs < (uint64_t(1) << 31)) {
     bool ok = true;
@@ -1161,6 +1218,36 @@ int pa_query_prepare(pa_query* q) {
     h.recs = (uint32_t*)q->recs.p;
   }
 
+  if (q->limit_mode) {
+    // first-seen table: twice the (segment, key) pairs that can exist, a power of two
+    uint64_t H = 1024;
+    while (H < 2 * limit_pairs && H <= (uint64_t(1) << 30)) H <<= 1;
+    if (H > (uint64_t(1) << 30))
+      return fail(PA_EUNSUPPORTED, "numGroupsLimit trimming: more than 2^29 distinct (segment, group) pairs possible");
+    const size_t hb = (size_t)H * 8;
+    rc = dev_alloc(q->lim_keys, hb);
+    if (!rc) rc = dev_alloc(q->lim_pos, hb);
+    if (!rc) rc = dev_alloc(q->lim_sk, hb);
+    if (!rc) rc = dev_alloc(q->lim_sorted, hb);
+    if (!rc) rc = dev_alloc(q->lim_thresh, (size_t)std::max(1, q->nseg) * 8);
+    if (rc) return rc;
+    q->lim_temp_bytes = 0;
+    PA_HIP(sort_u64(nullptr, &q->lim_temp_bytes, nullptr, nullptr, (int64_t)H, nullptr));
+    rc = dev_alloc(q->lim_temp, std::max<size_t>(q->lim_temp_bytes, 16));
+    if (rc) return rc;
+    LimitDesc& F = q->limit;
+    F.fkeys = (long long*)q->lim_keys.p;
+    F.fpos = (unsigned long long*)q->lim_pos.p;
+    F.fmask = (int64_t)H - 1;
+    F.sk = (unsigned long long*)q->lim_sk.p;
+    F.sorted = (unsigned long long*)q->lim_sorted.p;
+    F.thresh = (unsigned long long*)q->lim_thresh.p;
+    F.reached = h.matched_docs + 2;
+    F.limit = s.num_groups_limit;
+    F.eb = limit_eb;
+    q->limit_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * 16, first));
+  }
+
   // ---- upload descriptors
   rc = dev_alloc(q->dq, sizeof(DevQuery));
   if (rc) return rc;
@@ -1232,6 +1319,21 @@ int pa_query_reset(pa_query* q, void* stream) {
 int pa_query_scan(pa_query* q, void* stream) {
   if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
   if (q->num_tiles == 0) return PA_OK;
+  if (q->limit_mode) {  // first-seen positions, sort, thresholds, admitted aggregation
+    hipStream_t st = (hipStream_t)stream;
+    const DevQuery* dq = (const DevQuery*)q->dq.p;
+    const DevSeg* ds = (const DevSeg*)q->dsegs.p;
+    const LimitDesc& F = q->limit;
+    const int64_t H = F.fmask + 1;
+    PA_HIP(launch_fill_i64((int64_t*)F.fkeys, H, INT64_MAX, st));
+    PA_HIP(launch_fill_i64((int64_t*)F.fpos, H, -1, st));
+    PA_HIP(launch_fill_i64((int64_t*)F.thresh, std::max(1, q->nseg), -1, st));
+    PA_HIP(launch_limit_passes(dq, ds, F, q->limit_grid, 0, st));
+    size_t tb = q->lim_temp_bytes;
+    PA_HIP(sort_u64(q->lim_temp.p, &tb, F.sk, F.sorted, H, st));
+    PA_HIP(launch_limit_passes(dq, ds, F, q->limit_grid, 1, st));
+    return PA_OK;
+  }
   if (q->partitioned) {  // pass A, per-partition offsets, pass B, pass C
     hipStream_t st = (hipStream_t)stream;
     const DevQuery* dq = (const DevQuery*)q->dq.p;
@@ -1265,6 +1367,7 @@ int pa_query_set_accumulator_buffer(pa_query* q, void* device_buffer, uint64_t b
   DevQuery& h = q->hq;
   h.count = (unsigned long long*)(nb + ((char*)h.count - old));
   h.matched_docs = (unsigned long long*)(nb + ((char*)h.matched_docs - old));
+  if (q->limit_mode) q->limit.reached = h.matched_docs + 2;
   if (q->hashed) h.ht_keys = (long long*)(nb + ((char*)h.ht_keys - old));
   for (int a = 0; a < h.num_aggs; ++a) {
     if (q->agg_section[a] < 0) continue;
@@ -1365,6 +1468,7 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
     auto hsec = [&](int sec) { return hb + ((char*)q->sections[sec].ptr - dbase); };
     const uint64_t* docs = (const uint64_t*)hsec((int)q->sections.size() - 1);
     q->last_matched = (int64_t)docs[0];
+    q->last_reached = (int64_t)docs[2];
     if (docs[1]) return fail(PA_EUNSUPPORTED, "group-key table overflow (more distinct groups than slots)");
     const uint64_t* hc = (const uint64_t*)hsec(0);
     if (q->hashed) {
@@ -1388,13 +1492,14 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   }
   const int all = grouped ? 0 : 1;
   uint32_t total = 0;
-  uint64_t md[2] = {0, 0};
+  uint64_t md[3] = {0, 0, 0};
   PA_HIP(launch_compact((const unsigned long long*)q->sections[0].ptr, K, all, (uint32_t*)q->fetch_blocks.p, 0,
                         nullptr, 0, st));
   PA_HIP(hipMemcpyAsync(&total, (uint32_t*)q->fetch_blocks.p + nb, 4, hipMemcpyDeviceToHost, st));
-  PA_HIP(hipMemcpyAsync(md, q->sections.back().ptr, 16, hipMemcpyDeviceToHost, st));
+  PA_HIP(hipMemcpyAsync(md, q->sections.back().ptr, 24, hipMemcpyDeviceToHost, st));
   PA_HIP(hipStreamSynchronize(st));
   q->last_matched = (int64_t)md[0];
+  q->last_reached = (int64_t)md[2];
   if (md[1]) return fail(PA_EUNSUPPORTED, "group-key table overflow (more distinct groups than slots)");
   const int64_t m = (int64_t)total;
   const int64_t rows_cap = std::min<int64_t>(m, std::max<int64_t>(capacity, 0));
@@ -1487,6 +1592,10 @@ int32_t pa_query_num_eager_literals(const pa_query* q) { return q && q->prepared
 int32_t pa_query_lane_major(const pa_query* q) { return q && q->prepared ? q->lane_major : -1; }
 
 int64_t pa_query_matched_docs(const pa_query* q) { return q && q->prepared ? q->last_matched : -1; }
+
+int32_t pa_query_limit_trimming(const pa_query* q) { return q && q->prepared ? (q->limit_mode ? 1 : 0) : -1; }
+
+int64_t pa_query_num_groups_limit_reached(const pa_query* q) { return q && q->prepared ? q->last_reached : -1; }
 
 int pa_query_key_layout(const pa_query* q, int32_t* hashed, int32_t* shifts) {
   if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");

@@ -55,8 +55,11 @@ __device__ __forceinline__ uint32_t decode_global(const uint32_t* words, int64_t
   return __builtin_amdgcn_alignbit(hi, lo, (~(uint32_t)e1) & 31u) & nbits_mask(nb);
 }
 
+// G: the caller has no staged tile (the per-doc kernels of the numGroupsLimit path): always decode from HBM.
+template <bool G = false>
 __device__ __forceinline__ uint32_t decode_dict_id(const DevCol& c, const uint32_t* img, int doc_local,
                                                    int64_t doc) {
+  if constexpr (G) return decode_global(c.words, doc, c.nbits);
   return c.lds_off >= 0 ? decode_lds(img + c.lds_off, doc_local, c.nbits) : decode_global(c.words, doc, c.nbits);
 }
 
@@ -162,12 +165,13 @@ struct AggValue {
   double d;
 };
 
+template <bool G = false>
 __device__ __forceinline__ AggValue agg_value(const DevAgg& A, int a, const DevSeg* __restrict__ seg,
                                               const uint32_t* img, int doc_local, int64_t doc) {
   AggValue out{0, 0.0};
   const DevCol& c = seg->cols[A.slot];
   if (c.kind == COL_SV_DICT) {
-    const uint32_t id = decode_dict_id(c, img, doc_local, doc);
+    const uint32_t id = decode_dict_id<G>(c, img, doc_local, doc);
     if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
       out.i = gp(seg->hll_lut[a])[id];
     } else if (A.src != SRC_DOUBLE) {
@@ -232,6 +236,7 @@ struct Acc {
 
 // Group-key component of one doc for group-by column j: the table-wide key id of a dictionary column (remapped), or
 // the value bits of a raw column (hashed key space: INT/FLOAT 32 bits, LONG/DOUBLE 64 bits).
+template <bool G = false>
 __device__ __forceinline__ uint64_t gb_component(const DevCol& c, const int32_t* remap, const uint32_t* img,
                                                  int doc_local, int64_t doc) {
   if (c.kind == COL_SV_RAW) {
@@ -241,7 +246,7 @@ __device__ __forceinline__ uint64_t gb_component(const DevCol& c, const int32_t*
       default: return (uint64_t)gp((const int64_t*)c.raw)[doc];
     }
   }
-  uint32_t id = decode_dict_id(c, img, doc_local, doc);
+  uint32_t id = decode_dict_id<G>(c, img, doc_local, doc);
   if (remap != nullptr) id = (uint32_t)gp(remap)[id];
   return id;
 }
@@ -400,6 +405,30 @@ __device__ __forceinline__ void update_one(const DevAgg& A, int64_t key, const A
   }
 }
 
+// COUNT += 1 and every aggregation of one doc into accumulator slot `key`; an MV aggregation column contributes every
+// value of the doc (aggregateGroupByMV / *MVAggregationFunction).
+template <int STRAT, bool G = false>
+__device__ __forceinline__ void update_doc_key(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                               const uint32_t* img, int doc_local, int64_t doc, int64_t key,
+                                               const Acc<STRAT>& acc) {
+  acc.add_count(key, 1u);
+  for (int a = 0; a < q->num_aggs; ++a) {
+    const DevAgg& A = q->aggs[a];
+    if (A.type == PA_AGG_COUNT) continue;
+    const DevCol& c = seg->cols[A.slot];
+    if (c.kind == COL_MV_DICT) {
+      const int32_t v0 = gp(c.mv_off)[doc], v1 = gp(c.mv_off)[doc + 1];
+      if (A.type == PA_AGG_COUNT_MV) {
+        acc.add_i64(A, key, (int64_t)(v1 - v0));
+        continue;
+      }
+      for (int32_t vi = v0; vi < v1; ++vi) update_one<STRAT>(A, key, agg_value_mv(A, a, seg, c, vi), acc);
+    } else {
+      update_one<STRAT>(A, key, agg_value<G>(A, a, seg, img, doc_local, doc), acc);
+    }
+  }
+}
+
 // One matching doc of a query with a multi-value group-by or aggregation column, on its own lane (no wave
 // grouping): the doc expands into the cartesian product of its MV group-by values (DictionaryBasedGroupKeyGenerator
 // .getIntRawKeys; duplicates included, like the reference), and every key receives COUNT += 1 and every aggregation
@@ -440,22 +469,7 @@ __device__ void accumulate_doc_mv(const DevQuery* __restrict__ q, const DevSeg* 
     }
     key = key_slot(q, key);
     if (key < 0) continue;
-    acc.add_count(key, 1u);
-    for (int a = 0; a < q->num_aggs; ++a) {
-      const DevAgg& A = q->aggs[a];
-      if (A.type == PA_AGG_COUNT) continue;
-      const DevCol& c = seg->cols[A.slot];
-      if (c.kind == COL_MV_DICT) {
-        const int32_t v0 = gp(c.mv_off)[doc], v1 = gp(c.mv_off)[doc + 1];
-        if (A.type == PA_AGG_COUNT_MV) {
-          acc.add_i64(A, key, (int64_t)(v1 - v0));
-          continue;
-        }
-        for (int32_t vi = v0; vi < v1; ++vi) update_one<STRAT>(A, key, agg_value_mv(A, a, seg, c, vi), acc);
-      } else {
-        update_one<STRAT>(A, key, agg_value(A, a, seg, img, doc_local, doc), acc);
-      }
-    }
+    update_doc_key<STRAT>(q, seg, img, doc_local, doc, key, acc);
   }
 }
 
@@ -1144,6 +1158,189 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
       }
     }
   }
+}
+
+// ---------------------------------------------------------------- numGroupsLimit: first-seen group trimming
+// The reference's group-key generators hand out group ids per segment in first-seen order — docId order, and within a
+// doc the order getIntRawKeys / getLongRawKeys expand multi-value keys in (DictionaryBasedGroupKeyGenerator.java:473,
+// :668) — and once numGroupsLimit groups exist a new key gets INVALID_ID (IntGroupIdMap.getGroupId :992-1017,
+// LongMapBasedHolder.getGroupId :629-637, NoDictionarySingleColumnGroupKeyGenerator :419): the result holders skip its
+// docs in that segment (DoubleGroupByResultHolder.java:76). So a key is aggregated in segment s iff its first position
+// there (doc << eb | expansion index) is among the numGroupsLimit smallest first positions of the segment's distinct
+// keys. Three steps over all segments at once:
+//   1. limit_first_kernel: atomicMin of the position of every (matching doc, expanded key) into a (segment, key) table;
+//   2. radix-sort the words (segment << 52 | first position) (pa_sort.hip) and read off each segment's L-th smallest
+//      position: threshold T[s] = that position + 1 (limit_threshold_kernel);
+//   3. limit_agg_kernel: the aggregation over matching docs, admitting (doc, key) iff first[s, key] < T[s].
+// These are per-doc kernels (no staged tiles): this path only runs when the limit can bind.
+
+__device__ __forceinline__ bool doc_passes(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int64_t doc) {
+  bool ok = true, any = false;
+  for (int li = 0; li < q->num_leaves; ++li) {
+    const DevLeaf& L = seg->leaves[li];
+    if (ok && !any) any = leaf_match_doc(L, doc);
+    if (L.clause_end) {
+      ok = ok && any;
+      any = false;
+    }
+  }
+  return ok;
+}
+
+// Calls f(e, key) for every group key of one doc, e = the key's index in the reference's expansion: the last group-by
+// column is processed first, and a multi-value column with n values multiplies the keys so far by n with the column's
+// value index as the MORE significant digit (newRawKeys[v * cur + k], getIntRawKeys), i.e. e = sum_t v_t * prod_{t'<t}
+// n_t' over the MV columns taken from the last to the first.
+template <class F>
+__device__ __forceinline__ void for_each_key(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int64_t doc,
+                                             F&& f) {
+  int64_t base = 0;
+  int nmv = 0;
+  int mv_gb[PA_MAX_GROUP_BY];
+  int32_t mv_s[PA_MAX_GROUP_BY], mv_n[PA_MAX_GROUP_BY];
+  int64_t combos = 1;
+  for (int j = q->num_gb - 1; j >= 0; --j) {
+    const DevCol& c = seg->cols[q->gb_slot[j]];
+    if (c.kind == COL_MV_DICT) {
+      const int32_t s0 = gp(c.mv_off)[doc];
+      mv_gb[nmv] = j;
+      mv_s[nmv] = s0;
+      mv_n[nmv] = gp(c.mv_off)[doc + 1] - s0;
+      combos *= mv_n[nmv];
+      ++nmv;
+    } else {
+      base += (int64_t)(gb_component<true>(c, seg->remap[j], nullptr, 0, doc) * (uint64_t)q->gb_stride[j]);
+    }
+  }
+  for (int64_t e = 0; e < combos; ++e) {
+    int64_t key = base;
+    int64_t rem = e;
+    for (int t = 0; t < nmv; ++t) {
+      const int j = mv_gb[t];
+      const DevCol& c = seg->cols[q->gb_slot[j]];
+      const int64_t digit = rem % mv_n[t];
+      rem /= mv_n[t];
+      uint32_t id = decode_global(c.words, mv_s[t] + digit, c.nbits);
+      const int32_t* rm = seg->remap[j];
+      if (rm != nullptr) id = (uint32_t)gp(rm)[id];
+      key += (int64_t)id * q->gb_stride[j];
+    }
+    f(e, key);
+  }
+}
+
+// Slot of composite key ck = accumulator slot * nseg + segment in the first-seen table (linear probing, CAS insert on
+// the empty marker INT64_MAX); -1 when absent (lookup) or when the table is full (counted as an overflow).
+__device__ __forceinline__ int64_t first_slot(const DevQuery* __restrict__ q, const LimitDesc& F, int64_t ck, bool insert) {
+  AS1 long long* keys = gp(F.fkeys);
+  int64_t h = (int64_t)(mix64((uint64_t)ck) & (uint64_t)F.fmask);
+  for (int64_t probe = 0; probe <= F.fmask; ++probe) {
+    long long cur = __hip_atomic_load(keys + h, RLX);
+    if (cur == ck) return h;
+    if (cur == INT64_MAX) {
+      if (!insert) return -1;
+      long long expected = INT64_MAX;
+      if (__hip_atomic_compare_exchange_strong(keys + h, &expected, (long long)ck, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT) ||
+          expected == ck)
+        return h;
+    }
+    h = (h + 1) & F.fmask;
+  }
+  if (insert) __hip_atomic_fetch_add(gp(q->matched_docs) + 1, 1ull, RLX);
+  return -1;
+}
+
+// Grid-stride over the scan's tiles (DevSeg::first_wtile), one doc per thread.
+template <class F>
+__device__ __forceinline__ void for_each_doc(const DevQuery* __restrict__ q, const DevSeg* __restrict__ segs, F&& f) {
+  const int64_t tile_docs = (int64_t)q->steps * kWave;
+  for (int64_t t = blockIdx.x; t < q->total_wtiles; t += gridDim.x) {
+    const int si = find_segment(segs, q->num_segments, t);
+    const DevSeg* seg = segs + si;
+    const int64_t d0 = (t - seg->first_wtile) * tile_docs;
+    const int64_t d1 = min(d0 + tile_docs, (int64_t)seg->num_docs);
+    for (int64_t base = d0; base < d1; base += blockDim.x) f(si, seg, base + threadIdx.x, base + threadIdx.x < d1);
+  }
+}
+
+__global__ void __launch_bounds__(256) limit_first_kernel(const DevQuery* __restrict__ q, const DevSeg* __restrict__ segs,
+                                                          LimitDesc F) {
+  const int nseg = q->num_segments;
+  for_each_doc(q, segs, [&](int si, const DevSeg* seg, int64_t doc, bool valid) {
+    if (!valid || !doc_passes(q, seg, doc)) return;
+    for_each_key(q, seg, doc, [&](int64_t e, int64_t key) {
+      const int64_t slot = key_slot(q, key);
+      if (slot < 0) return;
+      const int64_t fs = first_slot(q, F, slot * nseg + si, true);
+      if (fs < 0) return;
+      __hip_atomic_fetch_min(gp(F.fpos) + fs, ((unsigned long long)doc << F.eb) | (unsigned long long)e, RLX);
+    });
+  });
+}
+
+// sort words: (segment << 52) | first position; empty slots sort last
+__global__ void limit_sortkeys_kernel(const DevQuery* __restrict__ q, LimitDesc F) {
+  const int64_t n = F.fmask + 1;
+  const int nseg = q->num_segments;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const long long ck = F.fkeys[i];
+    F.sk[i] = ck == INT64_MAX ? ~0ull : (((unsigned long long)(ck % nseg) << 52) | F.fpos[i]);
+  }
+}
+
+// sorted words: element i is the L-th of its segment iff sorted[i-L+1] has the same segment and sorted[i-L] does not
+__global__ void limit_threshold_kernel(LimitDesc F, int64_t n) {
+  const int64_t L = F.limit;
+  const unsigned long long* w = F.sorted;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long v = w[i];
+    if (v == ~0ull || i < L - 1) continue;
+    const unsigned long long s = v >> 52;
+    if ((w[i - L + 1] >> 52) != s) continue;
+    if (i - L >= 0 && (w[i - L] >> 52) == s) continue;
+    F.thresh[s] = (v & ((1ull << 52) - 1)) + 1;
+    __hip_atomic_fetch_add(F.reached, 1ull, RLX);  // this segment has >= numGroupsLimit groups
+  }
+}
+
+__global__ void __launch_bounds__(256) limit_agg_kernel(const DevQuery* __restrict__ q, const DevSeg* __restrict__ segs,
+                                                        LimitDesc F) {
+  const Acc<STRAT_GLOBAL> acc{q, nullptr};
+  const int nseg = q->num_segments;
+  const int lane = threadIdx.x & (kWave - 1);
+  for_each_doc(q, segs, [&](int si, const DevSeg* seg, int64_t doc, bool valid) {
+    const bool pass = valid && doc_passes(q, seg, doc);
+    const uint64_t wm = __ballot(pass);
+    if (lane == 0 && wm) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)__builtin_popcountll(wm), RLX);
+    if (!pass) return;
+    const unsigned long long T = F.thresh[si];
+    for_each_key(q, seg, doc, [&](int64_t e, int64_t key) {
+      const int64_t slot = key_slot(q, key);
+      if (slot < 0) return;
+      const int64_t fs = first_slot(q, F, slot * nseg + si, false);
+      if (fs < 0 || F.fpos[fs] >= T) return;  // INVALID_ID: the segment's group table was full at first sight
+      update_doc_key<STRAT_GLOBAL, true>(q, seg, nullptr, 0, doc, slot, acc);
+    });
+  });
+}
+
+hipError_t launch_limit_passes(const DevQuery* q, const DevSeg* segs, const LimitDesc& F, int grid, int phase,
+                               hipStream_t s) {
+  const int64_t n = F.fmask + 1;
+  const int g = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  switch (phase) {
+    case 0:
+      limit_first_kernel<<<grid, 256, 0, s>>>(q, segs, F);
+      limit_sortkeys_kernel<<<g, 256, 0, s>>>(q, F);
+      break;
+    case 1:
+      limit_threshold_kernel<<<g, 256, 0, s>>>(F, n);
+      limit_agg_kernel<<<grid, 256, 0, s>>>(q, segs, F);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- segment-load / query-prep kernels

@@ -17,6 +17,26 @@ struct CompactDesc {
 };
 hipError_t launch_compact(const unsigned long long* count, int64_t K, int all, uint32_t* block_sums, int64_t cap,
                           const CompactDesc* d, int phase, hipStream_t s);
+// numGroupsLimit first-seen trimming (pa_kernels.hip "numGroupsLimit"): the (segment, key) first-position table,
+// the sort buffers and the per-segment thresholds
+struct LimitDesc {
+  long long* fkeys;              // composite key: accumulator slot * num_segments + segment; INT64_MAX = empty
+  unsigned long long* fpos;      // first position (doc << eb | expansion index); UINT64_MAX = none
+  int64_t fmask;                 // slots - 1 (power of two)
+  unsigned long long* sk;        // sort input [slots]
+  unsigned long long* sorted;    // sort output [slots]
+  unsigned long long* thresh;    // [num_segments]: first positions below it are admitted; UINT64_MAX = all
+  unsigned long long* reached;   // segments whose distinct groups reached the limit (GroupByOperator.java:112)
+  int64_t limit;                 // numGroupsLimit
+  int32_t eb;                    // expansion-index bits
+  int32_t pad;
+};
+// phase 0: first-seen positions + sort words; phase 1: thresholds + aggregation
+hipError_t launch_limit_passes(const DevQuery* q, const DevSeg* segs, const LimitDesc& F, int grid, int phase,
+                               hipStream_t s);
+// hipcub radix sort of n 64-bit words (pa_sort.hip); temp == nullptr: *temp_bytes = the scratch size needed
+hipError_t sort_u64(void* temp, size_t* temp_bytes, const unsigned long long* in, unsigned long long* out, int64_t n,
+                    hipStream_t s);
 hipError_t launch_bswap_words(uint32_t* w, int64_t n, hipStream_t s);
 hipError_t launch_hll_lut_numeric(const int64_t* di, const double* dd, int32_t vtype, int32_t card, int32_t log2m,
                                   uint32_t* lut, hipStream_t s);

@@ -254,22 +254,11 @@ class GpuQueryExecutor:
             self.remaps.append(rm)
         spec.flags = self.flags
 
-        # numGroupsLimit (DictionaryBasedGroupKeyGenerator._globalGroupIdUpperBound): the per-segment first-seen
-        # group cap can only bind when a segment could produce more groups than the limit.
-        self.num_groups_limit_may_bind = False
-        if q.group_by:
-            lim = q.num_groups_limit
-            for seg in self.segs:
-                prod = 1
-                for name in q.group_by:
-                    col = seg.column(name)
-                    prod *= col.cardinality if col.has_dictionary else seg.num_docs
-                mv = any(not seg.column(name).single_value for name in q.group_by)
-                if (prod if mv else min(prod, seg.num_docs)) > lim:
-                    self.num_groups_limit_may_bind = True
-            if self.num_groups_limit_may_bind and self.enforce_num_groups_limit:
-                raise UnsupportedQuery("numGroupsLimit=%d may bind for this segment set (first-seen group trimming is "
-                                       "not implemented on the GPU yet); raise OPTION(numGroupsLimit=...)" % lim)
+        # numGroupsLimit (DictionaryBasedGroupKeyGenerator._globalGroupIdUpperBound): the per-segment first-seen group
+        # cap. The library decides whether it can bind and then runs the first-seen trimming passes on the GPU;
+        # enforce_num_groups_limit=False drops the cap (measurement tools only: results then differ from the
+        # reference whenever the cap binds).
+        spec.num_groups_limit = int(min(q.num_groups_limit, 2**31 - 1)) if (q.group_by and self.enforce_num_groups_limit) else 0
 
         self.spec = spec
         self.handle = L.check_ptr(lib.pa_query_create(ctypes.byref(spec), len(self.segs)), "pa_query_create")
@@ -341,6 +330,7 @@ class GpuQueryExecutor:
         out["plan"]["strategy"] = {0: "lds", 1: "global", 2: "partitioned"}[out["plan"]["strategy"]]
         out["plan"]["eager_literals"] = int(L.lib().pa_query_num_eager_literals(self.handle))
         out["plan"]["lane_major"] = int(L.lib().pa_query_lane_major(self.handle))
+        out["plan"]["limit_trimming"] = int(L.lib().pa_query_limit_trimming(self.handle))
         return out
 
     def fetch_arrays(self, stream=None):
@@ -419,7 +409,8 @@ class GpuQueryExecutor:
         rows = list(zip(*cols)) if cols else [()] * n
         if q.group_by:
             res.groups = {tuple(kc[r] for kc in key_cols): list(rows[r]) for r in range(n)}
-            res.num_groups_limit_reached = len(res.groups) >= q.num_groups_limit
+            # GroupByOperator.java:112 per segment, OR-ed by GroupByCombineOperator.java:154
+            res.num_groups_limit_reached = int(L.lib().pa_query_num_groups_limit_reached(self.handle)) > 0
         else:
             res.row = list(rows[0])
         return res

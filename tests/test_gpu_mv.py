@@ -139,3 +139,28 @@ def test_malformed_mv_index_rejected():
     assert lib.pa_segment_add_mv_dict_column(h, 0, good.ctypes.data, good.nbytes, col.num_bits, col.cardinality,
                                              col.total_num_values, L.PA_INT, dv.ctypes.data, None) == 0
     lib.pa_segment_destroy(h)
+
+
+@pytest.mark.parametrize("limit", [1, 37, 101, 700])
+def test_mv_num_groups_limit_trimming(limit):
+    """numGroupsLimit binding inside a doc's key expansion: group ids follow getIntRawKeys order (last group-by
+    column first; a later MV column's value index is the more significant digit), so the cut falls between two keys
+    of one doc exactly where the reference's IntGroupIdMap would put it."""
+    from pinot_amd import parse_sql
+    from pinot_amd.engine import GpuQueryExecutor, GpuSegment
+    mv = (("tags", 30, 4), ("tags2", 9, 3))
+    segs = [mv_segment(11, 9001, mv_cols=mv), mv_segment(12, 2500, mv_cols=mv)]
+    for sql in ("SELECT a, tags2, tags, COUNT(*), SUM(m), MAX(m) FROM t WHERE b > 10 GROUP BY a, tags2, tags "
+                "LIMIT 100000 OPTION(numGroupsLimit=%d)" % limit,
+                "SELECT tags, COUNT(*), SUMMV(tags), DISTINCTCOUNTHLLMV(tags2) FROM t GROUP BY tags LIMIT 100000 "
+                "OPTION(numGroupsLimit=%d)" % (limit % 31 + 1)):
+        gsegs = [GpuSegment(s) for s in segs]
+        try:
+            ex = GpuQueryExecutor(parse_sql(sql), gsegs)
+            assert ex.stats()["plan"]["limit_trimming"] == 1
+            ex.close()
+        finally:
+            for g in gsegs:
+                g.close()
+        got, exp, _ = run_both(sql, segs)
+        assert got.num_groups_limit_reached

@@ -40,6 +40,7 @@ def _close(a, b, rel):
 
 def assert_same(gpu, ora, rel=0.0):
     assert gpu.num_docs_scanned == ora.num_docs_scanned
+    assert gpu.num_groups_limit_reached == ora.num_groups_limit_reached
     if ora.group_by:
         assert set(gpu.groups) == set(ora.groups), (sorted(set(gpu.groups) ^ set(ora.groups))[:5])
         for k, vals in ora.groups.items():
@@ -342,15 +343,80 @@ def test_hashed_dictionary_key_space():
             g.close()
 
 
-def test_num_groups_limit_guard():
-    """Until first-seen trimming runs on the GPU, a query whose numGroupsLimit may bind fails loudly."""
-    from pinot_amd.engine import UnsupportedQuery
+# ------------------------------------------------------------------ numGroupsLimit first-seen trimming
+def _limit_run(sql, segs, expect_trim=True, rel=0.0):
+    q = parse_sql(sql)
+    gsegs = [GpuSegment(sg) for sg in segs]
+    try:
+        ex = GpuQueryExecutor(q, gsegs)
+        try:
+            assert ex.stats()["plan"]["limit_trimming"] == int(expect_trim)
+            got = ex.run()
+        finally:
+            ex.close()
+    finally:
+        for g in gsegs:
+            g.close()
+    exp = oracle.run_query(q, segs)
+    assert_same(got, exp, rel)
+    return got, exp
+
+
+@pytest.mark.parametrize("limit", [1, 7, 300, 5000])
+def test_num_groups_limit_trimming_sv(limit):
+    """Two dictionary dims (~1M possible keys) over segments of different sizes, filtered: each segment keeps its
+    first `limit` groups in docId order (IntGroupIdMap.getGroupId) and drops later keys' docs; the union over segments
+    and numGroupsLimitReached match the oracle's first-seen maps exactly."""
+    cols = {"k1": ("INT", 1000), "k2": ("LONG", 1000), "m": ("LONG", 5000), "f": ("INT", 10)}
+    segs = [make_segment(500 + i, n, cols) for i, n in enumerate((40000, 9001, 123))]
+    sql = ("SELECT k1, k2, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t WHERE f <> 3 GROUP BY k1, k2 LIMIT 100000000 "
+           "OPTION(numGroupsLimit=%d)" % limit)
+    got, exp = _limit_run(sql, segs)
+    assert got.num_groups_limit_reached
+    assert len(exp.groups) <= limit * len(segs)
+
+
+def test_num_groups_limit_default_binds():
+    """Default numGroupsLimit (100000) on a segment with more distinct keys: trimmed on the GPU like the reference."""
     cols = {"k1": ("INT", 1000), "k2": ("LONG", 1000)}
-    seg = make_segment(32, 200000, cols)
-    g = GpuSegment(seg)
-    with pytest.raises(UnsupportedQuery):
-        GpuQueryExecutor(parse_sql("SELECT k1, k2, COUNT(*) FROM t GROUP BY k1, k2"), [g])
-    g.close()
+    segs = [make_segment(32, 200000, cols)]
+    got, exp = _limit_run("SELECT k1, k2, COUNT(*) FROM t GROUP BY k1, k2 LIMIT 100000000", segs)
+    assert len(got.groups) == 100000 and got.num_groups_limit_reached
+
+
+def test_num_groups_limit_not_reached():
+    """The limit can bind in principle (key space > limit) but the filter leaves fewer groups: nothing is trimmed and
+    numGroupsLimitReached stays false."""
+    cols = {"k1": ("INT", 1000), "k2": ("LONG", 1000), "f": ("INT", 1000)}
+    segs = [make_segment(70 + i, 30000, cols) for i in range(2)]
+    got, exp = _limit_run("SELECT k1, k2, COUNT(*) FROM t WHERE f < 2 GROUP BY k1, k2 LIMIT 100000 "
+                          "OPTION(numGroupsLimit=20000)", segs)
+    assert not got.num_groups_limit_reached
+
+
+def test_num_groups_limit_hll_avg_double():
+    """DISTINCTCOUNTHLL, AVG and DOUBLE sums under trimming."""
+    cols = {"k1": ("INT", 300), "k2": ("INT", 200), "u": ("LONG", 50000), "d": ("DOUBLE", 5000)}
+    segs = [make_segment(80 + i, 20000, cols) for i in range(2)]
+    _limit_run("SELECT k1, k2, DISTINCTCOUNTHLL(u), AVG(d), SUM(d) FROM t GROUP BY k1, k2 LIMIT 100000 "
+               "OPTION(numGroupsLimit=1000)", segs, rel=DOUBLE_REL)
+
+
+def test_num_groups_limit_raw_hashed():
+    """No-dictionary group-by (NoDictionarySingle/MultiColumnGroupKeyGenerator: same first-seen cap) through the
+    hashed key space."""
+    cols = {"r": ("INT", 0), "k": ("INT", 50), "m": ("LONG", 1000)}
+    segs = [make_segment(90 + i, 25000, cols, no_dict=("r",)) for i in range(2)]
+    _limit_run("SELECT r, k, COUNT(*), SUM(m) FROM t GROUP BY r, k LIMIT 1000000 OPTION(numGroupsLimit=777)", segs)
+    _limit_run("SELECT r, COUNT(*), MAX(m) FROM t GROUP BY r LIMIT 1000000 OPTION(numGroupsLimit=500)", segs)
+
+
+def test_num_groups_limit_not_triggered_below_bound():
+    """A key space smaller than the limit never runs the trimming passes."""
+    cols = {"k1": ("INT", 20), "k2": ("INT", 30)}
+    segs = [make_segment(99, 5000, cols)]
+    _limit_run("SELECT k1, k2, COUNT(*) FROM t GROUP BY k1, k2 LIMIT 1000 OPTION(numGroupsLimit=601)", segs,
+               expect_trim=False)
 
 
 @pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LANE_MAJOR])
