@@ -28,6 +28,7 @@ PA_QF_WG_SHIFT = 12
 PA_QF_DEBUG_STREAM_ONLY = 1 << 16
 PA_QF_NO_LANE_MAJOR = 1 << 17
 PA_QF_NO_PARTITION = 1 << 21
+PA_QF_PART_SHIFT = 22
 PA_ACC_COUNT_U64, PA_ACC_SUM_I64, PA_ACC_SUM_F64, PA_ACC_MIN_I64, PA_ACC_MAX_I64, PA_ACC_HLL_U32, \
     PA_ACC_SUM_I64X2, PA_ACC_DOCS_U64, PA_ACC_KEYS_I64 = range(9)
 

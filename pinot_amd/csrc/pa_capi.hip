@@ -368,8 +368,9 @@ int to_cnf(const pa_query_spec& spec, std::vector<Clause>& out) {
 }
 
 constexpr size_t kFetchWholeBlockBytes = 1 << 20;
-constexpr size_t kPartLdsBytes = 64 * 1024;  // pass C accumulators of one partition (2 workgroups per CU)
+constexpr size_t kPartLdsChoices[4] = {144 * 1024, 64 * 1024, 96 * 1024, 144 * 1024};  // PA_QF_PART_SHIFT
 constexpr int64_t kMaxParts = 4096;          // partition counters of the scan passes: 16 KiB of LDS
+constexpr size_t kPartBinLdsBytes = 152 * 1024;  // part_bin_kernel: bins + counters (one 1024-thread workgroup per CU)
 constexpr int64_t kDirectMaxKeys = int64_t(1) << 27;  // direct-indexed key space limit (beyond: hashed keys)
 constexpr uint64_t kMaxHashSlots = uint64_t(1) << 28;
 
@@ -420,10 +421,11 @@ struct pa_query {
   int64_t ht_slots = 0;
   int key_shift[PA_MAX_GROUP_BY] = {0};
   int keys_section = -1;
-  bool partitioned = false;      // partitioned aggregation (STRAT_PCOUNT / STRAT_PSCATTER passes + part_agg_kernel)
-  int part_P = 0, part_shift = 0, rec_words = 0, part_lds_c = 0;
+  bool partitioned = false;      // partitioned aggregation (STRAT_PEMIT scan + part_bin_kernel + part_agg_kernel)
+  int part_P = 0, part_shift = 0, rec_words = 0, part_lds_c = 0, bin_slots = 0, bin_iter = 0, bin_parts = 0;
   std::vector<int> pay_off, part_agg_lds;
-  DevBuf part_hist, part_base, recs;
+  DevBuf part_hist, part_off, part_base, recs, emit, wave_cnt;
+  int bin_lds = 0;
   int64_t last_matched = -1;  // numDocsScanned read by the last fetch
   int64_t last_reached = -1;  // segments that reached numGroupsLimit, read by the last fetch
   // numGroupsLimit first-seen trimming (launch_limit_passes): on when some segment can hold numGroupsLimit groups
@@ -444,8 +446,11 @@ struct pa_query {
     dev_free(dsegs);
     dev_free(dplans);
     dev_free(part_hist);
+    dev_free(part_off);
     dev_free(part_base);
     dev_free(recs);
+    dev_free(emit);
+    dev_free(wave_cnt);
     dev_free(lim_keys);
     dev_free(lim_pos);
     dev_free(lim_sk);
@@ -978,11 +983,12 @@ int pa_query_prepare(pa_query* q) {
   for (int si = 0; si < q->nseg && lm; ++si)
     if (q->hsegs[si].num_staged > kLmStaged) lm = false;
   size_t part_hist_bytes = 0;  // partitioned aggregation: the per-partition LDS counters of the scan passes
-  auto plan_for = [&](int strat, bool use_lm) {
+  auto plan_for = [&](int strat, bool use_lm, bool only16 = false) {
     const bool lds_strategy = strat == STRAT_LDS;
     Plan best;
     for (int steps : {32, 16}) {
       if (use_lm && steps != 32) continue;
+      if (only16 && steps != 16) continue;
       if ((s.flags & PA_QF_STEPS16) && steps != 16) continue;
       if ((s.flags & PA_QF_STEPS32) && steps != 32) continue;
       int img_dw = kGuardWords, dma = 0;
@@ -997,7 +1003,7 @@ int pa_query_prepare(pa_query* q) {
         dma = std::max(dma, n);
       }
       const size_t img_bytes = (size_t)img_dw * 4;
-      const size_t acc_b = lds_strategy ? lds_acc : (strat == STRAT_PCOUNT ? part_hist_bytes : 0);
+      const size_t acc_b = lds_strategy ? lds_acc : (strat == STRAT_PEMIT ? part_hist_bytes : 0);
       for (int wg : {4, 3, 2, 1}) {
         if (force_wg && wg != force_wg) continue;
         const size_t per_wg = kLdsBudget / wg;
@@ -1029,9 +1035,13 @@ int pa_query_prepare(pa_query* q) {
   // want the most resident waves (measured, tools/bench_configs.py highcard): there the step-major plan wins when it
   // fits more workgroups per CU.
   auto plan_pick = [&](int strat) {
+    if (strat == STRAT_PEMIT) {  // the emit pass runs 1024-doc step-major tiles only (register budget of its batches)
+      lm = false;
+      return plan_for(strat, false, true);
+    }
     if (!lm) return plan_for(strat, false);
     Plan a = plan_for(strat, true);
-    if ((strat == STRAT_GLOBAL || strat == STRAT_PCOUNT) && dense) {
+    if ((strat == STRAT_GLOBAL || strat == STRAT_PEMIT) && dense) {
       Plan b = plan_for(strat, false);
       if (b.score >= 0 && b.wg_per_cu > a.wg_per_cu) {
         lm = false;
@@ -1053,7 +1063,7 @@ int pa_query_prepare(pa_query* q) {
   q->partitioned = false;
   if (q->strategy == STRAT_GLOBAL && dense && !q->has_mv && !q->hashed && !q->limit_mode &&
       !(s.flags & (PA_QF_NO_PARTITION | PA_QF_FORCE_GLOBAL)) &&
-      K <= (int64_t(1) << 32) && q->num_docs < (uint64_t(1) << 31)) {
+      K < (int64_t(1) << 32) && q->num_docs < (uint64_t(1) << 30)) {
     bool ok = true;
     size_t per_key = 4;  // u32 count
     int words = 1;       // key
@@ -1074,12 +1084,24 @@ int pa_query_prepare(pa_query* q) {
         words += agg_src[a] == SRC_INT ? 1 : 2;
       }
     }
+    words = std::max(words, 2);  // COUNT-only records carry an unused value word: records are >= 8 bytes
     int64_t kr = 1;
-    while (ok && (size_t)(kr * 2) * per_key <= kPartLdsBytes) kr *= 2;
+    const size_t part_lds = kPartLdsChoices[(s.flags >> PA_QF_PART_SHIFT) & 3];
+    while (ok && (size_t)(kr * 2) * per_key <= part_lds) kr *= 2;
     const int64_t P = ok ? (K + kr - 1) / kr : 0;
+    // part_bin_kernel: per-partition LDS bins of kPartGroup..64 records within kPartBinLdsBytes; when even one-group
+    // bins of all P partitions do not fit, groups of bin_parts partitions are binned one read of the records each
+    int bin_slots = 0, bin_parts = 0;
+    if (ok && P > 0) {
+      const size_t per_slot = (size_t)words * 4;
+      bin_slots = kPartGroup;
+      while ((size_t)P * (2 * bin_slots * per_slot + 8) <= kPartBinLdsBytes && bin_slots < 64) bin_slots *= 2;
+      bin_parts = (int)std::min<int64_t>(P, (int64_t)(kPartBinLdsBytes / (bin_slots * per_slot + 8)));
+      if (bin_parts < 1) ok = false;
+    }
     if (ok && kr >= 256 && P >= 2 && P <= kMaxParts) {
-      part_hist_bytes = ((size_t)P * 4 + 15) & ~(size_t)15;
-      Plan pp = plan_pick(STRAT_PCOUNT);
+      part_hist_bytes = ((size_t)P * 4 + 4 * kWavesPerWG + 15) & ~(size_t)15;  // counters + wave record cursors
+      Plan pp = plan_pick(STRAT_PEMIT);
       if (pp.score >= 0) {
         plan = pp;
         q->partitioned = true;
@@ -1087,6 +1109,11 @@ int pa_query_prepare(pa_query* q) {
         q->part_shift = __builtin_ctzll((uint64_t)kr);
         q->rec_words = words;
         q->pay_off = pay;
+        q->bin_slots = bin_slots;
+        // records per thread per fill round: about a quarter of a bin per partition on uniform keys
+        q->bin_parts = bin_parts;
+        q->bin_iter = (int)std::max<int64_t>(1, std::min<int64_t>(4, (int64_t)bin_parts * bin_slots / (4 * kPartBinThreads)));
+        q->bin_lds = (int)(8 * (size_t)bin_parts + (size_t)bin_parts * bin_slots * words * 4);
         // pass C LDS layout: u32 count[kr], then every aggregation's accumulators for kr keys (8-byte aligned)
         size_t off = ((size_t)kr * 4 + 15) & ~(size_t)15;
         q->part_agg_lds.assign(s.num_aggs, 0);
@@ -1171,6 +1198,7 @@ int pa_query_prepare(pa_query* q) {
     h.ht_keys = (long long*)q->sections[q->keys_section].ptr;
   }
   h.has_mv = q->has_mv;
+  h.xcd_major = dense ? 1 : 0;
   h.lds_count_off = 0;
   h.lds_acc_bytes = q->strategy == STRAT_LDS ? (uint32_t)lds_acc : (q->partitioned ? (uint32_t)part_hist_bytes : 0);
   for (int a = 0; a < s.num_aggs; ++a) {
@@ -1203,19 +1231,35 @@ int pa_query_prepare(pa_query* q) {
   if (q->partitioned) {
     // records: at most one per doc (every bound doc may match); hist: [grid][P]; base: [P + 1]
     dev_free(q->part_hist);
+    dev_free(q->part_off);
     dev_free(q->part_base);
     dev_free(q->recs);
+    dev_free(q->emit);
+    dev_free(q->wave_cnt);
+    // emit buffer: every wave's range holds all docs of its tiles; partitions: every doc plus each (workgroup,
+    // partition) range's padding
+    const size_t emit_recs = (size_t)q->num_tiles * (size_t)q->steps * kWave;
+    const size_t part_recs = (size_t)q->num_docs + (size_t)q->grid * q->part_P * (kPartGroup - 1);
     rc = dev_alloc(q->part_hist, (size_t)q->grid * q->part_P * 4);
+    if (!rc) rc = dev_alloc(q->part_off, (size_t)q->grid * q->part_P * 4);
     if (!rc) rc = dev_alloc(q->part_base, (size_t)(q->part_P + 1) * 4);
-    if (!rc) rc = dev_alloc(q->recs, std::max<size_t>(16, (size_t)q->num_docs * q->rec_words * 4));
+    if (!rc) rc = dev_alloc(q->recs, std::max<size_t>(16, part_recs * q->rec_words * 4));
+    if (!rc) rc = dev_alloc(q->emit, std::max<size_t>(16, emit_recs * q->rec_words * 4));
+    if (!rc) rc = dev_alloc(q->wave_cnt, (size_t)q->grid * kWavesPerWG * 4);
     if (rc) return rc;
     h.part_shift = q->part_shift;
     h.num_parts = q->part_P;
     h.rec_words = q->rec_words;
     h.part_lds_bytes = (uint32_t)q->part_lds_c;
     h.part_hist = (uint32_t*)q->part_hist.p;
+    h.part_off = (uint32_t*)q->part_off.p;
     h.part_base = (uint32_t*)q->part_base.p;
     h.recs = (uint32_t*)q->recs.p;
+    h.emit = (uint32_t*)q->emit.p;
+    h.wave_cnt = (uint32_t*)q->wave_cnt.p;
+    h.bin_slots = q->bin_slots;
+    h.bin_iter = q->bin_iter;
+    h.bin_parts = q->bin_parts;
   }
 
   if (q->limit_mode) {
@@ -1291,8 +1335,8 @@ int pa_query_prepare(pa_query* q) {
   if (rc) return rc;
   PA_HIP(hipMemcpy(q->dplans.p, q->hplans.data(), sizeof(LmSegPlan) * q->hplans.size(), hipMemcpyHostToDevice));
   if (q->partitioned) {
-    PA_HIP(set_scan_lds_limit(STRAT_PCOUNT, q->steps, q->lane_major, q->lds_bytes));
-    PA_HIP(set_scan_lds_limit(STRAT_PSCATTER, q->steps, q->lane_major, q->lds_bytes));
+    PA_HIP(set_scan_lds_limit(STRAT_PEMIT, q->steps, q->lane_major, q->lds_bytes));
+    PA_HIP(set_part_bin_lds_limit(q->bin_lds));
     PA_HIP(set_part_agg_lds_limit(q->part_lds_c));
   } else {
     PA_HIP(set_scan_lds_limit(q->strategy, q->steps, q->lane_major, q->lds_bytes));
@@ -1334,14 +1378,14 @@ int pa_query_scan(pa_query* q, void* stream) {
     PA_HIP(launch_limit_passes(dq, ds, F, q->limit_grid, 1, st));
     return PA_OK;
   }
-  if (q->partitioned) {  // pass A, per-partition offsets, pass B, pass C
+  if (q->partitioned) {  // emit scan, per-partition offsets, binning into partitions, per-partition aggregation
     hipStream_t st = (hipStream_t)stream;
     const DevQuery* dq = (const DevQuery*)q->dq.p;
-    PA_HIP(launch_scan(STRAT_PCOUNT, q->steps, q->lane_major, q->grid, q->lds_bytes, dq, (const DevSeg*)q->dsegs.p,
+    PA_HIP(launch_scan(STRAT_PEMIT, q->steps, q->lane_major, q->grid, q->lds_bytes, dq, (const DevSeg*)q->dsegs.p,
                        (const LmSegPlan*)q->dplans.p, st));
-    PA_HIP(launch_part_offsets((uint32_t*)q->part_hist.p, q->grid, q->part_P, (uint32_t*)q->part_base.p, st));
-    PA_HIP(launch_scan(STRAT_PSCATTER, q->steps, q->lane_major, q->grid, q->lds_bytes, dq, (const DevSeg*)q->dsegs.p,
-                       (const LmSegPlan*)q->dplans.p, st));
+    PA_HIP(launch_part_offsets((const uint32_t*)q->part_hist.p, (uint32_t*)q->part_off.p, q->grid, q->part_P,
+                               (uint32_t*)q->part_base.p, st));
+    PA_HIP(launch_part_bin(dq, q->grid, q->bin_lds, st));
     PA_HIP(launch_part_agg(dq, q->part_P, q->part_lds_c, st));
     return PA_OK;
   }
@@ -1577,7 +1621,7 @@ int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs
 int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t* dma_slots, int32_t* ring,
                   int32_t* wg_per_cu, int32_t* grid, int32_t* lds_bytes) {
   if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
-  if (strategy) *strategy = q->partitioned ? STRAT_PCOUNT : q->strategy;
+  if (strategy) *strategy = q->partitioned ? STRAT_PEMIT : q->strategy;
   if (steps) *steps = q->steps;
   if (dma_slots) *dma_slots = q->dma_slots;
   if (ring) *ring = q->plan_ring;

@@ -17,16 +17,20 @@ namespace pa {
 constexpr int kWave = 64;
 constexpr int kWavesPerWG = 4;
 constexpr int kWGSize = kWave * kWavesPerWG;
+constexpr int kPartGroup = 16;      // partitioned aggregation: records per store burst / range padding unit
+constexpr int kPartBinThreads = 1024;
 constexpr int kSteps = 32;                    // 64-doc steps per wave tile
 constexpr int kWTileDocs = kWave * kSteps;    // 2048 docs: one wave tile; 64*nb stream words per column
 constexpr int kMaxSlots = 12;                 // distinct columns referenced by one query
 constexpr int kGuardWords = 4;
 
 enum ColKind : int32_t { COL_NONE = 0, COL_SV_DICT = 1, COL_SV_RAW = 2, COL_MV_DICT = 3 };
-// STRAT_PCOUNT / STRAT_PSCATTER: the two scan passes of partitioned aggregation (high-cardinality dense GROUP BY):
-// pass A counts matching docs per (workgroup, key partition), pass B writes one record (key, values) per matching doc
-// into its partition, then part_agg_kernel aggregates every partition in LDS (no per-doc device-scope atomics).
-enum Strategy : int32_t { STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PCOUNT = 2, STRAT_PSCATTER = 3 };
+// STRAT_PEMIT: the scan pass of partitioned aggregation (high-cardinality dense GROUP BY): every matching doc's record
+// (key, values) is written to its wave's contiguous record range (coalesced) and counted per (workgroup, key
+// partition) in LDS; part_bin_kernel then moves each workgroup's records into their partitions through LDS bins
+// (whole 16-record groups per store burst), and part_agg_kernel aggregates every partition in LDS (no per-doc
+// device-scope atomics).
+enum Strategy : int32_t { STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PEMIT = 2 };
 // SUM/MIN/MAX value source. SRC_INT: every value fits int32 (one exact int64 accumulator);
 // SRC_LONG: 64-bit values, SUM kept exactly as a (low 32 bits unsigned, high 32 bits signed) pair of int64
 // sums = a 96-bit total for up to 2^32 docs per key; SRC_DOUBLE: FLOAT/DOUBLE.
@@ -114,7 +118,7 @@ struct DevQuery {
   int32_t dma_per_tile;      // LDS-DMA wave instructions per wave tile (max over segments)
   int32_t lane_major;        // 1: scan_lm_kernel (docs 32*lane + i of a tile), 0: scan_kernel (docs 64*i + lane)
   int32_t has_mv;            // a group-by or aggregation column is multi-value: per-lane key expansion path
-  int32_t pad2;
+  int32_t xcd_major;         // tiles walked in XCD-major block order (xcd_major_block): dense queries
   unsigned long long* matched_docs;  // [0]: docs that passed the filter (numDocsScanned), [1]: group-table overflows
   int32_t hashed;            // packed keys through the open-addressing table ht_keys (gb_stride = 1 << shift)
   int32_t pad3;
@@ -124,9 +128,17 @@ struct DevQuery {
   int32_t num_parts;
   int32_t rec_words;         // words per record: key + values
   uint32_t part_lds_bytes;   // part_agg_kernel: LDS accumulator bytes for one partition
-  uint32_t* part_hist;       // [grid][num_parts]: pass A counts, then (in place) each workgroup's offset in a partition
+  uint32_t* part_hist;       // [grid][num_parts]: records per (workgroup, partition) of the emit pass
+  uint32_t* part_off;        // [grid][num_parts]: first record of a workgroup's range in its partition (ranges padded
+                             // to whole kPartGroup-record groups with sentinel records, key 0xffffffff)
   uint32_t* part_base;       // [num_parts + 1]: first record of every partition
-  uint32_t* recs;            // records, partition-major
+  uint32_t* recs;            // records, partition-major (part_bin_kernel output)
+  uint32_t* emit;            // records of the emit pass: wave w's from record (first tile of w) * tile docs on
+  uint32_t* wave_cnt;        // [grid * kWavesPerWG]: records each wave emitted
+  int32_t bin_slots;         // part_bin_kernel: records per LDS bin (power of two >= kPartGroup)
+  int32_t bin_iter;          // part_bin_kernel: records per thread per fill round
+  int32_t bin_parts;         // part_bin_kernel: partitions binned per read of the records (all P when they fit LDS)
+  int32_t pad4;
   int32_t staged_slots[kMaxSlots];
   int32_t gb_slot[PA_MAX_GROUP_BY];
   int64_t gb_stride[PA_MAX_GROUP_BY];

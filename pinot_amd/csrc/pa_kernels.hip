@@ -473,13 +473,12 @@ __device__ void accumulate_doc_mv(const DevQuery* __restrict__ q, const DevSeg* 
   }
 }
 
-// Partitioned aggregation, passes A (STRAT_PCOUNT) and B (STRAT_PSCATTER) for one matching doc: the table-wide key
-// (DictionaryBasedGroupKeyGenerator raw key) picks partition key >> part_shift; pass A counts it in the workgroup's
-// LDS histogram, pass B claims the next slot of the workgroup's range of that partition and writes the record
-// (key, then every aggregation's value: int32, or int64 / double bits as two words).
-template <int STRAT>
-__device__ __forceinline__ void partition_doc(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
-                                              const uint32_t* img, int doc_local, int64_t doc, uint32_t* part_lds) {
+// Partitioned aggregation, emit pass (STRAT_PEMIT) for one matching doc: the table-wide key (DictionaryBasedGroupKeyGenerator
+// raw key) picks partition key >> part_shift, counted in the workgroup's LDS histogram; the record (key, then every
+// aggregation's value: int32, or int64 / double bits as two words) goes to record index `pos` of the emit buffer (the
+// lanes of one step write consecutive records: coalesced).
+__device__ __forceinline__ int64_t emit_key(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                            const uint32_t* img, int doc_local, int64_t doc) {
   int64_t key = 0;
   for (int j = 0; j < q->num_gb; ++j) {
     const DevCol& c = seg->cols[q->gb_slot[j]];
@@ -488,14 +487,17 @@ __device__ __forceinline__ void partition_doc(const DevQuery* __restrict__ q, co
     if (rm != nullptr) id = (uint32_t)gp(rm)[id];
     key += (int64_t)id * q->gb_stride[j];
   }
-  const uint32_t p = (uint32_t)(key >> q->part_shift);
-  if (STRAT == STRAT_PCOUNT) {
-    atomicAdd(part_lds + p, 1u);
-    return;
-  }
-  const uint32_t pos = atomicAdd(part_lds + p, 1u);
-  AS1 uint32_t* r = gp(q->recs) + (size_t)pos * (uint32_t)q->rec_words;
-  if (q->rec_words <= 2) {
+  return key;
+}
+
+__device__ __forceinline__ void emit_doc(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                         const uint32_t* img, int doc_local, int64_t doc, uint32_t* part_lds,
+                                         uint32_t pos) {
+  const int64_t key = emit_key(q, seg, img, doc_local, doc);
+  atomicAdd(part_lds + (uint32_t)(key >> q->part_shift), 1u);
+  const int W = q->rec_words;
+  AS1 uint32_t* r = gp(q->emit) + (size_t)pos * (uint32_t)W;
+  if (W <= 2) {
     // the common record (key, one int32 value shared by every aggregation of one column): one 8-byte store
     uint32_t v = 0;
     for (int a = 0; a < q->num_aggs; ++a) {
@@ -665,10 +667,23 @@ __device__ __forceinline__ bool leaf_match_doc(const DevLeaf& L, int64_t doc) {
 // The rare part of a tile (some doc survived the eager clauses): lazy clauses per surviving doc, then aggregation.
 // Returns the docs that matched.
 // LM: doc of bit i of lane l = 32l + i (lane-major tile), else 64i + l.
+// A wave-uniform pointer the compiler may hold in VGPRs: readfirstlane puts it in SGPRs, so the descriptor fields
+// behind it are scalar loads (vector loads of descriptors need vmcnt waits, which also wait for the in-flight DMA ring).
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return (T*)(((uint64_t)hi << 32) | lo);
+}
+
 template <int STRAT, int STEPS, int LM>
-__device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+__device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg_in,
                                                 const uint32_t* img, int64_t doc_base, uint32_t m, int lane,
                                                 unsigned char* lds) {
+  const DevSeg* __restrict__ seg = uniform_ptr(seg_in);
+  doc_base = ((int64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)doc_base >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)doc_base);
   const Acc<STRAT> acc{q, lds};
   auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
   const int nleaves = q->num_leaves;
@@ -693,9 +708,112 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
     }
     if (__ballot(m != 0) == 0) return 0;
   }
-  if constexpr (STRAT == STRAT_PCOUNT || STRAT == STRAT_PSCATTER) {
-    for (int i = 0; i < STEPS; ++i)
-      if ((m >> i) & 1u) partition_doc<STRAT>(q, seg, img, local(i), doc_base + local(i), (uint32_t*)lds);
+  if constexpr (STRAT == STRAT_PEMIT) {
+    // the wave's record cursor lives in LDS after the partition counters (wave-uniform)
+    uint32_t* cur = (uint32_t*)lds + q->num_parts + (threadIdx.x >> 6);
+    uint32_t c = __builtin_amdgcn_readfirstlane(*cur);
+    if (q->rec_words <= 2 && q->num_gb <= 2) {
+      // (key, one int32 value) records over <= 2 dictionary group-by columns. The descriptors are read once per tile
+      // into registers (reading them per doc through the generic segment pointer reloads them after every LDS atomic,
+      // each load behind a vmcnt wait that also drains the tile ring). Every dictId decode, then every
+      // remap / value gather (they overlap), then keys + LDS histogram, then the coalesced record stores, 8 steps at a time.
+      int va = -1;
+      for (int a = 0; a < q->num_aggs && va < 0; ++a)
+        if (q->aggs[a].type != PA_AGG_COUNT) va = a;
+      const int ngb = q->num_gb;
+      const DevCol& c0 = seg->cols[q->gb_slot[0]];
+      const int gl0 = c0.lds_off, gn0 = c0.nbits;
+      const uint32_t* gw0 = c0.words;
+      const int32_t* rm0 = seg->remap[0];
+      const uint32_t st0 = (uint32_t)q->gb_stride[0];
+      int gl1 = -1, gn1 = 1;
+      const uint32_t* gw1 = nullptr;
+      const int32_t* rm1 = nullptr;
+      uint32_t st1 = 0;
+      if (ngb > 1) {
+        const DevCol& c1 = seg->cols[q->gb_slot[1]];
+        gl1 = c1.lds_off;
+        gn1 = c1.nbits;
+        gw1 = c1.words;
+        rm1 = seg->remap[1];
+        st1 = (uint32_t)q->gb_stride[1];
+      }
+      int vkind = 0, vl = -1, vn = 1, vtype = 0;  // vkind 1: dictionary column, 2: raw INT / LONG column
+      const uint32_t* vw = nullptr;
+      const int64_t* vd = nullptr;
+      const void* vraw = nullptr;
+      if (va >= 0) {
+        const DevCol& cv = seg->cols[q->aggs[va].slot];
+        vkind = cv.kind == COL_SV_DICT ? 1 : 2;
+        vl = cv.lds_off;
+        vn = cv.nbits;
+        vw = cv.words;
+        vd = cv.dict_i64;
+        vraw = cv.raw;
+        vtype = cv.vtype;
+      }
+      const int shift = q->part_shift;
+      AS1 uint64_t* out = (AS1 uint64_t*)gp(q->emit);
+      constexpr int kEB = 8;  // steps per batch (register budget: 3 words per step and lane)
+#pragma unroll 1
+      for (int h = 0; h < STEPS; h += kEB) {
+        uint32_t id0[kEB], id1[kEB], vv[kEB];
+#pragma unroll
+        for (int i = 0; i < kEB; ++i) {
+          id0[i] = id1[i] = vv[i] = 0u;
+          if ((m >> (h + i)) & 1u) {
+            const int dl = local(h + i);
+            const int64_t doc = doc_base + dl;
+            id0[i] = gl0 >= 0 ? decode_lds(img + gl0, dl, gn0) : decode_global(gw0, doc, gn0);
+            if (ngb > 1) id1[i] = gl1 >= 0 ? decode_lds(img + gl1, dl, gn1) : decode_global(gw1, doc, gn1);
+            if (vkind == 1) vv[i] = vl >= 0 ? decode_lds(img + vl, dl, vn) : decode_global(vw, doc, vn);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < kEB; ++i) {
+          if ((m >> (h + i)) & 1u) {
+            const int64_t doc = doc_base + local(h + i);
+            if (rm0 != nullptr) id0[i] = (uint32_t)gp(rm0)[id0[i]];
+            if (rm1 != nullptr) id1[i] = (uint32_t)gp(rm1)[id1[i]];
+            if (vkind == 1) vv[i] = (uint32_t)gp(vd)[vv[i]];
+            else if (vkind == 2) vv[i] = vtype == PA_INT ? (uint32_t)gp((const int32_t*)vraw)[doc]
+                                                         : (uint32_t)gp((const int64_t*)vraw)[doc];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < kEB; ++i) {
+          if ((m >> (h + i)) & 1u) {
+            id0[i] = id0[i] * st0 + id1[i] * st1;  // table-wide key (< 2^32 on this path)
+            atomicAdd((uint32_t*)lds + (id0[i] >> shift), 1u);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < kEB; ++i) {
+          const bool mine = (m >> (h + i)) & 1u;
+          const uint64_t sm = __ballot(mine);
+          if (sm == 0) continue;
+          if (mine) {
+            const uint32_t rank =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+            out[c + rank] = ((uint64_t)vv[i] << 32) | id0[i];
+          }
+          c += (uint32_t)__builtin_popcountll(sm);
+        }
+      }
+    } else {
+      for (int i = 0; i < STEPS; ++i) {
+        const bool mine = (m >> i) & 1u;
+        const uint64_t sm = __ballot(mine);
+        if (sm == 0) continue;
+        if (mine) {
+          const uint32_t rank =
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+          emit_doc(q, seg, img, local(i), doc_base + local(i), (uint32_t*)lds, c + rank);
+        }
+        c += (uint32_t)__builtin_popcountll(sm);
+      }
+    }
+    if (lane == 0) *cur = c;
   } else if (q->has_mv) {
     for (int i = 0; i < STEPS; ++i)
       if ((m >> i) & 1u) accumulate_doc_mv<STRAT>(q, seg, img, local(i), doc_base + local(i), acc);
@@ -945,6 +1063,16 @@ __device__ __forceinline__ void lm_wait_issue(const LmIssue& I, uint32_t& slot_o
   for (; issued < D; ++issued) dma16_masked(I.dummy, dst0, 1ull);
 }
 
+// Workgroups are dispatched to the 8 XCDs round-robin (block b runs on XCD b % 8). For queries that gather per matching
+// doc (dense), the scan gives block b the logical index of its place in XCD-major order, so the workgroups of one XCD
+// walk one contiguous eighth of the tiles: the segments (dictionaries, remaps) an XCD touches at a time are few, and
+// their lines stay in that XCD's L2 (configs[2]: HBM fetch of the emit pass 8.8 GB -> 0.9 GB per launch).
+__device__ __forceinline__ int64_t xcd_major_block(int64_t b, int64_t G) {
+  constexpr int kXcds = 8;
+  const int64_t x = b % kXcds, j = b / kXcds, per = G / kXcds, extra = G % kXcds;
+  return x * per + (x < extra ? x : extra) + j;
+}
+
 // LM = 1: lane-major tiles (STEPS must be 32) driven by the per-segment plan tables `plans`; LM = 0: step-major.
 template <int STRAT, int STEPS, int LM>
 __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __restrict__ q,
@@ -980,19 +1108,24 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
       }
     }
     __syncthreads();
-  } else if (STRAT == STRAT_PCOUNT || STRAT == STRAT_PSCATTER) {
-    // pass A: zeroed per-partition counters; pass B: this workgroup's first slot in every partition
+  } else if (STRAT == STRAT_PEMIT) {
+    // zeroed per-partition counters, then every wave's record cursor: the first record of its emit range
     uint32_t* pl = (uint32_t*)lds_acc;
     const int P = q->num_parts;
-    for (int p = threadIdx.x; p < P; p += kWGSize)
-      pl[p] = STRAT == STRAT_PCOUNT ? 0u : q->part_base[p] + q->part_hist[(size_t)blockIdx.x * P + p];
+    for (int p = threadIdx.x; p < P; p += kWGSize) pl[p] = 0u;
+    if (threadIdx.x < kWavesPerWG) {
+      const int64_t gwi = (q->xcd_major ? xcd_major_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x) * kWavesPerWG +
+                          threadIdx.x;
+      pl[P + threadIdx.x] = (uint32_t)(gwi * q->total_wtiles / ((int64_t)gridDim.x * kWavesPerWG) * (q->steps * kWave));
+    }
     __syncthreads();
   }
 
   uint32_t matched = 0;  // docs of this lane that passed the filter (numDocsScanned)
   const int64_t T = q->total_wtiles;
   const int64_t W = (int64_t)gridDim.x * kWavesPerWG;
-  const int64_t gw = (int64_t)blockIdx.x * kWavesPerWG + wave;
+  const int64_t lb = q->xcd_major ? xcd_major_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;  // logical block
+  const int64_t gw = lb * kWavesPerWG + wave;
   const int64_t t0 = gw * T / W;
   const int64_t t1 = (gw + 1) * T / W;
   if (t0 < t1) {
@@ -1110,15 +1243,17 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
     }
   }
 
-  if (STRAT != STRAT_PSCATTER) {  // (pass B sees the same docs as pass A)
+  {
     const int64_t wm = wave_sum_i64((int64_t)matched);
     if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)wm, RLX);
   }
-  if (STRAT == STRAT_PCOUNT) {
+  if (STRAT == STRAT_PEMIT) {
     __syncthreads();
     const uint32_t* pl = (const uint32_t*)lds_acc;
     const int P = q->num_parts;
-    for (int p = threadIdx.x; p < P; p += kWGSize) gp(q->part_hist)[(size_t)blockIdx.x * P + p] = pl[p];
+    for (int p = threadIdx.x; p < P; p += kWGSize) gp(q->part_hist)[(size_t)lb * P + p] = pl[p];
+    if (lane == 0)
+      gp(q->wave_cnt)[gw] = pl[P + wave] - (uint32_t)(t0 * (q->steps * kWave));
   }
   if (STRAT == STRAT_LDS) {
     __syncthreads();
@@ -1477,25 +1612,173 @@ hipError_t launch_compact(const unsigned long long* count, int64_t K, int all, u
 
 
 // ---------------------------------------------------------------- partitioned aggregation: offsets + pass C
-// Block p: exclusive scan of the G workgroup counts of partition p (hist[wg][p], in place); total -> totals[p].
-__global__ void __launch_bounds__(256) part_scan_kernel(uint32_t* hist, int G, int P, uint32_t* totals) {
+// Block p: exclusive scan of the G workgroup counts of partition p, each rounded up to whole kPartGroup-record groups
+// (-> off[wg][p], relative to the partition); padded total -> totals[p].
+__global__ void __launch_bounds__(256) part_scan_kernel(const uint32_t* hist, uint32_t* off, int G, int P,
+                                                        uint32_t* totals) {
   __shared__ uint32_t sh[256];
   const int p = blockIdx.x;
   uint32_t carry = 0;
   for (int base = 0; base < G; base += 256) {
     const int wg = base + threadIdx.x;
-    const uint32_t x = wg < G ? hist[(size_t)wg * P + p] : 0u;
+    const uint32_t x = wg < G ? (hist[(size_t)wg * P + p] + (kPartGroup - 1)) & ~(uint32_t)(kPartGroup - 1) : 0u;
     uint32_t tot;
     const uint32_t ex = block_exclusive_scan_256(x, sh, &tot);
-    if (wg < G) hist[(size_t)wg * P + p] = carry + ex;
+    if (wg < G) off[(size_t)wg * P + p] = carry + ex;
     carry += tot;
   }
   if (threadIdx.x == 0) totals[p] = carry;
 }
 
+// Block b moves the records workgroup b of the emit pass wrote (its waves' ranges of the emit buffer) into b's range of
+// every partition: each fill round drops bin_iter records per thread into per-partition LDS bins (bin_slots records
+// each), then every bin holding a whole group of kPartGroup records stores its whole groups with one contiguous burst
+// (one 128-B line per group for 2-word records) and keeps the rest; a record finding its bin full goes straight to
+// the partition range. At the end each bin's rest goes out padded with sentinel records (key 0xffffffff) up to the
+// range's padded size. When the bins of all P partitions do not fit LDS, the partitions are taken bin_parts at a time
+// (one read of the workgroup's records per group of partitions). Order inside a partition does not matter to the
+// aggregation (integer results are exact; a DOUBLE sum is order-dependent only in its last bits, like the atomics).
+__global__ void __launch_bounds__(kPartBinThreads) part_bin_kernel(const DevQuery* __restrict__ q) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int P = q->num_parts;
+  const int PB = q->bin_parts;
+  const int W = q->rec_words;
+  const int BS = q->bin_slots;
+  uint32_t* binc = smem;           // [PB] records in the bin (may exceed BS while filling: the excess went out directly)
+  uint32_t* outp = smem + PB;      // [PB] next output record of this workgroup's range in the partition
+  uint32_t* bins = smem + 2 * PB;  // [PB][BS][W]
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  constexpr int kWaves = kPartBinThreads / 64;
+  // the emit ranges of the workgroup's waves
+  const int64_t Wt = (int64_t)gridDim.x * kWavesPerWG;
+  const int64_t tile_docs = (int64_t)q->steps * kWave;
+  uint32_t rs[kWavesPerWG], rn[kWavesPerWG];
+  uint32_t n_all = 0;
+#pragma unroll
+  for (int k = 0; k < kWavesPerWG; ++k) {
+    const int64_t gwi = (int64_t)b * kWavesPerWG + k;
+    rs[k] = (uint32_t)(gwi * q->total_wtiles / Wt * tile_docs);
+    rn[k] = q->wave_cnt[gwi];
+    n_all += rn[k];
+  }
+  const AS1 uint32_t* src = gp((const uint32_t*)q->emit);
+  AS1 uint32_t* dst = gp(q->recs);
+  const int shift = q->part_shift;
+  const uint32_t round = (uint32_t)q->bin_iter * kPartBinThreads;
+  for (int plo = 0; plo < P; plo += PB) {
+    const int np = min(PB, P - plo);
+    for (int p = tid; p < np; p += kPartBinThreads) {
+      binc[p] = 0u;
+      outp[p] = q->part_base[plo + p] + q->part_off[(size_t)b * P + plo + p];
+    }
+    __syncthreads();
+    // round k: the records loaded during round k-1's flush are binned, then round k+1's loads are issued before this
+    // round's flush (their latency hides behind it)
+    const int iters = q->bin_iter;  // 1..4
+    uint32_t at[4], w0[4], w1[4];
+    bool ok[4];
+    auto load_round = [&](uint32_t base) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        uint32_t i = base + (uint32_t)r * kPartBinThreads + tid;
+        ok[r] = r < iters && i < n_all;
+        at[r] = 0u;
+        w0[r] = w1[r] = 0u;
+        if (!ok[r]) continue;
+        bool found = false;
+#pragma unroll
+        for (int k = 0; k < kWavesPerWG; ++k) {  // static indices only: rs / rn stay in registers
+          if (!found) {
+            if (i < rn[k]) {
+              at[r] = rs[k] + i;
+              found = true;
+            } else {
+              i -= rn[k];
+            }
+          }
+        }
+        const AS1 uint32_t* rec = src + (size_t)at[r] * (uint32_t)W;
+        if (W == 2) {
+          const uint64_t v = __builtin_nontemporal_load((const AS1 uint64_t*)rec);
+          w0[r] = (uint32_t)v;
+          w1[r] = (uint32_t)(v >> 32);
+        } else {
+          w0[r] = rec[0];
+        }
+      }
+    };
+    load_round(0);
+    for (uint32_t base = 0; base < n_all; base += round) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (!ok[r]) continue;
+        const AS1 uint32_t* rec = src + (size_t)at[r] * (uint32_t)W;
+        const uint32_t p = (w0[r] >> shift) - (uint32_t)plo;
+        if (p >= (uint32_t)np) continue;  // another group of partitions
+        const uint32_t slot = atomicAdd(binc + p, 1u);
+        if (slot < (uint32_t)BS) {
+          uint32_t* d = bins + ((size_t)p * BS + slot) * W;
+          if (W == 2) {
+            *(uint64_t*)d = ((uint64_t)w1[r] << 32) | w0[r];
+          } else {
+            d[0] = w0[r];
+            for (int e = 1; e < W; ++e) d[e] = rec[e];
+          }
+        } else {  // bin full: straight to the range
+          const uint32_t o = atomicAdd(outp + p, 1u);
+          AS1 uint32_t* d = dst + (size_t)o * (uint32_t)W;
+          if (W == 2) {
+            *(AS1 uint64_t*)d = ((uint64_t)w1[r] << 32) | w0[r];
+          } else {
+            d[0] = w0[r];
+            for (int e = 1; e < W; ++e) d[e] = rec[e];
+          }
+        }
+      }
+      __syncthreads();
+      load_round(base + round);
+      // flush whole groups: one wave per bin
+      for (int p = wave; p < np; p += kWaves) {
+        const uint32_t n = min(binc[p], (uint32_t)BS);
+        const uint32_t g = n & ~(uint32_t)(kPartGroup - 1);
+        if (g != 0) {
+          const uint32_t o = outp[p];  // only this wave touches bin p in this phase
+          const uint32_t* bsrc = bins + (size_t)p * BS * W;
+          AS1 uint32_t* d = dst + (size_t)o * (uint32_t)W;
+          if (W == 2) {
+            for (uint32_t e = lane; e < g; e += 64) ((AS1 uint64_t*)d)[e] = ((const uint64_t*)bsrc)[e];
+          } else {
+            for (uint32_t e = lane; e < g * W; e += 64) d[e] = bsrc[e];
+          }
+          // the rest (< kPartGroup records) to the front of the bin: source [g, n) and target [0, n - g) are disjoint
+          uint32_t* bdst = bins + (size_t)p * BS * W;
+          for (uint32_t e = lane; e < (n - g) * W; e += 64) bdst[e] = bsrc[g * W + e];
+          if (lane == 0) outp[p] = o + g;
+        }
+        if (lane == 0) binc[p] = n - g;
+      }
+      __syncthreads();
+    }
+    // the rest of every bin, padded with sentinels up to the end of the range
+    for (int p = wave; p < np; p += kWaves) {
+      const uint32_t n = binc[p];
+      const uint32_t o = outp[p];
+      const uint32_t h = q->part_hist[(size_t)b * P + plo + p];
+      const uint32_t pad = ((h + (kPartGroup - 1)) & ~(uint32_t)(kPartGroup - 1)) - h;
+      const uint32_t* bsrc = bins + (size_t)p * BS * W;
+      AS1 uint32_t* d = dst + (size_t)o * (uint32_t)W;
+      for (uint32_t e = lane; e < (n + pad) * W; e += 64) d[e] = e < n * W ? bsrc[e] : (e % W == 0 ? 0xffffffffu : 0u);
+    }
+    __syncthreads();
+  }
+}
+
 // Pass C, block p: aggregate the records of partition p (keys [p << shift, (p+1) << shift)) in LDS, then add the
 // partition's non-empty keys into the global accumulators (this block owns those keys: plain read-modify-write).
-__global__ void __launch_bounds__(256) part_agg_kernel(const DevQuery* __restrict__ q) {
+constexpr int kPartAggThreads = 512;
+__global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuery* __restrict__ q) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   unsigned char* lds = (unsigned char*)smem;
   const int p = blockIdx.x;
@@ -1503,20 +1786,61 @@ __global__ void __launch_bounds__(256) part_agg_kernel(const DevQuery* __restric
   const int64_t kbase = (int64_t)p << q->part_shift;
   const int64_t nk = min(KR, q->num_keys - kbase);
   uint32_t* cnt = (uint32_t*)lds;
-  for (int64_t k = threadIdx.x; k < KR; k += 256) cnt[k] = 0;
+  for (int64_t k = threadIdx.x; k < KR; k += kPartAggThreads) cnt[k] = 0;
   for (int a = 0; a < q->num_aggs; ++a) {
     const DevAgg& A = q->aggs[a];
     if (A.type == PA_AGG_COUNT) continue;
     int64_t* r = (int64_t*)(lds + A.lds_off);
     const int64_t init = A.type == PA_AGG_MIN ? INT64_MAX : (A.type == PA_AGG_MAX ? INT64_MIN : 0);
     const int64_t n = (A.type == PA_AGG_SUM && A.src == SRC_LONG) ? 2 * KR : KR;
-    for (int64_t k = threadIdx.x; k < n; k += 256) r[k] = init;
+    for (int64_t k = threadIdx.x; k < n; k += kPartAggThreads) r[k] = init;
   }
   __syncthreads();
   const uint32_t r0 = q->part_base[p], r1 = q->part_base[p + 1];
   const int W = q->rec_words;
-  for (uint32_t ri = r0 + threadIdx.x; ri < r1; ri += 256) {
+  uint32_t rstart = r0;
+  if (W == 2) {
+    // (key, int32 value) records, 8 per thread in flight: every load first, then the LDS updates
+    constexpr int kB = 8;
+    int va = -1;
+    for (int a = 0; a < q->num_aggs && va < 0; ++a)
+      if (q->aggs[a].type != PA_AGG_COUNT) va = a;
+    const uint32_t span = kB * kPartAggThreads;
+    uint32_t base = r0;
+    for (; base + span <= r1; base += span) {
+      uint64_t v[kB];
+#pragma unroll
+      for (int j = 0; j < kB; ++j) v[j] = __builtin_nontemporal_load(gp((const uint64_t*)q->recs) + base + j * kPartAggThreads + threadIdx.x);
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        const uint32_t key = (uint32_t)v[j];
+        if (key == 0xffffffffu) continue;  // range padding (part_bin_kernel)
+        const int64_t lk = (int64_t)key - kbase;
+        atomicAdd(cnt + lk, 1u);
+        const int64_t iv = (int64_t)(int32_t)(uint32_t)(v[j] >> 32);
+        for (int a = va < 0 ? 0 : va; a < q->num_aggs; ++a) {
+          const DevAgg& A = q->aggs[a];
+          if (A.type == PA_AGG_COUNT) continue;
+          if (A.type == PA_AGG_SUM) {
+            if (A.src == SRC_LONG) {
+              atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk, (unsigned long long)(uint32_t)iv);
+              atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk + 1, (unsigned long long)(iv >> 32));
+            } else {
+              atomicAdd((unsigned long long*)(lds + A.lds_off) + lk, (unsigned long long)iv);
+            }
+          } else if (A.type == PA_AGG_MIN) {
+            atomicMin((long long*)(lds + A.lds_off) + lk, (long long)iv);
+          } else {
+            atomicMax((long long*)(lds + A.lds_off) + lk, (long long)iv);
+          }
+        }
+      }
+    }
+    rstart = base;
+  }
+  for (uint32_t ri = rstart + threadIdx.x; ri < r1; ri += kPartAggThreads) {
     const AS1 uint32_t* rec = gp(q->recs) + (size_t)ri * (uint32_t)W;
+    if (rec[0] == 0xffffffffu) continue;  // range padding (part_bin_kernel)
     const int64_t lk = (int64_t)rec[0] - kbase;
     atomicAdd(cnt + lk, 1u);
     for (int a = 0; a < q->num_aggs; ++a) {
@@ -1542,7 +1866,7 @@ __global__ void __launch_bounds__(256) part_agg_kernel(const DevQuery* __restric
     }
   }
   __syncthreads();
-  for (int64_t lk = threadIdx.x; lk < nk; lk += 256) {
+  for (int64_t lk = threadIdx.x; lk < nk; lk += kPartAggThreads) {
     const uint32_t c = cnt[lk];
     if (c == 0) continue;
     const int64_t k = kbase + lk;
@@ -1574,9 +1898,18 @@ __global__ void __launch_bounds__(256) part_agg_kernel(const DevQuery* __restric
   }
 }
 
-hipError_t launch_part_offsets(uint32_t* hist, int G, int P, uint32_t* part_base, hipStream_t s) {
-  part_scan_kernel<<<P, 256, 0, s>>>(hist, G, P, part_base);
+hipError_t launch_part_offsets(const uint32_t* hist, uint32_t* off, int G, int P, uint32_t* part_base, hipStream_t s) {
+  part_scan_kernel<<<P, 256, 0, s>>>(hist, off, G, P, part_base);
   compact_scan_kernel<<<1, 256, 0, s>>>(part_base, P);
+  return hipGetLastError();
+}
+
+hipError_t set_part_bin_lds_limit(int lds_bytes) {
+  return hipFuncSetAttribute((const void*)part_bin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+}
+
+hipError_t launch_part_bin(const DevQuery* q, int G, int lds_bytes, hipStream_t s) {
+  part_bin_kernel<<<G, kPartBinThreads, (size_t)lds_bytes, s>>>(q);
   return hipGetLastError();
 }
 
@@ -1585,7 +1918,7 @@ hipError_t set_part_agg_lds_limit(int lds_bytes) {
 }
 
 hipError_t launch_part_agg(const DevQuery* q, int P, int lds_bytes, hipStream_t s) {
-  part_agg_kernel<<<P, 256, (size_t)lds_bytes, s>>>(q);
+  part_agg_kernel<<<P, kPartAggThreads, (size_t)lds_bytes, s>>>(q);
   return hipGetLastError();
 }
 
@@ -1634,8 +1967,7 @@ static const void* scan_fn_s(int steps, int lm) {
 static const void* scan_fn(int strategy, int steps, int lm) {
   switch (strategy) {
     case STRAT_LDS: return scan_fn_s<STRAT_LDS>(steps, lm);
-    case STRAT_PCOUNT: return scan_fn_s<STRAT_PCOUNT>(steps, lm);
-    case STRAT_PSCATTER: return scan_fn_s<STRAT_PSCATTER>(steps, lm);
+    case STRAT_PEMIT: return (const void*)scan_kernel<STRAT_PEMIT, 16, 0>;  // the planner's only emit layout
     default: return scan_fn_s<STRAT_GLOBAL>(steps, lm);
   }
 }

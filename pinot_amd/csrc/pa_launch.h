@@ -44,7 +44,9 @@ hipError_t launch_hll_lut_hashes(const int32_t* hashes, int32_t card, int32_t lo
 hipError_t launch_fill_i64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
 hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t* keys, int64_t n, void* out,
                          hipStream_t s);
-hipError_t launch_part_offsets(uint32_t* hist, int G, int P, uint32_t* part_base, hipStream_t s);
+hipError_t launch_part_offsets(const uint32_t* hist, uint32_t* off, int G, int P, uint32_t* part_base, hipStream_t s);
+hipError_t set_part_bin_lds_limit(int lds_bytes);
+hipError_t launch_part_bin(const DevQuery* q, int G, int lds_bytes, hipStream_t s);
 hipError_t set_part_agg_lds_limit(int lds_bytes);
 hipError_t launch_part_agg(const DevQuery* q, int P, int lds_bytes, hipStream_t s);
 hipError_t set_scan_lds_limit(int strategy, int steps, int lm, int bytes);

@@ -258,7 +258,9 @@ def test_high_cardinality_global_fallback():
     assert len(got.groups) > 100000
 
 
-@pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LANE_MAJOR, L.PA_QF_NO_PARTITION, L.PA_QF_STAGE_ALL])
+@pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LANE_MAJOR, L.PA_QF_NO_PARTITION, L.PA_QF_STAGE_ALL,
+                                   1 << L.PA_QF_PART_SHIFT, 2 << L.PA_QF_PART_SHIFT,
+                                   3 << L.PA_QF_PART_SHIFT | 1 << L.PA_QF_WG_SHIFT])
 def test_partitioned_aggregation(flags):
     """High-cardinality dense GROUP BY (BASELINE configs[2] shape): records partitioned by key range, aggregated per
     partition in LDS. INT / LONG (beyond int32) / DOUBLE / FLOAT values, SUM MIN MAX AVG, with and without a filter,
@@ -271,6 +273,7 @@ def test_partitioned_aggregation(flags):
         "OPTION(numGroupsLimit=2000000)",
         "SELECT k2, k1, SUM(big), MIN(big), MAX(f), SUM(f), MIN(g) FROM t WHERE m > {m} GROUP BY k2, k1 "
         "LIMIT 1000000 OPTION(numGroupsLimit=2000000)",
+        "SELECT k1, k2, COUNT(*) FROM t GROUP BY k1, k2 LIMIT 1000000 OPTION(numGroupsLimit=2000000)",
     ]
     mv = int(segs[0].column("m").dictionary[len(segs[0].column("m").dictionary) // 4])
     gsegs = [GpuSegment(sg) for sg in segs]
@@ -282,7 +285,8 @@ def test_partitioned_aggregation(flags):
             ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags)
             strategy = ex.stats()["plan"]["strategy"]
             ex.close()
-            assert strategy == ("global" if flags & L.PA_QF_NO_PARTITION else "partitioned"), strategy
+            if not flags & (3 << L.PA_QF_PART_SHIFT):  # (smaller partitions may not fit the binning LDS: global)
+                assert strategy == ("global" if flags & L.PA_QF_NO_PARTITION else "partitioned"), strategy
     finally:
         for g in gsegs:
             g.close()

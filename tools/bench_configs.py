@@ -72,7 +72,7 @@ WORKLOADS = {
 }
 
 
-def run(workload, nseg, docs, reps, only=None, no_stepmajor=False):
+def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None):
     import torch
     from pinot_amd import parse_sql
     from pinot_amd import _lib as L
@@ -95,8 +95,8 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False):
     for name, sql, flags in queries:
         if only and name != only:
             continue
-        variants = ((0, ""),) if no_stepmajor else ((0, ""), (L.PA_QF_NO_LANE_MAJOR, "_stepmajor"))
-        for extra, tag in variants:
+        vs = variants or (((0, ""),) if no_stepmajor else ((0, ""), (L.PA_QF_NO_LANE_MAJOR, "_stepmajor")))
+        for extra, tag in vs:
             ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags | extra)
             ex.execute(sp)
             torch.cuda.synchronize()
@@ -131,11 +131,19 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--plan", default=None, help="only this plan name (e.g. all_docs)")
     ap.add_argument("--no-stepmajor", action="store_true", help="skip the forced step-major variants")
+    ap.add_argument("--sweep-part", action="store_true",
+                    help="partitioned aggregation: sweep LDS per partition x workgroups per CU")
+    ap.add_argument("--flags", type=int, default=None, help="run this one PA_QF_* flag set only")
     args = ap.parse_args()
+    variants = None if args.flags is None else [(args.flags, "_f%d" % args.flags)]
+    if args.sweep_part:
+        from pinot_amd import _lib as L
+        variants = [(ps << L.PA_QF_PART_SHIFT | wg << L.PA_QF_WG_SHIFT, "_part%d_wg%d" % (ps, wg))
+                    for ps in (1, 2, 3) for wg in (0, 1, 2)]
     import torch
     torch.cuda.set_device(0)
     for w in (WORKLOADS if args.workload == "all" else [args.workload]):
-        run(w, args.segments, args.docs, args.reps, args.plan, args.no_stepmajor)
+        run(w, args.segments, args.docs, args.reps, args.plan, args.no_stepmajor, variants)
 
 
 if __name__ == "__main__":
