@@ -1739,37 +1739,45 @@ __global__ void __launch_bounds__(kPartBinThreads) part_bin_kernel(const DevQuer
       }
       __syncthreads();
       load_round(base + round);
-      // flush whole groups: one wave per bin
-      for (int p = wave; p < np; p += kWaves) {
-        const uint32_t n = min(binc[p], (uint32_t)BS);
-        const uint32_t g = n & ~(uint32_t)(kPartGroup - 1);
-        if (g != 0) {
-          const uint32_t o = outp[p];  // only this wave touches bin p in this phase
-          const uint32_t* bsrc = bins + (size_t)p * BS * W;
-          AS1 uint32_t* d = dst + (size_t)o * (uint32_t)W;
-          if (W == 2) {
-            for (uint32_t e = lane; e < g; e += 64) ((AS1 uint64_t*)d)[e] = ((const uint64_t*)bsrc)[e];
-          } else {
-            for (uint32_t e = lane; e < g * W; e += 64) d[e] = bsrc[e];
+      // flush whole groups: a wave takes 4 bins at a time, 16 lanes per bin (each burst is a run of whole 128-B lines)
+      const int sub = lane >> 4, sl = lane & 15;
+      for (int p0 = wave * 4; p0 < np; p0 += kWaves * 4) {
+        const int p = p0 + sub;
+        if (p < np) {
+          const uint32_t n = min(binc[p], (uint32_t)BS);
+          const uint32_t g = n & ~(uint32_t)(kPartGroup - 1);
+          if (g != 0) {
+            const uint32_t o = outp[p];  // only these 16 lanes touch bin p in this phase
+            uint32_t* bsrc = bins + (size_t)p * BS * W;
+            AS1 uint32_t* d = dst + (size_t)o * (uint32_t)W;
+            if (W == 2) {
+              for (uint32_t e = sl; e < g; e += 16) ((AS1 uint64_t*)d)[e] = ((const uint64_t*)bsrc)[e];
+            } else {
+              for (uint32_t e = sl; e < g * W; e += 16) d[e] = bsrc[e];
+            }
+            // the rest (< kPartGroup records) to the front of the bin: source [g, n) and target [0, n - g) are disjoint
+            for (uint32_t e = sl; e < (n - g) * W; e += 16) bsrc[e] = bsrc[g * W + e];
+            if (sl == 0) outp[p] = o + g;
           }
-          // the rest (< kPartGroup records) to the front of the bin: source [g, n) and target [0, n - g) are disjoint
-          uint32_t* bdst = bins + (size_t)p * BS * W;
-          for (uint32_t e = lane; e < (n - g) * W; e += 64) bdst[e] = bsrc[g * W + e];
-          if (lane == 0) outp[p] = o + g;
+          if (sl == 0) binc[p] = n - g;
         }
-        if (lane == 0) binc[p] = n - g;
       }
       __syncthreads();
     }
-    // the rest of every bin, padded with sentinels up to the end of the range
-    for (int p = wave; p < np; p += kWaves) {
-      const uint32_t n = binc[p];
-      const uint32_t o = outp[p];
-      const uint32_t h = q->part_hist[(size_t)b * P + plo + p];
-      const uint32_t pad = ((h + (kPartGroup - 1)) & ~(uint32_t)(kPartGroup - 1)) - h;
-      const uint32_t* bsrc = bins + (size_t)p * BS * W;
-      AS1 uint32_t* d = dst + (size_t)o * (uint32_t)W;
-      for (uint32_t e = lane; e < (n + pad) * W; e += 64) d[e] = e < n * W ? bsrc[e] : (e % W == 0 ? 0xffffffffu : 0u);
+    // the rest of every bin, padded with sentinels up to the end of the range (16 lanes per bin)
+    {
+      const int sub = lane >> 4, sl = lane & 15;
+      for (int p0 = wave * 4; p0 < np; p0 += kWaves * 4) {
+        const int p = p0 + sub;
+        if (p >= np) continue;
+        const uint32_t n = binc[p];
+        const uint32_t o = outp[p];
+        const uint32_t h = q->part_hist[(size_t)b * P + plo + p];
+        const uint32_t pad = ((h + (kPartGroup - 1)) & ~(uint32_t)(kPartGroup - 1)) - h;
+        const uint32_t* bsrc = bins + (size_t)p * BS * W;
+        AS1 uint32_t* d = dst + (size_t)o * (uint32_t)W;
+        for (uint32_t e = sl; e < (n + pad) * W; e += 16) d[e] = e < n * W ? bsrc[e] : (e % W == 0 ? 0xffffffffu : 0u);
+      }
     }
     __syncthreads();
   }
