@@ -369,6 +369,7 @@ int to_cnf(const pa_query_spec& spec, std::vector<Clause>& out) {
 
 constexpr size_t kFetchWholeBlockBytes = 1 << 20;
 constexpr size_t kPartLdsChoices[4] = {144 * 1024, 64 * 1024, 96 * 1024, 144 * 1024};  // PA_QF_PART_SHIFT
+constexpr int64_t kMinParts = 256;          // pass C parallelism: one workgroup per partition, >= one per CU
 constexpr int64_t kMaxParts = 4096;          // partition counters of the scan passes: 16 KiB of LDS
 constexpr size_t kPartBinLdsBytes = 152 * 1024;  // part_bin_kernel: bins + counters (one 1024-thread workgroup per CU)
 constexpr int64_t kDirectMaxKeys = int64_t(1) << 27;  // direct-indexed key space limit (beyond: hashed keys)
@@ -422,9 +423,11 @@ struct pa_query {
   int key_shift[PA_MAX_GROUP_BY] = {0};
   int keys_section = -1;
   bool partitioned = false;      // partitioned aggregation (STRAT_PEMIT scan + part_bin_kernel + part_agg_kernel)
-  int part_P = 0, part_shift = 0, rec_words = 0, part_lds_c = 0, bin_slots = 0, bin_iter = 0, bin_parts = 0;
+  int part_P = 0, part_shift = 0, rec_words = 0, part_lds_c = 0, bin_slots = 0, bin_iter = 0, bin_parts = 0, emit_val_agg = -1;
+  int hll_agg = -1, hll_key_shift = 0;
+  bool emit_fast = false;
   std::vector<int> pay_off, part_agg_lds;
-  DevBuf part_hist, part_off, part_base, recs, emit, wave_cnt;
+  DevBuf part_hist, part_off, part_base, recs, emit, wave_cnt, tile_rec;
   int bin_lds = 0;
   int64_t last_matched = -1;  // numDocsScanned read by the last fetch
   int64_t last_reached = -1;  // segments that reached numGroupsLimit, read by the last fetch
@@ -451,6 +454,7 @@ struct pa_query {
     dev_free(recs);
     dev_free(emit);
     dev_free(wave_cnt);
+    dev_free(tile_rec);
     dev_free(lim_keys);
     dev_free(lim_pos);
     dev_free(lim_sk);
@@ -761,6 +765,9 @@ int pa_query_prepare(pa_query* q) {
   q->hsegs.assign(q->nseg, DevSeg{});
   std::vector<char> staged(nslots, 0);
   std::vector<int> agg_src(s.num_aggs, SRC_INT);
+  std::vector<char> val_fast(s.num_aggs, 1);
+  std::vector<char> agg_mv(s.num_aggs, 0);  // the aggregation column is multi-value in some segment
+  bool gb_mv = false;                        // some group-by column is multi-value in some segment  // emit fast path: the value is a dictionary or raw INT/LONG/DOUBLE column
   
   
   
@@ -857,7 +864,10 @@ int pa_query_prepare(pa_query* q) {
       }
       if (dc.kind != COL_SV_DICT && dc.kind != COL_MV_DICT)
         return fail(PA_EINVAL, "group-by column is dictionary-encoded in segment 0 but not here");
-      if (dc.kind == COL_MV_DICT) q->has_mv = 1;
+      if (dc.kind == COL_MV_DICT) {
+        q->has_mv = 1;
+        gb_mv = true;
+      }
       if (q->has_remap[si][j]) {
         void* dp = nullptr;
         rc = upload_owned(q, q->remaps[si][j].data(), q->remaps[si][j].size() * 4, &dp);
@@ -874,13 +884,19 @@ int pa_query_prepare(pa_query* q) {
       const pa_agg_spec& A = s.aggs[a];
       if (A.type == PA_AGG_COUNT) continue;
       const Column* c = seg->cols.at(A.column_id);
-      if (c->kind == COL_MV_DICT) q->has_mv = 1;
+      if (c->kind == COL_MV_DICT) {
+        q->has_mv = 1;
+        agg_mv[a] = 1;
+      }
       if (A.type == PA_AGG_COUNT_MV) {
         if (c->kind != COL_MV_DICT) return fail(PA_EINVAL, "COUNT_MV on a single-value column");
         agg_src[a] = SRC_INT;
         continue;
       }
       const int src = (c->vtype == PA_FLOAT || c->vtype == PA_DOUBLE) ? SRC_DOUBLE : (c->fits_int32 ? SRC_INT : SRC_LONG);
+      if (!(c->kind == COL_SV_DICT ||
+            (c->kind == COL_SV_RAW && (c->vtype == PA_INT || c->vtype == PA_LONG || c->vtype == PA_DOUBLE))))
+        val_fast[a] = 0;
       if (A.type != PA_AGG_DISTINCTCOUNTHLL) {
         if (c->vtype == PA_STRING || c->vtype == PA_BYTES) return fail(PA_EINVAL, "numeric aggregation on a non-numeric column");
         if (c->kind == COL_SV_DICT && !c->dict.p) return fail(PA_EINVAL, "dictionary values missing");
@@ -1061,7 +1077,11 @@ int pa_query_prepare(pa_query* q) {
   // (count per (workgroup, partition); write one record per matching doc into its partition) + one LDS aggregation
   // per partition, instead of ~(1 + aggregations) device-scope atomics per matching doc on random keys.
   q->partitioned = false;
-  if (q->strategy == STRAT_GLOBAL && dense && !q->has_mv && !q->hashed && !q->limit_mode &&
+  // A DISTINCTCOUNTHLL(MV) joins as one record per value (u8 registers per key in pass C); other multi-value columns
+  // keep the per-doc atomic paths.
+  q->hll_agg = -1;
+  q->hll_key_shift = 0;
+  if (q->strategy == STRAT_GLOBAL && dense && !gb_mv && !q->hashed && !q->limit_mode &&
       !(s.flags & (PA_QF_NO_PARTITION | PA_QF_FORCE_GLOBAL)) &&
       K < (int64_t(1) << 32) && q->num_docs < (uint64_t(1) << 30)) {
     bool ok = true;
@@ -1071,12 +1091,24 @@ int pa_query_prepare(pa_query* q) {
     for (int a = 0; a < s.num_aggs && ok; ++a) {
       const int t = s.aggs[a].type;
       if (t == PA_AGG_COUNT) continue;
-      if (t == PA_AGG_DISTINCTCOUNTHLL || t == PA_AGG_COUNT_MV) { ok = false; break; }
+      if (t == PA_AGG_COUNT_MV) { ok = false; break; }
+      if (t == PA_AGG_DISTINCTCOUNTHLL) {
+        // one per query; word 0 = key << (log2m + 6) | register << 6 | rank << 1 | first must fit 32 bits
+        const int lg = s.aggs[a].log2m;
+        if (q->hll_agg >= 0 || lg + 6 >= 32 || K > (int64_t(1) << (32 - (lg + 6)))) { ok = false; break; }
+        q->hll_agg = a;
+        q->hll_key_shift = lg + 6;
+        per_key += (size_t)1 << lg;  // u8 registers
+        continue;
+      }
+      if (agg_mv[a]) { ok = false; break; }
       per_key += (t == PA_AGG_SUM && agg_src[a] == SRC_LONG) ? 16 : 8;
       // one payload per distinct (column, value source): SUM/MIN/MAX of one column share it
       int shared = -1;
       for (int b = 0; b < a; ++b)
-        if (s.aggs[b].type != PA_AGG_COUNT && agg_slot[b] == agg_slot[a] && agg_src[b] == agg_src[a]) shared = pay[b];
+        if (s.aggs[b].type != PA_AGG_COUNT && s.aggs[b].type != PA_AGG_DISTINCTCOUNTHLL && agg_slot[b] == agg_slot[a] &&
+            agg_src[b] == agg_src[a])
+          shared = pay[b];
       if (shared >= 0) {
         pay[a] = shared;
       } else {
@@ -1087,7 +1119,10 @@ int pa_query_prepare(pa_query* q) {
     words = std::max(words, 2);  // COUNT-only records carry an unused value word: records are >= 8 bytes
     int64_t kr = 1;
     const size_t part_lds = kPartLdsChoices[(s.flags >> PA_QF_PART_SHIFT) & 3];
-    while (ok && (size_t)(kr * 2) * per_key <= part_lds) kr *= 2;
+    // largest partitions that fit pass C's LDS, but at least kMinParts of them (pass C runs one workgroup each) unless
+    // that would take them below 256 keys
+    while (ok && (size_t)(kr * 2) * per_key <= part_lds && ((K + 2 * kr - 1) / (2 * kr) >= kMinParts || kr < 256))
+      kr *= 2;
     const int64_t P = ok ? (K + kr - 1) / kr : 0;
     // part_bin_kernel: per-partition LDS bins of kPartGroup..64 records within kPartBinLdsBytes; when even one-group
     // bins of all P partitions do not fit, groups of bin_parts partitions are binned one read of the records each
@@ -1109,6 +1144,14 @@ int pa_query_prepare(pa_query* q) {
         q->part_shift = __builtin_ctzll((uint64_t)kr);
         q->rec_words = words;
         q->pay_off = pay;
+        // emit fast path: one payload (or none) from a dictionary / raw INT, LONG, DOUBLE column
+        q->emit_val_agg = -1;
+        q->emit_fast = words <= 3 && q->hll_agg < 0;
+        for (int a = 0; a < s.num_aggs; ++a) {
+          if (s.aggs[a].type == PA_AGG_COUNT || s.aggs[a].type == PA_AGG_DISTINCTCOUNTHLL) continue;
+          if (q->emit_val_agg < 0) q->emit_val_agg = a;
+          if (pay[a] != 1 || !val_fast[a]) q->emit_fast = false;
+        }
         q->bin_slots = bin_slots;
         // records per thread per fill round: about a quarter of a bin per partition on uniform keys
         q->bin_parts = bin_parts;
@@ -1121,11 +1164,16 @@ int pa_query_prepare(pa_query* q) {
           const int t = s.aggs[a].type;
           if (t == PA_AGG_COUNT) continue;
           q->part_agg_lds[a] = (int)off;
-          off += (size_t)kr * ((t == PA_AGG_SUM && agg_src[a] == SRC_LONG) ? 16 : 8);
+          if (t == PA_AGG_DISTINCTCOUNTHLL) off += (((size_t)kr << s.aggs[a].log2m) + 15) & ~(size_t)15;
+          else off += (size_t)kr * ((t == PA_AGG_SUM && agg_src[a] == SRC_LONG) ? 16 : 8);
         }
         q->part_lds_c = (int)off;
       }
     }
+  }
+  if (!q->partitioned) {
+    q->hll_agg = -1;
+    q->hll_key_shift = 0;
   }
   if (q->strategy == STRAT_GLOBAL && !q->partitioned) plan = plan_pick(STRAT_GLOBAL);
   if (plan.score < 0) return fail(PA_EUNSUPPORTED, "staged columns too wide for the LDS tile ring");
@@ -1238,8 +1286,29 @@ int pa_query_prepare(pa_query* q) {
     dev_free(q->wave_cnt);
     // emit buffer: every wave's range holds all docs of its tiles; partitions: every doc plus each (workgroup,
     // partition) range's padding
-    const size_t emit_recs = (size_t)q->num_tiles * (size_t)q->steps * kWave;
-    const size_t part_recs = (size_t)q->num_docs + (size_t)q->grid * q->part_P * (kPartGroup - 1);
+    size_t emit_recs = (size_t)q->num_tiles * (size_t)q->steps * kWave;
+    size_t doc_recs = (size_t)q->num_docs;
+    dev_free(q->tile_rec);
+    h.tile_rec_base = nullptr;
+    if (q->hll_agg >= 0) {
+      // one record per value of the HLL column: every wave tile's first record from a scan of per-tile counts
+      rc = dev_alloc(q->tile_rec, ((size_t)q->num_tiles + 1) * 4);
+      if (rc) return rc;
+      for (int si = 0; si < q->nseg; ++si) {
+        const DevSeg& hs = q->hsegs[si];
+        const DevCol& dc = hs.cols[agg_slot[q->hll_agg]];
+        PA_HIP(launch_tile_records(dc.kind == COL_MV_DICT ? dc.mv_off : nullptr, hs.num_docs, q->steps * kWave,
+                                   hs.num_wtiles, (uint32_t*)q->tile_rec.p + hs.first_wtile, nullptr));
+      }
+      PA_HIP(launch_exclusive_scan_u32((uint32_t*)q->tile_rec.p, (int64_t)q->num_tiles, nullptr));
+      uint32_t total = 0;
+      PA_HIP(hipMemcpy(&total, (uint32_t*)q->tile_rec.p + q->num_tiles, 4, hipMemcpyDeviceToHost));
+      if (total >= (1u << 31)) return fail(PA_EUNSUPPORTED, "more than 2^31 HLL values in one partitioned query");
+      emit_recs = total;
+      doc_recs = total;
+      h.tile_rec_base = (const uint32_t*)q->tile_rec.p;
+    }
+    const size_t part_recs = doc_recs + (size_t)q->grid * q->part_P * (kPartGroup - 1);
     rc = dev_alloc(q->part_hist, (size_t)q->grid * q->part_P * 4);
     if (!rc) rc = dev_alloc(q->part_off, (size_t)q->grid * q->part_P * 4);
     if (!rc) rc = dev_alloc(q->part_base, (size_t)(q->part_P + 1) * 4);
@@ -1260,6 +1329,10 @@ int pa_query_prepare(pa_query* q) {
     h.bin_slots = q->bin_slots;
     h.bin_iter = q->bin_iter;
     h.bin_parts = q->bin_parts;
+    h.emit_fast = q->emit_fast ? 1 : 0;
+    h.emit_val_agg = q->emit_val_agg;
+    h.hll_agg = q->hll_agg;
+    h.key_shift = q->hll_key_shift;
   }
 
   if (q->limit_mode) {

@@ -138,7 +138,15 @@ struct DevQuery {
   int32_t bin_slots;         // part_bin_kernel: records per LDS bin (power of two >= kPartGroup)
   int32_t bin_iter;          // part_bin_kernel: records per thread per fill round
   int32_t bin_parts;         // part_bin_kernel: partitions binned per read of the records (all P when they fit LDS)
+  int32_t emit_fast;         // emit pass: (key, value) records of 2 or 3 words through the batched fast path
+  int32_t emit_val_agg;      // emit fast path: the aggregation whose value the records carry (-1: COUNT only)
+  int32_t hll_agg;           // partitioned DISTINCTCOUNTHLL(MV): its aggregation index (-1: none). Record word 0 is then
+                             // key << key_shift | register << 6 | rank << 1 | first-record-of-the-doc; one record per
+                             // value of an MV column (one with rank 0 for a doc without values)
+  int32_t key_shift;         // 0, or log2m + 6 with hll_agg
   int32_t pad4;
+  const uint32_t* tile_rec_base;  // with hll_agg: [total_wtiles + 1] first emit record of every wave tile (records of
+                                  // the tiles before it, max(1, values) per doc); nullptr: one record per doc
   int32_t staged_slots[kMaxSlots];
   int32_t gb_slot[PA_MAX_GROUP_BY];
   int64_t gb_stride[PA_MAX_GROUP_BY];

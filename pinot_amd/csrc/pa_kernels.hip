@@ -525,6 +525,55 @@ __device__ __forceinline__ void emit_doc(const DevQuery* __restrict__ q, const D
   }
 }
 
+// Records a matching doc emits with a partitioned DISTINCTCOUNTHLL(MV): one per value of an MV column (at least one).
+__device__ __forceinline__ uint32_t emit_count_hll(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                                   int64_t doc) {
+  const DevCol& c = seg->cols[q->aggs[q->hll_agg].slot];
+  if (c.kind != COL_MV_DICT) return 1u;
+  const int32_t n = gp(c.mv_off)[doc + 1] - gp(c.mv_off)[doc];
+  return n > 0 ? (uint32_t)n : 1u;
+}
+
+// The records of one matching doc with a partitioned DISTINCTCOUNTHLL(MV), from record index `pos`: word 0 packs the
+// key, the HLL register and rank of one value and the doc's first-record flag (COUNT and the per-doc aggregations count
+// only first records); the per-doc payload words follow, as in emit_doc.
+__device__ __forceinline__ void emit_doc_hll(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                             const uint32_t* img, int doc_local, int64_t doc, uint32_t* part_lds,
+                                             uint32_t pos, uint32_t n) {
+  const int64_t key = emit_key(q, seg, img, doc_local, doc);
+  atomicAdd(part_lds + (uint32_t)(key >> q->part_shift), n);
+  const int W = q->rec_words;
+  const uint32_t kw = (uint32_t)key << q->key_shift;
+  const int ha = q->hll_agg;
+  const DevAgg& H = q->aggs[ha];
+  const DevCol& hc = seg->cols[H.slot];
+  int32_t v0 = 0, v1 = 0;
+  if (hc.kind == COL_MV_DICT) {
+    v0 = gp(hc.mv_off)[doc];
+    v1 = gp(hc.mv_off)[doc + 1];
+  }
+  for (uint32_t e = 0; e < n; ++e) {
+    uint32_t hv;  // (register << 8) | rank; 0 = no value
+    if (hc.kind == COL_MV_DICT) hv = v0 + (int32_t)e < v1 ? (uint32_t)agg_value_mv(H, ha, seg, hc, v0 + e).i : 0u;
+    else hv = (uint32_t)agg_value(H, ha, seg, img, doc_local, doc).i;
+    AS1 uint32_t* r = gp(q->emit) + (size_t)(pos + e) * (uint32_t)W;
+    r[0] = kw | ((hv >> 8) << 6) | ((hv & 0xffu) << 1) | (e == 0 ? 1u : 0u);
+    for (int a = 0; a < q->num_aggs; ++a) {
+      const DevAgg& A = q->aggs[a];
+      if (A.type == PA_AGG_COUNT || a == ha) continue;
+      if (e != 0) continue;  // payloads matter in the first record only
+      const AggValue v = agg_value(A, a, seg, img, doc_local, doc);
+      if (A.src == SRC_INT) {
+        r[A.pay_off] = (uint32_t)v.i;
+      } else {
+        const int64_t b = A.src == SRC_DOUBLE ? __builtin_bit_cast(int64_t, v.d) : v.i;
+        r[A.pay_off] = (uint32_t)b;
+        r[A.pay_off + 1] = (uint32_t)(b >> 32);
+      }
+    }
+  }
+}
+
 // Match word of one leaf over a whole wave tile: bit i of lane l <=> doc 64*i + l of the tile matches.
 // Leaf parameters are loaded once per tile; the 32 decodes are independent, so the LDS reads pipeline.
 template <int STEPS>
@@ -712,90 +761,113 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
     // the wave's record cursor lives in LDS after the partition counters (wave-uniform)
     uint32_t* cur = (uint32_t*)lds + q->num_parts + (threadIdx.x >> 6);
     uint32_t c = __builtin_amdgcn_readfirstlane(*cur);
-    if (q->rec_words <= 2 && q->num_gb <= 2) {
-      // (key, one int32 value) records over <= 2 dictionary group-by columns. The descriptors are read once per tile
-      // into registers (reading them per doc through the generic segment pointer reloads them after every LDS atomic,
-      // each load behind a vmcnt wait that also drains the tile ring). Every dictId decode, then every
-      // remap / value gather (they overlap), then keys + LDS histogram, then the coalesced record stores, 8 steps at a time.
-      int va = -1;
-      for (int a = 0; a < q->num_aggs && va < 0; ++a)
-        if (q->aggs[a].type != PA_AGG_COUNT) va = a;
+    if (q->hll_agg >= 0) {
+      // a variable number of records per doc: wave prefix sum of the counts gives every lane its first record
+      for (int i = 0; i < STEPS; ++i) {
+        const bool mine = (m >> i) & 1u;
+        if (__ballot(mine) == 0) continue;
+        const uint32_t n = mine ? emit_count_hll(q, seg, doc_base + local(i)) : 0u;
+        uint32_t incl = n;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+          const uint32_t t = __shfl_up(incl, o, kWave);
+          if (lane >= o) incl += t;
+        }
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+        if (mine) emit_doc_hll(q, seg, img, local(i), doc_base + local(i), (uint32_t*)lds, c + incl - n, n);
+        c += total;
+      }
+    } else
+    // fast path: (key, value) records of 2 or 3 words with the value from a dictionary column or a raw INT / LONG /
+    // DOUBLE column
+    if (q->emit_fast) {
+      // Descriptors through the constant address space: the segment is read-only during the kernel and its pointer
+      // is wave-uniform, so every field is a scalar load the compiler keeps across the LDS atomics and the record
+      // stores (through the generic pointer they were vector loads, reloaded after every LDS atomic, each behind a
+      // vmcnt wait that also drained the tile ring). Per batch of 8 steps: per group-by column every dictId decode,
+      // then every remap gather (they overlap), then the value gathers, then keys + LDS histogram, then the
+      // coalesced record stores.
+      typedef const __attribute__((address_space(4))) DevSeg CSeg;
+      CSeg* cs = (CSeg*)(uintptr_t)seg;
       const int ngb = q->num_gb;
-      const DevCol& c0 = seg->cols[q->gb_slot[0]];
-      const int gl0 = c0.lds_off, gn0 = c0.nbits;
-      const uint32_t* gw0 = c0.words;
-      const int32_t* rm0 = seg->remap[0];
-      const uint32_t st0 = (uint32_t)q->gb_stride[0];
-      int gl1 = -1, gn1 = 1;
-      const uint32_t* gw1 = nullptr;
-      const int32_t* rm1 = nullptr;
-      uint32_t st1 = 0;
-      if (ngb > 1) {
-        const DevCol& c1 = seg->cols[q->gb_slot[1]];
-        gl1 = c1.lds_off;
-        gn1 = c1.nbits;
-        gw1 = c1.words;
-        rm1 = seg->remap[1];
-        st1 = (uint32_t)q->gb_stride[1];
-      }
-      int vkind = 0, vl = -1, vn = 1, vtype = 0;  // vkind 1: dictionary column, 2: raw INT / LONG column
-      const uint32_t* vw = nullptr;
-      const int64_t* vd = nullptr;
-      const void* vraw = nullptr;
-      if (va >= 0) {
-        const DevCol& cv = seg->cols[q->aggs[va].slot];
-        vkind = cv.kind == COL_SV_DICT ? 1 : 2;
-        vl = cv.lds_off;
-        vn = cv.nbits;
-        vw = cv.words;
-        vd = cv.dict_i64;
-        vraw = cv.raw;
-        vtype = cv.vtype;
-      }
+      const int va = q->emit_val_agg;
+      const int W = q->rec_words;  // 2: 32-bit value, 3: 64-bit value
+      const int vslot = va >= 0 ? q->aggs[va].slot : 0;
+      const int vkind = va >= 0 ? cs->cols[vslot].kind : 0;
+      const int vl = cs->cols[vslot].lds_off, vn = cs->cols[vslot].nbits, vtype = cs->cols[vslot].vtype;
+      const uint32_t* vw = cs->cols[vslot].words;
+      const uint64_t* vd = q->aggs[va < 0 ? 0 : va].src == SRC_DOUBLE ? (const uint64_t*)cs->cols[vslot].dict_f64
+                                                                      : (const uint64_t*)cs->cols[vslot].dict_i64;
+      const void* vraw = cs->cols[vslot].raw;
       const int shift = q->part_shift;
-      AS1 uint64_t* out = (AS1 uint64_t*)gp(q->emit);
-      constexpr int kEB = 8;  // steps per batch (register budget: 3 words per step and lane)
+      constexpr int kEB = 8;  // steps per batch (register budget)
 #pragma unroll 1
       for (int h = 0; h < STEPS; h += kEB) {
-        uint32_t id0[kEB], id1[kEB], vv[kEB];
+        uint32_t key[kEB], lo[kEB], hi[kEB];
 #pragma unroll
-        for (int i = 0; i < kEB; ++i) {
-          id0[i] = id1[i] = vv[i] = 0u;
-          if ((m >> (h + i)) & 1u) {
-            const int dl = local(h + i);
-            const int64_t doc = doc_base + dl;
-            id0[i] = gl0 >= 0 ? decode_lds(img + gl0, dl, gn0) : decode_global(gw0, doc, gn0);
-            if (ngb > 1) id1[i] = gl1 >= 0 ? decode_lds(img + gl1, dl, gn1) : decode_global(gw1, doc, gn1);
-            if (vkind == 1) vv[i] = vl >= 0 ? decode_lds(img + vl, dl, vn) : decode_global(vw, doc, vn);
+        for (int i = 0; i < kEB; ++i) key[i] = lo[i] = hi[i] = 0u;
+        for (int j = 0; j < ngb; ++j) {
+          const int slot = q->gb_slot[j];
+          const int gl = cs->cols[slot].lds_off, gn = cs->cols[slot].nbits;
+          const uint32_t* gw = cs->cols[slot].words;
+          const int32_t* rm = cs->remap[j];
+          const uint32_t st = (uint32_t)q->gb_stride[j];
+          uint32_t id[kEB];
+#pragma unroll
+          for (int i = 0; i < kEB; ++i) {
+            id[i] = 0u;
+            if ((m >> (h + i)) & 1u) {
+              const int dl = local(h + i);
+              id[i] = gl >= 0 ? decode_lds(img + gl, dl, gn) : decode_global(gw, doc_base + dl, gn);
+            }
+          }
+          if (rm != nullptr) {
+#pragma unroll
+            for (int i = 0; i < kEB; ++i)
+              if ((m >> (h + i)) & 1u) id[i] = (uint32_t)gp(rm)[id[i]];
+          }
+#pragma unroll
+          for (int i = 0; i < kEB; ++i) key[i] += id[i] * st;  // table-wide key (< 2^32 on this path)
+        }
+        if (vkind != 0) {
+#pragma unroll
+          for (int i = 0; i < kEB; ++i) {
+            if ((m >> (h + i)) & 1u) {
+              const int dl = local(h + i);
+              const int64_t doc = doc_base + dl;
+              uint64_t v;
+              if (vkind == COL_SV_DICT) {
+                const uint32_t vid = vl >= 0 ? decode_lds(img + vl, dl, vn) : decode_global(vw, doc, vn);
+                v = gp(vd)[vid];
+              } else if (vtype == PA_INT) {
+                v = (uint64_t)(int64_t)gp((const int32_t*)vraw)[doc];
+              } else {  // LONG, or DOUBLE bits (a SUM/MIN/MAX over a raw DOUBLE column reads the bits unchanged)
+                v = gp((const uint64_t*)vraw)[doc];
+              }
+              lo[i] = (uint32_t)v;
+              hi[i] = (uint32_t)(v >> 32);
+            }
           }
         }
 #pragma unroll
-        for (int i = 0; i < kEB; ++i) {
-          if ((m >> (h + i)) & 1u) {
-            const int64_t doc = doc_base + local(h + i);
-            if (rm0 != nullptr) id0[i] = (uint32_t)gp(rm0)[id0[i]];
-            if (rm1 != nullptr) id1[i] = (uint32_t)gp(rm1)[id1[i]];
-            if (vkind == 1) vv[i] = (uint32_t)gp(vd)[vv[i]];
-            else if (vkind == 2) vv[i] = vtype == PA_INT ? (uint32_t)gp((const int32_t*)vraw)[doc]
-                                                         : (uint32_t)gp((const int64_t*)vraw)[doc];
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < kEB; ++i) {
-          if ((m >> (h + i)) & 1u) {
-            id0[i] = id0[i] * st0 + id1[i] * st1;  // table-wide key (< 2^32 on this path)
-            atomicAdd((uint32_t*)lds + (id0[i] >> shift), 1u);
-          }
-        }
+        for (int i = 0; i < kEB; ++i)
+          if ((m >> (h + i)) & 1u) atomicAdd((uint32_t*)lds + (key[i] >> shift), 1u);
 #pragma unroll
         for (int i = 0; i < kEB; ++i) {
           const bool mine = (m >> (h + i)) & 1u;
           const uint64_t sm = __ballot(mine);
           if (sm == 0) continue;
           if (mine) {
-            const uint32_t rank =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-            out[c + rank] = ((uint64_t)vv[i] << 32) | id0[i];
+            const uint32_t pos = c + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+            if (W == 2) {
+              ((AS1 uint64_t*)gp(q->emit))[pos] = ((uint64_t)lo[i] << 32) | key[i];
+            } else {
+              AS1 uint32_t* r = gp(q->emit) + (size_t)pos * 3u;
+              r[0] = key[i];
+              r[1] = lo[i];
+              r[2] = hi[i];
+            }
           }
           c += (uint32_t)__builtin_popcountll(sm);
         }
@@ -1116,7 +1188,8 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
     if (threadIdx.x < kWavesPerWG) {
       const int64_t gwi = (q->xcd_major ? xcd_major_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x) * kWavesPerWG +
                           threadIdx.x;
-      pl[P + threadIdx.x] = (uint32_t)(gwi * q->total_wtiles / ((int64_t)gridDim.x * kWavesPerWG) * (q->steps * kWave));
+      const int64_t tw = gwi * q->total_wtiles / ((int64_t)gridDim.x * kWavesPerWG);
+      pl[P + threadIdx.x] = q->tile_rec_base ? q->tile_rec_base[tw] : (uint32_t)(tw * (q->steps * kWave));
     }
     __syncthreads();
   }
@@ -1253,7 +1326,7 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
     const int P = q->num_parts;
     for (int p = threadIdx.x; p < P; p += kWGSize) gp(q->part_hist)[(size_t)lb * P + p] = pl[p];
     if (lane == 0)
-      gp(q->wave_cnt)[gw] = pl[P + wave] - (uint32_t)(t0 * (q->steps * kWave));
+      gp(q->wave_cnt)[gw] = pl[P + wave] - (q->tile_rec_base ? q->tile_rec_base[t0] : (uint32_t)(t0 * (q->steps * kWave)));
   }
   if (STRAT == STRAT_LDS) {
     __syncthreads();
@@ -1659,13 +1732,14 @@ __global__ void __launch_bounds__(kPartBinThreads) part_bin_kernel(const DevQuer
 #pragma unroll
   for (int k = 0; k < kWavesPerWG; ++k) {
     const int64_t gwi = (int64_t)b * kWavesPerWG + k;
-    rs[k] = (uint32_t)(gwi * q->total_wtiles / Wt * tile_docs);
+    const int64_t tw = gwi * q->total_wtiles / Wt;
+    rs[k] = q->tile_rec_base ? q->tile_rec_base[tw] : (uint32_t)(tw * tile_docs);
     rn[k] = q->wave_cnt[gwi];
     n_all += rn[k];
   }
   const AS1 uint32_t* src = gp((const uint32_t*)q->emit);
   AS1 uint32_t* dst = gp(q->recs);
-  const int shift = q->part_shift;
+  const int shift = q->part_shift + q->key_shift;  // record word 0 -> partition
   const uint32_t round = (uint32_t)q->bin_iter * kPartBinThreads;
   for (int plo = 0; plo < P; plo += PB) {
     const int np = min(PB, P - plo);
@@ -1798,6 +1872,11 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
   for (int a = 0; a < q->num_aggs; ++a) {
     const DevAgg& A = q->aggs[a];
     if (A.type == PA_AGG_COUNT) continue;
+    if (A.type == PA_AGG_DISTINCTCOUNTHLL) {  // one byte per register
+      uint32_t* r = (uint32_t*)(lds + A.lds_off);
+      for (int64_t k = threadIdx.x; k < (KR << A.log2m) / 4; k += kPartAggThreads) r[k] = 0u;
+      continue;
+    }
     int64_t* r = (int64_t*)(lds + A.lds_off);
     const int64_t init = A.type == PA_AGG_MIN ? INT64_MAX : (A.type == PA_AGG_MAX ? INT64_MIN : 0);
     const int64_t n = (A.type == PA_AGG_SUM && A.src == SRC_LONG) ? 2 * KR : KR;
@@ -1806,8 +1885,9 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
   __syncthreads();
   const uint32_t r0 = q->part_base[p], r1 = q->part_base[p + 1];
   const int W = q->rec_words;
+  const int ks = q->key_shift;
   uint32_t rstart = r0;
-  if (W == 2) {
+  if (W == 2 && ks == 0) {
     // (key, int32 value) records, 8 per thread in flight: every load first, then the LDS updates
     constexpr int kB = 8;
     int va = -1;
@@ -1848,12 +1928,30 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
   }
   for (uint32_t ri = rstart + threadIdx.x; ri < r1; ri += kPartAggThreads) {
     const AS1 uint32_t* rec = gp(q->recs) + (size_t)ri * (uint32_t)W;
-    if (rec[0] == 0xffffffffu) continue;  // range padding (part_bin_kernel)
-    const int64_t lk = (int64_t)rec[0] - kbase;
+    const uint32_t w0 = rec[0];
+    if (w0 == 0xffffffffu) continue;  // range padding (part_bin_kernel; never a valid record: its rank field is 31)
+    const int64_t lk = (int64_t)(w0 >> ks) - kbase;
+    if (ks != 0) {  // DISTINCTCOUNTHLL(MV) record: register max of one value, the rest on the doc's first record only
+      const DevAgg& H = q->aggs[q->hll_agg];
+      const uint32_t rank = (w0 >> 1) & 31u;
+      if (rank != 0) {
+        const uint32_t idx = ((uint32_t)lk << H.log2m) | ((w0 >> 6) & ((1u << H.log2m) - 1u));
+        uint32_t* wp = (uint32_t*)(lds + H.lds_off) + (idx >> 2);
+        const uint32_t sh = (idx & 3u) * 8u;
+        uint32_t old = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (((old >> sh) & 0xffu) < rank) {  // byte max by compare-and-swap (rarely more than one try)
+          const uint32_t nw = (old & ~(0xffu << sh)) | (rank << sh);
+          const uint32_t prev = atomicCAS(wp, old, nw);
+          if (prev == old) break;
+          old = prev;
+        }
+      }
+      if ((w0 & 1u) == 0) continue;
+    }
     atomicAdd(cnt + lk, 1u);
     for (int a = 0; a < q->num_aggs; ++a) {
       const DevAgg& A = q->aggs[a];
-      if (A.type == PA_AGG_COUNT) continue;
+      if (A.type == PA_AGG_COUNT || A.type == PA_AGG_DISTINCTCOUNTHLL) continue;
       int64_t iv;
       if (A.src == SRC_INT) iv = (int64_t)(int32_t)rec[A.pay_off];
       else iv = (int64_t)(((uint64_t)rec[A.pay_off + 1] << 32) | rec[A.pay_off]);
@@ -1904,6 +2002,44 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
       }
     }
   }
+  if (q->hll_agg >= 0) {  // the partition's registers (bytes) into the u32 global registers it owns
+    const DevAgg& H = q->aggs[q->hll_agg];
+    const unsigned char* reg = lds + H.lds_off;
+    const int64_t n = nk << H.log2m;
+    for (int64_t i = threadIdx.x; i < n; i += kPartAggThreads) {
+      const uint32_t v = reg[i];
+      if (v == 0) continue;
+      AS1 uint32_t* g = gp(H.acc_hll) + ((kbase << H.log2m) + i);
+      if (v > *g) *g = v;
+    }
+  }
+}
+
+// Records of every wave tile of one segment for the emit pass with a partitioned DISTINCTCOUNTHLL(MV): max(1, values)
+// per doc of a multi-value column (mv_off), one per doc otherwise.
+__global__ void tile_records_kernel(const int32_t* mv_off, int32_t num_docs, int32_t tile_docs, int32_t ntiles,
+                                    uint32_t* out) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += gridDim.x * blockDim.x) {
+    const int32_t d0 = t * tile_docs, d1 = min(num_docs, d0 + tile_docs);
+    uint32_t n = 0;
+    if (mv_off == nullptr) {
+      n = d1 > d0 ? (uint32_t)(d1 - d0) : 0u;
+    } else {
+      for (int32_t d = d0; d < d1; ++d) n += (uint32_t)max(1, mv_off[d + 1] - mv_off[d]);
+    }
+    out[t] = n;
+  }
+}
+
+hipError_t launch_tile_records(const int32_t* mv_off, int32_t num_docs, int32_t tile_docs, int32_t ntiles,
+                               uint32_t* out, hipStream_t s) {
+  if (ntiles > 0) tile_records_kernel<<<(ntiles + 255) / 256, 256, 0, s>>>(mv_off, num_docs, tile_docs, ntiles, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_exclusive_scan_u32(uint32_t* v, int64_t n, hipStream_t s) {
+  compact_scan_kernel<<<1, 256, 0, s>>>(v, n);
+  return hipGetLastError();
 }
 
 hipError_t launch_part_offsets(const uint32_t* hist, uint32_t* off, int G, int P, uint32_t* part_base, hipStream_t s) {

@@ -46,6 +46,9 @@ hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t*
                          hipStream_t s);
 hipError_t launch_part_offsets(const uint32_t* hist, uint32_t* off, int G, int P, uint32_t* part_base, hipStream_t s);
 hipError_t set_part_bin_lds_limit(int lds_bytes);
+hipError_t launch_tile_records(const int32_t* mv_off, int32_t num_docs, int32_t tile_docs, int32_t ntiles,
+                               uint32_t* out, hipStream_t s);
+hipError_t launch_exclusive_scan_u32(uint32_t* v, int64_t n, hipStream_t s);
 hipError_t launch_part_bin(const DevQuery* q, int G, int lds_bytes, hipStream_t s);
 hipError_t set_part_agg_lds_limit(int lds_bytes);
 hipError_t launch_part_agg(const DevQuery* q, int P, int lds_bytes, hipStream_t s);

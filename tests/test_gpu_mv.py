@@ -15,6 +15,8 @@ import pytest
 
 from pinot_amd import _lib as L
 from pinot_amd.segment import create_segment
+from pinot_amd import parse_sql
+from pinot_amd.engine import GpuQueryExecutor, GpuSegment
 from test_gpu_parity import DOUBLE_REL, run_both
 
 pytestmark = pytest.mark.gpu
@@ -120,6 +122,33 @@ def test_star_schema_config4_shape():
             for i, n in enumerate((40009, 17011))]
     run_both("SELECT d1, d2, d3, d4, SUM(r), DISTINCTCOUNTHLLMV(tags), COUNT(*) FROM t WHERE d4 <> 14 "
              "GROUP BY d1, d2, d3, d4 LIMIT 100000", segs, rel=DOUBLE_REL)
+
+
+@pytest.mark.parametrize("flags", [0, L.PA_QF_NO_PARTITION])
+def test_star_schema_partitioned_hll(flags):
+    """configs[4] shape over a key space that takes the partitioned path: one record per MV value carries the HLL
+    register and rank, COUNT / SUM(r) count each doc once; HLL registers bit-exact, SUM(r) within DOUBLE_REL. Also an SV
+    DISTINCTCOUNTHLL and a COUNT-only HLL query."""
+    sv = (("d1", 64), ("d2", 32), ("d3", 16), ("d4", 8))
+    segs = [mv_segment(30 + i, n, mv_cols=(("tags", 300, 6),), sv_cols=sv, raw_double=True)
+            for i, n in enumerate((50021, 20011))]
+    gsegs = [GpuSegment(sg) for sg in segs]
+    try:
+        for sql in ("SELECT d1, d2, d3, d4, SUM(r), DISTINCTCOUNTHLLMV(tags), COUNT(*) FROM t GROUP BY d1, d2, d3, d4 "
+                    "LIMIT 1000000 OPTION(numGroupsLimit=1000000)",
+                    "SELECT d1, d2, d3, d4, DISTINCTCOUNTHLL(m), MAX(m) FROM t GROUP BY d1, d2, d3, d4 "
+                    "LIMIT 1000000 OPTION(numGroupsLimit=1000000)",
+                    "SELECT d4, d3, d2, d1, DISTINCTCOUNTHLLMV(tags) FROM t GROUP BY d4, d3, d2, d1 "
+                    "LIMIT 1000000 OPTION(numGroupsLimit=1000000)"):
+            got, exp, _ = run_both(sql, segs, gsegs=gsegs, flags=flags, rel=DOUBLE_REL)
+            assert len(got.groups) > 30000
+            ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags)
+            strategy = ex.stats()["plan"]["strategy"]
+            ex.close()
+            assert strategy == ("global" if flags else "partitioned"), (sql, strategy)
+    finally:
+        for g in gsegs:
+            g.close()
 
 
 def test_malformed_mv_index_rejected():

@@ -292,6 +292,30 @@ def test_partitioned_aggregation(flags):
             g.close()
 
 
+def test_partitioned_raw_values():
+    """Partitioned aggregation with raw (no-dictionary) value columns: INT and LONG (32/64-bit record payloads), DOUBLE
+    (bits), FLOAT (widened: generic emit), 4 group-by columns, a value column dictionary-encoded in one segment and raw
+    in the other; identical to the oracle (DOUBLE sums within DOUBLE_REL)."""
+    cols = {"k1": ("INT", 40), "k2": ("INT", 30), "k3": ("LONG", 20), "k4": ("INT", 16), "ri": ("INT", 500),
+            "rl": ("LONG", 0), "rd": ("DOUBLE", 0), "rf": ("FLOAT", 0)}
+    segs = [make_segment(90, 150007, cols, no_dict=("ri", "rl", "rd", "rf")),
+            make_segment(92, 60001, cols, no_dict=("rl", "rd", "rf"))]
+    gsegs = [GpuSegment(sg) for sg in segs]
+    try:
+        for agg in ("SUM(ri), MIN(ri)", "SUM(rl), MAX(rl)", "SUM(rd), MIN(rd), MAX(rd)", "SUM(rf)", "COUNT(*)"):
+            sql = ("SELECT k1, k2, k3, k4, COUNT(*), %s FROM t GROUP BY k1, k2, k3, k4 LIMIT 10000000 "
+                   "OPTION(numGroupsLimit=10000000)" % agg)
+            got, exp, _ = run_both(sql, segs, gsegs=gsegs, rel=DOUBLE_REL)
+            ex = GpuQueryExecutor(parse_sql(sql), gsegs)
+            strategy = ex.stats()["plan"]["strategy"]
+            ex.close()
+            assert strategy == "partitioned", (agg, strategy)
+            assert len(got.groups) > 100000
+    finally:
+        for g in gsegs:
+            g.close()
+
+
 @pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LANE_MAJOR])
 def test_raw_group_by_hashed(flags):
     """GROUP BY raw (no-dictionary) columns — INT, LONG, DOUBLE, and mixed with dictionary columns — through the hashed

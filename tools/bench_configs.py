@@ -68,6 +68,13 @@ WORKLOADS = {
     "star": (star_segment, [
         ("all_docs", "SELECT d1, d2, d3, d4, SUM(r), DISTINCTCOUNTHLLMV(tags) FROM t GROUP BY d1, d2, d3, d4 "
                      "LIMIT 1000000 OPTION(numGroupsLimit=1000000)", 0),
+        # decomposition of all_docs (which part of the work costs what)
+        ("count_only", "SELECT d1, d2, d3, d4, COUNT(*) FROM t GROUP BY d1, d2, d3, d4 "
+                       "LIMIT 1000000 OPTION(numGroupsLimit=1000000)", 0),
+        ("sum_only", "SELECT d1, d2, d3, d4, SUM(r) FROM t GROUP BY d1, d2, d3, d4 "
+                     "LIMIT 1000000 OPTION(numGroupsLimit=1000000)", 0),
+        ("hll_only", "SELECT d1, d2, d3, d4, DISTINCTCOUNTHLLMV(tags) FROM t GROUP BY d1, d2, d3, d4 "
+                     "LIMIT 1000000 OPTION(numGroupsLimit=1000000)", 0),
     ]),
 }
 
