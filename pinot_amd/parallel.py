@@ -64,6 +64,23 @@ def merge_results_across_ranks(executor, dst=0, group=None):
     return merge_intermediate(gathered) if rank == dst else None
 
 
+def section_runs(sections):
+    """[(kind, byte offset, elements)] -> [(kind, dtype, start byte, end byte)]: adjacent sections with the same reduce
+    op and element type merge into one collective over the byte span they cover (the 256-B alignment gaps between
+    them are zero and stay zero under SUM/MIN/MAX). The bench query's COUNT + 2x SUM(LONG) + numDocsScanned sections
+    become one RCCL reduce per step instead of four: small-message latency, not bytes, is the cost of this merge."""
+    runs = []
+    for kind, off, n in sorted(sections, key=lambda s: s[1]):
+        dt = SECTION_DTYPE[kind]
+        es = torch.empty(0, dtype=dt).element_size()
+        op = SECTION_OP[kind]
+        if op is not None and runs and SECTION_OP[runs[-1][0]] == op and runs[-1][1] == dt:
+            runs[-1][3] = off + n * es
+        else:
+            runs.append([kind, dt, off, off + n * es])
+    return [tuple(r) for r in runs]
+
+
 class DistributedAccumulators:
     """Moves an executor's accumulators into one torch-owned device block and reduces it across ranks (direct key
     spaces: the same key id addresses the same accumulator row on every GPU)."""
@@ -78,12 +95,8 @@ class DistributedAccumulators:
         pad = (-base) % 256
         self.base = base + pad
         L.check(lib.pa_query_set_accumulator_buffer(executor.handle, self.base, nbytes), "set_accumulator_buffer")
-        self.views = []
-        for kind, ptr, n in executor.sections():
-            off = ptr - self.base + pad
-            dt = SECTION_DTYPE[kind]
-            es = torch.empty(0, dtype=dt).element_size()
-            self.views.append((kind, self.buf[off:off + n * es].view(dt)))
+        runs = section_runs([(kind, ptr - self.base + pad, n) for kind, ptr, n in executor.sections()])
+        self.views = [(kind, self.buf[a:b].view(dt)) for kind, dt, a, b in runs]
 
     def reduce(self, dst=0, all_reduce=False):
         reduce_sections(self.views, dst=dst, all_reduce=all_reduce)

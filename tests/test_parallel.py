@@ -154,3 +154,81 @@ def test_gloo_key_based_merge_for_hashed_key_spaces():
                 exp[k] = [c, sm, mx]
     assert groups == exp
     assert docs == 201
+
+
+def _block_layout(secs):
+    """pa_capi.hip accumulator block: sections at 256-byte aligned offsets (gaps zero, as pa_query_reset leaves them)."""
+    offs, total = [], 0
+    for k, a in secs:
+        offs.append(total)
+        total += (a.nbytes + 255) & ~255
+    buf = np.zeros(total, dtype=np.uint8)
+    for o, (k, a) in zip(offs, secs):
+        buf[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8)
+    return buf, offs
+
+
+def _secs_with_docs(rank):
+    secs, _ = partial(rank)
+    # the bench query's layout: COUNT, 2x SUM(LONG), numDocsScanned — then the rest
+    return [secs[0], secs[1], (L.PA_ACC_SUM_I64X2, secs[1][1] * 3),
+            (L.PA_ACC_DOCS_U64, np.array([5 + rank, 0, 1], np.int64))] + secs[2:]
+
+
+def test_section_runs_merge_adjacent_same_op():
+    from pinot_amd.parallel import section_runs
+    secs = _secs_with_docs(0)
+    _, offs = _block_layout(secs)
+    runs = section_runs([(k, o, a.size) for (k, a), o in zip(secs, offs)])
+    # COUNT + SUM_I64X2 + SUM_I64X2 + DOCS -> one SUM run; then f64 SUM, MIN, MAX, HLL each on their own
+    assert [r[0] for r in runs] == [L.PA_ACC_COUNT_U64, L.PA_ACC_SUM_F64, L.PA_ACC_MIN_I64, L.PA_ACC_MAX_I64,
+                                    L.PA_ACC_HLL_U32]
+    assert runs[0][2] == 0 and runs[0][3] == offs[3] + 3 * 8
+    # a keys section (not element-wise reducible) never merges
+    r2 = section_runs([(L.PA_ACC_COUNT_U64, 0, 4), (L.PA_ACC_KEYS_I64, 256, 4), (L.PA_ACC_DOCS_U64, 512, 3)])
+    assert len(r2) == 3
+
+
+def _runs_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pinot_amd.parallel import section_runs
+    secs = _secs_with_docs(rank)
+    buf, offs = _block_layout(secs)
+    t = torch.from_numpy(buf)
+    runs = section_runs([(k, o, a.size) for (k, a), o in zip(secs, offs)])
+    reduce_sections([(k, t[a:b].view(dt)) for k, dt, a, b in runs], dst=0)
+    if rank == 0:
+        out[0] = t.numpy().copy()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_reduce_over_merged_section_runs():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_runs_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    parts = [_secs_with_docs(r) for r in range(world)]
+    bufs = [_block_layout(p)[0] for p in parts]
+    _, offs = _block_layout(parts[0])
+    got = out[0]
+    for i, (k, a) in enumerate(parts[0]):
+        dt = np.int32 if SECTION_DTYPE[k] == torch.int32 else a.dtype
+        g = got[offs[i]:offs[i] + a.nbytes].view(dt)
+        xs = [b[offs[i]:offs[i] + a.nbytes].view(dt) for b in bufs]
+        if k in (L.PA_ACC_MIN_I64,):
+            exp = np.minimum(*xs)
+        elif k in (L.PA_ACC_MAX_I64, L.PA_ACC_HLL_U32):
+            exp = np.maximum(*xs)
+        else:
+            exp = xs[0] + xs[1]
+        if k == L.PA_ACC_SUM_F64:
+            assert np.allclose(g, exp, rtol=1e-12, atol=0)
+        else:
+            assert np.array_equal(g, exp), k
+    # the alignment gaps stay zero
+    mask = np.ones(len(got), bool)
+    for o, (k, a) in zip(offs, parts[0]):
+        mask[o:o + a.nbytes] = False
+    assert not got[mask].any()
