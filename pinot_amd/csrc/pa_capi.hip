@@ -1527,9 +1527,12 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   // Decodes `nrows` host rows into the caller's arrays: row r has key key_of(r), count hc[r] and the aggregation
   // section rows at sec(section)[r * per]. Rows with a zero count are skipped when `skip_empty`.
   // `order` (optional) lists the rows to emit, in output order (hashed key spaces: sorted by packed key).
+  // `hll_u8`: HLL register rows arrive already narrowed to one byte per register (GPU compaction path).
   auto decode = [&](int64_t nrows, const uint64_t* hc, const std::function<const char*(int)>& sec,
                     const std::function<int64_t(int64_t)>& key_of, bool skip_empty,
-                    const std::vector<int64_t>* order) -> int64_t {
+                    const std::vector<int64_t>* order, bool hll_u8) -> int64_t {
+    const char* asec[PA_MAX_AGGS];  // section base per aggregation, resolved once (not per row)
+    for (int a = 0; a < s.num_aggs; ++a) asec[a] = q->agg_section[a] >= 0 ? sec(q->agg_section[a]) : nullptr;
     int64_t n = 0;
     const int64_t total = order ? (int64_t)order->size() : nrows;
     for (int64_t oi = 0; oi < total; ++oi) {
@@ -1546,13 +1549,17 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
             outd[n] = (double)hc[r];
             continue;
           }
-          const char* sp = sec(q->agg_section[a]);
+          const char* sp = asec[a];
           const int src = q->hq.aggs[a].src;
           if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
             const int64_t per = int64_t(1) << A.log2m;
-            const uint32_t* rg = (const uint32_t*)sp + r * per;
             uint8_t* o = (uint8_t*)out_aggs[a] + n * per;
-            for (int64_t j = 0; j < per; ++j) o[j] = (uint8_t)rg[j];
+            if (hll_u8) {
+              std::memcpy(o, (const uint8_t*)sp + r * per, (size_t)per);
+            } else {
+              const uint32_t* rg = (const uint32_t*)sp + r * per;
+              for (int64_t j = 0; j < per; ++j) o[j] = (uint8_t)rg[j];
+            }
           } else if (A.type == PA_AGG_SUM || A.type == PA_AGG_COUNT_MV) {
             const int64_t* hv = (const int64_t*)sp;
             // SRC_LONG: exact 96-bit total, rounded once (the reference's double of the exact sum)
@@ -1594,9 +1601,9 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
       for (int64_t r = 0; r < K; ++r)
         if (hc[r]) order.push_back(r);
       std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return hk[a] < hk[b]; });
-      return decode(K, hc, hsec, [&](int64_t r) { return hk[r]; }, false, &order);
+      return decode(K, hc, hsec, [&](int64_t r) { return hk[r]; }, false, &order, false);
     }
-    return decode(K, hc, hsec, [](int64_t r) { return r; }, grouped, nullptr);
+    return decode(K, hc, hsec, [](int64_t r) { return r; }, grouped, nullptr, false);
   }
 
   // Large key spaces: ordered compaction of the non-empty keys on the GPU (count + scan, then key ids and every
@@ -1635,7 +1642,7 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   size_t bytes = ((size_t)rows * 8 + 255) & ~(size_t)255;
   for (int sec : secs) {
     const Section& sc = q->sections[sec];
-    const int es = sc.kind == PA_ACC_HLL_U32 ? 4 : 8;
+    const int es = sc.kind == PA_ACC_HLL_U32 ? 1 : 8;  // HLL registers (< 64) narrowed to bytes by the gather
     const int64_t per = sc.n / K;
     offs.push_back(bytes);
     bytes += ((size_t)rows * per * es + 255) & ~(size_t)255;
@@ -1656,6 +1663,7 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   for (size_t i = 0; i < secs.size(); ++i) {
     const Section& sc = q->sections[secs[i]];
     d.es[i] = sc.kind == PA_ACC_HLL_U32 ? 4 : 8;
+    d.oes[i] = sc.kind == PA_ACC_HLL_U32 ? 1 : d.es[i];
     d.per[i] = sc.n / K;
     d.src[i] = sc.ptr;
     d.dst[i] = dstage + offs[i];
@@ -1675,11 +1683,11 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
     std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return pk[a] < pk[b]; });
     order.resize(rows_cap);
     decode(rows, (const uint64_t*)hsec[0], [&](int sec) { return hsec[sec]; }, [&](int64_t r) { return pk[r]; },
-           false, &order);
+           false, &order, true);
     return m;
   }
   decode(rows, (const uint64_t*)hsec[0], [&](int sec) { return hsec[sec]; }, [&](int64_t r) { return hkeys[r]; },
-         false, nullptr);
+         false, nullptr, true);
   return m;
 }
 

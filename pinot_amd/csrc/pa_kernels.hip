@@ -1660,6 +1660,11 @@ __global__ void __launch_bounds__(256) compact_gather_kernel(const unsigned long
           const uint64_t* src = (const uint64_t*)d.src[si] + k * per;
           uint64_t* dst = (uint64_t*)d.dst[si] + pos * per;
           for (int64_t e = 0; e < per; ++e) dst[e] = src[e];
+        } else if (d.oes[si] == 1) {  // HLL registers (< 64): one byte each in the staging block
+          const uint32_t* src = (const uint32_t*)d.src[si] + k * per;
+          uint32_t* dst = (uint32_t*)((uint8_t*)d.dst[si] + pos * per);  // per is a power of two >= 16
+          for (int64_t e = 0; e < per; e += 4)
+            dst[e >> 2] = (src[e] & 0xffu) | (src[e + 1] & 0xffu) << 8 | (src[e + 2] & 0xffu) << 16 | src[e + 3] << 24;
         } else {
           const uint32_t* src = (const uint32_t*)d.src[si] + k * per;
           uint32_t* dst = (uint32_t*)d.dst[si] + pos * per;

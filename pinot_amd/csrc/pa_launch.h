@@ -9,7 +9,8 @@ namespace pa {
 constexpr int kMaxCompactSections = PA_MAX_AGGS + 2;
 struct CompactDesc {
   int32_t nsec;
-  int32_t es[kMaxCompactSections];
+  int32_t es[kMaxCompactSections];   // source element bytes (8, or 4 = HLL registers)
+  int32_t oes[kMaxCompactSections];  // output element bytes (es, or 1: HLL registers narrowed to bytes)
   int64_t per[kMaxCompactSections];
   const void* src[kMaxCompactSections];
   void* dst[kMaxCompactSections];

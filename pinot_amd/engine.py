@@ -338,6 +338,10 @@ class GpuQueryExecutor:
         [one array per GPU accumulator: float64[n], or uint8[n << log2m] HLL registers]). Synchronises `stream`."""
         lib = L.lib()
         cap = 1 if not self.query.group_by else min(self.num_keys, 1 << 16)
+        if self.query.group_by and self.num_keys > 1 << 16:
+            # large key space: a capacity-0 call runs only the GPU count pass and returns the number of non-empty
+            # groups, so the gather + copy run once, at the exact size
+            cap = max(1, L.check(lib.pa_query_fetch(self.handle, stream, 0, None, None, None), "pa_query_fetch"))
         while True:
             keys = np.empty(cap, dtype=np.int64)
             counts = np.empty(cap, dtype=np.int64)

@@ -258,6 +258,27 @@ def test_high_cardinality_global_fallback():
     assert len(got.groups) > 100000
 
 
+def test_large_fetch_hll_registers_and_count_probe():
+    """Accumulator block > 1 MiB with HLL registers: GPU compaction narrows registers to bytes, the host copies them
+    as-is; >65536 keys makes fetch_arrays probe the group count first (capacity-0 call). Registers bit-exact."""
+    cols = {"k1": ("INT", 300), "k2": ("INT", 400), "v": ("LONG", 70000), "m": ("LONG", 100)}
+    seg = make_segment(31, 200000, cols)
+    got, exp, _ = run_both("SELECT k1, k2, COUNT(*), DISTINCTCOUNTHLL(v), SUM(m) FROM t GROUP BY k1, k2 "
+                           "LIMIT 1000000 OPTION(numGroupsLimit=2000000)", [seg])
+    assert len(got.groups) > 20000  # synth draws skewed dictIds; the key space is 120000 (> 65536: probe)
+    gs = [GpuSegment(seg)]
+    ex = GpuQueryExecutor(parse_sql("SELECT k1, COUNT(*), DISTINCTCOUNTHLL(v, 12) FROM t WHERE k2 < 100 GROUP BY k1"),
+                          gs)
+    ex.execute()
+    keys, counts, outs = ex.fetch_arrays()
+    hi = [i for i, a in enumerate(ex.pa_aggs) if a[0] == L.PA_AGG_DISTINCTCOUNTHLL][0]
+    assert outs[hi].dtype == np.uint8 and len(outs[hi]) == len(keys) << 12
+    ora = oracle.run_query(ex.query, [seg])
+    assert len(keys) == len(ora.groups)
+    ex.close()
+    gs[0].close()
+
+
 @pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LANE_MAJOR, L.PA_QF_NO_PARTITION, L.PA_QF_STAGE_ALL,
                                    1 << L.PA_QF_PART_SHIFT, 2 << L.PA_QF_PART_SHIFT,
                                    3 << L.PA_QF_PART_SHIFT | 1 << L.PA_QF_WG_SHIFT])

@@ -116,6 +116,7 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
             torch.cuda.synchronize()
             ms = a.elapsed_time(b) / reps
             ex.execute(sp)
+            torch.cuda.synchronize()  # fetch_ms = compaction + copy + host decode only
             t1 = time.perf_counter()
             keys, counts, outs = ex.fetch_arrays(sp)
             fetch_ms = (time.perf_counter() - t1) * 1e3
