@@ -241,7 +241,8 @@ void* pa_query_section(const pa_query* q, int32_t section, int32_t* kind, int64_
  * COUNT/SUM/MIN/MAX (the reference's intermediate type), uint8[capacity << log2m] for HLL registers.
  * For aggregation-only queries key 0 is always returned (count may be 0).
  * Returns the number of groups (may exceed capacity: then only `capacity` were written), <0 on error.
- * Synchronises `stream`. */
+ * capacity = 0 (output pointers may be NULL) only counts the groups — for large key spaces just the GPU count pass —
+ * so a caller can size its arrays exactly before the real fetch. Synchronises `stream`. */
 int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out_keys,
                        int64_t* out_counts, void* const* out_aggs);
 
