@@ -112,13 +112,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
+    # under a torch.distributed launcher (RANK set) the RCCL path runs even at world size 1 (rehearsal of N>1)
+    distributed = world > 1 or "RANK" in os.environ
+    if distributed:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=device)
 
     from pinot_amd import parse_sql
     from pinot_amd.engine import GpuQueryExecutor, GpuSegment
-    from pinot_amd.parallel import DistributedAccumulators, shard_segments
+    from pinot_amd.parallel import DistributedAccumulators, shard_segments, table_dictionaries
 
     q = parse_sql(QUERY)
     total_segments = args.segments * world
@@ -140,8 +142,11 @@ def main():
         rank, len(gsegs), sum(g.segment.num_docs for g in gsegs), sum(g.device_bytes for g in gsegs) / 1e9,
         time.perf_counter() - t_setup))
 
-    ex = GpuQueryExecutor(q, gsegs, flags=args.flags)
-    dacc = DistributedAccumulators(ex, device) if world > 1 else None
+    # N>1: every rank groups over the same table-wide dictionaries (union over all ranks' segments), so key ids line up
+    # across GPUs and the partial aggregates reduce element-wise
+    td = table_dictionaries(q, [g.segment for g in gsegs]) if distributed else None
+    ex = GpuQueryExecutor(q, gsegs, flags=args.flags, table_dicts=td)
+    dacc = DistributedAccumulators(ex, device) if distributed else None
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
 
@@ -169,17 +174,17 @@ def main():
     torch.cuda.synchronize()
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
 
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -235,7 +240,7 @@ def main():
     ex.close()
     for g in gsegs:
         g.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -131,9 +131,14 @@ def _flatten_filter(f, leaves, ops):
 
 
 class GpuQueryExecutor:
-    def __init__(self, query: Q.Query, gpu_segments: List[GpuSegment], flags=0, enforce_num_groups_limit=True):
+    def __init__(self, query: Q.Query, gpu_segments: List[GpuSegment], flags=0, enforce_num_groups_limit=True,
+                 table_dicts=None):
+        """table_dicts: optional {group-by column: sorted unique values} — the table-wide dictionary every rank of a
+        multi-GPU query must share so that key ids address the same accumulator rows everywhere
+        (parallel.table_dictionaries builds it); by default it is the union of these segments' dictionaries."""
         if not gpu_segments:
             raise ValueError("no segments")
+        self.table_dicts = table_dicts or {}
         self.query = query
         self.gsegs = gpu_segments
         self.segs = [g.segment for g in gpu_segments]
@@ -236,9 +241,14 @@ class GpuQueryExecutor:
                 raise UnsupportedQuery("group-by column %s is dictionary-encoded in some segments only" % name)
             self.raw_group_by.append(None)
             dicts = [s.column(name).dictionary for s in self.segs]
-            first = dicts[0]
-            same = all(d is first or (len(d) == len(first) and np.array_equal(d, first)) for d in dicts)
-            gd = first if same else np.unique(np.concatenate(dicts))
+            if name in self.table_dicts:
+                gd = np.asarray(self.table_dicts[name])
+                if not all(np.isin(d, gd).all() for d in dicts):
+                    raise ValueError("table dictionary of %s misses values of a bound segment" % name)
+            else:
+                first = dicts[0]
+                same = all(d is first or (len(d) == len(first) and np.array_equal(d, first)) for d in dicts)
+                gd = first if same else np.unique(np.concatenate(dicts))
             self.global_dicts.append(gd)
             spec.group_by_columns[j] = ids[name]
             spec.group_by_cardinality[j] = len(gd)

@@ -5,6 +5,9 @@ accumulates it into the SAME table-wide key space; the GroupByCombineOperator / 
 partial aggregates across GPUs then becomes one collective per accumulator section over RCCL (xGMI):
 SUM for COUNT/SUM, MIN for MIN, MAX for MAX and for HLL registers (HyperLogLog.addAll == register max).
 """
+import hashlib
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -81,6 +84,50 @@ def section_runs(sections):
     return [tuple(r) for r in runs]
 
 
+def table_dictionaries(query, segments, group=None):
+    """Table-wide dictionaries of the query's dictionary-encoded group-by columns, agreed across ranks: the union of
+    every rank's segment dictionaries (the value-keyed combine of GroupByCombineOperator needs the same key id for
+    the same value on every GPU before accumulators can be reduced element-wise). Pass the result to
+    GpuQueryExecutor(table_dicts=...) on every rank."""
+    local = {}
+    for name in query.group_by:
+        ds = [s.column(name).dictionary for s in segments if s.column(name).has_dictionary]
+        if ds:
+            local[name] = np.unique(np.concatenate(ds))
+    world = dist.get_world_size(group)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, local, group=group)
+    out = {}
+    for name in query.group_by:
+        parts = [g[name] for g in gathered if name in g]
+        if parts:
+            out[name] = np.unique(np.concatenate(parts))
+    return out
+
+
+def key_space_fingerprint(executor):
+    """62-bit digest of an executor's table-wide key space (key count + every group-by dictionary's values)."""
+    h = hashlib.blake2b(np.int64(executor.num_keys).tobytes(), digest_size=8)
+    for gd in executor.global_dicts:
+        if gd is None:
+            h.update(b"<raw>")
+        elif np.asarray(gd).dtype.kind in "USO":
+            h.update("\x00".join(map(str, gd)).encode())
+        else:
+            h.update(np.ascontiguousarray(gd).tobytes())
+        h.update(b"|")
+    return int.from_bytes(h.digest(), "little") & ((1 << 62) - 1)
+
+
+def check_same_key_space(fingerprint, device, group=None):
+    """Raises unless every rank holds the same key space (element-wise section reduces would be silently wrong)."""
+    t = torch.tensor([fingerprint, -fingerprint], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    if int(t[0]) != fingerprint or -int(t[1]) != fingerprint:
+        raise L.PinotAmdError("ranks hold different group-key spaces: build the executors with "
+                              "table_dicts=parallel.table_dictionaries(...)")
+
+
 class DistributedAccumulators:
     """Moves an executor's accumulators into one torch-owned device block and reduces it across ranks (direct key
     spaces: the same key id addresses the same accumulator row on every GPU)."""
@@ -88,6 +135,8 @@ class DistributedAccumulators:
     def __init__(self, executor, device):
         if getattr(executor, "hashed", False):
             raise L.PinotAmdError("hashed key space: merge with merge_results_across_ranks (slots differ per GPU)")
+        if dist.is_initialized():
+            check_same_key_space(key_space_fingerprint(executor), device)
         lib = L.lib()
         nbytes = int(lib.pa_query_accumulator_bytes(executor.handle))
         self.buf = torch.zeros(nbytes + 512, dtype=torch.uint8, device=device)

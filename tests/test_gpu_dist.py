@@ -1,0 +1,84 @@
+"""Multi-GPU merge on one GPU: two executors stand for two ranks whose segments carry DIFFERENT dictionaries. With the
+agreed table-wide dictionaries (parallel.table_dictionaries' union) their accumulator blocks line up key for key, so
+the element-wise reduce of the merged section runs (what RCCL does across GPUs) equals the oracle over all segments.
+A world-size-1 RCCL group runs the real DistributedAccumulators path (key-space check + reduce calls)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+import oracle
+from pinot_amd import _lib as L
+from pinot_amd import parse_sql
+from pinot_amd.engine import GpuQueryExecutor, GpuSegment
+from pinot_amd.parallel import SECTION_OP, DistributedAccumulators, key_space_fingerprint
+from synth import make_segment
+from test_gpu_parity import assert_same
+
+pytestmark = pytest.mark.gpu
+
+COLS = {"d1": ("INT", 60), "d2": ("STRING", 12), "m": ("LONG", 4000), "f": ("DOUBLE", 300)}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def rccl_world1():
+    dist.init_process_group("nccl", rank=0, world_size=1, init_method="tcp://127.0.0.1:%d" % _port(),
+                            device_id=torch.device("cuda", 0))
+    yield
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sql", [
+    "SELECT d1, COUNT(*), SUM(m), MIN(m), MAX(f), DISTINCTCOUNTHLL(m) FROM t GROUP BY d1 LIMIT 1000",
+    "SELECT d1, d2, COUNT(*), SUM(f), AVG(m) FROM t WHERE m > 0 GROUP BY d1, d2 LIMIT 10000",
+    "SELECT COUNT(*), SUM(m), MIN(f), MAX(m) FROM t WHERE d1 < 0",
+])
+def test_two_rank_merge_with_table_dictionaries(sql, rccl_world1):
+    shards = [[make_segment(500 + 10 * r + i, n, COLS) for i, n in enumerate((20011, 7001))] for r in range(2)]
+    q = parse_sql(sql)
+    td = {}
+    for name in q.group_by:
+        td[name] = np.unique(np.concatenate([s.column(name).dictionary for sh in shards for s in sh]))
+    gsegs = [[GpuSegment(s) for s in sh] for sh in shards]
+    exs = [GpuQueryExecutor(q, g, table_dicts=td) for g in gsegs]
+    try:
+        if q.group_by:
+            assert key_space_fingerprint(exs[0]) == key_space_fingerprint(exs[1])
+            plain = [GpuQueryExecutor(q, g) for g in gsegs]  # own-segment dictionaries: key spaces differ
+            assert key_space_fingerprint(plain[0]) != key_space_fingerprint(plain[1])
+            for e in plain:
+                e.close()
+        accs = [DistributedAccumulators(e, torch.device("cuda", 0)) for e in exs]
+        for e in exs:
+            e.execute()
+        torch.cuda.synchronize()
+        for (k0, t0), (k1, t1) in zip(accs[0].views, accs[1].views):
+            assert k0 == k1 and t0.shape == t1.shape
+            op = SECTION_OP[k0]
+            if op == dist.ReduceOp.SUM:
+                t0.add_(t1)
+            elif op == dist.ReduceOp.MIN:
+                torch.minimum(t0, t1, out=t0)
+            else:
+                torch.maximum(t0, t1, out=t0)
+        accs[0].reduce(dst=0)  # world size 1: RCCL reduce in place (identity)
+        got = exs[0].fetch()
+        exp = oracle.run_query(q, shards[0] + shards[1])
+        assert_same(got, exp, rel=1e-9)
+    finally:
+        for e in exs:
+            e.close()
+        for g in gsegs:
+            for x in g:
+                x.close()

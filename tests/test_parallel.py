@@ -232,3 +232,56 @@ def test_gloo_reduce_over_merged_section_runs():
     for o, (k, a) in zip(offs, parts[0]):
         mask[o:o + a.nbytes] = False
     assert not got[mask].any()
+
+
+def _dict_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pinot_amd import parse_sql
+    from pinot_amd.parallel import check_same_key_space, table_dictionaries
+    from synth import make_segment
+    q = parse_sql("SELECT d, s, COUNT(*) FROM t GROUP BY d, s")
+    segs = [make_segment(40 + 2 * rank + i, 500, {"d": ("INT", 30 + 10 * rank), "s": ("STRING", 5 + rank)})
+            for i in range(2)]
+    td = table_dictionaries(q, segs)
+    out[rank] = {k: v.tolist() for k, v in td.items()}
+    check_same_key_space(12345, "cpu")  # same on both ranks: passes
+    try:
+        check_same_key_space(100 + rank, "cpu")
+        out["raised%d" % rank] = False
+    except L.PinotAmdError:
+        out["raised%d" % rank] = True
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_table_dictionaries_and_key_space_check():
+    """Ranks whose segments carry different dictionaries agree on one table-wide dictionary per group-by column (the
+    union), and a key-space mismatch is refused on every rank instead of reducing misaligned accumulator rows."""
+    from synth import make_segment
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_dict_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    assert out[0] == out[1]
+    for name in ("d", "s"):
+        exp = set()
+        for r in range(world):
+            for i in range(2):
+                cols = {"d": ("INT", 30 + 10 * r), "s": ("STRING", 5 + r)}
+                exp |= set(make_segment(40 + 2 * r + i, 500, cols).column(name).dictionary.tolist())
+        assert out[0][name] == sorted(exp)
+    assert out["raised0"] and out["raised1"]
+
+
+def test_key_space_fingerprint_distinguishes_dictionaries():
+    from pinot_amd.parallel import key_space_fingerprint
+
+    class _E:
+        def __init__(self, n, dicts):
+            self.num_keys, self.global_dicts = n, dicts
+    a = key_space_fingerprint(_E(6, [np.array([1, 2, 3]), np.array(["x", "y"])]))
+    assert a == key_space_fingerprint(_E(6, [np.array([1, 2, 3]), np.array(["x", "y"])]))
+    assert a != key_space_fingerprint(_E(6, [np.array([1, 2, 4]), np.array(["x", "y"])]))
+    assert a != key_space_fingerprint(_E(6, [np.array([1, 2, 3]), np.array(["x", "z"])]))
+    assert a != key_space_fingerprint(_E(6, [np.array([1, 2, 3]), None]))
