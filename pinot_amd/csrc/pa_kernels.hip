@@ -525,54 +525,9 @@ __device__ __forceinline__ void emit_doc(const DevQuery* __restrict__ q, const D
   }
 }
 
-// Records a matching doc emits with a partitioned DISTINCTCOUNTHLL(MV): one per value of an MV column (at least one).
-__device__ __forceinline__ uint32_t emit_count_hll(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
-                                                   int64_t doc) {
-  const DevCol& c = seg->cols[q->aggs[q->hll_agg].slot];
-  if (c.kind != COL_MV_DICT) return 1u;
-  const int32_t n = gp(c.mv_off)[doc + 1] - gp(c.mv_off)[doc];
-  return n > 0 ? (uint32_t)n : 1u;
-}
-
-// The records of one matching doc with a partitioned DISTINCTCOUNTHLL(MV), from record index `pos`: word 0 packs the
-// key, the HLL register and rank of one value and the doc's first-record flag (COUNT and the per-doc aggregations count
-// only first records); the per-doc payload words follow, as in emit_doc.
-__device__ __forceinline__ void emit_doc_hll(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
-                                             const uint32_t* img, int doc_local, int64_t doc, uint32_t* part_lds,
-                                             uint32_t pos, uint32_t n) {
-  const int64_t key = emit_key(q, seg, img, doc_local, doc);
-  atomicAdd(part_lds + (uint32_t)(key >> q->part_shift), n);
-  const int W = q->rec_words;
-  const uint32_t kw = (uint32_t)key << q->key_shift;
-  const int ha = q->hll_agg;
-  const DevAgg& H = q->aggs[ha];
-  const DevCol& hc = seg->cols[H.slot];
-  int32_t v0 = 0, v1 = 0;
-  if (hc.kind == COL_MV_DICT) {
-    v0 = gp(hc.mv_off)[doc];
-    v1 = gp(hc.mv_off)[doc + 1];
-  }
-  for (uint32_t e = 0; e < n; ++e) {
-    uint32_t hv;  // (register << 8) | rank; 0 = no value
-    if (hc.kind == COL_MV_DICT) hv = v0 + (int32_t)e < v1 ? (uint32_t)agg_value_mv(H, ha, seg, hc, v0 + e).i : 0u;
-    else hv = (uint32_t)agg_value(H, ha, seg, img, doc_local, doc).i;
-    AS1 uint32_t* r = gp(q->emit) + (size_t)(pos + e) * (uint32_t)W;
-    r[0] = kw | ((hv >> 8) << 6) | ((hv & 0xffu) << 1) | (e == 0 ? 1u : 0u);
-    for (int a = 0; a < q->num_aggs; ++a) {
-      const DevAgg& A = q->aggs[a];
-      if (A.type == PA_AGG_COUNT || a == ha) continue;
-      if (e != 0) continue;  // payloads matter in the first record only
-      const AggValue v = agg_value(A, a, seg, img, doc_local, doc);
-      if (A.src == SRC_INT) {
-        r[A.pay_off] = (uint32_t)v.i;
-      } else {
-        const int64_t b = A.src == SRC_DOUBLE ? __builtin_bit_cast(int64_t, v.d) : v.i;
-        r[A.pay_off] = (uint32_t)b;
-        r[A.pay_off + 1] = (uint32_t)(b >> 32);
-      }
-    }
-  }
-}
+// Partitioned DISTINCTCOUNTHLL(MV) records (written value-parallel in tile_survivors): one per value of an MV column (at
+// least one per matching doc); word 0 packs the key, the HLL register and rank of one value and the doc's first-record
+// flag (COUNT and the per-doc aggregations count only first records); the per-doc payload words follow, as in emit_doc.
 
 // Match word of one leaf over a whole wave tile: bit i of lane l <=> doc 64*i + l of the tile matches.
 // Leaf parameters are loaded once per tile; the 32 decodes are independent, so the LDS reads pipeline.
@@ -762,11 +717,36 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
     uint32_t* cur = (uint32_t*)lds + q->num_parts + (threadIdx.x >> 6);
     uint32_t c = __builtin_amdgcn_readfirstlane(*cur);
     if (q->hll_agg >= 0) {
-      // a variable number of records per doc: wave prefix sum of the counts gives every lane its first record
+      // A variable number of records per doc (one per value of the HLL column). Per step: each matching lane computes
+      // its doc's key, record count n (histogram += n) and first-record payload words; a wave prefix sum of n gives
+      // every doc its first record. Then the wave writes word 0 of the step's records VALUE-parallel: lane j takes
+      // record g = base + j, finds the doc owning it (binary search over the prefix sums with 6 lane shuffles) and
+      // decodes that value — no per-lane loop over a doc's values (divergent: max n over the wave), and consecutive
+      // lanes read consecutive MV values and store consecutive records (coalesced).
+      const int ha = q->hll_agg;
+      const DevAgg& H = q->aggs[ha];
+      const DevCol& hc = seg->cols[H.slot];
+      const bool hmv = hc.kind == COL_MV_DICT;
+      const int W = q->rec_words;
       for (int i = 0; i < STEPS; ++i) {
         const bool mine = (m >> i) & 1u;
         if (__ballot(mine) == 0) continue;
-        const uint32_t n = mine ? emit_count_hll(q, seg, doc_base + local(i)) : 0u;
+        const int64_t doc = doc_base + local(i);
+        uint32_t n = 0, kw = 0, hv_sv = 0;
+        int32_t v0 = 0, nv = 0;
+        if (mine) {
+          if (hmv) {
+            v0 = gp(hc.mv_off)[doc];
+            nv = gp(hc.mv_off)[doc + 1] - v0;
+            n = nv > 0 ? (uint32_t)nv : 1u;
+          } else {
+            n = 1u;
+            hv_sv = (uint32_t)agg_value(H, ha, seg, img, local(i), doc).i;
+          }
+          const int64_t key = emit_key(q, seg, img, local(i), doc);
+          atomicAdd((uint32_t*)lds + (uint32_t)(key >> q->part_shift), n);
+          kw = (uint32_t)key << q->key_shift;
+        }
         uint32_t incl = n;
 #pragma unroll
         for (int o = 1; o < kWave; o <<= 1) {
@@ -774,7 +754,43 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
           if (lane >= o) incl += t;
         }
         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
-        if (mine) emit_doc_hll(q, seg, img, local(i), doc_base + local(i), (uint32_t*)lds, c + incl - n, n);
+        if (mine && W > 1) {  // per-doc payloads: words 1.. of the doc's first record
+          AS1 uint32_t* r = gp(q->emit) + (size_t)(c + incl - n) * (uint32_t)W;
+          for (int a = 0; a < q->num_aggs; ++a) {
+            const DevAgg& A = q->aggs[a];
+            if (A.type == PA_AGG_COUNT || a == ha) continue;
+            const AggValue v = agg_value(A, a, seg, img, local(i), doc);
+            if (A.src == SRC_INT) {
+              r[A.pay_off] = (uint32_t)v.i;
+            } else {
+              const int64_t b = A.src == SRC_DOUBLE ? __builtin_bit_cast(int64_t, v.d) : v.i;
+              r[A.pay_off] = (uint32_t)b;
+              r[A.pay_off + 1] = (uint32_t)(b >> 32);
+            }
+          }
+        }
+        for (uint32_t b = 0; b < total; b += kWave) {
+          const uint32_t g = b + (uint32_t)lane;
+          int ow = 0;  // owner lane: the first lane whose inclusive prefix exceeds g
+#pragma unroll
+          for (int st = kWave / 2; st >= 1; st >>= 1) {
+            const uint32_t v = (uint32_t)__shfl((int)incl, ow + st - 1, kWave);
+            if (v <= g) ow += st;
+          }
+          ow = ow < kWave ? ow : kWave - 1;
+          const uint32_t o_incl = (uint32_t)__shfl((int)incl, ow, kWave), o_n = (uint32_t)__shfl((int)n, ow, kWave);
+          const uint32_t o_kw = (uint32_t)__shfl((int)kw, ow, kWave);
+          const int32_t o_v0 = __shfl(v0, ow, kWave), o_nv = __shfl(nv, ow, kWave);
+          const uint32_t o_hv = (uint32_t)__shfl((int)hv_sv, ow, kWave);
+          if (g < total) {
+            const uint32_t e = g - (o_incl - o_n);
+            uint32_t hv;  // (register << 8) | rank; 0 = no value
+            if (hmv) hv = (int32_t)e < o_nv ? (uint32_t)agg_value_mv(H, ha, seg, hc, (int64_t)o_v0 + e).i : 0u;
+            else hv = o_hv;
+            gp(q->emit)[(size_t)(c + g) * (uint32_t)W] =
+                o_kw | ((hv >> 8) << 6) | ((hv & 0xffu) << 1) | (e == 0 ? 1u : 0u);
+          }
+        }
         c += total;
       }
     } else
