@@ -727,6 +727,9 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
       const DevAgg& H = q->aggs[ha];
       const DevCol& hc = seg->cols[H.slot];
       const bool hmv = hc.kind == COL_MV_DICT;
+      const uint32_t* hwords = hc.words;  // MV column's packed values
+      const int hnb = hc.nbits;
+      const uint32_t* hlut = seg->hll_lut[ha];  // dictId -> (register << 8) | rank
       const int W = q->rec_words;
       for (int i = 0; i < STEPS; ++i) {
         const bool mine = (m >> i) & 1u;
@@ -769,26 +772,36 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
             }
           }
         }
-        for (uint32_t b = 0; b < total; b += kWave) {
-          const uint32_t g = b + (uint32_t)lane;
-          int ow = 0;  // owner lane: the first lane whose inclusive prefix exceeds g
+        // kHB record chunks of 64 per round: all their MV-value loads are issued, then all LUT gathers, then all
+        // stores, so the dependent load chains of a step's chunks overlap instead of running one after another
+        constexpr int kHB = 4;
+        for (uint32_t b = 0; b < total; b += kHB * kWave) {
+          uint32_t w0[kHB], id[kHB];
+          int32_t ok[kHB];
 #pragma unroll
-          for (int st = kWave / 2; st >= 1; st >>= 1) {
-            const uint32_t v = (uint32_t)__shfl((int)incl, ow + st - 1, kWave);
-            if (v <= g) ow += st;
-          }
-          ow = ow < kWave ? ow : kWave - 1;
-          const uint32_t o_incl = (uint32_t)__shfl((int)incl, ow, kWave), o_n = (uint32_t)__shfl((int)n, ow, kWave);
-          const uint32_t o_kw = (uint32_t)__shfl((int)kw, ow, kWave);
-          const int32_t o_v0 = __shfl(v0, ow, kWave), o_nv = __shfl(nv, ow, kWave);
-          const uint32_t o_hv = (uint32_t)__shfl((int)hv_sv, ow, kWave);
-          if (g < total) {
+          for (int k = 0; k < kHB; ++k) {
+            const uint32_t g = b + (uint32_t)(k * kWave + lane);
+            int ow = 0;  // owner lane: the first lane whose inclusive prefix exceeds g
+#pragma unroll
+            for (int st = kWave / 2; st >= 1; st >>= 1) {
+              const uint32_t v = (uint32_t)__shfl((int)incl, ow + st - 1, kWave);
+              if (v <= g) ow += st;
+            }
+            ow = ow < kWave ? ow : kWave - 1;
+            const uint32_t o_incl = (uint32_t)__shfl((int)incl, ow, kWave), o_n = (uint32_t)__shfl((int)n, ow, kWave);
+            const uint32_t o_kw = (uint32_t)__shfl((int)kw, ow, kWave);
+            const int32_t o_v0 = __shfl(v0, ow, kWave), o_nv = __shfl(nv, ow, kWave);
+            const uint32_t o_hv = (uint32_t)__shfl((int)hv_sv, ow, kWave);
             const uint32_t e = g - (o_incl - o_n);
-            uint32_t hv;  // (register << 8) | rank; 0 = no value
-            if (hmv) hv = (int32_t)e < o_nv ? (uint32_t)agg_value_mv(H, ha, seg, hc, (int64_t)o_v0 + e).i : 0u;
-            else hv = o_hv;
-            gp(q->emit)[(size_t)(c + g) * (uint32_t)W] =
-                o_kw | ((hv >> 8) << 6) | ((hv & 0xffu) << 1) | (e == 0 ? 1u : 0u);
+            ok[k] = g < total ? (hmv ? ((int32_t)e < o_nv ? 2 : 1) : 1) : 0;  // 2: an MV value to look up
+            w0[k] = o_kw | (e == 0 ? 1u : 0u);
+            id[k] = ok[k] == 2 ? decode_global(hwords, (int64_t)o_v0 + e, hnb) : (hmv ? 0u : o_hv);
+          }
+#pragma unroll
+          for (int k = 0; k < kHB; ++k) {
+            const uint32_t hv = ok[k] == 2 ? gp(hlut)[id[k]] : (ok[k] == 1 ? id[k] : 0u);  // (register << 8) | rank
+            if (ok[k]) gp(q->emit)[(size_t)(c + b + (uint32_t)(k * kWave + lane)) * (uint32_t)W] =
+                w0[k] | ((hv >> 8) << 6) | ((hv & 0xffu) << 1);
           }
         }
         c += total;
