@@ -1960,10 +1960,10 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
     }
     rstart = base;
   }
-  for (uint32_t ri = rstart + threadIdx.x; ri < r1; ri += kPartAggThreads) {
+  // one record (index ri, word 0 already loaded)
+  auto proc = [&](uint32_t ri, uint32_t w0) {
+    if (w0 == 0xffffffffu) return;  // range padding (part_bin_kernel; never a valid record: its rank field is 31)
     const AS1 uint32_t* rec = gp(q->recs) + (size_t)ri * (uint32_t)W;
-    const uint32_t w0 = rec[0];
-    if (w0 == 0xffffffffu) continue;  // range padding (part_bin_kernel; never a valid record: its rank field is 31)
     const int64_t lk = (int64_t)(w0 >> ks) - kbase;
     if (ks != 0) {  // DISTINCTCOUNTHLL(MV) record: register max of one value, the rest on the doc's first record only
       const DevAgg& H = q->aggs[q->hll_agg];
@@ -1980,7 +1980,7 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
           old = prev;
         }
       }
-      if ((w0 & 1u) == 0) continue;
+      if ((w0 & 1u) == 0) return;
     }
     atomicAdd(cnt + lk, 1u);
     for (int a = 0; a < q->num_aggs; ++a) {
@@ -2004,7 +2004,23 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
         else atomicMax((long long*)(lds + A.lds_off) + lk, (long long)e);
       }
     }
+  };
+  if (ks != 0) {
+    // DISTINCTCOUNTHLL(MV) records: word 0 of 8 records per thread in flight, then their register updates
+    constexpr int kB = 8;
+    const uint32_t span = kB * kPartAggThreads;
+    uint32_t base = r0;
+    for (; base + span <= r1; base += span) {
+      uint32_t w[kB];
+#pragma unroll
+      for (int j = 0; j < kB; ++j)
+        w[j] = __builtin_nontemporal_load(gp(q->recs) + (size_t)(base + j * kPartAggThreads + threadIdx.x) * (uint32_t)W);
+#pragma unroll
+      for (int j = 0; j < kB; ++j) proc(base + j * kPartAggThreads + threadIdx.x, w[j]);
+    }
+    rstart = base;
   }
+  for (uint32_t ri = rstart + threadIdx.x; ri < r1; ri += kPartAggThreads) proc(ri, gp(q->recs)[(size_t)ri * (uint32_t)W]);
   __syncthreads();
   for (int64_t lk = threadIdx.x; lk < nk; lk += kPartAggThreads) {
     const uint32_t c = cnt[lk];
