@@ -1960,6 +1960,23 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
     }
     rstart = base;
   }
+  // one aggregation update of local key lk with the record's value bits iv
+  auto apply = [&](const DevAgg& A, int64_t lk, int64_t iv) {
+    if (A.type == PA_AGG_SUM) {
+      if (A.src == SRC_INT) {
+        atomicAdd((unsigned long long*)(lds + A.lds_off) + lk, (unsigned long long)iv);
+      } else if (A.src == SRC_LONG) {
+        atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk, (unsigned long long)(uint32_t)iv);
+        atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk + 1, (unsigned long long)(iv >> 32));
+      } else {
+        atomicAdd((double*)(lds + A.lds_off) + lk, __builtin_bit_cast(double, iv));
+      }
+    } else {
+      const int64_t e = A.src != SRC_DOUBLE ? iv : f64_order_encode(__builtin_bit_cast(double, iv));
+      if (A.type == PA_AGG_MIN) atomicMin((long long*)(lds + A.lds_off) + lk, (long long)e);
+      else atomicMax((long long*)(lds + A.lds_off) + lk, (long long)e);
+    }
+  };
   // one record (index ri, word 0 already loaded)
   auto proc = [&](uint32_t ri, uint32_t w0) {
     if (w0 == 0xffffffffu) return;  // range padding (part_bin_kernel; never a valid record: its rank field is 31)
@@ -1989,22 +2006,40 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
       int64_t iv;
       if (A.src == SRC_INT) iv = (int64_t)(int32_t)rec[A.pay_off];
       else iv = (int64_t)(((uint64_t)rec[A.pay_off + 1] << 32) | rec[A.pay_off]);
-      if (A.type == PA_AGG_SUM) {
-        if (A.src == SRC_INT) {
-          atomicAdd((unsigned long long*)(lds + A.lds_off) + lk, (unsigned long long)iv);
-        } else if (A.src == SRC_LONG) {
-          atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk, (unsigned long long)(uint32_t)iv);
-          atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk + 1, (unsigned long long)(iv >> 32));
-        } else {
-          atomicAdd((double*)(lds + A.lds_off) + lk, __builtin_bit_cast(double, iv));
-        }
-      } else {
-        const int64_t e = A.src != SRC_DOUBLE ? iv : f64_order_encode(__builtin_bit_cast(double, iv));
-        if (A.type == PA_AGG_MIN) atomicMin((long long*)(lds + A.lds_off) + lk, (long long)e);
-        else atomicMax((long long*)(lds + A.lds_off) + lk, (long long)e);
-      }
+      apply(A, lk, iv);
     }
   };
+  // (key, one 64-bit value) records: exactly one non-COUNT aggregation, of a LONG / DOUBLE value at word 1
+  int va = -1, nva = 0;
+  for (int a = 0; a < q->num_aggs; ++a)
+    if (q->aggs[a].type != PA_AGG_COUNT) {
+      va = a;
+      ++nva;
+    }
+  if (W == 3 && ks == 0 && nva == 1 && q->aggs[va].src != SRC_INT && q->aggs[va].pay_off == 1) {
+    // 8 records per thread in flight, then the LDS updates
+    constexpr int kB = 8;
+    const uint32_t span = kB * kPartAggThreads;
+    uint32_t base = r0;
+    for (; base + span <= r1; base += span) {
+      uint32_t k[kB], lo[kB], hi[kB];
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        const AS1 uint32_t* rec = gp(q->recs) + (size_t)(base + j * kPartAggThreads + threadIdx.x) * 3u;
+        k[j] = __builtin_nontemporal_load(rec);
+        lo[j] = __builtin_nontemporal_load(rec + 1);
+        hi[j] = __builtin_nontemporal_load(rec + 2);
+      }
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        if (k[j] == 0xffffffffu) continue;  // range padding (part_bin_kernel)
+        const int64_t lk = (int64_t)k[j] - kbase;
+        atomicAdd(cnt + lk, 1u);
+        apply(q->aggs[va], lk, (int64_t)(((uint64_t)hi[j] << 32) | lo[j]));
+      }
+    }
+    rstart = base;
+  }
   if (ks != 0) {
     // DISTINCTCOUNTHLL(MV) records: word 0 of 8 records per thread in flight, then their register updates
     constexpr int kB = 8;

@@ -323,7 +323,9 @@ def test_partitioned_raw_values():
             make_segment(92, 60001, cols, no_dict=("rl", "rd", "rf"))]
     gsegs = [GpuSegment(sg) for sg in segs]
     try:
-        for agg in ("SUM(ri), MIN(ri)", "SUM(rl), MAX(rl)", "SUM(rd), MIN(rd), MAX(rd)", "SUM(rf)", "COUNT(*)"):
+        # single LONG / DOUBLE aggregations: 3-word records (pass C's batched 64-bit path)
+        for agg in ("SUM(ri), MIN(ri)", "SUM(rl), MAX(rl)", "SUM(rd), MIN(rd), MAX(rd)", "SUM(rf)", "COUNT(*)",
+                    "MAX(rl)", "SUM(rd)", "MIN(rd)", "SUM(rl)"):
             sql = ("SELECT k1, k2, k3, k4, COUNT(*), %s FROM t GROUP BY k1, k2, k3, k4 LIMIT 10000000 "
                    "OPTION(numGroupsLimit=10000000)" % agg)
             got, exp, _ = run_both(sql, segs, gsegs=gsegs, rel=DOUBLE_REL)
