@@ -120,7 +120,7 @@ def main():
 
     from pinot_amd import parse_sql
     from pinot_amd.engine import GpuQueryExecutor, GpuSegment
-    from pinot_amd.parallel import DistributedAccumulators, shard_segments, table_dictionaries
+    from pinot_amd.parallel import DistributedAccumulators, shard_segments, table_layout
 
     q = parse_sql(QUERY)
     total_segments = args.segments * world
@@ -144,8 +144,9 @@ def main():
 
     # N>1: every rank groups over the same table-wide dictionaries (union over all ranks' segments), so key ids line up
     # across GPUs and the partial aggregates reduce element-wise
-    td = table_dictionaries(q, [g.segment for g in gsegs]) if distributed else None
-    ex = GpuQueryExecutor(q, gsegs, flags=args.flags, table_dicts=td)
+    # (and on the SUM accumulator widths), so the accumulator blocks line up element for element
+    td, wide = table_layout(q, [g.segment for g in gsegs]) if distributed else (None, ())
+    ex = GpuQueryExecutor(q, gsegs, flags=args.flags, table_dicts=td, wide_sum_columns=wide)
     dacc = DistributedAccumulators(ex, device) if distributed else None
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream

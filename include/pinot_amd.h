@@ -145,8 +145,13 @@ typedef struct {
   int32_t type;      /* PA_AGG_* */
   int32_t column_id; /* ignored for COUNT */
   int32_t log2m;     /* DISTINCTCOUNTHLL only (CommonConstants.Helix.DEFAULT_HYPERLOGLOG_LOG2M = 8) */
-  int32_t reserved;
+  int32_t flags;     /* PA_AGGF_* */
 } pa_agg_spec;
+
+/* SUM over an INT/LONG column: keep the exact 96-bit (low 32 unsigned, high 32 signed) pair accumulator
+ * (PA_ACC_SUM_I64X2) even when every value of the bound segments fits int32. A multi-GPU query sets it on every rank
+ * when any rank holds a value outside int32, so all ranks get the same accumulator layout for the RCCL reduce. */
+#define PA_AGGF_WIDE_SUM 1
 
 typedef struct {
   int32_t num_leaves;

@@ -112,10 +112,13 @@ def murmur_hash(value, data_type):
 # ------------------------------------------------------------------ predicate evaluators (restated)
 def _parse(raw, data_type):
     if data_type in ("INT", "LONG"):
-        try:
-            return int(str(raw))
-        except ValueError:
-            return int(float(str(raw)))
+        # Integer.parseInt / Long.parseLong: sign + decimal digits within range, else NumberFormatException
+        s = str(raw)
+        bits = 32 if data_type == "INT" else 64
+        body = s[1:] if s[:1] in ("+", "-") else s
+        if not body or not all("0" <= ch <= "9" for ch in body) or not -(1 << (bits - 1)) <= int(s) < (1 << (bits - 1)):
+            raise ValueError("NumberFormatException: %r" % s)
+        return int(s)
     if data_type == "FLOAT":
         return float(np.float32(float(raw)))
     if data_type == "DOUBLE":

@@ -179,19 +179,23 @@ static int64_t next_set_bit(const uint8_t* bits, int64_t from, int64_t nbits) {
   return -1;
 }
 
-/* value range [start, end) of the current doc of every MV column (sequential-docId context of the reader) */
+/* value range [start, end) of the current doc of every MV column: the sequential-docId reader context
+ * (FixedBitMVForwardIndexReader's ChunkReaderContext), one per oracle_run_segment call so concurrent calls from
+ * several threads (bench.py's cpu_baseline) never share it */
 #define OMAX_COLS 32
-static int64_t g_mv_start[OMAX_COLS], g_mv_end[OMAX_COLS];
+typedef struct {
+  int64_t start[OMAX_COLS], end[OMAX_COLS];
+} mv_cursor;
 
-static void mv_advance(const oracle_col* cols, int ncols, int64_t doc, int64_t num_docs) {
+static void mv_advance(mv_cursor* mc, const oracle_col* cols, int ncols, int64_t doc, int64_t num_docs) {
   for (int c = 0; c < ncols && c < OMAX_COLS; ++c) {
     if (cols[c].kind != OC_MV_DICT) continue;
-    const int64_t start = doc == 0 ? 0 : g_mv_end[c];
+    const int64_t start = doc == 0 ? 0 : mc->end[c];
     int64_t end = doc == num_docs - 1 ? cols[c].mv_num_values
                                       : next_set_bit(cols[c].mv_bitmap, start + 1, cols[c].mv_num_values);
     if (end < 0) end = cols[c].mv_num_values;
-    g_mv_start[c] = start;
-    g_mv_end[c] = end;
+    mc->start[c] = start;
+    mc->end[c] = end;
   }
 }
 
@@ -204,10 +208,10 @@ static double raw_double(const oracle_col* c, int64_t doc) {
   }
 }
 
-static int leaf_match(const oracle_leaf* L, const oracle_col* cols, int64_t doc) {
+static int leaf_match(const mv_cursor* mc, const oracle_leaf* L, const oracle_col* cols, int64_t doc) {
   const oracle_col* c = &cols[L->col];
   if (L->kind == 0 && c->kind == OC_MV_DICT) {
-    for (int64_t v = g_mv_start[L->col]; v < g_mv_end[L->col]; ++v) {
+    for (int64_t v = mc->start[L->col]; v < mc->end[L->col]; ++v) {
       const int m = L->match[oracle_read_int(c->fwd, v, c->num_bits)];
       if (L->exclusive && !m) return 0;
       if (!L->exclusive && m) return 1;
@@ -233,13 +237,13 @@ static int leaf_match(const oracle_leaf* L, const oracle_col* cols, int64_t doc)
   return 1;
 }
 
-static int filter_match(const oracle_query* q, const oracle_col* cols, int64_t doc) {
+static int filter_match(const mv_cursor* mc, const oracle_query* q, const oracle_col* cols, int64_t doc) {
   if (q->num_ops == 0) return 1;
   int st[64];
   int sp = 0;
   for (int i = 0; i < q->num_ops; ++i) {
     const int op = q->ops[i] & 0xff;
-    if (op == OQ_LEAF) st[sp++] = leaf_match(&q->leaves[(q->ops[i] >> 8) & 0xff], cols, doc);
+    if (op == OQ_LEAF) st[sp++] = leaf_match(mc, &q->leaves[(q->ops[i] >> 8) & 0xff], cols, doc);
     else if (op == OQ_NOT) st[sp - 1] = !st[sp - 1];
     else {
       const int b = st[--sp];
@@ -300,13 +304,8 @@ static int32_t gmap_get(gmap* m, int64_t key, int64_t limit) {
 int64_t oracle_run_segment(const oracle_col* cols, int64_t num_docs, const oracle_query* q, int64_t capacity,
                            int64_t* out_keys, int64_t* out_counts, double* out_vals, uint8_t* const* out_hll,
                            int64_t* out_num_matched) {
-  int64_t stride[16];
-  int64_t s = 1;
-  for (int j = 0; j < q->num_gb; ++j) {
-    stride[j] = s;
-    s *= cols[q->gb_col[j]].cardinality;
-  }
   gmap map;
+  memset(&map, 0, sizeof(map));
   const int grouped = q->num_gb > 0;
   if (grouped && gmap_init(&map, capacity < 1 ? 1 : capacity) != 0) return -1;
   int64_t ngroups = grouped ? 0 : 1;
@@ -326,9 +325,11 @@ int64_t oracle_run_segment(const oracle_col* cols, int64_t num_docs, const oracl
   for (int l = 0; l < q->num_leaves; ++l) if (q->leaves[l].col + 1 > ncols) ncols = q->leaves[l].col + 1;
   int64_t* raw_keys = NULL;
   int64_t raw_cap = 0;
+  mv_cursor mc;
+  memset(&mc, 0, sizeof(mc));
   for (int64_t doc = 0; doc < num_docs; ++doc) {
-    mv_advance(cols, ncols, doc, num_docs);
-    if (!filter_match(q, cols, doc)) continue;
+    mv_advance(&mc, cols, ncols, doc, num_docs);
+    if (!filter_match(&mc, q, cols, doc)) continue;
     matched++;
     /* group keys of this doc: getIntRawKeys (one key for SV-only group-by) */
     int64_t nkeys = 1;
@@ -338,13 +339,13 @@ int64_t oracle_run_segment(const oracle_col* cols, int64_t num_docs, const oracl
       for (int j = q->num_gb - 1; j >= 0; --j) {
         const oracle_col* gc = &cols[q->gb_col[j]];
         const int64_t card = gc->cardinality;
-        if (gc->kind != OC_MV_DICT || g_mv_end[q->gb_col[j]] - g_mv_start[q->gb_col[j]] == 1) {
-          const int32_t id = gc->kind == OC_MV_DICT ? oracle_read_int(gc->fwd, g_mv_start[q->gb_col[j]], gc->num_bits)
+        if (gc->kind != OC_MV_DICT || mc.end[q->gb_col[j]] - mc.start[q->gb_col[j]] == 1) {
+          const int32_t id = gc->kind == OC_MV_DICT ? oracle_read_int(gc->fwd, mc.start[q->gb_col[j]], gc->num_bits)
                                                     : dict_id(gc, doc);
           if (!have_array) rawkey = rawkey * card + id;
           else for (int64_t k = 0; k < nkeys; ++k) raw_keys[k] = raw_keys[k] * card + id;
         } else {
-          const int64_t s0 = g_mv_start[q->gb_col[j]], nv = g_mv_end[q->gb_col[j]] - s0;
+          const int64_t s0 = mc.start[q->gb_col[j]], nv = mc.end[q->gb_col[j]] - s0;
           const int64_t cur = have_array ? nkeys : 1;
           if (cur * nv > raw_cap) {
             raw_cap = cur * nv * 2;
@@ -394,8 +395,8 @@ int64_t oracle_run_segment(const oracle_col* cols, int64_t num_docs, const oracl
         if (t == OA_COUNT) continue;
         const oracle_col* c = &cols[q->agg_col[a]];
         const int mv = c->kind == OC_MV_DICT;
-        const int64_t v0 = mv ? g_mv_start[q->agg_col[a]] : doc;
-        const int64_t v1 = mv ? g_mv_end[q->agg_col[a]] : doc + 1;
+        const int64_t v0 = mv ? mc.start[q->agg_col[a]] : doc;
+        const int64_t v1 = mv ? mc.end[q->agg_col[a]] : doc + 1;
         for (int64_t vi = v0; vi < v1; ++vi) {
           if (t == OA_COUNTMV) {
             out_vals[a * capacity + g] += 1.0;

@@ -56,7 +56,10 @@ class LeafSpec(ctypes.Structure):
 
 class AggSpec(ctypes.Structure):
     _fields_ = [("type", ctypes.c_int32), ("column_id", ctypes.c_int32), ("log2m", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("flags", ctypes.c_int32)]
+
+
+PA_AGGF_WIDE_SUM = 1
 
 
 class QuerySpec(ctypes.Structure):

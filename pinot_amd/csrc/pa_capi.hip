@@ -893,7 +893,9 @@ int pa_query_prepare(pa_query* q) {
         agg_src[a] = SRC_INT;
         continue;
       }
-      const int src = (c->vtype == PA_FLOAT || c->vtype == PA_DOUBLE) ? SRC_DOUBLE : (c->fits_int32 ? SRC_INT : SRC_LONG);
+      const bool wide = (A.flags & PA_AGGF_WIDE_SUM) && A.type == PA_AGG_SUM;  // layout agreed across ranks
+      const int src = (c->vtype == PA_FLOAT || c->vtype == PA_DOUBLE) ? SRC_DOUBLE
+                                                                     : ((c->fits_int32 && !wide) ? SRC_INT : SRC_LONG);
       if (!(c->kind == COL_SV_DICT ||
             (c->kind == COL_SV_RAW && (c->vtype == PA_INT || c->vtype == PA_LONG || c->vtype == PA_DOUBLE))))
         val_fast[a] = 0;

@@ -132,13 +132,16 @@ def _flatten_filter(f, leaves, ops):
 
 class GpuQueryExecutor:
     def __init__(self, query: Q.Query, gpu_segments: List[GpuSegment], flags=0, enforce_num_groups_limit=True,
-                 table_dicts=None):
+                 table_dicts=None, wide_sum_columns=()):
         """table_dicts: optional {group-by column: sorted unique values} — the table-wide dictionary every rank of a
         multi-GPU query must share so that key ids address the same accumulator rows everywhere
-        (parallel.table_dictionaries builds it); by default it is the union of these segments' dictionaries."""
+        (parallel.table_layout builds it); by default it is the union of these segments' dictionaries.
+        wide_sum_columns: columns whose SUM keeps the 64-bit (PA_AGGF_WIDE_SUM) accumulator layout even if these
+        segments' values all fit int32 — agreed across ranks by parallel.table_layout."""
         if not gpu_segments:
             raise ValueError("no segments")
         self.table_dicts = table_dicts or {}
+        self.wide_sum_columns = set(wide_sum_columns or ())
         self.query = query
         self.gsegs = gpu_segments
         self.segs = [g.segment for g in gpu_segments]
@@ -189,10 +192,13 @@ class GpuQueryExecutor:
         if len(self.pa_aggs) > L.PA_MAX_AGGS:
             raise UnsupportedQuery("too many aggregations")
         spec.num_aggs = len(self.pa_aggs)
+        names = {cid: name for name, cid in ids.items()}
         for i, (t, cid, log2m) in enumerate(self.pa_aggs):
             spec.aggs[i].type = t
             spec.aggs[i].column_id = max(cid, 0)
             spec.aggs[i].log2m = log2m
+            if t == L.PA_AGG_SUM and names.get(cid) in self.wide_sum_columns:
+                spec.aggs[i].flags = L.PA_AGGF_WIDE_SUM
 
         # filter
         filt = P.expand_raw_in(q.filter, seg0) if q.filter is not None else None

@@ -147,6 +147,9 @@ class HyperLogLog:
             alpha_mm = (0.7213 / (1 + 1.079 / m)) * m * m
         estimate = alpha_mm * (1 / register_sum)
         if estimate <= (5.0 / 2.0) * m:
+            if zeros == 0:
+                # linearCounting(m, 0.0) = m * log(m / 0.0) = +Infinity; Math.round(+Infinity) == Long.MAX_VALUE
+                return (1 << 63) - 1
             return int(math.floor(m * math.log(m / zeros) + 0.5))  # Math.round
         return int(math.floor(estimate + 0.5))
 

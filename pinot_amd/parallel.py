@@ -38,7 +38,7 @@ SECTION_DTYPE = {
 
 
 def shard_segments(num_segments, rank, world_size):
-    """Contiguous segment ranges per rank (each GPU owns a segment set)."""
+    """Contiguous segment ranges per rank (each GPU owns a segment set; ranks differ by at most one segment)."""
     per = num_segments // world_size
     extra = num_segments % world_size
     start = rank * per + min(rank, extra)
@@ -84,6 +84,53 @@ def section_runs(sections):
     return [tuple(r) for r in runs]
 
 
+SUM_FUNCTIONS = ("SUM", "AVG", "SUMMV", "AVGMV")
+
+
+def wide_sum_columns_local(query, segments):
+    """Columns of this rank's segments whose SUM needs the 64-bit accumulator (PA_AGGF_WIDE_SUM): LONG columns that are
+    raw or hold a dictionary value outside int32 (the library picks SUM_I64 for all-int32 columns, SUM_I64X2 else)."""
+    out = set()
+    for a in query.aggregations:
+        if a.function not in SUM_FUNCTIONS or a.column in out:
+            continue
+        for s in segments:
+            c = s.column(a.column)
+            if c.data_type != "LONG":
+                continue
+            if not c.has_dictionary:
+                out.add(a.column)
+                break
+            d = np.asarray(c.dictionary, dtype=np.int64)
+            if len(d) and (d.min() < -(1 << 31) or d.max() >= (1 << 31)):
+                out.add(a.column)
+                break
+    return out
+
+
+def table_layout(query, segments, group=None):
+    """Everything the ranks of one multi-GPU query must agree on before building their executors, in one all-gather:
+    the table-wide dictionary of every dictionary-encoded group-by column (the union over all ranks' segments: the
+    value-keyed combine of GroupByCombineOperator needs the same key id for the same value on every GPU) and the SUM
+    columns that need the wide accumulator on some rank. Pass both to GpuQueryExecutor(table_dicts=...,
+    wide_sum_columns=...) on every rank."""
+    local = {"dicts": {}, "wide": sorted(wide_sum_columns_local(query, segments))}
+    for name in query.group_by:
+        ds = [s.column(name).dictionary for s in segments if s.column(name).has_dictionary]
+        if ds:
+            local["dicts"][name] = np.unique(np.concatenate(ds))
+    world = dist.get_world_size(group)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, local, group=group)
+    dicts = {}
+    for name in query.group_by:
+        parts = [g["dicts"][name] for g in gathered if name in g["dicts"]]
+        if parts:
+            dicts[name] = np.unique(np.concatenate(parts))
+    wide = sorted(set().union(*[set(g["wide"]) for g in gathered]))
+    return dicts, wide
+
+
 def table_dictionaries(query, segments, group=None):
     """Table-wide dictionaries of the query's dictionary-encoded group-by columns, agreed across ranks: the union of
     every rank's segment dictionaries (the value-keyed combine of GroupByCombineOperator needs the same key id for
@@ -106,8 +153,16 @@ def table_dictionaries(query, segments, group=None):
 
 
 def key_space_fingerprint(executor):
-    """62-bit digest of an executor's table-wide key space (key count + every group-by dictionary's values)."""
+    """62-bit digest of everything an element-wise cross-GPU reduce relies on: the table-wide key space (key count +
+    every group-by dictionary's values), whether it is hashed, and the accumulator block layout (every section's kind
+    and element count, the block size) — a SUM over INT on one rank and over values beyond int32 on another would
+    otherwise hand RCCL collectives of different lengths."""
+    lib = L.lib()
     h = hashlib.blake2b(np.int64(executor.num_keys).tobytes(), digest_size=8)
+    h.update(b"hashed" if getattr(executor, "hashed", False) else b"direct")
+    h.update(np.int64(lib.pa_query_accumulator_bytes(executor.handle)).tobytes())
+    for kind, _, n in executor.sections():
+        h.update(np.array([kind, n], dtype=np.int64).tobytes())
     for gd in executor.global_dicts:
         if gd is None:
             h.update(b"<raw>")
@@ -120,12 +175,14 @@ def key_space_fingerprint(executor):
 
 
 def check_same_key_space(fingerprint, device, group=None):
-    """Raises unless every rank holds the same key space (element-wise section reduces would be silently wrong)."""
+    """Raises on EVERY rank unless all ranks hold the same key space and accumulator layout (element-wise section
+    reduces would hang or be silently wrong). A rank that cannot take part passes fingerprint -1: the collective still
+    runs everywhere, so no rank is left blocked in it."""
     t = torch.tensor([fingerprint, -fingerprint], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-    if int(t[0]) != fingerprint or -int(t[1]) != fingerprint:
-        raise L.PinotAmdError("ranks hold different group-key spaces: build the executors with "
-                              "table_dicts=parallel.table_dictionaries(...)")
+    if int(t[0]) != fingerprint or -int(t[1]) != fingerprint or fingerprint < 0:
+        raise L.PinotAmdError("ranks hold different group-key spaces or accumulator layouts (or a hashed key space): "
+                              "build the executors with parallel.table_layout(...)")
 
 
 class DistributedAccumulators:
@@ -133,10 +190,12 @@ class DistributedAccumulators:
     spaces: the same key id addresses the same accumulator row on every GPU)."""
 
     def __init__(self, executor, device):
-        if getattr(executor, "hashed", False):
-            raise L.PinotAmdError("hashed key space: merge with merge_results_across_ranks (slots differ per GPU)")
+        hashed = getattr(executor, "hashed", False)
         if dist.is_initialized():
-            check_same_key_space(key_space_fingerprint(executor), device)
+            # the collective first, on every rank (a hashed rank joins with -1 and every rank then raises)
+            check_same_key_space(-1 if hashed else key_space_fingerprint(executor), device)
+        if hashed:
+            raise L.PinotAmdError("hashed key space: merge with merge_results_across_ranks (slots differ per GPU)")
         lib = L.lib()
         nbytes = int(lib.pa_query_accumulator_bytes(executor.handle))
         self.buf = torch.zeros(nbytes + 512, dtype=torch.uint8, device=device)
@@ -144,6 +203,9 @@ class DistributedAccumulators:
         pad = (-base) % 256
         self.base = base + pad
         L.check(lib.pa_query_set_accumulator_buffer(executor.handle, self.base, nbytes), "set_accumulator_buffer")
+        # the library now reads and writes this torch-owned block: the executor keeps it alive for as long as it lives
+        # (pa_query_set_accumulator_buffer: the caller owns the block and must outlive the query)
+        executor._acc_owner = self.buf
         runs = section_runs([(kind, ptr - self.base + pad, n) for kind, ptr, n in executor.sections()])
         self.views = [(kind, self.buf[a:b].view(dt)) for kind, dt, a, b in runs]
 

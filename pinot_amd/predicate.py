@@ -10,6 +10,7 @@ scanning; the GPU then replaces their applySV loops).
                       (insertionIndexOf on the sorted dictionary -> [startDictId, endDictId))
 Raw (no-dictionary) columns resolve to inclusive value ranges, like the *RawValueBased* evaluators.
 """
+import re
 from dataclasses import dataclass
 from typing import Optional
 
@@ -22,14 +23,25 @@ INT_MIN, INT_MAX = -(1 << 31), (1 << 31) - 1
 LONG_MIN, LONG_MAX = -(1 << 63), (1 << 63) - 1
 
 
+_JAVA_INTEGER = re.compile(r"[+-]?[0-9]+\Z")
+
+
+def parse_integral(raw, data_type):
+    """Integer.parseInt / Long.parseLong, exactly: an optional sign and decimal digits, within the type's range
+    (IntDictionary.insertionIndexOf / RangePredicateEvaluatorFactory.java:80-85 parse the literal this way). Anything
+    else — '1.5', '1e3', ' 7', a value past the type's range — is a NumberFormatException in the reference, so the
+    query is refused rather than answered for a rounded literal."""
+    s = str(raw)
+    lo, hi = (INT_MIN, INT_MAX) if data_type == "INT" else (LONG_MIN, LONG_MAX)
+    if not _JAVA_INTEGER.match(s) or not lo <= int(s) <= hi:
+        raise ValueError("NumberFormatException: %r is not a valid %s literal" % (s, data_type))
+    return int(s)
+
+
 def stored_value(raw, data_type):
     """PredicateUtils.getStoredValue + the type's parse (Integer.parseInt, Long.parseLong, ...)."""
     if data_type in ("INT", "LONG"):
-        s = str(raw)
-        try:
-            return int(s)
-        except ValueError:
-            return int(float(s))
+        return parse_integral(raw, data_type)
     if data_type == "FLOAT":
         return np.float32(float(raw))
     if data_type == "DOUBLE":

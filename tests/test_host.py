@@ -1,0 +1,49 @@
+"""Host-side logic of the hot path's callers (no GPU): predicate literal parsing and HyperLogLog estimates."""
+import numpy as np
+import pytest
+
+import oracle
+from pinot_amd import parse_sql
+from pinot_amd import predicate as P
+from pinot_amd.hll import HyperLogLog
+
+
+def test_hll_all_registers_nonzero_small_estimate():
+    """Every register set but the estimate in the small range: linearCounting(m, 0) = m * log(m / 0.0) = +Infinity in
+    stream-lib, and Math.round(+Infinity) == Long.MAX_VALUE (no ZeroDivisionError)."""
+    h = HyperLogLog(8, np.ones(256, dtype=np.uint8))
+    assert h.cardinality() == (1 << 63) - 1
+    h = HyperLogLog(4, np.ones(16, dtype=np.uint8))
+    assert h.cardinality() == (1 << 63) - 1
+    # one zero register: the ordinary linear-counting branch
+    r = np.ones(256, dtype=np.uint8)
+    r[0] = 0
+    assert HyperLogLog(8, r).cardinality() == round(256 * np.log(256.0))
+
+
+@pytest.mark.parametrize("lit,dtype,ok", [
+    ("17", "INT", 17), ("-17", "INT", -17), ("+5", "INT", 5), ("2147483647", "INT", 2147483647),
+    ("2147483648", "INT", None), ("1.5", "INT", None), ("1.0", "INT", None), ("1e3", "LONG", None),
+    (" 7", "INT", None), ("1_000", "INT", None), ("9223372036854775807", "LONG", (1 << 63) - 1),
+    ("9223372036854775808", "LONG", None), ("123456789012345678", "LONG", 123456789012345678),
+])
+def test_integral_literals_parse_like_java(lit, dtype, ok):
+    """Integer.parseInt / Long.parseLong: a non-integral or out-of-range literal on an INT/LONG column is a
+    NumberFormatException in the reference (IntDictionary.insertionIndexOf, RangePredicateEvaluatorFactory.java:80-85),
+    never a truncated bound; LONG literals past 2^53 parse exactly. The oracle's restatement agrees."""
+    if ok is None:
+        with pytest.raises(ValueError):
+            P.stored_value(lit, dtype)
+        with pytest.raises(ValueError):
+            oracle._parse(lit, dtype)
+    else:
+        assert P.stored_value(lit, dtype) == ok
+        assert oracle._parse(lit, dtype) == ok
+
+
+def test_fractional_bound_on_int_column_is_refused():
+    from pinot_amd.segment import create_segment
+    seg = create_segment("s", {"m": np.arange(10, dtype=np.int32)}, {"m": "INT"})
+    q = parse_sql("SELECT COUNT(*) FROM t WHERE m >= 1.5")
+    with pytest.raises(ValueError):
+        P.dictionary_leaf(q.filter, seg.column("m"))

@@ -278,10 +278,47 @@ def test_key_space_fingerprint_distinguishes_dictionaries():
     from pinot_amd.parallel import key_space_fingerprint
 
     class _E:
-        def __init__(self, n, dicts):
-            self.num_keys, self.global_dicts = n, dicts
+        def __init__(self, n, dicts, secs=((L.PA_ACC_COUNT_U64, 6), (L.PA_ACC_SUM_I64, 6))):
+            self.num_keys, self.global_dicts, self.handle, self._secs = n, dicts, None, secs
+
+        def sections(self):
+            return [(k, 0, n) for k, n in self._secs]
     a = key_space_fingerprint(_E(6, [np.array([1, 2, 3]), np.array(["x", "y"])]))
+    # same key space, a SUM kept wide on one rank only: a different accumulator layout
+    assert a != key_space_fingerprint(_E(6, [np.array([1, 2, 3]), np.array(["x", "y"])],
+                                         ((L.PA_ACC_COUNT_U64, 6), (L.PA_ACC_SUM_I64X2, 12))))
     assert a == key_space_fingerprint(_E(6, [np.array([1, 2, 3]), np.array(["x", "y"])]))
     assert a != key_space_fingerprint(_E(6, [np.array([1, 2, 4]), np.array(["x", "y"])]))
     assert a != key_space_fingerprint(_E(6, [np.array([1, 2, 3]), np.array(["x", "z"])]))
     assert a != key_space_fingerprint(_E(6, [np.array([1, 2, 3]), None]))
+
+
+def _layout_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pinot_amd import parse_sql
+    from pinot_amd.parallel import table_layout
+    from pinot_amd.segment import create_segment
+    q = parse_sql("SELECT k, SUM(m), AVG(n), SUM(i) FROM t GROUP BY k")
+    rng = np.random.default_rng(rank)
+    m = rng.integers(0, 1000, size=300).astype(np.int64)
+    if rank == 1:
+        m[7] = 1 << 40  # only rank 1 holds a LONG value outside int32
+    seg = create_segment("s%d" % rank, {"k": rng.integers(0, 5, size=300).astype(np.int32), "m": m,
+                                        "n": rng.integers(0, 9, size=300).astype(np.int64),
+                                        "i": rng.integers(0, 9, size=300).astype(np.int32)},
+                         {"k": "INT", "m": "LONG", "n": "LONG", "i": "INT"})
+    dicts, wide = table_layout(q, [seg])
+    out[rank] = (sorted(dicts), list(wide))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_table_layout_agrees_on_wide_sums():
+    """A LONG column whose values fit int32 on one rank but not on the other: both ranks agree to keep the wide SUM
+    accumulator (otherwise the ranks' accumulator blocks differ in size and RCCL reduces misaligned data)."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_layout_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    assert out[0] == out[1] == (["k"], ["m"])
