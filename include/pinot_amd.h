@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define PA_ABI_VERSION 1
+#define PA_ABI_VERSION 2
 
 /* limits of one query shape */
 #define PA_MAX_LEAVES 16
@@ -96,6 +96,10 @@ extern "C" {
 #define PA_AGG_MAX 3
 #define PA_AGG_DISTINCTCOUNTHLL 4
 #define PA_AGG_COUNT_MV 5 /* COUNTMV: number of values of an MV column (AVGMV = SUM over an MV column / COUNTMV) */
+#define PA_AGG_DISTINCTCOUNT 6 /* exact DISTINCTCOUNT over a dictionary-encoded column: per group, one presence byte per
+                                  table-wide value id of the column (pa_agg_spec.num_values of them; segment dictIds are
+                                  mapped by pa_query_bind_value_remap) — the value set of DistinctCountAggregationFunction
+                                  (BaseDistinctAggregateAggregationFunction) as a bitmap over the table's values */
 /* SUM / MIN / MAX / DISTINCTCOUNTHLL over a multi-value column aggregate every value of the doc (SUMMV, MINMV, MAXMV,
  * DISTINCTCOUNTHLLMV); a multi-value group-by column expands a doc into one key per value (cartesian product over
  * several MV columns), as DictionaryBasedGroupKeyGenerator.getIntRawKeys does. */
@@ -146,6 +150,7 @@ typedef struct {
   int32_t column_id; /* ignored for COUNT */
   int32_t log2m;     /* DISTINCTCOUNTHLL only (CommonConstants.Helix.DEFAULT_HYPERLOGLOG_LOG2M = 8) */
   int32_t flags;     /* PA_AGGF_* */
+  int64_t num_values; /* DISTINCTCOUNT: size of the column's table-wide value dictionary (ignored otherwise) */
 } pa_agg_spec;
 
 /* SUM over an INT/LONG column: keep the exact 96-bit (low 32 unsigned, high 32 signed) pair accumulator
@@ -206,6 +211,11 @@ pa_query* pa_query_create(const pa_query_spec* spec, int32_t num_segments);
 int pa_query_bind_segment(pa_query* q, int32_t index, const pa_segment* seg,
                           const pa_leaf_params* leaf_params, const int32_t* const* group_remaps);
 
+/* DISTINCTCOUNT aggregation `agg` on the segment bound at `index`: remap[d] = the table-wide value id of the segment's
+ * dictId d (int32[segment cardinality]; NULL = identity, the segment's dictionary IS the table-wide one). Call after
+ * pa_query_bind_segment, before pa_query_prepare. */
+int pa_query_bind_value_remap(pa_query* q, int32_t index, int32_t agg, const int32_t* remap);
+
 /* Uploads per-segment parameters, builds the tile schedule and HLL lookup tables, sizes the
  * accumulators. Must be called once after every segment is bound. */
 int pa_query_prepare(pa_query* q);
@@ -226,12 +236,15 @@ int pa_query_scan(pa_query* q, void* stream);
 #define PA_ACC_SUM_F64 2   /* reduce SUM */
 #define PA_ACC_MIN_I64 3   /* reduce MIN (ordered encoding for floating values) */
 #define PA_ACC_MAX_I64 4   /* reduce MAX */
-#define PA_ACC_HLL_U32 5   /* reduce MAX */
+#define PA_ACC_HLL_U8 5    /* reduce MAX; one byte per register: [key << log2m | register] */
 #define PA_ACC_SUM_I64X2 6 /* reduce SUM; [2k] = sum of low 32 bits (unsigned), [2k+1] = sum of high 32 bits */
 #define PA_ACC_DOCS_U64 7  /* reduce SUM; [0] docs that passed the filter (numDocsScanned), [1] group-table overflows,
-                              [2] segments whose distinct groups reached numGroupsLimit */
+                              [2] segments whose distinct groups reached numGroupsLimit, [3] internal consistency
+                              errors (must stay 0; fetch fails otherwise) */
 #define PA_ACC_KEYS_I64 8  /* hashed key space only: slot -> packed key (INT64_MAX = empty); not element-wise
                               reducible across GPUs (slots differ): merge fetched groups by key instead */
+#define PA_ACC_PRESENCE_U8 9 /* reduce MAX; DISTINCTCOUNT: [key * stride + value id] = 1 if the group saw the value,
+                                stride = num_values rounded up to 16 bytes */
 /* All sections live in one device block of pa_query_accumulator_bytes() bytes (256-byte aligned sections).
  * pa_query_set_accumulator_buffer lets the caller own that block (e.g. memory its collective library
  * registered) instead of the library: call after pa_query_prepare; `bytes` must be >= the size. */

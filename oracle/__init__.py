@@ -253,13 +253,14 @@ def _flatten(f, leaves, ops, segment):
         leaves.append(f)
 
 
-_AGG = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "DISTINCTCOUNTHLL": 4, "COUNTMV": 5}
+_AGG = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "DISTINCTCOUNTHLL": 4, "COUNTMV": 5, "DISTINCTCOUNT": 6}
 # query function -> oracle accumulators (the *MV forms read every value of the MV column; AVG = SUM + group count,
 # AVGMV = SUM + COUNTMV over the column)
 _ORACLE_FNS = {"SUM": ("SUM",), "AVG": ("SUM",), "MIN": ("MIN",), "MAX": ("MAX",),
                "DISTINCTCOUNTHLL": ("DISTINCTCOUNTHLL",), "SUMMV": ("SUM",), "MINMV": ("MIN",), "MAXMV": ("MAX",),
                "DISTINCTCOUNTHLLMV": ("DISTINCTCOUNTHLL",), "COUNTMV": ("COUNTMV",), "AVGMV": ("SUM", "COUNTMV"),
-               "COUNT": ("COUNT",)}
+               "COUNT": ("COUNT",), "MINMAXRANGE": ("MIN", "MAX"), "MINMAXRANGEMV": ("MIN", "MAX"),
+               "DISTINCTCOUNT": ("DISTINCTCOUNT",), "DISTINCTCOUNTMV": ("DISTINCTCOUNT",)}
 
 
 def _pack_msb(ids, nb):
@@ -386,8 +387,13 @@ def run_segment(query, segment):
     keys = np.zeros(cap, dtype=np.int64)
     counts = np.zeros(cap, dtype=np.int64)
     vals = np.zeros(max(1, len(oaggs)) * cap, dtype=np.float64)
-    hll_bufs = [np.zeros(cap << k[2], dtype=np.uint8) if k[0] == "DISTINCTCOUNTHLL" else np.zeros(1, np.uint8)
-                for k in oaggs] or [np.zeros(1, np.uint8)]
+    def _buf(k):
+        if k[0] == "DISTINCTCOUNTHLL":
+            return np.zeros(cap << k[2], dtype=np.uint8)
+        if k[0] == "DISTINCTCOUNT":
+            return np.zeros(cap * segment.column(k[1]).cardinality, dtype=np.uint8)
+        return np.zeros(1, np.uint8)
+    hll_bufs = [_buf(k) for k in oaggs] or [np.zeros(1, np.uint8)]
     hll_ptrs = (ctypes.c_void_p * len(hll_bufs))(*[b.ctypes.data for b in hll_bufs])
     matched = ctypes.c_int64()
     n = lib().oracle_run_segment(ctypes.cast(ocols, ctypes.c_void_p), segment.num_docs, ctypes.byref(oq), cap,
@@ -413,6 +419,10 @@ def run_segment(query, segment):
             if k[0] == "DISTINCTCOUNTHLL":
                 mm = 1 << k[2]
                 row.append(hll_bufs[ai][g * mm:(g + 1) * mm].copy())
+            elif k[0] == "DISTINCTCOUNT":
+                col = segment.column(k[1])
+                card = col.cardinality
+                row.append(set(col.dictionary[np.flatnonzero(hll_bufs[ai][g * card:(g + 1) * card])].tolist()))
             else:
                 row.append(float(vals[ai * cap + g]))
         out[key] = (int(counts[g]), row)
@@ -421,7 +431,7 @@ def run_segment(query, segment):
 
 def run_query(query, segments):
     """Server-level intermediate result for a segment set, merged by key value in segment order."""
-    from pinot_amd.engine import AvgPair, IntermediateResult
+    from pinot_amd.engine import AvgPair, IntermediateResult, MinMaxRangePair
     from pinot_amd.hll import HyperLogLog
     merged = {}
     oaggs, amap = None, None
@@ -447,13 +457,16 @@ def run_query(query, segments):
                     acc[1][ai] = max(acc[1][ai], row[ai])
                 elif k[0] == "DISTINCTCOUNTHLL":
                     acc[1][ai] = np.maximum(acc[1][ai], row[ai])
+                elif k[0] == "DISTINCTCOUNT":
+                    acc[1][ai] = acc[1][ai] | row[ai]
     out = IntermediateResult(list(query.aggregations), list(query.group_by))
     out.num_total_docs = sum(s.num_docs for s in segments)
     out.num_docs_scanned = scanned
     out.num_groups_limit_reached = limit_reached
     if not query.group_by and () not in merged:
         merged[()] = [0, [np.zeros(1 << k[2], np.uint8) if k[0] == "DISTINCTCOUNTHLL" else
-                          (0.0 if k[0] in ("SUM", "COUNT", "COUNTMV") else (np.inf if k[0] == "MIN" else -np.inf))
+                          (set() if k[0] == "DISTINCTCOUNT" else
+                           (0.0 if k[0] in ("SUM", "COUNT", "COUNTMV") else (np.inf if k[0] == "MIN" else -np.inf)))
                           for k in oaggs]]
     for key, (cnt, row) in merged.items():
         vals = []
@@ -468,6 +481,10 @@ def run_query(query, segments):
                 vals.append(int(row[ai]))
             elif a.function in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV"):
                 vals.append(HyperLogLog(a.log2m, row[ai] if isinstance(row[ai], np.ndarray) else None))
+            elif a.function in ("MINMAXRANGE", "MINMAXRANGEMV"):
+                vals.append(MinMaxRangePair(row[ai[0]], row[ai[1]]))
+            elif a.function in ("DISTINCTCOUNT", "DISTINCTCOUNTMV"):
+                vals.append(set(row[ai]))
             else:
                 vals.append(row[ai])
         if query.group_by:

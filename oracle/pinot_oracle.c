@@ -16,6 +16,8 @@
  *  - DISTINCTCOUNTHLL:   stream-lib 2.9.8 MurmurHash.hashLong / hash(byte[]) + HyperLogLog.offerHashed
  *                        (offering every doc's value; register max is idempotent, so this equals the reference's
  *                        dictId-bitmap-then-offer of DistinctCountHLLAggregationFunction.java:176-183)
+ *  - DISTINCTCOUNT:      per group the set of dictIds seen (DistinctCountAggregationFunction /
+ *                        BaseDistinctAggregateAggregationFunction: a dictId bitmap per group, values at extraction)
  *  - multi-value:        FixedBitMVForwardIndexReader.getDictIdMV in docId order (readers/forward/
  *                        FixedBitMVForwardIndexReader.java:106-146: start = previous end, end = next set bit of the
  *                        row-start bitmap, numValues for the last doc), MV leaves via
@@ -130,7 +132,7 @@ static void hll_offer(uint8_t* regs, int32_t log2m, int32_t hashed) {
 /* ------------------------------------------------------------------ query */
 enum { OC_DICT = 0, OC_RAW_I32 = 1, OC_RAW_I64 = 2, OC_RAW_F32 = 3, OC_RAW_F64 = 4, OC_MV_DICT = 5 };
 enum { OQ_LEAF = 0, OQ_AND = 1, OQ_OR = 2, OQ_NOT = 3 };
-enum { OA_COUNT = 0, OA_SUM = 1, OA_MIN = 2, OA_MAX = 3, OA_HLL = 4, OA_COUNTMV = 5 };
+enum { OA_COUNT = 0, OA_SUM = 1, OA_MIN = 2, OA_MAX = 3, OA_HLL = 4, OA_COUNTMV = 5, OA_DISTINCT = 6 };
 
 typedef struct {
   int32_t kind;
@@ -317,6 +319,7 @@ int64_t oracle_run_segment(const oracle_col* cols, int64_t num_docs, const oracl
     const double init = q->agg_type[a] == OA_MIN ? INFINITY : (q->agg_type[a] == OA_MAX ? -INFINITY : 0.0);
     for (int64_t g = 0; g < capacity; ++g) out_vals[a * capacity + g] = init;
     if (q->agg_type[a] == OA_HLL) memset(out_hll[a], 0, (size_t)capacity << q->agg_log2m[a]);
+    if (q->agg_type[a] == OA_DISTINCT) memset(out_hll[a], 0, (size_t)capacity * (size_t)cols[q->agg_col[a]].cardinality);
   }
   int64_t matched = 0;
   int ncols = 0;
@@ -400,6 +403,10 @@ int64_t oracle_run_segment(const oracle_col* cols, int64_t num_docs, const oracl
         for (int64_t vi = v0; vi < v1; ++vi) {
           if (t == OA_COUNTMV) {
             out_vals[a * capacity + g] += 1.0;
+            continue;
+          }
+          if (t == OA_DISTINCT) { /* the group's value set, as dictId presence (DistinctCountAggregationFunction) */
+            out_hll[a][(size_t)g * (size_t)c->cardinality + (size_t)oracle_read_int(c->fwd, vi, c->num_bits)] = 1;
             continue;
           }
           if (t == OA_HLL) {

@@ -16,7 +16,7 @@ PA_MAX_AGGS = 16
 PA_INT, PA_LONG, PA_FLOAT, PA_DOUBLE, PA_STRING, PA_BYTES = range(6)
 PA_LEAF_DICT_RANGE, PA_LEAF_DICT_SET, PA_LEAF_RAW_RANGE, PA_LEAF_MV_DICT_RANGE, PA_LEAF_MV_DICT_SET = range(5)
 PA_OP_LEAF, PA_OP_AND, PA_OP_OR, PA_OP_NOT = range(4)
-PA_AGG_COUNT, PA_AGG_SUM, PA_AGG_MIN, PA_AGG_MAX, PA_AGG_DISTINCTCOUNTHLL, PA_AGG_COUNT_MV = range(6)
+PA_AGG_COUNT, PA_AGG_SUM, PA_AGG_MIN, PA_AGG_MAX, PA_AGG_DISTINCTCOUNTHLL, PA_AGG_COUNT_MV, PA_AGG_DISTINCTCOUNT = range(7)
 PA_QF_STAGE_ALL = 1
 PA_QF_FORCE_GLOBAL = 2
 PA_QF_STEPS16 = 1 << 4
@@ -29,15 +29,16 @@ PA_QF_DEBUG_STREAM_ONLY = 1 << 16
 PA_QF_NO_LANE_MAJOR = 1 << 17
 PA_QF_NO_PARTITION = 1 << 21
 PA_QF_PART_SHIFT = 22
-PA_ACC_COUNT_U64, PA_ACC_SUM_I64, PA_ACC_SUM_F64, PA_ACC_MIN_I64, PA_ACC_MAX_I64, PA_ACC_HLL_U32, \
-    PA_ACC_SUM_I64X2, PA_ACC_DOCS_U64, PA_ACC_KEYS_I64 = range(9)
+PA_ACC_COUNT_U64, PA_ACC_SUM_I64, PA_ACC_SUM_F64, PA_ACC_MIN_I64, PA_ACC_MAX_I64, PA_ACC_HLL_U8, \
+    PA_ACC_SUM_I64X2, PA_ACC_DOCS_U64, PA_ACC_KEYS_I64, PA_ACC_PRESENCE_U8 = range(10)
+ABI_VERSION = 2
 
 # every symbol declared in include/pinot_amd.h
 EXPORTED = [
     "pa_abi_version", "pa_device_count", "pa_set_device", "pa_last_error",
     "pa_segment_create", "pa_segment_add_sv_dict_column", "pa_segment_add_mv_dict_column",
     "pa_segment_add_raw_column", "pa_segment_num_docs", "pa_segment_device_bytes", "pa_segment_destroy",
-    "pa_query_create", "pa_query_bind_segment", "pa_query_prepare", "pa_query_num_keys",
+    "pa_query_create", "pa_query_bind_segment", "pa_query_bind_value_remap", "pa_query_prepare", "pa_query_num_keys",
     "pa_query_execute", "pa_query_reset", "pa_query_scan", "pa_query_num_eager_literals", "pa_query_lane_major",
     "pa_query_accumulator_bytes", "pa_query_set_accumulator_buffer", "pa_query_num_sections", "pa_query_section",
     "pa_query_fetch", "pa_query_matched_docs", "pa_query_key_layout", "pa_query_limit_trimming",
@@ -56,7 +57,7 @@ class LeafSpec(ctypes.Structure):
 
 class AggSpec(ctypes.Structure):
     _fields_ = [("type", ctypes.c_int32), ("column_id", ctypes.c_int32), ("log2m", ctypes.c_int32),
-                ("flags", ctypes.c_int32)]
+                ("flags", ctypes.c_int32), ("num_values", ctypes.c_int64)]
 
 
 PA_AGGF_WIDE_SUM = 1
@@ -106,6 +107,7 @@ def _declare(lib):
         "pa_segment_destroy": (None, [vp]),
         "pa_query_create": (vp, [ctypes.POINTER(QuerySpec), i32]),
         "pa_query_bind_segment": (ctypes.c_int, [vp, i32, vp, ctypes.POINTER(LeafParams), vp]),
+        "pa_query_bind_value_remap": (ctypes.c_int, [vp, i32, i32, vp]),
         "pa_query_prepare": (ctypes.c_int, [vp]),
         "pa_query_num_keys": (i64, [vp]),
         "pa_query_execute": (ctypes.c_int, [vp, vp]),
@@ -140,8 +142,8 @@ def lib():
             raise PinotAmdError("%s is missing: run `python -m pinot_amd.build` (hipcc, gfx950)" % LIB_PATH)
         _lib = ctypes.CDLL(LIB_PATH)
         _declare(_lib)
-        if _lib.pa_abi_version() != 1:
-            raise PinotAmdError("ABI version mismatch")
+        if _lib.pa_abi_version() != ABI_VERSION:
+            raise PinotAmdError("ABI version mismatch: %s is stale, rebuild it" % LIB_PATH)
     return _lib
 
 

@@ -5,10 +5,13 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <functional>
 #include <map>
+#include <mutex>
+#include <numeric>
 #include <string>
 #include <utility>
 #include <vector>
@@ -26,6 +29,19 @@ int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+
+// PA_DEBUG_PLAN=1: the planner's decisions on stderr (why a query takes a strategy)
+bool plan_debug() {
+  static const bool on = std::getenv("PA_DEBUG_PLAN") != nullptr;
+  return on;
+}
+#define PLAN_LOG(...)                                  \
+  do {                                                 \
+    if (plan_debug()) {                                \
+      std::fprintf(stderr, "[pa plan] " __VA_ARGS__); \
+      std::fputc('\n', stderr);                       \
+    }                                                  \
+  } while (0)
 
 #define PA_HIP(call)                                                                  \
   do {                                                                                \
@@ -68,6 +84,8 @@ struct Column {
   int64_t total_values = 0;
   int32_t max_values = 1;   // MV: most values in one row
   bool fits_int32 = false;  // every dictionary value (INT/LONG) fits in int32
+  std::vector<uint64_t> hvals;  // host copy of the dictionary values (8-byte bits): table-wide value dictionaries
+  uint64_t dict_hash = 0;       // FNV-1a of hvals: identical dictionaries across segments are found without a compare
   DevBuf words;   // guard + stream + pad (SV dict)
   DevBuf raw;     // raw values (SV raw)
   DevBuf dict;    // int64 or double
@@ -102,6 +120,10 @@ int upload_dict(Column* c, int32_t vtype, int32_t card, const void* dict_values,
     int rc = dev_alloc(c->dict, (size_t)card * 8);
     if (rc) return rc;
     PA_HIP(hipMemcpy(c->dict.p, dict_values, (size_t)card * 8, hipMemcpyHostToDevice));
+    c->hvals.assign((const uint64_t*)dict_values, (const uint64_t*)dict_values + card);
+    uint64_t hsh = 1469598103934665603ull ^ (uint64_t)card;
+    for (uint64_t v : c->hvals) hsh = (hsh ^ v) * 1099511628211ull;
+    c->dict_hash = hsh;
     if (vtype == PA_INT || vtype == PA_LONG) {
       const int64_t* v = (const int64_t*)dict_values;
       c->fits_int32 = true;
@@ -370,16 +392,67 @@ int to_cnf(const pa_query_spec& spec, std::vector<Clause>& out) {
 constexpr size_t kFetchWholeBlockBytes = 1 << 20;
 constexpr size_t kPartLdsChoices[4] = {144 * 1024, 64 * 1024, 96 * 1024, 144 * 1024};  // PA_QF_PART_SHIFT
 constexpr int64_t kMinParts = 256;          // pass C parallelism: one workgroup per partition, >= one per CU
-constexpr int64_t kMaxParts = 4096;          // partition counters of the scan passes: 16 KiB of LDS
-constexpr size_t kPartBinLdsBytes = 152 * 1024;  // part_bin_kernel: bins + counters (one 1024-thread workgroup per CU)
+constexpr int64_t kMaxParts = 4096;          // partitions of one query (both streams)
 constexpr int64_t kDirectMaxKeys = int64_t(1) << 27;  // direct-indexed key space limit (beyond: hashed keys)
 constexpr uint64_t kMaxHashSlots = uint64_t(1) << 28;
+constexpr size_t kLdsBudget = 160 * 1024;
 
 struct Section {
   int32_t kind;
   void* ptr;
   int64_t n;
 };
+
+// Per-device pooled scratch of the partitioned queries (histograms, range offsets, partition bases, records): sized by
+// the largest query prepared on the device and shared by all of them, so a query costs no allocation. Stream-ordered
+// hand-off: a scan enqueues its kernels behind the previous user's (hipStreamWaitEvent when that was another stream)
+// and records its own completion event; growing waits for that event before the old block is freed.
+struct ScratchArena {
+  std::mutex mu;
+  void* p = nullptr;
+  size_t n = 0;
+  hipEvent_t last = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool used = false;
+};
+
+ScratchArena* arena_for(int dev) {
+  static std::mutex m;
+  static std::map<int, ScratchArena*> arenas;
+  std::lock_guard<std::mutex> g(m);
+  ScratchArena*& a = arenas[dev];
+  if (!a) a = new ScratchArena();  // lives for the process (freed with it)
+  return a;
+}
+
+// Grows the arena to at least `bytes` (caller holds a->mu).
+int arena_grow(ScratchArena* a, size_t bytes) {
+  if (a->n >= bytes) return PA_OK;
+  if (a->used) PA_HIP(hipEventSynchronize(a->last));
+  if (a->p) PA_HIP(hipFree(a->p));
+  a->p = nullptr;
+  a->n = 0;
+  hipError_t e = hipMalloc(&a->p, bytes);
+  if (e != hipSuccess) {
+    a->p = nullptr;
+    return fail(PA_ENOMEM, "scratch arena hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+  }
+  a->n = bytes;
+  if (!a->last) PA_HIP(hipEventCreateWithFlags(&a->last, hipEventDisableTiming));
+  return PA_OK;
+}
+
+// DISTINCTCOUNT presence bytes per key: the table-wide value count rounded up to whole 16-byte units
+inline int64_t presence_stride(const pa_agg_spec& A) { return (A.num_values + 15) & ~int64_t(15); }
+// element bytes of an accumulator section
+inline size_t section_es(int32_t kind) { return (kind == PA_ACC_HLL_U8 || kind == PA_ACC_PRESENCE_U8) ? 1 : 8; }
+
+// Order key of an 8-byte dictionary value: the value itself (INT/LONG) or its order-preserving image (FLOAT/DOUBLE,
+// Double.compare order: -0.0 < 0.0), so distinct values get distinct keys in value order.
+inline int64_t value_order_key(uint64_t bits, int32_t vtype) {
+  return (vtype == PA_FLOAT || vtype == PA_DOUBLE) ? f64_order_encode(__builtin_bit_cast(double, bits))
+                                                    : (int64_t)bits;
+}
 
 }  // namespace
 
@@ -391,6 +464,7 @@ struct pa_query {
   std::vector<std::vector<std::vector<uint32_t>>> luts;        // [seg][leaf]
   std::vector<std::vector<std::vector<int32_t>>> remaps;       // [seg][gb]
   std::vector<std::vector<char>> has_remap;
+  std::vector<std::vector<std::vector<int32_t>>> vremaps;      // [seg][agg] DISTINCTCOUNT value remaps (empty = identity)
   bool prepared = false;
 
   // plan
@@ -422,13 +496,15 @@ struct pa_query {
   int64_t ht_slots = 0;
   int key_shift[PA_MAX_GROUP_BY] = {0};
   int keys_section = -1;
-  bool partitioned = false;      // partitioned aggregation (STRAT_PEMIT scan + part_bin_kernel + part_agg_kernel)
-  int part_P = 0, part_shift = 0, rec_words = 0, part_lds_c = 0, bin_slots = 0, bin_iter = 0, bin_parts = 0, emit_val_agg = -1;
-  int hll_agg = -1, hll_key_shift = 0;
-  bool emit_fast = false;
-  std::vector<int> pay_off, part_agg_lds;
-  DevBuf part_hist, part_off, part_base, recs, emit, wave_cnt, tile_rec;
-  int bin_lds = 0;
+  // partitioned aggregation: count pass (own descriptors: it stages only the filter and group-by columns), range
+  // offsets, emit pass (hq / hsegs), pass C; scratch in the device arena at these offsets
+  bool partitioned = false;
+  DevQuery hq_count;
+  std::vector<DevSeg> hsegs_count;
+  DevBuf dq_count, dsegs_count;
+  int count_lds = 0, count_ring = 0, part_lds_c = 0;
+  size_t sc_hist = 0, sc_off = 0, sc_base = 0, sc_recs_v = 0, sc_recs_h = 0, sc_bytes = 0;
+  int scratch_dev = 0;
   int64_t last_matched = -1;  // numDocsScanned read by the last fetch
   int64_t last_reached = -1;  // segments that reached numGroupsLimit, read by the last fetch
   // numGroupsLimit first-seen trimming (launch_limit_passes): on when some segment can hold numGroupsLimit groups
@@ -438,7 +514,7 @@ struct pa_query {
   DevBuf lim_keys, lim_pos, lim_sk, lim_sorted, lim_thresh, lim_temp;
   size_t lim_temp_bytes = 0;
   std::vector<LmSegPlan> hplans;
-  std::vector<DevBuf> owned;  // LUTs, remaps, HLL LUTs
+  std::vector<DevBuf> owned;  // LUTs, remaps, HLL LUTs, value dictionaries
   DevBuf acc;                 // all accumulator sections (unless the caller provided the block)
   void* external_acc = nullptr;
   std::vector<Section> sections;
@@ -448,13 +524,8 @@ struct pa_query {
     dev_free(dq);
     dev_free(dsegs);
     dev_free(dplans);
-    dev_free(part_hist);
-    dev_free(part_off);
-    dev_free(part_base);
-    dev_free(recs);
-    dev_free(emit);
-    dev_free(wave_cnt);
-    dev_free(tile_rec);
+    dev_free(dq_count);
+    dev_free(dsegs_count);
     dev_free(lim_keys);
     dev_free(lim_pos);
     dev_free(lim_sk);
@@ -513,74 +584,31 @@ int upload_owned(pa_query* q, const void* host, size_t bytes, void** dev) {
   return PA_OK;
 }
 
-}  // namespace
+// ---------------------------------------------------------------- planning units of pa_query_prepare
+// State handed from one unit to the next.
+struct Prep {
+  std::vector<char> clause_mv;
+  double post_density = 1.0;
+  bool has_filter = false;
+  bool dense = true;
+  bool stage_all = false, stage_post = false;
+  std::vector<int> leaf_slot, gb_slot, agg_slot;
+  std::vector<char> slot_eager, slot_post, slot_gb;
+  std::vector<int64_t> stride;
+  std::vector<char> gb_raw;
+  uint64_t limit_pairs = 0;
+  int limit_eb = 0;
+  std::vector<int> agg_src;
+  std::vector<char> val_fast, agg_mv;
+  bool gb_mv = false;
+  bool lm = false;
+  size_t lds_acc = 0;  // LDS strategy: accumulator bytes
+  std::vector<size_t> agg_lds;
+};
 
-extern "C" {
-
-pa_query* pa_query_create(const pa_query_spec* spec, int32_t num_segments) {
-  if (!spec || num_segments < 0) {
-    fail(PA_EINVAL, "bad query spec");
-    return nullptr;
-  }
-  if (spec->num_leaves < 0 || spec->num_leaves > PA_MAX_LEAVES || spec->num_ops < 0 || spec->num_ops > PA_MAX_OPS ||
-      spec->num_group_by < 0 || spec->num_group_by > PA_MAX_GROUP_BY || spec->num_aggs < 0 ||
-      spec->num_aggs > PA_MAX_AGGS) {
-    fail(PA_EINVAL, "query spec counts out of range");
-    return nullptr;
-  }
-  pa_query* q = new pa_query();
-  q->spec = *spec;
-  q->nseg = num_segments;
-  q->segs.assign(num_segments, nullptr);
-  q->leaf_params.resize(num_segments);
-  q->luts.resize(num_segments);
-  q->remaps.resize(num_segments);
-  q->has_remap.resize(num_segments);
-  return q;
-}
-
-int pa_query_bind_segment(pa_query* q, int32_t index, const pa_segment* seg, const pa_leaf_params* leaf_params,
-                          const int32_t* const* group_remaps) {
-  if (!q || !seg || index < 0 || index >= q->nseg) return fail(PA_EINVAL, "bad bind arguments");
-  if (q->prepared) return fail(PA_EINVAL, "query already prepared");
+// Filter: CNF, clause order (most selective first), eager/lazy split, column slots of the leaves.
+int plan_filter(pa_query* q, Prep& P) {
   const pa_query_spec& s = q->spec;
-  q->segs[index] = seg;
-  q->leaf_params[index].assign(leaf_params, leaf_params + s.num_leaves);
-  q->luts[index].assign(s.num_leaves, {});
-  for (int l = 0; l < s.num_leaves; ++l) {
-    const int kind = s.leaves[l].kind;
-    if (kind == PA_LEAF_DICT_SET || kind == PA_LEAF_MV_DICT_SET) {
-      auto it = seg->cols.find(s.leaves[l].column_id);
-      if (it == seg->cols.end()) return fail(PA_EINVAL, "leaf column missing in segment");
-      if (!leaf_params[l].lut) return fail(PA_EINVAL, "DICT_SET leaf without lut");
-      const size_t words = ((size_t)it->second->cardinality + 31) / 32;
-      q->luts[index][l].assign(leaf_params[l].lut, leaf_params[l].lut + words);
-    }
-  }
-  q->remaps[index].assign(s.num_group_by, {});
-  q->has_remap[index].assign(s.num_group_by, 0);
-  for (int j = 0; j < s.num_group_by; ++j) {
-    if (group_remaps && group_remaps[j]) {
-      auto it = seg->cols.find(s.group_by_columns[j]);
-      if (it == seg->cols.end()) return fail(PA_EINVAL, "group-by column missing in segment");
-      const int32_t card = it->second->cardinality;
-      q->remaps[index][j].assign(group_remaps[j], group_remaps[j] + card);
-      for (int32_t v : q->remaps[index][j])
-        if (v < 0 || v >= s.group_by_cardinality[j]) return fail(PA_EINVAL, "group remap id outside the key space");
-      q->has_remap[index][j] = 1;
-    }
-  }
-  return PA_OK;
-}
-
-int pa_query_prepare(pa_query* q) {
-  if (!q) return fail(PA_EINVAL, "null query");
-  if (q->prepared) return PA_OK;
-  const pa_query_spec& s = q->spec;
-  for (int i = 0; i < q->nseg; ++i)
-    if (!q->segs[i]) return fail(PA_EINVAL, "segment " + std::to_string(i) + " not bound");
-
-  // ---- CNF + slots
   std::vector<Clause> cnf;
   int rc = to_cnf(s, cnf);
   if (rc) return rc;
@@ -588,9 +616,9 @@ int pa_query_prepare(pa_query* q) {
     const int k = s.leaves[leaf].kind;
     return k == PA_LEAF_MV_DICT_RANGE || k == PA_LEAF_MV_DICT_SET;
   };
-  std::vector<char> clause_mv(cnf.size(), 0);  // clauses with an MV literal are evaluated per doc (lazily), last
+  P.clause_mv.assign(cnf.size(), 0);  // clauses with an MV literal are evaluated per doc (lazily), last
   for (size_t c = 0; c < cnf.size(); ++c)
-    for (const Literal& lit : cnf[c]) clause_mv[c] |= is_mv_leaf(lit.leaf);
+    for (const Literal& lit : cnf[c]) P.clause_mv[c] |= is_mv_leaf(lit.leaf);
   // Clause order and late materialisation. Clauses are evaluated most selective first (estimated from the
   // matching-dictId fraction, i.e. assuming dictIds are equally frequent; only speed depends on the estimate).
   // The leading clauses whose expected survivors per wave tile exceed kLazyDensity run on whole staged tiles
@@ -610,17 +638,17 @@ int pa_query_prepare(pa_query* q) {
   std::vector<size_t> order(cnf.size());
   for (size_t c = 0; c < cnf.size(); ++c) order[c] = c;
   std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
-    if (clause_mv[a] != clause_mv[b]) return clause_mv[a] < clause_mv[b];
+    if (P.clause_mv[a] != P.clause_mv[b]) return P.clause_mv[a] < P.clause_mv[b];
     return csel[a] < csel[b];
   });
   const bool no_lazy = (s.flags & (PA_QF_STAGE_ALL | PA_QF_NO_LAZY)) != 0;
   size_t eager_clauses = 0;
   double density = (double)kWTileDocs;  // expected surviving docs per wave tile
-  while (eager_clauses < cnf.size() && !clause_mv[order[eager_clauses]] &&
+  while (eager_clauses < cnf.size() && !P.clause_mv[order[eager_clauses]] &&
          (no_lazy || eager_clauses == 0 || density > kLazyDensity))
     density *= csel[order[eager_clauses++]];
-  double post_density = density;
-  for (size_t c = eager_clauses; c < cnf.size(); ++c) post_density *= csel[order[c]];
+  P.post_density = density;
+  for (size_t c = eager_clauses; c < cnf.size(); ++c) P.post_density *= csel[order[c]];
   q->literals.clear();
   q->clause_end.clear();
   q->num_eager = 0;
@@ -632,57 +660,71 @@ int pa_query_prepare(pa_query* q) {
     }
     if (oc < eager_clauses) q->num_eager = (int)q->literals.size();
   }
-  std::vector<char> slot_eager(kMaxSlots, 0);
-  std::vector<int> leaf_slot(s.num_leaves, -1);
+  P.slot_eager.assign(kMaxSlots, 0);
+  P.leaf_slot.assign(s.num_leaves, -1);
   for (int l = 0; l < s.num_leaves; ++l) {
     const int sl = slot_of(q, s.leaves[l].column_id);
     if (sl < 0) return fail(PA_EUNSUPPORTED, "too many distinct columns in one query");
-    leaf_slot[l] = sl;
+    P.leaf_slot[l] = sl;
   }
-  for (int li = 0; li < q->num_eager; ++li) slot_eager[leaf_slot[q->literals[li].leaf]] = 1;
-  std::vector<int> gb_slot(s.num_group_by);
+  for (int li = 0; li < q->num_eager; ++li) P.slot_eager[P.leaf_slot[q->literals[li].leaf]] = 1;
+  P.has_filter = !q->literals.empty();
+  P.dense = !P.has_filter || P.post_density >= 1.0;
+  return PA_OK;
+}
+
+// Column slots of the group-by columns and aggregations; which slots are staged with the filter columns.
+int plan_slots(pa_query* q, Prep& P) {
+  const pa_query_spec& s = q->spec;
+  P.gb_slot.assign(s.num_group_by, 0);
+  P.slot_gb.assign(kMaxSlots, 0);
   for (int j = 0; j < s.num_group_by; ++j) {
-    gb_slot[j] = slot_of(q, s.group_by_columns[j]);
-    if (gb_slot[j] < 0) return fail(PA_EUNSUPPORTED, "too many distinct columns in one query");
+    P.gb_slot[j] = slot_of(q, s.group_by_columns[j]);
+    if (P.gb_slot[j] < 0) return fail(PA_EUNSUPPORTED, "too many distinct columns in one query");
+    P.slot_gb[P.gb_slot[j]] = 1;
   }
-  std::vector<int> agg_slot(s.num_aggs, 0);
+  P.agg_slot.assign(s.num_aggs, 0);
   for (int a = 0; a < s.num_aggs; ++a) {
     const int t = s.aggs[a].type;
-    if (t < PA_AGG_COUNT || t > PA_AGG_COUNT_MV) return fail(PA_EINVAL, "bad aggregation type");
+    if (t < PA_AGG_COUNT || t > PA_AGG_DISTINCTCOUNT) return fail(PA_EINVAL, "bad aggregation type");
     if (t == PA_AGG_COUNT) continue;
-    agg_slot[a] = slot_of(q, s.aggs[a].column_id);
-    if (agg_slot[a] < 0) return fail(PA_EUNSUPPORTED, "too many distinct columns in one query");
+    P.agg_slot[a] = slot_of(q, s.aggs[a].column_id);
+    if (P.agg_slot[a] < 0) return fail(PA_EUNSUPPORTED, "too many distinct columns in one query");
     if (t == PA_AGG_DISTINCTCOUNTHLL && (s.aggs[a].log2m < 4 || s.aggs[a].log2m > 16))
       return fail(PA_EINVAL, "log2m must be 4..16");
+    if (t == PA_AGG_DISTINCTCOUNT && (s.aggs[a].num_values < 1 || s.aggs[a].num_values > INT32_MAX))
+      return fail(PA_EINVAL, "DISTINCTCOUNT needs the table-wide value count (1..2^31-1)");
   }
-  const int nslots = (int)q->slot_cols.size();
-  const bool has_filter = !q->literals.empty();
   // Post-filter columns (group-by keys, aggregated values) are staged with the filter columns when the filter lets
   // more than kLazyPost docs per wave tile through; below that each surviving doc reads them from HBM.
   const double kLazyPost = 0.25;
-  const bool stage_all = !has_filter || (s.flags & PA_QF_STAGE_ALL);
-  const bool stage_post = stage_all || post_density > kLazyPost;
-  std::vector<char> slot_post(kMaxSlots, 0);
-  for (int j = 0; j < s.num_group_by; ++j) slot_post[gb_slot[j]] = 1;
+  P.stage_all = !P.has_filter || (s.flags & PA_QF_STAGE_ALL);
+  P.stage_post = P.stage_all || P.post_density > kLazyPost;
+  P.slot_post.assign(kMaxSlots, 0);
+  for (int j = 0; j < s.num_group_by; ++j) P.slot_post[P.gb_slot[j]] = 1;
   for (int a = 0; a < s.num_aggs; ++a)
-    if (s.aggs[a].type != PA_AGG_COUNT) slot_post[agg_slot[a]] = 1;
+    if (s.aggs[a].type != PA_AGG_COUNT) P.slot_post[P.agg_slot[a]] = 1;
+  return PA_OK;
+}
 
-  // ---- key space. Direct: table-wide key id = sum_j id_j * prod_{k<j} card_k (DictionaryBasedGroupKeyGenerator raw
-  // key) indexes the accumulators, when every group-by column has a dictionary and the product fits kDirectMaxKeys.
-  // Hashed: the components (dictionary key ids, raw value bits for no-dictionary columns) are packed side by side into
-  // one 64-bit key, mapped to an accumulator slot by a global open-addressing table (the IntMap / LongMap /
-  // NoDictionary*GroupKeyGenerator holders of the reference).
+// Key space. Direct: table-wide key id = sum_j id_j * prod_{k<j} card_k (DictionaryBasedGroupKeyGenerator raw key)
+// indexes the accumulators, when every group-by column has a dictionary and the product fits kDirectMaxKeys. Hashed:
+// the components (dictionary key ids, raw value bits for no-dictionary columns) are packed side by side into one
+// 64-bit key, mapped to an accumulator slot by a global open-addressing table (the IntMap / LongMap /
+// NoDictionary*GroupKeyGenerator holders of the reference).
+int plan_key_space(pa_query* q, Prep& P) {
+  const pa_query_spec& s = q->spec;
   q->hashed = false;
   std::vector<int> gb_bits(s.num_group_by, 0);
-  std::vector<char> gb_raw(s.num_group_by, 0);
+  P.gb_raw.assign(s.num_group_by, 0);
   bool direct_ok = true;
   int64_t K = 1;
-  std::vector<int64_t> stride(s.num_group_by);
+  P.stride.assign(s.num_group_by, 0);
   for (int j = 0; j < s.num_group_by; ++j) {
     auto it = q->segs[0]->cols.find(s.group_by_columns[j]);
     if (it == q->segs[0]->cols.end()) return fail(PA_EINVAL, "group-by column missing in segment 0");
     if (it->second->kind == COL_SV_RAW) {
-      gb_raw[j] = 1;
+      P.gb_raw[j] = 1;
       const int vt = it->second->vtype;
       gb_bits[j] = (vt == PA_INT || vt == PA_FLOAT) ? 32 : 64;
       direct_ok = false;
@@ -691,7 +733,7 @@ int pa_query_prepare(pa_query* q) {
     const int64_t card = s.group_by_cardinality[j];
     if (card < 1) return fail(PA_EINVAL, "group_by_cardinality < 1 for a dictionary column");
     gb_bits[j] = std::max(1, 64 - __builtin_clzll((unsigned long long)std::max<int64_t>(card - 1, 1)));
-    stride[j] = K;
+    P.stride[j] = K;
     if (K > kDirectMaxKeys / card) direct_ok = false;
     else K *= card;
   }
@@ -699,7 +741,7 @@ int pa_query_prepare(pa_query* q) {
     int total_bits = 0;
     for (int j = 0; j < s.num_group_by; ++j) {
       if (total_bits + gb_bits[j] > 64) return fail(PA_EUNSUPPORTED, "packed group key wider than 64 bits");
-      stride[j] = total_bits < 64 ? (int64_t)(uint64_t(1) << total_bits) : 0;
+      P.stride[j] = total_bits < 64 ? (int64_t)(uint64_t(1) << total_bits) : 0;
       q->key_shift[j] = total_bits;
       total_bits += gb_bits[j];
     }
@@ -721,57 +763,63 @@ int pa_query_prepare(pa_query* q) {
     K = (int64_t)H + 1;  // + the reserved slot of the key INT64_MAX (the table's empty marker)
   }
   q->num_keys = K;
+  return PA_OK;
+}
 
-  // ---- numGroupsLimit. The reference caps each segment's group table at numGroupsLimit first-seen groups
-  // (DictionaryBasedGroupKeyGenerator._globalGroupIdUpperBound, NoDictionary*GroupKeyGenerator). It can only bind
-  // when a segment can hold that many distinct keys: min(product of its key cardinalities (a raw column: its docs),
-  // its expanded (doc, key) pairs). Then the first-seen trimming passes run instead of the fused scan.
+// numGroupsLimit. The reference caps each segment's group table at numGroupsLimit first-seen groups
+// (DictionaryBasedGroupKeyGenerator._globalGroupIdUpperBound, NoDictionary*GroupKeyGenerator). It can only bind when a
+// segment can hold that many distinct keys: min(product of its key cardinalities (a raw column: its docs), its
+// expanded (doc, key) pairs). Then the first-seen trimming passes run instead of the fused scan.
+int plan_limit(pa_query* q, Prep& P) {
+  const pa_query_spec& s = q->spec;
   q->limit_mode = false;
-  uint64_t limit_pairs = 0;  // bound on distinct (segment, key) pairs
-  int limit_eb = 0;
-  if (s.num_group_by > 0 && s.num_groups_limit > 0) {
-    auto sat_mul = [](uint64_t a, uint64_t b) { return (b != 0 && a > UINT64_MAX / b) ? UINT64_MAX : a * b; };
-    uint64_t max_exp = 1;
-    for (int si = 0; si < q->nseg; ++si) {
-      const pa_segment* seg = q->segs[si];
-      uint64_t distinct = 1, per_doc = 1;
-      int nmv = 0;
-      int64_t mv_total = 0;
-      for (int j = 0; j < s.num_group_by; ++j) {
-        auto it = seg->cols.find(s.group_by_columns[j]);
-        if (it == seg->cols.end()) return fail(PA_EINVAL, "group-by column missing in segment " + std::to_string(si));
-        const Column* c = it->second;
-        distinct = sat_mul(distinct, c->kind == COL_SV_RAW ? (uint64_t)seg->num_docs : (uint64_t)c->cardinality);
-        if (c->kind == COL_MV_DICT) {
-          per_doc = sat_mul(per_doc, (uint64_t)c->max_values);
-          mv_total = c->total_values;
-          ++nmv;
-        }
+  P.limit_pairs = 0;
+  P.limit_eb = 0;
+  if (s.num_group_by == 0 || s.num_groups_limit <= 0) return PA_OK;
+  auto sat_mul = [](uint64_t a, uint64_t b) { return (b != 0 && a > UINT64_MAX / b) ? UINT64_MAX : a * b; };
+  uint64_t max_exp = 1;
+  for (int si = 0; si < q->nseg; ++si) {
+    const pa_segment* seg = q->segs[si];
+    uint64_t distinct = 1, per_doc = 1;
+    int nmv = 0;
+    int64_t mv_total = 0;
+    for (int j = 0; j < s.num_group_by; ++j) {
+      auto it = seg->cols.find(s.group_by_columns[j]);
+      if (it == seg->cols.end()) return fail(PA_EINVAL, "group-by column missing in segment " + std::to_string(si));
+      const Column* c = it->second;
+      distinct = sat_mul(distinct, c->kind == COL_SV_RAW ? (uint64_t)seg->num_docs : (uint64_t)c->cardinality);
+      if (c->kind == COL_MV_DICT) {
+        per_doc = sat_mul(per_doc, (uint64_t)c->max_values);
+        mv_total = c->total_values;
+        ++nmv;
       }
-      const uint64_t pairs = nmv == 1 ? (uint64_t)mv_total : sat_mul((uint64_t)seg->num_docs, per_doc);
-      const uint64_t bound = std::min(distinct, pairs);
-      if (bound >= (uint64_t)s.num_groups_limit) q->limit_mode = true;
-      limit_pairs = std::min<uint64_t>(UINT64_MAX / 4, limit_pairs + bound);
-      max_exp = std::max(max_exp, per_doc);
     }
-    while (limit_eb < 63 && (uint64_t(1) << limit_eb) < max_exp) ++limit_eb;
-    if (q->limit_mode) {
-      if (limit_eb > 21) return fail(PA_EUNSUPPORTED, "numGroupsLimit trimming: more than 2^21 group keys in one doc");
-      if (q->nseg >= 4095) return fail(PA_EUNSUPPORTED, "numGroupsLimit trimming: more than 4094 segments in one query");
-    }
+    const uint64_t pairs = nmv == 1 ? (uint64_t)mv_total : sat_mul((uint64_t)seg->num_docs, per_doc);
+    const uint64_t bound = std::min(distinct, pairs);
+    if (bound >= (uint64_t)s.num_groups_limit) q->limit_mode = true;
+    P.limit_pairs = std::min<uint64_t>(UINT64_MAX / 4, P.limit_pairs + bound);
+    max_exp = std::max(max_exp, per_doc);
   }
+  while (P.limit_eb < 63 && (uint64_t(1) << P.limit_eb) < max_exp) ++P.limit_eb;
+  if (q->limit_mode) {
+    if (P.limit_eb > 21) return fail(PA_EUNSUPPORTED, "numGroupsLimit trimming: more than 2^21 group keys in one doc");
+    if (q->nseg >= 4095) return fail(PA_EUNSUPPORTED, "numGroupsLimit trimming: more than 4094 segments in one query");
+  }
+  return PA_OK;
+}
 
-  // ---- per-segment descriptors
+// Per-segment descriptors: columns (the staged set of the main scan pass), filter literals in the segment's dictId
+// space, group-by remaps, aggregation value sources, HLL lookup tables.
+int build_segments(pa_query* q, Prep& P) {
+  const pa_query_spec& s = q->spec;
+  const int nslots = (int)q->slot_cols.size();
   q->hsegs.assign(q->nseg, DevSeg{});
-  std::vector<char> staged(nslots, 0);
-  std::vector<int> agg_src(s.num_aggs, SRC_INT);
-  std::vector<char> val_fast(s.num_aggs, 1);
-  std::vector<char> agg_mv(s.num_aggs, 0);  // the aggregation column is multi-value in some segment
-  bool gb_mv = false;                        // some group-by column is multi-value in some segment  // emit fast path: the value is a dictionary or raw INT/LONG/DOUBLE column
-  
-  
-  
+  P.agg_src.assign(s.num_aggs, SRC_INT);
+  P.val_fast.assign(s.num_aggs, 1);  // emit fast path: the value is a dictionary or raw INT/LONG/DOUBLE column
+  P.agg_mv.assign(s.num_aggs, 0);    // the aggregation column is multi-value in some segment
+  P.gb_mv = false;                   // some group-by column is multi-value in some segment
   q->num_docs = 0;
+  int rc;
   for (int si = 0; si < q->nseg; ++si) {
     const pa_segment* seg = q->segs[si];
     DevSeg& d = q->hsegs[si];
@@ -793,9 +841,8 @@ int pa_query_prepare(pa_query* q) {
       dc.dict_i64 = (c->vtype == PA_INT || c->vtype == PA_LONG) ? (const int64_t*)c->dict.p : nullptr;
       dc.dict_f64 = (c->vtype == PA_FLOAT || c->vtype == PA_DOUBLE) ? (const double*)c->dict.p : nullptr;
       dc.lds_off = -1;
-      if (c->kind == COL_SV_DICT && (slot_eager[sl] || stage_all || (stage_post && slot_post[sl]))) {
-        staged[sl] = 1;
-        dc.lds_off = 0;  // staged; the region offset depends on the tile size (apply_layout below)
+      if (c->kind == COL_SV_DICT && (P.slot_eager[sl] || P.stage_all || (P.stage_post && P.slot_post[sl]))) {
+        dc.lds_off = 0;  // staged; the region offset depends on the tile size (apply_layout)
         d.stage[d.num_staged++] = StageDesc{dc.words, dc.nbits, 0};
       }
     }
@@ -805,7 +852,7 @@ int pa_query_prepare(pa_query* q) {
       const pa_leaf_params& p = q->leaf_params[si][lit.leaf];
       DevLeaf& L = d.leaves[li];
       L.kind = s.leaves[lit.leaf].kind;
-      L.slot = leaf_slot[lit.leaf];
+      L.slot = P.leaf_slot[lit.leaf];
       L.negate = (p.negate != 0) != lit.neg;
       L.clause_end = q->clause_end[li];
       const DevCol& dc = d.cols[L.slot];
@@ -856,8 +903,8 @@ int pa_query_prepare(pa_query* q) {
     }
     // group-by remaps
     for (int j = 0; j < s.num_group_by; ++j) {
-      const DevCol& dc = d.cols[gb_slot[j]];
-      if (gb_raw[j]) {
+      const DevCol& dc = d.cols[P.gb_slot[j]];
+      if (P.gb_raw[j]) {
         if (dc.kind != COL_SV_RAW || dc.vtype != q->segs[0]->cols.at(s.group_by_columns[j])->vtype)
           return fail(PA_EINVAL, "a raw group-by column must be raw with the same type in every segment");
         continue;
@@ -866,7 +913,7 @@ int pa_query_prepare(pa_query* q) {
         return fail(PA_EINVAL, "group-by column is dictionary-encoded in segment 0 but not here");
       if (dc.kind == COL_MV_DICT) {
         q->has_mv = 1;
-        gb_mv = true;
+        P.gb_mv = true;
       }
       if (q->has_remap[si][j]) {
         void* dp = nullptr;
@@ -886,11 +933,27 @@ int pa_query_prepare(pa_query* q) {
       const Column* c = seg->cols.at(A.column_id);
       if (c->kind == COL_MV_DICT) {
         q->has_mv = 1;
-        agg_mv[a] = 1;
+        P.agg_mv[a] = 1;
       }
       if (A.type == PA_AGG_COUNT_MV) {
         if (c->kind != COL_MV_DICT) return fail(PA_EINVAL, "COUNT_MV on a single-value column");
-        agg_src[a] = SRC_INT;
+        P.agg_src[a] = SRC_INT;
+        continue;
+      }
+      if (A.type == PA_AGG_DISTINCTCOUNT) {
+        if (c->kind != COL_SV_DICT && c->kind != COL_MV_DICT)
+          return fail(PA_EUNSUPPORTED, "DISTINCTCOUNT needs a dictionary-encoded column");
+        const std::vector<int32_t>& rm = q->vremaps[si][a];
+        if (!rm.empty()) {
+          void* dp = nullptr;
+          rc = upload_owned(q, rm.data(), rm.size() * 4, &dp);
+          if (rc) return rc;
+          d.hll_lut[a] = (const uint32_t*)dp;
+        } else if (c->cardinality > A.num_values) {
+          return fail(PA_EINVAL, "segment dictionary larger than the DISTINCTCOUNT value space without a remap");
+        }
+        P.agg_src[a] = SRC_INT;
+        P.val_fast[a] = 0;
         continue;
       }
       const bool wide = (A.flags & PA_AGGF_WIDE_SUM) && A.type == PA_AGG_SUM;  // layout agreed across ranks
@@ -898,17 +961,17 @@ int pa_query_prepare(pa_query* q) {
                                                                      : ((c->fits_int32 && !wide) ? SRC_INT : SRC_LONG);
       if (!(c->kind == COL_SV_DICT ||
             (c->kind == COL_SV_RAW && (c->vtype == PA_INT || c->vtype == PA_LONG || c->vtype == PA_DOUBLE))))
-        val_fast[a] = 0;
+        P.val_fast[a] = 0;
       if (A.type != PA_AGG_DISTINCTCOUNTHLL) {
         if (c->vtype == PA_STRING || c->vtype == PA_BYTES) return fail(PA_EINVAL, "numeric aggregation on a non-numeric column");
         if (c->kind == COL_SV_DICT && !c->dict.p) return fail(PA_EINVAL, "dictionary values missing");
       }
       if (si == 0) {
-        agg_src[a] = src;
-      } else if (agg_src[a] != src) {
-        if (agg_src[a] == SRC_DOUBLE || src == SRC_DOUBLE)
+        P.agg_src[a] = src;
+      } else if (P.agg_src[a] != src) {
+        if (P.agg_src[a] == SRC_DOUBLE || src == SRC_DOUBLE)
           return fail(PA_EINVAL, "aggregation column type differs across segments");
-        agg_src[a] = SRC_LONG;  // widen: some segment has values outside int32
+        P.agg_src[a] = SRC_LONG;  // widen: some segment has values outside int32
       }
       if (A.type == PA_AGG_DISTINCTCOUNTHLL && (c->kind == COL_SV_DICT || c->kind == COL_MV_DICT)) {
         DevBuf b;
@@ -928,9 +991,13 @@ int pa_query_prepare(pa_query* q) {
       }
     }
   }
-  
+  return PA_OK;
+}
 
-  // ---- accumulators (one device block, sections 256-byte aligned)
+// Accumulators: one device block, sections 256-byte aligned.
+int plan_accumulators(pa_query* q, Prep& P) {
+  const pa_query_spec& s = q->spec;
+  const int64_t K = q->num_keys;
   q->sections.clear();
   q->agg_section.assign(s.num_aggs, -1);
   std::vector<std::pair<int32_t, int64_t>> sec;  // kind, elements
@@ -940,13 +1007,14 @@ int pa_query_prepare(pa_query* q) {
     switch (A.type) {
       case PA_AGG_COUNT: continue;
       case PA_AGG_SUM:
-        if (agg_src[a] == SRC_LONG) sec.push_back({PA_ACC_SUM_I64X2, 2 * K});
-        else sec.push_back({agg_src[a] == SRC_INT ? PA_ACC_SUM_I64 : PA_ACC_SUM_F64, K});
+        if (P.agg_src[a] == SRC_LONG) sec.push_back({PA_ACC_SUM_I64X2, 2 * K});
+        else sec.push_back({P.agg_src[a] == SRC_INT ? PA_ACC_SUM_I64 : PA_ACC_SUM_F64, K});
         break;
       case PA_AGG_MIN: sec.push_back({PA_ACC_MIN_I64, K}); break;
       case PA_AGG_MAX: sec.push_back({PA_ACC_MAX_I64, K}); break;
-      case PA_AGG_DISTINCTCOUNTHLL: sec.push_back({PA_ACC_HLL_U32, K << A.log2m}); break;
+      case PA_AGG_DISTINCTCOUNTHLL: sec.push_back({PA_ACC_HLL_U8, K << A.log2m}); break;
       case PA_AGG_COUNT_MV: sec.push_back({PA_ACC_SUM_I64, K}); break;
+      case PA_AGG_DISTINCTCOUNT: sec.push_back({PA_ACC_PRESENCE_U8, K * presence_stride(A)}); break;
     }
     q->agg_section[a] = (int)sec.size() - 1;
   }
@@ -955,42 +1023,343 @@ int pa_query_prepare(pa_query* q) {
     sec.push_back({PA_ACC_KEYS_I64, K});  // slot -> packed key (INT64_MAX = empty)
     q->keys_section = (int)sec.size() - 1;
   }
-  sec.push_back({PA_ACC_DOCS_U64, 3});  // [0] numDocsScanned, [1] group-table overflows, [2] limit reached (last)
+  sec.push_back({PA_ACC_DOCS_U64, 4});  // [0] numDocsScanned, [1] group-table overflows, [2] limit reached, [3] errors
   size_t total = 0;
   std::vector<size_t> offs;
   for (auto& x : sec) {
     offs.push_back(total);
-    const size_t es = x.first == PA_ACC_HLL_U32 ? 4 : 8;
-    total += ((size_t)x.second * es + 255) & ~(size_t)255;
+    total += ((size_t)x.second * section_es(x.first) + 255) & ~(size_t)255;
   }
-  rc = dev_alloc(q->acc, total);
+  int rc = dev_alloc(q->acc, total);
   if (rc) return rc;
   for (size_t i = 0; i < sec.size(); ++i)
     q->sections.push_back({sec[i].first, (char*)q->acc.p + offs[i], sec[i].second});
-
-  // ---- strategy + LDS layout
-  size_t lds_acc = ((size_t)K * 4 + 15) & ~(size_t)15;  // u32 counts
-  std::vector<size_t> agg_lds(s.num_aggs, 0);
+  // LDS strategy layout: u32 counts, then every aggregation's WG-private accumulators
+  P.lds_acc = ((size_t)K * 4 + 15) & ~(size_t)15;
+  P.agg_lds.assign(s.num_aggs, 0);
   for (int a = 0; a < s.num_aggs; ++a) {
     const pa_agg_spec& A = s.aggs[a];
     if (A.type == PA_AGG_COUNT) continue;
-    agg_lds[a] = lds_acc;
+    P.agg_lds[a] = P.lds_acc;
     const size_t bytes = A.type == PA_AGG_DISTINCTCOUNTHLL ? ((size_t)K << A.log2m) * 4
-                         : (size_t)K * 8 * ((A.type == PA_AGG_SUM && agg_src[a] == SRC_LONG) ? 2 : 1);
-    lds_acc += (bytes + 15) & ~(size_t)15;
+                         : A.type == PA_AGG_DISTINCTCOUNT ? (size_t)K * presence_stride(A)
+                         : (size_t)K * 8 * ((A.type == PA_AGG_SUM && P.agg_src[a] == SRC_LONG) ? 2 : 1);
+    P.lds_acc += (bytes + 15) & ~(size_t)15;
   }
-  // ---- tile geometry: wave tile of 1024 or 2048 docs, D DMA instructions per tile, a ring of R tile images per
-  // wave (R-1 tiles in flight). Measured on MI355X (tools/sweep.py): the decode, not the DMA, is what needs
-  // hiding, so the plan maximises resident waves per CU (workgroups per CU, checked against the occupancy the
-  // compiled kernel really has), then prefers 2048-doc tiles, then bytes in flight (capped at 128 KiB per CU).
-  const size_t kLdsBudget = 160 * 1024;
-  struct Plan {
-    int steps = 0, dma = 0, ring = 0, wg_per_cu = 0, img_dw = 0;
-    size_t lds = 0;
-    double score = -1;
-  };
+  return PA_OK;
+}
+
+// Tile geometry of one scan pass: wave tile of 1024 or 2048 docs, D DMA instructions per tile, a ring of R tile images
+// per wave (R-1 tiles in flight). Measured on MI355X (tools/sweep.py): the decode, not the DMA, is what needs hiding,
+// so the plan maximises resident waves per CU (workgroups per CU, checked against the occupancy the compiled kernel
+// really has), then prefers 2048-doc tiles, then bytes in flight (capped at 128 KiB per CU).
+struct TilePlan {
+  int steps = 0, dma = 0, ring = 0, wg_per_cu = 0, img_dw = 0;
+  size_t lds = 0;
+  double score = -1;
+};
+
+TilePlan plan_tiles(const pa_query* q, const std::vector<DevSeg>& segs, int strat, bool use_lm, size_t acc_b,
+                    bool only16) {
+  const pa_query_spec& s = q->spec;
   const int force_ring = (s.flags >> PA_QF_RING_SHIFT) & 15;
   const int force_wg = (s.flags >> PA_QF_WG_SHIFT) & 7;
+  TilePlan best;
+  for (int steps : {32, 16}) {
+    if (use_lm && steps != 32) continue;
+    if (only16 && steps != 16) continue;
+    if ((s.flags & PA_QF_STEPS16) && steps != 16) continue;
+    if ((s.flags & PA_QF_STEPS32) && steps != 32) continue;
+    int img_dw = kGuardWords, dma = 0;
+    for (const DevSeg& d : segs) {
+      int dw = kGuardWords, n = 0;
+      for (int k = 0; k < d.num_staged; ++k) {
+        const int nb = d.stage[k].nbits;
+        dw += 2 * steps * nb + kGuardWords;
+        n += ((steps / 2) * nb + 63) / 64;
+      }
+      img_dw = std::max(img_dw, dw);
+      dma = std::max(dma, n);
+    }
+    const size_t img_bytes = (size_t)img_dw * 4;
+    for (int wg : {4, 3, 2, 1}) {
+      if (force_wg && wg != force_wg) continue;
+      const size_t per_wg = kLdsBudget / wg;
+      if (per_wg <= acc_b) continue;
+      int ring = (int)((per_wg - acc_b) / (kWavesPerWG * img_bytes));
+      ring = std::min(ring, 8);
+      if (force_ring) {
+        if (force_ring > ring) continue;
+        ring = force_ring;
+      }
+      if (ring < 2) continue;
+      const size_t lds = acc_b + (size_t)kWavesPerWG * ring * img_bytes;
+      int resident = 0;
+      if (set_scan_lds_limit(strat, steps, use_lm, (int)kLdsBudget) != hipSuccess ||
+          scan_occupancy(strat, steps, use_lm, (int)lds, &resident) != hipSuccess)
+        resident = wg;  // no device to ask (planning only): trust the LDS arithmetic
+      if (resident < wg) continue;
+      const double inflight = (double)wg * kWavesPerWG * (ring - 1) * img_bytes;
+      const double score = 1e7 * wg + (steps == 32 ? 1e6 : 0) + std::min(inflight, 128.0 * 1024);
+      if (score > best.score) best = TilePlan{steps, dma, ring, wg, img_dw, lds, score};
+    }
+  }
+  return best;
+}
+
+// Table-wide dictionary of an aggregation's value column (V_FMT_ID records carry a value id): segment 0's device
+// dictionary when every segment holds the same dictionary, else the sorted union with per-segment dictId remaps.
+// Returns the value-id bits, or -1 when the column is not dictionary-encoded everywhere.
+int value_dictionary(pa_query* q, const Prep& P, int a, const uint64_t** vdict) {
+  const pa_query_spec& s = q->spec;
+  const int32_t cid = s.aggs[a].column_id;
+  const Column* c0 = q->segs[0]->cols.at(cid);
+  if (c0->kind != COL_SV_DICT || c0->hvals.empty()) return -1;
+  bool same = true;
+  for (int si = 0; si < q->nseg; ++si) {
+    const Column* c = q->segs[si]->cols.at(cid);
+    if (c->kind != COL_SV_DICT || c->hvals.empty() || c->vtype != c0->vtype) return -1;
+    same = same && (c == c0 || (c->dict_hash == c0->dict_hash && c->hvals == c0->hvals));
+  }
+  for (int si = 0; si < q->nseg; ++si) q->hsegs[si].vremap = nullptr;
+  if (same) {
+    *vdict = (const uint64_t*)c0->dict.p;
+    return std::max(1, 32 - __builtin_clz((uint32_t)std::max(1, c0->cardinality - 1)));
+  }
+  const int32_t vt = c0->vtype;
+  std::vector<std::pair<int64_t, uint64_t>> all;  // (order key, value bits)
+  for (int si = 0; si < q->nseg; ++si)
+    for (uint64_t v : q->segs[si]->cols.at(cid)->hvals) all.push_back({value_order_key(v, vt), v});
+  std::sort(all.begin(), all.end());
+  all.erase(std::unique(all.begin(), all.end(), [](const auto& x, const auto& y) { return x.first == y.first; }),
+            all.end());
+  if (all.size() > (size_t)INT32_MAX) return -1;
+  std::vector<uint64_t> uni(all.size());
+  std::vector<int64_t> keys(all.size());
+  for (size_t i = 0; i < all.size(); ++i) {
+    keys[i] = all[i].first;
+    uni[i] = all[i].second;
+  }
+  void* dp = nullptr;
+  if (upload_owned(q, uni.data(), uni.size() * 8, &dp)) return -2;
+  *vdict = (const uint64_t*)dp;
+  for (int si = 0; si < q->nseg; ++si) {
+    const Column* c = q->segs[si]->cols.at(cid);
+    std::vector<int32_t> rm(c->hvals.size());
+    for (size_t i = 0; i < rm.size(); ++i)
+      rm[i] = (int32_t)(std::lower_bound(keys.begin(), keys.end(), value_order_key(c->hvals[i], vt)) - keys.begin());
+    void* rp = nullptr;
+    if (upload_owned(q, rm.data(), rm.size() * 4, &rp)) return -2;
+    q->hsegs[si].vremap = (const int32_t*)rp;
+  }
+  (void)P;
+  return std::max(1, 64 - __builtin_clzll((unsigned long long)std::max<size_t>(1, uni.size() - 1)));
+}
+
+// The staging of the count pass: the main pass's staged filter columns plus the group-by columns — no value columns.
+std::vector<DevSeg> count_pass_segments(const pa_query* q, const Prep& P) {
+  std::vector<DevSeg> out = q->hsegs;
+  const int nslots = (int)q->slot_cols.size();
+  for (DevSeg& d : out) {
+    d.num_staged = 0;
+    for (int sl = 0; sl < nslots; ++sl) {
+      DevCol& dc = d.cols[sl];
+      if (dc.lds_off < 0) continue;
+      bool filter_col = false;
+      for (size_t li = 0; li < q->literals.size(); ++li) filter_col |= d.leaves[li].slot == sl;
+      if (P.slot_gb[sl] || filter_col) {
+        d.stage[d.num_staged++] = StageDesc{dc.words, dc.nbits, 0};
+      } else {
+        dc.lds_off = -1;
+      }
+    }
+    for (size_t li = 0; li < q->literals.size(); ++li) d.leaves[li].lds_off = d.cols[d.leaves[li].slot].lds_off;
+  }
+  return out;
+}
+
+// Partitioned aggregation plan (BASELINE configs[2] / configs[4]): streams, record formats, key partitioning, bins,
+// LDS of the three kernels. Returns false when the query does not fit it (the per-doc global-atomic path runs).
+bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_plan) {
+  const pa_query_spec& s = q->spec;
+  const int64_t K = q->num_keys;
+  DevQuery& h = q->hq;
+  int hll = -1;
+  int nv = 0;
+  size_t per_key_v = 4;  // u32 count
+  for (int a = 0; a < s.num_aggs; ++a) {
+    const int t = s.aggs[a].type;
+    if (t == PA_AGG_COUNT) continue;
+    if (t == PA_AGG_COUNT_MV || t == PA_AGG_DISTINCTCOUNT) { PLAN_LOG("partitioned: no (exit 1)"); return false; }
+    if (t == PA_AGG_DISTINCTCOUNTHLL) {
+      if (hll >= 0) { PLAN_LOG("partitioned: no (exit 2)"); return false; }  // one H stream per query
+      hll = a;
+      continue;
+    }
+    if (P.agg_mv[a]) { PLAN_LOG("partitioned: no (exit 3)"); return false; }
+    per_key_v += (t == PA_AGG_SUM && P.agg_src[a] == SRC_LONG) ? 16 : 8;
+    ++nv;
+  }
+  const bool vstream = nv > 0 || hll < 0;
+  const size_t part_lds = kPartLdsChoices[(s.flags >> PA_QF_PART_SHIFT) & 3];
+  auto max_keys = [&](size_t per_key) {  // largest power-of-two key range whose accumulators fit pass C's LDS
+    int64_t kr = 1;
+    while ((size_t)(kr * 2) * per_key <= part_lds && kr < K) kr *= 2;
+    return kr;
+  };
+  // records each stream carries when every doc matches (dense plans): one per doc (V), one per HLL value (H)
+  uint64_t hrecs = 0;
+  if (hll >= 0)
+    for (const pa_segment* seg : q->segs) {
+      const Column* c = seg->cols.at(s.aggs[hll].column_id);
+      hrecs += c->kind == COL_MV_DICT ? (uint64_t)c->total_values : (uint64_t)seg->num_docs;
+    }
+  int64_t kr_v = 0, kr_h = 0, Pv = 0, Ph = 0;
+  if (hll >= 0) {
+    const int lg = s.aggs[hll].log2m;
+    kr_h = max_keys(((size_t)1 << lg) + (vstream ? 0 : 4));
+    Ph = (K + kr_h - 1) / kr_h;
+    const int ksh = __builtin_ctzll((uint64_t)kr_h);
+    if (ksh + lg + 6 > 32) { PLAN_LOG("partitioned: no (exit 4)"); return false; }  // H record: key offset | register | rank | first in 32 bits
+  }
+  if (vstream) {
+    kr_v = max_keys(per_key_v);
+    if (hll >= 0) {
+      // as many records per V partition as per H partition (pass C's workgroups take about equally long)
+      const double want = std::max(1.0, (double)Ph * (double)q->num_docs / (double)std::max<uint64_t>(1, hrecs));
+      while (kr_v > 1 && (double)((K + kr_v - 1) / kr_v) < want / 1.5) kr_v /= 2;
+    } else {
+      // at least kMinParts partitions (pass C runs one workgroup each) unless that takes them below 256 keys
+      while (kr_v > 256 && (K + kr_v - 1) / kr_v < kMinParts) kr_v /= 2;
+    }
+    Pv = (K + kr_v - 1) / kr_v;
+  }
+  if (Pv + Ph < 2 || Pv + Ph > kMaxParts) { PLAN_LOG("partitioned: no (exit 5)"); return false; }
+  const int ksv = vstream ? __builtin_ctzll((uint64_t)kr_v) : 0;
+  // V record format: one payload slot per distinct (column, value source); SUM/MIN/MAX of one column share it
+  std::vector<int> pay(s.num_aggs, 0);
+  int words = 1, slots = 0, va = -1;
+  for (int a = 0; a < s.num_aggs; ++a) {
+    const int t = s.aggs[a].type;
+    if (t == PA_AGG_COUNT || t == PA_AGG_DISTINCTCOUNTHLL) continue;
+    int shared = -1;
+    for (int b = 0; b < a; ++b)
+      if (s.aggs[b].type != PA_AGG_COUNT && s.aggs[b].type != PA_AGG_DISTINCTCOUNTHLL && P.agg_slot[b] == P.agg_slot[a] &&
+          P.agg_src[b] == P.agg_src[a])
+        shared = pay[b];
+    if (shared >= 0) {
+      pay[a] = shared;
+    } else {
+      pay[a] = words;
+      words += P.agg_src[a] == SRC_INT ? 1 : 2;
+      ++slots;
+      if (va < 0) va = a;
+    }
+  }
+  int fmt = V_FMT_KEY, W = 1;
+  const uint64_t* vdict = nullptr;
+  if (slots == 1) {
+    const int vbits = P.val_fast[va] ? value_dictionary(q, P, va, &vdict) : -1;
+    if (vbits == -2) { PLAN_LOG("partitioned: no (exit 6)"); return false; }  // (allocation failure: reported by pa_last_error)
+    if (vbits > 0 && vbits + ksv <= 31) {
+      fmt = V_FMT_ID;
+      W = 1;
+    } else if (!P.val_fast[va]) {
+      fmt = V_FMT_GEN;
+      W = words;
+    } else {
+      fmt = P.agg_src[va] == SRC_INT ? V_FMT_32 : V_FMT_64;
+      W = fmt == V_FMT_32 ? 2 : 3;
+    }
+    if (fmt != V_FMT_ID)
+      for (int si = 0; si < q->nseg; ++si) q->hsegs[si].vremap = nullptr;
+  } else if (slots > 1) {
+    fmt = V_FMT_GEN;
+    W = words;
+  }
+  if (W > kMaxVWords) { PLAN_LOG("partitioned: no (exit 7)"); return false; }
+  // bins: a full bin is whole 128-byte lines (V: BS * W * 4 bytes; H: 32 four-byte records)
+  int bs_v = vstream ? 128 / std::gcd(128, 4 * W) : 0;
+  int bs_h = hll >= 0 ? 32 : 0;
+  const int Ptot = (int)(Pv + Ph);
+  auto emit_state = [&](int bv, int bh) {
+    size_t b = (size_t)Ptot * 16 + (size_t)Ptot * 8;  // cnt, done, front, back + start
+    b = (b + 15) & ~(size_t)15;
+    b += (size_t)Pv * bv * W * 4 + (size_t)Ph * bh * 4;
+    return (b + 15) & ~(size_t)15;
+  };
+  // the emit pass stages its columns in a ring next to the bins: halve the bins (down to 64-byte bursts) while they
+  // do not fit or cost resident waves (at least two workgroups per CU hide the per-record gathers)
+  emit_plan = plan_tiles(q, q->hsegs, STRAT_PEMIT, false, emit_state(bs_v, bs_h), true);
+  while ((emit_plan.score < 0 || emit_plan.wg_per_cu < 2) && (bs_h > 16 || (bs_v * W > 16 && bs_v % 8 == 0))) {
+    const int bv2 = (bs_v * W > 16 && bs_v % 8 == 0) ? bs_v / 2 : bs_v;
+    const int bh2 = bs_h > 16 ? bs_h / 2 : bs_h;
+    TilePlan t = plan_tiles(q, q->hsegs, STRAT_PEMIT, false, emit_state(bv2, bh2), true);
+    if (emit_plan.score >= 0 && t.score >= 0 && t.wg_per_cu <= emit_plan.wg_per_cu)
+      break;  // no more resident waves from smaller bins: keep the larger bursts
+    bs_v = bv2;
+    bs_h = bh2;
+    emit_plan = t;
+  }
+  if (emit_plan.score < 0) { PLAN_LOG("partitioned: no (exit 8)"); return false; }
+  q->hsegs_count = count_pass_segments(q, P);
+  count_plan = plan_tiles(q, q->hsegs_count, STRAT_PCOUNT, false, ((size_t)Ptot * 4 + 15) & ~(size_t)15, true);
+  if (count_plan.score < 0) { PLAN_LOG("partitioned: no (exit 9)"); return false; }
+
+  // descriptors (the rest of hq is filled by fill_devquery)
+  h.num_parts = Ptot;
+  h.pv = (int32_t)Pv;
+  h.kshift_v = ksv;
+  h.kshift_h = hll >= 0 ? __builtin_ctzll((uint64_t)kr_h) : 0;
+  h.v_fmt = fmt;
+  h.rec_words_v = W;
+  h.bs_v = bs_v;
+  h.bs_h = bs_h;
+  h.h_first = (hll >= 0 && !vstream) ? 1 : 0;
+  h.hll_agg = hll;
+  h.emit_val_agg = slots == 1 ? va : -1;
+  h.vdict = vdict;
+  size_t o = 0;
+  h.lds_cnt = (uint32_t)o; o += (size_t)Ptot * 4;
+  h.lds_done = (uint32_t)o; o += (size_t)Ptot * 4;
+  h.lds_front = (uint32_t)o; o += (size_t)Ptot * 4;
+  h.lds_back = (uint32_t)o; o += (size_t)Ptot * 4;
+  o = (o + 7) & ~(size_t)7;
+  h.lds_start = (uint32_t)o; o += (size_t)Ptot * 8;
+  o = (o + 15) & ~(size_t)15;
+  h.lds_bins_v = (uint32_t)o; o += (size_t)Pv * bs_v * W * 4;
+  o = (o + 15) & ~(size_t)15;
+  h.lds_bins_h = (uint32_t)o;
+  // pass C LDS: V: u32 count[kr_v], then every aggregation's accumulators (8-byte aligned); H: u8 registers (+ counts)
+  size_t lv = 0;
+  std::vector<int> agg_lds(s.num_aggs, 0);
+  if (vstream) {
+    lv = ((size_t)kr_v * 4 + 15) & ~(size_t)15;
+    for (int a = 0; a < s.num_aggs; ++a) {
+      const int t = s.aggs[a].type;
+      if (t == PA_AGG_COUNT || t == PA_AGG_DISTINCTCOUNTHLL) continue;
+      agg_lds[a] = (int)lv;
+      lv += (size_t)kr_v * ((t == PA_AGG_SUM && P.agg_src[a] == SRC_LONG) ? 16 : 8);
+    }
+  }
+  size_t lh = hll >= 0 ? ((size_t)kr_h << s.aggs[hll].log2m) + (vstream ? 0 : (size_t)kr_h * 4) : 0;
+  q->part_lds_c = (int)std::max(lv, lh);
+  for (int a = 0; a < s.num_aggs; ++a) {
+    h.aggs[a].lds_off = agg_lds[a];
+    h.aggs[a].pay_off = pay[a];
+  }
+  q->partitioned = true;
+  PLAN_LOG("partitioned: K=%lld Pv=%lld (kr %lld, fmt %d, W %d, bs %d) Ph=%lld (kr %lld, bs %d) emit lds %zu wg %d ring %d; "
+           "count lds %zu wg %d", (long long)K, (long long)Pv, (long long)kr_v, fmt, W, bs_v, (long long)Ph,
+           (long long)kr_h, bs_h, emit_plan.lds, emit_plan.wg_per_cu, emit_plan.ring, count_plan.lds,
+           count_plan.wg_per_cu);
+  return true;
+}
+
+// Strategy + tile plan of the main pass.
+int plan_kernels(pa_query* q, Prep& P, TilePlan& plan, TilePlan& count_plan) {
+  const pa_query_spec& s = q->spec;
+  const int64_t K = q->num_keys;
   // Lane-major kernel: every eager literal is a dictionary leaf on a staged column and the per-segment plan table
   // has room for the staged columns and eager literals (otherwise the step-major kernel runs the query).
   bool lm = !(s.flags & (PA_QF_NO_LANE_MAJOR | PA_QF_STEPS16)) && q->num_eager <= kLmEager;
@@ -1000,67 +1369,14 @@ int pa_query_prepare(pa_query* q) {
   }
   for (int si = 0; si < q->nseg && lm; ++si)
     if (q->hsegs[si].num_staged > kLmStaged) lm = false;
-  size_t part_hist_bytes = 0;  // partitioned aggregation: the per-partition LDS counters of the scan passes
-  auto plan_for = [&](int strat, bool use_lm, bool only16 = false) {
-    const bool lds_strategy = strat == STRAT_LDS;
-    Plan best;
-    for (int steps : {32, 16}) {
-      if (use_lm && steps != 32) continue;
-      if (only16 && steps != 16) continue;
-      if ((s.flags & PA_QF_STEPS16) && steps != 16) continue;
-      if ((s.flags & PA_QF_STEPS32) && steps != 32) continue;
-      int img_dw = kGuardWords, dma = 0;
-      for (int si = 0; si < q->nseg; ++si) {
-        int dw = kGuardWords, n = 0;
-        for (int k = 0; k < q->hsegs[si].num_staged; ++k) {
-          const int nb = q->hsegs[si].stage[k].nbits;
-          dw += 2 * steps * nb + kGuardWords;
-          n += ((steps / 2) * nb + 63) / 64;
-        }
-        img_dw = std::max(img_dw, dw);
-        dma = std::max(dma, n);
-      }
-      const size_t img_bytes = (size_t)img_dw * 4;
-      const size_t acc_b = lds_strategy ? lds_acc : (strat == STRAT_PEMIT ? part_hist_bytes : 0);
-      for (int wg : {4, 3, 2, 1}) {
-        if (force_wg && wg != force_wg) continue;
-        const size_t per_wg = kLdsBudget / wg;
-        if (per_wg <= acc_b) continue;
-        int ring = (int)((per_wg - acc_b) / (kWavesPerWG * img_bytes));
-        ring = std::min(ring, 8);
-        if (force_ring) {
-          if (force_ring > ring) continue;
-          ring = force_ring;
-        }
-        if (ring < 2) continue;
-        const size_t lds = acc_b + (size_t)kWavesPerWG * ring * img_bytes;
-        int resident = 0;
-        if (set_scan_lds_limit(strat, steps, use_lm, (int)kLdsBudget) != hipSuccess ||
-            scan_occupancy(strat, steps, use_lm, (int)lds, &resident) != hipSuccess)
-          resident = wg;  // no device to ask (planning only): trust the LDS arithmetic
-        if (resident < wg) continue;
-        const double inflight = (double)wg * kWavesPerWG * (ring - 1) * img_bytes;
-        const double score = 1e7 * wg + (steps == 32 ? 1e6 : 0) + std::min(inflight, 128.0 * 1024);
-        if (score > best.score) best = Plan{steps, dma, ring, wg, img_dw, lds, score};
-      }
-    }
-    return best;
-  };
-  // LDS-privatised accumulators when many docs are expected to reach them (and the key space fits); otherwise the
-  // LDS goes to tile rings (more resident waves) and the rare survivors update global accumulators directly.
-  const bool dense = !has_filter || post_density >= 1.0;
   // Tile layout: lane-major when it applies, except for dense queries on global accumulators, whose per-doc atomics
   // want the most resident waves (measured, tools/bench_configs.py highcard): there the step-major plan wins when it
   // fits more workgroups per CU.
-  auto plan_pick = [&](int strat) {
-    if (strat == STRAT_PEMIT) {  // the emit pass runs 1024-doc step-major tiles only (register budget of its batches)
-      lm = false;
-      return plan_for(strat, false, true);
-    }
-    if (!lm) return plan_for(strat, false);
-    Plan a = plan_for(strat, true);
-    if ((strat == STRAT_GLOBAL || strat == STRAT_PEMIT) && dense) {
-      Plan b = plan_for(strat, false);
+  auto plan_pick = [&](int strat, size_t acc_b) {
+    if (!lm) return plan_tiles(q, q->hsegs, strat, false, acc_b, false);
+    TilePlan a = plan_tiles(q, q->hsegs, strat, true, acc_b, false);
+    if (strat == STRAT_GLOBAL && P.dense) {
+      TilePlan b = plan_tiles(q, q->hsegs, strat, false, acc_b, false);
       if (b.score >= 0 && b.wg_per_cu > a.wg_per_cu) {
         lm = false;
         return b;
@@ -1068,133 +1384,44 @@ int pa_query_prepare(pa_query* q) {
     }
     return a;
   };
-  Plan plan;
+  // LDS-privatised accumulators when many docs are expected to reach them (and the key space fits); otherwise the
+  // LDS goes to tile rings (more resident waves) and the rare survivors update global accumulators directly.
   q->strategy = STRAT_GLOBAL;
-  if (!(s.flags & PA_QF_FORCE_GLOBAL) && !q->limit_mode && !q->hashed && lds_acc <= 64 * 1024 &&
-      (dense || (s.flags & PA_QF_FORCE_LDS))) {
-    plan = plan_pick(STRAT_LDS);
+  if (!(s.flags & PA_QF_FORCE_GLOBAL) && !q->limit_mode && !q->hashed && P.lds_acc <= 64 * 1024 &&
+      (P.dense || (s.flags & PA_QF_FORCE_LDS))) {
+    plan = plan_pick(STRAT_LDS, P.lds_acc);
     if (plan.score >= 0) q->strategy = STRAT_LDS;
   }
-  // Partitioned aggregation for dense queries whose key space does not fit LDS (BASELINE configs[2]): two scan passes
-  // (count per (workgroup, partition); write one record per matching doc into its partition) + one LDS aggregation
-  // per partition, instead of ~(1 + aggregations) device-scope atomics per matching doc on random keys.
+  // Partitioned aggregation for dense queries whose key space does not fit LDS (BASELINE configs[2], configs[4]):
+  // count pass + emit pass into key partitions + one LDS aggregation per partition, instead of ~(1 + aggregations)
+  // device-scope atomics per matching doc on random keys.
   q->partitioned = false;
-  // A DISTINCTCOUNTHLL(MV) joins as one record per value (u8 registers per key in pass C); other multi-value columns
-  // keep the per-doc atomic paths.
-  q->hll_agg = -1;
-  q->hll_key_shift = 0;
-  if (q->strategy == STRAT_GLOBAL && dense && !gb_mv && !q->hashed && !q->limit_mode &&
-      !(s.flags & (PA_QF_NO_PARTITION | PA_QF_FORCE_GLOBAL)) &&
-      K < (int64_t(1) << 32) && q->num_docs < (uint64_t(1) << 30)) {
-    bool ok = true;
-    size_t per_key = 4;  // u32 count
-    int words = 1;       // key
-    std::vector<int> pay(s.num_aggs, 0);
-    for (int a = 0; a < s.num_aggs && ok; ++a) {
-      const int t = s.aggs[a].type;
-      if (t == PA_AGG_COUNT) continue;
-      if (t == PA_AGG_COUNT_MV) { ok = false; break; }
-      if (t == PA_AGG_DISTINCTCOUNTHLL) {
-        // one per query; word 0 = key << (log2m + 6) | register << 6 | rank << 1 | first must fit 32 bits
-        const int lg = s.aggs[a].log2m;
-        if (q->hll_agg >= 0 || lg + 6 >= 32 || K > (int64_t(1) << (32 - (lg + 6)))) { ok = false; break; }
-        q->hll_agg = a;
-        q->hll_key_shift = lg + 6;
-        per_key += (size_t)1 << lg;  // u8 registers
-        continue;
-      }
-      if (agg_mv[a]) { ok = false; break; }
-      per_key += (t == PA_AGG_SUM && agg_src[a] == SRC_LONG) ? 16 : 8;
-      // one payload per distinct (column, value source): SUM/MIN/MAX of one column share it
-      int shared = -1;
-      for (int b = 0; b < a; ++b)
-        if (s.aggs[b].type != PA_AGG_COUNT && s.aggs[b].type != PA_AGG_DISTINCTCOUNTHLL && agg_slot[b] == agg_slot[a] &&
-            agg_src[b] == agg_src[a])
-          shared = pay[b];
-      if (shared >= 0) {
-        pay[a] = shared;
-      } else {
-        pay[a] = words;
-        words += agg_src[a] == SRC_INT ? 1 : 2;
-      }
-    }
-    words = std::max(words, 2);  // COUNT-only records carry an unused value word: records are >= 8 bytes
-    int64_t kr = 1;
-    const size_t part_lds = kPartLdsChoices[(s.flags >> PA_QF_PART_SHIFT) & 3];
-    // largest partitions that fit pass C's LDS, but at least kMinParts of them (pass C runs one workgroup each) unless
-    // that would take them below 256 keys
-    while (ok && (size_t)(kr * 2) * per_key <= part_lds && ((K + 2 * kr - 1) / (2 * kr) >= kMinParts || kr < 256))
-      kr *= 2;
-    const int64_t P = ok ? (K + kr - 1) / kr : 0;
-    // part_bin_kernel: per-partition LDS bins of kPartGroup..64 records within kPartBinLdsBytes; when even one-group
-    // bins of all P partitions do not fit, groups of bin_parts partitions are binned one read of the records each
-    int bin_slots = 0, bin_parts = 0;
-    if (ok && P > 0) {
-      const size_t per_slot = (size_t)words * 4;
-      bin_slots = kPartGroup;
-      while ((size_t)P * (2 * bin_slots * per_slot + 8) <= kPartBinLdsBytes && bin_slots < 64) bin_slots *= 2;
-      bin_parts = (int)std::min<int64_t>(P, (int64_t)(kPartBinLdsBytes / (bin_slots * per_slot + 8)));
-      if (bin_parts < 1) ok = false;
-    }
-    if (ok && kr >= 256 && P >= 2 && P <= kMaxParts) {
-      part_hist_bytes = ((size_t)P * 4 + 4 * kWavesPerWG + 15) & ~(size_t)15;  // counters + wave record cursors
-      Plan pp = plan_pick(STRAT_PEMIT);
-      if (pp.score >= 0) {
-        plan = pp;
-        q->partitioned = true;
-        q->part_P = (int)P;
-        q->part_shift = __builtin_ctzll((uint64_t)kr);
-        q->rec_words = words;
-        q->pay_off = pay;
-        // emit fast path: one payload (or none) from a dictionary / raw INT, LONG, DOUBLE column
-        q->emit_val_agg = -1;
-        q->emit_fast = words <= 3 && q->hll_agg < 0;
-        for (int a = 0; a < s.num_aggs; ++a) {
-          if (s.aggs[a].type == PA_AGG_COUNT || s.aggs[a].type == PA_AGG_DISTINCTCOUNTHLL) continue;
-          if (q->emit_val_agg < 0) q->emit_val_agg = a;
-          if (pay[a] != 1 || !val_fast[a]) q->emit_fast = false;
-        }
-        q->bin_slots = bin_slots;
-        // records per thread per fill round: about a quarter of a bin per partition on uniform keys
-        q->bin_parts = bin_parts;
-        q->bin_iter = (int)std::max<int64_t>(1, std::min<int64_t>(4, (int64_t)bin_parts * bin_slots / (4 * kPartBinThreads)));
-        q->bin_lds = (int)(8 * (size_t)bin_parts + (size_t)bin_parts * bin_slots * words * 4);
-        // pass C LDS layout: u32 count[kr], then every aggregation's accumulators for kr keys (8-byte aligned)
-        size_t off = ((size_t)kr * 4 + 15) & ~(size_t)15;
-        q->part_agg_lds.assign(s.num_aggs, 0);
-        for (int a = 0; a < s.num_aggs; ++a) {
-          const int t = s.aggs[a].type;
-          if (t == PA_AGG_COUNT) continue;
-          q->part_agg_lds[a] = (int)off;
-          if (t == PA_AGG_DISTINCTCOUNTHLL) off += (((size_t)kr << s.aggs[a].log2m) + 15) & ~(size_t)15;
-          else off += (size_t)kr * ((t == PA_AGG_SUM && agg_src[a] == SRC_LONG) ? 16 : 8);
-        }
-        q->part_lds_c = (int)off;
-      }
+  PLAN_LOG("K=%lld strategy=%d dense=%d (post density %.3g) gb_mv=%d hashed=%d limit=%d", (long long)K, q->strategy,
+           (int)P.dense, P.post_density, (int)P.gb_mv, (int)q->hashed, (int)q->limit_mode);
+  if (q->strategy == STRAT_GLOBAL && P.dense && !P.gb_mv && !q->hashed && !q->limit_mode &&
+      !(s.flags & (PA_QF_NO_PARTITION | PA_QF_FORCE_GLOBAL)) && K < (int64_t(1) << 32)) {
+    TilePlan e;
+    if (plan_partitions(q, P, e, count_plan)) {
+      plan = e;
+      lm = false;
     }
   }
-  if (!q->partitioned) {
-    q->hll_agg = -1;
-    q->hll_key_shift = 0;
-  }
-  if (q->strategy == STRAT_GLOBAL && !q->partitioned) plan = plan_pick(STRAT_GLOBAL);
+  if (q->strategy == STRAT_GLOBAL && !q->partitioned) plan = plan_pick(STRAT_GLOBAL, 0);
   if (plan.score < 0) return fail(PA_EUNSUPPORTED, "staged columns too wide for the LDS tile ring");
+  P.lm = lm;
   q->lds_bytes = (int)plan.lds;
   q->steps = plan.steps;
   q->dma_slots = plan.dma;
+  return PA_OK;
+}
 
-  // ---- apply the layout: tiles per segment, LDS regions, staged bytes
+// Tiles per segment, LDS regions of the staged columns, staged bytes.
+void apply_layout(std::vector<DevSeg>& segs, int steps, int nslots, int nleaves, const void* dummy,
+                  uint64_t* staged_bytes, int64_t* total_tiles) {
   int64_t first = 0;
-  q->staged_bytes = 0;
-  void* dummy = nullptr;  // 256 readable bytes: source of the DMA padding instructions
-  {
-    std::vector<char> z(256, 0);
-    rc = upload_owned(q, z.data(), z.size(), &dummy);
-    if (rc) return rc;
-  }
-  for (int si = 0; si < q->nseg; ++si) {
-    DevSeg& d = q->hsegs[si];
-    const int64_t tile_docs = (int64_t)plan.steps * kWave;
+  uint64_t staged = 0;
+  for (DevSeg& d : segs) {
+    const int64_t tile_docs = (int64_t)steps * kWave;
     d.num_wtiles = (int32_t)((d.num_docs + tile_docs - 1) / tile_docs);
     d.first_wtile = first;
     first += d.num_wtiles;
@@ -1204,42 +1431,46 @@ int pa_query_prepare(pa_query* q) {
       d.stage[k].lds_off = off;
       for (int sl = 0; sl < nslots; ++sl)
         if (d.cols[sl].lds_off >= 0 && d.cols[sl].words == d.stage[k].words) d.cols[sl].lds_off = off;
-      q->staged_bytes += (uint64_t)d.num_wtiles * 2 * plan.steps * d.stage[k].nbits * 4;
-      off += 2 * plan.steps * d.stage[k].nbits + kGuardWords;
+      staged += (uint64_t)d.num_wtiles * 2 * steps * d.stage[k].nbits * 4;
+      off += 2 * steps * d.stage[k].nbits + kGuardWords;
     }
     d.image_dwords = off;
-    for (size_t li = 0; li < q->literals.size(); ++li) d.leaves[li].lds_off = d.cols[d.leaves[li].slot].lds_off;
+    for (int li = 0; li < nleaves; ++li) d.leaves[li].lds_off = d.cols[d.leaves[li].slot].lds_off;
   }
-  const int image_max = plan.img_dw;
+  if (staged_bytes) *staged_bytes = staged;
+  if (total_tiles) *total_tiles = first;
+}
 
-  DevQuery& h = q->hq;
-  std::memset(&h, 0, sizeof(h));
+// The scan descriptor of the main pass (and of the count pass, derived from it).
+void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t total_tiles) {
+  const pa_query_spec& s = q->spec;
+  const int nslots = (int)q->slot_cols.size();
+  DevQuery& h = q->hq;  // partition fields were set by plan_partitions; everything else here
   h.num_segments = q->nseg;
   h.num_slots = nslots;
   h.num_leaves = (int32_t)q->literals.size();
   h.num_gb = s.num_group_by;
   h.num_aggs = s.num_aggs;
-  h.strategy = q->strategy;
-  h.image_dwords_max = image_max;
+  h.strategy = q->partitioned ? STRAT_PEMIT : q->strategy;
+  h.image_dwords_max = plan.img_dw;
   h.num_staged = 0;
-  for (int sl = 0; sl < nslots; ++sl)
-    if (staged[sl]) h.staged_slots[h.num_staged++] = sl;
-  for (int j = 0; j < s.num_group_by; ++j) {
-    h.gb_slot[j] = gb_slot[j];
-    h.gb_stride[j] = stride[j];
+  for (int sl = 0; sl < nslots; ++sl) {
+    bool st = false;
+    for (const DevSeg& d : q->hsegs) st |= d.cols[sl].lds_off >= 0;
+    if (st) h.staged_slots[h.num_staged++] = sl;
   }
-  h.num_keys = K;
-  h.total_wtiles = first;
+  for (int j = 0; j < s.num_group_by; ++j) {
+    h.gb_slot[j] = P.gb_slot[j];
+    h.gb_stride[j] = P.stride[j];
+  }
+  h.num_keys = q->num_keys;
+  h.total_wtiles = total_tiles;
   h.ring = plan.ring;
   h.num_eager = q->num_eager;
   h.dma_per_tile = plan.dma;
   h.steps = plan.steps;
   h.debug_stream_only = (s.flags & PA_QF_DEBUG_STREAM_ONLY) ? 1 : 0;
-  h.lane_major = lm ? 1 : 0;
-  q->lane_major = lm ? 1 : 0;
-  q->plan_ring = plan.ring;
-  q->plan_wg = plan.wg_per_cu;
-  q->num_tiles = (uint64_t)first;
+  h.lane_major = P.lm ? 1 : 0;
   h.count = (unsigned long long*)q->sections[0].ptr;
   h.matched_docs = (unsigned long long*)q->sections.back().ptr;
   h.hashed = q->hashed ? 1 : 0;
@@ -1248,134 +1479,113 @@ int pa_query_prepare(pa_query* q) {
     h.ht_keys = (long long*)q->sections[q->keys_section].ptr;
   }
   h.has_mv = q->has_mv;
-  h.xcd_major = dense ? 1 : 0;
+  h.xcd_major = P.dense ? 1 : 0;
   h.lds_count_off = 0;
-  h.lds_acc_bytes = q->strategy == STRAT_LDS ? (uint32_t)lds_acc : (q->partitioned ? (uint32_t)part_hist_bytes : 0);
+  h.lds_acc_bytes = q->strategy == STRAT_LDS ? (uint32_t)P.lds_acc : 0;
+  if (!q->partitioned) {
+    h.hll_agg = -1;
+    h.pv = 0;
+    h.num_parts = 0;
+  }
   for (int a = 0; a < s.num_aggs; ++a) {
     DevAgg& A = h.aggs[a];
     A.type = s.aggs[a].type;
-    A.slot = agg_slot[a];
+    A.slot = P.agg_slot[a];
     A.log2m = s.aggs[a].log2m;
-    A.src = agg_src[a];
-    A.lds_off = q->partitioned ? q->part_agg_lds[a] : (int32_t)agg_lds[a];
-    A.pay_off = q->partitioned ? q->pay_off[a] : 0;
+    A.src = P.agg_src[a];
+    A.nvals = s.aggs[a].type == PA_AGG_DISTINCTCOUNT ? presence_stride(s.aggs[a]) : 0;
+    if (!q->partitioned) {
+      A.lds_off = (int32_t)P.agg_lds[a];
+      A.pay_off = 0;
+    }
     if (q->agg_section[a] >= 0) {
       void* p = q->sections[q->agg_section[a]].ptr;
       A.acc_i64 = (int64_t*)p;
       A.acc_f64 = (double*)p;
-      A.acc_hll = (uint32_t*)p;
+      A.acc_hll = (uint8_t*)p;
     }
   }
+}
 
-  // ---- grid: persistent waves, enough workgroups to cover the CUs several times over
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) {
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
-  }
-  int wg_per_cu = plan.wg_per_cu;
-  if (wg_per_cu < 1) wg_per_cu = 1;
-  const int64_t max_wg = (int64_t)cus * wg_per_cu;
-  const int64_t want = (first + kWavesPerWG - 1) / kWavesPerWG;
-  q->grid = (int)std::max<int64_t>(1, std::min(max_wg, want));
-  if (q->partitioned) {
-    // records: at most one per doc (every bound doc may match); hist: [grid][P]; base: [P + 1]
-    dev_free(q->part_hist);
-    dev_free(q->part_off);
-    dev_free(q->part_base);
-    dev_free(q->recs);
-    dev_free(q->emit);
-    dev_free(q->wave_cnt);
-    // emit buffer: every wave's range holds all docs of its tiles; partitions: every doc plus each (workgroup,
-    // partition) range's padding
-    size_t emit_recs = (size_t)q->num_tiles * (size_t)q->steps * kWave;
-    size_t doc_recs = (size_t)q->num_docs;
-    dev_free(q->tile_rec);
-    h.tile_rec_base = nullptr;
-    if (q->hll_agg >= 0) {
-      // one record per value of the HLL column: every wave tile's first record from a scan of per-tile counts
-      rc = dev_alloc(q->tile_rec, ((size_t)q->num_tiles + 1) * 4);
-      if (rc) return rc;
-      for (int si = 0; si < q->nseg; ++si) {
-        const DevSeg& hs = q->hsegs[si];
-        const DevCol& dc = hs.cols[agg_slot[q->hll_agg]];
-        PA_HIP(launch_tile_records(dc.kind == COL_MV_DICT ? dc.mv_off : nullptr, hs.num_docs, q->steps * kWave,
-                                   hs.num_wtiles, (uint32_t*)q->tile_rec.p + hs.first_wtile, nullptr));
-      }
-      PA_HIP(launch_exclusive_scan_u32((uint32_t*)q->tile_rec.p, (int64_t)q->num_tiles, nullptr));
-      uint32_t total = 0;
-      PA_HIP(hipMemcpy(&total, (uint32_t*)q->tile_rec.p + q->num_tiles, 4, hipMemcpyDeviceToHost));
-      if (total >= (1u << 31)) return fail(PA_EUNSUPPORTED, "more than 2^31 HLL values in one partitioned query");
-      emit_recs = total;
-      doc_recs = total;
-      h.tile_rec_base = (const uint32_t*)q->tile_rec.p;
+// Scratch of a partitioned query (offsets into the device arena) and the arena's size for it.
+int plan_scratch(pa_query* q, const Prep& P) {
+  const DevQuery& h = q->hq;
+  const size_t G = (size_t)q->grid, Pn = (size_t)h.num_parts;
+  uint64_t vrecs = 0, hrecs = 0;
+  if (h.pv > 0) vrecs = q->num_docs + (uint64_t)G * h.pv * (h.bs_v - 1);
+  if (h.hll_agg >= 0) {
+    const int32_t cid = q->spec.aggs[h.hll_agg].column_id;
+    for (const pa_segment* seg : q->segs) {
+      const Column* c = seg->cols.at(cid);
+      hrecs += c->kind == COL_MV_DICT ? (uint64_t)c->total_values : (uint64_t)seg->num_docs;
     }
-    const size_t part_recs = doc_recs + (size_t)q->grid * q->part_P * (kPartGroup - 1);
-    rc = dev_alloc(q->part_hist, (size_t)q->grid * q->part_P * 4);
-    if (!rc) rc = dev_alloc(q->part_off, (size_t)q->grid * q->part_P * 4);
-    if (!rc) rc = dev_alloc(q->part_base, (size_t)(q->part_P + 1) * 4);
-    if (!rc) rc = dev_alloc(q->recs, std::max<size_t>(16, part_recs * q->rec_words * 4));
-    if (!rc) rc = dev_alloc(q->emit, std::max<size_t>(16, emit_recs * q->rec_words * 4));
-    if (!rc) rc = dev_alloc(q->wave_cnt, (size_t)q->grid * kWavesPerWG * 4);
-    if (rc) return rc;
-    h.part_shift = q->part_shift;
-    h.num_parts = q->part_P;
-    h.rec_words = q->rec_words;
-    h.part_lds_bytes = (uint32_t)q->part_lds_c;
-    h.part_hist = (uint32_t*)q->part_hist.p;
-    h.part_off = (uint32_t*)q->part_off.p;
-    h.part_base = (uint32_t*)q->part_base.p;
-    h.recs = (uint32_t*)q->recs.p;
-    h.emit = (uint32_t*)q->emit.p;
-    h.wave_cnt = (uint32_t*)q->wave_cnt.p;
-    h.bin_slots = q->bin_slots;
-    h.bin_iter = q->bin_iter;
-    h.bin_parts = q->bin_parts;
-    h.emit_fast = q->emit_fast ? 1 : 0;
-    h.emit_val_agg = q->emit_val_agg;
-    h.hll_agg = q->hll_agg;
-    h.key_shift = q->hll_key_shift;
+    hrecs += (uint64_t)G * (Pn - h.pv) * (h.bs_h - 1);
   }
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t o = 0;
+  q->sc_hist = o; o += al(G * Pn * 4);
+  q->sc_off = o; o += al(G * Pn * 4);
+  q->sc_base = o; o += al((Pn + 2) * 8);
+  q->sc_recs_v = o; o += al((size_t)vrecs * h.rec_words_v * 4);
+  q->sc_recs_h = o; o += al((size_t)hrecs * 4);
+  q->sc_bytes = std::max<size_t>(o, 256);
+  (void)P;
+  if (hipGetDevice(&q->scratch_dev) != hipSuccess) q->scratch_dev = 0;
+  ScratchArena* a = arena_for(q->scratch_dev);
+  std::lock_guard<std::mutex> g(a->mu);
+  return arena_grow(a, q->sc_bytes);
+}
 
-  if (q->limit_mode) {
-    // first-seen table: twice the (segment, key) pairs that can exist, a power of two
-    uint64_t H = 1024;
-    while (H < 2 * limit_pairs && H <= (uint64_t(1) << 30)) H <<= 1;
-    if (H > (uint64_t(1) << 30))
-      return fail(PA_EUNSUPPORTED, "numGroupsLimit trimming: more than 2^29 distinct (segment, group) pairs possible");
-    const size_t hb = (size_t)H * 8;
-    rc = dev_alloc(q->lim_keys, hb);
-    if (!rc) rc = dev_alloc(q->lim_pos, hb);
-    if (!rc) rc = dev_alloc(q->lim_sk, hb);
-    if (!rc) rc = dev_alloc(q->lim_sorted, hb);
-    if (!rc) rc = dev_alloc(q->lim_thresh, (size_t)std::max(1, q->nseg) * 8);
-    if (rc) return rc;
-    q->lim_temp_bytes = 0;
-    PA_HIP(sort_u64(nullptr, &q->lim_temp_bytes, nullptr, nullptr, (int64_t)H, nullptr));
-    rc = dev_alloc(q->lim_temp, std::max<size_t>(q->lim_temp_bytes, 16));
-    if (rc) return rc;
-    LimitDesc& F = q->limit;
-    F.fkeys = (long long*)q->lim_keys.p;
-    F.fpos = (unsigned long long*)q->lim_pos.p;
-    F.fmask = (int64_t)H - 1;
-    F.sk = (unsigned long long*)q->lim_sk.p;
-    F.sorted = (unsigned long long*)q->lim_sorted.p;
-    F.thresh = (unsigned long long*)q->lim_thresh.p;
-    F.reached = h.matched_docs + 2;
-    F.limit = s.num_groups_limit;
-    F.eb = limit_eb;
-    q->limit_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * 16, first));
-  }
+int plan_limit_buffers(pa_query* q, const Prep& P, int cus, int64_t total_tiles) {
+  const pa_query_spec& s = q->spec;
+  // first-seen table: twice the (segment, key) pairs that can exist, a power of two
+  uint64_t H = 1024;
+  while (H < 2 * P.limit_pairs && H <= (uint64_t(1) << 30)) H <<= 1;
+  if (H > (uint64_t(1) << 30))
+    return fail(PA_EUNSUPPORTED, "numGroupsLimit trimming: more than 2^29 distinct (segment, group) pairs possible");
+  const size_t hb = (size_t)H * 8;
+  int rc = dev_alloc(q->lim_keys, hb);
+  if (!rc) rc = dev_alloc(q->lim_pos, hb);
+  if (!rc) rc = dev_alloc(q->lim_sk, hb);
+  if (!rc) rc = dev_alloc(q->lim_sorted, hb);
+  if (!rc) rc = dev_alloc(q->lim_thresh, (size_t)std::max(1, q->nseg) * 8);
+  if (rc) return rc;
+  q->lim_temp_bytes = 0;
+  PA_HIP(sort_u64(nullptr, &q->lim_temp_bytes, nullptr, nullptr, (int64_t)H, nullptr));
+  rc = dev_alloc(q->lim_temp, std::max<size_t>(q->lim_temp_bytes, 16));
+  if (rc) return rc;
+  LimitDesc& F = q->limit;
+  F.fkeys = (long long*)q->lim_keys.p;
+  F.fpos = (unsigned long long*)q->lim_pos.p;
+  F.fmask = (int64_t)H - 1;
+  F.sk = (unsigned long long*)q->lim_sk.p;
+  F.sorted = (unsigned long long*)q->lim_sorted.p;
+  F.thresh = (unsigned long long*)q->lim_thresh.p;
+  F.reached = q->hq.matched_docs + 2;
+  F.limit = s.num_groups_limit;
+  F.eb = P.limit_eb;
+  q->limit_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * 16, total_tiles));
+  return PA_OK;
+}
 
-  // ---- upload descriptors
-  rc = dev_alloc(q->dq, sizeof(DevQuery));
+// Device copies of the descriptors (+ the lane-major plan tables).
+int upload_descriptors(pa_query* q) {
+  int rc = dev_alloc(q->dq, sizeof(DevQuery));
   if (rc) return rc;
   rc = dev_alloc(q->dsegs, sizeof(DevSeg) * std::max(1, q->nseg));
   if (rc) return rc;
-  PA_HIP(hipMemcpy(q->dq.p, &h, sizeof(DevQuery), hipMemcpyHostToDevice));
+  PA_HIP(hipMemcpy(q->dq.p, &q->hq, sizeof(DevQuery), hipMemcpyHostToDevice));
   if (q->nseg) PA_HIP(hipMemcpy(q->dsegs.p, q->hsegs.data(), sizeof(DevSeg) * q->nseg, hipMemcpyHostToDevice));
+  if (q->partitioned) {
+    rc = dev_alloc(q->dq_count, sizeof(DevQuery));
+    if (!rc) rc = dev_alloc(q->dsegs_count, sizeof(DevSeg) * std::max(1, q->nseg));
+    if (rc) return rc;
+    PA_HIP(hipMemcpy(q->dq_count.p, &q->hq_count, sizeof(DevQuery), hipMemcpyHostToDevice));
+    if (q->nseg)
+      PA_HIP(hipMemcpy(q->dsegs_count.p, q->hsegs_count.data(), sizeof(DevSeg) * q->nseg, hipMemcpyHostToDevice));
+  }
   q->hplans.assign(std::max(1, q->nseg), LmSegPlan{});
-  if (lm) {
+  if (q->lane_major) {
     for (int si = 0; si < q->nseg; ++si) {
       const DevSeg& d = q->hsegs[si];
       LmSegPlan& P = q->hplans[si];
@@ -1410,12 +1620,173 @@ int pa_query_prepare(pa_query* q) {
   if (rc) return rc;
   PA_HIP(hipMemcpy(q->dplans.p, q->hplans.data(), sizeof(LmSegPlan) * q->hplans.size(), hipMemcpyHostToDevice));
   if (q->partitioned) {
-    PA_HIP(set_scan_lds_limit(STRAT_PEMIT, q->steps, q->lane_major, q->lds_bytes));
-    PA_HIP(set_part_bin_lds_limit(q->bin_lds));
+    PA_HIP(set_scan_lds_limit(STRAT_PEMIT, q->steps, 0, q->lds_bytes));
+    PA_HIP(set_scan_lds_limit(STRAT_PCOUNT, q->steps, 0, q->count_lds));
     PA_HIP(set_part_agg_lds_limit(q->part_lds_c));
   } else {
     PA_HIP(set_scan_lds_limit(q->strategy, q->steps, q->lane_major, q->lds_bytes));
   }
+  return PA_OK;
+}
+
+PartScratch scratch_of(const pa_query* q, void* base) {
+  char* b = (char*)base;
+  return PartScratch{(uint32_t*)(b + q->sc_hist), (uint32_t*)(b + q->sc_off), (uint64_t*)(b + q->sc_base),
+                     (uint32_t*)(b + q->sc_recs_v), (uint32_t*)(b + q->sc_recs_h)};
+}
+
+}  // namespace
+
+extern "C" {
+
+pa_query* pa_query_create(const pa_query_spec* spec, int32_t num_segments) {
+  if (!spec || num_segments < 0) {
+    fail(PA_EINVAL, "bad query spec");
+    return nullptr;
+  }
+  if (spec->num_leaves < 0 || spec->num_leaves > PA_MAX_LEAVES || spec->num_ops < 0 || spec->num_ops > PA_MAX_OPS ||
+      spec->num_group_by < 0 || spec->num_group_by > PA_MAX_GROUP_BY || spec->num_aggs < 0 ||
+      spec->num_aggs > PA_MAX_AGGS) {
+    fail(PA_EINVAL, "query spec counts out of range");
+    return nullptr;
+  }
+  pa_query* q = new pa_query();
+  q->spec = *spec;
+  q->nseg = num_segments;
+  q->segs.assign(num_segments, nullptr);
+  q->leaf_params.resize(num_segments);
+  q->luts.resize(num_segments);
+  q->remaps.resize(num_segments);
+  q->has_remap.resize(num_segments);
+  q->vremaps.assign(num_segments, std::vector<std::vector<int32_t>>(spec->num_aggs));
+  return q;
+}
+
+int pa_query_bind_segment(pa_query* q, int32_t index, const pa_segment* seg, const pa_leaf_params* leaf_params,
+                          const int32_t* const* group_remaps) {
+  if (!q || !seg || index < 0 || index >= q->nseg) return fail(PA_EINVAL, "bad bind arguments");
+  if (q->prepared) return fail(PA_EINVAL, "query already prepared");
+  const pa_query_spec& s = q->spec;
+  q->segs[index] = seg;
+  q->leaf_params[index].assign(leaf_params, leaf_params + s.num_leaves);
+  q->luts[index].assign(s.num_leaves, {});
+  for (int l = 0; l < s.num_leaves; ++l) {
+    const int kind = s.leaves[l].kind;
+    if (kind == PA_LEAF_DICT_SET || kind == PA_LEAF_MV_DICT_SET) {
+      auto it = seg->cols.find(s.leaves[l].column_id);
+      if (it == seg->cols.end()) return fail(PA_EINVAL, "leaf column missing in segment");
+      if (!leaf_params[l].lut) return fail(PA_EINVAL, "DICT_SET leaf without lut");
+      const size_t words = ((size_t)it->second->cardinality + 31) / 32;
+      q->luts[index][l].assign(leaf_params[l].lut, leaf_params[l].lut + words);
+    }
+  }
+  q->remaps[index].assign(s.num_group_by, {});
+  q->has_remap[index].assign(s.num_group_by, 0);
+  for (int j = 0; j < s.num_group_by; ++j) {
+    if (group_remaps && group_remaps[j]) {
+      auto it = seg->cols.find(s.group_by_columns[j]);
+      if (it == seg->cols.end()) return fail(PA_EINVAL, "group-by column missing in segment");
+      const int32_t card = it->second->cardinality;
+      q->remaps[index][j].assign(group_remaps[j], group_remaps[j] + card);
+      for (int32_t v : q->remaps[index][j])
+        if (v < 0 || v >= s.group_by_cardinality[j]) return fail(PA_EINVAL, "group remap id outside the key space");
+      q->has_remap[index][j] = 1;
+    }
+  }
+  return PA_OK;
+}
+
+int pa_query_bind_value_remap(pa_query* q, int32_t index, int32_t agg, const int32_t* remap) {
+  if (!q || index < 0 || index >= q->nseg || agg < 0 || agg >= q->spec.num_aggs) return fail(PA_EINVAL, "bad remap arguments");
+  if (q->prepared) return fail(PA_EINVAL, "query already prepared");
+  if (!q->segs[index]) return fail(PA_EINVAL, "bind the segment before its value remaps");
+  const pa_agg_spec& A = q->spec.aggs[agg];
+  if (A.type != PA_AGG_DISTINCTCOUNT) return fail(PA_EINVAL, "value remaps belong to DISTINCTCOUNT aggregations");
+  auto it = q->segs[index]->cols.find(A.column_id);
+  if (it == q->segs[index]->cols.end()) return fail(PA_EINVAL, "aggregation column missing in segment");
+  q->vremaps[index][agg].clear();
+  if (!remap) return PA_OK;
+  const int32_t card = it->second->cardinality;
+  q->vremaps[index][agg].assign(remap, remap + card);
+  for (int32_t v : q->vremaps[index][agg])
+    if (v < 0 || v >= A.num_values) return fail(PA_EINVAL, "value remap id outside the table-wide value dictionary");
+  return PA_OK;
+}
+
+int pa_query_prepare(pa_query* q) {
+  if (!q) return fail(PA_EINVAL, "null query");
+  if (q->prepared) return PA_OK;
+  for (int i = 0; i < q->nseg; ++i)
+    if (!q->segs[i]) return fail(PA_EINVAL, "segment " + std::to_string(i) + " not bound");
+  Prep P;
+  std::memset(&q->hq, 0, sizeof(q->hq));
+  int rc = plan_filter(q, P);
+  if (!rc) rc = plan_slots(q, P);
+  if (!rc) rc = plan_key_space(q, P);
+  if (!rc) rc = plan_limit(q, P);
+  if (!rc) rc = build_segments(q, P);
+  if (!rc) rc = plan_accumulators(q, P);
+  TilePlan plan, count_plan;
+  if (!rc) rc = plan_kernels(q, P, plan, count_plan);
+  if (rc) return rc;
+
+  // layout: tiles per segment, LDS regions (the count pass has its own staging), staged bytes
+  void* dummy = nullptr;  // 256 readable bytes: source of the DMA padding instructions
+  {
+    std::vector<char> z(256, 0);
+    rc = upload_owned(q, z.data(), z.size(), &dummy);
+    if (rc) return rc;
+  }
+  const int nslots = (int)q->slot_cols.size();
+  int64_t total_tiles = 0;
+  apply_layout(q->hsegs, plan.steps, nslots, (int)q->literals.size(), dummy, &q->staged_bytes, &total_tiles);
+  q->num_tiles = (uint64_t)total_tiles;
+  q->lane_major = P.lm ? 1 : 0;
+  q->plan_ring = plan.ring;
+  q->plan_wg = plan.wg_per_cu;
+  fill_devquery(q, P, plan, total_tiles);
+
+  // grid: persistent waves, enough workgroups to cover the CUs several times over
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
+  }
+  const int64_t max_wg = (int64_t)cus * std::max(1, plan.wg_per_cu);
+  const int64_t want = (total_tiles + kWavesPerWG - 1) / kWavesPerWG;
+  q->grid = (int)std::max<int64_t>(1, std::min(max_wg, want));
+
+  if (q->partitioned) {
+    // the count pass: the same tiles, waves and grid; only the group-by and filter columns staged
+    int64_t ct = 0;
+    apply_layout(q->hsegs_count, plan.steps, nslots, (int)q->literals.size(), dummy, nullptr, &ct);
+    if (ct != total_tiles) return fail(PA_EINVAL, "internal: count pass tiles differ");
+    DevQuery& c = q->hq_count;
+    c = q->hq;
+    c.strategy = STRAT_PCOUNT;
+    c.image_dwords_max = count_plan.img_dw;
+    c.ring = count_plan.ring;
+    c.dma_per_tile = count_plan.dma;
+    c.num_staged = 0;
+    for (int sl = 0; sl < nslots; ++sl) {
+      bool st = false;
+      for (const DevSeg& d : q->hsegs_count) st |= d.cols[sl].lds_off >= 0;
+      if (st) c.staged_slots[c.num_staged++] = sl;
+    }
+    c.lds_acc_bytes = (uint32_t)(((size_t)q->hq.num_parts * 4 + 15) & ~(size_t)15);
+    q->count_lds = (int)count_plan.lds;
+    q->count_ring = count_plan.ring;
+    // the emit pass's LDS: partition bin state + bins in front of the ring
+    q->hq.lds_acc_bytes = (uint32_t)(plan.lds - (size_t)kWavesPerWG * plan.ring * plan.img_dw * 4);
+    rc = plan_scratch(q, P);
+    if (rc) return rc;
+  }
+  if (q->limit_mode) {
+    rc = plan_limit_buffers(q, P, cus, total_tiles);
+    if (rc) return rc;
+  }
+  rc = upload_descriptors(q);
+  if (rc) return rc;
   PA_HIP(hipDeviceSynchronize());
   q->prepared = true;
   return PA_OK;
@@ -1438,8 +1809,8 @@ int pa_query_reset(pa_query* q, void* stream) {
 int pa_query_scan(pa_query* q, void* stream) {
   if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
   if (q->num_tiles == 0) return PA_OK;
+  hipStream_t st = (hipStream_t)stream;
   if (q->limit_mode) {  // first-seen positions, sort, thresholds, admitted aggregation
-    hipStream_t st = (hipStream_t)stream;
     const DevQuery* dq = (const DevQuery*)q->dq.p;
     const DevSeg* ds = (const DevSeg*)q->dsegs.p;
     const LimitDesc& F = q->limit;
@@ -1453,19 +1824,28 @@ int pa_query_scan(pa_query* q, void* stream) {
     PA_HIP(launch_limit_passes(dq, ds, F, q->limit_grid, 1, st));
     return PA_OK;
   }
-  if (q->partitioned) {  // emit scan, per-partition offsets, binning into partitions, per-partition aggregation
-    hipStream_t st = (hipStream_t)stream;
-    const DevQuery* dq = (const DevQuery*)q->dq.p;
-    PA_HIP(launch_scan(STRAT_PEMIT, q->steps, q->lane_major, q->grid, q->lds_bytes, dq, (const DevSeg*)q->dsegs.p,
-                       (const LmSegPlan*)q->dplans.p, st));
-    PA_HIP(launch_part_offsets((const uint32_t*)q->part_hist.p, (uint32_t*)q->part_off.p, q->grid, q->part_P,
-                               (uint32_t*)q->part_base.p, st));
-    PA_HIP(launch_part_bin(dq, q->grid, q->bin_lds, st));
-    PA_HIP(launch_part_agg(dq, q->part_P, q->part_lds_c, st));
+  if (q->partitioned) {  // count pass, range offsets, emit pass into the partitions, per-partition aggregation
+    ScratchArena* a = arena_for(q->scratch_dev);
+    std::lock_guard<std::mutex> g(a->mu);
+    int rc = arena_grow(a, q->sc_bytes);
+    if (rc) return rc;
+    if (a->used && a->last_stream != st) PA_HIP(hipStreamWaitEvent(st, a->last, 0));
+    const PartScratch ps = scratch_of(q, a->p);
+    const LmSegPlan* plans = (const LmSegPlan*)q->dplans.p;
+    PA_HIP(launch_scan(STRAT_PCOUNT, q->steps, 0, q->grid, q->count_lds, (const DevQuery*)q->dq_count.p,
+                       (const DevSeg*)q->dsegs_count.p, plans, ps, st));
+    PA_HIP(launch_part_offsets(&q->hq, ps, q->grid, st));
+    PA_HIP(launch_scan(STRAT_PEMIT, q->steps, 0, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p,
+                       (const DevSeg*)q->dsegs.p, plans, ps, st));
+    PA_HIP(launch_part_agg((const DevQuery*)q->dq.p, ps, q->hq.num_parts, q->part_lds_c, st));
+    PA_HIP(hipEventRecord(a->last, st));
+    a->last_stream = st;
+    a->used = true;
     return PA_OK;
   }
+  PartScratch none{};
   PA_HIP(launch_scan(q->strategy, q->steps, q->lane_major, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p,
-                     (const DevSeg*)q->dsegs.p, (const LmSegPlan*)q->dplans.p, (hipStream_t)stream));
+                     (const DevSeg*)q->dsegs.p, (const LmSegPlan*)q->dplans.p, none, st));
   return PA_OK;
 }
 
@@ -1483,19 +1863,26 @@ int pa_query_set_accumulator_buffer(pa_query* q, void* device_buffer, uint64_t b
   char* old = (char*)(q->external_acc ? q->external_acc : q->acc.p);
   char* nb = (char*)device_buffer;
   for (Section& s : q->sections) s.ptr = nb + ((char*)s.ptr - old);
-  DevQuery& h = q->hq;
-  h.count = (unsigned long long*)(nb + ((char*)h.count - old));
-  h.matched_docs = (unsigned long long*)(nb + ((char*)h.matched_docs - old));
-  if (q->limit_mode) q->limit.reached = h.matched_docs + 2;
-  if (q->hashed) h.ht_keys = (long long*)(nb + ((char*)h.ht_keys - old));
-  for (int a = 0; a < h.num_aggs; ++a) {
-    if (q->agg_section[a] < 0) continue;
-    void* p = q->sections[q->agg_section[a]].ptr;
-    h.aggs[a].acc_i64 = (int64_t*)p;
-    h.aggs[a].acc_f64 = (double*)p;
-    h.aggs[a].acc_hll = (uint32_t*)p;
+  // every scan descriptor of the query (the partitioned count pass has its own) points into the new block
+  auto relocate = [&](DevQuery& h) {
+    h.count = (unsigned long long*)(nb + ((char*)h.count - old));
+    h.matched_docs = (unsigned long long*)(nb + ((char*)h.matched_docs - old));
+    if (q->hashed) h.ht_keys = (long long*)(nb + ((char*)h.ht_keys - old));
+    for (int a = 0; a < h.num_aggs; ++a) {
+      if (q->agg_section[a] < 0) continue;
+      void* p = q->sections[q->agg_section[a]].ptr;
+      h.aggs[a].acc_i64 = (int64_t*)p;
+      h.aggs[a].acc_f64 = (double*)p;
+      h.aggs[a].acc_hll = (uint8_t*)p;
+    }
+  };
+  relocate(q->hq);
+  if (q->limit_mode) q->limit.reached = q->hq.matched_docs + 2;
+  PA_HIP(hipMemcpy(q->dq.p, &q->hq, sizeof(DevQuery), hipMemcpyHostToDevice));
+  if (q->partitioned) {
+    relocate(q->hq_count);
+    PA_HIP(hipMemcpy(q->dq_count.p, &q->hq_count, sizeof(DevQuery), hipMemcpyHostToDevice));
   }
-  PA_HIP(hipMemcpy(q->dq.p, &h, sizeof(DevQuery), hipMemcpyHostToDevice));
   if (!q->external_acc) {
     const size_t n = q->acc.n;
     dev_free(q->acc);
@@ -1529,10 +1916,9 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   // Decodes `nrows` host rows into the caller's arrays: row r has key key_of(r), count hc[r] and the aggregation
   // section rows at sec(section)[r * per]. Rows with a zero count are skipped when `skip_empty`.
   // `order` (optional) lists the rows to emit, in output order (hashed key spaces: sorted by packed key).
-  // `hll_u8`: HLL register rows arrive already narrowed to one byte per register (GPU compaction path).
   auto decode = [&](int64_t nrows, const uint64_t* hc, const std::function<const char*(int)>& sec,
                     const std::function<int64_t(int64_t)>& key_of, bool skip_empty,
-                    const std::vector<int64_t>* order, bool hll_u8) -> int64_t {
+                    const std::vector<int64_t>* order) -> int64_t {
     const char* asec[PA_MAX_AGGS];  // section base per aggregation, resolved once (not per row)
     for (int a = 0; a < s.num_aggs; ++a) asec[a] = q->agg_section[a] >= 0 ? sec(q->agg_section[a]) : nullptr;
     int64_t n = 0;
@@ -1553,15 +1939,10 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
           }
           const char* sp = asec[a];
           const int src = q->hq.aggs[a].src;
-          if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
-            const int64_t per = int64_t(1) << A.log2m;
+          if (A.type == PA_AGG_DISTINCTCOUNTHLL || A.type == PA_AGG_DISTINCTCOUNT) {
+            const int64_t per = A.type == PA_AGG_DISTINCTCOUNT ? presence_stride(A) : int64_t(1) << A.log2m;
             uint8_t* o = (uint8_t*)out_aggs[a] + n * per;
-            if (hll_u8) {
-              std::memcpy(o, (const uint8_t*)sp + r * per, (size_t)per);
-            } else {
-              const uint32_t* rg = (const uint32_t*)sp + r * per;
-              for (int64_t j = 0; j < per; ++j) o[j] = (uint8_t)rg[j];
-            }
+            std::memcpy(o, (const uint8_t*)sp + r * per, (size_t)per);
           } else if (A.type == PA_AGG_SUM || A.type == PA_AGG_COUNT_MV) {
             const int64_t* hv = (const int64_t*)sp;
             // SRC_LONG: exact 96-bit total, rounded once (the reference's double of the exact sum)
@@ -1596,6 +1977,7 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
     q->last_matched = (int64_t)docs[0];
     q->last_reached = (int64_t)docs[2];
     if (docs[1]) return fail(PA_EUNSUPPORTED, "group-key table overflow (more distinct groups than slots)");
+    if (docs[3]) return fail(PA_EHIP, "internal: partitioned passes disagree on record counts");
     const uint64_t* hc = (const uint64_t*)hsec(0);
     if (q->hashed) {
       const int64_t* hk = (const int64_t*)hsec(q->keys_section);
@@ -1603,9 +1985,9 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
       for (int64_t r = 0; r < K; ++r)
         if (hc[r]) order.push_back(r);
       std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return hk[a] < hk[b]; });
-      return decode(K, hc, hsec, [&](int64_t r) { return hk[r]; }, false, &order, false);
+      return decode(K, hc, hsec, [&](int64_t r) { return hk[r]; }, false, &order);
     }
-    return decode(K, hc, hsec, [](int64_t r) { return r; }, grouped, nullptr, false);
+    return decode(K, hc, hsec, [](int64_t r) { return r; }, grouped, nullptr);
   }
 
   // Large key spaces: ordered compaction of the non-empty keys on the GPU (count + scan, then key ids and every
@@ -1618,15 +2000,16 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   }
   const int all = grouped ? 0 : 1;
   uint32_t total = 0;
-  uint64_t md[3] = {0, 0, 0};
+  uint64_t md[4] = {0, 0, 0, 0};
   PA_HIP(launch_compact((const unsigned long long*)q->sections[0].ptr, K, all, (uint32_t*)q->fetch_blocks.p, 0,
                         nullptr, 0, st));
   PA_HIP(hipMemcpyAsync(&total, (uint32_t*)q->fetch_blocks.p + nb, 4, hipMemcpyDeviceToHost, st));
-  PA_HIP(hipMemcpyAsync(md, q->sections.back().ptr, 24, hipMemcpyDeviceToHost, st));
+  PA_HIP(hipMemcpyAsync(md, q->sections.back().ptr, 32, hipMemcpyDeviceToHost, st));
   PA_HIP(hipStreamSynchronize(st));
   q->last_matched = (int64_t)md[0];
   q->last_reached = (int64_t)md[2];
   if (md[1]) return fail(PA_EUNSUPPORTED, "group-key table overflow (more distinct groups than slots)");
+  if (md[3]) return fail(PA_EHIP, "internal: partitioned passes disagree on record counts");
   const int64_t m = (int64_t)total;
   const int64_t rows_cap = std::min<int64_t>(m, std::max<int64_t>(capacity, 0));
   if (rows_cap == 0) return m;
@@ -1644,7 +2027,7 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   size_t bytes = ((size_t)rows * 8 + 255) & ~(size_t)255;
   for (int sec : secs) {
     const Section& sc = q->sections[sec];
-    const int es = sc.kind == PA_ACC_HLL_U32 ? 1 : 8;  // HLL registers (< 64) narrowed to bytes by the gather
+    const int es = (int)section_es(sc.kind);  // HLL registers / presence: one byte each
     const int64_t per = sc.n / K;
     offs.push_back(bytes);
     bytes += ((size_t)rows * per * es + 255) & ~(size_t)255;
@@ -1664,8 +2047,7 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   d.keys = (int64_t*)dstage;
   for (size_t i = 0; i < secs.size(); ++i) {
     const Section& sc = q->sections[secs[i]];
-    d.es[i] = sc.kind == PA_ACC_HLL_U32 ? 4 : 8;
-    d.oes[i] = sc.kind == PA_ACC_HLL_U32 ? 1 : d.es[i];
+    d.es[i] = (int32_t)section_es(sc.kind);
     d.per[i] = sc.n / K;
     d.src[i] = sc.ptr;
     d.dst[i] = dstage + offs[i];
@@ -1685,11 +2067,11 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
     std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return pk[a] < pk[b]; });
     order.resize(rows_cap);
     decode(rows, (const uint64_t*)hsec[0], [&](int sec) { return hsec[sec]; }, [&](int64_t r) { return pk[r]; },
-           false, &order, true);
+           false, &order);
     return m;
   }
   decode(rows, (const uint64_t*)hsec[0], [&](int sec) { return hsec[sec]; }, [&](int64_t r) { return hkeys[r]; },
-         false, nullptr, true);
+         false, nullptr);
   return m;
 }
 

@@ -17,20 +17,29 @@ namespace pa {
 constexpr int kWave = 64;
 constexpr int kWavesPerWG = 4;
 constexpr int kWGSize = kWave * kWavesPerWG;
-constexpr int kPartGroup = 16;      // partitioned aggregation: records per store burst / range padding unit
-constexpr int kPartBinThreads = 1024;
 constexpr int kSteps = 32;                    // 64-doc steps per wave tile
 constexpr int kWTileDocs = kWave * kSteps;    // 2048 docs: one wave tile; 64*nb stream words per column
 constexpr int kMaxSlots = 12;                 // distinct columns referenced by one query
 constexpr int kGuardWords = 4;
 
 enum ColKind : int32_t { COL_NONE = 0, COL_SV_DICT = 1, COL_SV_RAW = 2, COL_MV_DICT = 3 };
-// STRAT_PEMIT: the scan pass of partitioned aggregation (high-cardinality dense GROUP BY): every matching doc's record
-// (key, values) is written to its wave's contiguous record range (coalesced) and counted per (workgroup, key
-// partition) in LDS; part_bin_kernel then moves each workgroup's records into their partitions through LDS bins
-// (whole 16-record groups per store burst), and part_agg_kernel aggregates every partition in LDS (no per-doc
-// device-scope atomics).
-enum Strategy : int32_t { STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PEMIT = 2 };
+// Partitioned aggregation (high-cardinality dense GROUP BY), three kernels over the same tile -> wave schedule:
+//   STRAT_PCOUNT: the count pass — filter + group key of every doc, records per (workgroup, key partition) counted in
+//                 LDS (its group-by columns only; numDocsScanned is counted here);
+//   (part_scan_kernel: exclusive scans -> every (workgroup, partition) owns a padded range of its partition);
+//   STRAT_PEMIT:  the emit pass — the same docs' records go into per-partition LDS bins, and a full bin leaves as one
+//                 contiguous burst into the workgroup's range of its partition (each record crosses HBM once);
+//   part_agg_kernel: one workgroup per partition aggregates its records in LDS and stores its key range.
+// Two record streams: V (one record per matching doc: COUNT + SUM/MIN/MAX payloads) and H (one record per value of
+// the DISTINCTCOUNTHLL(MV) column: key | register | rank), each with its own key partitioning.
+enum Strategy : int32_t { STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PEMIT = 2, STRAT_PCOUNT = 3 };
+// V record formats (word 0 always holds the key's offset inside its partition, key & ((1 << kshift_v) - 1)):
+//   V_FMT_KEY: COUNT only, one word;  V_FMT_ID: one word, | value id << kshift_v (the value column's table-wide value
+//   dictionary `vdict`);  V_FMT_32: + the int32 value;  V_FMT_64: + the 64-bit value (int64, or double bits);
+//   V_FMT_GEN: + every payload at its DevAgg::pay_off (one or two words each).
+enum VFormat : int32_t { V_FMT_KEY = 0, V_FMT_ID = 1, V_FMT_32 = 2, V_FMT_64 = 3, V_FMT_GEN = 4 };
+constexpr int kMaxVWords = 9;       // V record words (key + at most four 64-bit payloads)
+constexpr uint32_t kSentinel = 0xffffffffu;  // word 0 of a padding record (never a valid V or H record)
 // SUM/MIN/MAX value source. SRC_INT: every value fits int32 (one exact int64 accumulator);
 // SRC_LONG: 64-bit values, SUM kept exactly as a (low 32 bits unsigned, high 32 bits signed) pair of int64
 // sums = a 96-bit total for up to 2^32 docs per key; SRC_DOUBLE: FLOAT/DOUBLE.
@@ -86,7 +95,9 @@ struct DevSeg {
   DevCol cols[kMaxSlots];
   DevLeaf leaves[PA_MAX_LEAVES];
   const int32_t* remap[PA_MAX_GROUP_BY];   // dictId -> table-wide key id (nullptr = identity)
-  const uint32_t* hll_lut[PA_MAX_AGGS];    // dictId -> (register index << 8) | rank
+  const int32_t* vremap;                   // V_FMT_ID: dictId of the value column -> table-wide value id (nullptr = id)
+  const uint32_t* hll_lut[PA_MAX_AGGS];    // HLL: dictId -> (register index << 8) | rank; DISTINCTCOUNT: dictId ->
+                                           // table-wide value id (nullptr = identity)
 };
 
 struct DevAgg {
@@ -96,9 +107,10 @@ struct DevAgg {
   int32_t src;               // AccSrc
   int64_t* acc_i64;          // SUM(int) [K], SUM(long) [2K: lo, hi], MIN / MAX (ordered encoding for doubles)
   double* acc_f64;           // SUM(double)
-  uint32_t* acc_hll;         // [num_keys << log2m]
+  uint8_t* acc_hll;          // [num_keys << log2m] one byte per register; DISTINCTCOUNT: [num_keys * nvals] presence
+  int64_t nvals;             // DISTINCTCOUNT: presence bytes per key (table-wide values, rounded up to 16)
   int32_t lds_off;           // LDS strategy / partition aggregation: byte offset of the WG-private copy
-  int32_t pay_off;           // partitioned aggregation: word offset of the value inside a record
+  int32_t pay_off;           // partitioned aggregation, V_FMT_GEN: word offset of the value inside a V record
 };
 
 struct DevQuery {
@@ -119,34 +131,28 @@ struct DevQuery {
   int32_t lane_major;        // 1: scan_lm_kernel (docs 32*lane + i of a tile), 0: scan_kernel (docs 64*i + lane)
   int32_t has_mv;            // a group-by or aggregation column is multi-value: per-lane key expansion path
   int32_t xcd_major;         // tiles walked in XCD-major block order (xcd_major_block): dense queries
-  unsigned long long* matched_docs;  // [0]: docs that passed the filter (numDocsScanned), [1]: group-table overflows
+  unsigned long long* matched_docs;  // [0]: docs that passed the filter (numDocsScanned), [1]: group-table overflows,
+                                     // [2]: segments that reached numGroupsLimit, [3]: internal consistency errors
   int32_t hashed;            // packed keys through the open-addressing table ht_keys (gb_stride = 1 << shift)
   int32_t pad3;
   int64_t ht_mask;           // table slots - 1 (power of two); slot ht_mask + 1 is reserved for the key INT64_MAX
   long long* ht_keys;        // slot -> packed key, INT64_MAX = empty
-  int32_t part_shift;        // partitioned aggregation: 1 << part_shift table-wide keys per partition
-  int32_t num_parts;
-  int32_t rec_words;         // words per record: key + values
-  uint32_t part_lds_bytes;   // part_agg_kernel: LDS accumulator bytes for one partition
-  uint32_t* part_hist;       // [grid][num_parts]: records per (workgroup, partition) of the emit pass
-  uint32_t* part_off;        // [grid][num_parts]: first record of a workgroup's range in its partition (ranges padded
-                             // to whole kPartGroup-record groups with sentinel records, key 0xffffffff)
-  uint32_t* part_base;       // [num_parts + 1]: first record of every partition
-  uint32_t* recs;            // records, partition-major (part_bin_kernel output)
-  uint32_t* emit;            // records of the emit pass: wave w's from record (first tile of w) * tile docs on
-  uint32_t* wave_cnt;        // [grid * kWavesPerWG]: records each wave emitted
-  int32_t bin_slots;         // part_bin_kernel: records per LDS bin (power of two >= kPartGroup)
-  int32_t bin_iter;          // part_bin_kernel: records per thread per fill round
-  int32_t bin_parts;         // part_bin_kernel: partitions binned per read of the records (all P when they fit LDS)
-  int32_t emit_fast;         // emit pass: (key, value) records of 2 or 3 words through the batched fast path
-  int32_t emit_val_agg;      // emit fast path: the aggregation whose value the records carry (-1: COUNT only)
-  int32_t hll_agg;           // partitioned DISTINCTCOUNTHLL(MV): its aggregation index (-1: none). Record word 0 is then
-                             // key << key_shift | register << 6 | rank << 1 | first-record-of-the-doc; one record per
-                             // value of an MV column (one with rank 0 for a doc without values)
-  int32_t key_shift;         // 0, or log2m + 6 with hll_agg
+  // partitioned aggregation (STRAT_PCOUNT / STRAT_PEMIT / part_agg_kernel)
+  int32_t num_parts;         // P = pv + ph; V partitions [0, pv), H partitions [pv, P)
+  int32_t pv;                // V partitions (0: no V stream)
+  int32_t kshift_v;          // V partition of key k: k >> kshift_v
+  int32_t kshift_h;          // H partition of key k: k >> kshift_h
+  int32_t v_fmt;             // VFormat
+  int32_t rec_words_v;       // words per V record (1..kMaxVWords)
+  int32_t bs_v, bs_h;        // records per LDS bin (a full bin = one store burst of whole 16-byte units)
+  int32_t h_first;           // H records carry the first-value-of-the-doc flag (no V stream: COUNT comes from H)
+  int32_t hll_agg;           // the partitioned DISTINCTCOUNTHLL(MV) aggregation (-1: no H stream); H record =
+                             // key offset << (log2m + 6) | register << 6 | rank << 1 | first
+  int32_t emit_val_agg;      // V_FMT_ID/32/64: the aggregation whose column the value comes from (-1: COUNT only)
   int32_t pad4;
-  const uint32_t* tile_rec_base;  // with hll_agg: [total_wtiles + 1] first emit record of every wave tile (records of
-                                  // the tiles before it, max(1, values) per doc); nullptr: one record per doc
+  uint32_t lds_cnt, lds_done, lds_front, lds_back, lds_start;  // STRAT_PEMIT LDS (bytes): per-partition bin state
+  uint32_t lds_bins_v, lds_bins_h;                            // STRAT_PEMIT LDS (bytes): the V and H bins
+  const uint64_t* vdict;     // V_FMT_ID: table-wide values of the value column (int64, or double bits)
   int32_t staged_slots[kMaxSlots];
   int32_t gb_slot[PA_MAX_GROUP_BY];
   int64_t gb_stride[PA_MAX_GROUP_BY];
@@ -154,8 +160,17 @@ struct DevQuery {
   int64_t total_wtiles;
   unsigned long long* count; // [num_keys]
   uint32_t lds_count_off;    // LDS strategy: byte offset of u32 count[num_keys]
-  uint32_t lds_acc_bytes;    // LDS strategy: bytes of the WG-private accumulator block
+  uint32_t lds_acc_bytes;    // LDS bytes in front of the tile ring: LDS strategy accumulators / partition state
   DevAgg aggs[PA_MAX_AGGS];
+};
+
+// Scratch of a partitioned query, handed to its kernels per launch (it lives in the device's pooled arena).
+struct PartScratch {
+  uint32_t* hist;    // [grid][P] records per (workgroup, partition): count pass
+  uint32_t* off;     // [grid][P] first record of the workgroup's range, relative to its partition
+  uint64_t* base;    // [P + 2] first record of every partition: V at [0, pv], H at [pv + 1, P + 1] (stream-relative)
+  uint32_t* recs_v;  // V records, partition-major, rec_words_v words each
+  uint32_t* recs_h;  // H records, partition-major, one word each
 };
 
 // Per-segment table of the lane-major scan kernel (scan_lm_kernel): 64 dwords, loaded at segment entry into ONE

@@ -30,6 +30,7 @@ __device__ __forceinline__ AS1 T* gp(T* p) { return (AS1 T*)p; }
 template <class T>
 __device__ __forceinline__ const AS1 T* gp(const T* p) { return (const AS1 T*)p; }
 #define RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // one 16-byte load / store
 
 __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -174,6 +175,8 @@ __device__ __forceinline__ AggValue agg_value(const DevAgg& A, int a, const DevS
     const uint32_t id = decode_dict_id<G>(c, img, doc_local, doc);
     if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
       out.i = gp(seg->hll_lut[a])[id];
+    } else if (A.type == PA_AGG_DISTINCTCOUNT) {
+      out.i = seg->hll_lut[a] != nullptr ? gp(seg->hll_lut[a])[id] : id;  // table-wide value id
     } else if (A.src != SRC_DOUBLE) {
       out.i = gp(c.dict_i64)[id];
     } else {
@@ -201,11 +204,25 @@ __device__ __forceinline__ AggValue agg_value(const DevAgg& A, int a, const DevS
   return out;
 }
 
+// Register max on one byte of the u8 HLL registers in HBM (there are no byte atomics: compare-and-swap on the word
+// holding it; registers only grow, so the loop ends as soon as the byte is already >= v).
+__device__ __forceinline__ void atomic_max_u8(uint8_t* p, uint32_t v) {
+  AS1 uint32_t* w = (AS1 uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
+  const uint32_t sh = ((uint32_t)(uintptr_t)p & 3u) * 8u;
+  uint32_t old = __hip_atomic_load(w, RLX);
+  while (((old >> sh) & 0xffu) < v) {
+    const uint32_t nw = (old & ~(0xffu << sh)) | (v << sh);
+    if (__hip_atomic_compare_exchange_strong(w, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      break;
+  }
+}
+
 // ---- accumulator targets ----
 template <int STRAT>
 struct Acc {
   const DevQuery* q;
   unsigned char* lds;
+  const PartScratch* ps;  // partitioned passes only
 
   __device__ __forceinline__ void add_count(int64_t key, uint32_t n) const {
     if (STRAT == STRAT_LDS) atomicAdd((uint32_t*)(lds + q->lds_count_off) + key, n);
@@ -227,10 +244,15 @@ struct Acc {
     if (STRAT == STRAT_LDS) atomicMax((long long*)(lds + A.lds_off) + key, (long long)v);
     else __hip_atomic_fetch_max(gp((long long*)A.acc_i64) + key, (long long)v, RLX);
   }
+  // DISTINCTCOUNT: the group saw value id v (an idempotent byte store: no atomic needed)
+  __device__ __forceinline__ void set_presence(const DevAgg& A, int64_t key, int64_t v) const {
+    if (STRAT == STRAT_LDS) ((uint8_t*)(lds + A.lds_off))[key * A.nvals + v] = 1;
+    else gp(A.acc_hll)[key * A.nvals + v] = 1;
+  }
   __device__ __forceinline__ void max_hll(const DevAgg& A, int64_t key, uint32_t jr) const {
     const int64_t idx = (key << A.log2m) + (jr >> 8);
     if (STRAT == STRAT_LDS) atomicMax((uint32_t*)(lds + A.lds_off) + idx, jr & 0xffu);
-    else __hip_atomic_fetch_max(gp(A.acc_hll) + idx, jr & 0xffu, RLX);
+    else atomic_max_u8(A.acc_hll + idx, jr & 0xffu);
   }
 };
 
@@ -328,6 +350,8 @@ __device__ __forceinline__ void accumulate_step(const DevQuery* __restrict__ q, 
       if (in) v = agg_value(A, a, seg, img, doc_local, doc);
       if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
         if (in) acc.max_hll(A, key, (uint32_t)v.i);
+      } else if (A.type == PA_AGG_DISTINCTCOUNT) {
+        if (in) acc.set_presence(A, key, v.i);
       } else if (grouped) {
         if (A.type == PA_AGG_SUM) {
           if (A.src == SRC_INT) {
@@ -380,6 +404,7 @@ __device__ __forceinline__ AggValue agg_value_mv(const DevAgg& A, int a, const D
   AggValue out{0, 0.0};
   const uint32_t id = decode_global(c.words, vi, c.nbits);
   if (A.type == PA_AGG_DISTINCTCOUNTHLL) out.i = gp(seg->hll_lut[a])[id];
+  else if (A.type == PA_AGG_DISTINCTCOUNT) out.i = seg->hll_lut[a] != nullptr ? gp(seg->hll_lut[a])[id] : id;
   else if (A.src != SRC_DOUBLE) out.i = gp(c.dict_i64)[id];
   else out.d = gp(c.dict_f64)[id];
   return out;
@@ -389,6 +414,8 @@ template <int STRAT>
 __device__ __forceinline__ void update_one(const DevAgg& A, int64_t key, const AggValue& v, const Acc<STRAT>& acc) {
   if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
     acc.max_hll(A, key, (uint32_t)v.i);
+  } else if (A.type == PA_AGG_DISTINCTCOUNT) {
+    acc.set_presence(A, key, v.i);
   } else if (A.type == PA_AGG_SUM) {
     if (A.src == SRC_INT) {
       acc.add_i64(A, key, v.i);
@@ -472,62 +499,6 @@ __device__ void accumulate_doc_mv(const DevQuery* __restrict__ q, const DevSeg* 
     update_doc_key<STRAT>(q, seg, img, doc_local, doc, key, acc);
   }
 }
-
-// Partitioned aggregation, emit pass (STRAT_PEMIT) for one matching doc: the table-wide key (DictionaryBasedGroupKeyGenerator
-// raw key) picks partition key >> part_shift, counted in the workgroup's LDS histogram; the record (key, then every
-// aggregation's value: int32, or int64 / double bits as two words) goes to record index `pos` of the emit buffer (the
-// lanes of one step write consecutive records: coalesced).
-__device__ __forceinline__ int64_t emit_key(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
-                                            const uint32_t* img, int doc_local, int64_t doc) {
-  int64_t key = 0;
-  for (int j = 0; j < q->num_gb; ++j) {
-    const DevCol& c = seg->cols[q->gb_slot[j]];
-    uint32_t id = decode_dict_id(c, img, doc_local, doc);
-    const int32_t* rm = seg->remap[j];
-    if (rm != nullptr) id = (uint32_t)gp(rm)[id];
-    key += (int64_t)id * q->gb_stride[j];
-  }
-  return key;
-}
-
-__device__ __forceinline__ void emit_doc(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
-                                         const uint32_t* img, int doc_local, int64_t doc, uint32_t* part_lds,
-                                         uint32_t pos) {
-  const int64_t key = emit_key(q, seg, img, doc_local, doc);
-  atomicAdd(part_lds + (uint32_t)(key >> q->part_shift), 1u);
-  const int W = q->rec_words;
-  AS1 uint32_t* r = gp(q->emit) + (size_t)pos * (uint32_t)W;
-  if (W <= 2) {
-    // the common record (key, one int32 value shared by every aggregation of one column): one 8-byte store
-    uint32_t v = 0;
-    for (int a = 0; a < q->num_aggs; ++a) {
-      const DevAgg& A = q->aggs[a];
-      if (A.type != PA_AGG_COUNT) {
-        v = (uint32_t)agg_value(A, a, seg, img, doc_local, doc).i;
-        break;
-      }
-    }
-    *(AS1 uint64_t*)r = ((uint64_t)v << 32) | (uint32_t)key;
-    return;
-  }
-  r[0] = (uint32_t)key;
-  for (int a = 0; a < q->num_aggs; ++a) {
-    const DevAgg& A = q->aggs[a];
-    if (A.type == PA_AGG_COUNT) continue;
-    const AggValue v = agg_value(A, a, seg, img, doc_local, doc);
-    if (A.src == SRC_INT) {
-      r[A.pay_off] = (uint32_t)v.i;
-    } else {
-      const int64_t b = A.src == SRC_DOUBLE ? __builtin_bit_cast(int64_t, v.d) : v.i;
-      r[A.pay_off] = (uint32_t)b;
-      r[A.pay_off + 1] = (uint32_t)(b >> 32);
-    }
-  }
-}
-
-// Partitioned DISTINCTCOUNTHLL(MV) records (written value-parallel in tile_survivors): one per value of an MV column (at
-// least one per matching doc); word 0 packs the key, the HLL register and rank of one value and the doc's first-record
-// flag (COUNT and the per-doc aggregations count only first records); the per-doc payload words follow, as in emit_doc.
 
 // Match word of one leaf over a whole wave tile: bit i of lane l <=> doc 64*i + l of the tile matches.
 // Leaf parameters are loaded once per tile; the 32 decodes are independent, so the LDS reads pipeline.
@@ -681,14 +652,306 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
   return (T*)(((uint64_t)hi << 32) | lo);
 }
 
+// ---------------------------------------------------------------- partitioned aggregation: count + emit passes
+// LDS bin state of the emit pass, per partition (V partitions first, then H): records in the bin (may pass the bin
+// size while a flush is in progress: the excess goes straight to the range), records written into it, the range's next
+// whole-bin slot (front) and its last free record (back), and the range's first record in the stream.
+// All of it through address-space-3 pointers: ds_* instructions. A flat access could alias global memory, and waiting
+// for one (flat loads count in vmcnt) would drain the tile ring's LDS-DMA.
+typedef __attribute__((address_space(3))) uint64_t lds_u64_t;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4_t;
+struct BinState {
+  lds_u32_t* cnt;
+  lds_u32_t* done;
+  lds_u32_t* front;
+  lds_u32_t* back;
+  lds_u64_t* start;
+};
+
+__device__ __forceinline__ lds_u32_t* lds_ptr(const void* p) { return (lds_u32_t*)(uintptr_t)lds_addr(p); }
+
+__device__ __forceinline__ BinState bin_state(const DevQuery* __restrict__ q, unsigned char* lds) {
+  return BinState{lds_ptr(lds + q->lds_cnt), lds_ptr(lds + q->lds_done), lds_ptr(lds + q->lds_front),
+                  lds_ptr(lds + q->lds_back), (lds_u64_t*)lds_ptr(lds + q->lds_start)};
+}
+
+#define WG_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP
+
+// One record (nw words of r) into partition p's LDS bin of BS records. The lane whose write completes the bin stores
+// the whole bin (BS * nw words, whole 16-byte units) at the range's front slot, then empties it; a record arriving
+// while the bin is full goes straight to the back end of the range. Every (workgroup, partition) range holds exactly
+// the records the count pass counted, so front and back meet (checked at the end of the pass).
+// Ordering: LDS executes the DS instructions of one wave in issue order and serialises those of different waves, so
+// "write the slot, then count it done" and "read the bin, then reset the counters" need only the compiler to keep
+// program order (a signal fence). Acquire/release atomics would also wait for every outstanding global load, i.e.
+// drain the tile ring's LDS-DMA on every record.
+template <int WM>
+__device__ __forceinline__ void bin_put(const BinState& B, uint32_t p, lds_u32_t* bin, uint32_t BS, int nw,
+                                        const uint32_t (&r)[WM], AS1 uint32_t* recs) {
+  const uint32_t s = __hip_atomic_fetch_add(B.cnt + p, 1u, WG_RLX);
+  if (s < BS) {
+#pragma unroll
+    for (int w = 0; w < WM; ++w)
+      if (w < nw) bin[s * (uint32_t)nw + w] = r[w];
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint32_t f = __hip_atomic_fetch_add(B.done + p, 1u, WG_RLX);
+    if (f == BS - 1u) {
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      const uint32_t o = B.front[p];
+      B.front[p] = o + BS;
+      AS1 u32x4* d = (AS1 u32x4*)(recs + (B.start[p] + o) * (uint64_t)nw);
+      const lds_u32x4_t* sb = (const lds_u32x4_t*)bin;
+      const uint32_t n16 = (BS * (uint32_t)nw) >> 2;
+      for (uint32_t i = 0; i < n16; ++i) d[i] = sb[i];
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      __hip_atomic_store(B.done + p, 0u, WG_RLX);
+      __hip_atomic_store(B.cnt + p, 0u, WG_RLX);
+    }
+  } else {
+    const uint32_t o = __hip_atomic_fetch_sub(B.back + p, 1u, WG_RLX) - 1u;
+    AS1 uint32_t* d = recs + (B.start[p] + o) * (uint64_t)nw;
+#pragma unroll
+    for (int w = 0; w < WM; ++w)
+      if (w < nw) d[w] = r[w];
+  }
+}
+
+// The matching docs of one tile (match words m) in the count pass (STRAT_PCOUNT: per (workgroup, partition) record
+// counts in LDS) or the emit pass (STRAT_PEMIT: the records into the partition bins). Per batch of 8 steps: every
+// group-by dictId decode, then every remap gather (they overlap), then the table-wide keys; then per stream.
+template <int STRAT, int STEPS, int LM>
+__device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                          const uint32_t* img, int64_t doc_base, uint32_t m, int lane,
+                                          unsigned char* lds, const PartScratch& ps) {
+  // Descriptors through the constant address space: the segment is read-only during the kernel and its pointer is
+  // wave-uniform, so every field is a scalar load the compiler keeps across the LDS atomics and the record stores.
+  typedef const __attribute__((address_space(4))) DevSeg CSeg;
+  CSeg* cs = (CSeg*)(uintptr_t)seg;
+  auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
+  const int ngb = q->num_gb;
+  const int pv = q->pv;
+  const int ksv = q->kshift_v, ksh = q->kshift_h;
+  const int ha = q->hll_agg;
+  const int hslot = ha >= 0 ? q->aggs[ha].slot : 0;
+  const bool hmv = ha >= 0 && cs->cols[hslot].kind == COL_MV_DICT;
+  const int32_t* hoff = cs->cols[hslot].mv_off;
+  constexpr int kEB = 8;  // steps per batch (register budget)
+#pragma unroll 1
+  for (int h = 0; h < STEPS; h += kEB) {
+    if (__ballot((m >> h) != 0) == 0) break;  // wave-uniform: the H records below shuffle across all 64 lanes
+    uint32_t key[kEB];
+#pragma unroll
+    for (int i = 0; i < kEB; ++i) key[i] = 0u;
+    for (int j = 0; j < ngb; ++j) {
+      const int slot = q->gb_slot[j];
+      const int gl = cs->cols[slot].lds_off, gn = cs->cols[slot].nbits;
+      const uint32_t* gw = cs->cols[slot].words;
+      const int32_t* rm = cs->remap[j];
+      const uint32_t st = (uint32_t)q->gb_stride[j];
+      uint32_t id[kEB];
+#pragma unroll
+      for (int i = 0; i < kEB; ++i) {
+        id[i] = 0u;
+        if ((m >> (h + i)) & 1u) {
+          const int dl = local(h + i);
+          id[i] = gl >= 0 ? decode_lds(img + gl, dl, gn) : decode_global(gw, doc_base + dl, gn);
+        }
+      }
+      if (rm != nullptr) {
+#pragma unroll
+        for (int i = 0; i < kEB; ++i)
+          if ((m >> (h + i)) & 1u) id[i] = (uint32_t)gp(rm)[id[i]];
+      }
+#pragma unroll
+      for (int i = 0; i < kEB; ++i) key[i] += id[i] * st;  // table-wide key (< 2^32 on this path)
+    }
+    if constexpr (STRAT == STRAT_PCOUNT) {
+      lds_u32_t* hist = lds_ptr(lds);
+      uint32_t n[kEB];
+#pragma unroll
+      for (int i = 0; i < kEB; ++i) {
+        n[i] = 1u;
+        if (hmv && ((m >> (h + i)) & 1u)) {
+          const int64_t doc = doc_base + local(h + i);
+          const int32_t nv = gp(hoff)[doc + 1] - gp(hoff)[doc];
+          n[i] = nv > 0 ? (uint32_t)nv : 1u;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kEB; ++i) {
+        if (!((m >> (h + i)) & 1u)) continue;
+        if (pv) __hip_atomic_fetch_add(hist + (key[i] >> ksv), 1u, WG_RLX);
+        if (ha >= 0) __hip_atomic_fetch_add(hist + pv + (key[i] >> ksh), n[i], WG_RLX);
+      }
+    } else {
+      const BinState B = bin_state(q, lds);
+      if (pv) {
+        // V records: the value (or its table-wide value id) of the one payload column, batched like the keys
+        const int fmt = q->v_fmt;
+        const int W = q->rec_words_v;
+        const uint32_t BS = (uint32_t)q->bs_v;
+        lds_u32_t* bins = lds_ptr(lds + q->lds_bins_v);
+        const uint32_t kmask = (1u << ksv) - 1u;
+        uint32_t lo[kEB], hi[kEB];
+#pragma unroll
+        for (int i = 0; i < kEB; ++i) lo[i] = hi[i] = 0u;
+        if (fmt == V_FMT_ID || fmt == V_FMT_32 || fmt == V_FMT_64) {
+          const int va = q->emit_val_agg;
+          const int vslot = q->aggs[va].slot;
+          const int vkind = cs->cols[vslot].kind;
+          const int vl = cs->cols[vslot].lds_off, vn = cs->cols[vslot].nbits, vtype = cs->cols[vslot].vtype;
+          const uint32_t* vw = cs->cols[vslot].words;
+          const uint64_t* vd = q->aggs[va].src == SRC_DOUBLE ? (const uint64_t*)cs->cols[vslot].dict_f64
+                                                              : (const uint64_t*)cs->cols[vslot].dict_i64;
+          const int32_t* vrm = cs->vremap;
+          const void* vraw = cs->cols[vslot].raw;
+#pragma unroll
+          for (int i = 0; i < kEB; ++i) {
+            if (!((m >> (h + i)) & 1u)) continue;
+            const int dl = local(h + i);
+            const int64_t doc = doc_base + dl;
+            if (vkind == COL_SV_DICT) {
+              const uint32_t vid = vl >= 0 ? decode_lds(img + vl, dl, vn) : decode_global(vw, doc, vn);
+              if (fmt == V_FMT_ID) {
+                lo[i] = vrm != nullptr ? (uint32_t)gp(vrm)[vid] : vid;
+              } else {
+                const uint64_t v = gp(vd)[vid];
+                lo[i] = (uint32_t)v;
+                hi[i] = (uint32_t)(v >> 32);
+              }
+            } else if (vtype == PA_INT) {
+              lo[i] = (uint32_t)gp((const int32_t*)vraw)[doc];
+              hi[i] = (uint32_t)((int32_t)lo[i] >> 31);
+            } else {  // LONG, or DOUBLE bits (a SUM/MIN/MAX over a raw DOUBLE column reads the bits unchanged)
+              const uint64_t v = gp((const uint64_t*)vraw)[doc];
+              lo[i] = (uint32_t)v;
+              hi[i] = (uint32_t)(v >> 32);
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < kEB; ++i) {
+          if (!((m >> (h + i)) & 1u)) continue;
+          const uint32_t p = key[i] >> ksv;
+          uint32_t r[kMaxVWords];
+          r[0] = key[i] & kmask;
+#pragma unroll
+          for (int w = 1; w < kMaxVWords; ++w) r[w] = 0u;
+          if (fmt == V_FMT_ID) {
+            r[0] |= lo[i] << ksv;
+          } else if (fmt == V_FMT_32) {
+            r[1] = lo[i];
+          } else if (fmt == V_FMT_64) {
+            r[1] = lo[i];
+            r[2] = hi[i];
+          } else if (fmt == V_FMT_GEN) {
+            const int dl = local(h + i);
+            const int64_t doc = doc_base + dl;
+            for (int a = 0; a < q->num_aggs; ++a) {
+              const DevAgg& A = q->aggs[a];
+              if (A.type == PA_AGG_COUNT || a == ha) continue;
+              const AggValue v = agg_value(A, a, seg, img, dl, doc);
+              const int po = A.pay_off;
+              if (A.src == SRC_INT) {
+                if (po < kMaxVWords) r[po] = (uint32_t)v.i;
+              } else {
+                const int64_t b = A.src == SRC_DOUBLE ? __builtin_bit_cast(int64_t, v.d) : v.i;
+                if (po + 1 < kMaxVWords) {
+                  r[po] = (uint32_t)b;
+                  r[po + 1] = (uint32_t)(b >> 32);
+                }
+              }
+            }
+          }
+          bin_put<kMaxVWords>(B, p, bins + p * BS * (uint32_t)W, BS, W, r, gp(ps.recs_v));
+        }
+      }
+      if (ha >= 0) {
+        // H records, value-parallel per step: each matching lane's doc owns n = max(1, values) consecutive records of
+        // the step; lane j takes record g = b + j, finds its owner by a 6-shuffle binary search over the inclusive
+        // prefix sums of n, and decodes that value (coalesced MV reads, no per-lane loop over a doc's values)
+        const DevAgg& H = q->aggs[ha];
+        const uint32_t* hwords = cs->cols[hslot].words;
+        const int hnb = cs->cols[hslot].nbits;
+        const uint32_t* hlut = cs->hll_lut[ha];  // dictId -> (register << 8) | rank
+        const uint32_t BS = (uint32_t)q->bs_h;
+        lds_u32_t* bins = lds_ptr(lds + q->lds_bins_h);
+        const uint32_t kmask = (1u << ksh) - 1u;
+        const int fsh = H.log2m + 6;
+        const uint32_t first_bit = q->h_first ? 1u : 0u;
+#pragma unroll 1
+        for (int i = 0; i < kEB; ++i) {
+          const bool mine = (m >> (h + i)) & 1u;
+          if (__ballot(mine) == 0) continue;
+          const int dl = local(h + i);
+          const int64_t doc = doc_base + dl;
+          uint32_t n = 0, hv_sv = 0;
+          int32_t v0 = 0, nv = 0;
+          if (mine) {
+            if (hmv) {
+              v0 = gp(hoff)[doc];
+              nv = gp(hoff)[doc + 1] - v0;
+              n = nv > 0 ? (uint32_t)nv : 1u;
+            } else {
+              n = 1u;
+              hv_sv = (uint32_t)agg_value(H, ha, seg, img, dl, doc).i;
+            }
+          }
+          uint32_t incl = n;
+#pragma unroll
+          for (int o = 1; o < kWave; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o, kWave);
+            if (lane >= o) incl += t;
+          }
+          const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+          const uint32_t kk = key[i];
+          constexpr int kHB = 4;  // record chunks of 64 per round: their loads overlap
+          for (uint32_t b = 0; b < total; b += kHB * kWave) {
+            uint32_t w0[kHB], id[kHB], pk[kHB];
+            int32_t ok[kHB];
+#pragma unroll
+            for (int k = 0; k < kHB; ++k) {
+              const uint32_t g = b + (uint32_t)(k * kWave + lane);
+              int ow = 0;  // owner lane: the first lane whose inclusive prefix exceeds g
+#pragma unroll
+              for (int st = kWave / 2; st >= 1; st >>= 1) {
+                const uint32_t v = (uint32_t)__shfl((int)incl, ow + st - 1, kWave);
+                if (v <= g) ow += st;
+              }
+              ow = ow < kWave ? ow : kWave - 1;
+              const uint32_t o_incl = (uint32_t)__shfl((int)incl, ow, kWave), o_n = (uint32_t)__shfl((int)n, ow, kWave);
+              const uint32_t o_key = (uint32_t)__shfl((int)kk, ow, kWave);
+              const int32_t o_v0 = __shfl(v0, ow, kWave), o_nv = __shfl(nv, ow, kWave);
+              const uint32_t o_hv = (uint32_t)__shfl((int)hv_sv, ow, kWave);
+              const uint32_t e = g - (o_incl - o_n);
+              ok[k] = g < total ? (hmv ? ((int32_t)e < o_nv ? 2 : 1) : 1) : 0;  // 2: an MV value to look up
+              pk[k] = o_key >> ksh;
+              w0[k] = ((o_key & kmask) << fsh) | (e == 0 ? first_bit : 0u);
+              id[k] = ok[k] == 2 ? decode_global(hwords, (int64_t)o_v0 + e, hnb) : (hmv ? 0u : o_hv);
+            }
+#pragma unroll
+            for (int k = 0; k < kHB; ++k) {
+              if (!ok[k]) continue;
+              const uint32_t hv = ok[k] == 2 ? gp(hlut)[id[k]] : id[k];  // (register << 8) | rank (rank 0: no value)
+              const uint32_t r[1] = {w0[k] | ((hv >> 8) << 6) | ((hv & 0xffu) << 1)};
+              const uint32_t ph = pk[k];
+              bin_put<1>(B, (uint32_t)pv + ph, bins + ph * BS, BS, 1, r, gp(ps.recs_h));
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
 template <int STRAT, int STEPS, int LM>
 __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg_in,
                                                 const uint32_t* img, int64_t doc_base, uint32_t m, int lane,
-                                                unsigned char* lds) {
+                                                unsigned char* lds, const PartScratch& ps) {
   const DevSeg* __restrict__ seg = uniform_ptr(seg_in);
   doc_base = ((int64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)doc_base >> 32)) << 32) |
              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)doc_base);
-  const Acc<STRAT> acc{q, lds};
+  const Acc<STRAT> acc{q, lds, &ps};
   auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
   const int nleaves = q->num_leaves;
   const int neager = q->num_eager;
@@ -712,209 +975,8 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
     }
     if (__ballot(m != 0) == 0) return 0;
   }
-  if constexpr (STRAT == STRAT_PEMIT) {
-    // the wave's record cursor lives in LDS after the partition counters (wave-uniform)
-    uint32_t* cur = (uint32_t*)lds + q->num_parts + (threadIdx.x >> 6);
-    uint32_t c = __builtin_amdgcn_readfirstlane(*cur);
-    if (q->hll_agg >= 0) {
-      // A variable number of records per doc (one per value of the HLL column). Per step: each matching lane computes
-      // its doc's key, record count n (histogram += n) and first-record payload words; a wave prefix sum of n gives
-      // every doc its first record. Then the wave writes word 0 of the step's records VALUE-parallel: lane j takes
-      // record g = base + j, finds the doc owning it (binary search over the prefix sums with 6 lane shuffles) and
-      // decodes that value — no per-lane loop over a doc's values (divergent: max n over the wave), and consecutive
-      // lanes read consecutive MV values and store consecutive records (coalesced).
-      const int ha = q->hll_agg;
-      const DevAgg& H = q->aggs[ha];
-      const DevCol& hc = seg->cols[H.slot];
-      const bool hmv = hc.kind == COL_MV_DICT;
-      const uint32_t* hwords = hc.words;  // MV column's packed values
-      const int hnb = hc.nbits;
-      const uint32_t* hlut = seg->hll_lut[ha];  // dictId -> (register << 8) | rank
-      const int W = q->rec_words;
-      for (int i = 0; i < STEPS; ++i) {
-        const bool mine = (m >> i) & 1u;
-        if (__ballot(mine) == 0) continue;
-        const int64_t doc = doc_base + local(i);
-        uint32_t n = 0, kw = 0, hv_sv = 0;
-        int32_t v0 = 0, nv = 0;
-        if (mine) {
-          if (hmv) {
-            v0 = gp(hc.mv_off)[doc];
-            nv = gp(hc.mv_off)[doc + 1] - v0;
-            n = nv > 0 ? (uint32_t)nv : 1u;
-          } else {
-            n = 1u;
-            hv_sv = (uint32_t)agg_value(H, ha, seg, img, local(i), doc).i;
-          }
-          const int64_t key = emit_key(q, seg, img, local(i), doc);
-          atomicAdd((uint32_t*)lds + (uint32_t)(key >> q->part_shift), n);
-          kw = (uint32_t)key << q->key_shift;
-        }
-        uint32_t incl = n;
-#pragma unroll
-        for (int o = 1; o < kWave; o <<= 1) {
-          const uint32_t t = __shfl_up(incl, o, kWave);
-          if (lane >= o) incl += t;
-        }
-        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
-        if (mine && W > 1) {  // per-doc payloads: words 1.. of the doc's first record
-          AS1 uint32_t* r = gp(q->emit) + (size_t)(c + incl - n) * (uint32_t)W;
-          for (int a = 0; a < q->num_aggs; ++a) {
-            const DevAgg& A = q->aggs[a];
-            if (A.type == PA_AGG_COUNT || a == ha) continue;
-            const AggValue v = agg_value(A, a, seg, img, local(i), doc);
-            if (A.src == SRC_INT) {
-              r[A.pay_off] = (uint32_t)v.i;
-            } else {
-              const int64_t b = A.src == SRC_DOUBLE ? __builtin_bit_cast(int64_t, v.d) : v.i;
-              r[A.pay_off] = (uint32_t)b;
-              r[A.pay_off + 1] = (uint32_t)(b >> 32);
-            }
-          }
-        }
-        // kHB record chunks of 64 per round: all their MV-value loads are issued, then all LUT gathers, then all
-        // stores, so the dependent load chains of a step's chunks overlap instead of running one after another
-        constexpr int kHB = 4;
-        for (uint32_t b = 0; b < total; b += kHB * kWave) {
-          uint32_t w0[kHB], id[kHB];
-          int32_t ok[kHB];
-#pragma unroll
-          for (int k = 0; k < kHB; ++k) {
-            const uint32_t g = b + (uint32_t)(k * kWave + lane);
-            int ow = 0;  // owner lane: the first lane whose inclusive prefix exceeds g
-#pragma unroll
-            for (int st = kWave / 2; st >= 1; st >>= 1) {
-              const uint32_t v = (uint32_t)__shfl((int)incl, ow + st - 1, kWave);
-              if (v <= g) ow += st;
-            }
-            ow = ow < kWave ? ow : kWave - 1;
-            const uint32_t o_incl = (uint32_t)__shfl((int)incl, ow, kWave), o_n = (uint32_t)__shfl((int)n, ow, kWave);
-            const uint32_t o_kw = (uint32_t)__shfl((int)kw, ow, kWave);
-            const int32_t o_v0 = __shfl(v0, ow, kWave), o_nv = __shfl(nv, ow, kWave);
-            const uint32_t o_hv = (uint32_t)__shfl((int)hv_sv, ow, kWave);
-            const uint32_t e = g - (o_incl - o_n);
-            ok[k] = g < total ? (hmv ? ((int32_t)e < o_nv ? 2 : 1) : 1) : 0;  // 2: an MV value to look up
-            w0[k] = o_kw | (e == 0 ? 1u : 0u);
-            id[k] = ok[k] == 2 ? decode_global(hwords, (int64_t)o_v0 + e, hnb) : (hmv ? 0u : o_hv);
-          }
-#pragma unroll
-          for (int k = 0; k < kHB; ++k) {
-            const uint32_t hv = ok[k] == 2 ? gp(hlut)[id[k]] : (ok[k] == 1 ? id[k] : 0u);  // (register << 8) | rank
-            if (ok[k]) gp(q->emit)[(size_t)(c + b + (uint32_t)(k * kWave + lane)) * (uint32_t)W] =
-                w0[k] | ((hv >> 8) << 6) | ((hv & 0xffu) << 1);
-          }
-        }
-        c += total;
-      }
-    } else
-    // fast path: (key, value) records of 2 or 3 words with the value from a dictionary column or a raw INT / LONG /
-    // DOUBLE column
-    if (q->emit_fast) {
-      // Descriptors through the constant address space: the segment is read-only during the kernel and its pointer
-      // is wave-uniform, so every field is a scalar load the compiler keeps across the LDS atomics and the record
-      // stores (through the generic pointer they were vector loads, reloaded after every LDS atomic, each behind a
-      // vmcnt wait that also drained the tile ring). Per batch of 8 steps: per group-by column every dictId decode,
-      // then every remap gather (they overlap), then the value gathers, then keys + LDS histogram, then the
-      // coalesced record stores.
-      typedef const __attribute__((address_space(4))) DevSeg CSeg;
-      CSeg* cs = (CSeg*)(uintptr_t)seg;
-      const int ngb = q->num_gb;
-      const int va = q->emit_val_agg;
-      const int W = q->rec_words;  // 2: 32-bit value, 3: 64-bit value
-      const int vslot = va >= 0 ? q->aggs[va].slot : 0;
-      const int vkind = va >= 0 ? cs->cols[vslot].kind : 0;
-      const int vl = cs->cols[vslot].lds_off, vn = cs->cols[vslot].nbits, vtype = cs->cols[vslot].vtype;
-      const uint32_t* vw = cs->cols[vslot].words;
-      const uint64_t* vd = q->aggs[va < 0 ? 0 : va].src == SRC_DOUBLE ? (const uint64_t*)cs->cols[vslot].dict_f64
-                                                                      : (const uint64_t*)cs->cols[vslot].dict_i64;
-      const void* vraw = cs->cols[vslot].raw;
-      const int shift = q->part_shift;
-      constexpr int kEB = 8;  // steps per batch (register budget)
-#pragma unroll 1
-      for (int h = 0; h < STEPS; h += kEB) {
-        uint32_t key[kEB], lo[kEB], hi[kEB];
-#pragma unroll
-        for (int i = 0; i < kEB; ++i) key[i] = lo[i] = hi[i] = 0u;
-        for (int j = 0; j < ngb; ++j) {
-          const int slot = q->gb_slot[j];
-          const int gl = cs->cols[slot].lds_off, gn = cs->cols[slot].nbits;
-          const uint32_t* gw = cs->cols[slot].words;
-          const int32_t* rm = cs->remap[j];
-          const uint32_t st = (uint32_t)q->gb_stride[j];
-          uint32_t id[kEB];
-#pragma unroll
-          for (int i = 0; i < kEB; ++i) {
-            id[i] = 0u;
-            if ((m >> (h + i)) & 1u) {
-              const int dl = local(h + i);
-              id[i] = gl >= 0 ? decode_lds(img + gl, dl, gn) : decode_global(gw, doc_base + dl, gn);
-            }
-          }
-          if (rm != nullptr) {
-#pragma unroll
-            for (int i = 0; i < kEB; ++i)
-              if ((m >> (h + i)) & 1u) id[i] = (uint32_t)gp(rm)[id[i]];
-          }
-#pragma unroll
-          for (int i = 0; i < kEB; ++i) key[i] += id[i] * st;  // table-wide key (< 2^32 on this path)
-        }
-        if (vkind != 0) {
-#pragma unroll
-          for (int i = 0; i < kEB; ++i) {
-            if ((m >> (h + i)) & 1u) {
-              const int dl = local(h + i);
-              const int64_t doc = doc_base + dl;
-              uint64_t v;
-              if (vkind == COL_SV_DICT) {
-                const uint32_t vid = vl >= 0 ? decode_lds(img + vl, dl, vn) : decode_global(vw, doc, vn);
-                v = gp(vd)[vid];
-              } else if (vtype == PA_INT) {
-                v = (uint64_t)(int64_t)gp((const int32_t*)vraw)[doc];
-              } else {  // LONG, or DOUBLE bits (a SUM/MIN/MAX over a raw DOUBLE column reads the bits unchanged)
-                v = gp((const uint64_t*)vraw)[doc];
-              }
-              lo[i] = (uint32_t)v;
-              hi[i] = (uint32_t)(v >> 32);
-            }
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < kEB; ++i)
-          if ((m >> (h + i)) & 1u) atomicAdd((uint32_t*)lds + (key[i] >> shift), 1u);
-#pragma unroll
-        for (int i = 0; i < kEB; ++i) {
-          const bool mine = (m >> (h + i)) & 1u;
-          const uint64_t sm = __ballot(mine);
-          if (sm == 0) continue;
-          if (mine) {
-            const uint32_t pos = c + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-            if (W == 2) {
-              ((AS1 uint64_t*)gp(q->emit))[pos] = ((uint64_t)lo[i] << 32) | key[i];
-            } else {
-              AS1 uint32_t* r = gp(q->emit) + (size_t)pos * 3u;
-              r[0] = key[i];
-              r[1] = lo[i];
-              r[2] = hi[i];
-            }
-          }
-          c += (uint32_t)__builtin_popcountll(sm);
-        }
-      }
-    } else {
-      for (int i = 0; i < STEPS; ++i) {
-        const bool mine = (m >> i) & 1u;
-        const uint64_t sm = __ballot(mine);
-        if (sm == 0) continue;
-        if (mine) {
-          const uint32_t rank =
-              __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-          emit_doc(q, seg, img, local(i), doc_base + local(i), (uint32_t*)lds, c + rank);
-        }
-        c += (uint32_t)__builtin_popcountll(sm);
-      }
-    }
-    if (lane == 0) *cur = c;
+  if constexpr (STRAT == STRAT_PCOUNT || STRAT == STRAT_PEMIT) {
+    part_tile<STRAT, STEPS, LM>(q, seg, img, doc_base, m, lane, lds, ps);
   } else if (q->has_mv) {
     for (int i = 0; i < STEPS; ++i)
       if ((m >> i) & 1u) accumulate_doc_mv<STRAT>(q, seg, img, local(i), doc_base + local(i), acc);
@@ -959,7 +1021,7 @@ __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, con
     }
   }
   if (__ballot(m != 0) == 0) return;
-  matched += tile_survivors<STRAT, STEPS, 0>(q, seg, img, doc_base, m, lane, acc.lds);
+  matched += tile_survivors<STRAT, STEPS, 0>(q, seg, img, doc_base, m, lane, acc.lds, *acc.ps);
 }
 
 
@@ -1085,7 +1147,7 @@ __device__ __forceinline__ void process_tile_lm(const DevQuery* __restrict__ q, 
     }
   }
   if (__ballot(m != 0) == 0) return;
-  matched += tile_survivors<STRAT, 32, 1>(q, seg, img, doc_base, m, lane, acc.lds);
+  matched += tile_survivors<STRAT, 32, 1>(q, seg, img, doc_base, m, lane, acc.lds, *acc.ps);
 }
 
 __device__ __forceinline__ int find_segment(const DevSeg* __restrict__ segs, int nseg, int64_t t) {
@@ -1178,7 +1240,7 @@ __device__ __forceinline__ int64_t xcd_major_block(int64_t b, int64_t G) {
 template <int STRAT, int STEPS, int LM>
 __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __restrict__ q,
                                                        const DevSeg* __restrict__ segs,
-                                                       const LmSegPlan* __restrict__ plans) {
+                                                       const LmSegPlan* __restrict__ plans, PartScratch ps) {
   static_assert(!LM || STEPS == 32, "lane-major tiles are 2048 docs");
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63;
@@ -1189,7 +1251,7 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
   const uint32_t acc_dwords = STRAT != STRAT_GLOBAL ? (q->lds_acc_bytes >> 2) : 0u;
   const int img_dw = q->image_dwords_max;
   uint32_t* ring = smem + acc_dwords + wave * q->ring * img_dw;
-  Acc<STRAT> acc{q, lds_acc};
+  Acc<STRAT> acc{q, lds_acc, &ps};
 
   if (STRAT == STRAT_LDS) {
     const int64_t K = q->num_keys;
@@ -1201,6 +1263,9 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
       if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
         uint32_t* r = (uint32_t*)(lds_acc + A.lds_off);
         for (int64_t k = threadIdx.x; k < (K << A.log2m); k += kWGSize) r[k] = 0;
+      } else if (A.type == PA_AGG_DISTINCTCOUNT) {
+        uint32_t* r = (uint32_t*)(lds_acc + A.lds_off);
+        for (int64_t k = threadIdx.x; k < K * A.nvals / 4; k += kWGSize) r[k] = 0;
       } else {
         int64_t* r = (int64_t*)(lds_acc + A.lds_off);
         const int64_t init = A.type == PA_AGG_MIN ? INT64_MAX : (A.type == PA_AGG_MAX ? INT64_MIN : 0);  // SUM, COUNT_MV: 0
@@ -1209,16 +1274,22 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
       }
     }
     __syncthreads();
+  } else if (STRAT == STRAT_PCOUNT) {
+    uint32_t* hist = (uint32_t*)lds_acc;
+    for (int p = threadIdx.x; p < q->num_parts; p += kWGSize) hist[p] = 0u;
+    __syncthreads();
   } else if (STRAT == STRAT_PEMIT) {
-    // zeroed per-partition counters, then every wave's record cursor: the first record of its emit range
-    uint32_t* pl = (uint32_t*)lds_acc;
-    const int P = q->num_parts;
-    for (int p = threadIdx.x; p < P; p += kWGSize) pl[p] = 0u;
-    if (threadIdx.x < kWavesPerWG) {
-      const int64_t gwi = (q->xcd_major ? xcd_major_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x) * kWavesPerWG +
-                          threadIdx.x;
-      const int64_t tw = gwi * q->total_wtiles / ((int64_t)gridDim.x * kWavesPerWG);
-      pl[P + threadIdx.x] = q->tile_rec_base ? q->tile_rec_base[tw] : (uint32_t)(tw * (q->steps * kWave));
+    // every partition's bin empty; its range in the stream: the partition base + this workgroup's offset (part_scan),
+    // holding exactly the records the count pass counted here
+    const BinState B = bin_state(q, lds_acc);
+    const int64_t lbi = q->xcd_major ? xcd_major_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int P = q->num_parts, pv = q->pv;
+    for (int p = threadIdx.x; p < P; p += kWGSize) {
+      B.cnt[p] = 0u;
+      B.done[p] = 0u;
+      B.front[p] = 0u;
+      B.back[p] = gp(ps.hist)[lbi * P + p];
+      B.start[p] = gp(ps.base)[p < pv ? p : p + 1] + gp(ps.off)[lbi * P + p];
     }
     __syncthreads();
   }
@@ -1305,7 +1376,7 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
                 if (neg0) m = ~m;
                 if (__ballot(m != 0) != 0)
                   matched += tile_survivors<STRAT, 32, 1>(q, seg, ring + slot_off, (t - seg_first) * kWTileDocs, m,
-                                                          lane, acc.lds);
+                                                          lane, acc.lds, *acc.ps);
               } else {
                 process_tile_lm<STRAT>(q, seg, pp, t - seg_first, ring + slot_off, ring_lds + 4u * slot_off, lane, acc,
                                        matched);
@@ -1345,17 +1416,38 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
     }
   }
 
-  {
+  if (STRAT != STRAT_PEMIT) {  // (the partitioned count pass counts numDocsScanned; its emit pass sees the same docs)
     const int64_t wm = wave_sum_i64((int64_t)matched);
     if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)wm, RLX);
   }
-  if (STRAT == STRAT_PEMIT) {
+  if (STRAT == STRAT_PCOUNT) {
     __syncthreads();
-    const uint32_t* pl = (const uint32_t*)lds_acc;
-    const int P = q->num_parts;
-    for (int p = threadIdx.x; p < P; p += kWGSize) gp(q->part_hist)[(size_t)lb * P + p] = pl[p];
-    if (lane == 0)
-      gp(q->wave_cnt)[gw] = pl[P + wave] - (q->tile_rec_base ? q->tile_rec_base[t0] : (uint32_t)(t0 * (q->steps * kWave)));
+    const uint32_t* hist = (const uint32_t*)lds_acc;
+    for (int p = threadIdx.x; p < q->num_parts; p += kWGSize) gp(ps.hist)[lb * q->num_parts + p] = hist[p];
+  }
+  if (STRAT == STRAT_PEMIT) {
+    // every bin's rest (< one bin) between the range's front and back, then sentinel records up to the padded end
+    __syncthreads();
+    const BinState B = bin_state(q, lds_acc);
+    const int P = q->num_parts, pv = q->pv;
+    for (int p = threadIdx.x; p < P; p += kWGSize) {
+      const bool isv = p < pv;
+      const uint32_t nw = isv ? (uint32_t)q->rec_words_v : 1u;
+      const uint32_t BS = (uint32_t)(isv ? q->bs_v : q->bs_h);
+      const lds_u32_t* bin = isv ? lds_ptr(lds_acc + q->lds_bins_v) + (uint32_t)p * BS * nw
+                                 : lds_ptr(lds_acc + q->lds_bins_h) + (uint32_t)(p - pv) * BS;
+      AS1 uint32_t* recs = gp(isv ? ps.recs_v : ps.recs_h);
+      const uint32_t n = B.cnt[p], o = B.front[p];
+      const uint32_t h = gp(ps.hist)[lb * P + p];
+      if (n >= BS || o + n != B.back[p])  // the emit pass must see exactly the count pass's records
+        __hip_atomic_fetch_add(gp(q->matched_docs) + 3, 1ull, RLX);
+      AS1 uint32_t* d = recs + (B.start[p] + o) * (uint64_t)nw;
+      const uint32_t nn = n < BS ? n : BS;
+      for (uint32_t e = 0; e < nn * nw; ++e) d[e] = bin[e];
+      const uint32_t padded = (h + BS - 1u) / BS * BS;
+      AS1 uint32_t* z = recs + (B.start[p] + h) * (uint64_t)nw;
+      for (uint32_t e = 0; e < (padded - h) * nw; ++e) z[e] = (e % nw) == 0 ? kSentinel : 0u;
+    }
   }
   if (STRAT == STRAT_LDS) {
     __syncthreads();
@@ -1384,11 +1476,21 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
             break;
           case PA_AGG_MIN: __hip_atomic_fetch_min(gp((long long*)A.acc_i64) + k, ((const long long*)(lds_acc + A.lds_off))[k], RLX); break;
           case PA_AGG_MAX: __hip_atomic_fetch_max(gp((long long*)A.acc_i64) + k, ((const long long*)(lds_acc + A.lds_off))[k], RLX); break;
+          case PA_AGG_DISTINCTCOUNT: {  // presence words with a value seen here -> bytes of the global block
+            const uint32_t* r = (const uint32_t*)(lds_acc + A.lds_off + k * A.nvals);
+            AS1 uint8_t* g = gp(A.acc_hll) + k * A.nvals;
+            for (int64_t j = 0; j < A.nvals / 4; ++j) {
+              const uint32_t w = r[j];
+              if (w == 0) continue;
+              for (int b = 0; b < 4; ++b)
+                if ((w >> (8 * b)) & 0xffu) g[4 * j + b] = 1;
+            }
+          } break;
           case PA_AGG_DISTINCTCOUNTHLL: {
             const uint32_t* r = (const uint32_t*)(lds_acc + A.lds_off) + (k << A.log2m);
-            uint32_t* g = A.acc_hll + (k << A.log2m);
+            uint8_t* g = A.acc_hll + (k << A.log2m);
             for (int j = 0; j < (1 << A.log2m); ++j)
-              if (r[j] != 0) __hip_atomic_fetch_max(gp(g) + j, r[j], RLX);
+              if (r[j] != 0) atomic_max_u8(g + j, r[j]);
           } break;
           default: break;
         }
@@ -1543,7 +1645,7 @@ __global__ void limit_threshold_kernel(LimitDesc F, int64_t n) {
 
 __global__ void __launch_bounds__(256) limit_agg_kernel(const DevQuery* __restrict__ q, const DevSeg* __restrict__ segs,
                                                         LimitDesc F) {
-  const Acc<STRAT_GLOBAL> acc{q, nullptr};
+  const Acc<STRAT_GLOBAL> acc{q, nullptr, nullptr};
   const int nseg = q->num_segments;
   const int lane = threadIdx.x & (kWave - 1);
   for_each_doc(q, segs, [&](int si, const DevSeg* seg, int64_t doc, bool valid) {
@@ -1689,11 +1791,10 @@ __global__ void __launch_bounds__(256) compact_gather_kernel(const unsigned long
           const uint64_t* src = (const uint64_t*)d.src[si] + k * per;
           uint64_t* dst = (uint64_t*)d.dst[si] + pos * per;
           for (int64_t e = 0; e < per; ++e) dst[e] = src[e];
-        } else if (d.oes[si] == 1) {  // HLL registers (< 64): one byte each in the staging block
-          const uint32_t* src = (const uint32_t*)d.src[si] + k * per;
-          uint32_t* dst = (uint32_t*)((uint8_t*)d.dst[si] + pos * per);  // per is a power of two >= 16
-          for (int64_t e = 0; e < per; e += 4)
-            dst[e >> 2] = (src[e] & 0xffu) | (src[e + 1] & 0xffu) << 8 | (src[e + 2] & 0xffu) << 16 | src[e + 3] << 24;
+        } else if (d.es[si] == 1) {  // HLL registers, one byte each (per is a power of two >= 16)
+          const u32x4* src = (const u32x4*)((const uint8_t*)d.src[si] + k * per);
+          u32x4* dst = (u32x4*)((uint8_t*)d.dst[si] + pos * per);
+          for (int64_t e = 0; e < per / 16; ++e) dst[e] = src[e];
         } else {
           const uint32_t* src = (const uint32_t*)d.src[si] + k * per;
           uint32_t* dst = (uint32_t*)d.dst[si] + pos * per;
@@ -1719,426 +1820,239 @@ hipError_t launch_compact(const unsigned long long* count, int64_t K, int all, u
 
 
 // ---------------------------------------------------------------- partitioned aggregation: offsets + pass C
-// Block p: exclusive scan of the G workgroup counts of partition p, each rounded up to whole kPartGroup-record groups
-// (-> off[wg][p], relative to the partition); padded total -> totals[p].
-__global__ void __launch_bounds__(256) part_scan_kernel(const uint32_t* hist, uint32_t* off, int G, int P,
-                                                        uint32_t* totals) {
-  __shared__ uint32_t sh[256];
+__device__ __forceinline__ uint64_t block_exclusive_scan_256_u64(uint64_t v, uint64_t* sh, uint64_t* total) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const uint64_t add = t >= o ? sh[t - o] : 0ull;
+    __syncthreads();
+    sh[t] += add;
+    __syncthreads();
+  }
+  const uint64_t incl = sh[t];
+  if (total) *total = sh[255];
+  __syncthreads();
+  return incl - v;
+}
+
+// Block p: exclusive scan over the G workgroups of partition p's record counts, each rounded up to whole bins of the
+// partition's stream (-> off[wg][p], relative to the partition); the padded total -> the partition's base slot.
+__global__ void __launch_bounds__(256) part_scan_kernel(const uint32_t* hist, uint32_t* off, int G, int P, int pv,
+                                                        uint32_t bs_v, uint32_t bs_h, uint64_t* base) {
+  __shared__ uint64_t sh[256];
   const int p = blockIdx.x;
-  uint32_t carry = 0;
-  for (int base = 0; base < G; base += 256) {
-    const int wg = base + threadIdx.x;
-    const uint32_t x = wg < G ? (hist[(size_t)wg * P + p] + (kPartGroup - 1)) & ~(uint32_t)(kPartGroup - 1) : 0u;
-    uint32_t tot;
-    const uint32_t ex = block_exclusive_scan_256(x, sh, &tot);
-    if (wg < G) off[(size_t)wg * P + p] = carry + ex;
+  const uint32_t bs = p < pv ? bs_v : bs_h;
+  uint64_t carry = 0;
+  for (int b0 = 0; b0 < G; b0 += 256) {
+    const int wg = b0 + threadIdx.x;
+    const uint64_t x = wg < G ? (uint64_t)((hist[(size_t)wg * P + p] + bs - 1u) / bs * bs) : 0ull;
+    uint64_t tot;
+    const uint64_t ex = block_exclusive_scan_256_u64(x, sh, &tot);
+    if (wg < G) off[(size_t)wg * P + p] = (uint32_t)(carry + ex);
     carry += tot;
   }
-  if (threadIdx.x == 0) totals[p] = carry;
+  if (threadIdx.x == 0) base[p < pv ? p : p + 1] = carry;
 }
 
-// Block b moves the records workgroup b of the emit pass wrote (its waves' ranges of the emit buffer) into b's range of
-// every partition: each fill round drops bin_iter records per thread into per-partition LDS bins (bin_slots records
-// each), then every bin holding a whole group of kPartGroup records stores its whole groups with one contiguous burst
-// (one 128-B line per group for 2-word records) and keeps the rest; a record finding its bin full goes straight to
-// the partition range. At the end each bin's rest goes out padded with sentinel records (key 0xffffffff) up to the
-// range's padded size. When the bins of all P partitions do not fit LDS, the partitions are taken bin_parts at a time
-// (one read of the workgroup's records per group of partitions). Order inside a partition does not matter to the
-// aggregation (integer results are exact; a DOUBLE sum is order-dependent only in its last bits, like the atomics).
-__global__ void __launch_bounds__(kPartBinThreads) part_bin_kernel(const DevQuery* __restrict__ q) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const int P = q->num_parts;
-  const int PB = q->bin_parts;
-  const int W = q->rec_words;
-  const int BS = q->bin_slots;
-  uint32_t* binc = smem;           // [PB] records in the bin (may exceed BS while filling: the excess went out directly)
-  uint32_t* outp = smem + PB;      // [PB] next output record of this workgroup's range in the partition
-  uint32_t* bins = smem + 2 * PB;  // [PB][BS][W]
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  constexpr int kWaves = kPartBinThreads / 64;
-  // the emit ranges of the workgroup's waves
-  const int64_t Wt = (int64_t)gridDim.x * kWavesPerWG;
-  const int64_t tile_docs = (int64_t)q->steps * kWave;
-  uint32_t rs[kWavesPerWG], rn[kWavesPerWG];
-  uint32_t n_all = 0;
-#pragma unroll
-  for (int k = 0; k < kWavesPerWG; ++k) {
-    const int64_t gwi = (int64_t)b * kWavesPerWG + k;
-    const int64_t tw = gwi * q->total_wtiles / Wt;
-    rs[k] = q->tile_rec_base ? q->tile_rec_base[tw] : (uint32_t)(tw * tile_docs);
-    rn[k] = q->wave_cnt[gwi];
-    n_all += rn[k];
+// single workgroup: in-place exclusive scan of n 64-bit counts; v[n] = total
+__global__ void __launch_bounds__(256) scan_u64_kernel(uint64_t* v, int64_t n) {
+  __shared__ uint64_t sh[256];
+  uint64_t carry = 0;
+  for (int64_t b0 = 0; b0 < n; b0 += 256) {
+    const int64_t i = b0 + threadIdx.x;
+    const uint64_t x = i < n ? v[i] : 0ull;
+    uint64_t tot;
+    const uint64_t ex = block_exclusive_scan_256_u64(x, sh, &tot);
+    if (i < n) v[i] = carry + ex;
+    carry += tot;
   }
-  const AS1 uint32_t* src = gp((const uint32_t*)q->emit);
-  AS1 uint32_t* dst = gp(q->recs);
-  const int shift = q->part_shift + q->key_shift;  // record word 0 -> partition
-  const uint32_t round = (uint32_t)q->bin_iter * kPartBinThreads;
-  for (int plo = 0; plo < P; plo += PB) {
-    const int np = min(PB, P - plo);
-    for (int p = tid; p < np; p += kPartBinThreads) {
-      binc[p] = 0u;
-      outp[p] = q->part_base[plo + p] + q->part_off[(size_t)b * P + plo + p];
-    }
-    __syncthreads();
-    // round k: the records loaded during round k-1's flush are binned, then round k+1's loads are issued before this
-    // round's flush (their latency hides behind it)
-    const int iters = q->bin_iter;  // 1..4
-    uint32_t at[4], w0[4], w1[4];
-    bool ok[4];
-    auto load_round = [&](uint32_t base) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        uint32_t i = base + (uint32_t)r * kPartBinThreads + tid;
-        ok[r] = r < iters && i < n_all;
-        at[r] = 0u;
-        w0[r] = w1[r] = 0u;
-        if (!ok[r]) continue;
-        bool found = false;
-#pragma unroll
-        for (int k = 0; k < kWavesPerWG; ++k) {  // static indices only: rs / rn stay in registers
-          if (!found) {
-            if (i < rn[k]) {
-              at[r] = rs[k] + i;
-              found = true;
-            } else {
-              i -= rn[k];
-            }
-          }
-        }
-        const AS1 uint32_t* rec = src + (size_t)at[r] * (uint32_t)W;
-        if (W == 2) {
-          const uint64_t v = __builtin_nontemporal_load((const AS1 uint64_t*)rec);
-          w0[r] = (uint32_t)v;
-          w1[r] = (uint32_t)(v >> 32);
-        } else {
-          w0[r] = rec[0];
-        }
-      }
-    };
-    load_round(0);
-    for (uint32_t base = 0; base < n_all; base += round) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (!ok[r]) continue;
-        const AS1 uint32_t* rec = src + (size_t)at[r] * (uint32_t)W;
-        const uint32_t p = (w0[r] >> shift) - (uint32_t)plo;
-        if (p >= (uint32_t)np) continue;  // another group of partitions
-        const uint32_t slot = atomicAdd(binc + p, 1u);
-        if (slot < (uint32_t)BS) {
-          uint32_t* d = bins + ((size_t)p * BS + slot) * W;
-          if (W == 2) {
-            *(uint64_t*)d = ((uint64_t)w1[r] << 32) | w0[r];
-          } else {
-            d[0] = w0[r];
-            for (int e = 1; e < W; ++e) d[e] = rec[e];
-          }
-        } else {  // bin full: straight to the range
-          const uint32_t o = atomicAdd(outp + p, 1u);
-          AS1 uint32_t* d = dst + (size_t)o * (uint32_t)W;
-          if (W == 2) {
-            *(AS1 uint64_t*)d = ((uint64_t)w1[r] << 32) | w0[r];
-          } else {
-            d[0] = w0[r];
-            for (int e = 1; e < W; ++e) d[e] = rec[e];
-          }
-        }
-      }
-      __syncthreads();
-      load_round(base + round);
-      // flush whole groups: a wave takes 4 bins at a time, 16 lanes per bin (each burst is a run of whole 128-B lines)
-      const int sub = lane >> 4, sl = lane & 15;
-      for (int p0 = wave * 4; p0 < np; p0 += kWaves * 4) {
-        const int p = p0 + sub;
-        if (p < np) {
-          const uint32_t n = min(binc[p], (uint32_t)BS);
-          const uint32_t g = n & ~(uint32_t)(kPartGroup - 1);
-          if (g != 0) {
-            const uint32_t o = outp[p];  // only these 16 lanes touch bin p in this phase
-            uint32_t* bsrc = bins + (size_t)p * BS * W;
-            AS1 uint32_t* d = dst + (size_t)o * (uint32_t)W;
-            if (W == 2) {
-              for (uint32_t e = sl; e < g; e += 16) ((AS1 uint64_t*)d)[e] = ((const uint64_t*)bsrc)[e];
-            } else {
-              for (uint32_t e = sl; e < g * W; e += 16) d[e] = bsrc[e];
-            }
-            // the rest (< kPartGroup records) to the front of the bin: source [g, n) and target [0, n - g) are disjoint
-            for (uint32_t e = sl; e < (n - g) * W; e += 16) bsrc[e] = bsrc[g * W + e];
-            if (sl == 0) outp[p] = o + g;
-          }
-          if (sl == 0) binc[p] = n - g;
-        }
-      }
-      __syncthreads();
-    }
-    // the rest of every bin, padded with sentinels up to the end of the range (16 lanes per bin)
-    {
-      const int sub = lane >> 4, sl = lane & 15;
-      for (int p0 = wave * 4; p0 < np; p0 += kWaves * 4) {
-        const int p = p0 + sub;
-        if (p >= np) continue;
-        const uint32_t n = binc[p];
-        const uint32_t o = outp[p];
-        const uint32_t h = q->part_hist[(size_t)b * P + plo + p];
-        const uint32_t pad = ((h + (kPartGroup - 1)) & ~(uint32_t)(kPartGroup - 1)) - h;
-        const uint32_t* bsrc = bins + (size_t)p * BS * W;
-        AS1 uint32_t* d = dst + (size_t)o * (uint32_t)W;
-        for (uint32_t e = sl; e < (n + pad) * W; e += 16) d[e] = e < n * W ? bsrc[e] : (e % W == 0 ? 0xffffffffu : 0u);
-      }
-    }
-    __syncthreads();
-  }
+  if (threadIdx.x == 0) v[n] = carry;
 }
 
-// Pass C, block p: aggregate the records of partition p (keys [p << shift, (p+1) << shift)) in LDS, then add the
-// partition's non-empty keys into the global accumulators (this block owns those keys: plain read-modify-write).
+// Pass C. One workgroup per partition: V partitions aggregate COUNT/SUM/MIN/MAX of their key range in LDS, H
+// partitions the u8 HLL registers (and COUNT from first-value flags when there is no V stream); either way the
+// workgroup owns its keys and stores every accumulator of its range (empty keys get the identities), so no global
+// atomics and no read of the accumulators.
 constexpr int kPartAggThreads = 512;
-__global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuery* __restrict__ q) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  unsigned char* lds = (unsigned char*)smem;
-  const int p = blockIdx.x;
-  const int64_t KR = int64_t(1) << q->part_shift;
-  const int64_t kbase = (int64_t)p << q->part_shift;
+
+// one aggregation update of local key lk with the value bits iv (int64, or double bits)
+__device__ __forceinline__ void part_apply(const DevAgg& A, unsigned char* lds, int64_t lk, int64_t iv) {
+  if (A.type == PA_AGG_SUM) {
+    if (A.src == SRC_INT) {
+      atomicAdd((unsigned long long*)(lds + A.lds_off) + lk, (unsigned long long)iv);
+    } else if (A.src == SRC_LONG) {
+      atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk, (unsigned long long)(uint32_t)iv);
+      atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk + 1, (unsigned long long)(iv >> 32));
+    } else {
+      atomicAdd((double*)(lds + A.lds_off) + lk, __builtin_bit_cast(double, iv));
+    }
+  } else {
+    const int64_t e = A.src != SRC_DOUBLE ? iv : f64_order_encode(__builtin_bit_cast(double, iv));
+    if (A.type == PA_AGG_MIN) atomicMin((long long*)(lds + A.lds_off) + lk, (long long)e);
+    else atomicMax((long long*)(lds + A.lds_off) + lk, (long long)e);
+  }
+}
+
+__device__ void part_agg_v(const DevQuery* __restrict__ q, const PartScratch& ps, int p, unsigned char* lds) {
+  const int ks = q->kshift_v;
+  const int64_t KR = int64_t(1) << ks;
+  const int64_t kbase = (int64_t)p << ks;
   const int64_t nk = min(KR, q->num_keys - kbase);
   uint32_t* cnt = (uint32_t*)lds;
   for (int64_t k = threadIdx.x; k < KR; k += kPartAggThreads) cnt[k] = 0;
   for (int a = 0; a < q->num_aggs; ++a) {
     const DevAgg& A = q->aggs[a];
-    if (A.type == PA_AGG_COUNT) continue;
-    if (A.type == PA_AGG_DISTINCTCOUNTHLL) {  // one byte per register
-      uint32_t* r = (uint32_t*)(lds + A.lds_off);
-      for (int64_t k = threadIdx.x; k < (KR << A.log2m) / 4; k += kPartAggThreads) r[k] = 0u;
-      continue;
-    }
+    if (A.type == PA_AGG_COUNT || A.type == PA_AGG_DISTINCTCOUNTHLL) continue;  // (HLL: the H partitions)
     int64_t* r = (int64_t*)(lds + A.lds_off);
     const int64_t init = A.type == PA_AGG_MIN ? INT64_MAX : (A.type == PA_AGG_MAX ? INT64_MIN : 0);
     const int64_t n = (A.type == PA_AGG_SUM && A.src == SRC_LONG) ? 2 * KR : KR;
     for (int64_t k = threadIdx.x; k < n; k += kPartAggThreads) r[k] = init;
   }
   __syncthreads();
-  const uint32_t r0 = q->part_base[p], r1 = q->part_base[p + 1];
-  const int W = q->rec_words;
-  const int ks = q->key_shift;
-  uint32_t rstart = r0;
-  if (W == 2 && ks == 0) {
-    // (key, int32 value) records, 8 per thread in flight: every load first, then the LDS updates
-    constexpr int kB = 8;
-    int va = -1;
-    for (int a = 0; a < q->num_aggs && va < 0; ++a)
-      if (q->aggs[a].type != PA_AGG_COUNT) va = a;
-    const uint32_t span = kB * kPartAggThreads;
-    uint32_t base = r0;
-    for (; base + span <= r1; base += span) {
-      uint64_t v[kB];
+  const uint64_t r0 = gp(ps.base)[p], r1 = gp(ps.base)[p + 1];
+  const int W = q->rec_words_v;
+  const int fmt = q->v_fmt;
+  const uint32_t kmask = (uint32_t)(KR - 1);
+  const AS1 uint32_t* recs = gp((const uint32_t*)ps.recs_v);
+  const AS1 uint64_t* vdict = gp(q->vdict);
+  // 8 records per thread in flight: every load of the batch first, then the LDS updates
+  constexpr int kB = 8;
+  const uint64_t span = (uint64_t)kB * kPartAggThreads;
+  for (uint64_t b0 = r0; b0 < r1; b0 += span) {
+    uint32_t w0[kB], w1[kB], w2[kB];
 #pragma unroll
-      for (int j = 0; j < kB; ++j) v[j] = __builtin_nontemporal_load(gp((const uint64_t*)q->recs) + base + j * kPartAggThreads + threadIdx.x);
+    for (int j = 0; j < kB; ++j) {
+      const uint64_t ri = b0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
+      w0[j] = kSentinel;
+      w1[j] = w2[j] = 0u;
+      if (ri < r1) {
+        const AS1 uint32_t* rec = recs + ri * (uint64_t)W;
+        w0[j] = __builtin_nontemporal_load(rec);
+        if (fmt == V_FMT_32 || fmt == V_FMT_64) w1[j] = __builtin_nontemporal_load(rec + 1);
+        if (fmt == V_FMT_64) w2[j] = __builtin_nontemporal_load(rec + 2);
+      }
+    }
+    int64_t iv[kB];
 #pragma unroll
-      for (int j = 0; j < kB; ++j) {
-        const uint32_t key = (uint32_t)v[j];
-        if (key == 0xffffffffu) continue;  // range padding (part_bin_kernel)
-        const int64_t lk = (int64_t)key - kbase;
-        atomicAdd(cnt + lk, 1u);
-        const int64_t iv = (int64_t)(int32_t)(uint32_t)(v[j] >> 32);
-        for (int a = va < 0 ? 0 : va; a < q->num_aggs; ++a) {
+    for (int j = 0; j < kB; ++j) {  // V_FMT_ID: the table-wide value of the record's value id (L2-resident dictionary)
+      iv[j] = 0;
+      if (w0[j] == kSentinel) continue;
+      if (fmt == V_FMT_ID) iv[j] = (int64_t)vdict[w0[j] >> ks];
+      else if (fmt == V_FMT_32) iv[j] = (int64_t)(int32_t)w1[j];
+      else if (fmt == V_FMT_64) iv[j] = (int64_t)(((uint64_t)w2[j] << 32) | w1[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      if (w0[j] == kSentinel) continue;
+      const int64_t lk = (int64_t)(w0[j] & kmask);
+      atomicAdd(cnt + lk, 1u);
+      if (fmt == V_FMT_KEY) continue;
+      if (fmt == V_FMT_GEN) {
+        const uint64_t ri = b0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
+        const AS1 uint32_t* rec = recs + ri * (uint64_t)W;
+        for (int a = 0; a < q->num_aggs; ++a) {
           const DevAgg& A = q->aggs[a];
-          if (A.type == PA_AGG_COUNT) continue;
-          if (A.type == PA_AGG_SUM) {
-            if (A.src == SRC_LONG) {
-              atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk, (unsigned long long)(uint32_t)iv);
-              atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk + 1, (unsigned long long)(iv >> 32));
-            } else {
-              atomicAdd((unsigned long long*)(lds + A.lds_off) + lk, (unsigned long long)iv);
-            }
-          } else if (A.type == PA_AGG_MIN) {
-            atomicMin((long long*)(lds + A.lds_off) + lk, (long long)iv);
-          } else {
-            atomicMax((long long*)(lds + A.lds_off) + lk, (long long)iv);
-          }
+          if (A.type == PA_AGG_COUNT || A.type == PA_AGG_DISTINCTCOUNTHLL) continue;
+          const int64_t v = A.src == SRC_INT ? (int64_t)(int32_t)rec[A.pay_off]
+                                             : (int64_t)(((uint64_t)rec[A.pay_off + 1] << 32) | rec[A.pay_off]);
+          part_apply(A, lds, lk, v);
         }
-      }
-    }
-    rstart = base;
-  }
-  // one aggregation update of local key lk with the record's value bits iv
-  auto apply = [&](const DevAgg& A, int64_t lk, int64_t iv) {
-    if (A.type == PA_AGG_SUM) {
-      if (A.src == SRC_INT) {
-        atomicAdd((unsigned long long*)(lds + A.lds_off) + lk, (unsigned long long)iv);
-      } else if (A.src == SRC_LONG) {
-        atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk, (unsigned long long)(uint32_t)iv);
-        atomicAdd((unsigned long long*)(lds + A.lds_off) + 2 * lk + 1, (unsigned long long)(iv >> 32));
       } else {
-        atomicAdd((double*)(lds + A.lds_off) + lk, __builtin_bit_cast(double, iv));
-      }
-    } else {
-      const int64_t e = A.src != SRC_DOUBLE ? iv : f64_order_encode(__builtin_bit_cast(double, iv));
-      if (A.type == PA_AGG_MIN) atomicMin((long long*)(lds + A.lds_off) + lk, (long long)e);
-      else atomicMax((long long*)(lds + A.lds_off) + lk, (long long)e);
-    }
-  };
-  // one record (index ri, word 0 already loaded)
-  auto proc = [&](uint32_t ri, uint32_t w0) {
-    if (w0 == 0xffffffffu) return;  // range padding (part_bin_kernel; never a valid record: its rank field is 31)
-    const AS1 uint32_t* rec = gp(q->recs) + (size_t)ri * (uint32_t)W;
-    const int64_t lk = (int64_t)(w0 >> ks) - kbase;
-    if (ks != 0) {  // DISTINCTCOUNTHLL(MV) record: register max of one value, the rest on the doc's first record only
-      const DevAgg& H = q->aggs[q->hll_agg];
-      const uint32_t rank = (w0 >> 1) & 31u;
-      if (rank != 0) {
-        const uint32_t idx = ((uint32_t)lk << H.log2m) | ((w0 >> 6) & ((1u << H.log2m) - 1u));
-        uint32_t* wp = (uint32_t*)(lds + H.lds_off) + (idx >> 2);
-        const uint32_t sh = (idx & 3u) * 8u;
-        uint32_t old = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        while (((old >> sh) & 0xffu) < rank) {  // byte max by compare-and-swap (rarely more than one try)
-          const uint32_t nw = (old & ~(0xffu << sh)) | (rank << sh);
-          const uint32_t prev = atomicCAS(wp, old, nw);
-          if (prev == old) break;
-          old = prev;
+        for (int a = 0; a < q->num_aggs; ++a) {
+          const DevAgg& A = q->aggs[a];
+          if (A.type == PA_AGG_COUNT || A.type == PA_AGG_DISTINCTCOUNTHLL) continue;
+          part_apply(A, lds, lk, iv[j]);
         }
       }
-      if ((w0 & 1u) == 0) return;
     }
-    atomicAdd(cnt + lk, 1u);
+  }
+  __syncthreads();
+  // this workgroup owns keys [kbase, kbase + nk): plain stores of every accumulator
+  for (int64_t lk = threadIdx.x; lk < nk; lk += kPartAggThreads) {
+    const int64_t k = kbase + lk;
+    gp(q->count)[k] = cnt[lk];
     for (int a = 0; a < q->num_aggs; ++a) {
       const DevAgg& A = q->aggs[a];
       if (A.type == PA_AGG_COUNT || A.type == PA_AGG_DISTINCTCOUNTHLL) continue;
-      int64_t iv;
-      if (A.src == SRC_INT) iv = (int64_t)(int32_t)rec[A.pay_off];
-      else iv = (int64_t)(((uint64_t)rec[A.pay_off + 1] << 32) | rec[A.pay_off]);
-      apply(A, lk, iv);
-    }
-  };
-  // (key, one 64-bit value) records: exactly one non-COUNT aggregation, of a LONG / DOUBLE value at word 1
-  int va = -1, nva = 0;
-  for (int a = 0; a < q->num_aggs; ++a)
-    if (q->aggs[a].type != PA_AGG_COUNT) {
-      va = a;
-      ++nva;
-    }
-  if (W == 3 && ks == 0 && nva == 1 && q->aggs[va].src != SRC_INT && q->aggs[va].pay_off == 1) {
-    // 8 records per thread in flight, then the LDS updates
-    constexpr int kB = 8;
-    const uint32_t span = kB * kPartAggThreads;
-    uint32_t base = r0;
-    for (; base + span <= r1; base += span) {
-      uint32_t k[kB], lo[kB], hi[kB];
-#pragma unroll
-      for (int j = 0; j < kB; ++j) {
-        const AS1 uint32_t* rec = gp(q->recs) + (size_t)(base + j * kPartAggThreads + threadIdx.x) * 3u;
-        k[j] = __builtin_nontemporal_load(rec);
-        lo[j] = __builtin_nontemporal_load(rec + 1);
-        hi[j] = __builtin_nontemporal_load(rec + 2);
-      }
-#pragma unroll
-      for (int j = 0; j < kB; ++j) {
-        if (k[j] == 0xffffffffu) continue;  // range padding (part_bin_kernel)
-        const int64_t lk = (int64_t)k[j] - kbase;
-        atomicAdd(cnt + lk, 1u);
-        apply(q->aggs[va], lk, (int64_t)(((uint64_t)hi[j] << 32) | lo[j]));
+      const int64_t* r = (const int64_t*)(lds + A.lds_off);
+      if (A.type == PA_AGG_SUM && A.src == SRC_LONG) {
+        gp(A.acc_i64)[2 * k] = r[2 * lk];
+        gp(A.acc_i64)[2 * k + 1] = r[2 * lk + 1];
+      } else {
+        gp(A.acc_i64)[k] = r[lk];  // SUM(int) / SUM(double) bits / MIN / MAX
       }
     }
-    rstart = base;
   }
-  if (ks != 0) {
-    // DISTINCTCOUNTHLL(MV) records: word 0 of 8 records per thread in flight, then their register updates
-    constexpr int kB = 8;
-    const uint32_t span = kB * kPartAggThreads;
-    uint32_t base = r0;
-    for (; base + span <= r1; base += span) {
-      uint32_t w[kB];
-#pragma unroll
-      for (int j = 0; j < kB; ++j)
-        w[j] = __builtin_nontemporal_load(gp(q->recs) + (size_t)(base + j * kPartAggThreads + threadIdx.x) * (uint32_t)W);
-#pragma unroll
-      for (int j = 0; j < kB; ++j) proc(base + j * kPartAggThreads + threadIdx.x, w[j]);
-    }
-    rstart = base;
-  }
-  for (uint32_t ri = rstart + threadIdx.x; ri < r1; ri += kPartAggThreads) proc(ri, gp(q->recs)[(size_t)ri * (uint32_t)W]);
+}
+
+__device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps, int ph, unsigned char* lds) {
+  const DevAgg& H = q->aggs[q->hll_agg];
+  const int lg = H.log2m;
+  const int ks = q->kshift_h;
+  const int64_t KR = int64_t(1) << ks;
+  const int64_t kbase = (int64_t)ph << ks;
+  const int64_t nk = min(KR, q->num_keys - kbase);
+  const bool first = q->h_first != 0;
+  uint32_t* regw = (uint32_t*)lds;                      // KR << lg one-byte registers, as words
+  uint32_t* cnt = (uint32_t*)(lds + ((size_t)KR << lg));  // first-value counts (h_first)
+  for (int64_t k = threadIdx.x; k < (KR << lg) / 4; k += kPartAggThreads) regw[k] = 0u;
+  if (first)
+    for (int64_t k = threadIdx.x; k < KR; k += kPartAggThreads) cnt[k] = 0u;
   __syncthreads();
-  for (int64_t lk = threadIdx.x; lk < nk; lk += kPartAggThreads) {
-    const uint32_t c = cnt[lk];
-    if (c == 0) continue;
-    const int64_t k = kbase + lk;
-    gp(q->count)[k] += c;
-    for (int a = 0; a < q->num_aggs; ++a) {
-      const DevAgg& A = q->aggs[a];
-      switch (A.type) {
-        case PA_AGG_SUM:
-          if (A.src == SRC_INT) {
-            gp(A.acc_i64)[k] += ((const int64_t*)(lds + A.lds_off))[lk];
-          } else if (A.src == SRC_LONG) {
-            gp(A.acc_i64)[2 * k] += ((const int64_t*)(lds + A.lds_off))[2 * lk];
-            gp(A.acc_i64)[2 * k + 1] += ((const int64_t*)(lds + A.lds_off))[2 * lk + 1];
-          } else {
-            gp(A.acc_f64)[k] += ((const double*)(lds + A.lds_off))[lk];
-          }
-          break;
-        case PA_AGG_MIN: {
-          const int64_t v = ((const int64_t*)(lds + A.lds_off))[lk];
-          if (v < gp(A.acc_i64)[k]) gp(A.acc_i64)[k] = v;
-        } break;
-        case PA_AGG_MAX: {
-          const int64_t v = ((const int64_t*)(lds + A.lds_off))[lk];
-          if (v > gp(A.acc_i64)[k]) gp(A.acc_i64)[k] = v;
-        } break;
-        default: break;
+  const int pv = q->pv;
+  const uint64_t r0 = gp(ps.base)[pv + 1 + ph], r1 = gp(ps.base)[pv + 2 + ph];
+  const AS1 uint32_t* recs = gp((const uint32_t*)ps.recs_h);
+  const uint32_t rmask = (1u << lg) - 1u;
+  constexpr int kB = 8;
+  const uint64_t span = (uint64_t)kB * kPartAggThreads;
+  for (uint64_t b0 = r0; b0 < r1; b0 += span) {
+    uint32_t w[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const uint64_t ri = b0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
+      w[j] = ri < r1 ? __builtin_nontemporal_load(recs + ri) : kSentinel;
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      if (w[j] == kSentinel) continue;  // (never a valid record: its rank field would be 31)
+      const uint32_t lk = w[j] >> (lg + 6);
+      const uint32_t rank = (w[j] >> 1) & 31u;
+      if (rank != 0) {
+        const uint32_t idx = (lk << lg) | ((w[j] >> 6) & rmask);
+        uint32_t* wp = regw + (idx >> 2);
+        const uint32_t sh = (idx & 3u) * 8u;
+        uint32_t old = __hip_atomic_load(wp, WG_RLX);
+        while (((old >> sh) & 0xffu) < rank) {  // byte max by compare-and-swap (rarely more than one try)
+          const uint32_t nw = (old & ~(0xffu << sh)) | (rank << sh);
+          if (__hip_atomic_compare_exchange_strong(wp, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP))
+            break;
+        }
       }
+      if (first && (w[j] & 1u)) atomicAdd(cnt + lk, 1u);
     }
   }
-  if (q->hll_agg >= 0) {  // the partition's registers (bytes) into the u32 global registers it owns
-    const DevAgg& H = q->aggs[q->hll_agg];
-    const unsigned char* reg = lds + H.lds_off;
-    const int64_t n = nk << H.log2m;
-    for (int64_t i = threadIdx.x; i < n; i += kPartAggThreads) {
-      const uint32_t v = reg[i];
-      if (v == 0) continue;
-      AS1 uint32_t* g = gp(H.acc_hll) + ((kbase << H.log2m) + i);
-      if (v > *g) *g = v;
-    }
-  }
+  __syncthreads();
+  // the partition's registers (16-byte stores: 2^lg >= 16 bytes per key) and, without a V stream, its counts
+  AS1 u32x4* g = (AS1 u32x4*)(H.acc_hll + ((size_t)kbase << lg));
+  const u32x4* l = (const u32x4*)lds;
+  for (int64_t i = threadIdx.x; i < (nk << lg) / 16; i += kPartAggThreads) g[i] = l[i];
+  if (first)
+    for (int64_t lk = threadIdx.x; lk < nk; lk += kPartAggThreads) gp(q->count)[kbase + lk] = cnt[lk];
 }
 
-// Records of every wave tile of one segment for the emit pass with a partitioned DISTINCTCOUNTHLL(MV): max(1, values)
-// per doc of a multi-value column (mv_off), one per doc otherwise.
-__global__ void tile_records_kernel(const int32_t* mv_off, int32_t num_docs, int32_t tile_docs, int32_t ntiles,
-                                    uint32_t* out) {
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += gridDim.x * blockDim.x) {
-    const int32_t d0 = t * tile_docs, d1 = min(num_docs, d0 + tile_docs);
-    uint32_t n = 0;
-    if (mv_off == nullptr) {
-      n = d1 > d0 ? (uint32_t)(d1 - d0) : 0u;
-    } else {
-      for (int32_t d = d0; d < d1; ++d) n += (uint32_t)max(1, mv_off[d + 1] - mv_off[d]);
-    }
-    out[t] = n;
-  }
+__global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuery* __restrict__ q, PartScratch ps) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  if ((int)blockIdx.x < q->pv) part_agg_v(q, ps, (int)blockIdx.x, (unsigned char*)smem);
+  else part_agg_h(q, ps, (int)blockIdx.x - q->pv, (unsigned char*)smem);
 }
 
-hipError_t launch_tile_records(const int32_t* mv_off, int32_t num_docs, int32_t tile_docs, int32_t ntiles,
-                               uint32_t* out, hipStream_t s) {
-  if (ntiles > 0) tile_records_kernel<<<(ntiles + 255) / 256, 256, 0, s>>>(mv_off, num_docs, tile_docs, ntiles, out);
-  return hipGetLastError();
-}
-
-hipError_t launch_exclusive_scan_u32(uint32_t* v, int64_t n, hipStream_t s) {
-  compact_scan_kernel<<<1, 256, 0, s>>>(v, n);
-  return hipGetLastError();
-}
-
-hipError_t launch_part_offsets(const uint32_t* hist, uint32_t* off, int G, int P, uint32_t* part_base, hipStream_t s) {
-  part_scan_kernel<<<P, 256, 0, s>>>(hist, off, G, P, part_base);
-  compact_scan_kernel<<<1, 256, 0, s>>>(part_base, P);
-  return hipGetLastError();
-}
-
-hipError_t set_part_bin_lds_limit(int lds_bytes) {
-  return hipFuncSetAttribute((const void*)part_bin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-}
-
-hipError_t launch_part_bin(const DevQuery* q, int G, int lds_bytes, hipStream_t s) {
-  part_bin_kernel<<<G, kPartBinThreads, (size_t)lds_bytes, s>>>(q);
+hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G, hipStream_t s) {
+  const int P = hq->num_parts, pv = hq->pv;
+  part_scan_kernel<<<P, 256, 0, s>>>(ps.hist, ps.off, G, P, pv, (uint32_t)hq->bs_v, (uint32_t)hq->bs_h, ps.base);
+  if (pv > 0) scan_u64_kernel<<<1, 256, 0, s>>>(ps.base, pv);
+  if (P > pv) scan_u64_kernel<<<1, 256, 0, s>>>(ps.base + pv + 1, P - pv);
   return hipGetLastError();
 }
 
@@ -2146,8 +2060,8 @@ hipError_t set_part_agg_lds_limit(int lds_bytes) {
   return hipFuncSetAttribute((const void*)part_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
 }
 
-hipError_t launch_part_agg(const DevQuery* q, int P, int lds_bytes, hipStream_t s) {
-  part_agg_kernel<<<P, kPartAggThreads, (size_t)lds_bytes, s>>>(q);
+hipError_t launch_part_agg(const DevQuery* q, const PartScratch& ps, int P, int lds_bytes, hipStream_t s) {
+  part_agg_kernel<<<P, kPartAggThreads, (size_t)lds_bytes, s>>>(q, ps);
   return hipGetLastError();
 }
 
@@ -2196,7 +2110,8 @@ static const void* scan_fn_s(int steps, int lm) {
 static const void* scan_fn(int strategy, int steps, int lm) {
   switch (strategy) {
     case STRAT_LDS: return scan_fn_s<STRAT_LDS>(steps, lm);
-    case STRAT_PEMIT: return (const void*)scan_kernel<STRAT_PEMIT, 16, 0>;  // the planner's only emit layout
+    case STRAT_PEMIT: return (const void*)scan_kernel<STRAT_PEMIT, 16, 0>;    // the planner's only partitioned layout
+    case STRAT_PCOUNT: return (const void*)scan_kernel<STRAT_PCOUNT, 16, 0>;
     default: return scan_fn_s<STRAT_GLOBAL>(steps, lm);
   }
 }
@@ -2211,8 +2126,9 @@ hipError_t scan_occupancy(int strategy, int steps, int lm, int lds_bytes, int* b
 }
 
 hipError_t launch_scan(int strategy, int steps, int lm, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs,
-                       const LmSegPlan* plans, hipStream_t s) {
-  void* args[] = {(void*)&q, (void*)&segs, (void*)&plans};
+                       const LmSegPlan* plans, const PartScratch& ps, hipStream_t s) {
+  PartScratch pcopy = ps;
+  void* args[] = {(void*)&q, (void*)&segs, (void*)&plans, (void*)&pcopy};
   return hipLaunchKernel(scan_fn(strategy, steps, lm), dim3(grid), dim3(kWGSize), args, (size_t)lds_bytes, s);
 }
 

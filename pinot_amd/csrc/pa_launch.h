@@ -9,8 +9,7 @@ namespace pa {
 constexpr int kMaxCompactSections = PA_MAX_AGGS + 2;
 struct CompactDesc {
   int32_t nsec;
-  int32_t es[kMaxCompactSections];   // source element bytes (8, or 4 = HLL registers)
-  int32_t oes[kMaxCompactSections];  // output element bytes (es, or 1: HLL registers narrowed to bytes)
+  int32_t es[kMaxCompactSections];   // element bytes (8, or 1 = HLL registers)
   int64_t per[kMaxCompactSections];
   const void* src[kMaxCompactSections];
   void* dst[kMaxCompactSections];
@@ -45,16 +44,12 @@ hipError_t launch_hll_lut_hashes(const int32_t* hashes, int32_t card, int32_t lo
 hipError_t launch_fill_i64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
 hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t* keys, int64_t n, void* out,
                          hipStream_t s);
-hipError_t launch_part_offsets(const uint32_t* hist, uint32_t* off, int G, int P, uint32_t* part_base, hipStream_t s);
-hipError_t set_part_bin_lds_limit(int lds_bytes);
-hipError_t launch_tile_records(const int32_t* mv_off, int32_t num_docs, int32_t tile_docs, int32_t ntiles,
-                               uint32_t* out, hipStream_t s);
-hipError_t launch_exclusive_scan_u32(uint32_t* v, int64_t n, hipStream_t s);
-hipError_t launch_part_bin(const DevQuery* q, int G, int lds_bytes, hipStream_t s);
+// partitioned aggregation: per-(workgroup, partition) range offsets + partition bases (after the count pass)
+hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G, hipStream_t s);
 hipError_t set_part_agg_lds_limit(int lds_bytes);
-hipError_t launch_part_agg(const DevQuery* q, int P, int lds_bytes, hipStream_t s);
+hipError_t launch_part_agg(const DevQuery* q, const PartScratch& ps, int P, int lds_bytes, hipStream_t s);
 hipError_t set_scan_lds_limit(int strategy, int steps, int lm, int bytes);
 hipError_t scan_occupancy(int strategy, int steps, int lm, int lds_bytes, int* blocks_per_cu);
 hipError_t launch_scan(int strategy, int steps, int lm, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs,
-                       const LmSegPlan* plans, hipStream_t s);
+                       const LmSegPlan* plans, const PartScratch& ps, hipStream_t s);
 }  // namespace pa

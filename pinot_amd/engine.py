@@ -104,6 +104,13 @@ class AvgPair:
 
 
 @dataclass
+class MinMaxRangePair:
+    """MinMaxRangeAggregationFunction intermediate result (MinMaxRangePair: min, max; empty = (+inf, -inf))."""
+    min: float
+    max: float
+
+
+@dataclass
 class IntermediateResult:
     """What the server returns for the segment set (AggregationResultsBlock / GroupByResultsBlock contents)."""
     aggregations: List[Q.Aggregation]
@@ -132,15 +139,19 @@ def _flatten_filter(f, leaves, ops):
 
 class GpuQueryExecutor:
     def __init__(self, query: Q.Query, gpu_segments: List[GpuSegment], flags=0, enforce_num_groups_limit=True,
-                 table_dicts=None, wide_sum_columns=()):
+                 table_dicts=None, wide_sum_columns=(), value_dicts=None):
         """table_dicts: optional {group-by column: sorted unique values} — the table-wide dictionary every rank of a
         multi-GPU query must share so that key ids address the same accumulator rows everywhere
         (parallel.table_layout builds it); by default it is the union of these segments' dictionaries.
         wide_sum_columns: columns whose SUM keeps the 64-bit (PA_AGGF_WIDE_SUM) accumulator layout even if these
-        segments' values all fit int32 — agreed across ranks by parallel.table_layout."""
+        segments' values all fit int32 — agreed across ranks by parallel.table_layout.
+        value_dicts: optional {DISTINCTCOUNT column: sorted unique values} — the table-wide value dictionary whose ids
+        the presence bytes index (every rank of a multi-GPU query must share it); by default the union of these
+        segments' dictionaries."""
         if not gpu_segments:
             raise ValueError("no segments")
         self.table_dicts = table_dicts or {}
+        self.table_value_dicts = value_dicts or {}
         self.wide_sum_columns = set(wide_sum_columns or ())
         self.query = query
         self.gsegs = gpu_segments
@@ -187,18 +198,38 @@ class GpuQueryExecutor:
                 self.agg_map.append(acc_index((L.PA_AGG_MAX, ids[a.column], 0)))
             elif fn in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV"):
                 self.agg_map.append(acc_index((L.PA_AGG_DISTINCTCOUNTHLL, ids[a.column], a.log2m)))
+            elif fn in ("MINMAXRANGE", "MINMAXRANGEMV"):
+                # MinMaxRangePair(min, max): the MIN and MAX accumulators of the column
+                self.agg_map.append((acc_index((L.PA_AGG_MIN, ids[a.column], 0)),
+                                     acc_index((L.PA_AGG_MAX, ids[a.column], 0))))
+            elif fn in ("DISTINCTCOUNT", "DISTINCTCOUNTMV"):
+                if not all(sg.column(a.column).has_dictionary for sg in self.segs):
+                    raise UnsupportedQuery("DISTINCTCOUNT on a raw (no-dictionary) column %s" % a.column)
+                self.agg_map.append(acc_index((L.PA_AGG_DISTINCTCOUNT, ids[a.column], 0)))
             else:
                 raise UnsupportedQuery("aggregation %s" % fn)
         if len(self.pa_aggs) > L.PA_MAX_AGGS:
             raise UnsupportedQuery("too many aggregations")
         spec.num_aggs = len(self.pa_aggs)
         names = {cid: name for name, cid in ids.items()}
+        # DISTINCTCOUNT: the table-wide value dictionary of the column (presence byte j <=> value value_dicts[j])
+        self.value_dicts = {}
         for i, (t, cid, log2m) in enumerate(self.pa_aggs):
             spec.aggs[i].type = t
             spec.aggs[i].column_id = max(cid, 0)
             spec.aggs[i].log2m = log2m
             if t == L.PA_AGG_SUM and names.get(cid) in self.wide_sum_columns:
                 spec.aggs[i].flags = L.PA_AGGF_WIDE_SUM
+            if t == L.PA_AGG_DISTINCTCOUNT:
+                name = names[cid]
+                if name in self.table_value_dicts:
+                    vd = np.asarray(self.table_value_dicts[name])
+                else:
+                    ds = [sg.column(name).dictionary for sg in self.segs]
+                    same = all(d is ds[0] or (len(d) == len(ds[0]) and np.array_equal(d, ds[0])) for d in ds)
+                    vd = ds[0] if same else np.unique(np.concatenate(ds))
+                self.value_dicts[i] = vd
+                spec.aggs[i].num_values = len(vd)
 
         # filter
         filt = P.expand_raw_in(q.filter, seg0) if q.filter is not None else None
@@ -303,6 +334,15 @@ class GpuQueryExecutor:
                     self._keep.append(rm)
                     rms[j] = rm.ctypes.data
             L.check(lib.pa_query_bind_segment(self.handle, si, g.handle, arr, rms), "pa_query_bind_segment")
+            for i, vd in self.value_dicts.items():
+                d = self.segs[si].column(names[self.pa_aggs[i][1]]).dictionary
+                if d is vd or (len(d) == len(vd) and np.array_equal(d, vd)):
+                    continue
+                if not np.isin(d, vd).all():
+                    raise ValueError("DISTINCTCOUNT value dictionary misses values of a bound segment")
+                rm = np.searchsorted(vd, d).astype(np.int32)
+                self._keep.append(rm)
+                L.check(lib.pa_query_bind_value_remap(self.handle, si, i, rm.ctypes.data), "pa_query_bind_value_remap")
         L.check(lib.pa_query_prepare(self.handle), "pa_query_prepare")
         self.num_keys = int(lib.pa_query_num_keys(self.handle))
         hashed, shifts = ctypes.c_int32(), (ctypes.c_int32 * max(1, len(q.group_by)))()
@@ -363,7 +403,12 @@ class GpuQueryExecutor:
             counts = np.empty(cap, dtype=np.int64)
             outs, ptrs = [], (ctypes.c_void_p * max(1, len(self.pa_aggs)))()
             for i, (t, _, log2m) in enumerate(self.pa_aggs):
-                o = np.empty(cap << log2m, dtype=np.uint8) if t == L.PA_AGG_DISTINCTCOUNTHLL else np.empty(cap, np.float64)
+                if t == L.PA_AGG_DISTINCTCOUNTHLL:
+                    o = np.empty(cap << log2m, dtype=np.uint8)
+                elif t == L.PA_AGG_DISTINCTCOUNT:
+                    o = np.empty(cap * self._presence_stride(i), dtype=np.uint8)
+                else:
+                    o = np.empty(cap, np.float64)
                 outs.append(o)
                 ptrs[i] = o.ctypes.data
             n = L.check(lib.pa_query_fetch(self.handle, stream, cap, keys.ctypes.data, counts.ctypes.data, ptrs),
@@ -371,9 +416,14 @@ class GpuQueryExecutor:
             if n <= cap:
                 break
             cap = n
-        outs = [o[: n << self.pa_aggs[i][2]] if self.pa_aggs[i][0] == L.PA_AGG_DISTINCTCOUNTHLL else o[:n]
+        outs = [o[: n << self.pa_aggs[i][2]] if self.pa_aggs[i][0] == L.PA_AGG_DISTINCTCOUNTHLL else
+                (o[: n * self._presence_stride(i)] if self.pa_aggs[i][0] == L.PA_AGG_DISTINCTCOUNT else o[:n])
                 for i, o in enumerate(outs)]
         return keys[:n], counts[:n], outs
+
+    def _presence_stride(self, i):
+        """DISTINCTCOUNT presence bytes per group: the value count rounded up to 16 (PA_ACC_PRESENCE_U8)."""
+        return (len(self.value_dicts[i]) + 15) & ~15
 
     def key_values(self, keys):
         """Keys -> one value array per group-by column (DictionaryBasedGroupKeyGenerator.getKeys). Direct key space:
@@ -424,6 +474,13 @@ class GpuQueryExecutor:
                 log2m = self.pa_aggs[pi][2]
                 regs = outs[pi].reshape(n, 1 << log2m)
                 cols.append([HyperLogLog(log2m, regs[r]) for r in range(n)])
+            elif a.function in ("MINMAXRANGE", "MINMAXRANGEMV"):
+                cols.append([MinMaxRangePair(lo, hi) for lo, hi in zip(outs[pi[0]].tolist(), outs[pi[1]].tolist())])
+            elif a.function in ("DISTINCTCOUNT", "DISTINCTCOUNTMV"):
+                # the value set of DistinctCountAggregationFunction (BaseDistinctAggregateAggregationFunction)
+                vd = self.value_dicts[pi]
+                pres = outs[pi].reshape(n, self._presence_stride(pi))[:, :len(vd)]
+                cols.append([set(vd[np.flatnonzero(pres[r])].tolist()) for r in range(n)])
             else:
                 cols.append(outs[pi].tolist())
         rows = list(zip(*cols)) if cols else [()] * n

@@ -20,7 +20,7 @@ SECTION_OP = {
     L.PA_ACC_SUM_F64: dist.ReduceOp.SUM,
     L.PA_ACC_MIN_I64: dist.ReduceOp.MIN,
     L.PA_ACC_MAX_I64: dist.ReduceOp.MAX,
-    L.PA_ACC_HLL_U32: dist.ReduceOp.MAX,
+    L.PA_ACC_HLL_U8: dist.ReduceOp.MAX,
     L.PA_ACC_DOCS_U64: dist.ReduceOp.SUM,
     L.PA_ACC_KEYS_I64: None,  # not element-wise reducible (hashed key spaces)
 }
@@ -31,7 +31,7 @@ SECTION_DTYPE = {
     L.PA_ACC_SUM_F64: torch.float64,
     L.PA_ACC_MIN_I64: torch.int64,
     L.PA_ACC_MAX_I64: torch.int64,
-    L.PA_ACC_HLL_U32: torch.int32,  # registers are < 32: signed max == unsigned max
+    L.PA_ACC_HLL_U8: torch.uint8,  # one byte per register (HyperLogLog.addAll == register max)
     L.PA_ACC_DOCS_U64: torch.int64,
     L.PA_ACC_KEYS_I64: torch.int64,
 }

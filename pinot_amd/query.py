@@ -8,7 +8,8 @@ filter: AND / OR / NOT / ( ) over  col = v | col != v | col <> v | col < v | col
         col BETWEEN a AND b | col IN (...) | col NOT IN (...)
 Comparison predicates become RangePredicate exactly as the reference's RequestContextUtils does
 (pinot-common/.../request/context/RequestContextUtils.java: >, >=, <, <=, BETWEEN -> RANGE).
-Aggregations: COUNT(*), SUM, MIN, MAX, AVG, DISTINCTCOUNTHLL(col[, log2m]).
+Aggregations: COUNT(*), SUM, MIN, MAX, AVG, MINMAXRANGE, DISTINCTCOUNT, DISTINCTCOUNTHLL(col[, log2m]) and their *MV
+forms.
 """
 import re
 from dataclasses import dataclass, field
@@ -74,8 +75,9 @@ PREDICATES = (EqPredicate, NotEqPredicate, InPredicate, NotInPredicate, RangePre
 
 # AggregationFunctionType names the hot path runs: single-value functions and their multi-value (*MV) forms, which
 # aggregate every value of a multi-value column (SumMVAggregationFunction, CountMVAggregationFunction, ...)
-SUPPORTED_FUNCTIONS = ("SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNTHLL",
-                       "COUNTMV", "SUMMV", "MINMV", "MAXMV", "AVGMV", "DISTINCTCOUNTHLLMV")
+SUPPORTED_FUNCTIONS = ("SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNTHLL", "MINMAXRANGE", "DISTINCTCOUNT",
+                       "COUNTMV", "SUMMV", "MINMV", "MAXMV", "AVGMV", "DISTINCTCOUNTHLLMV", "MINMAXRANGEMV",
+                       "DISTINCTCOUNTMV")
 
 
 def base_function(fn):

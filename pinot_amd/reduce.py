@@ -1,7 +1,8 @@
 """Server trim + broker reduce of intermediate results (the callers either side of the hot path).
 
   merge_intermediate   ~ GroupByDataTableReducer / AggregationDataTableReducer merging server DataTables
-                         (AggregationFunction.merge: COUNT/SUM +, MIN min, MAX max, AVG pair +, HLL addAll)
+                         (AggregationFunction.merge: COUNT/SUM +, MIN min, MAX max, AVG pair +, HLL addAll,
+                         MINMAXRANGE pair min/max, DISTINCTCOUNT set union)
   server_trim          ~ IndexedTable.finish on the server (IndexedTable.java:149): with ORDER BY keep the top
                          max(limit*5, minServerGroupTrimSize) groups (GroupByUtils.getTableCapacity); without
                          ORDER BY keep `limit` groups (GroupByCombineOperator.java:63-73)
@@ -11,7 +12,7 @@ import math
 from functools import cmp_to_key
 
 from . import query as Q
-from .engine import AvgPair, IntermediateResult
+from .engine import AvgPair, IntermediateResult, MinMaxRangePair
 from .hll import HyperLogLog
 
 
@@ -27,6 +28,10 @@ def merge_value(fn, a, b):
         return AvgPair(a.sum + b.sum, a.count + b.count)
     if fn == "DISTINCTCOUNTHLL":
         return HyperLogLog(a.log2m, a.registers).add_all(b)
+    if fn == "MINMAXRANGE":  # MinMaxRangePair.apply
+        return MinMaxRangePair(min(a.min, b.min), max(a.max, b.max))
+    if fn == "DISTINCTCOUNT":  # BaseDistinctAggregateAggregationFunction.merge: set union
+        return set(a) | set(b)
     raise ValueError(fn)
 
 
@@ -36,6 +41,10 @@ def final_value(fn, v):
         return v.sum / v.count if v.count else -math.inf
     if fn == "DISTINCTCOUNTHLL":
         return v.cardinality()
+    if fn == "MINMAXRANGE":  # MinMaxRangeAggregationFunction.extractFinalResult: max - min
+        return v.max - v.min
+    if fn == "DISTINCTCOUNT":  # DistinctCountAggregationFunction.extractFinalResult: the set's size
+        return len(v)
     return v
 
 

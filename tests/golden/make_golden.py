@@ -36,77 +36,95 @@ GROUP_BY = " GROUP BY column9 ORDER BY v1 DESC, v2 DESC LIMIT 1"
 CASES = []
 
 
-def case(source, sql, rows, delta=0.0):
-    CASES.append({"source": source, "sql": sql, "rows": rows, "delta": delta})
+def case(source, sql, rows, delta=0.0, stats=None):
+    """stats: the testInterSegmentsResult arguments (numDocsScanned, numEntriesScannedInFilter,
+    numEntriesScannedPostFilter, numTotalDocs) the reference asserts for this case (QueriesTestUtils.java)."""
+    CASES.append({"source": source, "sql": sql, "rows": rows, "delta": delta, "stats": stats})
+
+
+# the four execution statistics of the aggregation test's shapes (InterSegmentAggregationSingleValueQueriesTest.java):
+# no filter / FILTER, aggregation-only / GROUP BY; `post` = numEntriesScannedPostFilter
+def st(filtered, post):
+    return [24516, 252256, post, 120000] if filtered else [120000, 0, post, 120000]
 
 
 # ---- InterSegmentAggregationSingleValueQueriesTest
 q = "SELECT COUNT(*) FROM testTable"
-case(AGG + ":47-50", q, [[120000]])
-case(AGG + ":52-54", q + FILTER, [[24516]])
+case(AGG + ":47-54", q, [[120000]], stats=st(0, 0))
+case(AGG + ":56-58", q + FILTER, [[24516]], stats=st(1, 0))
 gb = " GROUP BY column9 ORDER BY COUNT(*) DESC LIMIT 1"
-case(AGG + ":56-59", q + gb, [[64420]])
-case(AGG + ":61-63", q + FILTER + gb, [[17080]])
+case(AGG + ":60-63", q + gb, [[64420]], stats=st(0, 120000))
+case(AGG + ":65-67", q + FILTER + gb, [[17080]], stats=st(1, 24516))
 q = "SELECT MAX(column1) AS v1, MAX(column3) AS v2 FROM testTable"
-case(AGG + ":89-100", q, [[2146952047.0, 2147419555.0]])
-case(AGG + ":102-105", q + FILTER, [[2146952047.0, 999813884.0]])
-case(AGG + ":107-110", q + GROUP_BY, [[2146952047.0, 2146630496.0]])
-case(AGG + ":112-115", q + FILTER + GROUP_BY, [[2146952047.0, 999813884.0]])
+case(AGG + ":93-102", q, [[2146952047.0, 2147419555.0]], stats=st(0, 0))
+case(AGG + ":104-107", q + FILTER, [[2146952047.0, 999813884.0]], stats=st(1, 49032))
+case(AGG + ":109-112", q + GROUP_BY, [[2146952047.0, 2146630496.0]], stats=st(0, 360000))
+case(AGG + ":114-117", q + FILTER + GROUP_BY, [[2146952047.0, 999813884.0]], stats=st(1, 73548))
 q = "SELECT MIN(column1) AS v1, MIN(column3) AS v2 FROM testTable"
 gb = " GROUP BY column9 ORDER BY v1, v2 LIMIT 1"
-case(AGG + ":119-130", q, [[240528.0, 17891.0]])
-case(AGG + ":132-135", q + FILTER, [[101116473.0, 20396372.0]])
-case(AGG + ":137-141", q + gb, [[240528.0, 17891.0]])
-case(AGG + ":143-146", q + FILTER + gb, [[101116473.0, 91804599.0]])
+case(AGG + ":122-131", q, [[240528.0, 17891.0]], stats=st(0, 0))
+case(AGG + ":133-136", q + FILTER, [[101116473.0, 20396372.0]], stats=st(1, 49032))
+case(AGG + ":138-142", q + gb, [[240528.0, 17891.0]], stats=st(0, 360000))
+case(AGG + ":144-147", q + FILTER + gb, [[101116473.0, 91804599.0]], stats=st(1, 73548))
 q = "SELECT SUM(column1) AS v1, SUM(column3) AS v2 FROM testTable"
-case(AGG + ":150-158", q, [[129268741751388.0, 129156636756600.0]])
-case(AGG + ":160-163", q + FILTER, [[27503790384288.0, 12429178874916.0]])
-case(AGG + ":165-168", q + GROUP_BY, [[69526727335224.0, 69225631719808.0]])
-case(AGG + ":170-173", q + FILTER + GROUP_BY, [[19058003631876.0, 8606725456500.0]])
+case(AGG + ":152-159", q, [[129268741751388.0, 129156636756600.0]], stats=st(0, 240000))
+case(AGG + ":161-164", q + FILTER, [[27503790384288.0, 12429178874916.0]], stats=st(1, 49032))
+case(AGG + ":166-169", q + GROUP_BY, [[69526727335224.0, 69225631719808.0]], stats=st(0, 360000))
+case(AGG + ":171-174", q + FILTER + GROUP_BY, [[19058003631876.0, 8606725456500.0]], stats=st(1, 73548))
 q = "SELECT AVG(column1) AS v1, AVG(column3) AS v2 FROM testTable"
-case(AGG + ":177-185", q, [[1077239514.5949, 1076305306.305]], 1e-5)
-case(AGG + ":187-191", q + FILTER, [[1121871038.68037, 506982332.96280]], 1e-5)
-case(AGG + ":193-197", q + GROUP_BY, [[2142595699.0, 334963174.0]])
-case(AGG + ":199-202", q + FILTER + GROUP_BY, [[2142595699.0, 334963174.0]])
+case(AGG + ":179-186", q, [[1077239514.5949, 1076305306.305]], 1e-5, stats=st(0, 240000))
+case(AGG + ":188-192", q + FILTER, [[1121871038.68037, 506982332.96280]], 1e-5, stats=st(1, 49032))
+case(AGG + ":194-197", q + GROUP_BY, [[2142595699.0, 334963174.0]], stats=st(0, 360000))
+case(AGG + ":199-202", q + FILTER + GROUP_BY, [[2142595699.0, 334963174.0]], stats=st(1, 73548))
+q = "SELECT MINMAXRANGE(column1) AS v1, MINMAXRANGE(column3) AS v2 FROM testTable"
+case(AGG + ":207-216", q, [[2146711519.0, 2147401664.0]], stats=st(0, 0))
+case(AGG + ":218-221", q + FILTER, [[2045835574.0, 979417512.0]], stats=st(1, 49032))
+case(AGG + ":223-226", q + GROUP_BY, [[2146711519.0, 2146612605.0]], stats=st(0, 360000))
+case(AGG + ":228-231", q + FILTER + GROUP_BY, [[2044094181.0, 979417512.0]], stats=st(1, 73548))
+q = "SELECT DISTINCTCOUNT(column1) AS v1, DISTINCTCOUNT(column3) AS v2 FROM testTable"
+case(AGG + ":236-245", q, [[6582, 21910]], stats=st(0, 0))
+case(AGG + ":247-249", q + FILTER, [[1872, 4556]], stats=st(1, 49032))
+case(AGG + ":251-253", q + GROUP_BY, [[3495, 11961]], stats=st(0, 360000))
+case(AGG + ":255-257", q + FILTER + GROUP_BY, [[1272, 3289]], stats=st(1, 73548))
 q = "SELECT DISTINCTCOUNTHLL(column1) AS v1, DISTINCTCOUNTHLL(column3) AS v2 FROM testTable"
-case(AGG + ":261-271", q, [[5977, 23825]])
-case(AGG + ":273-275", q + FILTER, [[1886, 4492]])
-case(AGG + ":277-279", q + GROUP_BY, [[3592, 11889]])
-case(AGG + ":281-283", q + FILTER + GROUP_BY, [[1324, 3197]])
+case(AGG + ":262-271", q, [[5977, 23825]], stats=st(0, 0))
+case(AGG + ":273-275", q + FILTER, [[1886, 4492]], stats=st(1, 49032))
+case(AGG + ":277-279", q + GROUP_BY, [[3592, 11889]], stats=st(0, 360000))
+case(AGG + ":281-283", q + FILTER + GROUP_BY, [[1324, 3197]], stats=st(1, 73548))
 
 # ---- InterSegmentGroupBySingleValueQueriesTest.groupByOrderByDataProvider
 c11 = [["", 5935285005452.0], ["P", 88832999206836.0], ["gFuH", 63202785888.0], ["o", 18105331533948.0],
        ["t", 16331923219264.0]]
-case(GBY + ":66-71", "SELECT column11, SUM(column1) FROM testTable GROUP BY column11 ORDER BY column11", c11)
+case(GBY + ":66-71", "SELECT column11, SUM(column1) FROM testTable GROUP BY column11 ORDER BY column11", c11, stats=[120000, 0, 240000, 120000])
 case(GBY + ":73-77", "SELECT column11, sum(column1) FROM testTable GROUP BY column11 ORDER BY column11 DESC",
-     list(reversed(c11)))
+     list(reversed(c11)), stats=[120000, 0, 240000, 120000])
 case(GBY + ":79-84", "SELECT column11, Sum(column1) FROM testTable GROUP BY column11 ORDER BY column11 LIMIT 3",
-     c11[:3])
+     c11[:3], stats=[120000, 0, 240000, 120000])
 two = [["", "HEuxNvH", 3789390396216.0], ["", "KrNxpdycSiwoRohEiTIlLqDHnx", 733802350944.0],
        ["", "MaztCmmxxgguBUxPti", 1333941430664.0], ["", "dJWwFk", 55470665124.0],
        ["", "oZgnrlDEtjjVpUoFLol", 22680162504.0], ["P", "HEuxNvH", 21998672845052.0],
        ["P", "KrNxpdycSiwoRohEiTIlLqDHnx", 18069909216728.0], ["P", "MaztCmmxxgguBUxPti", 27177029040008.0],
        ["P", "TTltMtFiRqUjvOG", 4462670055540.0], ["P", "XcBNHe", 120021767504.0]]
 case(GBY + ":86-99", "SELECT column11, column12, SUM(column1) FROM testTable GROUP BY column11, column12 "
-     "ORDER BY column11, column12", two)
+     "ORDER BY column11, column12", two, stats=[120000, 0, 360000, 120000])
 case(GBY + ":101-110", "SELECT column11, column12, SUM(column1) FROM testTable GROUP BY column11, column12 "
      "ORDER BY column11, column12 LIMIT 15",
      two + [["P", "dJWwFk", 6224665921376.0], ["P", "fykKFqiw", 1574451324140.0], ["P", "gFuH", 860077643636.0],
-            ["P", "oZgnrlDEtjjVpUoFLol", 8345501392852.0], ["gFuH", "HEuxNvH", 29872400856.0]])
+            ["P", "oZgnrlDEtjjVpUoFLol", 8345501392852.0], ["gFuH", "HEuxNvH", 29872400856.0]], stats=[120000, 0, 360000, 120000])
 case(GBY + ":112-121", "SELECT column11, column12, SUM(column1) FROM testTable GROUP BY column11, column12 "
      "ORDER BY column11, column12 DESC",
      [["", "oZgnrlDEtjjVpUoFLol", 22680162504.0], ["", "dJWwFk", 55470665124.0],
       ["", "MaztCmmxxgguBUxPti", 1333941430664.0], ["", "KrNxpdycSiwoRohEiTIlLqDHnx", 733802350944.0],
       ["", "HEuxNvH", 3789390396216.0], ["P", "oZgnrlDEtjjVpUoFLol", 8345501392852.0],
       ["P", "gFuH", 860077643636.0], ["P", "fykKFqiw", 1574451324140.0], ["P", "dJWwFk", 6224665921376.0],
-      ["P", "XcBNHe", 120021767504.0]])
+      ["P", "XcBNHe", 120021767504.0]], stats=[120000, 0, 360000, 120000])
 case(GBY + ":123-132", "SELECT column11, column12, SUM(column1) FROM testTable GROUP BY column11, column12 "
      "ORDER BY column11, sum(column1)",
      [["", "oZgnrlDEtjjVpUoFLol", 22680162504.0], ["", "dJWwFk", 55470665124.0],
       ["", "KrNxpdycSiwoRohEiTIlLqDHnx", 733802350944.0], ["", "MaztCmmxxgguBUxPti", 1333941430664.0],
       ["", "HEuxNvH", 3789390396216.0], ["P", "XcBNHe", 120021767504.0], ["P", "gFuH", 860077643636.0],
       ["P", "fykKFqiw", 1574451324140.0], ["P", "TTltMtFiRqUjvOG", 4462670055540.0],
-      ["P", "dJWwFk", 6224665921376.0]])
+      ["P", "dJWwFk", 6224665921376.0]], stats=[120000, 0, 360000, 120000])
 case(GBY + ":134-157", "SELECT column11, column12, SUM(column1) FROM testTable GROUP BY column11, column12 "
      "ORDER BY SUM(column1) DESC LIMIT 50",
      [["P", "MaztCmmxxgguBUxPti", 27177029040008.0], ["P", "HEuxNvH", 21998672845052.0],
@@ -125,30 +143,46 @@ case(GBY + ":134-157", "SELECT column11, column12, SUM(column1) FROM testTable G
       ["o", "fykKFqiw", 62975165296.0], ["", "dJWwFk", 55470665124.0],
       ["gFuH", "HEuxNvH", 29872400856.0], ["gFuH", "MaztCmmxxgguBUxPti", 29170832184.0],
       ["", "oZgnrlDEtjjVpUoFLol", 22680162504.0], ["t", "XcBNHe", 11276063956.0],
-      ["gFuH", "KrNxpdycSiwoRohEiTIlLqDHnx", 4159552848.0], ["o", "gFuH", 2628604920.0]])
+      ["gFuH", "KrNxpdycSiwoRohEiTIlLqDHnx", 4159552848.0], ["o", "gFuH", 2628604920.0]], stats=[120000, 0, 360000, 120000])
 case(GBY + ":159-167", "SELECT sum(column1), MIN(column6) FROM testTable GROUP BY column11 ORDER BY column11",
      [[5935285005452.0, 2.96467636E8], [88832999206836.0, 1689277.0], [63202785888.0, 2.96467636E8],
-      [18105331533948.0, 2.96467636E8], [16331923219264.0, 1980174.0]])
+      [18105331533948.0, 2.96467636E8], [16331923219264.0, 1980174.0]], stats=[120000, 0, 360000, 120000])
 case(GBY + ":169-178", "SELECT column11, column12, SUM(column1) FROM testTable GROUP BY column11, column12 "
      "ORDER BY SUM  (\tcolumn1) DESC LIMIT 3",
      [["P", "MaztCmmxxgguBUxPti", 27177029040008.0], ["P", "HEuxNvH", 21998672845052.0],
-      ["P", "KrNxpdycSiwoRohEiTIlLqDHnx", 18069909216728.0]])
+      ["P", "KrNxpdycSiwoRohEiTIlLqDHnx", 18069909216728.0]], stats=[120000, 0, 360000, 120000])
 c12min = [["XcBNHe", 329467557.0], ["fykKFqiw", 296467636.0], ["gFuH", 296467636.0], ["HEuxNvH", 6043515.0],
           ["MaztCmmxxgguBUxPti", 6043515.0], ["dJWwFk", 6043515.0], ["KrNxpdycSiwoRohEiTIlLqDHnx", 1980174.0],
           ["TTltMtFiRqUjvOG", 1980174.0], ["oZgnrlDEtjjVpUoFLol", 1689277.0]]
 case(GBY + ":180-189", "SELECT column12, MIN(column6) FROM testTable GROUP BY column12 "
-     "ORDER BY Min(column6) DESC, column12", c12min)
+     "ORDER BY Min(column6) DESC, column12", c12min, stats=[120000, 0, 240000, 120000])
 case(GBY + ":191-198", "SELECT column12 FROM testTable GROUP BY column12 ORDER BY Min(column6) DESC, column12",
-     [[r[0]] for r in c12min])
+     [[r[0]] for r in c12min], stats=[120000, 0, 240000, 120000])
 case(GBY + ":200-204", "SELECT column12 FROM testTable GROUP BY column12 ORDER BY Min(column6) DESC, "
-     "SUM(column1) LIMIT 3", [["XcBNHe"], ["gFuH"], ["fykKFqiw"]])
+     "SUM(column1) LIMIT 3", [["XcBNHe"], ["gFuH"], ["fykKFqiw"]], stats=[120000, 0, 360000, 120000])
 case(GBY + ":206-213", "SELECT column12, MIN(column6) FROM testTable GROUP BY column12 "
      "ORDER BY Min(column6) DESC, SUM(column1) LIMIT 3",
-     [["XcBNHe", 329467557.0], ["gFuH", 296467636.0], ["fykKFqiw", 296467636.0]])
+     [["XcBNHe", 329467557.0], ["gFuH", 296467636.0], ["fykKFqiw", 296467636.0]], stats=[120000, 0, 360000, 120000])
 case(GBY + ":215-225", "select column17, count(*) from testTable group by column17 order by column17 limit 15",
      [[83386499, 2924], [217787432, 3892], [227908817, 6564], [402773817, 7304], [423049234, 6556],
       [561673250, 7420], [635942547, 3308], [638936844, 3816], [939479517, 3116], [984091268, 3824],
-      [1230252339, 5620], [1284373442, 7428], [1555255521, 2900], [1618904660, 2744], [1670085862, 3388]])
+      [1230252339, 5620], [1284373442, 7428], [1555255521, 2900], [1618904660, 2744], [1670085862, 3388]], stats=[120000, 0, 120000, 120000])
+
+# Object type aggregations (groupByOrderByDataProvider)
+g6 = [["", 296467636.0], ["P", 909380310.3521485], ["gFuH", 296467636.0], ["o", 296467636.0], ["t", 526245333.3900426]]
+case(GBY + ":244-249", "SELECT column11, AVG(column6) FROM testTable GROUP BY column11  ORDER BY column11", g6,
+     stats=[120000, 0, 240000, 120000])
+case(GBY + ":251-257", "SELECT column11, AVG(column6) FROM testTable GROUP BY column11 ORDER BY AVG(column6), column11 DESC",
+     [["o", 296467636.0], ["gFuH", 296467636.0], ["", 296467636.0], ["t", 526245333.3900426],
+      ["P", 909380310.3521485]], stats=[120000, 0, 240000, 120000])
+d12 = [["HEuxNvH", 5], ["KrNxpdycSiwoRohEiTIlLqDHnx", 5], ["MaztCmmxxgguBUxPti", 5], ["TTltMtFiRqUjvOG", 3],
+       ["XcBNHe", 2], ["dJWwFk", 4], ["fykKFqiw", 3], ["gFuH", 3], ["oZgnrlDEtjjVpUoFLol", 4]]
+case(GBY + ":259-267", "SELECT column12, DISTINCTCOUNT(column11) FROM testTable GROUP BY column12 ORDER BY column12", d12,
+     stats=[120000, 0, 240000, 120000])
+case(GBY + ":269-277", "SELECT column12, DISTINCTCOUNT(column11) FROM testTable GROUP BY column12 "
+     "ORDER BY DistinctCount(column11), column12 DESC",
+     [["XcBNHe", 2], ["gFuH", 3], ["fykKFqiw", 3], ["TTltMtFiRqUjvOG", 3], ["oZgnrlDEtjjVpUoFLol", 4], ["dJWwFk", 4],
+      ["MaztCmmxxgguBUxPti", 5], ["KrNxpdycSiwoRohEiTIlLqDHnx", 5], ["HEuxNvH", 5]], stats=[120000, 0, 240000, 120000])
 
 
 def main():

@@ -23,17 +23,17 @@ def test_library_exports_every_symbol():
     lib = ctypes.CDLL(path)
     missing = [s for s in _declared() if not hasattr(lib, s)]
     assert not missing, missing
-    assert _lib.lib().pa_abi_version() == 1
+    assert _lib.lib().pa_abi_version() == _lib.ABI_VERSION
 
 
 def test_struct_layout_matches_header():
     """ctypes mirrors of the C structs have the sizes the compiled library expects."""
     from pinot_amd import _lib as L
-    # pa_query_spec: 4 + 16*8 + 4 + 48*4 + 4 + 8*4 (+4 pad) + 8*8 + 4 + 16*16 + 4 + 4
+    # pa_query_spec: 4 + 16*8 + 4 + 48*4 + 4 + 8*4 (+4 pad) + 8*8 + 4 (+4 pad) + 16*24 + 4 + 4
     assert ctypes.sizeof(L.LeafSpec) == 8
-    assert ctypes.sizeof(L.AggSpec) == 16
+    assert ctypes.sizeof(L.AggSpec) == 24
     assert ctypes.sizeof(L.LeafParams) == 56
-    assert ctypes.sizeof(L.QuerySpec) == 704
+    assert ctypes.sizeof(L.QuerySpec) == 832
 
 
 def test_product_path_does_not_import_oracle():

@@ -91,6 +91,9 @@ def test_mv_group_by(sql):
     "GROUP BY a LIMIT 100",
     "SELECT tags, COUNTMV(tags), SUMMV(tags), DISTINCTCOUNTHLLMV(tags) FROM t WHERE b > 40 GROUP BY tags LIMIT 1000",
     "SELECT COUNT(*), SUMMV(tags) FROM t WHERE tags = 999999",
+    "SELECT a, DISTINCTCOUNTMV(tags), MINMAXRANGEMV(tags), DISTINCTCOUNT(b), MINMAXRANGE(m) FROM t WHERE b > 20 "
+    "GROUP BY a LIMIT 100",
+    "SELECT DISTINCTCOUNTMV(tags), MINMAXRANGEMV(tags) FROM t WHERE a = 14",
 ])
 def test_mv_aggregations(sql):
     segs = [mv_segment(7, 12007), mv_segment(8, 2048)]

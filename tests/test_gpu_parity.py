@@ -13,7 +13,7 @@ import oracle
 from conftest import rows_match
 from pinot_amd import _lib as L
 from pinot_amd import parse_sql
-from pinot_amd.engine import AvgPair, GpuQueryExecutor, GpuSegment
+from pinot_amd.engine import AvgPair, GpuQueryExecutor, GpuSegment, MinMaxRangePair
 from pinot_amd.hll import HyperLogLog
 from pinot_amd.reduce import final_result_table, merge_intermediate, server_trim
 from synth import make_segment
@@ -26,6 +26,10 @@ DOUBLE_REL = 1e-9
 def _close(a, b, rel):
     if isinstance(b, HyperLogLog):
         return isinstance(a, HyperLogLog) and a == b
+    if isinstance(b, set):  # DISTINCTCOUNT value sets: exact
+        return isinstance(a, set) and a == b
+    if isinstance(b, MinMaxRangePair):
+        return _close(a.min, b.min, rel) and _close(a.max, b.max, rel)
     if isinstance(b, AvgPair):
         return a.count == b.count and _close(a.sum, b.sum, rel)
     if isinstance(b, int) and not isinstance(b, bool):
@@ -110,6 +114,11 @@ QUERIES = [
     "SELECT COUNT(*) FROM t WHERE d1 != {d1a} AND NOT (d2 = 's00004_xxxx' OR m1 >= {m1a})",
     "SELECT d1, d2, d3, COUNT(*), SUM(m1) FROM t WHERE f1 < 0 GROUP BY d1, d2, d3 LIMIT 100000 "
     "OPTION(numGroupsLimit=1000000)",
+    # exact DISTINCTCOUNT (per-group value presence over the table-wide value dictionary) and MINMAXRANGE
+    "SELECT d1, MINMAXRANGE(m1), DISTINCTCOUNT(d3), DISTINCTCOUNT(d2), MINMAXRANGE(f2), COUNT(*) FROM t "
+    "WHERE d3 > {d3a} GROUP BY d1 LIMIT 100",
+    "SELECT MINMAXRANGE(f1), MINMAXRANGE(m2), DISTINCTCOUNT(m1), DISTINCTCOUNT(f2), DISTINCTCOUNT(d2) FROM t "
+    "WHERE d2 NOT IN ('s00001_x') OR m1 < {m1a}",
 ]
 
 
@@ -227,6 +236,9 @@ def test_different_dictionaries_remap():
     cols = {"k1": ("INT", 40), "k2": ("STRING", 15), "m": ("INT", 100)}
     segs = [make_segment(s, 7000 + s, cols) for s in (21, 22, 23, 24)]
     run_both("SELECT k1, k2, COUNT(*), SUM(m), MIN(m), DISTINCTCOUNTHLL(m) FROM t GROUP BY k1, k2 LIMIT 10000", segs)
+    # DISTINCTCOUNT over per-segment dictionaries: segment dictIds remapped to the table-wide value ids
+    run_both("SELECT k1, DISTINCTCOUNT(m), DISTINCTCOUNT(k2), MINMAXRANGE(m) FROM t GROUP BY k1 LIMIT 10000", segs)
+    run_both("SELECT DISTINCTCOUNT(m), DISTINCTCOUNT(k2) FROM t WHERE k1 > 0", segs)
 
 
 def test_long_sum_beyond_2_53():
@@ -289,25 +301,50 @@ def test_partitioned_aggregation(flags):
     cols = {"k1": ("INT", 700), "k2": ("LONG", 900), "m": ("INT", 5000), "big": ("LONG", 3000), "f": ("DOUBLE", 800),
             "g": ("FLOAT", 600)}
     segs = [make_segment(70 + i, n, cols) for i, n in enumerate((120011, 40009))]
+    # (the second query's records carry three 64-bit payloads over a 2.5M-key space: their LDS bins may not fit next
+    # to the tile ring, and then the per-doc global-atomic path runs it — same results either way)
     queries = [
-        "SELECT k1, k2, COUNT(*), SUM(m), MIN(m), MAX(m), AVG(m) FROM t GROUP BY k1, k2 LIMIT 1000000 "
-        "OPTION(numGroupsLimit=2000000)",
-        "SELECT k2, k1, SUM(big), MIN(big), MAX(f), SUM(f), MIN(g) FROM t WHERE m > {m} GROUP BY k2, k1 "
-        "LIMIT 1000000 OPTION(numGroupsLimit=2000000)",
-        "SELECT k1, k2, COUNT(*) FROM t GROUP BY k1, k2 LIMIT 1000000 OPTION(numGroupsLimit=2000000)",
+        ("SELECT k1, k2, COUNT(*), SUM(m), MIN(m), MAX(m), AVG(m) FROM t GROUP BY k1, k2 LIMIT 1000000 "
+         "OPTION(numGroupsLimit=2000000)", True),
+        ("SELECT k2, k1, SUM(big), MIN(big), MAX(f), SUM(f), MIN(g) FROM t WHERE m > {m} GROUP BY k2, k1 "
+         "LIMIT 1000000 OPTION(numGroupsLimit=2000000)", False),
+        ("SELECT k1, k2, COUNT(*) FROM t GROUP BY k1, k2 LIMIT 1000000 OPTION(numGroupsLimit=2000000)", True),
     ]
     mv = int(segs[0].column("m").dictionary[len(segs[0].column("m").dictionary) // 4])
     gsegs = [GpuSegment(sg) for sg in segs]
     try:
-        for sql in queries:
+        for sql, must in queries:
             sql = sql.format(m=mv)
             got, exp, _ = run_both(sql, segs, gsegs=gsegs, flags=flags, rel=DOUBLE_REL)
             assert len(got.groups) > 50000
             ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags)
             strategy = ex.stats()["plan"]["strategy"]
             ex.close()
-            if not flags & (3 << L.PA_QF_PART_SHIFT):  # (smaller partitions may not fit the binning LDS: global)
-                assert strategy == ("global" if flags & L.PA_QF_NO_PARTITION else "partitioned"), strategy
+            if flags & L.PA_QF_NO_PARTITION:
+                assert strategy == "global", strategy
+            elif must and not flags & (3 << L.PA_QF_PART_SHIFT):  # (smaller partitions may not fit the bins' LDS)
+                assert strategy == "partitioned", strategy
+    finally:
+        for g in gsegs:
+            g.close()
+
+
+def test_partitioned_generic_records():
+    """V records with several payloads (V_FMT_GEN: LONG beyond int32, DOUBLE, FLOAT widened to double) over one shared
+    table-wide key space small enough for the emit pass's bins; identical to the oracle."""
+    cols = {"k1": ("INT", 400), "k2": ("INT", 300), "big": ("LONG", 3000), "f": ("DOUBLE", 800), "g": ("FLOAT", 600)}
+    base = make_segment(77, 150011, cols)
+    segs = [base, base]  # one dictionary per column: the key space stays 400 x 300
+    sql = ("SELECT k2, k1, COUNT(*), SUM(big), MIN(big), MAX(f), SUM(f), MIN(g) FROM t GROUP BY k2, k1 "
+           "LIMIT 1000000 OPTION(numGroupsLimit=2000000)")
+    gsegs = [GpuSegment(sg) for sg in segs]
+    try:
+        got, exp, _ = run_both(sql, segs, gsegs=gsegs, rel=DOUBLE_REL)
+        ex = GpuQueryExecutor(parse_sql(sql), gsegs)
+        strategy = ex.stats()["plan"]["strategy"]
+        ex.close()
+        assert strategy == "partitioned", strategy
+        assert len(got.groups) > 10000
     finally:
         for g in gsegs:
             g.close()

@@ -42,9 +42,9 @@ def partial(rank):
     dsum = rng.standard_normal(K)
     dmin = f64_order_encode(rng.standard_normal(K) * 1e6)
     imax = rng.integers(-(1 << 40), 1 << 40, K).astype(np.int64)
-    hll = rng.integers(0, 26, K << LOG2M).astype(np.int32)
+    hll = rng.integers(0, 26, K << LOG2M).astype(np.uint8)
     return [(L.PA_ACC_COUNT_U64, count), (L.PA_ACC_SUM_I64X2, sum_x2), (L.PA_ACC_SUM_F64, dsum),
-            (L.PA_ACC_MIN_I64, dmin), (L.PA_ACC_MAX_I64, imax), (L.PA_ACC_HLL_U32, hll)], vals
+            (L.PA_ACC_MIN_I64, dmin), (L.PA_ACC_MAX_I64, imax), (L.PA_ACC_HLL_U8, hll)], vals
 
 
 def _worker(rank, world, port, all_reduce, out):
@@ -172,7 +172,7 @@ def _secs_with_docs(rank):
     secs, _ = partial(rank)
     # the bench query's layout: COUNT, 2x SUM(LONG), numDocsScanned — then the rest
     return [secs[0], secs[1], (L.PA_ACC_SUM_I64X2, secs[1][1] * 3),
-            (L.PA_ACC_DOCS_U64, np.array([5 + rank, 0, 1], np.int64))] + secs[2:]
+            (L.PA_ACC_DOCS_U64, np.array([5 + rank, 0, 1, 0], np.int64))] + secs[2:]
 
 
 def test_section_runs_merge_adjacent_same_op():
@@ -182,8 +182,8 @@ def test_section_runs_merge_adjacent_same_op():
     runs = section_runs([(k, o, a.size) for (k, a), o in zip(secs, offs)])
     # COUNT + SUM_I64X2 + SUM_I64X2 + DOCS -> one SUM run; then f64 SUM, MIN, MAX, HLL each on their own
     assert [r[0] for r in runs] == [L.PA_ACC_COUNT_U64, L.PA_ACC_SUM_F64, L.PA_ACC_MIN_I64, L.PA_ACC_MAX_I64,
-                                    L.PA_ACC_HLL_U32]
-    assert runs[0][2] == 0 and runs[0][3] == offs[3] + 3 * 8
+                                    L.PA_ACC_HLL_U8]
+    assert runs[0][2] == 0 and runs[0][3] == offs[3] + 4 * 8
     # a keys section (not element-wise reducible) never merges
     r2 = section_runs([(L.PA_ACC_COUNT_U64, 0, 4), (L.PA_ACC_KEYS_I64, 256, 4), (L.PA_ACC_DOCS_U64, 512, 3)])
     assert len(r2) == 3
@@ -214,12 +214,12 @@ def test_gloo_reduce_over_merged_section_runs():
     _, offs = _block_layout(parts[0])
     got = out[0]
     for i, (k, a) in enumerate(parts[0]):
-        dt = np.int32 if SECTION_DTYPE[k] == torch.int32 else a.dtype
+        dt = a.dtype
         g = got[offs[i]:offs[i] + a.nbytes].view(dt)
         xs = [b[offs[i]:offs[i] + a.nbytes].view(dt) for b in bufs]
         if k in (L.PA_ACC_MIN_I64,):
             exp = np.minimum(*xs)
-        elif k in (L.PA_ACC_MAX_I64, L.PA_ACC_HLL_U32):
+        elif k in (L.PA_ACC_MAX_I64, L.PA_ACC_HLL_U8):
             exp = np.maximum(*xs)
         else:
             exp = xs[0] + xs[1]
