@@ -503,6 +503,8 @@ struct pa_query {
   std::vector<DevSeg> hsegs_count;
   DevBuf dq_count, dsegs_count;
   int count_lds = 0, count_ring = 0, part_lds_c = 0;
+  int emit_strat = 0;   // the emit kernel variant (pemit_strat)
+  int count_k = 1;      // count-pass workgroups per emit workgroup
   size_t sc_hist = 0, sc_off = 0, sc_base = 0, sc_recs_v = 0, sc_recs_h = 0, sc_bytes = 0;
   int scratch_dev = 0;
   int64_t last_matched = -1;  // numDocsScanned read by the last fetch
@@ -1290,11 +1292,13 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
   };
   // the emit pass stages its columns in a ring next to the bins: halve the bins (down to 64-byte bursts) while they
   // do not fit or cost resident waves (at least two workgroups per CU hide the per-record gathers)
-  emit_plan = plan_tiles(q, q->hsegs, STRAT_PEMIT, false, emit_state(bs_v, bs_h), true);
+  const int es = pemit_strat(vstream ? fmt : -1, hll >= 0 ? 1 : 0);
+  q->emit_strat = es;
+  emit_plan = plan_tiles(q, q->hsegs, es, false, emit_state(bs_v, bs_h), true);
   while ((emit_plan.score < 0 || emit_plan.wg_per_cu < 2) && (bs_h > 16 || (bs_v * W > 16 && bs_v % 8 == 0))) {
     const int bv2 = (bs_v * W > 16 && bs_v % 8 == 0) ? bs_v / 2 : bs_v;
     const int bh2 = bs_h > 16 ? bs_h / 2 : bs_h;
-    TilePlan t = plan_tiles(q, q->hsegs, STRAT_PEMIT, false, emit_state(bv2, bh2), true);
+    TilePlan t = plan_tiles(q, q->hsegs, es, false, emit_state(bv2, bh2), true);
     if (emit_plan.score >= 0 && t.score >= 0 && t.wg_per_cu <= emit_plan.wg_per_cu)
       break;  // no more resident waves from smaller bins: keep the larger bursts
     bs_v = bv2;
@@ -1470,6 +1474,10 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
   h.dma_per_tile = plan.dma;
   h.steps = plan.steps;
   h.debug_stream_only = (s.flags & PA_QF_DEBUG_STREAM_ONLY) ? 1 : 0;
+  {
+    const char* e = std::getenv("PA_DEBUG_EMIT");  // measurement only (see DevQuery::debug_emit)
+    h.debug_emit = e ? std::atoi(e) : 0;
+  }
   h.lane_major = P.lm ? 1 : 0;
   h.count = (unsigned long long*)q->sections[0].ptr;
   h.matched_docs = (unsigned long long*)q->sections.back().ptr;
@@ -1523,7 +1531,7 @@ int plan_scratch(pa_query* q, const Prep& P) {
   }
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   size_t o = 0;
-  q->sc_hist = o; o += al(G * Pn * 4);
+  q->sc_hist = o; o += al(G * (size_t)q->count_k * Pn * 4);  // count-pass rows (k per emit workgroup)
   q->sc_off = o; o += al(G * Pn * 4);
   q->sc_base = o; o += al((Pn + 2) * 8);
   q->sc_recs_v = o; o += al((size_t)vrecs * h.rec_words_v * 4);
@@ -1620,7 +1628,7 @@ int upload_descriptors(pa_query* q) {
   if (rc) return rc;
   PA_HIP(hipMemcpy(q->dplans.p, q->hplans.data(), sizeof(LmSegPlan) * q->hplans.size(), hipMemcpyHostToDevice));
   if (q->partitioned) {
-    PA_HIP(set_scan_lds_limit(STRAT_PEMIT, q->steps, 0, q->lds_bytes));
+    PA_HIP(set_scan_lds_limit(q->emit_strat, q->steps, 0, q->lds_bytes));
     PA_HIP(set_scan_lds_limit(STRAT_PCOUNT, q->steps, 0, q->count_lds));
     PA_HIP(set_part_agg_lds_limit(q->part_lds_c));
   } else {
@@ -1776,6 +1784,10 @@ int pa_query_prepare(pa_query* q) {
     c.lds_acc_bytes = (uint32_t)(((size_t)q->hq.num_parts * 4 + 15) & ~(size_t)15);
     q->count_lds = (int)count_plan.lds;
     q->count_ring = count_plan.ring;
+    // the count pass stages fewer columns, so more of its workgroups fit a CU: k per emit workgroup (each walks 1/k of
+    // that workgroup's tiles; part_scan_kernel sums their rows), as many as are resident at once
+    q->count_k = std::max(1, count_plan.wg_per_cu / std::max(1, plan.wg_per_cu));
+    while (q->count_k > 1 && (int64_t)q->grid * q->count_k * kWavesPerWG > total_tiles) --q->count_k;
     // the emit pass's LDS: partition bin state + bins in front of the ring
     q->hq.lds_acc_bytes = (uint32_t)(plan.lds - (size_t)kWavesPerWG * plan.ring * plan.img_dw * 4);
     rc = plan_scratch(q, P);
@@ -1832,10 +1844,10 @@ int pa_query_scan(pa_query* q, void* stream) {
     if (a->used && a->last_stream != st) PA_HIP(hipStreamWaitEvent(st, a->last, 0));
     const PartScratch ps = scratch_of(q, a->p);
     const LmSegPlan* plans = (const LmSegPlan*)q->dplans.p;
-    PA_HIP(launch_scan(STRAT_PCOUNT, q->steps, 0, q->grid, q->count_lds, (const DevQuery*)q->dq_count.p,
+    PA_HIP(launch_scan(STRAT_PCOUNT, q->steps, 0, q->grid * q->count_k, q->count_lds, (const DevQuery*)q->dq_count.p,
                        (const DevSeg*)q->dsegs_count.p, plans, ps, st));
-    PA_HIP(launch_part_offsets(&q->hq, ps, q->grid, st));
-    PA_HIP(launch_scan(STRAT_PEMIT, q->steps, 0, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p,
+    PA_HIP(launch_part_offsets(&q->hq, ps, q->grid, q->count_k, st));
+    PA_HIP(launch_scan(q->emit_strat, q->steps, 0, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p,
                        (const DevSeg*)q->dsegs.p, plans, ps, st));
     PA_HIP(launch_part_agg((const DevQuery*)q->dq.p, ps, q->hq.num_parts, q->part_lds_c, st));
     PA_HIP(hipEventRecord(a->last, st));

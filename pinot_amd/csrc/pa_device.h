@@ -33,6 +33,13 @@ enum ColKind : int32_t { COL_NONE = 0, COL_SV_DICT = 1, COL_SV_RAW = 2, COL_MV_D
 // Two record streams: V (one record per matching doc: COUNT + SUM/MIN/MAX payloads) and H (one record per value of
 // the DISTINCTCOUNTHLL(MV) column: key | register | rank), each with its own key partitioning.
 enum Strategy : int32_t { STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PEMIT = 2, STRAT_PCOUNT = 3 };
+// The emit pass's kernel variant (launch code): the V record format (-1: no V stream) and whether there is an H stream
+// are template parameters, so each variant's record loop is straight-line code (no per-record format branches).
+constexpr int kPemitBase = 16;
+__host__ __device__ constexpr int pemit_strat(int vf, int hh) { return kPemitBase + 2 * (vf + 1) + (hh ? 1 : 0); }
+__host__ __device__ constexpr bool is_pemit(int s) { return s >= kPemitBase; }
+__host__ __device__ constexpr int pemit_vf(int s) { return (s - kPemitBase) / 2 - 1; }
+__host__ __device__ constexpr bool pemit_hh(int s) { return ((s - kPemitBase) & 1) != 0; }
 // V record formats (word 0 always holds the key's offset inside its partition, key & ((1 << kshift_v) - 1)):
 //   V_FMT_KEY: COUNT only, one word;  V_FMT_ID: one word, | value id << kshift_v (the value column's table-wide value
 //   dictionary `vdict`);  V_FMT_32: + the int32 value;  V_FMT_64: + the 64-bit value (int64, or double bits);
@@ -149,7 +156,8 @@ struct DevQuery {
   int32_t hll_agg;           // the partitioned DISTINCTCOUNTHLL(MV) aggregation (-1: no H stream); H record =
                              // key offset << (log2m + 6) | register << 6 | rank << 1 | first
   int32_t emit_val_agg;      // V_FMT_ID/32/64: the aggregation whose column the value comes from (-1: COUNT only)
-  int32_t pad4;
+  int32_t debug_emit;        // measurement only (PA_DEBUG_EMIT): bit 0 skips the emit pass's record stores, bit 1 its HLL
+                             // dictionary gathers, bit 2 its MV value reads (wrong results; isolates the waits)
   uint32_t lds_cnt, lds_done, lds_front, lds_back, lds_start;  // STRAT_PEMIT LDS (bytes): per-partition bin state
   uint32_t lds_bins_v, lds_bins_h;                            // STRAT_PEMIT LDS (bytes): the V and H bins
   const uint64_t* vdict;     // V_FMT_ID: table-wide values of the value column (int64, or double bits)

@@ -677,44 +677,68 @@ __device__ __forceinline__ BinState bin_state(const DevQuery* __restrict__ q, un
 
 #define WG_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP
 
-// One record (nw words of r) into partition p's LDS bin of BS records. The lane whose write completes the bin stores
-// the whole bin (BS * nw words, whole 16-byte units) at the range's front slot, then empties it; a record arriving
-// while the bin is full goes straight to the back end of the range. Every (workgroup, partition) range holds exactly
-// the records the count pass counted, so front and back meet (checked at the end of the pass).
+// Wave-level put: every lane calls it (uniform control flow); an active lane puts one record (the first nw words of
+// r) into partition p's LDS bin of BS records (bins: the stream's partitions from p0 on, BS * nw words each). The lane whose write
+// completes a bin marks it; then the whole wave stores every marked bin (BS * nw words as whole 16-byte units, one
+// per lane: one store instruction per bin instead of one lane's serial loop) at its range's front slot and empties
+// it. A record arriving while its bin is full goes straight to the back end of the range. Every (workgroup,
+// partition) range holds exactly the records the count pass counted, so front and back meet (checked at the end).
 // Ordering: LDS executes the DS instructions of one wave in issue order and serialises those of different waves, so
 // "write the slot, then count it done" and "read the bin, then reset the counters" need only the compiler to keep
 // program order (a signal fence). Acquire/release atomics would also wait for every outstanding global load, i.e.
-// drain the tile ring's LDS-DMA on every record.
+// drain the tile ring's LDS-DMA on every record. Only the wave that completed a bin touches its front and counters
+// until it resets them.
 template <int WM>
-__device__ __forceinline__ void bin_put(const BinState& B, uint32_t p, lds_u32_t* bin, uint32_t BS, int nw,
-                                        const uint32_t (&r)[WM], AS1 uint32_t* recs) {
-  const uint32_t s = __hip_atomic_fetch_add(B.cnt + p, 1u, WG_RLX);
-  if (s < BS) {
+__device__ __forceinline__ void bin_put_wave(const BinState& B, bool active, uint32_t p, uint32_t p0, lds_u32_t* bins,
+                                             uint32_t BS, uint32_t nw, const uint32_t (&r)[WM], AS1 uint32_t* recs,
+                                             int lane, int dbg) {
+  bool full = false;
+  if (active) {
+    const uint32_t s = __hip_atomic_fetch_add(B.cnt + p, 1u, WG_RLX);
+    if (s < BS) {
+      lds_u32_t* slot = bins + ((p - p0) * BS + s) * nw;
 #pragma unroll
-    for (int w = 0; w < WM; ++w)
-      if (w < nw) bin[s * (uint32_t)nw + w] = r[w];
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const uint32_t f = __hip_atomic_fetch_add(B.done + p, 1u, WG_RLX);
-    if (f == BS - 1u) {
+      for (int w = 0; w < WM; ++w)
+        if ((uint32_t)w < nw) slot[w] = r[w];
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      const uint32_t o = B.front[p];
-      B.front[p] = o + BS;
-      AS1 u32x4* d = (AS1 u32x4*)(recs + (B.start[p] + o) * (uint64_t)nw);
-      const lds_u32x4_t* sb = (const lds_u32x4_t*)bin;
-      const uint32_t n16 = (BS * (uint32_t)nw) >> 2;
-      for (uint32_t i = 0; i < n16; ++i) d[i] = sb[i];
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      full = __hip_atomic_fetch_add(B.done + p, 1u, WG_RLX) == BS - 1u;
+    } else if (!(dbg & 1)) {
+      const uint32_t o = __hip_atomic_fetch_sub(B.back + p, 1u, WG_RLX) - 1u;
+      AS1 uint32_t* d = recs + (B.start[p] + o) * (uint64_t)nw;
+#pragma unroll
+      for (int w = 0; w < WM; ++w)
+        if ((uint32_t)w < nw) d[w] = r[w];
+    }
+  }
+  uint64_t fm = __ballot(full);
+  if (fm == 0) return;
+  if (dbg & 1) {  // (measurement only: drop the bins)
+    if (full) {
       __hip_atomic_store(B.done + p, 0u, WG_RLX);
       __hip_atomic_store(B.cnt + p, 0u, WG_RLX);
     }
-  } else {
-    const uint32_t o = __hip_atomic_fetch_sub(B.back + p, 1u, WG_RLX) - 1u;
-    AS1 uint32_t* d = recs + (B.start[p] + o) * (uint64_t)nw;
-#pragma unroll
-    for (int w = 0; w < WM; ++w)
-      if (w < nw) d[w] = r[w];
+    return;
+  }
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  const uint32_t n16 = (BS * nw) >> 2;
+  while (fm) {
+    const int l = __builtin_ctzll(fm);
+    fm &= fm - 1;
+    const uint32_t pp = (uint32_t)__builtin_amdgcn_readlane((int)p, l);
+    const uint32_t o = B.front[pp];  // (every lane reads the same word: a broadcast)
+    AS1 u32x4* d = (AS1 u32x4*)(recs + (B.start[pp] + o) * (uint64_t)nw);
+    const lds_u32x4_t* sb = (const lds_u32x4_t*)(bins + (pp - p0) * BS * nw);
+    for (uint32_t c = (uint32_t)lane; c < n16; c += kWave) d[c] = sb[c];
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (lane == 0) {
+      B.front[pp] = o + BS;
+      __hip_atomic_store(B.done + pp, 0u, WG_RLX);
+      __hip_atomic_store(B.cnt + pp, 0u, WG_RLX);
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
   }
 }
+
 
 // The matching docs of one tile (match words m) in the count pass (STRAT_PCOUNT: per (workgroup, partition) record
 // counts in LDS) or the emit pass (STRAT_PEMIT: the records into the partition bins). Per batch of 8 steps: every
@@ -784,18 +808,20 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
         if (ha >= 0) __hip_atomic_fetch_add(hist + pv + (key[i] >> ksh), n[i], WG_RLX);
       }
     } else {
+      constexpr int VF = pemit_vf(STRAT);
       const BinState B = bin_state(q, lds);
-      if (pv) {
+      const int dbg = q->debug_emit;
+      if constexpr (VF >= 0) {
         // V records: the value (or its table-wide value id) of the one payload column, batched like the keys
-        const int fmt = q->v_fmt;
-        const int W = q->rec_words_v;
+        constexpr int NW = VF == V_FMT_GEN ? kMaxVWords : (VF == V_FMT_32 ? 2 : (VF == V_FMT_64 ? 3 : 1));
+        const uint32_t W = VF == V_FMT_GEN ? (uint32_t)q->rec_words_v : (uint32_t)NW;
         const uint32_t BS = (uint32_t)q->bs_v;
         lds_u32_t* bins = lds_ptr(lds + q->lds_bins_v);
         const uint32_t kmask = (1u << ksv) - 1u;
         uint32_t lo[kEB], hi[kEB];
 #pragma unroll
         for (int i = 0; i < kEB; ++i) lo[i] = hi[i] = 0u;
-        if (fmt == V_FMT_ID || fmt == V_FMT_32 || fmt == V_FMT_64) {
+        if constexpr (VF == V_FMT_ID || VF == V_FMT_32 || VF == V_FMT_64) {
           const int va = q->emit_val_agg;
           const int vslot = q->aggs[va].slot;
           const int vkind = cs->cols[vslot].kind;
@@ -805,25 +831,45 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
                                                               : (const uint64_t*)cs->cols[vslot].dict_i64;
           const int32_t* vrm = cs->vremap;
           const void* vraw = cs->cols[vslot].raw;
+          if (vkind == COL_SV_DICT) {
+            uint32_t vid[kEB];
 #pragma unroll
-          for (int i = 0; i < kEB; ++i) {
-            if (!((m >> (h + i)) & 1u)) continue;
-            const int dl = local(h + i);
-            const int64_t doc = doc_base + dl;
-            if (vkind == COL_SV_DICT) {
-              const uint32_t vid = vl >= 0 ? decode_lds(img + vl, dl, vn) : decode_global(vw, doc, vn);
-              if (fmt == V_FMT_ID) {
-                lo[i] = vrm != nullptr ? (uint32_t)gp(vrm)[vid] : vid;
-              } else {
-                const uint64_t v = gp(vd)[vid];
+            for (int i = 0; i < kEB; ++i) {
+              vid[i] = 0u;
+              if ((m >> (h + i)) & 1u) {
+                const int dl = local(h + i);
+                vid[i] = vl >= 0 ? decode_lds(img + vl, dl, vn) : decode_global(vw, doc_base + dl, vn);
+              }
+            }
+            if constexpr (VF == V_FMT_ID) {
+              if (vrm != nullptr) {
+#pragma unroll
+                for (int i = 0; i < kEB; ++i)
+                  if ((m >> (h + i)) & 1u) vid[i] = (uint32_t)gp(vrm)[vid[i]];
+              }
+#pragma unroll
+              for (int i = 0; i < kEB; ++i) lo[i] = vid[i];
+            } else {
+#pragma unroll
+              for (int i = 0; i < kEB; ++i) {
+                if (!((m >> (h + i)) & 1u)) continue;
+                const uint64_t v = gp(vd)[vid[i]];
                 lo[i] = (uint32_t)v;
                 hi[i] = (uint32_t)(v >> 32);
               }
-            } else if (vtype == PA_INT) {
-              lo[i] = (uint32_t)gp((const int32_t*)vraw)[doc];
+            }
+          } else if (vtype == PA_INT) {
+#pragma unroll
+            for (int i = 0; i < kEB; ++i) {
+              if (!((m >> (h + i)) & 1u)) continue;
+              lo[i] = (uint32_t)gp((const int32_t*)vraw)[doc_base + local(h + i)];
               hi[i] = (uint32_t)((int32_t)lo[i] >> 31);
-            } else {  // LONG, or DOUBLE bits (a SUM/MIN/MAX over a raw DOUBLE column reads the bits unchanged)
-              const uint64_t v = gp((const uint64_t*)vraw)[doc];
+            }
+          } else {  // LONG, or DOUBLE bits (a SUM/MIN/MAX over a raw DOUBLE column reads the bits unchanged)
+#pragma unroll
+            for (int i = 0; i < kEB; ++i) {
+              if (!((m >> (h + i)) & 1u)) continue;
+              const uint64_t v = gp((const uint64_t*)vraw)[doc_base + local(h + i)];
               lo[i] = (uint32_t)v;
               hi[i] = (uint32_t)(v >> 32);
             }
@@ -831,42 +877,45 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
         }
 #pragma unroll
         for (int i = 0; i < kEB; ++i) {
-          if (!((m >> (h + i)) & 1u)) continue;
+          const bool mine = (m >> (h + i)) & 1u;
+          if (__ballot(mine) == 0) continue;
           const uint32_t p = key[i] >> ksv;
-          uint32_t r[kMaxVWords];
+          uint32_t r[NW];
           r[0] = key[i] & kmask;
 #pragma unroll
-          for (int w = 1; w < kMaxVWords; ++w) r[w] = 0u;
-          if (fmt == V_FMT_ID) {
+          for (int w = 1; w < NW; ++w) r[w] = 0u;
+          if constexpr (VF == V_FMT_ID) {
             r[0] |= lo[i] << ksv;
-          } else if (fmt == V_FMT_32) {
+          } else if constexpr (VF == V_FMT_32) {
             r[1] = lo[i];
-          } else if (fmt == V_FMT_64) {
+          } else if constexpr (VF == V_FMT_64) {
             r[1] = lo[i];
             r[2] = hi[i];
-          } else if (fmt == V_FMT_GEN) {
-            const int dl = local(h + i);
-            const int64_t doc = doc_base + dl;
-            for (int a = 0; a < q->num_aggs; ++a) {
-              const DevAgg& A = q->aggs[a];
-              if (A.type == PA_AGG_COUNT || a == ha) continue;
-              const AggValue v = agg_value(A, a, seg, img, dl, doc);
-              const int po = A.pay_off;
-              if (A.src == SRC_INT) {
-                if (po < kMaxVWords) r[po] = (uint32_t)v.i;
-              } else {
-                const int64_t b = A.src == SRC_DOUBLE ? __builtin_bit_cast(int64_t, v.d) : v.i;
-                if (po + 1 < kMaxVWords) {
-                  r[po] = (uint32_t)b;
-                  r[po + 1] = (uint32_t)(b >> 32);
+          } else if constexpr (VF == V_FMT_GEN) {
+            if (mine) {
+              const int dl = local(h + i);
+              const int64_t doc = doc_base + dl;
+              for (int a = 0; a < q->num_aggs; ++a) {
+                const DevAgg& A = q->aggs[a];
+                if (A.type == PA_AGG_COUNT || a == ha) continue;
+                const AggValue v = agg_value(A, a, seg, img, dl, doc);
+                const int po = A.pay_off;
+                if (A.src == SRC_INT) {
+                  if (po < kMaxVWords) r[po] = (uint32_t)v.i;
+                } else {
+                  const int64_t b = A.src == SRC_DOUBLE ? __builtin_bit_cast(int64_t, v.d) : v.i;
+                  if (po + 1 < kMaxVWords) {
+                    r[po] = (uint32_t)b;
+                    r[po + 1] = (uint32_t)(b >> 32);
+                  }
                 }
               }
             }
           }
-          bin_put<kMaxVWords>(B, p, bins + p * BS * (uint32_t)W, BS, W, r, gp(ps.recs_v));
+          bin_put_wave<NW>(B, mine, p, 0u, bins, BS, W, r, gp(ps.recs_v), lane, dbg);
         }
       }
-      if (ha >= 0) {
+      if constexpr (pemit_hh(STRAT)) {
         // H records, value-parallel per step: each matching lane's doc owns n = max(1, values) consecutive records of
         // the step; lane j takes record g = b + j, finds its owner by a 6-shuffle binary search over the inclusive
         // prefix sums of n, and decodes that value (coalesced MV reads, no per-lane loop over a doc's values)
@@ -927,15 +976,16 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
               ok[k] = g < total ? (hmv ? ((int32_t)e < o_nv ? 2 : 1) : 1) : 0;  // 2: an MV value to look up
               pk[k] = o_key >> ksh;
               w0[k] = ((o_key & kmask) << fsh) | (e == 0 ? first_bit : 0u);
-              id[k] = ok[k] == 2 ? decode_global(hwords, (int64_t)o_v0 + e, hnb) : (hmv ? 0u : o_hv);
+              id[k] = ok[k] == 2 ? ((dbg & 4) ? e : decode_global(hwords, (int64_t)o_v0 + e, hnb)) : (hmv ? 0u : o_hv);
             }
+            uint32_t hv[kHB];
+#pragma unroll
+            for (int k = 0; k < kHB; ++k) hv[k] = ok[k] == 2 && !(dbg & 2) ? gp(hlut)[id[k]] : id[k];  // (register << 8) | rank
 #pragma unroll
             for (int k = 0; k < kHB; ++k) {
-              if (!ok[k]) continue;
-              const uint32_t hv = ok[k] == 2 ? gp(hlut)[id[k]] : id[k];  // (register << 8) | rank (rank 0: no value)
-              const uint32_t r[1] = {w0[k] | ((hv >> 8) << 6) | ((hv & 0xffu) << 1)};
-              const uint32_t ph = pk[k];
-              bin_put<1>(B, (uint32_t)pv + ph, bins + ph * BS, BS, 1, r, gp(ps.recs_h));
+              if (__ballot(ok[k] != 0) == 0) break;  // (chunks fill in order: the rest are empty too)
+              const uint32_t r[1] = {w0[k] | ((hv[k] >> 8) << 6) | ((hv[k] & 0xffu) << 1)};
+              bin_put_wave<1>(B, ok[k] != 0, (uint32_t)pv + pk[k], (uint32_t)pv, bins, BS, 1u, r, gp(ps.recs_h), lane, dbg);
             }
           }
         }
@@ -975,7 +1025,7 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
     }
     if (__ballot(m != 0) == 0) return 0;
   }
-  if constexpr (STRAT == STRAT_PCOUNT || STRAT == STRAT_PEMIT) {
+  if constexpr (STRAT == STRAT_PCOUNT || is_pemit(STRAT)) {
     part_tile<STRAT, STEPS, LM>(q, seg, img, doc_base, m, lane, lds, ps);
   } else if (q->has_mv) {
     for (int i = 0; i < STEPS; ++i)
@@ -1278,7 +1328,7 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
     uint32_t* hist = (uint32_t*)lds_acc;
     for (int p = threadIdx.x; p < q->num_parts; p += kWGSize) hist[p] = 0u;
     __syncthreads();
-  } else if (STRAT == STRAT_PEMIT) {
+  } else if (is_pemit(STRAT)) {
     // every partition's bin empty; its range in the stream: the partition base + this workgroup's offset (part_scan),
     // holding exactly the records the count pass counted here
     const BinState B = bin_state(q, lds_acc);
@@ -1416,7 +1466,7 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
     }
   }
 
-  if (STRAT != STRAT_PEMIT) {  // (the partitioned count pass counts numDocsScanned; its emit pass sees the same docs)
+  if (!is_pemit(STRAT)) {  // (the partitioned count pass counts numDocsScanned; its emit pass sees the same docs)
     const int64_t wm = wave_sum_i64((int64_t)matched);
     if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)wm, RLX);
   }
@@ -1425,7 +1475,7 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
     const uint32_t* hist = (const uint32_t*)lds_acc;
     for (int p = threadIdx.x; p < q->num_parts; p += kWGSize) gp(ps.hist)[lb * q->num_parts + p] = hist[p];
   }
-  if (STRAT == STRAT_PEMIT) {
+  if (is_pemit(STRAT)) {
     // every bin's rest (< one bin) between the range's front and back, then sentinel records up to the padded end
     __syncthreads();
     const BinState B = bin_state(q, lds_acc);
@@ -1836,9 +1886,13 @@ __device__ __forceinline__ uint64_t block_exclusive_scan_256_u64(uint64_t v, uin
   return incl - v;
 }
 
-// Block p: exclusive scan over the G workgroups of partition p's record counts, each rounded up to whole bins of the
-// partition's stream (-> off[wg][p], relative to the partition); the padded total -> the partition's base slot.
-__global__ void __launch_bounds__(256) part_scan_kernel(const uint32_t* hist, uint32_t* off, int G, int P, int pv,
+// Block p: exclusive scan over the G emit workgroups of partition p's record counts, each rounded up to whole bins of
+// the partition's stream (-> off[wg][p], relative to the partition); the padded total -> the partition's base slot.
+// The count pass ran k workgroups per emit workgroup (more resident waves: it stages fewer columns): emit workgroup wg
+// walked exactly the tiles of count workgroups [wg*k, wg*k + k) (both split the tiles by the same formula), so its
+// counts are the sum of those k rows, stored back into row wg (rows wg*k.. are read before any row is written: the
+// scan's barriers separate them, and a later chunk of 256 reads only rows >= its own first row * k).
+__global__ void __launch_bounds__(256) part_scan_kernel(uint32_t* hist, uint32_t* off, int G, int k, int P, int pv,
                                                         uint32_t bs_v, uint32_t bs_h, uint64_t* base) {
   __shared__ uint64_t sh[256];
   const int p = blockIdx.x;
@@ -1846,10 +1900,16 @@ __global__ void __launch_bounds__(256) part_scan_kernel(const uint32_t* hist, ui
   uint64_t carry = 0;
   for (int b0 = 0; b0 < G; b0 += 256) {
     const int wg = b0 + threadIdx.x;
-    const uint64_t x = wg < G ? (uint64_t)((hist[(size_t)wg * P + p] + bs - 1u) / bs * bs) : 0ull;
+    uint32_t n = 0;
+    if (wg < G)
+      for (int j = 0; j < k; ++j) n += hist[((size_t)wg * k + j) * P + p];
+    const uint64_t x = (uint64_t)((n + bs - 1u) / bs * bs);
     uint64_t tot;
     const uint64_t ex = block_exclusive_scan_256_u64(x, sh, &tot);
-    if (wg < G) off[(size_t)wg * P + p] = (uint32_t)(carry + ex);
+    if (wg < G) {
+      off[(size_t)wg * P + p] = (uint32_t)(carry + ex);
+      if (k > 1) hist[(size_t)wg * P + p] = n;
+    }
     carry += tot;
   }
   if (threadIdx.x == 0) base[p < pv ? p : p + 1] = carry;
@@ -2048,9 +2108,9 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
   else part_agg_h(q, ps, (int)blockIdx.x - q->pv, (unsigned char*)smem);
 }
 
-hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G, hipStream_t s) {
+hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G, int k, hipStream_t s) {
   const int P = hq->num_parts, pv = hq->pv;
-  part_scan_kernel<<<P, 256, 0, s>>>(ps.hist, ps.off, G, P, pv, (uint32_t)hq->bs_v, (uint32_t)hq->bs_h, ps.base);
+  part_scan_kernel<<<P, 256, 0, s>>>(ps.hist, ps.off, G, k, P, pv, (uint32_t)hq->bs_v, (uint32_t)hq->bs_h, ps.base);
   if (pv > 0) scan_u64_kernel<<<1, 256, 0, s>>>(ps.base, pv);
   if (P > pv) scan_u64_kernel<<<1, 256, 0, s>>>(ps.base + pv + 1, P - pv);
   return hipGetLastError();
@@ -2110,8 +2170,14 @@ static const void* scan_fn_s(int steps, int lm) {
 static const void* scan_fn(int strategy, int steps, int lm) {
   switch (strategy) {
     case STRAT_LDS: return scan_fn_s<STRAT_LDS>(steps, lm);
-    case STRAT_PEMIT: return (const void*)scan_kernel<STRAT_PEMIT, 16, 0>;    // the planner's only partitioned layout
-    case STRAT_PCOUNT: return (const void*)scan_kernel<STRAT_PCOUNT, 16, 0>;
+    case STRAT_PCOUNT: return (const void*)scan_kernel<STRAT_PCOUNT, 16, 0>;  // the planner's only partitioned layout
+#define PA_PEMIT_CASE(VF, HH) \
+  case pemit_strat(VF, HH): return (const void*)scan_kernel<pemit_strat(VF, HH), 16, 0>;
+    PA_PEMIT_CASE(-1, 1)
+    PA_PEMIT_CASE(V_FMT_KEY, 0) PA_PEMIT_CASE(V_FMT_KEY, 1) PA_PEMIT_CASE(V_FMT_ID, 0) PA_PEMIT_CASE(V_FMT_ID, 1)
+    PA_PEMIT_CASE(V_FMT_32, 0) PA_PEMIT_CASE(V_FMT_32, 1) PA_PEMIT_CASE(V_FMT_64, 0) PA_PEMIT_CASE(V_FMT_64, 1)
+    PA_PEMIT_CASE(V_FMT_GEN, 0) PA_PEMIT_CASE(V_FMT_GEN, 1)
+#undef PA_PEMIT_CASE
     default: return scan_fn_s<STRAT_GLOBAL>(steps, lm);
   }
 }

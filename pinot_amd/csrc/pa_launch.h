@@ -44,8 +44,9 @@ hipError_t launch_hll_lut_hashes(const int32_t* hashes, int32_t card, int32_t lo
 hipError_t launch_fill_i64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
 hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t* keys, int64_t n, void* out,
                          hipStream_t s);
-// partitioned aggregation: per-(workgroup, partition) range offsets + partition bases (after the count pass)
-hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G, hipStream_t s);
+// partitioned aggregation: per-(workgroup, partition) range offsets + partition bases (after the count pass, which ran
+// k workgroups per emit workgroup)
+hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G, int k, hipStream_t s);
 hipError_t set_part_agg_lds_limit(int lds_bytes);
 hipError_t launch_part_agg(const DevQuery* q, const PartScratch& ps, int P, int lds_bytes, hipStream_t s);
 hipError_t set_scan_lds_limit(int strategy, int steps, int lm, int bytes);

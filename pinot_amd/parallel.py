@@ -22,6 +22,7 @@ SECTION_OP = {
     L.PA_ACC_MAX_I64: dist.ReduceOp.MAX,
     L.PA_ACC_HLL_U8: dist.ReduceOp.MAX,
     L.PA_ACC_DOCS_U64: dist.ReduceOp.SUM,
+    L.PA_ACC_PRESENCE_U8: dist.ReduceOp.MAX,  # DISTINCTCOUNT value presence bytes (set union)
     L.PA_ACC_KEYS_I64: None,  # not element-wise reducible (hashed key spaces)
 }
 SECTION_DTYPE = {
@@ -33,8 +34,16 @@ SECTION_DTYPE = {
     L.PA_ACC_MAX_I64: torch.int64,
     L.PA_ACC_HLL_U8: torch.uint8,  # one byte per register (HyperLogLog.addAll == register max)
     L.PA_ACC_DOCS_U64: torch.int64,
+    L.PA_ACC_PRESENCE_U8: torch.uint8,
     L.PA_ACC_KEYS_I64: torch.int64,
 }
+# identity of each per-key section (what pa_query_reset leaves in an empty slot)
+SECTION_IDENTITY = {
+    L.PA_ACC_MIN_I64: (1 << 63) - 1,
+    L.PA_ACC_MAX_I64: -(1 << 63),
+    L.PA_ACC_KEYS_I64: (1 << 63) - 1,  # the empty-slot marker
+}
+_SCATTER_REDUCE = {dist.ReduceOp.SUM: "sum", dist.ReduceOp.MIN: "amin", dist.ReduceOp.MAX: "amax"}
 
 
 def shard_segments(num_segments, rank, world_size):
@@ -65,6 +74,103 @@ def merge_results_across_ranks(executor, dst=0, group=None):
     gathered = [None] * world if rank == dst else None
     dist.gather_object(res, gathered, dst=dst, group=group)
     return merge_intermediate(gathered) if rank == dst else None
+
+
+def merge_hashed_sections(views, num_slots, group=None):
+    """Device-side merge of hashed key spaces across ranks (GroupByCombineOperator semantics, value-keyed: a packed key
+    means the same group values on every rank once parallel.table_layout agreed the dictionaries, but sits in a
+    different slot of each rank's table). views: [(section kind, 1-D tensor)] of ONE rank's accumulator block, the
+    per-key sections holding num_slots rows each (row width = elements / num_slots) plus the PA_ACC_DOCS_U64 counters.
+
+    Every rank: compact its occupied slots (count > 0) into byte rows, all-gather them over the collective backend
+    (RCCL on GPUs), then merge by packed key on its own device — torch.unique over the keys and one scatter-reduce per
+    section (SUM for counts/sums, MIN, MAX for maxima, HLL registers and DISTINCTCOUNT presence) — and write the merged
+    groups back into the block: slots [0, groups) in ascending key order, every other slot empty. pa_query_fetch reads
+    slots by count and key, not by position, so the executor's own fetch then returns the merged result on every rank.
+    Raises when the merged groups do not fit the table."""
+    kinds = [k for k, _ in views]
+    if L.PA_ACC_KEYS_I64 not in kinds or L.PA_ACC_COUNT_U64 not in kinds:
+        raise L.PinotAmdError("merge_hashed_sections: the block has no key or count section")
+    docs = [t for k, t in views if k == L.PA_ACC_DOCS_U64]
+    per_key = [(k, t) for k, t in views if k != L.PA_ACC_DOCS_U64]
+    for t in docs:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    count = dict(per_key)[L.PA_ACC_COUNT_U64]
+    dev = count.device
+    occ = torch.nonzero(count.view(num_slots) > 0).flatten()
+    m = int(occ.numel())
+    # one byte row per occupied slot: every per-key section's row, concatenated
+    parts, layout = [], []
+    for k, t in per_key:
+        w = t.numel() // num_slots
+        rows = t.view(num_slots, w)[occ]
+        b = rows.contiguous().view(torch.uint8).view(m, -1) if m else torch.empty(0, w * t.element_size(),
+                                                                                  dtype=torch.uint8, device=dev)
+        layout.append((k, t.dtype, w, b.shape[1]))
+        parts.append(b)
+    local = torch.cat(parts, dim=1) if parts else torch.empty(m, 0, dtype=torch.uint8, device=dev)
+    rb = local.shape[1]
+    world = dist.get_world_size(group)
+    sizes = torch.tensor([m], dtype=torch.int64, device=dev)
+    all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
+    dist.all_gather(all_sizes, sizes, group=group)
+    ns = [int(s.item()) for s in all_sizes]
+    mx = max(ns)
+    padded = torch.zeros(mx, rb, dtype=torch.uint8, device=dev)
+    padded[:m] = local
+    gathered = [torch.empty_like(padded) for _ in range(world)]
+    dist.all_gather(gathered, padded, group=group)
+    rows = torch.cat([g[:n] for g, n in zip(gathered, ns)], dim=0)
+    # unpack per section, merge by packed key
+    cols, o = {}, 0
+    for k, dt, w, nb in layout:
+        cols[k] = rows[:, o:o + nb].contiguous().view(dt).view(-1, w)
+        o += nb
+    keys = cols[L.PA_ACC_KEYS_I64][:, 0]
+    uniq, inv = torch.unique(keys, sorted=True, return_inverse=True)
+    u = int(uniq.numel())
+    if u > num_slots:
+        raise L.PinotAmdError("merged groups (%d) exceed the hashed table's %d slots" % (u, num_slots))
+    for k, t in per_key:
+        w = t.numel() // num_slots
+        out = t.view(num_slots, w)
+        out.fill_(SECTION_IDENTITY.get(k, 0))
+        if k == L.PA_ACC_KEYS_I64:
+            out[:u, 0] = uniq
+            continue
+        acc = torch.full((u, w), SECTION_IDENTITY.get(k, 0), dtype=t.dtype, device=dev)
+        acc.scatter_reduce_(0, inv.view(-1, 1).expand(-1, w), cols[k], reduce=_SCATTER_REDUCE[SECTION_OP[k]],
+                            include_self=True)
+        out[:u] = acc
+    return u
+
+
+class HashedAccumulators:
+    """The hashed-key-space counterpart of DistributedAccumulators: moves an executor's accumulator block into a
+    torch-owned device buffer (construct it BEFORE executing the query: the block is relocated, not copied), and
+    merge() runs merge_hashed_sections over it on every rank, after which executor.fetch() returns the merged groups
+    on every rank."""
+
+    def __init__(self, executor, device):
+        if not getattr(executor, "hashed", False):
+            raise L.PinotAmdError("HashedAccumulators: direct key spaces reduce element-wise (DistributedAccumulators)")
+        lib = L.lib()
+        nbytes = int(lib.pa_query_accumulator_bytes(executor.handle))
+        self.buf = torch.zeros(nbytes + 512, dtype=torch.uint8, device=device)
+        pad = (-self.buf.data_ptr()) % 256
+        base = self.buf.data_ptr() + pad
+        L.check(lib.pa_query_set_accumulator_buffer(executor.handle, base, nbytes), "set_accumulator_buffer")
+        executor._acc_owner = self.buf  # the library reads and writes this block for the executor's lifetime
+        self.num_slots = int(executor.num_keys)
+        self.views = []
+        for kind, ptr, n in executor.sections():
+            off = ptr - self.buf.data_ptr()
+            dt = SECTION_DTYPE[kind]
+            es = torch.empty(0, dtype=dt).element_size()
+            self.views.append((kind, self.buf[off:off + n * es].view(dt)))
+
+    def merge(self, group=None):
+        return merge_hashed_sections(self.views, self.num_slots, group=group)
 
 
 def section_runs(sections):

@@ -82,3 +82,35 @@ def test_two_rank_merge_with_table_dictionaries(sql, rccl_world1):
         for g in gsegs:
             for x in g:
                 x.close()
+
+
+@pytest.mark.parametrize("sql", [
+    "SELECT r, COUNT(*), SUM(m), MIN(f), MAX(m), DISTINCTCOUNTHLL(d1) FROM t GROUP BY r LIMIT 100000",
+    "SELECT d1, r, COUNT(*), AVG(f) FROM t WHERE m > 0 GROUP BY d1, r LIMIT 100000",
+])
+def test_hashed_key_space_device_merge(sql, rccl_world1):
+    """HashedAccumulators on a hashed key space (GROUP BY a raw column): the block moves into a torch buffer, the
+    RCCL merge (world size 1: all-gather of this rank's compacted rows, merge by packed key) rewrites it as groups
+    [0, n) in key order, and the library's own fetch of the rewritten block equals the oracle."""
+    from pinot_amd.parallel import HashedAccumulators
+    cols = dict(COLS, r=("LONG", 0))
+    segs = [make_segment(900 + i, n, cols, no_dict=("r",)) for i, n in enumerate((15013, 9001))]
+    q = parse_sql(sql)
+    gsegs = [GpuSegment(s) for s in segs]
+    ex = GpuQueryExecutor(q, gsegs)
+    try:
+        assert ex.hashed
+        acc = HashedAccumulators(ex, torch.device("cuda", 0))
+        ex.execute()
+        torch.cuda.synchronize()
+        before = ex.fetch()
+        n = acc.merge()
+        torch.cuda.synchronize()
+        got = ex.fetch()
+        assert n == len(got.groups) == len(before.groups)
+        exp = oracle.run_query(q, segs)
+        assert_same(got, exp, rel=1e-9)
+    finally:
+        ex.close()
+        for g in gsegs:
+            g.close()

@@ -322,3 +322,88 @@ def test_gloo_table_layout_agrees_on_wide_sums():
     out = mgr.dict()
     mp.spawn(_layout_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     assert out[0] == out[1] == (["k"], ["m"])
+
+
+NS = 64  # hashed table slots per rank
+HLOG = 4  # HLL log2m of the hashed-merge test (16 registers per key)
+
+
+def _hashed_partial(rank):
+    """One rank's hashed table: 20 groups at random slots (keys from a shared pool of 30, so ranks overlap), every
+    other slot empty (key INT64_MAX, count 0, identities) — the block pa_query_scan leaves for a hashed key space."""
+    rng = np.random.default_rng(700 + rank)
+    pool = np.array([-(1 << 62), -5, 0, 3, (1 << 63) - 1] + list(range(100, 125)), dtype=np.int64)
+    keys_used = rng.choice(pool, size=20, replace=False)
+    slots = rng.choice(NS, size=20, replace=False)
+    keys = np.full(NS, (1 << 63) - 1, np.int64)
+    count = np.zeros(NS, np.int64)
+    sx2 = np.zeros(2 * NS, np.int64)
+    dsum = np.zeros(NS)
+    dmin = np.full(NS, (1 << 63) - 1, np.int64)
+    imax = np.full(NS, -(1 << 63), np.int64)
+    hll = np.zeros(NS << HLOG, np.uint8)
+    pres = np.zeros(NS * 16, np.uint8)
+    groups = {}
+    for k, s in zip(keys_used.tolist(), slots.tolist()):
+        keys[s] = k
+        count[s] = rng.integers(1, 50)
+        v = int(rng.integers(-(1 << 40), 1 << 40))
+        sx2[2 * s], sx2[2 * s + 1] = v & 0xFFFFFFFF, v >> 32
+        dsum[s] = rng.standard_normal()
+        dmin[s] = f64_order_encode(rng.standard_normal() * 100)
+        imax[s] = rng.integers(-1000, 1000)
+        hll[s << HLOG:(s + 1) << HLOG] = rng.integers(0, 20, 1 << HLOG)
+        pres[s * 16:(s + 1) * 16] = rng.integers(0, 2, 16)
+        groups[k] = (int(count[s]), v, float(dsum[s]), int(dmin[s]), int(imax[s]),
+                     hll[s << HLOG:(s + 1) << HLOG].copy(), pres[s * 16:(s + 1) * 16].copy())
+    secs = [(L.PA_ACC_COUNT_U64, count), (L.PA_ACC_SUM_I64X2, sx2), (L.PA_ACC_SUM_F64, dsum),
+            (L.PA_ACC_MIN_I64, dmin), (L.PA_ACC_MAX_I64, imax), (L.PA_ACC_HLL_U8, hll),
+            (L.PA_ACC_PRESENCE_U8, pres), (L.PA_ACC_KEYS_I64, keys),
+            (L.PA_ACC_DOCS_U64, np.array([1000 + rank, 0, 0, 0], np.int64))]
+    return secs, groups
+
+
+def _hashed_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pinot_amd.parallel import merge_hashed_sections
+    secs, _ = _hashed_partial(rank)
+    views = [(k, torch.from_numpy(np.ascontiguousarray(a)).to(SECTION_DTYPE[k])) for k, a in secs]
+    u = merge_hashed_sections(views, NS)
+    out[rank] = (u, [t.numpy().copy() for _, t in views])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_device_side_merge_of_hashed_key_spaces():
+    """parallel.merge_hashed_sections (the RCCL path of hashed key spaces: all-gather of compacted rows + merge by
+    packed key) reproduces the key-based merge of GroupByCombineOperator on every rank, in the block layout the
+    library's fetch reads (groups in ascending key order, every other slot empty)."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_hashed_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    exp = {}
+    for r in range(world):
+        for k, (c, v, ds, mn, mx, h, p) in _hashed_partial(r)[1].items():
+            if k in exp:
+                e = exp[k]
+                exp[k] = (e[0] + c, e[1] + v, e[2] + ds, min(e[3], mn), max(e[4], mx), np.maximum(e[5], h),
+                          np.maximum(e[6], p))
+            else:
+                exp[k] = (c, v, ds, mn, mx, h, p)
+    ks = sorted(exp)
+    for r in range(world):
+        u, (count, sx2, dsum, dmin, imax, hll, pres, keys, docs) = out[r]
+        assert u == len(ks)
+        assert keys[:u].tolist() == ks and (keys[u:] == (1 << 63) - 1).all()
+        assert (count[u:] == 0).all() and (dmin[u:] == (1 << 63) - 1).all() and (imax[u:] == -(1 << 63)).all()
+        assert docs.tolist() == [2001, 0, 0, 0]
+        for i, k in enumerate(ks):
+            c, v, ds, mn, mx, h, p = exp[k]
+            assert count[i] == c
+            assert int(sx2[2 * i]) + (int(sx2[2 * i + 1]) << 32) == v
+            assert abs(dsum[i] - ds) <= 1e-12 * max(1.0, abs(ds))
+            assert dmin[i] == mn and imax[i] == mx
+            assert np.array_equal(hll[i << HLOG:(i + 1) << HLOG], h)
+            assert np.array_equal(pres[i * 16:(i + 1) * 16], p)
