@@ -276,6 +276,16 @@ int32_t pa_query_limit_trimming(const pa_query* q);
  * error. */
 int64_t pa_query_num_groups_limit_reached(const pa_query* q);
 
+/* Per-leaf doc bitmaps of one bound segment, for the execution statistics (numEntriesScannedInFilter): the reference
+ * counts the docs its filter operators scan (SVScanDocIdIterator.java:76-142: next / advance / applyAnd; AndDocIdSet /
+ * OrDocIdSet iterator construction), which depends on which docs each predicate matches and on the segment's indexes,
+ * so the host restates that accounting (pinot_amd/filter_stats.py) over these bitmaps. Writes, for every filter leaf l
+ * of the spec (pa_query_spec.leaves order), pa_query_leaf_bitmap_words(q, segment) 32-bit words at device_out +
+ * l * words: bit (doc & 31) of word (doc >> 5) = the leaf's predicate (with its per-segment negate) on doc.
+ * Asynchronous on `stream`. */
+int64_t pa_query_leaf_bitmap_words(const pa_query* q, int32_t segment);
+int pa_query_leaf_bitmaps(pa_query* q, int32_t segment, uint32_t* device_out, void* stream);
+
 /* Group-key layout. Direct (hashed = 0): key = sum_j id_j * prod_{k<j} cardinality_k. Hashed (hashed = 1, chosen when
  * a group-by column is raw or the product of cardinalities is too large to address): the key packs component j
  * (a table-wide key id, or the raw value's bits: 32 for INT/FLOAT, 64 for LONG/DOUBLE) at bit shifts[j]. Keys returned

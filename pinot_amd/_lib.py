@@ -42,7 +42,7 @@ EXPORTED = [
     "pa_query_execute", "pa_query_reset", "pa_query_scan", "pa_query_num_eager_literals", "pa_query_lane_major",
     "pa_query_accumulator_bytes", "pa_query_set_accumulator_buffer", "pa_query_num_sections", "pa_query_section",
     "pa_query_fetch", "pa_query_matched_docs", "pa_query_key_layout", "pa_query_limit_trimming",
-    "pa_query_num_groups_limit_reached", "pa_query_stats",
+    "pa_query_num_groups_limit_reached", "pa_query_stats", "pa_query_leaf_bitmap_words", "pa_query_leaf_bitmaps",
     "pa_query_plan", "pa_query_destroy",
 ]
 
@@ -125,6 +125,8 @@ def _declare(lib):
         "pa_query_limit_trimming": (i32, [vp]),
         "pa_query_num_groups_limit_reached": (ctypes.c_int64, [vp]),
         "pa_query_stats": (ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "pa_query_leaf_bitmap_words": (ctypes.c_int64, [vp, i32]),
+        "pa_query_leaf_bitmaps": (ctypes.c_int, [vp, i32, vp, vp]),
         "pa_query_plan": (ctypes.c_int, [vp] + [ctypes.POINTER(i32)] * 7),
         "pa_query_destroy": (None, [vp]),
     }

@@ -2087,6 +2087,30 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   return m;
 }
 
+int64_t pa_query_leaf_bitmap_words(const pa_query* q, int32_t segment) {
+  if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
+  if (segment < 0 || segment >= q->nseg) return fail(PA_EINVAL, "segment index out of range");
+  return ((int64_t)q->segs[segment]->num_docs + 63) / 64 * 2;
+}
+
+int pa_query_leaf_bitmaps(pa_query* q, int32_t segment, uint32_t* device_out, void* stream) {
+  const int64_t words = pa_query_leaf_bitmap_words(q, segment);
+  if (words < 0) return (int)words;
+  if (!device_out) return fail(PA_EINVAL, "null bitmap buffer");
+  hipStream_t st = (hipStream_t)stream;
+  const DevSeg* ds = (const DevSeg*)q->dsegs.p + segment;
+  for (int l = 0; l < q->spec.num_leaves; ++l) {
+    // the leaf's first CNF literal: literal value = leaf value XOR the literal's negation
+    int li = -1;
+    for (size_t i = 0; i < q->literals.size() && li < 0; ++i)
+      if (q->literals[i].leaf == l) li = (int)i;
+    if (li < 0) return fail(PA_EUNSUPPORTED, "filter leaf " + std::to_string(l) + " has no literal in the plan");
+    PA_HIP(launch_leaf_bitmap(ds, li, q->literals[li].neg ? 1 : 0, q->segs[segment]->num_docs,
+                              device_out + (size_t)l * words, st));
+  }
+  return PA_OK;
+}
+
 int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs, uint64_t* num_tiles) {
   if (!q) return fail(PA_EINVAL, "null query");
   if (staged_bytes) *staged_bytes = q->staged_bytes;

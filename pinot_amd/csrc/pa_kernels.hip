@@ -1489,7 +1489,7 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
       AS1 uint32_t* recs = gp(isv ? ps.recs_v : ps.recs_h);
       const uint32_t n = B.cnt[p], o = B.front[p];
       const uint32_t h = gp(ps.hist)[lb * P + p];
-      if (n >= BS || o + n != B.back[p])  // the emit pass must see exactly the count pass's records
+      if ((n >= BS || o + n != B.back[p]) && !q->debug_emit)  // the emit pass must see exactly the count pass's records
         __hip_atomic_fetch_add(gp(q->matched_docs) + 3, 1ull, RLX);
       AS1 uint32_t* d = recs + (B.start[p] + o) * (uint64_t)nw;
       const uint32_t nn = n < BS ? n : BS;
@@ -1733,6 +1733,28 @@ hipError_t launch_limit_passes(const DevQuery* q, const DevSeg* segs, const Limi
 }
 
 // ---------------------------------------------------------------- segment-load / query-prep kernels
+
+// One filter literal over every doc of one segment -> a doc bitmap (execution statistics; pa_query_leaf_bitmaps):
+// 64 docs per wave step, one ballot, two words.
+__global__ void __launch_bounds__(256) leaf_bitmap_kernel(const DevSeg* __restrict__ seg, int li, int flip,
+                                                          int64_t num_docs, uint32_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
+  for (int64_t c = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; c * kWave < num_docs; c += waves) {
+    const int64_t doc = c * kWave + lane;
+    const bool m = doc < num_docs && (leaf_match_doc(seg->leaves[li], doc) != (flip != 0));
+    const uint64_t b = __ballot(m);
+    if (lane < 2) gp(out)[2 * c + lane] = (uint32_t)(b >> (32 * lane));
+  }
+}
+
+hipError_t launch_leaf_bitmap(const DevSeg* seg, int li, int flip, int64_t num_docs, uint32_t* out, hipStream_t s) {
+  const int64_t steps = (num_docs + kWave - 1) / kWave;
+  int64_t g = (steps + 3) / 4;
+  g = g < 1 ? 1 : (g > 4096 ? 4096 : g);
+  leaf_bitmap_kernel<<<(int)g, 256, 0, s>>>(seg, li, flip, num_docs, out);
+  return hipGetLastError();
+}
 
 __global__ void bswap_words_kernel(uint32_t* w, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)

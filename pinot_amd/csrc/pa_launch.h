@@ -15,6 +15,8 @@ struct CompactDesc {
   void* dst[kMaxCompactSections];
   int64_t* keys;
 };
+// one filter literal of one segment -> doc bitmap (execution statistics)
+hipError_t launch_leaf_bitmap(const DevSeg* seg, int li, int flip, int64_t num_docs, uint32_t* out, hipStream_t s);
 hipError_t launch_compact(const unsigned long long* count, int64_t K, int all, uint32_t* block_sums, int64_t cap,
                           const CompactDesc* d, int phase, hipStream_t s);
 // numGroupsLimit first-seen trimming (pa_kernels.hip "numGroupsLimit"): the (segment, key) first-position table,

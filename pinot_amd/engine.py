@@ -120,6 +120,9 @@ class IntermediateResult:
     num_docs_scanned: int = 0
     num_total_docs: int = 0
     num_groups_limit_reached: bool = False
+    # DataTable execution statistics (fetch(execution_stats=True); filter_stats.py)
+    num_entries_scanned_in_filter: int = 0
+    num_entries_scanned_post_filter: int = 0
 
 
 def _flatten_filter(f, leaves, ops):
@@ -451,7 +454,32 @@ class GpuQueryExecutor:
                 out.append(comp.view(np.float64))
         return out
 
-    def fetch(self, stream=None) -> IntermediateResult:
+    def leaf_bitmaps(self, segment_index, stream=None):
+        """bool[leaves, num_docs]: every filter leaf (the engine's flattened leaf order) on every doc of one bound
+        segment, computed on the GPU (pa_query_leaf_bitmaps). Synchronises `stream`."""
+        import torch
+        lib = L.lib()
+        nl = int(self.spec.num_leaves)
+        n = self.segs[segment_index].num_docs
+        if nl == 0:
+            return np.zeros((0, n), dtype=bool)
+        words = L.check(lib.pa_query_leaf_bitmap_words(self.handle, segment_index), "pa_query_leaf_bitmap_words")
+        buf = torch.zeros(nl * words, dtype=torch.int32, device=torch.device("cuda", torch.cuda.current_device()))
+        L.check(lib.pa_query_leaf_bitmaps(self.handle, segment_index, buf.data_ptr(), stream), "pa_query_leaf_bitmaps")
+        torch.cuda.synchronize()  # (device-wide: covers `stream`)
+        w = buf.cpu().numpy().view(np.uint8).reshape(nl, words * 4)
+        return np.unpackbits(w, axis=1, bitorder="little")[:, :n].astype(bool)
+
+    def execution_stats(self, stream=None):
+        """(numEntriesScannedInFilter, numEntriesScannedPostFilter) of this server's segments: the reference's
+        operator accounting (filter_stats.py) over GPU leaf bitmaps."""
+        from . import filter_stats as FS
+        return FS.server_stats(self.query, self.segs, lambda si: self.leaf_bitmaps(si, stream))
+
+    def fetch(self, stream=None, execution_stats=False) -> IntermediateResult:
+        """execution_stats=True also fills numEntriesScannedInFilter / PostFilter (one leaf-bitmap pass per segment on
+        the GPU plus the host restatement of the reference's accounting: meant for result metadata, not the hot
+        loop)."""
         lib = L.lib()
         q = self.query
         keys, counts, outs = self.fetch_arrays(stream)
@@ -459,6 +487,8 @@ class GpuQueryExecutor:
         res = IntermediateResult(list(q.aggregations), list(q.group_by))
         res.num_total_docs = sum(s.num_docs for s in self.segs)
         res.num_docs_scanned = int(lib.pa_query_matched_docs(self.handle))
+        if execution_stats:
+            res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter = self.execution_stats(stream)
         key_cols = [kc.tolist() for kc in self.key_values(keys)]
         cols = []  # one python list per query aggregation
         for a, pi in zip(q.aggregations, self.agg_map):

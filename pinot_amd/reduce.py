@@ -55,6 +55,8 @@ def merge_intermediate(results):
     for r in results:
         out.num_docs_scanned += r.num_docs_scanned
         out.num_total_docs += r.num_total_docs
+        out.num_entries_scanned_in_filter += r.num_entries_scanned_in_filter
+        out.num_entries_scanned_post_filter += r.num_entries_scanned_post_filter
         out.num_groups_limit_reached |= r.num_groups_limit_reached
         if out.group_by:
             for k, vals in r.groups.items():
@@ -113,6 +115,8 @@ def server_trim(res: IntermediateResult, query: Q.Query) -> IntermediateResult:
     keep = {r[2] for r in rows[:trim]}
     out = IntermediateResult(res.aggregations, res.group_by, {k: v for k, v in res.groups.items() if k in keep})
     out.num_docs_scanned, out.num_total_docs = res.num_docs_scanned, res.num_total_docs
+    out.num_entries_scanned_in_filter = res.num_entries_scanned_in_filter
+    out.num_entries_scanned_post_filter = res.num_entries_scanned_post_filter
     out.num_groups_limit_reached = res.num_groups_limit_reached
     return out
 

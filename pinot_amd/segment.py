@@ -62,6 +62,8 @@ class Column:
     raw_values: Optional[np.ndarray] = None   # no-dictionary columns
     is_sorted: bool = False
     single_value: bool = True
+    inverted_index: bool = False              # index metadata the filter-statistics restatement needs (the GPU
+    range_index: bool = False                 # scan itself never uses an index: filter_stats.py)
     total_num_values: int = 0                 # MV: values over all docs (FixedBitMVForwardIndexWriter totalNumValues)
     max_num_multi_values: int = 0             # MV: longest row
 
@@ -71,6 +73,12 @@ class Column:
         header = nchunks * 4
         bitmap = (self.total_num_values + 7) // 8
         return dpc, header, header, header + bitmap
+
+    def mv_lengths(self, num_docs):
+        """Values per doc of a multi-value column (from the forward index's doc-start bitmap)."""
+        _, _, boff, roff = self.mv_layout(num_docs)
+        starts = np.flatnonzero(np.unpackbits(self.fwd_bytes[boff:roff])[:self.total_num_values])
+        return np.diff(np.append(starts, self.total_num_values))
 
     def mv_dict_ids(self, num_docs):
         """Per-doc dictId arrays decoded from the MV forward index bytes (vectorised test helper)."""
@@ -204,9 +212,10 @@ def build_column(name, values, data_type, has_dictionary=True) -> Column:
 
 
 def create_segment(name, data: Dict[str, np.ndarray], schema: Dict[str, str], no_dictionary_columns=(),
-                   multi_value_columns=()) -> Segment:
+                   multi_value_columns=(), inverted_index_columns=(), range_index_columns=()) -> Segment:
     """Builds an immutable segment from column arrays. schema: column -> data type; a multi-value column's data is a
-    sequence of per-doc value arrays."""
+    sequence of per-doc value arrays. inverted_index_columns / range_index_columns: the table config's index lists
+    (SegmentGeneratorConfig.setIndexOn), kept as column metadata for the execution statistics."""
     n = None
     seg = None
     for col_name, dtype in schema.items():
@@ -222,6 +231,10 @@ def create_segment(name, data: Dict[str, np.ndarray], schema: Dict[str, str], no
             seg.columns[col_name] = build_column(col_name, vals, dtype, col_name not in no_dictionary_columns)
     if seg is None:
         seg = Segment(name=name, num_docs=0)
+    for c in inverted_index_columns:
+        seg.column(c).inverted_index = True
+    for c in range_index_columns:
+        seg.column(c).range_index = True
     return seg
 
 

@@ -27,7 +27,10 @@ def golden_segment(golden_spec):
     """The reference's BaseSingleValueQueriesTest segment, rebuilt by our segment creator."""
     from pinot_amd.segment import create_segment
     data = np.load(os.path.join(GOLDEN, "test_data_sv.npz"))
-    return create_segment("testTable_126164076_167572854", {k: data[k] for k in data.files}, golden_spec["schema"])
+    # BaseSingleValueQueriesTest.java:124-125: inverted indexes on column6/7/11/17/18 (column5 and daysSinceEpoch come
+    # out sorted): index metadata for the execution statistics only
+    return create_segment("testTable_126164076_167572854", {k: data[k] for k in data.files}, golden_spec["schema"],
+                          inverted_index_columns=("column6", "column7", "column11", "column17", "column18"))
 
 
 def rows_match(got, expected, delta):

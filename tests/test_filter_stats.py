@@ -1,0 +1,146 @@
+"""DataTable execution statistics (pinot_amd/filter_stats.py): the reference's filter-operator accounting restated
+over per-leaf doc bitmaps, checked against the statistics the reference's own tests assert
+(QueriesTestUtils.testInterSegmentsResult in InterSegmentAggregationSingleValueQueriesTest /
+InterSegmentGroupBySingleValueQueriesTest: numDocsScanned, numEntriesScannedInFilter, numEntriesScannedPostFilter,
+numTotalDocs; tests/golden/sv_queries.json). Here the leaf bitmaps come from a numpy evaluation of each leaf on the
+golden segment (test-side); the -m gpu golden test takes them from the GPU (pa_query_leaf_bitmaps)."""
+import numpy as np
+import pytest
+
+import oracle
+from pinot_amd import filter_stats as FS
+from pinot_amd import parse_sql
+from pinot_amd import predicate as P
+from pinot_amd import query as Q
+from pinot_amd.engine import _flatten_filter
+
+
+def leaf_masks(query, seg):
+    """bool[leaves, docs] in the engine's leaf order (expand_raw_in + postfix flattening), evaluated with numpy."""
+    if query.filter is None:
+        return None
+    leaves, ops = [], []
+    _flatten_filter(P.expand_raw_in(query.filter, seg), leaves, ops)
+    out = np.zeros((len(leaves), seg.num_docs), dtype=bool)
+    for i, pred in enumerate(leaves):
+        col = seg.column(pred.column)
+        assert col.has_dictionary and col.single_value
+        ids = oracle.read_ints(col.fwd_bytes, seg.num_docs, col.num_bits)
+        out[i] = oracle._dict_match(pred, col)[ids].astype(bool)
+    return out
+
+
+def golden_stats(case, seg, servers, per_server):
+    q = parse_sql(case["sql"])
+    segs = [seg] * per_server
+    masks = leaf_masks(q, seg)
+    in_f, post = FS.server_stats(q, segs, lambda si: masks)
+    docs = oracle.run_query(q, segs).num_docs_scanned
+    return [docs * servers, in_f * servers, post * servers, seg.num_docs * per_server * servers]
+
+
+def test_golden_execution_statistics(golden_spec, golden_segment):
+    """All four statistics of every golden case (51 queries: aggregation-only and group-by, with and without the
+    reference's FILTER, whose numEntriesScannedInFilter 252256 follows from the sorted daysSinceEpoch range, the
+    applyAnd chain over column1/column3 and the AndDocIdIterator/OrDocIdIterator leap-frog of column6's scan)."""
+    bad = []
+    for case in golden_spec["cases"]:
+        got = golden_stats(case, golden_segment, golden_spec["servers"], golden_spec["segments_per_server"])
+        if got != case["stats"]:
+            bad.append((case["source"], case["sql"][:80], got, case["stats"]))
+    assert not bad, bad
+
+
+def _seg(n=5000, seed=3):
+    from pinot_amd.segment import create_segment
+    rng = np.random.default_rng(seed)
+    data = {"s": np.sort(rng.integers(0, 50, n)).astype(np.int32), "a": rng.integers(0, 100, n).astype(np.int32),
+            "b": rng.integers(0, 100, n).astype(np.int32), "c": rng.integers(0, 20, n).astype(np.int32)}
+    return create_segment("x", data, {k: "INT" for k in data}, inverted_index_columns=("c",))
+
+
+@pytest.mark.parametrize("where,expect", [
+    # one scan leaf: the projection's next() reads every doc
+    ("a < 50", lambda m, n: n),
+    # index-only filters read nothing
+    ("s = 7", lambda m, n: 0),
+    ("c IN (1, 2, 3)", lambda m, n: 0),
+    ("s = 7 AND c = 3", lambda m, n: 0),
+    # sorted + scans: applyAnd over the sorted range, then over its survivors
+    ("s BETWEEN 10 AND 20 AND a < 50 AND b > 30",
+     lambda m, n: m["s"].sum() + (m["s"] & m["a"]).sum()),
+    # inverted + scan
+    ("c = 4 AND a >= 10", lambda m, n: m["c"].sum()),
+    # scans only: AndDocIdIterator leap-frogs (first scan reads up to each candidate, the second from it)
+    ("a < 30 AND b < 30", None),
+    # always-true / always-false leaves fold away (dictionary evaluators)
+    ("a < 1000 AND s = 7", lambda m, n: 0),
+    ("a > 1000 OR c = 2", lambda m, n: 0),
+])
+def test_filter_accounting_shapes(where, expect):
+    seg = _seg()
+    q = parse_sql("SELECT COUNT(*) FROM t WHERE " + where)
+    masks = leaf_masks(q, seg)
+    got = FS.entries_scanned_in_filter(q.filter, seg, masks)
+    if expect is None:
+        # reference: AndDocIdIterator.next() -> a.advance(t) reads [t, next a-match], b.advance reads [t, next b-match]
+        a = masks[0]
+        b = masks[1]
+        n = seg.num_docs
+        exp, t = 0, 0
+        ia, ib = np.flatnonzero(a), np.flatnonzero(b)
+        na = nb = -1  # not used by the protocol (advance always re-reads from the target)
+        while True:
+            j = np.searchsorted(ia, t)
+            if j == len(ia):
+                exp += n - t
+                break
+            x = int(ia[j]); exp += x - t + 1; mx = x
+            while True:
+                k = np.searchsorted(ib, mx)
+                if k == len(ib):
+                    exp += n - mx
+                    break
+                y = int(ib[k]); exp += y - mx + 1
+                if y == mx:
+                    break
+                j = np.searchsorted(ia, y)
+                if j == len(ia):
+                    exp += n - y
+                    mx = None
+                    break
+                x = int(ia[j]); exp += x - y + 1; mx = x
+                if x == y:
+                    break
+            if mx is None or k == len(ib):
+                break
+            t = mx + 1
+        assert got == exp
+    else:
+        names = {}
+        for li, pred in enumerate(_leaves(q, seg)):
+            names[pred.column] = masks[li]
+        assert got == expect(names, seg.num_docs)
+
+
+def _leaves(q, seg):
+    leaves, ops = [], []
+    _flatten_filter(P.expand_raw_in(q.filter, seg), leaves, ops)
+    return leaves
+
+
+def test_post_filter_rules(golden_segment):
+    """numEntriesScannedPostFilter: 0 for the non-scan plans (metadata/dictionary aggregations on a match-all filter,
+    COUNT(*)), docs x projected columns otherwise (AggregationPlanNode.java:97-115, ProjectionOperator)."""
+    seg = golden_segment
+    for sql, cols in [("SELECT MAX(column1), MIN(column3) FROM t", 0), ("SELECT COUNT(*) FROM t", 0),
+                      ("SELECT SUM(column1) FROM t", 1), ("SELECT SUM(column1), MAX(column3) FROM t", 2),
+                      ("SELECT column9, MAX(column1) FROM t GROUP BY column9", 2),
+                      ("SELECT COUNT(*) FROM t WHERE column1 > 100000000", 0),
+                      ("SELECT MAX(column1) FROM t WHERE column1 > 100", 0),  # always true: match-all, non-scan
+                      ("SELECT MAX(column1) FROM t WHERE column1 > 100000000", 1)]:
+        q = parse_sql(sql)
+        masks = leaf_masks(q, seg)
+        _, post = FS.server_stats(q, [seg], lambda si: masks)
+        docs = seg.num_docs if q.filter is None else int(masks[0].sum())
+        assert post == docs * cols, sql

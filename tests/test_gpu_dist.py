@@ -86,15 +86,15 @@ def test_two_rank_merge_with_table_dictionaries(sql, rccl_world1):
 
 @pytest.mark.parametrize("sql", [
     "SELECT r, COUNT(*), SUM(m), MIN(f), MAX(m), DISTINCTCOUNTHLL(d1) FROM t GROUP BY r LIMIT 100000",
-    "SELECT d1, r, COUNT(*), AVG(f) FROM t WHERE m > 0 GROUP BY d1, r LIMIT 100000",
+    "SELECT d1, ri, COUNT(*), AVG(f) FROM t WHERE m > 0 GROUP BY d1, ri LIMIT 100000",
 ])
 def test_hashed_key_space_device_merge(sql, rccl_world1):
     """HashedAccumulators on a hashed key space (GROUP BY a raw column): the block moves into a torch buffer, the
     RCCL merge (world size 1: all-gather of this rank's compacted rows, merge by packed key) rewrites it as groups
     [0, n) in key order, and the library's own fetch of the rewritten block equals the oracle."""
     from pinot_amd.parallel import HashedAccumulators
-    cols = dict(COLS, r=("LONG", 0))
-    segs = [make_segment(900 + i, n, cols, no_dict=("r",)) for i, n in enumerate((15013, 9001))]
+    cols = dict(COLS, r=("LONG", 0), ri=("INT", 0))
+    segs = [make_segment(900 + i, n, cols, no_dict=("r", "ri")) for i, n in enumerate((15013, 9001))]
     q = parse_sql(sql)
     gsegs = [GpuSegment(s) for s in segs]
     ex = GpuQueryExecutor(q, gsegs)

@@ -81,13 +81,21 @@ def test_golden_cases_gpu(golden_spec, golden_segment):
         for case in golden_spec["cases"]:
             q = parse_sql(case["sql"])
             ex = GpuQueryExecutor(q, [g, g])  # one server = 2 copies of the segment
-            server = ex.run()
+            ex.execute()
+            server = ex.fetch(execution_stats=True)  # + the DataTable statistics (GPU leaf bitmaps)
             ex.close()
             exp = oracle.run_query(q, [golden_segment] * 2)
             assert_same(server, exp)
-            got = final_result_table(merge_intermediate([server_trim(server, q)] * 2), q)
+            broker = merge_intermediate([server_trim(server, q)] * 2)
+            got = final_result_table(broker, q)
             if not rows_match(got, case["rows"], case["delta"]):
                 failures.append((case["source"], got[:3], case["rows"][:3]))
+            # testInterSegmentsResult: numDocsScanned, numEntriesScannedInFilter, numEntriesScannedPostFilter,
+            # numTotalDocs summed over the broker's servers
+            stats = [broker.num_docs_scanned, broker.num_entries_scanned_in_filter,
+                     broker.num_entries_scanned_post_filter, broker.num_total_docs]
+            if stats != case["stats"]:
+                failures.append((case["source"], "stats", stats, case["stats"]))
     finally:
         g.close()
     assert not failures, failures
