@@ -188,6 +188,8 @@ typedef struct {
 #define PA_QF_DEBUG_STREAM_ONLY (1 << 16) /* measurement only: stream the tiles, skip decode (results invalid) */
 #define PA_QF_NO_LANE_MAJOR (1 << 17)     /* use the step-major scan kernel even when the lane-major one applies */
 #define PA_QF_NO_PARTITION (1 << 21)      /* high-cardinality dense GROUP BY: per-doc global atomics, not partitioned */
+#define PA_QF_NO_SPLIT_EMIT (1 << 24)     /* partitioned aggregation with both record streams: one emit kernel for both
+                                             (default: a V launch and an H launch, each holding only its own bins) */
 #define PA_QF_PART_SHIFT 22               /* bits 22..23: LDS per partition of the partitioned aggregation (0 = auto,
                                              1 = 64 KiB, 2 = 96 KiB, 3 = 144 KiB): larger partitions = fewer record
                                              write fronts per XCD */

@@ -504,6 +504,12 @@ struct pa_query {
   DevBuf dq_count, dsegs_count;
   int count_lds = 0, count_ring = 0, part_lds_c = 0;
   int emit_strat = 0;   // the emit kernel variant (pemit_strat)
+  // both streams: the emit pass runs as two launches (V records, then H records), each with only its own bins in LDS
+  // (more resident workgroups than one kernel holding both): the H launch's descriptor, variant and plan
+  bool split_emit = false;
+  DevQuery hq_h;
+  DevBuf dq_h;
+  int emit_h_strat = 0, emit_h_lds = 0, emit_h_ring = 0, emit_h_wg = 0;
   int count_k = 1;      // count-pass workgroups per emit workgroup
   size_t sc_hist = 0, sc_off = 0, sc_base = 0, sc_recs_v = 0, sc_recs_h = 0, sc_bytes = 0;
   int scratch_dev = 0;
@@ -527,6 +533,7 @@ struct pa_query {
     dev_free(dsegs);
     dev_free(dplans);
     dev_free(dq_count);
+    dev_free(dq_h);
     dev_free(dsegs_count);
     dev_free(lim_keys);
     dev_free(lim_pos);
@@ -1063,6 +1070,7 @@ struct TilePlan {
 
 TilePlan plan_tiles(const pa_query* q, const std::vector<DevSeg>& segs, int strat, bool use_lm, size_t acc_b,
                     bool only16) {
+  const int wpw = scan_waves(strat);  // waves per workgroup of this kernel variant
   const pa_query_spec& s = q->spec;
   const int force_ring = (s.flags >> PA_QF_RING_SHIFT) & 15;
   const int force_wg = (s.flags >> PA_QF_WG_SHIFT) & 7;
@@ -1088,21 +1096,21 @@ TilePlan plan_tiles(const pa_query* q, const std::vector<DevSeg>& segs, int stra
       if (force_wg && wg != force_wg) continue;
       const size_t per_wg = kLdsBudget / wg;
       if (per_wg <= acc_b) continue;
-      int ring = (int)((per_wg - acc_b) / (kWavesPerWG * img_bytes));
+      int ring = (int)((per_wg - acc_b) / (wpw * img_bytes));
       ring = std::min(ring, 8);
       if (force_ring) {
         if (force_ring > ring) continue;
         ring = force_ring;
       }
       if (ring < 2) continue;
-      const size_t lds = acc_b + (size_t)kWavesPerWG * ring * img_bytes;
+      const size_t lds = acc_b + (size_t)wpw * ring * img_bytes;
       int resident = 0;
       if (set_scan_lds_limit(strat, steps, use_lm, (int)kLdsBudget) != hipSuccess ||
           scan_occupancy(strat, steps, use_lm, (int)lds, &resident) != hipSuccess)
         resident = wg;  // no device to ask (planning only): trust the LDS arithmetic
       if (resident < wg) continue;
-      const double inflight = (double)wg * kWavesPerWG * (ring - 1) * img_bytes;
-      const double score = 1e7 * wg + (steps == 32 ? 1e6 : 0) + std::min(inflight, 128.0 * 1024);
+      const double inflight = (double)wg * wpw * (ring - 1) * img_bytes;
+      const double score = 1e7 * wg * wpw / kWavesPerWG + (steps == 32 ? 1e6 : 0) + std::min(inflight, 128.0 * 1024);
       if (score > best.score) best = TilePlan{steps, dma, ring, wg, img_dw, lds, score};
     }
   }
@@ -1292,18 +1300,52 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
   };
   // the emit pass stages its columns in a ring next to the bins: halve the bins (down to 64-byte bursts) while they
   // do not fit or cost resident waves (at least two workgroups per CU hide the per-record gathers)
-  const int es = pemit_strat(vstream ? fmt : -1, hll >= 0 ? 1 : 0);
-  q->emit_strat = es;
-  emit_plan = plan_tiles(q, q->hsegs, es, false, emit_state(bs_v, bs_h), true);
-  while ((emit_plan.score < 0 || emit_plan.wg_per_cu < 2) && (bs_h > 16 || (bs_v * W > 16 && bs_v % 8 == 0))) {
-    const int bv2 = (bs_v * W > 16 && bs_v % 8 == 0) ? bs_v / 2 : bs_v;
-    const int bh2 = bs_h > 16 ? bs_h / 2 : bs_h;
-    TilePlan t = plan_tiles(q, q->hsegs, es, false, emit_state(bv2, bh2), true);
-    if (emit_plan.score >= 0 && t.score >= 0 && t.wg_per_cu <= emit_plan.wg_per_cu)
-      break;  // no more resident waves from smaller bins: keep the larger bursts
-    bs_v = bv2;
-    bs_h = bh2;
-    emit_plan = t;
+  // both streams: two emit launches (V, then H), each holding only its own stream's bins
+  const bool split = vstream && hll >= 0 && !(s.flags & PA_QF_NO_SPLIT_EMIT);
+  q->split_emit = split;
+  // Each launch: 4-wave or 16-wave workgroups (the bins are per workgroup: shared by 16 waves they leave LDS for more
+  // resident waves when the tile images are small), whichever keeps more waves resident; bins halve (down to 64-byte
+  // bursts) while they do not fit or cost resident waves (at least 8 waves per CU hide the per-record gathers).
+  auto plan_emit = [&](int vf, int hh, bool with_v, bool with_h, int& bv, int& bh, int& strat) {
+    auto lds_of = [&](int v, int h2) { return emit_state(with_v ? v : 0, with_h ? h2 : 0); };
+    TilePlan best;
+    int best_bv = bv, best_bh = bh;
+    for (int big : {0, 1}) {
+      const int es = pemit_strat(vf, hh, big);
+      const int wpw = scan_waves(es);
+      int v = bv, h2 = bh;
+      TilePlan e = plan_tiles(q, q->hsegs, es, false, lds_of(v, h2), true);
+      while ((e.score < 0 || e.wg_per_cu * wpw < 2 * kWavesPerWG) &&
+             ((with_h && h2 > 16) || (with_v && v * W > 16 && v % 8 == 0))) {
+        const int v2 = (with_v && v * W > 16 && v % 8 == 0) ? v / 2 : v;
+        const int hh2 = (with_h && h2 > 16) ? h2 / 2 : h2;
+        TilePlan t = plan_tiles(q, q->hsegs, es, false, lds_of(v2, hh2), true);
+        if (e.score >= 0 && t.score >= 0 && t.wg_per_cu <= e.wg_per_cu)
+          break;  // no more resident waves from smaller bins: keep the larger bursts
+        v = v2;
+        h2 = hh2;
+        e = t;
+      }
+      if (e.score > best.score) {
+        best = e;
+        best_bv = v;
+        best_bh = h2;
+        strat = es;
+      }
+    }
+    bv = best_bv;
+    bh = best_bh;
+    return best;
+  };
+  if (split) {
+    emit_plan = plan_emit(fmt, 0, true, false, bs_v, bs_h, q->emit_strat);
+    TilePlan eh = plan_emit(-1, 1, false, true, bs_v, bs_h, q->emit_h_strat);
+    if (eh.score < 0) { PLAN_LOG("partitioned: no (exit 8h)"); return false; }
+    q->emit_h_lds = (int)eh.lds;
+    q->emit_h_ring = eh.ring;
+    q->emit_h_wg = eh.wg_per_cu;
+  } else {
+    emit_plan = plan_emit(vstream ? fmt : -1, hll >= 0 ? 1 : 0, vstream, hll >= 0, bs_v, bs_h, q->emit_strat);
   }
   if (emit_plan.score < 0) { PLAN_LOG("partitioned: no (exit 8)"); return false; }
   q->hsegs_count = count_pass_segments(q, P);
@@ -1331,9 +1373,12 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
   o = (o + 7) & ~(size_t)7;
   h.lds_start = (uint32_t)o; o += (size_t)Ptot * 8;
   o = (o + 15) & ~(size_t)15;
-  h.lds_bins_v = (uint32_t)o; o += (size_t)Pv * bs_v * W * 4;
+  h.lds_bins_v = (uint32_t)o;
+  if (!split) o += (size_t)Pv * bs_v * W * 4;  // (split: each launch's bins start right after the state)
   o = (o + 15) & ~(size_t)15;
   h.lds_bins_h = (uint32_t)o;
+  h.part_lo = 0;
+  h.part_hi = split ? (int32_t)Pv : Ptot;
   // pass C LDS: V: u32 count[kr_v], then every aggregation's accumulators (8-byte aligned); H: u8 registers (+ counts)
   size_t lv = 0;
   std::vector<int> agg_lds(s.num_aggs, 0);
@@ -1354,9 +1399,9 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
   }
   q->partitioned = true;
   PLAN_LOG("partitioned: K=%lld Pv=%lld (kr %lld, fmt %d, W %d, bs %d) Ph=%lld (kr %lld, bs %d) emit lds %zu wg %d ring %d; "
-           "count lds %zu wg %d", (long long)K, (long long)Pv, (long long)kr_v, fmt, W, bs_v, (long long)Ph,
-           (long long)kr_h, bs_h, emit_plan.lds, emit_plan.wg_per_cu, emit_plan.ring, count_plan.lds,
-           count_plan.wg_per_cu);
+           "split %d strat %d/%d (H lds %d wg %d ring %d); count lds %zu wg %d", (long long)K, (long long)Pv, (long long)kr_v, fmt,
+           W, bs_v, (long long)Ph, (long long)kr_h, bs_h, emit_plan.lds, emit_plan.wg_per_cu, emit_plan.ring,
+           (int)split, q->emit_strat, q->emit_h_strat, q->emit_h_lds, q->emit_h_wg, q->emit_h_ring, count_plan.lds, count_plan.wg_per_cu);
   return true;
 }
 
@@ -1589,6 +1634,11 @@ int upload_descriptors(pa_query* q) {
     if (!rc) rc = dev_alloc(q->dsegs_count, sizeof(DevSeg) * std::max(1, q->nseg));
     if (rc) return rc;
     PA_HIP(hipMemcpy(q->dq_count.p, &q->hq_count, sizeof(DevQuery), hipMemcpyHostToDevice));
+    if (q->split_emit) {
+      rc = dev_alloc(q->dq_h, sizeof(DevQuery));
+      if (rc) return rc;
+      PA_HIP(hipMemcpy(q->dq_h.p, &q->hq_h, sizeof(DevQuery), hipMemcpyHostToDevice));
+    }
     if (q->nseg)
       PA_HIP(hipMemcpy(q->dsegs_count.p, q->hsegs_count.data(), sizeof(DevSeg) * q->nseg, hipMemcpyHostToDevice));
   }
@@ -1629,6 +1679,7 @@ int upload_descriptors(pa_query* q) {
   PA_HIP(hipMemcpy(q->dplans.p, q->hplans.data(), sizeof(LmSegPlan) * q->hplans.size(), hipMemcpyHostToDevice));
   if (q->partitioned) {
     PA_HIP(set_scan_lds_limit(q->emit_strat, q->steps, 0, q->lds_bytes));
+    if (q->split_emit) PA_HIP(set_scan_lds_limit(q->emit_h_strat, q->steps, 0, q->emit_h_lds));
     PA_HIP(set_scan_lds_limit(STRAT_PCOUNT, q->steps, 0, q->count_lds));
     PA_HIP(set_part_agg_lds_limit(q->part_lds_c));
   } else {
@@ -1760,8 +1811,10 @@ int pa_query_prepare(pa_query* q) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
   }
-  const int64_t max_wg = (int64_t)cus * std::max(1, plan.wg_per_cu);
-  const int64_t want = (total_tiles + kWavesPerWG - 1) / kWavesPerWG;
+  const int wg_cu = q->split_emit ? std::min(plan.wg_per_cu, q->emit_h_wg) : plan.wg_per_cu;
+  const int64_t max_wg = (int64_t)cus * std::max(1, wg_cu);
+  const int wpw = q->partitioned ? scan_waves(q->emit_strat) : kWavesPerWG;
+  const int64_t want = (total_tiles + wpw - 1) / wpw;
   q->grid = (int)std::max<int64_t>(1, std::min(max_wg, want));
 
   if (q->partitioned) {
@@ -1786,10 +1839,20 @@ int pa_query_prepare(pa_query* q) {
     q->count_ring = count_plan.ring;
     // the count pass stages fewer columns, so more of its workgroups fit a CU: k per emit workgroup (each walks 1/k of
     // that workgroup's tiles; part_scan_kernel sums their rows), as many as are resident at once
-    q->count_k = std::max(1, count_plan.wg_per_cu / std::max(1, plan.wg_per_cu));
+    q->count_k = std::max(1, count_plan.wg_per_cu / std::max(1, wg_cu));
     while (q->count_k > 1 && (int64_t)q->grid * q->count_k * kWavesPerWG > total_tiles) --q->count_k;
     // the emit pass's LDS: partition bin state + bins in front of the ring
-    q->hq.lds_acc_bytes = (uint32_t)(plan.lds - (size_t)kWavesPerWG * plan.ring * plan.img_dw * 4);
+    q->hq.lds_acc_bytes = (uint32_t)(plan.lds - (size_t)wpw * plan.ring * plan.img_dw * 4);
+    if (q->split_emit) {  // the H launch: same tiles and staging, its own ring depth, bins and partitions
+      DevQuery& e = q->hq_h;
+      e = q->hq;
+      e.strategy = STRAT_PEMIT;
+      e.ring = q->emit_h_ring;
+      e.lds_acc_bytes = (uint32_t)((size_t)q->emit_h_lds -
+                                   (size_t)scan_waves(q->emit_h_strat) * q->emit_h_ring * plan.img_dw * 4);
+      e.part_lo = q->hq.pv;
+      e.part_hi = q->hq.num_parts;
+    }
     rc = plan_scratch(q, P);
     if (rc) return rc;
   }
@@ -1849,6 +1912,9 @@ int pa_query_scan(pa_query* q, void* stream) {
     PA_HIP(launch_part_offsets(&q->hq, ps, q->grid, q->count_k, st));
     PA_HIP(launch_scan(q->emit_strat, q->steps, 0, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p,
                        (const DevSeg*)q->dsegs.p, plans, ps, st));
+    if (q->split_emit)
+      PA_HIP(launch_scan(q->emit_h_strat, q->steps, 0, q->grid, q->emit_h_lds, (const DevQuery*)q->dq_h.p,
+                         (const DevSeg*)q->dsegs.p, plans, ps, st));
     PA_HIP(launch_part_agg((const DevQuery*)q->dq.p, ps, q->hq.num_parts, q->part_lds_c, st));
     PA_HIP(hipEventRecord(a->last, st));
     a->last_stream = st;
@@ -1894,6 +1960,10 @@ int pa_query_set_accumulator_buffer(pa_query* q, void* device_buffer, uint64_t b
   if (q->partitioned) {
     relocate(q->hq_count);
     PA_HIP(hipMemcpy(q->dq_count.p, &q->hq_count, sizeof(DevQuery), hipMemcpyHostToDevice));
+    if (q->split_emit) {
+      relocate(q->hq_h);
+      PA_HIP(hipMemcpy(q->dq_h.p, &q->hq_h, sizeof(DevQuery), hipMemcpyHostToDevice));
+    }
   }
   if (!q->external_acc) {
     const size_t n = q->acc.n;

@@ -17,6 +17,7 @@ namespace pa {
 constexpr int kWave = 64;
 constexpr int kWavesPerWG = 4;
 constexpr int kWGSize = kWave * kWavesPerWG;
+// waves per workgroup of a scan-kernel variant (emit variants may run 16-wave workgroups)
 constexpr int kSteps = 32;                    // 64-doc steps per wave tile
 constexpr int kWTileDocs = kWave * kSteps;    // 2048 docs: one wave tile; 64*nb stream words per column
 constexpr int kMaxSlots = 12;                 // distinct columns referenced by one query
@@ -35,17 +36,25 @@ enum ColKind : int32_t { COL_NONE = 0, COL_SV_DICT = 1, COL_SV_RAW = 2, COL_MV_D
 enum Strategy : int32_t { STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PEMIT = 2, STRAT_PCOUNT = 3 };
 // The emit pass's kernel variant (launch code): the V record format (-1: no V stream) and whether there is an H stream
 // are template parameters, so each variant's record loop is straight-line code (no per-record format branches).
+// `big`: 16-wave workgroups (the partition bins and their state are per workgroup, so sharing them among more waves
+// leaves LDS for more resident waves when the tile images are small).
 constexpr int kPemitBase = 16;
-__host__ __device__ constexpr int pemit_strat(int vf, int hh) { return kPemitBase + 2 * (vf + 1) + (hh ? 1 : 0); }
+constexpr int kEmitBigWaves = 16;
+__host__ __device__ constexpr int pemit_strat(int vf, int hh, int big = 0) {
+  return kPemitBase + 2 * (vf + 1) + (hh ? 1 : 0) + (big ? 16 : 0);
+}
 __host__ __device__ constexpr bool is_pemit(int s) { return s >= kPemitBase; }
-__host__ __device__ constexpr int pemit_vf(int s) { return (s - kPemitBase) / 2 - 1; }
+__host__ __device__ constexpr int pemit_vf(int s) { return (((s - kPemitBase) & 15) >> 1) - 1; }
 __host__ __device__ constexpr bool pemit_hh(int s) { return ((s - kPemitBase) & 1) != 0; }
+__host__ __device__ constexpr int pemit_big(int s) { return (s - kPemitBase) >= 16 ? 1 : 0; }
+__host__ __device__ constexpr int scan_waves(int s) { return is_pemit(s) && pemit_big(s) ? kEmitBigWaves : kWavesPerWG; }
 // V record formats (word 0 always holds the key's offset inside its partition, key & ((1 << kshift_v) - 1)):
 //   V_FMT_KEY: COUNT only, one word;  V_FMT_ID: one word, | value id << kshift_v (the value column's table-wide value
 //   dictionary `vdict`);  V_FMT_32: + the int32 value;  V_FMT_64: + the 64-bit value (int64, or double bits);
 //   V_FMT_GEN: + every payload at its DevAgg::pay_off (one or two words each).
 enum VFormat : int32_t { V_FMT_KEY = 0, V_FMT_ID = 1, V_FMT_32 = 2, V_FMT_64 = 3, V_FMT_GEN = 4 };
 constexpr int kMaxVWords = 9;       // V record words (key + at most four 64-bit payloads)
+constexpr int kDocVals = 8;         // H records: docs with at most this many values take the doc-reserved emit path
 constexpr uint32_t kSentinel = 0xffffffffu;  // word 0 of a padding record (never a valid V or H record)
 // SUM/MIN/MAX value source. SRC_INT: every value fits int32 (one exact int64 accumulator);
 // SRC_LONG: 64-bit values, SUM kept exactly as a (low 32 bits unsigned, high 32 bits signed) pair of int64
@@ -156,6 +165,7 @@ struct DevQuery {
   int32_t hll_agg;           // the partitioned DISTINCTCOUNTHLL(MV) aggregation (-1: no H stream); H record =
                              // key offset << (log2m + 6) | register << 6 | rank << 1 | first
   int32_t emit_val_agg;      // V_FMT_ID/32/64: the aggregation whose column the value comes from (-1: COUNT only)
+  int32_t part_lo, part_hi;   // emit pass: the partitions this launch emits ([0, pv) V, [pv, P) H, or all)
   int32_t debug_emit;        // measurement only (PA_DEBUG_EMIT): bit 0 skips the emit pass's record stores, bit 1 its HLL
                              // dictionary gathers, bit 2 its MV value reads (wrong results; isolates the waits)
   uint32_t lds_cnt, lds_done, lds_front, lds_back, lds_start;  // STRAT_PEMIT LDS (bytes): per-partition bin state

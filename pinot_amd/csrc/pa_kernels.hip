@@ -677,66 +677,138 @@ __device__ __forceinline__ BinState bin_state(const DevQuery* __restrict__ q, un
 
 #define WG_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP
 
-// Wave-level put: every lane calls it (uniform control flow); an active lane puts one record (the first nw words of
-// r) into partition p's LDS bin of BS records (bins: the stream's partitions from p0 on, BS * nw words each). The lane whose write
-// completes a bin marks it; then the whole wave stores every marked bin (BS * nw words as whole 16-byte units, one
-// per lane: one store instruction per bin instead of one lane's serial loop) at its range's front slot and empties
-// it. A record arriving while its bin is full goes straight to the back end of the range. Every (workgroup,
-// partition) range holds exactly the records the count pass counted, so front and back meet (checked at the end).
+// Wave-level put of K records per lane: every lane calls it (uniform control flow); record k of an active lane (the
+// first nw words of r[k]) goes into partition p[k]'s LDS bin of BS records (bins: the stream's partitions from p0 on,
+// BS * nw words each). Phases, each a run of independent LDS operations (one wait per phase, not per record):
+// claim slots (cnt), write them, count them written (done); a record whose bin is full goes straight to the back end
+// of its range (back). The lane whose write completes a bin marks it, and the wave then stores every marked bin of the
+// batch at its range's front slot — several bins per store instruction (L lanes per bin, one 16-byte unit each) —
+// and empties it. Every (workgroup, partition) range holds exactly the records the count pass counted, so front and
+// back meet (checked at the end of the pass).
 // Ordering: LDS executes the DS instructions of one wave in issue order and serialises those of different waves, so
 // "write the slot, then count it done" and "read the bin, then reset the counters" need only the compiler to keep
 // program order (a signal fence). Acquire/release atomics would also wait for every outstanding global load, i.e.
 // drain the tile ring's LDS-DMA on every record. Only the wave that completed a bin touches its front and counters
-// until it resets them.
+// until it resets them (a bin fills at most once per batch: it stays full until its flush).
+template <int K>
+__device__ __forceinline__ void flush_full_bins(const BinState& B, const bool (&full)[K], const uint32_t (&p)[K],
+                                                uint32_t p0, lds_u32_t* bins, uint32_t BS, uint32_t nw,
+                                                AS1 uint32_t* recs, int lane, int dbg);
+
+template <int K, int WM>
+__device__ __forceinline__ void bin_put_batch(const BinState& B, const bool (&act)[K], const uint32_t (&p)[K],
+                                              uint32_t p0, lds_u32_t* bins, uint32_t BS, uint32_t nw,
+                                              const uint32_t (&r)[K][WM], AS1 uint32_t* recs, int lane, int dbg) {
+  uint32_t s[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) s[k] = act[k] ? __hip_atomic_fetch_add(B.cnt + p[k], 1u, WG_RLX) : 0xffffffffu;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (s[k] < BS) {
+      lds_u32_t* slot = bins + ((p[k] - p0) * BS + s[k]) * nw;
+#pragma unroll
+      for (int w = 0; w < WM; ++w)
+        if ((uint32_t)w < nw) slot[w] = r[k][w];
+    }
+  }
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  bool full[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) full[k] = s[k] < BS && __hip_atomic_fetch_add(B.done + p[k], 1u, WG_RLX) == BS - 1u;
+  if (!(dbg & 1)) {
+    uint32_t o[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      o[k] = (act[k] && s[k] >= BS) ? __hip_atomic_fetch_sub(B.back + p[k], 1u, WG_RLX) - 1u : 0u;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (act[k] && s[k] >= BS) {
+        AS1 uint32_t* d = recs + (B.start[p[k]] + o[k]) * (uint64_t)nw;
+#pragma unroll
+        for (int w = 0; w < WM; ++w)
+          if ((uint32_t)w < nw) d[w] = r[k][w];
+      }
+    }
+  }
+  flush_full_bins<K>(B, full, p, p0, bins, BS, nw, recs, lane, dbg);
+}
+
+// The flush half of a put: every bin some lane completed (full[k]) is stored at its range's front slot — several bins
+// per store instruction (L lanes per bin, one 16-byte unit each) — and emptied.
+template <int K>
+__device__ __forceinline__ void flush_full_bins(const BinState& B, const bool (&full)[K], const uint32_t (&p)[K],
+                                                uint32_t p0, lds_u32_t* bins, uint32_t BS, uint32_t nw,
+                                                AS1 uint32_t* recs, int lane, int dbg) {
+  uint64_t fm[K];
+  uint64_t any = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    fm[k] = __ballot(full[k]);
+    any |= fm[k];
+  }
+  if (any == 0) return;
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  if (dbg & 1) {  // (measurement only: drop the bins)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (full[k]) {
+        __hip_atomic_store(B.done + p[k], 0u, WG_RLX);
+        __hip_atomic_store(B.cnt + p[k], 0u, WG_RLX);
+      }
+    }
+    return;
+  }
+  // L lanes per bin (the bin's 16-byte units, rounded up to a power of two), G = 64 / L bins per store round
+  const uint32_t n16 = (BS * nw) >> 2;
+  uint32_t L = 1;
+  while (L < n16 && L < (uint32_t)kWave) L <<= 1;
+  const uint32_t G = (uint32_t)kWave / L;
+  const uint32_t grp = (uint32_t)lane / L, c0 = (uint32_t)lane % L;
+  uint32_t mine = 0xffffffffu, g = 0;
+  auto store_round = [&]() {
+    const bool on = grp < g;
+    uint32_t o = 0;
+    if (on) {
+      o = B.front[mine];
+      AS1 u32x4* d = (AS1 u32x4*)(recs + (B.start[mine] + o) * (uint64_t)nw);
+      const lds_u32x4_t* sb = (const lds_u32x4_t*)(bins + (mine - p0) * BS * nw);
+      for (uint32_t c = c0; c < n16; c += L) d[c] = sb[c];
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (on && c0 == 0) {
+      B.front[mine] = o + BS;
+      __hip_atomic_store(B.done + mine, 0u, WG_RLX);
+      __hip_atomic_store(B.cnt + mine, 0u, WG_RLX);
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    g = 0;
+    mine = 0xffffffffu;
+  };
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    uint64_t m = fm[k];
+    while (m) {
+      const int l = __builtin_ctzll(m);
+      m &= m - 1;
+      const uint32_t pp = (uint32_t)__builtin_amdgcn_readlane((int)p[k], l);
+      if (grp == g) mine = pp;
+      if (++g == G) store_round();
+    }
+  }
+  if (g) store_round();
+}
+
+// One record per lane (K = 1).
 template <int WM>
 __device__ __forceinline__ void bin_put_wave(const BinState& B, bool active, uint32_t p, uint32_t p0, lds_u32_t* bins,
                                              uint32_t BS, uint32_t nw, const uint32_t (&r)[WM], AS1 uint32_t* recs,
                                              int lane, int dbg) {
-  bool full = false;
-  if (active) {
-    const uint32_t s = __hip_atomic_fetch_add(B.cnt + p, 1u, WG_RLX);
-    if (s < BS) {
-      lds_u32_t* slot = bins + ((p - p0) * BS + s) * nw;
+  const bool a[1] = {active};
+  const uint32_t pk[1] = {p};
+  uint32_t rr[1][WM];
 #pragma unroll
-      for (int w = 0; w < WM; ++w)
-        if ((uint32_t)w < nw) slot[w] = r[w];
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      full = __hip_atomic_fetch_add(B.done + p, 1u, WG_RLX) == BS - 1u;
-    } else if (!(dbg & 1)) {
-      const uint32_t o = __hip_atomic_fetch_sub(B.back + p, 1u, WG_RLX) - 1u;
-      AS1 uint32_t* d = recs + (B.start[p] + o) * (uint64_t)nw;
-#pragma unroll
-      for (int w = 0; w < WM; ++w)
-        if ((uint32_t)w < nw) d[w] = r[w];
-    }
-  }
-  uint64_t fm = __ballot(full);
-  if (fm == 0) return;
-  if (dbg & 1) {  // (measurement only: drop the bins)
-    if (full) {
-      __hip_atomic_store(B.done + p, 0u, WG_RLX);
-      __hip_atomic_store(B.cnt + p, 0u, WG_RLX);
-    }
-    return;
-  }
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  const uint32_t n16 = (BS * nw) >> 2;
-  while (fm) {
-    const int l = __builtin_ctzll(fm);
-    fm &= fm - 1;
-    const uint32_t pp = (uint32_t)__builtin_amdgcn_readlane((int)p, l);
-    const uint32_t o = B.front[pp];  // (every lane reads the same word: a broadcast)
-    AS1 u32x4* d = (AS1 u32x4*)(recs + (B.start[pp] + o) * (uint64_t)nw);
-    const lds_u32x4_t* sb = (const lds_u32x4_t*)(bins + (pp - p0) * BS * nw);
-    for (uint32_t c = (uint32_t)lane; c < n16; c += kWave) d[c] = sb[c];
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (lane == 0) {
-      B.front[pp] = o + BS;
-      __hip_atomic_store(B.done + pp, 0u, WG_RLX);
-      __hip_atomic_store(B.cnt + pp, 0u, WG_RLX);
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  }
+  for (int w = 0; w < WM; ++w) rr[0][w] = r[w];
+  bin_put_batch<1, WM>(B, a, pk, p0, bins, BS, nw, rr, recs, lane, dbg);
 }
 
 
@@ -875,6 +947,29 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
             }
           }
         }
+        if constexpr (VF != V_FMT_GEN) {
+          // the batch's records (one per matching doc of the kEB steps) in one put: every LDS phase runs once
+          bool act[kEB];
+          uint32_t pk[kEB], r[kEB][NW];
+#pragma unroll
+          for (int i = 0; i < kEB; ++i) {
+            act[i] = (m >> (h + i)) & 1u;
+            pk[i] = key[i] >> ksv;
+            r[i][0] = key[i] & kmask;
+#pragma unroll
+            for (int w = 1; w < NW; ++w) r[i][w] = 0u;
+            if constexpr (VF == V_FMT_ID) {
+              r[i][0] |= lo[i] << ksv;
+            } else if constexpr (VF == V_FMT_32) {
+              r[i][1] = lo[i];
+            } else if constexpr (VF == V_FMT_64) {
+              r[i][1] = lo[i];
+              r[i][2] = hi[i];
+            }
+          }
+          bin_put_batch<kEB, NW>(B, act, pk, 0u, bins, BS, W, r, gp(ps.recs_v), lane, dbg);
+        }
+        if constexpr (VF == V_FMT_GEN) {  // every payload of the record (one put per step: up to kMaxVWords words)
 #pragma unroll
         for (int i = 0; i < kEB; ++i) {
           const bool mine = (m >> (h + i)) & 1u;
@@ -884,14 +979,7 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
           r[0] = key[i] & kmask;
 #pragma unroll
           for (int w = 1; w < NW; ++w) r[w] = 0u;
-          if constexpr (VF == V_FMT_ID) {
-            r[0] |= lo[i] << ksv;
-          } else if constexpr (VF == V_FMT_32) {
-            r[1] = lo[i];
-          } else if constexpr (VF == V_FMT_64) {
-            r[1] = lo[i];
-            r[2] = hi[i];
-          } else if constexpr (VF == V_FMT_GEN) {
+          {
             if (mine) {
               const int dl = local(h + i);
               const int64_t doc = doc_base + dl;
@@ -914,6 +1002,7 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
           }
           bin_put_wave<NW>(B, mine, p, 0u, bins, BS, W, r, gp(ps.recs_v), lane, dbg);
         }
+        }
       }
       if constexpr (pemit_hh(STRAT)) {
         // H records, value-parallel per step: each matching lane's doc owns n = max(1, values) consecutive records of
@@ -928,6 +1017,91 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
         const uint32_t kmask = (1u << ksh) - 1u;
         const int fsh = H.log2m + 6;
         const uint32_t first_bit = q->h_first ? 1u : 0u;
+        // every step's value ranges first (one wait for the batch)
+        int32_t v0s[kEB], nvs[kEB];
+#pragma unroll
+        for (int i = 0; i < kEB; ++i) {
+          v0s[i] = nvs[i] = 0;
+          if (hmv && ((m >> (h + i)) & 1u)) {
+            const int64_t doc = doc_base + local(h + i);
+            v0s[i] = gp(hoff)[doc];
+            nvs[i] = gp(hoff)[doc + 1] - v0s[i];
+          }
+        }
+        // Doc-reserved batch path (every matching doc of the batch has at most kDocVals records), kHS steps at a time
+        // with every phase a run of independent operations (one wait per phase): reserve each doc's consecutive bin
+        // slots (one cnt atomic per doc; records past the bin's end are reserved at the back of the range), decode
+        // every value of every doc (each lane its own docs: the step's docs are consecutive, so their values are one
+        // short stretch of the MV stream and the loads stay nearly coalesced), gather their (register, rank), write
+        // the records, count them done (one atomic per doc), store the bins that filled.
+        bool big = false;
+#pragma unroll
+        for (int i = 0; i < kEB; ++i) big |= ((m >> (h + i)) & 1u) && nvs[i] > kDocVals;
+        if (hmv && __ballot(big) == 0) {
+          constexpr int kHS = 4;
+#pragma unroll
+          for (int h2 = 0; h2 < kEB; h2 += kHS) {
+            bool mn[kHS];
+            uint32_t nn[kHS], pp[kHS], sl[kHS], inb[kHS], db[kHS];
+            uint32_t maxn = 0;
+#pragma unroll
+            for (int j = 0; j < kHS; ++j) {
+              const int i = h2 + j;
+              mn[j] = (m >> (h + i)) & 1u;
+              nn[j] = mn[j] ? (nvs[i] > 0 ? (uint32_t)nvs[i] : 1u) : 0u;
+              maxn = max(maxn, nn[j]);
+              pp[j] = (uint32_t)pv + (key[i] >> ksh);
+            }
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) maxn = max(maxn, (uint32_t)__shfl_xor((int)maxn, o, kWave));
+            maxn = (uint32_t)__builtin_amdgcn_readfirstlane((int)maxn);
+            if (maxn == 0) continue;
+#pragma unroll
+            for (int j = 0; j < kHS; ++j) sl[j] = mn[j] ? __hip_atomic_fetch_add(B.cnt + pp[j], nn[j], WG_RLX) : 0u;
+#pragma unroll
+            for (int j = 0; j < kHS; ++j) {
+              inb[j] = (mn[j] && sl[j] < BS) ? min(nn[j], BS - sl[j]) : 0u;
+              const uint32_t nd = nn[j] - inb[j];
+              db[j] = (nd && !(dbg & 1)) ? __hip_atomic_fetch_sub(B.back + pp[j], nd, WG_RLX) - nd : 0u;
+            }
+            uint32_t val[kHS][kDocVals];
+#pragma unroll
+            for (int j = 0; j < kHS; ++j)
+#pragma unroll
+              for (int e = 0; e < kDocVals; ++e) {
+                val[j][e] = 0u;
+                if ((uint32_t)e < maxn && e < nvs[h2 + j] && mn[j])
+                  val[j][e] = (dbg & 4) ? (uint32_t)e : decode_global(hwords, (int64_t)v0s[h2 + j] + e, hnb);
+              }
+#pragma unroll
+            for (int j = 0; j < kHS; ++j)
+#pragma unroll
+              for (int e = 0; e < kDocVals; ++e)
+                if ((uint32_t)e < maxn && e < nvs[h2 + j] && mn[j] && !(dbg & 2)) val[j][e] = gp(hlut)[val[j][e]];
+#pragma unroll
+            for (int j = 0; j < kHS; ++j) {
+              const uint32_t w = (key[h2 + j] & kmask) << fsh;
+              lds_u32_t* bin = bins + (pp[j] - (uint32_t)pv) * BS + sl[j];
+              AS1 uint32_t* dd = gp(ps.recs_h) + (B.start[pp[j]] + db[j]) - inb[j];
+#pragma unroll
+              for (int e = 0; e < kDocVals; ++e) {
+                if ((uint32_t)e >= maxn || (uint32_t)e >= nn[j]) continue;
+                // (an empty doc's one record has rank 0: no register update; it carries the first-value flag)
+                const uint32_t hv = e < nvs[h2 + j] ? val[j][e] : 0u;
+                const uint32_t r = w | (e == 0 ? first_bit : 0u) | ((hv >> 8) << 6) | ((hv & 0xffu) << 1);
+                if ((uint32_t)e < inb[j]) bin[e] = r;
+                else if (!(dbg & 1)) dd[e] = r;
+              }
+            }
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            bool full[kHS];
+#pragma unroll
+            for (int j = 0; j < kHS; ++j)
+              full[j] = inb[j] > 0 && __hip_atomic_fetch_add(B.done + pp[j], inb[j], WG_RLX) + inb[j] == BS;
+            flush_full_bins<kHS>(B, full, pp, (uint32_t)pv, bins, BS, 1u, gp(ps.recs_h), lane, dbg);
+          }
+          continue;  // (the batch loop `h`)
+        }
 #pragma unroll 1
         for (int i = 0; i < kEB; ++i) {
           const bool mine = (m >> (h + i)) & 1u;
@@ -935,16 +1109,64 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
           const int dl = local(h + i);
           const int64_t doc = doc_base + dl;
           uint32_t n = 0, hv_sv = 0;
-          int32_t v0 = 0, nv = 0;
+          const int32_t v0 = v0s[i], nv = nvs[i];
           if (mine) {
             if (hmv) {
-              v0 = gp(hoff)[doc];
-              nv = gp(hoff)[doc + 1] - v0;
               n = nv > 0 ? (uint32_t)nv : 1u;
             } else {
               n = 1u;
               hv_sv = (uint32_t)agg_value(H, ha, seg, img, dl, doc).i;
             }
+          }
+          if (__ballot(n > (uint32_t)kDocVals) == 0) {
+            // Doc-reserved path (every doc of the step has at most kDocVals records): one slot reservation per doc
+            // (its records are consecutive in its bin), each lane decodes its own doc's values (the step's docs are
+            // consecutive, so their values are one short stretch of the MV stream: the loads stay nearly coalesced),
+            // one done count per doc. Records past the bin's end go to the back of the range.
+            uint32_t maxn = n;
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) maxn = max(maxn, (uint32_t)__shfl_xor((int)maxn, o, kWave));
+            maxn = (uint32_t)__builtin_amdgcn_readfirstlane((int)maxn);
+            const uint32_t kk = key[i];
+            const uint32_t p = (uint32_t)pv + (kk >> ksh);
+            const uint32_t sl = mine ? __hip_atomic_fetch_add(B.cnt + p, n, WG_RLX) : 0u;
+            const uint32_t inbin = (mine && sl < BS) ? min(n, BS - sl) : 0u;
+            const uint32_t nd = mine ? n - inbin : 0u;
+            uint32_t db = 0;
+            if (nd && !(dbg & 1)) db = __hip_atomic_fetch_sub(B.back + p, nd, WG_RLX) - nd;
+            uint32_t hvv[kDocVals];
+            if (hmv) {
+              uint32_t idv[kDocVals];
+#pragma unroll
+              for (int e = 0; e < kDocVals; ++e) {
+                idv[e] = 0u;
+                if ((uint32_t)e < maxn && mine && e < nv)
+                  idv[e] = (dbg & 4) ? (uint32_t)e : decode_global(hwords, (int64_t)v0 + e, hnb);
+              }
+#pragma unroll
+              for (int e = 0; e < kDocVals; ++e) {
+                hvv[e] = 0u;  // (an empty doc's one record: rank 0, no register update)
+                if ((uint32_t)e < maxn && mine && e < nv) hvv[e] = (dbg & 2) ? idv[e] : gp(hlut)[idv[e]];
+              }
+            } else {
+#pragma unroll
+              for (int e = 0; e < kDocVals; ++e) hvv[e] = hv_sv;
+            }
+            const uint32_t w = (kk & kmask) << fsh;
+            lds_u32_t* bin = bins + (p - (uint32_t)pv) * BS + sl;
+            AS1 uint32_t* dd = gp(ps.recs_h) + (B.start[p] + db) - inbin;
+#pragma unroll
+            for (int e = 0; e < kDocVals; ++e) {
+              if ((uint32_t)e >= maxn || !mine || (uint32_t)e >= n) continue;
+              const uint32_t r = w | (e == 0 ? first_bit : 0u) | ((hvv[e] >> 8) << 6) | ((hvv[e] & 0xffu) << 1);
+              if ((uint32_t)e < inbin) bin[e] = r;
+              else if (!(dbg & 1)) dd[e] = r;
+            }
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            bool full[1] = {inbin > 0 && __hip_atomic_fetch_add(B.done + p, inbin, WG_RLX) + inbin == BS};
+            const uint32_t pa[1] = {p};
+            flush_full_bins<1>(B, full, pa, (uint32_t)pv, bins, BS, 1u, gp(ps.recs_h), lane, dbg);
+            continue;
           }
           uint32_t incl = n;
 #pragma unroll
@@ -981,12 +1203,15 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
             uint32_t hv[kHB];
 #pragma unroll
             for (int k = 0; k < kHB; ++k) hv[k] = ok[k] == 2 && !(dbg & 2) ? gp(hlut)[id[k]] : id[k];  // (register << 8) | rank
+            bool act[kHB];
+            uint32_t pp[kHB], r[kHB][1];
 #pragma unroll
             for (int k = 0; k < kHB; ++k) {
-              if (__ballot(ok[k] != 0) == 0) break;  // (chunks fill in order: the rest are empty too)
-              const uint32_t r[1] = {w0[k] | ((hv[k] >> 8) << 6) | ((hv[k] & 0xffu) << 1)};
-              bin_put_wave<1>(B, ok[k] != 0, (uint32_t)pv + pk[k], (uint32_t)pv, bins, BS, 1u, r, gp(ps.recs_h), lane, dbg);
+              act[k] = ok[k] != 0;
+              pp[k] = (uint32_t)pv + pk[k];
+              r[k][0] = w0[k] | ((hv[k] >> 8) << 6) | ((hv[k] & 0xffu) << 1);
             }
+            bin_put_batch<kHB, 1>(B, act, pp, (uint32_t)pv, bins, BS, 1u, r, gp(ps.recs_h), lane, dbg);
           }
         }
       }
@@ -1288,10 +1513,12 @@ __device__ __forceinline__ int64_t xcd_major_block(int64_t b, int64_t G) {
 
 // LM = 1: lane-major tiles (STEPS must be 32) driven by the per-segment plan tables `plans`; LM = 0: step-major.
 template <int STRAT, int STEPS, int LM>
-__global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __restrict__ q,
+__global__ void __launch_bounds__(scan_waves(STRAT) * kWave, scan_waves(STRAT) == kWavesPerWG ? 4 : 1) scan_kernel(const DevQuery* __restrict__ q,
                                                        const DevSeg* __restrict__ segs,
                                                        const LmSegPlan* __restrict__ plans, PartScratch ps) {
   static_assert(!LM || STEPS == 32, "lane-major tiles are 2048 docs");
+  constexpr int WPW = scan_waves(STRAT);  // waves per workgroup
+  constexpr int WGS = WPW * kWave;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63;
   // wave-uniform by construction; readfirstlane makes the compiler keep the whole tile/segment cursor in SGPRs
@@ -1306,27 +1533,27 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
   if (STRAT == STRAT_LDS) {
     const int64_t K = q->num_keys;
     uint32_t* cnt = (uint32_t*)(lds_acc + q->lds_count_off);
-    for (int64_t k = threadIdx.x; k < K; k += kWGSize) cnt[k] = 0;
+    for (int64_t k = threadIdx.x; k < K; k += WGS) cnt[k] = 0;
     for (int a = 0; a < q->num_aggs; ++a) {
       const DevAgg& A = q->aggs[a];
       if (A.type == PA_AGG_COUNT) continue;
       if (A.type == PA_AGG_DISTINCTCOUNTHLL) {
         uint32_t* r = (uint32_t*)(lds_acc + A.lds_off);
-        for (int64_t k = threadIdx.x; k < (K << A.log2m); k += kWGSize) r[k] = 0;
+        for (int64_t k = threadIdx.x; k < (K << A.log2m); k += WGS) r[k] = 0;
       } else if (A.type == PA_AGG_DISTINCTCOUNT) {
         uint32_t* r = (uint32_t*)(lds_acc + A.lds_off);
-        for (int64_t k = threadIdx.x; k < K * A.nvals / 4; k += kWGSize) r[k] = 0;
+        for (int64_t k = threadIdx.x; k < K * A.nvals / 4; k += WGS) r[k] = 0;
       } else {
         int64_t* r = (int64_t*)(lds_acc + A.lds_off);
         const int64_t init = A.type == PA_AGG_MIN ? INT64_MAX : (A.type == PA_AGG_MAX ? INT64_MIN : 0);  // SUM, COUNT_MV: 0
         const int64_t n = (A.type == PA_AGG_SUM && A.src == SRC_LONG) ? 2 * K : K;
-        for (int64_t k = threadIdx.x; k < n; k += kWGSize) r[k] = init;  // SUM(double) 0.0 == all-zero bits
+        for (int64_t k = threadIdx.x; k < n; k += WGS) r[k] = init;  // SUM(double) 0.0 == all-zero bits
       }
     }
     __syncthreads();
   } else if (STRAT == STRAT_PCOUNT) {
     uint32_t* hist = (uint32_t*)lds_acc;
-    for (int p = threadIdx.x; p < q->num_parts; p += kWGSize) hist[p] = 0u;
+    for (int p = threadIdx.x; p < q->num_parts; p += WGS) hist[p] = 0u;
     __syncthreads();
   } else if (is_pemit(STRAT)) {
     // every partition's bin empty; its range in the stream: the partition base + this workgroup's offset (part_scan),
@@ -1334,7 +1561,7 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
     const BinState B = bin_state(q, lds_acc);
     const int64_t lbi = q->xcd_major ? xcd_major_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
     const int P = q->num_parts, pv = q->pv;
-    for (int p = threadIdx.x; p < P; p += kWGSize) {
+    for (int p = q->part_lo + threadIdx.x; p < q->part_hi; p += WGS) {
       B.cnt[p] = 0u;
       B.done[p] = 0u;
       B.front[p] = 0u;
@@ -1346,9 +1573,9 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
 
   uint32_t matched = 0;  // docs of this lane that passed the filter (numDocsScanned)
   const int64_t T = q->total_wtiles;
-  const int64_t W = (int64_t)gridDim.x * kWavesPerWG;
+  const int64_t W = (int64_t)gridDim.x * WPW;
   const int64_t lb = q->xcd_major ? xcd_major_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;  // logical block
-  const int64_t gw = lb * kWavesPerWG + wave;
+  const int64_t gw = lb * WPW + wave;
   const int64_t t0 = gw * T / W;
   const int64_t t1 = (gw + 1) * T / W;
   if (t0 < t1) {
@@ -1473,14 +1700,14 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
   if (STRAT == STRAT_PCOUNT) {
     __syncthreads();
     const uint32_t* hist = (const uint32_t*)lds_acc;
-    for (int p = threadIdx.x; p < q->num_parts; p += kWGSize) gp(ps.hist)[lb * q->num_parts + p] = hist[p];
+    for (int p = threadIdx.x; p < q->num_parts; p += WGS) gp(ps.hist)[lb * q->num_parts + p] = hist[p];
   }
   if (is_pemit(STRAT)) {
     // every bin's rest (< one bin) between the range's front and back, then sentinel records up to the padded end
     __syncthreads();
     const BinState B = bin_state(q, lds_acc);
     const int P = q->num_parts, pv = q->pv;
-    for (int p = threadIdx.x; p < P; p += kWGSize) {
+    for (int p = q->part_lo + threadIdx.x; p < q->part_hi; p += WGS) {
       const bool isv = p < pv;
       const uint32_t nw = isv ? (uint32_t)q->rec_words_v : 1u;
       const uint32_t BS = (uint32_t)(isv ? q->bs_v : q->bs_h);
@@ -1503,7 +1730,7 @@ __global__ void __launch_bounds__(kWGSize, 4) scan_kernel(const DevQuery* __rest
     __syncthreads();
     const int64_t K = q->num_keys;
     const uint32_t* cnt = (const uint32_t*)(lds_acc + q->lds_count_off);
-    for (int64_t k = threadIdx.x; k < K; k += kWGSize) {
+    for (int64_t k = threadIdx.x; k < K; k += WGS) {
       const uint32_t c = cnt[k];
       if (c == 0) continue;
       __hip_atomic_fetch_add(gp(q->count) + k, (unsigned long long)c, RLX);
@@ -2194,7 +2421,8 @@ static const void* scan_fn(int strategy, int steps, int lm) {
     case STRAT_LDS: return scan_fn_s<STRAT_LDS>(steps, lm);
     case STRAT_PCOUNT: return (const void*)scan_kernel<STRAT_PCOUNT, 16, 0>;  // the planner's only partitioned layout
 #define PA_PEMIT_CASE(VF, HH) \
-  case pemit_strat(VF, HH): return (const void*)scan_kernel<pemit_strat(VF, HH), 16, 0>;
+  case pemit_strat(VF, HH): return (const void*)scan_kernel<pemit_strat(VF, HH), 16, 0>; \
+  case pemit_strat(VF, HH, 1): return (const void*)scan_kernel<pemit_strat(VF, HH, 1), 16, 0>;
     PA_PEMIT_CASE(-1, 1)
     PA_PEMIT_CASE(V_FMT_KEY, 0) PA_PEMIT_CASE(V_FMT_KEY, 1) PA_PEMIT_CASE(V_FMT_ID, 0) PA_PEMIT_CASE(V_FMT_ID, 1)
     PA_PEMIT_CASE(V_FMT_32, 0) PA_PEMIT_CASE(V_FMT_32, 1) PA_PEMIT_CASE(V_FMT_64, 0) PA_PEMIT_CASE(V_FMT_64, 1)
@@ -2209,7 +2437,7 @@ hipError_t set_scan_lds_limit(int strategy, int steps, int lm, int bytes) {
 }
 
 hipError_t scan_occupancy(int strategy, int steps, int lm, int lds_bytes, int* blocks_per_cu) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, scan_fn(strategy, steps, lm), kWGSize,
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, scan_fn(strategy, steps, lm), scan_waves(strategy) * kWave,
                                                       (size_t)lds_bytes);
 }
 
@@ -2217,7 +2445,8 @@ hipError_t launch_scan(int strategy, int steps, int lm, int grid, int lds_bytes,
                        const LmSegPlan* plans, const PartScratch& ps, hipStream_t s) {
   PartScratch pcopy = ps;
   void* args[] = {(void*)&q, (void*)&segs, (void*)&plans, (void*)&pcopy};
-  return hipLaunchKernel(scan_fn(strategy, steps, lm), dim3(grid), dim3(kWGSize), args, (size_t)lds_bytes, s);
+  return hipLaunchKernel(scan_fn(strategy, steps, lm), dim3(grid), dim3(scan_waves(strategy) * kWave), args,
+                         (size_t)lds_bytes, s);
 }
 
 }  // namespace pa

@@ -127,13 +127,16 @@ def test_star_schema_config4_shape():
              "GROUP BY d1, d2, d3, d4 LIMIT 100000", segs, rel=DOUBLE_REL)
 
 
-@pytest.mark.parametrize("flags", [0, L.PA_QF_NO_PARTITION])
-def test_star_schema_partitioned_hll(flags):
+@pytest.mark.parametrize("flags,max_len,skew", [(0, 6, False), (L.PA_QF_NO_PARTITION, 6, False),
+                                                (L.PA_QF_NO_SPLIT_EMIT, 6, False), (0, 20, False), (0, 24, True)])
+def test_star_schema_partitioned_hll(flags, max_len, skew):
     """configs[4] shape over a key space that takes the partitioned path: one record per MV value carries the HLL
     register and rank, COUNT / SUM(r) count each doc once; HLL registers bit-exact, SUM(r) within DOUBLE_REL. Also an SV
-    DISTINCTCOUNTHLL and a COUNT-only HLL query."""
+    DISTINCTCOUNTHLL and a COUNT-only HLL query. Rows of up to 6 values take the doc-reserved emit path, longer rows
+    (up to 20, or skewed: mostly 1 value, some up to 24) the value-parallel one in the same batches; the V and H
+    records are emitted by two launches by default, by one with PA_QF_NO_SPLIT_EMIT."""
     sv = (("d1", 64), ("d2", 32), ("d3", 16), ("d4", 8))
-    segs = [mv_segment(30 + i, n, mv_cols=(("tags", 300, 6),), sv_cols=sv, raw_double=True)
+    segs = [mv_segment(30 + i, n, mv_cols=(("tags", 300, max_len),), sv_cols=sv, raw_double=True, skew=skew)
             for i, n in enumerate((50021, 20011))]
     gsegs = [GpuSegment(sg) for sg in segs]
     try:
@@ -148,7 +151,7 @@ def test_star_schema_partitioned_hll(flags):
             ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags)
             strategy = ex.stats()["plan"]["strategy"]
             ex.close()
-            assert strategy == ("global" if flags else "partitioned"), (sql, strategy)
+            assert strategy == ("global" if flags & L.PA_QF_NO_PARTITION else "partitioned"), (sql, strategy)
     finally:
         for g in gsegs:
             g.close()
