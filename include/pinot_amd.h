@@ -190,6 +190,7 @@ typedef struct {
 #define PA_QF_NO_PARTITION (1 << 21)      /* high-cardinality dense GROUP BY: per-doc global atomics, not partitioned */
 #define PA_QF_NO_SPLIT_EMIT (1 << 24)     /* partitioned aggregation with both record streams: one emit kernel for both
                                              (default: a V launch and an H launch, each holding only its own bins) */
+#define PA_QF_NO_LIMIT_WALK (1 << 25)     /* numGroupsLimit: first-position + sort trimming even where the prefix walk applies */
 #define PA_QF_PART_SHIFT 22               /* bits 22..23: LDS per partition of the partitioned aggregation (0 = auto,
                                              1 = 64 KiB, 2 = 96 KiB, 3 = 144 KiB): larger partitions = fewer record
                                              write fronts per XCD */
@@ -270,8 +271,9 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
  * differs from the sum of the group counts), <0 on error. */
 int64_t pa_query_matched_docs(const pa_query* q);
 
-/* numGroupsLimit: 1 if the first-seen trimming path runs for this query (some segment can reach the limit), 0 if
- * not, <0 if not prepared. */
+/* numGroupsLimit: 0 if no segment can reach the limit; 1 if the first-position + sort trimming passes run; 2 if the
+ * prefix walk runs (SV group-by over a direct key space: limit_walk_kernel + admission inside the scan); <0 if not
+ * prepared. */
 int32_t pa_query_limit_trimming(const pa_query* q);
 /* Segments whose distinct groups reached numGroupsLimit in the last pa_query_fetch (the reference's
  * numGroupsLimitReached is this > 0: GroupByOperator.java:112 per segment, GroupByCombineOperator.java:154 OR), <0 on

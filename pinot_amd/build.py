@@ -24,10 +24,21 @@ def build(force=False, verbose=False):
     if not force and not _stale():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", LIB + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
+    # one object per source, compiled in parallel (each translation unit holds its own kernels), then one link
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
+        cmd = [hipcc] + [f for f in FLAGS if f != "-shared"] + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    if any(p.wait() != 0 for p in procs):
+        raise RuntimeError("hipcc failed")
+    cmd = [hipcc] + FLAGS + objs + ["-o", LIB + ".tmp"]
     subprocess.run(cmd, check=True)
+    for o in objs:
+        os.remove(o)
     os.replace(LIB + ".tmp", LIB)
     return LIB
 

@@ -395,6 +395,7 @@ constexpr int64_t kMinParts = 256;          // pass C parallelism: one workgroup
 constexpr int64_t kMaxParts = 4096;          // partitions of one query (both streams)
 constexpr int64_t kDirectMaxKeys = int64_t(1) << 27;  // direct-indexed key space limit (beyond: hashed keys)
 constexpr uint64_t kMaxHashSlots = uint64_t(1) << 28;
+constexpr uint64_t kWalkMaxBitmapBytes = uint64_t(4) << 30;  // numGroupsLimit walk: admitted-key bitmaps of a query
 constexpr size_t kLdsBudget = 160 * 1024;
 
 struct Section {
@@ -518,6 +519,11 @@ struct pa_query {
   // numGroupsLimit first-seen trimming (launch_limit_passes): on when some segment can hold numGroupsLimit groups
   bool limit_mode = false;
   LimitDesc limit{};
+  // numGroupsLimit, walk form (limit_walk_kernel + admission inside the scan): admitted-key bitmaps of the segments
+  // where the limit can bind (walk_words words each)
+  bool limit_walk = false;
+  int64_t walk_words = 0;
+  DevBuf lim_admit;
   int limit_grid = 0;
   DevBuf lim_keys, lim_pos, lim_sk, lim_sorted, lim_thresh, lim_temp;
   size_t lim_temp_bytes = 0;
@@ -541,6 +547,7 @@ struct pa_query {
     dev_free(lim_sorted);
     dev_free(lim_thresh);
     dev_free(lim_temp);
+    dev_free(lim_admit);
     if (host_acc) (void)hipHostFree(host_acc);
     dev_free(fetch_blocks);
     dev_free(fetch_stage);
@@ -607,6 +614,7 @@ struct Prep {
   std::vector<char> gb_raw;
   uint64_t limit_pairs = 0;
   int limit_eb = 0;
+  std::vector<char> limit_bind;  // per segment: the limit can bind there
   std::vector<int> agg_src;
   std::vector<char> val_fast, agg_mv;
   bool gb_mv = false;
@@ -782,8 +790,10 @@ int plan_key_space(pa_query* q, Prep& P) {
 int plan_limit(pa_query* q, Prep& P) {
   const pa_query_spec& s = q->spec;
   q->limit_mode = false;
+  q->limit_walk = false;
   P.limit_pairs = 0;
   P.limit_eb = 0;
+  P.limit_bind.assign(q->nseg, 0);
   if (s.num_group_by == 0 || s.num_groups_limit <= 0) return PA_OK;
   auto sat_mul = [](uint64_t a, uint64_t b) { return (b != 0 && a > UINT64_MAX / b) ? UINT64_MAX : a * b; };
   uint64_t max_exp = 1;
@@ -806,10 +816,21 @@ int plan_limit(pa_query* q, Prep& P) {
     const uint64_t pairs = nmv == 1 ? (uint64_t)mv_total : sat_mul((uint64_t)seg->num_docs, per_doc);
     const uint64_t bound = std::min(distinct, pairs);
     if (bound >= (uint64_t)s.num_groups_limit) q->limit_mode = true;
+    P.limit_bind[si] = bound >= (uint64_t)s.num_groups_limit;
     P.limit_pairs = std::min<uint64_t>(UINT64_MAX / 4, P.limit_pairs + bound);
     max_exp = std::max(max_exp, per_doc);
   }
   while (P.limit_eb < 63 && (uint64_t(1) << P.limit_eb) < max_exp) ++P.limit_eb;
+  // Walk form: one key per doc (no MV group-by) in a direct key space; its bitmaps (LDS while they fit, else HBM)
+  // take at most kWalkMaxBitmapBytes
+  int64_t nbind = 0;
+  for (int si = 0; si < q->nseg; ++si) nbind += P.limit_bind[si] ? 1 : 0;
+  if (q->limit_mode && !q->hashed && max_exp == 1 && (uint64_t)nbind * (uint64_t)((q->num_keys + 31) / 32) * 4 <=
+      kWalkMaxBitmapBytes && !(s.flags & PA_QF_NO_LIMIT_WALK)) {
+    q->limit_mode = false;
+    q->limit_walk = true;
+    q->walk_words = (q->num_keys + 31) / 32;
+  }
   if (q->limit_mode) {
     if (P.limit_eb > 21) return fail(PA_EUNSUPPORTED, "numGroupsLimit trimming: more than 2^21 group keys in one doc");
     if (q->nseg >= 4095) return fail(PA_EUNSUPPORTED, "numGroupsLimit trimming: more than 4094 segments in one query");
@@ -1513,6 +1534,7 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
     h.gb_stride[j] = P.stride[j];
   }
   h.num_keys = q->num_keys;
+  h.num_groups_limit = s.num_groups_limit;
   h.total_wtiles = total_tiles;
   h.ring = plan.ring;
   h.num_eager = q->num_eager;
@@ -1587,6 +1609,19 @@ int plan_scratch(pa_query* q, const Prep& P) {
   ScratchArena* a = arena_for(q->scratch_dev);
   std::lock_guard<std::mutex> g(a->mu);
   return arena_grow(a, q->sc_bytes);
+}
+
+// Walk form of numGroupsLimit: one admitted-key bitmap per segment where the limit can bind (DevSeg::admit).
+int plan_walk(pa_query* q, const Prep& P) {
+  if (!q->limit_walk) return PA_OK;
+  int64_t n = 0;
+  for (int si = 0; si < q->nseg; ++si) n += P.limit_bind[si] ? 1 : 0;
+  int rc = dev_alloc(q->lim_admit, (size_t)std::max<int64_t>(1, n) * (size_t)q->walk_words * 4);
+  if (rc) return rc;
+  int64_t k = 0;
+  for (int si = 0; si < q->nseg; ++si)
+    q->hsegs[si].admit = P.limit_bind[si] ? (const uint32_t*)q->lim_admit.p + (k++) * q->walk_words : nullptr;
+  return PA_OK;
 }
 
 int plan_limit_buffers(pa_query* q, const Prep& P, int cus, int64_t total_tiles) {
@@ -1784,6 +1819,7 @@ int pa_query_prepare(pa_query* q) {
   if (!rc) rc = plan_key_space(q, P);
   if (!rc) rc = plan_limit(q, P);
   if (!rc) rc = build_segments(q, P);
+  if (!rc) rc = plan_walk(q, P);
   if (!rc) rc = plan_accumulators(q, P);
   TilePlan plan, count_plan;
   if (!rc) rc = plan_kernels(q, P, plan, count_plan);
@@ -1885,6 +1921,10 @@ int pa_query_scan(pa_query* q, void* stream) {
   if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
   if (q->num_tiles == 0) return PA_OK;
   hipStream_t st = (hipStream_t)stream;
+  if (q->limit_walk) {  // admitted keys of every segment where the limit can bind, before any pass tests them
+    if (q->walk_words > kWalkMaxWords) PA_HIP(hipMemsetAsync(q->lim_admit.p, 0, q->lim_admit.n, st));
+    PA_HIP(launch_limit_walk((const DevQuery*)q->dq.p, (const DevSeg*)q->dsegs.p, q->nseg, q->walk_words, st));
+  }
   if (q->limit_mode) {  // first-seen positions, sort, thresholds, admitted aggregation
     const DevQuery* dq = (const DevQuery*)q->dq.p;
     const DevSeg* ds = (const DevSeg*)q->dsegs.p;
@@ -2208,7 +2248,9 @@ int32_t pa_query_lane_major(const pa_query* q) { return q && q->prepared ? q->la
 
 int64_t pa_query_matched_docs(const pa_query* q) { return q && q->prepared ? q->last_matched : -1; }
 
-int32_t pa_query_limit_trimming(const pa_query* q) { return q && q->prepared ? (q->limit_mode ? 1 : 0) : -1; }
+int32_t pa_query_limit_trimming(const pa_query* q) {
+  return q && q->prepared ? (q->limit_mode ? 1 : (q->limit_walk ? 2 : 0)) : -1;
+}
 
 int64_t pa_query_num_groups_limit_reached(const pa_query* q) { return q && q->prepared ? q->last_reached : -1; }
 

@@ -114,6 +114,8 @@ struct DevSeg {
   const int32_t* vremap;                   // V_FMT_ID: dictId of the value column -> table-wide value id (nullptr = id)
   const uint32_t* hll_lut[PA_MAX_AGGS];    // HLL: dictId -> (register index << 8) | rank; DISTINCTCOUNT: dictId ->
                                            // table-wide value id (nullptr = identity)
+  const uint32_t* admit;                   // numGroupsLimit walk: bitmap of the table-wide keys admitted in this
+                                           // segment (limit_walk_kernel writes it); nullptr = every key admitted
 };
 
 struct DevAgg {
@@ -180,6 +182,7 @@ struct DevQuery {
   uint32_t lds_count_off;    // LDS strategy: byte offset of u32 count[num_keys]
   uint32_t lds_acc_bytes;    // LDS bytes in front of the tile ring: LDS strategy accumulators / partition state
   DevAgg aggs[PA_MAX_AGGS];
+  int64_t num_groups_limit;  // numGroupsLimit (limit_walk_kernel)
 };
 
 // Scratch of a partitioned query, handed to its kernels per launch (it lives in the device's pooled arena).

@@ -1219,6 +1219,50 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
   }
 }
 
+// numGroupsLimit (walk form): the docs of match words m whose table-wide group key is admitted in this segment
+// (seg->admit, written by limit_walk_kernel). Eight steps per batch: every dictId decode, then every remap gather, then
+// every bitmap gather (their latencies overlap).
+template <int LM, int STEPS>
+__device__ __forceinline__ uint32_t admitted_docs(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                                  const uint32_t* img, int64_t doc_base, uint32_t m, int lane) {
+  auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
+  const uint32_t* adm = seg->admit;
+  const int ngb = q->num_gb;
+  constexpr int kB = 8;
+#pragma unroll 1
+  for (int h = 0; h < STEPS; h += kB) {
+    if (__ballot(((m >> h) & 0xffu) != 0) == 0) continue;
+    uint32_t key[kB];
+#pragma unroll
+    for (int i = 0; i < kB; ++i) key[i] = 0u;
+    for (int j = 0; j < ngb; ++j) {
+      const DevCol& c = seg->cols[q->gb_slot[j]];
+      const int32_t* rm = seg->remap[j];
+      const uint32_t st = (uint32_t)q->gb_stride[j];
+      uint32_t id[kB];
+#pragma unroll
+      for (int i = 0; i < kB; ++i) {
+        id[i] = 0u;
+        if ((m >> (h + i)) & 1u) id[i] = decode_dict_id<false>(c, img, local(h + i), doc_base + local(h + i));
+      }
+      if (rm != nullptr) {
+#pragma unroll
+        for (int i = 0; i < kB; ++i)
+          if ((m >> (h + i)) & 1u) id[i] = (uint32_t)gp(rm)[id[i]];
+      }
+#pragma unroll
+      for (int i = 0; i < kB; ++i) key[i] += id[i] * st;  // direct key space of at most kWalkMaxKeys keys
+    }
+    uint32_t w[kB];
+#pragma unroll
+    for (int i = 0; i < kB; ++i) w[i] = ((m >> (h + i)) & 1u) ? gp(adm)[key[i] >> 5] : 0u;
+#pragma unroll
+    for (int i = 0; i < kB; ++i)
+      if (!((w[i] >> (key[i] & 31u)) & 1u)) m &= ~(1u << (h + i));
+  }
+  return m;
+}
+
 template <int STRAT, int STEPS, int LM>
 __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg_in,
                                                 const uint32_t* img, int64_t doc_base, uint32_t m, int lane,
@@ -1250,6 +1294,11 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
     }
     if (__ballot(m != 0) == 0) return 0;
   }
+  const uint32_t scanned = m;  // numDocsScanned counts every doc the filter kept, admitted or not
+  if (seg->admit != nullptr) {
+    m = admitted_docs<LM, STEPS>(q, seg, img, doc_base, m, lane);
+    if (__ballot(m != 0) == 0) return (uint32_t)__builtin_popcount(scanned);
+  }
   if constexpr (STRAT == STRAT_PCOUNT || is_pemit(STRAT)) {
     part_tile<STRAT, STEPS, LM>(q, seg, img, doc_base, m, lane, lds, ps);
   } else if (q->has_mv) {
@@ -1263,7 +1312,7 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
     }
   }
   __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // vmcnt(0): no compiler-visible load left pending
-  return (uint32_t)__builtin_popcount(m);
+  return (uint32_t)__builtin_popcount(scanned);
 }
 
 template <int STRAT, int STEPS>
@@ -1939,6 +1988,133 @@ __global__ void __launch_bounds__(256) limit_agg_kernel(const DevQuery* __restri
       update_doc_key<STRAT_GLOBAL, true>(q, seg, nullptr, 0, doc, slot, acc);
     });
   });
+}
+
+// ---- walk form (SV group-by columns over a direct key space of at most kWalkMaxKeys keys)
+// A key is admitted in segment s iff it occurs among the segment's matching docs before the doc that brings its
+// numGroupsLimit-th distinct key, i.e. iff it is in the set of keys seen in the docId prefix [0, T_s). With keys
+// spread over a segment, that prefix is short (the first L distinct keys show up within ~L docs when keys are dense),
+// so one workgroup per segment walks it in docId order with the key set as an LDS bitmap, instead of a first-position
+// pass over every doc: rounds of kWalkRound docs mark their keys with LDS atomicOr (the old bit tells "new": the
+// number of distinct new keys of a round is exact in any order); the round in which the count reaches L is undone and
+// replayed by one wave in docId order (64 docs at a time, duplicates inside a step resolved by lane order), stopping
+// at the L-th distinct key. The bitmap is then the segment's admitted keys (admitted_docs tests it in the scan).
+constexpr int kWalkThreads = 1024;
+constexpr int kWalkPerThread = 8;
+constexpr int kWalkRound = kWalkThreads * kWalkPerThread;
+constexpr uint32_t kNoKey = 0xffffffffu;
+
+__device__ __forceinline__ uint32_t walk_key(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int64_t doc) {
+  if (doc >= seg->num_docs || !doc_passes(q, seg, doc)) return kNoKey;
+  uint32_t key = 0;
+  for (int j = 0; j < q->num_gb; ++j)
+    key += (uint32_t)gb_component<true>(seg->cols[q->gb_slot[j]], seg->remap[j], nullptr, 0, doc) *
+           (uint32_t)q->gb_stride[j];
+  return key;
+}
+
+// G: the bitmap is the segment's admit bitmap in HBM (zeroed by the host; key spaces beyond kWalkMaxWords * 32 keys),
+// else an LDS copy written out at the end.
+template <bool G>
+__global__ void __launch_bounds__(kWalkThreads) limit_walk_kernel(const DevQuery* __restrict__ q,
+                                                                   const DevSeg* __restrict__ segs, int64_t words) {
+  extern __shared__ uint32_t lds_seen[];
+  __shared__ uint32_t round_new[2];  // by round parity: a round resets its counter while the last one may be read
+  const DevSeg* seg = segs + blockIdx.x;
+  uint32_t* adm = (uint32_t*)seg->admit;
+  if (adm == nullptr) return;  // (workgroup-uniform) the limit cannot bind in this segment
+  uint32_t* seen = G ? adm : lds_seen;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  if (!G)
+    for (int64_t w = tid; w < words; w += kWalkThreads) seen[w] = 0u;
+  const int64_t L = q->num_groups_limit;
+  const int64_t nd = seg->num_docs;
+  int64_t cnt = 0;  // distinct keys before the current round
+  bool reached = false;
+  __syncthreads();
+  int par = 0;
+  for (int64_t d0 = 0; d0 < nd && !reached; d0 += kWalkRound, par ^= 1) {
+    if (tid == 0) round_new[par] = 0u;
+    uint32_t key[kWalkPerThread];
+#pragma unroll
+    for (int k = 0; k < kWalkPerThread; ++k) key[k] = walk_key(q, seg, d0 + (int64_t)k * kWalkThreads + tid);
+    __syncthreads();
+    uint32_t mine = 0;  // bit k: this thread's doc k brought a key new to the bitmap
+#pragma unroll
+    for (int k = 0; k < kWalkPerThread; ++k) {
+      if (key[k] == kNoKey) continue;
+      const uint32_t b = 1u << (key[k] & 31u);
+      if (!(atomicOr(seen + (key[k] >> 5), b) & b)) mine |= 1u << k;
+    }
+    uint32_t n = (uint32_t)__builtin_popcount(mine);
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) n += (uint32_t)__shfl_xor((int)n, o, kWave);
+    if (lane == 0 && n) atomicAdd(&round_new[par], n);
+    __syncthreads();
+    const int64_t rn = round_new[par];  // workgroup-uniform
+    if (cnt + rn < L) {
+      cnt += rn;
+      continue;
+    }
+    // the L-th distinct key appears in this round: undo its marks, replay it in docId order with one wave
+#pragma unroll
+    for (int k = 0; k < kWalkPerThread; ++k)
+      if ((mine >> k) & 1u) atomicAnd(seen + (key[k] >> 5), ~(1u << (key[k] & 31u)));
+    __syncthreads();
+    if (tid < kWave) {
+      for (int64_t b = d0; b < d0 + kWalkRound && b < nd; b += kWave) {
+        const uint32_t k0 = walk_key(q, seg, b + lane);
+        // (an atomic load: in HBM the bitmap's lines may sit stale in this CU's L1 after the atomics at L2)
+        bool cand = k0 != kNoKey &&
+                    !((__hip_atomic_load(seen + (k0 >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (k0 & 31u)) & 1u);
+        // a key new to the bitmap counts at its first lane only
+        uint64_t cm = __ballot(cand);
+        bool dup = false;
+        while (cm) {
+          const int j = __builtin_ctzll(cm);
+          cm &= cm - 1;
+          const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)k0, j);
+          dup |= j < lane && kj == k0;
+        }
+        const bool nw = cand && !dup;
+        const uint64_t nm = __ballot(nw);
+        const int64_t c = __builtin_popcountll(nm);
+        uint64_t take = nm;
+        if (cnt + c >= L) {  // keep the first L - cnt new keys of this step
+          int64_t need = L - cnt;
+          uint64_t t = 0, r = nm;
+          while (need-- > 0) {
+            const uint64_t low = r & (~r + 1);
+            t |= low;
+            r &= r - 1;
+          }
+          take = t;
+        }
+        if ((take >> lane) & 1ull) atomicOr(seen + (k0 >> 5), 1u << (k0 & 31u));
+        cnt += __builtin_popcountll(take);
+        if (cnt >= L) break;
+      }
+    }
+    reached = true;
+    __syncthreads();
+  }
+  __syncthreads();
+  if (!G)
+    for (int64_t w = tid; w < words; w += kWalkThreads) gp(adm)[w] = seen[w];
+  if (reached && tid == 0) __hip_atomic_fetch_add(gp(q->matched_docs) + 2, 1ull, RLX);  // numGroupsLimitReached
+}
+
+hipError_t launch_limit_walk(const DevQuery* q, const DevSeg* segs, int nseg, int64_t words, hipStream_t s) {
+  if (words > kWalkMaxWords) {
+    limit_walk_kernel<true><<<nseg, kWalkThreads, 0, s>>>(q, segs, words);
+    return hipGetLastError();
+  }
+  const size_t lds = (size_t)words * 4;
+  hipError_t e = hipFuncSetAttribute((const void*)limit_walk_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  limit_walk_kernel<false><<<nseg, kWalkThreads, lds, s>>>(q, segs, words);
+  return hipGetLastError();
 }
 
 hipError_t launch_limit_passes(const DevQuery* q, const DevSeg* segs, const LimitDesc& F, int grid, int phase,

@@ -440,11 +440,17 @@ def test_hashed_dictionary_key_space():
 
 
 # ------------------------------------------------------------------ numGroupsLimit first-seen trimming
-def _limit_run(sql, segs, expect_trim=True, rel=0.0):
+# trimming modes (pa_query_limit_trimming): 0 none, 1 first positions + sort, 2 prefix walk
+WALK = 2
+SORTED = 1
+LIMIT_PATHS = [(0, WALK), (L.PA_QF_NO_LIMIT_WALK, SORTED)]
+
+
+def _limit_run(sql, segs, expect_trim=SORTED, rel=0.0, flags=0):
     q = parse_sql(sql)
     gsegs = [GpuSegment(sg) for sg in segs]
     try:
-        ex = GpuQueryExecutor(q, gsegs)
+        ex = GpuQueryExecutor(q, gsegs, flags=flags)
         try:
             assert ex.stats()["plan"]["limit_trimming"] == int(expect_trim)
             got = ex.run()
@@ -458,8 +464,9 @@ def _limit_run(sql, segs, expect_trim=True, rel=0.0):
     return got, exp
 
 
-@pytest.mark.parametrize("limit", [1, 7, 300, 5000])
-def test_num_groups_limit_trimming_sv(limit):
+@pytest.mark.parametrize("flags,mode", LIMIT_PATHS)
+@pytest.mark.parametrize("limit", [1, 7, 300, 5000, 30000])
+def test_num_groups_limit_trimming_sv(limit, flags, mode):
     """Two dictionary dims (~1M possible keys) over segments of different sizes, filtered: each segment keeps its
     first `limit` groups in docId order (IntGroupIdMap.getGroupId) and drops later keys' docs; the union over segments
     and numGroupsLimitReached match the oracle's first-seen maps exactly."""
@@ -467,17 +474,31 @@ def test_num_groups_limit_trimming_sv(limit):
     segs = [make_segment(500 + i, n, cols) for i, n in enumerate((40000, 9001, 123))]
     sql = ("SELECT k1, k2, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t WHERE f <> 3 GROUP BY k1, k2 LIMIT 100000000 "
            "OPTION(numGroupsLimit=%d)" % limit)
-    got, exp = _limit_run(sql, segs)
+    got, exp = _limit_run(sql, segs, mode, flags=flags)
     assert got.num_groups_limit_reached
     assert len(exp.groups) <= limit * len(segs)
+
+
+@pytest.mark.parametrize("flags", [0, L.PA_QF_FORCE_GLOBAL, L.PA_QF_NO_PARTITION, L.PA_QF_NO_LANE_MAJOR])
+def test_num_groups_limit_walk_every_strategy(flags):
+    """The walk's admitted keys are tested inside every scan strategy (partitioned count + emit passes, global
+    atomics, step-/lane-major tiles): dense 2-dim keys, segments whose crossing round is the first, a later one, or
+    never comes (fewer matching groups than the limit)."""
+    cols = {"k1": ("INT", 1000), "k2": ("LONG", 1000), "m": ("LONG", 5000), "f": ("INT", 10)}
+    segs = [make_segment(700 + i, n, cols) for i, n in enumerate((60000, 16000, 2500, 47000))]
+    sql = ("SELECT k1, k2, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t WHERE f <> 3 GROUP BY k1, k2 LIMIT 100000000 "
+           "OPTION(numGroupsLimit=15000)")
+    got, exp = _limit_run(sql, segs, WALK, flags=flags)
+    assert got.num_groups_limit_reached
 
 
 def test_num_groups_limit_default_binds():
     """Default numGroupsLimit (100000) on a segment with more distinct keys: trimmed on the GPU like the reference."""
     cols = {"k1": ("INT", 1000), "k2": ("LONG", 1000)}
     segs = [make_segment(32, 200000, cols)]
-    got, exp = _limit_run("SELECT k1, k2, COUNT(*) FROM t GROUP BY k1, k2 LIMIT 100000000", segs)
-    assert len(got.groups) == 100000 and got.num_groups_limit_reached
+    for flags, mode in LIMIT_PATHS:
+        got, exp = _limit_run("SELECT k1, k2, COUNT(*) FROM t GROUP BY k1, k2 LIMIT 100000000", segs, mode, flags=flags)
+        assert len(got.groups) == 100000 and got.num_groups_limit_reached
 
 
 def test_num_groups_limit_not_reached():
@@ -485,17 +506,19 @@ def test_num_groups_limit_not_reached():
     numGroupsLimitReached stays false."""
     cols = {"k1": ("INT", 1000), "k2": ("LONG", 1000), "f": ("INT", 1000)}
     segs = [make_segment(70 + i, 30000, cols) for i in range(2)]
-    got, exp = _limit_run("SELECT k1, k2, COUNT(*) FROM t WHERE f < 2 GROUP BY k1, k2 LIMIT 100000 "
-                          "OPTION(numGroupsLimit=20000)", segs)
-    assert not got.num_groups_limit_reached
+    for flags, mode in LIMIT_PATHS:
+        got, exp = _limit_run("SELECT k1, k2, COUNT(*) FROM t WHERE f < 2 GROUP BY k1, k2 LIMIT 100000 "
+                              "OPTION(numGroupsLimit=20000)", segs, mode, flags=flags)
+        assert not got.num_groups_limit_reached
 
 
 def test_num_groups_limit_hll_avg_double():
     """DISTINCTCOUNTHLL, AVG and DOUBLE sums under trimming."""
     cols = {"k1": ("INT", 300), "k2": ("INT", 200), "u": ("LONG", 50000), "d": ("DOUBLE", 5000)}
     segs = [make_segment(80 + i, 20000, cols) for i in range(2)]
-    _limit_run("SELECT k1, k2, DISTINCTCOUNTHLL(u), AVG(d), SUM(d) FROM t GROUP BY k1, k2 LIMIT 100000 "
-               "OPTION(numGroupsLimit=1000)", segs, rel=DOUBLE_REL)
+    for flags, mode in LIMIT_PATHS:
+        _limit_run("SELECT k1, k2, DISTINCTCOUNTHLL(u), AVG(d), SUM(d) FROM t GROUP BY k1, k2 LIMIT 100000 "
+                   "OPTION(numGroupsLimit=1000)", segs, mode, rel=DOUBLE_REL, flags=flags)
 
 
 def test_num_groups_limit_raw_hashed():
@@ -512,7 +535,7 @@ def test_num_groups_limit_not_triggered_below_bound():
     cols = {"k1": ("INT", 20), "k2": ("INT", 30)}
     segs = [make_segment(99, 5000, cols)]
     _limit_run("SELECT k1, k2, COUNT(*) FROM t GROUP BY k1, k2 LIMIT 1000 OPTION(numGroupsLimit=601)", segs,
-               expect_trim=False)
+               expect_trim=0)
 
 
 @pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LANE_MAJOR])

@@ -64,6 +64,8 @@ WORKLOADS = {
                      "OPTION(numGroupsLimit=2000000)", 0),
         ("filtered_10pct", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t WHERE m < 6554 GROUP BY d1, d2 "
                            "LIMIT 2000000 OPTION(numGroupsLimit=2000000)", 0),
+        # the default numGroupsLimit (100000 < 1M keys): first-seen trimming per segment (a11)
+        ("default_limit", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000", 0),
     ]),
     "star": (star_segment, [
         ("all_docs", "SELECT d1, d2, d3, d4, SUM(r), DISTINCTCOUNTHLLMV(tags) FROM t GROUP BY d1, d2, d3, d4 "
