@@ -504,6 +504,7 @@ struct pa_query {
   std::vector<DevSeg> hsegs_count;
   DevBuf dq_count, dsegs_count;
   int count_lds = 0, count_ring = 0, part_lds_c = 0;
+  int part_vk = -1;     // part_agg_kernel variant (vk_code, kVkGeneric)
   int emit_strat = 0;   // the emit kernel variant (pemit_strat)
   // both streams: the emit pass runs as two launches (V records, then H records), each with only its own bins in LDS
   // (more resident workgroups than one kernel holding both): the H launch's descriptor, variant and plan
@@ -1314,9 +1315,9 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
   int bs_h = hll >= 0 ? 32 : 0;
   const int Ptot = (int)(Pv + Ph);
   auto emit_state = [&](int bv, int bh) {
-    size_t b = (size_t)Ptot * 16 + (size_t)Ptot * 8;  // cnt, done, front, back + start
+    size_t b = (size_t)Ptot * 16 + (size_t)Ph * 4 + (size_t)Ptot * 8;  // cnt, done, front, back, H slack + start
     b = (b + 15) & ~(size_t)15;
-    b += (size_t)Pv * bv * W * 4 + (size_t)Ph * bh * 4;
+    b += (size_t)Pv * bv * W * 4 + (size_t)Ph * (bh ? bh + kDocVals : 0) * 4;  // H bins: + a crossing doc's tail
     return (b + 15) & ~(size_t)15;
   };
   // the emit pass stages its columns in a ring next to the bins: halve the bins (down to 64-byte bursts) while they
@@ -1385,12 +1386,37 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
   h.h_first = (hll >= 0 && !vstream) ? 1 : 0;
   h.hll_agg = hll;
   h.emit_val_agg = slots == 1 ? va : -1;
+  // specialised V pass C: one payload, at most one SUM / MIN / MAX
+  h.vop_sum = h.vop_min = h.vop_max = -1;
+  q->part_vk = kVkGeneric;
+  if (vstream && fmt != V_FMT_GEN) {
+    bool ok = true;
+    for (int a = 0; a < s.num_aggs && ok; ++a) {
+      const int t = s.aggs[a].type;
+      int32_t* slot = t == PA_AGG_SUM ? &h.vop_sum : (t == PA_AGG_MIN ? &h.vop_min : (t == PA_AGG_MAX ? &h.vop_max : nullptr));
+      if (t == PA_AGG_COUNT || t == PA_AGG_DISTINCTCOUNTHLL) continue;
+      if (!slot || *slot >= 0) ok = false;
+      else *slot = a;
+    }
+    if (ok) q->part_vk = vk_code(h.vop_sum >= 0 ? 1 + P.agg_src[h.vop_sum] : 0, h.vop_min >= 0, h.vop_max >= 0);
+  }
+  // value ids in value order: the table-wide union is sorted; a shared segment dictionary is checked
+  h.v_id_order = 0;
+  if (fmt == V_FMT_ID) {
+    const Column* c0 = q->segs[0]->cols.at(s.aggs[va].column_id);
+    bool sorted = true;
+    if (q->hsegs[0].vremap == nullptr)
+      for (size_t i = 1; i < c0->hvals.size() && sorted; ++i)
+        sorted = value_order_key(c0->hvals[i - 1], c0->vtype) < value_order_key(c0->hvals[i], c0->vtype);
+    h.v_id_order = sorted ? 1 : 0;
+  }
   h.vdict = vdict;
   size_t o = 0;
   h.lds_cnt = (uint32_t)o; o += (size_t)Ptot * 4;
   h.lds_done = (uint32_t)o; o += (size_t)Ptot * 4;
   h.lds_front = (uint32_t)o; o += (size_t)Ptot * 4;
   h.lds_back = (uint32_t)o; o += (size_t)Ptot * 4;
+  h.lds_slack = (uint32_t)o; o += (size_t)Ph * 4;
   o = (o + 7) & ~(size_t)7;
   h.lds_start = (uint32_t)o; o += (size_t)Ptot * 8;
   o = (o + 15) & ~(size_t)15;
@@ -1716,7 +1742,7 @@ int upload_descriptors(pa_query* q) {
     PA_HIP(set_scan_lds_limit(q->emit_strat, q->steps, 0, q->lds_bytes));
     if (q->split_emit) PA_HIP(set_scan_lds_limit(q->emit_h_strat, q->steps, 0, q->emit_h_lds));
     PA_HIP(set_scan_lds_limit(STRAT_PCOUNT, q->steps, 0, q->count_lds));
-    PA_HIP(set_part_agg_lds_limit(q->part_lds_c));
+    PA_HIP(set_part_agg_lds_limit(q->part_vk, q->part_lds_c));
   } else {
     PA_HIP(set_scan_lds_limit(q->strategy, q->steps, q->lane_major, q->lds_bytes));
   }
@@ -1955,7 +1981,7 @@ int pa_query_scan(pa_query* q, void* stream) {
     if (q->split_emit)
       PA_HIP(launch_scan(q->emit_h_strat, q->steps, 0, q->grid, q->emit_h_lds, (const DevQuery*)q->dq_h.p,
                          (const DevSeg*)q->dsegs.p, plans, ps, st));
-    PA_HIP(launch_part_agg((const DevQuery*)q->dq.p, ps, q->hq.num_parts, q->part_lds_c, st));
+    PA_HIP(launch_part_agg(q->part_vk, (const DevQuery*)q->dq.p, ps, q->hq.num_parts, q->part_lds_c, st));
     PA_HIP(hipEventRecord(a->last, st));
     a->last_stream = st;
     a->used = true;

@@ -171,6 +171,8 @@ struct DevQuery {
   int32_t debug_emit;        // measurement only (PA_DEBUG_EMIT): bit 0 skips the emit pass's record stores, bit 1 its HLL
                              // dictionary gathers, bit 2 its MV value reads (wrong results; isolates the waits)
   uint32_t lds_cnt, lds_done, lds_front, lds_back, lds_start;  // STRAT_PEMIT LDS (bytes): per-partition bin state
+  uint32_t lds_slack, pad_slack;  // STRAT_PEMIT LDS (bytes): per-partition parked tail of an H bin
+  // (H bins are bs_h + kDocVals records apart: the doc whose records cross the bin end parks its tail past it)
   uint32_t lds_bins_v, lds_bins_h;                            // STRAT_PEMIT LDS (bytes): the V and H bins
   const uint64_t* vdict;     // V_FMT_ID: table-wide values of the value column (int64, or double bits)
   int32_t staged_slots[kMaxSlots];
@@ -183,7 +185,15 @@ struct DevQuery {
   uint32_t lds_acc_bytes;    // LDS bytes in front of the tile ring: LDS strategy accumulators / partition state
   DevAgg aggs[PA_MAX_AGGS];
   int64_t num_groups_limit;  // numGroupsLimit (limit_walk_kernel)
+  // pass C of the V stream, specialised (part_agg_kernel<VK>): every non-COUNT aggregation reads the one payload of a
+  // V_FMT_ID/32/64 record and there is at most one SUM, one MIN and one MAX: their aggregation indices (-1 = none),
+  // and whether V_FMT_ID value ids are in value order (MIN/MAX then run on the 32-bit ids)
+  int32_t vop_sum, vop_min, vop_max;
+  int32_t v_id_order;
 };
+// part_agg_kernel variant: -1 generic, else sum kind (0 none, 1 + AccSrc) | MIN << 2 | MAX << 3
+constexpr int kVkGeneric = -1;
+__host__ __device__ constexpr int vk_code(int sum_kind, bool mn, bool mx) { return sum_kind | (mn ? 4 : 0) | (mx ? 8 : 0); }
 
 // Scratch of a partitioned query, handed to its kernels per launch (it lives in the device's pooled arena).
 struct PartScratch {

@@ -666,13 +666,15 @@ struct BinState {
   lds_u32_t* front;
   lds_u32_t* back;
   lds_u64_t* start;
+  lds_u32_t* slk;   // H bins: records of the doc that crossed the bin end, parked past it (<= kDocVals - 1)
 };
 
 __device__ __forceinline__ lds_u32_t* lds_ptr(const void* p) { return (lds_u32_t*)(uintptr_t)lds_addr(p); }
 
 __device__ __forceinline__ BinState bin_state(const DevQuery* __restrict__ q, unsigned char* lds) {
   return BinState{lds_ptr(lds + q->lds_cnt), lds_ptr(lds + q->lds_done), lds_ptr(lds + q->lds_front),
-                  lds_ptr(lds + q->lds_back), (lds_u64_t*)lds_ptr(lds + q->lds_start)};
+                  lds_ptr(lds + q->lds_back), (lds_u64_t*)lds_ptr(lds + q->lds_start),
+                  lds_ptr(lds + q->lds_slack) - q->pv};  // (slack words exist for the H partitions only)
 }
 
 #define WG_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP
@@ -690,22 +692,24 @@ __device__ __forceinline__ BinState bin_state(const DevQuery* __restrict__ q, un
 // program order (a signal fence). Acquire/release atomics would also wait for every outstanding global load, i.e.
 // drain the tile ring's LDS-DMA on every record. Only the wave that completed a bin touches its front and counters
 // until it resets them (a bin fills at most once per batch: it stays full until its flush).
-template <int K>
+template <int K, bool SL = false>
 __device__ __forceinline__ void flush_full_bins(const BinState& B, const bool (&full)[K], const uint32_t (&p)[K],
                                                 uint32_t p0, lds_u32_t* bins, uint32_t BS, uint32_t nw,
-                                                AS1 uint32_t* recs, int lane, int dbg);
+                                                AS1 uint32_t* recs, int lane, int dbg, uint32_t BST = 0);
 
-template <int K, int WM>
+template <int K, int WM, bool SL = false>
 __device__ __forceinline__ void bin_put_batch(const BinState& B, const bool (&act)[K], const uint32_t (&p)[K],
                                               uint32_t p0, lds_u32_t* bins, uint32_t BS, uint32_t nw,
-                                              const uint32_t (&r)[K][WM], AS1 uint32_t* recs, int lane, int dbg) {
+                                              const uint32_t (&r)[K][WM], AS1 uint32_t* recs, int lane, int dbg,
+                                              uint32_t BST = 0) {
+  if (BST == 0) BST = BS;
   uint32_t s[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) s[k] = act[k] ? __hip_atomic_fetch_add(B.cnt + p[k], 1u, WG_RLX) : 0xffffffffu;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     if (s[k] < BS) {
-      lds_u32_t* slot = bins + ((p[k] - p0) * BS + s[k]) * nw;
+      lds_u32_t* slot = bins + ((p[k] - p0) * BST + s[k]) * nw;
 #pragma unroll
       for (int w = 0; w < WM; ++w)
         if ((uint32_t)w < nw) slot[w] = r[k][w];
@@ -730,15 +734,18 @@ __device__ __forceinline__ void bin_put_batch(const BinState& B, const bool (&ac
       }
     }
   }
-  flush_full_bins<K>(B, full, p, p0, bins, BS, nw, recs, lane, dbg);
+  flush_full_bins<K, SL>(B, full, p, p0, bins, BS, nw, recs, lane, dbg, BST);
 }
 
 // The flush half of a put: every bin some lane completed (full[k]) is stored at its range's front slot — several bins
 // per store instruction (L lanes per bin, one 16-byte unit each) — and emptied.
-template <int K>
+// SL (H bins of the doc-reserved path): bins are BST records apart and may hold a crossing doc's tail past BS
+// (B.slk); after the store it moves to the bin's front and the bin restarts with it.
+template <int K, bool SL>
 __device__ __forceinline__ void flush_full_bins(const BinState& B, const bool (&full)[K], const uint32_t (&p)[K],
                                                 uint32_t p0, lds_u32_t* bins, uint32_t BS, uint32_t nw,
-                                                AS1 uint32_t* recs, int lane, int dbg) {
+                                                AS1 uint32_t* recs, int lane, int dbg, uint32_t BST) {
+  if (BST == 0) BST = BS;
   uint64_t fm[K];
   uint64_t any = 0;
 #pragma unroll
@@ -752,8 +759,10 @@ __device__ __forceinline__ void flush_full_bins(const BinState& B, const bool (&
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       if (full[k]) {
-        __hip_atomic_store(B.done + p[k], 0u, WG_RLX);
-        __hip_atomic_store(B.cnt + p[k], 0u, WG_RLX);
+        const uint32_t r = SL ? B.slk[p[k]] : 0u;
+        if (SL) B.slk[p[k]] = 0u;
+        __hip_atomic_store(B.done + p[k], r, WG_RLX);
+        __hip_atomic_store(B.cnt + p[k], r, WG_RLX);
       }
     }
     return;
@@ -767,18 +776,25 @@ __device__ __forceinline__ void flush_full_bins(const BinState& B, const bool (&
   uint32_t mine = 0xffffffffu, g = 0;
   auto store_round = [&]() {
     const bool on = grp < g;
-    uint32_t o = 0;
+    uint32_t o = 0, r = 0;
     if (on) {
       o = B.front[mine];
       AS1 u32x4* d = (AS1 u32x4*)(recs + (B.start[mine] + o) * (uint64_t)nw);
-      const lds_u32x4_t* sb = (const lds_u32x4_t*)(bins + (mine - p0) * BS * nw);
+      const lds_u32x4_t* sb = (const lds_u32x4_t*)(bins + (mine - p0) * BST * nw);
       for (uint32_t c = c0; c < n16; c += L) d[c] = sb[c];
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (SL && on) {  // the parked tail (one record per lane, nw == 1) to the bin's front
+      r = B.slk[mine];
+      lds_u32_t* b1 = bins + (mine - p0) * BST;
+      for (uint32_t c = c0; c < r; c += L) b1[c] = b1[BS + c];  // (r < kDocVals; L may be smaller)
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     if (on && c0 == 0) {
       B.front[mine] = o + BS;
-      __hip_atomic_store(B.done + mine, 0u, WG_RLX);
-      __hip_atomic_store(B.cnt + mine, 0u, WG_RLX);
+      if (SL) B.slk[mine] = 0u;
+      __hip_atomic_store(B.done + mine, r, WG_RLX);
+      __hip_atomic_store(B.cnt + mine, r, WG_RLX);
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     g = 0;
@@ -1013,6 +1029,7 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
         const int hnb = cs->cols[hslot].nbits;
         const uint32_t* hlut = cs->hll_lut[ha];  // dictId -> (register << 8) | rank
         const uint32_t BS = (uint32_t)q->bs_h;
+        const uint32_t BST = BS + (uint32_t)kDocVals;  // bin stride: room for a crossing doc's tail
         lds_u32_t* bins = lds_ptr(lds + q->lds_bins_h);
         const uint32_t kmask = (1u << ksh) - 1u;
         const int fsh = H.log2m + 6;
@@ -1058,11 +1075,14 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
             if (maxn == 0) continue;
 #pragma unroll
             for (int j = 0; j < kHS; ++j) sl[j] = mn[j] ? __hip_atomic_fetch_add(B.cnt + pp[j], nn[j], WG_RLX) : 0u;
+            // a doc whose slot lies in the bin keeps all its records there (a tail past BS parks in the slack); a doc
+            // arriving while the bin is full goes to the back of the range whole
+            bool bk[kHS];
 #pragma unroll
             for (int j = 0; j < kHS; ++j) {
+              bk[j] = mn[j] && sl[j] >= BS;
               inb[j] = (mn[j] && sl[j] < BS) ? min(nn[j], BS - sl[j]) : 0u;
-              const uint32_t nd = nn[j] - inb[j];
-              db[j] = (nd && !(dbg & 1)) ? __hip_atomic_fetch_sub(B.back + pp[j], nd, WG_RLX) - nd : 0u;
+              db[j] = (bk[j] && !(dbg & 1)) ? __hip_atomic_fetch_sub(B.back + pp[j], nn[j], WG_RLX) - nn[j] : 0u;
             }
             uint32_t val[kHS][kDocVals];
 #pragma unroll
@@ -1081,24 +1101,25 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
 #pragma unroll
             for (int j = 0; j < kHS; ++j) {
               const uint32_t w = (key[h2 + j] & kmask) << fsh;
-              lds_u32_t* bin = bins + (pp[j] - (uint32_t)pv) * BS + sl[j];
-              AS1 uint32_t* dd = gp(ps.recs_h) + (B.start[pp[j]] + db[j]) - inb[j];
+              lds_u32_t* bin = bins + (pp[j] - (uint32_t)pv) * BST + sl[j];
+              AS1 uint32_t* dd = gp(ps.recs_h) + (B.start[pp[j]] + db[j]);
 #pragma unroll
               for (int e = 0; e < kDocVals; ++e) {
                 if ((uint32_t)e >= maxn || (uint32_t)e >= nn[j]) continue;
                 // (an empty doc's one record has rank 0: no register update; it carries the first-value flag)
                 const uint32_t hv = e < nvs[h2 + j] ? val[j][e] : 0u;
                 const uint32_t r = w | (e == 0 ? first_bit : 0u) | ((hv >> 8) << 6) | ((hv & 0xffu) << 1);
-                if ((uint32_t)e < inb[j]) bin[e] = r;
+                if (!bk[j]) bin[e] = r;
                 else if (!(dbg & 1)) dd[e] = r;
               }
+              if (inb[j] && inb[j] < nn[j]) B.slk[pp[j]] = nn[j] - inb[j];  // the crossing doc's parked tail
             }
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
             bool full[kHS];
 #pragma unroll
             for (int j = 0; j < kHS; ++j)
               full[j] = inb[j] > 0 && __hip_atomic_fetch_add(B.done + pp[j], inb[j], WG_RLX) + inb[j] == BS;
-            flush_full_bins<kHS>(B, full, pp, (uint32_t)pv, bins, BS, 1u, gp(ps.recs_h), lane, dbg);
+            flush_full_bins<kHS, true>(B, full, pp, (uint32_t)pv, bins, BS, 1u, gp(ps.recs_h), lane, dbg, BST);
           }
           continue;  // (the batch loop `h`)
         }
@@ -1131,9 +1152,9 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
             const uint32_t p = (uint32_t)pv + (kk >> ksh);
             const uint32_t sl = mine ? __hip_atomic_fetch_add(B.cnt + p, n, WG_RLX) : 0u;
             const uint32_t inbin = (mine && sl < BS) ? min(n, BS - sl) : 0u;
-            const uint32_t nd = mine ? n - inbin : 0u;
+            const bool bk = mine && sl >= BS;  // (see the batched path: a tail past BS parks in the slack)
             uint32_t db = 0;
-            if (nd && !(dbg & 1)) db = __hip_atomic_fetch_sub(B.back + p, nd, WG_RLX) - nd;
+            if (bk && !(dbg & 1)) db = __hip_atomic_fetch_sub(B.back + p, n, WG_RLX) - n;
             uint32_t hvv[kDocVals];
             if (hmv) {
               uint32_t idv[kDocVals];
@@ -1153,19 +1174,20 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
               for (int e = 0; e < kDocVals; ++e) hvv[e] = hv_sv;
             }
             const uint32_t w = (kk & kmask) << fsh;
-            lds_u32_t* bin = bins + (p - (uint32_t)pv) * BS + sl;
-            AS1 uint32_t* dd = gp(ps.recs_h) + (B.start[p] + db) - inbin;
+            lds_u32_t* bin = bins + (p - (uint32_t)pv) * BST + sl;
+            AS1 uint32_t* dd = gp(ps.recs_h) + (B.start[p] + db);
 #pragma unroll
             for (int e = 0; e < kDocVals; ++e) {
               if ((uint32_t)e >= maxn || !mine || (uint32_t)e >= n) continue;
               const uint32_t r = w | (e == 0 ? first_bit : 0u) | ((hvv[e] >> 8) << 6) | ((hvv[e] & 0xffu) << 1);
-              if ((uint32_t)e < inbin) bin[e] = r;
+              if (!bk) bin[e] = r;
               else if (!(dbg & 1)) dd[e] = r;
             }
+            if (inbin && inbin < n) B.slk[p] = n - inbin;
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
             bool full[1] = {inbin > 0 && __hip_atomic_fetch_add(B.done + p, inbin, WG_RLX) + inbin == BS};
             const uint32_t pa[1] = {p};
-            flush_full_bins<1>(B, full, pa, (uint32_t)pv, bins, BS, 1u, gp(ps.recs_h), lane, dbg);
+            flush_full_bins<1, true>(B, full, pa, (uint32_t)pv, bins, BS, 1u, gp(ps.recs_h), lane, dbg, BST);
             continue;
           }
           uint32_t incl = n;
@@ -1211,7 +1233,7 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
               pp[k] = (uint32_t)pv + pk[k];
               r[k][0] = w0[k] | ((hv[k] >> 8) << 6) | ((hv[k] & 0xffu) << 1);
             }
-            bin_put_batch<kHB, 1>(B, act, pp, (uint32_t)pv, bins, BS, 1u, r, gp(ps.recs_h), lane, dbg);
+            bin_put_batch<kHB, 1, true>(B, act, pp, (uint32_t)pv, bins, BS, 1u, r, gp(ps.recs_h), lane, dbg, BST);
           }
         }
       }
@@ -1614,6 +1636,7 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, scan_waves(STRAT) =
       B.cnt[p] = 0u;
       B.done[p] = 0u;
       B.front[p] = 0u;
+      if (p >= pv) B.slk[p] = 0u;
       B.back[p] = gp(ps.hist)[lbi * P + p];
       B.start[p] = gp(ps.base)[p < pv ? p : p + 1] + gp(ps.off)[lbi * P + p];
     }
@@ -1761,7 +1784,7 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, scan_waves(STRAT) =
       const uint32_t nw = isv ? (uint32_t)q->rec_words_v : 1u;
       const uint32_t BS = (uint32_t)(isv ? q->bs_v : q->bs_h);
       const lds_u32_t* bin = isv ? lds_ptr(lds_acc + q->lds_bins_v) + (uint32_t)p * BS * nw
-                                 : lds_ptr(lds_acc + q->lds_bins_h) + (uint32_t)(p - pv) * BS;
+                                 : lds_ptr(lds_acc + q->lds_bins_h) + (uint32_t)(p - pv) * (BS + (uint32_t)kDocVals);
       AS1 uint32_t* recs = gp(isv ? ps.recs_v : ps.recs_h);
       const uint32_t n = B.cnt[p], o = B.front[p];
       const uint32_t h = gp(ps.hist)[lb * P + p];
@@ -2471,6 +2494,137 @@ __device__ void part_agg_v(const DevQuery* __restrict__ q, const PartScratch& ps
   }
 }
 
+// Specialised V pass C (VK = vk_code): one payload per record, at most one SUM / MIN / MAX; every descriptor field is
+// read once into registers, the record loop is straight-line. V_FMT_ID records with value ids in value order keep
+// MIN/MAX as 32-bit ids (the value is looked up once per key at the store), so the per-record dictionary gather is
+// only needed by SUM.
+template <int VK>
+__device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratch& ps, int p, unsigned char* lds) {
+  constexpr int SK = VK & 3;
+  constexpr bool MN = (VK & 4) != 0, MX = (VK & 8) != 0;
+  const int ks = q->kshift_v;
+  const int64_t KR = int64_t(1) << ks;
+  const int64_t kbase = (int64_t)p << ks;
+  const int64_t nk = min(KR, q->num_keys - kbase);
+  const int fmt = q->v_fmt;
+  const bool ids = fmt == V_FMT_ID && q->v_id_order != 0;  // MIN/MAX on value ids
+  const int W = q->rec_words_v;
+  const int as = q->vop_sum, amn = q->vop_min, amx = q->vop_max;
+  const uint32_t off_s = SK ? (uint32_t)q->aggs[as].lds_off : 0u;
+  const uint32_t off_mn = MN ? (uint32_t)q->aggs[amn].lds_off : 0u;
+  const uint32_t off_mx = MX ? (uint32_t)q->aggs[amx].lds_off : 0u;
+  const bool dbl_mn = MN && q->aggs[amn].src == SRC_DOUBLE, dbl_mx = MX && q->aggs[amx].src == SRC_DOUBLE;
+  lds_u32_t* cnt = lds_ptr(lds);
+  for (int64_t k = threadIdx.x; k < KR; k += kPartAggThreads) {
+    cnt[k] = 0u;
+    if (SK) {
+      ((lds_u64_t*)lds_ptr(lds + off_s))[k] = 0ull;
+      if (SK == 1 + SRC_LONG) ((lds_u64_t*)lds_ptr(lds + off_s))[KR + k] = 0ull;
+    }
+    if (MN) {
+      if (ids) lds_ptr(lds + off_mn)[k] = 0xffffffffu;
+      else ((lds_u64_t*)lds_ptr(lds + off_mn))[k] = (uint64_t)INT64_MAX;
+    }
+    if (MX) {
+      if (ids) lds_ptr(lds + off_mx)[k] = 0u;
+      else ((lds_u64_t*)lds_ptr(lds + off_mx))[k] = (uint64_t)INT64_MIN;
+    }
+  }
+  __syncthreads();
+  const uint64_t r0 = gp(ps.base)[p], r1 = gp(ps.base)[p + 1];
+  const uint32_t kmask = (uint32_t)(KR - 1);
+  const AS1 uint32_t* recs = gp((const uint32_t*)ps.recs_v);
+  const AS1 uint64_t* vdict = gp(q->vdict);
+  constexpr int kB = 16;  // records per thread in flight
+  const uint64_t span = (uint64_t)kB * kPartAggThreads;
+  for (uint64_t b0 = r0; b0 < r1; b0 += span) {
+    uint32_t w0[kB], w1[kB], w2[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const uint64_t ri = b0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
+      w0[j] = kSentinel;
+      w1[j] = w2[j] = 0u;
+      if (ri < r1) {
+        const AS1 uint32_t* rec = recs + ri * (uint64_t)W;
+        w0[j] = __builtin_nontemporal_load(rec);
+        if (fmt == V_FMT_32 || fmt == V_FMT_64) w1[j] = __builtin_nontemporal_load(rec + 1);
+        if (fmt == V_FMT_64) w2[j] = __builtin_nontemporal_load(rec + 2);
+      }
+    }
+    int64_t iv[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      iv[j] = 0;
+      if (w0[j] == kSentinel) continue;
+      if (fmt == V_FMT_ID) {
+        if (SK || !ids) iv[j] = (int64_t)vdict[w0[j] >> ks];
+      } else if (fmt == V_FMT_32) {
+        iv[j] = (int64_t)(int32_t)w1[j];
+      } else if (fmt == V_FMT_64) {
+        iv[j] = (int64_t)(((uint64_t)w2[j] << 32) | w1[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      if (w0[j] == kSentinel) continue;
+      const uint32_t lk = w0[j] & kmask;
+      __hip_atomic_fetch_add(cnt + lk, 1u, WG_RLX);
+      if (SK == 1 + SRC_INT) {
+        __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + lk, (uint64_t)iv[j], WG_RLX);
+      } else if (SK == 1 + SRC_LONG) {
+        __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + 2 * lk, (uint64_t)(uint32_t)iv[j], WG_RLX);
+        __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + 2 * lk + 1, (uint64_t)(iv[j] >> 32), WG_RLX);
+      } else if (SK == 1 + SRC_DOUBLE) {
+        atomicAdd((double*)(lds + off_s) + lk, __builtin_bit_cast(double, iv[j]));
+      }
+      if (ids) {
+        const uint32_t id = w0[j] >> ks;
+        if (MN) __hip_atomic_fetch_min(lds_ptr(lds + off_mn) + lk, id, WG_RLX);
+        if (MX) __hip_atomic_fetch_max(lds_ptr(lds + off_mx) + lk, id, WG_RLX);
+      } else {
+        if (MN) {
+          const int64_t e = dbl_mn ? f64_order_encode(__builtin_bit_cast(double, iv[j])) : iv[j];
+          __hip_atomic_fetch_min((__attribute__((address_space(3))) int64_t*)lds_ptr(lds + off_mn) + lk, e, WG_RLX);
+        }
+        if (MX) {
+          const int64_t e = dbl_mx ? f64_order_encode(__builtin_bit_cast(double, iv[j])) : iv[j];
+          __hip_atomic_fetch_max((__attribute__((address_space(3))) int64_t*)lds_ptr(lds + off_mx) + lk, e, WG_RLX);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // this workgroup owns keys [kbase, kbase + nk): plain stores of every accumulator
+  AS1 unsigned long long* gc = gp(q->count);
+  AS1 int64_t* gs = SK ? gp(q->aggs[as].acc_i64) : nullptr;
+  AS1 int64_t* gmn = MN ? gp(q->aggs[amn].acc_i64) : nullptr;
+  AS1 int64_t* gmx = MX ? gp(q->aggs[amx].acc_i64) : nullptr;
+  for (int64_t lk = threadIdx.x; lk < nk; lk += kPartAggThreads) {
+    const int64_t k = kbase + lk;
+    const uint32_t c = cnt[lk];
+    gc[k] = c;
+    if (SK == 1 + SRC_LONG) {
+      gs[2 * k] = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[2 * lk];
+      gs[2 * k + 1] = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[2 * lk + 1];
+    } else if (SK) {
+      gs[k] = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[lk];  // SUM(int) / SUM(double) bits
+    }
+    if (ids) {
+      if (MN) {
+        const uint64_t v = c ? vdict[lds_ptr(lds + off_mn)[lk]] : 0ull;
+        gmn[k] = c == 0 ? INT64_MAX : (dbl_mn ? f64_order_encode(__builtin_bit_cast(double, v)) : (int64_t)v);
+      }
+      if (MX) {
+        const uint64_t v = c ? vdict[lds_ptr(lds + off_mx)[lk]] : 0ull;
+        gmx[k] = c == 0 ? INT64_MIN : (dbl_mx ? f64_order_encode(__builtin_bit_cast(double, v)) : (int64_t)v);
+      }
+    } else {
+      if (MN) gmn[k] = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_mn))[lk];
+      if (MX) gmx[k] = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_mx))[lk];
+    }
+  }
+}
+
 __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps, int ph, unsigned char* lds) {
   const DevAgg& H = q->aggs[q->hll_agg];
   const int lg = H.log2m;
@@ -2527,10 +2681,27 @@ __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps
     for (int64_t lk = threadIdx.x; lk < nk; lk += kPartAggThreads) gp(q->count)[kbase + lk] = cnt[lk];
 }
 
+template <int VK>
 __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuery* __restrict__ q, PartScratch ps) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  if ((int)blockIdx.x < q->pv) part_agg_v(q, ps, (int)blockIdx.x, (unsigned char*)smem);
-  else part_agg_h(q, ps, (int)blockIdx.x - q->pv, (unsigned char*)smem);
+  if ((int)blockIdx.x < q->pv) {
+    if constexpr (VK == kVkGeneric) part_agg_v(q, ps, (int)blockIdx.x, (unsigned char*)smem);
+    else part_agg_v_fast<VK>(q, ps, (int)blockIdx.x, (unsigned char*)smem);
+  } else {
+    part_agg_h(q, ps, (int)blockIdx.x - q->pv, (unsigned char*)smem);
+  }
+}
+
+template <int VK>
+static const void* part_agg_fn() { return (const void*)part_agg_kernel<VK>; }
+static const void* part_agg_variant(int vk) {
+  switch (vk) {
+#define PA_VK(c) case c: return part_agg_fn<c>();
+    PA_VK(0) PA_VK(1) PA_VK(2) PA_VK(3) PA_VK(4) PA_VK(5) PA_VK(6) PA_VK(7)
+    PA_VK(8) PA_VK(9) PA_VK(10) PA_VK(11) PA_VK(12) PA_VK(13) PA_VK(14) PA_VK(15)
+#undef PA_VK
+    default: return part_agg_fn<kVkGeneric>();
+  }
 }
 
 hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G, int k, hipStream_t s) {
@@ -2541,13 +2712,13 @@ hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G,
   return hipGetLastError();
 }
 
-hipError_t set_part_agg_lds_limit(int lds_bytes) {
-  return hipFuncSetAttribute((const void*)part_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+hipError_t set_part_agg_lds_limit(int vk, int lds_bytes) {
+  return hipFuncSetAttribute(part_agg_variant(vk), hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
 }
 
-hipError_t launch_part_agg(const DevQuery* q, const PartScratch& ps, int P, int lds_bytes, hipStream_t s) {
-  part_agg_kernel<<<P, kPartAggThreads, (size_t)lds_bytes, s>>>(q, ps);
-  return hipGetLastError();
+hipError_t launch_part_agg(int vk, const DevQuery* q, const PartScratch& ps, int P, int lds_bytes, hipStream_t s) {
+  void* args[] = {(void*)&q, (void*)&ps};
+  return hipLaunchKernel(part_agg_variant(vk), dim3(P), dim3(kPartAggThreads), args, (size_t)lds_bytes, s);
 }
 
 static int grid_for(int64_t n, int block) {

@@ -52,8 +52,9 @@ hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t*
 // partitioned aggregation: per-(workgroup, partition) range offsets + partition bases (after the count pass, which ran
 // k workgroups per emit workgroup)
 hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G, int k, hipStream_t s);
-hipError_t set_part_agg_lds_limit(int lds_bytes);
-hipError_t launch_part_agg(const DevQuery* q, const PartScratch& ps, int P, int lds_bytes, hipStream_t s);
+// vk: the pass-C variant of the V stream (vk_code / kVkGeneric)
+hipError_t set_part_agg_lds_limit(int vk, int lds_bytes);
+hipError_t launch_part_agg(int vk, const DevQuery* q, const PartScratch& ps, int P, int lds_bytes, hipStream_t s);
 hipError_t set_scan_lds_limit(int strategy, int steps, int lm, int bytes);
 hipError_t scan_occupancy(int strategy, int steps, int lm, int lds_bytes, int* blocks_per_cu);
 hipError_t launch_scan(int strategy, int steps, int lm, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs,

@@ -64,6 +64,13 @@ WORKLOADS = {
                      "OPTION(numGroupsLimit=2000000)", 0),
         ("filtered_10pct", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t WHERE m < 6554 GROUP BY d1, d2 "
                            "LIMIT 2000000 OPTION(numGroupsLimit=2000000)", 0),
+        # decomposition of all_docs (which part of the work costs what)
+        ("count_only", "SELECT d1, d2, COUNT(*) FROM t GROUP BY d1, d2 LIMIT 2000000 "
+                       "OPTION(numGroupsLimit=2000000)", 0),
+        ("minmax_only", "SELECT d1, d2, MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000 "
+                        "OPTION(numGroupsLimit=2000000)", 0),
+        ("sum_only", "SELECT d1, d2, SUM(m) FROM t GROUP BY d1, d2 LIMIT 2000000 "
+                     "OPTION(numGroupsLimit=2000000)", 0),
         # the default numGroupsLimit (100000 < 1M keys): first-seen trimming per segment (a11)
         ("default_limit", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000", 0),
     ]),
