@@ -1142,6 +1142,19 @@ TilePlan plan_tiles(const pa_query* q, const std::vector<DevSeg>& segs, int stra
 // Table-wide dictionary of an aggregation's value column (V_FMT_ID records carry a value id): segment 0's device
 // dictionary when every segment holds the same dictionary, else the sorted union with per-segment dictId remaps.
 // Returns the value-id bits, or -1 when the column is not dictionary-encoded everywhere.
+// An INT/LONG dictionary whose values are base + step * id (an arithmetic progression, e.g. a dense range): pass C then
+// computes a value from its id instead of gathering it.
+bool affine_dictionary(const std::vector<uint64_t>& v, int32_t vtype, int64_t* base, int64_t* step) {
+  if (v.empty() || (vtype != PA_INT && vtype != PA_LONG)) return false;
+  const int64_t b = (int64_t)v[0];
+  const int64_t st = v.size() > 1 ? (int64_t)(v[1] - v[0]) : 0;
+  for (size_t i = 1; i < v.size(); ++i)
+    if ((uint64_t)v[i] - (uint64_t)v[i - 1] != (uint64_t)st) return false;
+  *base = b;
+  *step = st;
+  return true;
+}
+
 int value_dictionary(pa_query* q, const Prep& P, int a, const uint64_t** vdict) {
   const pa_query_spec& s = q->spec;
   const int32_t cid = s.aggs[a].column_id;
@@ -1154,8 +1167,15 @@ int value_dictionary(pa_query* q, const Prep& P, int a, const uint64_t** vdict) 
     same = same && (c == c0 || (c->dict_hash == c0->dict_hash && c->hvals == c0->hvals));
   }
   for (int si = 0; si < q->nseg; ++si) q->hsegs[si].vremap = nullptr;
+  q->hq.v_affine = 0;
   if (same) {
     *vdict = (const uint64_t*)c0->dict.p;
+    int64_t b = 0, st = 0;
+    if (affine_dictionary(c0->hvals, c0->vtype, &b, &st)) {
+      q->hq.v_affine = 1;
+      q->hq.v_base = b;
+      q->hq.v_step = st;
+    }
     return std::max(1, 32 - __builtin_clz((uint32_t)std::max(1, c0->cardinality - 1)));
   }
   const int32_t vt = c0->vtype;
@@ -1175,6 +1195,14 @@ int value_dictionary(pa_query* q, const Prep& P, int a, const uint64_t** vdict) 
   void* dp = nullptr;
   if (upload_owned(q, uni.data(), uni.size() * 8, &dp)) return -2;
   *vdict = (const uint64_t*)dp;
+  {
+    int64_t b = 0, st = 0;
+    if (affine_dictionary(uni, vt, &b, &st)) {
+      q->hq.v_affine = 1;
+      q->hq.v_base = b;
+      q->hq.v_step = st;
+    }
+  }
   for (int si = 0; si < q->nseg; ++si) {
     const Column* c = q->segs[si]->cols.at(cid);
     std::vector<int32_t> rm(c->hvals.size());

@@ -190,6 +190,9 @@ struct DevQuery {
   // and whether V_FMT_ID value ids are in value order (MIN/MAX then run on the 32-bit ids)
   int32_t vop_sum, vop_min, vop_max;
   int32_t v_id_order;
+  // V_FMT_ID value dictionary that is an arithmetic progression (INT/LONG): value = v_base + v_step * id, no gather
+  int32_t v_affine, pad_affine;
+  int64_t v_base, v_step;
 };
 // part_agg_kernel variant: -1 generic, else sum kind (0 none, 1 + AccSrc) | MIN << 2 | MAX << 3
 constexpr int kVkGeneric = -1;

@@ -2535,6 +2535,8 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   const uint32_t kmask = (uint32_t)(KR - 1);
   const AS1 uint32_t* recs = gp((const uint32_t*)ps.recs_v);
   const AS1 uint64_t* vdict = gp(q->vdict);
+  const bool aff = q->v_affine != 0;
+  const int64_t vbase = q->v_base, vstep = q->v_step;
   constexpr int kB = 16;  // records per thread in flight
   const uint64_t span = (uint64_t)kB * kPartAggThreads;
   for (uint64_t b0 = r0; b0 < r1; b0 += span) {
@@ -2557,7 +2559,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
       iv[j] = 0;
       if (w0[j] == kSentinel) continue;
       if (fmt == V_FMT_ID) {
-        if (SK || !ids) iv[j] = (int64_t)vdict[w0[j] >> ks];
+        if (SK || !ids) iv[j] = aff ? vbase + vstep * (int64_t)(w0[j] >> ks) : (int64_t)vdict[w0[j] >> ks];
       } else if (fmt == V_FMT_32) {
         iv[j] = (int64_t)(int32_t)w1[j];
       } else if (fmt == V_FMT_64) {

@@ -43,6 +43,17 @@ def highcard_segment(seed, docs):
         "m": sv_spec(rng, docs, 1 << 16, "LONG")})
 
 
+def highcard_rd_segment(seed, docs):
+    """configs[2] with a non-arithmetic value dictionary: m's 65536 values are sorted random distinct longs, so pass C
+    looks every SUM value up in the dictionary (the affine shortcut does not apply)."""
+    seg = highcard_segment(seed, docs)
+    rng = np.random.default_rng(10_000 + seed)
+    vals = np.unique(rng.integers(0, 1 << 40, size=70_000))[:1 << 16]
+    assert len(vals) == 1 << 16
+    seg.columns["m"].dictionary = np.sort(vals).astype(np.int64)
+    return seg
+
+
 def star_segment(seed, docs, avg_mv=3):
     from pinot_amd.segment import Column, mv_column_from_flat, segment_from_dict_ids
     rng = np.random.default_rng(seed)
@@ -74,6 +85,10 @@ WORKLOADS = {
         # the default numGroupsLimit (100000 < 1M keys): first-seen trimming per segment (a11)
         ("default_limit", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000", 0),
     ]),
+    "highcard_rd": (highcard_rd_segment, [
+        ("all_docs", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000 "
+                     "OPTION(numGroupsLimit=2000000)", 0),
+    ]),
     "star": (star_segment, [
         ("all_docs", "SELECT d1, d2, d3, d4, SUM(r), DISTINCTCOUNTHLLMV(tags) FROM t GROUP BY d1, d2, d3, d4 "
                      "LIMIT 1000000 OPTION(numGroupsLimit=1000000)", 0),
@@ -104,6 +119,8 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
         for c in seg.columns.values():  # HBM holds the data now; keep only the dictionaries
             c.fwd_bytes = None
             c.raw_values = None
+        if (i + 1) % 10 == 0:
+            log("  %d/%d segments resident, %.1f s" % (i + 1, nseg, time.perf_counter() - t0))
     log("%s: %d segments x %d docs resident (%.1f GB), %.1f s" % (
         workload, nseg, docs, sum(g.device_bytes for g in gsegs) / 1e9, time.perf_counter() - t0))
     stream = torch.cuda.current_stream()

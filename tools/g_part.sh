@@ -7,6 +7,7 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -k "partition or star o
 tail -2 $out/tests.log
 timeout -k 10 300 python -u tools/bench_configs.py --workload highcard --no-stepmajor > $out/configs.json 2> $out/configs.err || { echo hc_failed; tail -20 $out/configs.err; exit 2; }
 timeout -k 10 300 python -u tools/bench_configs.py --workload star --no-stepmajor >> $out/configs.json 2>> $out/configs.err || { echo star_failed; tail -20 $out/configs.err; exit 3; }
+timeout -k 10 300 python -u tools/bench_configs.py --workload highcard_rd --no-stepmajor >> $out/configs.json 2>> $out/configs.err || { echo hcrd_failed; tail -20 $out/configs.err; exit 4; }
 python3 -c "
 import json
 for l in open('$out/configs.json'):
