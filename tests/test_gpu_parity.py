@@ -317,6 +317,9 @@ def test_partitioned_aggregation(flags):
         ("SELECT k2, k1, SUM(big), MIN(big), MAX(f), SUM(f), MIN(g) FROM t WHERE m > {m} GROUP BY k2, k1 "
          "LIMIT 1000000 OPTION(numGroupsLimit=2000000)", False),
         ("SELECT k1, k2, COUNT(*) FROM t GROUP BY k1, k2 LIMIT 1000000 OPTION(numGroupsLimit=2000000)", True),
+        # one 64-bit payload (value ids, negative values): pass C's one-int64 SUM when the partition bounds it
+        ("SELECT k1, k2, SUM(big), MIN(big), MAX(big) FROM t GROUP BY k1, k2 LIMIT 1000000 "
+         "OPTION(numGroupsLimit=2000000)", True),
     ]
     mv = int(segs[0].column("m").dictionary[len(segs[0].column("m").dictionary) // 4])
     gsegs = [GpuSegment(sg) for sg in segs]
@@ -489,6 +492,16 @@ def test_num_groups_limit_walk_every_strategy(flags):
     sql = ("SELECT k1, k2, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t WHERE f <> 3 GROUP BY k1, k2 LIMIT 100000000 "
            "OPTION(numGroupsLimit=15000)")
     got, exp = _limit_run(sql, segs, WALK, flags=flags)
+    assert got.num_groups_limit_reached
+
+
+def test_num_groups_limit_walk_hbm_bitmap():
+    """Key spaces beyond the walk's LDS bitmap (1.28M keys: 1500 x 1000 here) keep the admitted-key bitmap in HBM
+    (limit_walk_kernel<true>); same first-seen groups as the oracle."""
+    cols = {"k1": ("INT", 1500), "k2": ("LONG", 1000), "m": ("LONG", 5000)}
+    segs = [make_segment(740 + i, n, cols) for i, n in enumerate((30000, 12000))]
+    got, exp = _limit_run("SELECT k1, k2, COUNT(*), SUM(m) FROM t GROUP BY k1, k2 LIMIT 100000000 "
+                          "OPTION(numGroupsLimit=9000)", segs, WALK)
     assert got.num_groups_limit_reached
 
 
