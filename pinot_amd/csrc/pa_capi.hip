@@ -1144,6 +1144,17 @@ TilePlan plan_tiles(const pa_query* q, const std::vector<DevSeg>& segs, int stra
 // Returns the value-id bits, or -1 when the column is not dictionary-encoded everywhere.
 // An INT/LONG dictionary whose values are base + step * id (an arithmetic progression, e.g. a dense range): pass C then
 // computes a value from its id instead of gathering it.
+uint64_t max_abs_value(const std::vector<uint64_t>& v, int32_t vtype) {
+  if (vtype != PA_INT && vtype != PA_LONG) return 0;
+  uint64_t m = 0;
+  for (uint64_t x : v) {
+    const int64_t y = (int64_t)x;
+    if (y == INT64_MIN) return 0;
+    m = std::max<uint64_t>(m, (uint64_t)(y < 0 ? -y : y));
+  }
+  return m;
+}
+
 bool affine_dictionary(const std::vector<uint64_t>& v, int32_t vtype, int64_t* base, int64_t* step) {
   if (v.empty() || (vtype != PA_INT && vtype != PA_LONG)) return false;
   const int64_t b = (int64_t)v[0];
@@ -1168,8 +1179,10 @@ int value_dictionary(pa_query* q, const Prep& P, int a, const uint64_t** vdict) 
   }
   for (int si = 0; si < q->nseg; ++si) q->hsegs[si].vremap = nullptr;
   q->hq.v_affine = 0;
+  q->hq.v_maxabs = 0;
   if (same) {
     *vdict = (const uint64_t*)c0->dict.p;
+    q->hq.v_maxabs = max_abs_value(c0->hvals, c0->vtype);
     int64_t b = 0, st = 0;
     if (affine_dictionary(c0->hvals, c0->vtype, &b, &st)) {
       q->hq.v_affine = 1;
@@ -1195,6 +1208,7 @@ int value_dictionary(pa_query* q, const Prep& P, int a, const uint64_t** vdict) 
   void* dp = nullptr;
   if (upload_owned(q, uni.data(), uni.size() * 8, &dp)) return -2;
   *vdict = (const uint64_t*)dp;
+  q->hq.v_maxabs = max_abs_value(uni, vt);
   {
     int64_t b = 0, st = 0;
     if (affine_dictionary(uni, vt, &b, &st)) {
@@ -1261,6 +1275,50 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
     ++nv;
   }
   const bool vstream = nv > 0 || hll < 0;
+  // V record format: one payload slot per distinct (column, value source); SUM/MIN/MAX of one column share it
+  std::vector<int> pay(s.num_aggs, 0);
+  int words = 1, slots = 0, va = -1;
+  for (int a = 0; a < s.num_aggs; ++a) {
+    const int t = s.aggs[a].type;
+    if (t == PA_AGG_COUNT || t == PA_AGG_DISTINCTCOUNTHLL) continue;
+    int shared = -1;
+    for (int b = 0; b < a; ++b)
+      if (s.aggs[b].type != PA_AGG_COUNT && s.aggs[b].type != PA_AGG_DISTINCTCOUNTHLL && P.agg_slot[b] == P.agg_slot[a] &&
+          P.agg_src[b] == P.agg_src[a])
+        shared = pay[b];
+    if (shared >= 0) {
+      pay[a] = shared;
+    } else {
+      pay[a] = words;
+      words += P.agg_src[a] == SRC_INT ? 1 : 2;
+      ++slots;
+      if (va < 0) va = a;
+    }
+  }
+  const uint64_t* vdict = nullptr;
+  const int vbits = (slots == 1 && P.val_fast[va]) ? value_dictionary(q, P, va, &vdict) : -1;
+  if (vbits == -2) { PLAN_LOG("partitioned: no (exit 6)"); return false; }  // (allocation failure: reported by pa_last_error)
+  // specialised V pass C: one payload, at most one SUM / MIN / MAX
+  h.vop_sum = h.vop_min = h.vop_max = -1;
+  bool vk_fast = vstream && slots <= 1;
+  for (int a = 0; a < s.num_aggs && vk_fast; ++a) {
+    const int t = s.aggs[a].type;
+    int32_t* slot = t == PA_AGG_SUM ? &h.vop_sum : (t == PA_AGG_MIN ? &h.vop_min : (t == PA_AGG_MAX ? &h.vop_max : nullptr));
+    if (t == PA_AGG_COUNT || t == PA_AGG_DISTINCTCOUNTHLL) continue;
+    if (!slot || *slot >= 0) vk_fast = false;
+    else *slot = a;
+  }
+  // value ids in value order: the table-wide union is sorted; a shared segment dictionary is checked
+  bool sorted_ids = false;
+  if (vbits > 0) {
+    sorted_ids = true;
+    const Column* c0 = q->segs[0]->cols.at(s.aggs[va].column_id);
+    if (q->hsegs[0].vremap == nullptr)
+      for (size_t i = 1; i < c0->hvals.size() && sorted_ids; ++i)
+        sorted_ids = value_order_key(c0->hvals[i - 1], c0->vtype) < value_order_key(c0->hvals[i], c0->vtype);
+  }
+  // (pass C's MIN/MAX slots stay 8 bytes even when they hold 4-byte value ids: sizing them at 4 bytes doubles the keys
+  // per partition and halves pass C's workgroups, measured slower on configs[2] with 64-bit values, r02_v6)
   const size_t part_lds = kPartLdsChoices[(s.flags >> PA_QF_PART_SHIFT) & 3];
   auto max_keys = [&](size_t per_key) {  // largest power-of-two key range whose accumulators fit pass C's LDS
     int64_t kr = 1;
@@ -1296,31 +1354,8 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
   }
   if (Pv + Ph < 2 || Pv + Ph > kMaxParts) { PLAN_LOG("partitioned: no (exit 5)"); return false; }
   const int ksv = vstream ? __builtin_ctzll((uint64_t)kr_v) : 0;
-  // V record format: one payload slot per distinct (column, value source); SUM/MIN/MAX of one column share it
-  std::vector<int> pay(s.num_aggs, 0);
-  int words = 1, slots = 0, va = -1;
-  for (int a = 0; a < s.num_aggs; ++a) {
-    const int t = s.aggs[a].type;
-    if (t == PA_AGG_COUNT || t == PA_AGG_DISTINCTCOUNTHLL) continue;
-    int shared = -1;
-    for (int b = 0; b < a; ++b)
-      if (s.aggs[b].type != PA_AGG_COUNT && s.aggs[b].type != PA_AGG_DISTINCTCOUNTHLL && P.agg_slot[b] == P.agg_slot[a] &&
-          P.agg_src[b] == P.agg_src[a])
-        shared = pay[b];
-    if (shared >= 0) {
-      pay[a] = shared;
-    } else {
-      pay[a] = words;
-      words += P.agg_src[a] == SRC_INT ? 1 : 2;
-      ++slots;
-      if (va < 0) va = a;
-    }
-  }
   int fmt = V_FMT_KEY, W = 1;
-  const uint64_t* vdict = nullptr;
   if (slots == 1) {
-    const int vbits = P.val_fast[va] ? value_dictionary(q, P, va, &vdict) : -1;
-    if (vbits == -2) { PLAN_LOG("partitioned: no (exit 6)"); return false; }  // (allocation failure: reported by pa_last_error)
     if (vbits > 0 && vbits + ksv <= 31) {
       fmt = V_FMT_ID;
       W = 1;
@@ -1356,25 +1391,34 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
   // Each launch: 4-wave or 16-wave workgroups (the bins are per workgroup: shared by 16 waves they leave LDS for more
   // resident waves when the tile images are small), whichever keeps more waves resident; bins halve (down to 64-byte
   // bursts) while they do not fit or cost resident waves (at least 8 waves per CU hide the per-record gathers).
+  // resident waves per CU the emit plan wants before it keeps larger bins (PA_EMIT_MIN_WAVES: measurement override)
+  static const int emit_min_waves = std::getenv("PA_EMIT_MIN_WAVES") ? std::atoi(std::getenv("PA_EMIT_MIN_WAVES"))
+                                                                      : 2 * kWavesPerWG;
   auto plan_emit = [&](int vf, int hh, bool with_v, bool with_h, int& bv, int& bh, int& strat) {
     auto lds_of = [&](int v, int h2) { return emit_state(with_v ? v : 0, with_h ? h2 : 0); };
     TilePlan best;
     int best_bv = bv, best_bh = bh;
+    static const int force_big = std::getenv("PA_EMIT_BIG") ? std::atoi(std::getenv("PA_EMIT_BIG")) : -1;  // (measurement)
     for (int big : {0, 1}) {
+      if (force_big >= 0 && big != force_big) continue;
       const int es = pemit_strat(vf, hh, big);
       const int wpw = scan_waves(es);
       int v = bv, h2 = bh;
       TilePlan e = plan_tiles(q, q->hsegs, es, false, lds_of(v, h2), true);
-      while ((e.score < 0 || e.wg_per_cu * wpw < 2 * kWavesPerWG) &&
-             ((with_h && h2 > 16) || (with_v && v * W > 16 && v % 8 == 0))) {
-        const int v2 = (with_v && v * W > 16 && v % 8 == 0) ? v / 2 : v;
-        const int hh2 = (with_h && h2 > 16) ? h2 / 2 : h2;
-        TilePlan t = plan_tiles(q, q->hsegs, es, false, lds_of(v2, hh2), true);
-        if (e.score >= 0 && t.score >= 0 && t.wg_per_cu <= e.wg_per_cu)
-          break;  // no more resident waves from smaller bins: keep the larger bursts
-        v = v2;
-        h2 = hh2;
-        e = t;
+      // while below emit_min_waves: try every smaller bin size (down to 64-byte bursts) and keep the one with the most
+      // resident waves (ties: the larger bursts). A halving step alone may not add a workgroup (the tile plan spends
+      // the freed LDS on a deeper ring) while the next one does.
+      int cv = v, ch = h2;
+      while ((e.score < 0 || e.wg_per_cu * wpw < emit_min_waves) &&
+             ((with_h && ch > 16) || (with_v && cv * W > 16 && cv % 8 == 0))) {
+        cv = (with_v && cv * W > 16 && cv % 8 == 0) ? cv / 2 : cv;
+        ch = (with_h && ch > 16) ? ch / 2 : ch;
+        TilePlan t = plan_tiles(q, q->hsegs, es, false, lds_of(cv, ch), true);
+        if (t.score >= 0 && (e.score < 0 || t.wg_per_cu > e.wg_per_cu)) {
+          v = cv;
+          h2 = ch;
+          e = t;
+        }
       }
       if (e.score > best.score) {
         best = e;
@@ -1414,30 +1458,11 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
   h.h_first = (hll >= 0 && !vstream) ? 1 : 0;
   h.hll_agg = hll;
   h.emit_val_agg = slots == 1 ? va : -1;
-  // specialised V pass C: one payload, at most one SUM / MIN / MAX
-  h.vop_sum = h.vop_min = h.vop_max = -1;
-  q->part_vk = kVkGeneric;
-  if (vstream && fmt != V_FMT_GEN) {
-    bool ok = true;
-    for (int a = 0; a < s.num_aggs && ok; ++a) {
-      const int t = s.aggs[a].type;
-      int32_t* slot = t == PA_AGG_SUM ? &h.vop_sum : (t == PA_AGG_MIN ? &h.vop_min : (t == PA_AGG_MAX ? &h.vop_max : nullptr));
-      if (t == PA_AGG_COUNT || t == PA_AGG_DISTINCTCOUNTHLL) continue;
-      if (!slot || *slot >= 0) ok = false;
-      else *slot = a;
-    }
-    if (ok) q->part_vk = vk_code(h.vop_sum >= 0 ? 1 + P.agg_src[h.vop_sum] : 0, h.vop_min >= 0, h.vop_max >= 0);
-  }
-  // value ids in value order: the table-wide union is sorted; a shared segment dictionary is checked
-  h.v_id_order = 0;
-  if (fmt == V_FMT_ID) {
-    const Column* c0 = q->segs[0]->cols.at(s.aggs[va].column_id);
-    bool sorted = true;
-    if (q->hsegs[0].vremap == nullptr)
-      for (size_t i = 1; i < c0->hvals.size() && sorted; ++i)
-        sorted = value_order_key(c0->hvals[i - 1], c0->vtype) < value_order_key(c0->hvals[i], c0->vtype);
-    h.v_id_order = sorted ? 1 : 0;
-  }
+  q->part_vk = (vk_fast && fmt != V_FMT_GEN)
+                   ? vk_code(h.vop_sum >= 0 ? 1 + P.agg_src[h.vop_sum] : 0, h.vop_min >= 0, h.vop_max >= 0)
+                   : kVkGeneric;
+  h.v_id_order = (fmt == V_FMT_ID && sorted_ids) ? 1 : 0;
+
   h.vdict = vdict;
   size_t o = 0;
   h.lds_cnt = (uint32_t)o; o += (size_t)Ptot * 4;

@@ -193,6 +193,9 @@ struct DevQuery {
   // V_FMT_ID value dictionary that is an arithmetic progression (INT/LONG): value = v_base + v_step * id, no gather
   int32_t v_affine, pad_affine;
   int64_t v_base, v_step;
+  // V_FMT_ID INT/LONG value dictionary: the largest |value| (0 = unknown); a 64-bit SUM whose partition's record count
+  // times it stays below 2^62 accumulates in one int64 instead of the 32/32-bit split pair
+  uint64_t v_maxabs;
 };
 // part_agg_kernel variant: -1 generic, else sum kind (0 none, 1 + AccSrc) | MIN << 2 | MAX << 3
 constexpr int kVkGeneric = -1;

@@ -2532,6 +2532,9 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   }
   __syncthreads();
   const uint64_t r0 = gp(ps.base)[p], r1 = gp(ps.base)[p + 1];
+  // 64-bit SUM in one int64 per key when this partition's records cannot overflow it
+  const bool narrow = SK == 1 + SRC_LONG && fmt == V_FMT_ID && q->v_maxabs > 0 &&
+                      (r1 - r0) < ((uint64_t)1 << 62) / q->v_maxabs;
   const uint32_t kmask = (uint32_t)(KR - 1);
   const AS1 uint32_t* recs = gp((const uint32_t*)ps.recs_v);
   const AS1 uint64_t* vdict = gp(q->vdict);
@@ -2574,8 +2577,12 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
       if (SK == 1 + SRC_INT) {
         __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + lk, (uint64_t)iv[j], WG_RLX);
       } else if (SK == 1 + SRC_LONG) {
-        __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + 2 * lk, (uint64_t)(uint32_t)iv[j], WG_RLX);
-        __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + 2 * lk + 1, (uint64_t)(iv[j] >> 32), WG_RLX);
+        if (narrow) {
+          __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + 2 * lk, (uint64_t)iv[j], WG_RLX);
+        } else {
+          __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + 2 * lk, (uint64_t)(uint32_t)iv[j], WG_RLX);
+          __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + 2 * lk + 1, (uint64_t)(iv[j] >> 32), WG_RLX);
+        }
       } else if (SK == 1 + SRC_DOUBLE) {
         atomicAdd((double*)(lds + off_s) + lk, __builtin_bit_cast(double, iv[j]));
       }
@@ -2606,8 +2613,11 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
     const uint32_t c = cnt[lk];
     gc[k] = c;
     if (SK == 1 + SRC_LONG) {
-      gs[2 * k] = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[2 * lk];
-      gs[2 * k + 1] = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[2 * lk + 1];
+      const int64_t lo = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[2 * lk];
+      const int64_t hi = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[2 * lk + 1];
+      // (narrow: lo holds the whole sum S; the pair is (S mod 2^32, S >> 32), the same total)
+      gs[2 * k] = narrow ? (int64_t)(uint32_t)lo : lo;
+      gs[2 * k + 1] = narrow ? (lo >> 32) : hi;
     } else if (SK) {
       gs[k] = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[lk];  // SUM(int) / SUM(double) bits
     }
