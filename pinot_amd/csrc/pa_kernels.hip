@@ -828,6 +828,78 @@ __device__ __forceinline__ void bin_put_wave(const BinState& B, bool active, uin
 }
 
 
+// Batched decodes of part_tile: every load of a batch is issued before any of their results is used. (A load whose
+// result is consumed inside a per-lane branch gets its wait inside that branch: the batch's round trips serialise.)
+// Packed values idx[i] of the stream `words` (nb bits each) for the lanes with on[i]; 0 elsewhere.
+template <int N>
+__device__ __forceinline__ void decode_global_batch(const uint32_t* words, const int64_t (&idx)[N], const bool (&on)[N],
+                                                    int nb, uint32_t (&out)[N]) {
+  uint32_t lo[N], hi[N], sh[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint64_t e1 = (uint64_t)idx[i] * (uint64_t)nb + (uint64_t)(nb - 1);
+    const int64_t we = (int64_t)(e1 >> 5);
+    sh[i] = (~(uint32_t)e1) & 31u;
+    lo[i] = hi[i] = 0u;
+    if (on[i]) {
+      lo[i] = gp(words)[we];
+      hi[i] = gp(words)[we - 1];
+    }
+  }
+  const uint32_t mask = nbits_mask(nb);
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = on[i] ? (__builtin_amdgcn_alignbit(hi[i], lo[i], sh[i]) & mask) : 0u;
+}
+
+// dictIds of the docs of steps h .. h+N-1 (match bits m) of a column: from the staged tile image (region `loff`; every
+// doc of the batch lies in the image, so all are read and the matching ones kept) or, lazily, from HBM.
+template <int N, int LM>
+__device__ __forceinline__ void decode_batch(int loff, int nb, const uint32_t* words, const uint32_t* img,
+                                             int64_t doc_base, int h, uint32_t m, int lane, uint32_t (&id)[N]) {
+  auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
+  if (loff >= 0) {
+    const uint32_t* region = img + loff;
+    const uint32_t mask = nbits_mask(nb);
+    uint32_t lo[N], hi[N], sh[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const uint32_t e1 = (uint32_t)local(h + i) * (uint32_t)nb + (uint32_t)(nb - 1);
+      const int we = (int)(e1 >> 5);
+      lo[i] = region[we];
+      hi[i] = region[we - 1];
+      sh[i] = (~e1) & 31u;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      id[i] = ((m >> (h + i)) & 1u) ? (__builtin_amdgcn_alignbit(hi[i], lo[i], sh[i]) & mask) : 0u;
+  } else {
+    int64_t idx[N];
+    bool on[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      idx[i] = doc_base + local(h + i);
+      on[i] = (m >> (h + i)) & 1u;
+    }
+    decode_global_batch<N>(words, idx, on, nb, id);
+  }
+}
+
+// MV value range [v0, v1) of the matching docs of steps h .. h+N-1 (0, 0 elsewhere, or without an MV column).
+template <int N, int LM>
+__device__ __forceinline__ void mv_ranges(bool hmv, const int32_t* hoff, int64_t doc_base, int h, uint32_t m, int lane,
+                                          int32_t (&v0)[N], int32_t (&v1)[N]) {
+  auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    v0[i] = v1[i] = 0;
+    if (hmv && ((m >> (h + i)) & 1u)) {
+      const int64_t doc = doc_base + local(h + i);
+      v0[i] = gp(hoff)[doc];
+      v1[i] = gp(hoff)[doc + 1];
+    }
+  }
+}
+
 // The matching docs of one tile (match words m) in the count pass (STRAT_PCOUNT: per (workgroup, partition) record
 // counts in LDS) or the emit pass (STRAT_PEMIT: the records into the partition bins). Per batch of 8 steps: every
 // group-by dictId decode, then every remap gather (they overlap), then the table-wide keys; then per stream.
@@ -861,14 +933,7 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
       const int32_t* rm = cs->remap[j];
       const uint32_t st = (uint32_t)q->gb_stride[j];
       uint32_t id[kEB];
-#pragma unroll
-      for (int i = 0; i < kEB; ++i) {
-        id[i] = 0u;
-        if ((m >> (h + i)) & 1u) {
-          const int dl = local(h + i);
-          id[i] = gl >= 0 ? decode_lds(img + gl, dl, gn) : decode_global(gw, doc_base + dl, gn);
-        }
-      }
+      decode_batch<kEB, LM>(gl, gn, gw, img, doc_base, h, m, lane, id);
       if (rm != nullptr) {
 #pragma unroll
         for (int i = 0; i < kEB; ++i)
@@ -880,14 +945,11 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
     if constexpr (STRAT == STRAT_PCOUNT) {
       lds_u32_t* hist = lds_ptr(lds);
       uint32_t n[kEB];
+      {
+        int32_t v0[kEB], v1[kEB];
+        mv_ranges<kEB, LM>(hmv, hoff, doc_base, h, m, lane, v0, v1);
 #pragma unroll
-      for (int i = 0; i < kEB; ++i) {
-        n[i] = 1u;
-        if (hmv && ((m >> (h + i)) & 1u)) {
-          const int64_t doc = doc_base + local(h + i);
-          const int32_t nv = gp(hoff)[doc + 1] - gp(hoff)[doc];
-          n[i] = nv > 0 ? (uint32_t)nv : 1u;
-        }
+        for (int i = 0; i < kEB; ++i) n[i] = v1[i] - v0[i] > 0 ? (uint32_t)(v1[i] - v0[i]) : 1u;
       }
 #pragma unroll
       for (int i = 0; i < kEB; ++i) {
@@ -921,14 +983,7 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
           const void* vraw = cs->cols[vslot].raw;
           if (vkind == COL_SV_DICT) {
             uint32_t vid[kEB];
-#pragma unroll
-            for (int i = 0; i < kEB; ++i) {
-              vid[i] = 0u;
-              if ((m >> (h + i)) & 1u) {
-                const int dl = local(h + i);
-                vid[i] = vl >= 0 ? decode_lds(img + vl, dl, vn) : decode_global(vw, doc_base + dl, vn);
-              }
-            }
+            decode_batch<kEB, LM>(vl, vn, vw, img, doc_base, h, m, lane, vid);
             if constexpr (VF == V_FMT_ID) {
               if (vrm != nullptr) {
 #pragma unroll
@@ -1036,15 +1091,9 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
         const uint32_t first_bit = q->h_first ? 1u : 0u;
         // every step's value ranges first (one wait for the batch)
         int32_t v0s[kEB], nvs[kEB];
+        mv_ranges<kEB, LM>(hmv, hoff, doc_base, h, m, lane, v0s, nvs);
 #pragma unroll
-        for (int i = 0; i < kEB; ++i) {
-          v0s[i] = nvs[i] = 0;
-          if (hmv && ((m >> (h + i)) & 1u)) {
-            const int64_t doc = doc_base + local(h + i);
-            v0s[i] = gp(hoff)[doc];
-            nvs[i] = gp(hoff)[doc + 1] - v0s[i];
-          }
-        }
+        for (int i = 0; i < kEB; ++i) nvs[i] -= v0s[i];
         // Doc-reserved batch path (every matching doc of the batch has at most kDocVals records), kHS steps at a time
         // with every phase a run of independent operations (one wait per phase): reserve each doc's consecutive bin
         // slots (one cnt atomic per doc; records past the bin's end are reserved at the back of the range), decode
@@ -1086,13 +1135,21 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
             }
             uint32_t val[kHS][kDocVals];
 #pragma unroll
-            for (int j = 0; j < kHS; ++j)
+            for (int j = 0; j < kHS; ++j) {
+              int64_t vi[kDocVals];
+              bool von[kDocVals];
 #pragma unroll
               for (int e = 0; e < kDocVals; ++e) {
-                val[j][e] = 0u;
-                if ((uint32_t)e < maxn && e < nvs[h2 + j] && mn[j])
-                  val[j][e] = (dbg & 4) ? (uint32_t)e : decode_global(hwords, (int64_t)v0s[h2 + j] + e, hnb);
+                vi[e] = (int64_t)v0s[h2 + j] + e;
+                von[e] = (uint32_t)e < maxn && e < nvs[h2 + j] && mn[j];
               }
+              if (dbg & 4) {
+#pragma unroll
+                for (int e = 0; e < kDocVals; ++e) val[j][e] = von[e] ? (uint32_t)e : 0u;
+              } else {
+                decode_global_batch<kDocVals>(hwords, vi, von, hnb, val[j]);
+              }
+            }
 #pragma unroll
             for (int j = 0; j < kHS; ++j)
 #pragma unroll
@@ -1158,11 +1215,18 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
             uint32_t hvv[kDocVals];
             if (hmv) {
               uint32_t idv[kDocVals];
+              int64_t vi[kDocVals];
+              bool von[kDocVals];
 #pragma unroll
               for (int e = 0; e < kDocVals; ++e) {
-                idv[e] = 0u;
-                if ((uint32_t)e < maxn && mine && e < nv)
-                  idv[e] = (dbg & 4) ? (uint32_t)e : decode_global(hwords, (int64_t)v0 + e, hnb);
+                vi[e] = (int64_t)v0 + e;
+                von[e] = (uint32_t)e < maxn && mine && e < nv;
+              }
+              if (dbg & 4) {
+#pragma unroll
+                for (int e = 0; e < kDocVals; ++e) idv[e] = von[e] ? (uint32_t)e : 0u;
+              } else {
+                decode_global_batch<kDocVals>(hwords, vi, von, hnb, idv);
               }
 #pragma unroll
               for (int e = 0; e < kDocVals; ++e) {
@@ -1200,8 +1264,10 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
           const uint32_t kk = key[i];
           constexpr int kHB = 4;  // record chunks of 64 per round: their loads overlap
           for (uint32_t b = 0; b < total; b += kHB * kWave) {
-            uint32_t w0[kHB], id[kHB], pk[kHB];
+            uint32_t w0[kHB], id[kHB], pk[kHB], alt[kHB];
             int32_t ok[kHB];
+            int64_t vi[kHB];
+            bool von[kHB];
 #pragma unroll
             for (int k = 0; k < kHB; ++k) {
               const uint32_t g = b + (uint32_t)(k * kWave + lane);
@@ -1220,8 +1286,14 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
               ok[k] = g < total ? (hmv ? ((int32_t)e < o_nv ? 2 : 1) : 1) : 0;  // 2: an MV value to look up
               pk[k] = o_key >> ksh;
               w0[k] = ((o_key & kmask) << fsh) | (e == 0 ? first_bit : 0u);
-              id[k] = ok[k] == 2 ? ((dbg & 4) ? e : decode_global(hwords, (int64_t)o_v0 + e, hnb)) : (hmv ? 0u : o_hv);
+              vi[k] = (int64_t)o_v0 + e;
+              von[k] = ok[k] == 2 && !(dbg & 4);
+              alt[k] = ok[k] == 2 ? e : (hmv ? 0u : o_hv);  // (e: measurement only, PA_DEBUG_EMIT bit 2)
             }
+            decode_global_batch<kHB>(hwords, vi, von, hnb, id);
+#pragma unroll
+            for (int k = 0; k < kHB; ++k)
+              if (!von[k]) id[k] = alt[k];
             uint32_t hv[kHB];
 #pragma unroll
             for (int k = 0; k < kHB; ++k) hv[k] = ok[k] == 2 && !(dbg & 2) ? gp(hlut)[id[k]] : id[k];  // (register << 8) | rank
