@@ -1104,7 +1104,7 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
 #pragma unroll
         for (int i = 0; i < kEB; ++i) big |= ((m >> (h + i)) & 1u) && nvs[i] > kDocVals;
         if (hmv && __ballot(big) == 0) {
-          constexpr int kHS = 4;
+          constexpr int kHS = 2;
 #pragma unroll
           for (int h2 = 0; h2 < kEB; h2 += kHS) {
             bool mn[kHS];
