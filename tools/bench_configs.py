@@ -99,6 +99,9 @@ WORKLOADS = {
                      "LIMIT 1000000 OPTION(numGroupsLimit=1000000)", 0),
         ("hll_only", "SELECT d1, d2, d3, d4, DISTINCTCOUNTHLLMV(tags) FROM t GROUP BY d1, d2, d3, d4 "
                      "LIMIT 1000000 OPTION(numGroupsLimit=1000000)", 0),
+        # the default numGroupsLimit (100000 < 262144 keys): first-seen trimming per segment (walk form: SV group-by)
+        ("default_limit", "SELECT d1, d2, d3, d4, SUM(r), DISTINCTCOUNTHLLMV(tags) FROM t GROUP BY d1, d2, d3, d4 "
+                          "LIMIT 1000000", 0),
     ]),
 }
 
