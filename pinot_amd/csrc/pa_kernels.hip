@@ -884,18 +884,41 @@ __device__ __forceinline__ void decode_batch(int loff, int nb, const uint32_t* w
   }
 }
 
-// MV value range [v0, v1) of the matching docs of steps h .. h+N-1 (0, 0 elsewhere, or without an MV column).
+// MV value range [v0, v1) of the matching docs of steps h .. h+N-1 (0, 0 elsewhere, or without an MV column); nd =
+// the segment's docs (hoff holds nd + 1 offsets).
 template <int N, int LM>
-__device__ __forceinline__ void mv_ranges(bool hmv, const int32_t* hoff, int64_t doc_base, int h, uint32_t m, int lane,
-                                          int32_t (&v0)[N], int32_t (&v1)[N]) {
+__device__ __forceinline__ void mv_ranges(bool hmv, const int32_t* hoff, int64_t nd, int64_t doc_base, int h, uint32_t m,
+                                          int lane, int32_t (&v0)[N], int32_t (&v1)[N]) {
   auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
+  if constexpr (!LM) {
+    // step i holds docs doc_base + 64 i + lane: a doc's end offset is the next lane's start offset, so one coalesced
+    // load per step (every doc of the step, clamped to nd) plus lane 63's end offset
+    int32_t a[N], b[N];
 #pragma unroll
-  for (int i = 0; i < N; ++i) {
-    v0[i] = v1[i] = 0;
-    if (hmv && ((m >> (h + i)) & 1u)) {
-      const int64_t doc = doc_base + local(h + i);
-      v0[i] = gp(hoff)[doc];
-      v1[i] = gp(hoff)[doc + 1];
+    for (int i = 0; i < N; ++i) {
+      a[i] = b[i] = 0;
+      if (hmv) {
+        const int64_t doc = doc_base + local(h + i);
+        a[i] = gp(hoff)[doc < nd ? doc : nd];
+        if (lane == kWave - 1) b[i] = gp(hoff)[doc + 1 < nd ? doc + 1 : nd];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int32_t nx = __shfl_down(a[i], 1, kWave);
+      const bool on = hmv && ((m >> (h + i)) & 1u);
+      v0[i] = on ? a[i] : 0;
+      v1[i] = on ? (lane == kWave - 1 ? b[i] : nx) : 0;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      v0[i] = v1[i] = 0;
+      if (hmv && ((m >> (h + i)) & 1u)) {
+        const int64_t doc = doc_base + local(h + i);
+        v0[i] = gp(hoff)[doc];
+        v1[i] = gp(hoff)[doc + 1];
+      }
     }
   }
 }
@@ -947,7 +970,7 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
       uint32_t n[kEB];
       {
         int32_t v0[kEB], v1[kEB];
-        mv_ranges<kEB, LM>(hmv, hoff, doc_base, h, m, lane, v0, v1);
+        mv_ranges<kEB, LM>(hmv, hoff, (int64_t)cs->num_docs, doc_base, h, m, lane, v0, v1);
 #pragma unroll
         for (int i = 0; i < kEB; ++i) n[i] = v1[i] - v0[i] > 0 ? (uint32_t)(v1[i] - v0[i]) : 1u;
       }
@@ -1091,7 +1114,7 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
         const uint32_t first_bit = q->h_first ? 1u : 0u;
         // every step's value ranges first (one wait for the batch)
         int32_t v0s[kEB], nvs[kEB];
-        mv_ranges<kEB, LM>(hmv, hoff, doc_base, h, m, lane, v0s, nvs);
+        mv_ranges<kEB, LM>(hmv, hoff, (int64_t)cs->num_docs, doc_base, h, m, lane, v0s, nvs);
 #pragma unroll
         for (int i = 0; i < kEB; ++i) nvs[i] -= v0s[i];
         // Doc-reserved batch path (every matching doc of the batch has at most kDocVals records), kHS steps at a time
