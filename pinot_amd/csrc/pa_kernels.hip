@@ -942,7 +942,9 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
   const int hslot = ha >= 0 ? q->aggs[ha].slot : 0;
   const bool hmv = ha >= 0 && cs->cols[hslot].kind == COL_MV_DICT;
   const int32_t* hoff = cs->cols[hslot].mv_off;
-  constexpr int kEB = 8;  // steps per batch (register budget; 4 for the H-only emit measured slower: 4.83 vs 4.65 ms)
+  // steps per batch (register budget; 4 for the H-only emit measured slower: 4.83 vs 4.65 ms). The V-only emit of
+  // 4-wave workgroups runs at most 2 workgroups per CU (its LDS bins), so it has the VGPRs for a whole tile per batch.
+  constexpr int kEB = (is_pemit(STRAT) && !pemit_hh(STRAT) && !pemit_big(STRAT) && pemit_vf(STRAT) != V_FMT_GEN) ? 16 : 8;
 #pragma unroll 1
   for (int h = 0; h < STEPS; h += kEB) {
     if (__ballot((m >> h) != 0) == 0) break;  // wave-uniform: the H records below shuffle across all 64 lanes
@@ -1677,9 +1679,14 @@ __device__ __forceinline__ int64_t xcd_major_block(int64_t b, int64_t G) {
   return x * per + (x < extra ? x : extra) + j;
 }
 
+// The V-only emit of 4-wave workgroups (one whole tile per batch in part_tile): compiled for 2 workgroups per CU.
+__host__ __device__ constexpr bool emit_v_wide(int s) {
+  return is_pemit(s) && !pemit_hh(s) && !pemit_big(s) && pemit_vf(s) != V_FMT_GEN;
+}
+
 // LM = 1: lane-major tiles (STEPS must be 32) driven by the per-segment plan tables `plans`; LM = 0: step-major.
 template <int STRAT, int STEPS, int LM>
-__global__ void __launch_bounds__(scan_waves(STRAT) * kWave, scan_waves(STRAT) == kWavesPerWG ? 4 : 1) scan_kernel(const DevQuery* __restrict__ q,
+__global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) ? 2 : (scan_waves(STRAT) == kWavesPerWG ? 4 : 1)) scan_kernel(const DevQuery* __restrict__ q,
                                                        const DevSeg* __restrict__ segs,
                                                        const LmSegPlan* __restrict__ plans, PartScratch ps) {
   static_assert(!LM || STEPS == 32, "lane-major tiles are 2048 docs");
