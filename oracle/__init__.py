@@ -270,12 +270,8 @@ def _pack_msb(ids, nb):
     return np.packbits(bits)
 
 
-def run_segment(query, segment):
-    """Per-segment intermediate result: {key tuple (values): [count, per-oracle-agg values]}; () for agg-only.
-
-    Raw (no-dictionary) group-by columns are grouped by value, as the reference's NoDictionarySingleColumn /
-    NoDictionaryMultiColumnGroupKeyGenerator do (value -> group id map): the oracle gives each one a virtual sorted
-    dictionary of its distinct values (its own column slot, so the same column can still be filtered or aggregated raw)."""
+def _run_segment_raw(query, segment):
+    """The C scan of one segment; results as arrays (_SegRaw)."""
     from pinot_amd import query as Q  # noqa: F401
     cols_order = sorted(query.columns())
     cidx = {c: i for i, c in enumerate(cols_order)}
@@ -402,6 +398,27 @@ def run_segment(query, segment):
     if n < 0:
         raise MemoryError("oracle allocation failed")
     n = min(n, cap)
+    return _SegRaw(n, keys, counts, vals, hll_bufs, oaggs, amap, int(matched.value), cap, virt)
+
+
+class _SegRaw:
+    """Array form of one segment's oracle result: raw keys (DictionaryBasedGroupKeyGenerator raw key over the segment's
+    own dictionaries, column 0 least significant) in first-seen order, counts, per-accumulator values."""
+
+    def __init__(self, n, keys, counts, vals, hll_bufs, oaggs, amap, matched, cap, virt):
+        self.n, self.keys, self.counts, self.vals, self.hll_bufs = n, keys, counts, vals, hll_bufs
+        self.oaggs, self.amap, self.matched, self.cap, self.virt = oaggs, amap, matched, cap, virt
+
+
+def run_segment(query, segment):
+    """Per-segment intermediate result: {key tuple (values): [count, per-oracle-agg values]}; () for agg-only.
+
+    Raw (no-dictionary) group-by columns are grouped by value, as the reference's NoDictionarySingleColumn /
+    NoDictionaryMultiColumnGroupKeyGenerator do (value -> group id map): the oracle gives each one a virtual sorted
+    dictionary of its distinct values (its own column slot, so the same column can still be filtered or aggregated raw)."""
+    r = _run_segment_raw(query, segment)
+    n, keys, counts, vals, hll_bufs, oaggs, amap, cap, virt = (r.n, r.keys, r.counts, r.vals, r.hll_bufs, r.oaggs,
+                                                               r.amap, r.cap, r.virt)
     out = {}
     for g in range(n):
         if query.group_by:
@@ -426,7 +443,7 @@ def run_segment(query, segment):
             else:
                 row.append(float(vals[ai * cap + g]))
         out[key] = (int(counts[g]), row)
-    return out, oaggs, amap, int(matched.value)
+    return out, oaggs, amap, r.matched
 
 
 def run_query(query, segments):
@@ -492,3 +509,50 @@ def run_query(query, segments):
         else:
             out.row = vals
     return out
+
+
+def run_query_arrays(query, segments):
+    """run_query's server-level merge in array form, for the BASELINE-sized configs tests (up to ~1M groups, where the
+    per-group Python objects of run_query cost more than the scan). Every segment must share one dictionary per
+    group-by column, so the oracle's raw key (column 0 least significant) IS the GPU's table-wide key. Returns a dict:
+    keys (ascending int64), counts (int64), accs (one array per oracle accumulator, in `oaggs` order: float64[n], or
+    uint8[n, 2^log2m] HLL registers), oaggs, amap, matched (numDocsScanned) and limit_reached."""
+    for c in query.group_by:
+        d0 = segments[0].column(c).dictionary
+        if not all(s.column(c).dictionary is d0 or np.array_equal(s.column(c).dictionary, d0) for s in segments):
+            raise ValueError("run_query_arrays: segments must share the dictionary of group-by column %s" % c)
+    raws = [_run_segment_raw(query, s) for s in segments]
+    oaggs, amap = raws[0].oaggs, raws[0].amap
+    if any(k[0] == "DISTINCTCOUNT" for k in oaggs):
+        raise ValueError("run_query_arrays: DISTINCTCOUNT is compared through run_query")
+    seg_keys = [r.keys[:r.n] if query.group_by else np.zeros(r.n, np.int64) for r in raws]
+    uniq = np.unique(np.concatenate(seg_keys)) if seg_keys else np.zeros(0, np.int64)
+    if not query.group_by:
+        uniq = np.zeros(1, np.int64)
+    u = len(uniq)
+    cnt = np.zeros(u, np.int64)
+    accs = []
+    for k in oaggs:
+        if k[0] == "DISTINCTCOUNTHLL":
+            accs.append(np.zeros((u, 1 << k[2]), np.uint8))
+        else:
+            accs.append(np.full(u, np.inf if k[0] == "MIN" else (-np.inf if k[0] == "MAX" else 0.0)))
+    for r, sk in zip(raws, seg_keys):
+        idx = np.searchsorted(uniq, sk)  # a key occurs once per segment: plain fancy-index updates
+        cnt[idx] += r.counts[:r.n]
+        for ai, k in enumerate(oaggs):
+            if k[0] == "DISTINCTCOUNTHLL":
+                m = 1 << k[2]
+                part = r.hll_bufs[ai][:r.n * m].reshape(r.n, m)
+                accs[ai][idx] = np.maximum(accs[ai][idx], part)
+            else:
+                part = r.vals[ai * r.cap: ai * r.cap + r.n]
+                if k[0] == "MIN":
+                    accs[ai][idx] = np.minimum(accs[ai][idx], part)
+                elif k[0] == "MAX":
+                    accs[ai][idx] = np.maximum(accs[ai][idx], part)
+                else:
+                    accs[ai][idx] += part
+    limit_reached = bool(query.group_by) and any(r.n >= query.num_groups_limit for r in raws)
+    return {"keys": uniq.astype(np.int64), "counts": cnt, "accs": accs, "oaggs": oaggs, "amap": amap,
+            "matched": sum(r.matched for r in raws), "limit_reached": limit_reached}

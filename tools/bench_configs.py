@@ -54,6 +54,19 @@ def highcard_rd_segment(seed, docs):
     return seg
 
 
+def sumscan_segment(seed, docs):
+    """configs[0]: a fixed-bit dictionary-encoded INT dimension (daysSinceEpoch, 1024 days = 10 bits) and a LONG metric
+    m whose 16384 dictionary values (14 bits) are sorted random longs (no arithmetic shortcut: every SUM value is a
+    dictionary lookup)."""
+    from pinot_amd.segment import segment_from_dict_ids
+    rng = np.random.default_rng(seed)
+    vals = np.unique(np.random.default_rng(777).integers(0, 1 << 36, size=20_000))[:1 << 14].astype(np.int64)
+    assert len(vals) == 1 << 14
+    return segment_from_dict_ids("ss%d" % seed, docs, {
+        "daysSinceEpoch": sv_spec(rng, docs, 1024, base=17000),
+        "m": ("LONG", vals, sv_spec(rng, docs, 1 << 14)[2])})
+
+
 def star_segment(seed, docs, avg_mv=3):
     from pinot_amd.segment import Column, mv_column_from_flat, segment_from_dict_ids
     rng = np.random.default_rng(seed)
@@ -70,6 +83,13 @@ def star_segment(seed, docs, avg_mv=3):
 
 
 WORKLOADS = {
+    # configs[0]: COUNT(*), SUM(m) WHERE day BETWEEN a AND b at ~10 % / ~50 % / 100 % selectivity (day dictionary
+    # 17000..17999, uniform)
+    "sumscan": (sumscan_segment, [
+        ("sel_10pct", "SELECT COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17201", 0),
+        ("sel_50pct", "SELECT COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17611", 0),
+        ("sel_100pct", "SELECT COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17000 AND 18023", 0),
+    ]),
     "highcard": (highcard_segment, [
         ("all_docs", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000 "
                      "OPTION(numGroupsLimit=2000000)", 0),
