@@ -1536,8 +1536,20 @@ int plan_kernels(pa_query* q, Prep& P, TilePlan& plan, TilePlan& count_plan) {
   // LDS-privatised accumulators when many docs are expected to reach them (and the key space fits); otherwise the
   // LDS goes to tile rings (more resident waves) and the rare survivors update global accumulators directly.
   q->strategy = STRAT_GLOBAL;
-  if (!(s.flags & PA_QF_FORCE_GLOBAL) && !q->limit_mode && !q->hashed && P.lds_acc <= 64 * 1024 &&
-      (P.dense || (s.flags & PA_QF_FORCE_LDS))) {
+  // Aggregation-only over single-value columns (configs[0]'s COUNT(*), SUM(m) WHERE ...): running totals in every lane's
+  // registers, reduced once per wave at the end of the kernel (STRAT_LANE)
+  bool lane_acc = s.num_group_by == 0 && !q->has_mv && !q->limit_mode && !q->hashed && s.num_aggs <= kLaneAggs &&
+                  !(s.flags & (PA_QF_NO_LANE_ACC | PA_QF_FORCE_GLOBAL | PA_QF_FORCE_LDS));
+  for (int a = 0; a < s.num_aggs && lane_acc; ++a) {
+    const int t = s.aggs[a].type;
+    lane_acc = t == PA_AGG_COUNT || t == PA_AGG_SUM || t == PA_AGG_MIN || t == PA_AGG_MAX;
+  }
+  if (lane_acc) {
+    plan = plan_pick(STRAT_LANE, 0);
+    if (plan.score >= 0) q->strategy = STRAT_LANE;
+  }
+  if (q->strategy == STRAT_GLOBAL && !(s.flags & PA_QF_FORCE_GLOBAL) && !q->limit_mode && !q->hashed &&
+      P.lds_acc <= 64 * 1024 && (P.dense || (s.flags & PA_QF_FORCE_LDS))) {
     plan = plan_pick(STRAT_LDS, P.lds_acc);
     if (plan.score >= 0) q->strategy = STRAT_LDS;
   }

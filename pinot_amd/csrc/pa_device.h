@@ -33,7 +33,11 @@ enum ColKind : int32_t { COL_NONE = 0, COL_SV_DICT = 1, COL_SV_RAW = 2, COL_MV_D
 //   part_agg_kernel: one workgroup per partition aggregates its records in LDS and stores its key range.
 // Two record streams: V (one record per matching doc: COUNT + SUM/MIN/MAX payloads) and H (one record per value of
 // the DISTINCTCOUNTHLL(MV) column: key | register | rank), each with its own key partitioning.
-enum Strategy : int32_t { STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PEMIT = 2, STRAT_PCOUNT = 3 };
+// STRAT_LANE: aggregation-only queries (no GROUP BY) over single-value columns: every lane keeps its own running
+// COUNT/SUM/MIN/MAX in registers for the whole kernel and the wave reduces them once at the end (no per-step reduction,
+// no LDS or global atomics per doc).
+enum Strategy : int32_t { STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PEMIT = 2, STRAT_PCOUNT = 3, STRAT_LANE = 4 };
+constexpr int kLaneAggs = 4;  // STRAT_LANE: at most this many non-COUNT aggregations
 // The emit pass's kernel variant (launch code): the V record format (-1: no V stream) and whether there is an H stream
 // are template parameters, so each variant's record loop is straight-line code (no per-record format branches).
 // `big`: 16-wave workgroups (the partition bins and their state are per workgroup, so sharing them among more waves

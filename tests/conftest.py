@@ -49,3 +49,17 @@ def rows_match(got, expected, delta):
             elif float(a) != float(b):
                 return False
     return True
+
+
+_TORCH_GPU = []
+
+
+def pytest_runtest_setup(item):
+    """Before the first GPU test: initialise torch's HIP runtime on device 0. Torch's ROCm wheel carries its own HIP
+    runtime; when libpinot_amd's (the system ROCm one) initialises the device first, torch later finds no GPU and the
+    RCCL (ProcessGroupNCCL) tests cannot start. Order-independent GPU tests need torch first."""
+    if item.get_closest_marker("gpu") is not None and not _TORCH_GPU:
+        import torch
+        torch.cuda.set_device(0)
+        torch.zeros(1, device="cuda")
+        _TORCH_GPU.append(True)

@@ -87,12 +87,20 @@ def test_configs0_count_sum_day_range(sumscan, plan):
     q = parse_sql(sql)
     ex = GpuQueryExecutor(q, [g])
     try:
-        assert _plan(ex)["lane_major"] == 1
+        p = _plan(ex)
+        assert p["lane_major"] == 1 and p["strategy"] == "lane", p
         got = ex.run()
     finally:
         ex.close()
     exp = oracle.run_query(q, [seg])
     assert_same(got, exp)
+    # the LDS-accumulator path (the strategy before per-lane registers) agrees
+    ex = GpuQueryExecutor(q, [g], flags=L.PA_QF_NO_LANE_ACC)
+    try:
+        assert _plan(ex)["strategy"] != "lane"
+        assert_same(ex.run(), exp)
+    finally:
+        ex.close()
     frac = got.row[0] / seg.num_docs
     assert {"sel_10pct": 0.1, "sel_50pct": 0.5, "sel_100pct": 1.0}[plan] == pytest.approx(frac, abs=0.02)
 

@@ -151,7 +151,8 @@ def test_random_queries(seed, qi):
 
 @pytest.mark.parametrize("flags", [L.PA_QF_FORCE_GLOBAL, L.PA_QF_STAGE_ALL, L.PA_QF_FORCE_GLOBAL | L.PA_QF_STAGE_ALL,
                                    L.PA_QF_NO_LANE_MAJOR, L.PA_QF_NO_LANE_MAJOR | L.PA_QF_FORCE_GLOBAL,
-                                   L.PA_QF_NO_LANE_MAJOR | L.PA_QF_STAGE_ALL | L.PA_QF_NO_LAZY])
+                                   L.PA_QF_NO_LANE_MAJOR | L.PA_QF_STAGE_ALL | L.PA_QF_NO_LAZY, L.PA_QF_NO_LANE_ACC,
+                                   L.PA_QF_NO_LANE_ACC | L.PA_QF_NO_LANE_MAJOR])
 def test_strategies_agree(flags):
     """LDS-privatised vs global accumulators, staged vs lazy post-filter columns, lane-major vs step-major tiles:
     identical results."""

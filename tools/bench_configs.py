@@ -56,11 +56,12 @@ def highcard_rd_segment(seed, docs):
 
 def sumscan_segment(seed, docs):
     """configs[0]: a fixed-bit dictionary-encoded INT dimension (daysSinceEpoch, 1024 days = 10 bits) and a LONG metric
-    m whose 16384 dictionary values (14 bits) are sorted random longs (no arithmetic shortcut: every SUM value is a
-    dictionary lookup)."""
+    m whose 16384 dictionary values (14 bits) are sorted random longs below 2^29 (no arithmetic shortcut: every SUM value
+    is a dictionary lookup; a 10M-doc segment's sum stays below 2^53, where the reference's double accumulation is
+    exact)."""
     from pinot_amd.segment import segment_from_dict_ids
     rng = np.random.default_rng(seed)
-    vals = np.unique(np.random.default_rng(777).integers(0, 1 << 36, size=20_000))[:1 << 14].astype(np.int64)
+    vals = np.unique(np.random.default_rng(777).integers(0, 1 << 29, size=20_000))[:1 << 14].astype(np.int64)
     assert len(vals) == 1 << 14
     return segment_from_dict_ids("ss%d" % seed, docs, {
         "daysSinceEpoch": sv_spec(rng, docs, 1024, base=17000),
