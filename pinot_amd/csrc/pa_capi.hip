@@ -84,6 +84,7 @@ struct Column {
   int64_t total_values = 0;
   int32_t max_values = 1;   // MV: most values in one row
   bool fits_int32 = false;  // every dictionary value (INT/LONG) fits in int32
+  bool dict_sorted = false; // dictionary values strictly ascending (COLF_DICT_SORTED)
   std::vector<uint64_t> hvals;  // host copy of the dictionary values (8-byte bits): table-wide value dictionaries
   uint64_t dict_hash = 0;       // FNV-1a of hvals: identical dictionaries across segments are found without a compare
   DevBuf words;   // guard + stream + pad (SV dict)
@@ -113,6 +114,13 @@ struct pa_segment {
 
 namespace {
 
+// Order key of an 8-byte dictionary value: the value itself (INT/LONG) or its order-preserving image (FLOAT/DOUBLE,
+// Double.compare order: -0.0 < 0.0), so distinct values get distinct keys in value order.
+inline int64_t value_order_key(uint64_t bits, int32_t vtype) {
+  return (vtype == PA_FLOAT || vtype == PA_DOUBLE) ? f64_order_encode(__builtin_bit_cast(double, bits))
+                                                    : (int64_t)bits;
+}
+
 int upload_dict(Column* c, int32_t vtype, int32_t card, const void* dict_values, const int32_t* dict_hashes) {
   c->vtype = vtype;
   c->cardinality = card;
@@ -129,6 +137,10 @@ int upload_dict(Column* c, int32_t vtype, int32_t card, const void* dict_values,
       c->fits_int32 = true;
       for (int32_t i = 0; i < card && c->fits_int32; ++i) c->fits_int32 = v[i] >= INT32_MIN && v[i] <= INT32_MAX;
     }
+    // sorted dictionary (the reference's dictionaries always are: SegmentDictionaryCreator sorts the unique values)
+    c->dict_sorted = true;
+    for (int32_t i = 1; i < card && c->dict_sorted; ++i)
+      c->dict_sorted = value_order_key(c->hvals[i - 1], vtype) < value_order_key(c->hvals[i], vtype);
   }
   if (dict_hashes != nullptr) {
     int rc = dev_alloc(c->hashes, (size_t)card * 4);
@@ -448,12 +460,6 @@ inline int64_t presence_stride(const pa_agg_spec& A) { return (A.num_values + 15
 // element bytes of an accumulator section
 inline size_t section_es(int32_t kind) { return (kind == PA_ACC_HLL_U8 || kind == PA_ACC_PRESENCE_U8) ? 1 : 8; }
 
-// Order key of an 8-byte dictionary value: the value itself (INT/LONG) or its order-preserving image (FLOAT/DOUBLE,
-// Double.compare order: -0.0 < 0.0), so distinct values get distinct keys in value order.
-inline int64_t value_order_key(uint64_t bits, int32_t vtype) {
-  return (vtype == PA_FLOAT || vtype == PA_DOUBLE) ? f64_order_encode(__builtin_bit_cast(double, bits))
-                                                    : (int64_t)bits;
-}
 
 }  // namespace
 
@@ -872,6 +878,8 @@ int build_segments(pa_query* q, Prep& P) {
       dc.dict_i64 = (c->vtype == PA_INT || c->vtype == PA_LONG) ? (const int64_t*)c->dict.p : nullptr;
       dc.dict_f64 = (c->vtype == PA_FLOAT || c->vtype == PA_DOUBLE) ? (const double*)c->dict.p : nullptr;
       dc.lds_off = -1;
+      dc.card = c->cardinality;
+      dc.flags = c->dict_sorted ? COLF_DICT_SORTED : 0;
       if (c->kind == COL_SV_DICT && (P.slot_eager[sl] || P.stage_all || (P.stage_post && P.slot_post[sl]))) {
         dc.lds_off = 0;  // staged; the region offset depends on the tile size (apply_layout)
         d.stage[d.num_staged++] = StageDesc{dc.words, dc.nbits, 0};

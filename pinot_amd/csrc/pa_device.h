@@ -75,7 +75,11 @@ struct DevCol {
   int32_t nbits;
   int32_t vtype;             // PA_INT..PA_BYTES
   int32_t lds_off;           // staged: dword offset of the column's region inside a wave image; -1 = lazy
+  int32_t card;              // dictionary columns: cardinality (dictIds < card)
+  int32_t flags;             // COLF_*
 };
+constexpr int32_t COLF_DICT_SORTED = 1;  // dictionary values strictly ascending (INT/LONG by value, FLOAT/DOUBLE in
+                                         // Double.compare order): MIN/MAX of values = the values of the MIN/MAX dictId
 
 // One CNF literal for one segment. The column fields the leaf reads are copied in, so evaluating a leaf
 // costs one scalar-load round per tile (no dependent leaf -> column descriptor chain).

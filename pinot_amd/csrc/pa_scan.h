@@ -1393,10 +1393,16 @@ __device__ __forceinline__ uint32_t admitted_docs(const DevQuery* __restrict__ q
 // sum; MIN / MAX r0 = running min / max (doubles in the order-preserving encoding). The wave reduces them once, at the
 // end of the kernel (lane_acc_flush). Reference: AggregationOperator -> SumAggregationFunction.aggregate (a running sum
 // over the block's values), Min/MaxAggregationFunction.aggregate.
+// MIN / MAX over a sorted dictionary run on dictIds (rid[a]: the lane's min / max dictId within the current segment),
+// folded into r0 as a value at the end of every segment run (lane_acc_segment_end).
 struct LaneAcc {
   int64_t r0[kLaneAggs];
   int64_t r1[kLaneAggs];
+  uint32_t rid[kLaneAggs];
+  uint32_t idm;  // bit a: rid[a] was updated in the current segment run
 };
+
+__device__ __forceinline__ uint32_t rid_init(int t) { return t == PA_AGG_MIN ? 0xffffffffu : 0u; }
 
 __device__ __forceinline__ void lane_acc_init(const DevQuery* __restrict__ q, LaneAcc& la) {
 #pragma unroll
@@ -1404,7 +1410,110 @@ __device__ __forceinline__ void lane_acc_init(const DevQuery* __restrict__ q, La
     const int t = a < q->num_aggs ? q->aggs[a].type : PA_AGG_COUNT;
     la.r0[a] = t == PA_AGG_MIN ? INT64_MAX : (t == PA_AGG_MAX ? INT64_MIN : 0);
     la.r1[a] = 0;
+    la.rid[a] = rid_init(t);
   }
+  la.idm = 0;
+}
+
+// Lane-major fast path modes (lane_agg_lm)
+enum LaneMode : int { LM_SUM_INT = 0, LM_SUM_LONG = 1, LM_SUM_DOUBLE = 2, LM_MIN_ID = 3, LM_MAX_ID = 4 };
+
+// One aggregation over the 32 docs of this lane in a lane-major tile (docs 32*lane + i, match bit i of m) from a staged
+// dictionary column of NB-bit ids: the lane's NB stream words are read once and every id is a constant-shift extract.
+// SUM: the value is a buffer load of dict[id] with a buffer resource bounded by the dictionary, and a doc that does not
+// match asks for index 0xffffffff (its bit of ~m spread by a signed bitfield extract, ORed into the id): out of range,
+// so the load returns 0 — no per-doc branch or select. MIN_ID / MAX_ID track the smallest / largest matching dictId
+// (0xffffffff is neutral under unsigned min; a non-matching id is ANDed to 0 for max).
+template <int NB>
+__device__ __forceinline__ void lane_agg_lm(uint32_t region_lds, int lane, uint32_t m, int mode,
+                                            __amdgpu_buffer_rsrc_t dict, int64_t& r0, int64_t& r1, uint32_t& rid) {
+  const lds_u32_t* p = (const lds_u32_t*)(uintptr_t)(region_lds + (uint32_t)lane * (uint32_t)(NB * 4));
+  constexpr int H = NB > 16 ? 2 : 1;  // halves of 16 docs for wide columns (live stream words stay ~NB/2 + 1)
+  constexpr int DPH = 32 / H;
+  const uint32_t nm = ~m;
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    constexpr int WMAX = (DPH * NB + 31) / 32 + 1;
+    const int wlo = (h * DPH * NB) >> 5;
+    uint32_t w[WMAX];
+#pragma unroll
+    for (int j = 0; j < WMAX; ++j) w[j] = (wlo + j < NB) ? p[wlo + j] : 0u;
+    auto id_of = [&](int i) -> uint32_t {
+      const int s = i * NB, j = (s >> 5) - wlo, o = s & 31;
+      if (o + NB <= 32) return __builtin_amdgcn_ubfe(w[j], (uint32_t)(32 - o - NB), (uint32_t)NB);
+      return __builtin_amdgcn_alignbit(w[j], w[(j + 1 < WMAX) ? j + 1 : j], 32 - o) >> (32 - NB);
+    };
+    if (mode <= LM_SUM_DOUBLE) {
+      uint64_t v[DPH];
+#pragma unroll
+      for (int k = 0; k < DPH; ++k) {
+        const int i = h * DPH + k;
+        const uint32_t off = (id_of(i) << 3) | (uint32_t)__builtin_amdgcn_sbfe((int)nm, (uint32_t)i, 1u);
+        v[k] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(dict, off, 0, 0));
+      }
+      if (mode == LM_SUM_INT) {
+#pragma unroll
+        for (int k = 0; k < DPH; ++k) r0 += (int64_t)v[k];
+      } else if (mode == LM_SUM_LONG) {
+#pragma unroll
+        for (int k = 0; k < DPH; ++k) {
+          r0 += (int64_t)(uint32_t)v[k];
+          r1 += (int64_t)v[k] >> 32;
+        }
+      } else {
+        double d = __builtin_bit_cast(double, r0);
+#pragma unroll
+        for (int k = 0; k < DPH; ++k) d += __builtin_bit_cast(double, v[k]);
+        r0 = __builtin_bit_cast(int64_t, d);
+      }
+    } else if (mode == LM_MIN_ID) {
+#pragma unroll
+      for (int k = 0; k < DPH; ++k) {
+        const int i = h * DPH + k;
+        rid = min(rid, id_of(i) | (uint32_t)__builtin_amdgcn_sbfe((int)nm, (uint32_t)i, 1u));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < DPH; ++k) {
+        const int i = h * DPH + k;
+        rid = max(rid, id_of(i) & (uint32_t)__builtin_amdgcn_sbfe((int)m, (uint32_t)i, 1u));
+      }
+    }
+  }
+}
+
+__device__ __noinline__ void lane_agg_lm_any(int nb, uint32_t region_lds, int lane, uint32_t m, int mode,
+                                                __amdgpu_buffer_rsrc_t dict, int64_t& r0, int64_t& r1, uint32_t& rid) {
+  switch (nb) {
+#define PA_LA_CASE(N) \
+  case N: lane_agg_lm<N>(region_lds, lane, m, mode, dict, r0, r1, rid); break;
+    PA_LA_CASE(1) PA_LA_CASE(2) PA_LA_CASE(3) PA_LA_CASE(4) PA_LA_CASE(5) PA_LA_CASE(6) PA_LA_CASE(7) PA_LA_CASE(8)
+    PA_LA_CASE(9) PA_LA_CASE(10) PA_LA_CASE(11) PA_LA_CASE(12) PA_LA_CASE(13) PA_LA_CASE(14) PA_LA_CASE(15)
+    PA_LA_CASE(16) PA_LA_CASE(17) PA_LA_CASE(18) PA_LA_CASE(19) PA_LA_CASE(20) PA_LA_CASE(21) PA_LA_CASE(22)
+    PA_LA_CASE(23) PA_LA_CASE(24) PA_LA_CASE(25) PA_LA_CASE(26) PA_LA_CASE(27) PA_LA_CASE(28) PA_LA_CASE(29)
+    PA_LA_CASE(30) PA_LA_CASE(31)
+#undef PA_LA_CASE
+    default: break;
+  }
+}
+
+// End of a wave's run over one segment: MIN / MAX dictIds of the segment -> values, folded into r0 (only when the
+// lane kept some doc of the segment: a MAX dictId of 0 is otherwise meaningless).
+__device__ __forceinline__ void lane_acc_segment_end(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                                     LaneAcc& la, bool any) {
+#pragma unroll
+  for (int a = 0; a < kLaneAggs; ++a) {
+    if (a >= q->num_aggs) break;
+    const int t = q->aggs[a].type;
+    if (t != PA_AGG_MIN && t != PA_AGG_MAX) continue;
+    const uint32_t id = la.rid[a];
+    la.rid[a] = rid_init(t);
+    if (!((la.idm >> a) & 1u) || !any || (t == PA_AGG_MIN && id == 0xffffffffu)) continue;
+    const DevCol& c = seg->cols[q->aggs[a].slot];
+    const int64_t e = q->aggs[a].src == SRC_DOUBLE ? f64_order_encode(gp(c.dict_f64)[id]) : gp(c.dict_i64)[id];
+    la.r0[a] = t == PA_AGG_MIN ? (e < la.r0[a] ? e : la.r0[a]) : (e > la.r0[a] ? e : la.r0[a]);
+  }
+  la.idm = 0;
 }
 
 // The matching docs (match words m) of one tile into the lane accumulators: per aggregation, 8 steps per batch — every
@@ -1432,6 +1541,18 @@ __device__ __forceinline__ void lane_acc_tile(const DevQuery* __restrict__ q, co
                                              : (const uint64_t*)cs->cols[slot].dict_i64;
     const void* raw = cs->cols[slot].raw;
     int64_t r0 = la.r0[a], r1 = la.r1[a];
+    if (LM && kind == COL_SV_DICT && loff >= 0 &&
+        (type == PA_AGG_SUM || (cs->cols[slot].flags & COLF_DICT_SORTED))) {
+      const int mode = type == PA_AGG_SUM ? (src == SRC_INT ? LM_SUM_INT : (src == SRC_LONG ? LM_SUM_LONG : LM_SUM_DOUBLE))
+                                          : (type == PA_AGG_MIN ? LM_MIN_ID : LM_MAX_ID);
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)dict, (short)0, cs->cols[slot].card * 8, 0x00020000);
+      lane_agg_lm_any(nb, lds_addr(img + loff), lane, m, mode, rs, r0, r1, la.rid[a]);
+      if (mode >= LM_MIN_ID) la.idm |= 1u << a;
+      la.r0[a] = r0;
+      la.r1[a] = r1;
+      continue;
+    }
 #pragma unroll 1
     for (int h = 0; h < STEPS; h += kB) {
       if (__ballot(((m >> h) & 0xffu) != 0) == 0) continue;
@@ -1923,6 +2044,7 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
     while (t < t1) {
       // segment-outer / tile-inner: `seg` is invariant in the inner loop, so its descriptors stay in SGPRs
       const DevSeg* seg = segs + si;
+      const uint32_t matched_seg0 = matched;
       const int64_t seg_first = seg->first_wtile;
       const int64_t seg_end = min(t1, seg_first + (int64_t)seg->num_wtiles);
       const uint32_t pp = LM ? ((const uint32_t*)(plans + si))[lane] : 0u;  // process segment's plan table
@@ -1998,6 +2120,7 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
         }
         pslot = pslot + 1 == R ? 0 : pslot + 1;
       }
+      if constexpr (STRAT == STRAT_LANE) lane_acc_segment_end(q, seg, la, matched != matched_seg0);
       if (t < t1) {
         ++si;
         while (t >= segs[si].first_wtile + segs[si].num_wtiles) ++si;

@@ -68,6 +68,17 @@ def sumscan_segment(seed, docs):
         "m": ("LONG", vals, sv_spec(rng, docs, 1 << 14)[2])})
 
 
+def sumscan_raw_segment(seed, docs):
+    """configs[0] with the LONG metric stored raw (no dictionary: Pinot's usual metric layout, noDictionaryColumns):
+    8 bytes per doc, read straight from HBM."""
+    from pinot_amd.segment import Column
+    seg = sumscan_segment(seed, docs)
+    m = Column(name="m", data_type="LONG", has_dictionary=False)
+    m.raw_values = np.random.default_rng(seed + 5).integers(0, 1 << 29, size=docs, dtype=np.int64)
+    seg.columns["m"] = m
+    return seg
+
+
 def star_segment(seed, docs, avg_mv=3):
     from pinot_amd.segment import Column, mv_column_from_flat, segment_from_dict_ids
     rng = np.random.default_rng(seed)
@@ -87,6 +98,16 @@ WORKLOADS = {
     # configs[0]: COUNT(*), SUM(m) WHERE day BETWEEN a AND b at ~10 % / ~50 % / 100 % selectivity (day dictionary
     # 17000..17999, uniform)
     "sumscan": (sumscan_segment, [
+        ("sel_0p1pct", "SELECT COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch = 17100", 0),
+        ("sel_1pct", "SELECT COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17109", 0),
+        ("count_10pct", "SELECT COUNT(*) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17201", 0),
+        ("count_100pct", "SELECT COUNT(*) FROM t WHERE daysSinceEpoch BETWEEN 17000 AND 18023", 0),
+        ("min_100pct", "SELECT MIN(m) FROM t WHERE daysSinceEpoch BETWEEN 17000 AND 18023", 0),
+        ("sel_10pct", "SELECT COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17201", 0),
+        ("sel_50pct", "SELECT COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17611", 0),
+        ("sel_100pct", "SELECT COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17000 AND 18023", 0),
+    ]),
+    "sumscan_raw": (sumscan_raw_segment, [
         ("sel_10pct", "SELECT COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17201", 0),
         ("sel_50pct", "SELECT COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17611", 0),
         ("sel_100pct", "SELECT COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17000 AND 18023", 0),
@@ -127,19 +148,32 @@ WORKLOADS = {
 }
 
 
-def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None):
+def cpu_port_baseline(sql, host_segs):
+    """bench.py's cpu_baseline (the C oracle port, one segment per thread) over the kept host segments."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("pa_bench_main", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from pinot_amd import parse_sql
+    return bench.cpu_baseline(parse_sql(sql), host_segs)
+
+
+def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None, cpu_sample=0):
     import torch
     from pinot_amd import parse_sql
     from pinot_amd import _lib as L
     from pinot_amd.engine import GpuQueryExecutor, GpuSegment
     make, queries = WORKLOADS[workload]
     t0 = time.perf_counter()
-    gsegs, cids = [], None
+    gsegs, cids, host = [], None, []
     for i in range(nseg):
         seg = make(100 + i, docs)
         if cids is None:
             cids = {n: j for j, n in enumerate(sorted(seg.columns))}
         gsegs.append(GpuSegment(seg, column_ids=cids, device=0))
+        if len(host) < cpu_sample:
+            host.append(seg)  # (kept whole for the CPU baseline)
+            continue
         for c in seg.columns.values():  # HBM holds the data now; keep only the dictionaries
             c.fwd_bytes = None
             c.raw_values = None
@@ -171,11 +205,24 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
             keys, counts, outs = ex.fetch_arrays(sp)
             fetch_ms = (time.perf_counter() - t1) * 1e3
             st = ex.stats()
-            print(json.dumps({"workload": workload, "plan_name": name + tag, "kernel_ms": round(ms, 4),
+            extra = {}
+            if cpu_sample:
+                # roofline of the fused scan: algorithmic bytes = the staged forward-index bytes + for
+                # raw value columns 8 (or 4) bytes per matching doc
+                matched = int(L.lib().pa_query_matched_docs(ex.handle))
+                agg_cols = {a.column for a in parse_sql(sql).aggregations if a.column}
+                raw_b = sum((4 if c.data_type in ("INT", "FLOAT") else 8) for c in gsegs[0].segment.columns.values()
+                            if not c.has_dictionary and c.name in agg_cols)
+                algo = st["staged_bytes"] + raw_b * matched
+                extra["roofline"] = {"bound": "hbm", "achieved": algo / (ms * 1e-3) / 1e9, "peak": 8000.0,
+                                     "unit": "GB/s", "frac": algo / (ms * 1e-3) / 1e9 / 8000.0,
+                                     "algorithmic_bytes_per_launch": algo}
+                extra["cpu_baseline"] = cpu_port_baseline(sql, host)
+            print(json.dumps(dict({"workload": workload, "plan_name": name + tag, "kernel_ms": round(ms, 4),
                               "rows_per_s": st["num_docs"] / (ms * 1e-3), "staged_bytes": st["staged_bytes"],
                               "staged_GBps": st["staged_bytes"] / (ms * 1e-3) / 1e9, "fetch_ms": round(fetch_ms, 2),
                               "groups": int(len(keys)), "matched_docs": int(L.lib().pa_query_matched_docs(ex.handle)),
-                              "plan": st["plan"], "segments": nseg, "docs_per_segment": docs}), flush=True)
+                              "plan": st["plan"], "segments": nseg, "docs_per_segment": docs}, **extra)), flush=True)
             ex.close()
     for g in gsegs:
         g.close()
@@ -192,6 +239,8 @@ def main():
     ap.add_argument("--sweep-part", action="store_true",
                     help="partitioned aggregation: sweep LDS per partition x workgroups per CU")
     ap.add_argument("--flags", type=int, default=None, help="run this one PA_QF_* flag set only")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="keep this many segments on the host: roofline + the C-port CPU baseline per line")
     args = ap.parse_args()
     variants = None if args.flags is None else [(args.flags, "_f%d" % args.flags)]
     if args.sweep_part:
@@ -201,7 +250,7 @@ def main():
     import torch
     torch.cuda.set_device(0)
     for w in (WORKLOADS if args.workload == "all" else [args.workload]):
-        run(w, args.segments, args.docs, args.reps, args.plan, args.no_stepmajor, variants)
+        run(w, args.segments, args.docs, args.reps, args.plan, args.no_stepmajor, variants, args.cpu_sample)
 
 
 if __name__ == "__main__":
