@@ -145,8 +145,8 @@ def main():
     # N>1: every rank groups over the same table-wide dictionaries (union over all ranks' segments), so key ids line up
     # across GPUs and the partial aggregates reduce element-wise
     # (and on the SUM accumulator widths), so the accumulator blocks line up element for element
-    td, wide = table_layout(q, [g.segment for g in gsegs]) if distributed else (None, ())
-    ex = GpuQueryExecutor(q, gsegs, flags=args.flags, table_dicts=td, wide_sum_columns=wide)
+    kw = table_layout(q, [g.segment for g in gsegs]).executor_kwargs() if distributed else {}
+    ex = GpuQueryExecutor(q, gsegs, flags=args.flags, **kw)
     dacc = DistributedAccumulators(ex, device) if distributed else None
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream

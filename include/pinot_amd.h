@@ -174,6 +174,9 @@ typedef struct {
   int32_t num_groups_limit; /* numGroupsLimit (QueryOptionsUtils / InstancePlanMakerImplV2, default 100000); 0 = none.
                                When some segment can hold that many distinct groups, the reference's first-seen trimming
                                runs on the GPU (DictionaryBasedGroupKeyGenerator IntGroupIdMap.getGroupId :992-1017) */
+  int64_t hash_keys_bound; /* hashed key spaces: the table holds at least 2 x this many keys (0 = size from the bound
+                              segments alone). A multi-GPU query passes the largest per-rank bound of all ranks so every
+                              rank's table can hold its share of the cross-GPU merge (parallel.table_layout) */
 } pa_query_spec;
 
 #define PA_QF_STAGE_ALL 1  /* stage post-filter columns through LDS even when a filter exists */

@@ -260,7 +260,9 @@ _ORACLE_FNS = {"SUM": ("SUM",), "AVG": ("SUM",), "MIN": ("MIN",), "MAX": ("MAX",
                "DISTINCTCOUNTHLL": ("DISTINCTCOUNTHLL",), "SUMMV": ("SUM",), "MINMV": ("MIN",), "MAXMV": ("MAX",),
                "DISTINCTCOUNTHLLMV": ("DISTINCTCOUNTHLL",), "COUNTMV": ("COUNTMV",), "AVGMV": ("SUM", "COUNTMV"),
                "COUNT": ("COUNT",), "MINMAXRANGE": ("MIN", "MAX"), "MINMAXRANGEMV": ("MIN", "MAX"),
-               "DISTINCTCOUNT": ("DISTINCTCOUNT",), "DISTINCTCOUNTMV": ("DISTINCTCOUNT",)}
+               "DISTINCTCOUNT": ("DISTINCTCOUNT",), "DISTINCTCOUNTMV": ("DISTINCTCOUNT",),
+               "DISTINCTSUM": ("DISTINCTCOUNT",), "DISTINCTSUMMV": ("DISTINCTCOUNT",),
+               "DISTINCTAVG": ("DISTINCTCOUNT",), "DISTINCTAVGMV": ("DISTINCTCOUNT",)}
 
 
 def _pack_msb(ids, nb):
@@ -500,7 +502,8 @@ def run_query(query, segments):
                 vals.append(HyperLogLog(a.log2m, row[ai] if isinstance(row[ai], np.ndarray) else None))
             elif a.function in ("MINMAXRANGE", "MINMAXRANGEMV"):
                 vals.append(MinMaxRangePair(row[ai[0]], row[ai[1]]))
-            elif a.function in ("DISTINCTCOUNT", "DISTINCTCOUNTMV"):
+            elif a.function in ("DISTINCTCOUNT", "DISTINCTCOUNTMV", "DISTINCTSUM", "DISTINCTSUMMV", "DISTINCTAVG",
+                                "DISTINCTAVGMV"):
                 vals.append(set(row[ai]))
             else:
                 vals.append(row[ai])

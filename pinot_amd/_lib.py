@@ -79,6 +79,7 @@ class QuerySpec(ctypes.Structure):
         ("aggs", AggSpec * PA_MAX_AGGS),
         ("flags", ctypes.c_int32),
         ("num_groups_limit", ctypes.c_int32),
+        ("hash_keys_bound", ctypes.c_int64),
     ]
 
 

@@ -780,6 +780,7 @@ int plan_key_space(pa_query* q, Prep& P) {
       }
       bound += n;
     }
+    if (s.hash_keys_bound > 0) bound = std::max<uint64_t>(bound, (uint64_t)s.hash_keys_bound);
     uint64_t H = 1024;
     while (H < 2 * bound && H < kMaxHashSlots) H <<= 1;
     q->hashed = true;

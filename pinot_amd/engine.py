@@ -142,7 +142,7 @@ def _flatten_filter(f, leaves, ops):
 
 class GpuQueryExecutor:
     def __init__(self, query: Q.Query, gpu_segments: List[GpuSegment], flags=0, enforce_num_groups_limit=True,
-                 table_dicts=None, wide_sum_columns=(), value_dicts=None):
+                 table_dicts=None, wide_sum_columns=(), value_dicts=None, hash_keys_bound=0):
         """table_dicts: optional {group-by column: sorted unique values} — the table-wide dictionary every rank of a
         multi-GPU query must share so that key ids address the same accumulator rows everywhere
         (parallel.table_layout builds it); by default it is the union of these segments' dictionaries.
@@ -150,12 +150,15 @@ class GpuQueryExecutor:
         segments' values all fit int32 — agreed across ranks by parallel.table_layout.
         value_dicts: optional {DISTINCTCOUNT column: sorted unique values} — the table-wide value dictionary whose ids
         the presence bytes index (every rank of a multi-GPU query must share it); by default the union of these
-        segments' dictionaries."""
+        segments' dictionaries.
+        hash_keys_bound: hashed key spaces: size the slot table for at least this many keys (parallel.table_layout
+        agrees on the largest rank's bound so every rank's table can take its share of the cross-GPU merge)."""
         if not gpu_segments:
             raise ValueError("no segments")
         self.table_dicts = table_dicts or {}
         self.table_value_dicts = value_dicts or {}
         self.wide_sum_columns = set(wide_sum_columns or ())
+        self.hash_keys_bound = int(hash_keys_bound or 0)
         self.query = query
         self.gsegs = gpu_segments
         self.segs = [g.segment for g in gpu_segments]
@@ -205,9 +208,9 @@ class GpuQueryExecutor:
                 # MinMaxRangePair(min, max): the MIN and MAX accumulators of the column
                 self.agg_map.append((acc_index((L.PA_AGG_MIN, ids[a.column], 0)),
                                      acc_index((L.PA_AGG_MAX, ids[a.column], 0))))
-            elif fn in ("DISTINCTCOUNT", "DISTINCTCOUNTMV"):
+            elif fn in Q.DISTINCT_SET_FUNCTIONS:
                 if not all(sg.column(a.column).has_dictionary for sg in self.segs):
-                    raise UnsupportedQuery("DISTINCTCOUNT on a raw (no-dictionary) column %s" % a.column)
+                    raise UnsupportedQuery("%s on a raw (no-dictionary) column %s" % (fn, a.column))
                 self.agg_map.append(acc_index((L.PA_AGG_DISTINCTCOUNT, ids[a.column], 0)))
             else:
                 raise UnsupportedQuery("aggregation %s" % fn)
@@ -303,6 +306,7 @@ class GpuQueryExecutor:
                     rm.append(np.searchsorted(gd, d).astype(np.int32))
             self.remaps.append(rm)
         spec.flags = self.flags
+        spec.hash_keys_bound = self.hash_keys_bound
 
         # numGroupsLimit (DictionaryBasedGroupKeyGenerator._globalGroupIdUpperBound): the per-segment first-seen group
         # cap. The library decides whether it can bind and then runs the first-seen trimming passes on the GPU;
@@ -506,8 +510,8 @@ class GpuQueryExecutor:
                 cols.append([HyperLogLog(log2m, regs[r]) for r in range(n)])
             elif a.function in ("MINMAXRANGE", "MINMAXRANGEMV"):
                 cols.append([MinMaxRangePair(lo, hi) for lo, hi in zip(outs[pi[0]].tolist(), outs[pi[1]].tolist())])
-            elif a.function in ("DISTINCTCOUNT", "DISTINCTCOUNTMV"):
-                # the value set of DistinctCountAggregationFunction (BaseDistinctAggregateAggregationFunction)
+            elif a.function in Q.DISTINCT_SET_FUNCTIONS:
+                # the value set of BaseDistinctAggregateAggregationFunction (DISTINCTCOUNT / DISTINCTSUM / DISTINCTAVG)
                 vd = self.value_dicts[pi]
                 pres = outs[pi].reshape(n, self._presence_stride(pi))[:, :len(vd)]
                 cols.append([set(vd[np.flatnonzero(pres[r])].tolist()) for r in range(n)])

@@ -430,8 +430,10 @@ def filter_is_match_all(filt, segment, bitmaps, index_info=None):
     return _build(_flatten(filt), segment, _LeafCursor(bitmaps, segment), index_info).kind == "all"
 
 
+# AggregationPlanNode.java:49-53
 DICTIONARY_BASED = {"MIN", "MINMV", "MAX", "MAXMV", "MINMAXRANGE", "MINMAXRANGEMV", "DISTINCTCOUNT", "DISTINCTCOUNTMV",
-                    "DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV"}
+                    "DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV", "DISTINCTSUM", "DISTINCTAVG", "DISTINCTSUMMV",
+                    "DISTINCTAVGMV"}
 METADATA_BASED = {"COUNT", "MIN", "MINMV", "MAX", "MAXMV", "MINMAXRANGE", "MINMAXRANGEMV"}
 
 

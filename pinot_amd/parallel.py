@@ -6,6 +6,7 @@ partial aggregates across GPUs then becomes one collective per accumulator secti
 SUM for COUNT/SUM, MIN for MIN, MAX for MAX and for HLL registers (HyperLogLog.addAll == register max).
 """
 import hashlib
+from dataclasses import dataclass, field
 
 import numpy as np
 import torch
@@ -63,40 +64,52 @@ def reduce_sections(views, dst=0, group=None, all_reduce=False):
             dist.reduce(t, dst=dst, op=SECTION_OP[kind], group=group)
 
 
-def merge_results_across_ranks(executor, dst=0, group=None):
-    """Key-based merge for hashed key spaces (accumulator slots differ per GPU, so sections cannot be reduced element-
-    wise): every rank fetches its groups and rank `dst` merges them by key value (GroupByCombineOperator / broker
-    reduce semantics, reduce.merge_intermediate). Returns the merged IntermediateResult on `dst`, None elsewhere."""
-    from .reduce import merge_intermediate
-    res = executor.fetch()
-    rank = dist.get_rank(group)
-    world = dist.get_world_size(group)
-    gathered = [None] * world if rank == dst else None
-    dist.gather_object(res, gathered, dst=dst, group=group)
-    return merge_intermediate(gathered) if rank == dst else None
+def key_owner(keys, world):
+    """Rank that owns packed key `keys` in the cross-GPU merge of hashed key spaces: a multiplicative hash of the key,
+    its high bits taken modulo the world size (int64 tensor ops: products wrap, the arithmetic shift is masked)."""
+    h = keys ^ (keys >> 31)
+    h = h * -7046029254386353131  # 0x9E3779B97F4A7C15 as a signed int64
+    return ((h >> 33) & 0x7FFFFFFF) % world
 
 
-def merge_hashed_sections(views, num_slots, group=None):
+def row_layout_fingerprint(views, num_slots, extra=b""):
+    """62-bit digest of what the ranks of a hashed merge must share: every section's kind and row width (elements per
+    slot, not the slot count) and `extra` (the key space: dictionaries and DISTINCTCOUNT value dictionaries)."""
+    h = hashlib.blake2b(extra, digest_size=8)
+    for k, t in views:
+        w = t.numel() if k == L.PA_ACC_DOCS_U64 else t.numel() // max(1, num_slots)
+        h.update(np.array([k, w, t.element_size()], dtype=np.int64).tobytes())
+    return int.from_bytes(h.digest(), "little") & ((1 << 62) - 1)
+
+
+def merge_hashed_sections(views, num_slots, group=None, layout_extra=b""):
     """Device-side merge of hashed key spaces across ranks (GroupByCombineOperator semantics, value-keyed: a packed key
     means the same group values on every rank once parallel.table_layout agreed the dictionaries, but sits in a
     different slot of each rank's table). views: [(section kind, 1-D tensor)] of ONE rank's accumulator block, the
     per-key sections holding num_slots rows each (row width = elements / num_slots) plus the PA_ACC_DOCS_U64 counters.
 
-    Every rank: compact its occupied slots (count > 0) into byte rows, all-gather them over the collective backend
-    (RCCL on GPUs), then merge by packed key on its own device — torch.unique over the keys and one scatter-reduce per
-    section (SUM for counts/sums, MIN, MAX for maxima, HLL registers and DISTINCTCOUNT presence) — and write the merged
-    groups back into the block: slots [0, groups) in ascending key order, every other slot empty. pa_query_fetch reads
-    slots by count and key, not by position, so the executor's own fetch then returns the merged result on every rank.
-    Raises when the merged groups do not fit the table."""
+    The key space is split across ranks by a hash of the packed key (key_owner): every rank compacts its occupied slots
+    (count > 0) into byte rows, sends each row to the rank that owns its key (one all-to-all over the collective
+    backend: RCCL on GPUs, so no rank ever holds the whole union), and merges the rows it receives by packed key on its
+    own device — torch.unique over the keys and one scatter-reduce per section (SUM for counts/sums, MIN, MAX for
+    maxima, HLL registers and DISTINCTCOUNT presence). The merged share goes back into the block: slots [0, groups) in
+    ascending key order, every other slot empty, so the executor's own fetch returns this rank's share. The shares are
+    disjoint and together are the merged result: each rank's fetch is one partial DataTable of disjoint groups, which
+    the broker's reduce concatenates (numDocsScanned and the other counters stay per rank: the broker sums them).
+
+    Before any exchange the ranks agree on the row layout (row_layout_fingerprint, one all-reduce: mismatched widths
+    would hand the all-to-all rows of different sizes), and after the merge on whether every share fit its table
+    (tables sized from parallel.table_layout's agreed key bound hold twice the largest rank's keys, and a share is
+    ~1/world of the union); every rank raises together otherwise. Returns this rank's merged group count."""
     kinds = [k for k, _ in views]
     if L.PA_ACC_KEYS_I64 not in kinds or L.PA_ACC_COUNT_U64 not in kinds:
         raise L.PinotAmdError("merge_hashed_sections: the block has no key or count section")
-    docs = [t for k, t in views if k == L.PA_ACC_DOCS_U64]
     per_key = [(k, t) for k, t in views if k != L.PA_ACC_DOCS_U64]
-    for t in docs:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     count = dict(per_key)[L.PA_ACC_COUNT_U64]
     dev = count.device
+    check_same_key_space(row_layout_fingerprint(views, num_slots, layout_extra), dev, group=group,
+                         what="hashed merge: ranks hold different accumulator row layouts or key spaces")
+    world = dist.get_world_size(group)
     occ = torch.nonzero(count.view(num_slots) > 0).flatten()
     m = int(occ.numel())
     # one byte row per occupied slot: every per-key section's row, concatenated
@@ -110,17 +123,17 @@ def merge_hashed_sections(views, num_slots, group=None):
         parts.append(b)
     local = torch.cat(parts, dim=1) if parts else torch.empty(m, 0, dtype=torch.uint8, device=dev)
     rb = local.shape[1]
-    world = dist.get_world_size(group)
-    sizes = torch.tensor([m], dtype=torch.int64, device=dev)
-    all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
-    dist.all_gather(all_sizes, sizes, group=group)
-    ns = [int(s.item()) for s in all_sizes]
-    mx = max(ns)
-    padded = torch.zeros(mx, rb, dtype=torch.uint8, device=dev)
-    padded[:m] = local
-    gathered = [torch.empty_like(padded) for _ in range(world)]
-    dist.all_gather(gathered, padded, group=group)
-    rows = torch.cat([g[:n] for g, n in zip(gathered, ns)], dim=0)
+    keys_local = dict(per_key)[L.PA_ACC_KEYS_I64].view(num_slots)[occ]
+    # rows grouped by owner rank, then one all-to-all of the row counts and one of the rows
+    owner = key_owner(keys_local, world)
+    order = torch.argsort(owner, stable=True)
+    local = local[order]
+    send_n = torch.bincount(owner, minlength=world).to(torch.int64)
+    recv_n = torch.empty_like(send_n)
+    dist.all_to_all_single(recv_n, send_n, group=group)
+    sn, rn = send_n.tolist(), recv_n.tolist()
+    rows = torch.empty(sum(rn), rb, dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(rows, local.contiguous(), output_split_sizes=rn, input_split_sizes=sn, group=group)
     # unpack per section, merge by packed key
     cols, o = {}, 0
     for k, dt, w, nb in layout:
@@ -129,8 +142,12 @@ def merge_hashed_sections(views, num_slots, group=None):
     keys = cols[L.PA_ACC_KEYS_I64][:, 0]
     uniq, inv = torch.unique(keys, sorted=True, return_inverse=True)
     u = int(uniq.numel())
-    if u > num_slots:
-        raise L.PinotAmdError("merged groups (%d) exceed the hashed table's %d slots" % (u, num_slots))
+    # every rank learns whether some share overflowed its table before any rank rewrites its block
+    flag = torch.tensor([u - num_slots], dtype=torch.int64, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    if int(flag.item()) > 0:
+        raise L.PinotAmdError("hashed merge: a rank's share of the merged groups exceeds its table by %d slots (size "
+                              "the tables with parallel.table_layout's hash_keys_bound)" % int(flag.item()))
     for k, t in per_key:
         w = t.numel() // num_slots
         out = t.view(num_slots, w)
@@ -148,8 +165,8 @@ def merge_hashed_sections(views, num_slots, group=None):
 class HashedAccumulators:
     """The hashed-key-space counterpart of DistributedAccumulators: moves an executor's accumulator block into a
     torch-owned device buffer (construct it BEFORE executing the query: the block is relocated, not copied), and
-    merge() runs merge_hashed_sections over it on every rank, after which executor.fetch() returns the merged groups
-    on every rank."""
+    merge() runs merge_hashed_sections over it on every rank, after which executor.fetch() returns this rank's share
+    of the merged groups (disjoint across ranks)."""
 
     def __init__(self, executor, device):
         if not getattr(executor, "hashed", False):
@@ -162,6 +179,7 @@ class HashedAccumulators:
         L.check(lib.pa_query_set_accumulator_buffer(executor.handle, base, nbytes), "set_accumulator_buffer")
         executor._acc_owner = self.buf  # the library reads and writes this block for the executor's lifetime
         self.num_slots = int(executor.num_keys)
+        self.key_space = key_space_bytes(executor)
         self.views = []
         for kind, ptr, n in executor.sections():
             off = ptr - self.buf.data_ptr()
@@ -170,7 +188,7 @@ class HashedAccumulators:
             self.views.append((kind, self.buf[off:off + n * es].view(dt)))
 
     def merge(self, group=None):
-        return merge_hashed_sections(self.views, self.num_slots, group=group)
+        return merge_hashed_sections(self.views, self.num_slots, group=group, layout_extra=self.key_space)
 
 
 def section_runs(sections):
@@ -214,81 +232,121 @@ def wide_sum_columns_local(query, segments):
     return out
 
 
+def hash_keys_bound_local(query, segments):
+    """The hashed key space's key bound of these segments (pa_capi.hip plan_key_space): every doc a key, or twice the
+    values of a multi-value group-by column."""
+    b = 0
+    for s in segments:
+        n = s.num_docs
+        for name in query.group_by:
+            c = s.column(name)
+            if not c.single_value:
+                n = max(n, int(c.total_num_values)) * 2
+        b += n
+    return b
+
+
+@dataclass
+class TableLayout:
+    """What the ranks of one multi-GPU query agree on before building their executors (table_layout)."""
+    dicts: dict = field(default_factory=dict)        # group-by column -> table-wide dictionary (sorted unique values)
+    wide: list = field(default_factory=list)         # SUM columns that keep the 64-bit accumulator on every rank
+    value_dicts: dict = field(default_factory=dict)  # DISTINCTCOUNT column -> table-wide value dictionary
+    hash_keys_bound: int = 0                         # the largest rank's hashed key bound (equal tables everywhere)
+
+    def executor_kwargs(self):
+        """Keyword arguments of GpuQueryExecutor that make every rank's accumulator block line up."""
+        return dict(table_dicts=self.dicts, wide_sum_columns=self.wide, value_dicts=self.value_dicts,
+                    hash_keys_bound=self.hash_keys_bound)
+
+
+from .query import DISTINCT_SET_FUNCTIONS as DISTINCT_FUNCTIONS  # noqa: E402
+
+
 def table_layout(query, segments, group=None):
     """Everything the ranks of one multi-GPU query must agree on before building their executors, in one all-gather:
     the table-wide dictionary of every dictionary-encoded group-by column (the union over all ranks' segments: the
-    value-keyed combine of GroupByCombineOperator needs the same key id for the same value on every GPU) and the SUM
-    columns that need the wide accumulator on some rank. Pass both to GpuQueryExecutor(table_dicts=...,
-    wide_sum_columns=...) on every rank."""
-    local = {"dicts": {}, "wide": sorted(wide_sum_columns_local(query, segments))}
+    value-keyed combine of GroupByCombineOperator needs the same key id for the same value on every GPU), the SUM
+    columns that need the wide accumulator on some rank, the table-wide value dictionary of every DISTINCTCOUNT column
+    (presence byte j must mean the same value on every rank before the uint8-MAX reduce ORs them) and the largest
+    rank's hashed key bound (every rank's hashed table then has the same slots). Returns a TableLayout; build every
+    rank's executor with GpuQueryExecutor(..., **layout.executor_kwargs())."""
+    local = {"dicts": {}, "vals": {}, "wide": sorted(wide_sum_columns_local(query, segments)),
+             "hb": hash_keys_bound_local(query, segments)}
     for name in query.group_by:
         ds = [s.column(name).dictionary for s in segments if s.column(name).has_dictionary]
         if ds:
             local["dicts"][name] = np.unique(np.concatenate(ds))
+    for a in query.aggregations:
+        if a.function in DISTINCT_FUNCTIONS and a.column not in local["vals"]:
+            ds = [s.column(a.column).dictionary for s in segments if s.column(a.column).has_dictionary]
+            if ds:
+                local["vals"][a.column] = np.unique(np.concatenate(ds))
     world = dist.get_world_size(group)
     gathered = [None] * world
     dist.all_gather_object(gathered, local, group=group)
-    dicts = {}
+    out = TableLayout()
     for name in query.group_by:
         parts = [g["dicts"][name] for g in gathered if name in g["dicts"]]
         if parts:
-            dicts[name] = np.unique(np.concatenate(parts))
-    wide = sorted(set().union(*[set(g["wide"]) for g in gathered]))
-    return dicts, wide
-
-
-def table_dictionaries(query, segments, group=None):
-    """Table-wide dictionaries of the query's dictionary-encoded group-by columns, agreed across ranks: the union of
-    every rank's segment dictionaries (the value-keyed combine of GroupByCombineOperator needs the same key id for
-    the same value on every GPU before accumulators can be reduced element-wise). Pass the result to
-    GpuQueryExecutor(table_dicts=...) on every rank."""
-    local = {}
-    for name in query.group_by:
-        ds = [s.column(name).dictionary for s in segments if s.column(name).has_dictionary]
-        if ds:
-            local[name] = np.unique(np.concatenate(ds))
-    world = dist.get_world_size(group)
-    gathered = [None] * world
-    dist.all_gather_object(gathered, local, group=group)
-    out = {}
-    for name in query.group_by:
-        parts = [g[name] for g in gathered if name in g]
-        if parts:
-            out[name] = np.unique(np.concatenate(parts))
+            out.dicts[name] = np.unique(np.concatenate(parts))
+    for name in sorted(set().union(*[set(g["vals"]) for g in gathered])):
+        out.value_dicts[name] = np.unique(np.concatenate([g["vals"][name] for g in gathered if name in g["vals"]]))
+    out.wide = sorted(set().union(*[set(g["wide"]) for g in gathered]))
+    out.hash_keys_bound = max(int(g["hb"]) for g in gathered)
     return out
 
 
+def table_dictionaries(query, segments, group=None):
+    """Table-wide dictionaries of the query's dictionary-encoded group-by columns, agreed across ranks (table_layout's
+    first half, for callers that need only the key space)."""
+    return table_layout(query, segments, group=group).dicts
+
+
+def _array_bytes(a):
+    a = np.asarray(a)
+    if a.dtype.kind in "USO":
+        return "\x00".join(map(str, a.tolist())).encode()
+    return np.ascontiguousarray(a).tobytes()
+
+
+def key_space_bytes(executor):
+    """Byte image of an executor's key space: every group-by dictionary (or <raw>) and every DISTINCTCOUNT value
+    dictionary, in a fixed order."""
+    parts = []
+    for gd in executor.global_dicts:
+        parts.append(b"<raw>" if gd is None else _array_bytes(gd))
+        parts.append(b"|")
+    for i in sorted(getattr(executor, "value_dicts", {}) or {}):
+        parts.append(b"V%d:" % i + _array_bytes(executor.value_dicts[i]) + b"|")
+    return b"".join(parts)
+
+
 def key_space_fingerprint(executor):
-    """62-bit digest of everything an element-wise cross-GPU reduce relies on: the table-wide key space (key count +
-    every group-by dictionary's values), whether it is hashed, and the accumulator block layout (every section's kind
-    and element count, the block size) — a SUM over INT on one rank and over values beyond int32 on another would
-    otherwise hand RCCL collectives of different lengths."""
+    """62-bit digest of everything an element-wise cross-GPU reduce relies on: the table-wide key space (key count,
+    every group-by dictionary's values and every DISTINCTCOUNT value dictionary), whether it is hashed, and the
+    accumulator block layout (every section's kind and element count, the block size) — a SUM over INT on one rank and
+    over values beyond int32 on another would otherwise hand RCCL collectives of different lengths, and presence bytes
+    over different value dictionaries would OR unrelated values."""
     lib = L.lib()
     h = hashlib.blake2b(np.int64(executor.num_keys).tobytes(), digest_size=8)
     h.update(b"hashed" if getattr(executor, "hashed", False) else b"direct")
     h.update(np.int64(lib.pa_query_accumulator_bytes(executor.handle)).tobytes())
     for kind, _, n in executor.sections():
         h.update(np.array([kind, n], dtype=np.int64).tobytes())
-    for gd in executor.global_dicts:
-        if gd is None:
-            h.update(b"<raw>")
-        elif np.asarray(gd).dtype.kind in "USO":
-            h.update("\x00".join(map(str, gd)).encode())
-        else:
-            h.update(np.ascontiguousarray(gd).tobytes())
-        h.update(b"|")
+    h.update(key_space_bytes(executor))
     return int.from_bytes(h.digest(), "little") & ((1 << 62) - 1)
 
 
-def check_same_key_space(fingerprint, device, group=None):
+def check_same_key_space(fingerprint, device, group=None, what=None):
     """Raises on EVERY rank unless all ranks hold the same key space and accumulator layout (element-wise section
     reduces would hang or be silently wrong). A rank that cannot take part passes fingerprint -1: the collective still
     runs everywhere, so no rank is left blocked in it."""
     t = torch.tensor([fingerprint, -fingerprint], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     if int(t[0]) != fingerprint or -int(t[1]) != fingerprint or fingerprint < 0:
-        raise L.PinotAmdError("ranks hold different group-key spaces or accumulator layouts (or a hashed key space): "
-                              "build the executors with parallel.table_layout(...)")
+        raise L.PinotAmdError(what or "ranks hold different group-key spaces or accumulator layouts (or a hashed key "
+                              "space): build the executors with parallel.table_layout(...).executor_kwargs()")
 
 
 class DistributedAccumulators:
@@ -301,7 +359,7 @@ class DistributedAccumulators:
             # the collective first, on every rank (a hashed rank joins with -1 and every rank then raises)
             check_same_key_space(-1 if hashed else key_space_fingerprint(executor), device)
         if hashed:
-            raise L.PinotAmdError("hashed key space: merge with merge_results_across_ranks (slots differ per GPU)")
+            raise L.PinotAmdError("hashed key space: merge with HashedAccumulators (slots differ per GPU)")
         lib = L.lib()
         nbytes = int(lib.pa_query_accumulator_bytes(executor.handle))
         self.buf = torch.zeros(nbytes + 512, dtype=torch.uint8, device=device)

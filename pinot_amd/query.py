@@ -8,7 +8,7 @@ filter: AND / OR / NOT / ( ) over  col = v | col != v | col <> v | col < v | col
         col BETWEEN a AND b | col IN (...) | col NOT IN (...)
 Comparison predicates become RangePredicate exactly as the reference's RequestContextUtils does
 (pinot-common/.../request/context/RequestContextUtils.java: >, >=, <, <=, BETWEEN -> RANGE).
-Aggregations: COUNT(*), SUM, MIN, MAX, AVG, MINMAXRANGE, DISTINCTCOUNT, DISTINCTCOUNTHLL(col[, log2m]) and their *MV
+Aggregations: COUNT(*), SUM, MIN, MAX, AVG, MINMAXRANGE, DISTINCTCOUNT, DISTINCTSUM, DISTINCTAVG, DISTINCTCOUNTHLL(col[, log2m]) and their *MV
 forms.
 """
 import re
@@ -76,8 +76,13 @@ PREDICATES = (EqPredicate, NotEqPredicate, InPredicate, NotInPredicate, RangePre
 # AggregationFunctionType names the hot path runs: single-value functions and their multi-value (*MV) forms, which
 # aggregate every value of a multi-value column (SumMVAggregationFunction, CountMVAggregationFunction, ...)
 SUPPORTED_FUNCTIONS = ("SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNTHLL", "MINMAXRANGE", "DISTINCTCOUNT",
+                       "DISTINCTSUM", "DISTINCTAVG",
                        "COUNTMV", "SUMMV", "MINMV", "MAXMV", "AVGMV", "DISTINCTCOUNTHLLMV", "MINMAXRANGEMV",
-                       "DISTINCTCOUNTMV")
+                       "DISTINCTCOUNTMV", "DISTINCTSUMMV", "DISTINCTAVGMV")
+# BaseDistinctAggregateAggregationFunction subclasses: the intermediate result is the set of distinct values (one
+# presence accumulator on the GPU); they differ only in extractFinalResult (size / sum / average)
+DISTINCT_SET_FUNCTIONS = ("DISTINCTCOUNT", "DISTINCTSUM", "DISTINCTAVG", "DISTINCTCOUNTMV", "DISTINCTSUMMV",
+                          "DISTINCTAVGMV")
 
 
 def base_function(fn):

@@ -2,7 +2,7 @@
 
   merge_intermediate   ~ GroupByDataTableReducer / AggregationDataTableReducer merging server DataTables
                          (AggregationFunction.merge: COUNT/SUM +, MIN min, MAX max, AVG pair +, HLL addAll,
-                         MINMAXRANGE pair min/max, DISTINCTCOUNT set union)
+                         MINMAXRANGE pair min/max, DISTINCTCOUNT / DISTINCTSUM / DISTINCTAVG set union)
   server_trim          ~ IndexedTable.finish on the server (IndexedTable.java:149): with ORDER BY keep the top
                          max(limit*5, minServerGroupTrimSize) groups (GroupByUtils.getTableCapacity); without
                          ORDER BY keep `limit` groups (GroupByCombineOperator.java:63-73)
@@ -30,7 +30,7 @@ def merge_value(fn, a, b):
         return HyperLogLog(a.log2m, a.registers).add_all(b)
     if fn == "MINMAXRANGE":  # MinMaxRangePair.apply
         return MinMaxRangePair(min(a.min, b.min), max(a.max, b.max))
-    if fn == "DISTINCTCOUNT":  # BaseDistinctAggregateAggregationFunction.merge: set union
+    if fn in ("DISTINCTCOUNT", "DISTINCTSUM", "DISTINCTAVG"):  # BaseDistinctAggregateAggregationFunction.merge: union
         return set(a) | set(b)
     raise ValueError(fn)
 
@@ -45,6 +45,16 @@ def final_value(fn, v):
         return v.max - v.min
     if fn == "DISTINCTCOUNT":  # DistinctCountAggregationFunction.extractFinalResult: the set's size
         return len(v)
+    if fn in ("DISTINCTSUM", "DISTINCTAVG"):
+        # DistinctSumAggregationFunction / DistinctAvgAggregationFunction.extractFinalResult: a double sum over the set
+        # in its iteration order, divided by its size for the average (0/0 = NaN for an empty set, as in Java)
+        s = 0.0
+        for x in v:
+            s += float(x)
+        if fn == "DISTINCTSUM":
+            return s
+        return s / len(v) if len(v) else math.nan
+    return v
     return v
 
 

@@ -36,10 +36,14 @@ GROUP_BY = " GROUP BY column9 ORDER BY v1 DESC, v2 DESC LIMIT 1"
 CASES = []
 
 
-def case(source, sql, rows, delta=0.0, stats=None):
+def case(source, sql, rows, delta=0.0, stats=None, limit_reached=None):
     """stats: the testInterSegmentsResult arguments (numDocsScanned, numEntriesScannedInFilter,
-    numEntriesScannedPostFilter, numTotalDocs) the reference asserts for this case (QueriesTestUtils.java)."""
-    CASES.append({"source": source, "sql": sql, "rows": rows, "delta": delta, "stats": stats})
+    numEntriesScannedPostFilter, numTotalDocs) the reference asserts for this case (QueriesTestUtils.java).
+    rows None: the reference asserts no result table; limit_reached: its assert on isNumGroupsLimitReached()."""
+    c = {"source": source, "sql": sql, "rows": rows, "delta": delta, "stats": stats}
+    if limit_reached is not None:
+        c["limit_reached"] = limit_reached
+    CASES.append(c)
 
 
 # the four execution statistics of the aggregation test's shapes (InterSegmentAggregationSingleValueQueriesTest.java):
@@ -91,6 +95,21 @@ case(AGG + ":262-271", q, [[5977, 23825]], stats=st(0, 0))
 case(AGG + ":273-275", q + FILTER, [[1886, 4492]], stats=st(1, 49032))
 case(AGG + ":277-279", q + GROUP_BY, [[3592, 11889]], stats=st(0, 360000))
 case(AGG + ":281-283", q + FILTER + GROUP_BY, [[1324, 3197]], stats=st(1, 73548))
+# testNumGroupsLimit: only numGroupsLimitReached is asserted (no result table, no statistics); the second query runs on
+# a server whose InstancePlanMakerImplV2 has numGroupsLimit = 1000 (column1 has 6582 values per segment)
+q = "SELECT COUNT(*) FROM testTable GROUP BY column1"
+case(AGG + ":765-768", q, None, limit_reached=False)
+case(AGG + ":770-774", q + " OPTION(numGroupsLimit=1000)", None, limit_reached=True)
+q = "select DISTINCTSUM(column1) as v1, DISTINCTSUM(column3) as v2 from testTable"
+case(AGG + ":779-788", q, [[7074556592262.0, 23553878404013.0]], stats=st(0, 0))
+case(AGG + ":790-793", q + FILTER, [[2062916453604.0, 2334011146274.0]], stats=st(1, 49032))
+case(AGG + ":795-798", q + GROUP_BY, [[3745055692019.0, 12836683389098.0]], stats=st(0, 360000))
+case(AGG + ":800-803", q + FILTER + GROUP_BY, [[1397706323624.0, 1686328722268.0]], stats=st(1, 73548))
+q = "select DISTINCTAVG(column1) as v1, DISTINCTAVG(column3) as v2 from testTable"
+case(AGG + ":808-818", q, [[1074833879.1039197, 1075028681.150753]], stats=st(0, 0))
+case(AGG + ":820-824", q + FILTER, [[1101985285.0448718, 512293930.26207197]], stats=st(1, 49032))
+case(AGG + ":826-830", q + GROUP_BY, [[2142595699.0, 334963174.0]], stats=st(0, 360000))
+case(AGG + ":832-836", q + FILTER + GROUP_BY, [[2142595699.0, 334963174.0]], stats=st(1, 73548))
 
 # ---- InterSegmentGroupBySingleValueQueriesTest.groupByOrderByDataProvider
 c11 = [["", 5935285005452.0], ["P", 88832999206836.0], ["gFuH", 63202785888.0], ["o", 18105331533948.0],

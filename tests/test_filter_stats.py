@@ -45,6 +45,8 @@ def test_golden_execution_statistics(golden_spec, golden_segment):
     applyAnd chain over column1/column3 and the AndDocIdIterator/OrDocIdIterator leap-frog of column6's scan)."""
     bad = []
     for case in golden_spec["cases"]:
+        if case["stats"] is None:  # (testNumGroupsLimit asserts no statistics)
+            continue
         got = golden_stats(case, golden_segment, golden_spec["servers"], golden_spec["segments_per_server"])
         if got != case["stats"]:
             bad.append((case["source"], case["sql"][:80], got, case["stats"]))

@@ -255,8 +255,8 @@ def test_configs3_two_rank_merge_and_rccl_reduce(adanalytics):
                             device_id=torch.device("cuda", 0))
     exs = []
     try:
-        td, wide = table_layout(q, [seg0, seg1])
-        exs = [GpuQueryExecutor(q, [g], table_dicts=td, wide_sum_columns=wide) for g in (g0, g1)]
+        kw = table_layout(q, [seg0, seg1]).executor_kwargs()
+        exs = [GpuQueryExecutor(q, [g], **kw) for g in (g0, g1)]
         assert key_space_fingerprint(exs[0]) == key_space_fingerprint(exs[1])
         accs = [DistributedAccumulators(e, torch.device("cuda", 0)) for e in exs]
         for e in exs:

@@ -90,7 +90,7 @@ def test_two_rank_merge_with_table_dictionaries(sql, rccl_world1):
 ])
 def test_hashed_key_space_device_merge(sql, rccl_world1):
     """HashedAccumulators on a hashed key space (GROUP BY a raw column): the block moves into a torch buffer, the
-    RCCL merge (world size 1: all-gather of this rank's compacted rows, merge by packed key) rewrites it as groups
+    RCCL merge (world size 1: all-to-all of this rank's compacted rows to their key owners, merge by packed key) rewrites it as groups
     [0, n) in key order, and the library's own fetch of the rewritten block equals the oracle."""
     from pinot_amd.parallel import HashedAccumulators
     cols = dict(COLS, r=("LONG", 0), ri=("INT", 0))

@@ -14,16 +14,20 @@ from conftest import rows_match
 
 def _broker(query, segment, servers=2, per_server=2):
     server = server_trim(oracle.run_query(query, [segment] * per_server), query)
-    return final_result_table(merge_intermediate([server] * servers), query)
+    merged = merge_intermediate([server] * servers)
+    return final_result_table(merged, query), merged
 
 
 def test_golden_cases(golden_spec, golden_segment):
     failures = []
     for case in golden_spec["cases"]:
         q = parse_sql(case["sql"])
-        got = _broker(q, golden_segment)
-        if not rows_match(got, case["rows"], case["delta"]):
+        got, merged = _broker(q, golden_segment)
+        if case["rows"] is not None and not rows_match(got, case["rows"], case["delta"]):
             failures.append((case["source"], case["sql"], got[:5], case["rows"][:5]))
+        # BrokerResponseNative.isNumGroupsLimitReached: OR over the servers' DataTable metadata
+        if "limit_reached" in case and merged.num_groups_limit_reached != case["limit_reached"]:
+            failures.append((case["source"], "numGroupsLimitReached", merged.num_groups_limit_reached))
     assert not failures, "\n".join(map(str, failures))
 
 

@@ -112,50 +112,6 @@ def test_shard_segments_partition(n, world):
     assert max(map(len, parts)) - min(map(len, parts)) <= 1
 
 
-class _FakeExecutor:
-    """Stands in for a GpuQueryExecutor on CPU: fetch() returns this rank's partial groups."""
-
-    def __init__(self, rank):
-        from pinot_amd.engine import IntermediateResult
-        from pinot_amd.query import Aggregation
-        self.res = IntermediateResult([Aggregation("COUNT"), Aggregation("SUM", "m"), Aggregation("MAX", "m")], ["k"])
-        rng = np.random.default_rng(rank)
-        for k in rng.choice(50, size=30, replace=False).tolist():
-            self.res.groups[(k,)] = [int(rng.integers(1, 10)), float(rng.integers(0, 100)), float(rng.integers(0, 9))]
-        self.res.num_docs_scanned = 100 + rank
-
-    def fetch(self):
-        return self.res
-
-
-def _merge_worker(rank, world, port, out):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    from pinot_amd.parallel import merge_results_across_ranks
-    merged = merge_results_across_ranks(_FakeExecutor(rank), dst=0)
-    if rank == 0:
-        out[0] = (merged.groups, merged.num_docs_scanned)
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-def test_gloo_key_based_merge_for_hashed_key_spaces():
-    world = 2
-    mgr = mp.Manager()
-    out = mgr.dict()
-    mp.spawn(_merge_worker, args=(world, _free_port(), out), nprocs=world, join=True)
-    groups, docs = out[0]
-    exp = {}
-    for r in range(world):
-        for k, (c, sm, mx) in _FakeExecutor(r).res.groups.items():
-            if k in exp:
-                exp[k] = [exp[k][0] + c, exp[k][1] + sm, max(exp[k][2], mx)]
-            else:
-                exp[k] = [c, sm, mx]
-    assert groups == exp
-    assert docs == 201
-
-
 def _block_layout(secs):
     """pa_capi.hip accumulator block: sections at 256-byte aligned offsets (gaps zero, as pa_query_reset leaves them)."""
     offs, total = [], 0
@@ -308,8 +264,8 @@ def _layout_worker(rank, world, port, out):
                                         "n": rng.integers(0, 9, size=300).astype(np.int64),
                                         "i": rng.integers(0, 9, size=300).astype(np.int32)},
                          {"k": "INT", "m": "LONG", "n": "LONG", "i": "INT"})
-    dicts, wide = table_layout(q, [seg])
-    out[rank] = (sorted(dicts), list(wide))
+    lay = table_layout(q, [seg])
+    out[rank] = (sorted(lay.dicts), list(lay.wide))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -363,43 +319,47 @@ def _hashed_partial(rank):
     return secs, groups
 
 
-def _hashed_worker(rank, world, port, out):
+def _hashed_worker(rank, world, port, out, partial_fn=None, extra=b""):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from pinot_amd.parallel import merge_hashed_sections
-    secs, _ = _hashed_partial(rank)
+    secs, _ = (partial_fn or _hashed_partial)(rank)
     views = [(k, torch.from_numpy(np.ascontiguousarray(a)).to(SECTION_DTYPE[k])) for k, a in secs]
-    u = merge_hashed_sections(views, NS)
-    out[rank] = (u, [t.numpy().copy() for _, t in views])
+    try:
+        u = merge_hashed_sections(views, NS, layout_extra=extra if isinstance(extra, bytes) else extra[rank])
+        out[rank] = (u, [t.numpy().copy() for _, t in views])
+    except L.PinotAmdError as e:
+        out[rank] = ("raised", str(e))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gloo_device_side_merge_of_hashed_key_spaces():
-    """parallel.merge_hashed_sections (the RCCL path of hashed key spaces: all-gather of compacted rows + merge by
-    packed key) reproduces the key-based merge of GroupByCombineOperator on every rank, in the block layout the
-    library's fetch reads (groups in ascending key order, every other slot empty)."""
-    world = 2
-    mgr = mp.Manager()
-    out = mgr.dict()
-    mp.spawn(_hashed_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+def _expected_union(partials):
     exp = {}
-    for r in range(world):
-        for k, (c, v, ds, mn, mx, h, p) in _hashed_partial(r)[1].items():
+    for groups in partials:
+        for k, (c, v, ds, mn, mx, h, p) in groups.items():
             if k in exp:
                 e = exp[k]
                 exp[k] = (e[0] + c, e[1] + v, e[2] + ds, min(e[3], mn), max(e[4], mx), np.maximum(e[5], h),
                           np.maximum(e[6], p))
             else:
                 exp[k] = (c, v, ds, mn, mx, h, p)
-    ks = sorted(exp)
+    return exp
+
+
+def _check_shares(out, world, exp, docs_of):
+    """Every rank's block holds its share (the keys key_owner assigns it) in ascending key order, every other slot
+    empty; the shares are disjoint and their union is the merged result; numDocsScanned stays per rank."""
+    from pinot_amd.parallel import key_owner
+    seen = []
     for r in range(world):
         u, (count, sx2, dsum, dmin, imax, hll, pres, keys, docs) = out[r]
-        assert u == len(ks)
-        assert keys[:u].tolist() == ks and (keys[u:] == (1 << 63) - 1).all()
+        share = sorted(k for k in exp if int(key_owner(torch.tensor([k], dtype=torch.int64), world)[0]) == r)
+        assert u == len(share)
+        assert keys[:u].tolist() == share and (keys[u:] == (1 << 63) - 1).all()
         assert (count[u:] == 0).all() and (dmin[u:] == (1 << 63) - 1).all() and (imax[u:] == -(1 << 63)).all()
-        assert docs.tolist() == [2001, 0, 0, 0]
-        for i, k in enumerate(ks):
+        assert docs.tolist() == docs_of(r)
+        for i, k in enumerate(share):
             c, v, ds, mn, mx, h, p = exp[k]
             assert count[i] == c
             assert int(sx2[2 * i]) + (int(sx2[2 * i + 1]) << 32) == v
@@ -407,3 +367,118 @@ def test_gloo_device_side_merge_of_hashed_key_spaces():
             assert dmin[i] == mn and imax[i] == mx
             assert np.array_equal(hll[i << HLOG:(i + 1) << HLOG], h)
             assert np.array_equal(pres[i * 16:(i + 1) * 16], p)
+        seen += share
+    assert sorted(seen) == sorted(exp)  # disjoint + complete
+
+
+def test_gloo_device_side_merge_of_hashed_key_spaces():
+    """parallel.merge_hashed_sections (the RCCL path of hashed key spaces: rows sent to the rank owning their key by
+    one all-to-all, merged by packed key there) reproduces the key-based merge of GroupByCombineOperator across the
+    ranks' shares, in the block layout the library's fetch reads (groups in ascending key order, others empty)."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_hashed_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    exp = _expected_union([_hashed_partial(r)[1] for r in range(world)])
+    _check_shares(out, world, exp, lambda r: [1000 + r, 0, 0, 0])
+
+
+def _disjoint_partial(rank):
+    """40 groups per rank with keys no other rank holds (the case hashed key spaces exist for: high-cardinality raw
+    keys): the union (120 at world 3) is larger than one rank's table of NS slots."""
+    rng = np.random.default_rng(900 + rank)
+    keys_used = (np.arange(40, dtype=np.int64) * 7919 + rank) * (1 << 20) - (1 << 40)
+    slots = rng.choice(NS, size=40, replace=False)
+    keys = np.full(NS, (1 << 63) - 1, np.int64)
+    count = np.zeros(NS, np.int64)
+    sx2 = np.zeros(2 * NS, np.int64)
+    dsum = np.zeros(NS)
+    dmin = np.full(NS, (1 << 63) - 1, np.int64)
+    imax = np.full(NS, -(1 << 63), np.int64)
+    hll = np.zeros(NS << HLOG, np.uint8)
+    pres = np.zeros(NS * 16, np.uint8)
+    groups = {}
+    for k, s in zip(keys_used.tolist(), slots.tolist()):
+        keys[s] = k
+        count[s] = rng.integers(1, 50)
+        v = int(rng.integers(-(1 << 40), 1 << 40))
+        sx2[2 * s], sx2[2 * s + 1] = v & 0xFFFFFFFF, v >> 32
+        dsum[s] = rng.standard_normal()
+        dmin[s] = f64_order_encode(rng.standard_normal() * 100)
+        imax[s] = rng.integers(-1000, 1000)
+        hll[s << HLOG:(s + 1) << HLOG] = rng.integers(0, 20, 1 << HLOG)
+        pres[s * 16:(s + 1) * 16] = rng.integers(0, 2, 16)
+        groups[k] = (int(count[s]), v, float(dsum[s]), int(dmin[s]), int(imax[s]),
+                     hll[s << HLOG:(s + 1) << HLOG].copy(), pres[s * 16:(s + 1) * 16].copy())
+    secs = [(L.PA_ACC_COUNT_U64, count), (L.PA_ACC_SUM_I64X2, sx2), (L.PA_ACC_SUM_F64, dsum),
+            (L.PA_ACC_MIN_I64, dmin), (L.PA_ACC_MAX_I64, imax), (L.PA_ACC_HLL_U8, hll),
+            (L.PA_ACC_PRESENCE_U8, pres), (L.PA_ACC_KEYS_I64, keys),
+            (L.PA_ACC_DOCS_U64, np.array([7 * rank, 0, 0, 0], np.int64))]
+    return secs, groups
+
+
+def test_gloo_hashed_merge_of_disjoint_keys_larger_than_one_table():
+    """World size 3, every rank's keys disjoint from the others' and the union (120 groups) larger than one rank's
+    table (64 slots): the key-partitioned merge leaves each rank a share that fits, matching the single-process
+    merge (the all-gather design it replaces had to raise here)."""
+    world = 3
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_hashed_worker, args=(world, _free_port(), out, _disjoint_partial), nprocs=world, join=True)
+    exp = _expected_union([_disjoint_partial(r)[1] for r in range(world)])
+    assert len(exp) == 120 > NS
+    _check_shares(out, world, exp, lambda r: [7 * r, 0, 0, 0])
+
+
+def test_gloo_hashed_merge_refuses_mismatched_key_spaces():
+    """Ranks whose key spaces differ (e.g. DISTINCTCOUNT value dictionaries of the same size but different values)
+    all raise before any row is exchanged."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_hashed_worker, args=(world, _free_port(), out, None, [b"V0:abc|", b"V0:abd|"]), nprocs=world, join=True)
+    assert out[0][0] == "raised" and out[1][0] == "raised"
+
+
+def test_key_space_fingerprint_covers_distinct_value_dictionaries():
+    """presence byte j must mean the same value on every rank before the uint8-MAX reduce."""
+    from pinot_amd.parallel import key_space_fingerprint
+
+    class _E:
+        num_keys, global_dicts, handle = 6, [np.array([1, 2, 3])], None
+
+        def __init__(self, vd):
+            self.value_dicts = vd
+
+        def sections(self):
+            return [(L.PA_ACC_COUNT_U64, 0, 6), (L.PA_ACC_PRESENCE_U8, 0, 6 * 16)]
+    a = key_space_fingerprint(_E({1: np.array([10, 20, 30])}))
+    assert a == key_space_fingerprint(_E({1: np.array([10, 20, 30])}))
+    assert a != key_space_fingerprint(_E({1: np.array([10, 20, 31])}))  # same size, different values
+
+
+def _distinct_layout_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pinot_amd import parse_sql
+    from pinot_amd.parallel import table_layout
+    from pinot_amd.segment import create_segment
+    q = parse_sql("SELECT k, DISTINCTCOUNT(v), COUNT(*) FROM t GROUP BY k")
+    rng = np.random.default_rng(rank)
+    # disjoint, equal-sized value dictionaries: rank 0 holds 0..49, rank 1 holds 100..149
+    v = (rng.permutation(50).repeat(4) + 100 * rank).astype(np.int32)
+    seg = create_segment("s%d" % rank, {"k": rng.integers(0, 5, size=200).astype(np.int32), "v": v},
+                         {"k": "INT", "v": "INT"})
+    lay = table_layout(q, [seg])
+    out[rank] = (lay.value_dicts["v"].tolist(), lay.hash_keys_bound, lay.executor_kwargs()["value_dicts"] is lay.value_dicts)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_table_layout_agrees_on_distinct_value_dictionaries():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_distinct_layout_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    exp = list(range(50)) + list(range(100, 150))
+    assert out[0] == out[1] == (exp, 200, True)
