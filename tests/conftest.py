@@ -63,3 +63,20 @@ def pytest_runtest_setup(item):
         torch.cuda.set_device(0)
         torch.zeros(1, device="cuda")
         _TORCH_GPU.append(True)
+
+
+@pytest.fixture(scope="session")
+def query_executor_spec():
+    with open(os.path.join(GOLDEN, "query_executor.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def query_executor_segments(query_executor_spec):
+    """QueryExecutorTest's server: 2 segments of simpleData200001.avro + 2 empty segments (test_empty_data.json)."""
+    from pinot_amd.segment import create_segment
+    schema = query_executor_spec["schema"]
+    data = np.load(os.path.join(GOLDEN, "simple_data.npz"))
+    simple = create_segment("testTable_0", {k: data[k] for k in data.files}, schema)
+    empty = create_segment("testTable_2", {k: np.zeros(0, np.int32) for k in schema}, schema)
+    return [simple if s == "simple" else empty for s in query_executor_spec["segments"]]

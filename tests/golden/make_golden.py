@@ -4,6 +4,8 @@ Run here (needs /root/reference; the GPU box never runs this):  python tests/gol
 
   test_data_sv.npz   the 11 columns BaseSingleValueQueriesTest.java:95-104 selects from
                      pinot-core/src/test/resources/data/test_data-sv.avro (30000 rows, no nulls)
+  simple_data.npz    dim0/dim1/met of pinot-core/src/test/resources/data/simpleData200001.avro (200001 rows)
+  query_executor.json  QueryExecutorTest.java's server-level aggregation results on it
   sv_queries.json    queries + expected broker ResultTables transcribed from
                      pinot-core/src/test/java/org/apache/pinot/queries/InterSegmentAggregationSingleValueQueriesTest.java
                      and InterSegmentGroupBySingleValueQueriesTest.java (source file:line in every case).
@@ -204,7 +206,27 @@ case(GBY + ":269-277", "SELECT column12, DISTINCTCOUNT(column11) FROM testTable 
       ["MaztCmmxxgguBUxPti", 5], ["KrNxpdycSiwoRohEiTIlLqDHnx", 5], ["HEuxNvH", 5]], stats=[120000, 0, 240000, 120000])
 
 
+# ---- QueryExecutorTest (server level: ServerQueryExecutorV1Impl over 2 segments of simpleData200001.avro + 2 empty
+# segments from test_empty_data.json; the asserted value is the AggregationResultsBlock's intermediate result)
+QE = "pinot-core/src/test/java/org/apache/pinot/core/query/executor/QueryExecutorTest.java"
+SIMPLE_AVRO = "/root/reference/pinot-core/src/test/resources/data/simpleData200001.avro"
+SIMPLE_SCHEMA = {"dim0": "INT", "dim1": "INT", "met": "INT"}  # SegmentTestUtils.extractSchemaFromAvroWithoutTime
+QE_CASES = [
+    {"source": QE + ":152-160", "sql": "SELECT COUNT(*) FROM testTable_OFFLINE", "value": 400002},
+    {"source": QE + ":162-170", "sql": "SELECT SUM(met) FROM testTable_OFFLINE", "value": 40000200000.0},
+    {"source": QE + ":172-180", "sql": "SELECT MAX(met) FROM testTable_OFFLINE", "value": 200000.0},
+    {"source": QE + ":182-190", "sql": "SELECT MIN(met) FROM testTable_OFFLINE", "value": 0.0},
+]
+
+
 def main():
+    _, srecs = avro_min.read_avro(SIMPLE_AVRO)
+    np.savez_compressed(os.path.join(HERE, "simple_data.npz"),
+                        **{c: np.array([r[c] for r in srecs], dtype=np.int32) for c in SIMPLE_SCHEMA})
+    with open(os.path.join(HERE, "query_executor.json"), "w") as f:
+        # the server's segments: 2 x simpleData200001 + 2 empty (QueryExecutorTest.java:76-77)
+        json.dump({"schema": SIMPLE_SCHEMA, "segments": ["simple", "simple", "empty", "empty"], "cases": QE_CASES},
+                  f, indent=1)
     _, recs = avro_min.read_avro(AVRO)
     cols = {}
     for name, dt in SCHEMA.items():

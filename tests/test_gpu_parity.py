@@ -103,6 +103,22 @@ def test_golden_cases_gpu(golden_spec, golden_segment):
     assert not failures, failures
 
 
+def test_query_executor_cases_gpu(query_executor_spec, query_executor_segments):
+    """QueryExecutorTest.java:152-190 on the GPU: one server of 2 x simpleData200001 + 2 empty segments; the
+    AggregationResultsBlock value (COUNT long, SUM/MIN/MAX double) and numDocsScanned."""
+    gs = [GpuSegment(s) for s in query_executor_segments]
+    try:
+        for case in query_executor_spec["cases"]:
+            ex = GpuQueryExecutor(parse_sql(case["sql"]), gs)
+            res = ex.run()
+            ex.close()
+            assert res.row[0] == case["value"] and type(res.row[0]) is type(case["value"]), (case["source"], res.row)
+            assert res.num_docs_scanned == 400002 and res.num_total_docs == 400002
+    finally:
+        for g in gs:
+            g.close()
+
+
 # ------------------------------------------------------------------ randomized parity vs the oracle
 COLS = {"d1": ("INT", 50), "d2": ("STRING", 20), "d3": ("LONG", 3000), "m1": ("INT", 500), "m2": ("LONG", 10000),
         "f1": ("DOUBLE", 200), "f2": ("FLOAT", 300), "r1": ("DOUBLE", 0), "r2": ("INT", 0), "r3": ("LONG", 0)}

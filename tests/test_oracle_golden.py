@@ -59,3 +59,11 @@ def test_num_bits_per_value():
     """PinotDataBitSet.getNumBitsPerValue javadoc examples (PinotDataBitSet.java:49-56)."""
     from pinot_amd.segment import num_bits_per_value
     assert [num_bits_per_value(v) for v in (0, 1, 2, 9, 113)] == [1, 1, 2, 4, 7]
+
+
+def test_query_executor_cases(query_executor_spec, query_executor_segments):
+    """QueryExecutorTest.java:152-190: the server-level AggregationResultsBlock value over 2 x simpleData200001 + 2
+    empty segments (COUNT long, SUM/MIN/MAX double)."""
+    for case in query_executor_spec["cases"]:
+        res = oracle.run_query(parse_sql(case["sql"]), query_executor_segments)
+        assert res.row[0] == case["value"] and type(res.row[0]) is type(case["value"]), (case["source"], res.row)
