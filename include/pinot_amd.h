@@ -306,7 +306,9 @@ int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs
                    uint64_t* num_tiles);
 
 /* The kernel plan chosen by pa_query_prepare: accumulator strategy (0 = LDS-privatised, 1 = global atomics,
- * 2 = partitioned: records partitioned by key range, then aggregated per partition in LDS), 64-doc
+ * 2 = partitioned: records partitioned by key range, then aggregated per partition in LDS; aggregation-only queries
+ * 4..7 = per-lane register accumulators: 4 any column kinds, 5 COUNT only, 6 raw columns only, 7 dictionary
+ * columns only), 64-doc
  * steps per wave tile, DMA instructions per tile, tile images per wave, workgroups per CU, grid, LDS bytes. */
 /* Filter literals evaluated on whole staged tiles (the rest only on the docs those matched). */
 int32_t pa_query_num_eager_literals(const pa_query* q);

@@ -720,14 +720,23 @@ int plan_slots(pa_query* q, Prep& P) {
       return fail(PA_EINVAL, "DISTINCTCOUNT needs the table-wide value count (1..2^31-1)");
   }
   // Post-filter columns (group-by keys, aggregated values) are staged with the filter columns when the filter lets
-  // more than kLazyPost docs per wave tile through; below that each surviving doc reads them from HBM.
-  const double kLazyPost = 0.25;
-  P.stage_all = !P.has_filter || (s.flags & PA_QF_STAGE_ALL);
-  P.stage_post = P.stage_all || P.post_density > kLazyPost;
+  // enough docs per wave tile through; below that each surviving doc reads them from HBM. Staging costs the columns'
+  // whole tile (256 * nb bytes per nb-bit column); a lazy doc costs about one 64-byte sector per column, and its reads
+  // sit on the doc's dependency chain, so lazy is chosen below half the byte break-even: 2 * sum(nb) docs per tile (and
+  // never below the old fixed floor of a quarter doc).
   P.slot_post.assign(kMaxSlots, 0);
   for (int j = 0; j < s.num_group_by; ++j) P.slot_post[P.gb_slot[j]] = 1;
   for (int a = 0; a < s.num_aggs; ++a)
     if (s.aggs[a].type != PA_AGG_COUNT) P.slot_post[P.agg_slot[a]] = 1;
+  int post_bits = 0;
+  for (int sl = 0; sl < kMaxSlots; ++sl) {
+    if (!P.slot_post[sl] || sl >= (int)q->slot_cols.size() || !q->nseg) continue;
+    auto it = q->segs[0]->cols.find(q->slot_cols[sl]);
+    if (it != q->segs[0]->cols.end() && it->second->kind == COL_SV_DICT) post_bits += it->second->nbits;
+  }
+  const double kLazyPost = std::max(0.25, 2.0 * post_bits);
+  P.stage_all = !P.has_filter || (s.flags & PA_QF_STAGE_ALL);
+  P.stage_post = P.stage_all || P.post_density > kLazyPost;
   return PA_OK;
 }
 
@@ -1554,8 +1563,32 @@ int plan_kernels(pa_query* q, Prep& P, TilePlan& plan, TilePlan& count_plan) {
     lane_acc = t == PA_AGG_COUNT || t == PA_AGG_SUM || t == PA_AGG_MIN || t == PA_AGG_MAX;
   }
   if (lane_acc) {
-    plan = plan_pick(STRAT_LANE, 0);
-    if (plan.score >= 0) q->strategy = STRAT_LANE;
+    // lane-major tiles run the kernel variant of the aggregation columns' kind (raw / dictionary / none) when every
+    // bound segment agrees on it
+    int lane_strat = STRAT_LANE;
+    if (lm) {
+      bool any_raw = false, any_dict = false, other = false;
+      for (int a = 0; a < s.num_aggs; ++a) {
+        if (s.aggs[a].type == PA_AGG_COUNT) continue;
+        for (int si = 0; si < q->nseg; ++si) {
+          auto it = q->segs[si]->cols.find(s.aggs[a].column_id);
+          const int k = it == q->segs[si]->cols.end() ? COL_NONE : it->second->kind;
+          any_raw |= k == COL_SV_RAW;
+          any_dict |= k == COL_SV_DICT;
+          other |= k != COL_SV_RAW && k != COL_SV_DICT;
+        }
+      }
+      if (!other && !any_raw && !any_dict) lane_strat = STRAT_LANE_CNT;
+      else if (!other && any_raw && !any_dict) lane_strat = STRAT_LANE_RAW;
+      else if (!other && any_dict && !any_raw) lane_strat = STRAT_LANE_DICT;
+    }
+    // the lane accumulators' LDS slots (kLaneAccBytes per thread and aggregation; none for COUNT only)
+    const size_t lane_b = lane_strat == STRAT_LANE_CNT ? 0 : (size_t)s.num_aggs * kWGSize * kLaneAccBytes;
+    plan = plan_pick(lane_strat, lane_b);
+    if (plan.score >= 0) {
+      q->strategy = lane_strat;
+      P.lds_acc = lane_b;
+    }
   }
   if (q->strategy == STRAT_GLOBAL && !(s.flags & PA_QF_FORCE_GLOBAL) && !q->limit_mode && !q->hashed &&
       P.lds_acc <= 64 * 1024 && (P.dense || (s.flags & PA_QF_FORCE_LDS))) {
@@ -1656,7 +1689,7 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
   h.has_mv = q->has_mv;
   h.xcd_major = P.dense ? 1 : 0;
   h.lds_count_off = 0;
-  h.lds_acc_bytes = q->strategy == STRAT_LDS ? (uint32_t)P.lds_acc : 0;
+  h.lds_acc_bytes = (q->strategy == STRAT_LDS || is_lane(q->strategy)) ? (uint32_t)P.lds_acc : 0;
   if (!q->partitioned) {
     h.hll_agg = -1;
     h.pv = 0;

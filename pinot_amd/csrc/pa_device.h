@@ -36,8 +36,16 @@ enum ColKind : int32_t { COL_NONE = 0, COL_SV_DICT = 1, COL_SV_RAW = 2, COL_MV_D
 // STRAT_LANE: aggregation-only queries (no GROUP BY) over single-value columns: every lane keeps its own running
 // COUNT/SUM/MIN/MAX in registers for the whole kernel and the wave reduces them once at the end (no per-step reduction,
 // no LDS or global atomics per doc).
-enum Strategy : int32_t { STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PEMIT = 2, STRAT_PCOUNT = 3, STRAT_LANE = 4 };
-constexpr int kLaneAggs = 4;  // STRAT_LANE: at most this many non-COUNT aggregations
+// STRAT_LANE_CNT / _RAW / _DICT: the lane-major STRAT_LANE kernel compiled for one kind of aggregation column only (no
+// value aggregation / raw columns only / dictionary columns only), so each variant holds just its own paths (the
+// all-kinds kernel spills); STRAT_LANE runs mixed sets and step-major tiles.
+enum Strategy : int32_t {
+  STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PEMIT = 2, STRAT_PCOUNT = 3, STRAT_LANE = 4,
+  STRAT_LANE_CNT = 5, STRAT_LANE_RAW = 6, STRAT_LANE_DICT = 7
+};
+__host__ __device__ constexpr bool is_lane(int s) { return s >= STRAT_LANE && s <= STRAT_LANE_DICT; }
+constexpr int kLaneAggs = 4;  // STRAT_LANE: at most this many aggregations (COUNT included)
+constexpr int kLaneAccBytes = 20;  // STRAT_LANE: LDS bytes per thread and aggregation (int64 pair + a dictId)
 // The emit pass's kernel variant (launch code): the V record format (-1: no V stream) and whether there is an H stream
 // are template parameters, so each variant's record loop is straight-line code (no per-record format branches).
 // `big`: 16-wave workgroups (the partition bins and their state are per workgroup, so sharing them among more waves

@@ -1396,23 +1396,46 @@ __device__ __forceinline__ uint32_t admitted_docs(const DevQuery* __restrict__ q
 // MIN / MAX over a sorted dictionary run on dictIds (rid[a]: the lane's min / max dictId within the current segment),
 // folded into r0 as a value at the end of every segment run (lane_acc_segment_end).
 struct LaneAcc {
-  int64_t r0[kLaneAggs];
-  int64_t r1[kLaneAggs];
-  uint32_t rid[kLaneAggs];
-  uint32_t idm;  // bit a: rid[a] was updated in the current segment run
+  // Per-thread slots in LDS (the workgroup's lane-accumulator area at the front of the dynamic LDS: kLaneAccBytes per
+  // thread and aggregation), so no accumulator occupies a VGPR across the tile loop: aggregation a of thread t keeps
+  // (r0, r1) at pair + 16 * (a * WGS + t) and its dictId at id + 4 * (a * WGS + t) (consecutive threads 16 / 4 bytes
+  // apart: conflict-free ds_read_b128 / ds_read_b32).
+  uint32_t pair;   // LDS byte address of aggregation 0's (r0, r1) slot of this thread
+  uint32_t id;     // LDS byte address of aggregation 0's dictId slot of this thread
+  uint32_t astr;   // bytes between aggregations' pair slots (16 * WGS); dictId slots: astr / 4
+  uint32_t idm;    // bit a: aggregation a's dictId was updated in the current segment run
 };
+typedef __attribute__((address_space(3))) int64_t lds_i64_t;
+__device__ __forceinline__ void la_get(const LaneAcc& la, int a, int64_t& r0, int64_t& r1) {
+  const lds_i64_t* p = (const lds_i64_t*)(uintptr_t)(la.pair + (uint32_t)a * la.astr);
+  r0 = p[0];
+  r1 = p[1];
+}
+__device__ __forceinline__ void la_set(const LaneAcc& la, int a, int64_t r0, int64_t r1) {
+  lds_i64_t* p = (lds_i64_t*)(uintptr_t)(la.pair + (uint32_t)a * la.astr);
+  p[0] = r0;
+  p[1] = r1;
+}
+__device__ __forceinline__ uint32_t la_rid(const LaneAcc& la, int a) {
+  return *(const lds_u32_t*)(uintptr_t)(la.id + (uint32_t)a * (la.astr >> 2));
+}
+__device__ __forceinline__ void la_set_rid(const LaneAcc& la, int a, uint32_t v) {
+  *(lds_u32_t*)(uintptr_t)(la.id + (uint32_t)a * (la.astr >> 2)) = v;
+}
 
 __device__ __forceinline__ uint32_t rid_init(int t) { return t == PA_AGG_MIN ? 0xffffffffu : 0u; }
 
-__device__ __forceinline__ void lane_acc_init(const DevQuery* __restrict__ q, LaneAcc& la) {
-#pragma unroll
-  for (int a = 0; a < kLaneAggs; ++a) {
-    const int t = a < q->num_aggs ? q->aggs[a].type : PA_AGG_COUNT;
-    la.r0[a] = t == PA_AGG_MIN ? INT64_MAX : (t == PA_AGG_MAX ? INT64_MIN : 0);
-    la.r1[a] = 0;
-    la.rid[a] = rid_init(t);
-  }
+__device__ __forceinline__ void lane_acc_init(const DevQuery* __restrict__ q, LaneAcc& la, const void* lds_area,
+                                              int wgs) {
+  la.astr = 16u * (uint32_t)wgs;
+  la.pair = lds_addr(lds_area) + 16u * threadIdx.x;
+  la.id = lds_addr(lds_area) + (uint32_t)q->num_aggs * la.astr + 4u * threadIdx.x;
   la.idm = 0;
+  for (int a = 0; a < q->num_aggs && a < kLaneAggs; ++a) {
+    const int t = q->aggs[a].type;
+    la_set(la, a, t == PA_AGG_MIN ? INT64_MAX : (t == PA_AGG_MAX ? INT64_MIN : 0), 0);
+    la_set_rid(la, a, rid_init(t));
+  }
 }
 
 // Lane-major fast path modes (lane_agg_lm)
@@ -1506,20 +1529,129 @@ __device__ __forceinline__ void lane_acc_segment_end(const DevQuery* __restrict_
     if (a >= q->num_aggs) break;
     const int t = q->aggs[a].type;
     if (t != PA_AGG_MIN && t != PA_AGG_MAX) continue;
-    const uint32_t id = la.rid[a];
-    la.rid[a] = rid_init(t);
+    const uint32_t id = la_rid(la, a);
+    la_set_rid(la, a, rid_init(t));
     if (!((la.idm >> a) & 1u) || !any || (t == PA_AGG_MIN && id == 0xffffffffu)) continue;
     const DevCol& c = seg->cols[q->aggs[a].slot];
     const int64_t e = q->aggs[a].src == SRC_DOUBLE ? f64_order_encode(gp(c.dict_f64)[id]) : gp(c.dict_i64)[id];
-    la.r0[a] = t == PA_AGG_MIN ? (e < la.r0[a] ? e : la.r0[a]) : (e > la.r0[a] ? e : la.r0[a]);
+    int64_t r0, r1;
+    la_get(la, a, r0, r1);
+    la_set(la, a, t == PA_AGG_MIN ? (e < r0 ? e : r0) : (e > r0 ? e : r0), r1);
   }
   la.idm = 0;
+}
+
+// One value (int64, or double bits for SRC_DOUBLE) into a lane accumulator pair: SUM over int32-range values r0 += v;
+// 64-bit integer SUM as the exact split pair (r0 += low 32 bits unsigned, r1 += high 32 bits signed); double SUM in
+// r0's bits; MIN / MAX on the order-preserving encoding.
+__device__ __forceinline__ void lane_fold(int type, int src, uint64_t v, int64_t& r0, int64_t& r1) {
+  if (type == PA_AGG_SUM) {
+    if (src == SRC_INT) {
+      r0 += (int64_t)v;
+    } else if (src == SRC_LONG) {
+      r0 += (int64_t)(uint32_t)v;
+      r1 += (int64_t)v >> 32;
+    } else {
+      r0 = __builtin_bit_cast(int64_t, __builtin_bit_cast(double, r0) + __builtin_bit_cast(double, v));
+    }
+  } else {
+    const int64_t e = src == SRC_DOUBLE ? f64_order_encode(__builtin_bit_cast(double, v)) : (int64_t)v;
+    r0 = type == PA_AGG_MIN ? (e < r0 ? e : r0) : (e > r0 ? e : r0);
+  }
+}
+
+// A raw value as the 64-bit pattern lane_fold takes: INT sign-extended, FLOAT widened to double bits, LONG / DOUBLE as is.
+__device__ __forceinline__ uint64_t raw_bits(int vtype, uint64_t x) {
+  switch (vtype) {
+    case PA_INT: return (uint64_t)(int64_t)(int32_t)(uint32_t)x;
+    case PA_FLOAT: return __builtin_bit_cast(uint64_t, (double)__builtin_bit_cast(float, (uint32_t)x));
+    default: return x;
+  }
+}
+
+// Sparse lane-major tile (few matching docs): each lane walks its own set bits of m (doc 32*lane + i), four per batch so
+// their loads overlap; the wave loops max-popcount times instead of over all 32 docs. `load(i)` issues the value load of
+// doc i (nothing is consumed before all four are issued).
+template <class LOAD>
+__device__ __forceinline__ void lane_sparse(uint32_t m, int type, int src, LOAD load, int64_t& r0, int64_t& r1) {
+  while (__ballot(m != 0) != 0) {
+    bool on[4];
+    uint64_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      on[k] = m != 0;
+      const int i = on[k] ? __builtin_ctz(m) : 0;
+      m &= m - 1u;
+      v[k] = on[k] ? load(i) : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (on[k]) lane_fold(type, src, v[k], r0, r1);
+  }
+}
+
+// lane_sparse for MIN / MAX of a sorted dictionary: the smallest / largest matching dictId (dec(i) = dictId of doc i).
+template <class DEC>
+__device__ __forceinline__ void lane_sparse_ids(uint32_t m, bool is_min, DEC dec, uint32_t& rid) {
+  while (__ballot(m != 0) != 0) {
+    bool on[4];
+    uint32_t id[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      on[k] = m != 0;
+      const int i = on[k] ? __builtin_ctz(m) : 0;
+      m &= m - 1u;
+      id[k] = on[k] ? dec(i) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (on[k]) rid = is_min ? min(rid, id[k]) : max(rid, id[k]);
+  }
+}
+
+// Dense lane-major tile of a raw column of VB-byte values: the whole tile's values as coalesced 16-byte loads
+// (instruction k, lane l: docs VPL*(64k + l) .. + VPL-1 of the tile, VPL = 16 / VB), every value's match bit read from
+// the lane owning its doc in the lane-major layout (doc d: lane d >> 5, bit d & 31) by one ds_bpermute per
+// instruction. Non-matching values are skipped by a select (no per-doc branch). Raw columns are padded to whole wave
+// tiles, so the last tile's loads stay in bounds. 32 VGPRs of loads per batch, all issued before use.
+template <int VB>
+__device__ __forceinline__ void lane_raw_dense(const char* tile, uint32_t m, int lane, int vtype, int type, int src,
+                                               int64_t& r0, int64_t& r1) {
+  constexpr int VPL = 16 / VB;        // values per lane per instruction
+  constexpr int NI = 2048 * VB / 1024;  // instructions per tile
+  constexpr int KB = VB == 8 ? 4 : 8;
+  const AS1 u32x4* p = (const AS1 u32x4*)tile + lane;
+#pragma unroll
+  for (int k0 = 0; k0 < NI; k0 += KB) {
+    u32x4 w[KB];
+    uint32_t mb[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      w[k] = p[(k0 + k) * kWave];
+      // owner of doc VPL*(64k + l): lane 2*VPL*k + (VPL*l >> 5); its bits VPL*l & 31 .. + VPL-1
+      const int owner = 2 * VPL * (k0 + k) + ((VPL * lane) >> 5);
+      mb[k] = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)m) >> ((VPL * lane) & 31);
+    }
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+#pragma unroll
+      for (int j = 0; j < VPL; ++j) {
+        const uint64_t x = VB == 8 ? ((uint64_t)w[k][2 * j + 1] << 32) | w[k][2 * j] : (uint64_t)w[k][j];
+        const bool on = (mb[k] >> j) & 1u;
+        if (type == PA_AGG_SUM) {
+          lane_fold(type, src, on ? raw_bits(vtype, x) : 0ull, r0, r1);  // (+0 / +0.0 for a doc that does not match)
+        } else if (on) {
+          lane_fold(type, src, raw_bits(vtype, x), r0, r1);
+        }
+      }
+    }
+  }
 }
 
 // The matching docs (match words m) of one tile into the lane accumulators: per aggregation, 8 steps per batch — every
 // value load of the batch is issued before any is used (staged dictIds from the tile image, lazy ones and raw values from
 // HBM, then the dictionary gathers).
-template <int LM, int STEPS>
+template <int LM, int STEPS, int STRAT>
 __device__ __forceinline__ void lane_acc_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
                                               const uint32_t* img, int64_t doc_base, uint32_t m, int lane,
                                               LaneAcc& la) {
@@ -1528,9 +1660,22 @@ __device__ __forceinline__ void lane_acc_tile(const DevQuery* __restrict__ q, co
   auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
   constexpr int kB = 8;
   const int na = q->num_aggs;
+  // matching docs of the tile: the wave's total and the largest count of one lane (sparse vs dense paths)
+  uint32_t tot = 0, mx = 0;
+  if constexpr (LM) {
+    tot = mx = (uint32_t)__builtin_popcount(m);
 #pragma unroll
-  for (int a = 0; a < kLaneAggs; ++a) {
-    if (a >= na) break;
+    for (int o = 1; o < kWave; o <<= 1) {
+      tot += (uint32_t)__shfl_xor((int)tot, o, kWave);
+      mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, kWave));
+    }
+    tot = (uint32_t)__builtin_amdgcn_readfirstlane((int)tot);
+    mx = (uint32_t)__builtin_amdgcn_readfirstlane((int)mx);
+  }
+  // one copy of the per-aggregation code (a loop that is not unrolled; the accumulators live in LDS): the unrolled form
+  // replicated every path per aggregation and spilled
+#pragma unroll 1
+  for (int a = 0; a < na && a < kLaneAggs; ++a) {
     const int type = q->aggs[a].type;
     if (type == PA_AGG_COUNT) continue;
     const int slot = q->aggs[a].slot, src = q->aggs[a].src;
@@ -1540,18 +1685,68 @@ __device__ __forceinline__ void lane_acc_tile(const DevQuery* __restrict__ q, co
     const uint64_t* dict = src == SRC_DOUBLE ? (const uint64_t*)cs->cols[slot].dict_f64
                                              : (const uint64_t*)cs->cols[slot].dict_i64;
     const void* raw = cs->cols[slot].raw;
-    int64_t r0 = la.r0[a], r1 = la.r1[a];
+    int64_t r0, r1;
+    la_get(la, a, r0, r1);
+    uint32_t rid = la_rid(la, a);
+    do {  // (break: this aggregation is done)
+    if (STRAT == STRAT_LANE_DICT) {
+    } else if (LM && kind == COL_SV_RAW) {
+      // raw column: per-doc loads of the few matching docs, or the whole tile as coalesced 16-byte loads (a sparse
+      // tile's loads touch at most `tot` lines; the dense read is 2048 * VB bytes = 16 * VB lines of 128 B)
+      const int vb = (vtype == PA_INT || vtype == PA_FLOAT) ? 4 : 8;
+      if (tot <= (uint32_t)(6 * vb)) {
+        const int64_t d0 = doc_base + 32 * lane;
+        if (vb == 4) {
+          const AS1 uint32_t* rp = gp((const uint32_t*)raw) + d0;
+          lane_sparse(m, type, src, [&](int i) { return raw_bits(vtype, rp[i]); }, r0, r1);
+        } else {
+          const AS1 uint64_t* rp = gp((const uint64_t*)raw) + d0;
+          lane_sparse(m, type, src, [&](int i) { return rp[i]; }, r0, r1);
+        }
+      } else if (vb == 4) {
+        lane_raw_dense<4>((const char*)raw + doc_base * 4, m, lane, vtype, type, src, r0, r1);
+      } else {
+        lane_raw_dense<8>((const char*)raw + doc_base * 8, m, lane, vtype, type, src, r0, r1);
+      }
+      break;
+    }
+    if (STRAT == STRAT_LANE_RAW) break;  // (the raw kernel's columns are all raw: handled above)
+    if constexpr (STRAT == STRAT_LANE_DICT) {
+      // dictionary kernel: every tile walks the lanes' set bits (a lane's matching docs one after another, the wave
+      // max-popcount times): decode from the staged image (or HBM when lazy), then MIN / MAX of a sorted dictionary on
+      // the dictIds, anything else on the gathered values. One path (no per-width unpack calls): nothing spills.
+      auto dec = [&](int i) -> uint32_t {
+        return loff >= 0 ? decode_lds(img + loff, 32 * lane + i, nb) : decode_global(words, doc_base + 32 * lane + i, nb);
+      };
+      if (type != PA_AGG_SUM && (cs->cols[slot].flags & COLF_DICT_SORTED)) {
+        lane_sparse_ids(m, type == PA_AGG_MIN, dec, rid);
+        la.idm |= 1u << a;
+      } else {
+        lane_sparse(m, type, src, [&](int i) { return gp(dict)[dec(i)]; }, r0, r1);
+      }
+      break;
+    }
+    if (LM && kind == COL_SV_DICT && mx <= 12 &&
+        !(type != PA_AGG_SUM && (cs->cols[slot].flags & COLF_DICT_SORTED) && loff >= 0)) {
+      // dictionary column, few matching docs per lane: decode only those (staged image or HBM) and gather their values
+      if (loff >= 0) {
+        const uint32_t* region = img + loff;
+        lane_sparse(m, type, src, [&](int i) { return gp(dict)[decode_lds(region, 32 * lane + i, nb)]; }, r0, r1);
+      } else {
+        const int64_t d0 = doc_base + 32 * lane;
+        lane_sparse(m, type, src, [&](int i) { return gp(dict)[decode_global(words, d0 + i, nb)]; }, r0, r1);
+      }
+      break;
+    }
     if (LM && kind == COL_SV_DICT && loff >= 0 &&
         (type == PA_AGG_SUM || (cs->cols[slot].flags & COLF_DICT_SORTED))) {
       const int mode = type == PA_AGG_SUM ? (src == SRC_INT ? LM_SUM_INT : (src == SRC_LONG ? LM_SUM_LONG : LM_SUM_DOUBLE))
                                           : (type == PA_AGG_MIN ? LM_MIN_ID : LM_MAX_ID);
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
           (void*)dict, (short)0, cs->cols[slot].card * 8, 0x00020000);
-      lane_agg_lm_any(nb, lds_addr(img + loff), lane, m, mode, rs, r0, r1, la.rid[a]);
+      lane_agg_lm_any(nb, lds_addr(img + loff), lane, m, mode, rs, r0, r1, rid);
       if (mode >= LM_MIN_ID) la.idm |= 1u << a;
-      la.r0[a] = r0;
-      la.r1[a] = r1;
-      continue;
+      break;
     }
 #pragma unroll 1
     for (int h = 0; h < STEPS; h += kB) {
@@ -1601,8 +1796,9 @@ __device__ __forceinline__ void lane_acc_tile(const DevQuery* __restrict__ q, co
         }
       }
     }
-    la.r0[a] = r0;
-    la.r1[a] = r1;
+    } while (false);
+    la_set(la, a, r0, r1);
+    la_set_rid(la, a, rid);
   }
 }
 
@@ -1613,25 +1809,27 @@ __device__ __forceinline__ void lane_acc_flush(const DevQuery* __restrict__ q, c
     if (a >= q->num_aggs) break;
     const DevAgg& A = q->aggs[a];
     if (A.type == PA_AGG_COUNT) continue;
+    int64_t r0, r1;
+    la_get(la, a, r0, r1);
     if (A.type == PA_AGG_SUM) {
       if (A.src == SRC_DOUBLE) {
-        const double s = wave_sum_f64(__builtin_bit_cast(double, la.r0[a]));
+        const double s = wave_sum_f64(__builtin_bit_cast(double, r0));
         if (lane == 0) __hip_atomic_fetch_add(gp(A.acc_f64), s, RLX);
       } else if (A.src == SRC_LONG) {
-        const int64_t lo = wave_sum_i64(la.r0[a]), hi = wave_sum_i64(la.r1[a]);
+        const int64_t lo = wave_sum_i64(r0), hi = wave_sum_i64(r1);
         if (lane == 0) {
           __hip_atomic_fetch_add(gp((unsigned long long*)A.acc_i64), (unsigned long long)lo, RLX);
           __hip_atomic_fetch_add(gp((unsigned long long*)A.acc_i64) + 1, (unsigned long long)hi, RLX);
         }
       } else {
-        const int64_t s = wave_sum_i64(la.r0[a]);
+        const int64_t s = wave_sum_i64(r0);
         if (lane == 0) __hip_atomic_fetch_add(gp((unsigned long long*)A.acc_i64), (unsigned long long)s, RLX);
       }
     } else if (A.type == PA_AGG_MIN) {
-      const int64_t r = wave_min_i64(la.r0[a]);
+      const int64_t r = wave_min_i64(r0);
       if (lane == 0 && r != INT64_MAX) __hip_atomic_fetch_min(gp((long long*)A.acc_i64), (long long)r, RLX);
     } else {
-      const int64_t r = wave_max_i64(la.r0[a]);
+      const int64_t r = wave_max_i64(r0);
       if (lane == 0 && r != INT64_MIN) __hip_atomic_fetch_max(gp((long long*)A.acc_i64), (long long)r, RLX);
     }
   }
@@ -1673,8 +1871,8 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
     m = admitted_docs<LM, STEPS>(q, seg, img, doc_base, m, lane);
     if (__ballot(m != 0) == 0) return (uint32_t)__builtin_popcount(scanned);
   }
-  if constexpr (STRAT == STRAT_LANE) {
-    lane_acc_tile<LM, STEPS>(q, seg, img, doc_base, m, lane, la);
+  if constexpr (is_lane(STRAT)) {
+    if constexpr (STRAT != STRAT_LANE_CNT) lane_acc_tile<LM, STEPS, STRAT>(q, seg, img, doc_base, m, lane, la);
   } else if constexpr (STRAT == STRAT_PCOUNT || is_pemit(STRAT)) {
     part_tile<STRAT, STEPS, LM>(q, seg, img, doc_base, m, lane, lds, ps);
   } else if (q->has_mv) {
@@ -2004,7 +2202,7 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
 
   uint32_t matched = 0;  // docs of this lane that passed the filter (numDocsScanned)
   LaneAcc la;
-  if constexpr (STRAT == STRAT_LANE) lane_acc_init(q, la);
+  if constexpr (is_lane(STRAT) && STRAT != STRAT_LANE_CNT) lane_acc_init(q, la, smem, WGS);
   const int64_t T = q->total_wtiles;
   const int64_t W = (int64_t)gridDim.x * WPW;
   const int64_t lb = q->xcd_major ? xcd_major_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;  // logical block
@@ -2120,7 +2318,7 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
         }
         pslot = pslot + 1 == R ? 0 : pslot + 1;
       }
-      if constexpr (STRAT == STRAT_LANE) lane_acc_segment_end(q, seg, la, matched != matched_seg0);
+      if constexpr (is_lane(STRAT) && STRAT != STRAT_LANE_CNT) lane_acc_segment_end(q, seg, la, matched != matched_seg0);
       if (t < t1) {
         ++si;
         while (t >= segs[si].first_wtile + segs[si].num_wtiles) ++si;
@@ -2131,9 +2329,9 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
   if (!is_pemit(STRAT)) {  // (the partitioned count pass counts numDocsScanned; its emit pass sees the same docs)
     const int64_t wm = wave_sum_i64((int64_t)matched);
     if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)wm, RLX);
-    if constexpr (STRAT == STRAT_LANE) {  // COUNT(*) of an aggregation-only query = the docs the filter kept
+    if constexpr (is_lane(STRAT)) {  // COUNT(*) of an aggregation-only query = the docs the filter kept
       if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->count), (unsigned long long)wm, RLX);
-      lane_acc_flush(q, la, lane);
+      if constexpr (STRAT != STRAT_LANE_CNT) lane_acc_flush(q, la, lane);
     }
   }
   if (STRAT == STRAT_PCOUNT) {
@@ -2217,7 +2415,8 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
 
 // Kernel-pointer getters of the scan variants, one translation unit per group (parallel builds): nullptr when the
 // unit does not hold the strategy.
-const void* scan_fn_std(int strategy, int steps, int lm);   // pa_scan_std.hip: LDS, GLOBAL, LANE
+const void* scan_fn_std(int strategy, int steps, int lm);   // pa_scan_std.hip: LDS, GLOBAL (LANE via scan_fn_lane)
+const void* scan_fn_lane(int strategy, int steps, int lm);  // pa_scan_lane.hip: LANE and its variants
 const void* scan_fn_part_a(int strategy);                  // pa_scan_part_a.hip: PCOUNT + emit variants (one part)
 const void* scan_fn_part_b(int strategy);                  // pa_scan_part_b.hip: the other emit variants
 

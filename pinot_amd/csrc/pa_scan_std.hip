@@ -1,4 +1,5 @@
-// Scan-kernel variants of the direct strategies: LDS-privatised accumulators, global atomics, per-lane registers.
+// Scan-kernel variants of the direct strategies: LDS-privatised accumulators, global atomics (per-lane registers:
+// pa_scan_lane.hip).
 #include "pa_scan.h"
 
 namespace pa {
@@ -13,7 +14,10 @@ const void* scan_fn_std(int strategy, int steps, int lm) {
   switch (strategy) {
     case STRAT_LDS: return fn_s<STRAT_LDS>(steps, lm);
     case STRAT_GLOBAL: return fn_s<STRAT_GLOBAL>(steps, lm);
-    case STRAT_LANE: return fn_s<STRAT_LANE>(steps, lm);
+    case STRAT_LANE:
+    case STRAT_LANE_CNT:
+    case STRAT_LANE_RAW:
+    case STRAT_LANE_DICT: return scan_fn_lane(strategy, steps, lm);
     default: return nullptr;
   }
 }

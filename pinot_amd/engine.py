@@ -46,6 +46,8 @@ class GpuSegment:
         self.column_ids = dict(column_ids or column_ids_for(segment))
         self.handle = L.check_ptr(lib.pa_segment_create(segment.num_docs), "pa_segment_create")
         self._keep = []
+        if segment.num_docs == 0:
+            return  # an empty segment has no column indexes (SegmentColumnarIndexCreator.java:124 writes none)
         for name in (columns if columns is not None else segment.columns):
             self._add(name)
 
@@ -160,12 +162,15 @@ class GpuQueryExecutor:
         self.wide_sum_columns = set(wide_sum_columns or ())
         self.hash_keys_bound = int(hash_keys_bound or 0)
         self.query = query
-        self.gsegs = gpu_segments
-        self.segs = [g.segment for g in gpu_segments]
+        # empty segments hold no indexes and contribute nothing but their (zero) doc count: only the others are bound
+        self.all_segs = [g.segment for g in gpu_segments]
+        self.gsegs = [g for g in gpu_segments if g.segment.num_docs > 0]
+        self.segs = [g.segment for g in self.gsegs]
         self.flags = flags
         self.enforce_num_groups_limit = enforce_num_groups_limit
         self.handle = None
-        self._plan()
+        if self.segs:
+            self._plan()
 
     # ------------------------------------------------------------------ planning
     def _plan(self):
@@ -364,6 +369,8 @@ class GpuQueryExecutor:
 
     # ------------------------------------------------------------------ execution
     def execute(self, stream=None):
+        if not self.segs:
+            return  # (every bound segment is empty: nothing to scan)
         L.check(L.lib().pa_query_execute(self.handle, stream), "pa_query_execute")
 
     def reset(self, stream=None):
@@ -390,7 +397,7 @@ class GpuQueryExecutor:
         L.check(L.lib().pa_query_plan(self.handle, *[ctypes.byref(v) for v in vals]), "plan")
         names = ("strategy", "steps", "dma_slots", "ring", "wg_per_cu", "grid", "lds_bytes")
         out["plan"] = {n: v.value for n, v in zip(names, vals)}
-        out["plan"]["strategy"] = {0: "lds", 1: "global", 2: "partitioned", 4: "lane"}[out["plan"]["strategy"]]
+        out["plan"]["strategy"] = {0: "lds", 1: "global", 2: "partitioned", 4: "lane", 5: "lane", 6: "lane", 7: "lane"}[out["plan"]["strategy"]]
         out["plan"]["eager_literals"] = int(L.lib().pa_query_num_eager_literals(self.handle))
         out["plan"]["lane_major"] = int(L.lib().pa_query_lane_major(self.handle))
         out["plan"]["limit_trimming"] = int(L.lib().pa_query_limit_trimming(self.handle))
@@ -486,10 +493,12 @@ class GpuQueryExecutor:
         loop)."""
         lib = L.lib()
         q = self.query
+        if not self.segs:
+            return self._empty_result()
         keys, counts, outs = self.fetch_arrays(stream)
         n = len(keys)
         res = IntermediateResult(list(q.aggregations), list(q.group_by))
-        res.num_total_docs = sum(s.num_docs for s in self.segs)
+        res.num_total_docs = sum(s.num_docs for s in self.all_segs)
         res.num_docs_scanned = int(lib.pa_query_matched_docs(self.handle))
         if execution_stats:
             res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter = self.execution_stats(stream)
@@ -524,6 +533,23 @@ class GpuQueryExecutor:
             res.num_groups_limit_reached = int(L.lib().pa_query_num_groups_limit_reached(self.handle)) > 0
         else:
             res.row = list(rows[0])
+        return res
+
+    def _empty_result(self):
+        """The results block of a segment set without docs: no groups, or the aggregation functions' empty
+        intermediate results (COUNT 0, SUM 0.0, MIN +inf, MAX -inf, AVG (0.0, 0), empty HLL / value set)."""
+        q = self.query
+        res = IntermediateResult(list(q.aggregations), list(q.group_by))
+        if not q.group_by:
+            row = []
+            for a in q.aggregations:
+                fn = Q.base_function(a.function)
+                row.append({"COUNT": 0, "SUM": 0.0, "MIN": float("inf"), "MAX": float("-inf")}.get(fn) if fn in
+                           ("COUNT", "SUM", "MIN", "MAX") else
+                           AvgPair(0.0, 0) if fn == "AVG" else
+                           HyperLogLog(a.log2m) if fn == "DISTINCTCOUNTHLL" else
+                           MinMaxRangePair(float("inf"), float("-inf")) if fn == "MINMAXRANGE" else set())
+            res.row = row
         return res
 
     def run(self, stream=None) -> IntermediateResult:

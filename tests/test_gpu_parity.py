@@ -114,6 +114,13 @@ def test_query_executor_cases_gpu(query_executor_spec, query_executor_segments):
             ex.close()
             assert res.row[0] == case["value"] and type(res.row[0]) is type(case["value"]), (case["source"], res.row)
             assert res.num_docs_scanned == 400002 and res.num_total_docs == 400002
+        # only the empty segments: the aggregation functions' empty results, as the oracle gives them
+        q = parse_sql("SELECT COUNT(*), SUM(met), MIN(met), MAX(met) FROM testTable_OFFLINE")
+        ex = GpuQueryExecutor(q, gs[2:])
+        res = ex.run()
+        ex.close()
+        exp = oracle.run_query(q, query_executor_segments[2:])
+        assert res.row == exp.row and res.num_docs_scanned == 0, (res.row, exp.row)
     finally:
         for g in gs:
             g.close()

@@ -206,17 +206,22 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
             fetch_ms = (time.perf_counter() - t1) * 1e3
             st = ex.stats()
             extra = {}
+            # roofline of the fused scan: algorithmic bytes = the staged forward-index bytes + for each
+            # raw value column the 64-byte sectors holding a matching doc (matches spread uniformly: a fraction
+            # 1 - (1 - p)^(64 / value bytes) of the column's sectors at selectivity p)
+            matched = int(L.lib().pa_query_matched_docs(ex.handle))
+            agg_cols = {a.column for a in parse_sql(sql).aggregations if a.column}
+            p = matched / max(1, st["num_docs"])
+            raw_bytes = 0.0
+            for c in gsegs[0].segment.columns.values():
+                if not c.has_dictionary and c.name in agg_cols:
+                    vb = 4 if c.data_type in ("INT", "FLOAT") else 8
+                    raw_bytes += st["num_docs"] * vb * (1.0 - (1.0 - p) ** (64 // vb))
+            algo = st["staged_bytes"] + int(raw_bytes)
+            extra["roofline"] = {"bound": "hbm", "achieved": algo / (ms * 1e-3) / 1e9, "peak": 8000.0,
+                                 "unit": "GB/s", "frac": algo / (ms * 1e-3) / 1e9 / 8000.0,
+                                 "algorithmic_bytes_per_launch": algo}
             if cpu_sample:
-                # roofline of the fused scan: algorithmic bytes = the staged forward-index bytes + for
-                # raw value columns 8 (or 4) bytes per matching doc
-                matched = int(L.lib().pa_query_matched_docs(ex.handle))
-                agg_cols = {a.column for a in parse_sql(sql).aggregations if a.column}
-                raw_b = sum((4 if c.data_type in ("INT", "FLOAT") else 8) for c in gsegs[0].segment.columns.values()
-                            if not c.has_dictionary and c.name in agg_cols)
-                algo = st["staged_bytes"] + raw_b * matched
-                extra["roofline"] = {"bound": "hbm", "achieved": algo / (ms * 1e-3) / 1e9, "peak": 8000.0,
-                                     "unit": "GB/s", "frac": algo / (ms * 1e-3) / 1e9 / 8000.0,
-                                     "algorithmic_bytes_per_launch": algo}
                 extra["cpu_baseline"] = cpu_port_baseline(sql, host)
             print(json.dumps(dict({"workload": workload, "plan_name": name + tag, "kernel_ms": round(ms, 4),
                               "rows_per_s": st["num_docs"] / (ms * 1e-3), "staged_bytes": st["staged_bytes"],
