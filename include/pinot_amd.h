@@ -109,6 +109,10 @@ int pa_abi_version(void);
 int pa_device_count(void);
 int pa_set_device(int device);
 const char* pa_last_error(void);
+/* Page-locked host memory of the library's runtime, for fetch output arrays: pa_query_fetch then copies each result
+ * column straight into it by DMA (a pooled buffer the caller reuses across fetches). NULL on failure. */
+void* pa_host_alloc(uint64_t bytes);
+void pa_host_free(void* p);
 
 /* ---------------------------------------------------------------- segments (HBM resident) */
 typedef struct pa_segment pa_segment;

@@ -38,7 +38,7 @@ ABI_VERSION = 2
 
 # every symbol declared in include/pinot_amd.h
 EXPORTED = [
-    "pa_abi_version", "pa_device_count", "pa_set_device", "pa_last_error",
+    "pa_abi_version", "pa_device_count", "pa_set_device", "pa_last_error", "pa_host_alloc", "pa_host_free",
     "pa_segment_create", "pa_segment_add_sv_dict_column", "pa_segment_add_mv_dict_column",
     "pa_segment_add_raw_column", "pa_segment_num_docs", "pa_segment_device_bytes", "pa_segment_destroy",
     "pa_query_create", "pa_query_bind_segment", "pa_query_bind_value_remap", "pa_query_prepare", "pa_query_num_keys",
@@ -102,6 +102,8 @@ def _declare(lib):
         "pa_device_count": (ctypes.c_int, []),
         "pa_set_device": (ctypes.c_int, [ctypes.c_int]),
         "pa_last_error": (ctypes.c_char_p, []),
+        "pa_host_alloc": (vp, [u64]),
+        "pa_host_free": (None, [vp]),
         "pa_segment_create": (vp, [i32]),
         "pa_segment_add_sv_dict_column": (ctypes.c_int, [vp, i32, vp, u64, i32, i32, i32, vp, vp]),
         "pa_segment_add_mv_dict_column": (ctypes.c_int, [vp, i32, vp, u64, i32, i32, i64, i32, vp, vp]),

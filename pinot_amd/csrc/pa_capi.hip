@@ -169,6 +169,19 @@ int pa_set_device(int device) {
 
 const char* pa_last_error(void) { return g_err.c_str(); }
 
+void* pa_host_alloc(uint64_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, std::max<uint64_t>(bytes, 16), hipHostMallocDefault) != hipSuccess) {
+    fail(PA_ENOMEM, "hipHostMalloc failed");
+    return nullptr;
+  }
+  return p;
+}
+
+void pa_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 pa_segment* pa_segment_create(int32_t num_docs) {
   if (num_docs < 0) {
     fail(PA_EINVAL, "num_docs < 0");
@@ -2268,6 +2281,44 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   const int64_t m = (int64_t)total;
   const int64_t rows_cap = std::min<int64_t>(m, std::max<int64_t>(capacity, 0));
   if (rows_cap == 0) return m;
+  if (!q->hashed) {
+    // Direct key space: the compaction writes the caller's representation (key ids, counts, doubles / register bytes)
+    // into staging columns on the GPU, and each column goes to the caller's array in one copy (a DMA straight into
+    // pinned memory when the caller's arrays are pinned: engine.py keeps a reused pinned output pool). No host decode.
+    FinalDesc f;
+    std::memset(&f, 0, sizeof(f));
+    f.nagg = s.num_aggs;
+    std::vector<size_t> off(s.num_aggs, 0);
+    size_t bytes = ((size_t)rows_cap * 16 + 255) & ~(size_t)255;  // keys | counts
+    for (int a = 0; a < s.num_aggs; ++a) {
+      const pa_agg_spec& A = s.aggs[a];
+      f.type[a] = A.type;
+      f.src[a] = q->hq.aggs[a].src;
+      f.sec[a] = q->agg_section[a] >= 0 ? q->sections[q->agg_section[a]].ptr : nullptr;
+      f.per[a] = A.type == PA_AGG_DISTINCTCOUNT ? presence_stride(A)
+                                                : (A.type == PA_AGG_DISTINCTCOUNTHLL ? (int64_t(1) << A.log2m) : 8);
+      off[a] = bytes;
+      bytes += ((size_t)rows_cap * (size_t)f.per[a] + 255) & ~(size_t)255;
+    }
+    if (q->fetch_stage.n < bytes) {
+      dev_free(q->fetch_stage);
+      int rc = dev_alloc(q->fetch_stage, bytes);
+      if (rc) return rc;
+    }
+    char* ds = (char*)q->fetch_stage.p;
+    f.keys = (int64_t*)ds;
+    f.counts = (int64_t*)(ds + (size_t)rows_cap * 8);
+    for (int a = 0; a < s.num_aggs; ++a) f.out[a] = ds + off[a];
+    PA_HIP(launch_compact_final((const unsigned long long*)q->sections[0].ptr, K, all,
+                                (const uint32_t*)q->fetch_blocks.p, rows_cap, &f, st));
+    if (out_keys) PA_HIP(hipMemcpyAsync(out_keys, f.keys, (size_t)rows_cap * 8, hipMemcpyDeviceToHost, st));
+    if (out_counts) PA_HIP(hipMemcpyAsync(out_counts, f.counts, (size_t)rows_cap * 8, hipMemcpyDeviceToHost, st));
+    for (int a = 0; a < s.num_aggs; ++a)
+      if (out_aggs && out_aggs[a])
+        PA_HIP(hipMemcpyAsync(out_aggs[a], f.out[a], (size_t)rows_cap * (size_t)f.per[a], hipMemcpyDeviceToHost, st));
+    PA_HIP(hipStreamSynchronize(st));
+    return m;
+  }
   // staging: keys | count | one block per aggregation section (rows x per x es), 256-byte aligned pieces
   CompactDesc d;
   std::memset(&d, 0, sizeof(d));

@@ -461,6 +461,111 @@ __global__ void __launch_bounds__(256) compact_gather_kernel(const unsigned long
   }
 }
 
+// Correctly rounded (nearest, ties to even) double of the signed 128-bit integer hi:lo — the host's (double)__int128 of
+// an exact 96-bit SUM (PA_ACC_SUM_I64X2), an int64 SUM or an integer MIN / MAX, computed with integer operations only.
+__device__ double i128_to_double(int64_t hi, uint64_t lo) {
+  const bool neg = hi < 0;
+  uint64_t mh = (uint64_t)hi, ml = lo;
+  if (neg) {
+    ml = ~ml + 1ull;
+    mh = ~mh + (ml == 0 ? 1ull : 0ull);
+  }
+  if (mh == 0 && ml < (1ull << 53)) return neg ? -(double)ml : (double)ml;  // (exact)
+  const int msb = mh ? 127 - __builtin_clzll(mh) : 63 - __builtin_clzll(ml);
+  const int s = msb - 52;  // bits below the 53-bit significand (>= 1 here)
+  auto bit = [&](int i) -> uint64_t { return i >= 64 ? (mh >> (i - 64)) & 1ull : (ml >> i) & 1ull; };
+  uint64_t sig = s >= 64 ? mh >> (s - 64) : ((ml >> s) | (mh << (64 - s)));
+  sig &= (1ull << 53) - 1ull;
+  sig |= 1ull << 52;  // (the leading bit; the masks above keep exactly 53 bits)
+  const uint64_t half = bit(s - 1);
+  bool sticky;
+  const int t = s - 1;  // bits [0, t) below the half bit
+  if (t <= 0) sticky = false;
+  else if (t >= 64) sticky = ml != 0 || (t > 64 && (mh & ((1ull << (t - 64)) - 1ull)) != 0);
+  else sticky = (ml & ((1ull << t) - 1ull)) != 0;
+  int e = s;
+  if (half && (sticky || (sig & 1ull))) {
+    ++sig;
+    if (sig == (1ull << 53)) {
+      sig >>= 1;
+      ++e;
+    }
+  }
+  const double d = ldexp((double)sig, e);
+  return neg ? -d : d;
+}
+
+// Block b covers keys [2048b, 2048b + 2048) as in compact_gather_kernel; positions first (thread t counts keys 8t..8t+7,
+// scans, and records each key's position in LDS), then thread t writes the rows of keys t + 256 j: consecutive threads,
+// consecutive rows, 8-byte columns stored as 512-byte wave bursts.
+__global__ void __launch_bounds__(256) compact_final_kernel(const unsigned long long* count, int64_t K, int all,
+                                                            const uint32_t* block_off, int64_t cap, FinalDesc d) {
+  __shared__ uint32_t sh[256];
+  __shared__ uint32_t pos[kCompactKeys];
+  const int64_t kb = (int64_t)blockIdx.x * kCompactKeys;
+  const int64_t k0 = kb + 8 * threadIdx.x;
+  uint32_t c = 0;
+  for (int j = 0; j < 8; ++j) c += (k0 + j < K) && (all || count[k0 + j] != 0);
+  uint32_t p = block_exclusive_scan_256(c, sh, nullptr);
+  for (int j = 0; j < 8; ++j) {
+    const bool on = (k0 + j < K) && (all || count[k0 + j] != 0);
+    pos[8 * threadIdx.x + j] = on ? p : 0xffffffffu;
+    p += on ? 1u : 0u;
+  }
+  __syncthreads();
+  const int64_t base = block_off[blockIdx.x];
+  for (int j = 0; j < kCompactKeys / 256; ++j) {
+    const int kl = threadIdx.x + 256 * j;
+    const uint32_t pl = pos[kl];
+    if (pl == 0xffffffffu) continue;
+    const int64_t r = base + pl;
+    if (r >= cap) continue;
+    const int64_t k = kb + kl;
+    const unsigned long long cnt = count[k];
+    d.keys[r] = k;
+    d.counts[r] = (int64_t)cnt;
+    for (int a = 0; a < d.nagg; ++a) {
+      const int t = d.type[a];
+      if (t == PA_AGG_DISTINCTCOUNTHLL || t == PA_AGG_DISTINCTCOUNT) {
+        const int64_t per = d.per[a];  // (a multiple of 16 bytes)
+        const u32x4* src = (const u32x4*)((const uint8_t*)d.sec[a] + k * per);
+        u32x4* dst = (u32x4*)((uint8_t*)d.out[a] + r * per);
+        for (int64_t e = 0; e < per / 16; ++e) dst[e] = src[e];
+        continue;
+      }
+      double v;
+      if (t == PA_AGG_COUNT) {
+        v = (double)cnt;
+      } else if (t == PA_AGG_SUM || t == PA_AGG_COUNT_MV) {
+        const int64_t* sv = (const int64_t*)d.sec[a];
+        if (d.src[a] == SRC_LONG) {  // exact 96-bit total hi * 2^32 + lo, rounded once
+          const int64_t hs = sv[2 * k + 1];
+          const uint64_t ls = (uint64_t)sv[2 * k];
+          const uint64_t l0 = (uint64_t)hs << 32;
+          const uint64_t lo = l0 + ls;
+          v = i128_to_double((hs >> 32) + (lo < l0 ? 1 : 0), lo);
+        } else if (d.src[a] == SRC_INT || t == PA_AGG_COUNT_MV) {
+          v = i128_to_double(sv[k] >> 63, (uint64_t)sv[k]);
+        } else {
+          v = ((const double*)d.sec[a])[k];
+        }
+      } else {  // MIN / MAX (an empty aggregation-only result: +/-inf, Min/MaxAggregationFunction DEFAULT_VALUE)
+        const int64_t e8 = ((const int64_t*)d.sec[a])[k];
+        if (cnt == 0) v = t == PA_AGG_MIN ? __builtin_inf() : -__builtin_inf();
+        else v = d.src[a] != SRC_DOUBLE ? i128_to_double(e8 >> 63, (uint64_t)e8) : f64_order_decode(e8);
+      }
+      ((double*)d.out[a])[r] = v;
+    }
+  }
+}
+
+hipError_t launch_compact_final(const unsigned long long* count, int64_t K, int all, const uint32_t* block_off,
+                                int64_t cap, const FinalDesc* d, hipStream_t s) {
+  const int64_t nb = (K + kCompactKeys - 1) / kCompactKeys;
+  compact_final_kernel<<<(unsigned)nb, 256, 0, s>>>(count, K, all, block_off, cap, *d);
+  return hipGetLastError();
+}
+
 hipError_t launch_compact(const unsigned long long* count, int64_t K, int all, uint32_t* block_sums, int64_t cap,
                           const CompactDesc* d, int phase, hipStream_t s) {
   const int64_t nb = (K + kCompactKeys - 1) / kCompactKeys;

@@ -15,6 +15,21 @@ struct CompactDesc {
   void* dst[kMaxCompactSections];
   int64_t* keys;
 };
+// Final-format compaction of a direct key space (fetch of large key spaces): the non-empty keys in key order, every
+// column already in the caller's representation (key ids int64, counts int64, per aggregation double or its HLL /
+// presence bytes), one output row per thread (coalesced stores), so the host only copies.
+struct FinalDesc {
+  int32_t nagg;
+  int32_t type[PA_MAX_AGGS];   // PA_AGG_*
+  int32_t src[PA_MAX_AGGS];    // AccSrc of SUM / MIN / MAX
+  int64_t per[PA_MAX_AGGS];    // HLL / presence: bytes per row
+  const void* sec[PA_MAX_AGGS];  // the aggregation's accumulator section (nullptr: COUNT)
+  void* out[PA_MAX_AGGS];      // staging column: double[n], or per bytes x n
+  int64_t* keys;               // staging: key ids
+  int64_t* counts;             // staging: counts
+};
+hipError_t launch_compact_final(const unsigned long long* count, int64_t K, int all, const uint32_t* block_off,
+                                int64_t cap, const FinalDesc* d, hipStream_t s);
 // one filter literal of one segment -> doc bitmap (execution statistics)
 hipError_t launch_leaf_bitmap(const DevSeg* seg, int li, int flip, int64_t num_docs, uint32_t* out, hipStream_t s);
 hipError_t launch_compact(const unsigned long long* count, int64_t K, int all, uint32_t* block_sums, int64_t cap,

@@ -927,6 +927,91 @@ __device__ __forceinline__ void mv_ranges(bool hmv, const int32_t* hoff, int64_t
   }
 }
 
+typedef const __attribute__((address_space(4))) DevSeg CSegT;  // segment descriptor via the constant address space
+
+// Table-wide keys (< 2^32 on the partitioned path) of the docs of steps h .. h+N-1 (match bits m): every group-by
+// dictId decode, then every remap gather (they overlap), then the keys.
+template <int N, int LM>
+__device__ __forceinline__ void part_keys(const DevQuery* __restrict__ q, CSegT* cs, const uint32_t* img,
+                                          int64_t doc_base, int h, uint32_t m, int lane, uint32_t (&key)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) key[i] = 0u;
+  for (int j = 0; j < q->num_gb; ++j) {
+    const int slot = q->gb_slot[j];
+    const int gl = cs->cols[slot].lds_off, gn = cs->cols[slot].nbits;
+    const uint32_t* gw = cs->cols[slot].words;
+    const int32_t* rm = cs->remap[j];
+    const uint32_t st = (uint32_t)q->gb_stride[j];
+    uint32_t id[N];
+    decode_batch<N, LM>(gl, gn, gw, img, doc_base, h, m, lane, id);
+    if (rm != nullptr) {
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        if ((m >> (h + i)) & 1u) id[i] = (uint32_t)gp(rm)[id[i]];
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) key[i] += id[i] * st;
+  }
+}
+
+// The V payload of one value column for the docs of steps h .. h+N-1: V_FMT_ID its table-wide value id (lo), V_FMT_32 /
+// V_FMT_64 its value bits (lo, hi): a dictionary gather, or the raw value (a raw DOUBLE's bits unchanged).
+template <int N, int LM, int VF>
+__device__ __forceinline__ void part_vvals(const DevQuery* __restrict__ q, CSegT* cs, const uint32_t* img,
+                                           int64_t doc_base, int h, uint32_t m, int lane, uint32_t (&lo)[N],
+                                           uint32_t (&hi)[N]) {
+  auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
+#pragma unroll
+  for (int i = 0; i < N; ++i) lo[i] = hi[i] = 0u;
+  if constexpr (VF == V_FMT_ID || VF == V_FMT_32 || VF == V_FMT_64) {
+    const int va = q->emit_val_agg;
+    const int vslot = q->aggs[va].slot;
+    const int vkind = cs->cols[vslot].kind;
+    const int vl = cs->cols[vslot].lds_off, vn = cs->cols[vslot].nbits, vtype = cs->cols[vslot].vtype;
+    const uint32_t* vw = cs->cols[vslot].words;
+    const uint64_t* vd = q->aggs[va].src == SRC_DOUBLE ? (const uint64_t*)cs->cols[vslot].dict_f64
+                                                        : (const uint64_t*)cs->cols[vslot].dict_i64;
+    const int32_t* vrm = cs->vremap;
+    const void* vraw = cs->cols[vslot].raw;
+    if (vkind == COL_SV_DICT) {
+      uint32_t vid[N];
+      decode_batch<N, LM>(vl, vn, vw, img, doc_base, h, m, lane, vid);
+      if constexpr (VF == V_FMT_ID) {
+        if (vrm != nullptr) {
+#pragma unroll
+          for (int i = 0; i < N; ++i)
+            if ((m >> (h + i)) & 1u) vid[i] = (uint32_t)gp(vrm)[vid[i]];
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) lo[i] = vid[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          if (!((m >> (h + i)) & 1u)) continue;
+          const uint64_t v = gp(vd)[vid[i]];
+          lo[i] = (uint32_t)v;
+          hi[i] = (uint32_t)(v >> 32);
+        }
+      }
+    } else if (vtype == PA_INT) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        if (!((m >> (h + i)) & 1u)) continue;
+        lo[i] = (uint32_t)gp((const int32_t*)vraw)[doc_base + local(h + i)];
+        hi[i] = (uint32_t)((int32_t)lo[i] >> 31);
+      }
+    } else {  // LONG, or DOUBLE bits (a SUM/MIN/MAX over a raw DOUBLE column reads the bits unchanged)
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        if (!((m >> (h + i)) & 1u)) continue;
+        const uint64_t v = gp((const uint64_t*)vraw)[doc_base + local(h + i)];
+        lo[i] = (uint32_t)v;
+        hi[i] = (uint32_t)(v >> 32);
+      }
+    }
+  }
+}
+
 // The matching docs of one tile (match words m) in the count pass (STRAT_PCOUNT: per (workgroup, partition) record
 // counts in LDS) or the emit pass (STRAT_PEMIT: the records into the partition bins). Per batch of 8 steps: every
 // group-by dictId decode, then every remap gather (they overlap), then the table-wide keys; then per stream.
@@ -936,10 +1021,8 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
                                           unsigned char* lds, const PartScratch& ps) {
   // Descriptors through the constant address space: the segment is read-only during the kernel and its pointer is
   // wave-uniform, so every field is a scalar load the compiler keeps across the LDS atomics and the record stores.
-  typedef const __attribute__((address_space(4))) DevSeg CSeg;
-  CSeg* cs = (CSeg*)(uintptr_t)seg;
+  CSegT* cs = (CSegT*)(uintptr_t)seg;
   auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
-  const int ngb = q->num_gb;
   const int pv = q->pv;
   const int ksv = q->kshift_v, ksh = q->kshift_h;
   const int ha = q->hll_agg;
@@ -953,24 +1036,7 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
   for (int h = 0; h < STEPS; h += kEB) {
     if (__ballot((m >> h) != 0) == 0) break;  // wave-uniform: the H records below shuffle across all 64 lanes
     uint32_t key[kEB];
-#pragma unroll
-    for (int i = 0; i < kEB; ++i) key[i] = 0u;
-    for (int j = 0; j < ngb; ++j) {
-      const int slot = q->gb_slot[j];
-      const int gl = cs->cols[slot].lds_off, gn = cs->cols[slot].nbits;
-      const uint32_t* gw = cs->cols[slot].words;
-      const int32_t* rm = cs->remap[j];
-      const uint32_t st = (uint32_t)q->gb_stride[j];
-      uint32_t id[kEB];
-      decode_batch<kEB, LM>(gl, gn, gw, img, doc_base, h, m, lane, id);
-      if (rm != nullptr) {
-#pragma unroll
-        for (int i = 0; i < kEB; ++i)
-          if ((m >> (h + i)) & 1u) id[i] = (uint32_t)gp(rm)[id[i]];
-      }
-#pragma unroll
-      for (int i = 0; i < kEB; ++i) key[i] += id[i] * st;  // table-wide key (< 2^32 on this path)
-    }
+    part_keys<kEB, LM>(q, cs, img, doc_base, h, m, lane, key);  // table-wide key (< 2^32 on this path)
     if constexpr (STRAT == STRAT_PCOUNT) {
       lds_u32_t* hist = lds_ptr(lds);
       uint32_t n[kEB];
@@ -998,55 +1064,7 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
         lds_u32_t* bins = lds_ptr(lds + q->lds_bins_v);
         const uint32_t kmask = (1u << ksv) - 1u;
         uint32_t lo[kEB], hi[kEB];
-#pragma unroll
-        for (int i = 0; i < kEB; ++i) lo[i] = hi[i] = 0u;
-        if constexpr (VF == V_FMT_ID || VF == V_FMT_32 || VF == V_FMT_64) {
-          const int va = q->emit_val_agg;
-          const int vslot = q->aggs[va].slot;
-          const int vkind = cs->cols[vslot].kind;
-          const int vl = cs->cols[vslot].lds_off, vn = cs->cols[vslot].nbits, vtype = cs->cols[vslot].vtype;
-          const uint32_t* vw = cs->cols[vslot].words;
-          const uint64_t* vd = q->aggs[va].src == SRC_DOUBLE ? (const uint64_t*)cs->cols[vslot].dict_f64
-                                                              : (const uint64_t*)cs->cols[vslot].dict_i64;
-          const int32_t* vrm = cs->vremap;
-          const void* vraw = cs->cols[vslot].raw;
-          if (vkind == COL_SV_DICT) {
-            uint32_t vid[kEB];
-            decode_batch<kEB, LM>(vl, vn, vw, img, doc_base, h, m, lane, vid);
-            if constexpr (VF == V_FMT_ID) {
-              if (vrm != nullptr) {
-#pragma unroll
-                for (int i = 0; i < kEB; ++i)
-                  if ((m >> (h + i)) & 1u) vid[i] = (uint32_t)gp(vrm)[vid[i]];
-              }
-#pragma unroll
-              for (int i = 0; i < kEB; ++i) lo[i] = vid[i];
-            } else {
-#pragma unroll
-              for (int i = 0; i < kEB; ++i) {
-                if (!((m >> (h + i)) & 1u)) continue;
-                const uint64_t v = gp(vd)[vid[i]];
-                lo[i] = (uint32_t)v;
-                hi[i] = (uint32_t)(v >> 32);
-              }
-            }
-          } else if (vtype == PA_INT) {
-#pragma unroll
-            for (int i = 0; i < kEB; ++i) {
-              if (!((m >> (h + i)) & 1u)) continue;
-              lo[i] = (uint32_t)gp((const int32_t*)vraw)[doc_base + local(h + i)];
-              hi[i] = (uint32_t)((int32_t)lo[i] >> 31);
-            }
-          } else {  // LONG, or DOUBLE bits (a SUM/MIN/MAX over a raw DOUBLE column reads the bits unchanged)
-#pragma unroll
-            for (int i = 0; i < kEB; ++i) {
-              if (!((m >> (h + i)) & 1u)) continue;
-              const uint64_t v = gp((const uint64_t*)vraw)[doc_base + local(h + i)];
-              lo[i] = (uint32_t)v;
-              hi[i] = (uint32_t)(v >> 32);
-            }
-          }
-        }
+        part_vvals<kEB, LM, VF>(q, cs, img, doc_base, h, m, lane, lo, hi);
         if constexpr (VF != V_FMT_GEN) {
           // the batch's records (one per matching doc of the kEB steps) in one put: every LDS phase runs once
           bool act[kEB];
@@ -1875,6 +1893,7 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
     if constexpr (STRAT != STRAT_LANE_CNT) lane_acc_tile<LM, STEPS, STRAT>(q, seg, img, doc_base, m, lane, la);
   } else if constexpr (STRAT == STRAT_PCOUNT || is_pemit(STRAT)) {
     part_tile<STRAT, STEPS, LM>(q, seg, img, doc_base, m, lane, lds, ps);
+
   } else if (q->has_mv) {
     for (int i = 0; i < STEPS; ++i)
       if ((m >> i) & 1u) accumulate_doc_mv<STRAT>(q, seg, img, local(i), doc_base + local(i), acc);

@@ -127,6 +127,36 @@ class IntermediateResult:
     num_entries_scanned_post_filter: int = 0
 
 
+class PinnedPool:
+    """Page-locked host buffers (pa_host_alloc) reused across fetches: pa_query_fetch DMAs every result column straight
+    into them. Arrays handed out are views, valid until the pool's next fetch. One pool per process (OUTPUT_POOL): a
+    server's queries fetch one after another, and pinning memory costs far more than a fetch."""
+
+    def __init__(self):
+        self.bufs = {}  # slot -> (address, bytes)
+
+    def array(self, slot, count, dtype):
+        dt = np.dtype(dtype)
+        need = max(16, int(count) * dt.itemsize)
+        addr, size = self.bufs.get(slot, (None, 0))
+        if size < need:
+            if addr:
+                L.lib().pa_host_free(addr)
+            size = max(need, size * 2)
+            addr = L.check_ptr(L.lib().pa_host_alloc(size), "pa_host_alloc")
+            self.bufs[slot] = (addr, size)
+        raw = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(addr))
+        return raw[:int(count) * dt.itemsize].view(dt)
+
+    def close(self):
+        for addr, _ in self.bufs.values():
+            L.lib().pa_host_free(addr)
+        self.bufs = {}
+
+
+OUTPUT_POOL = PinnedPool()
+
+
 def _flatten_filter(f, leaves, ops):
     """Filter tree -> leaves + postfix program (PA_OP_*)."""
     if isinstance(f, (Q.And, Q.Or)):
@@ -403,26 +433,29 @@ class GpuQueryExecutor:
         out["plan"]["limit_trimming"] = int(L.lib().pa_query_limit_trimming(self.handle))
         return out
 
-    def fetch_arrays(self, stream=None):
+    def fetch_arrays(self, stream=None, pooled=False):
         """Non-empty groups in ascending table-wide key order as arrays: (keys int64[n], counts int64[n],
-        [one array per GPU accumulator: float64[n], or uint8[n << log2m] HLL registers]). Synchronises `stream`."""
+        [one array per GPU accumulator: float64[n], or uint8[n << log2m] HLL registers]). Synchronises `stream`.
+        pooled=True: the arrays are views of the process's page-locked output pool (OUTPUT_POOL: each column arrives by
+        one DMA; valid until the next pooled fetch of any executor) instead of fresh arrays."""
         lib = L.lib()
+        alloc = (lambda slot, n, dt: OUTPUT_POOL.array(slot, n, dt)) if pooled else (lambda slot, n, dt: np.empty(n, dt))
         cap = 1 if not self.query.group_by else min(self.num_keys, 1 << 16)
         if self.query.group_by and self.num_keys > 1 << 16:
             # large key space: a capacity-0 call runs only the GPU count pass and returns the number of non-empty
             # groups, so the gather + copy run once, at the exact size
             cap = max(1, L.check(lib.pa_query_fetch(self.handle, stream, 0, None, None, None), "pa_query_fetch"))
         while True:
-            keys = np.empty(cap, dtype=np.int64)
-            counts = np.empty(cap, dtype=np.int64)
+            keys = alloc("keys", cap, np.int64)
+            counts = alloc("counts", cap, np.int64)
             outs, ptrs = [], (ctypes.c_void_p * max(1, len(self.pa_aggs)))()
             for i, (t, _, log2m) in enumerate(self.pa_aggs):
                 if t == L.PA_AGG_DISTINCTCOUNTHLL:
-                    o = np.empty(cap << log2m, dtype=np.uint8)
+                    o = alloc(i, cap << log2m, np.uint8)
                 elif t == L.PA_AGG_DISTINCTCOUNT:
-                    o = np.empty(cap * self._presence_stride(i), dtype=np.uint8)
+                    o = alloc(i, cap * self._presence_stride(i), np.uint8)
                 else:
-                    o = np.empty(cap, np.float64)
+                    o = alloc(i, cap, np.float64)
                 outs.append(o)
                 ptrs[i] = o.ctypes.data
             n = L.check(lib.pa_query_fetch(self.handle, stream, cap, keys.ctypes.data, counts.ctypes.data, ptrs),
@@ -495,7 +528,7 @@ class GpuQueryExecutor:
         q = self.query
         if not self.segs:
             return self._empty_result()
-        keys, counts, outs = self.fetch_arrays(stream)
+        keys, counts, outs = self.fetch_arrays(stream, pooled=True)  # (converted to Python objects below)
         n = len(keys)
         res = IntermediateResult(list(q.aggregations), list(q.group_by))
         res.num_total_docs = sum(s.num_docs for s in self.all_segs)
