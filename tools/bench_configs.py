@@ -145,6 +145,13 @@ WORKLOADS = {
         ("default_limit", "SELECT d1, d2, d3, d4, SUM(r), DISTINCTCOUNTHLLMV(tags) FROM t GROUP BY d1, d2, d3, d4 "
                           "LIMIT 1000000", 0),
     ]),
+    # MV group-by (a doc expands into one key per value of tags): 64 x 4096 keys, so the default numGroupsLimit (100000)
+    # binds in every segment and the sorted-form first-seen trimming runs (a11'); untrimmed for comparison
+    "mvgroup": (star_segment, [
+        ("untrimmed", "SELECT d3, tags, COUNT(*), SUM(r) FROM t GROUP BY d3, tags LIMIT 1000000 "
+                      "OPTION(numGroupsLimit=1000000)", 0),
+        ("default_limit", "SELECT d3, tags, COUNT(*), SUM(r) FROM t GROUP BY d3, tags LIMIT 1000000", 0),
+    ]),
 }
 
 
