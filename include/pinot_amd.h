@@ -199,6 +199,8 @@ typedef struct {
                                              (default: a V launch and an H launch, each holding only its own bins) */
 #define PA_QF_NO_LIMIT_WALK (1 << 25)     /* numGroupsLimit: first-position + sort trimming even where the prefix walk applies */
 #define PA_QF_NO_LANE_ACC (1 << 26)       /* aggregation-only query: LDS/global accumulators instead of per-lane registers */
+#define PA_QF_NO_LANE_HIST (1 << 27)      /* aggregation-only SUM over a shared dictionary: gather each doc's value instead
+                                             of counting dictIds in an LDS histogram */
 #define PA_QF_PART_SHIFT 22               /* bits 22..23: LDS per partition of the partitioned aggregation (0 = auto,
                                              1 = 64 KiB, 2 = 96 KiB, 3 = 144 KiB): larger partitions = fewer record
                                              write fronts per XCD */

@@ -32,6 +32,7 @@ PA_QF_PART_SHIFT = 22
 PA_QF_NO_SPLIT_EMIT = 1 << 24
 PA_QF_NO_LIMIT_WALK = 1 << 25
 PA_QF_NO_LANE_ACC = 1 << 26
+PA_QF_NO_LANE_HIST = 1 << 27
 PA_ACC_COUNT_U64, PA_ACC_SUM_I64, PA_ACC_SUM_F64, PA_ACC_MIN_I64, PA_ACC_MAX_I64, PA_ACC_HLL_U8, \
     PA_ACC_SUM_I64X2, PA_ACC_DOCS_U64, PA_ACC_KEYS_I64, PA_ACC_PRESENCE_U8 = range(10)
 ABI_VERSION = 2

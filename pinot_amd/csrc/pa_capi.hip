@@ -545,8 +545,7 @@ struct pa_query {
   int64_t walk_words = 0;
   DevBuf lim_admit;
   int limit_grid = 0;
-  DevBuf lim_keys, lim_pos, lim_sk, lim_sorted, lim_thresh, lim_temp;
-  size_t lim_temp_bytes = 0;
+  DevBuf lim_keys, lim_pos, lim_hist, lim_sel, lim_thresh;
   std::vector<LmSegPlan> hplans;
   std::vector<DevBuf> owned;  // LUTs, remaps, HLL LUTs, value dictionaries
   DevBuf acc;                 // all accumulator sections (unless the caller provided the block)
@@ -563,10 +562,9 @@ struct pa_query {
     dev_free(dsegs_count);
     dev_free(lim_keys);
     dev_free(lim_pos);
-    dev_free(lim_sk);
-    dev_free(lim_sorted);
+    dev_free(lim_hist);
+    dev_free(lim_sel);
     dev_free(lim_thresh);
-    dev_free(lim_temp);
     dev_free(lim_admit);
     if (host_acc) (void)hipHostFree(host_acc);
     dev_free(fetch_blocks);
@@ -1596,7 +1594,27 @@ int plan_kernels(pa_query* q, Prep& P, TilePlan& plan, TilePlan& count_plan) {
       else if (!other && any_dict && !any_raw) lane_strat = STRAT_LANE_DICT;
     }
     // the lane accumulators' LDS slots (kLaneAccBytes per thread and aggregation; none for COUNT only)
-    const size_t lane_b = lane_strat == STRAT_LANE_CNT ? 0 : (size_t)s.num_aggs * kWGSize * kLaneAccBytes;
+    size_t lane_b = lane_strat == STRAT_LANE_CNT ? 0 : (size_t)s.num_aggs * kWGSize * kLaneAccBytes;
+    // dictionary kernel: a SUM over a column whose dictionary every bound segment shares (same values) counts dictIds in
+    // an LDS histogram instead of gathering a value per doc, when the histogram fits (kLaneHistMax ids)
+    for (int a = 0; a < s.num_aggs; ++a) {
+      q->hq.aggs[a].hist_card = 0;
+      q->hq.aggs[a].hist_off = 0;
+      if (lane_strat != STRAT_LANE_DICT || s.aggs[a].type != PA_AGG_SUM || q->nseg == 0) continue;
+      const Column* c0 = q->segs[0]->cols.at(s.aggs[a].column_id);
+      if (c0->cardinality > kLaneHistMax || c0->hvals.size() != (size_t)c0->cardinality) continue;
+      bool shared = true;
+      for (int si = 1; si < q->nseg && shared; ++si) {
+        const Column* c = q->segs[si]->cols.at(s.aggs[a].column_id);
+        shared = c->cardinality == c0->cardinality && c->vtype == c0->vtype && c->dict_hash == c0->dict_hash &&
+                 c->hvals == c0->hvals;
+      }
+      if (!shared || (s.flags & PA_QF_NO_LANE_HIST)) continue;
+      lane_b = (lane_b + 15) & ~(size_t)15;
+      q->hq.aggs[a].hist_card = c0->cardinality;
+      q->hq.aggs[a].hist_off = (int32_t)lane_b;
+      lane_b += (size_t)c0->cardinality * 4;
+    }
     plan = plan_pick(lane_strat, lane_b);
     if (plan.score >= 0) {
       q->strategy = lane_strat;
@@ -1780,20 +1798,26 @@ int plan_limit_buffers(pa_query* q, const Prep& P, int cus, int64_t total_tiles)
   const size_t hb = (size_t)H * 8;
   int rc = dev_alloc(q->lim_keys, hb);
   if (!rc) rc = dev_alloc(q->lim_pos, hb);
-  if (!rc) rc = dev_alloc(q->lim_sk, hb);
-  if (!rc) rc = dev_alloc(q->lim_sorted, hb);
-  if (!rc) rc = dev_alloc(q->lim_thresh, (size_t)std::max(1, q->nseg) * 8);
-  if (rc) return rc;
-  q->lim_temp_bytes = 0;
-  PA_HIP(sort_u64(nullptr, &q->lim_temp_bytes, nullptr, nullptr, (int64_t)H, nullptr));
-  rc = dev_alloc(q->lim_temp, std::max<size_t>(q->lim_temp_bytes, 16));
+  const size_t ns = (size_t)std::max(1, q->nseg);
+  if (!rc) rc = dev_alloc(q->lim_hist, ns * 256 * 4);
+  if (!rc) rc = dev_alloc(q->lim_sel, ns * 16);
+  if (!rc) rc = dev_alloc(q->lim_thresh, ns * 8);
   if (rc) return rc;
   LimitDesc& F = q->limit;
   F.fkeys = (long long*)q->lim_keys.p;
   F.fpos = (unsigned long long*)q->lim_pos.p;
   F.fmask = (int64_t)H - 1;
-  F.sk = (unsigned long long*)q->lim_sk.p;
-  F.sorted = (unsigned long long*)q->lim_sorted.p;
+  F.hist = (uint32_t*)q->lim_hist.p;
+  F.prefix = (unsigned long long*)q->lim_sel.p;
+  F.rank = (long long*)q->lim_sel.p + ns;
+  F.nseg = q->nseg;
+  {  // first positions doc << eb | expansion index are below 2^(bits(max docs) + eb)
+    int64_t maxd = 1;
+    for (int si = 0; si < q->nseg; ++si) maxd = std::max<int64_t>(maxd, q->segs[si]->num_docs);
+    int b = 0;
+    while (b < 63 && (int64_t(1) << b) < maxd) ++b;
+    F.pos_bits = std::max(8, b + P.limit_eb);
+  }
   F.thresh = (unsigned long long*)q->lim_thresh.p;
   F.reached = q->hq.matched_docs + 2;
   F.limit = s.num_groups_limit;
@@ -2071,7 +2095,7 @@ int pa_query_scan(pa_query* q, void* stream) {
     if (q->walk_words > kWalkMaxWords) PA_HIP(hipMemsetAsync(q->lim_admit.p, 0, q->lim_admit.n, st));
     PA_HIP(launch_limit_walk((const DevQuery*)q->dq.p, (const DevSeg*)q->dsegs.p, q->nseg, q->walk_words, st));
   }
-  if (q->limit_mode) {  // first-seen positions, sort, thresholds, admitted aggregation
+  if (q->limit_mode) {  // first-seen positions, per-segment selection of the threshold, admitted aggregation
     const DevQuery* dq = (const DevQuery*)q->dq.p;
     const DevSeg* ds = (const DevSeg*)q->dsegs.p;
     const LimitDesc& F = q->limit;
@@ -2079,10 +2103,10 @@ int pa_query_scan(pa_query* q, void* stream) {
     PA_HIP(launch_fill_i64((int64_t*)F.fkeys, H, INT64_MAX, st));
     PA_HIP(launch_fill_i64((int64_t*)F.fpos, H, -1, st));
     PA_HIP(launch_fill_i64((int64_t*)F.thresh, std::max(1, q->nseg), -1, st));
+    PA_HIP(launch_fill_i64((int64_t*)F.hist, std::max(1, q->nseg) * 128, 0, st));
     PA_HIP(launch_limit_passes(dq, ds, F, q->limit_grid, 0, st));
-    size_t tb = q->lim_temp_bytes;
-    PA_HIP(sort_u64(q->lim_temp.p, &tb, F.sk, F.sorted, H, st));
     PA_HIP(launch_limit_passes(dq, ds, F, q->limit_grid, 1, st));
+    PA_HIP(launch_limit_passes(dq, ds, F, q->limit_grid, 2, st));
     return PA_OK;
   }
   if (q->partitioned) {  // count pass, range offsets, emit pass into the partitions, per-partition aggregation

@@ -46,6 +46,7 @@ enum Strategy : int32_t {
 __host__ __device__ constexpr bool is_lane(int s) { return s >= STRAT_LANE && s <= STRAT_LANE_DICT; }
 constexpr int kLaneAggs = 4;  // STRAT_LANE: at most this many aggregations (COUNT included)
 constexpr int kLaneAccBytes = 20;  // STRAT_LANE: LDS bytes per thread and aggregation (int64 pair + a dictId)
+constexpr int kLaneHistMax = 16384;  // STRAT_LANE_DICT: largest shared dictionary counted in an LDS histogram
 // The emit pass's kernel variant (launch code): the V record format (-1: no V stream) and whether there is an H stream
 // are template parameters, so each variant's record loop is straight-line code (no per-record format branches).
 // `big`: 16-wave workgroups (the partition bins and their state are per workgroup, so sharing them among more waves
@@ -145,6 +146,10 @@ struct DevAgg {
   int64_t nvals;             // DISTINCTCOUNT: presence bytes per key (table-wide values, rounded up to 16)
   int32_t lds_off;           // LDS strategy / partition aggregation: byte offset of the WG-private copy
   int32_t pay_off;           // partitioned aggregation, V_FMT_GEN: word offset of the value inside a V record
+  // STRAT_LANE_DICT, SUM over a dictionary column that every bound segment shares: per-workgroup dictId counts in LDS
+  // (u32[hist_card] at byte hist_off); the sum is sum(count[id] * dict[id]) once at the end (no per-doc gather)
+  int32_t hist_card;         // 0 = the per-doc gather path
+  int32_t hist_off;
 };
 
 struct DevQuery {

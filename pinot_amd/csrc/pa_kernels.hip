@@ -14,8 +14,9 @@ namespace pa {
 // there (doc << eb | expansion index) is among the numGroupsLimit smallest first positions of the segment's distinct
 // keys. Three steps over all segments at once:
 //   1. limit_first_kernel: atomicMin of the position of every (matching doc, expanded key) into a (segment, key) table;
-//   2. radix-sort the words (segment << 52 | first position) (pa_sort.hip) and read off each segment's L-th smallest
-//      position: threshold T[s] = that position + 1 (limit_threshold_kernel);
+//   2. per segment, select the L-th smallest first position by 8-bit digit passes from the top (limit_hist_kernel
+//      counts the digits of the entries still in the running, limit_pick_kernel picks the digit holding the rank):
+//      threshold T[s] = that position + 1;
 //   3. limit_agg_kernel: the aggregation over matching docs, admitting (doc, key) iff first[s, key] < T[s].
 // These are per-doc kernels (no staged tiles): this path only runs when the limit can bind.
 
@@ -124,28 +125,77 @@ __global__ void __launch_bounds__(256) limit_first_kernel(const DevQuery* __rest
   });
 }
 
-// sort words: (segment << 52) | first position; empty slots sort last
-__global__ void limit_sortkeys_kernel(const DevQuery* __restrict__ q, LimitDesc F) {
+// Radix select of every segment's L-th smallest first position (L = numGroupsLimit; first positions are distinct within
+// a segment: each belongs to one (doc, expansion) and so to one key). One digit pass per 8 bits from the top: count the
+// digits of the entries whose higher digits equal the segment's prefix (per-workgroup LDS histograms when the segments'
+// histograms fit, flushed with one global add per nonzero bucket), then per segment pick the digit holding the wanted
+// rank. After the last pass the prefix is the L-th smallest value itself.
+constexpr int kSelBuckets = 256;
+constexpr int kSelLdsSegs = 48;  // LDS histograms up to this many segments (48 KiB)
+
+__global__ void __launch_bounds__(256) limit_hist_kernel(LimitDesc F, int nseg, int shift, int first) {
+  __shared__ uint32_t lh[kSelLdsSegs * kSelBuckets];
+  const bool lds = nseg <= kSelLdsSegs;
+  if (lds) {
+    for (int i = threadIdx.x; i < nseg * kSelBuckets; i += 256) lh[i] = 0u;
+    __syncthreads();
+  }
   const int64_t n = F.fmask + 1;
-  const int nseg = q->num_segments;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const long long ck = F.fkeys[i];
-    F.sk[i] = ck == INT64_MAX ? ~0ull : (((unsigned long long)(ck % nseg) << 52) | F.fpos[i]);
+    if (ck == INT64_MAX) continue;
+    const int s = (int)(ck % nseg);
+    const unsigned long long v = F.fpos[i];
+    // (a rank < 0: the segment is out of the selection; the entries above the prefix's digits do not count)
+    if (!first && (F.rank[s] < 0 || ((v ^ F.prefix[s]) >> (shift + 8)) != 0)) continue;
+    const uint32_t d = (uint32_t)(v >> shift) & (kSelBuckets - 1);
+    if (lds) atomicAdd(&lh[s * kSelBuckets + d], 1u);
+    else __hip_atomic_fetch_add(&F.hist[(size_t)s * kSelBuckets + d], 1u, RLX);
+  }
+  if (lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nseg * kSelBuckets; i += 256)
+      if (lh[i]) __hip_atomic_fetch_add(&F.hist[i], lh[i], RLX);
   }
 }
 
-// sorted words: element i is the L-th of its segment iff sorted[i-L+1] has the same segment and sorted[i-L] does not
-__global__ void limit_threshold_kernel(LimitDesc F, int64_t n) {
-  const int64_t L = F.limit;
-  const unsigned long long* w = F.sorted;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const unsigned long long v = w[i];
-    if (v == ~0ull || i < L - 1) continue;
-    const unsigned long long s = v >> 52;
-    if ((w[i - L + 1] >> 52) != s) continue;
-    if (i - L >= 0 && (w[i - L] >> 52) == s) continue;
-    F.thresh[s] = (v & ((1ull << 52) - 1)) + 1;
-    __hip_atomic_fetch_add(F.reached, 1ull, RLX);  // this segment has >= numGroupsLimit groups
+// One wave per segment: the digit whose cumulative count first reaches the wanted rank (the first pass also decides
+// whether the segment holds L groups at all); the histogram is cleared for the next pass. Last pass: the threshold.
+__global__ void __launch_bounds__(64) limit_pick_kernel(LimitDesc F, int shift, int first, int last) {
+  const int s = blockIdx.x;
+  const int lane = threadIdx.x;
+  uint32_t* h = F.hist + (size_t)s * kSelBuckets;
+  uint32_t c[kSelBuckets / 64];
+  uint64_t tot = 0;
+  for (int j = 0; j < kSelBuckets / 64; ++j) {  // lane owns buckets 4 lane .. 4 lane + 3
+    c[j] = h[4 * lane + j];
+    tot += c[j];
+  }
+  uint64_t incl = tot;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  const uint64_t all = __shfl(incl, 63, 64);
+  long long r = first ? (long long)F.limit : F.rank[s];
+  const bool active = first ? (int64_t)all >= F.limit : r >= 0;
+  for (int j = 0; j < kSelBuckets / 64; ++j) h[4 * lane + j] = 0u;
+  if (!active) {
+    if (lane == 0 && first) F.rank[s] = -1;
+    return;
+  }
+  uint64_t below = incl - tot;  // entries in lower buckets of this lane's first bucket
+  for (int j = 0; j < kSelBuckets / 64; ++j) {
+    if ((long long)below < r && (long long)(below + c[j]) >= r) {
+      const unsigned long long p = (first ? 0ull : F.prefix[s]) | ((unsigned long long)(4 * lane + j) << shift);
+      F.prefix[s] = p;
+      F.rank[s] = r - (long long)below;
+      if (last) {
+        F.thresh[s] = p + 1;  // admit first positions up to and including the L-th
+        __hip_atomic_fetch_add(F.reached, 1ull, RLX);  // this segment has >= numGroupsLimit groups
+      }
+    }
+    below += c[j];
   }
 }
 
@@ -300,14 +350,21 @@ hipError_t launch_limit_walk(const DevQuery* q, const DevSeg* segs, int nseg, in
 hipError_t launch_limit_passes(const DevQuery* q, const DevSeg* segs, const LimitDesc& F, int grid, int phase,
                                hipStream_t s) {
   const int64_t n = F.fmask + 1;
-  const int g = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  const int g = (int)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
   switch (phase) {
     case 0:
       limit_first_kernel<<<grid, 256, 0, s>>>(q, segs, F);
-      limit_sortkeys_kernel<<<g, 256, 0, s>>>(q, F);
       break;
-    case 1:
-      limit_threshold_kernel<<<g, 256, 0, s>>>(F, n);
+    case 1: {
+      const int nseg = F.nseg;
+      const int passes = (F.pos_bits + 7) / 8;
+      for (int p = 0; p < passes; ++p) {
+        const int shift = 8 * (passes - 1 - p);
+        limit_hist_kernel<<<g, 256, 0, s>>>(F, nseg, shift, p == 0);
+        limit_pick_kernel<<<nseg, 64, 0, s>>>(F, shift, p == 0, p == passes - 1);
+      }
+    } break;
+    case 2:
       limit_agg_kernel<<<grid, 256, 0, s>>>(q, segs, F);
       break;
     default: return hipErrorInvalidValue;

@@ -40,20 +40,22 @@ struct LimitDesc {
   long long* fkeys;              // composite key: accumulator slot * num_segments + segment; INT64_MAX = empty
   unsigned long long* fpos;      // first position (doc << eb | expansion index); UINT64_MAX = none
   int64_t fmask;                 // slots - 1 (power of two)
-  unsigned long long* sk;        // sort input [slots]
-  unsigned long long* sorted;    // sort output [slots]
+  uint32_t* hist;                // radix select: [num_segments][256] digit counts of the current pass
+  unsigned long long* prefix;    // radix select: [num_segments] the selected value's digits found so far
+  long long* rank;               // radix select: [num_segments] rank still to find among the prefix's values (1-based;
+                                 // < 0: the segment has fewer than `limit` groups, nothing is trimmed)
   unsigned long long* thresh;    // [num_segments]: first positions below it are admitted; UINT64_MAX = all
   unsigned long long* reached;   // segments whose distinct groups reached the limit (GroupByOperator.java:112)
   int64_t limit;                 // numGroupsLimit
   int32_t eb;                    // expansion-index bits
+  int32_t pos_bits;              // first positions are < 2^pos_bits (radix select digit passes)
+  int32_t nseg;                  // segments of the query
   int32_t pad;
 };
-// phase 0: first-seen positions + sort words; phase 1: thresholds + aggregation
+// phase 0: first-seen positions; 1: per segment the numGroupsLimit-th smallest first position (radix select, 8-bit
+// digits from the top) -> thresholds; 2: aggregation of the admitted (doc, key) pairs
 hipError_t launch_limit_passes(const DevQuery* q, const DevSeg* segs, const LimitDesc& F, int grid, int phase,
                                hipStream_t s);
-// hipcub radix sort of n 64-bit words (pa_sort.hip); temp == nullptr: *temp_bytes = the scratch size needed
-hipError_t sort_u64(void* temp, size_t* temp_bytes, const unsigned long long* in, unsigned long long* out, int64_t n,
-                    hipStream_t s);
 // numGroupsLimit walk form: one workgroup per segment with a non-null DevSeg::admit; `words` = bitmap words (K / 32)
 constexpr int64_t kWalkMaxWords = 40000;  // LDS bitmap of at most 160000 bytes
 hipError_t launch_limit_walk(const DevQuery* q, const DevSeg* segs, int nseg, int64_t words, hipStream_t s);

@@ -1608,6 +1608,26 @@ __device__ __forceinline__ void lane_sparse(uint32_t m, int type, int src, LOAD 
   }
 }
 
+// lane_sparse for a dictId histogram: every matching doc adds one to hist[dictId] (dec(i) = dictId of doc i); the
+// decodes of a batch of four are issued before their (non-returning) LDS adds.
+template <class DEC>
+__device__ __forceinline__ void lane_sparse_hist(uint32_t m, DEC dec, lds_u32_t* hist) {
+  while (__ballot(m != 0) != 0) {
+    bool on[4];
+    uint32_t id[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      on[k] = m != 0;
+      const int i = on[k] ? __builtin_ctz(m) : 0;
+      m &= m - 1u;
+      id[k] = on[k] ? dec(i) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (on[k]) __hip_atomic_fetch_add(hist + id[k], 1u, WG_RLX);
+  }
+}
+
 // lane_sparse for MIN / MAX of a sorted dictionary: the smallest / largest matching dictId (dec(i) = dictId of doc i).
 template <class DEC>
 __device__ __forceinline__ void lane_sparse_ids(uint32_t m, bool is_min, DEC dec, uint32_t& rid) {
@@ -1672,7 +1692,7 @@ __device__ __forceinline__ void lane_raw_dense(const char* tile, uint32_t m, int
 template <int LM, int STEPS, int STRAT>
 __device__ __forceinline__ void lane_acc_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
                                               const uint32_t* img, int64_t doc_base, uint32_t m, int lane,
-                                              LaneAcc& la) {
+                                              LaneAcc& la, unsigned char* lds) {
   typedef const __attribute__((address_space(4))) DevSeg CSeg;
   CSeg* cs = (CSeg*)(uintptr_t)seg;
   auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
@@ -1730,6 +1750,14 @@ __device__ __forceinline__ void lane_acc_tile(const DevQuery* __restrict__ q, co
     }
     if (STRAT == STRAT_LANE_RAW) break;  // (the raw kernel's columns are all raw: handled above)
     if constexpr (STRAT == STRAT_LANE_DICT) {
+      if (type == PA_AGG_SUM && q->aggs[a].hist_card > 0) {
+        // shared dictionary: count the dictIds in the workgroup's LDS histogram (the values come in at the end)
+        lds_u32_t* hist = lds_ptr(lds + q->aggs[a].hist_off);
+        lane_sparse_hist(m, [&](int i) -> uint32_t {
+          return loff >= 0 ? decode_lds(img + loff, 32 * lane + i, nb) : decode_global(words, doc_base + 32 * lane + i, nb);
+        }, hist);
+        break;
+      }
       // dictionary kernel: every tile walks the lanes' set bits (a lane's matching docs one after another, the wave
       // max-popcount times): decode from the staged image (or HBM when lazy), then MIN / MAX of a sorted dictionary on
       // the dictIds, anything else on the gathered values. One path (no per-width unpack calls): nothing spills.
@@ -1890,7 +1918,7 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
     if (__ballot(m != 0) == 0) return (uint32_t)__builtin_popcount(scanned);
   }
   if constexpr (is_lane(STRAT)) {
-    if constexpr (STRAT != STRAT_LANE_CNT) lane_acc_tile<LM, STEPS, STRAT>(q, seg, img, doc_base, m, lane, la);
+    if constexpr (STRAT != STRAT_LANE_CNT) lane_acc_tile<LM, STEPS, STRAT>(q, seg, img, doc_base, m, lane, la, lds);
   } else if constexpr (STRAT == STRAT_PCOUNT || is_pemit(STRAT)) {
     part_tile<STRAT, STEPS, LM>(q, seg, img, doc_base, m, lane, lds, ps);
 
@@ -2222,6 +2250,15 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
   uint32_t matched = 0;  // docs of this lane that passed the filter (numDocsScanned)
   LaneAcc la;
   if constexpr (is_lane(STRAT) && STRAT != STRAT_LANE_CNT) lane_acc_init(q, la, smem, WGS);
+  if constexpr (STRAT == STRAT_LANE_DICT) {  // the dictId histograms of SUMs over a shared dictionary
+    for (int a = 0; a < q->num_aggs; ++a) {
+      const int hc = q->aggs[a].hist_card;
+      if (hc <= 0) continue;
+      uint32_t* h = (uint32_t*)(lds_acc + q->aggs[a].hist_off);
+      for (int i = threadIdx.x; i < hc; i += WGS) h[i] = 0u;
+    }
+    __syncthreads();
+  }
   const int64_t T = q->total_wtiles;
   const int64_t W = (int64_t)gridDim.x * WPW;
   const int64_t lb = q->xcd_major ? xcd_major_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;  // logical block
@@ -2350,6 +2387,35 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
     if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)wm, RLX);
     if constexpr (is_lane(STRAT)) {  // COUNT(*) of an aggregation-only query = the docs the filter kept
       if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->count), (unsigned long long)wm, RLX);
+      if constexpr (STRAT == STRAT_LANE_DICT) {
+        // each thread folds histogram entries t, t + WGS, ... : count * value into its lane accumulator (exact split
+        // pair for 64-bit values: count < 2^32, so count * low32 and count * high32 fit their int64 halves)
+        __syncthreads();
+        for (int a = 0; a < q->num_aggs; ++a) {
+          const DevAgg& A = q->aggs[a];
+          if (A.hist_card <= 0) continue;
+          const uint32_t* h = (const uint32_t*)(lds_acc + A.hist_off);
+          const DevCol& c = segs[0].cols[A.slot];
+          int64_t r0, r1;
+          la_get(la, a, r0, r1);
+          for (int i = threadIdx.x; i < A.hist_card; i += WGS) {
+            const uint32_t n = h[i];
+            if (n == 0) continue;
+            if (A.src == SRC_DOUBLE) {
+              r0 = __builtin_bit_cast(int64_t, __builtin_bit_cast(double, r0) + (double)n * gp(c.dict_f64)[i]);
+            } else {
+              const int64_t v = gp(c.dict_i64)[i];
+              if (A.src == SRC_INT) {
+                r0 += (int64_t)n * v;
+              } else {
+                r0 += (int64_t)n * (int64_t)(uint32_t)v;
+                r1 += (int64_t)n * (v >> 32);
+              }
+            }
+          }
+          la_set(la, a, r0, r1);
+        }
+      }
       if constexpr (STRAT != STRAT_LANE_CNT) lane_acc_flush(q, la, lane);
     }
   }

@@ -12,6 +12,7 @@ Sum/Min/MaxAggregationFunction.aggregate. Bars: bit-exact COUNT, integer SUM, MI
 import numpy as np
 import pytest
 
+from pinot_amd import _lib as L
 from pinot_amd import parse_sql
 from pinot_amd.engine import GpuQueryExecutor, GpuSegment
 from pinot_amd.segment import create_segment
@@ -85,3 +86,31 @@ def test_lane_no_filter_and_empty_result(lane_segments):
         finally:
             ex.close()
         assert_same(got, oracle.run_query(q, segs), DOUBLE_REL)
+
+
+@pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LANE_HIST])
+def test_lane_sum_over_shared_dictionary(flags):
+    """SUM over a dictionary every bound segment shares: dictId counts in the workgroup's LDS histogram, values folded in
+    once at the end (exact split sums for 64-bit values, here up to 2^40 over ~2^18 docs: past 2^53 in total) — against
+    the oracle and against the per-doc gather path (PA_QF_NO_LANE_HIST)."""
+    rng = np.random.default_rng(11)
+    n = 200_003
+    pool_l = np.unique(rng.integers(-(1 << 40), 1 << 40, size=9000))
+    pool_d = np.unique(np.round(rng.normal(0, 1e5, size=5000), 3))
+    data = {"day": rng.integers(0, 4000, size=n).astype(np.int32), "dl": pool_l[rng.integers(0, len(pool_l), n)],
+            "dd": pool_d[rng.integers(0, len(pool_d), n)], "di": rng.integers(-1000, 1000, size=n).astype(np.int32)}
+    seg = create_segment("shared", data, {"day": "INT", "dl": "LONG", "dd": "DOUBLE", "di": "INT"})
+    g = GpuSegment(seg)
+    try:
+        for sql in ("SELECT COUNT(*), SUM(dl), SUM(dd), SUM(di) FROM t WHERE day < 3000",
+                    "SELECT SUM(dl) FROM t WHERE day < 40", "SELECT SUM(dd), MAX(dl) FROM t"):
+            q = parse_sql(sql)
+            ex = GpuQueryExecutor(q, [g, g, g], flags=flags)  # three segments, one dictionary per column
+            try:
+                assert ex.stats()["plan"]["strategy"] == "lane"
+                got = ex.run()
+            finally:
+                ex.close()
+            assert_same(got, oracle.run_query(q, [seg, seg, seg]), DOUBLE_REL)
+    finally:
+        g.close()
