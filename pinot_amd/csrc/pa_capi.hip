@@ -83,7 +83,7 @@ struct Column {
   int32_t cardinality = 0;
   int64_t total_values = 0;
   int32_t max_values = 1;   // MV: most values in one row
-  bool fits_int32 = false;  // every dictionary value (INT/LONG) fits in int32
+  bool fits_int32 = false;  // every value (dictionary or raw, INT/LONG) fits in int32
   bool dict_sorted = false; // dictionary values strictly ascending (COLF_DICT_SORTED)
   std::vector<uint64_t> hvals;  // host copy of the dictionary values (8-byte bits): table-wide value dictionaries
   uint64_t dict_hash = 0;       // FNV-1a of hvals: identical dictionaries across segments are found without a compare
@@ -318,6 +318,12 @@ int pa_segment_add_raw_column(pa_segment* seg, int32_t column_id, int32_t value_
       hipMemcpy(c->raw.p, values, (size_t)seg->num_docs * esz, hipMemcpyHostToDevice) != hipSuccess) {
     delete c;
     return fail(PA_EHIP, "raw column upload failed");
+  }
+  if (value_type == PA_LONG) {  // (Pinot's column metadata min/max): int32-range LONG metrics sum in one int64 slot
+    const int64_t* v = (const int64_t*)values;
+    bool fits = true;
+    for (int32_t i = 0; i < seg->num_docs; ++i) fits &= v[i] >= INT32_MIN && v[i] <= INT32_MAX;
+    c->fits_int32 = fits;
   }
   seg->bytes += c->raw.n;
   seg->cols[column_id] = c;
@@ -1730,6 +1736,23 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
   h.xcd_major = P.dense ? 1 : 0;
   h.lds_count_off = 0;
   h.lds_acc_bytes = (q->strategy == STRAT_LDS || is_lane(q->strategy)) ? (uint32_t)P.lds_acc : 0;
+  // LDS strategy: the one column every non-COUNT aggregation (SUM / MIN / MAX only) reads, if raw in segment 0 (the
+  // kernel checks each segment's column kind): dense lane-major tiles then load its values coalesced
+  h.lds_raw_slot = -1;
+  if (q->strategy == STRAT_LDS && q->nseg > 0) {
+    int slot = -1;
+    bool ok = true;
+    for (int a = 0; a < s.num_aggs && ok; ++a) {
+      const int t = s.aggs[a].type;
+      if (t == PA_AGG_COUNT) continue;
+      ok = (t == PA_AGG_SUM || t == PA_AGG_MIN || t == PA_AGG_MAX) && (slot < 0 || slot == P.agg_slot[a]);
+      slot = P.agg_slot[a];
+    }
+    if (ok && slot >= 0) {
+      auto it = q->segs[0]->cols.find(q->slot_cols[slot]);
+      if (it != q->segs[0]->cols.end() && it->second->kind == COL_SV_RAW) h.lds_raw_slot = slot;
+    }
+  }
   if (!q->partitioned) {
     h.hll_agg = -1;
     h.pv = 0;

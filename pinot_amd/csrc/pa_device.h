@@ -217,6 +217,8 @@ struct DevQuery {
   // V_FMT_ID INT/LONG value dictionary: the largest |value| (0 = unknown); a 64-bit SUM whose partition's record count
   // times it stays below 2^62 accumulates in one int64 instead of the 32/32-bit split pair
   uint64_t v_maxabs;
+  // STRAT_LDS, lane-major: the one raw column every non-COUNT aggregation reads (-1: none / several / not all raw)
+  int32_t lds_raw_slot, pad_raw;
 };
 // part_agg_kernel variant: -1 generic, else sum kind (0 none, 1 + AccSrc) | MIN << 2 | MAX << 3
 constexpr int kVkGeneric = -1;

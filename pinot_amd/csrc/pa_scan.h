@@ -25,6 +25,11 @@
 namespace pa {
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+// Descriptors through the constant address space: read-only during every kernel, so their fields are scalar loads the
+// compiler may keep in registers across LDS atomics and stores (a generic pointer is re-read after each of them, and
+// every scalar load's lgkmcnt wait also waits for the LDS operations in flight).
+typedef const __attribute__((address_space(4))) struct DevSeg CSegT;
+typedef const __attribute__((address_space(4))) struct DevQuery CQ;
 
 // Every HBM access goes through address-space-1 pointers: global_* instructions instead of flat_*. A flat
 // access may alias LDS, which makes the compiler put vmcnt(0) in front of later LDS reads.
@@ -82,6 +87,13 @@ __device__ __forceinline__ void vm_wait() {
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
+
+typedef __attribute__((address_space(3))) uint64_t lds_u64_t;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4_t;
+__device__ __forceinline__ lds_u32_t* lds_ptr(const void* p) { return (lds_u32_t*)(uintptr_t)lds_addr(p); }
+
+#define WG_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP
+
 
 // One LDS-DMA wave instruction (global_load_lds_dwordx4): lane l copies 16 bytes from its `src` to
 // lds_base + 16*l. Issued as inline asm on purpose: the compiler's waitcnt pass cannot disambiguate LDS-DMA
@@ -436,6 +448,184 @@ __device__ __forceinline__ void update_one(const DevAgg& A, int64_t key, const A
   }
 }
 
+// One aggregation update of group `key` in the workgroup's LDS accumulators (STRAT_LDS layout: DevAgg::lds_off), through
+// address-space-3 pointers (ds_* atomics). v: AggValue of agg_value (HLL: register << 8 | rank; DISTINCTCOUNT: value id).
+__device__ __forceinline__ void lds_update(int type, int src, int log2m, int64_t nvals, uint32_t off,
+                                           unsigned char* lds, int64_t key, const AggValue& v) {
+  unsigned char* b = lds + off;
+  switch (type) {
+    case PA_AGG_SUM:
+      if (src == SRC_INT) {
+        __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(b) + key, (uint64_t)v.i, WG_RLX);
+      } else if (src == SRC_LONG) {
+        __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(b) + 2 * key, (uint64_t)(uint32_t)v.i, WG_RLX);
+        __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(b) + 2 * key + 1, (uint64_t)(v.i >> 32), WG_RLX);
+      } else {
+        __hip_atomic_fetch_add((__attribute__((address_space(3))) double*)lds_ptr(b) + key, v.d, WG_RLX);
+      }
+      break;
+    case PA_AGG_COUNT_MV:
+      __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(b) + key, (uint64_t)v.i, WG_RLX);
+      break;
+    case PA_AGG_MIN:
+    case PA_AGG_MAX: {
+      const int64_t e = src != SRC_DOUBLE ? v.i : f64_order_encode(v.d);
+      __attribute__((address_space(3))) int64_t* t = (__attribute__((address_space(3))) int64_t*)lds_ptr(b) + key;
+      if (type == PA_AGG_MIN) __hip_atomic_fetch_min(t, e, WG_RLX);
+      else __hip_atomic_fetch_max(t, e, WG_RLX);
+    } break;
+    case PA_AGG_DISTINCTCOUNTHLL:
+      __hip_atomic_fetch_max(lds_ptr(b) + ((key << log2m) + ((uint32_t)v.i >> 8)), (uint32_t)v.i & 0xffu, WG_RLX);
+      break;
+    case PA_AGG_DISTINCTCOUNT:
+      ((__attribute__((address_space(3))) uint8_t*)lds_ptr(b))[key * nvals + v.i] = 1;
+      break;
+    default: break;
+  }
+}
+
+// LDS-privatised accumulators, lane-major tile: each lane walks its own matching docs (doc 32 * lane + i), four per
+// batch — every group-by decode of the batch, then every remap gather, then every aggregation value load, then the LDS
+// updates — so a tile costs the wave max-popcount / 4 dependent round trips instead of one per 64-doc step (the
+// step-major path waits on each step's value loads before its wave-level key grouping). Lanes sharing a key meet in
+// the LDS atomics (DefaultGroupByExecutor.aggregateGroupBySV per doc).
+__device__ __forceinline__ void accumulate_lds_lm(const DevQuery* __restrict__ q_in, const DevSeg* __restrict__ seg,
+                                                  const uint32_t* img, int64_t doc_base, uint32_t m, int lane,
+                                                  unsigned char* lds) {
+  CQ* q = (CQ*)(uintptr_t)q_in;
+  CSegT* cs = (CSegT*)(uintptr_t)seg;
+  constexpr int kB = 4;
+  const int64_t d0 = doc_base + 32 * lane;
+  lds_u32_t* cnt = lds_ptr(lds + q->lds_count_off);
+  const int ngb = q->num_gb, na = q->num_aggs;
+  while (__ballot(m != 0) != 0) {
+    bool on[kB];
+    int il[kB];
+#pragma unroll
+    for (int k = 0; k < kB; ++k) {
+      on[k] = m != 0;
+      il[k] = on[k] ? __builtin_ctz(m) : 0;
+      m &= m - 1u;
+    }
+    int64_t key[kB];
+#pragma unroll
+    for (int k = 0; k < kB; ++k) key[k] = 0;
+    for (int j = 0; j < ngb; ++j) {
+      const int slot = q->gb_slot[j];
+      const int gl = cs->cols[slot].lds_off, gn = cs->cols[slot].nbits;
+      const uint32_t* gw = cs->cols[slot].words;
+      const int32_t* rm = cs->remap[j];
+      const int64_t st = q->gb_stride[j];
+      uint32_t id[kB];
+#pragma unroll
+      for (int k = 0; k < kB; ++k) {
+        id[k] = 0u;
+        if (on[k]) id[k] = gl >= 0 ? decode_lds(img + gl, 32 * lane + il[k], gn) : decode_global(gw, d0 + il[k], gn);
+      }
+      if (rm != nullptr) {
+#pragma unroll
+        for (int k = 0; k < kB; ++k)
+          if (on[k]) id[k] = (uint32_t)gp(rm)[id[k]];
+      }
+#pragma unroll
+      for (int k = 0; k < kB; ++k) key[k] += (int64_t)id[k] * st;
+    }
+#pragma unroll
+    for (int k = 0; k < kB; ++k)
+      if (on[k]) __hip_atomic_fetch_add(cnt + key[k], 1u, WG_RLX);
+    for (int a = 0; a < na; ++a) {
+      const int type = q->aggs[a].type;
+      if (type == PA_AGG_COUNT) continue;
+      const DevAgg& A = q_in->aggs[a];
+      AggValue v[kB];
+#pragma unroll
+      for (int k = 0; k < kB; ++k)
+        v[k] = on[k] ? agg_value(A, a, seg, img, 32 * lane + il[k], d0 + il[k]) : AggValue{0, 0.0};
+      const int src = q->aggs[a].src, lg = q->aggs[a].log2m;
+      const int64_t nv = q->aggs[a].nvals;
+      const uint32_t off = (uint32_t)q->aggs[a].lds_off;
+#pragma unroll
+      for (int k = 0; k < kB; ++k)
+        if (on[k]) lds_update(type, src, lg, nv, off, lds, key[k], v[k]);
+    }
+  }
+}
+
+// accumulate_lds_lm for a dense lane-major tile whose non-COUNT aggregations (SUM / MIN / MAX) all read one raw column
+// (slot q->lds_raw_slot): that column's values of the tile arrive as coalesced 16-byte loads (instruction k, lane l:
+// docs VPL * (64 k + l) + j, as in lane_raw_dense) with their match bits from the lanes owning the docs (ds_bpermute);
+// the lane decodes the group key of each such doc from the staged image (any doc of the tile is in it) and updates.
+template <int VB>
+__device__ __forceinline__ void accumulate_lds_raw_dense(const DevQuery* __restrict__ q_in,
+                                                         const DevSeg* __restrict__ seg, const uint32_t* img,
+                                                         int64_t doc_base, uint32_t m, int lane, unsigned char* lds) {
+  CQ* q = (CQ*)(uintptr_t)q_in;
+  CSegT* cs = (CSegT*)(uintptr_t)seg;
+  constexpr int VPL = 16 / VB;
+  constexpr int NI = 2048 * VB / 1024;
+  constexpr int KB = VB == 8 ? 4 : 8;  // loads in flight per batch (16 VGPRs of values)
+  const int rs = q->lds_raw_slot;
+  const int vt = cs->cols[rs].vtype;
+  const AS1 u32x4* p = (const AS1 u32x4*)((const char*)cs->cols[rs].raw + doc_base * VB) + lane;
+  lds_u32_t* cnt = lds_ptr(lds + q->lds_count_off);
+  const int ngb = q->num_gb, na = q->num_aggs;
+#pragma unroll 1
+  for (int k0 = 0; k0 < NI; k0 += KB) {
+    u32x4 w[KB];
+    uint32_t mb[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      w[k] = p[(k0 + k) * kWave];
+      const int owner = 2 * VPL * (k0 + k) + ((VPL * lane) >> 5);
+      mb[k] = ((uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)m) >> ((VPL * lane) & 31)) & ((1u << VPL) - 1u);
+    }
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int k1 = k0 + k;
+      int64_t key[VPL];
+#pragma unroll
+      for (int j = 0; j < VPL; ++j) key[j] = 0;
+      for (int g = 0; g < ngb; ++g) {
+        const int slot = q->gb_slot[g];
+        const int gl = cs->cols[slot].lds_off, gn = cs->cols[slot].nbits;
+        const uint32_t* gw = cs->cols[slot].words;
+        const int32_t* rm = cs->remap[g];
+        const int64_t st = q->gb_stride[g];
+        uint32_t id[VPL];
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+          const int dl = VPL * (64 * k1 + lane) + j;  // tile-local doc (lane-major image: any doc is decodable here)
+          id[j] = 0u;
+          if ((mb[k] >> j) & 1u) id[j] = gl >= 0 ? decode_lds(img + gl, dl, gn) : decode_global(gw, doc_base + dl, gn);
+        }
+        if (rm != nullptr) {
+#pragma unroll
+          for (int j = 0; j < VPL; ++j)
+            if ((mb[k] >> j) & 1u) id[j] = (uint32_t)gp(rm)[id[j]];
+        }
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) key[j] += (int64_t)id[j] * st;
+      }
+#pragma unroll
+      for (int j = 0; j < VPL; ++j) {
+        if (!((mb[k] >> j) & 1u)) continue;
+        const uint64_t x = VB == 8 ? ((uint64_t)w[k][2 * j + 1] << 32) | w[k][2 * j] : (uint64_t)w[k][j];
+        AggValue v;
+        if (vt == PA_INT) { v.i = (int64_t)(int32_t)(uint32_t)x; v.d = (double)v.i; }
+        else if (vt == PA_LONG) { v.i = (int64_t)x; v.d = (double)v.i; }
+        else if (vt == PA_FLOAT) { v.d = __builtin_bit_cast(float, (uint32_t)x); v.i = (int64_t)(int32_t)(uint32_t)x; }
+        else { v.d = __builtin_bit_cast(double, x); v.i = (int64_t)x; }
+        __hip_atomic_fetch_add(cnt + key[j], 1u, WG_RLX);
+        for (int a = 0; a < na; ++a) {
+          const int type = q->aggs[a].type;
+          if (type == PA_AGG_COUNT) continue;
+          lds_update(type, q->aggs[a].src, 0, 0, (uint32_t)q->aggs[a].lds_off, lds, key[j], v);
+        }
+      }
+    }
+  }
+}
+
 // COUNT += 1 and every aggregation of one doc into accumulator slot `key`; an MV aggregation column contributes every
 // value of the doc (aggregateGroupByMV / *MVAggregationFunction).
 template <int STRAT, bool G = false>
@@ -662,8 +852,6 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
 // whole-bin slot (front) and its last free record (back), and the range's first record in the stream.
 // All of it through address-space-3 pointers: ds_* instructions. A flat access could alias global memory, and waiting
 // for one (flat loads count in vmcnt) would drain the tile ring's LDS-DMA.
-typedef __attribute__((address_space(3))) uint64_t lds_u64_t;
-typedef __attribute__((address_space(3))) u32x4 lds_u32x4_t;
 struct BinState {
   lds_u32_t* cnt;
   lds_u32_t* done;
@@ -673,15 +861,11 @@ struct BinState {
   lds_u32_t* slk;   // H bins: records of the doc that crossed the bin end, parked past it (<= kDocVals - 1)
 };
 
-__device__ __forceinline__ lds_u32_t* lds_ptr(const void* p) { return (lds_u32_t*)(uintptr_t)lds_addr(p); }
-
 __device__ __forceinline__ BinState bin_state(const DevQuery* __restrict__ q, unsigned char* lds) {
   return BinState{lds_ptr(lds + q->lds_cnt), lds_ptr(lds + q->lds_done), lds_ptr(lds + q->lds_front),
                   lds_ptr(lds + q->lds_back), (lds_u64_t*)lds_ptr(lds + q->lds_start),
                   lds_ptr(lds + q->lds_slack) - q->pv};  // (slack words exist for the H partitions only)
 }
-
-#define WG_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP
 
 // Wave-level put of K records per lane: every lane calls it (uniform control flow); record k of an active lane (the
 // first nw words of r[k]) goes into partition p[k]'s LDS bin of BS records (bins: the stream's partitions from p0 on,
@@ -927,7 +1111,6 @@ __device__ __forceinline__ void mv_ranges(bool hmv, const int32_t* hoff, int64_t
   }
 }
 
-typedef const __attribute__((address_space(4))) DevSeg CSegT;  // segment descriptor via the constant address space
 
 // Table-wide keys (< 2^32 on the partitioned path) of the docs of steps h .. h+N-1 (match bits m): every group-by
 // dictId decode, then every remap gather (they overlap), then the keys.
@@ -1922,6 +2105,26 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
   } else if constexpr (STRAT == STRAT_PCOUNT || is_pemit(STRAT)) {
     part_tile<STRAT, STEPS, LM>(q, seg, img, doc_base, m, lane, lds, ps);
 
+  } else if (q->has_mv) {
+    for (int i = 0; i < STEPS; ++i)
+      if ((m >> i) & 1u) accumulate_doc_mv<STRAT>(q, seg, img, local(i), doc_base + local(i), acc);
+  } else if constexpr (STRAT == STRAT_LDS && LM) {
+    // a dense tile whose aggregations all read one raw column: that column's tile as coalesced loads
+    const int rs = q->hashed ? -1 : q->lds_raw_slot;
+    if (rs >= 0 && seg->cols[rs].kind == COL_SV_RAW) {
+      uint32_t tot = (uint32_t)__builtin_popcount(m);
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) tot += (uint32_t)__shfl_xor((int)tot, o, kWave);
+      if (tot > 256u) {
+        const int vt = seg->cols[rs].vtype;
+        if (vt == PA_INT || vt == PA_FLOAT) accumulate_lds_raw_dense<4>(q, seg, img, doc_base, m, lane, lds);
+        else accumulate_lds_raw_dense<8>(q, seg, img, doc_base, m, lane, lds);
+      } else {
+        accumulate_lds_lm(q, seg, img, doc_base, m, lane, lds);
+      }
+    } else {
+      accumulate_lds_lm(q, seg, img, doc_base, m, lane, lds);
+    }
   } else if (q->has_mv) {
     for (int i = 0; i < STEPS; ++i)
       if ((m >> i) & 1u) accumulate_doc_mv<STRAT>(q, seg, img, local(i), doc_base + local(i), acc);

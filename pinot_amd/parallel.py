@@ -213,7 +213,8 @@ SUM_FUNCTIONS = ("SUM", "AVG", "SUMMV", "AVGMV")
 
 def wide_sum_columns_local(query, segments):
     """Columns of this rank's segments whose SUM needs the 64-bit accumulator (PA_AGGF_WIDE_SUM): LONG columns that are
-    raw or hold a dictionary value outside int32 (the library picks SUM_I64 for all-int32 columns, SUM_I64X2 else)."""
+    hold a value outside int32, raw or in the dictionary (the library picks SUM_I64 for all-int32 columns, SUM_I64X2
+    else: pa_capi.hip pa_segment_add_raw_column / upload_dict)."""
     out = set()
     for a in query.aggregations:
         if a.function not in SUM_FUNCTIONS or a.column in out:
@@ -222,10 +223,7 @@ def wide_sum_columns_local(query, segments):
             c = s.column(a.column)
             if c.data_type != "LONG":
                 continue
-            if not c.has_dictionary:
-                out.add(a.column)
-                break
-            d = np.asarray(c.dictionary, dtype=np.int64)
+            d = np.asarray(c.dictionary if c.has_dictionary else c.raw_values, dtype=np.int64)
             if len(d) and (d.min() < -(1 << 31) or d.max() >= (1 << 31)):
                 out.add(a.column)
                 break

@@ -34,9 +34,13 @@ def _segment(seed, n):
         "rd": rng.normal(0, 1e6, size=n),
         "dl": rng.integers(0, 1 << 14, size=n).astype(np.int64) * 37 - 99999,  # dictionary LONG metric
         "dd": np.round(rng.normal(0, 100, size=n), 2),                          # dictionary DOUBLE metric
+        "rs": rng.integers(-(1 << 31), 1 << 31, size=n).astype(np.int64),      # raw LONG in int32 range (SUM_I64)
+        "g": rng.integers(0, 700, size=n).astype(np.int32),                    # group-by dimension
     }
-    schema = {"day": "INT", "ri": "INT", "rl": "LONG", "rf": "FLOAT", "rd": "DOUBLE", "dl": "LONG", "dd": "DOUBLE"}
-    return create_segment("lane%d" % seed, data, schema, no_dictionary_columns=("ri", "rl", "rf", "rd"))
+    data["rs"][:2] = [-(1 << 31), (1 << 31) - 1]
+    schema = {"day": "INT", "ri": "INT", "rl": "LONG", "rf": "FLOAT", "rd": "DOUBLE", "dl": "LONG", "dd": "DOUBLE",
+              "rs": "LONG", "g": "INT"}
+    return create_segment("lane%d" % seed, data, schema, no_dictionary_columns=("ri", "rl", "rf", "rd", "rs"))
 
 
 @pytest.fixture(scope="module")
@@ -57,6 +61,7 @@ AGGS = [
     "SUM(rd), MIN(rd), MAX(rd)",
     "COUNT(*), SUM(dl), MIN(dl), MAX(dl)",
     "SUM(dd), MIN(dd), MAX(dd), SUM(rl)",
+    "COUNT(*), SUM(rs), MIN(rs), MAX(rs)",
 ]
 
 
@@ -116,3 +121,25 @@ def test_lane_sum_over_shared_dictionary(flags):
             assert_same(got, oracle.run_query(q, [seg, seg, seg]), DOUBLE_REL)
     finally:
         g.close()
+
+
+GROUP_AGGS = ["COUNT(*), SUM(rs)", "SUM(rl), MIN(rl)", "SUM(rd), MAX(rd), COUNT(*)", "SUM(ri), MIN(rf), MAX(ri)",
+              "SUM(dl), SUM(rs)"]
+
+
+@pytest.mark.parametrize("sel", ["1pct", "30pct", "all"])
+@pytest.mark.parametrize("aggs", GROUP_AGGS)
+def test_lds_group_by_raw_metrics(lane_segments, sel, aggs):
+    """Filter + GROUP BY over raw metrics on the LDS-accumulator strategy, lane-major tiles (pa_scan.h
+    accumulate_lds_lm; accumulate_lds_raw_dense when every non-COUNT aggregation reads one raw column and the wave's tile
+    is dense): INT / LONG (int32-range: one int64 slot; wider: the split pair) / FLOAT / DOUBLE values and 700 groups."""
+    segs, gs = lane_segments
+    q = parse_sql("SELECT g, %s FROM t WHERE day < %d GROUP BY g LIMIT 1000" % (aggs, SELECTIVITY[sel]))
+    ex = GpuQueryExecutor(q, gs)
+    try:
+        st = ex.stats()["plan"]
+        assert st["strategy"] == "lds" and st["lane_major"] == 1, st
+        got = ex.run()
+    finally:
+        ex.close()
+    assert_same(got, oracle.run_query(q, segs), DOUBLE_REL)

@@ -112,6 +112,19 @@ WORKLOADS = {
         ("sel_50pct", "SELECT COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17611", 0),
         ("sel_100pct", "SELECT COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17000 AND 18023", 0),
     ]),
+    # the north-star shape on configs[0]'s columns: filter + GROUP BY SUM (1024-day key space, raw LONG metric)
+    "sumgroup": (sumscan_raw_segment, [
+        ("sel_10pct", "SELECT daysSinceEpoch, COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17201 "
+                      "GROUP BY daysSinceEpoch LIMIT 2000", 0),
+        ("sel_50pct", "SELECT daysSinceEpoch, COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17611 "
+                      "GROUP BY daysSinceEpoch LIMIT 2000", 0),
+    ]),
+    "sumgroup_dict": (sumscan_segment, [
+        ("sel_10pct", "SELECT daysSinceEpoch, COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17201 "
+                      "GROUP BY daysSinceEpoch LIMIT 2000", 0),
+        ("sel_50pct", "SELECT daysSinceEpoch, COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17611 "
+                      "GROUP BY daysSinceEpoch LIMIT 2000", 0),
+    ]),
     "highcard": (highcard_segment, [
         ("all_docs", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000 "
                      "OPTION(numGroupsLimit=2000000)", 0),
