@@ -33,6 +33,8 @@ PA_QF_NO_SPLIT_EMIT = 1 << 24
 PA_QF_NO_LIMIT_WALK = 1 << 25
 PA_QF_NO_LANE_ACC = 1 << 26
 PA_QF_NO_LANE_HIST = 1 << 27
+PA_BIT_AND, PA_BIT_OR, PA_BIT_NOT = -1, -2, -3
+PA_BIT_PROG_MAX = 64
 PA_ACC_COUNT_U64, PA_ACC_SUM_I64, PA_ACC_SUM_F64, PA_ACC_MIN_I64, PA_ACC_MAX_I64, PA_ACC_HLL_U8, \
     PA_ACC_SUM_I64X2, PA_ACC_DOCS_U64, PA_ACC_KEYS_I64, PA_ACC_PRESENCE_U8 = range(10)
 ABI_VERSION = 2
@@ -47,6 +49,7 @@ EXPORTED = [
     "pa_query_accumulator_bytes", "pa_query_set_accumulator_buffer", "pa_query_num_sections", "pa_query_section",
     "pa_query_fetch", "pa_query_matched_docs", "pa_query_key_layout", "pa_query_limit_trimming",
     "pa_query_num_groups_limit_reached", "pa_query_stats", "pa_query_leaf_bitmap_words", "pa_query_leaf_bitmaps",
+    "pa_bitmap_counts_scratch_bytes", "pa_bitmap_counts",
     "pa_query_plan", "pa_query_destroy",
 ]
 
@@ -134,6 +137,8 @@ def _declare(lib):
         "pa_query_stats": (ctypes.c_int, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "pa_query_leaf_bitmap_words": (ctypes.c_int64, [vp, i32]),
         "pa_query_leaf_bitmaps": (ctypes.c_int, [vp, i32, vp, vp]),
+        "pa_bitmap_counts_scratch_bytes": (i64, [i64]),
+        "pa_bitmap_counts": (ctypes.c_int, [vp, i64, i32, i64, vp, i32, vp, i32, vp, vp, vp]),
         "pa_query_plan": (ctypes.c_int, [vp] + [ctypes.POINTER(i32)] * 7),
         "pa_query_destroy": (None, [vp]),
     }

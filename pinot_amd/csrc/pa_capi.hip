@@ -2461,6 +2461,48 @@ int pa_query_leaf_bitmaps(pa_query* q, int32_t segment, uint32_t* device_out, vo
   return PA_OK;
 }
 
+int64_t pa_bitmap_counts_scratch_bytes(int64_t words) {
+  if (words < 0) return fail(PA_EINVAL, "negative word count");
+  return 4 * bit_count_scratch_words(words);
+}
+
+int pa_bitmap_counts(const uint32_t* device_bitmaps, int64_t words, int32_t num_leaves, int64_t num_docs,
+                     const int32_t* prog_a, int32_t len_a, const int32_t* prog_b, int32_t len_b, void* device_scratch,
+                     int64_t* device_out, void* stream) {
+  if (!device_out || num_docs < 0 || words < (num_docs + 31) / 32) return fail(PA_EINVAL, "bad bitmap counts arguments");
+  if (num_docs > 0 && !device_bitmaps) return fail(PA_EINVAL, "null bitmaps");
+  BitProgs P{};
+  const int32_t* progs[2] = {prog_a, prog_b};
+  const int32_t lens[2] = {len_a, len_b};
+  for (int k = 0; k < 2; ++k) {
+    if (lens[k] < 0 || lens[k] > kBitProgMax || (k == 0 && lens[k] == 0) || (lens[k] > 0 && !progs[k]))
+      return fail(PA_EINVAL, "bitmap program length out of range");
+    int depth = 0;
+    for (int i = 0; i < lens[k]; ++i) {
+      const int32_t t = progs[k][i];
+      if (t >= 0) {
+        if (t >= num_leaves) return fail(PA_EINVAL, "bitmap program names a leaf out of range");
+        if (++depth > kBitProgStack) return fail(PA_EINVAL, "bitmap program too deep");
+      } else if (t == PA_BIT_NOT) {
+        if (depth < 1) return fail(PA_EINVAL, "bitmap program: NOT on an empty stack");
+      } else if (t == PA_BIT_AND || t == PA_BIT_OR) {
+        if (depth < 2) return fail(PA_EINVAL, "bitmap program: AND/OR needs two masks");
+        --depth;
+      } else {
+        return fail(PA_EINVAL, "bitmap program: unknown token");
+      }
+      P.tok[k * kBitProgMax + i] = t;
+    }
+    if (lens[k] > 0 && depth != 1) return fail(PA_EINVAL, "bitmap program must leave exactly one mask");
+  }
+  P.len_a = len_a;
+  P.len_b = len_b;
+  if (len_b > 0 && num_docs > 0 && !device_scratch) return fail(PA_EINVAL, "null scratch");
+  PA_HIP(launch_bit_counts(P, device_bitmaps, words, num_docs, (uint32_t*)device_scratch,
+                           (unsigned long long*)device_out, (hipStream_t)stream));
+  return PA_OK;
+}
+
 int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs, uint64_t* num_tiles) {
   if (!q) return fail(PA_EINVAL, "null query");
   if (staged_bytes) *staged_bytes = q->staged_bytes;

@@ -396,6 +396,179 @@ hipError_t launch_leaf_bitmap(const DevSeg* seg, int li, int flip, int64_t num_d
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- execution statistics over leaf bitmaps
+// Doc masks A and B are postfix programs over the leaf bitmaps (BitProgs). Word w of a mask: 32 docs. The counts feed
+// the closed forms of filter_stats.py: popcounts for the applyAnd chains and the post-filter docs, and for an AND of two
+// scan iterators (AndDocIdIterator.java:39-73 leap-frogging SVScanDocIdIterator.advance, which reads from the target
+// to the next match) the number of leaps. Labelled docs: A-only (1), B-only (2), both (3). In the sequence of labelled
+// docs, a leap starts at an A-only doc preceded by a both-doc (or the segment start), and at every A-only / B-only doc
+// preceded by the other of the two.
+constexpr int kBitBlockWords = 1024;  // words per workgroup: 256 threads x 4
+
+__device__ __forceinline__ uint32_t bit_prog_word(const BitProgs& P, int base, int len, const uint32_t* __restrict__ bm,
+                                                  int64_t words, int64_t w, uint32_t valid) {
+  uint32_t st[kBitProgStack];
+  int sp = 0;
+  for (int i = 0; i < len; ++i) {
+    const int t = P.tok[base + i];
+    if (t >= 0) {
+      st[sp++] = gp(bm)[(int64_t)t * words + w] & valid;
+    } else if (t == PA_BIT_NOT) {
+      st[sp - 1] = ~st[sp - 1] & valid;
+    } else {
+      --sp;
+      st[sp - 1] = t == PA_BIT_AND ? (st[sp - 1] & st[sp]) : (st[sp - 1] | st[sp]);
+    }
+  }
+  return sp > 0 ? st[0] : 0u;
+}
+
+__device__ __forceinline__ void bit_masks(const BitProgs& P, const uint32_t* bm, int64_t words, int64_t num_docs,
+                                          int64_t w, uint32_t& a, uint32_t& b) {
+  a = b = 0u;
+  const int64_t left = num_docs - 32 * w;
+  if (left <= 0) return;
+  const uint32_t valid = left >= 32 ? 0xffffffffu : ((1u << left) - 1u);
+  a = bit_prog_word(P, 0, P.len_a, bm, words, w, valid);
+  if (P.len_b > 0) b = bit_prog_word(P, kBitProgMax, P.len_b, bm, words, w, valid);
+}
+
+// label of the highest labelled doc of a word (0: none)
+__device__ __forceinline__ uint32_t last_label(uint32_t a, uint32_t b) {
+  const uint32_t l = a | b;
+  if (l == 0u) return 0u;
+  const int p = 31 - __builtin_clz(l);
+  return ((a >> p) & 1u) | (((b >> p) & 1u) << 1);
+}
+
+__device__ __forceinline__ uint32_t later_label(uint32_t x, uint32_t y) { return y != 0u ? y : x; }
+
+// inclusive "last labelled" scan over the 256 threads of the block (threads in order); returns the exclusive value
+__device__ __forceinline__ uint32_t block_last_exclusive(uint32_t v, uint32_t* lds4, uint32_t* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t u = (uint32_t)__shfl_up((int)inc, o, kWave);
+    if (lane >= o) inc = later_label(u, inc);
+  }
+  if (lane == kWave - 1) lds4[wv] = inc;
+  __syncthreads();
+  uint32_t before = 0u, all = 0u;
+  for (int i = 0; i < 4; ++i) {
+    if (i < wv) before = later_label(before, lds4[i]);
+    all = later_label(all, lds4[i]);
+  }
+  uint32_t exc = (uint32_t)__shfl_up((int)inc, 1, kWave);
+  exc = lane == 0 ? before : later_label(before, exc);
+  *total = all;
+  return exc;
+}
+
+__global__ void __launch_bounds__(256) bit_last_kernel(BitProgs P, const uint32_t* __restrict__ bm, int64_t words,
+                                                       int64_t num_docs, uint32_t* __restrict__ block_last) {
+  __shared__ uint32_t lds4[4];
+  const int64_t w0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  uint32_t last = 0u;
+  for (int k = 0; k < 4; ++k) {
+    uint32_t a, b;
+    bit_masks(P, bm, words, num_docs, w0 + k, a, b);
+    last = later_label(last, last_label(a, b));
+  }
+  uint32_t total;
+  block_last_exclusive(last, lds4, &total);
+  if (threadIdx.x == 0) gp(block_last)[blockIdx.x] = total;
+}
+
+// one workgroup: block_in[i] = last label of blocks < i, or 3 (segment start) when none
+__global__ void __launch_bounds__(1024) bit_carry_kernel(const uint32_t* __restrict__ block_last, int64_t nb,
+                                                         uint32_t* __restrict__ block_in) {
+  __shared__ uint32_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (nb + 1023) / 1024;
+  const int64_t b0 = t * per, b1 = b0 + per < nb ? b0 + per : nb;
+  uint32_t v = 0u;
+  for (int64_t i = b0; i < b1; ++i) v = later_label(v, gp(block_last)[i]);
+  part[t] = v;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+    const uint32_t u = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] = later_label(u, part[t]);
+    __syncthreads();
+  }
+  uint32_t run = t > 0 ? part[t - 1] : 0u;
+  for (int64_t i = b0; i < b1; ++i) {
+    gp(block_in)[i] = run != 0u ? run : 3u;
+    run = later_label(run, gp(block_last)[i]);
+  }
+}
+
+__global__ void __launch_bounds__(256) bit_count_kernel(BitProgs P, const uint32_t* __restrict__ bm, int64_t words,
+                                                        int64_t num_docs, const uint32_t* __restrict__ block_in,
+                                                        unsigned long long* __restrict__ out) {
+  __shared__ uint32_t lds4[4];
+  const int64_t w0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  uint32_t a[4], b[4];
+  uint32_t last = 0u;
+  for (int k = 0; k < 4; ++k) {
+    bit_masks(P, bm, words, num_docs, w0 + k, a[k], b[k]);
+    last = later_label(last, last_label(a[k], b[k]));
+  }
+  unsigned long long pa = 0, pb = 0, pab = 0, leaps = 0;
+  for (int k = 0; k < 4; ++k) {
+    pa += __builtin_popcount(a[k]);
+    pb += __builtin_popcount(b[k]);
+    pab += __builtin_popcount(a[k] & b[k]);
+  }
+  if (P.len_b > 0) {
+    uint32_t total;
+    uint32_t prev = block_last_exclusive(last, lds4, &total);
+    if (prev == 0u) prev = gp(block_in)[blockIdx.x];
+    for (int k = 0; k < 4; ++k) {
+      uint32_t l = a[k] | b[k];
+      while (l != 0u) {
+        const int p = __builtin_ctz(l);
+        l &= l - 1u;
+        const uint32_t lab = ((a[k] >> p) & 1u) | (((b[k] >> p) & 1u) << 1);
+        if ((lab == 1u && prev == 3u) || (lab != 3u && prev != 3u && lab != prev)) ++leaps;
+        prev = lab;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    pa += __shfl_xor(pa, o, kWave);
+    pb += __shfl_xor(pb, o, kWave);
+    pab += __shfl_xor(pab, o, kWave);
+    leaps += __shfl_xor(leaps, o, kWave);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(out + 0, pa);
+    atomicAdd(out + 1, pb);
+    atomicAdd(out + 2, pab);
+    atomicAdd(out + 3, leaps);
+  }
+}
+
+int64_t bit_count_scratch_words(int64_t words) { return 2 * ((words + kBitBlockWords - 1) / kBitBlockWords); }
+
+hipError_t launch_bit_counts(const BitProgs& P, const uint32_t* bm, int64_t words, int64_t num_docs,
+                             uint32_t* scratch, unsigned long long* out, hipStream_t s) {
+  const int64_t live = (num_docs + 31) / 32;
+  const int64_t nb = (live + kBitBlockWords - 1) / kBitBlockWords;
+  if (nb == 0) return hipSuccess;
+  if (nb > INT32_MAX) return hipErrorInvalidValue;
+  uint32_t* block_last = scratch;
+  uint32_t* block_in = scratch + nb;
+  if (P.len_b > 0) {
+    bit_last_kernel<<<(int)nb, 256, 0, s>>>(P, bm, words, num_docs, block_last);
+    bit_carry_kernel<<<1, 1024, 0, s>>>(block_last, nb, block_in);
+  }
+  bit_count_kernel<<<(int)nb, 256, 0, s>>>(P, bm, words, num_docs, block_in, out);
+  return hipGetLastError();
+}
+
 __global__ void bswap_words_kernel(uint32_t* w, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     w[i] = __builtin_bswap32(w[i]);

@@ -32,6 +32,17 @@ hipError_t launch_compact_final(const unsigned long long* count, int64_t K, int 
                                 int64_t cap, const FinalDesc* d, hipStream_t s);
 // one filter literal of one segment -> doc bitmap (execution statistics)
 hipError_t launch_leaf_bitmap(const DevSeg* seg, int li, int flip, int64_t num_docs, uint32_t* out, hipStream_t s);
+// Execution-statistics counts over leaf bitmaps (pa_bitmap_counts): postfix programs A (tok[0..len_a)) and B
+// (tok[kBitProgMax..+len_b)).
+constexpr int kBitProgMax = 64;
+constexpr int kBitProgStack = 16;
+struct BitProgs {
+  int32_t len_a, len_b;
+  int32_t tok[2 * kBitProgMax];
+};
+int64_t bit_count_scratch_words(int64_t words);
+hipError_t launch_bit_counts(const BitProgs& P, const uint32_t* bm, int64_t words, int64_t num_docs,
+                             uint32_t* scratch, unsigned long long* out, hipStream_t s);
 hipError_t launch_compact(const unsigned long long* count, int64_t K, int all, uint32_t* block_sums, int64_t cap,
                           const CompactDesc* d, int phase, hipStream_t s);
 // numGroupsLimit first-seen trimming (pa_kernels.hip "numGroupsLimit"): the (segment, key) first-position table,

@@ -489,12 +489,12 @@ __device__ __forceinline__ void lds_update(int type, int src, int log2m, int64_t
 // updates — so a tile costs the wave max-popcount / 4 dependent round trips instead of one per 64-doc step (the
 // step-major path waits on each step's value loads before its wave-level key grouping). Lanes sharing a key meet in
 // the LDS atomics (DefaultGroupByExecutor.aggregateGroupBySV per doc).
+template <int kB>
 __device__ __forceinline__ void accumulate_lds_lm(const DevQuery* __restrict__ q_in, const DevSeg* __restrict__ seg,
                                                   const uint32_t* img, int64_t doc_base, uint32_t m, int lane,
                                                   unsigned char* lds) {
   CQ* q = (CQ*)(uintptr_t)q_in;
   CSegT* cs = (CSegT*)(uintptr_t)seg;
-  constexpr int kB = 4;
   const int64_t d0 = doc_base + 32 * lane;
   lds_u32_t* cnt = lds_ptr(lds + q->lds_count_off);
   const int ngb = q->num_gb, na = q->num_aggs;
@@ -2109,21 +2109,20 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
     for (int i = 0; i < STEPS; ++i)
       if ((m >> i) & 1u) accumulate_doc_mv<STRAT>(q, seg, img, local(i), doc_base + local(i), acc);
   } else if constexpr (STRAT == STRAT_LDS && LM) {
-    // a dense tile whose aggregations all read one raw column: that column's tile as coalesced loads
-    const int rs = q->hashed ? -1 : q->lds_raw_slot;
-    if (rs >= 0 && seg->cols[rs].kind == COL_SV_RAW) {
-      uint32_t tot = (uint32_t)__builtin_popcount(m);
+    // matches of the wave's tile: a dense tile whose aggregations all read one raw column takes that column's tile as
+    // coalesced loads; else per-lane batches, 8 docs deep when most lanes have that many (more gathers in flight)
+    uint32_t tot = (uint32_t)__builtin_popcount(m);
 #pragma unroll
-      for (int o = 1; o < kWave; o <<= 1) tot += (uint32_t)__shfl_xor((int)tot, o, kWave);
-      if (tot > 256u) {
-        const int vt = seg->cols[rs].vtype;
-        if (vt == PA_INT || vt == PA_FLOAT) accumulate_lds_raw_dense<4>(q, seg, img, doc_base, m, lane, lds);
-        else accumulate_lds_raw_dense<8>(q, seg, img, doc_base, m, lane, lds);
-      } else {
-        accumulate_lds_lm(q, seg, img, doc_base, m, lane, lds);
-      }
+    for (int o = 1; o < kWave; o <<= 1) tot += (uint32_t)__shfl_xor((int)tot, o, kWave);
+    const int rs = q->hashed ? -1 : q->lds_raw_slot;
+    if (tot > 256u && rs >= 0 && seg->cols[rs].kind == COL_SV_RAW) {
+      const int vt = seg->cols[rs].vtype;
+      if (vt == PA_INT || vt == PA_FLOAT) accumulate_lds_raw_dense<4>(q, seg, img, doc_base, m, lane, lds);
+      else accumulate_lds_raw_dense<8>(q, seg, img, doc_base, m, lane, lds);
+    } else if (tot > 512u) {
+      accumulate_lds_lm<8>(q, seg, img, doc_base, m, lane, lds);
     } else {
-      accumulate_lds_lm(q, seg, img, doc_base, m, lane, lds);
+      accumulate_lds_lm<4>(q, seg, img, doc_base, m, lane, lds);
     }
   } else if (q->has_mv) {
     for (int i = 0; i < STEPS; ++i)

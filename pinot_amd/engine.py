@@ -516,14 +516,14 @@ class GpuQueryExecutor:
 
     def execution_stats(self, stream=None):
         """(numEntriesScannedInFilter, numEntriesScannedPostFilter) of this server's segments: the reference's
-        operator accounting (filter_stats.py) over GPU leaf bitmaps."""
+        operator accounting (filter_stats.py), closed forms over counts the GPU takes from its leaf bitmaps
+        (pa_bitmap_counts), the iterator replay over host bitmaps only for operator trees without one."""
         from . import filter_stats as FS
-        return FS.server_stats(self.query, self.segs, lambda si: self.leaf_bitmaps(si, stream))
+        return FS.server_stats_device(self.query, self.segs, self, stream)
 
     def fetch(self, stream=None, execution_stats=False) -> IntermediateResult:
-        """execution_stats=True also fills numEntriesScannedInFilter / PostFilter (one leaf-bitmap pass per segment on
-        the GPU plus the host restatement of the reference's accounting: meant for result metadata, not the hot
-        loop)."""
+        """execution_stats=True also fills numEntriesScannedInFilter / PostFilter (one leaf-bitmap pass and a few
+        count kernels per segment on the GPU, one synchronisation: execution_stats)."""
         lib = L.lib()
         q = self.query
         if not self.segs:

@@ -23,6 +23,8 @@ Compile-time filter rewrites of the reference other than AND/OR flattening (Flat
 restated (MergeRangeFilterOptimizer, MergeEqInFilterOptimizer, ...): filters they would rewrite get the counts of the
 unrewritten tree. Parity is pinned by the reference's golden statistics (InterSegmentAggregationSingleValueQueriesTest,
 InterSegmentGroupBySingleValueQueriesTest: tests/golden/sv_queries.json)."""
+import ctypes
+
 import numpy as np
 
 from . import query as Q
@@ -476,3 +478,198 @@ def server_stats(query, segments, leaf_bitmaps):
         docs = seg.num_docs if query.filter is None else int(filter_mask(query.filter, seg, bitmaps).sum())
         post += docs * ncols
     return in_filter, post
+
+
+# ------------------------------------------------------------------ device path: closed forms over GPU counts
+# The iterator replay above is O(matching docs) on the host. The projection's iteration has closed forms for the
+# operator trees queries usually have, whose inputs are counts over the leaf bitmaps that the GPU computes without
+# moving the bitmaps (pa_bitmap_counts):
+#   * a scan iterator driven by next() to EOF reads every entry: num_docs (SV), the column's value count (MV);
+#     OR / NOT children are driven by next() to EOF too, so their costs add (NOT calls its child's next() once past
+#     EOF: free for every iterator but a leap-frogging AND);
+#   * AND with index-based children (AndDocIdSet.java:92-140): each SV scan child's applyAnd reads the docs that survive
+#     the index children and the scan children before it: popcounts of AND chains;
+#   * AND of two SV scan iterators leap-frogged by AndDocIdIterator: every advance(t) reads [t, next match of the
+#     advancing iterator], so the reads telescope to num_docs - matches + advance calls - 1, and the advance calls are
+#     2 per match + 1 + the leaps (pa_bitmap_counts): num_docs + popcount(A & B) + leaps.
+# Other shapes (an AND leap-frogging an OR / NOT / a third iterator, MV applyAnd) keep the host replay.
+class _Unsupported(Exception):
+    pass
+
+
+def _rpn(f, start):
+    """Postfix program (pa_bitmap_counts tokens) of an expanded predicate subtree over the leaves [start, ...)."""
+    from . import _lib as L
+    if isinstance(f, (Q.And, Q.Or)):
+        out, k = [], start
+        for i, c in enumerate(f.children):
+            out += _rpn(c, k)
+            k += _count_leaves(c)
+            if i:
+                out.append(L.PA_BIT_AND if isinstance(f, Q.And) else L.PA_BIT_OR)
+        return out
+    if isinstance(f, Q.Not):
+        return _rpn(f.child, start) + [L.PA_BIT_NOT]
+    return [start]
+
+
+class _RpnCursor(_LeafCursor):
+    """_LeafCursor whose masks are postfix programs instead of host bitmaps."""
+
+    def __init__(self, segment):
+        super().__init__(None, segment)
+
+    def take(self, pred):
+        sub = expand_raw_in(pred, self.segment)
+        p = _rpn(sub, self.k)
+        self.k += _count_leaves(sub)
+        return p
+
+
+def _and_prog(progs):
+    from . import _lib as L
+    out = list(progs[0])
+    for p in progs[1:]:
+        out += list(p) + [L.PA_BIT_AND]
+    return out
+
+
+class _Terms:
+    """A count as constant + sum of coef * (request field); requests are (program A, program B) of one segment."""
+
+    def __init__(self, const=0):
+        self.const, self.terms = const, []
+
+    def add(self, other):
+        self.const += other.const
+        self.terms += other.terms
+        return self
+
+    def request(self, reqs, si, a, b, field, coef=1):
+        from . import _lib as L
+        if len(a) > L.PA_BIT_PROG_MAX or len(b) > L.PA_BIT_PROG_MAX:
+            raise _Unsupported("bitmap program too long")
+        key = (si, tuple(a), tuple(b))
+        if key not in reqs:
+            reqs[key] = len(reqs)
+        self.terms.append((reqs[key], field, coef))
+        return self
+
+    def value(self, counts):
+        return self.const + sum(int(counts[r, f]) * c for r, f, c in self.terms)
+
+
+def _cost_next(op, seg, si, reqs):
+    """numEntriesScannedInFilter of op's iterator driven by next() to EOF, as _Terms."""
+    n = seg.num_docs
+    if op.kind in ("empty", "all", "sorted", "bitmap"):
+        return _Terms(0)
+    if op.kind == "scan":
+        return _Terms(n if op.weights is None else int(np.sum(op.weights, dtype=np.int64)))
+    if op.kind == "not":
+        c = op.children[0]
+        if c.kind == "and" and not any(k.kind in ("sorted", "bitmap") for k in c.children):
+            # NotDocIdIterator.next() calls its child's next() once more after EOF: an AndDocIdIterator re-runs its
+            # last leap-frog chain then (no closed form kept for that tail)
+            raise _Unsupported("NOT over a leap-frogging AND")
+        return _cost_next(c, seg, si, reqs)
+    if op.kind == "or":
+        t = _Terms(0)
+        for c in op.children:
+            t.add(_cost_next(c, seg, si, reqs))
+        return t
+    # AND: the iterator construction of _iterator / AndDocIdSet
+    kids = op.children
+    index = [c for c in kids if c.kind == "sorted"] + [c for c in kids if c.kind == "bitmap"]
+    scans = [c for c in kids if c.kind == "scan"]
+    rest = [c for c in kids if c.kind not in ("sorted", "bitmap", "scan")]
+    if (index and scans) or len(index) > 1:
+        if rest:
+            raise _Unsupported("AND leap-frogs a merged index set with other iterators")
+        t = _Terms(0)
+        docs = _and_prog([c.mask for c in index])
+        for s in scans:
+            if s.weights is not None:
+                raise _Unsupported("MV applyAnd")
+            t.request(reqs, si, docs, [], 0)
+            docs = _and_prog([docs, s.mask])
+        return t
+    if len(kids) == 2 and all(c.kind == "scan" and c.weights is None for c in kids):
+        return _Terms(n).request(reqs, si, kids[0].mask, kids[1].mask, 2).request(reqs, si, kids[0].mask,
+                                                                                    kids[1].mask, 3)
+    raise _Unsupported("AND leap-frogging other than two SV scans")
+
+
+def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps):
+    """server_stats through the closed forms above. counts_fn(reqs) -> int64[len(reqs), 4]: for every request
+    (segment index, program A, program B) -> row, pa_bitmap_counts' four counts. Segments without a closed form replay
+    the iterators over leaf_bitmaps(i) (host bitmaps, as server_stats)."""
+    ncols = projected_columns(query)
+    filt = query.filter
+    reqs = {}
+    plans = []  # per segment: None (non-scan plan), "host", or (in_filter _Terms, docs _Terms)
+    for si, seg in enumerate(segments):
+        if filt is None:
+            plans.append(None if non_scan_plan(query, seg, True) else (_Terms(0), _Terms(seg.num_docs)))
+            continue
+        try:
+            op = _build(_flatten(filt), seg, _RpnCursor(seg), segment_index_info(seg))
+            if non_scan_plan(query, seg, op.kind == "all"):
+                plans.append(None)
+                continue
+            cost = _Terms(0) if op.kind in ("empty", "all") else _cost_next(op, seg, si, reqs)
+            docs = _Terms(0).request(reqs, si, _rpn(expand_raw_in(filt, seg), 0), [], 0)
+            plans.append((cost, docs))
+        except _Unsupported:
+            plans.append("host")
+    counts = counts_fn(reqs) if reqs else None
+    in_filter = post = 0
+    for p in plans:
+        if p is not None and p != "host":
+            in_filter += p[0].value(counts)
+            post += p[1].value(counts) * ncols
+    host = [si for si, p in enumerate(plans) if p == "host"]
+    if host:
+        hi, hp = server_stats(query, [segments[si] for si in host], lambda i: leaf_bitmaps(host[i]))
+        in_filter += hi
+        post += hp
+    return in_filter, post
+
+
+def device_counts(executor, segments, reqs, stream=None):
+    """pa_bitmap_counts for every request, per segment over one pa_query_leaf_bitmaps pass into a reused device
+    buffer; one synchronisation at the end."""
+    import torch
+    from . import _lib as L
+    lib = L.lib()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    out = torch.zeros((len(reqs), 4), dtype=torch.int64, device=dev)
+    by_seg = {}
+    for (si, a, b), r in reqs.items():
+        by_seg.setdefault(si, []).append((a, b, r))
+    nl = int(executor.spec.num_leaves)
+    words = {si: int(L.check(lib.pa_query_leaf_bitmap_words(executor.handle, si), "pa_query_leaf_bitmap_words"))
+             for si in by_seg}
+    wmax = max(words.values())
+    bm = torch.empty(max(1, nl * wmax), dtype=torch.int32, device=dev)
+    scratch = torch.empty(max(1, int(lib.pa_bitmap_counts_scratch_bytes(wmax)) // 4), dtype=torch.int32, device=dev)
+    progs = {}
+
+    def prog(p):
+        if p not in progs:
+            progs[p] = (ctypes.c_int32 * max(1, len(p)))(*p)
+        return progs[p]
+    bp, sp, op = bm.data_ptr(), scratch.data_ptr(), out.data_ptr()
+    for si, rs in by_seg.items():
+        L.check(lib.pa_query_leaf_bitmaps(executor.handle, si, bp, stream), "pa_query_leaf_bitmaps")
+        for a, b, r in rs:
+            L.check(lib.pa_bitmap_counts(bp, words[si], nl, segments[si].num_docs, prog(a), len(a), prog(b), len(b),
+                                         sp, op + 32 * r, stream), "pa_bitmap_counts")
+    torch.cuda.synchronize()  # (device-wide: covers `stream`)
+    return out.cpu().numpy()
+
+
+def server_stats_device(query, segments, executor, stream=None):
+    """server_stats with the counts computed on the GPU (device_counts); same results."""
+    return server_stats_closed_form(query, segments, lambda reqs: device_counts(executor, segments, reqs, stream),
+                                    lambda si: executor.leaf_bitmaps(si, stream))

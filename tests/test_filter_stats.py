@@ -146,3 +146,101 @@ def test_post_filter_rules(golden_segment):
         _, post = FS.server_stats(q, [seg], lambda si: masks)
         docs = seg.num_docs if q.filter is None else int(masks[0].sum())
         assert post == docs * cols, sql
+
+
+# ---------------------------------------------------------------- closed forms (filter_stats.server_stats_closed_form)
+def _np_prog(prog, masks, n):
+    from pinot_amd import _lib as L
+    st = []
+    for t in prog:
+        if t >= 0:
+            st.append(masks[t].copy())
+        elif t == L.PA_BIT_NOT:
+            st[-1] = ~st[-1]
+        else:
+            y = st.pop()
+            st[-1] = (st[-1] & y) if t == L.PA_BIT_AND else (st[-1] | y)
+    assert len(st) == 1
+    return st[0][:n]
+
+
+def np_leaps(a, b):
+    """pa_bitmap_counts' leap count, restated doc by doc (test-side)."""
+    lab = a.astype(np.int64) + 2 * b.astype(np.int64)
+    seq = lab[lab != 0]
+    prev = np.concatenate([[3], seq[:-1]])
+    return int(np.sum(((seq == 1) & (prev == 3)) | ((seq != 3) & (prev != 3) & (seq != prev))))
+
+
+def np_counts(masks_of, segments):
+    """counts_fn of server_stats_closed_form emulated with numpy over host leaf masks (test-side pa_bitmap_counts)."""
+    def fn(reqs):
+        out = np.zeros((len(reqs), 4), dtype=np.int64)
+        for (si, a, b), r in reqs.items():
+            m, n = masks_of(si), segments[si].num_docs
+            A = _np_prog(a, m, n)
+            B = _np_prog(b, m, n) if b else np.zeros(n, dtype=bool)
+            out[r] = [A.sum(), B.sum(), (A & B).sum(), np_leaps(A, B) if b else 0]
+        return out
+    return fn
+
+
+def test_leap_count_closed_form_matches_and_iterator():
+    """num_docs + popcount(A & B) + leaps = the reads of AndDocIdIterator over two SVScanDocIdIterators, on random masks
+    of many densities (including empty, full, a match at the last doc)."""
+    rng = np.random.default_rng(5)
+    for trial in range(300):
+        n = int(rng.integers(1, 400))
+        pa, pb = rng.random(2) ** 2
+        a, b = rng.random(n) < pa, rng.random(n) < pb
+        if trial % 7 == 0:
+            a[-1] = b[-1] = True
+        it = FS._AndIt([FS._ScanIt(a), FS._ScanIt(b)])
+        while it.next() != FS.EOF:
+            pass
+        replay = it.its[0].entries + it.its[1].entries
+        assert replay == n + int((a & b).sum()) + np_leaps(a, b), (trial, n)
+
+
+CLOSED_FORM_WHERES = [
+    "a < 30 AND b < 30", "a < 90 AND b >= 5", "a = 3 AND b = 4", "a < 50", "NOT a < 50", "a < 10 OR b < 10",
+    "s BETWEEN 10 AND 20 AND a < 50 AND b > 30", "c = 4 AND a >= 10", "c IN (1, 2) AND s < 30 AND a < 60",
+    "NOT (c = 3 AND a < 20)", "NOT (a < 10 OR b < 20)", "a IN (1, 5, 7) AND b NOT IN (3, 4)",
+    "s = 7", "c IN (1, 2, 3)", "a < 1000 AND s = 7",
+]
+HOST_WHERES = ["a < 30 AND b < 30 AND c < 10 AND s > 3 AND a > 2", "a < 50 AND (b < 10 OR s = 3)",
+               "(a < 10 OR b < 10) AND c = 3", "NOT (a < 10 AND b < 20)"]
+
+
+@pytest.mark.parametrize("where", CLOSED_FORM_WHERES + HOST_WHERES)
+def test_closed_form_matches_replay(where):
+    """server_stats_closed_form (counts emulated with numpy) = server_stats (iterator replay), and the closed form is
+    taken for every shape in CLOSED_FORM_WHERES (the replay is never asked for)."""
+    segs = [_seg(3000, 3), _seg(4097, 4)]
+    for sql in ("SELECT COUNT(*) FROM t WHERE " + where, "SELECT SUM(a), MAX(b) FROM t WHERE " + where,
+                "SELECT c, SUM(a) FROM t WHERE %s GROUP BY c" % where):
+        q = parse_sql(sql)
+        masks = [leaf_masks(q, s) for s in segs]
+        want = FS.server_stats(q, segs, lambda si: masks[si])
+
+        def host(si):
+            assert where in HOST_WHERES, "closed form expected for " + where
+            return masks[si]
+        got = FS.server_stats_closed_form(q, segs, np_counts(lambda si: masks[si], segs), host)
+        assert got == want, sql
+
+
+def test_closed_form_golden_statistics(golden_spec, golden_segment):
+    """The golden statistics through the closed forms (numpy-emulated counts)."""
+    bad = []
+    for case in golden_spec["cases"]:
+        if case["stats"] is None:
+            continue
+        q = parse_sql(case["sql"])
+        segs = [golden_segment] * golden_spec["segments_per_server"]
+        masks = leaf_masks(q, golden_segment)
+        got = FS.server_stats_closed_form(q, segs, np_counts(lambda si: masks, segs), lambda si: masks)
+        want = FS.server_stats(q, segs, lambda si: masks)
+        if got != want:
+            bad.append((case["sql"][:80], got, want))
+    assert not bad, bad

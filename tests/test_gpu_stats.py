@@ -1,0 +1,91 @@
+"""Execution statistics on the GPU (pa_bitmap_counts + filter_stats closed forms) against the host iterator replay.
+
+pa_bitmap_counts is checked against a numpy restatement of its four counts on random leaf bitmaps (one word to
+multi-workgroup sizes, densities down to a few set bits so the cross-workgroup label carry is exercised); the
+executor's execution_stats() (closed forms over those counts) against filter_stats.server_stats (the replay of the
+reference's iterators, SVScanDocIdIterator / AndDocIdIterator / OrDocIdIterator / NotDocIdIterator) over the same
+GPU leaf bitmaps. Bit-exact integers."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from pinot_amd import _lib as L
+from pinot_amd import filter_stats as FS
+from pinot_amd import parse_sql
+from pinot_amd.engine import GpuQueryExecutor, GpuSegment
+from pinot_amd.segment import create_segment
+from test_filter_stats import CLOSED_FORM_WHERES, HOST_WHERES, _np_prog, np_leaps
+
+pytestmark = pytest.mark.gpu
+
+AND, OR, NOT = L.PA_BIT_AND, L.PA_BIT_OR, L.PA_BIT_NOT
+
+
+def _device_counts(bits, n, a, b):
+    lib = L.lib()
+    nl, words = bits.shape
+    dev = torch.device("cuda", torch.cuda.current_device())
+    bm = torch.from_numpy(np.ascontiguousarray(bits).view(np.int32).reshape(-1)).to(dev)
+    out = torch.zeros(4, dtype=torch.int64, device=dev)
+    scratch = torch.empty(max(1, int(lib.pa_bitmap_counts_scratch_bytes(words)) // 4), dtype=torch.int32, device=dev)
+    pa = (ctypes.c_int32 * max(1, len(a)))(*a)
+    pb = (ctypes.c_int32 * max(1, len(b)))(*b)
+    L.check(lib.pa_bitmap_counts(bm.data_ptr(), words, nl, n, pa, len(a), pb, len(b), scratch.data_ptr(),
+                                 out.data_ptr(), None), "pa_bitmap_counts")
+    torch.cuda.synchronize()
+    return out.cpu().numpy().tolist()
+
+
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 5000, 32 * 1024 + 7, 3_000_001])
+def test_bitmap_counts_kernel(n):
+    rng = np.random.default_rng(n)
+    words = (n + 63) // 64 * 2
+    progs = [([0], [1]), ([0, 1, OR], [2, NOT]), ([0, NOT, 2, AND], [1]), ([2], []), ([0, 1, AND, 2, OR], [0, NOT])]
+    for dens in ([0.5, 0.5, 0.5], [0.02, 0.3, 0.9], [3.0 / n, 2.0 / n, 0.5], [1.0, 1.0, 0.0]):
+        masks = np.stack([rng.random(n) < d for d in dens])
+        bits = np.zeros((3, words * 32), dtype=bool)
+        bits[:, :n] = masks
+        packed = np.packbits(bits, axis=1, bitorder="little").view(np.uint32)
+        for a, b in progs:
+            A = _np_prog(a, masks, n)
+            B = _np_prog(b, masks, n) if b else np.zeros(n, dtype=bool)
+            want = [int(A.sum()), int(B.sum()), int((A & B).sum()), np_leaps(A, B) if b else 0]
+            assert _device_counts(packed, n, a, b) == want, (dens, a, b)
+
+
+def test_bitmap_counts_rejects_bad_programs():
+    lib = L.lib()
+    for a in ([], [0, 1], [AND], [5], [0, -9], [0] * 17 + [AND] * 16):
+        pa = (ctypes.c_int32 * max(1, len(a)))(*a)
+        rc = lib.pa_bitmap_counts(None, 0, 3, 0, pa, len(a), None, 0, None, ctypes.c_void_p(8), None)
+        assert rc < 0, a
+
+
+def _segment(seed, n):
+    rng = np.random.default_rng(seed)
+    data = {"s": np.sort(rng.integers(0, 50, n)).astype(np.int32), "a": rng.integers(0, 100, n).astype(np.int32),
+            "b": rng.integers(0, 100, n).astype(np.int32), "c": rng.integers(0, 20, n).astype(np.int32)}
+    return create_segment("st%d" % seed, data, {k: "INT" for k in data}, inverted_index_columns=("c",))
+
+
+def test_execution_stats_device_vs_replay():
+    """Every shape of test_filter_stats' closed-form list (and the replay-only shapes) over 3 segments of up to 200K
+    docs: the executor's statistics = the host replay over the same GPU bitmaps."""
+    segs = [_segment(1, 200_003), _segment(2, 70_000), _segment(3, 1025)]
+    gs = [GpuSegment(s) for s in segs]
+    try:
+        for where in CLOSED_FORM_WHERES + HOST_WHERES:
+            for sql in ("SELECT COUNT(*) FROM t WHERE " + where, "SELECT c, SUM(a) FROM t WHERE %s GROUP BY c" % where):
+                q = parse_sql(sql)
+                ex = GpuQueryExecutor(q, gs)
+                try:
+                    got = ex.execution_stats()
+                    want = FS.server_stats(q, ex.segs, lambda si: ex.leaf_bitmaps(si))
+                finally:
+                    ex.close()
+                assert got == want, sql
+    finally:
+        for g in gs:
+            g.close()

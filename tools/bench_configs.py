@@ -125,6 +125,10 @@ WORKLOADS = {
         ("sel_50pct", "SELECT daysSinceEpoch, COUNT(*), SUM(m) FROM t WHERE daysSinceEpoch BETWEEN 17100 AND 17611 "
                       "GROUP BY daysSinceEpoch LIMIT 2000", 0),
     ]),
+    # configs[1]: bench.py's AdAnalytics segments and README query (execution statistics: --exec-stats)
+    "adanalytics": (lambda seed, docs: _bench().make_segment(seed, docs), [
+        ("readme", None, 0),
+    ]),
     "highcard": (highcard_segment, [
         ("all_docs", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000 "
                      "OPTION(numGroupsLimit=2000000)", 0),
@@ -178,7 +182,15 @@ def cpu_port_baseline(sql, host_segs):
     return bench.cpu_baseline(parse_sql(sql), host_segs)
 
 
-def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None, cpu_sample=0):
+def _bench():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_main", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None, cpu_sample=0, exec_stats=False):
     import torch
     from pinot_amd import parse_sql
     from pinot_amd import _lib as L
@@ -206,6 +218,7 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
     for name, sql, flags in queries:
         if only and name != only:
             continue
+        sql = sql or _bench().QUERY
         vs = variants or (((0, ""),) if no_stepmajor else ((0, ""), (L.PA_QF_NO_LANE_MAJOR, "_stepmajor")))
         for extra, tag in vs:
             ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags | extra)
@@ -250,6 +263,14 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
                                  "algorithmic_bytes_per_launch": algo}
             if cpu_sample:
                 extra["cpu_baseline"] = cpu_port_baseline(sql, host)
+            if exec_stats:
+                # numEntriesScannedInFilter / PostFilter of every segment (leaf bitmaps + counts on the GPU, closed
+                # forms on the host: filter_stats.server_stats_device); the first call warms the allocator
+                ex.execution_stats(sp)
+                t3 = time.perf_counter()
+                in_f, post = ex.execution_stats(sp)
+                extra["exec_stats"] = {"ms": round((time.perf_counter() - t3) * 1e3, 3), "scan_ms": round(ms, 4),
+                                       "entries_in_filter": in_f, "entries_post_filter": post}
             print(json.dumps(dict({"workload": workload, "plan_name": name + tag, "kernel_ms": round(ms, 4),
                               "rows_per_s": st["num_docs"] / (ms * 1e-3), "staged_bytes": st["staged_bytes"],
                               "staged_GBps": st["staged_bytes"] / (ms * 1e-3) / 1e9, "fetch_ms": round(fetch_ms, 2), "e2e_ms": round(e2e_ms, 2),
@@ -271,6 +292,7 @@ def main():
     ap.add_argument("--sweep-part", action="store_true",
                     help="partitioned aggregation: sweep LDS per partition x workgroups per CU")
     ap.add_argument("--flags", type=int, default=None, help="run this one PA_QF_* flag set only")
+    ap.add_argument("--exec-stats", action="store_true", help="also time the execution statistics per plan")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="keep this many segments on the host: roofline + the C-port CPU baseline per line")
     args = ap.parse_args()
@@ -282,7 +304,8 @@ def main():
     import torch
     torch.cuda.set_device(0)
     for w in (WORKLOADS if args.workload == "all" else [args.workload]):
-        run(w, args.segments, args.docs, args.reps, args.plan, args.no_stepmajor, variants, args.cpu_sample)
+        run(w, args.segments, args.docs, args.reps, args.plan, args.no_stepmajor, variants, args.cpu_sample,
+            args.exec_stats)
 
 
 if __name__ == "__main__":
