@@ -300,7 +300,8 @@ int64_t pa_query_num_groups_limit_reached(const pa_query* q);
 int64_t pa_query_leaf_bitmap_words(const pa_query* q, int32_t segment);
 int pa_query_leaf_bitmaps(pa_query* q, int32_t segment, uint32_t* device_out, void* stream);
 
-/* Counts over leaf doc bitmaps (pa_query_leaf_bitmaps' layout: leaf l's `words` words at device_bitmaps + l * words)
+/* Counts over leaf doc bitmaps (pa_query_leaf_bitmaps' layout: leaf l's `words` words at device_bitmaps + l * words,
+ * `words` a multiple of 4 covering num_docs)
  * for the execution statistics' closed forms (pinot_amd/filter_stats.py device path), replacing the doc-by-doc replay of
  * the reference's iterators (SVScanDocIdIterator.java:76-142, AndDocIdIterator.java:39-73, AndDocIdSet.java:72-186).
  * prog_a / prog_b: postfix programs over the leaves (a token >= 0 pushes leaf `token`; PA_BIT_AND / PA_BIT_OR pop two
@@ -309,7 +310,8 @@ int pa_query_leaf_bitmaps(pa_query* q, int32_t segment, uint32_t* device_out, vo
  * popcount(A & B), and — when len_b > 0 — the leaps of AND(A, B)'s leap-frogging over two scan iterators (labelled
  * docs A-only / B-only / both, in doc order: an A-only doc after a both-doc or at the segment start, or an A-only /
  * B-only doc after the other, starts a leap), from which numEntriesScannedInFilter = num_docs + popcount(A & B) + leaps.
- * device_scratch: pa_bitmap_counts_scratch_bytes(words) bytes (unused when len_b == 0). Asynchronous on `stream`. */
+ * device_scratch: pa_bitmap_counts_scratch_bytes(words) bytes. Returns when the counts are written (synchronises
+ * `stream`). */
 #define PA_BIT_AND (-1)
 #define PA_BIT_OR (-2)
 #define PA_BIT_NOT (-3)
@@ -318,6 +320,13 @@ int64_t pa_bitmap_counts_scratch_bytes(int64_t words);
 int pa_bitmap_counts(const uint32_t* device_bitmaps, int64_t words, int32_t num_leaves, int64_t num_docs,
                      const int32_t* prog_a, int32_t len_a, const int32_t* prog_b, int32_t len_b, void* device_scratch,
                      int64_t* device_out, void* stream);
+/* The same counts for many (segment, program A, program B) requests of a prepared query in one pass: the leaf
+ * bitmaps of every requested segment (pa_query_leaf_bitmaps) in one launch, then the count kernels for all requests
+ * in one launch each. Request r: segments[r], its programs at programs + r * 2 * PA_BIT_PROG_MAX (A, then B at
+ * + PA_BIT_PROG_MAX), lengths[2r], lengths[2r + 1] (B may be empty). Writes out[4r .. 4r + 3] (host memory) and
+ * returns when they are written (synchronises `stream`). Device scratch is owned by the query. */
+int pa_query_filter_counts(pa_query* q, int32_t num_requests, const int32_t* segments, const int32_t* programs,
+                           const int32_t* lengths, int64_t* out, void* stream);
 
 /* Group-key layout. Direct (hashed = 0): key = sum_j id_j * prod_{k<j} cardinality_k. Hashed (hashed = 1, chosen when
  * a group-by column is raw or the product of cardinalities is too large to address): the key packs component j

@@ -49,7 +49,7 @@ EXPORTED = [
     "pa_query_accumulator_bytes", "pa_query_set_accumulator_buffer", "pa_query_num_sections", "pa_query_section",
     "pa_query_fetch", "pa_query_matched_docs", "pa_query_key_layout", "pa_query_limit_trimming",
     "pa_query_num_groups_limit_reached", "pa_query_stats", "pa_query_leaf_bitmap_words", "pa_query_leaf_bitmaps",
-    "pa_bitmap_counts_scratch_bytes", "pa_bitmap_counts",
+    "pa_bitmap_counts_scratch_bytes", "pa_bitmap_counts", "pa_query_filter_counts",
     "pa_query_plan", "pa_query_destroy",
 ]
 
@@ -139,6 +139,7 @@ def _declare(lib):
         "pa_query_leaf_bitmaps": (ctypes.c_int, [vp, i32, vp, vp]),
         "pa_bitmap_counts_scratch_bytes": (i64, [i64]),
         "pa_bitmap_counts": (ctypes.c_int, [vp, i64, i32, i64, vp, i32, vp, i32, vp, vp, vp]),
+        "pa_query_filter_counts": (ctypes.c_int, [vp, i32, vp, vp, vp, vp, vp]),
         "pa_query_plan": (ctypes.c_int, [vp] + [ctypes.POINTER(i32)] * 7),
         "pa_query_destroy": (None, [vp]),
     }

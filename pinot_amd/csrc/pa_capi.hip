@@ -552,6 +552,7 @@ struct pa_query {
   DevBuf lim_admit;
   int limit_grid = 0;
   DevBuf lim_keys, lim_pos, lim_hist, lim_sel, lim_thresh;
+  DevBuf stat_buf;  // pa_query_filter_counts: leaf bitmaps, scratch, counts, jobs (grown on demand)
   std::vector<LmSegPlan> hplans;
   std::vector<DevBuf> owned;  // LUTs, remaps, HLL LUTs, value dictionaries
   DevBuf acc;                 // all accumulator sections (unless the caller provided the block)
@@ -571,6 +572,7 @@ struct pa_query {
     dev_free(lim_hist);
     dev_free(lim_sel);
     dev_free(lim_thresh);
+    dev_free(stat_buf);
     dev_free(lim_admit);
     if (host_acc) (void)hipHostFree(host_acc);
     dev_free(fetch_blocks);
@@ -2437,10 +2439,13 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   return m;
 }
 
+// words per leaf bitmap: whole 64-doc steps, rounded up to 4 words (the count kernels read 16-byte groups)
+int64_t leaf_words(int64_t num_docs) { return (num_docs + 127) / 128 * 4; }
+
 int64_t pa_query_leaf_bitmap_words(const pa_query* q, int32_t segment) {
   if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
   if (segment < 0 || segment >= q->nseg) return fail(PA_EINVAL, "segment index out of range");
-  return ((int64_t)q->segs[segment]->num_docs + 63) / 64 * 2;
+  return leaf_words((int64_t)q->segs[segment]->num_docs);
 }
 
 int pa_query_leaf_bitmaps(pa_query* q, int32_t segment, uint32_t* device_out, void* stream) {
@@ -2461,45 +2466,207 @@ int pa_query_leaf_bitmaps(pa_query* q, int32_t segment, uint32_t* device_out, vo
   return PA_OK;
 }
 
+// Validated postfix program of pa_bitmap_counts / pa_query_filter_counts into tok[0..len).
+int check_bit_prog(const int32_t* prog, int32_t len, int32_t num_leaves, bool required, int32_t* tok) {
+  if (len < 0 || len > kBitProgMax || (required && len == 0) || (len > 0 && !prog))
+    return fail(PA_EINVAL, "bitmap program length out of range");
+  int depth = 0;
+  for (int i = 0; i < len; ++i) {
+    const int32_t t = prog[i];
+    if (t >= 0) {
+      if (t >= num_leaves) return fail(PA_EINVAL, "bitmap program names a leaf out of range");
+      if (++depth > kBitProgStack) return fail(PA_EINVAL, "bitmap program too deep");
+    } else if (t == PA_BIT_NOT) {
+      if (depth < 1) return fail(PA_EINVAL, "bitmap program: NOT on an empty stack");
+    } else if (t == PA_BIT_AND || t == PA_BIT_OR) {
+      if (depth < 2) return fail(PA_EINVAL, "bitmap program: AND/OR needs two masks");
+      --depth;
+    } else {
+      return fail(PA_EINVAL, "bitmap program: unknown token");
+    }
+    tok[i] = t;
+  }
+  if (len > 0 && depth != 1) return fail(PA_EINVAL, "bitmap program must leave exactly one mask");
+  return PA_OK;
+}
+
+constexpr size_t kBitTokBytes = 2 * kBitProgMax * 4;
+
+// The count kernels keep up to 4 leaves' words in registers: renumber the programs' leaf tokens to positions in
+// job.uleaf when they use at most 4 distinct leaves (else nu = 0: leaf ids, loaded in program order).
+void renumber_leaves(BitJob& job, int32_t* tok) {
+  int32_t u[4];
+  int nu = 0;
+  const int lens[2] = {job.len_a, job.len_b};
+  for (int k = 0; k < 2; ++k)
+    for (int i = 0; i < lens[k]; ++i) {
+      const int32_t t = tok[k * kBitProgMax + i];
+      if (t < 0) continue;
+      int p = 0;
+      while (p < nu && u[p] != t) ++p;
+      if (p == nu) {
+        if (nu == 4) {
+          job.nu = 0;
+          return;
+        }
+        u[nu++] = t;
+      }
+    }
+  for (int k = 0; k < 2; ++k)
+    for (int i = 0; i < lens[k]; ++i) {
+      int32_t& t = tok[k * kBitProgMax + i];
+      if (t < 0) continue;
+      int p = 0;
+      while (u[p] != t) ++p;
+      t = p;
+    }
+  job.nu = nu;
+  for (int p = 0; p < 4; ++p) job.uleaf[p] = p < nu ? u[p] : 0;
+}
+
+BitJob make_bit_job(const uint32_t* bm, int64_t words, int64_t num_docs, int64_t first_block, const int32_t* tok,
+                    int32_t len_a, int32_t len_b, uint32_t* scratch, int64_t* out) {
+  BitJob j{};
+  j.bm = bm;
+  j.words = words;
+  j.num_docs = num_docs;
+  j.first_block = first_block;
+  j.nb = bit_count_blocks(num_docs);
+  j.tok = tok;
+  j.len_a = len_a;
+  j.len_b = len_b;
+  j.scratch = scratch;
+  // the partial counts after block_last / block_in, 8-byte aligned (bit_count_scratch_words: 10 words per workgroup)
+  j.part = scratch ? (unsigned long long*)(((uintptr_t)(scratch + 2 * j.nb) + 7) & ~(uintptr_t)7) : nullptr;
+  j.out = (unsigned long long*)out;
+  return j;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 int64_t pa_bitmap_counts_scratch_bytes(int64_t words) {
   if (words < 0) return fail(PA_EINVAL, "negative word count");
-  return 4 * bit_count_scratch_words(words);
+  return (int64_t)(align256(4 * (size_t)bit_count_scratch_words(words)) + align256(4 * (size_t)bit_count_blocks(32 * words)) +
+                   align256(sizeof(BitJob)) + kBitTokBytes);
 }
 
 int pa_bitmap_counts(const uint32_t* device_bitmaps, int64_t words, int32_t num_leaves, int64_t num_docs,
                      const int32_t* prog_a, int32_t len_a, const int32_t* prog_b, int32_t len_b, void* device_scratch,
                      int64_t* device_out, void* stream) {
-  if (!device_out || num_docs < 0 || words < (num_docs + 31) / 32) return fail(PA_EINVAL, "bad bitmap counts arguments");
+  if (!device_out || num_docs < 0 || words < (num_docs + 31) / 32 || words % 4 != 0)
+    return fail(PA_EINVAL, "bad bitmap counts arguments (words: a multiple of 4 covering num_docs)");
   if (num_docs > 0 && !device_bitmaps) return fail(PA_EINVAL, "null bitmaps");
-  BitProgs P{};
-  const int32_t* progs[2] = {prog_a, prog_b};
-  const int32_t lens[2] = {len_a, len_b};
-  for (int k = 0; k < 2; ++k) {
-    if (lens[k] < 0 || lens[k] > kBitProgMax || (k == 0 && lens[k] == 0) || (lens[k] > 0 && !progs[k]))
-      return fail(PA_EINVAL, "bitmap program length out of range");
-    int depth = 0;
-    for (int i = 0; i < lens[k]; ++i) {
-      const int32_t t = progs[k][i];
-      if (t >= 0) {
-        if (t >= num_leaves) return fail(PA_EINVAL, "bitmap program names a leaf out of range");
-        if (++depth > kBitProgStack) return fail(PA_EINVAL, "bitmap program too deep");
-      } else if (t == PA_BIT_NOT) {
-        if (depth < 1) return fail(PA_EINVAL, "bitmap program: NOT on an empty stack");
-      } else if (t == PA_BIT_AND || t == PA_BIT_OR) {
-        if (depth < 2) return fail(PA_EINVAL, "bitmap program: AND/OR needs two masks");
-        --depth;
-      } else {
-        return fail(PA_EINVAL, "bitmap program: unknown token");
-      }
-      P.tok[k * kBitProgMax + i] = t;
-    }
-    if (lens[k] > 0 && depth != 1) return fail(PA_EINVAL, "bitmap program must leave exactly one mask");
+  struct {
+    BitJob job;
+    int32_t tok[2 * kBitProgMax];
+  } h{};
+  int rc = check_bit_prog(prog_a, len_a, num_leaves, true, h.tok);
+  if (!rc) rc = check_bit_prog(prog_b, len_b, num_leaves, false, h.tok + kBitProgMax);
+  if (rc) return rc;
+  if (num_docs == 0) return PA_OK;
+  if (!device_scratch) return fail(PA_EINVAL, "null scratch");
+  char* sc = (char*)device_scratch;
+  const size_t off_table = align256(4 * (size_t)bit_count_scratch_words(words));
+  const size_t off_job = off_table + align256(4 * (size_t)bit_count_blocks(32 * words));
+  const size_t off_tok = off_job + align256(sizeof(BitJob));
+  h.job = make_bit_job(device_bitmaps, words, num_docs, 0, (const int32_t*)(sc + off_tok), len_a, len_b,
+                       (uint32_t*)sc, device_out);
+  renumber_leaves(h.job, h.tok);
+  hipStream_t st = (hipStream_t)stream;
+  PA_HIP(hipMemcpyAsync(sc + off_job, &h.job, sizeof(BitJob), hipMemcpyHostToDevice, st));
+  PA_HIP(hipMemcpyAsync(sc + off_tok, h.tok, kBitTokBytes, hipMemcpyHostToDevice, st));
+  PA_HIP(launch_bit_counts_batch((const BitJob*)(sc + off_job), 1, h.job.nb, len_b > 0, (int32_t*)(sc + off_table), st));
+  PA_HIP(hipStreamSynchronize(st));  // (the host staging above is on this stack frame)
+  return PA_OK;
+}
+
+int pa_query_filter_counts(pa_query* q, int32_t num_requests, const int32_t* segments, const int32_t* programs,
+                           const int32_t* lengths, int64_t* out, void* stream) {
+  if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
+  if (num_requests < 0 || (num_requests > 0 && (!segments || !programs || !lengths || !out)))
+    return fail(PA_EINVAL, "bad filter counts arguments");
+  if (num_requests == 0) return PA_OK;
+  const int nl = q->spec.num_leaves;
+  std::vector<int> leaf_lit(nl, -1);
+  for (int l = 0; l < nl; ++l) {
+    for (size_t i = 0; i < q->literals.size() && leaf_lit[l] < 0; ++i)
+      if (q->literals[i].leaf == l) leaf_lit[l] = (int)i;
+    if (leaf_lit[l] < 0) return fail(PA_EUNSUPPORTED, "filter leaf " + std::to_string(l) + " has no literal in the plan");
   }
-  P.len_a = len_a;
-  P.len_b = len_b;
-  if (len_b > 0 && num_docs > 0 && !device_scratch) return fail(PA_EINVAL, "null scratch");
-  PA_HIP(launch_bit_counts(P, device_bitmaps, words, num_docs, (uint32_t*)device_scratch,
-                           (unsigned long long*)device_out, (hipStream_t)stream));
+  // device layout: leaf bitmaps of every requested segment | per-request scratch | counts | jobs | leaf jobs | tokens
+  std::vector<int64_t> bm_off(q->nseg, -1);
+  size_t bm_words = 0;
+  for (int r = 0; r < num_requests; ++r) {
+    const int si = segments[r];
+    if (si < 0 || si >= q->nseg) return fail(PA_EINVAL, "request names a segment out of range");
+    if (bm_off[si] < 0) {
+      bm_off[si] = (int64_t)bm_words;
+      bm_words += (size_t)nl * (size_t)leaf_words(q->segs[si]->num_docs);
+    }
+  }
+  std::vector<int64_t> sc_off(num_requests);
+  size_t sc_words = 0;
+  std::vector<BitJob> jobs(num_requests);
+  std::vector<int32_t> tok((size_t)num_requests * 2 * kBitProgMax, 0);
+  bool any_b = false;
+  int64_t blocks = 0;
+  for (int r = 0; r < num_requests; ++r) {
+    int32_t* t = tok.data() + (size_t)r * 2 * kBitProgMax;
+    const int la = lengths[2 * r], lb = lengths[2 * r + 1];
+    int rc = check_bit_prog(programs + (size_t)r * 2 * kBitProgMax, la, nl, true, t);
+    if (!rc) rc = check_bit_prog(programs + (size_t)r * 2 * kBitProgMax + kBitProgMax, lb, nl, false, t + kBitProgMax);
+    if (rc) return rc;
+    any_b |= lb > 0;
+    const int64_t n = q->segs[segments[r]]->num_docs;
+    const int64_t words = leaf_words(n);
+    sc_off[r] = (int64_t)sc_words;
+    sc_words += (size_t)bit_count_scratch_words(words);
+    jobs[r] = make_bit_job(nullptr, words, n, blocks, nullptr, la, lb, nullptr, nullptr);
+    renumber_leaves(jobs[r], t);
+    blocks += jobs[r].nb;
+  }
+  std::vector<LeafJob> ljobs;
+  int64_t lblocks = 0;
+  for (int si = 0; si < q->nseg; ++si) {
+    if (bm_off[si] < 0 || q->segs[si]->num_docs == 0) continue;
+    const int64_t n = q->segs[si]->num_docs, words = leaf_words(n);
+    for (int l = 0; l < nl; ++l) {
+      ljobs.push_back(LeafJob{(const DevSeg*)q->dsegs.p + si, nullptr, n, lblocks, leaf_lit[l],
+                              q->literals[leaf_lit[l]].neg ? 1 : 0});
+      ljobs.back().out = (uint32_t*)(intptr_t)(bm_off[si] + (int64_t)l * words);  // (word offset; rebased below)
+      lblocks += leaf_bitmap_blocks(n);
+    }
+  }
+  const size_t o_bm = 0, o_sc = align256(4 * bm_words), o_out = o_sc + align256(4 * sc_words),
+               o_jobs = o_out + align256(32 * (size_t)num_requests),
+               o_ljobs = o_jobs + align256(sizeof(BitJob) * num_requests),
+               o_tok = o_ljobs + align256(sizeof(LeafJob) * std::max<size_t>(1, ljobs.size())),
+               o_table = o_tok + align256(4 * tok.size()), total = o_table + 4 * (size_t)std::max<int64_t>(1, blocks);
+  if (q->stat_buf.n < total) {
+    dev_free(q->stat_buf);
+    int rc = dev_alloc(q->stat_buf, total);
+    if (rc) return rc;
+  }
+  char* base = (char*)q->stat_buf.p;
+  for (int r = 0; r < num_requests; ++r) {
+    jobs[r].bm = (const uint32_t*)(base + o_bm) + bm_off[segments[r]];
+    jobs[r].tok = (const int32_t*)(base + o_tok) + (size_t)r * 2 * kBitProgMax;
+    jobs[r].scratch = (uint32_t*)(base + o_sc) + sc_off[r];
+    jobs[r].part = (unsigned long long*)(((uintptr_t)(jobs[r].scratch + 2 * jobs[r].nb) + 7) & ~(uintptr_t)7);
+    jobs[r].out = (unsigned long long*)(base + o_out) + 4 * (size_t)r;
+  }
+  for (LeafJob& lj : ljobs) lj.out = (uint32_t*)(base + o_bm) + (intptr_t)lj.out;
+  hipStream_t st = (hipStream_t)stream;
+  PA_HIP(hipMemcpyAsync(base + o_jobs, jobs.data(), sizeof(BitJob) * num_requests, hipMemcpyHostToDevice, st));
+  if (!ljobs.empty())
+    PA_HIP(hipMemcpyAsync(base + o_ljobs, ljobs.data(), sizeof(LeafJob) * ljobs.size(), hipMemcpyHostToDevice, st));
+  PA_HIP(hipMemcpyAsync(base + o_tok, tok.data(), 4 * tok.size(), hipMemcpyHostToDevice, st));
+  PA_HIP(hipMemsetAsync(base + o_out, 0, 32 * (size_t)num_requests, st));
+  PA_HIP(launch_leaf_bitmaps_batch((const LeafJob*)(base + o_ljobs), (int)ljobs.size(), lblocks, st));
+  PA_HIP(launch_bit_counts_batch((const BitJob*)(base + o_jobs), num_requests, blocks, any_b,
+                                 (int32_t*)(base + o_table), st));
+  PA_HIP(hipMemcpyAsync(out, base + o_out, 32 * (size_t)num_requests, hipMemcpyDeviceToHost, st));
+  PA_HIP(hipStreamSynchronize(st));
   return PA_OK;
 }
 

@@ -397,40 +397,96 @@ hipError_t launch_leaf_bitmap(const DevSeg* seg, int li, int flip, int64_t num_d
 }
 
 // ---------------------------------------------------------------- execution statistics over leaf bitmaps
-// Doc masks A and B are postfix programs over the leaf bitmaps (BitProgs). Word w of a mask: 32 docs. The counts feed
-// the closed forms of filter_stats.py: popcounts for the applyAnd chains and the post-filter docs, and for an AND of two
-// scan iterators (AndDocIdIterator.java:39-73 leap-frogging SVScanDocIdIterator.advance, which reads from the target
-// to the next match) the number of leaps. Labelled docs: A-only (1), B-only (2), both (3). In the sequence of labelled
-// docs, a leap starts at an A-only doc preceded by a both-doc (or the segment start), and at every A-only / B-only doc
-// preceded by the other of the two.
-constexpr int kBitBlockWords = 1024;  // words per workgroup: 256 threads x 4
+// Doc masks A and B are postfix programs over the leaf bitmaps. Word w of a mask: 32 docs. The counts feed the closed
+// forms of filter_stats.py: popcounts for the applyAnd chains and the post-filter docs, and for an AND of two scan
+// iterators (AndDocIdIterator.java:39-73 leap-frogging SVScanDocIdIterator.advance, which reads from the target to the
+// next match) the number of leaps. Labelled docs: A-only (1), B-only (2), both (3). In the sequence of labelled docs, a
+// leap starts at an A-only doc preceded by a both-doc (or the segment start), and at every A-only / B-only doc preceded
+// by the other of the two.
+// Batched form (pa_query_filter_counts): one launch per kernel for every request of every segment; a workgroup finds
+// its job by binary search over the jobs' first workgroup.
+constexpr int kBitBlockWords = 256 * 4 * kBitGroups;  // words per workgroup: 256 threads x kBitGroups 16-byte groups
 
-__device__ __forceinline__ uint32_t bit_prog_word(const BitProgs& P, int base, int len, const uint32_t* __restrict__ bm,
-                                                  int64_t words, int64_t w, uint32_t valid) {
-  uint32_t st[kBitProgStack];
-  int sp = 0;
-  for (int i = 0; i < len; ++i) {
-    const int t = P.tok[base + i];
-    if (t >= 0) {
-      st[sp++] = gp(bm)[(int64_t)t * words + w] & valid;
-    } else if (t == PA_BIT_NOT) {
-      st[sp - 1] = ~st[sp - 1] & valid;
-    } else {
-      --sp;
-      st[sp - 1] = t == PA_BIT_AND ? (st[sp - 1] & st[sp]) : (st[sp - 1] | st[sp]);
-    }
-  }
-  return sp > 0 ? st[0] : 0u;
+// Per-workgroup copy of the job and its programs, and an LDS operand stack per thread ([depth][thread]; a private
+// array would live in scratch memory).
+struct BitShared {
+  BitJob J;
+  int32_t tok[2 * kBitProgMax];
+  uint32_t stk[kBitProgStack][256];
+  uint32_t lds4[4];
+  unsigned long long part[4][4];
+};
+
+__device__ __forceinline__ void bit_load_job(const BitJob* __restrict__ jobs, int j, BitShared& S) {
+  if (threadIdx.x < sizeof(BitJob) / 4) ((uint32_t*)&S.J)[threadIdx.x] = gp((const uint32_t*)(jobs + j))[threadIdx.x];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * kBitProgMax; i += blockDim.x) S.tok[i] = gp(S.J.tok)[i];
+  __syncthreads();
 }
 
-__device__ __forceinline__ void bit_masks(const BitProgs& P, const uint32_t* bm, int64_t words, int64_t num_docs,
-                                          int64_t w, uint32_t& a, uint32_t& b) {
-  a = b = 0u;
-  const int64_t left = num_docs - 32 * w;
-  if (left <= 0) return;
-  const uint32_t valid = left >= 32 ? 0xffffffffu : ((1u << left) - 1u);
-  a = bit_prog_word(P, 0, P.len_a, bm, words, w, valid);
-  if (P.len_b > 0) b = bit_prog_word(P, kBitProgMax, P.len_b, bm, words, w, valid);
+// The thread's words of the job's leaves used by its programs (nu <= 4 distinct leaves, tokens renumbered to their
+// positions by the host): one 16-byte load per leaf and group, every load of a group issued before any is used.
+struct BitWords {
+  u32x4 lw[kBitGroups][4];
+};
+
+__device__ __forceinline__ void bit_load_words(const BitShared& S, int64_t w0, BitWords& W) {
+#pragma unroll
+  for (int g = 0; g < kBitGroups; ++g) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      W.lw[g][p] = u32x4{0u, 0u, 0u, 0u};
+      // (leaf bitmaps hold a multiple of 4 words covering num_docs: a group that starts before num_docs is in bounds)
+      if (p < S.J.nu && 32 * (w0 + 4 * g) < S.J.num_docs)
+        W.lw[g][p] = *(const AS1 u32x4*)(gp(S.J.bm) + (int64_t)S.J.uleaf[p] * S.J.words + w0 + 4 * g);
+    }
+  }
+}
+
+// word k of group g of one program's mask
+__device__ __forceinline__ uint32_t bit_eval(BitShared& S, int base, int len, const BitWords& W, int g, int k,
+                                             int64_t w, uint32_t valid) {
+  const int t0 = threadIdx.x;
+  int sp = 0;
+  for (int i = 0; i < len; ++i) {
+    const int t = S.tok[base + i];
+    if (t >= 0) {
+      uint32_t x;
+      if (S.J.nu > 0) {
+        x = t == 0 ? W.lw[g][0][k] : (t == 1 ? W.lw[g][1][k] : (t == 2 ? W.lw[g][2][k] : W.lw[g][3][k]));
+      } else {
+        x = gp(S.J.bm)[(int64_t)t * S.J.words + w];  // (more than 4 leaves: loads in program order)
+      }
+      S.stk[sp++][t0] = x & valid;
+    } else if (t == PA_BIT_NOT) {
+      S.stk[sp - 1][t0] = ~S.stk[sp - 1][t0] & valid;
+    } else {
+      --sp;
+      const uint32_t x = S.stk[sp - 1][t0], y = S.stk[sp][t0];
+      S.stk[sp - 1][t0] = t == PA_BIT_AND ? (x & y) : (x | y);
+    }
+  }
+  return S.stk[0][t0];
+}
+
+// masks A and B of the thread's kBitGroups * 4 words (w0 ..)
+__device__ __forceinline__ void bit_masks(BitShared& S, int64_t w0, uint32_t (&a)[kBitGroups * 4],
+                                          uint32_t (&b)[kBitGroups * 4]) {
+  BitWords W;
+  bit_load_words(S, w0, W);
+#pragma unroll
+  for (int g = 0; g < kBitGroups; ++g) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t w = w0 + 4 * g + k;
+      const int64_t left = S.J.num_docs - 32 * w;
+      const uint32_t valid = left >= 32 ? 0xffffffffu : (left <= 0 ? 0u : ((1u << left) - 1u));
+      a[4 * g + k] = b[4 * g + k] = 0u;
+      if (valid == 0u) continue;
+      a[4 * g + k] = bit_eval(S, 0, S.J.len_a, W, g, k, w, valid);
+      if (S.J.len_b > 0) b[4 * g + k] = bit_eval(S, kBitProgMax, S.J.len_b, W, g, k, w, valid);
+    }
+  }
 }
 
 // label of the highest labelled doc of a word (0: none)
@@ -443,7 +499,8 @@ __device__ __forceinline__ uint32_t last_label(uint32_t a, uint32_t b) {
 
 __device__ __forceinline__ uint32_t later_label(uint32_t x, uint32_t y) { return y != 0u ? y : x; }
 
-// inclusive "last labelled" scan over the 256 threads of the block (threads in order); returns the exclusive value
+// "last labelled" scan over the 256 threads of the workgroup (threads in doc order): the exclusive value per thread,
+// and the workgroup's last label in *total
 __device__ __forceinline__ uint32_t block_last_exclusive(uint32_t v, uint32_t* lds4, uint32_t* total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t inc = v;
@@ -465,28 +522,27 @@ __device__ __forceinline__ uint32_t block_last_exclusive(uint32_t v, uint32_t* l
   return exc;
 }
 
-__global__ void __launch_bounds__(256) bit_last_kernel(BitProgs P, const uint32_t* __restrict__ bm, int64_t words,
-                                                       int64_t num_docs, uint32_t* __restrict__ block_last) {
-  __shared__ uint32_t lds4[4];
-  const int64_t w0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+constexpr int kBitThreadWords = 4 * kBitGroups;
+
+__device__ __forceinline__ void bit_last_block(BitShared& S, int64_t blk) {
+  const int64_t w0 = (blk * 256 + threadIdx.x) * kBitThreadWords;
+  uint32_t a[kBitThreadWords], b[kBitThreadWords];
+  bit_masks(S, w0, a, b);
   uint32_t last = 0u;
-  for (int k = 0; k < 4; ++k) {
-    uint32_t a, b;
-    bit_masks(P, bm, words, num_docs, w0 + k, a, b);
-    last = later_label(last, last_label(a, b));
-  }
+#pragma unroll
+  for (int k = 0; k < kBitThreadWords; ++k) last = later_label(last, last_label(a[k], b[k]));
   uint32_t total;
-  block_last_exclusive(last, lds4, &total);
-  if (threadIdx.x == 0) gp(block_last)[blockIdx.x] = total;
+  block_last_exclusive(last, S.lds4, &total);
+  if (threadIdx.x == 0) gp(S.J.scratch)[blk] = total;
 }
 
-// one workgroup: block_in[i] = last label of blocks < i, or 3 (segment start) when none
-__global__ void __launch_bounds__(1024) bit_carry_kernel(const uint32_t* __restrict__ block_last, int64_t nb,
-                                                         uint32_t* __restrict__ block_in) {
-  __shared__ uint32_t part[1024];
+// 1024 threads: block_in[i] = last label of the job's workgroups < i, or 3 (segment start) when none
+__device__ __forceinline__ void bit_carry_block(const BitJob& J, uint32_t* part) {
+  const uint32_t* block_last = J.scratch;
+  uint32_t* block_in = J.scratch + J.nb;
   const int t = threadIdx.x;
-  const int64_t per = (nb + 1023) / 1024;
-  const int64_t b0 = t * per, b1 = b0 + per < nb ? b0 + per : nb;
+  const int64_t per = (J.nb + 1023) / 1024;
+  const int64_t b0 = t * per, b1 = b0 + per < J.nb ? b0 + per : J.nb;
   uint32_t v = 0u;
   for (int64_t i = b0; i < b1; ++i) v = later_label(v, gp(block_last)[i]);
   part[t] = v;
@@ -504,28 +560,25 @@ __global__ void __launch_bounds__(1024) bit_carry_kernel(const uint32_t* __restr
   }
 }
 
-__global__ void __launch_bounds__(256) bit_count_kernel(BitProgs P, const uint32_t* __restrict__ bm, int64_t words,
-                                                        int64_t num_docs, const uint32_t* __restrict__ block_in,
-                                                        unsigned long long* __restrict__ out) {
-  __shared__ uint32_t lds4[4];
-  const int64_t w0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  uint32_t a[4], b[4];
+__device__ __forceinline__ void bit_count_block(BitShared& S, int64_t blk) {
+  const int64_t w0 = (blk * 256 + threadIdx.x) * kBitThreadWords;
+  uint32_t a[kBitThreadWords], b[kBitThreadWords];
+  bit_masks(S, w0, a, b);
   uint32_t last = 0u;
-  for (int k = 0; k < 4; ++k) {
-    bit_masks(P, bm, words, num_docs, w0 + k, a[k], b[k]);
-    last = later_label(last, last_label(a[k], b[k]));
-  }
   unsigned long long pa = 0, pb = 0, pab = 0, leaps = 0;
-  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+  for (int k = 0; k < kBitThreadWords; ++k) {
+    last = later_label(last, last_label(a[k], b[k]));
     pa += __builtin_popcount(a[k]);
     pb += __builtin_popcount(b[k]);
     pab += __builtin_popcount(a[k] & b[k]);
   }
-  if (P.len_b > 0) {
+  if (S.J.len_b > 0) {
     uint32_t total;
-    uint32_t prev = block_last_exclusive(last, lds4, &total);
-    if (prev == 0u) prev = gp(block_in)[blockIdx.x];
-    for (int k = 0; k < 4; ++k) {
+    uint32_t prev = block_last_exclusive(last, S.lds4, &total);
+    if (prev == 0u) prev = gp(S.J.scratch + S.J.nb)[blk];
+#pragma unroll
+    for (int k = 0; k < kBitThreadWords; ++k) {
       uint32_t l = a[k] | b[k];
       while (l != 0u) {
         const int p = __builtin_ctz(l);
@@ -543,29 +596,200 @@ __global__ void __launch_bounds__(256) bit_count_kernel(BitProgs P, const uint32
     pab += __shfl_xor(pab, o, kWave);
     leaps += __shfl_xor(leaps, o, kWave);
   }
+  // the workgroup's four counts into its partial slot (summed per job by bit_sum_batch_kernel: no atomics on one
+  // address from every workgroup)
   if ((threadIdx.x & 63) == 0) {
-    atomicAdd(out + 0, pa);
-    atomicAdd(out + 1, pb);
-    atomicAdd(out + 2, pab);
-    atomicAdd(out + 3, leaps);
+    const int wv = threadIdx.x >> 6;
+    S.part[wv][0] = pa;
+    S.part[wv][1] = pb;
+    S.part[wv][2] = pab;
+    S.part[wv][3] = leaps;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int f = threadIdx.x;
+    gp(S.J.part)[4 * blk + f] = S.part[0][f] + S.part[1][f] + S.part[2][f] + S.part[3][f];
   }
 }
 
-int64_t bit_count_scratch_words(int64_t words) { return 2 * ((words + kBitBlockWords - 1) / kBitBlockWords); }
-
-hipError_t launch_bit_counts(const BitProgs& P, const uint32_t* bm, int64_t words, int64_t num_docs,
-                             uint32_t* scratch, unsigned long long* out, hipStream_t s) {
-  const int64_t live = (num_docs + 31) / 32;
-  const int64_t nb = (live + kBitBlockWords - 1) / kBitBlockWords;
-  if (nb == 0) return hipSuccess;
-  if (nb > INT32_MAX) return hipErrorInvalidValue;
-  uint32_t* block_last = scratch;
-  uint32_t* block_in = scratch + nb;
-  if (P.len_b > 0) {
-    bit_last_kernel<<<(int)nb, 256, 0, s>>>(P, bm, words, num_docs, block_last);
-    bit_carry_kernel<<<1, 1024, 0, s>>>(block_last, nb, block_in);
+// 1024 threads per job: out[f] = sum over the job's workgroups of part[4 * blk + f]
+__global__ void __launch_bounds__(1024) bit_sum_batch_kernel(const BitJob* __restrict__ jobs) {
+  __shared__ unsigned long long red[16][4];
+  const BitJob& J = jobs[blockIdx.x];
+  unsigned long long v[4] = {0, 0, 0, 0};
+  for (int64_t b = threadIdx.x; b < J.nb; b += 1024)
+    for (int f = 0; f < 4; ++f) v[f] += gp(J.part)[4 * b + f];
+  for (int f = 0; f < 4; ++f)
+    for (int o = 32; o > 0; o >>= 1) v[f] += __shfl_xor(v[f], o, kWave);
+  if ((threadIdx.x & 63) == 0)
+    for (int f = 0; f < 4; ++f) red[threadIdx.x >> 6][f] = v[f];
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    unsigned long long t = 0;
+    for (int w = 0; w < 16; ++w) t += red[w][threadIdx.x];
+    gp(J.out)[threadIdx.x] += t;  // (the caller zeroes out; pa_bitmap_counts adds)
   }
-  bit_count_kernel<<<(int)nb, 256, 0, s>>>(P, bm, words, num_docs, block_in, out);
+}
+
+// block -> job tables (one workgroup per job writes its range)
+__global__ void __launch_bounds__(256) bit_block_table_kernel(const BitJob* __restrict__ jobs,
+                                                              int32_t* __restrict__ table) {
+  const BitJob& J = jobs[blockIdx.x];
+  for (int64_t b = threadIdx.x; b < J.nb; b += blockDim.x) gp(table)[J.first_block + b] = (int32_t)blockIdx.x;
+}
+
+__global__ void __launch_bounds__(256) bit_last_batch_kernel(const BitJob* __restrict__ jobs,
+                                                             const int32_t* __restrict__ table) {
+  __shared__ BitShared S;
+  bit_load_job(jobs, gp(table)[blockIdx.x], S);
+  if (S.J.len_b > 0) bit_last_block(S, blockIdx.x - S.J.first_block);
+}
+
+__global__ void __launch_bounds__(1024) bit_carry_batch_kernel(const BitJob* __restrict__ jobs) {
+  __shared__ uint32_t part[1024];
+  const BitJob& J = jobs[blockIdx.x];
+  if (J.len_b > 0 && J.nb > 0) bit_carry_block(J, part);
+}
+
+__global__ void __launch_bounds__(256) bit_count_batch_kernel(const BitJob* __restrict__ jobs,
+                                                              const int32_t* __restrict__ table) {
+  __shared__ BitShared S;
+  bit_load_job(jobs, gp(table)[blockIdx.x], S);
+  bit_count_block(S, blockIdx.x - S.J.first_block);
+}
+
+int64_t bit_count_blocks(int64_t num_docs) { return ((num_docs + 31) / 32 + kBitBlockWords - 1) / kBitBlockWords; }
+
+// per workgroup: block_last, block_in (u32) and the four partial counts (u64)
+int64_t bit_count_scratch_words(int64_t words) { return 10 * ((words + kBitBlockWords - 1) / kBitBlockWords); }
+
+hipError_t launch_bit_counts_batch(const BitJob* jobs, int nj, int64_t total_blocks, bool any_b, int32_t* table,
+                                   hipStream_t s) {
+  if (nj == 0 || total_blocks == 0) return hipSuccess;
+  if (total_blocks > INT32_MAX) return hipErrorInvalidValue;
+  bit_block_table_kernel<<<nj, 256, 0, s>>>(jobs, table);
+  if (any_b) {
+    bit_last_batch_kernel<<<(int)total_blocks, 256, 0, s>>>(jobs, table);
+    bit_carry_batch_kernel<<<nj, 1024, 0, s>>>(jobs);
+  }
+  bit_count_batch_kernel<<<(int)total_blocks, 256, 0, s>>>(jobs, table);
+  bit_sum_batch_kernel<<<nj, 1024, 0, s>>>(jobs);
+  return hipGetLastError();
+}
+
+// Leaf bitmaps of many (segment, leaf) pairs in one launch: job j covers wave steps [first_step, first_step + steps)
+// of its segment (64 docs per step, one ballot, two words), as leaf_bitmap_kernel.
+constexpr int kLeafStepsPerWave = 128;  // wave steps (64 docs) per wave
+constexpr int kLeafBatch = 16;         // steps whose loads are in flight together
+
+// kLeafBatch wave steps from s0 of one leaf: every load of the batch issued before any is used
+__device__ __forceinline__ void leaf_bitmap_batch(const DevLeaf& L, int64_t n, int flip, uint32_t* out, int64_t s0,
+                                                  int lane) {
+  if (s0 * kWave >= n) return;
+  if (L.kind == PA_LEAF_DICT_RANGE || L.kind == PA_LEAF_DICT_SET) {
+    // (forward indexes are padded to whole wave tiles: the decodes past num_docs stay in bounds)
+    uint32_t id[kLeafBatch];
+#pragma unroll
+    for (int k = 0; k < kLeafBatch; ++k) id[k] = decode_global(L.words, (s0 + k) * kWave + lane, L.nbits);
+    bool m[kLeafBatch];
+    if (L.kind == PA_LEAF_DICT_RANGE) {
+      const int sh = 32 - L.nbits;
+      const uint32_t lo = (uint32_t)L.lo >> sh;
+      const uint32_t span = (uint32_t)(((uint64_t)(uint32_t)L.span + 1u) >> sh);
+#pragma unroll
+      for (int k = 0; k < kLeafBatch; ++k) m[k] = (id[k] - lo) < span;
+    } else {
+#pragma unroll
+      for (int k = 0; k < kLeafBatch; ++k) m[k] = (gp(L.lut)[id[k] >> 5] >> (id[k] & 31u)) & 1u;
+    }
+#pragma unroll
+    for (int k = 0; k < kLeafBatch; ++k) {
+      const int64_t st = s0 + k;
+      const int64_t doc = st * kWave + lane;
+      const uint64_t b = __ballot(doc < n && (m[k] != ((L.negate != 0) != (flip != 0))));
+      if (st * kWave < n && lane < 2) gp(out)[2 * st + lane] = (uint32_t)(b >> (32 * lane));
+    }
+    return;
+  }
+  for (int k = 0; k < kLeafBatch; ++k) {
+    const int64_t st = s0 + k;
+    const int64_t doc = st * kWave + lane;
+    if (st * kWave >= n) break;
+    const bool m = doc < n && (leaf_match_doc(L, doc) != (flip != 0));
+    const uint64_t b = __ballot(m);
+    if (lane < 2) gp(out)[2 * st + lane] = (uint32_t)(b >> (32 * lane));
+  }
+}
+
+
+// Single-value dictionary leaves, lane-major: a wave takes a whole wave tile (2048 docs), lane l docs [32l, 32l + 32),
+// which are exactly the lane's nb stream words (the same layout the scan stages): the tile's 64 * nb words arrive as
+// coalesced 16-byte loads into the wave's LDS region, and leaf_lm decodes the lane's 32 docs into one bitmap word.
+constexpr int kLeafTilesPerWave = 4;
+
+__device__ __forceinline__ void leaf_bitmap_tiles_lm(const DevLeaf& L, int64_t n, int flip, uint32_t* out,
+                                                     int64_t t0, int lane, uint32_t* region) {
+  const int nb = L.nbits;
+  const uint32_t region_lds = lds_addr(region);
+  for (int64_t t = t0; t < t0 + kLeafTilesPerWave; ++t) {
+    const int64_t base = t * kWTileDocs;
+    if (base >= n) return;
+    const AS1 u32x4* src = (const AS1 u32x4*)(gp(L.words) + t * (int64_t)(kWave * nb));
+    for (int c = lane; c < 16 * nb; c += kWave) ((lds_u32x4_t*)lds_ptr(region))[c] = src[c];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the region written before the decode reads it
+    uint32_t bits = leaf_lm_any(nb, L.kind, region_lds, lane, (uint32_t)L.lo, (uint32_t)L.span, L.lut);
+    if ((L.negate != 0) != (flip != 0)) bits = ~bits;
+    const int64_t left = n - (base + 32 * lane);
+    bits &= left >= 32 ? 0xffffffffu : (left <= 0 ? 0u : ((1u << left) - 1u));
+    // (a leaf's bitmap holds (n + 127) / 128 * 4 words, not whole tiles: the next leaf's bitmap follows it)
+    if (t * kWave + lane < (n + 127) / 128 * 4) gp(out)[t * kWave + lane] = bits;
+    asm volatile("" ::: "memory");  // (this tile's reads before the next tile's writes)
+  }
+}
+
+__global__ void __launch_bounds__(256) leaf_bitmaps_batch_kernel(const LeafJob* __restrict__ jobs, int nj) {
+  __shared__ LeafJob SJ;
+  __shared__ DevLeaf SL;
+  __shared__ u32x4 regions[4][kWave * 32 / 4];  // one wave tile of a <= 32-bit column per wave
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = nj - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid].first_block <= (int64_t)blockIdx.x) lo = mid;
+      else hi = mid - 1;
+    }
+    SJ = jobs[lo];
+  }
+  __syncthreads();
+  if (threadIdx.x < sizeof(DevLeaf) / 4)
+    ((uint32_t*)&SL)[threadIdx.x] = gp((const uint32_t*)&SJ.seg->leaves[SJ.li])[threadIdx.x];
+  __syncthreads();
+  const DevLeaf L = SL;  // (registers)
+  const int64_t n = SJ.num_docs;
+  uint32_t* out = SJ.out;
+  const int flip = SJ.flip;
+  const int lane = threadIdx.x & 63;
+  const int64_t blk = (int64_t)blockIdx.x - SJ.first_block;
+  if (L.kind == PA_LEAF_DICT_RANGE || L.kind == PA_LEAF_DICT_SET) {
+    leaf_bitmap_tiles_lm(L, n, flip, out, (blk * 4 + (threadIdx.x >> 6)) * kLeafTilesPerWave, lane,
+                         (uint32_t*)regions[threadIdx.x >> 6]);
+    return;
+  }
+  // MV and raw leaves: per doc (leaf_match_doc), 64 docs per step
+  const int64_t sw = (blk * 4 + (threadIdx.x >> 6)) * kLeafStepsPerWave;
+  for (int64_t s0 = sw; s0 < sw + kLeafStepsPerWave; s0 += kLeafBatch) leaf_bitmap_batch(L, n, flip, out, s0, lane);
+}
+
+static_assert(kLeafStepsPerWave * kWave == kLeafTilesPerWave * kWTileDocs, "one work split for both leaf paths");
+
+int64_t leaf_bitmap_blocks(int64_t num_docs) {
+  return ((num_docs + kWave - 1) / kWave + 4 * kLeafStepsPerWave - 1) / (4 * kLeafStepsPerWave);
+}
+
+hipError_t launch_leaf_bitmaps_batch(const LeafJob* jobs, int nj, int64_t total_blocks, hipStream_t s) {
+  if (nj == 0 || total_blocks == 0) return hipSuccess;
+  if (total_blocks > INT32_MAX) return hipErrorInvalidValue;
+  leaf_bitmaps_batch_kernel<<<(int)total_blocks, 256, 0, s>>>(jobs, nj);
   return hipGetLastError();
 }
 

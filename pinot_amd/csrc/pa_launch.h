@@ -32,17 +32,35 @@ hipError_t launch_compact_final(const unsigned long long* count, int64_t K, int 
                                 int64_t cap, const FinalDesc* d, hipStream_t s);
 // one filter literal of one segment -> doc bitmap (execution statistics)
 hipError_t launch_leaf_bitmap(const DevSeg* seg, int li, int flip, int64_t num_docs, uint32_t* out, hipStream_t s);
-// Execution-statistics counts over leaf bitmaps (pa_bitmap_counts): postfix programs A (tok[0..len_a)) and B
-// (tok[kBitProgMax..+len_b)).
+// Execution-statistics counts over leaf bitmaps (pa_bitmap_counts, pa_query_filter_counts): per job, postfix
+// programs A (tok[0..len_a)) and B (tok[kBitProgMax..+len_b)) over one segment's leaf bitmaps.
 constexpr int kBitProgMax = 64;
 constexpr int kBitProgStack = 16;
-struct BitProgs {
+constexpr int kBitGroups = 4;  // 16-byte word groups per thread of the count kernels
+struct BitJob {
+  const uint32_t* bm;  // the segment's leaf bitmaps, leaf l at bm + l * words
+  int64_t words, num_docs;
+  int64_t first_block, nb;
+  const int32_t* tok;  // program A at tok[0..len_a), B at tok[kBitProgMax..+len_b)
   int32_t len_a, len_b;
-  int32_t tok[2 * kBitProgMax];
+  int32_t nu, pad;     // nu > 0: the programs use leaves uleaf[0..nu) and their leaf tokens are positions in it
+  int32_t uleaf[4];
+  uint32_t* scratch;   // block_last[nb], block_in[nb]
+  unsigned long long* part;  // [nb][4] per-workgroup counts
+  unsigned long long* out;
 };
+struct LeafJob {  // leaf bitmap of one (segment, leaf): workgroups [first_block, + leaf_bitmap_blocks(num_docs))
+  const DevSeg* seg;
+  uint32_t* out;
+  int64_t num_docs, first_block;
+  int32_t li, flip;
+};
+int64_t leaf_bitmap_blocks(int64_t num_docs);
+int64_t bit_count_blocks(int64_t num_docs);
 int64_t bit_count_scratch_words(int64_t words);
-hipError_t launch_bit_counts(const BitProgs& P, const uint32_t* bm, int64_t words, int64_t num_docs,
-                             uint32_t* scratch, unsigned long long* out, hipStream_t s);
+hipError_t launch_bit_counts_batch(const BitJob* jobs, int nj, int64_t total_blocks, bool any_b, int32_t* table,
+                                   hipStream_t s);
+hipError_t launch_leaf_bitmaps_batch(const LeafJob* jobs, int nj, int64_t total_blocks, hipStream_t s);
 hipError_t launch_compact(const unsigned long long* count, int64_t K, int all, uint32_t* block_sums, int64_t cap,
                           const CompactDesc* d, int phase, hipStream_t s);
 // numGroupsLimit first-seen trimming (pa_kernels.hip "numGroupsLimit"): the (segment, key) first-position table,

@@ -286,6 +286,7 @@ class GpuQueryExecutor:
                 col = seg.column(pred.column)
                 params.append(P.dictionary_leaf(pred, col) if col.has_dictionary else P.raw_leaf(pred, col))
             per_seg.append(params)
+        self.leaf_params = per_seg  # (also the execution statistics' leaf evaluators: filter_stats)
         spec.num_leaves = len(leaves)
         for li, pred in enumerate(leaves):
             kinds = {ps[li].kind for ps in per_seg}

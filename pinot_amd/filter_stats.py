@@ -27,8 +27,9 @@ import ctypes
 
 import numpy as np
 
+from . import _lib as L
 from . import query as Q
-from .predicate import dictionary_leaf, expand_raw_in
+from .predicate import DictLeaf, dictionary_leaf, expand_raw_in
 
 EOF = -1
 BATCH = 256  # BlockDocIdIterator.OPTIMAL_ITERATOR_BATCH_SIZE
@@ -295,14 +296,19 @@ class _LeafCursor:
         self.k += _count_leaves(sub)
         return m
 
+    def param(self):
+        return None
 
-def _leaf_op(pred, seg, mask, index_info):
-    """FilterOperatorUtils.getLeafFilterOperator (no null handling)."""
+
+def _leaf_op(pred, seg, mask, index_info, lf=None):
+    """FilterOperatorUtils.getLeafFilterOperator (no null handling). lf: the leaf's dictionary_leaf when the caller
+    has it already (the executor's bound leaf parameters)."""
     col = seg.column(pred.column)
     sv = col.single_value
     if col.has_dictionary:
         # dictionary-based predicate evaluators: always false with no matching dictId, always true with all of them
-        lf = dictionary_leaf(pred, col)
+        if lf is None:
+            lf = dictionary_leaf(pred, col)
         n = (lf.hi - lf.lo) if lf.ids is None else len(np.unique(lf.ids))
         n = max(0, n)
         if lf.negate:
@@ -353,7 +359,8 @@ def _build(f, seg, cursor, index_info):
         if c.kind == "empty":
             return _Op("all")
         return _Op("not", c.prio, children=[c])
-    return _leaf_op(f, seg, cursor.take(f), index_info)
+    mask = cursor.take(f)
+    return _leaf_op(f, seg, mask, index_info, cursor.param())
 
 
 def _iterator(op, n, scans):
@@ -499,7 +506,6 @@ class _Unsupported(Exception):
 
 def _rpn(f, start):
     """Postfix program (pa_bitmap_counts tokens) of an expanded predicate subtree over the leaves [start, ...)."""
-    from . import _lib as L
     if isinstance(f, (Q.And, Q.Or)):
         out, k = [], start
         for i, c in enumerate(f.children):
@@ -516,18 +522,27 @@ def _rpn(f, start):
 class _RpnCursor(_LeafCursor):
     """_LeafCursor whose masks are postfix programs instead of host bitmaps."""
 
-    def __init__(self, segment):
+    def __init__(self, segment, params=None):
         super().__init__(None, segment)
+        self.params, self.last = params, None
 
     def take(self, pred):
         sub = expand_raw_in(pred, self.segment)
         p = _rpn(sub, self.k)
-        self.k += _count_leaves(sub)
+        n = _count_leaves(sub)
+        self.last = self.k if n == 1 else None
+        self.k += n
         return p
+
+    def param(self):
+        """The bound leaf parameters of the last single-leaf predicate (DictLeaf for a dictionary column)."""
+        if self.params is None or self.last is None:
+            return None
+        lf = self.params[self.last]
+        return lf if isinstance(lf, DictLeaf) else None
 
 
 def _and_prog(progs):
-    from . import _lib as L
     out = list(progs[0])
     for p in progs[1:]:
         out += list(p) + [L.PA_BIT_AND]
@@ -546,7 +561,6 @@ class _Terms:
         return self
 
     def request(self, reqs, si, a, b, field, coef=1):
-        from . import _lib as L
         if len(a) > L.PA_BIT_PROG_MAX or len(b) > L.PA_BIT_PROG_MAX:
             raise _Unsupported("bitmap program too long")
         key = (si, tuple(a), tuple(b))
@@ -600,20 +614,23 @@ def _cost_next(op, seg, si, reqs):
     raise _Unsupported("AND leap-frogging other than two SV scans")
 
 
-def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps):
+def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps, leaf_params=None):
     """server_stats through the closed forms above. counts_fn(reqs) -> int64[len(reqs), 4]: for every request
     (segment index, program A, program B) -> row, pa_bitmap_counts' four counts. Segments without a closed form replay
-    the iterators over leaf_bitmaps(i) (host bitmaps, as server_stats)."""
+    the iterators over leaf_bitmaps(i) (host bitmaps, as server_stats). leaf_params[i]: segment i's bound leaf
+    parameters in leaf order (GpuQueryExecutor.leaf_params), reused instead of re-matching the dictionaries."""
     ncols = projected_columns(query)
     filt = query.filter
     reqs = {}
     plans = []  # per segment: None (non-scan plan), "host", or (in_filter _Terms, docs _Terms)
+    flat = _flatten(filt) if filt is not None else None
     for si, seg in enumerate(segments):
         if filt is None:
             plans.append(None if non_scan_plan(query, seg, True) else (_Terms(0), _Terms(seg.num_docs)))
             continue
         try:
-            op = _build(_flatten(filt), seg, _RpnCursor(seg), segment_index_info(seg))
+            op = _build(flat, seg, _RpnCursor(seg, None if leaf_params is None else leaf_params[si]),
+                        segment_index_info(seg))
             if non_scan_plan(query, seg, op.kind == "all"):
                 plans.append(None)
                 continue
@@ -637,39 +654,26 @@ def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps):
 
 
 def device_counts(executor, segments, reqs, stream=None):
-    """pa_bitmap_counts for every request, per segment over one pa_query_leaf_bitmaps pass into a reused device
-    buffer; one synchronisation at the end."""
-    import torch
-    from . import _lib as L
-    lib = L.lib()
-    dev = torch.device("cuda", torch.cuda.current_device())
-    out = torch.zeros((len(reqs), 4), dtype=torch.int64, device=dev)
-    by_seg = {}
+    """pa_bitmap_counts' four counts for every request (segment index, program A, program B): one
+    pa_query_filter_counts call (leaf bitmaps of every requested segment, then the count kernels, one launch each)."""
+    n = len(reqs)
+    pm = L.PA_BIT_PROG_MAX
+    segs = np.zeros(n, dtype=np.int32)
+    progs = np.zeros((n, 2, pm), dtype=np.int32)
+    lens = np.zeros((n, 2), dtype=np.int32)
     for (si, a, b), r in reqs.items():
-        by_seg.setdefault(si, []).append((a, b, r))
-    nl = int(executor.spec.num_leaves)
-    words = {si: int(L.check(lib.pa_query_leaf_bitmap_words(executor.handle, si), "pa_query_leaf_bitmap_words"))
-             for si in by_seg}
-    wmax = max(words.values())
-    bm = torch.empty(max(1, nl * wmax), dtype=torch.int32, device=dev)
-    scratch = torch.empty(max(1, int(lib.pa_bitmap_counts_scratch_bytes(wmax)) // 4), dtype=torch.int32, device=dev)
-    progs = {}
-
-    def prog(p):
-        if p not in progs:
-            progs[p] = (ctypes.c_int32 * max(1, len(p)))(*p)
-        return progs[p]
-    bp, sp, op = bm.data_ptr(), scratch.data_ptr(), out.data_ptr()
-    for si, rs in by_seg.items():
-        L.check(lib.pa_query_leaf_bitmaps(executor.handle, si, bp, stream), "pa_query_leaf_bitmaps")
-        for a, b, r in rs:
-            L.check(lib.pa_bitmap_counts(bp, words[si], nl, segments[si].num_docs, prog(a), len(a), prog(b), len(b),
-                                         sp, op + 32 * r, stream), "pa_bitmap_counts")
-    torch.cuda.synchronize()  # (device-wide: covers `stream`)
-    return out.cpu().numpy()
+        segs[r] = si
+        progs[r, 0, :len(a)] = a
+        progs[r, 1, :len(b)] = b
+        lens[r] = (len(a), len(b))
+    out = np.zeros((n, 4), dtype=np.int64)
+    L.check(L.lib().pa_query_filter_counts(executor.handle, n, segs.ctypes.data, progs.ctypes.data, lens.ctypes.data,
+                                           out.ctypes.data, stream), "pa_query_filter_counts")
+    return out
 
 
 def server_stats_device(query, segments, executor, stream=None):
     """server_stats with the counts computed on the GPU (device_counts); same results."""
     return server_stats_closed_form(query, segments, lambda reqs: device_counts(executor, segments, reqs, stream),
-                                    lambda si: executor.leaf_bitmaps(si, stream))
+                                    lambda si: executor.leaf_bitmaps(si, stream),
+                                    getattr(executor, "leaf_params", None))

@@ -41,7 +41,7 @@ def _device_counts(bits, n, a, b):
 @pytest.mark.parametrize("n", [1, 31, 32, 33, 5000, 32 * 1024 + 7, 3_000_001])
 def test_bitmap_counts_kernel(n):
     rng = np.random.default_rng(n)
-    words = (n + 63) // 64 * 2
+    words = (n + 127) // 128 * 4
     progs = [([0], [1]), ([0, 1, OR], [2, NOT]), ([0, NOT, 2, AND], [1]), ([2], []), ([0, 1, AND, 2, OR], [0, NOT])]
     for dens in ([0.5, 0.5, 0.5], [0.02, 0.3, 0.9], [3.0 / n, 2.0 / n, 0.5], [1.0, 1.0, 0.0]):
         masks = np.stack([rng.random(n) < d for d in dens])
@@ -66,8 +66,10 @@ def test_bitmap_counts_rejects_bad_programs():
 def _segment(seed, n):
     rng = np.random.default_rng(seed)
     data = {"s": np.sort(rng.integers(0, 50, n)).astype(np.int32), "a": rng.integers(0, 100, n).astype(np.int32),
-            "b": rng.integers(0, 100, n).astype(np.int32), "c": rng.integers(0, 20, n).astype(np.int32)}
-    return create_segment("st%d" % seed, data, {k: "INT" for k in data}, inverted_index_columns=("c",))
+            "b": rng.integers(0, 100, n).astype(np.int32), "c": rng.integers(0, 20, n).astype(np.int32),
+            "r": rng.integers(0, 5000, n).astype(np.int32), "w": rng.integers(0, 1 << 20, n).astype(np.int32)}
+    return create_segment("st%d" % seed, data, {k: "INT" for k in data}, inverted_index_columns=("c",),
+                          no_dictionary_columns=("r",))
 
 
 def test_execution_stats_device_vs_replay():
@@ -76,7 +78,9 @@ def test_execution_stats_device_vs_replay():
     segs = [_segment(1, 200_003), _segment(2, 70_000), _segment(3, 1025)]
     gs = [GpuSegment(s) for s in segs]
     try:
-        for where in CLOSED_FORM_WHERES + HOST_WHERES:
+        # (+ a raw column: per-doc leaf path; a 20-bit dictionary: wide lane-major decode)
+        for where in CLOSED_FORM_WHERES + HOST_WHERES + ["r < 1000 AND a < 50", "r BETWEEN 10 AND 20 OR b = 3",
+                                                          "w < 300000 AND b < 40", "w IN (5, 77, 1000) OR a = 1"]:
             for sql in ("SELECT COUNT(*) FROM t WHERE " + where, "SELECT c, SUM(a) FROM t WHERE %s GROUP BY c" % where):
                 q = parse_sql(sql)
                 ex = GpuQueryExecutor(q, gs)

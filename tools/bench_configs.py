@@ -266,11 +266,21 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
             if exec_stats:
                 # numEntriesScannedInFilter / PostFilter of every segment (leaf bitmaps + counts on the GPU, closed
                 # forms on the host: filter_stats.server_stats_device); the first call warms the allocator
+                from pinot_amd import filter_stats as FS
                 ex.execution_stats(sp)
+                dev = []
+
+                def counts(reqs):
+                    t = time.perf_counter()
+                    r = FS.device_counts(ex, ex.segs, reqs, sp)
+                    dev.append((time.perf_counter() - t) * 1e3)
+                    return r
                 t3 = time.perf_counter()
-                in_f, post = ex.execution_stats(sp)
+                in_f, post = FS.server_stats_closed_form(ex.query, ex.segs, counts, lambda si: ex.leaf_bitmaps(si, sp),
+                                                         ex.leaf_params)
                 extra["exec_stats"] = {"ms": round((time.perf_counter() - t3) * 1e3, 3), "scan_ms": round(ms, 4),
-                                       "entries_in_filter": in_f, "entries_post_filter": post}
+                                       "device_counts_ms": round(sum(dev), 3), "entries_in_filter": in_f,
+                                       "entries_post_filter": post}
             print(json.dumps(dict({"workload": workload, "plan_name": name + tag, "kernel_ms": round(ms, 4),
                               "rows_per_s": st["num_docs"] / (ms * 1e-3), "staged_bytes": st["staged_bytes"],
                               "staged_GBps": st["staged_bytes"] / (ms * 1e-3) / 1e9, "fetch_ms": round(fetch_ms, 2), "e2e_ms": round(e2e_ms, 2),
