@@ -489,6 +489,25 @@ __device__ __forceinline__ void bit_masks(BitShared& S, int64_t w0, uint32_t (&a
   }
 }
 
+// Leaps of one word in constant time. Labelled docs L = a | b; for X a subset of L, the labelled docs whose predecessor
+// within the word is in X are (~L + (X << 1)) & L: each X bit's carry runs through the unlabelled docs above it and
+// stops at the next labelled doc (carries of different X bits never meet: each stops at a labelled doc first). The
+// word's lowest labelled doc follows `prev` (the last label before the word); prev becomes the word's last label.
+__device__ __forceinline__ uint32_t word_leaps(uint32_t a, uint32_t b, uint32_t& prev) {
+  const uint32_t l = a | b;
+  if (l == 0u) return 0u;
+  const uint32_t a1 = a & ~b, b1 = b & ~a, c = a & b, z = ~l;
+  const uint32_t after_c = (z + (c << 1)) & l, after_a = (z + (a1 << 1)) & l, after_b = (z + (b1 << 1)) & l;
+  uint32_t n = (uint32_t)(__builtin_popcount(a1 & after_c) + __builtin_popcount(a1 & after_b) +
+                          __builtin_popcount(b1 & after_a));
+  const int p0 = __builtin_ctz(l);
+  const uint32_t first = ((a >> p0) & 1u) | (((b >> p0) & 1u) << 1);
+  n += ((first == 1u && prev == 3u) || (first != 3u && prev != 3u && first != prev)) ? 1u : 0u;
+  const int p1 = 31 - __builtin_clz(l);
+  prev = ((a >> p1) & 1u) | (((b >> p1) & 1u) << 1);
+  return n;
+}
+
 // label of the highest labelled doc of a word (0: none)
 __device__ __forceinline__ uint32_t last_label(uint32_t a, uint32_t b) {
   const uint32_t l = a | b;
@@ -578,16 +597,7 @@ __device__ __forceinline__ void bit_count_block(BitShared& S, int64_t blk) {
     uint32_t prev = block_last_exclusive(last, S.lds4, &total);
     if (prev == 0u) prev = gp(S.J.scratch + S.J.nb)[blk];
 #pragma unroll
-    for (int k = 0; k < kBitThreadWords; ++k) {
-      uint32_t l = a[k] | b[k];
-      while (l != 0u) {
-        const int p = __builtin_ctz(l);
-        l &= l - 1u;
-        const uint32_t lab = ((a[k] >> p) & 1u) | (((b[k] >> p) & 1u) << 1);
-        if ((lab == 1u && prev == 3u) || (lab != 3u && prev != 3u && lab != prev)) ++leaps;
-        prev = lab;
-      }
-    }
+    for (int k = 0; k < kBitThreadWords; ++k) leaps += word_leaps(a[k], b[k], prev);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {

@@ -36,7 +36,7 @@ hipError_t launch_leaf_bitmap(const DevSeg* seg, int li, int flip, int64_t num_d
 // programs A (tok[0..len_a)) and B (tok[kBitProgMax..+len_b)) over one segment's leaf bitmaps.
 constexpr int kBitProgMax = 64;
 constexpr int kBitProgStack = 16;
-constexpr int kBitGroups = 4;  // 16-byte word groups per thread of the count kernels
+constexpr int kBitGroups = 2;  // 16-byte word groups per thread of the count kernels
 struct BitJob {
   const uint32_t* bm;  // the segment's leaf bitmaps, leaf l at bm + l * words
   int64_t words, num_docs;

@@ -42,6 +42,7 @@ class GpuSegment:
         lib = L.lib()
         if device is not None:
             L.check(lib.pa_set_device(int(device)), "pa_set_device")
+        self.device = None if device is None else int(device)  # (None: the caller's current device)
         self.segment = segment
         self.column_ids = dict(column_ids or column_ids_for(segment))
         self.handle = L.check_ptr(lib.pa_segment_create(segment.num_docs), "pa_segment_create")
@@ -196,6 +197,7 @@ class GpuQueryExecutor:
         self.all_segs = [g.segment for g in gpu_segments]
         self.gsegs = [g for g in gpu_segments if g.segment.num_docs > 0]
         self.segs = [g.segment for g in self.gsegs]
+        self.device = next((g.device for g in gpu_segments if g.device is not None), None)
         self.flags = flags
         self.enforce_num_groups_limit = enforce_num_groups_limit
         self.handle = None
@@ -499,6 +501,11 @@ class GpuQueryExecutor:
                 out.append(comp.view(np.float64))
         return out
 
+    def torch_device(self):
+        """The GPU holding this executor's segments (GpuSegment(device=...)), else the current device."""
+        import torch
+        return torch.device("cuda", self.device if self.device is not None else torch.cuda.current_device())
+
     def leaf_bitmaps(self, segment_index, stream=None):
         """bool[leaves, num_docs]: every filter leaf (the engine's flattened leaf order) on every doc of one bound
         segment, computed on the GPU (pa_query_leaf_bitmaps). Synchronises `stream`."""
@@ -509,9 +516,10 @@ class GpuQueryExecutor:
         if nl == 0:
             return np.zeros((0, n), dtype=bool)
         words = L.check(lib.pa_query_leaf_bitmap_words(self.handle, segment_index), "pa_query_leaf_bitmap_words")
-        buf = torch.zeros(nl * words, dtype=torch.int32, device=torch.device("cuda", torch.cuda.current_device()))
+        dev = self.torch_device()
+        buf = torch.zeros(nl * words, dtype=torch.int32, device=dev)
         L.check(lib.pa_query_leaf_bitmaps(self.handle, segment_index, buf.data_ptr(), stream), "pa_query_leaf_bitmaps")
-        torch.cuda.synchronize()  # (device-wide: covers `stream`)
+        torch.cuda.synchronize(dev)  # (device-wide: covers `stream`)
         w = buf.cpu().numpy().view(np.uint8).reshape(nl, words * 4)
         return np.unpackbits(w, axis=1, bitorder="little")[:, :n].astype(bool)
 
