@@ -201,6 +201,8 @@ typedef struct {
 #define PA_QF_NO_LANE_ACC (1 << 26)       /* aggregation-only query: LDS/global accumulators instead of per-lane registers */
 #define PA_QF_NO_LANE_HIST (1 << 27)      /* aggregation-only SUM over a shared dictionary: gather each doc's value instead
                                              of counting dictIds in an LDS histogram */
+#define PA_QF_LAZY_POST (1 << 28)         /* post-filter columns (group-by keys, aggregated values) read per matching doc
+                                             from HBM at any filter density, never staged with the filter columns */
 #define PA_QF_PART_SHIFT 22               /* bits 22..23: LDS per partition of the partitioned aggregation (0 = auto,
                                              1 = 64 KiB, 2 = 96 KiB, 3 = 144 KiB): larger partitions = fewer record
                                              write fronts per XCD */

@@ -33,6 +33,7 @@ PA_QF_NO_SPLIT_EMIT = 1 << 24
 PA_QF_NO_LIMIT_WALK = 1 << 25
 PA_QF_NO_LANE_ACC = 1 << 26
 PA_QF_NO_LANE_HIST = 1 << 27
+PA_QF_LAZY_POST = 1 << 28
 PA_BIT_AND, PA_BIT_OR, PA_BIT_NOT = -1, -2, -3
 PA_BIT_PROG_MAX = 64
 PA_ACC_COUNT_U64, PA_ACC_SUM_I64, PA_ACC_SUM_F64, PA_ACC_MIN_I64, PA_ACC_MAX_I64, PA_ACC_HLL_U8, \

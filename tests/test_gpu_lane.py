@@ -143,3 +143,20 @@ def test_lds_group_by_raw_metrics(lane_segments, sel, aggs):
     finally:
         ex.close()
     assert_same(got, oracle.run_query(q, segs), DOUBLE_REL)
+
+
+@pytest.mark.parametrize("sel", ["1pct", "30pct", "all"])
+@pytest.mark.parametrize("flags", [0, L.PA_QF_LAZY_POST])
+def test_lds_group_by_dictionary_metrics(lane_segments, sel, flags):
+    """Filter + GROUP BY over dictionary metrics on the LDS strategy, with the post-filter columns staged with the filter
+    column or read per matching doc from HBM (PA_QF_LAZY_POST)."""
+    segs, gs = lane_segments
+    q = parse_sql("SELECT g, COUNT(*), SUM(dl), MIN(dd), MAX(dl), SUM(dd) FROM t WHERE day < %d GROUP BY g LIMIT 1000"
+                  % SELECTIVITY[sel])
+    ex = GpuQueryExecutor(q, gs, flags=flags)
+    try:
+        assert ex.stats()["plan"]["strategy"] == "lds"
+        got = ex.run()
+    finally:
+        ex.close()
+    assert_same(got, oracle.run_query(q, segs), DOUBLE_REL)
