@@ -614,6 +614,32 @@ def _cost_next(op, seg, si, reqs):
     raise _Unsupported("AND leap-frogging other than two SV scans")
 
 
+def _filter_columns(f):
+    if isinstance(f, (Q.And, Q.Or)):
+        return set().union(*[_filter_columns(c) for c in f.children])
+    if isinstance(f, Q.Not):
+        return _filter_columns(f.child)
+    return {f.column}
+
+
+def _tree_signature(seg, fcols, params):
+    """Everything _build reads from a segment (the bound leaf parameters, each filter column's dictionary size,
+    sortedness and indexes), or None when the tree must be built per segment (no bound parameters; MV columns, whose
+    scan costs are per-doc value counts)."""
+    if params is None:
+        return None
+    cols = []
+    for name in fcols:
+        c = seg.column(name)
+        if not c.single_value:
+            return None
+        cols.append((c.has_dictionary, c.cardinality if c.has_dictionary else 0, bool(c.is_sorted),
+                     bool(getattr(c, "inverted_index", False)), bool(getattr(c, "range_index", False))))
+    leaves = tuple((p.kind, p.lo, p.hi, bool(p.negate), None if p.ids is None else len(np.unique(p.ids)))
+                   if isinstance(p, DictLeaf) else None for p in params)
+    return leaves, tuple(cols)
+
+
 def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps, leaf_params=None):
     """server_stats through the closed forms above. counts_fn(reqs) -> int64[len(reqs), 4]: for every request
     (segment index, program A, program B) -> row, pa_bitmap_counts' four counts. Segments without a closed form replay
@@ -624,18 +650,28 @@ def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps, leaf_para
     reqs = {}
     plans = []  # per segment: None (non-scan plan), "host", or (in_filter _Terms, docs _Terms)
     flat = _flatten(filt) if filt is not None else None
+    fcols = sorted(_filter_columns(filt)) if filt is not None else []
+    trees = {}  # operator tree + docs program per segment signature (segments of a table usually share one)
     for si, seg in enumerate(segments):
         if filt is None:
             plans.append(None if non_scan_plan(query, seg, True) else (_Terms(0), _Terms(seg.num_docs)))
             continue
         try:
-            op = _build(flat, seg, _RpnCursor(seg, None if leaf_params is None else leaf_params[si]),
-                        segment_index_info(seg))
+            params = None if leaf_params is None else leaf_params[si]
+            key = _tree_signature(seg, fcols, params)
+            if key is None or key not in trees:
+                tree = (_build(flat, seg, _RpnCursor(seg, params), segment_index_info(seg)),
+                        _rpn(expand_raw_in(filt, seg), 0))
+                if key is not None:
+                    trees[key] = tree
+            else:
+                tree = trees[key]
+            op, docs_prog = tree
             if non_scan_plan(query, seg, op.kind == "all"):
                 plans.append(None)
                 continue
             cost = _Terms(0) if op.kind in ("empty", "all") else _cost_next(op, seg, si, reqs)
-            docs = _Terms(0).request(reqs, si, _rpn(expand_raw_in(filt, seg), 0), [], 0)
+            docs = _Terms(0).request(reqs, si, docs_prog, [], 0)
             plans.append((cost, docs))
         except _Unsupported:
             plans.append("host")

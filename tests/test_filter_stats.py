@@ -228,6 +228,11 @@ def test_closed_form_matches_replay(where):
             return masks[si]
         got = FS.server_stats_closed_form(q, segs, np_counts(lambda si: masks[si], segs), host)
         assert got == want, sql
+        # with the executor's bound leaf parameters: operator trees shared by segments of one signature
+        params = [[P.dictionary_leaf(pred, s.column(pred.column)) for pred in _leaves(q, s)] for s in segs]
+        got = FS.server_stats_closed_form(q, segs + segs, np_counts(lambda si: masks[si % 2], segs + segs),
+                                          lambda si: host(si % 2), params + params)
+        assert got == tuple(2 * x for x in want), sql
 
 
 def test_closed_form_golden_statistics(golden_spec, golden_segment):

@@ -80,7 +80,8 @@ def test_execution_stats_device_vs_replay():
     try:
         # (+ a raw column: per-doc leaf path; a 20-bit dictionary: wide lane-major decode)
         for where in CLOSED_FORM_WHERES + HOST_WHERES + ["r < 1000 AND a < 50", "r BETWEEN 10 AND 20 OR b = 3",
-                                                          "w < 300000 AND b < 40", "w IN (5, 77, 1000) OR a = 1"]:
+                                                          "w < 300000 AND b < 40", "w IN (5, 77, 1000) OR a = 1",
+                                                          "r IN (3, 5, 7, 4000) AND b < 50", "NOT r IN (3, 5) AND a < 9"]:
             for sql in ("SELECT COUNT(*) FROM t WHERE " + where, "SELECT c, SUM(a) FROM t WHERE %s GROUP BY c" % where):
                 q = parse_sql(sql)
                 ex = GpuQueryExecutor(q, gs)
