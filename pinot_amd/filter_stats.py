@@ -326,6 +326,10 @@ def _leaf_op(pred, seg, mask, index_info, lf=None):
             return _Op("bitmap", LOW, mask)
     elif inverted:
         return _Op("bitmap", MEDIUM, mask)
+    elif ranged and isinstance(pred, Q.EqPredicate):
+        # RangeIndexBasedFilterOperator.canEvaluate: EQ on an exact range index (the bit-sliced v2 index every
+        # segment here is taken to have; FilterOperatorUtils.java:127-130)
+        return _Op("bitmap", LOW, mask)
     weights = None if sv else col.mv_lengths(seg.num_docs)
     return _Op("scan", SCAN_P + (0 if sv else 50), mask, weights=weights)
 

@@ -125,6 +125,19 @@ def test_filter_accounting_shapes(where, expect):
         assert got == expect(names, seg.num_docs)
 
 
+def test_range_index_serves_eq_but_not_in():
+    """FilterOperatorUtils.java:118-130 / RangeIndexBasedFilterOperator.canEvaluate: a range index answers RANGE and (exact
+    index) EQ predicates — no entries scanned — while IN still scans; an inverted index takes precedence."""
+    from pinot_amd.segment import create_segment
+    rng = np.random.default_rng(9)
+    n = 3000
+    data = {"a": rng.integers(0, 100, n).astype(np.int32), "b": rng.integers(0, 100, n).astype(np.int32)}
+    seg = create_segment("ri", data, {"a": "INT", "b": "INT"}, range_index_columns=("a",))
+    for where, scanned in (("a = 5", 0), ("a BETWEEN 3 AND 9", 0), ("a IN (1, 2)", n), ("b = 5", n)):
+        q = parse_sql("SELECT COUNT(*) FROM t WHERE " + where)
+        assert FS.entries_scanned_in_filter(q.filter, seg, leaf_masks(q, seg)) == scanned, where
+
+
 def _leaves(q, seg):
     leaves, ops = [], []
     _flatten_filter(P.expand_raw_in(q.filter, seg), leaves, ops)
