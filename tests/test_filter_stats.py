@@ -262,3 +262,37 @@ def test_closed_form_golden_statistics(golden_spec, golden_segment):
         if got != want:
             bad.append((case["sql"][:80], got, want))
     assert not bad, bad
+
+
+def _word_leaps(a, b, prev):
+    """pa_kernels.hip word_leaps restated on Python ints (32-bit words): (leaps, new prev)."""
+    m = 0xFFFFFFFF
+    l = a | b
+    if l == 0:
+        return 0, prev
+    a1, b1, c, z = a & ~b & m, b & ~a & m, a & b, ~l & m
+    after = lambda x: (z + ((x << 1) & m)) & m & l
+    n = bin(a1 & after(c)).count("1") + bin(a1 & after(b1)).count("1") + bin(b1 & after(a1)).count("1")
+    p0 = (l & -l).bit_length() - 1
+    first = ((a >> p0) & 1) | (((b >> p0) & 1) << 1)
+    n += 1 if (first == 1 and prev == 3) or (first != 3 and prev != 3 and first != prev) else 0
+    p1 = l.bit_length() - 1
+    return n, ((a >> p1) & 1) | (((b >> p1) & 1) << 1)
+
+
+def test_constant_time_word_leaps_match_the_sequence_rule():
+    """The count kernel's per-word bit-parallel leap count (carry trick) over random words and densities = the leap
+    rule applied doc by doc (np_leaps), chained across words."""
+    rng = np.random.default_rng(12)
+    for _ in range(200):
+        nw = int(rng.integers(1, 12))
+        pa, pb = rng.random(2) ** 2
+        a = rng.random(32 * nw) < pa
+        b = rng.random(32 * nw) < pb
+        wa = np.packbits(a, bitorder="little").view(np.uint32)
+        wb = np.packbits(b, bitorder="little").view(np.uint32)
+        prev, total = 3, 0
+        for x, y in zip(wa.tolist(), wb.tolist()):
+            n, prev = _word_leaps(x, y, prev)
+            total += n
+        assert total == np_leaps(a, b)
