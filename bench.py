@@ -38,8 +38,55 @@ COLUMNS = {  # name: (type, cardinality, dictionary values)
 }
 
 
+# Secondary lines (same columns and segments): the accountId IN list widened so the filter + GROUP BY SUM aggregates a
+# tenth / half of the docs (day range: 384 of the 512 days, 75 %; IN list: 13.3 % / 66.7 % of the 2^17 account ids).
+DAY_RANGE = (17532, 17915)
+SECONDARY = (("sel_10pct", 17476), ("sel_50pct", 87381))
+
+
+def secondary_query(n_ids):
+    ids = np.sort(np.random.default_rng(4242).choice(COLUMNS["accountId"][2](), size=n_ids, replace=False))
+    return ("SELECT sum(clicks), sum(impressions) FROM AdAnalyticsTable WHERE daysSinceEpoch BETWEEN %d AND %d "
+            "AND accountId IN (%s) GROUP BY daysSinceEpoch TOP 100" % (DAY_RANGE + (",".join(map(str, ids)),)))
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def _touched(p, per_sector):
+    """Fraction of 64-byte sectors holding at least one doc of a uniform selection of density p."""
+    p = min(1.0, max(0.0, p))
+    return 1.0 - (1.0 - p) ** max(1.0, per_sector)
+
+
+def algorithmic_bytes(ex, matched):
+    """HBM bytes one launch of the query's scan must read (the byte model of every roofline line): a column
+    the plan stages is read whole (nb / 8 bytes per doc for a dictionary column, the value bytes for a raw one); a column
+    read per surviving doc costs the 64-byte sectors holding a surviving doc, at the query's final density (lazy filter
+    clauses run at a density >= that: the model undercounts them); a multi-value column also its per-doc value offsets
+    (4 bytes) and its values' bits, sector-wise."""
+    from pinot_amd import _lib as L
+    q = ex.query
+    from pinot_amd.query import query_columns
+    names = query_columns(q)
+    docs = sum(sg.num_docs for sg in ex.segs)
+    p = matched / max(1, docs)
+    total = 0.0
+    for name in names:
+        staged = L.lib().pa_query_column_staged(ex.handle, ex.gsegs[0].column_ids[name]) == 1
+        for sg in ex.segs:
+            c = sg.column(name)
+            if not c.has_dictionary:
+                vb = 4 if c.data_type in ("INT", "FLOAT") else 8
+                total += sg.num_docs * vb * (1.0 if staged else _touched(p, 64 / vb))
+            elif c.single_value:
+                total += sg.num_docs * c.num_bits / 8 * (1.0 if staged else _touched(p, 512 / c.num_bits))
+            else:
+                total += sg.num_docs * 4 * _touched(p, 16)
+                total += c.total_num_values * c.num_bits / 8 * _touched(p * c.total_num_values / max(1, sg.num_docs),
+                                                                         512 / c.num_bits)
+    return int(total)
 
 
 def make_segment(seed, docs):
@@ -104,6 +151,7 @@ def main():
     ap.add_argument("--docs", type=int, default=10_000_000, help="docs per segment")
     ap.add_argument("--cpu-sample", type=int, default=16, help="segments in the CPU baseline sample (0 = skip)")
     ap.add_argument("--flags", type=int, default=0)
+    ap.add_argument("--no-secondary", action="store_true", help="skip the widened-IN-list secondary lines")
     args = ap.parse_args()
 
     import torch
@@ -163,17 +211,20 @@ def main():
         res = step()
     torch.cuda.synchronize()
 
-    # scan-kernel-only timing: HIP events on the stream the kernel is launched on, around `steps` back-to-back launches
-    # of the fused scan alone (one accumulator reset before the first event; the scans keep accumulating, which
-    # changes no byte the kernel reads). Per-launch duration = elapsed / steps, the figure rocprofv3 --stats averages.
-    ex.reset(sptr)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(args.steps):
-        ex.scan(sptr)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    def kernel_time(e, n):
+        """Per-launch scan time: HIP events on the launch stream around n back-to-back launches (one accumulator reset
+        before the first event; the scans keep accumulating, which changes no byte the kernel reads)."""
+        e.reset(sptr)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(n):
+            e.scan(sptr)
+        b.record(stream)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / n
+
+    # scan-kernel-only timing (per-launch duration = elapsed / steps, the figure rocprofv3 --stats averages)
+    kernel_ms = kernel_time(ex, args.steps)
 
     if distributed:
         dist.barrier()
@@ -190,13 +241,39 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # secondary lines: the same segments under the widened IN lists (kernel time, roofline on the same byte model)
+    secondary = []
+    if not args.no_secondary:
+        from pinot_amd import _lib as L
+        for name, n_ids in SECONDARY:
+            sql = secondary_query(n_ids)
+            e2 = GpuQueryExecutor(parse_sql(sql), gsegs, flags=args.flags, **kw)
+            for _ in range(args.warmup):
+                e2.execute(sptr)
+            torch.cuda.synchronize()
+            ms = kernel_time(e2, args.steps)
+            e2.execute(sptr)
+            r2 = e2.fetch(sptr) if rank == 0 else None
+            matched = int(L.lib().pa_query_matched_docs(e2.handle))
+            algo = algorithmic_bytes(e2, matched)
+            st2 = e2.stats()
+            secondary.append({
+                "workload": "adanalytics_in_list_" + name, "matched_fraction": matched / st2["num_docs"],
+                "query": sql[:sql.index("IN (") + 4] + "... %d account ids) GROUP BY daysSinceEpoch TOP 100" % n_ids,
+                "kernel_ms": ms, "rows_per_s": st2["num_docs"] / (ms * 1e-3),
+                "groups": len(r2.groups) if r2 is not None else None,
+                "roofline": {"bound": "hbm", "achieved": algo / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": algo,
+                             "plan": st2["plan"]}})
+            e2.close()
+
     st = ex.stats()
     rows_per_gpu = st["num_docs"]
     total_rows = rows_per_gpu * world
     if rank == 0:
-        # algorithmic bytes = forward-index bytes of the eagerly staged columns (the lazily read columns are only
-        # touched at the ~100 surviving docs: < 100 KB, neglected)
-        algo_bytes = st["staged_bytes"]
+        # algorithmic bytes (algorithmic_bytes): the staged accountId forward index + the sectors of the lazily read
+        # columns at the ~100 surviving docs
+        algo_bytes = algorithmic_bytes(ex, int(res.num_docs_scanned))
         achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
         cpu = cpu_baseline(q, host_sample) if host_sample else None
         out = {
@@ -236,6 +313,7 @@ def main():
                 "plan": st["plan"],
             },
             "cpu_baseline": cpu,
+            "secondary": secondary,
         }
         print(json.dumps(out), flush=True)
     ex.close()

@@ -203,6 +203,9 @@ typedef struct {
                                              of counting dictIds in an LDS histogram */
 #define PA_QF_LAZY_POST (1 << 28)         /* post-filter columns (group-by keys, aggregated values) read per matching doc
                                              from HBM at any filter density, never staged with the filter columns */
+#define PA_QF_NO_DENSE_GROUP (1 << 29)    /* filter + GROUP BY over a small key space: the LDS strategy (post-filter
+                                             columns per matching doc from HBM) instead of the dense group-by kernel
+                                             (every column staged, value dictionaries and remaps in LDS) */
 #define PA_QF_PART_SHIFT 22               /* bits 22..23: LDS per partition of the partitioned aggregation (0 = auto,
                                              1 = 64 KiB, 2 = 96 KiB, 3 = 144 KiB): larger partitions = fewer record
                                              write fronts per XCD */
@@ -344,8 +347,11 @@ int pa_query_stats(const pa_query* q, uint64_t* staged_bytes, uint64_t* num_docs
 /* The kernel plan chosen by pa_query_prepare: accumulator strategy (0 = LDS-privatised, 1 = global atomics,
  * 2 = partitioned: records partitioned by key range, then aggregated per partition in LDS; aggregation-only queries
  * 4..7 = per-lane register accumulators: 4 any column kinds, 5 COUNT only, 6 raw columns only, 7 dictionary
- * columns only), 64-doc
+ * columns only; 8 = dense GROUP BY over a small key box, every column staged), 64-doc
  * steps per wave tile, DMA instructions per tile, tile images per wave, workgroups per CU, grid, LDS bytes. */
+/* How the main scan pass reads a column (roofline byte model): 1 = staged (every word of every tile streamed through
+ * LDS), 0 = read per surviving doc from HBM, -1 = the query does not read it in the main pass. */
+int32_t pa_query_column_staged(const pa_query* q, int32_t column_id);
 /* Filter literals evaluated on whole staged tiles (the rest only on the docs those matched). */
 int32_t pa_query_num_eager_literals(const pa_query* q);
 /* 1 if the lane-major scan kernel was chosen (lane l owns docs [32l, 32l+32) of a tile), 0 step-major, <0 error. */

@@ -554,6 +554,8 @@ struct pa_query {
   DevBuf lim_keys, lim_pos, lim_hist, lim_sel, lim_thresh;
   DevBuf stat_buf;  // pa_query_filter_counts: leaf bitmaps, scratch, counts, jobs (grown on demand)
   std::vector<LmSegPlan> hplans;
+  std::vector<GdSegPlan> gdplans;  // STRAT_GDENSE: per-segment parameter tables
+  DevBuf dgdplans;
   std::vector<DevBuf> owned;  // LUTs, remaps, HLL LUTs, value dictionaries
   DevBuf acc;                 // all accumulator sections (unless the caller provided the block)
   void* external_acc = nullptr;
@@ -574,6 +576,7 @@ struct pa_query {
     dev_free(lim_thresh);
     dev_free(stat_buf);
     dev_free(lim_admit);
+    dev_free(dgdplans);
     if (host_acc) (void)hipHostFree(host_acc);
     dev_free(fetch_blocks);
     dev_free(fetch_stage);
@@ -647,6 +650,16 @@ struct Prep {
   bool lm = false;
   size_t lds_acc = 0;  // LDS strategy: accumulator bytes
   std::vector<size_t> agg_lds;
+  // STRAT_GDENSE (plan_gdense)
+  bool gdense = false;
+  std::vector<char> gd_stage_raw;          // per slot: raw aggregation column staged as a 32/64-bit "bit column"
+  size_t gd_lds = 0;                       // LDS bytes of the accumulators + tables (the ring follows)
+  int gd_rp_log2 = 0, gd_nkeys = 0, gd_tables = 0;
+  int gd_lo[PA_MAX_GROUP_BY] = {0}, gd_span[PA_MAX_GROUP_BY] = {0}, gd_ls[PA_MAX_GROUP_BY] = {0};
+  int gd_tab[PA_MAX_GROUP_BY] = {0}, gd_tab_n[PA_MAX_GROUP_BY] = {0};
+  std::vector<int> gd_vs, gd_op, gd_acc, gd_tab_a, gd_tab_an;
+  std::vector<int64_t> gd_base, gd_step;
+  std::vector<std::vector<const void*>> gd_src;  // [seg][agg] device dictionary behind the LDS value table
 };
 
 // Filter: CNF, clause order (most selective first), eager/lazy split, column slots of the leaves.
@@ -880,6 +893,268 @@ int plan_limit(pa_query* q, Prep& P) {
   return PA_OK;
 }
 
+bool affine_dictionary(const std::vector<uint64_t>& v, int32_t vtype, int64_t* base, int64_t* step);
+
+// STRAT_GDENSE (pa_gdense.h): a filter + GROUP BY whose matching docs are dense enough to stage every column the query
+// reads, over a small box of group keys, with COUNT / SUM / MIN / MAX over single-value columns. Decides eligibility, the
+// key box, each aggregation's value source and LDS operation, and the LDS layout (accumulators with per-lane replicas,
+// per-segment tables). Runs before build_segments, which stages the columns it asks for.
+int plan_gdense(pa_query* q, Prep& P) {
+  const pa_query_spec& s = q->spec;
+  P.gdense = false;
+  if (s.num_group_by < 1 || s.num_group_by > kGdMaxGb || q->nseg == 0 || q->hashed || q->limit_mode || q->limit_walk)
+    return PA_OK;
+  {
+    int nvalue = 0;
+    for (int a = 0; a < s.num_aggs; ++a) nvalue += s.aggs[a].type != PA_AGG_COUNT;
+    if (nvalue > kGdMaxAgg) return PA_OK;
+  }
+  if (s.flags & (PA_QF_NO_DENSE_GROUP | PA_QF_FORCE_GLOBAL | PA_QF_FORCE_LDS | PA_QF_LAZY_POST | PA_QF_NO_LANE_MAJOR |
+                 PA_QF_STEPS16 | PA_QF_DEBUG_STREAM_ONLY))
+    return PA_OK;
+  // every filter literal eager and a dictionary leaf on a staged column (no per-doc HBM reads in the tile loop)
+  if (q->num_eager != (int)q->literals.size()) return PA_OK;
+  for (const Literal& lit : q->literals) {
+    const int k = s.leaves[lit.leaf].kind;
+    if (k != PA_LEAF_DICT_RANGE && k != PA_LEAF_DICT_SET) return PA_OK;
+  }
+  // columns: group-by columns dictionary-encoded; aggregations COUNT / SUM / MIN / MAX over single-value columns of one
+  // kind in every segment
+  for (int si = 0; si < q->nseg; ++si)
+    for (int j = 0; j < s.num_group_by; ++j) {
+      auto it = q->segs[si]->cols.find(s.group_by_columns[j]);
+      if (it == q->segs[si]->cols.end() || it->second->kind != COL_SV_DICT) return PA_OK;
+    }
+  const int na = s.num_aggs;
+  std::vector<int> kind(na, COL_NONE);
+  for (int a = 0; a < na; ++a) {
+    const int t = s.aggs[a].type;
+    if (t == PA_AGG_COUNT) continue;
+    if (t != PA_AGG_SUM && t != PA_AGG_MIN && t != PA_AGG_MAX) return PA_OK;
+    for (int si = 0; si < q->nseg; ++si) {
+      auto it = q->segs[si]->cols.find(s.aggs[a].column_id);
+      if (it == q->segs[si]->cols.end()) return PA_OK;
+      const Column* c = it->second;
+      if (si == 0) kind[a] = c->kind;
+      if (c->kind != kind[a] || (c->kind != COL_SV_DICT && c->kind != COL_SV_RAW)) return PA_OK;
+      if (c->vtype != q->segs[0]->cols.at(s.aggs[a].column_id)->vtype) return PA_OK;
+      if (c->vtype != PA_INT && c->vtype != PA_LONG && c->vtype != PA_FLOAT && c->vtype != PA_DOUBLE) return PA_OK;
+      if (c->kind == COL_SV_DICT && c->hvals.size() != (size_t)c->cardinality) return PA_OK;
+    }
+  }
+  // staged columns (filter + post-filter, raw ones as 32/64-bit columns); tile images of the lane-major 2048-doc layout
+  // (at most kLmStaged columns and kLmEager literals) and of the step-major 1024-doc one (wide images)
+  std::vector<char> st(kMaxSlots, 0);
+  for (int li = 0; li < q->num_eager; ++li) st[P.leaf_slot[q->literals[li].leaf]] = 1;
+  for (int sl = 0; sl < kMaxSlots; ++sl) st[sl] |= P.slot_post[sl];
+  int nst = 0, post_bits = 0;
+  int img32 = kGuardWords, img16 = kGuardWords;
+  for (int si = 0; si < q->nseg; ++si) {
+    int n = 0, dw32 = kGuardWords, dw16 = kGuardWords, pb = 0;
+    for (int sl = 0; sl < (int)q->slot_cols.size(); ++sl) {
+      if (!st[sl]) continue;
+      const Column* c = q->segs[si]->cols.at(q->slot_cols[sl]);
+      const int nb = c->kind == COL_SV_RAW ? ((c->vtype == PA_INT || c->vtype == PA_FLOAT) ? 32 : 64) : c->nbits;
+      ++n;
+      dw32 += 2 * 32 * nb + kGuardWords;
+      dw16 += 2 * 16 * nb + kGuardWords;
+      if (P.slot_post[sl]) pb += nb;
+    }
+    nst = std::max(nst, n);
+    img32 = std::max(img32, dw32);
+    img16 = std::max(img16, dw16);
+    post_bits = std::max(post_bits, pb);
+  }
+  const bool lm_ok = nst <= kLmStaged && q->num_eager <= kLmEager;
+  const int max_img_dw = lm_ok ? std::min(img32, img16) : img16;  // (the smaller image decides whether it fits at all)
+  // density: staging the post-filter columns costs 256 nb bytes per tile and column; reading them per matching doc costs
+  // about a 64-byte sector each (and waits behind the ring): stage above half the byte break-even, like plan_slots
+  if (P.has_filter && P.post_density <= std::max(0.25, 2.0 * post_bits)) return PA_OK;
+  // key box: a CNF unit clause on a group-by column (DICT_RANGE / DICT_SET, not negated) bounds the table key ids of
+  // the docs that can match; union over segments (through their remaps), intersection over clauses
+  int64_t lo[PA_MAX_GROUP_BY], hi[PA_MAX_GROUP_BY];
+  for (int j = 0; j < s.num_group_by; ++j) {
+    lo[j] = 0;
+    hi[j] = s.group_by_cardinality[j];
+  }
+  for (size_t i = 0; i < q->literals.size(); ++i) {
+    const bool unit = q->clause_end[i] && (i == 0 || q->clause_end[i - 1]);
+    if (!unit) continue;
+    const Literal lit = q->literals[i];
+    for (int j = 0; j < s.num_group_by; ++j) {
+      if (s.leaves[lit.leaf].column_id != s.group_by_columns[j]) continue;
+      int64_t ulo = INT64_MAX, uhi = INT64_MIN;
+      bool bounded = true;
+      for (int si = 0; si < q->nseg && bounded; ++si) {
+        const pa_leaf_params& p = q->leaf_params[si][lit.leaf];
+        if ((p.negate != 0) != lit.neg) {
+          bounded = false;
+          break;
+        }
+        const Column* c = q->segs[si]->cols.at(s.group_by_columns[j]);
+        const std::vector<int32_t>* rm = q->has_remap[si][j] ? &q->remaps[si][j] : nullptr;
+        auto take = [&](int64_t id) {
+          const int64_t k = rm ? (int64_t)(*rm)[id] : id;
+          ulo = std::min(ulo, k);
+          uhi = std::max(uhi, k + 1);
+        };
+        if (s.leaves[lit.leaf].kind == PA_LEAF_DICT_RANGE) {
+          const int64_t a = std::max<int64_t>(0, p.lo), b = std::min<int64_t>(p.hi, c->cardinality);
+          if (rm) {
+            for (int64_t id = a; id < b; ++id) take(id);
+          } else if (b > a) {
+            take(a);
+            take(b - 1);
+          }
+        } else {
+          const std::vector<uint32_t>& lut = q->luts[si][lit.leaf];
+          for (int64_t id = 0; id < c->cardinality && (size_t)(id >> 5) < lut.size(); ++id)
+            if ((lut[id >> 5] >> (id & 31)) & 1u) take(id);
+        }
+      }
+      if (!bounded) continue;
+      if (ulo == INT64_MAX) ulo = uhi = 0;  // no segment can match: an empty box (a span of one key keeps it simple)
+      lo[j] = std::max(lo[j], ulo);
+      hi[j] = std::max(lo[j], std::min(hi[j], uhi));
+    }
+  }
+  int64_t nkeys = 1;
+  for (int j = 0; j < s.num_group_by; ++j) {
+    if (hi[j] <= lo[j]) hi[j] = lo[j] + 1;
+    P.gd_lo[j] = (int)lo[j];
+    P.gd_span[j] = (int)(hi[j] - lo[j]);
+    P.gd_ls[j] = (int)nkeys;
+    nkeys *= hi[j] - lo[j];
+    if (nkeys > kGdMaxKeys) return PA_OK;
+  }
+  P.gd_nkeys = (int)nkeys;
+  // per-segment key tables where some segment remaps the column
+  size_t tab_bytes = 0;
+  P.gd_tables = 0;
+  std::vector<size_t> gtab(s.num_group_by, 0), atab(na, 0);
+  for (int j = 0; j < s.num_group_by; ++j) {
+    P.gd_tab[j] = -1;
+    P.gd_tab_n[j] = 0;
+    bool any = false;
+    int32_t n = 0;
+    for (int si = 0; si < q->nseg; ++si) {
+      any |= q->has_remap[si][j] != 0;
+      n = std::max(n, q->segs[si]->cols.at(s.group_by_columns[j])->cardinality);
+    }
+    if (!any) continue;
+    P.gd_tab_n[j] = n;
+    gtab[j] = ((size_t)n * 4 + 15) & ~(size_t)15;
+    tab_bytes += gtab[j];
+    P.gd_tables = 1;
+  }
+  // aggregations: value source and LDS operation
+  P.gd_vs.assign(na, 0);
+  P.gd_op.assign(na, 0);
+  P.gd_acc.assign(na, 0);
+  P.gd_tab_a.assign(na, -1);
+  P.gd_tab_an.assign(na, 0);
+  P.gd_base.assign(na, 0);
+  P.gd_step.assign(na, 0);
+  P.gd_stage_raw.assign(kMaxSlots, 0);
+  P.gd_src.assign(q->nseg, std::vector<const void*>(na, nullptr));
+  std::vector<size_t> row(na, 0);  // accumulator bytes per key replica
+  for (int a = 0; a < na; ++a) {
+    const int t = s.aggs[a].type;
+    if (t == PA_AGG_COUNT) continue;
+    const Column* c0 = q->segs[0]->cols.at(s.aggs[a].column_id);
+    const int vt = c0->vtype;
+    const bool fl = vt == PA_FLOAT || vt == PA_DOUBLE;
+    bool fits = true, shared = true;
+    int32_t card = 0;
+    for (int si = 0; si < q->nseg; ++si) {
+      const Column* c = q->segs[si]->cols.at(s.aggs[a].column_id);
+      fits = fits && c->fits_int32;
+      shared = shared && (c == c0 || (c->dict_hash == c0->dict_hash && c->hvals == c0->hvals));
+      card = std::max(card, c->cardinality);
+    }
+    int vs, op;
+    if (kind[a] == COL_SV_RAW) {
+      P.gd_stage_raw[P.agg_slot[a]] = 1;
+      vs = vt == PA_INT ? GVS_RI32 : vt == PA_FLOAT ? GVS_RF32 : vt == PA_LONG ? GVS_RI64 : GVS_RF64;
+      op = t == PA_AGG_SUM ? (fl ? GOP_SUM_F : (fits ? GOP_SUM_I : GOP_SUM_L)) : (t == PA_AGG_MIN ? GOP_MIN_I : GOP_MAX_I);
+    } else {
+      int64_t b = 0, stp = 0;
+      if (t == PA_AGG_SUM && !fl && shared && affine_dictionary(c0->hvals, vt, &b, &stp)) {
+        vs = GVS_ID;
+        op = GOP_SUM_I;
+        P.gd_base[a] = b;
+        P.gd_step[a] = stp;
+      } else if (t != PA_AGG_SUM && shared && c0->dict_sorted) {
+        vs = GVS_ID;
+        op = t == PA_AGG_MIN ? GOP_MIN_U : GOP_MAX_U;
+      } else {
+        vs = fl ? GVS_TF : (fits ? GVS_T32 : GVS_T64);
+        op = t == PA_AGG_SUM ? (fl ? GOP_SUM_F : (fits ? GOP_SUM_I : GOP_SUM_L)) : (t == PA_AGG_MIN ? GOP_MIN_I : GOP_MAX_I);
+        P.gd_tab_an[a] = card;
+        atab[a] = ((size_t)card * (vs == GVS_T32 ? 4 : 8) + 15) & ~(size_t)15;
+        tab_bytes += atab[a];
+        P.gd_tables = 1;
+        // identical dictionaries share one device pointer: the workgroup loads the table once
+        std::map<uint64_t, std::vector<int>> first;  // dict hash -> segments holding a distinct dictionary with it
+        for (int si = 0; si < q->nseg; ++si) {
+          const Column* c = q->segs[si]->cols.at(s.aggs[a].column_id);
+          const void* src = c->dict.p;
+          for (int sj : first[c->dict_hash]) {
+            const Column* d = q->segs[sj]->cols.at(s.aggs[a].column_id);
+            if (d->hvals == c->hvals) {
+              src = d->dict.p;
+              break;
+            }
+          }
+          if (src == c->dict.p) first[c->dict_hash].push_back(si);
+          P.gd_src[si][a] = src;
+        }
+      }
+    }
+    P.gd_vs[a] = vs;
+    P.gd_op[a] = op;
+    row[a] = op == GOP_SUM_L ? 16 : (op == GOP_MIN_U || op == GOP_MAX_U) ? 4 : 8;
+  }
+  // LDS: replicated accumulators + tables + a ring of at least 2 tile images per wave (kGdWaves waves); replicas
+  // 256 / keys (a wave's 64 lanes spread over >= 4 addresses per key), fewer while that does not fit
+  auto acc_bytes = [&](int rpl) {
+    const size_t e = (size_t)nkeys << rpl;
+    size_t b = (e * 4 + 15) & ~(size_t)15;
+    for (int a = 0; a < na; ++a) b += (e * row[a] + 15) & ~(size_t)15;
+    return b;
+  };
+  const size_t ring_min = (size_t)kGdWaves * 2 * (size_t)max_img_dw * 4;
+  int rpl = 0;
+  while (rpl < 5 && ((int64_t)1 << (rpl + 1)) * nkeys <= 256) ++rpl;
+  while (rpl > 0 && acc_bytes(rpl) + tab_bytes + ring_min > kLdsBudget) --rpl;
+  if (acc_bytes(rpl) + tab_bytes + ring_min > kLdsBudget) return PA_OK;
+  P.gd_rp_log2 = rpl;
+  // layout: counts, per-aggregation accumulators, key tables, value tables
+  const size_t e = (size_t)nkeys << rpl;
+  size_t off = (e * 4 + 15) & ~(size_t)15;
+  for (int a = 0; a < na; ++a) {
+    if (s.aggs[a].type == PA_AGG_COUNT) continue;
+    P.gd_acc[a] = (int)off;
+    off += (e * row[a] + 15) & ~(size_t)15;
+  }
+  for (int j = 0; j < s.num_group_by; ++j) {
+    if (!gtab[j]) continue;
+    P.gd_tab[j] = (int)off;
+    off += gtab[j];
+  }
+  for (int a = 0; a < na; ++a) {
+    if (!atab[a]) continue;
+    P.gd_tab_a[a] = (int)off;
+    off += atab[a];
+  }
+  P.gd_lds = off;
+  P.gdense = true;
+  P.stage_post = true;  // every post-filter dictionary column with the filter columns (build_segments)
+  PLAN_LOG("gdense: keys %d (replicas %d), LDS acc+tables %zu, staged %d, img %d / %d dw", P.gd_nkeys, 1 << rpl, off,
+           nst, img32, img16);
+  return PA_OK;
+}
+
 // Per-segment descriptors: columns (the staged set of the main scan pass), filter literals in the segment's dictId
 // space, group-by remaps, aggregation value sources, HLL lookup tables.
 int build_segments(pa_query* q, Prep& P) {
@@ -918,8 +1193,14 @@ int build_segments(pa_query* q, Prep& P) {
       if (c->kind == COL_SV_DICT && (P.slot_eager[sl] || P.stage_all || (P.stage_post && P.slot_post[sl]))) {
         dc.lds_off = 0;  // staged; the region offset depends on the tile size (apply_layout)
         d.stage[d.num_staged++] = StageDesc{dc.words, dc.nbits, 0};
+      } else if (c->kind == COL_SV_RAW && P.gdense && P.gd_stage_raw[sl]) {
+        // STRAT_GDENSE: a raw column staged as a 32/64-bit column (a wave tile = 2048 values, 8 or 16 KiB)
+        dc.lds_off = 0;
+        d.stage[d.num_staged++] = StageDesc{(const uint32_t*)dc.raw, (c->vtype == PA_INT || c->vtype == PA_FLOAT) ? 32 : 64, 0};
       }
     }
+    if (P.gdense)
+      for (int a = 0; a < s.num_aggs; ++a) d.gd_src[a] = P.gd_src[si][a];
     // filter literals
     for (size_t li = 0; li < q->literals.size(); ++li) {
       const Literal lit = q->literals[li];
@@ -1579,9 +1860,21 @@ int plan_kernels(pa_query* q, Prep& P, TilePlan& plan, TilePlan& count_plan) {
   // LDS-privatised accumulators when many docs are expected to reach them (and the key space fits); otherwise the
   // LDS goes to tile rings (more resident waves) and the rare survivors update global accumulators directly.
   q->strategy = STRAT_GLOBAL;
+  // Dense filter + GROUP BY over a small key box, every column staged (plan_gdense decided the staging)
+  // (lane-major 2048-doc tiles when they keep as many resident waves as step-major 1024-doc ones: plan_tiles' score)
+  if (P.gdense) {
+    TilePlan a, b = plan_tiles(q, q->hsegs, STRAT_GDENSE, false, P.gd_lds, true);
+    if (lm) a = plan_tiles(q, q->hsegs, STRAT_GDENSE, true, P.gd_lds, false);
+    if (a.score >= 0 || b.score >= 0) {
+      lm = a.score >= b.score;
+      plan = lm ? a : b;
+      q->strategy = STRAT_GDENSE;
+      P.lds_acc = P.gd_lds;
+    }
+  }
   // Aggregation-only over single-value columns (configs[0]'s COUNT(*), SUM(m) WHERE ...): running totals in every lane's
   // registers, reduced once per wave at the end of the kernel (STRAT_LANE)
-  bool lane_acc = s.num_group_by == 0 && !q->has_mv && !q->limit_mode && !q->hashed && s.num_aggs <= kLaneAggs &&
+  bool lane_acc = q->strategy == STRAT_GLOBAL && s.num_group_by == 0 && !q->has_mv && !q->limit_mode && !q->hashed && s.num_aggs <= kLaneAggs &&
                   !(s.flags & (PA_QF_NO_LANE_ACC | PA_QF_FORCE_GLOBAL | PA_QF_FORCE_LDS));
   for (int a = 0; a < s.num_aggs && lane_acc; ++a) {
     const int t = s.aggs[a].type;
@@ -1687,7 +1980,9 @@ void apply_layout(std::vector<DevSeg>& segs, int steps, int nslots, int nleaves,
     for (int k = 0; k < d.num_staged; ++k) {
       d.stage[k].lds_off = off;
       for (int sl = 0; sl < nslots; ++sl)
-        if (d.cols[sl].lds_off >= 0 && d.cols[sl].words == d.stage[k].words) d.cols[sl].lds_off = off;
+        if (d.cols[sl].lds_off >= 0 &&
+            (d.cols[sl].kind == COL_SV_RAW ? (const uint32_t*)d.cols[sl].raw : d.cols[sl].words) == d.stage[k].words)
+          d.cols[sl].lds_off = off;
       staged += (uint64_t)d.num_wtiles * 2 * steps * d.stage[k].nbits * 4;
       off += 2 * steps * d.stage[k].nbits + kGuardWords;
     }
@@ -1741,9 +2036,51 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
     h.ht_keys = (long long*)q->sections[q->keys_section].ptr;
   }
   h.has_mv = q->has_mv;
-  h.xcd_major = P.dense ? 1 : 0;
+  h.xcd_major = (P.dense || q->strategy == STRAT_GDENSE) ? 1 : 0;
   h.lds_count_off = 0;
-  h.lds_acc_bytes = (q->strategy == STRAT_LDS || is_lane(q->strategy)) ? (uint32_t)P.lds_acc : 0;
+  h.lds_acc_bytes = (q->strategy == STRAT_LDS || q->strategy == STRAT_GDENSE || is_lane(q->strategy))
+                        ? (uint32_t)P.lds_acc : 0;
+  if (q->strategy == STRAT_GDENSE) {
+    // per-segment parameter tables (GdSegPlan): the query's key box and LDS layout + the segment's staged regions
+    q->gdplans.assign(std::max(1, q->nseg), GdSegPlan{});
+    for (int si = 0; si < q->nseg; ++si) {
+      GdSegPlan& g = q->gdplans[si];
+      std::memset(&g, 0, sizeof(g));
+      const DevSeg& d = q->hsegs[si];
+      g.ngb = s.num_group_by;
+      g.rpl = P.gd_rp_log2;
+      for (int j = 0; j < s.num_group_by; ++j) {
+        g.gb[j].reg = d.cols[P.gb_slot[j]].lds_off;
+        g.gb[j].nbits = d.cols[P.gb_slot[j]].nbits;
+        g.gb[j].tab = P.gd_tab[j];
+        g.gb[j].lo = P.gd_lo[j];
+        g.gb[j].span = P.gd_span[j];
+        g.gb[j].ls = P.gd_ls[j];
+      }
+      int k = 0;
+      for (int a = 0; a < s.num_aggs; ++a) {
+        if (s.aggs[a].type == PA_AGG_COUNT) continue;
+        g.ag[k].vs = P.gd_vs[a];
+        g.ag[k].op = P.gd_op[a];
+        g.ag[k].reg = d.cols[P.agg_slot[a]].lds_off;
+        g.ag[k].nbits = d.cols[P.agg_slot[a]].nbits;
+        g.ag[k].acc = P.gd_acc[a];
+        g.ag[k].tab = P.gd_tab_a[a];
+        ++k;
+      }
+      g.nagg = k;
+    }
+    h.gd_rp_log2 = P.gd_rp_log2;
+    h.gd_nkeys = P.gd_nkeys;
+    h.gd_tables = P.gd_tables;
+    for (int j = 0; j < s.num_group_by; ++j) {
+      h.gd_lo[j] = P.gd_lo[j];
+      h.gd_span[j] = P.gd_span[j];
+      h.gd_ls[j] = P.gd_ls[j];
+      h.gd_tab[j] = P.gd_tab[j];
+      h.gd_tab_n[j] = P.gd_tab_n[j];
+    }
+  }
   // LDS strategy: the one column every non-COUNT aggregation (SUM / MIN / MAX only) reads, if raw in segment 0 (the
   // kernel checks each segment's column kind): dense lane-major tiles then load its values coalesced
   h.lds_raw_slot = -1;
@@ -1773,6 +2110,15 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
     A.log2m = s.aggs[a].log2m;
     A.src = P.agg_src[a];
     A.nvals = s.aggs[a].type == PA_AGG_DISTINCTCOUNT ? presence_stride(s.aggs[a]) : 0;
+    if (q->strategy == STRAT_GDENSE) {
+      A.gd_vs = P.gd_vs[a];
+      A.gd_op = P.gd_op[a];
+      A.gd_acc = P.gd_acc[a];
+      A.gd_tab = P.gd_tab_a[a];
+      A.gd_tab_n = P.gd_tab_an[a];
+      A.gd_base = P.gd_base[a];
+      A.gd_step = P.gd_step[a];
+    }
     if (!q->partitioned) {
       A.lds_off = (int32_t)P.agg_lds[a];
       A.pay_off = 0;
@@ -1868,7 +2214,14 @@ int plan_limit_buffers(pa_query* q, const Prep& P, int cus, int64_t total_tiles)
 
 // Device copies of the descriptors (+ the lane-major plan tables).
 int upload_descriptors(pa_query* q) {
-  int rc = dev_alloc(q->dq, sizeof(DevQuery));
+  int rc;
+  if (q->strategy == STRAT_GDENSE) {
+    rc = dev_alloc(q->dgdplans, sizeof(GdSegPlan) * q->gdplans.size());
+    if (rc) return rc;
+    PA_HIP(hipMemcpy(q->dgdplans.p, q->gdplans.data(), sizeof(GdSegPlan) * q->gdplans.size(), hipMemcpyHostToDevice));
+    q->hq.gd_plans = (const uint32_t*)q->dgdplans.p;
+  }
+  rc = dev_alloc(q->dq, sizeof(DevQuery));
   if (rc) return rc;
   rc = dev_alloc(q->dsegs, sizeof(DevSeg) * std::max(1, q->nseg));
   if (rc) return rc;
@@ -2028,6 +2381,7 @@ int pa_query_prepare(pa_query* q) {
   if (!rc) rc = plan_slots(q, P);
   if (!rc) rc = plan_key_space(q, P);
   if (!rc) rc = plan_limit(q, P);
+  if (!rc) rc = plan_gdense(q, P);
   if (!rc) rc = build_segments(q, P);
   if (!rc) rc = plan_walk(q, P);
   if (!rc) rc = plan_accumulators(q, P);
@@ -2700,6 +3054,13 @@ int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t*
 int32_t pa_query_num_eager_literals(const pa_query* q) { return q && q->prepared ? q->num_eager : -1; }
 
 int32_t pa_query_lane_major(const pa_query* q) { return q && q->prepared ? q->lane_major : -1; }
+
+int32_t pa_query_column_staged(const pa_query* q, int32_t column_id) {
+  if (!q || !q->prepared || q->nseg == 0) return -1;
+  for (size_t sl = 0; sl < q->slot_cols.size(); ++sl)
+    if (q->slot_cols[sl] == column_id) return q->hsegs[0].cols[sl].lds_off >= 0 ? 1 : 0;
+  return -1;
+}
 
 int64_t pa_query_matched_docs(const pa_query* q) { return q && q->prepared ? q->last_matched : -1; }
 

@@ -39,10 +39,37 @@ enum ColKind : int32_t { COL_NONE = 0, COL_SV_DICT = 1, COL_SV_RAW = 2, COL_MV_D
 // STRAT_LANE_CNT / _RAW / _DICT: the lane-major STRAT_LANE kernel compiled for one kind of aggregation column only (no
 // value aggregation / raw columns only / dictionary columns only), so each variant holds just its own paths (the
 // all-kinds kernel spills); STRAT_LANE runs mixed sets and step-major tiles.
+// STRAT_GDENSE: filter + GROUP BY over a small key space whose matching docs are dense (pa_gdense.h): every column the
+// query reads is staged through the tile ring (raw metrics included), value dictionaries and group-key remaps sit in
+// LDS per segment, and the accumulators are LDS-privatised with per-lane replicas, so a matching doc costs LDS
+// operations only (no per-doc HBM access, which would wait behind the ring's in-flight DMA: vmcnt counts in order).
 enum Strategy : int32_t {
   STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PEMIT = 2, STRAT_PCOUNT = 3, STRAT_LANE = 4,
-  STRAT_LANE_CNT = 5, STRAT_LANE_RAW = 6, STRAT_LANE_DICT = 7
+  STRAT_LANE_CNT = 5, STRAT_LANE_RAW = 6, STRAT_LANE_DICT = 7, STRAT_GDENSE = 8
 };
+// STRAT_GDENSE value sources and LDS operations of one aggregation
+enum GdVs : int32_t {
+  GVS_ID = 0,    // the dictId itself (SUM over an affine dictionary shared by every segment; MIN/MAX of a shared sorted one)
+  GVS_T32 = 1,   // per-segment LDS table of int32 values (dictId -> value)
+  GVS_T64 = 2,   // per-segment LDS table of int64 values
+  GVS_TF = 3,    // per-segment LDS table of double values
+  GVS_RI32 = 4,  // staged raw INT
+  GVS_RF32 = 5,  // staged raw FLOAT
+  GVS_RI64 = 6,  // staged raw LONG
+  GVS_RF64 = 7   // staged raw DOUBLE
+};
+__host__ __device__ constexpr bool gvs_float(int vs) { return vs == GVS_TF || vs == GVS_RF32 || vs == GVS_RF64; }
+enum GdOp : int32_t {
+  GOP_SUM_I = 0,  // int64 sum of int32-range values (one ds_add_u64)
+  GOP_SUM_L = 1,  // exact pair: low 32 bits unsigned / high 32 bits signed (two ds_add_u64)
+  GOP_SUM_F = 2,  // ds_add_f64
+  GOP_MIN_I = 3,  // ds_min_i64 (ordered encoding of doubles)
+  GOP_MAX_I = 4,
+  GOP_MIN_U = 5,  // ds_min_u32 on dictIds (shared sorted dictionary: the value is looked up once per group at the end)
+  GOP_MAX_U = 6
+};
+constexpr int kGdWaves = 4;          // waves per STRAT_GDENSE workgroup
+constexpr int kGdMaxKeys = 16384;    // largest LDS key space of STRAT_GDENSE
 __host__ __device__ constexpr bool is_lane(int s) { return s >= STRAT_LANE && s <= STRAT_LANE_DICT; }
 constexpr int kLaneAggs = 4;  // STRAT_LANE: at most this many aggregations (COUNT included)
 constexpr int kLaneAccBytes = 20;  // STRAT_LANE: LDS bytes per thread and aggregation (int64 pair + a dictId)
@@ -133,6 +160,9 @@ struct DevSeg {
                                            // table-wide value id (nullptr = identity)
   const uint32_t* admit;                   // numGroupsLimit walk: bitmap of the table-wide keys admitted in this
                                            // segment (limit_walk_kernel writes it); nullptr = every key admitted
+  const void* gd_src[PA_MAX_AGGS];         // STRAT_GDENSE: device dictionary behind aggregation a's LDS value table
+                                           // (identical dictionaries of different segments share one pointer, so the
+                                           // table is loaded once per workgroup)
 };
 
 struct DevAgg {
@@ -150,6 +180,13 @@ struct DevAgg {
   // (u32[hist_card] at byte hist_off); the sum is sum(count[id] * dict[id]) once at the end (no per-doc gather)
   int32_t hist_card;         // 0 = the per-doc gather path
   int32_t hist_off;
+  // STRAT_GDENSE (pa_gdense.h)
+  int32_t gd_vs, gd_op;      // GdVs, GdOp
+  int32_t gd_acc;            // LDS byte offset of the replicated accumulators (K_lds << rp_log2 elements)
+  int32_t gd_tab;            // LDS byte offset of the per-segment value table (GVS_T32 / T64 / TF), else -1
+  int32_t gd_tab_n;          // table entries (largest segment cardinality)
+  int32_t gd_pad;
+  int64_t gd_base, gd_step;  // GVS_ID + GOP_SUM_I: value = base + step * dictId (affine shared dictionary)
 };
 
 struct DevQuery {
@@ -219,7 +256,41 @@ struct DevQuery {
   uint64_t v_maxabs;
   // STRAT_LDS, lane-major: the one raw column every non-COUNT aggregation reads (-1: none / several / not all raw)
   int32_t lds_raw_slot, pad_raw;
+  // STRAT_GDENSE: the LDS key space is the box the filter leaves to the group-by columns: component j = table key id of
+  // column j minus gd_lo[j] (< gd_span[j]), LDS key = sum_j component_j * gd_ls[j]; each key has 1 << gd_rp_log2
+  // replicas (lane l updates replica l & (replicas - 1)), so lanes sharing a key update different LDS banks
+  int32_t gd_rp_log2;
+  int32_t gd_nkeys;                  // LDS keys (product of the spans)
+  int32_t gd_lo[PA_MAX_GROUP_BY];
+  int32_t gd_span[PA_MAX_GROUP_BY];
+  int32_t gd_ls[PA_MAX_GROUP_BY];
+  int32_t gd_tab[PA_MAX_GROUP_BY];   // LDS byte offset of column j's per-segment key table (dictId -> component *
+                                     // gd_ls[j], -1 outside the box), or -1: component = dictId - gd_lo[j]
+  int32_t gd_tab_n[PA_MAX_GROUP_BY]; // key table entries (largest segment cardinality)
+  int32_t gd_tables;                 // some key or value table is loaded per segment
+  int32_t gd_pad;
+  const uint32_t* gd_plans;          // [num_segments][64]: GdSegPlan of every segment
 };
+// STRAT_GDENSE per-segment parameter table: 64 dwords, loaded once per segment into ONE VGPR (lane k holds dword k)
+// and read back with v_readlane at compile-time lanes, so the doc loop never issues a scalar load (an SMEM wait is an
+// lgkmcnt wait, which also waits for every LDS operation in flight).
+constexpr int kGdMaxGb = 3;    // group-by columns
+constexpr int kGdMaxAgg = 6;   // non-COUNT aggregations
+struct GdSegPlan {
+  int32_t ngb, nagg, rpl, pad;           // 0..3
+  struct {                               // 4 + 6j
+    int32_t reg, nbits;                  // staged region (dword offset in a tile image), bits per dictId
+    int32_t tab;                         // LDS byte offset of the key table, -1: component = dictId - lo
+    int32_t lo, span, ls;
+  } gb[kGdMaxGb];
+  struct {                               // 22 + 6k: the non-COUNT aggregations in order
+    int32_t vs, op;                      // GdVs, GdOp
+    int32_t reg, nbits;                  // staged region, bits per dictId (dictionary columns)
+    int32_t acc, tab;                    // LDS byte offsets: replicated accumulators, value table
+  } ag[kGdMaxAgg];
+  int32_t pad1[6];
+};
+static_assert(sizeof(GdSegPlan) == 256, "one dword per lane");
 // part_agg_kernel variant: -1 generic, else sum kind (0 none, 1 + AccSrc) | MIN << 2 | MAX << 3
 constexpr int kVkGeneric = -1;
 __host__ __device__ constexpr int vk_code(int sum_kind, bool mn, bool mx) { return sum_kind | (mn ? 4 : 0) | (mx ? 8 : 0); }

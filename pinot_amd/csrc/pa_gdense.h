@@ -1,0 +1,547 @@
+// Dense filter + GROUP BY over a small key space (STRAT_GDENSE), gfx950.
+//
+// Reference semantics: GroupByOperator -> DefaultGroupByExecutor.process (DefaultGroupByExecutor.java:131-158):
+// DictionaryBasedGroupKeyGenerator raw keys (:254-340) and {Count,Sum,Min,Max}AggregationFunction.aggregateGroupBySV
+// per matching doc, then GroupByCombineOperator's merge (one table-wide accumulator set per GPU here).
+//
+// Why a separate kernel: the LDS strategy of pa_scan.h reads a GROUP BY's post-filter columns per matching doc from HBM
+// and gathers dictionary values from HBM. Every such load is consumed while the next tiles' LDS-DMA is in flight, and
+// vmcnt counts loads, stores and LDS-DMA together in issue order: waiting for the doc's load waits for the ring too, so a
+// dense filter serialises the ring (GROUP BY day SUM(dictionary m) at 50 %: 0.056 of the HBM roofline). Here:
+//   * every column the query reads is staged by the wave's LDS-DMA ring: filter, group-by and aggregation columns,
+//     raw metrics as 4- or 8-byte "bit columns" (a 2048-doc tile of a raw LONG is 16 KiB, 16 DMA instructions);
+//   * value dictionaries (int32 / int64 / double) and group-key remaps sit in LDS, loaded once per segment by the
+//     workgroup (identical dictionaries of different segments share one load);
+//   * a workgroup owns one contiguous range of tiles and its waves interleave over it (wave w takes tiles t0 + w,
+//     t0 + w + 4, ...), so the four waves cross segment boundaries together and the per-segment tables can be swapped
+//     between two barriers;
+//   * accumulators are LDS-privatised over the box of group keys the filter admits (a unit clause day BETWEEN a AND b
+//     leaves b - a + 1 keys of that column), replicated so lanes sharing a key update different banks (lane l takes
+//     replica l & (R - 1)); one global atomic per non-empty key and aggregation at the end;
+//   * dense tiles are walked step-major (doc 64 i + lane: conflict-free LDS decodes of consecutive docs, the lane-major
+//     match bit fetched by ds_bpermute), sparse tiles lane-major (each lane its own matching docs).
+// A matching doc thus costs LDS operations only: decodes (ds_read2), table reads and ds_add/min/max atomics.
+#pragma once
+#include "pa_scan.h"
+
+namespace pa {
+
+typedef __attribute__((address_space(3))) int32_t lds_i32_t;
+typedef __attribute__((address_space(3))) int64_t lds_i64_t;
+typedef __attribute__((address_space(3))) double lds_f64_t;
+
+template <class T>
+__device__ __forceinline__ T* lds_at(uint32_t byte_addr) {
+  return (T*)(uintptr_t)byte_addr;
+}
+
+// Value of doc `doc` (0..2047) of an nb-bit column region of a staged tile image (region[-1] is a guard word).
+__device__ __forceinline__ uint32_t gd_decode(const lds_u32_t* region, uint32_t doc, uint32_t nb) {
+  const uint32_t e1 = doc * nb + (nb - 1u);
+  const uint32_t we = e1 >> 5;
+  return __builtin_amdgcn_alignbit(region[we - 1], region[we], (~e1) & 31u) & nbits_mask((int)nb);
+}
+
+// N docs per lane (doc[k], on[k]) of one staged tile image at LDS byte address img: group key, then COUNT and every
+// aggregation into replica r of the key's LDS accumulators. Every parameter comes from the segment's GdSegPlan in the
+// VGPR gt (v_readlane at compile-time lanes: no scalar loads, whose lgkmcnt waits would also wait for the LDS operations
+// in flight); every load is an LDS read. errs counts matching docs whose key fell outside the LDS box (cannot happen
+// when the planner's box is right; the query then reports an error).
+template <int N>
+__device__ __forceinline__ void gd_docs(uint32_t gt, uint32_t img, const uint32_t (&doc)[N], const bool (&on_in)[N],
+                                        uint32_t r, uint32_t base, uint32_t& errs) {
+  const int ngb = (int)rl(gt, 0), na = (int)rl(gt, 1);
+  const uint32_t rpl = rl(gt, 2);
+  uint32_t key[N];
+  bool on[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    key[k] = 0u;
+    on[k] = on_in[k];
+  }
+#pragma unroll
+  for (int j = 0; j < kGdMaxGb; ++j) {
+    if (j >= ngb) break;
+    const int o = 4 + 6 * j;
+    const lds_u32_t* reg = lds_at<const lds_u32_t>(img + 4u * rl(gt, o));
+    const uint32_t nb = rl(gt, o + 1);
+    uint32_t id[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) id[k] = gd_decode(reg, doc[k], nb);
+    const int tab = (int)rl(gt, o + 2);
+    if (tab >= 0) {
+      const lds_i32_t* t = lds_at<const lds_i32_t>(base + (uint32_t)tab);
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        const int32_t e = t[id[k]];
+        on[k] = on[k] && e >= 0;
+        key[k] += (uint32_t)e;
+      }
+    } else {
+      const uint32_t lo = rl(gt, o + 3), span = rl(gt, o + 4), ls = rl(gt, o + 5);
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        const uint32_t c0 = id[k] - lo;
+        on[k] = on[k] && c0 < span;
+        key[k] += c0 * ls;
+      }
+    }
+  }
+  uint32_t idx[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    errs += (on_in[k] && !on[k]) ? 1u : 0u;
+    idx[k] = (key[k] << rpl) | r;
+  }
+  {
+    lds_u32_t* cnt = lds_at<lds_u32_t>(base);
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if (on[k]) __hip_atomic_fetch_add(cnt + idx[k], 1u, WG_RLX);
+  }
+#pragma unroll
+  for (int g = 0; g < kGdMaxAgg; ++g) {
+    if (g >= na) break;
+    const int o = 22 + 6 * g;
+    const int vs = (int)rl(gt, o), op = (int)rl(gt, o + 1);
+    const uint32_t reg = img + 4u * rl(gt, o + 2);
+    const uint32_t acc = base + rl(gt, o + 4);
+    int64_t vi[N];
+    double vd[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      vi[k] = 0;
+      vd[k] = 0.0;
+    }
+    if (vs <= GVS_TF) {  // dictionary column: dictId from the staged stream, value from the LDS table (or the id)
+      const uint32_t nb = rl(gt, o + 3);
+      uint32_t id[N];
+#pragma unroll
+      for (int k = 0; k < N; ++k) id[k] = gd_decode(lds_at<const lds_u32_t>(reg), doc[k], nb);
+      const uint32_t tab = base + rl(gt, o + 5);
+      if (vs == GVS_ID) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) vi[k] = id[k];
+      } else if (vs == GVS_T32) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) vi[k] = lds_at<const lds_i32_t>(tab)[id[k]];
+      } else if (vs == GVS_T64) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) vi[k] = lds_at<const lds_i64_t>(tab)[id[k]];
+      } else {
+#pragma unroll
+        for (int k = 0; k < N; ++k) vd[k] = lds_at<const lds_f64_t>(tab)[id[k]];
+      }
+    } else if (vs == GVS_RI32) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) vi[k] = lds_at<const lds_i32_t>(reg)[doc[k]];
+    } else if (vs == GVS_RF32) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) vd[k] = __builtin_bit_cast(float, lds_at<const lds_u32_t>(reg)[doc[k]]);
+    } else if (vs == GVS_RI64) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) vi[k] = lds_at<const lds_i64_t>(reg)[doc[k]];
+    } else {
+#pragma unroll
+      for (int k = 0; k < N; ++k) vd[k] = lds_at<const lds_f64_t>(reg)[doc[k]];
+    }
+    const bool fl = gvs_float(vs);
+    switch (op) {
+      case GOP_SUM_I:
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+          if (on[k]) __hip_atomic_fetch_add(lds_at<lds_u64_t>(acc) + idx[k], (uint64_t)vi[k], WG_RLX);
+        break;
+      case GOP_SUM_L:
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+          if (!on[k]) continue;
+          __hip_atomic_fetch_add(lds_at<lds_u64_t>(acc) + 2 * idx[k], (uint64_t)(uint32_t)vi[k], WG_RLX);
+          __hip_atomic_fetch_add(lds_at<lds_u64_t>(acc) + 2 * idx[k] + 1, (uint64_t)(vi[k] >> 32), WG_RLX);
+        }
+        break;
+      case GOP_SUM_F:
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+          if (on[k]) __hip_atomic_fetch_add(lds_at<lds_f64_t>(acc) + idx[k], vd[k], WG_RLX);
+        break;
+      case GOP_MIN_I:
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+          if (on[k]) __hip_atomic_fetch_min(lds_at<lds_i64_t>(acc) + idx[k], fl ? f64_order_encode(vd[k]) : vi[k], WG_RLX);
+        break;
+      case GOP_MAX_I:
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+          if (on[k]) __hip_atomic_fetch_max(lds_at<lds_i64_t>(acc) + idx[k], fl ? f64_order_encode(vd[k]) : vi[k], WG_RLX);
+        break;
+      case GOP_MIN_U:
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+          if (on[k]) __hip_atomic_fetch_min(lds_at<lds_u32_t>(acc) + idx[k], (uint32_t)vi[k], WG_RLX);
+        break;
+      default:  // GOP_MAX_U
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+          if (on[k]) __hip_atomic_fetch_max(lds_at<lds_u32_t>(acc) + idx[k], (uint32_t)vi[k], WG_RLX);
+        break;
+    }
+  }
+}
+
+// Dense tile (2048-doc lane-major image), step-major walk: batch of SB steps, lane l takes doc 64 i + l of each; its
+// match bit lives in lane 2i + l/32 of the lane-major match words (bit l % 32).
+__device__ __forceinline__ void gd_tile_dense(uint32_t gt, uint32_t img, uint32_t m, int lane, uint32_t base,
+                                              uint32_t& errs) {
+  constexpr int SB = 4;
+  const uint32_t r = (uint32_t)lane & ((1u << rl(gt, 2)) - 1u);
+#pragma unroll 1
+  for (int i0 = 0; i0 < kSteps; i0 += SB) {
+    uint32_t doc[SB];
+    bool on[SB];
+    bool any = false;
+#pragma unroll
+    for (int s = 0; s < SB; ++s) {
+      const int src = 2 * (i0 + s) + (lane >> 5);
+      const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)m);
+      on[s] = (w >> (lane & 31)) & 1u;
+      doc[s] = (uint32_t)(kWave * (i0 + s) + lane);
+      any |= on[s];
+    }
+    if (__ballot(any) == 0) continue;
+    gd_docs<SB>(gt, img, doc, on, r, base, errs);
+  }
+}
+
+// Sparse tile: each lane walks its own matching docs, KB per batch; doc of bit i of lane l = LM ? 32 l + i : 64 i + l.
+template <int LM>
+__device__ __forceinline__ void gd_tile_sparse(uint32_t gt, uint32_t img, uint32_t m, int lane, uint32_t base,
+                                               uint32_t& errs) {
+  constexpr int KB = 4;
+  const uint32_t r = (uint32_t)lane & ((1u << rl(gt, 2)) - 1u);
+#pragma unroll 1
+  while (__ballot(m != 0) != 0) {
+    uint32_t doc[KB];
+    bool on[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      on[k] = m != 0;
+      const uint32_t i = on[k] ? (uint32_t)__builtin_ctz(m) : 0u;
+      doc[k] = LM ? 32u * (uint32_t)lane + i : (uint32_t)kWave * i + (uint32_t)lane;
+      m &= m - 1u;
+    }
+    gd_docs<KB>(gt, img, doc, on, r, base, errs);
+  }
+}
+
+// A tile is walked densely when most lanes hold at least this many matching docs of their 32 (16 step-major).
+constexpr int kGdDenseLaneMin = 10;
+
+// Filter of one lane-major tile (every literal eager: the planner's condition) + the tile's matching docs.
+__device__ __forceinline__ uint32_t gd_tile(uint32_t gt, uint32_t pp, int64_t wt, uint32_t img, int lane,
+                                            uint32_t base, uint32_t& errs) {
+  const int64_t doc_base = wt * kWTileDocs;
+  const int64_t rem = (int64_t)(int32_t)rl(pp, 2) - doc_base;
+  uint32_t m = 0xffffffffu;
+  if (rem < kWTileDocs) {
+    const int64_t n = rem - 32 * lane;  // docs of this lane's 32 that exist
+    m = n >= 32 ? 0xffffffffu : (n <= 0 ? 0u : ((1u << n) - 1u));
+  }
+  uint32_t clause = 0;
+  const int neager = (int)rl(pp, 1);
+  for (int l = 0; l < neager; ++l) {
+    const int b = 24 + 8 * l;
+    const int flags = (int)rl(pp, b + 5);
+    const uint32_t* lut = (const uint32_t*)(((uint64_t)rl(pp, b + 7) << 32) | rl(pp, b + 6));
+    uint32_t bits = leaf_lm_any((int)rl(pp, b + 1), (int)rl(pp, b), img + 4u * rl(pp, b + 2), lane, rl(pp, b + 3),
+                                rl(pp, b + 4), lut);
+    if (flags & 1) bits = ~bits;
+    clause |= bits;
+    if (flags & 2) {
+      m &= clause;
+      clause = 0;
+      if (__ballot(m != 0) == 0) return 0;
+    }
+  }
+  const uint32_t mine = (uint32_t)__builtin_popcount(m);
+  const uint64_t any = __ballot(mine != 0);
+  if (any == 0) return 0;
+  if (__builtin_popcountll(__ballot((int)mine >= kGdDenseLaneMin)) >= kWave / 2) gd_tile_dense(gt, img, m, lane, base, errs);
+  else gd_tile_sparse<1>(gt, img, m, lane, base, errs);
+  return mine;
+}
+
+// Step-major 1024-doc tiles (wide staged images: half the LDS of a 2048-doc tile): filter by leaf_bits (bit i of lane l
+// <=> doc 64 i + l), so the match bits are already in the order the dense walk takes them.
+constexpr int kGdSmSteps = 16;
+__device__ __forceinline__ uint32_t gd_tile_sm(uint32_t gt, const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                               int64_t wt, const uint32_t* img_ptr, uint32_t img, int lane,
+                                               uint32_t base, uint32_t& errs) {
+  constexpr int ST = kGdSmSteps;
+  const int64_t doc_base = wt * (ST * kWave);
+  const int64_t rem = (int64_t)seg->num_docs - doc_base;
+  uint32_t m;
+  if (rem >= ST * kWave) {
+    m = (1u << ST) - 1u;
+  } else {
+    const int64_t n = rem > lane ? (rem - lane + kWave - 1) / kWave : 0;
+    m = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
+  }
+  uint32_t clause = 0;
+  const int neager = q->num_eager;
+  for (int li = 0; li < neager; ++li) {
+    const DevLeaf& L = seg->leaves[li];
+    clause |= leaf_bits<ST>(L, img_ptr, doc_base, lane);
+    if (L.clause_end) {
+      m &= clause;
+      clause = 0;
+      if (__ballot(m != 0) == 0) return 0;
+    }
+  }
+  const uint32_t mine = (uint32_t)__builtin_popcount(m);
+  if (__ballot(mine != 0) == 0) return 0;
+  const uint32_t r = (uint32_t)lane & ((1u << rl(gt, 2)) - 1u);
+  if (__builtin_popcountll(__ballot((int)mine >= kGdDenseLaneMin / 2)) >= kWave / 2) {
+    constexpr int SB = 4;
+#pragma unroll 1
+    for (int i0 = 0; i0 < ST; i0 += SB) {
+      if (__ballot(((m >> i0) & ((1u << SB) - 1u)) != 0) == 0) continue;
+      uint32_t doc[SB];
+      bool on[SB];
+#pragma unroll
+      for (int k = 0; k < SB; ++k) {
+        on[k] = (m >> (i0 + k)) & 1u;
+        doc[k] = (uint32_t)(kWave * (i0 + k) + lane);
+      }
+      gd_docs<SB>(gt, img, doc, on, r, base, errs);
+    }
+  } else {
+    gd_tile_sparse<0>(gt, img, m, lane, base, errs);
+  }
+  return mine;
+}
+
+// Per-segment LDS tables: key tables of the group-by columns that have them and value tables of the aggregations.
+__device__ __forceinline__ bool gd_tables_differ(CQ* q, CSegT* a, CSegT* b) {
+  for (int j = 0; j < q->num_gb; ++j)
+    if (q->gd_tab[j] >= 0 && a->remap[j] != b->remap[j]) return true;
+  for (int i = 0; i < q->num_aggs; ++i)
+    if (q->aggs[i].gd_tab >= 0 && a->gd_src[i] != b->gd_src[i]) return true;
+  return false;
+}
+
+__device__ void gd_load_tables(CQ* q, CSegT* cs, unsigned char* lds, int tid, int nthreads) {
+  for (int j = 0; j < q->num_gb; ++j) {
+    const int tab = q->gd_tab[j];
+    if (tab < 0) continue;
+    int32_t* t = (int32_t*)(lds + tab);
+    const int32_t* rm = cs->remap[j];
+    const int32_t card = cs->cols[q->gb_slot[j]].card;
+    const int32_t lo = q->gd_lo[j], span = q->gd_span[j], ls = q->gd_ls[j];
+    for (int i = tid; i < q->gd_tab_n[j]; i += nthreads) {
+      int32_t e = -1;
+      if (i < card) {
+        const int32_t c = (rm != nullptr ? gp(rm)[i] : i) - lo;
+        if (c >= 0 && c < span) e = c * ls;
+      }
+      t[i] = e;
+    }
+  }
+  for (int a = 0; a < q->num_aggs; ++a) {
+    const int tab = q->aggs[a].gd_tab;
+    if (tab < 0) continue;
+    const int vs = q->aggs[a].gd_vs;
+    const int32_t card = cs->cols[q->aggs[a].slot].card;
+    const int n = q->aggs[a].gd_tab_n;
+    if (vs == GVS_TF) {
+      const double* src = (const double*)cs->gd_src[a];
+      double* t = (double*)(lds + tab);
+      for (int i = tid; i < n; i += nthreads) t[i] = i < card ? gp(src)[i] : 0.0;
+    } else {
+      const int64_t* src = (const int64_t*)cs->gd_src[a];
+      if (vs == GVS_T64) {
+        int64_t* t = (int64_t*)(lds + tab);
+        for (int i = tid; i < n; i += nthreads) t[i] = i < card ? gp(src)[i] : 0;
+      } else {
+        int32_t* t = (int32_t*)(lds + tab);
+        for (int i = tid; i < n; i += nthreads) t[i] = i < card ? (int32_t)gp(src)[i] : 0;
+      }
+    }
+  }
+}
+
+__device__ void gd_init(CQ* q, unsigned char* lds, int tid, int nthreads) {
+  const int64_t n = (int64_t)q->gd_nkeys << q->gd_rp_log2;
+  uint32_t* cnt = (uint32_t*)lds;
+  for (int64_t i = tid; i < n; i += nthreads) cnt[i] = 0u;
+  for (int a = 0; a < q->num_aggs; ++a) {
+    if (q->aggs[a].type == PA_AGG_COUNT) continue;
+    const int op = q->aggs[a].gd_op;
+    unsigned char* p = lds + q->aggs[a].gd_acc;
+    if (op == GOP_MIN_U || op == GOP_MAX_U) {
+      const uint32_t v = op == GOP_MIN_U ? 0xffffffffu : 0u;
+      for (int64_t i = tid; i < n; i += nthreads) ((uint32_t*)p)[i] = v;
+    } else {
+      const int64_t v = op == GOP_MIN_I ? INT64_MAX : (op == GOP_MAX_I ? INT64_MIN : 0);  // sums: 0 (0.0 == 0 bits)
+      const int64_t m = op == GOP_SUM_L ? 2 * n : n;
+      for (int64_t i = tid; i < m; i += nthreads) ((int64_t*)p)[i] = v;
+    }
+  }
+}
+
+// One global update per non-empty LDS key and aggregation: replicas reduced, the LDS key mapped back to the table-wide
+// key (component j + gd_lo[j] times the direct key-space stride), values in the accumulator section's representation.
+__device__ void gd_flush(const DevQuery* __restrict__ q, const DevSeg* __restrict__ segs, unsigned char* lds, int tid,
+                         int nthreads) {
+  const int nk = q->gd_nkeys;
+  const int rp = 1 << q->gd_rp_log2;
+  const uint32_t* cnt = (const uint32_t*)lds;
+  for (int kl = tid; kl < nk; kl += nthreads) {
+    uint64_t c = 0;
+    for (int r = 0; r < rp; ++r) c += cnt[kl * rp + r];
+    if (c == 0) continue;
+    int64_t key = 0;
+    for (int j = 0; j < q->num_gb; ++j) {
+      const int64_t comp = (kl / q->gd_ls[j]) % q->gd_span[j];
+      key += (comp + q->gd_lo[j]) * q->gb_stride[j];
+    }
+    __hip_atomic_fetch_add(gp(q->count) + key, (unsigned long long)c, RLX);
+    for (int a = 0; a < q->num_aggs; ++a) {
+      const DevAgg& A = q->aggs[a];
+      if (A.type == PA_AGG_COUNT) continue;
+      const unsigned char* p = lds + A.gd_acc;
+      switch (A.gd_op) {
+        case GOP_SUM_I:
+        case GOP_SUM_L: {
+          __int128 tot = 0;
+          if (A.gd_op == GOP_SUM_I) {
+            int64_t s = 0;
+            for (int r = 0; r < rp; ++r) s += ((const int64_t*)p)[kl * rp + r];
+            tot = A.gd_vs == GVS_ID ? (__int128)A.gd_base * (__int128)c + (__int128)A.gd_step * (__int128)s : (__int128)s;
+          } else {
+            int64_t lo = 0, hi = 0;
+            for (int r = 0; r < rp; ++r) {
+              lo += ((const int64_t*)p)[2 * (kl * rp + r)];
+              hi += ((const int64_t*)p)[2 * (kl * rp + r) + 1];
+            }
+            tot = (__int128)lo + ((__int128)hi << 32);
+          }
+          if (A.src == SRC_LONG) {
+            const uint64_t lo = (uint64_t)tot & 0xffffffffull;
+            const int64_t hi = (int64_t)(tot >> 32);
+            __hip_atomic_fetch_add(gp((unsigned long long*)A.acc_i64) + 2 * key, (unsigned long long)lo, RLX);
+            __hip_atomic_fetch_add(gp((unsigned long long*)A.acc_i64) + 2 * key + 1, (unsigned long long)hi, RLX);
+          } else {
+            __hip_atomic_fetch_add(gp((unsigned long long*)A.acc_i64) + key, (unsigned long long)(int64_t)tot, RLX);
+          }
+        } break;
+        case GOP_SUM_F: {
+          double s = 0.0;
+          for (int r = 0; r < rp; ++r) s += ((const double*)p)[kl * rp + r];
+          __hip_atomic_fetch_add(gp(A.acc_f64) + key, s, RLX);
+        } break;
+        case GOP_MIN_I:
+        case GOP_MAX_I: {
+          int64_t v = ((const int64_t*)p)[kl * rp];
+          for (int r = 1; r < rp; ++r) {
+            const int64_t w = ((const int64_t*)p)[kl * rp + r];
+            v = A.gd_op == GOP_MIN_I ? (w < v ? w : v) : (w > v ? w : v);
+          }
+          if (A.gd_op == GOP_MIN_I) __hip_atomic_fetch_min(gp((long long*)A.acc_i64) + key, (long long)v, RLX);
+          else __hip_atomic_fetch_max(gp((long long*)A.acc_i64) + key, (long long)v, RLX);
+        } break;
+        default: {  // GOP_MIN_U / GOP_MAX_U: dictId of the shared sorted dictionary -> its value
+          uint32_t v = ((const uint32_t*)p)[kl * rp];
+          for (int r = 1; r < rp; ++r) {
+            const uint32_t w = ((const uint32_t*)p)[kl * rp + r];
+            v = A.gd_op == GOP_MIN_U ? (w < v ? w : v) : (w > v ? w : v);
+          }
+          const DevCol& col = segs[0].cols[A.slot];
+          const int64_t e = A.src == SRC_DOUBLE ? f64_order_encode(gp(col.dict_f64)[v]) : gp(col.dict_i64)[v];
+          if (A.gd_op == GOP_MIN_U) __hip_atomic_fetch_min(gp((long long*)A.acc_i64) + key, (long long)e, RLX);
+          else __hip_atomic_fetch_max(gp((long long*)A.acc_i64) + key, (long long)e, RLX);
+        } break;
+      }
+    }
+  }
+}
+
+// The kernel. LDS: [accumulators | tables] (q->lds_acc_bytes) then each wave's ring of q->ring tile images.
+// LM = 1: lane-major 2048-doc tiles (per-segment plan tables); LM = 0: step-major 1024-doc tiles.
+template <int WPW, int LM>
+__global__ void __launch_bounds__(WPW * kWave, 1) gdense_kernel(const DevQuery* __restrict__ q_in,
+                                                                const DevSeg* __restrict__ segs,
+                                                                const LmSegPlan* __restrict__ plans, PartScratch) {
+  CQ* q = (CQ*)(uintptr_t)q_in;
+  constexpr int WGS = WPW * kWave;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  unsigned char* lds = (unsigned char*)smem;
+  const uint32_t base = lds_addr(smem);
+  const int img_dw = q->image_dwords_max;
+  const int R = q->ring, D = q->dma_per_tile;
+  const uint32_t ring_lds = base + q->lds_acc_bytes + 4u * (uint32_t)(wave * R * img_dw);
+  uint32_t* const ring = smem + (q->lds_acc_bytes >> 2) + wave * R * img_dw;
+  gd_init(q, lds, tid, WGS);
+  __syncthreads();
+  const int64_t T = q->total_wtiles, G = gridDim.x;
+  const int64_t lb = q->xcd_major ? xcd_major_block(blockIdx.x, G) : (int64_t)blockIdx.x;
+  const int64_t t0 = lb * T / G, t1 = (lb + 1) * T / G;
+  uint32_t matched = 0, errs = 0;
+  if (t0 < t1) {  // (workgroup-uniform)
+    const int nseg = q->num_segments;
+    // issue side: this wave's tiles t0 + wave + WPW k, LDS-DMA into its ring, R - 1 tiles ahead
+    int64_t ti = t0 + wave;
+    int isi = find_segment(segs, nseg, t0);
+    int64_t ifirst = segs[isi].first_wtile, iend = ifirst + segs[isi].num_wtiles;
+    uint32_t ip = LM ? ((const uint32_t*)(plans + isi))[lane] : 0u;
+    int islot = 0;
+    auto issue_next = [&]() {
+      while (ti >= iend) {
+        ++isi;
+        ifirst = segs[isi].first_wtile;
+        iend = ifirst + segs[isi].num_wtiles;
+        if (LM) ip = ((const uint32_t*)(plans + isi))[lane];
+      }
+      if constexpr (LM) stage_tile_lm(ip, ti - ifirst, ring_lds + 4u * (uint32_t)(islot * img_dw), lane, D);
+      else stage_tile<kGdSmSteps>(segs + isi, ti - ifirst, ring + islot * img_dw, lane, D);
+      ti += WPW;
+      islot = islot + 1 == R ? 0 : islot + 1;
+    };
+    for (int k = 0; k < R - 1 && ti < t1; ++k) issue_next();
+    const int s_first = find_segment(segs, nseg, t0), s_last = find_segment(segs, nseg, t1 - 1);
+    int64_t t = t0 + wave;
+    int pslot = 0;
+    for (int s = s_first; s <= s_last; ++s) {  // (every wave walks the same segments: the barriers below match)
+      CSegT* cs = (CSegT*)(uintptr_t)(segs + s);
+      if (q->gd_tables && (s == s_first || gd_tables_differ(q, (CSegT*)(uintptr_t)(segs + s - 1), cs))) {
+        __syncthreads();  // every wave is done with the previous segment's tables
+        gd_load_tables(q, cs, lds, tid, WGS);
+        __syncthreads();
+      }
+      const int64_t sfirst = cs->first_wtile;
+      const int64_t send = min(t1, sfirst + (int64_t)cs->num_wtiles);
+      const uint32_t pp = LM ? ((const uint32_t*)(plans + s))[lane] : 0u;
+      const uint32_t gt = gp(q->gd_plans)[(int64_t)s * 64 + lane];  // this segment's GdSegPlan, one dword per lane
+      for (; t < send; t += WPW) {
+        uint32_t slot_off = (uint32_t)(pslot * img_dw);
+        wait_tile((int)((ti - t) / WPW - 1), D, slot_off);  // tile t has landed (its younger tiles may still fly)
+        if (ti < t1) issue_next();
+        if constexpr (LM) matched += gd_tile(gt, pp, t - sfirst, ring_lds + 4u * slot_off, lane, base, errs);
+        else matched += gd_tile_sm(gt, q_in, segs + s, t - sfirst, ring + slot_off, ring_lds + 4u * slot_off, lane, base, errs);
+        pslot = pslot + 1 == R ? 0 : pslot + 1;
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // vmcnt(0): no DMA left in flight
+  const int64_t wm = wave_sum_i64((int64_t)matched);
+  const int64_t we = wave_sum_i64((int64_t)errs);
+  if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)wm, RLX);
+  if (lane == 0 && we != 0) __hip_atomic_fetch_add(gp(q->matched_docs) + 3, (unsigned long long)we, RLX);
+  __syncthreads();
+  gd_flush(q_in, segs, lds, tid, WGS);
+}
+
+}  // namespace pa

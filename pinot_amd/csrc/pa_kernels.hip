@@ -1516,6 +1516,7 @@ hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t*
 
 static const void* scan_fn(int strategy, int steps, int lm) {
   if (const void* f = scan_fn_std(strategy, steps, lm)) return f;
+  if (const void* f = scan_fn_gdense(strategy, lm)) return f;
   if (const void* f = scan_fn_part_a(strategy)) return f;
   return scan_fn_part_b(strategy);
 }

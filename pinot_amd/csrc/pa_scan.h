@@ -2706,5 +2706,6 @@ const void* scan_fn_std(int strategy, int steps, int lm);   // pa_scan_std.hip: 
 const void* scan_fn_lane(int strategy, int steps, int lm);  // pa_scan_lane.hip: LANE and its variants
 const void* scan_fn_part_a(int strategy);                  // pa_scan_part_a.hip: PCOUNT + emit variants (one part)
 const void* scan_fn_part_b(int strategy);                  // pa_scan_part_b.hip: the other emit variants
+const void* scan_fn_gdense(int strategy, int lm);          // pa_scan_gdense.hip: STRAT_GDENSE (pa_gdense.h)
 
 }  // namespace pa

@@ -1,0 +1,11 @@
+// The dense filter + GROUP BY kernel (STRAT_GDENSE, pa_gdense.h) in its own translation unit (parallel builds).
+#include "pa_gdense.h"
+
+namespace pa {
+
+const void* scan_fn_gdense(int strategy, int lm) {
+  if (strategy != STRAT_GDENSE) return nullptr;
+  return lm ? (const void*)gdense_kernel<kGdWaves, 1> : (const void*)gdense_kernel<kGdWaves, 0>;
+}
+
+}  // namespace pa

@@ -175,7 +175,7 @@ def _flatten_filter(f, leaves, ops):
 
 class GpuQueryExecutor:
     def __init__(self, query: Q.Query, gpu_segments: List[GpuSegment], flags=0, enforce_num_groups_limit=True,
-                 table_dicts=None, wide_sum_columns=(), value_dicts=None, hash_keys_bound=0):
+                 table_dicts=None, wide_sum_columns=(), value_dicts=None, hash_keys_bound=0, schema=None):
         """table_dicts: optional {group-by column: sorted unique values} — the table-wide dictionary every rank of a
         multi-GPU query must share so that key ids address the same accumulator rows everywhere
         (parallel.table_layout builds it); by default it is the union of these segments' dictionaries.
@@ -185,7 +185,10 @@ class GpuQueryExecutor:
         the presence bytes index (every rank of a multi-GPU query must share it); by default the union of these
         segments' dictionaries.
         hash_keys_bound: hashed key spaces: size the slot table for at least this many keys (parallel.table_layout
-        agrees on the largest rank's bound so every rank's table can take its share of the cross-GPU merge)."""
+        agrees on the largest rank's bound so every rank's table can take its share of the cross-GPU merge).
+        schema: {column: (data type, has dictionary, single value)} agreed across ranks (parallel.table_layout): when
+        every segment given here is empty, the executor plans over a one-doc placeholder segment of that schema and never
+        scans it, so the rank still holds a (zero) accumulator block of the agreed layout and joins the cross-GPU merge."""
         if not gpu_segments:
             raise ValueError("no segments")
         self.table_dicts = table_dicts or {}
@@ -201,8 +204,36 @@ class GpuQueryExecutor:
         self.flags = flags
         self.enforce_num_groups_limit = enforce_num_groups_limit
         self.handle = None
+        self.placeholder = None
+        if not self.segs and schema:
+            self.placeholder = GpuSegment(self._placeholder_segment(schema), column_ids=gpu_segments[0].column_ids,
+                                          device=self.device)
+            self.gsegs = [self.placeholder]
+            self.segs = [self.placeholder.segment]
         if self.segs:
             self._plan()
+        if self.placeholder is not None:
+            self.segs = []  # (nothing to scan; the plan only fixes the accumulator layout)
+
+    def _placeholder_segment(self, schema):
+        """One doc per column of the agreed schema: dictionary columns hold one value of the agreed table-wide dictionary
+        (group-by and DISTINCTCOUNT columns) or a zero, raw columns a zero, multi-value columns one value."""
+        from .segment import create_segment
+        data, types, raw, mv = {}, {}, [], []
+        for name in Q.query_columns(self.query):
+            dt, has_dict, sv = schema[name]
+            d = self.table_dicts.get(name)
+            if d is None:
+                d = self.table_value_dicts.get(name)
+            v = np.asarray(d)[:1] if d is not None and len(d) else np.array(["" if dt == "STRING" else 0])
+            v = v.astype({"INT": np.int32, "LONG": np.int64, "FLOAT": np.float32, "DOUBLE": np.float64}.get(dt, object))
+            data[name] = v if sv else [v]
+            types[name] = dt
+            if not has_dict:
+                raw.append(name)
+            if not sv:
+                mv.append(name)
+        return create_segment("placeholder", data, types, no_dictionary_columns=raw, multi_value_columns=mv)
 
     # ------------------------------------------------------------------ planning
     def _plan(self):
@@ -402,14 +433,18 @@ class GpuQueryExecutor:
 
     # ------------------------------------------------------------------ execution
     def execute(self, stream=None):
-        if not self.segs:
-            return  # (every bound segment is empty: nothing to scan)
+        if not self.segs:  # every bound segment is empty: nothing to scan (a placeholder plan: its block reset only)
+            if self.handle is not None:
+                L.check(L.lib().pa_query_reset(self.handle, stream), "pa_query_reset")
+            return
         L.check(L.lib().pa_query_execute(self.handle, stream), "pa_query_execute")
 
     def reset(self, stream=None):
         L.check(L.lib().pa_query_reset(self.handle, stream), "pa_query_reset")
 
     def scan(self, stream=None):
+        if not self.segs:
+            return
         L.check(L.lib().pa_query_scan(self.handle, stream), "pa_query_scan")
 
     def sections(self):
@@ -430,7 +465,8 @@ class GpuQueryExecutor:
         L.check(L.lib().pa_query_plan(self.handle, *[ctypes.byref(v) for v in vals]), "plan")
         names = ("strategy", "steps", "dma_slots", "ring", "wg_per_cu", "grid", "lds_bytes")
         out["plan"] = {n: v.value for n, v in zip(names, vals)}
-        out["plan"]["strategy"] = {0: "lds", 1: "global", 2: "partitioned", 4: "lane", 5: "lane", 6: "lane", 7: "lane"}[out["plan"]["strategy"]]
+        out["plan"]["strategy"] = {0: "lds", 1: "global", 2: "partitioned", 4: "lane", 5: "lane", 6: "lane", 7: "lane",
+                                    8: "lds_dense"}[out["plan"]["strategy"]]
         out["plan"]["eager_literals"] = int(L.lib().pa_query_num_eager_literals(self.handle))
         out["plan"]["lane_major"] = int(L.lib().pa_query_lane_major(self.handle))
         out["plan"]["limit_trimming"] = int(L.lib().pa_query_limit_trimming(self.handle))
@@ -535,7 +571,7 @@ class GpuQueryExecutor:
         count kernels per segment on the GPU, one synchronisation: execution_stats)."""
         lib = L.lib()
         q = self.query
-        if not self.segs:
+        if self.handle is None:
             return self._empty_result()
         keys, counts, outs = self.fetch_arrays(stream, pooled=True)  # (converted to Python objects below)
         n = len(keys)
@@ -602,6 +638,9 @@ class GpuQueryExecutor:
         if self.handle:
             L.lib().pa_query_destroy(self.handle)
             self.handle = None
+        if self.placeholder is not None:
+            self.placeholder.close()
+            self.placeholder = None
 
     def __del__(self):
         try:

@@ -169,6 +169,12 @@ class HashedAccumulators:
     of the merged groups (disjoint across ranks)."""
 
     def __init__(self, executor, device):
+        self.device = device
+        self.views = None
+        if executor.handle is None:
+            # a rank whose segments are all empty, built without the layout's schema (executor_kwargs): it has no block,
+            # so merge() joins the layout check with -1 and every rank raises there (none is left blocked)
+            return
         if not getattr(executor, "hashed", False):
             raise L.PinotAmdError("HashedAccumulators: direct key spaces reduce element-wise (DistributedAccumulators)")
         lib = L.lib()
@@ -188,6 +194,10 @@ class HashedAccumulators:
             self.views.append((kind, self.buf[off:off + n * es].view(dt)))
 
     def merge(self, group=None):
+        if self.views is None:
+            check_same_key_space(-1, self.device, group=group,
+                                 what="hashed merge: a rank holds only empty segments and no table layout (build its "
+                                      "executor with parallel.table_layout(...).executor_kwargs())")
         return merge_hashed_sections(self.views, self.num_slots, group=group, layout_extra=self.key_space)
 
 
@@ -251,14 +261,16 @@ class TableLayout:
     wide: list = field(default_factory=list)         # SUM columns that keep the 64-bit accumulator on every rank
     value_dicts: dict = field(default_factory=dict)  # DISTINCTCOUNT column -> table-wide value dictionary
     hash_keys_bound: int = 0                         # the largest rank's hashed key bound (equal tables everywhere)
+    schema: dict = field(default_factory=dict)       # column -> (data type, has dictionary, single value): lets a rank
+                                                     # whose segments are all empty plan the same accumulator block
 
     def executor_kwargs(self):
         """Keyword arguments of GpuQueryExecutor that make every rank's accumulator block line up."""
         return dict(table_dicts=self.dicts, wide_sum_columns=self.wide, value_dicts=self.value_dicts,
-                    hash_keys_bound=self.hash_keys_bound)
+                    hash_keys_bound=self.hash_keys_bound, schema=self.schema)
 
 
-from .query import DISTINCT_SET_FUNCTIONS as DISTINCT_FUNCTIONS  # noqa: E402
+from .query import DISTINCT_SET_FUNCTIONS as DISTINCT_FUNCTIONS, query_columns  # noqa: E402
 
 
 def table_layout(query, segments, group=None):
@@ -269,8 +281,13 @@ def table_layout(query, segments, group=None):
     (presence byte j must mean the same value on every rank before the uint8-MAX reduce ORs them) and the largest
     rank's hashed key bound (every rank's hashed table then has the same slots). Returns a TableLayout; build every
     rank's executor with GpuQueryExecutor(..., **layout.executor_kwargs())."""
+    segments = [s for s in segments if s.num_docs > 0]  # (empty segments hold no columns: SegmentColumnarIndexCreator)
     local = {"dicts": {}, "vals": {}, "wide": sorted(wide_sum_columns_local(query, segments)),
-             "hb": hash_keys_bound_local(query, segments)}
+             "hb": hash_keys_bound_local(query, segments), "schema": {}}
+    for s in segments:
+        for name in query_columns(query):
+            c = s.column(name)
+            local["schema"].setdefault(name, (c.data_type, bool(c.has_dictionary), bool(c.single_value)))
     for name in query.group_by:
         ds = [s.column(name).dictionary for s in segments if s.column(name).has_dictionary]
         if ds:
@@ -292,7 +309,11 @@ def table_layout(query, segments, group=None):
         out.value_dicts[name] = np.unique(np.concatenate([g["vals"][name] for g in gathered if name in g["vals"]]))
     out.wide = sorted(set().union(*[set(g["wide"]) for g in gathered]))
     out.hash_keys_bound = max(int(g["hb"]) for g in gathered)
+    for g in gathered:
+        for name, meta in g["schema"].items():
+            out.schema.setdefault(name, tuple(meta))
     return out
+
 
 
 def table_dictionaries(query, segments, group=None):
@@ -354,8 +375,12 @@ class DistributedAccumulators:
     def __init__(self, executor, device):
         hashed = getattr(executor, "hashed", False)
         if dist.is_initialized():
-            # the collective first, on every rank (a hashed rank joins with -1 and every rank then raises)
-            check_same_key_space(-1 if hashed else key_space_fingerprint(executor), device)
+            # the collective first, on every rank (a hashed rank, or one holding only empty segments and built without the
+            # layout's schema, joins with -1 and every rank then raises)
+            check_same_key_space(-1 if (hashed or executor.handle is None) else key_space_fingerprint(executor), device)
+        if executor.handle is None:
+            raise L.PinotAmdError("a rank holds only empty segments and no table layout: build its executor with "
+                                  "parallel.table_layout(...).executor_kwargs()")
         if hashed:
             raise L.PinotAmdError("hashed key space: merge with HashedAccumulators (slots differ per GPU)")
         lib = L.lib()

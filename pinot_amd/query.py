@@ -358,3 +358,22 @@ class _Parser:
 
 def parse_sql(sql: str) -> Query:
     return _Parser(sql).parse()
+
+
+def query_columns(query):
+    """Every column a query reads: filter leaves, group-by columns, aggregation columns."""
+    names = []
+
+    def walk(f):
+        for c in getattr(f, "children", ()) or ():
+            walk(c)
+        if getattr(f, "child", None) is not None:
+            walk(f.child)
+        if getattr(f, "column", None) is not None and f.column not in names:
+            names.append(f.column)
+    if query.filter is not None:
+        walk(query.filter)
+    for n in list(query.group_by) + [a.column for a in query.aggregations if a.column]:
+        if n not in names:
+            names.append(n)
+    return names

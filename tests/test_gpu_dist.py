@@ -114,3 +114,43 @@ def test_hashed_key_space_device_merge(sql, rccl_world1):
         ex.close()
         for g in gsegs:
             g.close()
+
+
+def test_rank_with_only_empty_segments_joins_the_merge(rccl_world1):
+    """a rank whose segments are all empty plans a placeholder block from the agreed layout
+    (parallel.table_layout: dictionaries, SUM widths, column schema), so its key-space fingerprint equals the other
+    ranks', its reset block reduces as the identity, and as the reduce's destination it fetches the whole result."""
+    from pinot_amd.parallel import TableLayout
+    from pinot_amd.segment import Segment
+    q = parse_sql("SELECT d1, COUNT(*), SUM(m), MIN(f), MAX(m), DISTINCTCOUNTHLL(m) FROM t WHERE m > 0 GROUP BY d1 "
+                  "LIMIT 1000")
+    segs = [make_segment(610 + i, n, COLS) for i, n in enumerate((12011, 3001))]
+    layout = TableLayout(dicts={"d1": np.unique(np.concatenate([s.column("d1").dictionary for s in segs]))},
+                         schema={n: (segs[0].column(n).data_type, True, True) for n in ("d1", "m", "f")})
+    full = [GpuSegment(s) for s in segs]
+    empty = [GpuSegment(Segment("e%d" % i, 0)) for i in range(2)]
+    ex_full = GpuQueryExecutor(q, full, **layout.executor_kwargs())
+    ex_empty = GpuQueryExecutor(q, empty, **layout.executor_kwargs())
+    try:
+        assert ex_empty.handle is not None and ex_empty.placeholder is not None
+        assert key_space_fingerprint(ex_full) == key_space_fingerprint(ex_empty)
+        a_full = DistributedAccumulators(ex_full, torch.device("cuda", 0))
+        a_empty = DistributedAccumulators(ex_empty, torch.device("cuda", 0))
+        ex_full.execute()
+        ex_empty.execute()  # (reset only: nothing to scan)
+        torch.cuda.synchronize()
+        for (k0, t0), (k1, t1) in zip(a_empty.views, a_full.views):  # the placeholder rank as the reduce's destination
+            op = SECTION_OP[k0]
+            if op == dist.ReduceOp.SUM:
+                t0.add_(t1)
+            elif op == dist.ReduceOp.MIN:
+                torch.minimum(t0, t1, out=t0)
+            else:
+                torch.maximum(t0, t1, out=t0)
+        got = ex_empty.fetch()
+        assert_same(got, oracle.run_query(q, segs), rel=1e-9)
+    finally:
+        for e in (ex_full, ex_empty):
+            e.close()
+        for g in full + empty:
+            g.close()

@@ -482,3 +482,58 @@ def test_gloo_table_layout_agrees_on_distinct_value_dictionaries():
     mp.spawn(_distinct_layout_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     exp = list(range(50)) + list(range(100, 150))
     assert out[0] == out[1] == (exp, 200, True)
+
+
+def _empty_rank_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pinot_amd import parse_sql
+    from pinot_amd.engine import GpuQueryExecutor, GpuSegment
+    from pinot_amd.parallel import DistributedAccumulators, HashedAccumulators, check_same_key_space, table_layout
+    from pinot_amd.segment import Segment
+    from synth import make_segment
+    q = parse_sql("SELECT d, COUNT(*), SUM(m), MAX(f) FROM t WHERE d > 3 GROUP BY d")
+    cols = {"d": ("INT", 30), "m": ("LONG", 400), "f": ("DOUBLE", 50)}
+    # rank 1 holds only empty segments
+    segs = [make_segment(70 + i, 300, cols) for i in range(2)] if rank == 0 else [Segment("e0", 0), Segment("e1", 0)]
+    layout = table_layout(q, segs)
+    out["schema%d" % rank] = sorted((k, tuple(v)) for k, v in layout.schema.items())
+    out["dict%d" % rank] = layout.dicts["d"].tolist()
+    if rank == 1:
+        # built without the layout, the empty-only rank has no accumulator block: it still joins the key-space check
+        # (with -1), so every rank raises instead of rank 0 blocking in the collective
+        ex = GpuQueryExecutor(q, [GpuSegment(s) for s in segs])
+        assert ex.handle is None
+        for acc_cls in (DistributedAccumulators, HashedAccumulators):
+            try:
+                acc = acc_cls(ex, "cpu")
+                if acc_cls is HashedAccumulators:
+                    acc.merge()
+                out["raised1_%s" % acc_cls.__name__] = False
+            except L.PinotAmdError:
+                out["raised1_%s" % acc_cls.__name__] = True
+    else:
+        for name in ("DistributedAccumulators", "HashedAccumulators"):
+            try:  # (the planned rank's side of the same check: its own fingerprint)
+                check_same_key_space(4242, "cpu")
+                out["raised0_" + name] = False
+            except L.PinotAmdError:
+                out["raised0_" + name] = True
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_rank_with_only_empty_segments():
+    """a rank whose segments are all empty. table_layout gathers the referenced columns' schema from the
+    ranks that hold docs (so that rank can plan a placeholder block of the agreed layout: test_gpu_dist.py); an executor
+    built without it has no block, and both merge paths still run the key-space collective on it so every rank raises
+    together — no rank is left blocked."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_empty_rank_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    assert out["schema0"] == out["schema1"] == [("d", ("INT", True, True)), ("f", ("DOUBLE", True, True)),
+                                                ("m", ("LONG", True, True))]
+    assert out["dict0"] == out["dict1"] and len(out["dict0"]) > 0
+    for name in ("DistributedAccumulators", "HashedAccumulators"):
+        assert out["raised0_" + name] and out["raised1_" + name]
