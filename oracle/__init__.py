@@ -448,8 +448,37 @@ def run_segment(query, segment):
     return out, oaggs, amap, r.matched
 
 
+def _constant_filters(query, segments):
+    """A filter with constant parts (TRUE / FALSE literals, literal = literal, column = same column) is folded first, as
+    the reference's IdenticalPredicateFilterOptimizer does; a FALSE filter becomes `x = v AND NOT x = v` (no doc)."""
+    import dataclasses
+    from pinot_amd import query as Q
+    from pinot_amd.optimizer import optimize_filter
+
+    def has_const(f):
+        if isinstance(f, (Q.And, Q.Or)):
+            return any(has_const(c) for c in f.children)
+        if isinstance(f, Q.Not):
+            return has_const(f.child)
+        return isinstance(f, (Q.BoolFilter, Q.Comparison))
+    if query.filter is None or not has_const(query.filter):
+        return query
+    seg = next((s for s in segments if s.num_docs > 0), None)
+    schema = {n: (c.data_type, bool(c.single_value)) for n, c in seg.columns.items()} if seg is not None else {}
+    f = optimize_filter(query.filter, schema)
+    if isinstance(f, Q.BoolFilter):
+        if f.value or seg is None:
+            f = None
+        else:
+            name = sorted(seg.columns)[0]
+            leaf = Q.EqPredicate(name, str(seg.column(name).dictionary[0]) if seg.column(name).has_dictionary else "0")
+            f = Q.And((leaf, Q.Not(leaf)))
+    return dataclasses.replace(query, filter=f)
+
+
 def run_query(query, segments):
     """Server-level intermediate result for a segment set, merged by key value in segment order."""
+    query = _constant_filters(query, segments)
     from pinot_amd.engine import AvgPair, IntermediateResult, MinMaxRangePair
     from pinot_amd.hll import HyperLogLog
     merged = {}

@@ -1861,14 +1861,26 @@ int plan_kernels(pa_query* q, Prep& P, TilePlan& plan, TilePlan& count_plan) {
   // LDS goes to tile rings (more resident waves) and the rare survivors update global accumulators directly.
   q->strategy = STRAT_GLOBAL;
   // Dense filter + GROUP BY over a small key box, every column staged (plan_gdense decided the staging)
-  // (lane-major 2048-doc tiles when they keep as many resident waves as step-major 1024-doc ones: plan_tiles' score)
+  // (4- or 8-wave workgroups, lane-major 2048-doc or step-major 1024-doc tiles: the most resident waves, then the
+  // larger tile: plan_tiles' score)
   if (P.gdense) {
-    TilePlan a, b = plan_tiles(q, q->hsegs, STRAT_GDENSE, false, P.gd_lds, true);
-    if (lm) a = plan_tiles(q, q->hsegs, STRAT_GDENSE, true, P.gd_lds, false);
-    if (a.score >= 0 || b.score >= 0) {
-      lm = a.score >= b.score;
-      plan = lm ? a : b;
-      q->strategy = STRAT_GDENSE;
+    TilePlan best;
+    bool best_lm = false;
+    int best_strat = STRAT_GDENSE;
+    for (int st : {STRAT_GDENSE8, STRAT_GDENSE})
+      for (int use_lm : {1, 0}) {
+        if (use_lm && !lm) continue;
+        const TilePlan t = plan_tiles(q, q->hsegs, st, use_lm != 0, P.gd_lds, use_lm == 0);
+        if (t.score > best.score) {
+          best = t;
+          best_lm = use_lm != 0;
+          best_strat = st;
+        }
+      }
+    if (best.score >= 0) {
+      lm = best_lm;
+      plan = best;
+      q->strategy = best_strat;
       P.lds_acc = P.gd_lds;
     }
   }
@@ -2036,11 +2048,11 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
     h.ht_keys = (long long*)q->sections[q->keys_section].ptr;
   }
   h.has_mv = q->has_mv;
-  h.xcd_major = (P.dense || q->strategy == STRAT_GDENSE) ? 1 : 0;
+  h.xcd_major = (P.dense || is_gdense(q->strategy)) ? 1 : 0;
   h.lds_count_off = 0;
-  h.lds_acc_bytes = (q->strategy == STRAT_LDS || q->strategy == STRAT_GDENSE || is_lane(q->strategy))
+  h.lds_acc_bytes = (q->strategy == STRAT_LDS || is_gdense(q->strategy) || is_lane(q->strategy))
                         ? (uint32_t)P.lds_acc : 0;
-  if (q->strategy == STRAT_GDENSE) {
+  if (is_gdense(q->strategy)) {
     // per-segment parameter tables (GdSegPlan): the query's key box and LDS layout + the segment's staged regions
     q->gdplans.assign(std::max(1, q->nseg), GdSegPlan{});
     for (int si = 0; si < q->nseg; ++si) {
@@ -2049,6 +2061,10 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
       const DevSeg& d = q->hsegs[si];
       g.ngb = s.num_group_by;
       g.rpl = P.gd_rp_log2;
+      {
+        const char* e = std::getenv("PA_DEBUG_EMIT");  // measurement only (pa_gdense.h knobs; results invalid)
+        g.pad = e ? std::atoi(e) : 0;
+      }
       for (int j = 0; j < s.num_group_by; ++j) {
         g.gb[j].reg = d.cols[P.gb_slot[j]].lds_off;
         g.gb[j].nbits = d.cols[P.gb_slot[j]].nbits;
@@ -2110,7 +2126,7 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
     A.log2m = s.aggs[a].log2m;
     A.src = P.agg_src[a];
     A.nvals = s.aggs[a].type == PA_AGG_DISTINCTCOUNT ? presence_stride(s.aggs[a]) : 0;
-    if (q->strategy == STRAT_GDENSE) {
+    if (is_gdense(q->strategy)) {
       A.gd_vs = P.gd_vs[a];
       A.gd_op = P.gd_op[a];
       A.gd_acc = P.gd_acc[a];
@@ -2215,7 +2231,7 @@ int plan_limit_buffers(pa_query* q, const Prep& P, int cus, int64_t total_tiles)
 // Device copies of the descriptors (+ the lane-major plan tables).
 int upload_descriptors(pa_query* q) {
   int rc;
-  if (q->strategy == STRAT_GDENSE) {
+  if (is_gdense(q->strategy)) {
     rc = dev_alloc(q->dgdplans, sizeof(GdSegPlan) * q->gdplans.size());
     if (rc) return rc;
     PA_HIP(hipMemcpy(q->dgdplans.p, q->gdplans.data(), sizeof(GdSegPlan) * q->gdplans.size(), hipMemcpyHostToDevice));
@@ -2413,7 +2429,7 @@ int pa_query_prepare(pa_query* q) {
   }
   const int wg_cu = q->split_emit ? std::min(plan.wg_per_cu, q->emit_h_wg) : plan.wg_per_cu;
   const int64_t max_wg = (int64_t)cus * std::max(1, wg_cu);
-  const int wpw = q->partitioned ? scan_waves(q->emit_strat) : kWavesPerWG;
+  const int wpw = q->partitioned ? scan_waves(q->emit_strat) : scan_waves(q->strategy);
   const int64_t want = (total_tiles + wpw - 1) / wpw;
   q->grid = (int)std::max<int64_t>(1, std::min(max_wg, want));
 

@@ -42,16 +42,68 @@ __device__ __forceinline__ uint32_t gd_decode(const lds_u32_t* region, uint32_t 
   return __builtin_amdgcn_alignbit(region[we - 1], region[we], (~e1) & 31u) & nbits_mask((int)nb);
 }
 
-// N docs per lane (doc[k], on[k]) of one staged tile image at LDS byte address img: group key, then COUNT and every
-// aggregation into replica r of the key's LDS accumulators. Every parameter comes from the segment's GdSegPlan in the
-// VGPR gt (v_readlane at compile-time lanes: no scalar loads, whose lgkmcnt waits would also wait for the LDS operations
-// in flight); every load is an LDS read. errs counts matching docs whose key fell outside the LDS box (cannot happen
-// when the planner's box is right; the query then reports an error).
+// Per-tile, per-lane view of the staged columns for the step-major walk: doc 64 i + lane of an nb-bit column has its
+// last bit at 64 nb i + (lane nb + nb - 1), and 64 nb i is a multiple of 32: the two stream words holding the value sit
+// at a lane constant plus 8 nb i bytes, and the alignbit shift is a lane constant. A decode is then one v_mad (address),
+// one ds_read2_b32 and alignbit + and. Raw columns: 4 or 8 bytes per doc, stride 256 / 512 bytes per step.
+struct GdLane {
+  uint32_t ga[kGdMaxGb], gs[kGdMaxGb];    // group-by column j: LDS address of step 0's word pair, alignbit shift
+  uint32_t va[kGdMaxAgg], vs[kGdMaxAgg];  // aggregation k: the same for its column (raw: the value's address)
+};
+
+__device__ __forceinline__ void gd_lane_setup(uint32_t gt, uint32_t img, int lane, GdLane& L) {
+  const int ngb = (int)rl(gt, 0), na = (int)rl(gt, 1);
+#pragma unroll
+  for (int j = 0; j < kGdMaxGb; ++j) {
+    if (j >= ngb) break;
+    const uint32_t nb = rl(gt, 5 + 6 * j);
+    const uint32_t c = (uint32_t)lane * nb + nb - 1u;
+    L.ga[j] = img + 4u * rl(gt, 4 + 6 * j) + 4u * ((c >> 5) - 1u);
+    L.gs[j] = (~c) & 31u;
+  }
+#pragma unroll
+  for (int k = 0; k < kGdMaxAgg; ++k) {
+    if (k >= na) break;
+    const int vsrc = (int)rl(gt, 22 + 6 * k);
+    const uint32_t reg = img + 4u * rl(gt, 24 + 6 * k);
+    if (vsrc <= GVS_TF) {
+      const uint32_t nb = rl(gt, 25 + 6 * k);
+      const uint32_t c = (uint32_t)lane * nb + nb - 1u;
+      L.va[k] = reg + 4u * ((c >> 5) - 1u);
+      L.vs[k] = (~c) & 31u;
+    } else {
+      L.va[k] = reg + (uint32_t)lane * ((vsrc == GVS_RI32 || vsrc == GVS_RF32) ? 4u : 8u);
+      L.vs[k] = 0u;
+    }
+  }
+}
+
+// dictId of step st[k] of a column: word pair at a + 8 nb st, shift sh
 template <int N>
-__device__ __forceinline__ void gd_docs(uint32_t gt, uint32_t img, const uint32_t (&doc)[N], const bool (&on_in)[N],
-                                        uint32_t r, uint32_t base, uint32_t& errs) {
+__device__ __forceinline__ void gd_dec(uint32_t a, uint32_t sh, uint32_t nb, const uint32_t (&st)[N], uint32_t (&id)[N]) {
+  const uint32_t stride = 8u * nb, mask = nbits_mask((int)nb);
+  uint32_t w0[N], w1[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const lds_u32_t* p = lds_at<const lds_u32_t>(a + st[k] * stride);
+    w0[k] = p[0];
+    w1[k] = p[1];
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) id[k] = __builtin_amdgcn_alignbit(w0[k], w1[k], sh) & mask;
+}
+
+// N docs per lane (step st[k] of the tile: doc 64 st[k] + lane; on[k]): group key, then COUNT and every aggregation into
+// replica r of the key's LDS accumulators. Parameters come from the segment's GdSegPlan in the VGPR gt (v_readlane at
+// compile-time lanes: no scalar loads, whose lgkmcnt waits would also wait for the LDS operations in flight); every load
+// is an LDS read. errs counts matching docs whose key fell outside the LDS box (cannot happen when the planner's box is
+// right; the query then reports an error).
+template <int N>
+__device__ __forceinline__ void gd_batch(uint32_t gt, const GdLane& L, const uint32_t (&st)[N], const bool (&on_in)[N],
+                                         uint32_t r, uint32_t base, uint32_t& errs) {
   const int ngb = (int)rl(gt, 0), na = (int)rl(gt, 1);
   const uint32_t rpl = rl(gt, 2);
+  const uint32_t dbg = rl(gt, 3);  // measurement only (PA_DEBUG_EMIT): 2 = no atomics, 4 = no value-table reads
   uint32_t key[N];
   bool on[N];
 #pragma unroll
@@ -63,11 +115,8 @@ __device__ __forceinline__ void gd_docs(uint32_t gt, uint32_t img, const uint32_
   for (int j = 0; j < kGdMaxGb; ++j) {
     if (j >= ngb) break;
     const int o = 4 + 6 * j;
-    const lds_u32_t* reg = lds_at<const lds_u32_t>(img + 4u * rl(gt, o));
-    const uint32_t nb = rl(gt, o + 1);
     uint32_t id[N];
-#pragma unroll
-    for (int k = 0; k < N; ++k) id[k] = gd_decode(reg, doc[k], nb);
+    gd_dec<N>(L.ga[j], L.gs[j], rl(gt, o + 1), st, id);
     const int tab = (int)rl(gt, o + 2);
     if (tab >= 0) {
       const lds_i32_t* t = lds_at<const lds_i32_t>(base + (uint32_t)tab);
@@ -93,7 +142,10 @@ __device__ __forceinline__ void gd_docs(uint32_t gt, uint32_t img, const uint32_
     errs += (on_in[k] && !on[k]) ? 1u : 0u;
     idx[k] = (key[k] << rpl) | r;
   }
-  {
+  if (dbg & 2) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) asm volatile("" ::"v"(idx[k]), "v"((uint32_t)on[k]));
+  } else {
     lds_u32_t* cnt = lds_at<lds_u32_t>(base);
 #pragma unroll
     for (int k = 0; k < N; ++k)
@@ -104,7 +156,6 @@ __device__ __forceinline__ void gd_docs(uint32_t gt, uint32_t img, const uint32_
     if (g >= na) break;
     const int o = 22 + 6 * g;
     const int vs = (int)rl(gt, o), op = (int)rl(gt, o + 1);
-    const uint32_t reg = img + 4u * rl(gt, o + 2);
     const uint32_t acc = base + rl(gt, o + 4);
     int64_t vi[N];
     double vd[N];
@@ -114,12 +165,10 @@ __device__ __forceinline__ void gd_docs(uint32_t gt, uint32_t img, const uint32_
       vd[k] = 0.0;
     }
     if (vs <= GVS_TF) {  // dictionary column: dictId from the staged stream, value from the LDS table (or the id)
-      const uint32_t nb = rl(gt, o + 3);
       uint32_t id[N];
-#pragma unroll
-      for (int k = 0; k < N; ++k) id[k] = gd_decode(lds_at<const lds_u32_t>(reg), doc[k], nb);
+      gd_dec<N>(L.va[g], L.vs[g], rl(gt, o + 3), st, id);
       const uint32_t tab = base + rl(gt, o + 5);
-      if (vs == GVS_ID) {
+      if (vs == GVS_ID || (dbg & 4)) {
 #pragma unroll
         for (int k = 0; k < N; ++k) vi[k] = id[k];
       } else if (vs == GVS_T32) {
@@ -134,18 +183,23 @@ __device__ __forceinline__ void gd_docs(uint32_t gt, uint32_t img, const uint32_
       }
     } else if (vs == GVS_RI32) {
 #pragma unroll
-      for (int k = 0; k < N; ++k) vi[k] = lds_at<const lds_i32_t>(reg)[doc[k]];
+      for (int k = 0; k < N; ++k) vi[k] = lds_at<const lds_i32_t>(L.va[g] + 256u * st[k])[0];
     } else if (vs == GVS_RF32) {
 #pragma unroll
-      for (int k = 0; k < N; ++k) vd[k] = __builtin_bit_cast(float, lds_at<const lds_u32_t>(reg)[doc[k]]);
+      for (int k = 0; k < N; ++k) vd[k] = __builtin_bit_cast(float, lds_at<const lds_u32_t>(L.va[g] + 256u * st[k])[0]);
     } else if (vs == GVS_RI64) {
 #pragma unroll
-      for (int k = 0; k < N; ++k) vi[k] = lds_at<const lds_i64_t>(reg)[doc[k]];
+      for (int k = 0; k < N; ++k) vi[k] = lds_at<const lds_i64_t>(L.va[g] + 512u * st[k])[0];
     } else {
 #pragma unroll
-      for (int k = 0; k < N; ++k) vd[k] = lds_at<const lds_f64_t>(reg)[doc[k]];
+      for (int k = 0; k < N; ++k) vd[k] = lds_at<const lds_f64_t>(L.va[g] + 512u * st[k])[0];
     }
     const bool fl = gvs_float(vs);
+    if (dbg & 2) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) asm volatile("" ::"v"((uint32_t)vi[k]), "v"((uint32_t)(vi[k] >> 32)), "v"(vd[k]));
+      continue;
+    }
     switch (op) {
       case GOP_SUM_I:
 #pragma unroll
@@ -189,55 +243,31 @@ __device__ __forceinline__ void gd_docs(uint32_t gt, uint32_t img, const uint32_
   }
 }
 
-// Dense tile (2048-doc lane-major image), step-major walk: batch of SB steps, lane l takes doc 64 i + l of each; its
-// match bit lives in lane 2i + l/32 of the lane-major match words (bit l % 32).
-__device__ __forceinline__ void gd_tile_dense(uint32_t gt, uint32_t img, uint32_t m, int lane, uint32_t base,
-                                              uint32_t& errs) {
-  constexpr int SB = 4;
-  const uint32_t r = (uint32_t)lane & ((1u << rl(gt, 2)) - 1u);
-#pragma unroll 1
-  for (int i0 = 0; i0 < kSteps; i0 += SB) {
-    uint32_t doc[SB];
-    bool on[SB];
-    bool any = false;
-#pragma unroll
-    for (int s = 0; s < SB; ++s) {
-      const int src = 2 * (i0 + s) + (lane >> 5);
-      const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)m);
-      on[s] = (w >> (lane & 31)) & 1u;
-      doc[s] = (uint32_t)(kWave * (i0 + s) + lane);
-      any |= on[s];
-    }
-    if (__ballot(any) == 0) continue;
-    gd_docs<SB>(gt, img, doc, on, r, base, errs);
-  }
-}
-
-// Sparse tile: each lane walks its own matching docs, KB per batch; doc of bit i of lane l = LM ? 32 l + i : 64 i + l.
-template <int LM>
-__device__ __forceinline__ void gd_tile_sparse(uint32_t gt, uint32_t img, uint32_t m, int lane, uint32_t base,
-                                               uint32_t& errs) {
+// The matching docs of one tile, step-major match bits s (bit i <=> doc 64 i + lane): every lane walks its own set bits,
+// KB per batch, so a batch is productive on every lane until the lanes run out of matches (max popcount over the
+// lanes batches: ~23 of 32 steps at 50 % density, ~7 at 10 %).
+__device__ __forceinline__ void gd_walk(uint32_t gt, uint32_t img, uint32_t s, int lane, uint32_t base, uint32_t& errs) {
   constexpr int KB = 4;
+  GdLane L;
+  gd_lane_setup(gt, img, lane, L);
   const uint32_t r = (uint32_t)lane & ((1u << rl(gt, 2)) - 1u);
 #pragma unroll 1
-  while (__ballot(m != 0) != 0) {
-    uint32_t doc[KB];
+  while (__ballot(s != 0) != 0) {
+    uint32_t st[KB];
     bool on[KB];
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
-      on[k] = m != 0;
-      const uint32_t i = on[k] ? (uint32_t)__builtin_ctz(m) : 0u;
-      doc[k] = LM ? 32u * (uint32_t)lane + i : (uint32_t)kWave * i + (uint32_t)lane;
-      m &= m - 1u;
+      on[k] = s != 0;
+      st[k] = on[k] ? (uint32_t)__builtin_ctz(s) : 0u;
+      s &= s - 1u;
     }
-    gd_docs<KB>(gt, img, doc, on, r, base, errs);
+    gd_batch<KB>(gt, L, st, on, r, base, errs);
   }
 }
 
-// A tile is walked densely when most lanes hold at least this many matching docs of their 32 (16 step-major).
-constexpr int kGdDenseLaneMin = 10;
-
-// Filter of one lane-major tile (every literal eager: the planner's condition) + the tile's matching docs.
+// Filter of one lane-major 2048-doc tile (every literal eager: the planner's condition), then the transpose of the match
+// words to step-major bits (lane l, bit i <=> doc 64 i + l lives in lane 2i + l/32, bit l % 32: one ds_bpermute per step)
+// and the walk.
 __device__ __forceinline__ uint32_t gd_tile(uint32_t gt, uint32_t pp, int64_t wt, uint32_t img, int lane,
                                             uint32_t base, uint32_t& errs) {
   const int64_t doc_base = wt * kWTileDocs;
@@ -264,15 +294,20 @@ __device__ __forceinline__ uint32_t gd_tile(uint32_t gt, uint32_t pp, int64_t wt
     }
   }
   const uint32_t mine = (uint32_t)__builtin_popcount(m);
-  const uint64_t any = __ballot(mine != 0);
-  if (any == 0) return 0;
-  if (__builtin_popcountll(__ballot((int)mine >= kGdDenseLaneMin)) >= kWave / 2) gd_tile_dense(gt, img, m, lane, base, errs);
-  else gd_tile_sparse<1>(gt, img, m, lane, base, errs);
+  if (__ballot(mine != 0) == 0) return 0;
+  if (rl(gt, 3) & 1) return mine;  // measurement only: filter only
+  uint32_t s = 0;
+  const int sh = lane & 31;
+#pragma unroll
+  for (int i = 0; i < kSteps; ++i) {
+    const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((2 * i + (lane >> 5)) << 2, (int)m);
+    s |= ((w >> sh) & 1u) << i;
+  }
+  gd_walk(gt, img, s, lane, base, errs);
   return mine;
 }
 
-// Step-major 1024-doc tiles (wide staged images: half the LDS of a 2048-doc tile): filter by leaf_bits (bit i of lane l
-// <=> doc 64 i + l), so the match bits are already in the order the dense walk takes them.
+// Step-major 1024-doc tiles: filter by leaf_bits (bit i of lane l <=> doc 64 i + l) straight into the walk's order.
 constexpr int kGdSmSteps = 16;
 __device__ __forceinline__ uint32_t gd_tile_sm(uint32_t gt, const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
                                                int64_t wt, const uint32_t* img_ptr, uint32_t img, int lane,
@@ -300,24 +335,8 @@ __device__ __forceinline__ uint32_t gd_tile_sm(uint32_t gt, const DevQuery* __re
   }
   const uint32_t mine = (uint32_t)__builtin_popcount(m);
   if (__ballot(mine != 0) == 0) return 0;
-  const uint32_t r = (uint32_t)lane & ((1u << rl(gt, 2)) - 1u);
-  if (__builtin_popcountll(__ballot((int)mine >= kGdDenseLaneMin / 2)) >= kWave / 2) {
-    constexpr int SB = 4;
-#pragma unroll 1
-    for (int i0 = 0; i0 < ST; i0 += SB) {
-      if (__ballot(((m >> i0) & ((1u << SB) - 1u)) != 0) == 0) continue;
-      uint32_t doc[SB];
-      bool on[SB];
-#pragma unroll
-      for (int k = 0; k < SB; ++k) {
-        on[k] = (m >> (i0 + k)) & 1u;
-        doc[k] = (uint32_t)(kWave * (i0 + k) + lane);
-      }
-      gd_docs<SB>(gt, img, doc, on, r, base, errs);
-    }
-  } else {
-    gd_tile_sparse<0>(gt, img, m, lane, base, errs);
-  }
+  if (rl(gt, 3) & 1) return mine;  // measurement only: filter only
+  gd_walk(gt, img, m, lane, base, errs);
   return mine;
 }
 

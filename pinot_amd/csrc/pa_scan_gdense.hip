@@ -4,8 +4,11 @@
 namespace pa {
 
 const void* scan_fn_gdense(int strategy, int lm) {
-  if (strategy != STRAT_GDENSE) return nullptr;
-  return lm ? (const void*)gdense_kernel<kGdWaves, 1> : (const void*)gdense_kernel<kGdWaves, 0>;
+  if (strategy == STRAT_GDENSE)
+    return lm ? (const void*)gdense_kernel<kGdWaves, 1> : (const void*)gdense_kernel<kGdWaves, 0>;
+  if (strategy == STRAT_GDENSE8)
+    return lm ? (const void*)gdense_kernel<2 * kGdWaves, 1> : (const void*)gdense_kernel<2 * kGdWaves, 0>;
+  return nullptr;
 }
 
 }  // namespace pa

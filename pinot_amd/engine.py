@@ -12,6 +12,7 @@ reference's intermediate results: COUNT -> long, SUM/MIN/MAX -> double, AVG -> (
 DISTINCTCOUNTHLL -> HyperLogLog.
 """
 import ctypes
+import dataclasses
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -21,6 +22,7 @@ from . import _lib as L
 from . import predicate as P
 from . import query as Q
 from .hll import HyperLogLog, hash_value
+from .optimizer import optimize_filter
 from .segment import Segment
 
 _VTYPE = {"INT": L.PA_INT, "LONG": L.PA_LONG, "FLOAT": L.PA_FLOAT, "DOUBLE": L.PA_DOUBLE, "STRING": L.PA_STRING}
@@ -205,6 +207,7 @@ class GpuQueryExecutor:
         self.enforce_num_groups_limit = enforce_num_groups_limit
         self.handle = None
         self.placeholder = None
+        self.match_none = False  # the rewritten filter is FALSE: the block stays reset, nothing is scanned
         if not self.segs and schema:
             self.placeholder = GpuSegment(self._placeholder_segment(schema), column_ids=gpu_segments[0].column_ids,
                                           device=self.device)
@@ -238,9 +241,19 @@ class GpuQueryExecutor:
     # ------------------------------------------------------------------ planning
     def _plan(self):
         lib = L.lib()
-        q = self.query
         ids = self.gsegs[0].column_ids
         seg0 = self.segs[0]
+        # the reference's compile-time filter rewrites (QueryOptimizer: merged ranges / IN lists, constant predicates),
+        # so the leaves below and the execution statistics follow the operator tree the reference builds
+        schema = {n: (c.data_type, bool(c.single_value)) for n, c in seg0.columns.items()}
+        filt = optimize_filter(self.query.filter, schema)
+        if isinstance(filt, Q.BoolFilter):
+            self.match_none = not filt.value  # FALSE: EmptyFilterOperator, TRUE: MatchAllFilterOperator
+            filt = None
+        if _has_comparison(filt):
+            raise UnsupportedQuery("comparison between two different columns")
+        self.query = dataclasses.replace(self.query, filter=filt)
+        q = self.query
         spec = L.QuerySpec()
 
         # aggregations -> GPU accumulators (AVG = SUM + group count, AVGMV = SUM + COUNT_MV over the MV column; the
@@ -433,7 +446,7 @@ class GpuQueryExecutor:
 
     # ------------------------------------------------------------------ execution
     def execute(self, stream=None):
-        if not self.segs:  # every bound segment is empty: nothing to scan (a placeholder plan: its block reset only)
+        if not self.segs or self.match_none:  # nothing to scan (a placeholder plan, a FALSE filter): block reset only
             if self.handle is not None:
                 L.check(L.lib().pa_query_reset(self.handle, stream), "pa_query_reset")
             return
@@ -443,7 +456,7 @@ class GpuQueryExecutor:
         L.check(L.lib().pa_query_reset(self.handle, stream), "pa_query_reset")
 
     def scan(self, stream=None):
-        if not self.segs:
+        if not self.segs or self.match_none:
             return
         L.check(L.lib().pa_query_scan(self.handle, stream), "pa_query_scan")
 
@@ -466,7 +479,7 @@ class GpuQueryExecutor:
         names = ("strategy", "steps", "dma_slots", "ring", "wg_per_cu", "grid", "lds_bytes")
         out["plan"] = {n: v.value for n, v in zip(names, vals)}
         out["plan"]["strategy"] = {0: "lds", 1: "global", 2: "partitioned", 4: "lane", 5: "lane", 6: "lane", 7: "lane",
-                                    8: "lds_dense"}[out["plan"]["strategy"]]
+                                    8: "lds_dense", 9: "lds_dense"}[out["plan"]["strategy"]]
         out["plan"]["eager_literals"] = int(L.lib().pa_query_num_eager_literals(self.handle))
         out["plan"]["lane_major"] = int(L.lib().pa_query_lane_major(self.handle))
         out["plan"]["limit_trimming"] = int(L.lib().pa_query_limit_trimming(self.handle))
@@ -564,6 +577,8 @@ class GpuQueryExecutor:
         operator accounting (filter_stats.py), closed forms over counts the GPU takes from its leaf bitmaps
         (pa_bitmap_counts), the iterator replay over host bitmaps only for operator trees without one."""
         from . import filter_stats as FS
+        if self.match_none:
+            return 0, 0  # EmptyFilterOperator: no entry read, no doc projected
         return FS.server_stats_device(self.query, self.segs, self, stream)
 
     def fetch(self, stream=None, execution_stats=False) -> IntermediateResult:
@@ -647,6 +662,14 @@ class GpuQueryExecutor:
             self.close()
         except Exception:
             pass
+
+
+def _has_comparison(f):
+    if isinstance(f, (Q.And, Q.Or)):
+        return any(_has_comparison(c) for c in f.children)
+    if isinstance(f, Q.Not):
+        return _has_comparison(f.child)
+    return isinstance(f, Q.Comparison)
 
 
 def _py(v):

@@ -19,10 +19,11 @@ reference's iterators over per-leaf doc bitmaps that the GPU computes (pa_query_
 numEntriesScannedPostFilter = numDocsScanned x projected columns (ProjectionOperator: the group-by and aggregation
 argument columns), 0 for the non-scan plans.
 
-Compile-time filter rewrites of the reference other than AND/OR flattening (FlattenAndOrFilterOptimizer) are not
-restated (MergeRangeFilterOptimizer, MergeEqInFilterOptimizer, ...): filters they would rewrite get the counts of the
-unrewritten tree. Parity is pinned by the reference's golden statistics (InterSegmentAggregationSingleValueQueriesTest,
-InterSegmentGroupBySingleValueQueriesTest: tests/golden/sv_queries.json)."""
+The executor hands this module the filter after the reference's compile-time rewrites (optimizer.py: AND/OR
+flattening, merged ranges and IN lists, constant predicates, numeric literals against the column type), so the
+operator tree is the one the reference's FilterPlanNode builds. Parity is pinned by the reference's golden statistics
+(InterSegmentAggregationSingleValueQueriesTest, InterSegmentGroupBySingleValueQueriesTest: tests/golden/sv_queries.json)
+and its rewrite fixtures (QueryOptimizerTest: tests/golden/query_optimizer.json)."""
 import ctypes
 
 import numpy as np

@@ -70,6 +70,22 @@ class Not:
     child: object
 
 
+@dataclass(frozen=True)
+class BoolFilter:
+    """A constant filter (the boolean literal expression the reference's filter optimizers produce: TRUE becomes
+    MatchAllFilterOperator, FALSE EmptyFilterOperator)."""
+    value: bool
+
+
+@dataclass(frozen=True)
+class Comparison:
+    """`a = b` / `a != b` where a side is not a plain column-vs-literal predicate (literal = literal, column = column):
+    folded by IdenticalPredicateFilterOptimizer / constant evaluation (optimizer.py); each side ("id"|"lit", text)."""
+    lhs: Tuple
+    op: str
+    rhs: Tuple
+
+
 PREDICATES = (EqPredicate, NotEqPredicate, InPredicate, NotInPredicate, RangePredicate)
 
 
@@ -144,7 +160,7 @@ class Query:
                     walk(c)
             elif isinstance(f, Not):
                 walk(f.child)
-            else:
+            elif hasattr(f, "column"):
                 cols.add(f.column)
         walk(self.filter)
         return cols
@@ -152,6 +168,7 @@ class Query:
 
 # ------------------------------------------------------------------ SQL subset parser
 _TOKEN = re.compile(r"\s*(?:(?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?)|(?P<str>'(?:[^']|'')*')|"
+                    r"(?P<qid>\"(?:[^\"]|\"\")*\")|"
                     r"(?P<op><>|!=|<=|>=|=|<|>|\(|\)|,|\*)|(?P<id>[A-Za-z_][A-Za-z0-9_\.]*))")
 
 
@@ -167,6 +184,8 @@ def _tokenize(sql):
             out.append(("lit", m.group("num")))
         elif m.group("str") is not None:
             out.append(("lit", m.group("str")[1:-1].replace("''", "'")))
+        elif m.group("qid") is not None:  # "quoted identifier"
+            out.append(("id", m.group("qid")[1:-1].replace('""', '"')))
         elif m.group("op") is not None:
             out.append(("op", m.group("op")))
         else:
@@ -258,6 +277,25 @@ class _Parser:
         return self.predicate()
 
     def predicate(self):
+        tok, nxt = self.peek(), self.peek(1)
+        if tok[0] == "id" and tok[1].upper() in ("TRUE", "FALSE") and not (nxt[0] == "op" and nxt[1] in
+                                                                           ("=", "!=", "<>", "<", "<=", ">", ">=")):
+            self.i += 1
+            return BoolFilter(tok[1].upper() == "TRUE")
+        if tok[0] == "lit" or (tok[0] == "id" and nxt[0] == "op" and nxt[1] in ("=", "!=", "<>") and
+                               self.peek(2)[0] == "id" and self.peek(2)[1].upper() not in ("TRUE", "FALSE")):
+            # literal = literal, column = column: a comparison the filter optimizers fold (optimizer.py)
+            lhs = (tok[0], tok[1])
+            self.i += 1
+            op = self.peek()
+            if op[0] != "op" or op[1] not in ("=", "!=", "<>"):
+                raise ValueError("expected = or != after %r" % (tok,))
+            self.i += 1
+            rhs = self.peek()
+            if rhs[0] not in ("id", "lit"):
+                raise ValueError("expected a literal or column at %r" % (rhs,))
+            self.i += 1
+            return Comparison(lhs, "=" if op[1] == "=" else "!=", (rhs[0], rhs[1]))
         col = self.ident()
         if self.kw("BETWEEN"):
             lo = self.literal()
@@ -358,6 +396,15 @@ class _Parser:
 
 def parse_sql(sql: str) -> Query:
     return _Parser(sql).parse()
+
+
+def parse_filter(text: str):
+    """A WHERE clause on its own (the filter tree parse_sql builds for it)."""
+    p = _Parser(text)
+    f = p.filter_or()
+    if p.peek()[0] is not None:
+        raise ValueError("trailing tokens: %r" % (p.t[p.i:],))
+    return f
 
 
 def query_columns(query):

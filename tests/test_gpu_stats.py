@@ -87,10 +87,41 @@ def test_execution_stats_device_vs_replay():
                 ex = GpuQueryExecutor(q, gs)
                 try:
                     got = ex.execution_stats()
-                    want = FS.server_stats(q, ex.segs, lambda si: ex.leaf_bitmaps(si))
+                    # (the executor holds the reference's rewritten filter: optimizer.py)
+                    want = FS.server_stats(ex.query, ex.segs, lambda si: ex.leaf_bitmaps(si))
                 finally:
                     ex.close()
                 assert got == want, sql
+    finally:
+        for g in gs:
+            g.close()
+
+
+def test_merged_range_is_one_scan_on_the_gpu():
+    """MergeRangeFilterOptimizer feeds the GPU statistics path: `a >= 10 AND a <= 40` is ONE scan of a (the reference's
+    rewritten RANGE predicate reads every entry once: numEntriesScannedInFilter = the docs), where the unrewritten AND
+    of two scans (the host replay of the original tree over its two leaves) reads more; the groups are the same."""
+    from pinot_amd.segment import unpack_bits
+    segs = [_segment(5, 120_001), _segment(6, 9000)]
+    gs = [GpuSegment(s) for s in segs]
+    try:
+        q = parse_sql("SELECT c, SUM(b) FROM t WHERE a >= 10 AND a <= 40 GROUP BY c")
+        ex = GpuQueryExecutor(q, gs)
+        try:
+            assert isinstance(ex.query.filter, type(q.filter.children[0]))  # one RANGE predicate
+            in_filter, post = ex.execution_stats()
+            res = ex.run()
+        finally:
+            ex.close()
+        total = sum(s.num_docs for s in segs)
+        assert in_filter == total
+        raw = 0
+        for s in segs:
+            col = s.column("a")
+            v = col.dictionary[unpack_bits(col.fwd_bytes, s.num_docs, col.num_bits)]
+            raw += FS.entries_scanned_in_filter(q.filter, s, np.asarray([v >= 10, v <= 40]))
+        assert raw > in_filter
+        assert post == res.num_docs_scanned * 2  # projected: c and b
     finally:
         for g in gs:
             g.close()
