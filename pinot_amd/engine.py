@@ -13,6 +13,7 @@ DISTINCTCOUNTHLL -> HyperLogLog.
 """
 import ctypes
 import dataclasses
+import threading
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -132,11 +133,13 @@ class IntermediateResult:
 
 class PinnedPool:
     """Page-locked host buffers (pa_host_alloc) reused across fetches: pa_query_fetch DMAs every result column straight
-    into them. Arrays handed out are views, valid until the pool's next fetch. One pool per process (OUTPUT_POOL): a
-    server's queries fetch one after another, and pinning memory costs far more than a fetch."""
+    into them. Arrays handed out are views, valid until the pool's next fetch from the same thread. One pool per thread
+    (OUTPUT_POOL is thread-local), so concurrent fetches from different threads never share a buffer; a slot that grows
+    retires its old buffer instead of freeing it (views an earlier fetch returned stay readable until close())."""
 
     def __init__(self):
         self.bufs = {}  # slot -> (address, bytes)
+        self.retired = []
 
     def array(self, slot, count, dtype):
         dt = np.dtype(dtype)
@@ -144,7 +147,7 @@ class PinnedPool:
         addr, size = self.bufs.get(slot, (None, 0))
         if size < need:
             if addr:
-                L.lib().pa_host_free(addr)
+                self.retired.append(addr)
             size = max(need, size * 2)
             addr = L.check_ptr(L.lib().pa_host_alloc(size), "pa_host_alloc")
             self.bufs[slot] = (addr, size)
@@ -154,10 +157,26 @@ class PinnedPool:
     def close(self):
         for addr, _ in self.bufs.values():
             L.lib().pa_host_free(addr)
+        for addr in self.retired:
+            L.lib().pa_host_free(addr)
         self.bufs = {}
+        self.retired = []
 
 
-OUTPUT_POOL = PinnedPool()
+class _ThreadPools(threading.local):
+    """OUTPUT_POOL: one PinnedPool per thread (attribute access forwards to this thread's pool)."""
+
+    def __init__(self):
+        self.pool = PinnedPool()
+
+    def array(self, slot, count, dtype):
+        return self.pool.array(slot, count, dtype)
+
+    def close(self):
+        self.pool.close()
+
+
+OUTPUT_POOL = _ThreadPools()
 
 
 def _flatten_filter(f, leaves, ops):

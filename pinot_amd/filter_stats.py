@@ -319,15 +319,18 @@ def _leaf_op(pred, seg, mask, index_info, lf=None):
         if n == col.cardinality:
             return _Op("all")
     sorted_col = col.has_dictionary and sv and bool(col.is_sorted)
-    inverted, ranged = index_info(pred.column)
+    inverted, ranged, exact = index_info(pred.column)
     if sorted_col:
         return _Op("sorted", HIGH, mask)
     if isinstance(pred, Q.RangePredicate):
         if ranged:
+            if not exact:  # RangeIndexBasedFilterOperator scans the index's partial matches (bucket bounds of a v1
+                # index): not restated
+                raise _Unsupported("RANGE predicate on an inexact (v1) range index")
             return _Op("bitmap", LOW, mask)
     elif inverted:
         return _Op("bitmap", MEDIUM, mask)
-    elif ranged and isinstance(pred, Q.EqPredicate):
+    elif ranged and exact and isinstance(pred, Q.EqPredicate):
         # RangeIndexBasedFilterOperator.canEvaluate: EQ on an exact range index (the bit-sliced v2 index every
         # segment here is taken to have; FilterOperatorUtils.java:127-130)
         return _Op("bitmap", LOW, mask)
@@ -410,15 +413,17 @@ def _iterator(op, n, scans):
 
 
 def segment_index_info(segment):
-    """index_info callback from the segment's column metadata: (inverted index, range index)."""
+    """index_info callback from the segment's column metadata: (inverted index, range index, range index exact)."""
     return lambda name: (bool(getattr(segment.column(name), "inverted_index", False)),
-                         bool(getattr(segment.column(name), "range_index", False)))
+                         bool(getattr(segment.column(name), "range_index", False)),
+                         bool(getattr(segment.column(name), "range_index_exact", True)))
 
 
 def entries_scanned_in_filter(filt, segment, bitmaps, index_info=None):
     """numEntriesScannedInFilter of one segment when the projection iterates the filter to the end.
     filt: the query's filter tree (None = no filter); bitmaps: bool[leaves, num_docs] in the engine's leaf order
-    (predicate.expand_raw_in + the engine's flattening); index_info(column) -> (inverted index, range index)."""
+    (predicate.expand_raw_in + the engine's flattening); index_info(column) -> (inverted index, range index, range index
+    exact)."""
     if filt is None:
         return 0
     index_info = index_info or segment_index_info(segment)
@@ -630,7 +635,9 @@ def _filter_columns(f):
 def _tree_signature(seg, fcols, params):
     """Everything _build reads from a segment (the bound leaf parameters, each filter column's dictionary size,
     sortedness and indexes), or None when the tree must be built per segment (no bound parameters; MV columns, whose
-    scan costs are per-doc value counts)."""
+    scan costs are per-doc value counts). Segments with equal signatures share one operator tree, so this key must list
+    EVERY segment attribute _build / _leaf_op read (index_info included): a new per-segment input of the leaf operator
+    choice goes here too, or trees leak across segments."""
     if params is None:
         return None
     cols = []
@@ -639,7 +646,8 @@ def _tree_signature(seg, fcols, params):
         if not c.single_value:
             return None
         cols.append((c.has_dictionary, c.cardinality if c.has_dictionary else 0, bool(c.is_sorted),
-                     bool(getattr(c, "inverted_index", False)), bool(getattr(c, "range_index", False))))
+                     bool(getattr(c, "inverted_index", False)), bool(getattr(c, "range_index", False)),
+                     bool(getattr(c, "range_index_exact", True))))
     leaves = tuple((p.kind, p.lo, p.hi, bool(p.negate), None if p.ids is None else len(np.unique(p.ids)))
                    if isinstance(p, DictLeaf) else None for p in params)
     return leaves, tuple(cols)

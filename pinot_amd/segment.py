@@ -64,6 +64,7 @@ class Column:
     single_value: bool = True
     inverted_index: bool = False              # index metadata the filter-statistics restatement needs (the GPU
     range_index: bool = False                 # scan itself never uses an index: filter_stats.py)
+    range_index_exact: bool = True            # bit-sliced (v2) range index: exact matches; v1: partial matches
     total_num_values: int = 0                 # MV: values over all docs (FixedBitMVForwardIndexWriter totalNumValues)
     max_num_multi_values: int = 0             # MV: longest row
 

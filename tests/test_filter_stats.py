@@ -296,3 +296,28 @@ def test_constant_time_word_leaps_match_the_sequence_rule():
             n, prev = _word_leaps(x, y, prev)
             total += n
         assert total == np_leaps(a, b)
+
+
+def test_operator_trees_not_shared_across_index_configurations():
+    """segments with the same data and dictionaries but different indexes on a filter column (none, an
+    exact range index, an inverted index, an inexact v1 range index) must not share an operator tree in the closed-form
+    planner (_tree_signature lists every index attribute _leaf_op reads): each gets its own accounting, equal to its
+    own replay. An EQ on an inexact range index scans (RangeIndexBasedFilterOperator.canEvaluate needs isExact)."""
+    from pinot_amd.segment import create_segment
+    rng = np.random.default_rng(21)
+    n = 4000
+    data = {"a": rng.integers(0, 60, n).astype(np.int32), "b": rng.integers(0, 100, n).astype(np.int32),
+            "c": rng.integers(0, 7, n).astype(np.int32)}
+    types = {"a": "INT", "b": "INT", "c": "INT"}
+    segs = [create_segment("plain", data, types), create_segment("ranged", data, types, range_index_columns=("a",)),
+            create_segment("inverted", data, types, inverted_index_columns=("a",)),
+            create_segment("v1", data, types, range_index_columns=("a",))]
+    segs[3].column("a").range_index_exact = False
+    q = parse_sql("SELECT c, SUM(b) FROM t WHERE a = 5 AND b < 50 GROUP BY c")
+    masks = [leaf_masks(q, s) for s in segs]
+    params = [[P.dictionary_leaf(pred, s.column(pred.column)) for pred in _leaves(q, s)] for s in segs]
+    got = FS.server_stats_closed_form(q, segs, np_counts(lambda si: masks[si], segs), lambda si: masks[si], params)
+    assert got == FS.server_stats(q, segs, lambda si: masks[si])
+    per = [FS.server_stats_closed_form(q, [s], np_counts(lambda si: masks[i], [s]), lambda si: masks[i], [params[i]])
+           for i, s in enumerate(segs)]
+    assert per[0] == per[3] != per[1] == per[2]  # scan vs index-served EQ
