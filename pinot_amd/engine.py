@@ -591,14 +591,16 @@ class GpuQueryExecutor:
         w = buf.cpu().numpy().view(np.uint8).reshape(nl, words * 4)
         return np.unpackbits(w, axis=1, bitorder="little")[:, :n].astype(bool)
 
-    def execution_stats(self, stream=None):
+    def execution_stats(self, stream=None, docs_total=None):
         """(numEntriesScannedInFilter, numEntriesScannedPostFilter) of this server's segments: the reference's
         operator accounting (filter_stats.py), closed forms over counts the GPU takes from its leaf bitmaps
         (pa_bitmap_counts), the iterator replay over host bitmaps only for operator trees without one."""
         from . import filter_stats as FS
         if self.match_none:
             return 0, 0  # EmptyFilterOperator: no entry read, no doc projected
-        return FS.server_stats_device(self.query, self.segs, self, stream)
+        if docs_total is None:  # numDocsScanned of the last fetch (< 0: none yet)
+            docs_total = int(L.lib().pa_query_matched_docs(self.handle))
+        return FS.server_stats_device(self.query, self.segs, self, stream, docs_total if docs_total >= 0 else None)
 
     def fetch(self, stream=None, execution_stats=False) -> IntermediateResult:
         """execution_stats=True also fills numEntriesScannedInFilter / PostFilter (one leaf-bitmap pass and a few
@@ -613,7 +615,8 @@ class GpuQueryExecutor:
         res.num_total_docs = sum(s.num_docs for s in self.all_segs)
         res.num_docs_scanned = int(lib.pa_query_matched_docs(self.handle))
         if execution_stats:
-            res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter = self.execution_stats(stream)
+            res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter = self.execution_stats(
+                stream, res.num_docs_scanned)
         key_cols = [kc.tolist() for kc in self.key_values(keys)]
         cols = []  # one python list per query aggregation
         for a, pi in zip(q.aggregations, self.agg_map):

@@ -653,11 +653,14 @@ def _tree_signature(seg, fcols, params):
     return leaves, tuple(cols)
 
 
-def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps, leaf_params=None):
+def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps, leaf_params=None, docs_total=None):
     """server_stats through the closed forms above. counts_fn(reqs) -> int64[len(reqs), 4]: for every request
     (segment index, program A, program B) -> row, pa_bitmap_counts' four counts. Segments without a closed form replay
     the iterators over leaf_bitmaps(i) (host bitmaps, as server_stats). leaf_params[i]: segment i's bound leaf
-    parameters in leaf order (GpuQueryExecutor.leaf_params), reused instead of re-matching the dictionaries."""
+    parameters in leaf order (GpuQueryExecutor.leaf_params), reused instead of re-matching the dictionaries.
+    docs_total: the scan's numDocsScanned over these segments, if known. When every segment's filter cost is a constant
+    (a scan driven to EOF reads every entry; OR / NOT of scans; index-served operators read none) the post-filter count
+    is docs_total x projected columns and counts_fn is never called: no pass over the filter columns."""
     ncols = projected_columns(query)
     filt = query.filter
     reqs = {}
@@ -667,7 +670,7 @@ def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps, leaf_para
     trees = {}  # operator tree + docs program per segment signature (segments of a table usually share one)
     for si, seg in enumerate(segments):
         if filt is None:
-            plans.append(None if non_scan_plan(query, seg, True) else (_Terms(0), _Terms(seg.num_docs)))
+            plans.append(None if non_scan_plan(query, seg, True) else (_Terms(0), None, _Terms(seg.num_docs)))
             continue
         try:
             params = None if leaf_params is None else leaf_params[si]
@@ -684,10 +687,18 @@ def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps, leaf_para
                 plans.append(None)
                 continue
             cost = _Terms(0) if op.kind in ("empty", "all") else _cost_next(op, seg, si, reqs)
-            docs = _Terms(0).request(reqs, si, docs_prog, [], 0)
-            plans.append((cost, docs))
+            plans.append((cost, docs_prog, None))
         except _Unsupported:
             plans.append("host")
+    constant = docs_total is not None and not reqs and all(p is not None and p != "host" for p in plans)
+    if constant:
+        return sum(p[0].value(None) for p in plans), int(docs_total) * ncols
+    for si, p in enumerate(plans):
+        if isinstance(p, tuple):
+            try:
+                plans[si] = (p[0], p[2] if p[1] is None else _Terms(0).request(reqs, si, p[1], [], 0))
+            except _Unsupported:
+                plans[si] = "host"
     counts = counts_fn(reqs) if reqs else None
     in_filter = post = 0
     for p in plans:
@@ -721,8 +732,9 @@ def device_counts(executor, segments, reqs, stream=None):
     return out
 
 
-def server_stats_device(query, segments, executor, stream=None):
-    """server_stats with the counts computed on the GPU (device_counts); same results."""
+def server_stats_device(query, segments, executor, stream=None, docs_total=None):
+    """server_stats with the counts computed on the GPU (device_counts); same results. docs_total: the executor's
+    numDocsScanned of its last scan (server_stats_closed_form: constant-cost filters then need no GPU pass)."""
     return server_stats_closed_form(query, segments, lambda reqs: device_counts(executor, segments, reqs, stream),
                                     lambda si: executor.leaf_bitmaps(si, stream),
-                                    getattr(executor, "leaf_params", None))
+                                    getattr(executor, "leaf_params", None), docs_total)

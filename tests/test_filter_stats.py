@@ -321,3 +321,21 @@ def test_operator_trees_not_shared_across_index_configurations():
     per = [FS.server_stats_closed_form(q, [s], np_counts(lambda si: masks[i], [s]), lambda si: masks[i], [params[i]])
            for i, s in enumerate(segs)]
     assert per[0] == per[3] != per[1] == per[2]  # scan vs index-served EQ
+
+
+@pytest.mark.parametrize("where", ["a < 50", "NOT a < 50", "a < 10 OR b < 10", "s = 7", "c IN (1, 2, 3)",
+                                   "NOT (a < 10 OR b < 20)"])
+def test_constant_cost_filters_need_no_counts(where):
+    """A filter whose entries are a constant (every scan driven to EOF reads all docs; index-served operators none):
+    given the scan's numDocsScanned the closed form never asks for counts, so the statistics cost no pass over the
+    filter columns (configs[0]'s day BETWEEN a AND b)."""
+    segs = [_seg(3000, 3), _seg(4097, 4)]
+
+    def boom(*_):
+        raise AssertionError("counts requested for a constant-cost filter")
+    for sql in ("SELECT COUNT(*), SUM(a) FROM t WHERE " + where, "SELECT c, SUM(a) FROM t WHERE %s GROUP BY c" % where):
+        q = parse_sql(sql)
+        masks = [leaf_masks(q, s) for s in segs]
+        want = FS.server_stats(q, segs, lambda si: masks[si])
+        docs = sum(int(FS.filter_mask(q.filter, s, masks[i]).sum()) for i, s in enumerate(segs))
+        assert FS.server_stats_closed_form(q, segs, boom, boom, docs_total=docs) == want, sql
