@@ -206,7 +206,9 @@ typedef struct {
 #define PA_QF_NO_DENSE_GROUP (1 << 29)    /* filter + GROUP BY over a small key space: the LDS strategy (post-filter
                                              columns per matching doc from HBM) instead of the dense group-by kernel
                                              (every column staged, value dictionaries and remaps in LDS) */
-#define PA_QF_PART_SHIFT 22               /* bits 22..23: LDS per partition of the partitioned aggregation (0 = auto,
+#define PA_QF_FILTER_STATS (1 << 30)      /* the scan also counts what the execution statistics of an AND of two scan
+                                             leaves need (pa_query_leap_leaf / pa_query_leap_counts) */
+#define PA_QF_PART_SHIFT 22              /* bits 22..23: LDS per partition of the partitioned aggregation (0 = auto,
                                              1 = 64 KiB, 2 = 96 KiB, 3 = 144 KiB): larger partitions = fewer record
                                              write fronts per XCD */
 
@@ -332,6 +334,14 @@ int pa_bitmap_counts(const uint32_t* device_bitmaps, int64_t words, int32_t num_
  * returns when they are written (synchronises `stream`). Device scratch is owned by the query. */
 int pa_query_filter_counts(pa_query* q, int32_t num_requests, const int32_t* segments, const int32_t* programs,
                            const int32_t* lengths, int64_t* out, void* stream);
+/* Execution statistics fused into the scan (PA_QF_FILTER_STATS). When the filter is an AND of two single-value scan
+ * leaves, one evaluated on whole tiles (E, sparse) and one per E doc (Z), the scan also counts per segment the docs
+ * that matched and the leaps of AndDocIdIterator(A = Z, B = E) (the counts pa_query_filter_counts gives for programs
+ * A = [Z], B = [E]): pa_query_leap_leaf returns E's leaf index (spec order) when the scan counts them, else -1.
+ * pa_query_leap_counts writes out[3 s .. 3 s + 2] = (matched docs, leaps, 1 if the segment's counts are unavailable:
+ * a neighbour search of the fused count gave up) for every bound segment s of the last scan (synchronises `stream`). */
+int32_t pa_query_leap_leaf(const pa_query* q);
+int pa_query_leap_counts(const pa_query* q, int64_t* out, void* stream);
 
 /* Group-key layout. Direct (hashed = 0): key = sum_j id_j * prod_{k<j} cardinality_k. Hashed (hashed = 1, chosen when
  * a group-by column is raw or the product of cardinalities is too large to address): the key packs component j

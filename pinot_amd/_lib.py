@@ -35,6 +35,7 @@ PA_QF_NO_LANE_ACC = 1 << 26
 PA_QF_NO_LANE_HIST = 1 << 27
 PA_QF_LAZY_POST = 1 << 28
 PA_QF_NO_DENSE_GROUP = 1 << 29
+PA_QF_FILTER_STATS = 1 << 30
 PA_BIT_AND, PA_BIT_OR, PA_BIT_NOT = -1, -2, -3
 PA_BIT_PROG_MAX = 64
 PA_ACC_COUNT_U64, PA_ACC_SUM_I64, PA_ACC_SUM_F64, PA_ACC_MIN_I64, PA_ACC_MAX_I64, PA_ACC_HLL_U8, \
@@ -52,7 +53,7 @@ EXPORTED = [
     "pa_query_fetch", "pa_query_matched_docs", "pa_query_key_layout", "pa_query_limit_trimming",
     "pa_query_num_groups_limit_reached", "pa_query_stats", "pa_query_leaf_bitmap_words", "pa_query_leaf_bitmaps",
     "pa_bitmap_counts_scratch_bytes", "pa_bitmap_counts", "pa_query_filter_counts",
-    "pa_query_plan", "pa_query_column_staged", "pa_query_destroy",
+    "pa_query_plan", "pa_query_column_staged", "pa_query_leap_leaf", "pa_query_leap_counts", "pa_query_destroy",
 ]
 
 
@@ -144,6 +145,8 @@ def _declare(lib):
         "pa_query_filter_counts": (ctypes.c_int, [vp, i32, vp, vp, vp, vp, vp]),
         "pa_query_plan": (ctypes.c_int, [vp] + [ctypes.POINTER(i32)] * 7),
         "pa_query_column_staged": (i32, [vp, i32]),
+        "pa_query_leap_leaf": (i32, [vp]),
+        "pa_query_leap_counts": (ctypes.c_int, [vp, vp, vp]),
         "pa_query_destroy": (None, [vp]),
     }
     for name, (res, args) in sig.items():

@@ -553,6 +553,8 @@ struct pa_query {
   int limit_grid = 0;
   DevBuf lim_keys, lim_pos, lim_hist, lim_sel, lim_thresh;
   DevBuf stat_buf;  // pa_query_filter_counts: leaf bitmaps, scratch, counts, jobs (grown on demand)
+  DevBuf leap_buf;  // PA_QF_FILTER_STATS fused into the scan: per segment (matched docs, leaps, gave up)
+  int leap_leaf = -1;  // the eager leaf (spec order) when the scan counts the leaps
   std::vector<LmSegPlan> hplans;
   std::vector<GdSegPlan> gdplans;  // STRAT_GDENSE: per-segment parameter tables
   DevBuf dgdplans;
@@ -575,6 +577,7 @@ struct pa_query {
     dev_free(lim_sel);
     dev_free(lim_thresh);
     dev_free(stat_buf);
+    dev_free(leap_buf);
     dev_free(lim_admit);
     dev_free(dgdplans);
     if (host_acc) (void)hipHostFree(host_acc);
@@ -634,6 +637,7 @@ int upload_owned(pa_query* q, const void* host, size_t bytes, void** dev) {
 struct Prep {
   std::vector<char> clause_mv;
   double post_density = 1.0;
+  double first_clause_sel = 1.0;  // estimated selectivity of the first (eager) clause
   bool has_filter = false;
   bool dense = true;
   bool stage_all = false, stage_post = false;
@@ -704,6 +708,7 @@ int plan_filter(pa_query* q, Prep& P) {
          (no_lazy || eager_clauses == 0 || density > kLazyDensity))
     density *= csel[order[eager_clauses++]];
   P.post_density = density;
+  P.first_clause_sel = cnf.empty() ? 1.0 : csel[order[0]];
   for (size_t c = eager_clauses; c < cnf.size(); ++c) P.post_density *= csel[order[c]];
   q->literals.clear();
   q->clause_end.clear();
@@ -1172,6 +1177,7 @@ int build_segments(pa_query* q, Prep& P) {
     DevSeg& d = q->hsegs[si];
     std::memset(&d, 0, sizeof(d));
     d.num_docs = seg->num_docs;
+    d.index = si;
     q->num_docs += (uint64_t)seg->num_docs;
     for (int sl = 0; sl < nslots; ++sl) {
       auto it = seg->cols.find(q->slot_cols[sl]);
@@ -2386,6 +2392,31 @@ int pa_query_bind_value_remap(pa_query* q, int32_t index, int32_t agg, const int
   return PA_OK;
 }
 
+// PA_QF_FILTER_STATS: the scan counts the leap-frog statistics itself (leap_tile) when the filter is an AND of two
+// single-value leaves whose first (eager) clause is sparse — each of its docs costs two short neighbour searches — and
+// the scan is one pass (the partitioned and numGroupsLimit plans run the tile loop more than once).
+static int plan_leaps(pa_query* q, const Prep& P) {
+  const pa_query_spec& s = q->spec;
+  q->leap_leaf = -1;
+  q->hq.leap_mode = 0;
+  q->hq.leap_out = nullptr;
+  if (!(s.flags & PA_QF_FILTER_STATS) || q->literals.size() != 2 || q->num_eager != 1) return PA_OK;
+  if (!q->clause_end[0] || !q->clause_end[1] || q->literals[0].neg || q->literals[1].neg) return PA_OK;
+  for (const Literal& lit : q->literals) {
+    const int k = s.leaves[lit.leaf].kind;
+    if (k == PA_LEAF_MV_DICT_RANGE || k == PA_LEAF_MV_DICT_SET) return PA_OK;
+  }
+  if (q->partitioned || q->limit_mode || q->limit_walk || is_gdense(q->strategy)) return PA_OK;
+  if (P.first_clause_sel > 1.0 / 256.0) return PA_OK;
+  int rc = dev_alloc(q->leap_buf, (size_t)std::max(1, q->nseg) * 3 * sizeof(unsigned long long));
+  if (rc) return rc;
+  PA_HIP(hipMemset(q->leap_buf.p, 0, q->leap_buf.n));
+  q->hq.leap_mode = 1;
+  q->hq.leap_out = (unsigned long long*)q->leap_buf.p;
+  q->leap_leaf = q->literals[0].leaf;
+  return PA_OK;
+}
+
 int pa_query_prepare(pa_query* q) {
   if (!q) return fail(PA_EINVAL, "null query");
   if (q->prepared) return PA_OK;
@@ -2420,6 +2451,8 @@ int pa_query_prepare(pa_query* q) {
   q->plan_ring = plan.ring;
   q->plan_wg = plan.wg_per_cu;
   fill_devquery(q, P, plan, total_tiles);
+  rc = plan_leaps(q, P);
+  if (rc) return rc;
 
   // grid: persistent waves, enough workgroups to cover the CUs several times over
   int dev = 0, cus = 256;
@@ -2490,6 +2523,7 @@ int pa_query_reset(pa_query* q, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   // one memset of the whole accumulator block, then the MIN/MAX sections to their identities
   PA_HIP(hipMemsetAsync(q->external_acc ? q->external_acc : q->acc.p, 0, q->acc.n, st));
+  if (q->hq.leap_mode) PA_HIP(hipMemsetAsync(q->leap_buf.p, 0, q->leap_buf.n, st));
   for (const Section& sc : q->sections) {
     if (sc.kind == PA_ACC_MIN_I64 || sc.kind == PA_ACC_KEYS_I64) PA_HIP(launch_fill_i64((int64_t*)sc.ptr, sc.n, INT64_MAX, st));
     else if (sc.kind == PA_ACC_MAX_I64) PA_HIP(launch_fill_i64((int64_t*)sc.ptr, sc.n, INT64_MIN, st));
@@ -3079,6 +3113,18 @@ int32_t pa_query_column_staged(const pa_query* q, int32_t column_id) {
 }
 
 int64_t pa_query_matched_docs(const pa_query* q) { return q && q->prepared ? q->last_matched : -1; }
+
+int32_t pa_query_leap_leaf(const pa_query* q) { return q && q->prepared ? q->leap_leaf : -1; }
+
+int pa_query_leap_counts(const pa_query* q, int64_t* out, void* stream) {
+  if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
+  if (q->leap_leaf < 0) return fail(PA_EINVAL, "the scan does not count the filter statistics (pa_query_leap_leaf)");
+  if (!out) return fail(PA_EINVAL, "null output");
+  hipStream_t st = (hipStream_t)stream;
+  PA_HIP(hipMemcpyAsync(out, q->leap_buf.p, (size_t)q->nseg * 3 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  PA_HIP(hipStreamSynchronize(st));
+  return PA_OK;
+}
 
 int32_t pa_query_limit_trimming(const pa_query* q) {
   return q && q->prepared ? (q->limit_mode ? 1 : (q->limit_walk ? 2 : 0)) : -1;

@@ -797,6 +797,16 @@ __device__ __forceinline__ uint32_t leaf_bits(const DevLeaf& L, const uint32_t* 
   return L.negate ? ~bits : bits;
 }
 
+// A wave-uniform pointer the compiler may hold in VGPRs: readfirstlane puts it in SGPRs, so the descriptor fields
+// behind it are scalar loads (vector loads of descriptors need vmcnt waits, which also wait for the in-flight DMA ring).
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return (T*)(((uint64_t)hi << 32) | lo);
+}
+
 // One literal on one doc, read straight from HBM: the lazy clauses, evaluated only on docs every eager clause
 // matched (the leap-frog evaluation of the reference's AndDocIdIterator: later iterators only advance to candidate
 // docs). DICT_RANGE bounds are stored MSB-aligned for leaf_bits; lo = lo' >> (32-nb), span = (hi' + 1) >> (32-nb).
@@ -833,18 +843,83 @@ __device__ __forceinline__ bool leaf_match_doc(const DevLeaf& L, int64_t doc) {
   return m != (L.negate != 0);
 }
 
-// The rare part of a tile (some doc survived the eager clauses): lazy clauses per surviving doc, then aggregation.
-// Returns the docs that matched.
-// LM: doc of bit i of lane l = 32l + i (lane-major tile), else 64i + l.
-// A wave-uniform pointer the compiler may hold in VGPRs: readfirstlane puts it in SGPRs, so the descriptor fields
-// behind it are scalar loads (vector loads of descriptors need vmcnt waits, which also wait for the in-flight DMA ring).
-template <class T>
-__device__ __forceinline__ T* uniform_ptr(T* p) {
-  const uint64_t v = (uint64_t)p;
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-  return (T*)(((uint64_t)hi << 32) | lo);
+// ---------------------------------------------------------------- fused execution statistics (DevQuery::leap_mode)
+// The filter is an AND of two single-value scan leaves: literal 0 (eager, E) and literal 1 (lazy, Z). The reference's
+// AndDocIdIterator leap-frogs them with A = Z and B = E (filter_stats._cost_next: numEntriesScannedInFilter = num_docs +
+// |A & B| + leaps). Label every doc A-only (1), B-only (2), both (3); in doc order a leap starts at each step
+// both -> A-only, start -> A-only, A-only -> B-only and B-only -> A-only between consecutive labelled docs
+// (pa_kernels.hip word_leaps). Every such step but the first has an E (= B) doc at one end, so
+//   leaps = [the segment's first labelled doc is A-only]
+//         + sum over E docs e of ([succ(e) is A-only] + [e is B-only and pred(e) is A-only]),
+// with pred / succ the nearest labelled docs before / after e. The scan knows e's label (the lazy clause runs on it);
+// pred and succ come from a wave-wide search over 64 docs per step, both leaves read straight from HBM, which stops at
+// the first labelled doc (so never past the neighbouring E doc). The planner enables this only for a sparse E; a
+// search that gives up (kLeapSearchSteps) flags the segment, whose counts the host then takes from leaf bitmaps.
+constexpr int kLeapSearchSteps = 64;  // 4096 docs
+
+// Label of the nearest labelled doc at or beyond `from` in direction dir (+1 / -1) inside the segment: 1, 2, 3; 0 if
+// the segment ends first; 4 if the search gave up.
+__device__ __noinline__ uint32_t leap_search(const DevSeg* seg_in, int64_t from, int dir, int lane) {
+  const DevSeg* __restrict__ seg = uniform_ptr(seg_in);
+  const int64_t n = seg->num_docs;
+  for (int k = 0; k < kLeapSearchSteps; ++k) {
+    const int64_t d = from + (int64_t)dir * (int64_t)(kWave * k + lane);
+    const bool in = d >= 0 && d < n;
+    uint32_t lbl = 0u;
+    if (in) lbl = (leaf_match_doc(seg->leaves[1], d) ? 1u : 0u) | (leaf_match_doc(seg->leaves[0], d) ? 2u : 0u);
+    const uint64_t hit = __ballot(lbl != 0u);
+    if (hit) return (uint32_t)__builtin_amdgcn_readlane((int)lbl, __builtin_ctzll(hit));  // lane order = distance
+    if (__ballot(in) != ~0ull) return 0u;
+  }
+  return 4u;
 }
+
+// One segment's counters (lane 0 adds them; nothing when all are zero).
+__device__ __forceinline__ void leap_add(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, uint32_t matched,
+                                         uint32_t leaps, uint32_t gave_up, int lane) {
+  if (lane == 0 && (matched | leaps | gave_up)) {
+    unsigned long long* o = q->leap_out + 3 * (int64_t)seg->index;
+    if (matched) atomicAdd(o, (unsigned long long)matched);
+    if (leaps) atomicAdd(o + 1, (unsigned long long)leaps);
+    if (gave_up) atomicOr(o + 2, 1ull);
+  }
+}
+
+// The E docs of one tile (e: eager clause bits, f: those that also matched the lazy clause), LM: doc of bit i of lane
+// l = 32 l + i, else 64 i + l.
+template <int LM>
+__device__ __noinline__ void leap_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int64_t doc_base,
+                                       uint32_t e, uint32_t f, int lane) {
+  uint32_t leaps = 0u, gave_up = 0u;
+  for (;;) {
+    const uint64_t any = __ballot(e != 0u);
+    if (any == 0) break;
+    const int l = __builtin_ctzll(any);
+    const int i = __builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)e, l));
+    const bool both = (((uint32_t)__builtin_amdgcn_readlane((int)f, l) >> i) & 1u) != 0u;
+    if (lane == l) e &= e - 1u;
+    const int64_t doc = doc_base + (LM ? 32 * l + i : kWave * i + l);
+    const uint32_t succ = leap_search(seg, doc + 1, 1, lane);
+    gave_up |= succ == 4u;
+    leaps += succ == 1u;
+    if (!both) {
+      const uint32_t pred = leap_search(seg, doc - 1, -1, lane);
+      gave_up |= pred == 4u;
+      leaps += pred == 1u;
+    }
+  }
+  uint32_t matched = (uint32_t)__builtin_popcount(f);
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) matched += (uint32_t)__shfl_xor((int)matched, o, kWave);
+  leap_add(q, seg, matched, leaps, gave_up, lane);
+}
+
+// The segment-start term: by the wave that takes the segment's first tile.
+__device__ __noinline__ void leap_segment_start(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int lane) {
+  const uint32_t first = leap_search(seg, 0, 1, lane);
+  leap_add(q, seg, 0u, first == 1u ? 1u : 0u, first == 4u ? 1u : 0u, lane);
+}
+
 
 // ---------------------------------------------------------------- partitioned aggregation: count + emit passes
 // LDS bin state of the emit pass, per partition (V partitions first, then H): records in the bin (may pass the bin
@@ -2064,6 +2139,9 @@ __device__ __forceinline__ void lane_acc_flush(const DevQuery* __restrict__ q, c
   }
 }
 
+// The rare part of a tile (some doc survived the eager clauses): lazy clauses per surviving doc, then aggregation.
+// Returns the docs that matched.
+// LM: doc of bit i of lane l = 32l + i (lane-major tile), else 64i + l.
 template <int STRAT, int STEPS, int LM>
 __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg_in,
                                                 const uint32_t* img, int64_t doc_base, uint32_t m, int lane,
@@ -2076,6 +2154,7 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
   const int nleaves = q->num_leaves;
   const int neager = q->num_eager;
   if (neager < nleaves) {
+    const uint32_t eager = m;
     // lazy clauses: only the docs the eager clauses kept, one step at a time, straight from HBM
     for (int i = 0; i < STEPS; ++i) {
       const uint32_t bit = 1u << i;
@@ -2093,6 +2172,8 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
       }
       if (!ok) m &= ~bit;
     }
+    if constexpr (STRAT != STRAT_PCOUNT && !is_pemit(STRAT))
+      if (q->leap_mode) leap_tile<LM>(q, seg, doc_base, eager, m, lane);
     if (__ballot(m != 0) == 0) return 0;
   }
   const uint32_t scanned = m;  // numDocsScanned counts every doc the filter kept, admitted or not
@@ -2143,6 +2224,8 @@ __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, con
                                              int64_t wt, const uint32_t* img, int lane, const Acc<STRAT>& acc,
                                              uint32_t& matched, LaneAcc& la) {
   const int64_t doc_base = wt * (STEPS * kWave);
+  if constexpr (STRAT != STRAT_PCOUNT && !is_pemit(STRAT))
+    if (doc_base == 0 && q->leap_mode) leap_segment_start(q, seg, lane);
   // docs of this tile owned by the lane: 64*i + lane < rem
   const int64_t rem = (int64_t)seg->num_docs - doc_base;
   // bit i <=> step i holds a doc of this segment (only the low STEPS bits: a negated leaf sets the others, and the
@@ -2270,6 +2353,8 @@ __device__ __forceinline__ void process_tile_lm(const DevQuery* __restrict__ q, 
                                                 uint32_t pp, int64_t wt, const uint32_t* img, uint32_t img_lds,
                                                 int lane, const Acc<STRAT>& acc, uint32_t& matched, LaneAcc& la) {
   const int64_t doc_base = wt * kWTileDocs;
+  if constexpr (STRAT != STRAT_PCOUNT && !is_pemit(STRAT))
+    if (doc_base == 0 && q->leap_mode) leap_segment_start(q, seg, lane);
   const int64_t rem = (int64_t)(int32_t)rl(pp, 2) - doc_base;
   uint32_t valid = 0xffffffffu;
   if (rem < kWTileDocs) {

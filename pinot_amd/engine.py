@@ -470,14 +470,17 @@ class GpuQueryExecutor:
                 L.check(L.lib().pa_query_reset(self.handle, stream), "pa_query_reset")
             return
         L.check(L.lib().pa_query_execute(self.handle, stream), "pa_query_execute")
+        self._scanned = True
 
     def reset(self, stream=None):
         L.check(L.lib().pa_query_reset(self.handle, stream), "pa_query_reset")
+        self._scanned = False
 
     def scan(self, stream=None):
         if not self.segs or self.match_none:
             return
         L.check(L.lib().pa_query_scan(self.handle, stream), "pa_query_scan")
+        self._scanned = True
 
     def sections(self):
         """[(kind, device_ptr, num_elements)] accumulator sections (for the cross-GPU reduce)."""
@@ -590,6 +593,20 @@ class GpuQueryExecutor:
         torch.cuda.synchronize(dev)  # (device-wide: covers `stream`)
         w = buf.cpu().numpy().view(np.uint8).reshape(nl, words * 4)
         return np.unpackbits(w, axis=1, bitorder="little")[:, :n].astype(bool)
+
+    def fused_leap_counts(self, stream=None):
+        """(E leaf, Z leaf, int64[segments, 3]) when the last scan counted the execution statistics of its two-leaf AND
+        itself (flags PA_QF_FILTER_STATS, pa_query_leap_counts: per segment matched docs, leaps of AndDocIdIterator(A = Z,
+        B = E), gave-up flag), else None. Synchronises `stream`."""
+        lib = L.lib()
+        if self.handle is None or not self.segs or not getattr(self, "_scanned", False):
+            return None
+        e = int(lib.pa_query_leap_leaf(self.handle))
+        if e < 0:
+            return None
+        out = np.zeros((len(self.segs), 3), dtype=np.int64)
+        L.check(lib.pa_query_leap_counts(self.handle, out.ctypes.data, stream), "pa_query_leap_counts")
+        return e, 1 - e, out
 
     def execution_stats(self, stream=None, docs_total=None):
         """(numEntriesScannedInFilter, numEntriesScannedPostFilter) of this server's segments: the reference's

@@ -580,7 +580,13 @@ class _Terms:
         return self
 
     def value(self, counts):
-        return self.const + sum(int(counts[r, f]) * c for r, f, c in self.terms)
+        v = self.const
+        for r, f, c in self.terms:
+            x = int(counts[r, f])
+            if x < 0:
+                raise RuntimeError("internal: count field %d of request %d not computed" % (f, r))
+            v += x * c
+        return v
 
 
 def _cost_next(op, seg, si, reqs):
@@ -732,9 +738,41 @@ def device_counts(executor, segments, reqs, stream=None):
     return out
 
 
+def fused_counts(reqs, fused, fallback):
+    """counts_fn rows from the counts the scan took itself (GpuQueryExecutor.fused_leap_counts: E leaf, Z leaf, per
+    segment matched docs / leaps / gave-up): the AND request (A = [Z], B = [E]) gets popcount(A & B) = the segment's
+    matched docs and the leaps, the post-filter request (the whole filter, no B) its popcount = the matched docs. Other
+    requests, and segments whose fused count gave up, go to fallback(reqs) (device_counts). Unknown fields are -1."""
+    e, z, arr = fused
+    out = np.full((len(reqs), 4), -1, dtype=np.int64)
+    rest = {}
+    for key, r in reqs.items():
+        si, a, b = key
+        row = None
+        if not arr[si, 2]:
+            if a == (z,) and b == (e,):
+                row = (-1, -1, arr[si, 0], arr[si, 1])
+            elif not b and a in ((z, e, L.PA_BIT_AND), (e, z, L.PA_BIT_AND)):
+                row = (arr[si, 0], -1, -1, -1)
+        if row is None:
+            rest[key] = len(rest)
+        else:
+            out[r] = row
+    if rest:
+        sub = fallback(rest)
+        for key, r2 in rest.items():
+            out[reqs[key]] = sub[r2]
+    return out
+
+
 def server_stats_device(query, segments, executor, stream=None, docs_total=None):
     """server_stats with the counts computed on the GPU (device_counts); same results. docs_total: the executor's
-    numDocsScanned of its last scan (server_stats_closed_form: constant-cost filters then need no GPU pass)."""
-    return server_stats_closed_form(query, segments, lambda reqs: device_counts(executor, segments, reqs, stream),
-                                    lambda si: executor.leaf_bitmaps(si, stream),
+    numDocsScanned of its last scan (server_stats_closed_form: constant-cost filters then need no GPU pass). When the
+    scan counted the statistics of its two-leaf AND itself (PA_QF_FILTER_STATS: fused_counts), no extra GPU pass runs
+    for the segments it covered."""
+    def counts(reqs):
+        fz = executor.fused_leap_counts(stream) if hasattr(executor, "fused_leap_counts") else None
+        dev = lambda rq: device_counts(executor, segments, rq, stream)
+        return dev(reqs) if fz is None else fused_counts(reqs, fz, dev)
+    return server_stats_closed_form(query, segments, counts, lambda si: executor.leaf_bitmaps(si, stream),
                                     getattr(executor, "leaf_params", None), docs_total)

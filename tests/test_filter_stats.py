@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
+from pinot_amd import _lib as L
 from pinot_amd import filter_stats as FS
 from pinot_amd import parse_sql
 from pinot_amd import predicate as P
@@ -339,3 +340,22 @@ def test_constant_cost_filters_need_no_counts(where):
         want = FS.server_stats(q, segs, lambda si: masks[si])
         docs = sum(int(FS.filter_mask(q.filter, s, masks[i]).sum()) for i, s in enumerate(segs))
         assert FS.server_stats_closed_form(q, segs, boom, boom, docs_total=docs) == want, sql
+
+
+def test_fused_counts_serve_only_their_requests():
+    """filter_stats.fused_counts: the AND request (A = [Z], B = [E]) and the whole-filter popcount come from the scan's
+    per-segment counts; other requests and gave-up segments from the fallback."""
+    AND = L.PA_BIT_AND
+    arr = np.array([[10, 4, 0], [3, 1, 1]], dtype=np.int64)
+    reqs = {(0, (1,), (0,)): 0, (0, (1, 0, AND), ()): 1, (1, (1,), (0,)): 2, (0, (0,), (1,)): 3}
+    asked = []
+
+    def fallback(rest):
+        asked.append(sorted(rest))
+        return np.array([[100 + r, 0, 0, 0] for r in range(len(rest))], dtype=np.int64)
+
+    out = FS.fused_counts(reqs, (0, 1, arr), fallback)
+    assert out[0].tolist() == [-1, -1, 10, 4]
+    assert out[1].tolist() == [10, -1, -1, -1]
+    assert asked == [sorted([(1, (1,), (0,)), (0, (0,), (1,))])]
+    assert out[2][0] >= 100 and out[3][0] >= 100

@@ -125,3 +125,55 @@ def test_merged_range_is_one_scan_on_the_gpu():
     finally:
         for g in gs:
             g.close()
+
+
+def _sparse_segment(seed, n, e_docs):
+    """z: 16 values (an A leaf matching ~1/16 .. 1/4 of the docs), y: 4096 values (a sparse A leaf), e: 65536 values,
+    with value 7 placed at e_docs (a sparse E leaf: segment ends, tile boundaries) plus a few random docs."""
+    rng = np.random.default_rng(seed)
+    e = rng.integers(8, 65536, n).astype(np.int32)
+    e[[d for d in e_docs if d < n]] = 7
+    e[rng.integers(0, n, 6)] = 7
+    data = {"z": rng.integers(0, 16, n).astype(np.int32), "y": rng.integers(0, 4096, n).astype(np.int32), "e": e,
+            "m": rng.integers(0, 1000, n).astype(np.int32)}
+    return create_segment("sp%d" % seed, data, {k: "INT" for k in data})
+
+
+def test_fused_execution_stats_match_the_replay(monkeypatch):
+    """PA_QF_FILTER_STATS: the scan counts the leaps of `z-leaf AND e-leaf` itself (E = the sparse eager e leaf, found
+    by neighbour searches from each E doc); the statistics equal the host replay, and no leaf-bitmap pass runs when
+    every search finished. A sparse A leaf (y) makes searches give up: those segments fall back to the bitmap counts,
+    with the same result. With E first in the reference's AND order the fused counts do not apply (fallback)."""
+    n0 = 300_007
+    segs = [_sparse_segment(1, n0, [0, 1, 2047, 2048, 4095, n0 - 1]), _sparse_segment(2, 70_000, [69_999]),
+            _sparse_segment(3, 1025, [512]), _sparse_segment(4, 5000, [])]
+    gs = [GpuSegment(s) for s in segs]
+    try:
+        cases = [("z < 2 AND e = 7", True), ("z BETWEEN 3 AND 6 AND e IN (7, 11)", True),
+                 ("z = 5 AND e = 7", True), ("y = 17 AND e = 7", False), ("e = 7 AND z < 2", False)]
+        for where, fused_only in cases:
+            for sql in ("SELECT COUNT(*) FROM t WHERE " + where, "SELECT z, SUM(m) FROM t WHERE %s GROUP BY z" % where):
+                q = parse_sql(sql)
+                ex = GpuQueryExecutor(q, gs, flags=L.PA_QF_FILTER_STATS)
+                try:
+                    ex.execute()
+                    fz = ex.fused_leap_counts()
+                    assert fz is not None, sql  # (a sparse E: the scan counted)
+                    if fused_only:
+                        called = []
+                        orig = FS.device_counts
+                        monkeypatch.setattr(FS, "device_counts", lambda *a, **k: called.append(1) or orig(*a, **k))
+                        got = ex.execution_stats()
+                        monkeypatch.setattr(FS, "device_counts", orig)
+                        assert not called, sql
+                    else:
+                        got = ex.execution_stats()
+                    want = FS.server_stats(ex.query, ex.segs, lambda si: ex.leaf_bitmaps(si))
+                    res = ex.fetch()
+                    assert fz[2][:, 0].sum() == res.num_docs_scanned
+                finally:
+                    ex.close()
+                assert got == want, sql
+    finally:
+        for g in gs:
+            g.close()

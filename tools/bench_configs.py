@@ -232,6 +232,8 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
         if sql.startswith("@"):
             sql = _bench().secondary_query(int(sql[1:]))
         vs = variants or (((0, ""),) if no_stepmajor else ((0, ""), (L.PA_QF_NO_LANE_MAJOR, "_stepmajor")))
+        def extra_flags(vs_, tag_):
+            return dict((t_, f_) for f_, t_ in vs_)[tag_]
         for extra, tag in vs:
             ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags | extra)
             ex.execute(sp)
@@ -268,23 +270,41 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
             if cpu_sample:
                 extra["cpu_baseline"] = cpu_port_baseline(sql, host)
             if exec_stats:
-                # numEntriesScannedInFilter / PostFilter of every segment (leaf bitmaps + counts on the GPU, closed
-                # forms on the host: filter_stats.server_stats_device); the first call warms the allocator
+                # numEntriesScannedInFilter / PostFilter of every segment: (a) the plain executor (leaf bitmaps +
+                # counts on the GPU when the closed forms need counts, filter_stats.server_stats_device); (b) a
+                # PA_QF_FILTER_STATS executor, whose scan counts the two-leaf AND's leaps itself (fused_counts): its
+                # scan time and the host closed form after it, against the plain scan (ms)
                 from pinot_amd import filter_stats as FS
-                ex.execution_stats(sp)
-                dev = []
-
-                def counts(reqs):
-                    t = time.perf_counter()
-                    r = FS.device_counts(ex, ex.segs, reqs, sp)
-                    dev.append((time.perf_counter() - t) * 1e3)
-                    return r
+                docs_total = int(L.lib().pa_query_matched_docs(ex.handle))
+                ex.execution_stats(sp, docs_total)  # (warms the allocator)
                 t3 = time.perf_counter()
-                in_f, post = FS.server_stats_closed_form(ex.query, ex.segs, counts, lambda si: ex.leaf_bitmaps(si, sp),
-                                                         ex.leaf_params)
-                extra["exec_stats"] = {"ms": round((time.perf_counter() - t3) * 1e3, 3), "scan_ms": round(ms, 4),
-                                       "device_counts_ms": round(sum(dev), 3), "entries_in_filter": in_f,
-                                       "entries_post_filter": post}
+                in_f, post = ex.execution_stats(sp, docs_total)
+                plain_ms = (time.perf_counter() - t3) * 1e3
+                fx = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags | extra_flags(vs, tag) | L.PA_QF_FILTER_STATS)
+                fx.execute(sp)
+                torch.cuda.synchronize()
+                fx.reset(sp)
+                a.record(stream)
+                for _ in range(reps):
+                    fx.scan(sp)
+                b.record(stream)
+                torch.cuda.synchronize()
+                fused_scan_ms = a.elapsed_time(b) / reps
+                fx.execute(sp)
+                fx.fetch_arrays(sp, pooled=True)  # (numDocsScanned of this scan)
+                fdocs = int(L.lib().pa_query_matched_docs(fx.handle))
+                fx.execution_stats(sp, fdocs)
+                t4 = time.perf_counter()
+                f_in, f_post = fx.execution_stats(sp, fdocs)
+                fused_host_ms = (time.perf_counter() - t4) * 1e3
+                fused = int(L.lib().pa_query_leap_leaf(fx.handle)) >= 0
+                fx.close()
+                assert (f_in, f_post) == (in_f, post), ((f_in, f_post), (in_f, post))
+                extra["exec_stats"] = {"scan_ms": round(ms, 4), "plain_stats_ms": round(plain_ms, 3),
+                                       "fused": fused, "fused_scan_ms": round(fused_scan_ms, 4),
+                                       "fused_host_ms": round(fused_host_ms, 3),
+                                       "overhead_vs_scan": round((fused_scan_ms + fused_host_ms) / ms - 1.0, 4),
+                                       "entries_in_filter": in_f, "entries_post_filter": post}
             print(json.dumps(dict({"workload": workload, "plan_name": name + tag, "kernel_ms": round(ms, 4),
                               "rows_per_s": st["num_docs"] / (ms * 1e-3), "staged_bytes": st["staged_bytes"],
                               "staged_GBps": st["staged_bytes"] / (ms * 1e-3) / 1e9, "fetch_ms": round(fetch_ms, 2), "e2e_ms": round(e2e_ms, 2),
