@@ -343,6 +343,19 @@ int pa_query_filter_counts(pa_query* q, int32_t num_requests, const int32_t* seg
 int32_t pa_query_leap_leaf(const pa_query* q);
 int pa_query_leap_counts(const pa_query* q, int64_t* out, void* stream);
 
+/* Cross-GPU merge of hashed key spaces (parallel.merge_hashed_sections around one all-to-all). A row is one slot of
+ * every per-key accumulator section (the numDocsScanned counters excluded) in section order: pa_query_row_bytes(q)
+ * bytes; the packed key is one of its 8-byte units. pa_query_pack_rows writes the occupied slots (count > 0) as rows
+ * grouped by the rank owning their key (a multiplicative hash of the packed key modulo `world`): counts[r] rows for
+ * rank r, ranks in order, at device_rows (or, with device_rows NULL, only the counts). pa_query_merge_rows resets the
+ * block and merges num_rows rows (from any rank holding the same key space) into it by packed key: SUM for counts
+ * and sums, MIN, MAX, byte max for HLL registers and DISTINCTCOUNT presence (GroupByCombineOperator's merge);
+ * *groups = the groups now held, *overflow = rows that found no free slot. Both synchronise `stream`. */
+int64_t pa_query_row_bytes(const pa_query* q);
+int pa_query_pack_rows(pa_query* q, int32_t world, void* device_rows, int64_t* counts, void* stream);
+int pa_query_merge_rows(pa_query* q, const void* device_rows, int64_t num_rows, int64_t* groups, int64_t* overflow,
+                        void* stream);
+
 /* Group-key layout. Direct (hashed = 0): key = sum_j id_j * prod_{k<j} cardinality_k. Hashed (hashed = 1, chosen when
  * a group-by column is raw or the product of cardinalities is too large to address): the key packs component j
  * (a table-wide key id, or the raw value's bits: 32 for INT/FLOAT, 64 for LONG/DOUBLE) at bit shifts[j]. Keys returned

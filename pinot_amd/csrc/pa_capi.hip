@@ -553,6 +553,7 @@ struct pa_query {
   int limit_grid = 0;
   DevBuf lim_keys, lim_pos, lim_hist, lim_sel, lim_thresh;
   DevBuf stat_buf;  // pa_query_filter_counts: leaf bitmaps, scratch, counts, jobs (grown on demand)
+  DevBuf merge_buf;  // pa_query_pack_rows / pa_query_merge_rows: row -> slot map and counters (grown on demand)
   DevBuf leap_buf;  // PA_QF_FILTER_STATS fused into the scan: per segment (matched docs, leaps, gave up)
   int leap_leaf = -1;  // the eager leaf (spec order) when the scan counts the leaps
   std::vector<LmSegPlan> hplans;
@@ -578,6 +579,7 @@ struct pa_query {
     dev_free(lim_thresh);
     dev_free(stat_buf);
     dev_free(leap_buf);
+    dev_free(merge_buf);
     dev_free(lim_admit);
     dev_free(dgdplans);
     if (host_acc) (void)hipHostFree(host_acc);
@@ -3113,6 +3115,109 @@ int32_t pa_query_column_staged(const pa_query* q, int32_t column_id) {
 }
 
 int64_t pa_query_matched_docs(const pa_query* q) { return q && q->prepared ? q->last_matched : -1; }
+
+// ---------------------------------------------------------------- cross-GPU merge of hashed key spaces
+// The row layout of a hashed block: every per-key section (numDocsScanned counters excluded) in section order.
+static int row_desc(const pa_query* q, RowDesc& d) {
+  if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
+  if (!q->hashed || q->keys_section < 0) return fail(PA_EINVAL, "row merge needs a hashed key space");
+  std::memset(&d, 0, sizeof(d));
+  int64_t off = 0;
+  for (const Section& sc : q->sections) {
+    if (sc.kind == PA_ACC_DOCS_U64) continue;
+    if (d.nsec >= kMaxRowSecs) return fail(PA_EINVAL, "internal: too many sections for a row");
+    RowSec& r = d.sec[d.nsec++];
+    switch (sc.kind) {
+      case PA_ACC_SUM_F64: r.op = ROW_ADD_F64; break;
+      case PA_ACC_MIN_I64: r.op = ROW_MIN_I64; break;
+      case PA_ACC_MAX_I64: r.op = ROW_MAX_I64; break;
+      case PA_ACC_HLL_U8: case PA_ACC_PRESENCE_U8: r.op = ROW_MAX_U8; break;
+      case PA_ACC_KEYS_I64: r.op = ROW_KEY; break;
+      default: r.op = ROW_ADD_U64; break;  // COUNT, SUM (int64 and the exact lo / hi pair)
+    }
+    r.slot_bytes = sc.n / q->num_keys * (int64_t)section_es(sc.kind);
+    if (r.slot_bytes % 8) return fail(PA_EINVAL, "internal: row section not a multiple of 8 bytes");
+    r.row_off = off;
+    r.base = sc.ptr;
+    if (sc.kind == PA_ACC_KEYS_I64) {
+      d.key_off = off;
+      d.keys = (long long*)sc.ptr;
+    }
+    if (sc.kind == PA_ACC_COUNT_U64) d.count = (const unsigned long long*)sc.ptr;
+    off += r.slot_bytes;
+  }
+  d.row_bytes = off;
+  d.num_slots = q->num_keys;
+  d.ht_mask = q->ht_slots - 1;
+  return PA_OK;
+}
+
+static int merge_scratch(pa_query* q, size_t bytes) {
+  if (q->merge_buf.n >= bytes) return PA_OK;
+  dev_free(q->merge_buf);
+  return dev_alloc(q->merge_buf, bytes);
+}
+
+int64_t pa_query_row_bytes(const pa_query* q) {
+  RowDesc d;
+  const int rc = row_desc(q, d);
+  return rc ? rc : d.row_bytes;
+}
+
+int pa_query_pack_rows(pa_query* q, int32_t world, void* device_rows, int64_t* counts, void* stream) {
+  RowDesc d;
+  int rc = row_desc(q, d);
+  if (rc) return rc;
+  if (world < 1 || world > 1024 || !counts) return fail(PA_EINVAL, "pack rows: bad world size or null counts");
+  hipStream_t st = (hipStream_t)stream;
+  // scratch: counts[world], cursor[world], row_slot[num_slots]
+  rc = merge_scratch(q, (size_t)(2 * world + d.num_slots) * 8);
+  if (rc) return rc;
+  unsigned long long* cnt = (unsigned long long*)q->merge_buf.p;
+  unsigned long long* cur = cnt + world;
+  int64_t* row_slot = (int64_t*)(cur + world);
+  PA_HIP(hipMemsetAsync(cnt, 0, (size_t)world * 8, st));
+  PA_HIP(launch_pack_index(d, world, 0, cnt, nullptr, nullptr, st));
+  std::vector<unsigned long long> h(world);
+  PA_HIP(hipMemcpyAsync(h.data(), cnt, (size_t)world * 8, hipMemcpyDeviceToHost, st));
+  PA_HIP(hipStreamSynchronize(st));
+  int64_t total = 0;
+  std::vector<unsigned long long> start(world);
+  for (int r = 0; r < world; ++r) {
+    counts[r] = (int64_t)h[r];
+    start[r] = (unsigned long long)total;
+    total += (int64_t)h[r];
+  }
+  if (!device_rows || total == 0) return PA_OK;
+  PA_HIP(hipMemcpyAsync(cur, start.data(), (size_t)world * 8, hipMemcpyHostToDevice, st));
+  PA_HIP(launch_pack_index(d, world, 1, nullptr, cur, row_slot, st));
+  PA_HIP(launch_pack_copy(d, row_slot, total, (unsigned char*)device_rows, st));
+  PA_HIP(hipStreamSynchronize(st));
+  return PA_OK;
+}
+
+int pa_query_merge_rows(pa_query* q, const void* device_rows, int64_t num_rows, int64_t* groups, int64_t* overflow,
+                        void* stream) {
+  RowDesc d;
+  int rc = row_desc(q, d);
+  if (rc) return rc;
+  if (num_rows < 0 || (num_rows > 0 && !device_rows)) return fail(PA_EINVAL, "merge rows: bad rows");
+  hipStream_t st = (hipStream_t)stream;
+  rc = pa_query_reset(q, stream);
+  if (rc) return rc;
+  rc = merge_scratch(q, (size_t)(4 + std::max<int64_t>(num_rows, d.num_slots)) * 8);
+  if (rc) return rc;
+  unsigned long long* ctr = (unsigned long long*)q->merge_buf.p;
+  int64_t* row_slot = (int64_t*)(ctr + 4);
+  PA_HIP(hipMemsetAsync(ctr, 0, 32, st));
+  PA_HIP(launch_merge_rows(d, (const unsigned char*)device_rows, num_rows, row_slot, ctr, st));
+  unsigned long long h[4];
+  PA_HIP(hipMemcpyAsync(h, ctr, 32, hipMemcpyDeviceToHost, st));
+  PA_HIP(hipStreamSynchronize(st));
+  if (groups) *groups = (int64_t)h[0];
+  if (overflow) *overflow = (int64_t)h[1];
+  return PA_OK;
+}
 
 int32_t pa_query_leap_leaf(const pa_query* q) { return q && q->prepared ? q->leap_leaf : -1; }
 

@@ -101,6 +101,33 @@ hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G,
 // vk: the pass-C variant of the V stream (vk_code / kVkGeneric)
 hipError_t set_part_agg_lds_limit(int vk, int lds_bytes);
 hipError_t launch_part_agg(int vk, const DevQuery* q, const PartScratch& ps, int P, int lds_bytes, hipStream_t s);
+// Cross-GPU merge of hashed key spaces (pa_merge.hip): a row is every per-key section's elements of one slot
+enum RowOp : int32_t { ROW_ADD_U64 = 0, ROW_ADD_F64 = 1, ROW_MIN_I64 = 2, ROW_MAX_I64 = 3, ROW_MAX_U8 = 4, ROW_KEY = 5 };
+constexpr int kMaxRowSecs = PA_MAX_AGGS + 2;
+struct RowSec {
+  int32_t op;          // RowOp
+  int32_t pad;
+  int64_t slot_bytes;  // bytes of one slot in the section (a multiple of 8)
+  int64_t row_off;     // byte offset of the section inside a row
+  void* base;          // the section in the accumulator block
+};
+struct RowDesc {
+  int32_t nsec;
+  int32_t pad;
+  int64_t row_bytes;
+  int64_t num_slots;   // table slots incl. the reserved one (num_keys)
+  int64_t ht_mask;     // probing mask (slots - 2)
+  int64_t key_off;     // byte offset of the packed key inside a row
+  const unsigned long long* count;
+  long long* keys;
+  RowSec sec[kMaxRowSecs];
+};
+hipError_t launch_pack_index(const RowDesc& d, int world, int phase, unsigned long long* counts,
+                             unsigned long long* cursor, int64_t* row_slot, hipStream_t s);
+hipError_t launch_pack_copy(const RowDesc& d, const int64_t* row_slot, int64_t rows, unsigned char* out, hipStream_t s);
+// counters: [0] groups inserted, [1] rows that found no free slot, [2] reserved-slot flag
+hipError_t launch_merge_rows(const RowDesc& d, const unsigned char* rows, int64_t n, int64_t* row_slot,
+                             unsigned long long* counters, hipStream_t s);
 hipError_t set_scan_lds_limit(int strategy, int steps, int lm, int bytes);
 hipError_t scan_occupancy(int strategy, int steps, int lm, int lds_bytes, int* blocks_per_cu);
 hipError_t launch_scan(int strategy, int steps, int lm, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs,

@@ -5,6 +5,7 @@ accumulates it into the SAME table-wide key space; the GroupByCombineOperator / 
 partial aggregates across GPUs then becomes one collective per accumulator section over RCCL (xGMI):
 SUM for COUNT/SUM, MIN for MIN, MAX for MAX and for HLL registers (HyperLogLog.addAll == register max).
 """
+import ctypes
 import hashlib
 from dataclasses import dataclass, field
 
@@ -44,7 +45,6 @@ SECTION_IDENTITY = {
     L.PA_ACC_MAX_I64: -(1 << 63),
     L.PA_ACC_KEYS_I64: (1 << 63) - 1,  # the empty-slot marker
 }
-_SCATTER_REDUCE = {dist.ReduceOp.SUM: "sum", dist.ReduceOp.MIN: "amin", dist.ReduceOp.MAX: "amax"}
 
 
 def shard_segments(num_segments, rank, world_size):
@@ -66,7 +66,8 @@ def reduce_sections(views, dst=0, group=None, all_reduce=False):
 
 def key_owner(keys, world):
     """Rank that owns packed key `keys` in the cross-GPU merge of hashed key spaces: a multiplicative hash of the key,
-    its high bits taken modulo the world size (int64 tensor ops: products wrap, the arithmetic shift is masked)."""
+    its high bits taken modulo the world size (int64 tensor ops: products wrap, the arithmetic shift is masked). The
+    library's pack kernel computes the same function (pa_merge.hip owner_of)."""
     h = keys ^ (keys >> 31)
     h = h * -7046029254386353131  # 0x9E3779B97F4A7C15 as a signed int64
     return ((h >> 33) & 0x7FFFFFFF) % world
@@ -82,84 +83,81 @@ def row_layout_fingerprint(views, num_slots, extra=b""):
     return int.from_bytes(h.digest(), "little") & ((1 << 62) - 1)
 
 
-def merge_hashed_sections(views, num_slots, group=None, layout_extra=b""):
+def merge_hashed_sections(views, num_slots, group=None, layout_extra=b"", rows=None):
     """Device-side merge of hashed key spaces across ranks (GroupByCombineOperator semantics, value-keyed: a packed key
     means the same group values on every rank once parallel.table_layout agreed the dictionaries, but sits in a
     different slot of each rank's table). views: [(section kind, 1-D tensor)] of ONE rank's accumulator block, the
     per-key sections holding num_slots rows each (row width = elements / num_slots) plus the PA_ACC_DOCS_U64 counters.
 
-    The key space is split across ranks by a hash of the packed key (key_owner): every rank compacts its occupied slots
-    (count > 0) into byte rows, sends each row to the rank that owns its key (one all-to-all over the collective
-    backend: RCCL on GPUs, so no rank ever holds the whole union), and merges the rows it receives by packed key on its
-    own device — torch.unique over the keys and one scatter-reduce per section (SUM for counts/sums, MIN, MAX for
-    maxima, HLL registers and DISTINCTCOUNT presence). The merged share goes back into the block: slots [0, groups) in
-    ascending key order, every other slot empty, so the executor's own fetch returns this rank's share. The shares are
-    disjoint and together are the merged result: each rank's fetch is one partial DataTable of disjoint groups, which
-    the broker's reduce concatenates (numDocsScanned and the other counters stay per rank: the broker sums them).
+    The key space is split across ranks by a hash of the packed key: every rank packs its occupied slots (count > 0)
+    into byte rows grouped by the rank that owns their key, sends each row there (one all-to-all over the collective
+    backend: RCCL on GPUs, so no rank ever holds the whole union), and merges the rows it receives by packed key into
+    its own block. `rows` does the two local halves: rows.pack(world) -> (uint8 [m, row bytes] grouped by owner rank,
+    rows per owner) and rows.merge(received) -> (groups held, rows that found no free slot); HashedAccumulators passes
+    LibraryRows (the library's pack / merge kernels: pa_query_pack_rows / pa_query_merge_rows). The merged share is
+    this rank's block afterwards, so the executor's own fetch returns it. The shares are disjoint and together are the
+    merged result: each rank's fetch is one partial DataTable of disjoint groups, which the broker's reduce
+    concatenates (numDocsScanned and the other counters stay per rank: the broker sums them).
 
     Before any exchange the ranks agree on the row layout (row_layout_fingerprint, one all-reduce: mismatched widths
     would hand the all-to-all rows of different sizes), and after the merge on whether every share fit its table
     (tables sized from parallel.table_layout's agreed key bound hold twice the largest rank's keys, and a share is
     ~1/world of the union); every rank raises together otherwise. Returns this rank's merged group count."""
+    if rows is None:
+        raise L.PinotAmdError("merge_hashed_sections: no row operations (HashedAccumulators passes the library's)")
     kinds = [k for k, _ in views]
     if L.PA_ACC_KEYS_I64 not in kinds or L.PA_ACC_COUNT_U64 not in kinds:
         raise L.PinotAmdError("merge_hashed_sections: the block has no key or count section")
-    per_key = [(k, t) for k, t in views if k != L.PA_ACC_DOCS_U64]
-    count = dict(per_key)[L.PA_ACC_COUNT_U64]
-    dev = count.device
+    dev = dict(views)[L.PA_ACC_COUNT_U64].device
     check_same_key_space(row_layout_fingerprint(views, num_slots, layout_extra), dev, group=group,
                          what="hashed merge: ranks hold different accumulator row layouts or key spaces")
     world = dist.get_world_size(group)
-    occ = torch.nonzero(count.view(num_slots) > 0).flatten()
-    m = int(occ.numel())
-    # one byte row per occupied slot: every per-key section's row, concatenated
-    parts, layout = [], []
-    for k, t in per_key:
-        w = t.numel() // num_slots
-        rows = t.view(num_slots, w)[occ]
-        b = rows.contiguous().view(torch.uint8).view(m, -1) if m else torch.empty(0, w * t.element_size(),
-                                                                                  dtype=torch.uint8, device=dev)
-        layout.append((k, t.dtype, w, b.shape[1]))
-        parts.append(b)
-    local = torch.cat(parts, dim=1) if parts else torch.empty(m, 0, dtype=torch.uint8, device=dev)
-    rb = local.shape[1]
-    keys_local = dict(per_key)[L.PA_ACC_KEYS_I64].view(num_slots)[occ]
-    # rows grouped by owner rank, then one all-to-all of the row counts and one of the rows
-    owner = key_owner(keys_local, world)
-    order = torch.argsort(owner, stable=True)
-    local = local[order]
-    send_n = torch.bincount(owner, minlength=world).to(torch.int64)
+    local, sn = rows.pack(world)
+    send_n = torch.tensor(sn, dtype=torch.int64, device=dev)
     recv_n = torch.empty_like(send_n)
     dist.all_to_all_single(recv_n, send_n, group=group)
-    sn, rn = send_n.tolist(), recv_n.tolist()
-    rows = torch.empty(sum(rn), rb, dtype=torch.uint8, device=dev)
-    dist.all_to_all_single(rows, local.contiguous(), output_split_sizes=rn, input_split_sizes=sn, group=group)
-    # unpack per section, merge by packed key
-    cols, o = {}, 0
-    for k, dt, w, nb in layout:
-        cols[k] = rows[:, o:o + nb].contiguous().view(dt).view(-1, w)
-        o += nb
-    keys = cols[L.PA_ACC_KEYS_I64][:, 0]
-    uniq, inv = torch.unique(keys, sorted=True, return_inverse=True)
-    u = int(uniq.numel())
-    # every rank learns whether some share overflowed its table before any rank rewrites its block
-    flag = torch.tensor([u - num_slots], dtype=torch.int64, device=dev)
+    rn = recv_n.tolist()
+    received = torch.empty(sum(rn), local.shape[1], dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(received, local.contiguous(), output_split_sizes=rn, input_split_sizes=list(sn),
+                           group=group)
+    u, over = rows.merge(received)
+    # every rank learns whether some share overflowed its table
+    flag = torch.tensor([over], dtype=torch.int64, device=dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
     if int(flag.item()) > 0:
-        raise L.PinotAmdError("hashed merge: a rank's share of the merged groups exceeds its table by %d slots (size "
+        raise L.PinotAmdError("hashed merge: a rank's share of the merged groups exceeds its table by %d rows (size "
                               "the tables with parallel.table_layout's hash_keys_bound)" % int(flag.item()))
-    for k, t in per_key:
-        w = t.numel() // num_slots
-        out = t.view(num_slots, w)
-        out.fill_(SECTION_IDENTITY.get(k, 0))
-        if k == L.PA_ACC_KEYS_I64:
-            out[:u, 0] = uniq
-            continue
-        acc = torch.full((u, w), SECTION_IDENTITY.get(k, 0), dtype=t.dtype, device=dev)
-        acc.scatter_reduce_(0, inv.view(-1, 1).expand(-1, w), cols[k], reduce=_SCATTER_REDUCE[SECTION_OP[k]],
-                            include_self=True)
-        out[:u] = acc
     return u
+
+
+class LibraryRows:
+    """The local halves of merge_hashed_sections on the device, through the library (pa_merge.hip): pack =
+    pa_query_pack_rows (occupied slots -> rows grouped by owner rank), merge = pa_query_merge_rows (reset the block,
+    insert every received row's packed key into the table, combine each accumulator with its section's operator)."""
+
+    def __init__(self, executor, device):
+        self.handle = executor.handle
+        self.device = device
+        self.row_bytes = L.check(L.lib().pa_query_row_bytes(self.handle), "pa_query_row_bytes")
+
+    def pack(self, world):
+        lib = L.lib()
+        counts = np.zeros(world, dtype=np.int64)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        L.check(lib.pa_query_pack_rows(self.handle, world, None, counts.ctypes.data, stream), "pa_query_pack_rows")
+        out = torch.empty(int(counts.sum()), self.row_bytes, dtype=torch.uint8, device=self.device)
+        if out.shape[0]:
+            L.check(lib.pa_query_pack_rows(self.handle, world, out.data_ptr(), counts.ctypes.data, stream),
+                    "pa_query_pack_rows")
+        return out, counts.tolist()
+
+    def merge(self, received):
+        groups, over = ctypes.c_int64(), ctypes.c_int64()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        L.check(L.lib().pa_query_merge_rows(self.handle, received.data_ptr() if received.shape[0] else None,
+                                            int(received.shape[0]), ctypes.byref(groups), ctypes.byref(over), stream),
+                "pa_query_merge_rows")
+        return int(groups.value), int(over.value)
 
 
 class HashedAccumulators:
@@ -186,6 +184,7 @@ class HashedAccumulators:
         executor._acc_owner = self.buf  # the library reads and writes this block for the executor's lifetime
         self.num_slots = int(executor.num_keys)
         self.key_space = key_space_bytes(executor)
+        self.rows = LibraryRows(executor, device)
         self.views = []
         for kind, ptr, n in executor.sections():
             off = ptr - self.buf.data_ptr()
@@ -198,7 +197,8 @@ class HashedAccumulators:
             check_same_key_space(-1, self.device, group=group,
                                  what="hashed merge: a rank holds only empty segments and no table layout (build its "
                                       "executor with parallel.table_layout(...).executor_kwargs())")
-        return merge_hashed_sections(self.views, self.num_slots, group=group, layout_extra=self.key_space)
+        return merge_hashed_sections(self.views, self.num_slots, group=group, layout_extra=self.key_space,
+                                     rows=self.rows)
 
 
 def section_runs(sections):

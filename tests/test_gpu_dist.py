@@ -154,3 +154,59 @@ def test_rank_with_only_empty_segments_joins_the_merge(rccl_world1):
             e.close()
         for g in full + empty:
             g.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_library_pack_and_merge_rows_across_simulated_ranks(world):
+    """The hashed merge's local halves on the GPU (parallel.LibraryRows: pa_query_pack_rows / pa_query_merge_rows)
+    with the all-to-all done by hand: `world` executors over disjoint segment sets stand for the ranks; each packs its
+    groups into rows per owner rank, rank r merges every rank's rows for r into its own block. Every rank then holds
+    exactly the groups key_owner gives it, and the union of the shares equals the oracle over all segments (COUNT,
+    exact SUM of LONG, SUM of DOUBLE within 1e-9, MIN / MAX, HLL registers)."""
+    from pinot_amd.parallel import LibraryRows, key_owner
+    cols = dict(COLS, r=("LONG", 0))
+    sql = "SELECT r, COUNT(*), SUM(m), SUM(f), MIN(f), MAX(m), DISTINCTCOUNTHLL(d1) FROM t GROUP BY r LIMIT 100000"
+    q = parse_sql(sql)
+    shards = [[make_segment(700 + 10 * w + i, n, cols, no_dict=("r",)) for i, n in enumerate((9001, 4003))]
+              for w in range(world)]
+    # (make_segment draws r in [-1000, 1000): the ranks hold overlapping keys)
+    gsegs = [[GpuSegment(s) for s in sh] for sh in shards]
+    dev = torch.device("cuda", 0)
+    bound = sum(s.num_docs for sh in shards for s in sh)
+    exs = [GpuQueryExecutor(q, g, hash_keys_bound=bound) for g in gsegs]
+    try:
+        rows = [LibraryRows(e, dev) for e in exs]
+        for e in exs:
+            assert e.hashed
+            e.execute()
+        torch.cuda.synchronize()
+        packed = [r.pack(world) for r in rows]
+        us = []
+        for w in range(world):
+            parts = []
+            for src in range(world):
+                buf, counts = packed[src]
+                lo = sum(counts[:w])
+                parts.append(buf[lo:lo + counts[w]])
+            u, over = rows[w].merge(torch.cat(parts))
+            assert over == 0
+            us.append(u)
+        torch.cuda.synchronize()
+        got_groups = {}
+        for w, e in enumerate(exs):
+            res = e.fetch()
+            assert len(res.groups) == us[w]
+            for key in res.groups:
+                assert int(key_owner(torch.tensor([int(key[0])], dtype=torch.int64), world)[0]) == w
+                assert key not in got_groups
+            got_groups.update(res.groups)
+        exp = oracle.run_query(q, [s for sh in shards for s in sh])
+        merged = exs[0].fetch()
+        merged.groups = got_groups
+        assert_same(merged, exp, rel=1e-9)
+    finally:
+        for e in exs:
+            e.close()
+        for g in gsegs:
+            for x in g:
+                x.close()

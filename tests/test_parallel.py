@@ -323,10 +323,12 @@ def _hashed_worker(rank, world, port, out, partial_fn=None, extra=b""):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from pinot_amd.parallel import merge_hashed_sections
+    from row_ops_ref import TorchRows
     secs, _ = (partial_fn or _hashed_partial)(rank)
     views = [(k, torch.from_numpy(np.ascontiguousarray(a)).to(SECTION_DTYPE[k])) for k, a in secs]
     try:
-        u = merge_hashed_sections(views, NS, layout_extra=extra if isinstance(extra, bytes) else extra[rank])
+        u = merge_hashed_sections(views, NS, layout_extra=extra if isinstance(extra, bytes) else extra[rank],
+                                  rows=TorchRows(views, NS))
         out[rank] = (u, [t.numpy().copy() for _, t in views])
     except L.PinotAmdError as e:
         out[rank] = ("raised", str(e))
