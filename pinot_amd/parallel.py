@@ -368,6 +368,35 @@ def check_same_key_space(fingerprint, device, group=None, what=None):
                               "space): build the executors with parallel.table_layout(...).executor_kwargs()")
 
 
+def reduce_scatter_sections(per_key, num_keys, group=None):
+    """per_key: [(section kind, 1-D tensor)] of the per-key sections of a direct key space (num_keys rows each; the
+    numDocsScanned counters excluded). Instead of reducing the whole block onto one rank, every rank ends up holding the
+    merged rows of its own key range — keys [r K', (r + 1) K') with K' = floor(K / world), one reduce-scatter per
+    section (each rank receives 1/world of the block: over xGMI every link carries 1/world of it per step instead of the
+    whole block converging on one GPU), and the K mod world remainder keys (all-reduced) on the last rank. Every other
+    row is reset to its section's identity (count 0: the executor's fetch skips it), so each rank's fetch returns its
+    share of the groups, disjoint across ranks — partial DataTables the broker concatenates; numDocsScanned and the
+    other counters stay per rank (the broker sums them). Returns the rank's key range (lo, hi)."""
+    world, r = dist.get_world_size(group), dist.get_rank(group)
+    K = int(num_keys)
+    kr = K // world
+    lo, hi = r * kr, (r + 1) * kr + (K - kr * world if r == world - 1 else 0)
+    for kind, t in per_key:
+        w = t.numel() // K
+        op, ident = SECTION_OP[kind], SECTION_IDENTITY.get(kind, 0)
+        out = torch.empty(kr * w, dtype=t.dtype, device=t.device)
+        if kr:
+            dist.reduce_scatter_tensor(out, t[:kr * world * w], op=op, group=group)
+        rem = t[kr * world * w:]
+        if rem.numel():
+            dist.all_reduce(rem, op=op, group=group)
+        t[:lo * w].fill_(ident)
+        t[lo * w:(lo + kr) * w].copy_(out)
+        if r != world - 1:
+            t[(lo + kr) * w:].fill_(ident)
+    return lo, hi
+
+
 class DistributedAccumulators:
     """Moves an executor's accumulators into one torch-owned device block and reduces it across ranks (direct key
     spaces: the same key id addresses the same accumulator row on every GPU)."""
@@ -395,6 +424,30 @@ class DistributedAccumulators:
         executor._acc_owner = self.buf
         runs = section_runs([(kind, ptr - self.base + pad, n) for kind, ptr, n in executor.sections()])
         self.views = [(kind, self.buf[a:b].view(dt)) for kind, dt, a, b in runs]
+        self.num_keys = int(executor.num_keys)
+        self.per_key = []  # [(kind, 1-D view)] of every per-key section (the counters excluded)
+        for kind, ptr, n in executor.sections():
+            if kind == L.PA_ACC_DOCS_U64:
+                continue
+            dt = SECTION_DTYPE[kind]
+            es = torch.empty(0, dtype=dt).element_size()
+            off = ptr - self.base + pad
+            self.per_key.append((kind, self.buf[off:off + n * es].view(dt)))
 
     def reduce(self, dst=0, all_reduce=False):
         reduce_sections(self.views, dst=dst, all_reduce=all_reduce)
+
+    def reduce_scatter(self, group=None):
+        """Large direct key spaces: every rank ends up holding the merged rows of its own key range
+        (reduce_scatter_sections), so each rank's fetch returns its share of the groups. Returns the range (lo, hi)."""
+        return reduce_scatter_sections(self.per_key, self.num_keys, group)
+
+    def merge(self, dst=0, group=None, scatter_keys=1 << 20):
+        """The cross-GPU merge this key space wants: key spaces of at least `scatter_keys` keys reduce-scatter (every
+        rank then fetches its share: returns True), smaller ones reduce onto rank `dst`, the one rank that fetches
+        (returns False)."""
+        if self.num_keys >= scatter_keys:
+            self.reduce_scatter(group)
+            return True
+        self.reduce(dst=dst)
+        return False

@@ -210,3 +210,24 @@ def test_library_pack_and_merge_rows_across_simulated_ranks(world):
         for g in gsegs:
             for x in g:
                 x.close()
+
+
+def test_reduce_scatter_merge_path(rccl_world1):
+    """DistributedAccumulators.merge on a key space at the scatter threshold runs reduce_scatter_sections over RCCL
+    (world size 1: the rank's range is the whole key space) and the fetch of the rewritten block equals the oracle."""
+    q = parse_sql("SELECT d1, d2, COUNT(*), SUM(m), MIN(f), MAX(m), DISTINCTCOUNTHLL(m) FROM t GROUP BY d1, d2 "
+                  "LIMIT 10000")
+    segs = [make_segment(820 + i, n, COLS) for i, n in enumerate((11003, 5001))]
+    gsegs = [GpuSegment(s) for s in segs]
+    ex = GpuQueryExecutor(q, gsegs)
+    try:
+        acc = DistributedAccumulators(ex, torch.device("cuda", 0))
+        ex.execute()
+        torch.cuda.synchronize()
+        assert acc.merge(scatter_keys=1) is True
+        torch.cuda.synchronize()
+        assert_same(ex.fetch(), oracle.run_query(q, segs), rel=1e-9)
+    finally:
+        ex.close()
+        for g in gsegs:
+            g.close()

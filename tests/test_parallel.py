@@ -539,3 +539,47 @@ def test_gloo_rank_with_only_empty_segments():
     assert out["dict0"] == out["dict1"] and len(out["dict0"]) > 0
     for name in ("DistributedAccumulators", "HashedAccumulators"):
         assert out["raised0_" + name] and out["raised1_" + name]
+
+
+def _rs_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pinot_amd.parallel import reduce_scatter_sections
+    secs, _ = partial(rank)
+    views = [(k, torch.from_numpy(np.ascontiguousarray(a)).to(SECTION_DTYPE[k])) for k, a in secs]
+    lo, hi = reduce_scatter_sections(views, K)
+    out[rank] = (lo, hi, [t.numpy().copy() for _, t in views])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_reduce_scatter_gives_each_rank_its_key_range(world):
+    """parallel.reduce_scatter_sections (large direct key spaces): rank r holds the merged rows of keys
+    [r K', (r + 1) K') (the last rank also the K mod world remainder), identities elsewhere; the ranges tile the key
+    space and every merged row equals the whole-block reduce."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_rs_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    parts = [partial(r) for r in range(world)]
+    exp_count = sum(p[0][0][1] for p in parts)
+    exp_sum = sum(p[1].astype(object) for p in parts)
+    exp_dsum = sum(p[0][2][1] for p in parts)
+    exp_min = np.minimum.reduce([p[0][3][1] for p in parts])
+    exp_max = np.maximum.reduce([p[0][4][1] for p in parts])
+    exp_hll = np.maximum.reduce([p[0][5][1] for p in parts])
+    covered = np.zeros(K, dtype=int)
+    for r in range(world):
+        lo, hi, (count, sx2, dsum, dmin, imax, hll) = out[r]
+        covered[lo:hi] += 1
+        mine = np.zeros(K, dtype=bool)
+        mine[lo:hi] = True
+        assert np.array_equal(count[mine], exp_count[mine]) and (count[~mine] == 0).all()
+        total = sx2[0::2].astype(object) + (sx2[1::2].astype(object) << 32)
+        assert all(a == b for a, b in zip(total[mine], exp_sum[mine])) and (sx2.reshape(K, 2)[~mine] == 0).all()
+        assert np.allclose(dsum[mine], exp_dsum[mine], rtol=1e-12, atol=0) and (dsum[~mine] == 0).all()
+        assert np.array_equal(dmin[mine], exp_min[mine]) and (dmin[~mine] == (1 << 63) - 1).all()
+        assert np.array_equal(imax[mine], exp_max[mine]) and (imax[~mine] == -(1 << 63)).all()
+        h = hll.reshape(K, -1)
+        assert np.array_equal(h[mine], exp_hll.reshape(K, -1)[mine]) and (h[~mine] == 0).all()
+    assert (covered == 1).all()
