@@ -145,8 +145,10 @@ def test_fused_execution_stats_match_the_replay(monkeypatch):
     every search finished. A sparse A leaf (y) makes searches give up: those segments fall back to the bitmap counts,
     with the same result. With E first in the reference's AND order the fused counts do not apply (fallback)."""
     n0 = 300_007
+    # (segments large enough that e's dictionary keeps e = 7 below 1 / 256 of the docs, which makes the planner
+    # evaluate the z clause lazily: the fused count's precondition)
     segs = [_sparse_segment(1, n0, [0, 1, 2047, 2048, 4095, n0 - 1]), _sparse_segment(2, 70_000, [69_999]),
-            _sparse_segment(3, 1025, [512]), _sparse_segment(4, 5000, [])]
+            _sparse_segment(3, 131_072, [65_536]), _sparse_segment(4, 200_000, [])]
     gs = [GpuSegment(s) for s in segs]
     try:
         cases = [("z < 2 AND e = 7", True), ("z BETWEEN 3 AND 6 AND e IN (7, 11)", True),
