@@ -1875,9 +1875,9 @@ int plan_kernels(pa_query* q, Prep& P, TilePlan& plan, TilePlan& count_plan) {
     TilePlan best;
     bool best_lm = false;
     int best_strat = STRAT_GDENSE;
-    for (int st : {STRAT_GDENSE8, STRAT_GDENSE})
+    for (int st : {STRAT_GDENSE12, STRAT_GDENSE8, STRAT_GDENSE})
       for (int use_lm : {1, 0}) {
-        if (use_lm && !lm) continue;
+        if (use_lm && (!lm || st == STRAT_GDENSE12)) continue;
         const TilePlan t = plan_tiles(q, q->hsegs, st, use_lm != 0, P.gd_lds, use_lm == 0);
         if (t.score > best.score) {
           best = t;

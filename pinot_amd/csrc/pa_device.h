@@ -45,11 +45,13 @@ enum ColKind : int32_t { COL_NONE = 0, COL_SV_DICT = 1, COL_SV_RAW = 2, COL_MV_D
 // operations only (no per-doc HBM access, which would wait behind the ring's in-flight DMA: vmcnt counts in order).
 enum Strategy : int32_t {
   STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PEMIT = 2, STRAT_PCOUNT = 3, STRAT_LANE = 4,
-  STRAT_LANE_CNT = 5, STRAT_LANE_RAW = 6, STRAT_LANE_DICT = 7, STRAT_GDENSE = 8, STRAT_GDENSE8 = 9
+  STRAT_LANE_CNT = 5, STRAT_LANE_RAW = 6, STRAT_LANE_DICT = 7, STRAT_GDENSE = 8, STRAT_GDENSE8 = 9,
+  STRAT_GDENSE12 = 10
 };
-// STRAT_GDENSE: 4-wave workgroups; STRAT_GDENSE8: the same kernel with 8-wave workgroups (2 waves per SIMD when one
-// workgroup fits a CU: the walk's LDS round trips and VALU issue overlap across waves)
-__host__ __device__ constexpr bool is_gdense(int s) { return s == STRAT_GDENSE || s == STRAT_GDENSE8; }
+// STRAT_GDENSE: 4-wave workgroups; STRAT_GDENSE8 / STRAT_GDENSE12: the same kernel with 8- / 12-wave workgroups (2 / 3
+// waves per SIMD when one workgroup fits a CU, e.g. beside a 64 KiB value table: the walk's LDS round trips and VALU
+// issue overlap across waves; 12 waves: step-major tiles only)
+__host__ __device__ constexpr bool is_gdense(int s) { return s == STRAT_GDENSE || s == STRAT_GDENSE8 || s == STRAT_GDENSE12; }
 // STRAT_GDENSE value sources and LDS operations of one aggregation
 enum GdVs : int32_t {
   GVS_ID = 0,    // the dictId itself (SUM over an affine dictionary shared by every segment; MIN/MAX of a shared sorted one)
@@ -91,7 +93,8 @@ __host__ __device__ constexpr int pemit_vf(int s) { return (((s - kPemitBase) & 
 __host__ __device__ constexpr bool pemit_hh(int s) { return ((s - kPemitBase) & 1) != 0; }
 __host__ __device__ constexpr int pemit_big(int s) { return (s - kPemitBase) >= 16 ? 1 : 0; }
 __host__ __device__ constexpr int scan_waves(int s) {
-  return is_pemit(s) && pemit_big(s) ? kEmitBigWaves : (s == STRAT_GDENSE8 ? 2 * kGdWaves : kWavesPerWG);
+  return is_pemit(s) && pemit_big(s) ? kEmitBigWaves
+                                       : (s == STRAT_GDENSE8 ? 2 * kGdWaves : (s == STRAT_GDENSE12 ? 3 * kGdWaves : kWavesPerWG));
 }
 // V record formats (word 0 always holds the key's offset inside its partition, key & ((1 << kshift_v) - 1)):
 //   V_FMT_KEY: COUNT only, one word;  V_FMT_ID: one word, | value id << kshift_v (the value column's table-wide value

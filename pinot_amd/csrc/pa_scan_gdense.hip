@@ -8,6 +8,7 @@ const void* scan_fn_gdense(int strategy, int lm) {
     return lm ? (const void*)gdense_kernel<kGdWaves, 1> : (const void*)gdense_kernel<kGdWaves, 0>;
   if (strategy == STRAT_GDENSE8)
     return lm ? (const void*)gdense_kernel<2 * kGdWaves, 1> : (const void*)gdense_kernel<2 * kGdWaves, 0>;
+  if (strategy == STRAT_GDENSE12 && !lm) return (const void*)gdense_kernel<3 * kGdWaves, 0>;
   return nullptr;
 }
 
