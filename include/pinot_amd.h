@@ -358,9 +358,13 @@ int pa_query_merge_rows(pa_query* q, const void* device_rows, int64_t num_rows, 
 
 /* Group-key layout. Direct (hashed = 0): key = sum_j id_j * prod_{k<j} cardinality_k. Hashed (hashed = 1, chosen when
  * a group-by column is raw or the product of cardinalities is too large to address): the key packs component j
- * (a table-wide key id, or the raw value's bits: 32 for INT/FLOAT, 64 for LONG/DOUBLE) at bit shifts[j]. Keys returned
- * by pa_query_fetch follow this layout. */
+ * (a table-wide key id, or the raw value's bits: 32 for INT/FLOAT, 64 for LONG/DOUBLE) at bit shifts[j]; components
+ * wider than 64 bits together take two key words (pa_query_key_words = 2: component j in word shifts[j] / 64 at bit
+ * shifts[j] % 64, e.g. GROUP BY two raw LONG columns — NoDictionaryMultiColumnGroupKeyGenerator's composite keys), and
+ * pa_query_fetch then writes two int64 per group into out_keys (out_keys holds 2 x capacity). Keys returned by
+ * pa_query_fetch follow this layout. */
 int pa_query_key_layout(const pa_query* q, int32_t* hashed, int32_t* shifts);
+int32_t pa_query_key_words(const pa_query* q);
 
 /* Kernel statistics of the last execute (for roofline accounting): bytes of forward index staged
  * (always-read columns), number of docs scanned. */

@@ -54,7 +54,7 @@ EXPORTED = [
     "pa_query_num_groups_limit_reached", "pa_query_stats", "pa_query_leaf_bitmap_words", "pa_query_leaf_bitmaps",
     "pa_bitmap_counts_scratch_bytes", "pa_bitmap_counts", "pa_query_filter_counts",
     "pa_query_plan", "pa_query_column_staged", "pa_query_leap_leaf", "pa_query_leap_counts",
-    "pa_query_row_bytes", "pa_query_pack_rows", "pa_query_merge_rows", "pa_query_destroy",
+    "pa_query_row_bytes", "pa_query_pack_rows", "pa_query_merge_rows", "pa_query_key_words", "pa_query_destroy",
 ]
 
 
@@ -149,6 +149,7 @@ def _declare(lib):
         "pa_query_leap_leaf": (i32, [vp]),
         "pa_query_leap_counts": (ctypes.c_int, [vp, vp, vp]),
         "pa_query_row_bytes": (i64, [vp]),
+        "pa_query_key_words": (i32, [vp]),
         "pa_query_pack_rows": (ctypes.c_int, [vp, i32, vp, vp, vp]),
         "pa_query_merge_rows": (ctypes.c_int, [vp, vp, i64, vp, vp, vp]),
         "pa_query_destroy": (None, [vp]),

@@ -519,6 +519,7 @@ struct pa_query {
   int lane_major = 0;
   int has_mv = 0;
   bool hashed = false;           // packed 64-bit keys through a global open-addressing table
+  int key_words = 1;             // hashed: 2 = two-word keys ([k0, k1, state] per slot)
   int64_t ht_slots = 0;
   int key_shift[PA_MAX_GROUP_BY] = {0};
   int keys_section = -1;
@@ -646,6 +647,7 @@ struct Prep {
   std::vector<int> leaf_slot, gb_slot, agg_slot;
   std::vector<char> slot_eager, slot_post, slot_gb;
   std::vector<int64_t> stride;
+  std::vector<int> gb_word;  // hashed, two-word keys: the word of each group-by component
   std::vector<char> gb_raw;
   uint64_t limit_pairs = 0;
   int limit_eb = 0;
@@ -793,6 +795,8 @@ int plan_slots(pa_query* q, Prep& P) {
 int plan_key_space(pa_query* q, Prep& P) {
   const pa_query_spec& s = q->spec;
   q->hashed = false;
+  q->key_words = 1;
+  P.gb_word.assign(s.num_group_by, 0);
   std::vector<int> gb_bits(s.num_group_by, 0);
   P.gb_raw.assign(s.num_group_by, 0);
   bool direct_ok = true;
@@ -816,12 +820,21 @@ int plan_key_space(pa_query* q, Prep& P) {
     else K *= card;
   }
   if (!direct_ok) {
+    // components side by side in one 64-bit word; wider together, in two words (a component never straddles them:
+    // first fit in column order), the table then keeping [k0, k1, state] per slot (pa_keys.h ht_slot2)
     int total_bits = 0;
+    for (int j = 0; j < s.num_group_by; ++j) total_bits += gb_bits[j];
+    q->key_words = total_bits > 64 ? 2 : 1;
+    int used[2] = {0, 0};
     for (int j = 0; j < s.num_group_by; ++j) {
-      if (total_bits + gb_bits[j] > 64) return fail(PA_EUNSUPPORTED, "packed group key wider than 64 bits");
-      P.stride[j] = total_bits < 64 ? (int64_t)(uint64_t(1) << total_bits) : 0;
-      q->key_shift[j] = total_bits;
-      total_bits += gb_bits[j];
+      int w = 0;
+      if (used[0] + gb_bits[j] > 64) w = 1;
+      if (q->key_words == 1 ? w != 0 : used[w] + gb_bits[j] > 64)
+        return fail(PA_EUNSUPPORTED, "packed group key wider than 128 bits");
+      P.gb_word[j] = w;
+      P.stride[j] = used[w] < 64 ? (int64_t)(uint64_t(1) << used[w]) : 0;
+      q->key_shift[j] = 64 * w + used[w];
+      used[w] += gb_bits[j];
     }
     // slots: twice the keys that can exist (docs, or docs x values for MV group-by), at least 1024, a power of two
     uint64_t bound = 0;
@@ -1383,7 +1396,8 @@ int plan_accumulators(pa_query* q, Prep& P) {
   }
   q->keys_section = -1;
   if (q->hashed) {
-    sec.push_back({PA_ACC_KEYS_I64, K});  // slot -> packed key (INT64_MAX = empty)
+    // slot -> packed key (INT64_MAX = empty), or [k0, k1, state] for two-word keys (state INT64_MAX = empty)
+    sec.push_back({PA_ACC_KEYS_I64, K * (q->key_words == 2 ? 3 : 1)});
     q->keys_section = (int)sec.size() - 1;
   }
   sec.push_back({PA_ACC_DOCS_U64, 4});  // [0] numDocsScanned, [1] group-table overflows, [2] limit reached, [3] errors
@@ -2051,6 +2065,8 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
   h.count = (unsigned long long*)q->sections[0].ptr;
   h.matched_docs = (unsigned long long*)q->sections.back().ptr;
   h.hashed = q->hashed ? 1 : 0;
+  h.key_words = q->key_words;
+  for (int j = 0; j < s.num_group_by; ++j) h.gb_word[j] = q->hashed ? P.gb_word[j] : 0;
   if (q->hashed) {
     h.ht_mask = q->ht_slots - 1;
     h.ht_keys = (long long*)q->sections[q->keys_section].ptr;
@@ -2651,11 +2667,13 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   const bool grouped = s.num_group_by != 0;
   char* dbase = (char*)(q->external_acc ? q->external_acc : q->acc.p);
 
-  // Decodes `nrows` host rows into the caller's arrays: row r has key key_of(r), count hc[r] and the aggregation
-  // section rows at sec(section)[r * per]. Rows with a zero count are skipped when `skip_empty`.
-  // `order` (optional) lists the rows to emit, in output order (hashed key spaces: sorted by packed key).
+  // Decodes `nrows` host rows into the caller's arrays: row r has key key_of(r, w) (word w < kw: two-word hashed keys
+  // fill out_keys[2 n], out_keys[2 n + 1]), count hc[r] and the aggregation section rows at sec(section)[r * per]. Rows
+  // with a zero count are skipped when `skip_empty`. `order` (optional) lists the rows to emit, in output order (hashed
+  // key spaces: sorted by packed key).
+  const int kw = q->hashed ? q->key_words : 1;
   auto decode = [&](int64_t nrows, const uint64_t* hc, const std::function<const char*(int)>& sec,
-                    const std::function<int64_t(int64_t)>& key_of, bool skip_empty,
+                    const std::function<int64_t(int64_t, int)>& key_of, bool skip_empty,
                     const std::vector<int64_t>* order) -> int64_t {
     const char* asec[PA_MAX_AGGS];  // section base per aggregation, resolved once (not per row)
     for (int a = 0; a < s.num_aggs; ++a) asec[a] = q->agg_section[a] >= 0 ? sec(q->agg_section[a]) : nullptr;
@@ -2665,7 +2683,8 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
       const int64_t r = order ? (*order)[oi] : oi;
       if (skip_empty && hc[r] == 0) continue;
       if (n < capacity) {
-        if (out_keys) out_keys[n] = key_of(r);
+        if (out_keys)
+          for (int w = 0; w < kw; ++w) out_keys[kw * n + w] = key_of(r, w);
         if (out_counts) out_counts[n] = (int64_t)hc[r];
         for (int a = 0; a < s.num_aggs; ++a) {
           if (!out_aggs || !out_aggs[a]) continue;
@@ -2719,13 +2738,16 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
     const uint64_t* hc = (const uint64_t*)hsec(0);
     if (q->hashed) {
       const int64_t* hk = (const int64_t*)hsec(q->keys_section);
+      const int ks = kw == 2 ? 3 : 1;  // key-section words per slot
       std::vector<int64_t> order;
       for (int64_t r = 0; r < K; ++r)
         if (hc[r]) order.push_back(r);
-      std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return hk[a] < hk[b]; });
-      return decode(K, hc, hsec, [&](int64_t r) { return hk[r]; }, false, &order);
+      std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+        return hk[ks * a] != hk[ks * b] ? hk[ks * a] < hk[ks * b] : (kw == 2 && hk[ks * a + 1] < hk[ks * b + 1]);
+      });
+      return decode(K, hc, hsec, [&](int64_t r, int w) { return hk[ks * r + w]; }, false, &order);
     }
-    return decode(K, hc, hsec, [](int64_t r) { return r; }, grouped, nullptr);
+    return decode(K, hc, hsec, [](int64_t r, int) { return r; }, grouped, nullptr);
   }
 
   // Large key spaces: ordered compaction of the non-empty keys on the GPU (count + scan, then key ids and every
@@ -2838,15 +2860,18 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   for (size_t i = 0; i < secs.size(); ++i) hsec[secs[i]] = hb + offs[i];
   if (q->hashed) {  // rows are slots: emit them in packed-key order
     const int64_t* pk = (const int64_t*)hsec[q->keys_section];
+    const int ks = kw == 2 ? 3 : 1;
     std::vector<int64_t> order(rows);
     for (int64_t r = 0; r < rows; ++r) order[r] = r;
-    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return pk[a] < pk[b]; });
+    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+      return pk[ks * a] != pk[ks * b] ? pk[ks * a] < pk[ks * b] : (kw == 2 && pk[ks * a + 1] < pk[ks * b + 1]);
+    });
     order.resize(rows_cap);
-    decode(rows, (const uint64_t*)hsec[0], [&](int sec) { return hsec[sec]; }, [&](int64_t r) { return pk[r]; },
-           false, &order);
+    decode(rows, (const uint64_t*)hsec[0], [&](int sec) { return hsec[sec]; },
+           [&](int64_t r, int w) { return pk[ks * r + w]; }, false, &order);
     return m;
   }
-  decode(rows, (const uint64_t*)hsec[0], [&](int sec) { return hsec[sec]; }, [&](int64_t r) { return hkeys[r]; },
+  decode(rows, (const uint64_t*)hsec[0], [&](int sec) { return hsec[sec]; }, [&](int64_t r, int) { return hkeys[r]; },
          false, nullptr);
   return m;
 }
@@ -3149,6 +3174,7 @@ static int row_desc(const pa_query* q, RowDesc& d) {
   d.row_bytes = off;
   d.num_slots = q->num_keys;
   d.ht_mask = q->ht_slots - 1;
+  d.key_words = q->key_words;
   return PA_OK;
 }
 
@@ -3244,6 +3270,8 @@ int pa_query_key_layout(const pa_query* q, int32_t* hashed, int32_t* shifts) {
     for (int j = 0; j < q->spec.num_group_by; ++j) shifts[j] = q->hashed ? q->key_shift[j] : 0;
   return PA_OK;
 }
+
+int32_t pa_query_key_words(const pa_query* q) { return q && q->prepared ? (q->hashed ? q->key_words : 1) : -1; }
 
 void pa_query_destroy(pa_query* q) { delete q; }
 

@@ -220,7 +220,8 @@ struct DevQuery {
   unsigned long long* matched_docs;  // [0]: docs that passed the filter (numDocsScanned), [1]: group-table overflows,
                                      // [2]: segments that reached numGroupsLimit, [3]: internal consistency errors
   int32_t hashed;            // packed keys through the open-addressing table ht_keys (gb_stride = 1 << shift)
-  int32_t pad3;
+  int32_t key_words;         // hashed: 1 = one 64-bit packed key per slot, 2 = two words + state (pa_keys.h)
+  int32_t gb_word[PA_MAX_GROUP_BY];  // hashed, two words: the key word group-by column j's component lands in (else 0)
   int64_t ht_mask;           // table slots - 1 (power of two); slot ht_mask + 1 is reserved for the key INT64_MAX
   long long* ht_keys;        // slot -> packed key, INT64_MAX = empty
   // partitioned aggregation (STRAT_PCOUNT / STRAT_PEMIT / part_agg_kernel)

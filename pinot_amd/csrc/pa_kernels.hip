@@ -40,7 +40,7 @@ __device__ __forceinline__ bool doc_passes(const DevQuery* __restrict__ q, const
 template <class F>
 __device__ __forceinline__ void for_each_key(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int64_t doc,
                                              F&& f) {
-  int64_t base = 0;
+  int64_t base[2] = {0, 0};
   int nmv = 0;
   int mv_gb[PA_MAX_GROUP_BY];
   int32_t mv_s[PA_MAX_GROUP_BY], mv_n[PA_MAX_GROUP_BY];
@@ -55,11 +55,11 @@ __device__ __forceinline__ void for_each_key(const DevQuery* __restrict__ q, con
       combos *= mv_n[nmv];
       ++nmv;
     } else {
-      base += (int64_t)(gb_component<true>(c, seg->remap[j], nullptr, 0, doc) * (uint64_t)q->gb_stride[j]);
+      base[q->gb_word[j]] += (int64_t)(gb_component<true>(c, seg->remap[j], nullptr, 0, doc) * (uint64_t)q->gb_stride[j]);
     }
   }
   for (int64_t e = 0; e < combos; ++e) {
-    int64_t key = base;
+    int64_t kw[2] = {base[0], base[1]};
     int64_t rem = e;
     for (int t = 0; t < nmv; ++t) {
       const int j = mv_gb[t];
@@ -69,9 +69,9 @@ __device__ __forceinline__ void for_each_key(const DevQuery* __restrict__ q, con
       uint32_t id = decode_global(c.words, mv_s[t] + digit, c.nbits);
       const int32_t* rm = seg->remap[j];
       if (rm != nullptr) id = (uint32_t)gp(rm)[id];
-      key += (int64_t)id * q->gb_stride[j];
+      kw[q->gb_word[j]] += (int64_t)id * q->gb_stride[j];
     }
-    f(e, key);
+    f(e, key_slot(q, kw[0], kw[1]));
   }
 }
 
@@ -115,8 +115,7 @@ __global__ void __launch_bounds__(256) limit_first_kernel(const DevQuery* __rest
   const int nseg = q->num_segments;
   for_each_doc(q, segs, [&](int si, const DevSeg* seg, int64_t doc, bool valid) {
     if (!valid || !doc_passes(q, seg, doc)) return;
-    for_each_key(q, seg, doc, [&](int64_t e, int64_t key) {
-      const int64_t slot = key_slot(q, key);
+    for_each_key(q, seg, doc, [&](int64_t e, int64_t slot) {
       if (slot < 0) return;
       const int64_t fs = first_slot(q, F, slot * nseg + si, true);
       if (fs < 0) return;
@@ -210,8 +209,7 @@ __global__ void __launch_bounds__(256) limit_agg_kernel(const DevQuery* __restri
     if (lane == 0 && wm) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)__builtin_popcountll(wm), RLX);
     if (!pass) return;
     const unsigned long long T = F.thresh[si];
-    for_each_key(q, seg, doc, [&](int64_t e, int64_t key) {
-      const int64_t slot = key_slot(q, key);
+    for_each_key(q, seg, doc, [&](int64_t e, int64_t slot) {
       if (slot < 0) return;
       const int64_t fs = first_slot(q, F, slot * nseg + si, false);
       if (fs < 0 || F.fpos[fs] >= T) return;  // INVALID_ID: the segment's group table was full at first sight

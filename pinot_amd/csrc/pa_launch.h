@@ -113,11 +113,11 @@ struct RowSec {
 };
 struct RowDesc {
   int32_t nsec;
-  int32_t pad;
+  int32_t key_words;   // 1: one packed key word per slot; 2: [k0, k1, state] (pa_keys.h)
   int64_t row_bytes;
   int64_t num_slots;   // table slots incl. the reserved one (num_keys)
   int64_t ht_mask;     // probing mask (slots - 2)
-  int64_t key_off;     // byte offset of the packed key inside a row
+  int64_t key_off;     // byte offset of the packed key (k0[, k1, state]) inside a row
   const unsigned long long* count;
   long long* keys;
   RowSec sec[kMaxRowSecs];

@@ -9,23 +9,17 @@
 // thread per (row, 8-byte unit), so the copies are coalesced within a row whatever the row size.
 #include <hip/hip_runtime.h>
 
+#include "pa_keys.h"
 #include "pa_launch.h"
 
 namespace pa {
 
 #define MRLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
 
-__device__ __forceinline__ uint64_t merge_mix64(uint64_t x) {  // (the scan's key_slot hash: pa_scan.h mix64)
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdULL;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ULL;
-  x ^= x >> 33;
-  return x;
-}
-
-// Rank that owns packed key k among `world` ranks.
-__device__ __forceinline__ int owner_of(int64_t k, int world) {
+// Rank that owns packed key (k0, k1) among `world` ranks (one-word keys: k1 = 0 is not mixed in, so the function is
+// parallel.key_owner's).
+__device__ __forceinline__ int owner_of(int64_t k0, int64_t k1, int words, int world) {
+  const int64_t k = words == 2 ? (int64_t)((uint64_t)k0 ^ mix64((uint64_t)k1)) : k0;
   int64_t h = k ^ (k >> 31);
   h = (int64_t)((uint64_t)h * 0x9E3779B97F4A7C15ULL);
   return (int)(((h >> 33) & 0x7FFFFFFF) % world);
@@ -45,7 +39,10 @@ __global__ void __launch_bounds__(256) pack_index_kernel(RowDesc d, int world, i
   for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x; s0 < d.num_slots; s0 += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = s0 + threadIdx.x;
     int o = -1;
-    if (s < d.num_slots && __hip_atomic_load(d.count + s, MRLX) > 0ull) o = owner_of(d.keys[s], world);
+    if (s < d.num_slots && __hip_atomic_load(d.count + s, MRLX) > 0ull) {
+      const int ks = d.key_words == 2 ? 3 : 1;
+      o = owner_of(d.keys[ks * s], d.key_words == 2 ? d.keys[ks * s + 1] : 0, d.key_words, world);
+    }
     for (int r = 0; r < world; ++r) {
       const uint64_t m = __ballot(o == r);
       if (m == 0) continue;
@@ -81,36 +78,43 @@ __global__ void __launch_bounds__(256) pack_copy_kernel(RowDesc d, const int64_t
 __global__ void __launch_bounds__(256) merge_keys_kernel(RowDesc d, const unsigned char* rows, int64_t n,
                                                           int64_t* row_slot, unsigned long long* counters) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t key = *(const int64_t*)(rows + r * d.row_bytes + d.key_off);
-    int64_t slot = -1;
-    if (key == INT64_MAX) {
+    const int64_t* kp = (const int64_t*)(rows + r * d.row_bytes + d.key_off);
+    int64_t slot;
+    if (d.key_words == 2) {
+      bool ins;
+      slot = ht_slot2(d.keys, d.ht_mask, kp[0], kp[1], &ins);
+      if (ins) atomicAdd(counters, 1ull);
+    } else if (kp[0] == INT64_MAX) {
       slot = d.ht_mask + 1;  // (the reserved slot is its own marker: its group is counted by the first such row)
       if (atomicCAS(counters + 2, 0ull, 1ull) == 0ull) atomicAdd(counters, 1ull);
     } else {
-      int64_t h = (int64_t)(merge_mix64((uint64_t)key) & (uint64_t)d.ht_mask);
-      for (int64_t probe = 0; probe <= d.ht_mask; ++probe) {
+      // (a new group is counted by the row whose CAS claimed the slot: compare the slot's word before and after)
+      const int64_t mask = d.ht_mask;
+      int64_t h = (int64_t)(mix64((uint64_t)kp[0]) & (uint64_t)mask);
+      slot = -1;
+      for (int64_t probe = 0; probe <= mask; ++probe) {
         long long cur = __hip_atomic_load(d.keys + h, MRLX);
-        if (cur == key) {
+        if (cur == kp[0]) {
           slot = h;
           break;
         }
         if (cur == INT64_MAX) {
           long long expected = INT64_MAX;
-          if (__hip_atomic_compare_exchange_strong(d.keys + h, &expected, (long long)key, __ATOMIC_RELAXED,
+          if (__hip_atomic_compare_exchange_strong(d.keys + h, &expected, (long long)kp[0], __ATOMIC_RELAXED,
                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
             slot = h;
             atomicAdd(counters, 1ull);
             break;
           }
-          if (expected == key) {
+          if (expected == kp[0]) {
             slot = h;
             break;
           }
         }
-        h = (h + 1) & d.ht_mask;
+        h = (h + 1) & mask;
       }
-      if (slot < 0) atomicAdd(counters + 1, 1ull);
     }
+    if (slot < 0) atomicAdd(counters + 1, 1ull);
     row_slot[r] = slot;
   }
 }

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include "pa_device.h"
 #include "pa_launch.h"
+#include "pa_keys.h"
 
 namespace pa {
 
@@ -289,38 +290,20 @@ __device__ __forceinline__ uint64_t gb_component(const DevCol& c, const int32_t*
   return id;
 }
 
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdULL;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ULL;
-  x ^= x >> 33;
-  return x;
-}
-
-// Hashed key space: the accumulator slot of a packed key (linear probing; insert by CAS on the empty marker
-// INT64_MAX, which itself lives in the reserved slot ht_mask + 1). -1 if the table is full (counted as an overflow:
-// the query then fails loudly at fetch).
-__device__ __forceinline__ int64_t key_slot(const DevQuery* __restrict__ q, int64_t key) {
-  if (!q->hashed) return key;
-  const int64_t mask = q->ht_mask;
-  if (key == INT64_MAX) return mask + 1;
-  AS1 long long* keys = gp(q->ht_keys);
-  int64_t h = (int64_t)(mix64((uint64_t)key) & (uint64_t)mask);
-  for (int64_t probe = 0; probe <= mask; ++probe) {
-    long long cur = __hip_atomic_load(keys + h, RLX);
-    if (cur == key) return h;
-    if (cur == INT64_MAX) {
-      long long expected = INT64_MAX;
-      if (__hip_atomic_compare_exchange_strong(keys + h, &expected, (long long)key, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT) ||
-          expected == key)
-        return h;
-    }
-    h = (h + 1) & mask;
+// Hashed key space: the accumulator slot of a packed key (pa_keys.h: one word, or two for components wider than 64
+// bits together, DevQuery::key_words; a direct key space's key is its slot). -1 if the table is full (counted as an
+// overflow: the query then fails loudly at fetch).
+__device__ __forceinline__ int64_t key_slot(const DevQuery* __restrict__ q, int64_t k0, int64_t k1 = 0) {
+  if (!q->hashed) return k0;
+  int64_t s;
+  if (q->key_words == 2) {
+    bool ins;
+    s = ht_slot2((long long*)q->ht_keys, q->ht_mask, k0, k1, &ins);
+  } else {
+    s = ht_slot1((long long*)q->ht_keys, q->ht_mask, k0);
   }
-  __hip_atomic_fetch_add(gp(q->matched_docs) + 1, 1ull, RLX);
-  return -1;
+  if (s < 0) __hip_atomic_fetch_add(gp(q->matched_docs) + 1, 1ull, RLX);
+  return s;
 }
 
 // Accumulate the matched lanes (`matched` = wave mask) of one 64-doc step.
@@ -333,9 +316,11 @@ __device__ __forceinline__ void accumulate_step(const DevQuery* __restrict__ q, 
   // key's accumulator slot in the hashed key space
   int64_t key = 0;
   if (mine) {
+    int64_t kw[2] = {0, 0};  // (two words: DevQuery::gb_word)
     for (int j = 0; j < q->num_gb; ++j)
-      key += (int64_t)(gb_component(seg->cols[q->gb_slot[j]], seg->remap[j], img, doc_local, doc) * (uint64_t)q->gb_stride[j]);
-    key = key_slot(q, key);
+      kw[q->gb_word[j]] += (int64_t)(gb_component(seg->cols[q->gb_slot[j]], seg->remap[j], img, doc_local, doc) *
+                                     (uint64_t)q->gb_stride[j]);
+    key = key_slot(q, kw[0], kw[1]);
     if (key < 0) mine = false;
   }
   matched &= __ballot(mine);
@@ -657,7 +642,7 @@ __device__ __forceinline__ void update_doc_key(const DevQuery* __restrict__ q, c
 template <int STRAT>
 __device__ void accumulate_doc_mv(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
                                   const uint32_t* img, int doc_local, int64_t doc, const Acc<STRAT>& acc) {
-  int64_t base_key = 0;
+  int64_t base_key[2] = {0, 0};
   int nmv = 0;
   int mv_gb[PA_MAX_GROUP_BY];
   int32_t mv_s[PA_MAX_GROUP_BY], mv_n[PA_MAX_GROUP_BY];
@@ -672,11 +657,11 @@ __device__ void accumulate_doc_mv(const DevQuery* __restrict__ q, const DevSeg* 
       combos *= mv_n[nmv];
       ++nmv;
     } else {
-      base_key += (int64_t)(gb_component(c, seg->remap[j], img, doc_local, doc) * (uint64_t)q->gb_stride[j]);
+      base_key[q->gb_word[j]] += (int64_t)(gb_component(c, seg->remap[j], img, doc_local, doc) * (uint64_t)q->gb_stride[j]);
     }
   }
   for (int64_t cb = 0; cb < combos; ++cb) {
-    int64_t key = base_key;
+    int64_t kw[2] = {base_key[0], base_key[1]};
     int64_t rem = cb;
     for (int t = 0; t < nmv; ++t) {
       const int j = mv_gb[t];
@@ -686,9 +671,9 @@ __device__ void accumulate_doc_mv(const DevQuery* __restrict__ q, const DevSeg* 
       uint32_t id = decode_global(c.words, mv_s[t] + digit, c.nbits);
       const int32_t* rm = seg->remap[j];
       if (rm != nullptr) id = (uint32_t)gp(rm)[id];
-      key += (int64_t)id * q->gb_stride[j];
+      kw[q->gb_word[j]] += (int64_t)id * q->gb_stride[j];
     }
-    key = key_slot(q, key);
+    const int64_t key = key_slot(q, kw[0], kw[1]);
     if (key < 0) continue;
     update_doc_key<STRAT>(q, seg, img, doc_local, doc, key, acc);
   }

@@ -457,6 +457,7 @@ class GpuQueryExecutor:
         L.check(lib.pa_query_key_layout(self.handle, ctypes.byref(hashed), shifts), "pa_query_key_layout")
         self.hashed = bool(hashed.value)
         self.key_shifts = list(shifts)[:len(q.group_by)]
+        self.key_words = int(lib.pa_query_key_words(self.handle))  # 2: two int64 per hashed key
         self.strides = []
         s = 1
         for gd in self.global_dicts:
@@ -519,8 +520,9 @@ class GpuQueryExecutor:
             # large key space: a capacity-0 call runs only the GPU count pass and returns the number of non-empty
             # groups, so the gather + copy run once, at the exact size
             cap = max(1, L.check(lib.pa_query_fetch(self.handle, stream, 0, None, None, None), "pa_query_fetch"))
+        kw = getattr(self, "key_words", 1)
         while True:
-            keys = alloc("keys", cap, np.int64)
+            keys = alloc("keys", cap * kw, np.int64)
             counts = alloc("counts", cap, np.int64)
             outs, ptrs = [], (ctypes.c_void_p * max(1, len(self.pa_aggs)))()
             for i, (t, _, log2m) in enumerate(self.pa_aggs):
@@ -540,7 +542,7 @@ class GpuQueryExecutor:
         outs = [o[: n << self.pa_aggs[i][2]] if self.pa_aggs[i][0] == L.PA_AGG_DISTINCTCOUNTHLL else
                 (o[: n * self._presence_stride(i)] if self.pa_aggs[i][0] == L.PA_AGG_DISTINCTCOUNT else o[:n])
                 for i, o in enumerate(outs)]
-        return keys[:n], counts[:n], outs
+        return (keys[:n] if kw == 1 else keys[:2 * n].reshape(n, 2)), counts[:n], outs
 
     def _presence_stride(self, i):
         """DISTINCTCOUNT presence bytes per group: the value count rounded up to 16 (PA_ACC_PRESENCE_U8)."""
@@ -549,12 +551,16 @@ class GpuQueryExecutor:
     def key_values(self, keys):
         """Keys -> one value array per group-by column (DictionaryBasedGroupKeyGenerator.getKeys). Direct key space:
         key = sum id_j * prod_{k<j} card_k. Hashed (pa_query_key_layout): component j at bit shift_j, a table-wide key
-        id for dictionary columns, the value bits for raw ones (INT/FLOAT 32 bits, LONG/DOUBLE 64)."""
+        id for dictionary columns, the value bits for raw ones (INT/FLOAT 32 bits, LONG/DOUBLE 64); two-word keys
+        (keys of shape (n, 2)): component j in word shift_j // 64 at bit shift_j % 64."""
         if not self.hashed:
             return [gd[(keys // st) % len(gd)] for gd, st in zip(self.global_dicts, self.strides)]
-        k = np.asarray(keys, dtype=np.int64).view(np.uint64)
+        kk = np.asarray(keys, dtype=np.int64)
+        words = [kk.view(np.uint64)] if kk.ndim == 1 else [np.ascontiguousarray(kk[:, w]).view(np.uint64)
+                                                           for w in range(kk.shape[1])]
         out = []
-        for gd, raw, sh in zip(self.global_dicts, self.raw_group_by, self.key_shifts):
+        for gd, raw, shw in zip(self.global_dicts, self.raw_group_by, self.key_shifts):
+            k, sh = words[shw // 64], shw % 64
             if gd is not None:
                 bits = max(1, int(len(gd) - 1).bit_length())
             else:

@@ -73,6 +73,20 @@ def key_owner(keys, world):
     return ((h >> 33) & 0x7FFFFFFF) % world
 
 
+def _mix64(x):
+    """pa_keys.h mix64 on int64 tensors (products wrap; logical shifts as masked arithmetic ones)."""
+    x = x ^ ((x >> 33) & 0x7FFFFFFF)
+    x = x * -49064778989728563  # 0xff51afd7ed558ccd as a signed int64
+    x = x ^ ((x >> 33) & 0x7FFFFFFF)
+    x = x * -4265267296055464877  # 0xc4ceb9fe1a85ec53
+    return x ^ ((x >> 33) & 0x7FFFFFFF)
+
+
+def key_owner2(k0, k1, world):
+    """key_owner of a two-word key (pa_merge.hip owner_of): the first word mixed with the second's hash."""
+    return key_owner(k0 ^ _mix64(k1), world)
+
+
 def row_layout_fingerprint(views, num_slots, extra=b""):
     """62-bit digest of what the ranks of a hashed merge must share: every section's kind and row width (elements per
     slot, not the slot count) and `extra` (the key space: dictionaries and DISTINCTCOUNT value dictionaries)."""

@@ -6,7 +6,7 @@ import torch
 import torch.distributed as dist
 
 from pinot_amd import _lib as L
-from pinot_amd.parallel import SECTION_IDENTITY, SECTION_OP, key_owner
+from pinot_amd.parallel import SECTION_IDENTITY, SECTION_OP, key_owner, key_owner2
 
 _SCATTER_REDUCE = {dist.ReduceOp.SUM: "sum", dist.ReduceOp.MIN: "amin", dist.ReduceOp.MAX: "amax"}
 
@@ -34,7 +34,10 @@ class TorchRows:
             self.layout.append((k, t.dtype, w, b.shape[1]))
             parts.append(b)
         local = torch.cat(parts, dim=1)
-        owner = key_owner(dict(self.per_key)[L.PA_ACC_KEYS_I64].view(ns)[occ], world)
+        kt = dict(self.per_key)[L.PA_ACC_KEYS_I64]
+        kw = kt.numel() // ns  # 1, or 3 for two-word keys: [k0, k1, state]
+        keys = kt.view(ns, kw)[occ]
+        owner = key_owner(keys[:, 0], world) if kw == 1 else key_owner2(keys[:, 0], keys[:, 1], world)
         order = torch.argsort(owner, stable=True)
         return local[order], torch.bincount(owner, minlength=world).tolist()
 
@@ -44,8 +47,11 @@ class TorchRows:
         for k, dt, w, nb in self.layout:
             cols[k] = rows[:, o:o + nb].contiguous().view(dt).view(-1, w)
             o += nb
-        uniq, inv = torch.unique(cols[L.PA_ACC_KEYS_I64][:, 0], sorted=True, return_inverse=True)
-        u = int(uniq.numel())
+        kc = cols[L.PA_ACC_KEYS_I64]
+        kw = kc.shape[1]
+        uniq, inv = torch.unique(kc[:, 0] if kw == 1 else kc[:, :2], dim=None if kw == 1 else 0, sorted=True,
+                                 return_inverse=True)
+        u = int(uniq.shape[0])
         if u > ns:
             return u, u - ns
         for k, t in self.per_key:
@@ -53,7 +59,11 @@ class TorchRows:
             out = t.view(ns, w)
             out.fill_(SECTION_IDENTITY.get(k, 0))
             if k == L.PA_ACC_KEYS_I64:
-                out[:u, 0] = uniq
+                if w == 1:
+                    out[:u, 0] = uniq
+                else:
+                    out[:u, :2] = uniq
+                    out[:u, 2] = 0  # (a state other than empty)
                 continue
             acc = torch.full((u, w), SECTION_IDENTITY.get(k, 0), dtype=t.dtype)
             acc.scatter_reduce_(0, inv.view(-1, 1).expand(-1, w), cols[k], reduce=_SCATTER_REDUCE[SECTION_OP[k]],

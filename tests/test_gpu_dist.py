@@ -156,19 +156,26 @@ def test_rank_with_only_empty_segments_joins_the_merge(rccl_world1):
             g.close()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_library_pack_and_merge_rows_across_simulated_ranks(world):
+@pytest.mark.parametrize("world,sql", [
+    (2, "SELECT r, COUNT(*), SUM(m), SUM(f), MIN(f), MAX(m), DISTINCTCOUNTHLL(d1) FROM t GROUP BY r LIMIT 100000"),
+    (3, "SELECT r, COUNT(*), SUM(m), SUM(f), MIN(f), MAX(m), DISTINCTCOUNTHLL(d1) FROM t GROUP BY r LIMIT 100000"),
+    # two-word keys (two raw LONG columns: 128 bits)
+    (3, "SELECT r, r2, COUNT(*), SUM(m), MAX(f) FROM t GROUP BY r, r2 LIMIT 100000"),
+])
+def test_library_pack_and_merge_rows_across_simulated_ranks(world, sql):
     """The hashed merge's local halves on the GPU (parallel.LibraryRows: pa_query_pack_rows / pa_query_merge_rows)
     with the all-to-all done by hand: `world` executors over disjoint segment sets stand for the ranks; each packs its
     groups into rows per owner rank, rank r merges every rank's rows for r into its own block. Every rank then holds
     exactly the groups key_owner gives it, and the union of the shares equals the oracle over all segments (COUNT,
     exact SUM of LONG, SUM of DOUBLE within 1e-9, MIN / MAX, HLL registers)."""
-    from pinot_amd.parallel import LibraryRows, key_owner
-    cols = dict(COLS, r=("LONG", 0))
-    sql = "SELECT r, COUNT(*), SUM(m), SUM(f), MIN(f), MAX(m), DISTINCTCOUNTHLL(d1) FROM t GROUP BY r LIMIT 100000"
+    from pinot_amd.parallel import LibraryRows, key_owner, key_owner2
+    cols = dict(COLS, r=("LONG", 0), r2=("LONG", 0))
     q = parse_sql(sql)
-    shards = [[make_segment(700 + 10 * w + i, n, cols, no_dict=("r",)) for i, n in enumerate((9001, 4003))]
+    shards = [[make_segment(700 + 10 * w + i, n, cols, no_dict=("r", "r2")) for i, n in enumerate((9001, 4003))]
               for w in range(world)]
+    for sh in shards:  # (r2 in a small range: (r, r2) pairs repeat across ranks)
+        for sg in sh:
+            sg.column("r2").raw_values = sg.column("r2").raw_values % 7
     # (make_segment draws r in [-1000, 1000): the ranks hold overlapping keys)
     gsegs = [[GpuSegment(s) for s in sh] for sh in shards]
     dev = torch.device("cuda", 0)
@@ -196,8 +203,13 @@ def test_library_pack_and_merge_rows_across_simulated_ranks(world):
         for w, e in enumerate(exs):
             res = e.fetch()
             assert len(res.groups) == us[w]
+            kw = e.key_words
+            ks, _, _ = e.fetch_arrays()
+            for k in (ks.tolist() if kw == 1 else [tuple(x) for x in ks.tolist()]):
+                own = key_owner(torch.tensor([k]), world) if kw == 1 else \
+                    key_owner2(torch.tensor([k[0]]), torch.tensor([k[1]]), world)
+                assert int(own[0]) == w
             for key in res.groups:
-                assert int(key_owner(torch.tensor([int(key[0])], dtype=torch.int64), world)[0]) == w
                 assert key not in got_groups
             got_groups.update(res.groups)
         exp = oracle.run_query(q, [s for sh in shards for s in sh])

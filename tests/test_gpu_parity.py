@@ -442,14 +442,46 @@ def test_raw_group_by_hashed(flags):
     assert len(got.groups) > 190_000
 
 
-def test_packed_key_wider_than_64_bits_is_refused():
-    """Packed group keys hold at most 64 bits (a raw LONG/DOUBLE column takes all of them): refused loudly."""
-    cols = {"d1": ("INT", 40), "r3": ("LONG", 0)}
-    seg = make_segment(85, 1000, cols, no_dict=("r3",))
-    g = GpuSegment(seg)
-    with pytest.raises(L.PinotAmdError):
-        GpuQueryExecutor(parse_sql("SELECT d1, r3, COUNT(*) FROM t GROUP BY d1, r3"), [g])
-    g.close()
+@pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LANE_MAJOR])
+def test_group_keys_wider_than_64_bits(flags):
+    """Group keys wider than one 64-bit word (NoDictionaryMultiColumnGroupKeyGenerator's composite keys): a dictionary
+    column + a raw LONG, two raw LONGs, raw DOUBLE + LONG + INT take two key words ([k0, k1, state] slots,
+    pa_keys.h ht_slot2); small and large fetch paths, a multi-value group-by column with a raw LONG, and the default
+    numGroupsLimit (first-seen trimming over two-word keys); identical to the oracle."""
+    cols = {"d1": ("INT", 40), "m": ("LONG", 300), "r2": ("INT", 0), "r3": ("LONG", 0), "r1": ("DOUBLE", 0),
+            "r4": ("LONG", 0)}
+    segs = [make_segment(85 + i, n, cols, no_dict=("r1", "r2", "r3", "r4")) for i, n in enumerate((9001, 3001))]
+    queries = [
+        "SELECT d1, r3, COUNT(*), SUM(m), MAX(m) FROM t GROUP BY d1, r3 LIMIT 100000",
+        "SELECT r3, r4, COUNT(*), MIN(m), SUM(r2) FROM t WHERE r2 > 0 GROUP BY r3, r4 LIMIT 100000",
+        "SELECT r1, r3, r2, AVG(m), DISTINCTCOUNTHLL(m) FROM t GROUP BY r1, r3, r2 LIMIT 100000",
+        "SELECT r3, d1, COUNT(*) FROM t WHERE d1 < 20 GROUP BY r3, d1 LIMIT 100000",
+    ]
+    gsegs = [GpuSegment(sg) for sg in segs]
+    try:
+        for sql in queries:
+            got, exp, _ = run_both(sql, segs, gsegs=gsegs, flags=flags, rel=DOUBLE_REL)
+            assert got.groups
+            ex = GpuQueryExecutor(parse_sql(sql), gsegs)
+            assert ex.hashed and ex.key_words == 2, sql
+            ex.close()
+        # the default numGroupsLimit binds (first-seen trimming of two-word keys)
+        got, exp, _ = run_both("SELECT r3, r4, COUNT(*) FROM t GROUP BY r3, r4 LIMIT 100000 OPTION(numGroupsLimit=500)",
+                               segs, gsegs=gsegs, flags=flags)
+        assert got.num_groups_limit_reached
+    finally:
+        for g in gsegs:
+            g.close()
+    # large fetch path: many distinct (LONG, LONG) pairs
+    rng = np.random.default_rng(7)
+    from pinot_amd.segment import create_segment
+    n = 150_000
+    big = create_segment("bigw", {"a": rng.integers(-(1 << 40), 1 << 40, size=n), "b": rng.integers(0, 3, size=n),
+                                  "m": rng.integers(0, 100, size=n)},
+                         {"a": "LONG", "b": "LONG", "m": "INT"}, no_dictionary_columns=("a", "b"))
+    got, exp, _ = run_both("SELECT a, b, COUNT(*), SUM(m) FROM t GROUP BY a, b LIMIT 1000000 "
+                           "OPTION(numGroupsLimit=1000000)", [big], flags=flags)
+    assert len(got.groups) > 140_000
 
 
 def test_hashed_dictionary_key_space():

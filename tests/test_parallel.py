@@ -583,3 +583,56 @@ def test_gloo_reduce_scatter_gives_each_rank_its_key_range(world):
         h = hll.reshape(K, -1)
         assert np.array_equal(h[mine], exp_hll.reshape(K, -1)[mine]) and (h[~mine] == 0).all()
     assert (covered == 1).all()
+
+
+def _wide_partial(rank):
+    """Two-word keys ([k0, k1, state] per slot): 40 groups per rank, half of them shared with the other ranks (same
+    (k0, k1)), some sharing k0 with a different k1."""
+    rng = np.random.default_rng(950 + rank)
+    k0 = np.concatenate([np.arange(20, dtype=np.int64) * 7919 - (1 << 50), np.full(20, 123456789 + rank, np.int64)])
+    k1 = np.concatenate([np.arange(20, dtype=np.int64), np.arange(20, dtype=np.int64) * 31 + rank])
+    slots = rng.choice(NS, size=40, replace=False)
+    keys = np.full(3 * NS, (1 << 63) - 1, np.int64)
+    count = np.zeros(NS, np.int64)
+    dsum = np.zeros(NS)
+    imax = np.full(NS, -(1 << 63), np.int64)
+    groups = {}
+    for a, b, s in zip(k0.tolist(), k1.tolist(), slots.tolist()):
+        keys[3 * s], keys[3 * s + 1], keys[3 * s + 2] = a, b, 5
+        count[s] = rng.integers(1, 50)
+        dsum[s] = rng.standard_normal()
+        imax[s] = rng.integers(-1000, 1000)
+        groups[(a, b)] = (int(count[s]), float(dsum[s]), int(imax[s]))
+    secs = [(L.PA_ACC_COUNT_U64, count), (L.PA_ACC_SUM_F64, dsum), (L.PA_ACC_MAX_I64, imax), (L.PA_ACC_KEYS_I64, keys),
+            (L.PA_ACC_DOCS_U64, np.array([10 + rank, 0, 0, 0], np.int64))]
+    return secs, groups
+
+
+def test_gloo_hashed_merge_of_two_word_keys():
+    """merge_hashed_sections with two-word keys (group keys wider than 64 bits): rows go to the rank key_owner2 picks,
+    and every rank ends with its share merged by (k0, k1) — keys sharing k0 stay distinct."""
+    world = 3
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_hashed_worker, args=(world, _free_port(), out, _wide_partial), nprocs=world, join=True)
+    from pinot_amd.parallel import key_owner2
+    exp = {}
+    for r in range(world):
+        for k, (c, ds, mx) in _wide_partial(r)[1].items():
+            e = exp.get(k, (0, 0.0, -(1 << 63)))
+            exp[k] = (e[0] + c, e[1] + ds, max(e[2], mx))
+    seen = []
+    for r in range(world):
+        u, (count, dsum, imax, keys, docs) = out[r]
+        share = sorted(k for k in exp
+                       if int(key_owner2(torch.tensor([k[0]]), torch.tensor([k[1]]), world)[0]) == r)
+        kk = keys.reshape(NS, 3)
+        assert u == len(share)
+        assert [tuple(x) for x in kk[:u, :2].tolist()] == share
+        for i, k in enumerate(share):
+            c, ds, mx = exp[k]
+            assert count[i] == c and abs(dsum[i] - ds) <= 1e-12 * max(1.0, abs(ds)) and imax[i] == mx
+        assert (count[u:] == 0).all()
+        assert docs.tolist() == [10 + r, 0, 0, 0]
+        seen += share
+    assert sorted(seen) == sorted(exp) and len(exp) == 20 + 20 * world
