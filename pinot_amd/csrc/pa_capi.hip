@@ -3229,12 +3229,16 @@ int pa_query_merge_rows(pa_query* q, const void* device_rows, int64_t num_rows, 
   if (rc) return rc;
   if (num_rows < 0 || (num_rows > 0 && !device_rows)) return fail(PA_EINVAL, "merge rows: bad rows");
   hipStream_t st = (hipStream_t)stream;
-  rc = pa_query_reset(q, stream);
-  if (rc) return rc;
-  rc = merge_scratch(q, (size_t)(4 + std::max<int64_t>(num_rows, d.num_slots)) * 8);
+  rc = merge_scratch(q, (size_t)(8 + std::max<int64_t>(num_rows, d.num_slots)) * 8);
   if (rc) return rc;
   unsigned long long* ctr = (unsigned long long*)q->merge_buf.p;
-  int64_t* row_slot = (int64_t*)(ctr + 4);
+  int64_t* row_slot = (int64_t*)(ctr + 8);
+  // the block is reset except its numDocsScanned counters, which stay this rank's (the broker sums them)
+  void* docs = q->sections.back().ptr;
+  PA_HIP(hipMemcpyAsync(ctr + 4, docs, 32, hipMemcpyDeviceToDevice, st));
+  rc = pa_query_reset(q, stream);
+  if (rc) return rc;
+  PA_HIP(hipMemcpyAsync(docs, ctr + 4, 32, hipMemcpyDeviceToDevice, st));
   PA_HIP(hipMemsetAsync(ctr, 0, 32, st));
   PA_HIP(launch_merge_rows(d, (const unsigned char*)device_rows, num_rows, row_slot, ctr, st));
   unsigned long long h[4];
