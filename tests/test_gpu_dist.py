@@ -120,12 +120,13 @@ def test_rank_with_only_empty_segments_joins_the_merge(rccl_world1):
     """a rank whose segments are all empty plans a placeholder block from the agreed layout
     (parallel.table_layout: dictionaries, SUM widths, column schema), so its key-space fingerprint equals the other
     ranks', its reset block reduces as the identity, and as the reduce's destination it fetches the whole result."""
-    from pinot_amd.parallel import TableLayout
+    from pinot_amd.parallel import TableLayout, wide_sum_columns_local
     from pinot_amd.segment import Segment
     q = parse_sql("SELECT d1, COUNT(*), SUM(m), MIN(f), MAX(m), DISTINCTCOUNTHLL(m) FROM t WHERE m > 0 GROUP BY d1 "
                   "LIMIT 1000")
     segs = [make_segment(610 + i, n, COLS) for i, n in enumerate((12011, 3001))]
     layout = TableLayout(dicts={"d1": np.unique(np.concatenate([s.column("d1").dictionary for s in segs]))},
+                         wide=sorted(wide_sum_columns_local(q, segs)),
                          schema={n: (segs[0].column(n).data_type, True, True) for n in ("d1", "m", "f")})
     full = [GpuSegment(s) for s in segs]
     empty = [GpuSegment(Segment("e%d" % i, 0)) for i in range(2)]
