@@ -201,8 +201,11 @@ def test_library_pack_and_merge_rows_across_simulated_ranks(world, sql):
             us.append(u)
         torch.cuda.synchronize()
         got_groups = {}
+        docs_scanned = total_docs = 0
         for w, e in enumerate(exs):
             res = e.fetch()
+            docs_scanned += res.num_docs_scanned  # (counters stay per rank: the broker sums them)
+            total_docs += res.num_total_docs
             assert len(res.groups) == us[w]
             kw = e.key_words
             ks, _, _ = e.fetch_arrays()
@@ -216,6 +219,7 @@ def test_library_pack_and_merge_rows_across_simulated_ranks(world, sql):
         exp = oracle.run_query(q, [s for sh in shards for s in sh])
         merged = exs[0].fetch()
         merged.groups = got_groups
+        merged.num_docs_scanned, merged.num_total_docs = docs_scanned, total_docs
         assert_same(merged, exp, rel=1e-9)
     finally:
         for e in exs:
