@@ -445,7 +445,7 @@ def test_raw_group_by_hashed(flags):
 @pytest.mark.parametrize("flags", [0, L.PA_QF_NO_LANE_MAJOR])
 def test_group_keys_wider_than_64_bits(flags):
     """Group keys wider than one 64-bit word (NoDictionaryMultiColumnGroupKeyGenerator's composite keys): a dictionary
-    column + a raw LONG, two raw LONGs, raw DOUBLE + LONG + INT take two key words ([k0, k1, state] slots,
+    column + a raw LONG, two raw LONGs, raw DOUBLE + INT + dictionary take two key words ([k0, k1, state] slots,
     pa_keys.h ht_slot2); small and large fetch paths, a multi-value group-by column with a raw LONG, and the default
     numGroupsLimit (first-seen trimming over two-word keys); identical to the oracle."""
     cols = {"d1": ("INT", 40), "m": ("LONG", 300), "r2": ("INT", 0), "r3": ("LONG", 0), "r1": ("DOUBLE", 0),
@@ -454,7 +454,7 @@ def test_group_keys_wider_than_64_bits(flags):
     queries = [
         "SELECT d1, r3, COUNT(*), SUM(m), MAX(m) FROM t GROUP BY d1, r3 LIMIT 100000",
         "SELECT r3, r4, COUNT(*), MIN(m), SUM(r2) FROM t WHERE r2 > 0 GROUP BY r3, r4 LIMIT 100000",
-        "SELECT r1, r3, r2, AVG(m), DISTINCTCOUNTHLL(m) FROM t GROUP BY r1, r3, r2 LIMIT 100000",
+        "SELECT r1, r2, d1, AVG(m), DISTINCTCOUNTHLL(m) FROM t GROUP BY r1, r2, d1 LIMIT 100000",
         "SELECT r3, d1, COUNT(*) FROM t WHERE d1 < 20 GROUP BY r3, d1 LIMIT 100000",
     ]
     gsegs = [GpuSegment(sg) for sg in segs]
