@@ -899,7 +899,7 @@ __device__ __noinline__ void leap_tile(const DevQuery* __restrict__ q, const Dev
   leap_add(q, seg, matched, leaps, gave_up, lane);
 }
 
-// The segment-start term: by the wave that takes the segment's first tile.
+// The segment-start term: by the wave that takes the segment's first tile (scan_kernel's segment loop).
 __device__ __noinline__ void leap_segment_start(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int lane) {
   const uint32_t first = leap_search(seg, 0, 1, lane);
   leap_add(q, seg, 0u, first == 1u ? 1u : 0u, first == 4u ? 1u : 0u, lane);
@@ -2209,8 +2209,6 @@ __device__ __forceinline__ void process_tile(const DevQuery* __restrict__ q, con
                                              int64_t wt, const uint32_t* img, int lane, const Acc<STRAT>& acc,
                                              uint32_t& matched, LaneAcc& la) {
   const int64_t doc_base = wt * (STEPS * kWave);
-  if constexpr (STRAT != STRAT_PCOUNT && !is_pemit(STRAT))
-    if (doc_base == 0 && q->leap_mode) leap_segment_start(q, seg, lane);
   // docs of this tile owned by the lane: 64*i + lane < rem
   const int64_t rem = (int64_t)seg->num_docs - doc_base;
   // bit i <=> step i holds a doc of this segment (only the low STEPS bits: a negated leaf sets the others, and the
@@ -2338,8 +2336,6 @@ __device__ __forceinline__ void process_tile_lm(const DevQuery* __restrict__ q, 
                                                 uint32_t pp, int64_t wt, const uint32_t* img, uint32_t img_lds,
                                                 int lane, const Acc<STRAT>& acc, uint32_t& matched, LaneAcc& la) {
   const int64_t doc_base = wt * kWTileDocs;
-  if constexpr (STRAT != STRAT_PCOUNT && !is_pemit(STRAT))
-    if (doc_base == 0 && q->leap_mode) leap_segment_start(q, seg, lane);
   const int64_t rem = (int64_t)(int32_t)rl(pp, 2) - doc_base;
   uint32_t valid = 0xffffffffu;
   if (rem < kWTileDocs) {
@@ -2572,6 +2568,9 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
       const DevSeg* seg = segs + si;
       const uint32_t matched_seg0 = matched;
       const int64_t seg_first = seg->first_wtile;
+      // fused statistics: the segment-start term, by the wave that takes the segment's first tile
+      if constexpr (STRAT != STRAT_PCOUNT && !is_pemit(STRAT))
+        if (t == seg_first && q->leap_mode) leap_segment_start(q, seg, lane);
       const int64_t seg_end = min(t1, seg_first + (int64_t)seg->num_wtiles);
       const uint32_t pp = LM ? ((const uint32_t*)(plans + si))[lane] : 0u;  // process segment's plan table
       const bool stream_only = q->debug_stream_only != 0;

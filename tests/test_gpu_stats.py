@@ -179,3 +179,28 @@ def test_fused_execution_stats_match_the_replay(monkeypatch):
     finally:
         for g in gs:
             g.close()
+
+
+def test_fused_statistics_on_the_steady_state_tile_loop():
+    """The fused count's segment-start term (the segment's first labelled doc A-only) on waves that walk many tiles
+    (ring of 2, one workgroup per CU: the hoisted steady-state loop, not the per-tile entry point): the statistics of
+    an AND whose segments all start with an A-only doc equal the host replay."""
+    segs = [_sparse_segment(11 + i, 4_000_000, [1_000_000 + 7 * i]) for i in range(2)]
+    # (z < 8 matches half the docs, e = 7 a handful: every segment's first labelled doc is A-only)
+    gs = [GpuSegment(s) for s in segs]
+    try:
+        q = parse_sql("SELECT COUNT(*) FROM t WHERE z < 8 AND e = 7")
+        flags = L.PA_QF_FILTER_STATS | (2 << L.PA_QF_RING_SHIFT) | (1 << L.PA_QF_WG_SHIFT)
+        ex = GpuQueryExecutor(q, gs, flags=flags)
+        try:
+            ex.execute()
+            fz = ex.fused_leap_counts()
+            assert fz is not None and not fz[2][:, 2].any()
+            got = ex.execution_stats()
+            want = FS.server_stats(ex.query, ex.segs, lambda si: ex.leaf_bitmaps(si))
+        finally:
+            ex.close()
+        assert got == want
+    finally:
+        for g in gs:
+            g.close()
