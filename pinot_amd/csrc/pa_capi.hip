@@ -2410,6 +2410,11 @@ int pa_query_bind_value_remap(pa_query* q, int32_t index, int32_t agg, const int
   return PA_OK;
 }
 
+// counters + list length + overflow flag of the fused statistics (pa_scan.h "fused execution statistics")
+static size_t leap_header_bytes(const pa_query* q) {
+  return ((size_t)std::max(1, q->nseg) * 3 + 2) * sizeof(unsigned long long);
+}
+
 // PA_QF_FILTER_STATS: the scan counts the leap-frog statistics itself (leap_tile) when the filter is an AND of two
 // single-value leaves whose first (eager) clause is sparse — each of its docs costs two short neighbour searches — and
 // the scan is one pass (the partitioned and numGroupsLimit plans run the tile loop more than once).
@@ -2426,11 +2431,14 @@ static int plan_leaps(pa_query* q, const Prep& P) {
   }
   if (q->partitioned || q->limit_mode || q->limit_walk || is_gdense(q->strategy)) return PA_OK;
   if (P.first_clause_sel > 1.0 / 256.0) return PA_OK;
-  int rc = dev_alloc(q->leap_buf, (size_t)std::max(1, q->nseg) * 3 * sizeof(unsigned long long));
+  // list capacity: twice the E docs the planner's estimate allows (its overflow only costs the bitmap fallback)
+  const int64_t cap = (int64_t)(2.0 * P.first_clause_sel * (double)q->num_docs) + 65536;
+  int rc = dev_alloc(q->leap_buf, ((size_t)std::max(1, q->nseg) * 3 + 2 + (size_t)cap) * sizeof(unsigned long long));
   if (rc) return rc;
-  PA_HIP(hipMemset(q->leap_buf.p, 0, q->leap_buf.n));
+  PA_HIP(hipMemset(q->leap_buf.p, 0, leap_header_bytes(q)));
   q->hq.leap_mode = 1;
   q->hq.leap_out = (unsigned long long*)q->leap_buf.p;
+  q->hq.leap_cap = cap;
   q->leap_leaf = q->literals[0].leaf;
   return PA_OK;
 }
@@ -2541,7 +2549,7 @@ int pa_query_reset(pa_query* q, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   // one memset of the whole accumulator block, then the MIN/MAX sections to their identities
   PA_HIP(hipMemsetAsync(q->external_acc ? q->external_acc : q->acc.p, 0, q->acc.n, st));
-  if (q->hq.leap_mode) PA_HIP(hipMemsetAsync(q->leap_buf.p, 0, q->leap_buf.n, st));
+  if (q->hq.leap_mode) PA_HIP(hipMemsetAsync(q->leap_buf.p, 0, leap_header_bytes(q), st));
   for (const Section& sc : q->sections) {
     if (sc.kind == PA_ACC_MIN_I64 || sc.kind == PA_ACC_KEYS_I64) PA_HIP(launch_fill_i64((int64_t*)sc.ptr, sc.n, INT64_MAX, st));
     else if (sc.kind == PA_ACC_MAX_I64) PA_HIP(launch_fill_i64((int64_t*)sc.ptr, sc.n, INT64_MIN, st));
@@ -2596,6 +2604,7 @@ int pa_query_scan(pa_query* q, void* stream) {
   PartScratch none{};
   PA_HIP(launch_scan(q->strategy, q->steps, q->lane_major, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p,
                      (const DevSeg*)q->dsegs.p, (const LmSegPlan*)q->dplans.p, none, st));
+  if (q->hq.leap_mode) PA_HIP(launch_leap_search((const DevQuery*)q->dq.p, (const DevSeg*)q->dsegs.p, st));
   return PA_OK;
 }
 
@@ -3256,8 +3265,15 @@ int pa_query_leap_counts(const pa_query* q, int64_t* out, void* stream) {
   if (q->leap_leaf < 0) return fail(PA_EINVAL, "the scan does not count the filter statistics (pa_query_leap_leaf)");
   if (!out) return fail(PA_EINVAL, "null output");
   hipStream_t st = (hipStream_t)stream;
-  PA_HIP(hipMemcpyAsync(out, q->leap_buf.p, (size_t)q->nseg * 3 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  std::vector<int64_t> h((size_t)q->nseg * 3 + 2);
+  PA_HIP(hipMemcpyAsync(h.data(), q->leap_buf.p, h.size() * sizeof(int64_t), hipMemcpyDeviceToHost, st));
   PA_HIP(hipStreamSynchronize(st));
+  const bool overflow = h[(size_t)q->nseg * 3 + 1] != 0;  // (the E-doc list was full: no segment's leaps are known)
+  for (int si = 0; si < q->nseg; ++si) {
+    out[3 * si] = h[3 * si];
+    out[3 * si + 1] = h[3 * si + 1];
+    out[3 * si + 2] = (h[3 * si + 2] || overflow) ? 1 : 0;
+  }
   return PA_OK;
 }
 

@@ -281,11 +281,12 @@ struct DevQuery {
   int32_t gd_tables;                 // some key or value table is loaded per segment
   int32_t gd_pad;
   const uint32_t* gd_plans;          // [num_segments][64]: GdSegPlan of every segment
-  // fused execution statistics (PA_QF_FILTER_STATS, leap_tile): 1 = literal 0 (eager, E) and literal 1 (lazy, Z) are
-  // the two scan leaves of an AND; leap_out[3 s ..]: segment s's matched docs, leaps, gave-up flag
+  // fused execution statistics (PA_QF_FILTER_STATS, leap_tile + leap_search_kernel): 1 = literal 0 (eager, E) and
+  // literal 1 (lazy, Z) are the two scan leaves of an AND
   int32_t leap_mode;
   int32_t pad_leap;
-  unsigned long long* leap_out;
+  unsigned long long* leap_out;  // (layout: pa_scan.h "fused execution statistics")
+  int64_t leap_cap;              // list capacity (E docs)
 };
 // STRAT_GDENSE per-segment parameter table: 64 dwords, loaded once per segment into ONE VGPR (lane k holds dword k)
 // and read back with v_readlane at compile-time lanes, so the doc loop never issues a scalar load (an SMEM wait is an

@@ -1512,6 +1512,47 @@ hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t*
   return hipGetLastError();
 }
 
+// Fused execution statistics after the scan (pa_scan.h "fused execution statistics"): one wave per listed E doc (its
+// successor's label, and for a B-only doc its predecessor's) and one per segment (its first labelled doc), each a
+// wave-wide neighbour search over both leaves; the leaps go into the segments' counters.
+__global__ void __launch_bounds__(256) leap_search_kernel(const DevQuery* __restrict__ q, const DevSeg* __restrict__ segs) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int nseg = q->num_segments;
+  const AS1 unsigned long long* hdr = gp(q->leap_out) + 3 * (int64_t)nseg;
+  if (hdr[1]) return;  // (the list overflowed: the host takes every segment's counts from leaf bitmaps)
+  const int64_t n = (int64_t)min(hdr[0], (unsigned long long)q->leap_cap);
+  const int64_t total = n + nseg;
+  const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t w = (int64_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); w < total; w += waves) {
+    int si;
+    uint32_t leaps = 0u, gave = 0u;
+    if (w < n) {
+      const uint64_t ent = gp(q->leap_out)[3 * (int64_t)nseg + 2 + w];
+      si = (int)(ent >> 40);
+      const int64_t doc = (int64_t)((ent >> 1) & ((1ull << 39) - 1ull));
+      const uint32_t succ = leap_search(segs + si, doc + 1, 1, lane);
+      leaps += succ == 1u;
+      gave |= succ == 4u;
+      if (!(ent & 1ull)) {
+        const uint32_t pred = leap_search(segs + si, doc - 1, -1, lane);
+        leaps += pred == 1u;
+        gave |= pred == 4u;
+      }
+    } else {
+      si = (int)(w - n);
+      const uint32_t first = leap_search(segs + si, 0, 1, lane);
+      leaps += first == 1u;
+      gave |= first == 4u;
+    }
+    leap_add(q, si, 0u, leaps, gave, lane);
+  }
+}
+
+hipError_t launch_leap_search(const DevQuery* q, const DevSeg* segs, hipStream_t s) {
+  hipLaunchKernelGGL(leap_search_kernel, dim3(2048), dim3(256), 0, s, q, segs);
+  return hipGetLastError();
+}
+
 static const void* scan_fn(int strategy, int steps, int lm) {
   if (const void* f = scan_fn_std(strategy, steps, lm)) return f;
   if (const void* f = scan_fn_gdense(strategy, lm)) return f;

@@ -836,10 +836,14 @@ __device__ __forceinline__ bool leaf_match_doc(const DevLeaf& L, int64_t doc) {
 // (pa_kernels.hip word_leaps). Every such step but the first has an E (= B) doc at one end, so
 //   leaps = [the segment's first labelled doc is A-only]
 //         + sum over E docs e of ([succ(e) is A-only] + [e is B-only and pred(e) is A-only]),
-// with pred / succ the nearest labelled docs before / after e. The scan knows e's label (the lazy clause runs on it);
-// pred and succ come from a wave-wide search over 64 docs per step, both leaves read straight from HBM, which stops at
-// the first labelled doc (so never past the neighbouring E doc). The planner enables this only for a sparse E; a
-// search that gives up (kLeapSearchSteps) flags the segment, whose counts the host then takes from leaf bitmaps.
+// with pred / succ the nearest labelled docs before / after e. The scan knows e's label (the lazy clause runs on it) and
+// appends (segment, doc, label) to a list (leap_tile); after the scan, leap_search_kernel (pa_kernels.hip) gives every
+// listed doc one wave: a wave-wide search over 64 docs per step, both leaves read straight from HBM, stops at the first
+// labelled doc (so never past the neighbouring E doc) — in the scan itself every search step's load would wait behind
+// the tile ring's in-flight DMA. The planner enables this only for a sparse E; a search that gives up
+// (kLeapSearchSteps) or a full list flags the segment(s), whose counts the host then takes from leaf bitmaps.
+// leap_out: [3 s]: segment s's matched docs, leaps, gave-up flag; [3 nseg]: listed docs; [3 nseg + 1]: list overflow;
+// [3 nseg + 2 ..]: the list, one (segment << 40 | doc << 1 | both) per E doc.
 constexpr int kLeapSearchSteps = 64;  // 4096 docs
 
 // Label of the nearest labelled doc at or beyond `from` in direction dir (+1 / -1) inside the segment: 1, 2, 3; 0 if
@@ -860,51 +864,54 @@ __device__ __noinline__ uint32_t leap_search(const DevSeg* seg_in, int64_t from,
 }
 
 // One segment's counters (lane 0 adds them; nothing when all are zero).
-__device__ __forceinline__ void leap_add(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, uint32_t matched,
-                                         uint32_t leaps, uint32_t gave_up, int lane) {
+__device__ __forceinline__ void leap_add(const DevQuery* __restrict__ q, int seg_index, uint32_t matched, uint32_t leaps,
+                                         uint32_t gave_up, int lane) {
   if (lane == 0 && (matched | leaps | gave_up)) {
-    unsigned long long* o = q->leap_out + 3 * (int64_t)seg->index;
+    unsigned long long* o = q->leap_out + 3 * (int64_t)seg_index;
     if (matched) atomicAdd(o, (unsigned long long)matched);
     if (leaps) atomicAdd(o + 1, (unsigned long long)leaps);
     if (gave_up) atomicOr(o + 2, 1ull);
   }
 }
 
-// The E docs of one tile (e: eager clause bits, f: those that also matched the lazy clause), LM: doc of bit i of lane
-// l = 32 l + i, else 64 i + l.
+// The E docs of one tile (e: eager clause bits, f: those that also matched the lazy clause) into the list, and the
+// tile's matched docs into the segment's counter. LM: doc of bit i of lane l = 32 l + i, else 64 i + l.
 template <int LM>
 __device__ __noinline__ void leap_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int64_t doc_base,
                                        uint32_t e, uint32_t f, int lane) {
-  uint32_t leaps = 0u, gave_up = 0u;
-  for (;;) {
-    const uint64_t any = __ballot(e != 0u);
-    if (any == 0) break;
-    const int l = __builtin_ctzll(any);
-    const int i = __builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)e, l));
-    const bool both = (((uint32_t)__builtin_amdgcn_readlane((int)f, l) >> i) & 1u) != 0u;
-    if (lane == l) e &= e - 1u;
-    const int64_t doc = doc_base + (LM ? 32 * l + i : kWave * i + l);
-    const uint32_t succ = leap_search(seg, doc + 1, 1, lane);
-    gave_up |= succ == 4u;
-    leaps += succ == 1u;
-    if (!both) {
-      const uint32_t pred = leap_search(seg, doc - 1, -1, lane);
-      gave_up |= pred == 4u;
-      leaps += pred == 1u;
-    }
+  const uint32_t mine = (uint32_t)__builtin_popcount(e);
+  uint32_t incl = mine;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)incl, o, kWave);
+    if (lane >= o) incl += t;
   }
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
   uint32_t matched = (uint32_t)__builtin_popcount(f);
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) matched += (uint32_t)__shfl_xor((int)matched, o, kWave);
-  leap_add(q, seg, matched, leaps, gave_up, lane);
+  const int si = seg->index;
+  const int nseg = q->num_segments;
+  unsigned long long* hdr = q->leap_out + 3 * (int64_t)nseg;
+  unsigned long long base = 0;
+  if (lane == 0 && total) base = atomicAdd(hdr, (unsigned long long)total);
+  base = (unsigned long long)__shfl((long long)base, 0, kWave);
+  const unsigned long long cap = (unsigned long long)q->leap_cap;
+  if (total && base + total > cap) {
+    if (lane == 0) atomicOr(hdr + 1, 1ull);  // (the host then takes every segment's counts from leaf bitmaps)
+  } else {
+    unsigned long long pos = base + (incl - mine);
+    while (e) {
+      const int i = __builtin_ctz(e);
+      e &= e - 1u;
+      const int64_t doc = doc_base + (LM ? 32 * lane + i : kWave * i + lane);
+      const uint64_t both = (f >> i) & 1u;
+      gp(q->leap_out)[3 * (int64_t)nseg + 2 + (int64_t)pos++] =
+          ((uint64_t)si << 40) | ((uint64_t)doc << 1) | both;
+    }
+  }
+  leap_add(q, si, matched, 0u, 0u, lane);
 }
-
-// The segment-start term: by the wave that takes the segment's first tile (scan_kernel's segment loop).
-__device__ __noinline__ void leap_segment_start(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int lane) {
-  const uint32_t first = leap_search(seg, 0, 1, lane);
-  leap_add(q, seg, 0u, first == 1u ? 1u : 0u, first == 4u ? 1u : 0u, lane);
-}
-
 
 // ---------------------------------------------------------------- partitioned aggregation: count + emit passes
 // LDS bin state of the emit pass, per partition (V partitions first, then H): records in the bin (may pass the bin
@@ -2568,9 +2575,6 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
       const DevSeg* seg = segs + si;
       const uint32_t matched_seg0 = matched;
       const int64_t seg_first = seg->first_wtile;
-      // fused statistics: the segment-start term, by the wave that takes the segment's first tile
-      if constexpr (STRAT != STRAT_PCOUNT && !is_pemit(STRAT))
-        if (t == seg_first && q->leap_mode) leap_segment_start(q, seg, lane);
       const int64_t seg_end = min(t1, seg_first + (int64_t)seg->num_wtiles);
       const uint32_t pp = LM ? ((const uint32_t*)(plans + si))[lane] : 0u;  // process segment's plan table
       const bool stream_only = q->debug_stream_only != 0;

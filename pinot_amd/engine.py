@@ -623,7 +623,10 @@ class GpuQueryExecutor:
             return 0, 0  # EmptyFilterOperator: no entry read, no doc projected
         if docs_total is None:  # numDocsScanned of the last fetch (< 0: none yet)
             docs_total = int(L.lib().pa_query_matched_docs(self.handle))
-        return FS.server_stats_device(self.query, self.segs, self, stream, docs_total if docs_total >= 0 else None)
+        if getattr(self, "_stats_plan", None) is None:  # the operator trees of this prepared query, planned once
+            self._stats_plan = FS.plan_stats(self.query, self.segs, getattr(self, "leaf_params", None))
+        return FS.server_stats_device(self.query, self.segs, self, stream, docs_total if docs_total >= 0 else None,
+                                      self._stats_plan)
 
     def fetch(self, stream=None, execution_stats=False) -> IntermediateResult:
         """execution_stats=True also fills numEntriesScannedInFilter / PostFilter (one leaf-bitmap pass and a few

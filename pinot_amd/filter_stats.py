@@ -659,18 +659,56 @@ def _tree_signature(seg, fcols, params):
     return leaves, tuple(cols)
 
 
-def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps, leaf_params=None, docs_total=None):
-    """server_stats through the closed forms above. counts_fn(reqs) -> int64[len(reqs), 4]: for every request
-    (segment index, program A, program B) -> row, pa_bitmap_counts' four counts. Segments without a closed form replay
-    the iterators over leaf_bitmaps(i) (host bitmaps, as server_stats). leaf_params[i]: segment i's bound leaf
-    parameters in leaf order (GpuQueryExecutor.leaf_params), reused instead of re-matching the dictionaries.
-    docs_total: the scan's numDocsScanned over these segments, if known. When every segment's filter cost is a constant
-    (a scan driven to EOF reads every entry; OR / NOT of scans; index-served operators read none) the post-filter count
-    is docs_total x projected columns and counts_fn is never called: no pass over the filter columns."""
+class _StatsPlan:
+    """The per-segment operator trees of one query over one segment set, reduced to what the statistics need: per
+    segment None (non-scan plan), "host" (replay) or (in-filter _Terms, docs program, constant docs _Terms), the
+    requests of the in-filter terms, and — built on first use — the full request set with the docs requests and the
+    terms as flat arrays (one numpy gather evaluates every segment). GpuQueryExecutor keeps it across executions of
+    its prepared query (the trees depend on the query and the segments, not on a scan's results)."""
+
+    def __init__(self, ncols, plans, reqs):
+        self.ncols, self.plans, self.reqs = ncols, plans, reqs
+        self.full = None
+        self.fused_cache = {}  # fused_counts' classification of the full request set
+
+    def constant_value(self):
+        """in-filter entries when every segment's filter cost is a constant (no request at all), else None."""
+        if self.reqs or not all(p is not None and p != "host" for p in self.plans):
+            return None
+        return sum(p[0].value(None) for p in self.plans)
+
+    def flat(self):
+        if self.full is None:
+            reqs = dict(self.reqs)
+            plans = list(self.plans)
+            for si, p in enumerate(plans):
+                if isinstance(p, tuple):
+                    try:
+                        plans[si] = (p[0], p[2] if p[1] is None else _Terms(0).request(reqs, si, p[1], [], 0))
+                    except _Unsupported:
+                        plans[si] = "host"
+            const_in = const_docs = 0
+            ti, td = [], []
+            for p in plans:
+                if p is None or p == "host":
+                    continue
+                const_in += p[0].const
+                const_docs += p[1].const
+                ti += p[0].terms
+                td += p[1].terms
+            arr = lambda t: (np.array([x[0] for x in t], dtype=np.int64), np.array([x[1] for x in t], dtype=np.int64),
+                             np.array([x[2] for x in t], dtype=np.int64))
+            host = [si for si, p in enumerate(plans) if p == "host"]
+            self.full = (reqs, const_in, arr(ti), const_docs, arr(td), host)
+        return self.full
+
+
+def plan_stats(query, segments, leaf_params=None):
+    """_StatsPlan of `query` over `segments` (server_stats_closed_form's planning half)."""
     ncols = projected_columns(query)
     filt = query.filter
     reqs = {}
-    plans = []  # per segment: None (non-scan plan), "host", or (in_filter _Terms, docs _Terms)
+    plans = []  # per segment: None (non-scan plan), "host", or (in_filter _Terms, docs program, constant docs _Terms)
     flat = _flatten(filt) if filt is not None else None
     fcols = sorted(_filter_columns(filt)) if filt is not None else []
     trees = {}  # operator tree + docs program per segment signature (segments of a table usually share one)
@@ -696,22 +734,31 @@ def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps, leaf_para
             plans.append((cost, docs_prog, None))
         except _Unsupported:
             plans.append("host")
-    constant = docs_total is not None and not reqs and all(p is not None and p != "host" for p in plans)
-    if constant:
-        return sum(p[0].value(None) for p in plans), int(docs_total) * ncols
-    for si, p in enumerate(plans):
-        if isinstance(p, tuple):
-            try:
-                plans[si] = (p[0], p[2] if p[1] is None else _Terms(0).request(reqs, si, p[1], [], 0))
-            except _Unsupported:
-                plans[si] = "host"
-    counts = counts_fn(reqs) if reqs else None
-    in_filter = post = 0
-    for p in plans:
-        if p is not None and p != "host":
-            in_filter += p[0].value(counts)
-            post += p[1].value(counts) * ncols
-    host = [si for si, p in enumerate(plans) if p == "host"]
+    return _StatsPlan(ncols, plans, reqs)
+
+
+def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps, leaf_params=None, docs_total=None, plan=None):
+    """server_stats through the closed forms above. counts_fn(reqs) -> int64[len(reqs), 4]: for every request
+    (segment index, program A, program B) -> row, pa_bitmap_counts' four counts. Segments without a closed form replay
+    the iterators over leaf_bitmaps(i) (host bitmaps, as server_stats). leaf_params[i]: segment i's bound leaf
+    parameters in leaf order (GpuQueryExecutor.leaf_params), reused instead of re-matching the dictionaries.
+    docs_total: the scan's numDocsScanned over these segments, if known. When every segment's filter cost is a constant
+    (a scan driven to EOF reads every entry; OR / NOT of scans; index-served operators read none) the post-filter count
+    is docs_total x projected columns and counts_fn is never called: no pass over the filter columns.
+    plan: a _StatsPlan of this query and these segments (plan_stats) to reuse; built here when None."""
+    if plan is None:
+        plan = plan_stats(query, segments, leaf_params)
+    if docs_total is not None:
+        c = plan.constant_value()
+        if c is not None:
+            return c, int(docs_total) * plan.ncols
+    reqs, const_in, (ri, fi, ci), const_docs, (rd, fd, cd), host = plan.flat()
+    counts = counts_fn(reqs) if reqs else np.zeros((0, 4), dtype=np.int64)
+    vi, vd = counts[ri, fi], counts[rd, fd]
+    if (vi < 0).any() or (vd < 0).any():
+        raise RuntimeError("internal: a count the closed forms need was not computed")
+    in_filter = const_in + int(np.dot(vi.astype(object), ci.astype(object))) if len(ri) else const_in
+    post = (const_docs + (int(np.dot(vd.astype(object), cd.astype(object))) if len(rd) else 0)) * plan.ncols
     if host:
         hi, hp = server_stats(query, [segments[si] for si in host], lambda i: leaf_bitmaps(host[i]))
         in_filter += hi
@@ -738,34 +785,54 @@ def device_counts(executor, segments, reqs, stream=None):
     return out
 
 
-def fused_counts(reqs, fused, fallback):
+def fused_counts(reqs, fused, fallback, cache=None):
     """counts_fn rows from the counts the scan took itself (GpuQueryExecutor.fused_leap_counts: E leaf, Z leaf, per
     segment matched docs / leaps / gave-up): the AND request (A = [Z], B = [E]) gets popcount(A & B) = the segment's
     matched docs and the leaps, the post-filter request (the whole filter, no B) its popcount = the matched docs. Other
-    requests, and segments whose fused count gave up, go to fallback(reqs) (device_counts). Unknown fields are -1."""
+    requests, and segments whose fused count gave up, go to fallback(reqs) (device_counts). Unknown fields are -1.
+    cache: a dict kept with the requests (their classification is the same for every execution)."""
     e, z, arr = fused
-    out = np.full((len(reqs), 4), -1, dtype=np.int64)
-    rest = {}
-    for key, r in reqs.items():
-        si, a, b = key
-        row = None
-        if not arr[si, 2]:
+    cls = None if cache is None else cache.get((e, z))
+    if cls is None:
+        rows = {0: [], 1: []}  # 0: AND requests, 1: whole-filter requests -> (row, segment)
+        other = []
+        for key, r in reqs.items():
+            si, a, b = key
             if a == (z,) and b == (e,):
-                row = (-1, -1, arr[si, 0], arr[si, 1])
+                rows[0].append((r, si))
             elif not b and a in ((z, e, L.PA_BIT_AND), (e, z, L.PA_BIT_AND)):
-                row = (arr[si, 0], -1, -1, -1)
-        if row is None:
-            rest[key] = len(rest)
+                rows[1].append((r, si))
+            else:
+                other.append(key)
+        cls = tuple(np.array(rows[k], dtype=np.int64).reshape(-1, 2) for k in (0, 1)) + (other,)
+        if cache is not None:
+            cache[(e, z)] = cls
+    and_rs, doc_rs, other = cls
+    out = np.full((len(reqs), 4), -1, dtype=np.int64)
+    rest = list(other)
+    inv = None
+    for rs, fields in ((and_rs, (2, 3)), (doc_rs, (0,))):
+        if not len(rs):
+            continue
+        ok = arr[rs[:, 1], 2] == 0
+        r, sg = rs[ok, 0], rs[ok, 1]
+        if fields == (2, 3):
+            out[r, 2], out[r, 3] = arr[sg, 0], arr[sg, 1]
         else:
-            out[r] = row
+            out[r, 0] = arr[sg, 0]
+        if not ok.all():  # (gave-up segments: from leaf bitmaps)
+            if inv is None:
+                inv = {v: k for k, v in reqs.items()}
+            rest += [inv[int(x)] for x in rs[~ok, 0]]
     if rest:
-        sub = fallback(rest)
-        for key, r2 in rest.items():
+        sub_reqs = {key: i for i, key in enumerate(rest)}
+        sub = fallback(sub_reqs)
+        for key, r2 in sub_reqs.items():
             out[reqs[key]] = sub[r2]
     return out
 
 
-def server_stats_device(query, segments, executor, stream=None, docs_total=None):
+def server_stats_device(query, segments, executor, stream=None, docs_total=None, plan=None):
     """server_stats with the counts computed on the GPU (device_counts); same results. docs_total: the executor's
     numDocsScanned of its last scan (server_stats_closed_form: constant-cost filters then need no GPU pass). When the
     scan counted the statistics of its two-leaf AND itself (PA_QF_FILTER_STATS: fused_counts), no extra GPU pass runs
@@ -773,6 +840,6 @@ def server_stats_device(query, segments, executor, stream=None, docs_total=None)
     def counts(reqs):
         fz = executor.fused_leap_counts(stream) if hasattr(executor, "fused_leap_counts") else None
         dev = lambda rq: device_counts(executor, segments, rq, stream)
-        return dev(reqs) if fz is None else fused_counts(reqs, fz, dev)
+        return dev(reqs) if fz is None else fused_counts(reqs, fz, dev, None if plan is None else plan.fused_cache)
     return server_stats_closed_form(query, segments, counts, lambda si: executor.leaf_bitmaps(si, stream),
-                                    getattr(executor, "leaf_params", None), docs_total)
+                                    getattr(executor, "leaf_params", None), docs_total, plan)
