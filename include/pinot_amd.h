@@ -194,6 +194,9 @@ typedef struct {
 #define PA_QF_WG_SHIFT 12             /* bits 12..14: workgroups per CU (1..4) */
 #define PA_QF_DEBUG_STREAM_ONLY (1 << 16) /* measurement only: stream the tiles, skip decode (results invalid) */
 #define PA_QF_NO_LANE_MAJOR (1 << 17)     /* use the step-major scan kernel even when the lane-major one applies */
+#define PA_QF_NO_REG_STAGE (1 << 18)      /* dense GROUP BY kernel: tiles staged by the LDS-DMA ring only, never through
+                                             VGPRs (the register-staged variants keep more bytes in flight beside large
+                                             LDS tables) */
 #define PA_QF_NO_PARTITION (1 << 21)      /* high-cardinality dense GROUP BY: per-doc global atomics, not partitioned */
 #define PA_QF_NO_SPLIT_EMIT (1 << 24)     /* partitioned aggregation with both record streams: one emit kernel for both
                                              (default: a V launch and an H launch, each holding only its own bins) */

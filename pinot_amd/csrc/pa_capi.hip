@@ -558,7 +558,7 @@ struct pa_query {
   DevBuf leap_buf;  // PA_QF_FILTER_STATS fused into the scan: per segment (matched docs, leaps, gave up)
   int leap_leaf = -1;  // the eager leaf (spec order) when the scan counts the leaps
   std::vector<LmSegPlan> hplans;
-  std::vector<GdSegPlan> gdplans;  // STRAT_GDENSE: per-segment parameter tables
+  std::vector<uint32_t> gdplans;  // STRAT_GDENSE: per-segment parameter tables (GdSegPlan + GdRsPlan, 128 dwords)
   DevBuf dgdplans;
   std::vector<DevBuf> owned;  // LUTs, remaps, HLL LUTs, value dictionaries
   DevBuf acc;                 // all accumulator sections (unless the caller provided the block)
@@ -1899,6 +1899,41 @@ int plan_kernels(pa_query* q, Prep& P, TilePlan& plan, TilePlan& count_plan) {
           best_strat = st;
         }
       }
+    // register-staged tiles (more bytes in flight than the LDS ring beside large tables) when every segment shares the
+    // LDS tables and a tile's load instructions fit a variant's register ring
+    bool shared = true;
+    for (int si = 1; si < q->nseg && shared; ++si) {
+      for (int j = 0; j < s.num_group_by; ++j)
+        shared = shared && (P.gd_tab[j] < 0 || q->hsegs[si].remap[j] == q->hsegs[0].remap[j]);
+      for (int a = 0; a < s.num_aggs; ++a)
+        shared = shared && (P.gd_tab_a[a] < 0 || P.gd_src[si][a] == P.gd_src[0][a]);
+    }
+    if (shared && !(s.flags & ((15u << PA_QF_RING_SHIFT) | (7u << PA_QF_WG_SHIFT) | PA_QF_NO_REG_STAGE))) {
+      int ins = 0, img_dw = kGuardWords;
+      for (const DevSeg& d : q->hsegs) {
+        int n = 0, dw = kGuardWords;
+        for (int k = 0; k < d.num_staged; ++k) {
+          n += ((kGdSmSteps / 2) * d.stage[k].nbits + 63) / 64;
+          dw += 2 * kGdSmSteps * d.stage[k].nbits + kGuardWords;
+        }
+        ins = std::max(ins, n);
+        img_dw = std::max(img_dw, dw);
+      }
+      for (int st : {STRAT_GDENSE_RS12, STRAT_GDENSE_RS8}) {
+        if (ins > gd_rs_dmax(st)) continue;
+        const size_t lds = P.gd_lds + (size_t)scan_waves(st) * img_dw * 4;
+        if (lds > kLdsBudget) continue;
+        int resident = 0;
+        if (set_scan_lds_limit(st, kGdSmSteps, 0, (int)kLdsBudget) != hipSuccess ||
+            scan_occupancy(st, kGdSmSteps, 0, (int)lds, &resident) != hipSuccess)
+          resident = 1;
+        if (resident < 1) continue;
+        best = TilePlan{kGdSmSteps, ins, 1, 1, img_dw, lds, 1e9};
+        best_lm = false;
+        best_strat = st;
+        break;
+      }
+    }
     if (best.score >= 0) {
       lm = best_lm;
       plan = best;
@@ -2078,11 +2113,25 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
                         ? (uint32_t)P.lds_acc : 0;
   if (is_gdense(q->strategy)) {
     // per-segment parameter tables (GdSegPlan): the query's key box and LDS layout + the segment's staged regions
-    q->gdplans.assign(std::max(1, q->nseg), GdSegPlan{});
+    q->gdplans.assign((size_t)std::max(1, q->nseg) * 128, 0u);
     for (int si = 0; si < q->nseg; ++si) {
-      GdSegPlan& g = q->gdplans[si];
-      std::memset(&g, 0, sizeof(g));
+      GdSegPlan& g = *(GdSegPlan*)&q->gdplans[(size_t)si * 128];
       const DevSeg& d = q->hsegs[si];
+      // register-staged variants: the tile's load instructions (stage_tile's order: columns, then 64-chunk groups)
+      GdRsPlan& rp = *(GdRsPlan*)&q->gdplans[(size_t)si * 128 + 64];
+      for (int k = 0; k < d.num_staged; ++k) {
+        const int nb = d.stage[k].nbits;
+        const int chunks = (kGdSmSteps / 2) * nb;
+        for (int c0 = 0; c0 < chunks && rp.ins < kGdRsMaxIns; c0 += 64) {
+          const uint64_t src = (uint64_t)(uintptr_t)d.stage[k].words + 16ull * (uint64_t)c0;
+          rp.in[rp.ins].src_lo = (uint32_t)src;
+          rp.in[rp.ins].src_hi = (uint32_t)(src >> 32);
+          rp.in[rp.ins].stride = (uint32_t)(2 * kGdSmSteps * nb * 4);
+          rp.in[rp.ins].lanes = (uint32_t)std::min(64, chunks - c0);
+          rp.in[rp.ins].dst = (uint32_t)(4 * d.stage[k].lds_off + 16 * c0);
+          ++rp.ins;
+        }
+      }
       g.ngb = s.num_group_by;
       g.rpl = P.gd_rp_log2;
       {
@@ -2256,9 +2305,9 @@ int plan_limit_buffers(pa_query* q, const Prep& P, int cus, int64_t total_tiles)
 int upload_descriptors(pa_query* q) {
   int rc;
   if (is_gdense(q->strategy)) {
-    rc = dev_alloc(q->dgdplans, sizeof(GdSegPlan) * q->gdplans.size());
+    rc = dev_alloc(q->dgdplans, sizeof(uint32_t) * q->gdplans.size());
     if (rc) return rc;
-    PA_HIP(hipMemcpy(q->dgdplans.p, q->gdplans.data(), sizeof(GdSegPlan) * q->gdplans.size(), hipMemcpyHostToDevice));
+    PA_HIP(hipMemcpy(q->dgdplans.p, q->gdplans.data(), sizeof(uint32_t) * q->gdplans.size(), hipMemcpyHostToDevice));
     q->hq.gd_plans = (const uint32_t*)q->dgdplans.p;
   }
   rc = dev_alloc(q->dq, sizeof(DevQuery));

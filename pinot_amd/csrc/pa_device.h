@@ -46,12 +46,21 @@ enum ColKind : int32_t { COL_NONE = 0, COL_SV_DICT = 1, COL_SV_RAW = 2, COL_MV_D
 enum Strategy : int32_t {
   STRAT_LDS = 0, STRAT_GLOBAL = 1, STRAT_PEMIT = 2, STRAT_PCOUNT = 3, STRAT_LANE = 4,
   STRAT_LANE_CNT = 5, STRAT_LANE_RAW = 6, STRAT_LANE_DICT = 7, STRAT_GDENSE = 8, STRAT_GDENSE8 = 9,
-  STRAT_GDENSE12 = 10
+  STRAT_GDENSE12 = 10,
+  // STRAT_GDENSE with register-staged tiles (gdense_rs_kernel): 12 waves, 4 tiles of <= 4 instructions in VGPRs; 8 waves,
+  // 3 tiles of <= 12 instructions
+  STRAT_GDENSE_RS12 = 11, STRAT_GDENSE_RS8 = 12
 };
 // STRAT_GDENSE: 4-wave workgroups; STRAT_GDENSE8 / STRAT_GDENSE12: the same kernel with 8- / 12-wave workgroups (2 / 3
 // waves per SIMD when one workgroup fits a CU, e.g. beside a 64 KiB value table: the walk's LDS round trips and VALU
 // issue overlap across waves; 12 waves: step-major tiles only)
-__host__ __device__ constexpr bool is_gdense(int s) { return s == STRAT_GDENSE || s == STRAT_GDENSE8 || s == STRAT_GDENSE12; }
+__host__ __device__ constexpr bool is_gdense(int s) {
+  return s == STRAT_GDENSE || s == STRAT_GDENSE8 || s == STRAT_GDENSE12 || s == STRAT_GDENSE_RS12 || s == STRAT_GDENSE_RS8;
+}
+__host__ __device__ constexpr bool is_gdense_rs(int s) { return s == STRAT_GDENSE_RS12 || s == STRAT_GDENSE_RS8; }
+// register ring of the register-staged variants: tiles in flight + 1, wave instructions per tile at most
+__host__ __device__ constexpr int gd_rs_ring(int s) { return s == STRAT_GDENSE_RS12 ? 4 : 3; }
+__host__ __device__ constexpr int gd_rs_dmax(int s) { return s == STRAT_GDENSE_RS12 ? 4 : 12; }
 // STRAT_GDENSE value sources and LDS operations of one aggregation
 enum GdVs : int32_t {
   GVS_ID = 0,    // the dictId itself (SUM over an affine dictionary shared by every segment; MIN/MAX of a shared sorted one)
@@ -74,6 +83,7 @@ enum GdOp : int32_t {
   GOP_MAX_U = 6
 };
 constexpr int kGdWaves = 4;          // waves per STRAT_GDENSE workgroup (STRAT_GDENSE8: 8)
+constexpr int kGdSmSteps = 16;        // 64-doc steps of a step-major STRAT_GDENSE tile (1024 docs)
 constexpr int kGdMaxKeys = 16384;    // largest LDS key space of STRAT_GDENSE
 __host__ __device__ constexpr bool is_lane(int s) { return s >= STRAT_LANE && s <= STRAT_LANE_DICT; }
 constexpr int kLaneAggs = 4;  // STRAT_LANE: at most this many aggregations (COUNT included)
@@ -94,7 +104,8 @@ __host__ __device__ constexpr bool pemit_hh(int s) { return ((s - kPemitBase) & 
 __host__ __device__ constexpr int pemit_big(int s) { return (s - kPemitBase) >= 16 ? 1 : 0; }
 __host__ __device__ constexpr int scan_waves(int s) {
   return is_pemit(s) && pemit_big(s) ? kEmitBigWaves
-                                       : (s == STRAT_GDENSE8 ? 2 * kGdWaves : (s == STRAT_GDENSE12 ? 3 * kGdWaves : kWavesPerWG));
+                                       : (s == STRAT_GDENSE8 || s == STRAT_GDENSE_RS8) ? 2 * kGdWaves
+                                       : (s == STRAT_GDENSE12 || s == STRAT_GDENSE_RS12) ? 3 * kGdWaves : kWavesPerWG;
 }
 // V record formats (word 0 always holds the key's offset inside its partition, key & ((1 << kshift_v) - 1)):
 //   V_FMT_KEY: COUNT only, one word;  V_FMT_ID: one word, | value id << kshift_v (the value column's table-wide value
@@ -293,6 +304,7 @@ struct DevQuery {
 // lgkmcnt wait, which also waits for every LDS operation in flight).
 constexpr int kGdMaxGb = 3;    // group-by columns
 constexpr int kGdMaxAgg = 6;   // non-COUNT aggregations
+// (gd_plans holds 128 dwords per segment: the GdSegPlan, then the GdRsPlan of the register-staged variants)
 struct GdSegPlan {
   int32_t ngb, nagg, rpl, pad;           // 0..3
   struct {                               // 4 + 6j
@@ -308,6 +320,20 @@ struct GdSegPlan {
   int32_t pad1[6];
 };
 static_assert(sizeof(GdSegPlan) == 256, "one dword per lane");
+// Register-staged tiles (STRAT_GDENSE_RS*): the wave instructions that load one 1024-doc tile of the segment's staged
+// columns into VGPRs — the same 16-byte-per-lane chunks the LDS-DMA would copy — and where each goes in the tile image.
+constexpr int kGdRsMaxIns = 12;
+struct GdRsPlan {
+  int32_t ins, pad;                      // 0, 1: instructions per tile
+  struct {                               // 2 + 5k
+    uint32_t src_lo, src_hi;             // the instruction's first chunk in tile 0 of the column's stream
+    uint32_t stride;                     // bytes per tile
+    uint32_t lanes;                      // lanes with a chunk
+    uint32_t dst;                        // byte offset of the first chunk in the tile image
+  } in[kGdRsMaxIns];
+  int32_t pad1[2];
+};
+static_assert(sizeof(GdRsPlan) == 256, "one dword per lane");
 // part_agg_kernel variant: -1 generic, else sum kind (0 none, 1 + AccSrc) | MIN << 2 | MAX << 3
 constexpr int kVkGeneric = -1;
 __host__ __device__ constexpr int vk_code(int sum_kind, bool mn, bool mx) { return sum_kind | (mn ? 4 : 0) | (mx ? 8 : 0); }

@@ -308,7 +308,6 @@ __device__ __forceinline__ uint32_t gd_tile(uint32_t gt, uint32_t pp, int64_t wt
 }
 
 // Step-major 1024-doc tiles: filter by leaf_bits (bit i of lane l <=> doc 64 i + l) straight into the walk's order.
-constexpr int kGdSmSteps = 16;
 __device__ __forceinline__ uint32_t gd_tile_sm(uint32_t gt, const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
                                                int64_t wt, const uint32_t* img_ptr, uint32_t img, int lane,
                                                uint32_t base, uint32_t& errs) {
@@ -543,7 +542,7 @@ __global__ void __launch_bounds__(WPW * kWave, 1) gdense_kernel(const DevQuery* 
       const int64_t sfirst = cs->first_wtile;
       const int64_t send = min(t1, sfirst + (int64_t)cs->num_wtiles);
       const uint32_t pp = LM ? ((const uint32_t*)(plans + s))[lane] : 0u;
-      const uint32_t gt = gp(q->gd_plans)[(int64_t)s * 64 + lane];  // this segment's GdSegPlan, one dword per lane
+      const uint32_t gt = gp(q->gd_plans)[(int64_t)s * 128 + lane];  // this segment's GdSegPlan, one dword per lane
       for (; t < send; t += WPW) {
         uint32_t slot_off = (uint32_t)(pslot * img_dw);
         wait_tile((int)((ti - t) / WPW - 1), D, slot_off);  // tile t has landed (its younger tiles may still fly)
@@ -555,6 +554,160 @@ __global__ void __launch_bounds__(WPW * kWave, 1) gdense_kernel(const DevQuery* 
     }
   }
   __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // vmcnt(0): no DMA left in flight
+  const int64_t wm = wave_sum_i64((int64_t)matched);
+  const int64_t we = wave_sum_i64((int64_t)errs);
+  if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)wm, RLX);
+  if (lane == 0 && we != 0) __hip_atomic_fetch_add(gp(q->matched_docs) + 3, (unsigned long long)we, RLX);
+  __syncthreads();
+  gd_flush(q_in, segs, lds, tid, WGS);
+}
+
+// ---------------------------------------------------------------- register-staged tiles (STRAT_GDENSE_RS*)
+// The LDS holds the accumulators, the value tables and ONE tile image per wave; the ring of tiles in flight lives in
+// VGPRs: each tile's staged columns are loaded with plain 16-byte global loads — the chunks the LDS-DMA would copy —
+// RS - 1 tiles ahead, and written into the wave's image just before the tile is walked. A 64 KiB value table then no
+// longer limits the bytes in flight per CU (DMA ring: 12 waves x 1 tile of 3 KiB; here 12 waves x 3 tiles). The
+// compiler counts the loads' vmcnt itself (ring slots are compile-time register arrays: the tile loop is unrolled by
+// RS). Used when every segment shares the LDS tables (loaded once) and a tile is at most DM wave instructions.
+template <int DM>
+__device__ __forceinline__ void rs_issue(uint32_t rp, int64_t wt, int lane, u32x4 (&r)[DM]) {
+  const int n = (int)rl(rp, 0);
+#pragma unroll DM
+  for (int k = 0; k < DM; ++k) {
+    const uint64_t src = ((uint64_t)rl(rp, 3 + 5 * k) << 32) | rl(rp, 2 + 5 * k);
+    const uint32_t stride = rl(rp, 4 + 5 * k), lanes = rl(rp, 5 + 5 * k);
+    if (k < n && (uint32_t)lane < lanes) r[k] = *(const AS1 u32x4*)(src + (uint64_t)wt * stride + 16u * (uint32_t)lane);
+  }
+}
+
+template <int DM>
+__device__ __forceinline__ void rs_store(uint32_t rp, uint32_t img, int lane, const u32x4 (&r)[DM]) {
+  const int n = (int)rl(rp, 0);
+#pragma unroll DM
+  for (int k = 0; k < DM; ++k) {
+    const uint32_t lanes = rl(rp, 5 + 5 * k), dst = rl(rp, 6 + 5 * k);
+    if (k < n && (uint32_t)lane < lanes) *lds_at<lds_u32x4_t>(img + dst + 16u * (uint32_t)lane) = r[k];
+  }
+}
+
+// issue cursor: the next tile this wave loads, its segment and that segment's GdRsPlan (one dword per lane)
+struct RsCursor {
+  int64_t ti;
+  int si;
+  int64_t first, end;
+  uint32_t rp;
+};
+
+template <int DM>
+__device__ __forceinline__ void rs_issue_next(CQ* q, const DevSeg* __restrict__ segs, RsCursor& c, int64_t t1, int wpw,
+                                              int lane, u32x4 (&r)[DM]) {
+  if (c.ti < t1) {
+    while (c.ti >= c.end) {
+      ++c.si;
+      c.first = segs[c.si].first_wtile;
+      c.end = c.first + segs[c.si].num_wtiles;
+      c.rp = gp(q->gd_plans)[(int64_t)c.si * 128 + 64 + lane];
+    }
+    rs_issue<DM>(c.rp, c.ti - c.first, lane, r);
+  }
+  c.ti += wpw;
+}
+
+// process cursor: the next tile this wave walks, its segment and that segment's GdSegPlan / GdRsPlan
+struct RsProc {
+  int64_t t;
+  int si;
+  int64_t first, end;
+  uint32_t gt, rp;
+};
+
+template <int RS, int DM>
+struct RsRing {
+  u32x4 s0[DM], s1[DM], s2[RS > 2 ? DM : 1], s3[RS > 3 ? DM : 1];
+};
+
+template <int J, int RS, int DM>
+__device__ __forceinline__ u32x4 (&rs_slot(RsRing<RS, DM>& r))[DM] {
+  if constexpr (J == 0) return r.s0;
+  else if constexpr (J == 1) return r.s1;
+  else if constexpr (J == 2) return r.s2;
+  else return r.s3;
+}
+
+// One tile: issue the next load into slot `refill` (free: its tile was walked last), then walk the tile in `cur`.
+template <int DM>
+__device__ __forceinline__ void rs_step(CQ* q, const DevQuery* __restrict__ q_in, const DevSeg* __restrict__ segs,
+                                        RsCursor& ic, RsProc& pc, int64_t t1, int wpw, int lane, uint32_t img,
+                                        const uint32_t* img_ptr, uint32_t base, uint32_t& matched, uint32_t& errs,
+                                        u32x4 (&refill)[DM], const u32x4 (&cur)[DM]) {
+  rs_issue_next<DM>(q, segs, ic, t1, wpw, lane, refill);
+  while (pc.t >= pc.end) {
+    ++pc.si;
+    pc.first = segs[pc.si].first_wtile;
+    pc.end = pc.first + segs[pc.si].num_wtiles;
+    pc.gt = gp(q->gd_plans)[(int64_t)pc.si * 128 + lane];
+    pc.rp = gp(q->gd_plans)[(int64_t)pc.si * 128 + 64 + lane];
+  }
+  rs_store<DM>(pc.rp, img, lane, cur);
+  matched += gd_tile_sm(pc.gt, q_in, segs + pc.si, pc.t - pc.first, img_ptr, img, lane, base, errs);
+  pc.t += wpw;
+}
+
+template <int WPW, int RS, int DM>
+__global__ void __launch_bounds__(WPW * kWave, 1) gdense_rs_kernel(const DevQuery* __restrict__ q_in,
+                                                                   const DevSeg* __restrict__ segs,
+                                                                   const LmSegPlan* __restrict__, PartScratch) {
+  CQ* q = (CQ*)(uintptr_t)q_in;
+  constexpr int WGS = WPW * kWave;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  unsigned char* lds = (unsigned char*)smem;
+  const uint32_t base = lds_addr(smem);
+  const int img_dw = q->image_dwords_max;
+  uint32_t* const img_ptr = smem + (q->lds_acc_bytes >> 2) + wave * img_dw;
+  const uint32_t img = base + q->lds_acc_bytes + 4u * (uint32_t)(wave * img_dw);
+  gd_init(q, lds, tid, WGS);
+  const int64_t T = q->total_wtiles, G = gridDim.x;
+  const int64_t lb = q->xcd_major ? xcd_major_block(blockIdx.x, G) : (int64_t)blockIdx.x;
+  const int64_t t0 = lb * T / G, t1 = (lb + 1) * T / G;
+  const int nseg = q->num_segments;
+  if (q->gd_tables && t0 < t1) gd_load_tables(q, (CSegT*)(uintptr_t)(segs + find_segment(segs, nseg, t0)), lds, tid, WGS);
+  __syncthreads();
+  uint32_t matched = 0, errs = 0;
+  if (t0 < t1) {
+    // issue cursor (segment, its plan) and process cursor
+    int64_t ti = t0 + wave;
+    int isi = find_segment(segs, nseg, t0);
+    int64_t ifirst = segs[isi].first_wtile, iend = ifirst + segs[isi].num_wtiles;
+    uint32_t rpi = gp(q->gd_plans)[(int64_t)isi * 128 + 64 + lane];
+    int64_t t = ti;
+    int psi = isi;
+    int64_t pfirst = ifirst, pend = iend;
+    uint32_t gt = gp(q->gd_plans)[(int64_t)psi * 128 + lane], rpp = rpi;
+    RsRing<RS, DM> ring;
+    RsCursor ic{ti, isi, ifirst, iend, rpi};
+    RsProc pc{t, psi, pfirst, pend, gt, rpp};
+    rs_issue_next<DM>(q, segs, ic, t1, WPW, lane, ring.s0);
+    if constexpr (RS > 2) rs_issue_next<DM>(q, segs, ic, t1, WPW, lane, ring.s1);
+    if constexpr (RS > 3) rs_issue_next<DM>(q, segs, ic, t1, WPW, lane, ring.s2);
+    while (pc.t < t1) {
+      // one tile per ring slot, every slot a compile-time register set: issue into the slot the last tile used, then
+      // store this slot's tile into the wave's image and walk it
+      rs_step<DM>(q, q_in, segs, ic, pc, t1, WPW, lane, img, img_ptr, base, matched, errs, rs_slot<RS - 1, RS, DM>(ring), ring.s0);
+      if (pc.t >= t1) break;
+      rs_step<DM>(q, q_in, segs, ic, pc, t1, WPW, lane, img, img_ptr, base, matched, errs, ring.s0, ring.s1);
+      if (pc.t >= t1) break;
+      if constexpr (RS > 2) {
+        rs_step<DM>(q, q_in, segs, ic, pc, t1, WPW, lane, img, img_ptr, base, matched, errs, ring.s1, ring.s2);
+        if (pc.t >= t1) break;
+      }
+      if constexpr (RS > 3) {
+        rs_step<DM>(q, q_in, segs, ic, pc, t1, WPW, lane, img, img_ptr, base, matched, errs, ring.s2, ring.s3);
+      }
+    }
+  }
   const int64_t wm = wave_sum_i64((int64_t)matched);
   const int64_t we = wave_sum_i64((int64_t)errs);
   if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)wm, RLX);

@@ -502,7 +502,7 @@ class GpuQueryExecutor:
         names = ("strategy", "steps", "dma_slots", "ring", "wg_per_cu", "grid", "lds_bytes")
         out["plan"] = {n: v.value for n, v in zip(names, vals)}
         out["plan"]["strategy"] = {0: "lds", 1: "global", 2: "partitioned", 4: "lane", 5: "lane", 6: "lane", 7: "lane",
-                                    8: "lds_dense", 9: "lds_dense", 10: "lds_dense"}[out["plan"]["strategy"]]
+                                    8: "lds_dense", 9: "lds_dense", 10: "lds_dense", 11: "lds_dense", 12: "lds_dense"}[out["plan"]["strategy"]]
         out["plan"]["eager_literals"] = int(L.lib().pa_query_num_eager_literals(self.handle))
         out["plan"]["lane_major"] = int(L.lib().pa_query_lane_major(self.handle))
         out["plan"]["limit_trimming"] = int(L.lib().pa_query_limit_trimming(self.handle))
