@@ -557,6 +557,7 @@ struct pa_query {
   DevBuf merge_buf;  // pa_query_pack_rows / pa_query_merge_rows: row -> slot map and counters (grown on demand)
   DevBuf leap_buf;  // PA_QF_FILTER_STATS fused into the scan: per segment (matched docs, leaps, gave up)
   int leap_leaf = -1;  // the eager leaf (spec order) when the scan counts the leaps
+  int64_t leap_slices = 0;
   std::vector<LmSegPlan> hplans;
   std::vector<uint32_t> gdplans;  // STRAT_GDENSE: per-segment parameter tables (GdSegPlan + GdRsPlan, 128 dwords)
   DevBuf dgdplans;
@@ -2461,7 +2462,7 @@ int pa_query_bind_value_remap(pa_query* q, int32_t index, int32_t agg, const int
 
 // counters + list length + overflow flag of the fused statistics (pa_scan.h "fused execution statistics")
 static size_t leap_header_bytes(const pa_query* q) {
-  return ((size_t)std::max(1, q->nseg) * 3 + 2) * sizeof(unsigned long long);
+  return ((size_t)std::max(1, q->nseg) * 3 + 1 + (size_t)q->leap_slices) * sizeof(unsigned long long);
 }
 
 // PA_QF_FILTER_STATS: the scan counts the leap-frog statistics itself (leap_tile) when the filter is an AND of two
@@ -2480,15 +2481,26 @@ static int plan_leaps(pa_query* q, const Prep& P) {
   }
   if (q->partitioned || q->limit_mode || q->limit_walk || is_gdense(q->strategy)) return PA_OK;
   if (P.first_clause_sel > 1.0 / 256.0) return PA_OK;
-  // list capacity: twice the E docs the planner's estimate allows (its overflow only costs the bitmap fallback)
-  const int64_t cap = (int64_t)(2.0 * P.first_clause_sel * (double)q->num_docs) + 65536;
-  int rc = dev_alloc(q->leap_buf, ((size_t)std::max(1, q->nseg) * 3 + 2 + (size_t)cap) * sizeof(unsigned long long));
+  q->hq.leap_mode = 1;
+  q->leap_leaf = q->literals[0].leaf;
+  return PA_OK;
+}
+
+// The fused statistics' buffer (layout: pa_scan.h "fused execution statistics"), once the grid is known: one list
+// slice per scan wave, each 16 x the E docs the planner's estimate gives a wave (a slice that overflows only costs
+// the bitmap fallback).
+static int alloc_leaps(pa_query* q, const Prep& P) {
+  if (!q->hq.leap_mode) return PA_OK;
+  const int64_t slices = (int64_t)q->grid * scan_waves(q->strategy);
+  const int64_t cap = (int64_t)(16.0 * P.first_clause_sel * (double)q->num_docs / (double)slices) + 256;
+  q->leap_slices = slices;
+  const size_t words = (size_t)std::max(1, q->nseg) * 3 + 1 + (size_t)slices + (size_t)slices * (size_t)cap;
+  int rc = dev_alloc(q->leap_buf, words * sizeof(unsigned long long));
   if (rc) return rc;
   PA_HIP(hipMemset(q->leap_buf.p, 0, leap_header_bytes(q)));
-  q->hq.leap_mode = 1;
   q->hq.leap_out = (unsigned long long*)q->leap_buf.p;
   q->hq.leap_cap = cap;
-  q->leap_leaf = q->literals[0].leaf;
+  q->hq.leap_slices = slices;
   return PA_OK;
 }
 
@@ -2584,6 +2596,8 @@ int pa_query_prepare(pa_query* q) {
     rc = plan_limit_buffers(q, P, cus, total_tiles);
     if (rc) return rc;
   }
+  rc = alloc_leaps(q, P);
+  if (rc) return rc;
   rc = upload_descriptors(q);
   if (rc) return rc;
   PA_HIP(hipDeviceSynchronize());
@@ -3314,10 +3328,10 @@ int pa_query_leap_counts(const pa_query* q, int64_t* out, void* stream) {
   if (q->leap_leaf < 0) return fail(PA_EINVAL, "the scan does not count the filter statistics (pa_query_leap_leaf)");
   if (!out) return fail(PA_EINVAL, "null output");
   hipStream_t st = (hipStream_t)stream;
-  std::vector<int64_t> h((size_t)q->nseg * 3 + 2);
+  std::vector<int64_t> h((size_t)q->nseg * 3 + 1);
   PA_HIP(hipMemcpyAsync(h.data(), q->leap_buf.p, h.size() * sizeof(int64_t), hipMemcpyDeviceToHost, st));
   PA_HIP(hipStreamSynchronize(st));
-  const bool overflow = h[(size_t)q->nseg * 3 + 1] != 0;  // (the E-doc list was full: no segment's leaps are known)
+  const bool overflow = h[(size_t)q->nseg * 3] != 0;  // (a wave's E-doc slice was full: no segment's leaps are known)
   for (int si = 0; si < q->nseg; ++si) {
     out[3 * si] = h[3 * si];
     out[3 * si + 1] = h[3 * si + 1];

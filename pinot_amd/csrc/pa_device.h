@@ -297,7 +297,8 @@ struct DevQuery {
   int32_t leap_mode;
   int32_t pad_leap;
   unsigned long long* leap_out;  // (layout: pa_scan.h "fused execution statistics")
-  int64_t leap_cap;              // list capacity (E docs)
+  int64_t leap_cap;              // list entries per scan wave (E docs)
+  int64_t leap_slices;           // scan waves (grid x waves per workgroup): one list slice each
 };
 // STRAT_GDENSE per-segment parameter table: 64 dwords, loaded once per segment into ONE VGPR (lane k holds dword k)
 // and read back with v_readlane at compile-time lanes, so the doc loop never issues a scalar load (an SMEM wait is an

@@ -1517,34 +1517,35 @@ hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t*
 // wave-wide neighbour search over both leaves; the leaps go into the segments' counters.
 __global__ void __launch_bounds__(256) leap_search_kernel(const DevQuery* __restrict__ q, const DevSeg* __restrict__ segs) {
   const int lane = threadIdx.x & (kWave - 1);
-  const int nseg = q->num_segments;
-  const AS1 unsigned long long* hdr = gp(q->leap_out) + 3 * (int64_t)nseg;
-  if (hdr[1]) return;  // (the list overflowed: the host takes every segment's counts from leaf bitmaps)
-  const int64_t n = (int64_t)min(hdr[0], (unsigned long long)q->leap_cap);
-  const int64_t total = n + nseg;
+  const int64_t nseg = q->num_segments, slices = q->leap_slices, cap = q->leap_cap;
+  const AS1 unsigned long long* hdr = gp(q->leap_out) + 3 * nseg;
+  if (hdr[0]) return;  // (a slice overflowed: the host takes every segment's counts from leaf bitmaps)
   const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t w = (int64_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); w < total; w += waves) {
-    int si;
-    uint32_t leaps = 0u, gave = 0u;
-    if (w < n) {
-      const uint64_t ent = gp(q->leap_out)[3 * (int64_t)nseg + 2 + w];
-      si = (int)(ent >> 40);
-      const int64_t doc = (int64_t)((ent >> 1) & ((1ull << 39) - 1ull));
-      const uint32_t succ = leap_search(segs + si, doc + 1, 1, lane);
-      leaps += succ == 1u;
-      gave |= succ == 4u;
-      if (!(ent & 1ull)) {
-        const uint32_t pred = leap_search(segs + si, doc - 1, -1, lane);
-        leaps += pred == 1u;
-        gave |= pred == 4u;
+  // wave w: slice w (every entry of it), then the segment starts
+  for (int64_t w = (int64_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); w < slices + nseg; w += waves) {
+    if (w < slices) {
+      const int64_t n = (int64_t)hdr[1 + w];
+      const AS1 unsigned long long* list = hdr + 1 + slices + w * cap;
+      for (int64_t k = 0; k < n; ++k) {
+        const uint64_t ent = list[k];
+        const int si = (int)(ent >> 40);
+        const int64_t doc = (int64_t)((ent >> 1) & ((1ull << 39) - 1ull));
+        uint32_t leaps = 0u, gave = 0u;
+        const uint32_t succ = leap_search(segs + si, doc + 1, 1, lane);
+        leaps += succ == 1u;
+        gave |= succ == 4u;
+        if (!(ent & 1ull)) {
+          const uint32_t pred = leap_search(segs + si, doc - 1, -1, lane);
+          leaps += pred == 1u;
+          gave |= pred == 4u;
+        }
+        leap_add(q, si, 0u, leaps, gave, lane);
       }
     } else {
-      si = (int)(w - n);
+      const int si = (int)(w - slices);
       const uint32_t first = leap_search(segs + si, 0, 1, lane);
-      leaps += first == 1u;
-      gave |= first == 4u;
+      leap_add(q, si, 0u, first == 1u ? 1u : 0u, first == 4u ? 1u : 0u, lane);
     }
-    leap_add(q, si, 0u, leaps, gave, lane);
   }
 }
 

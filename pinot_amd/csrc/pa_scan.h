@@ -842,8 +842,9 @@ __device__ __forceinline__ bool leaf_match_doc(const DevLeaf& L, int64_t doc) {
 // labelled doc (so never past the neighbouring E doc) — in the scan itself every search step's load would wait behind
 // the tile ring's in-flight DMA. The planner enables this only for a sparse E; a search that gives up
 // (kLeapSearchSteps) or a full list flags the segment(s), whose counts the host then takes from leaf bitmaps.
-// leap_out: [3 s]: segment s's matched docs, leaps, gave-up flag; [3 nseg]: listed docs; [3 nseg + 1]: list overflow;
-// [3 nseg + 2 ..]: the list, one (segment << 40 | doc << 1 | both) per E doc.
+// leap_out: [3 s]: segment s's matched docs, leaps, gave-up flag; [3 nseg]: list overflow flag; [3 nseg + 1 + w]: the
+// docs wave w of the scan listed; then the list: wave w's slice of leap_cap entries at [3 nseg + 1 + slices + w cap],
+// one (segment << 40 | doc << 1 | both) per E doc (a wave appends to its own slice: no atomic, no wait).
 constexpr int kLeapSearchSteps = 64;  // 4096 docs
 
 // Label of the nearest labelled doc at or beyond `from` in direction dir (+1 / -1) inside the segment: 1, 2, 3; 0 if
@@ -878,7 +879,7 @@ __device__ __forceinline__ void leap_add(const DevQuery* __restrict__ q, int seg
 // tile's matched docs into the segment's counter. LM: doc of bit i of lane l = 32 l + i, else 64 i + l.
 template <int LM>
 __device__ __noinline__ void leap_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int64_t doc_base,
-                                       uint32_t e, uint32_t f, int lane) {
+                                       uint32_t e, uint32_t f, int lane, uint32_t slice, uint32_t& listed) {
   const uint32_t mine = (uint32_t)__builtin_popcount(e);
   uint32_t incl = mine;
 #pragma unroll
@@ -891,25 +892,22 @@ __device__ __noinline__ void leap_tile(const DevQuery* __restrict__ q, const Dev
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) matched += (uint32_t)__shfl_xor((int)matched, o, kWave);
   const int si = seg->index;
-  const int nseg = q->num_segments;
-  unsigned long long* hdr = q->leap_out + 3 * (int64_t)nseg;
-  unsigned long long base = 0;
-  if (lane == 0 && total) base = atomicAdd(hdr, (unsigned long long)total);
-  base = (unsigned long long)__shfl((long long)base, 0, kWave);
-  const unsigned long long cap = (unsigned long long)q->leap_cap;
-  if (total && base + total > cap) {
-    if (lane == 0) atomicOr(hdr + 1, 1ull);  // (the host then takes every segment's counts from leaf bitmaps)
+  const int64_t nseg = q->num_segments;
+  const uint64_t cap = (uint64_t)q->leap_cap;
+  if ((uint64_t)listed + total > cap) {
+    if (lane == 0) atomicOr(q->leap_out + 3 * nseg, 1ull);  // (the host then takes every segment's counts from bitmaps)
   } else {
-    unsigned long long pos = base + (incl - mine);
+    AS1 unsigned long long* list =
+        gp(q->leap_out) + 3 * nseg + 1 + (int64_t)q->leap_slices + (int64_t)slice * (int64_t)cap;
+    uint32_t pos = listed + (incl - mine);
     while (e) {
       const int i = __builtin_ctz(e);
       e &= e - 1u;
       const int64_t doc = doc_base + (LM ? 32 * lane + i : kWave * i + lane);
-      const uint64_t both = (f >> i) & 1u;
-      gp(q->leap_out)[3 * (int64_t)nseg + 2 + (int64_t)pos++] =
-          ((uint64_t)si << 40) | ((uint64_t)doc << 1) | both;
+      list[pos++] = ((uint64_t)si << 40) | ((uint64_t)doc << 1) | ((f >> i) & 1u);
     }
   }
+  listed += total;
   leap_add(q, si, matched, 0u, 0u, lane);
 }
 
@@ -1672,6 +1670,8 @@ struct LaneAcc {
   uint32_t id;     // LDS byte address of aggregation 0's dictId slot of this thread
   uint32_t astr;   // bytes between aggregations' pair slots (16 * WGS); dictId slots: astr / 4
   uint32_t idm;    // bit a: aggregation a's dictId was updated in the current segment run
+  // fused execution statistics: this wave's slice of the E-doc list and the entries written so far
+  uint32_t leap_slice, leap_n;
 };
 typedef __attribute__((address_space(3))) int64_t lds_i64_t;
 __device__ __forceinline__ void la_get(const LaneAcc& la, int a, int64_t& r0, int64_t& r1) {
@@ -2165,7 +2165,7 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
       if (!ok) m &= ~bit;
     }
     if constexpr (STRAT != STRAT_PCOUNT && !is_pemit(STRAT))
-      if (q->leap_mode) leap_tile<LM>(q, seg, doc_base, eager, m, lane);
+      if (q->leap_mode) leap_tile<LM>(q, seg, doc_base, eager, m, lane, la.leap_slice, la.leap_n);
     if (__ballot(m != 0) == 0) return 0;
   }
   const uint32_t scanned = m;  // numDocsScanned counts every doc the filter kept, admitted or not
@@ -2524,6 +2524,8 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
 
   uint32_t matched = 0;  // docs of this lane that passed the filter (numDocsScanned)
   LaneAcc la;
+  la.leap_slice = (uint32_t)((q->xcd_major ? xcd_major_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x) * WPW + wave);
+  la.leap_n = 0u;
   if constexpr (is_lane(STRAT) && STRAT != STRAT_LANE_CNT) lane_acc_init(q, la, smem, WGS);
   if constexpr (STRAT == STRAT_LANE_DICT) {  // the dictId histograms of SUMs over a shared dictionary
     for (int a = 0; a < q->num_aggs; ++a) {
@@ -2657,6 +2659,9 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
     }
   }
 
+  if constexpr (STRAT != STRAT_PCOUNT && !is_pemit(STRAT))
+    if (q->leap_mode && lane == 0)  // (every wave: the search kernel reads every slice's count)
+      gp(q->leap_out)[3 * (int64_t)q->num_segments + 1 + la.leap_slice] = la.leap_n;
   if (!is_pemit(STRAT)) {  // (the partitioned count pass counts numDocsScanned; its emit pass sees the same docs)
     const int64_t wm = wave_sum_i64((int64_t)matched);
     if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)wm, RLX);
