@@ -312,8 +312,12 @@ __device__ __forceinline__ uint32_t gd_tile_sm(uint32_t gt, const DevQuery* __re
                                                int64_t wt, const uint32_t* img_ptr, uint32_t img, int lane,
                                                uint32_t base, uint32_t& errs) {
   constexpr int ST = kGdSmSteps;
+  // descriptors through the constant address space (scalar loads): a flat load of a descriptor field would be counted
+  // in vmcnt, and waiting for it would wait for every tile in flight
+  CSegT* cs = (CSegT*)(uintptr_t)uniform_ptr(seg);
+  CQ* cq = (CQ*)(uintptr_t)uniform_ptr(q);
   const int64_t doc_base = wt * (ST * kWave);
-  const int64_t rem = (int64_t)seg->num_docs - doc_base;
+  const int64_t rem = (int64_t)cs->num_docs - doc_base;
   uint32_t m;
   if (rem >= ST * kWave) {
     m = (1u << ST) - 1u;
@@ -322,9 +326,9 @@ __device__ __forceinline__ uint32_t gd_tile_sm(uint32_t gt, const DevQuery* __re
     m = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
   }
   uint32_t clause = 0;
-  const int neager = q->num_eager;
+  const int neager = cq->num_eager;
   for (int li = 0; li < neager; ++li) {
-    const DevLeaf& L = seg->leaves[li];
+    const auto& L = cs->leaves[li];
     clause |= leaf_bits<ST>(L, img_ptr, doc_base, lane);
     if (L.clause_end) {
       m &= clause;
@@ -569,14 +573,22 @@ __global__ void __launch_bounds__(WPW * kWave, 1) gdense_kernel(const DevQuery* 
 // longer limits the bytes in flight per CU (DMA ring: 12 waves x 1 tile of 3 KiB; here 12 waves x 3 tiles). The
 // compiler counts the loads' vmcnt itself (ring slots are compile-time register arrays: the tile loop is unrolled by
 // RS). Used when every segment shares the LDS tables (loaded once) and a tile is at most DM wave instructions.
+// Every tile issues exactly DM load instructions on every lane, unconditionally (an unused instruction re-reads
+// instruction 0's chunk, a lane past a column's chunks re-reads the column's last one): the compiler's in-order vmcnt
+// accounting then waits for exactly the ring slot being consumed. (A predicated load may or may not count, so the
+// compiler would wait for vmcnt(0) — every tile in flight — before each tile.)
 template <int DM>
 __device__ __forceinline__ void rs_issue(uint32_t rp, int64_t wt, int lane, u32x4 (&r)[DM]) {
   const int n = (int)rl(rp, 0);
+  const uint64_t src0 = ((uint64_t)rl(rp, 3) << 32) | rl(rp, 2);
+  const uint32_t stride0 = rl(rp, 4), lanes0 = rl(rp, 5);
 #pragma unroll DM
   for (int k = 0; k < DM; ++k) {
-    const uint64_t src = ((uint64_t)rl(rp, 3 + 5 * k) << 32) | rl(rp, 2 + 5 * k);
-    const uint32_t stride = rl(rp, 4 + 5 * k), lanes = rl(rp, 5 + 5 * k);
-    if (k < n && (uint32_t)lane < lanes) r[k] = *(const AS1 u32x4*)(src + (uint64_t)wt * stride + 16u * (uint32_t)lane);
+    const bool use = k < n;  // (wave-uniform)
+    const uint64_t src = use ? (((uint64_t)rl(rp, 3 + 5 * k) << 32) | rl(rp, 2 + 5 * k)) : src0;
+    const uint32_t stride = use ? rl(rp, 4 + 5 * k) : stride0, lanes = use ? rl(rp, 5 + 5 * k) : lanes0;
+    const uint32_t l = (uint32_t)lane < lanes ? (uint32_t)lane : lanes - 1u;
+    r[k] = *(const AS1 u32x4*)(src + (uint64_t)wt * stride + 16u * l);
   }
 }
 
@@ -603,9 +615,10 @@ __device__ __forceinline__ void rs_issue_next(CQ* q, const DevSeg* __restrict__ 
                                               int lane, u32x4 (&r)[DM]) {
   if (c.ti < t1) {
     while (c.ti >= c.end) {
-      ++c.si;
-      c.first = segs[c.si].first_wtile;
-      c.end = c.first + segs[c.si].num_wtiles;
+      c.si = __builtin_amdgcn_readfirstlane(c.si + 1);
+      CSegT* sg = (CSegT*)(uintptr_t)uniform_ptr(segs + c.si);
+      c.first = sg->first_wtile;
+      c.end = c.first + sg->num_wtiles;
       c.rp = gp(q->gd_plans)[(int64_t)c.si * 128 + 64 + lane];
     }
     rs_issue<DM>(c.rp, c.ti - c.first, lane, r);
@@ -642,14 +655,16 @@ __device__ __forceinline__ void rs_step(CQ* q, const DevQuery* __restrict__ q_in
                                         u32x4 (&refill)[DM], const u32x4 (&cur)[DM]) {
   rs_issue_next<DM>(q, segs, ic, t1, wpw, lane, refill);
   while (pc.t >= pc.end) {
-    ++pc.si;
-    pc.first = segs[pc.si].first_wtile;
-    pc.end = pc.first + segs[pc.si].num_wtiles;
+    pc.si = __builtin_amdgcn_readfirstlane(pc.si + 1);
+    CSegT* sg = (CSegT*)(uintptr_t)uniform_ptr(segs + pc.si);
+    pc.first = sg->first_wtile;
+    pc.end = pc.first + sg->num_wtiles;
     pc.gt = gp(q->gd_plans)[(int64_t)pc.si * 128 + lane];
     pc.rp = gp(q->gd_plans)[(int64_t)pc.si * 128 + 64 + lane];
   }
   rs_store<DM>(pc.rp, img, lane, cur);
-  matched += gd_tile_sm(pc.gt, q_in, segs + pc.si, pc.t - pc.first, img_ptr, img, lane, base, errs);
+  // (a wave-uniform segment pointer: its descriptor fields are scalar loads, which do not wait for the ring's loads)
+  matched += gd_tile_sm(pc.gt, q_in, uniform_ptr(segs + pc.si), pc.t - pc.first, img_ptr, img, lane, base, errs);
   pc.t += wpw;
 }
 

@@ -681,8 +681,8 @@ __device__ void accumulate_doc_mv(const DevQuery* __restrict__ q, const DevSeg* 
 
 // Match word of one leaf over a whole wave tile: bit i of lane l <=> doc 64*i + l of the tile matches.
 // Leaf parameters are loaded once per tile; the 32 decodes are independent, so the LDS reads pipeline.
-template <int STEPS>
-__device__ __forceinline__ uint32_t leaf_bits(const DevLeaf& L, const uint32_t* img, int64_t doc_base, int lane) {
+template <int STEPS, class LeafT = DevLeaf>
+__device__ __forceinline__ uint32_t leaf_bits(const LeafT& L, const uint32_t* img, int64_t doc_base, int lane) {
   uint32_t bits = 0;
   if (L.kind == PA_LEAF_DICT_RANGE || L.kind == PA_LEAF_DICT_SET) {
     const int nb = L.nbits;
