@@ -859,6 +859,25 @@ int plan_key_space(pa_query* q, Prep& P) {
   return PA_OK;
 }
 
+// The one multi-value group-by component (multi-value in every segment) of a query that partitions or walks its
+// (doc, value) pairs: its index, -1 when no group-by column is multi-value anywhere, -2 when several are or one is
+// multi-value in some segments only (the per-doc expansion paths run those).
+int mv_group_component(const pa_query* q) {
+  const pa_query_spec& s = q->spec;
+  int comp = -1;
+  for (int j = 0; j < s.num_group_by; ++j) {
+    int nmv = 0;
+    for (int si = 0; si < q->nseg; ++si) {
+      auto it = q->segs[si]->cols.find(s.group_by_columns[j]);
+      nmv += it != q->segs[si]->cols.end() && it->second->kind == COL_MV_DICT;
+    }
+    if (nmv == 0) continue;
+    if (nmv != q->nseg || comp >= 0) return -2;
+    comp = j;
+  }
+  return comp;
+}
+
 // numGroupsLimit. The reference caps each segment's group table at numGroupsLimit first-seen groups
 // (DictionaryBasedGroupKeyGenerator._globalGroupIdUpperBound, NoDictionary*GroupKeyGenerator). It can only bind when a
 // segment can hold that many distinct keys: min(product of its key cardinalities (a raw column: its docs), its
@@ -898,11 +917,15 @@ int plan_limit(pa_query* q, Prep& P) {
   }
   while (P.limit_eb < 63 && (uint64_t(1) << P.limit_eb) < max_exp) ++P.limit_eb;
   // Walk form: one key per doc (no MV group-by) in a direct key space; its bitmaps (LDS while they fit, else HBM)
-  // take at most kWalkMaxBitmapBytes
+  // take at most kWalkMaxBitmapBytes. One MV group-by column (keys per (doc, value) pair): the bitmap and its round
+  // snapshot in LDS.
   int64_t nbind = 0;
   for (int si = 0; si < q->nseg; ++si) nbind += P.limit_bind[si] ? 1 : 0;
-  if (q->limit_mode && !q->hashed && max_exp == 1 && (uint64_t)nbind * (uint64_t)((q->num_keys + 31) / 32) * 4 <=
-      kWalkMaxBitmapBytes && !(s.flags & PA_QF_NO_LIMIT_WALK)) {
+  const int64_t words = (q->num_keys + 31) / 32;
+  const int mvc = mv_group_component(q);
+  const bool walk_ok = (mvc == -1 && max_exp == 1) || (mvc >= 0 && 2 * words <= kWalkMaxWords);
+  if (q->limit_mode && !q->hashed && walk_ok &&
+      (uint64_t)nbind * (uint64_t)words * 4 <= kWalkMaxBitmapBytes && !(s.flags & PA_QF_NO_LIMIT_WALK)) {
     q->limit_mode = false;
     q->limit_walk = true;
     q->walk_words = (q->num_keys + 31) / 32;
@@ -1622,6 +1645,10 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
     ++nv;
   }
   const bool vstream = nv > 0 || hll < 0;
+  // a multi-value group-by column: one V record per (doc, value) pair (V stream only; one such column, multi-value in
+  // every segment)
+  const int mvc = mv_group_component(q);
+  if (mvc == -2 || (mvc >= 0 && hll >= 0)) { PLAN_LOG("partitioned: no (exit 10)"); return false; }
   // V record format: one payload slot per distinct (column, value source); SUM/MIN/MAX of one column share it
   std::vector<int> pay(s.num_aggs, 0);
   int words = 1, slots = 0, va = -1;
@@ -1720,6 +1747,7 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
     W = words;
   }
   if (W > kMaxVWords) { PLAN_LOG("partitioned: no (exit 7)"); return false; }
+  if (mvc >= 0 && fmt == V_FMT_GEN) { PLAN_LOG("partitioned: no (exit 12)"); return false; }
   // bins: a full bin is whole 128-byte lines (V: BS * W * 4 bytes; H: 32 four-byte records)
   int bs_v = vstream ? 128 / std::gcd(128, 4 * W) : 0;
   int bs_h = hll >= 0 ? 32 : 0;
@@ -2018,7 +2046,7 @@ int plan_kernels(pa_query* q, Prep& P, TilePlan& plan, TilePlan& count_plan) {
   q->partitioned = false;
   PLAN_LOG("K=%lld strategy=%d dense=%d (post density %.3g) gb_mv=%d hashed=%d limit=%d", (long long)K, q->strategy,
            (int)P.dense, P.post_density, (int)P.gb_mv, (int)q->hashed, (int)q->limit_mode);
-  if (q->strategy == STRAT_GLOBAL && P.dense && !P.gb_mv && !q->hashed && !q->limit_mode &&
+  if (q->strategy == STRAT_GLOBAL && P.dense && !q->hashed && !q->limit_mode &&
       !(s.flags & (PA_QF_NO_PARTITION | PA_QF_FORCE_GLOBAL)) && K < (int64_t(1) << 32)) {
     TilePlan e;
     if (plan_partitions(q, P, e, count_plan)) {
@@ -2108,6 +2136,7 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
     h.ht_keys = (long long*)q->sections[q->keys_section].ptr;
   }
   h.has_mv = q->has_mv;
+  h.gb_mv = std::max(-1, mv_group_component(q));
   h.xcd_major = (P.dense || is_gdense(q->strategy)) ? 1 : 0;
   h.lds_count_off = 0;
   h.lds_acc_bytes = (q->strategy == STRAT_LDS || is_gdense(q->strategy) || is_lane(q->strategy))
@@ -2227,7 +2256,15 @@ int plan_scratch(pa_query* q, const Prep& P) {
   const DevQuery& h = q->hq;
   const size_t G = (size_t)q->grid, Pn = (size_t)h.num_parts;
   uint64_t vrecs = 0, hrecs = 0;
-  if (h.pv > 0) vrecs = q->num_docs + (uint64_t)G * h.pv * (h.bs_v - 1);
+  if (h.pv > 0) {
+    vrecs = q->num_docs;
+    if (mv_group_component(q) >= 0) {  // one record per (doc, value) pair
+      vrecs = 0;
+      for (const pa_segment* seg : q->segs)
+        vrecs += (uint64_t)seg->cols.at(q->spec.group_by_columns[mv_group_component(q)])->total_values;
+    }
+    vrecs += (uint64_t)G * h.pv * (h.bs_v - 1);
+  }
   if (h.hll_agg >= 0) {
     const int32_t cid = q->spec.aggs[h.hll_agg].column_id;
     for (const pa_segment* seg : q->segs) {
@@ -2626,7 +2663,8 @@ int pa_query_scan(pa_query* q, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (q->limit_walk) {  // admitted keys of every segment where the limit can bind, before any pass tests them
     if (q->walk_words > kWalkMaxWords) PA_HIP(hipMemsetAsync(q->lim_admit.p, 0, q->lim_admit.n, st));
-    PA_HIP(launch_limit_walk((const DevQuery*)q->dq.p, (const DevSeg*)q->dsegs.p, q->nseg, q->walk_words, st));
+    PA_HIP(launch_limit_walk((const DevQuery*)q->dq.p, (const DevSeg*)q->dsegs.p, q->nseg, q->walk_words,
+                             q->hq.gb_mv >= 0, st));
   }
   if (q->limit_mode) {  // first-seen positions, per-segment selection of the threshold, admitted aggregation
     const DevQuery* dq = (const DevQuery*)q->dq.p;

@@ -332,7 +332,148 @@ __global__ void __launch_bounds__(kWalkThreads) limit_walk_kernel(const DevQuery
   if (reached && tid == 0) __hip_atomic_fetch_add(gp(q->matched_docs) + 2, 1ull, RLX);  // numGroupsLimitReached
 }
 
-hipError_t launch_limit_walk(const DevQuery* q, const DevSeg* segs, int nseg, int64_t words, hipStream_t s) {
+// ---- walk form with one multi-value group-by column (q->gb_mv): a doc brings one key per value, in the reference's
+// order (doc, then value index: getIntRawKeys with one MV column; a repeated value is not new the second time).
+// Rounds as in limit_walk_kernel, each from a snapshot of the LDS bitmap; the round in which the count reaches L is
+// rolled back to its snapshot and replayed by one wave, 64 keys at a time in (doc, value) order (each lane finds the
+// doc of its key by a binary search over the inclusive prefix sums of the 64 docs' value counts).
+__device__ __forceinline__ void walk_doc_mv(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int64_t doc,
+                                            uint32_t& base, int32_t& v0, uint32_t& n) {
+  base = 0u;
+  v0 = 0;
+  n = 0u;
+  if (doc >= seg->num_docs || !doc_passes(q, seg, doc)) return;
+  for (int j = 0; j < q->num_gb; ++j)
+    if (j != q->gb_mv)
+      base += (uint32_t)gb_component<true>(seg->cols[q->gb_slot[j]], seg->remap[j], nullptr, 0, doc) *
+              (uint32_t)q->gb_stride[j];
+  const int32_t* off = seg->cols[q->gb_slot[q->gb_mv]].mv_off;
+  v0 = gp(off)[doc];
+  n = (uint32_t)(gp(off)[doc + 1] - v0);
+}
+
+__device__ __forceinline__ uint32_t walk_mv_key(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                                uint32_t base, int64_t v) {
+  const int j = q->gb_mv;
+  const DevCol& c = seg->cols[q->gb_slot[j]];
+  uint32_t id = decode_global(c.words, v, c.nbits);
+  if (seg->remap[j] != nullptr) id = (uint32_t)gp(seg->remap[j])[id];
+  return base + id * (uint32_t)q->gb_stride[j];
+}
+
+__global__ void __launch_bounds__(kWalkThreads) limit_walk_mv_kernel(const DevQuery* __restrict__ q,
+                                                                      const DevSeg* __restrict__ segs, int64_t words) {
+  extern __shared__ uint32_t lds_walk[];
+  __shared__ uint32_t round_new[2];
+  uint32_t* seen = lds_walk;
+  uint32_t* snap = lds_walk + words;
+  const DevSeg* seg = segs + blockIdx.x;
+  uint32_t* adm = (uint32_t*)seg->admit;
+  if (adm == nullptr) return;  // (workgroup-uniform)
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  for (int64_t w = tid; w < words; w += kWalkThreads) seen[w] = 0u;
+  const int64_t L = q->num_groups_limit;
+  const int64_t nd = seg->num_docs;
+  int64_t cnt = 0;
+  bool reached = false;
+  int par = 0;
+  __syncthreads();
+  for (int64_t d0 = 0; d0 < nd && !reached; d0 += kWalkRound, par ^= 1) {
+    for (int64_t w = tid; w < words; w += kWalkThreads) snap[w] = seen[w];
+    if (tid == 0) round_new[par] = 0u;
+    __syncthreads();
+    uint32_t nnew = 0;
+    for (int k = 0; k < kWalkPerThread; ++k) {
+      uint32_t base, n;
+      int32_t v0;
+      walk_doc_mv(q, seg, d0 + (int64_t)k * kWalkThreads + tid, base, v0, n);
+      for (uint32_t e = 0; e < n; ++e) {
+        const uint32_t key = walk_mv_key(q, seg, base, (int64_t)v0 + e);
+        const uint32_t b = 1u << (key & 31u);
+        if (!(atomicOr(seen + (key >> 5), b) & b)) ++nnew;
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) nnew += (uint32_t)__shfl_xor((int)nnew, o, kWave);
+    if (lane == 0 && nnew) atomicAdd(&round_new[par], nnew);
+    __syncthreads();
+    const int64_t rn = round_new[par];  // workgroup-uniform
+    if (cnt + rn < L) {
+      cnt += rn;
+      continue;
+    }
+    for (int64_t w = tid; w < words; w += kWalkThreads) seen[w] = snap[w];  // roll the round back
+    __syncthreads();
+    if (tid < kWave) {
+      for (int64_t b = d0; b < d0 + kWalkRound && b < nd && cnt < L; b += kWave) {
+        uint32_t base, n;
+        int32_t v0;
+        walk_doc_mv(q, seg, b + lane, base, v0, n);
+        uint32_t incl = n;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+          const uint32_t t = __shfl_up(incl, o, kWave);
+          if (lane >= o) incl += t;
+        }
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+        for (uint32_t g0 = 0; g0 < total && cnt < L; g0 += kWave) {
+          const uint32_t g = g0 + (uint32_t)lane;
+          int ow = 0;
+#pragma unroll
+          for (int st = kWave / 2; st >= 1; st >>= 1) {
+            const uint32_t v = (uint32_t)__shfl((int)incl, ow + st - 1, kWave);
+            if (v <= g) ow += st;
+          }
+          ow = ow < kWave ? ow : kWave - 1;
+          const uint32_t o_incl = (uint32_t)__shfl((int)incl, ow, kWave), o_n = (uint32_t)__shfl((int)n, ow, kWave);
+          const uint32_t o_base = (uint32_t)__shfl((int)base, ow, kWave);
+          const int32_t o_v0 = __shfl(v0, ow, kWave);
+          const bool act = g < total;
+          const uint32_t k0 = act ? walk_mv_key(q, seg, o_base, (int64_t)o_v0 + (g - (o_incl - o_n))) : kNoKey;
+          const bool cand = act && !((seen[k0 >> 5] >> (k0 & 31u)) & 1u);
+          // a key new to the bitmap counts at its first record only
+          uint64_t cm = __ballot(cand);
+          bool dup = false;
+          while (cm) {
+            const int j = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)k0, j);
+            dup |= j < lane && kj == k0;
+          }
+          const bool nw = cand && !dup;
+          const uint64_t nm = __ballot(nw);
+          uint64_t take = nm;
+          if (cnt + __builtin_popcountll(nm) >= L) {  // keep the first L - cnt new keys of these records
+            int64_t need = L - cnt;
+            uint64_t t = 0, r = nm;
+            while (need-- > 0) {
+              t |= r & (~r + 1);
+              r &= r - 1;
+            }
+            take = t;
+          }
+          if ((take >> lane) & 1ull) atomicOr(seen + (k0 >> 5), 1u << (k0 & 31u));
+          cnt += __builtin_popcountll(take);
+        }
+      }
+    }
+    reached = true;
+    __syncthreads();
+  }
+  __syncthreads();
+  for (int64_t w = tid; w < words; w += kWalkThreads) gp(adm)[w] = seen[w];
+  if (reached && tid == 0) __hip_atomic_fetch_add(gp(q->matched_docs) + 2, 1ull, RLX);  // numGroupsLimitReached
+}
+
+hipError_t launch_limit_walk(const DevQuery* q, const DevSeg* segs, int nseg, int64_t words, bool mv, hipStream_t s) {
+  if (mv) {  // (the planner keeps 2 * words within kWalkMaxWords)
+    const size_t lds = (size_t)words * 8;
+    hipError_t e = hipFuncSetAttribute((const void*)limit_walk_mv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    limit_walk_mv_kernel<<<nseg, kWalkThreads, lds, s>>>(q, segs, words);
+    return hipGetLastError();
+  }
   if (words > kWalkMaxWords) {
     limit_walk_kernel<true><<<nseg, kWalkThreads, 0, s>>>(q, segs, words);
     return hipGetLastError();

@@ -87,7 +87,7 @@ hipError_t launch_limit_passes(const DevQuery* q, const DevSeg* segs, const Limi
                                hipStream_t s);
 // numGroupsLimit walk form: one workgroup per segment with a non-null DevSeg::admit; `words` = bitmap words (K / 32)
 constexpr int64_t kWalkMaxWords = 40000;  // LDS bitmap of at most 160000 bytes
-hipError_t launch_limit_walk(const DevQuery* q, const DevSeg* segs, int nseg, int64_t words, hipStream_t s);
+hipError_t launch_limit_walk(const DevQuery* q, const DevSeg* segs, int nseg, int64_t words, bool mv, hipStream_t s);
 hipError_t launch_bswap_words(uint32_t* w, int64_t n, hipStream_t s);
 hipError_t launch_hll_lut_numeric(const int64_t* di, const double* dd, int32_t vtype, int32_t card, int32_t log2m,
                                   uint32_t* lut, hipStream_t s);

@@ -675,6 +675,8 @@ __device__ void accumulate_doc_mv(const DevQuery* __restrict__ q, const DevSeg* 
     }
     const int64_t key = key_slot(q, kw[0], kw[1]);
     if (key < 0) continue;
+    // numGroupsLimit, walk form (direct key space): only the keys the segment admitted
+    if (seg->admit != nullptr && !((gp(seg->admit)[key >> 5] >> (key & 31)) & 1u)) continue;
     update_doc_key<STRAT>(q, seg, img, doc_local, doc, key, acc);
   }
 }
@@ -1185,6 +1187,7 @@ __device__ __forceinline__ void part_keys(const DevQuery* __restrict__ q, CSegT*
 #pragma unroll
   for (int i = 0; i < N; ++i) key[i] = 0u;
   for (int j = 0; j < q->num_gb; ++j) {
+    if (j == q->gb_mv) continue;  // (the multi-value component: per value, mv_key_records)
     const int slot = q->gb_slot[j];
     const int gl = cs->cols[slot].lds_off, gn = cs->cols[slot].nbits;
     const uint32_t* gw = cs->cols[slot].words;
@@ -1199,6 +1202,73 @@ __device__ __forceinline__ void part_keys(const DevQuery* __restrict__ q, CSegT*
     }
 #pragma unroll
     for (int i = 0; i < N; ++i) key[i] += id[i] * st;
+  }
+}
+
+// Element i (wave-uniform) of a register array without dynamic register indexing.
+template <int N, class T>
+__device__ __forceinline__ T pick(const T (&a)[N], int i) {
+  T r = a[0];
+#pragma unroll
+  for (int k = 1; k < N; ++k) r = i == k ? a[k] : r;
+  return r;
+}
+
+// The V records of one step of a query grouping by a multi-value column (DictionaryBasedGroupKeyGenerator
+// .getIntRawKeys: one key per value of the doc's MV group-by column, duplicates included; a doc without values has no
+// key). Lane l holds its doc's key without the MV component (`base`), its first value's index v0 and its value count n
+// (0: not matching); `adm` (numGroupsLimit walk form, else null) drops the keys the segment did not admit. Value-parallel, KB x 64 records per round: lane j takes record g = b + 64 k + j, finds the owner
+// lane (the first whose inclusive prefix sum of n exceeds g) by a 6-shuffle binary search and decodes that value
+// (consecutive records are consecutive values of the stream: the loads coalesce). f(act, key, owner) takes each round.
+template <int KB, class F>
+__device__ __forceinline__ void mv_key_records(const uint32_t* words, int nb, const int32_t* rm, uint32_t stride,
+                                               const uint32_t* adm, uint32_t base, int32_t v0, uint32_t n, int lane,
+                                               F&& f) {
+  uint32_t incl = n;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t t = __shfl_up(incl, o, kWave);
+    if (lane >= o) incl += t;
+  }
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+#pragma unroll 1
+  for (uint32_t b = 0; b < total; b += KB * kWave) {
+    bool act[KB];
+    uint32_t key[KB], id[KB];
+    int own[KB];
+    int64_t vi[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const uint32_t g = b + (uint32_t)(k * kWave + lane);
+      int ow = 0;
+#pragma unroll
+      for (int st = kWave / 2; st >= 1; st >>= 1) {
+        const uint32_t v = (uint32_t)__shfl((int)incl, ow + st - 1, kWave);
+        if (v <= g) ow += st;
+      }
+      ow = ow < kWave ? ow : kWave - 1;
+      const uint32_t o_incl = (uint32_t)__shfl((int)incl, ow, kWave), o_n = (uint32_t)__shfl((int)n, ow, kWave);
+      act[k] = g < total;
+      own[k] = ow;
+      key[k] = (uint32_t)__shfl((int)base, ow, kWave);
+      vi[k] = (int64_t)__shfl(v0, ow, kWave) + (int64_t)(g - (o_incl - o_n));
+    }
+    decode_global_batch<KB>(words, vi, act, nb, id);
+    if (rm != nullptr) {
+#pragma unroll
+      for (int k = 0; k < KB; ++k)
+        if (act[k]) id[k] = (uint32_t)gp(rm)[id[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < KB; ++k) key[k] += id[k] * stride;
+    if (adm != nullptr) {  // numGroupsLimit, walk form: the keys the segment admitted
+      uint32_t w[KB];
+#pragma unroll
+      for (int k = 0; k < KB; ++k) w[k] = act[k] ? gp(adm)[key[k] >> 5] : 0u;
+#pragma unroll
+      for (int k = 0; k < KB; ++k) act[k] = act[k] && ((w[k] >> (key[k] & 31u)) & 1u);
+    }
+    f(act, key, own);
   }
 }
 
@@ -1277,6 +1347,14 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
   const int hslot = ha >= 0 ? q->aggs[ha].slot : 0;
   const bool hmv = ha >= 0 && cs->cols[hslot].kind == COL_MV_DICT;
   const int32_t* hoff = cs->cols[hslot].mv_off;
+  // a multi-value group-by column (V stream only): one V record per (doc, value), mv_key_records
+  const int gmv = q->gb_mv;
+  const int mslot = gmv >= 0 ? q->gb_slot[gmv] : 0;
+  const int32_t* moff = cs->cols[mslot].mv_off;
+  const uint32_t* mwords = cs->cols[mslot].words;
+  const int mnb = cs->cols[mslot].nbits;
+  const int32_t* mrm = gmv >= 0 ? cs->remap[gmv] : nullptr;
+  const uint32_t mstride = gmv >= 0 ? (uint32_t)q->gb_stride[gmv] : 0u;
   // steps per batch (register budget; 4 for the H-only emit measured slower: 4.83 vs 4.65 ms). The V-only emit of
   // 4-wave workgroups runs at most 2 workgroups per CU (its LDS bins), so it has the VGPRs for a whole tile per batch.
   constexpr int kEB = (is_pemit(STRAT) && !pemit_hh(STRAT) && !pemit_big(STRAT) && pemit_vf(STRAT) != V_FMT_GEN) ? 16 : 8;
@@ -1287,6 +1365,22 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
     part_keys<kEB, LM>(q, cs, img, doc_base, h, m, lane, key);  // table-wide key (< 2^32 on this path)
     if constexpr (STRAT == STRAT_PCOUNT) {
       lds_u32_t* hist = lds_ptr(lds);
+      if (gmv >= 0) {  // one V record per (doc, value): count each value's partition
+        int32_t v0[kEB], v1[kEB];
+        mv_ranges<kEB, LM>(true, moff, (int64_t)cs->num_docs, doc_base, h, m, lane, v0, v1);
+#pragma unroll 1
+        for (int i = 0; i < kEB; ++i) {
+          if (__ballot((m >> (h + i)) & 1u) == 0) continue;
+          const int32_t a0 = pick(v0, i), a1 = pick(v1, i);
+          mv_key_records<4>(mwords, mnb, mrm, mstride, cs->admit, pick(key, i), a0, (uint32_t)(a1 - a0), lane,
+                            [&](const bool (&act)[4], const uint32_t (&k)[4], const int (&)[4]) {
+#pragma unroll
+                              for (int kk = 0; kk < 4; ++kk)
+                                if (act[kk]) __hip_atomic_fetch_add(hist + (k[kk] >> ksv), 1u, WG_RLX);
+                            });
+        }
+        continue;
+      }
       uint32_t n[kEB];
       {
         int32_t v0[kEB], v1[kEB];
@@ -1314,6 +1408,38 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
         uint32_t lo[kEB], hi[kEB];
         part_vvals<kEB, LM, VF>(q, cs, img, doc_base, h, m, lane, lo, hi);
         if constexpr (VF != V_FMT_GEN) {
+          if (gmv >= 0) {  // one record per (doc, value) pair, the doc's payload on each
+            int32_t v0[kEB], v1[kEB];
+            mv_ranges<kEB, LM>(true, moff, (int64_t)cs->num_docs, doc_base, h, m, lane, v0, v1);
+#pragma unroll 1
+            for (int i = 0; i < kEB; ++i) {
+              if (__ballot((m >> (h + i)) & 1u) == 0) continue;
+              const int32_t a0 = pick(v0, i), a1 = pick(v1, i);
+              const uint32_t dlo = pick(lo, i), dhi = pick(hi, i);
+              mv_key_records<4>(mwords, mnb, mrm, mstride, cs->admit, pick(key, i), a0, (uint32_t)(a1 - a0), lane,
+                                [&](const bool (&act)[4], const uint32_t (&k)[4], const int (&own)[4]) {
+                                  uint32_t pk[4], r[4][NW];
+#pragma unroll
+                                  for (int kk = 0; kk < 4; ++kk) {
+                                    const uint32_t olo = (uint32_t)__shfl((int)dlo, own[kk], kWave);
+                                    pk[kk] = k[kk] >> ksv;
+                                    r[kk][0] = k[kk] & kmask;
+#pragma unroll
+                                    for (int w = 1; w < NW; ++w) r[kk][w] = 0u;
+                                    if constexpr (VF == V_FMT_ID) {
+                                      r[kk][0] |= olo << ksv;
+                                    } else if constexpr (VF == V_FMT_32) {
+                                      r[kk][1] = olo;
+                                    } else if constexpr (VF == V_FMT_64) {
+                                      r[kk][1] = olo;
+                                      r[kk][2] = (uint32_t)__shfl((int)dhi, own[kk], kWave);
+                                    }
+                                  }
+                                  bin_put_batch<4, NW>(B, act, pk, 0u, bins, BS, W, r, gp(ps.recs_v), lane, dbg);
+                                });
+            }
+            continue;
+          }
           // the batch's records (one per matching doc of the kEB steps) in one put: every LDS phase runs once
           bool act[kEB];
           uint32_t pk[kEB], r[kEB][NW];
@@ -2169,7 +2295,8 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
     if (__ballot(m != 0) == 0) return 0;
   }
   const uint32_t scanned = m;  // numDocsScanned counts every doc the filter kept, admitted or not
-  if (seg->admit != nullptr) {
+  // (an MV group-by admits (doc, value) keys one by one: accumulate_doc_mv, mv_key_records)
+  if (seg->admit != nullptr && q->gb_mv < 0) {
     m = admitted_docs<LM, STEPS>(q, seg, img, doc_base, m, lane);
     if (__ballot(m != 0) == 0) return (uint32_t)__builtin_popcount(scanned);
   }

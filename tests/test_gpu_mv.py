@@ -157,6 +157,38 @@ def test_star_schema_partitioned_hll(flags, max_len, skew):
             g.close()
 
 
+@pytest.mark.parametrize("max_len,skew,flags", [(4, False, 0), (20, True, 0), (6, False, L.PA_QF_NO_PARTITION)])
+def test_mv_group_by_partitioned(max_len, skew, flags):
+    """GROUP BY an MV column over a key space that takes the partitioned path: one V record per (doc, value) pair
+    (getIntRawKeys expansion, duplicates included), each carrying the doc's payload — a dictionary LONG (value ids) or
+    a raw DOUBLE (64-bit records) — with the MV component least or most significant in the key; a second MV group-by
+    column keeps the per-doc global path. Identical to the oracle (DOUBLE sums within DOUBLE_REL)."""
+    sv = (("a", 64), ("b", 7))
+    segs = [mv_segment(40 + i, n, mv_cols=(("tags", 3000, max_len), ("tags2", 5, 2)), sv_cols=sv, raw_double=True,
+                       skew=skew) for i, n in enumerate((60013, 20011))]
+    gsegs = [GpuSegment(sg) for sg in segs]
+    try:
+        for sql, part in (
+                ("SELECT a, tags, COUNT(*), SUM(r) FROM t GROUP BY a, tags LIMIT 1000000 "
+                 "OPTION(numGroupsLimit=1000000)", True),
+                ("SELECT tags, a, COUNT(*), SUM(m), MIN(m) FROM t GROUP BY tags, a LIMIT 1000000 "
+                 "OPTION(numGroupsLimit=1000000)", True),
+                ("SELECT tags, b, COUNT(*) FROM t WHERE a < 60 GROUP BY tags, b LIMIT 1000000 "
+                 "OPTION(numGroupsLimit=1000000)", None),
+                ("SELECT a, tags, tags2, COUNT(*), MAX(r) FROM t GROUP BY a, tags, tags2 LIMIT 1000000 "
+                 "OPTION(numGroupsLimit=1000000)", False)):
+            got, exp, _ = run_both(sql, segs, gsegs=gsegs, flags=flags, rel=DOUBLE_REL)
+            assert len(got.groups) > 10000
+            ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags)
+            strategy = ex.stats()["plan"]["strategy"]
+            ex.close()
+            if part is not None:
+                assert strategy == ("partitioned" if part and not flags else "global"), (sql, strategy)
+    finally:
+        for g in gsegs:
+            g.close()
+
+
 def test_malformed_mv_index_rejected():
     """The C-ABI validates the row-start bitmap and chunk offsets of an MV forward index."""
     lib = L.lib()
@@ -180,22 +212,52 @@ def test_malformed_mv_index_rejected():
 def test_mv_num_groups_limit_trimming(limit):
     """numGroupsLimit binding inside a doc's key expansion: group ids follow getIntRawKeys order (last group-by
     column first; a later MV column's value index is the more significant digit), so the cut falls between two keys
-    of one doc exactly where the reference's IntGroupIdMap would put it."""
+    of one doc exactly where the reference's IntGroupIdMap would put it. Two MV group-by columns take the sorted form
+    (first positions, mode 1); one MV column the walk form (mode 2: a doc-order walk over (doc, value) keys, then
+    per-key admission), also with the walk disabled (sorted form) for comparison."""
     from pinot_amd import parse_sql
     from pinot_amd.engine import GpuQueryExecutor, GpuSegment
     mv = (("tags", 30, 4), ("tags2", 9, 3))
     segs = [mv_segment(11, 9001, mv_cols=mv), mv_segment(12, 2500, mv_cols=mv)]
-    for sql in ("SELECT a, tags2, tags, COUNT(*), SUM(m), MAX(m) FROM t WHERE b > 10 GROUP BY a, tags2, tags "
-                "LIMIT 100000 OPTION(numGroupsLimit=%d)" % limit,
-                "SELECT tags, COUNT(*), SUMMV(tags), DISTINCTCOUNTHLLMV(tags2) FROM t GROUP BY tags LIMIT 100000 "
-                "OPTION(numGroupsLimit=%d)" % (limit % 31 + 1)):
+    for sql, mode, flags in (
+            ("SELECT a, tags2, tags, COUNT(*), SUM(m), MAX(m) FROM t WHERE b > 10 GROUP BY a, tags2, tags "
+             "LIMIT 100000 OPTION(numGroupsLimit=%d)" % limit, 1, 0),
+            ("SELECT tags, COUNT(*), SUMMV(tags), DISTINCTCOUNTHLLMV(tags2) FROM t GROUP BY tags LIMIT 100000 "
+             "OPTION(numGroupsLimit=%d)" % (limit % 31 + 1), 2, 0),
+            ("SELECT a, tags, COUNT(*), SUM(m) FROM t WHERE b > 10 GROUP BY a, tags LIMIT 100000 "
+             "OPTION(numGroupsLimit=%d)" % limit, 2, 0),
+            ("SELECT tags, b, COUNT(*), MIN(m) FROM t GROUP BY tags, b LIMIT 100000 "
+             "OPTION(numGroupsLimit=%d)" % limit, 2, 0),
+            ("SELECT tags, b, COUNT(*), MIN(m) FROM t GROUP BY tags, b LIMIT 100000 "
+             "OPTION(numGroupsLimit=%d)" % limit, 1, L.PA_QF_NO_LIMIT_WALK)):
         gsegs = [GpuSegment(s) for s in segs]
         try:
-            ex = GpuQueryExecutor(parse_sql(sql), gsegs)
-            assert ex.stats()["plan"]["limit_trimming"] == 1
+            ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags)
+            assert ex.stats()["plan"]["limit_trimming"] == mode, sql
             ex.close()
         finally:
             for g in gsegs:
                 g.close()
-        got, exp, _ = run_both(sql, segs)
+        got, exp, _ = run_both(sql, segs, flags=flags)
         assert got.num_groups_limit_reached
+
+
+@pytest.mark.parametrize("limit", [5000, 60000])
+def test_mv_num_groups_limit_partitioned(limit):
+    """The walk form of numGroupsLimit on the partitioned MV path (the mvgroup shape at oracle size: 64 x 3000 keys,
+    dense): the count and emit passes admit each (doc, value) record by the segment's bitmap."""
+    sv = (("a", 64),)
+    segs = [mv_segment(50 + i, n, mv_cols=(("tags", 3000, 5),), sv_cols=sv, raw_double=True)
+            for i, n in enumerate((60013, 20011))]
+    sql = ("SELECT a, tags, COUNT(*), SUM(r) FROM t GROUP BY a, tags LIMIT 1000000 OPTION(numGroupsLimit=%d)" % limit)
+    gsegs = [GpuSegment(sg) for sg in segs]
+    try:
+        got, exp, _ = run_both(sql, segs, gsegs=gsegs, rel=DOUBLE_REL)
+        assert got.num_groups_limit_reached
+        ex = GpuQueryExecutor(parse_sql(sql), gsegs)
+        p = ex.stats()["plan"]
+        ex.close()
+        assert p["strategy"] == "partitioned" and p["limit_trimming"] == 2, p
+    finally:
+        for g in gsegs:
+            g.close()
