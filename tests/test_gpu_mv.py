@@ -224,7 +224,7 @@ def test_mv_num_groups_limit_trimming(limit):
              "LIMIT 100000 OPTION(numGroupsLimit=%d)" % limit, 1, 0),
             ("SELECT tags, COUNT(*), SUMMV(tags), DISTINCTCOUNTHLLMV(tags2) FROM t GROUP BY tags LIMIT 100000 "
              "OPTION(numGroupsLimit=%d)" % (limit % 31 + 1), 2, 0),
-            ("SELECT a, tags, COUNT(*), SUM(m) FROM t WHERE b > 10 GROUP BY a, tags LIMIT 100000 "
+            ("SELECT a, tags, b, COUNT(*), SUM(m) FROM t WHERE b > 10 GROUP BY a, tags, b LIMIT 100000 "
              "OPTION(numGroupsLimit=%d)" % limit, 2, 0),
             ("SELECT tags, b, COUNT(*), MIN(m) FROM t GROUP BY tags, b LIMIT 100000 "
              "OPTION(numGroupsLimit=%d)" % limit, 2, 0),
