@@ -28,6 +28,8 @@ PA_QF_WG_SHIFT = 12
 PA_QF_DEBUG_STREAM_ONLY = 1 << 16
 PA_QF_NO_LANE_MAJOR = 1 << 17
 PA_QF_NO_REG_STAGE = 1 << 18
+PA_QF_NO_BOX_FILTER = 1 << 19
+PA_QF_BOX_FILTER = 1 << 20
 PA_QF_NO_PARTITION = 1 << 21
 PA_QF_PART_SHIFT = 22
 PA_QF_NO_SPLIT_EMIT = 1 << 24

@@ -664,6 +664,7 @@ struct Prep {
   std::vector<char> gd_stage_raw;          // per slot: raw aggregation column staged as a 32/64-bit "bit column"
   size_t gd_lds = 0;                       // LDS bytes of the accumulators + tables (the ring follows)
   int gd_rp_log2 = 0, gd_nkeys = 0, gd_tables = 0;
+  bool gd_box = false;                     // the key box is exactly the filter (pa_gdense.h gd_box_tile)
   int gd_lo[PA_MAX_GROUP_BY] = {0}, gd_span[PA_MAX_GROUP_BY] = {0}, gd_ls[PA_MAX_GROUP_BY] = {0};
   int gd_tab[PA_MAX_GROUP_BY] = {0}, gd_tab_n[PA_MAX_GROUP_BY] = {0};
   std::vector<int> gd_vs, gd_op, gd_acc, gd_tab_a, gd_tab_an;
@@ -1021,10 +1022,18 @@ int plan_gdense(pa_query* q, Prep& P) {
     lo[j] = 0;
     hi[j] = s.group_by_cardinality[j];
   }
+  // The box IS the filter when every literal is a unit DICT_RANGE clause on a group-by column, not negated, with a
+  // non-empty hull: dictionaries are sorted, so the table key ids of a value range form one run, and a doc's key lies
+  // in the box iff its value lies in every range (the kernel then box-checks every doc instead of evaluating the filter
+  // and walking its matches)
+  bool box_exact = !q->literals.empty();
   for (size_t i = 0; i < q->literals.size(); ++i) {
     const bool unit = q->clause_end[i] && (i == 0 || q->clause_end[i - 1]);
-    if (!unit) continue;
     const Literal lit = q->literals[i];
+    bool on_gb = false;
+    for (int j = 0; j < s.num_group_by; ++j) on_gb |= s.leaves[lit.leaf].column_id == s.group_by_columns[j];
+    if (!unit || !on_gb || s.leaves[lit.leaf].kind != PA_LEAF_DICT_RANGE) box_exact = false;
+    if (!unit) continue;
     for (int j = 0; j < s.num_group_by; ++j) {
       if (s.leaves[lit.leaf].column_id != s.group_by_columns[j]) continue;
       int64_t ulo = INT64_MAX, uhi = INT64_MIN;
@@ -1056,15 +1065,24 @@ int plan_gdense(pa_query* q, Prep& P) {
             if ((lut[id >> 5] >> (id & 31)) & 1u) take(id);
         }
       }
-      if (!bounded) continue;
-      if (ulo == INT64_MAX) ulo = uhi = 0;  // no segment can match: an empty box (a span of one key keeps it simple)
+      if (!bounded) {
+        box_exact = false;
+        continue;
+      }
+      if (ulo == INT64_MAX) {  // no segment can match: an empty box (a span of one key keeps it simple)
+        ulo = uhi = 0;
+        box_exact = false;
+      }
       lo[j] = std::max(lo[j], ulo);
       hi[j] = std::max(lo[j], std::min(hi[j], uhi));
     }
   }
   int64_t nkeys = 1;
   for (int j = 0; j < s.num_group_by; ++j) {
-    if (hi[j] <= lo[j]) hi[j] = lo[j] + 1;
+    if (hi[j] <= lo[j]) {  // (disjoint ranges: nothing matches)
+      hi[j] = lo[j] + 1;
+      box_exact = false;
+    }
     P.gd_lo[j] = (int)lo[j];
     P.gd_span[j] = (int)(hi[j] - lo[j]);
     P.gd_ls[j] = (int)nkeys;
@@ -1072,6 +1090,9 @@ int plan_gdense(pa_query* q, Prep& P) {
     if (nkeys > kGdMaxKeys) return PA_OK;
   }
   P.gd_nkeys = (int)nkeys;
+  // the box as the filter from 30 % selectivity up (below it the filter + walk over the matches costs less VALU)
+  P.gd_box = box_exact && !(s.flags & PA_QF_NO_BOX_FILTER) &&
+             ((s.flags & PA_QF_BOX_FILTER) || P.post_density >= 0.3 * kWTileDocs);
   // per-segment key tables where some segment remaps the column
   size_t tab_bytes = 0;
   P.gd_tables = 0;
@@ -2164,6 +2185,7 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
       }
       g.ngb = s.num_group_by;
       g.rpl = P.gd_rp_log2;
+      g.box = P.gd_box ? 1 : 0;
       {
         const char* e = std::getenv("PA_DEBUG_EMIT");  // measurement only (pa_gdense.h knobs; results invalid)
         g.pad = e ? std::atoi(e) : 0;
@@ -2531,7 +2553,9 @@ static int alloc_leaps(pa_query* q, const Prep& P) {
   const int64_t slices = (int64_t)q->grid * scan_waves(q->strategy);
   const int64_t cap = (int64_t)(16.0 * P.first_clause_sel * (double)q->num_docs / (double)slices) + 256;
   q->leap_slices = slices;
-  const size_t words = (size_t)std::max(1, q->nseg) * 3 + 1 + (size_t)slices + (size_t)slices * (size_t)cap;
+  // (+ the search's prefix sums and contiguous copy of the slices: leap_prefix_kernel / leap_compact_kernel)
+  const size_t words = (size_t)std::max(1, q->nseg) * 3 + 1 + (size_t)slices + 2 * (size_t)slices * (size_t)cap +
+                       (size_t)slices + 1;
   int rc = dev_alloc(q->leap_buf, words * sizeof(unsigned long long));
   if (rc) return rc;
   PA_HIP(hipMemset(q->leap_buf.p, 0, leap_header_bytes(q)));

@@ -320,9 +320,11 @@ struct GdSegPlan {
     int32_t reg, nbits;                  // staged region, bits per dictId (dictionary columns)
     int32_t acc, tab;                    // LDS byte offsets: replicated accumulators, value table
   } ag[kGdMaxAgg];
-  int32_t pad1[6];
+  int32_t box;                           // 58: the key box is exactly the filter (gd_box_tile)
+  int32_t pad1[5];
 };
 static_assert(sizeof(GdSegPlan) == 256, "one dword per lane");
+constexpr int kGdBoxDword = 58;
 // Register-staged tiles (STRAT_GDENSE_RS*): the wave instructions that load one 1024-doc tile of the segment's staged
 // columns into VGPRs — the same 16-byte-per-lane chunks the LDS-DMA would copy — and where each goes in the tile image.
 constexpr int kGdRsMaxIns = 12;

@@ -98,7 +98,8 @@ __device__ __forceinline__ void gd_dec(uint32_t a, uint32_t sh, uint32_t nb, con
 // compile-time lanes: no scalar loads, whose lgkmcnt waits would also wait for the LDS operations in flight); every load
 // is an LDS read. errs counts matching docs whose key fell outside the LDS box (cannot happen when the planner's box is
 // right; the query then reports an error).
-template <int N>
+// BOX (the key box is the filter, gd_box_tile): errs counts the docs inside the box instead (numDocsScanned).
+template <int N, bool BOX = false>
 __device__ __forceinline__ void gd_batch(uint32_t gt, const GdLane& L, const uint32_t (&st)[N], const bool (&on_in)[N],
                                          uint32_t r, uint32_t base, uint32_t& errs) {
   const int ngb = (int)rl(gt, 0), na = (int)rl(gt, 1);
@@ -139,7 +140,7 @@ __device__ __forceinline__ void gd_batch(uint32_t gt, const GdLane& L, const uin
   uint32_t idx[N];
 #pragma unroll
   for (int k = 0; k < N; ++k) {
-    errs += (on_in[k] && !on[k]) ? 1u : 0u;
+    errs += BOX ? (on[k] ? 1u : 0u) : ((on_in[k] && !on[k]) ? 1u : 0u);
     idx[k] = (key[k] << rpl) | r;
   }
   if (dbg & 2) {
@@ -265,6 +266,29 @@ __device__ __forceinline__ void gd_walk(uint32_t gt, uint32_t img, uint32_t s, i
   }
 }
 
+// The filter is exactly the key box (GdSegPlan::box: unit DICT_RANGE clauses on group-by columns): every valid doc of a
+// step-major tile goes through gd_batch, whose box check is the filter, KB steps per batch at compile-time step offsets
+// — no filter evaluation, no walk. Returns the lane's docs inside the box.
+__device__ __forceinline__ uint32_t gd_box_tile(uint32_t gt, uint32_t img, uint32_t valid, int lane, uint32_t base) {
+  constexpr int KB = 4;
+  GdLane L;
+  gd_lane_setup(gt, img, lane, L);
+  const uint32_t r = (uint32_t)lane & ((1u << rl(gt, 2)) - 1u);
+  uint32_t inbox = 0;
+#pragma unroll
+  for (int s0 = 0; s0 < kGdSmSteps; s0 += KB) {
+    uint32_t st[KB];
+    bool on[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      st[k] = (uint32_t)(s0 + k);
+      on[k] = (valid >> (s0 + k)) & 1u;
+    }
+    gd_batch<KB, true>(gt, L, st, on, r, base, inbox);
+  }
+  return inbox;
+}
+
 // Filter of one lane-major 2048-doc tile (every literal eager: the planner's condition), then the transpose of the match
 // words to step-major bits (lane l, bit i <=> doc 64 i + l lives in lane 2i + l/32, bit l % 32: one ds_bpermute per step)
 // and the walk.
@@ -325,6 +349,7 @@ __device__ __forceinline__ uint32_t gd_tile_sm(uint32_t gt, const DevQuery* __re
     const int64_t n = rem > lane ? (rem - lane + kWave - 1) / kWave : 0;
     m = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
   }
+  if (rl(gt, kGdBoxDword)) return gd_box_tile(gt, img, m, lane, base);
   uint32_t clause = 0;
   const int neager = cq->num_eager;
   for (int li = 0; li < neager; ++li) {

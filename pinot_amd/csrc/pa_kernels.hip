@@ -1653,37 +1653,83 @@ hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t*
   return hipGetLastError();
 }
 
-// Fused execution statistics after the scan (pa_scan.h "fused execution statistics"): one wave per listed E doc (its
-// successor's label, and for a B-only doc its predecessor's) and one per segment (its first labelled doc), each a
-// wave-wide neighbour search over both leaves; the leaps go into the segments' counters.
-__global__ void __launch_bounds__(256) leap_search_kernel(const DevQuery* __restrict__ q, const DevSeg* __restrict__ segs) {
+// Fused execution statistics after the scan (pa_scan.h "fused execution statistics"). The scan waves' list slices hold
+// a few E docs each, unevenly (a Poisson spread: one wave walking its own slice's docs one search after another would
+// take the longest slice's time), so: (1) one workgroup takes the exclusive prefix sums of the slice lengths, (2) the
+// slices are copied into one contiguous list, (3) every wave searches its share of that list — one wave per listed E
+// doc (its successor's label, and for a B-only doc its predecessor's) and one per segment (its first labelled doc),
+// each a wave-wide neighbour search over both leaves; the leaps go into the segments' counters.
+// Layout after the slices (alloc_leaps): [slices + 1] prefix sums, then the contiguous list.
+constexpr int kLeapPrefixThreads = 1024;
+
+__global__ void __launch_bounds__(kLeapPrefixThreads) leap_prefix_kernel(const DevQuery* __restrict__ q) {
+  __shared__ unsigned long long part[kLeapPrefixThreads];
+  const int64_t nseg = q->num_segments, S = q->leap_slices;
+  const AS1 unsigned long long* hdr = gp(q->leap_out) + 3 * nseg;
+  AS1 unsigned long long* pre = gp(q->leap_out) + 3 * nseg + 1 + S + S * q->leap_cap;
+  const int t = threadIdx.x;
+  const int64_t per = (S + kLeapPrefixThreads - 1) / kLeapPrefixThreads;
+  const int64_t s0 = min(S, (int64_t)t * per), s1 = min(S, s0 + per);
+  unsigned long long sum = 0;
+  for (int64_t w = s0; w < s1; ++w) sum += hdr[1 + w];
+  part[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < kLeapPrefixThreads; o <<= 1) {  // inclusive scan of the partial sums
+    const unsigned long long v = t >= o ? part[t - o] : 0ull;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  unsigned long long run = part[t] - sum;
+  for (int64_t w = s0; w < s1; ++w) {
+    pre[w] = run;
+    run += hdr[1 + w];
+  }
+  if (t == kLeapPrefixThreads - 1) pre[S] = part[t];
+}
+
+__global__ void __launch_bounds__(256) leap_compact_kernel(const DevQuery* __restrict__ q) {
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t nseg = q->num_segments, slices = q->leap_slices, cap = q->leap_cap;
+  const int64_t nseg = q->num_segments, S = q->leap_slices, cap = q->leap_cap;
   const AS1 unsigned long long* hdr = gp(q->leap_out) + 3 * nseg;
   if (hdr[0]) return;  // (a slice overflowed: the host takes every segment's counts from leaf bitmaps)
+  const AS1 unsigned long long* pre = hdr + 1 + S + S * cap;
+  AS1 unsigned long long* out = gp(q->leap_out) + 3 * nseg + 1 + S + S * cap + S + 1;
   const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  // wave w: slice w (every entry of it), then the segment starts
-  for (int64_t w = (int64_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); w < slices + nseg; w += waves) {
-    if (w < slices) {
-      const int64_t n = (int64_t)hdr[1 + w];
-      const AS1 unsigned long long* list = hdr + 1 + slices + w * cap;
-      for (int64_t k = 0; k < n; ++k) {
-        const uint64_t ent = list[k];
-        const int si = (int)(ent >> 40);
-        const int64_t doc = (int64_t)((ent >> 1) & ((1ull << 39) - 1ull));
-        uint32_t leaps = 0u, gave = 0u;
-        const uint32_t succ = leap_search(segs + si, doc + 1, 1, lane);
-        leaps += succ == 1u;
-        gave |= succ == 4u;
-        if (!(ent & 1ull)) {
-          const uint32_t pred = leap_search(segs + si, doc - 1, -1, lane);
-          leaps += pred == 1u;
-          gave |= pred == 4u;
-        }
-        leap_add(q, si, 0u, leaps, gave, lane);
+  for (int64_t w = (int64_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); w < S; w += waves) {
+    const int64_t n = (int64_t)hdr[1 + w], d = (int64_t)pre[w];
+    const AS1 unsigned long long* list = hdr + 1 + S + w * cap;
+    for (int64_t k = lane; k < n; k += kWave) out[d + k] = list[k];
+  }
+}
+
+__global__ void __launch_bounds__(256) leap_search_kernel(const DevQuery* __restrict__ q, const DevSeg* __restrict__ segs) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t nseg = q->num_segments, S = q->leap_slices, cap = q->leap_cap;
+  const AS1 unsigned long long* hdr = gp(q->leap_out) + 3 * nseg;
+  if (hdr[0]) return;
+  const AS1 unsigned long long* pre = hdr + 1 + S + S * cap;
+  const AS1 unsigned long long* list = pre + S + 1;
+  const int64_t total = (int64_t)pre[S];
+  const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  // wave w: listed docs w, w + waves, ..., then the segment starts
+  for (int64_t w = (int64_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); w < total + nseg; w += waves) {
+    if (w < total) {
+      const uint64_t ent = list[w];
+      const int si = (int)(ent >> 40);
+      const int64_t doc = (int64_t)((ent >> 1) & ((1ull << 39) - 1ull));
+      uint32_t leaps = 0u, gave = 0u;
+      const uint32_t succ = leap_search(segs + si, doc + 1, 1, lane);
+      leaps += succ == 1u;
+      gave |= succ == 4u;
+      if (!(ent & 1ull)) {
+        const uint32_t pred = leap_search(segs + si, doc - 1, -1, lane);
+        leaps += pred == 1u;
+        gave |= pred == 4u;
       }
+      leap_add(q, si, 0u, leaps, gave, lane);
     } else {
-      const int si = (int)(w - slices);
+      const int si = (int)(w - total);
       const uint32_t first = leap_search(segs + si, 0, 1, lane);
       leap_add(q, si, 0u, first == 1u ? 1u : 0u, first == 4u ? 1u : 0u, lane);
     }
@@ -1691,6 +1737,8 @@ __global__ void __launch_bounds__(256) leap_search_kernel(const DevQuery* __rest
 }
 
 hipError_t launch_leap_search(const DevQuery* q, const DevSeg* segs, hipStream_t s) {
+  hipLaunchKernelGGL(leap_prefix_kernel, dim3(1), dim3(kLeapPrefixThreads), 0, s, q);
+  hipLaunchKernelGGL(leap_compact_kernel, dim3(512), dim3(256), 0, s, q);
   hipLaunchKernelGGL(leap_search_kernel, dim3(2048), dim3(256), 0, s, q, segs);
   return hipGetLastError();
 }

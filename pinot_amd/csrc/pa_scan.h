@@ -846,7 +846,8 @@ __device__ __forceinline__ bool leaf_match_doc(const DevLeaf& L, int64_t doc) {
 // (kLeapSearchSteps) or a full list flags the segment(s), whose counts the host then takes from leaf bitmaps.
 // leap_out: [3 s]: segment s's matched docs, leaps, gave-up flag; [3 nseg]: list overflow flag; [3 nseg + 1 + w]: the
 // docs wave w of the scan listed; then the list: wave w's slice of leap_cap entries at [3 nseg + 1 + slices + w cap],
-// one (segment << 40 | doc << 1 | both) per E doc (a wave appends to its own slice: no atomic, no wait).
+// one (segment << 40 | doc << 1 | both) per E doc (a wave appends to its own slice: no atomic, no wait); after the
+// slices, the search's [slices + 1] prefix sums of their lengths and the slices copied into one contiguous list.
 constexpr int kLeapSearchSteps = 64;  // 4096 docs
 
 // Label of the nearest labelled doc at or beyond `from` in direction dir (+1 / -1) inside the segment: 1, 2, 3; 0 if
@@ -1272,6 +1273,48 @@ __device__ __forceinline__ void mv_key_records(const uint32_t* words, int nb, co
   }
 }
 
+// The same records, each lane its own doc (every doc of the step has at most kDocVals values): all of a doc's values
+// decoded in one batch (the step's docs are consecutive, so their values are one short stretch of the stream and the
+// loads nearly coalesce), no cross-lane shuffles; f(act, key) for value index e = 0 .. maxn - 1 (maxn: the wave's
+// largest count).
+template <class F>
+__device__ __forceinline__ void mv_doc_records(const uint32_t* words, int nb, const int32_t* rm, uint32_t stride,
+                                               const uint32_t* adm, uint32_t base, int32_t v0, uint32_t n,
+                                               uint32_t maxn, F&& f) {
+  uint32_t id[kDocVals], key[kDocVals];
+  int64_t vi[kDocVals];
+  bool on[kDocVals];
+#pragma unroll
+  for (int e = 0; e < kDocVals; ++e) {
+    vi[e] = (int64_t)v0 + e;
+    on[e] = (uint32_t)e < n;
+  }
+  decode_global_batch<kDocVals>(words, vi, on, nb, id);
+  if (rm != nullptr) {
+#pragma unroll
+    for (int e = 0; e < kDocVals; ++e)
+      if (on[e]) id[e] = (uint32_t)gp(rm)[id[e]];
+  }
+#pragma unroll
+  for (int e = 0; e < kDocVals; ++e) key[e] = base + id[e] * stride;
+  if (adm != nullptr) {
+    uint32_t w[kDocVals];
+#pragma unroll
+    for (int e = 0; e < kDocVals; ++e) w[e] = on[e] ? gp(adm)[key[e] >> 5] : 0u;
+#pragma unroll
+    for (int e = 0; e < kDocVals; ++e) on[e] = on[e] && ((w[e] >> (key[e] & 31u)) & 1u);
+  }
+#pragma unroll
+  for (int e = 0; e < kDocVals; e += 2)
+    if ((uint32_t)e < maxn) f(e, on, key);
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, kWave));
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
 // The V payload of one value column for the docs of steps h .. h+N-1: V_FMT_ID its table-wide value id (lo), V_FMT_32 /
 // V_FMT_64 its value bits (lo, hi): a dictionary gather, or the raw value (a raw DOUBLE's bits unchanged).
 template <int N, int LM, int VF>
@@ -1372,7 +1415,16 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
         for (int i = 0; i < kEB; ++i) {
           if (__ballot((m >> (h + i)) & 1u) == 0) continue;
           const int32_t a0 = pick(v0, i), a1 = pick(v1, i);
-          mv_key_records<4>(mwords, mnb, mrm, mstride, cs->admit, pick(key, i), a0, (uint32_t)(a1 - a0), lane,
+          const uint32_t nv = (uint32_t)(a1 - a0), maxn = wave_max_u32(nv);
+          if (maxn <= (uint32_t)kDocVals) {
+            mv_doc_records(mwords, mnb, mrm, mstride, cs->admit, pick(key, i), a0, nv, maxn,
+                           [&](int e, const bool (&act)[kDocVals], const uint32_t (&k)[kDocVals]) {
+                             if (act[e]) __hip_atomic_fetch_add(hist + (k[e] >> ksv), 1u, WG_RLX);
+                             if (act[e + 1]) __hip_atomic_fetch_add(hist + (k[e + 1] >> ksv), 1u, WG_RLX);
+                           });
+            continue;
+          }
+          mv_key_records<4>(mwords, mnb, mrm, mstride, cs->admit, pick(key, i), a0, nv, lane,
                             [&](const bool (&act)[4], const uint32_t (&k)[4], const int (&)[4]) {
 #pragma unroll
                               for (int kk = 0; kk < 4; ++kk)
@@ -1416,7 +1468,34 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
               if (__ballot((m >> (h + i)) & 1u) == 0) continue;
               const int32_t a0 = pick(v0, i), a1 = pick(v1, i);
               const uint32_t dlo = pick(lo, i), dhi = pick(hi, i);
-              mv_key_records<4>(mwords, mnb, mrm, mstride, cs->admit, pick(key, i), a0, (uint32_t)(a1 - a0), lane,
+              const uint32_t nv = (uint32_t)(a1 - a0), maxn = wave_max_u32(nv);
+              // each record: key offset (| value id), the doc's payload
+              auto rec = [&](uint32_t k, uint32_t plo, uint32_t phi, uint32_t (&r)[NW]) {
+                r[0] = k & kmask;
+#pragma unroll
+                for (int w = 1; w < NW; ++w) r[w] = 0u;
+                if constexpr (VF == V_FMT_ID) {
+                  r[0] |= plo << ksv;
+                } else if constexpr (VF == V_FMT_32) {
+                  r[1] = plo;
+                } else if constexpr (VF == V_FMT_64) {
+                  r[1] = plo;
+                  r[2] = phi;
+                }
+              };
+              if (maxn <= (uint32_t)kDocVals) {  // each lane its own doc's records, two per put
+                mv_doc_records(mwords, mnb, mrm, mstride, cs->admit, pick(key, i), a0, nv, maxn,
+                               [&](int e, const bool (&act)[kDocVals], const uint32_t (&k)[kDocVals]) {
+                                 const bool a2[2] = {act[e], act[e + 1]};
+                                 const uint32_t pk[2] = {k[e] >> ksv, k[e + 1] >> ksv};
+                                 uint32_t r[2][NW];
+                                 rec(k[e], dlo, dhi, r[0]);
+                                 rec(k[e + 1], dlo, dhi, r[1]);
+                                 bin_put_batch<2, NW>(B, a2, pk, 0u, bins, BS, W, r, gp(ps.recs_v), lane, dbg);
+                               });
+                continue;
+              }
+              mv_key_records<4>(mwords, mnb, mrm, mstride, cs->admit, pick(key, i), a0, nv, lane,
                                 [&](const bool (&act)[4], const uint32_t (&k)[4], const int (&own)[4]) {
                                   uint32_t pk[4], r[4][NW];
 #pragma unroll

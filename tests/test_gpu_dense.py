@@ -149,3 +149,23 @@ def test_dense_not_chosen_for_sparse_or_wide(own_dicts):
         q = parse_sql(sql)
         got = _run(q, gs, expect_dense=dense)
         assert_same(got, oracle.run_query(q, segs), DOUBLE_REL)
+
+
+@pytest.mark.parametrize("flags", [0, L.PA_QF_BOX_FILTER, L.PA_QF_NO_BOX_FILTER, L.PA_QF_BOX_FILTER | L.PA_QF_NO_REG_STAGE])
+@pytest.mark.parametrize("dicts", ["own", "shared"])
+def test_dense_box_filter(own_dicts, shared_dict, dicts, flags):
+    """The key box as the filter (unit range clauses on group-by columns only: every doc box-checked, no filter pass,
+    no walk), forced at any selectivity, disabled, and automatic; filters the box does not capture exactly (a second
+    column, disjoint or empty ranges) keep the filter path. Groups and numDocsScanned identical to the oracle."""
+    segs, gs = own_dicts if dicts == "own" else shared_dict
+    for sql in (
+            "SELECT day, COUNT(*), SUM(dl), MAX(rd) FROM t WHERE day BETWEEN 1500 AND 2500 GROUP BY day LIMIT 2000",
+            "SELECT day, COUNT(*), SUM(da), MIN(rl) FROM t WHERE day >= 3900 GROUP BY day LIMIT 2000",
+            "SELECT w, h, COUNT(*), SUM(ri), SUM(dd) FROM t WHERE w BETWEEN 10 AND 17 AND h >= 2 GROUP BY w, h",
+            "SELECT w, SUM(rs), MAX(dw) FROM t WHERE w > 5 AND w < 30 AND w <= 20 GROUP BY w",
+            "SELECT w, COUNT(*) FROM t WHERE w > 30 AND w < 10 GROUP BY w",
+            "SELECT w, COUNT(*), SUM(ri) FROM t WHERE w BETWEEN 10 AND 12 AND day < 3000 GROUP BY w",
+            "SELECT w, h, COUNT(*) FROM t WHERE w BETWEEN 100 AND 200 GROUP BY w, h"):
+        q = parse_sql(sql)
+        got = _run(q, gs, flags=flags, expect_dense=None)
+        assert_same(got, oracle.run_query(q, segs), DOUBLE_REL)
