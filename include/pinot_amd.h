@@ -199,8 +199,8 @@ typedef struct {
                                              LDS tables) */
 #define PA_QF_NO_BOX_FILTER (1 << 19)     /* dense GROUP BY kernel: evaluate the filter even when it is exactly the group-key
                                              box (unit range clauses on group-by columns), then walk the matching docs */
-#define PA_QF_BOX_FILTER (1 << 20)        /* dense GROUP BY kernel: take the key box as the filter at any selectivity (default:
-                                             at 30 % and above; below it the walk over the filter's matches is cheaper) */
+#define PA_QF_BOX_FILTER (1 << 20)        /* dense GROUP BY kernel: take the key box as the filter (every doc box-checked
+                                             instead of filter + walk) when it is exactly the filter; opt-in */
 #define PA_QF_NO_PARTITION (1 << 21)      /* high-cardinality dense GROUP BY: per-doc global atomics, not partitioned */
 #define PA_QF_NO_SPLIT_EMIT (1 << 24)     /* partitioned aggregation with both record streams: one emit kernel for both
                                              (default: a V launch and an H launch, each holding only its own bins) */

@@ -539,6 +539,7 @@ struct pa_query {
   DevBuf dq_h;
   int emit_h_strat = 0, emit_h_lds = 0, emit_h_ring = 0, emit_h_wg = 0;
   int count_k = 1;      // count-pass workgroups per emit workgroup
+  int count_skip = -1;  // count pass: the group-by component it neither stages nor decodes (plan_partitions)
   size_t sc_hist = 0, sc_off = 0, sc_base = 0, sc_recs_v = 0, sc_recs_h = 0, sc_bytes = 0;
   int scratch_dev = 0;
   int64_t last_matched = -1;  // numDocsScanned read by the last fetch
@@ -1091,8 +1092,8 @@ int plan_gdense(pa_query* q, Prep& P) {
   }
   P.gd_nkeys = (int)nkeys;
   // the box as the filter from 30 % selectivity up (below it the filter + walk over the matches costs less VALU)
-  P.gd_box = box_exact && !(s.flags & PA_QF_NO_BOX_FILTER) &&
-             ((s.flags & PA_QF_BOX_FILTER) || P.post_density >= 0.3 * kWTileDocs);
+  // (opt-in: measured slower than filter + walk on configs[0]'s GROUP BY day at 50 %, r04_d10)
+  P.gd_box = box_exact && !(s.flags & PA_QF_NO_BOX_FILTER) && (s.flags & PA_QF_BOX_FILTER);
   // per-segment key tables where some segment remaps the column
   size_t tab_bytes = 0;
   P.gd_tables = 0;
@@ -1632,7 +1633,9 @@ std::vector<DevSeg> count_pass_segments(const pa_query* q, const Prep& P) {
       if (dc.lds_off < 0) continue;
       bool filter_col = false;
       for (size_t li = 0; li < q->literals.size(); ++li) filter_col |= d.leaves[li].slot == sl;
-      if (P.slot_gb[sl] || filter_col) {
+      bool gb_col = false;  // a group-by column the count pass decodes
+      for (int j = 0; j < q->spec.num_group_by; ++j) gb_col |= P.gb_slot[j] == sl && j != q->count_skip;
+      if (gb_col || filter_col) {
         d.stage[d.num_staged++] = StageDesc{dc.words, dc.nbits, 0};
       } else {
         dc.lds_off = -1;
@@ -1838,6 +1841,20 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
     emit_plan = plan_emit(vstream ? fmt : -1, hll >= 0 ? 1 : 0, vstream, hll >= 0, bs_v, bs_h, q->emit_strat);
   }
   if (emit_plan.score < 0) { PLAN_LOG("partitioned: no (exit 8)"); return false; }
+  // The count pass needs only a key's partition (key >> shift). Component 0 of a direct key space with a power-of-two
+  // cardinality no larger than the partition's key range never changes it: every other stride is a multiple of that
+  // cardinality, so the rest of the key is a multiple of it below the shift and component 0 cannot carry into the
+  // partition bits (configs[2]: d1 of GROUP BY d1, d2 — the count pass reads d2 only).
+  q->count_skip = -1;
+  {
+    const int64_t c0 = s.num_group_by > 0 ? s.group_by_cardinality[0] : 0;
+    const int sh = std::min(vstream ? ksv : 63, hll >= 0 ? (int)__builtin_ctzll((uint64_t)kr_h) : 63);
+    bool ok = s.num_group_by > 1 && !q->hashed && !q->limit_walk && P.stride[0] == 1 && c0 > 0 &&
+              (c0 & (c0 - 1)) == 0 && c0 <= (int64_t(1) << std::min(sh, 62));
+    for (size_t li = 0; li < q->literals.size() && ok; ++li) ok = P.leaf_slot[q->literals[li].leaf] != P.gb_slot[0];
+    for (int j = 1; j < s.num_group_by && ok; ++j) ok = P.gb_slot[j] != P.gb_slot[0];
+    if (ok) q->count_skip = 0;
+  }
   q->hsegs_count = count_pass_segments(q, P);
   count_plan = plan_tiles(q, q->hsegs_count, STRAT_PCOUNT, false, ((size_t)Ptot * 4 + 15) & ~(size_t)15, true);
   if (count_plan.score < 0) { PLAN_LOG("partitioned: no (exit 9)"); return false; }
@@ -2158,6 +2175,7 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
   }
   h.has_mv = q->has_mv;
   h.gb_mv = std::max(-1, mv_group_component(q));
+  h.count_skip_gb = -1;
   h.xcd_major = (P.dense || is_gdense(q->strategy)) ? 1 : 0;
   h.lds_count_off = 0;
   h.lds_acc_bytes = (q->strategy == STRAT_LDS || is_gdense(q->strategy) || is_lane(q->strategy))
@@ -2622,6 +2640,7 @@ int pa_query_prepare(pa_query* q) {
     DevQuery& c = q->hq_count;
     c = q->hq;
     c.strategy = STRAT_PCOUNT;
+    c.count_skip_gb = q->count_skip;
     c.image_dwords_max = count_plan.img_dw;
     c.ring = count_plan.ring;
     c.dma_per_tile = count_plan.dma;

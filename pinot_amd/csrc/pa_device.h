@@ -248,7 +248,7 @@ struct DevQuery {
                              // key offset << (log2m + 6) | register << 6 | rank << 1 | first
   int32_t emit_val_agg;      // V_FMT_ID/32/64: the aggregation whose column the value comes from (-1: COUNT only)
   int32_t gb_mv;             // the multi-value group-by component (V records: one per (doc, value) pair), -1: none
-  int32_t pad_gb_mv;
+  int32_t count_skip_gb;     // count pass: a group-by component that cannot change a key's partition (not staged), -1
   int32_t part_lo, part_hi;   // emit pass: the partitions this launch emits ([0, pv) V, [pv, P) H, or all)
   int32_t debug_emit;        // measurement only (PA_DEBUG_EMIT): bit 0 skips the emit pass's record stores, bit 1 its HLL
                              // dictionary gathers, bit 2 its MV value reads (wrong results; isolates the waits)

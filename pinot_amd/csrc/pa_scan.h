@@ -848,21 +848,31 @@ __device__ __forceinline__ bool leaf_match_doc(const DevLeaf& L, int64_t doc) {
 // docs wave w of the scan listed; then the list: wave w's slice of leap_cap entries at [3 nseg + 1 + slices + w cap],
 // one (segment << 40 | doc << 1 | both) per E doc (a wave appends to its own slice: no atomic, no wait); after the
 // slices, the search's [slices + 1] prefix sums of their lengths and the slices copied into one contiguous list.
-constexpr int kLeapSearchSteps = 64;  // 4096 docs
+constexpr int kLeapSearchSteps = 16;  // steps of kLeapSearchDocs docs: 4096 docs
+constexpr int kLeapSearchDocs = 4 * kWave;
 
 // Label of the nearest labelled doc at or beyond `from` in direction dir (+1 / -1) inside the segment: 1, 2, 3; 0 if
-// the segment ends first; 4 if the search gave up.
+// the segment ends first; 4 if the search gave up. A step reads 256 docs (4 per lane, their loads in flight together:
+// a step costs one round trip, so a wide step shortens the search's dependent chain).
 __device__ __noinline__ uint32_t leap_search(const DevSeg* seg_in, int64_t from, int dir, int lane) {
   const DevSeg* __restrict__ seg = uniform_ptr(seg_in);
   const int64_t n = seg->num_docs;
   for (int k = 0; k < kLeapSearchSteps; ++k) {
-    const int64_t d = from + (int64_t)dir * (int64_t)(kWave * k + lane);
-    const bool in = d >= 0 && d < n;
-    uint32_t lbl = 0u;
-    if (in) lbl = (leaf_match_doc(seg->leaves[1], d) ? 1u : 0u) | (leaf_match_doc(seg->leaves[0], d) ? 2u : 0u);
-    const uint64_t hit = __ballot(lbl != 0u);
-    if (hit) return (uint32_t)__builtin_amdgcn_readlane((int)lbl, __builtin_ctzll(hit));  // lane order = distance
-    if (__ballot(in) != ~0ull) return 0u;
+    uint32_t lbl[4];
+    bool in[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t d = from + (int64_t)dir * (int64_t)(kLeapSearchDocs * k + kWave * r + lane);
+      in[r] = d >= 0 && d < n;
+      lbl[r] = 0u;
+      if (in[r]) lbl[r] = (leaf_match_doc(seg->leaves[1], d) ? 1u : 0u) | (leaf_match_doc(seg->leaves[0], d) ? 2u : 0u);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // nearer rows first; in a row, lane order = distance
+      const uint64_t hit = __ballot(lbl[r] != 0u);
+      if (hit) return (uint32_t)__builtin_amdgcn_readlane((int)lbl[r], __builtin_ctzll(hit));
+      if (__ballot(in[r]) != ~0ull) return 0u;
+    }
   }
   return 4u;
 }
@@ -1188,7 +1198,8 @@ __device__ __forceinline__ void part_keys(const DevQuery* __restrict__ q, CSegT*
 #pragma unroll
   for (int i = 0; i < N; ++i) key[i] = 0u;
   for (int j = 0; j < q->num_gb; ++j) {
-    if (j == q->gb_mv) continue;  // (the multi-value component: per value, mv_key_records)
+    // (the multi-value component: per value, mv_key_records; the count pass's skipped component: below the partition)
+    if (j == q->gb_mv || j == q->count_skip_gb) continue;
     const int slot = q->gb_slot[j];
     const int gl = cs->cols[slot].lds_off, gn = cs->cols[slot].nbits;
     const uint32_t* gw = cs->cols[slot].words;
@@ -1401,6 +1412,46 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
   // steps per batch (register budget; 4 for the H-only emit measured slower: 4.83 vs 4.65 ms). The V-only emit of
   // 4-wave workgroups runs at most 2 workgroups per CU (its LDS bins), so it has the VGPRs for a whole tile per batch.
   constexpr int kEB = (is_pemit(STRAT) && !pemit_hh(STRAT) && !pemit_big(STRAT) && pemit_vf(STRAT) != V_FMT_GEN) ? 16 : 8;
+  if constexpr (STRAT == STRAT_PCOUNT && !LM) {
+    // Count pass of GROUP BY <sv>, <mv> whose SV component cannot change a partition (count_skip_gb): a record's
+    // partition is (value id * stride) >> shift, so a tile whose docs all match counts its whole value range as one
+    // coalesced stream (no per-doc expansion)
+    if (gmv >= 0 && q->num_gb == 2 && q->count_skip_gb == 1 - gmv && cs->admit == nullptr) {
+      const int64_t nd = (int64_t)cs->num_docs, rem = nd - doc_base;
+      uint32_t valid = STEPS == 32 ? 0xffffffffu : ((1u << STEPS) - 1u);
+      if (rem < STEPS * kWave) {
+        const int64_t n = rem > lane ? (rem - lane + kWave - 1) / kWave : 0;
+        valid = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
+      }
+      if (__ballot(m != valid) == 0) {
+        const int64_t d1 = rem < STEPS * kWave ? nd : doc_base + STEPS * kWave;
+        const int64_t vlo = gp(moff)[doc_base], vhi = gp(moff)[d1];
+        lds_u32_t* hist = lds_ptr(lds);
+        constexpr int kVB = 4;
+#pragma unroll 1
+        for (int64_t v = vlo; v < vhi; v += kVB * kWave) {
+          int64_t vi[kVB];
+          bool on[kVB];
+          uint32_t id[kVB];
+#pragma unroll
+          for (int k = 0; k < kVB; ++k) {
+            vi[k] = v + k * kWave + lane;
+            on[k] = vi[k] < vhi;
+          }
+          decode_global_batch<kVB>(mwords, vi, on, mnb, id);
+          if (mrm != nullptr) {
+#pragma unroll
+            for (int k = 0; k < kVB; ++k)
+              if (on[k]) id[k] = (uint32_t)gp(mrm)[id[k]];
+          }
+#pragma unroll
+          for (int k = 0; k < kVB; ++k)
+            if (on[k]) __hip_atomic_fetch_add(hist + ((id[k] * mstride) >> ksv), 1u, WG_RLX);
+        }
+        return;
+      }
+    }
+  }
 #pragma unroll 1
   for (int h = 0; h < STEPS; h += kEB) {
     if (__ballot((m >> h) != 0) == 0) break;  // wave-uniform: the H records below shuffle across all 64 lanes
@@ -1411,6 +1462,12 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
       if (gmv >= 0) {  // one V record per (doc, value): count each value's partition
         int32_t v0[kEB], v1[kEB];
         mv_ranges<kEB, LM>(true, moff, (int64_t)cs->num_docs, doc_base, h, m, lane, v0, v1);
+        if (q->count_skip_gb == gmv && cs->admit == nullptr) {  // the MV component cannot change the partition
+#pragma unroll
+          for (int i = 0; i < kEB; ++i)
+            if (v1[i] > v0[i]) __hip_atomic_fetch_add(hist + (key[i] >> ksv), (uint32_t)(v1[i] - v0[i]), WG_RLX);
+          continue;
+        }
 #pragma unroll 1
         for (int i = 0; i < kEB; ++i) {
           if (__ballot((m >> (h + i)) & 1u) == 0) continue;
