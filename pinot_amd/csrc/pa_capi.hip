@@ -540,6 +540,7 @@ struct pa_query {
   int emit_h_strat = 0, emit_h_lds = 0, emit_h_ring = 0, emit_h_wg = 0;
   int count_k = 1;      // count-pass workgroups per emit workgroup
   int count_skip = -1;  // count pass: the group-by component it neither stages nor decodes (plan_partitions)
+  int count_strat = STRAT_PCOUNT;  // STRAT_PCOUNT, or STRAT_PCOUNT_MV for a multi-value group-by
   size_t sc_hist = 0, sc_off = 0, sc_base = 0, sc_recs_v = 0, sc_recs_h = 0, sc_bytes = 0;
   int scratch_dev = 0;
   int64_t last_matched = -1;  // numDocsScanned read by the last fetch
@@ -1800,7 +1801,7 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
     static const int force_big = std::getenv("PA_EMIT_BIG") ? std::atoi(std::getenv("PA_EMIT_BIG")) : -1;  // (measurement)
     for (int big : {0, 1}) {
       if (force_big >= 0 && big != force_big) continue;
-      const int es = pemit_strat(vf, hh, big);
+      const int es = pemit_strat(vf, hh, big, mvc >= 0 ? 1 : 0);
       const int wpw = scan_waves(es);
       int v = bv, h2 = bh;
       TilePlan e = plan_tiles(q, q->hsegs, es, false, lds_of(v, h2), true);
@@ -1856,7 +1857,8 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
     if (ok) q->count_skip = 0;
   }
   q->hsegs_count = count_pass_segments(q, P);
-  count_plan = plan_tiles(q, q->hsegs_count, STRAT_PCOUNT, false, ((size_t)Ptot * 4 + 15) & ~(size_t)15, true);
+  q->count_strat = mvc >= 0 ? STRAT_PCOUNT_MV : STRAT_PCOUNT;
+  count_plan = plan_tiles(q, q->hsegs_count, q->count_strat, false, ((size_t)Ptot * 4 + 15) & ~(size_t)15, true);
   if (count_plan.score < 0) { PLAN_LOG("partitioned: no (exit 9)"); return false; }
 
   // descriptors (the rest of hq is filled by fill_devquery)
@@ -2445,7 +2447,7 @@ int upload_descriptors(pa_query* q) {
   if (q->partitioned) {
     PA_HIP(set_scan_lds_limit(q->emit_strat, q->steps, 0, q->lds_bytes));
     if (q->split_emit) PA_HIP(set_scan_lds_limit(q->emit_h_strat, q->steps, 0, q->emit_h_lds));
-    PA_HIP(set_scan_lds_limit(STRAT_PCOUNT, q->steps, 0, q->count_lds));
+    PA_HIP(set_scan_lds_limit(q->count_strat, q->steps, 0, q->count_lds));
     PA_HIP(set_part_agg_lds_limit(q->part_vk, q->part_lds_c));
   } else {
     PA_HIP(set_scan_lds_limit(q->strategy, q->steps, q->lane_major, q->lds_bytes));
@@ -2639,7 +2641,7 @@ int pa_query_prepare(pa_query* q) {
     if (ct != total_tiles) return fail(PA_EINVAL, "internal: count pass tiles differ");
     DevQuery& c = q->hq_count;
     c = q->hq;
-    c.strategy = STRAT_PCOUNT;
+    c.strategy = q->count_strat;
     c.count_skip_gb = q->count_skip;
     c.image_dwords_max = count_plan.img_dw;
     c.ring = count_plan.ring;
@@ -2731,7 +2733,7 @@ int pa_query_scan(pa_query* q, void* stream) {
     if (a->used && a->last_stream != st) PA_HIP(hipStreamWaitEvent(st, a->last, 0));
     const PartScratch ps = scratch_of(q, a->p);
     const LmSegPlan* plans = (const LmSegPlan*)q->dplans.p;
-    PA_HIP(launch_scan(STRAT_PCOUNT, q->steps, 0, q->grid * q->count_k, q->count_lds, (const DevQuery*)q->dq_count.p,
+    PA_HIP(launch_scan(q->count_strat, q->steps, 0, q->grid * q->count_k, q->count_lds, (const DevQuery*)q->dq_count.p,
                        (const DevSeg*)q->dsegs_count.p, plans, ps, st));
     PA_HIP(launch_part_offsets(&q->hq, ps, q->grid, q->count_k, st));
     PA_HIP(launch_scan(q->emit_strat, q->steps, 0, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p,

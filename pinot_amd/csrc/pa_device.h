@@ -49,8 +49,11 @@ enum Strategy : int32_t {
   STRAT_GDENSE12 = 10,
   // STRAT_GDENSE with register-staged tiles (gdense_rs_kernel): 12 waves, 4 tiles of <= 4 instructions in VGPRs; 8 waves,
   // 3 tiles of <= 12 instructions
-  STRAT_GDENSE_RS12 = 11, STRAT_GDENSE_RS8 = 12
+  STRAT_GDENSE_RS12 = 11, STRAT_GDENSE_RS8 = 12,
+  // the count pass of a query grouping by a multi-value column (one record per (doc, value) pair)
+  STRAT_PCOUNT_MV = 13
 };
+__host__ __device__ constexpr bool is_pcount(int s) { return s == STRAT_PCOUNT || s == STRAT_PCOUNT_MV; }
 // STRAT_GDENSE: 4-wave workgroups; STRAT_GDENSE8 / STRAT_GDENSE12: the same kernel with 8- / 12-wave workgroups (2 / 3
 // waves per SIMD when one workgroup fits a CU, e.g. beside a 64 KiB value table: the walk's LDS round trips and VALU
 // issue overlap across waves; 12 waves: step-major tiles only)
@@ -95,13 +98,17 @@ constexpr int kLaneHistMax = 16384;  // STRAT_LANE_DICT: largest shared dictiona
 // leaves LDS for more resident waves when the tile images are small).
 constexpr int kPemitBase = 16;
 constexpr int kEmitBigWaves = 16;
-__host__ __device__ constexpr int pemit_strat(int vf, int hh, int big = 0) {
-  return kPemitBase + 2 * (vf + 1) + (hh ? 1 : 0) + (big ? 16 : 0);
+// `mv`: the V records of a multi-value group-by (one per (doc, value) pair; V stream only, no generic records).
+__host__ __device__ constexpr int pemit_strat(int vf, int hh, int big = 0, int mv = 0) {
+  return kPemitBase + 2 * (vf + 1) + (hh ? 1 : 0) + (big ? 16 : 0) + (mv ? 32 : 0);
 }
 __host__ __device__ constexpr bool is_pemit(int s) { return s >= kPemitBase; }
 __host__ __device__ constexpr int pemit_vf(int s) { return (((s - kPemitBase) & 15) >> 1) - 1; }
 __host__ __device__ constexpr bool pemit_hh(int s) { return ((s - kPemitBase) & 1) != 0; }
-__host__ __device__ constexpr int pemit_big(int s) { return (s - kPemitBase) >= 16 ? 1 : 0; }
+__host__ __device__ constexpr int pemit_big(int s) { return ((s - kPemitBase) >> 4) & 1; }
+__host__ __device__ constexpr bool pemit_mv(int s) { return is_pemit(s) && (s - kPemitBase) >= 32; }
+// a partitioned pass (count or emit) of a multi-value group-by
+__host__ __device__ constexpr bool part_mv(int s) { return s == STRAT_PCOUNT_MV || pemit_mv(s); }
 __host__ __device__ constexpr int scan_waves(int s) {
   return is_pemit(s) && pemit_big(s) ? kEmitBigWaves
                                        : (s == STRAT_GDENSE8 || s == STRAT_GDENSE_RS8) ? 2 * kGdWaves

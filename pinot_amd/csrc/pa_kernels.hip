@@ -1747,6 +1747,7 @@ static const void* scan_fn(int strategy, int steps, int lm) {
   if (const void* f = scan_fn_std(strategy, steps, lm)) return f;
   if (const void* f = scan_fn_gdense(strategy, lm)) return f;
   if (const void* f = scan_fn_part_a(strategy)) return f;
+  if (const void* f = scan_fn_part_mv(strategy)) return f;
   return scan_fn_part_b(strategy);
 }
 

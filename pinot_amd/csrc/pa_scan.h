@@ -1286,8 +1286,8 @@ __device__ __forceinline__ void mv_key_records(const uint32_t* words, int nb, co
 
 // The same records, each lane its own doc (every doc of the step has at most kDocVals values): all of a doc's values
 // decoded in one batch (the step's docs are consecutive, so their values are one short stretch of the stream and the
-// loads nearly coalesce), no cross-lane shuffles; f(act, key) for value index e = 0 .. maxn - 1 (maxn: the wave's
-// largest count).
+// loads nearly coalesce), no cross-lane shuffles; f(act, key) takes all of them (act[e]: value e exists and is
+// admitted).
 template <class F>
 __device__ __forceinline__ void mv_doc_records(const uint32_t* words, int nb, const int32_t* rm, uint32_t stride,
                                                const uint32_t* adm, uint32_t base, int32_t v0, uint32_t n,
@@ -1315,9 +1315,8 @@ __device__ __forceinline__ void mv_doc_records(const uint32_t* words, int nb, co
 #pragma unroll
     for (int e = 0; e < kDocVals; ++e) on[e] = on[e] && ((w[e] >> (key[e] & 31u)) & 1u);
   }
-#pragma unroll
-  for (int e = 0; e < kDocVals; e += 2)
-    if ((uint32_t)e < maxn) f(e, on, key);
+  f(on, key);
+  (void)maxn;
 }
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
@@ -1384,35 +1383,24 @@ __device__ __forceinline__ void part_vvals(const DevQuery* __restrict__ q, CSegT
   }
 }
 
-// The matching docs of one tile (match words m) in the count pass (STRAT_PCOUNT: per (workgroup, partition) record
-// counts in LDS) or the emit pass (STRAT_PEMIT: the records into the partition bins). Per batch of 8 steps: every
-// group-by dictId decode, then every remap gather (they overlap), then the table-wide keys; then per stream.
+// part_tile of a query grouping by a multi-value column (one V record per (doc, value) pair; V stream only, no
+// generic records): the kernel variants STRAT_PCOUNT_MV / pemit_strat(.., mv = 1), so its expansion's registers stay out
+// of the SV variants' allocation.
 template <int STRAT, int STEPS, int LM>
-__device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+__device__ __forceinline__ void part_tile_mv(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
                                           const uint32_t* img, int64_t doc_base, uint32_t m, int lane,
                                           unsigned char* lds, const PartScratch& ps) {
-  // Descriptors through the constant address space: the segment is read-only during the kernel and its pointer is
-  // wave-uniform, so every field is a scalar load the compiler keeps across the LDS atomics and the record stores.
-  CSegT* cs = (CSegT*)(uintptr_t)seg;
-  auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
-  const int pv = q->pv;
-  const int ksv = q->kshift_v, ksh = q->kshift_h;
-  const int ha = q->hll_agg;
-  const int hslot = ha >= 0 ? q->aggs[ha].slot : 0;
-  const bool hmv = ha >= 0 && cs->cols[hslot].kind == COL_MV_DICT;
-  const int32_t* hoff = cs->cols[hslot].mv_off;
-  // a multi-value group-by column (V stream only): one V record per (doc, value), mv_key_records
+  CSegT* cs = (CSegT*)(uintptr_t)uniform_ptr(seg);
+  const int ksv = q->kshift_v;
   const int gmv = q->gb_mv;
-  const int mslot = gmv >= 0 ? q->gb_slot[gmv] : 0;
+  const int mslot = q->gb_slot[gmv];
   const int32_t* moff = cs->cols[mslot].mv_off;
   const uint32_t* mwords = cs->cols[mslot].words;
   const int mnb = cs->cols[mslot].nbits;
-  const int32_t* mrm = gmv >= 0 ? cs->remap[gmv] : nullptr;
-  const uint32_t mstride = gmv >= 0 ? (uint32_t)q->gb_stride[gmv] : 0u;
-  // steps per batch (register budget; 4 for the H-only emit measured slower: 4.83 vs 4.65 ms). The V-only emit of
-  // 4-wave workgroups runs at most 2 workgroups per CU (its LDS bins), so it has the VGPRs for a whole tile per batch.
-  constexpr int kEB = (is_pemit(STRAT) && !pemit_hh(STRAT) && !pemit_big(STRAT) && pemit_vf(STRAT) != V_FMT_GEN) ? 16 : 8;
-  if constexpr (STRAT == STRAT_PCOUNT && !LM) {
+  const int32_t* mrm = cs->remap[gmv];
+  const uint32_t mstride = (uint32_t)q->gb_stride[gmv];
+  constexpr int kEB = 8;
+  if constexpr (is_pcount(STRAT) && !LM) {
     // Count pass of GROUP BY <sv>, <mv> whose SV component cannot change a partition (count_skip_gb): a record's
     // partition is (value id * stride) >> shift, so a tile whose docs all match counts its whole value range as one
     // coalesced stream (no per-doc expansion)
@@ -1454,12 +1442,12 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
   }
 #pragma unroll 1
   for (int h = 0; h < STEPS; h += kEB) {
-    if (__ballot((m >> h) != 0) == 0) break;  // wave-uniform: the H records below shuffle across all 64 lanes
+    if (__ballot((m >> h) != 0) == 0) break;
     uint32_t key[kEB];
-    part_keys<kEB, LM>(q, cs, img, doc_base, h, m, lane, key);  // table-wide key (< 2^32 on this path)
-    if constexpr (STRAT == STRAT_PCOUNT) {
+    part_keys<kEB, LM>(q, cs, img, doc_base, h, m, lane, key);  // (without the MV component)
+    if constexpr (is_pcount(STRAT)) {
       lds_u32_t* hist = lds_ptr(lds);
-      if (gmv >= 0) {  // one V record per (doc, value): count each value's partition
+      {  // one V record per (doc, value): count each value's partition
         int32_t v0[kEB], v1[kEB];
         mv_ranges<kEB, LM>(true, moff, (int64_t)cs->num_docs, doc_base, h, m, lane, v0, v1);
         if (q->count_skip_gb == gmv && cs->admit == nullptr) {  // the MV component cannot change the partition
@@ -1468,16 +1456,17 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
             if (v1[i] > v0[i]) __hip_atomic_fetch_add(hist + (key[i] >> ksv), (uint32_t)(v1[i] - v0[i]), WG_RLX);
           continue;
         }
-#pragma unroll 1
-        for (int i = 0; i < kEB; ++i) {
+#pragma clang loop unroll(full)
+        for (int i = 0; i < kEB; ++i) {  // (unrolled: constant register indices)
           if (__ballot((m >> (h + i)) & 1u) == 0) continue;
           const int32_t a0 = pick(v0, i), a1 = pick(v1, i);
           const uint32_t nv = (uint32_t)(a1 - a0), maxn = wave_max_u32(nv);
           if (maxn <= (uint32_t)kDocVals) {
             mv_doc_records(mwords, mnb, mrm, mstride, cs->admit, pick(key, i), a0, nv, maxn,
-                           [&](int e, const bool (&act)[kDocVals], const uint32_t (&k)[kDocVals]) {
-                             if (act[e]) __hip_atomic_fetch_add(hist + (k[e] >> ksv), 1u, WG_RLX);
-                             if (act[e + 1]) __hip_atomic_fetch_add(hist + (k[e + 1] >> ksv), 1u, WG_RLX);
+                           [&](const bool (&act)[kDocVals], const uint32_t (&k)[kDocVals]) {
+#pragma unroll
+                             for (int e = 0; e < kDocVals; ++e)
+                               if (act[e]) __hip_atomic_fetch_add(hist + (k[e] >> ksv), 1u, WG_RLX);
                            });
             continue;
           }
@@ -1490,38 +1479,22 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
         }
         continue;
       }
-      uint32_t n[kEB];
-      {
-        int32_t v0[kEB], v1[kEB];
-        mv_ranges<kEB, LM>(hmv, hoff, (int64_t)cs->num_docs, doc_base, h, m, lane, v0, v1);
-#pragma unroll
-        for (int i = 0; i < kEB; ++i) n[i] = v1[i] - v0[i] > 0 ? (uint32_t)(v1[i] - v0[i]) : 1u;
-      }
-#pragma unroll
-      for (int i = 0; i < kEB; ++i) {
-        if (!((m >> (h + i)) & 1u)) continue;
-        if (pv) __hip_atomic_fetch_add(hist + (key[i] >> ksv), 1u, WG_RLX);
-        if (ha >= 0) __hip_atomic_fetch_add(hist + pv + (key[i] >> ksh), n[i], WG_RLX);
-      }
     } else {
       constexpr int VF = pemit_vf(STRAT);
+      constexpr int NW = VF == V_FMT_32 ? 2 : (VF == V_FMT_64 ? 3 : 1);
       const BinState B = bin_state(q, lds);
       const int dbg = q->debug_emit;
-      if constexpr (VF >= 0) {
-        // V records: the value (or its table-wide value id) of the one payload column, batched like the keys
-        constexpr int NW = VF == V_FMT_GEN ? kMaxVWords : (VF == V_FMT_32 ? 2 : (VF == V_FMT_64 ? 3 : 1));
-        const uint32_t W = VF == V_FMT_GEN ? (uint32_t)q->rec_words_v : (uint32_t)NW;
-        const uint32_t BS = (uint32_t)q->bs_v;
-        lds_u32_t* bins = lds_ptr(lds + q->lds_bins_v);
-        const uint32_t kmask = (1u << ksv) - 1u;
-        uint32_t lo[kEB], hi[kEB];
-        part_vvals<kEB, LM, VF>(q, cs, img, doc_base, h, m, lane, lo, hi);
-        if constexpr (VF != V_FMT_GEN) {
-          if (gmv >= 0) {  // one record per (doc, value) pair, the doc's payload on each
+      const uint32_t W = (uint32_t)NW;
+      const uint32_t BS = (uint32_t)q->bs_v;
+      lds_u32_t* bins = lds_ptr(lds + q->lds_bins_v);
+      const uint32_t kmask = (1u << ksv) - 1u;
+      uint32_t lo[kEB], hi[kEB];
+      part_vvals<kEB, LM, VF>(q, cs, img, doc_base, h, m, lane, lo, hi);
+          {  // one record per (doc, value) pair, the doc's payload on each
             int32_t v0[kEB], v1[kEB];
             mv_ranges<kEB, LM>(true, moff, (int64_t)cs->num_docs, doc_base, h, m, lane, v0, v1);
-#pragma unroll 1
-            for (int i = 0; i < kEB; ++i) {
+#pragma clang loop unroll(full)
+            for (int i = 0; i < kEB; ++i) {  // (unrolled: constant register indices)
               if (__ballot((m >> (h + i)) & 1u) == 0) continue;
               const int32_t a0 = pick(v0, i), a1 = pick(v1, i);
               const uint32_t dlo = pick(lo, i), dhi = pick(hi, i);
@@ -1540,15 +1513,16 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
                   r[2] = phi;
                 }
               };
-              if (maxn <= (uint32_t)kDocVals) {  // each lane its own doc's records, two per put
+              if (maxn <= (uint32_t)kDocVals) {  // each lane its own doc's records, all in one put (one wait per phase)
                 mv_doc_records(mwords, mnb, mrm, mstride, cs->admit, pick(key, i), a0, nv, maxn,
-                               [&](int e, const bool (&act)[kDocVals], const uint32_t (&k)[kDocVals]) {
-                                 const bool a2[2] = {act[e], act[e + 1]};
-                                 const uint32_t pk[2] = {k[e] >> ksv, k[e + 1] >> ksv};
-                                 uint32_t r[2][NW];
-                                 rec(k[e], dlo, dhi, r[0]);
-                                 rec(k[e + 1], dlo, dhi, r[1]);
-                                 bin_put_batch<2, NW>(B, a2, pk, 0u, bins, BS, W, r, gp(ps.recs_v), lane, dbg);
+                               [&](const bool (&act)[kDocVals], const uint32_t (&k)[kDocVals]) {
+                                 uint32_t pk[kDocVals], r[kDocVals][NW];
+#pragma unroll
+                                 for (int e = 0; e < kDocVals; ++e) {
+                                   pk[e] = k[e] >> ksv;
+                                   rec(k[e], dlo, dhi, r[e]);
+                                 }
+                                 bin_put_batch<kDocVals, NW>(B, act, pk, 0u, bins, BS, W, r, gp(ps.recs_v), lane, dbg);
                                });
                 continue;
               }
@@ -1576,6 +1550,68 @@ __device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const 
             }
             continue;
           }
+    }
+  }
+}
+
+// The matching docs of one tile (match words m) in the count pass (STRAT_PCOUNT: per (workgroup, partition) record
+// counts in LDS) or the emit pass (STRAT_PEMIT: the records into the partition bins). Per batch of 8 steps: every
+// group-by dictId decode, then every remap gather (they overlap), then the table-wide keys; then per stream.
+template <int STRAT, int STEPS, int LM>
+__device__ __forceinline__ void part_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
+                                          const uint32_t* img, int64_t doc_base, uint32_t m, int lane,
+                                          unsigned char* lds, const PartScratch& ps) {
+  // Descriptors through the constant address space: the segment is read-only during the kernel and its pointer is
+  // wave-uniform, so every field is a scalar load the compiler keeps across the LDS atomics and the record stores.
+  CSegT* cs = (CSegT*)(uintptr_t)seg;
+  auto local = [&](int i) { return LM ? 32 * lane + i : i * kWave + lane; };
+  const int pv = q->pv;
+  const int ksv = q->kshift_v, ksh = q->kshift_h;
+  const int ha = q->hll_agg;
+  const int hslot = ha >= 0 ? q->aggs[ha].slot : 0;
+  const bool hmv = ha >= 0 && cs->cols[hslot].kind == COL_MV_DICT;
+  const int32_t* hoff = cs->cols[hslot].mv_off;
+  // steps per batch (register budget; 4 for the H-only emit measured slower: 4.83 vs 4.65 ms). The V-only emit of
+  // 4-wave workgroups runs at most 2 workgroups per CU (its LDS bins), so it has the VGPRs for a whole tile per batch.
+  constexpr int kEB = (is_pemit(STRAT) && !pemit_hh(STRAT) && !pemit_big(STRAT) && pemit_vf(STRAT) != V_FMT_GEN) ? 16 : 8;
+  if constexpr (part_mv(STRAT)) {
+    part_tile_mv<STRAT, STEPS, LM>(q, seg, img, doc_base, m, lane, lds, ps);
+    return;
+  }
+#pragma unroll 1
+  for (int h = 0; h < STEPS; h += kEB) {
+    if (__ballot((m >> h) != 0) == 0) break;  // wave-uniform: the H records below shuffle across all 64 lanes
+    uint32_t key[kEB];
+    part_keys<kEB, LM>(q, cs, img, doc_base, h, m, lane, key);  // table-wide key (< 2^32 on this path)
+    if constexpr (is_pcount(STRAT)) {
+      lds_u32_t* hist = lds_ptr(lds);
+      uint32_t n[kEB];
+      {
+        int32_t v0[kEB], v1[kEB];
+        mv_ranges<kEB, LM>(hmv, hoff, (int64_t)cs->num_docs, doc_base, h, m, lane, v0, v1);
+#pragma unroll
+        for (int i = 0; i < kEB; ++i) n[i] = v1[i] - v0[i] > 0 ? (uint32_t)(v1[i] - v0[i]) : 1u;
+      }
+#pragma unroll
+      for (int i = 0; i < kEB; ++i) {
+        if (!((m >> (h + i)) & 1u)) continue;
+        if (pv) __hip_atomic_fetch_add(hist + (key[i] >> ksv), 1u, WG_RLX);
+        if (ha >= 0) __hip_atomic_fetch_add(hist + pv + (key[i] >> ksh), n[i], WG_RLX);
+      }
+    } else {
+      constexpr int VF = pemit_vf(STRAT);
+      const BinState B = bin_state(q, lds);
+      const int dbg = q->debug_emit;
+      if constexpr (VF >= 0) {
+        // V records: the value (or its table-wide value id) of the one payload column, batched like the keys
+        constexpr int NW = VF == V_FMT_GEN ? kMaxVWords : (VF == V_FMT_32 ? 2 : (VF == V_FMT_64 ? 3 : 1));
+        const uint32_t W = VF == V_FMT_GEN ? (uint32_t)q->rec_words_v : (uint32_t)NW;
+        const uint32_t BS = (uint32_t)q->bs_v;
+        lds_u32_t* bins = lds_ptr(lds + q->lds_bins_v);
+        const uint32_t kmask = (1u << ksv) - 1u;
+        uint32_t lo[kEB], hi[kEB];
+        part_vvals<kEB, LM, VF>(q, cs, img, doc_base, h, m, lane, lo, hi);
+        if constexpr (VF != V_FMT_GEN) {
           // the batch's records (one per matching doc of the kEB steps) in one put: every LDS phase runs once
           bool act[kEB];
           uint32_t pk[kEB], r[kEB][NW];
@@ -2426,7 +2462,7 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
       }
       if (!ok) m &= ~bit;
     }
-    if constexpr (STRAT != STRAT_PCOUNT && !is_pemit(STRAT))
+    if constexpr (!is_pcount(STRAT) && !is_pemit(STRAT))
       if (q->leap_mode) leap_tile<LM>(q, seg, doc_base, eager, m, lane, la.leap_slice, la.leap_n);
     if (__ballot(m != 0) == 0) return 0;
   }
@@ -2438,7 +2474,7 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
   }
   if constexpr (is_lane(STRAT)) {
     if constexpr (STRAT != STRAT_LANE_CNT) lane_acc_tile<LM, STEPS, STRAT>(q, seg, img, doc_base, m, lane, la, lds);
-  } else if constexpr (STRAT == STRAT_PCOUNT || is_pemit(STRAT)) {
+  } else if constexpr (is_pcount(STRAT) || is_pemit(STRAT)) {
     part_tile<STRAT, STEPS, LM>(q, seg, img, doc_base, m, lane, lds, ps);
 
   } else if (q->has_mv) {
@@ -2764,7 +2800,7 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
       }
     }
     __syncthreads();
-  } else if (STRAT == STRAT_PCOUNT) {
+  } else if (is_pcount(STRAT)) {
     uint32_t* hist = (uint32_t*)lds_acc;
     for (int p = threadIdx.x; p < q->num_parts; p += WGS) hist[p] = 0u;
     __syncthreads();
@@ -2922,7 +2958,7 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
     }
   }
 
-  if constexpr (STRAT != STRAT_PCOUNT && !is_pemit(STRAT))
+  if constexpr (!is_pcount(STRAT) && !is_pemit(STRAT))
     if (q->leap_mode && lane == 0)  // (every wave: the search kernel reads every slice's count)
       gp(q->leap_out)[3 * (int64_t)q->num_segments + 1 + la.leap_slice] = la.leap_n;
   if (!is_pemit(STRAT)) {  // (the partitioned count pass counts numDocsScanned; its emit pass sees the same docs)
@@ -2962,7 +2998,7 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
       if constexpr (STRAT != STRAT_LANE_CNT) lane_acc_flush(q, la, lane);
     }
   }
-  if (STRAT == STRAT_PCOUNT) {
+  if (is_pcount(STRAT)) {
     __syncthreads();
     const uint32_t* hist = (const uint32_t*)lds_acc;
     for (int p = threadIdx.x; p < q->num_parts; p += WGS) gp(ps.hist)[lb * q->num_parts + p] = hist[p];
@@ -3047,6 +3083,7 @@ const void* scan_fn_std(int strategy, int steps, int lm);   // pa_scan_std.hip: 
 const void* scan_fn_lane(int strategy, int steps, int lm);  // pa_scan_lane.hip: LANE and its variants
 const void* scan_fn_part_a(int strategy);                  // pa_scan_part_a.hip: PCOUNT + emit variants (one part)
 const void* scan_fn_part_b(int strategy);                  // pa_scan_part_b.hip: the other emit variants
+const void* scan_fn_part_mv(int strategy);                 // pa_scan_part_mv.hip: the multi-value group-by passes
 const void* scan_fn_gdense(int strategy, int lm);          // pa_scan_gdense.hip: STRAT_GDENSE (pa_gdense.h)
 
 }  // namespace pa

@@ -757,13 +757,22 @@ def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps, leaf_para
     vi, vd = counts[ri, fi], counts[rd, fd]
     if (vi < 0).any() or (vd < 0).any():
         raise RuntimeError("internal: a count the closed forms need was not computed")
-    in_filter = const_in + int(np.dot(vi.astype(object), ci.astype(object))) if len(ri) else const_in
-    post = (const_docs + (int(np.dot(vd.astype(object), cd.astype(object))) if len(rd) else 0)) * plan.ncols
+    in_filter = const_in + _exact_dot(vi, ci)
+    post = (const_docs + _exact_dot(vd, cd)) * plan.ncols
     if host:
         hi, hp = server_stats(query, [segments[si] for si in host], lambda i: leaf_bitmaps(host[i]))
         in_filter += hi
         post += hp
     return in_filter, post
+
+
+def _exact_dot(v, c):
+    """sum(v * c) as a Python int: int64 arithmetic when the magnitude bound keeps it exact, else object arithmetic."""
+    if not len(v):
+        return 0
+    if float(np.abs(v).max()) * float(np.abs(c).sum()) < 2.0 ** 62:
+        return int(np.dot(v.astype(np.int64), c.astype(np.int64)))
+    return int(np.dot(v.astype(object), c.astype(object)))
 
 
 def device_counts(executor, segments, reqs, stream=None):
