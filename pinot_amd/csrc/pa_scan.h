@@ -948,16 +948,16 @@ __device__ __forceinline__ BinState bin_state(const DevQuery* __restrict__ q, un
 // Wave-level put of K records per lane: every lane calls it (uniform control flow); record k of an active lane (the
 // first nw words of r[k]) goes into partition p[k]'s LDS bin of BS records (bins: the stream's partitions from p0 on,
 // BS * nw words each). Phases, each a run of independent LDS operations (one wait per phase, not per record):
-// claim slots (cnt), write them, count them written (done); a record whose bin is full goes straight to the back end
-// of its range (back). The lane whose write completes a bin marks it, and the wave then stores every marked bin of the
-// batch at its range's front slot — several bins per store instruction (L lanes per bin, one 16-byte unit each) —
-// and empties it. Every (workgroup, partition) range holds exactly the records the count pass counted, so front and
-// back meet (checked at the end of the pass).
+// claim slots (cnt), write them, count them written (done). The lane whose write completes a bin marks it, and the
+// wave then stores every marked bin of the batch at its range's front slot — several bins per store instruction (L
+// lanes per bin, one 16-byte unit each) — and empties it; a record whose bin was full claims again after that. Every
+// (workgroup, partition) range holds exactly the records the count pass counted, so front and back meet (checked at
+// the end of the pass; back moves only for H records, which go to the range's end when their bin is full).
 // Ordering: LDS executes the DS instructions of one wave in issue order and serialises those of different waves, so
 // "write the slot, then count it done" and "read the bin, then reset the counters" need only the compiler to keep
 // program order (a signal fence). Acquire/release atomics would also wait for every outstanding global load, i.e.
 // drain the tile ring's LDS-DMA on every record. Only the wave that completed a bin touches its front and counters
-// until it resets them (a bin fills at most once per batch: it stays full until its flush).
+// until it resets them (a bin fills at most once per claim round: it stays full until its flush).
 template <int K, bool SL = false>
 __device__ __forceinline__ void flush_full_bins(const BinState& B, const bool (&full)[K], const uint32_t (&p)[K],
                                                 uint32_t p0, lds_u32_t* bins, uint32_t BS, uint32_t nw,
@@ -969,38 +969,74 @@ __device__ __forceinline__ void bin_put_batch(const BinState& B, const bool (&ac
                                               const uint32_t (&r)[K][WM], AS1 uint32_t* recs, int lane, int dbg,
                                               uint32_t BST = 0) {
   if (BST == 0) BST = BS;
-  uint32_t s[K];
+  if constexpr (SL) {  // (H bins: the 16-wave H variants have no registers to spare for the retry loop)
+    uint32_t s[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) s[k] = act[k] ? __hip_atomic_fetch_add(B.cnt + p[k], 1u, WG_RLX) : 0xffffffffu;
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    if (s[k] < BS) {
-      lds_u32_t* slot = bins + ((p[k] - p0) * BST + s[k]) * nw;
-#pragma unroll
-      for (int w = 0; w < WM; ++w)
-        if ((uint32_t)w < nw) slot[w] = r[k][w];
-    }
-  }
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  bool full[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) full[k] = s[k] < BS && __hip_atomic_fetch_add(B.done + p[k], 1u, WG_RLX) == BS - 1u;
-  if (!(dbg & 1)) {
-    uint32_t o[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-      o[k] = (act[k] && s[k] >= BS) ? __hip_atomic_fetch_sub(B.back + p[k], 1u, WG_RLX) - 1u : 0u;
+    for (int k = 0; k < K; ++k) s[k] = act[k] ? __hip_atomic_fetch_add(B.cnt + p[k], 1u, WG_RLX) : 0xffffffffu;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      if (act[k] && s[k] >= BS) {
-        AS1 uint32_t* d = recs + (B.start[p[k]] + o[k]) * (uint64_t)nw;
+      if (s[k] < BS) {
+        lds_u32_t* slot = bins + ((p[k] - p0) * BST + s[k]) * nw;
 #pragma unroll
         for (int w = 0; w < WM; ++w)
-          if ((uint32_t)w < nw) d[w] = r[k][w];
+          if ((uint32_t)w < nw) slot[w] = r[k][w];
       }
     }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    bool full[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) full[k] = s[k] < BS && __hip_atomic_fetch_add(B.done + p[k], 1u, WG_RLX) == BS - 1u;
+    if (!(dbg & 1)) {  // a record whose bin is full goes straight to the back end of its range
+      uint32_t o[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        o[k] = (act[k] && s[k] >= BS) ? __hip_atomic_fetch_sub(B.back + p[k], 1u, WG_RLX) - 1u : 0u;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (act[k] && s[k] >= BS) {
+          AS1 uint32_t* d = recs + (B.start[p[k]] + o[k]) * (uint64_t)nw;
+#pragma unroll
+          for (int w = 0; w < WM; ++w)
+            if ((uint32_t)w < nw) d[w] = r[k][w];
+        }
+      }
+    }
+    flush_full_bins<K, SL>(B, full, p, p0, bins, BS, nw, recs, lane, dbg, BST);
+    return;
   }
-  flush_full_bins<K, SL>(B, full, p, p0, bins, BS, nw, recs, lane, dbg, BST);
+  // A record whose bin is full (claimed past BS while its completing wave flushes it) retries after this wave has
+  // flushed the bins it completed itself (so no wave waits for a bin whose flusher waits too): every record leaves
+  // through a whole-bin burst, never as a scattered store (a 4-byte store costs a whole 64-byte HBM write).
+  bool pend[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) pend[k] = act[k];
+  for (int round = 0;; ++round) {
+    uint32_t s[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) s[k] = pend[k] ? __hip_atomic_fetch_add(B.cnt + p[k], 1u, WG_RLX) : 0xffffffffu;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (s[k] < BS) {
+        lds_u32_t* slot = bins + ((p[k] - p0) * BST + s[k]) * nw;
+#pragma unroll
+        for (int w = 0; w < WM; ++w)
+          if ((uint32_t)w < nw) slot[w] = r[k][w];
+      }
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    bool full[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) full[k] = s[k] < BS && __hip_atomic_fetch_add(B.done + p[k], 1u, WG_RLX) == BS - 1u;
+    flush_full_bins<K, SL>(B, full, p, p0, bins, BS, nw, recs, lane, dbg, BST);
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      pend[k] = pend[k] && s[k] >= BS;
+      any |= pend[k];
+    }
+    if (__ballot(any) == 0) break;
+    if (round > 0) __builtin_amdgcn_s_sleep(2);  // (the bin's flush is a few hundred cycles away)
+  }
 }
 
 // The flush half of a put: every bin some lane completed (full[k]) is stored at its range's front slot — several bins
