@@ -952,7 +952,7 @@ __device__ __forceinline__ BinState bin_state(const DevQuery* __restrict__ q, un
 // wave then stores every marked bin of the batch at its range's front slot — several bins per store instruction (L
 // lanes per bin, one 16-byte unit each) — and empties it; a record whose bin was full claims again after that. Every
 // (workgroup, partition) range holds exactly the records the count pass counted, so front and back meet (checked at
-// the end of the pass; back moves only for H records, which go to the range's end when their bin is full).
+// the end of the pass). Without RETRY a record whose bin is full goes to the range's back end instead.
 // Ordering: LDS executes the DS instructions of one wave in issue order and serialises those of different waves, so
 // "write the slot, then count it done" and "read the bin, then reset the counters" need only the compiler to keep
 // program order (a signal fence). Acquire/release atomics would also wait for every outstanding global load, i.e.
@@ -963,13 +963,16 @@ __device__ __forceinline__ void flush_full_bins(const BinState& B, const bool (&
                                                 uint32_t p0, lds_u32_t* bins, uint32_t BS, uint32_t nw,
                                                 AS1 uint32_t* recs, int lane, int dbg, uint32_t BST = 0);
 
-template <int K, int WM, bool SL = false>
+template <int K, int WM, bool SL = false, bool RETRY = false>
 __device__ __forceinline__ void bin_put_batch(const BinState& B, const bool (&act)[K], const uint32_t (&p)[K],
                                               uint32_t p0, lds_u32_t* bins, uint32_t BS, uint32_t nw,
                                               const uint32_t (&r)[K][WM], AS1 uint32_t* recs, int lane, int dbg,
                                               uint32_t BST = 0) {
   if (BST == 0) BST = BS;
-  if constexpr (SL) {  // (H bins: the 16-wave H variants have no registers to spare for the retry loop)
+  // RETRY (the MV group-by's V records, several per doc: their bins fill fast and the back path's 4-byte stores
+  // dominated, r04_c1 -> r04_c3 emit 5.76 -> 4.86 ms) or the back path (one record per doc: the retry rounds cost
+  // more than the few scattered stores, configs[2] emit 1.29 -> 1.41 ms, configs[4] V emit 1.5 -> 1.9 ms)
+  if constexpr (!RETRY) {
     uint32_t s[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) s[k] = act[k] ? __hip_atomic_fetch_add(B.cnt + p[k], 1u, WG_RLX) : 0xffffffffu;
@@ -1558,7 +1561,8 @@ __device__ __forceinline__ void part_tile_mv(const DevQuery* __restrict__ q, con
                                    pk[e] = k[e] >> ksv;
                                    rec(k[e], dlo, dhi, r[e]);
                                  }
-                                 bin_put_batch<kDocVals, NW>(B, act, pk, 0u, bins, BS, W, r, gp(ps.recs_v), lane, dbg);
+                                 bin_put_batch<kDocVals, NW, false, true>(B, act, pk, 0u, bins, BS, W, r, gp(ps.recs_v),
+                                                                          lane, dbg);
                                });
                 continue;
               }
@@ -1581,7 +1585,8 @@ __device__ __forceinline__ void part_tile_mv(const DevQuery* __restrict__ q, con
                                       r[kk][2] = (uint32_t)__shfl((int)dhi, own[kk], kWave);
                                     }
                                   }
-                                  bin_put_batch<4, NW>(B, act, pk, 0u, bins, BS, W, r, gp(ps.recs_v), lane, dbg);
+                                  bin_put_batch<4, NW, false, true>(B, act, pk, 0u, bins, BS, W, r, gp(ps.recs_v), lane,
+                                                                    dbg);
                                 });
             }
             continue;

@@ -702,6 +702,43 @@ class _StatsPlan:
             self.full = (reqs, const_in, arr(ti), const_docs, arr(td), host)
         return self.full
 
+    def fused_form(self, e, z, nseg):
+        """The statistics as linear forms of the counts the scan took itself (fused_counts' per-segment matched docs m
+        and leaps l): in_filter = const_in + A.m + B.l, post = (const_docs + C.m) x ncols — or None when some request
+        is not one the scan covers (then fused_counts + the closed forms run). Cached per (E leaf, Z leaf)."""
+        key = ("form", e, z)
+        if key not in self.fused_cache:
+            reqs, const_in, (ri, fi, ci), const_docs, (rd, fd, cd), host = self.flat()
+            form = None
+            if not host and self.reqs:  # (no request: a constant-cost filter, server_stats_closed_form's shortcut)
+                row = {}  # request row -> (segment, kind): 0 the AND request, 1 the whole-filter request
+                ok = True
+                for (si, a, b), r in reqs.items():
+                    if a == (z,) and b == (e,):
+                        row[r] = (si, 0)
+                    elif not b and a in ((z, e, L.PA_BIT_AND), (e, z, L.PA_BIT_AND)):
+                        row[r] = (si, 1)
+                    else:
+                        ok = False
+                A, B, C = (np.zeros(nseg, dtype=np.int64) for _ in range(3))
+                for rows, fields, coef, dst in ((ri, fi, ci, "in"), (rd, fd, cd, "docs")):
+                    for r, f, c in zip(rows.tolist(), fields.tolist(), coef.tolist()):
+                        si, kind = row.get(r, (None, None))
+                        if si is None:
+                            ok = False
+                        elif kind == 0 and f == 2:  # popcount(A & B) = the segment's matched docs
+                            (A if dst == "in" else C)[si] += c
+                        elif kind == 0 and f == 3 and dst == "in":  # leaps
+                            B[si] += c
+                        elif kind == 1 and f == 0:  # the whole filter's popcount = matched docs
+                            (A if dst == "in" else C)[si] += c
+                        else:
+                            ok = False
+                if ok:
+                    form = (int(const_in), A, B, int(const_docs), C)
+            self.fused_cache[key] = form
+        return self.fused_cache[key]
+
 
 def plan_stats(query, segments, leaf_params=None):
     """_StatsPlan of `query` over `segments` (server_stats_closed_form's planning half)."""
@@ -846,8 +883,17 @@ def server_stats_device(query, segments, executor, stream=None, docs_total=None,
     numDocsScanned of its last scan (server_stats_closed_form: constant-cost filters then need no GPU pass). When the
     scan counted the statistics of its two-leaf AND itself (PA_QF_FILTER_STATS: fused_counts), no extra GPU pass runs
     for the segments it covered."""
+    fz = executor.fused_leap_counts(stream) if hasattr(executor, "fused_leap_counts") else None
+    if fz is not None and plan is not None:
+        # every request covered by the scan's own counts: two dot products (no request table, no gathers)
+        e, z, arr = fz
+        form = plan.fused_form(e, z, len(segments))
+        if form is not None and not arr[:, 2].any():
+            const_in, A, B, const_docs, C = form
+            m, lp = arr[:, 0], arr[:, 1]
+            return const_in + int(A @ m + B @ lp), (const_docs + int(C @ m)) * plan.ncols
+
     def counts(reqs):
-        fz = executor.fused_leap_counts(stream) if hasattr(executor, "fused_leap_counts") else None
         dev = lambda rq: device_counts(executor, segments, rq, stream)
         return dev(reqs) if fz is None else fused_counts(reqs, fz, dev, None if plan is None else plan.fused_cache)
     return server_stats_closed_form(query, segments, counts, lambda si: executor.leaf_bitmaps(si, stream),

@@ -359,3 +359,40 @@ def test_fused_counts_serve_only_their_requests():
     assert out[1].tolist() == [10, -1, -1, -1]
     assert asked == [sorted([(1, (1,), (0,)), (0, (0,), (1,))])]
     assert out[2][0] >= 100 and out[3][0] >= 100
+
+
+def test_fused_linear_form_equals_the_closed_forms(monkeypatch):
+    """server_stats_device's fast path (the statistics as linear forms of the scan's per-segment matched docs and
+    leaps, _StatsPlan.fused_form) gives what fused_counts + the closed forms give; a gave-up segment leaves it for the
+    general path (which asks the device counts for that segment)."""
+    segs = [_seg(4000, 11), _seg(3000, 12), _seg(5000, 13)]
+    q = parse_sql("SELECT COUNT(*), SUM(b) FROM t WHERE a < 20 AND b = 7")
+    plan = FS.plan_stats(q, segs)
+    reqs = plan.flat()[0]
+    e, z = None, None
+    for (si, a, b) in reqs:  # the two-leaf AND's request names the leaves: A = [Z], B = [E]
+        if len(a) == 1 and len(b) == 1:
+            z, e = a[0], b[0]
+    assert e is not None
+    rng = np.random.default_rng(5)
+    arr = np.stack([rng.integers(0, 500, 3), rng.integers(0, 900, 3), np.zeros(3, dtype=np.int64)], axis=1)
+
+    class Ex:
+        handle = None
+
+        def fused_leap_counts(self, stream=None):
+            return e, z, arr
+
+    def no_fallback(rq):
+        raise AssertionError(rq)
+
+    want = FS.server_stats_closed_form(q, segs, lambda rq: FS.fused_counts(rq, (e, z, arr), no_fallback), None, None,
+                                       777, plan)
+    assert plan.fused_form(e, z, len(segs)) is not None
+    assert FS.server_stats_device(q, segs, Ex(), None, 777, plan) == want
+    arr[1, 2] = 1  # segment 1 gave up
+    asked = []
+    monkeypatch.setattr(FS, "device_counts", lambda ex, sg, rq, st=None: asked.append(sorted(rq)) or
+                        np.zeros((len(rq), 4), dtype=np.int64))
+    FS.server_stats_device(q, segs, Ex(), None, 777, plan)
+    assert asked and all(k[0] == 1 for k in asked[0])
