@@ -2573,9 +2573,12 @@ static int alloc_leaps(pa_query* q, const Prep& P) {
   const int64_t slices = (int64_t)q->grid * scan_waves(q->strategy);
   const int64_t cap = (int64_t)(16.0 * P.first_clause_sel * (double)q->num_docs / (double)slices) + 256;
   q->leap_slices = slices;
-  // (+ the search's prefix sums and contiguous copy of the slices: leap_prefix_kernel / leap_compact_kernel)
-  const size_t words = (size_t)std::max(1, q->nseg) * 3 + 1 + (size_t)slices + 2 * (size_t)slices * (size_t)cap +
-                       (size_t)slices + 1;
+  if (slices > kLeapMaxSlices) {  // (the search kernel keeps the slices' prefix sums in LDS): the bitmap path instead
+    q->hq.leap_mode = 0;
+    q->leap_leaf = -1;
+    return PA_OK;
+  }
+  const size_t words = (size_t)std::max(1, q->nseg) * 3 + 1 + (size_t)slices + (size_t)slices * (size_t)cap;
   int rc = dev_alloc(q->leap_buf, words * sizeof(unsigned long long));
   if (rc) return rc;
   PA_HIP(hipMemset(q->leap_buf.p, 0, leap_header_bytes(q)));
@@ -2750,7 +2753,8 @@ int pa_query_scan(pa_query* q, void* stream) {
   PartScratch none{};
   PA_HIP(launch_scan(q->strategy, q->steps, q->lane_major, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p,
                      (const DevSeg*)q->dsegs.p, (const LmSegPlan*)q->dplans.p, none, st));
-  if (q->hq.leap_mode) PA_HIP(launch_leap_search((const DevQuery*)q->dq.p, (const DevSeg*)q->dsegs.p, st));
+  if (q->hq.leap_mode)
+    PA_HIP(launch_leap_search((const DevQuery*)q->dq.p, (const DevSeg*)q->dsegs.p, q->leap_slices, st));
   return PA_OK;
 }
 

@@ -1655,67 +1655,51 @@ hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t*
 
 // Fused execution statistics after the scan (pa_scan.h "fused execution statistics"). The scan waves' list slices hold
 // a few E docs each, unevenly (a Poisson spread: one wave walking its own slice's docs one search after another would
-// take the longest slice's time), so: (1) one workgroup takes the exclusive prefix sums of the slice lengths, (2) the
-// slices are copied into one contiguous list, (3) every wave searches its share of that list — one wave per listed E
-// doc (its successor's label, and for a B-only doc its predecessor's) and one per segment (its first labelled doc),
+// take the longest slice's time), so every workgroup first takes the prefix sums of the slice lengths into LDS, and
+// its waves then take listed docs g = w, w + waves, ... (the slice of g by a binary search in LDS): one wave per listed
+// E doc (its successor's label, and for a B-only doc its predecessor's) and one per segment (its first labelled doc),
 // each a wave-wide neighbour search over both leaves; the leaps go into the segments' counters.
-// Layout after the slices (alloc_leaps): [slices + 1] prefix sums, then the contiguous list.
-constexpr int kLeapPrefixThreads = 1024;
+constexpr int kLeapThreads = 1024;
 
-__global__ void __launch_bounds__(kLeapPrefixThreads) leap_prefix_kernel(const DevQuery* __restrict__ q) {
-  __shared__ unsigned long long part[kLeapPrefixThreads];
-  const int64_t nseg = q->num_segments, S = q->leap_slices;
+__global__ void __launch_bounds__(kLeapThreads) leap_search_kernel(const DevQuery* __restrict__ q,
+                                                                   const DevSeg* __restrict__ segs) {
+  extern __shared__ uint32_t pre[];  // [slices + 1]: exclusive prefix sums of the slice lengths
+  __shared__ uint32_t part[kLeapThreads];
+  const int t = threadIdx.x, lane = t & (kWave - 1);
+  const int64_t nseg = q->num_segments, S = q->leap_slices, cap = q->leap_cap;
   const AS1 unsigned long long* hdr = gp(q->leap_out) + 3 * nseg;
-  AS1 unsigned long long* pre = gp(q->leap_out) + 3 * nseg + 1 + S + S * q->leap_cap;
-  const int t = threadIdx.x;
-  const int64_t per = (S + kLeapPrefixThreads - 1) / kLeapPrefixThreads;
+  if (hdr[0]) return;  // (a slice overflowed: the host takes every segment's counts from leaf bitmaps)
+  const int64_t per = (S + kLeapThreads - 1) / kLeapThreads;
   const int64_t s0 = min(S, (int64_t)t * per), s1 = min(S, s0 + per);
-  unsigned long long sum = 0;
-  for (int64_t w = s0; w < s1; ++w) sum += hdr[1 + w];
+  uint32_t sum = 0;
+  for (int64_t w = s0; w < s1; ++w) sum += (uint32_t)hdr[1 + w];
   part[t] = sum;
   __syncthreads();
-  for (int o = 1; o < kLeapPrefixThreads; o <<= 1) {  // inclusive scan of the partial sums
-    const unsigned long long v = t >= o ? part[t - o] : 0ull;
+  for (int o = 1; o < kLeapThreads; o <<= 1) {  // inclusive scan of the partial sums
+    const uint32_t v = t >= o ? part[t - o] : 0u;
     __syncthreads();
     part[t] += v;
     __syncthreads();
   }
-  unsigned long long run = part[t] - sum;
+  uint32_t run = part[t] - sum;
   for (int64_t w = s0; w < s1; ++w) {
     pre[w] = run;
-    run += hdr[1 + w];
+    run += (uint32_t)hdr[1 + w];
   }
-  if (t == kLeapPrefixThreads - 1) pre[S] = part[t];
-}
-
-__global__ void __launch_bounds__(256) leap_compact_kernel(const DevQuery* __restrict__ q) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t nseg = q->num_segments, S = q->leap_slices, cap = q->leap_cap;
-  const AS1 unsigned long long* hdr = gp(q->leap_out) + 3 * nseg;
-  if (hdr[0]) return;  // (a slice overflowed: the host takes every segment's counts from leaf bitmaps)
-  const AS1 unsigned long long* pre = hdr + 1 + S + S * cap;
-  AS1 unsigned long long* out = gp(q->leap_out) + 3 * nseg + 1 + S + S * cap + S + 1;
-  const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t w = (int64_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); w < S; w += waves) {
-    const int64_t n = (int64_t)hdr[1 + w], d = (int64_t)pre[w];
-    const AS1 unsigned long long* list = hdr + 1 + S + w * cap;
-    for (int64_t k = lane; k < n; k += kWave) out[d + k] = list[k];
-  }
-}
-
-__global__ void __launch_bounds__(256) leap_search_kernel(const DevQuery* __restrict__ q, const DevSeg* __restrict__ segs) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t nseg = q->num_segments, S = q->leap_slices, cap = q->leap_cap;
-  const AS1 unsigned long long* hdr = gp(q->leap_out) + 3 * nseg;
-  if (hdr[0]) return;
-  const AS1 unsigned long long* pre = hdr + 1 + S + S * cap;
-  const AS1 unsigned long long* list = pre + S + 1;
-  const int64_t total = (int64_t)pre[S];
-  const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  // wave w: listed docs w, w + waves, ..., then the segment starts
-  for (int64_t w = (int64_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); w < total + nseg; w += waves) {
-    if (w < total) {
-      const uint64_t ent = list[w];
+  if (t == kLeapThreads - 1) pre[S] = part[t];
+  __syncthreads();
+  const int64_t total = pre[S];
+  const AS1 unsigned long long* lists = hdr + 1 + S;
+  const int64_t waves = ((int64_t)gridDim.x * kLeapThreads) >> 6;
+  for (int64_t g = (int64_t)blockIdx.x * (kLeapThreads >> 6) + (t >> 6); g < total + nseg; g += waves) {
+    if (g < total) {
+      int64_t lo = 0, hi = S;  // the last slice whose start is <= g
+      while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)pre[mid] <= g) lo = mid;
+        else hi = mid;
+      }
+      const uint64_t ent = lists[lo * cap + (g - (int64_t)pre[lo])];
       const int si = (int)(ent >> 40);
       const int64_t doc = (int64_t)((ent >> 1) & ((1ull << 39) - 1ull));
       uint32_t leaps = 0u, gave = 0u;
@@ -1729,17 +1713,18 @@ __global__ void __launch_bounds__(256) leap_search_kernel(const DevQuery* __rest
       }
       leap_add(q, si, 0u, leaps, gave, lane);
     } else {
-      const int si = (int)(w - total);
+      const int si = (int)(g - total);
       const uint32_t first = leap_search(segs + si, 0, 1, lane);
       leap_add(q, si, 0u, first == 1u ? 1u : 0u, first == 4u ? 1u : 0u, lane);
     }
   }
 }
 
-hipError_t launch_leap_search(const DevQuery* q, const DevSeg* segs, hipStream_t s) {
-  hipLaunchKernelGGL(leap_prefix_kernel, dim3(1), dim3(kLeapPrefixThreads), 0, s, q);
-  hipLaunchKernelGGL(leap_compact_kernel, dim3(512), dim3(256), 0, s, q);
-  hipLaunchKernelGGL(leap_search_kernel, dim3(2048), dim3(256), 0, s, q, segs);
+hipError_t launch_leap_search(const DevQuery* q, const DevSeg* segs, int64_t slices, hipStream_t s) {
+  const size_t lds = (size_t)(slices + 1) * 4;  // (alloc_leaps keeps slices within kLeapMaxSlices)
+  hipError_t e = hipFuncSetAttribute((const void*)leap_search_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(leap_search_kernel, dim3(256), dim3(kLeapThreads), lds, s, q, segs);
   return hipGetLastError();
 }
 

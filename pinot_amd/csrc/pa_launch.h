@@ -129,7 +129,8 @@ hipError_t launch_pack_copy(const RowDesc& d, const int64_t* row_slot, int64_t r
 hipError_t launch_merge_rows(const RowDesc& d, const unsigned char* rows, int64_t n, int64_t* row_slot,
                              unsigned long long* counters, hipStream_t s);
 // fused execution statistics: the neighbour searches of the E docs the scan listed (DevQuery::leap_mode)
-hipError_t launch_leap_search(const DevQuery* q, const DevSeg* segs, hipStream_t s);
+hipError_t launch_leap_search(const DevQuery* q, const DevSeg* segs, int64_t slices, hipStream_t s);
+constexpr int64_t kLeapMaxSlices = 16384;  // fused statistics: list slices (scan waves) the search kernel scans in LDS
 hipError_t set_scan_lds_limit(int strategy, int steps, int lm, int bytes);
 hipError_t scan_occupancy(int strategy, int steps, int lm, int lds_bytes, int* blocks_per_cu);
 hipError_t launch_scan(int strategy, int steps, int lm, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs,

@@ -846,33 +846,23 @@ __device__ __forceinline__ bool leaf_match_doc(const DevLeaf& L, int64_t doc) {
 // (kLeapSearchSteps) or a full list flags the segment(s), whose counts the host then takes from leaf bitmaps.
 // leap_out: [3 s]: segment s's matched docs, leaps, gave-up flag; [3 nseg]: list overflow flag; [3 nseg + 1 + w]: the
 // docs wave w of the scan listed; then the list: wave w's slice of leap_cap entries at [3 nseg + 1 + slices + w cap],
-// one (segment << 40 | doc << 1 | both) per E doc (a wave appends to its own slice: no atomic, no wait); after the
-// slices, the search's [slices + 1] prefix sums of their lengths and the slices copied into one contiguous list.
-constexpr int kLeapSearchSteps = 16;  // steps of kLeapSearchDocs docs: 4096 docs
-constexpr int kLeapSearchDocs = 4 * kWave;
+// one (segment << 40 | doc << 1 | both) per E doc (a wave appends to its own slice: no atomic, no wait).
+constexpr int kLeapSearchSteps = 64;  // 4096 docs
 
 // Label of the nearest labelled doc at or beyond `from` in direction dir (+1 / -1) inside the segment: 1, 2, 3; 0 if
-// the segment ends first; 4 if the search gave up. A step reads 256 docs (4 per lane, their loads in flight together:
-// a step costs one round trip, so a wide step shortens the search's dependent chain).
+// the segment ends first; 4 if the search gave up. (Four rows of 64 docs per step measured slower: 51 vs 34 us for
+// configs[1]'s list, r04_d1.)
 __device__ __noinline__ uint32_t leap_search(const DevSeg* seg_in, int64_t from, int dir, int lane) {
   const DevSeg* __restrict__ seg = uniform_ptr(seg_in);
   const int64_t n = seg->num_docs;
   for (int k = 0; k < kLeapSearchSteps; ++k) {
-    uint32_t lbl[4];
-    bool in[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t d = from + (int64_t)dir * (int64_t)(kLeapSearchDocs * k + kWave * r + lane);
-      in[r] = d >= 0 && d < n;
-      lbl[r] = 0u;
-      if (in[r]) lbl[r] = (leaf_match_doc(seg->leaves[1], d) ? 1u : 0u) | (leaf_match_doc(seg->leaves[0], d) ? 2u : 0u);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {  // nearer rows first; in a row, lane order = distance
-      const uint64_t hit = __ballot(lbl[r] != 0u);
-      if (hit) return (uint32_t)__builtin_amdgcn_readlane((int)lbl[r], __builtin_ctzll(hit));
-      if (__ballot(in[r]) != ~0ull) return 0u;
-    }
+    const int64_t d = from + (int64_t)dir * (int64_t)(kWave * k + lane);
+    const bool in = d >= 0 && d < n;
+    uint32_t lbl = 0u;
+    if (in) lbl = (leaf_match_doc(seg->leaves[1], d) ? 1u : 0u) | (leaf_match_doc(seg->leaves[0], d) ? 2u : 0u);
+    const uint64_t hit = __ballot(lbl != 0u);
+    if (hit) return (uint32_t)__builtin_amdgcn_readlane((int)lbl, __builtin_ctzll(hit));  // lane order = distance
+    if (__ballot(in) != ~0ull) return 0u;
   }
   return 4u;
 }
