@@ -338,6 +338,7 @@ __device__ __forceinline__ uint32_t gd_tile_sm(uint32_t gt, const DevQuery* __re
   constexpr int ST = kGdSmSteps;
   // descriptors through the constant address space (scalar loads): a flat load of a descriptor field would be counted
   // in vmcnt, and waiting for it would wait for every tile in flight
+  if (rl(gt, 3) & 32) return 0;  // measurement only: the tile streamed in, nothing evaluated
   CSegT* cs = (CSegT*)(uintptr_t)uniform_ptr(seg);
   CQ* cq = (CQ*)(uintptr_t)uniform_ptr(q);
   const int64_t doc_base = wt * (ST * kWave);

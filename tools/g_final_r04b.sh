@@ -15,6 +15,6 @@ timeout -k 10 400 python -u tools/bench_configs.py --workload sumscan --plan sel
 cat $out/exec_stats_*.json | python3 -c "import json,sys; [print(d['workload'], d['plan_name'], d['exec_stats']) for d in map(json.loads, sys.stdin)]"
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $out/stats_trace -o run --output-format csv -- python3 tools/bench_configs.py --workload adanalytics --segments 100 --reps 10 --no-stepmajor --exec-stats > /dev/null 2> $out/stats_trace.err || { echo stats_prof_failed; exit 3; }
 for w in highcard star mvgroup; do
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/kt_$w -o run --output-format csv -- python3 tools/bench_configs.py --workload $w --plan $([ $w = mvgroup ] && echo untrimmed || echo all_docs) --segments 20 --no-stepmajor > /dev/null 2> $out/kt_$w.err || true
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/kt_$w -o run --output-format csv -- python3 tools/bench_configs.py --workload $w --plan $([ $w = mvgroup ] && echo untrimmed || echo all_docs) --segments 20 --no-stepmajor > /dev/null 2> $out/kt_$w.err || { echo kt_failed $w; exit 4; }
 done
 echo all_ok
