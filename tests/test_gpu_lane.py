@@ -132,24 +132,30 @@ GROUP_AGGS = ["COUNT(*), SUM(rs)", "SUM(rl), MIN(rl)", "SUM(rd), MAX(rd), COUNT(
 def test_lds_group_by_raw_metrics(lane_segments, sel, aggs):
     """Filter + GROUP BY over raw metrics on the LDS-accumulator strategy, lane-major tiles (pa_scan.h
     accumulate_lds_lm; accumulate_lds_raw_dense when every non-COUNT aggregation reads one raw column and the wave's tile
-    is dense): INT / LONG (int32-range: one int64 slot; wider: the split pair) / FLOAT / DOUBLE values and 700 groups."""
+    is dense): INT / LONG (int32-range: one int64 slot; wider: the split pair) / FLOAT / DOUBLE values and 700 groups.
+    PA_QF_NO_DENSE_GROUP keeps the query on the LDS strategy (the planner may otherwise pick the dense GROUP BY kernel,
+    tests/test_gpu_dense.py); the default plan is checked against the oracle too."""
     segs, gs = lane_segments
     q = parse_sql("SELECT g, %s FROM t WHERE day < %d GROUP BY g LIMIT 1000" % (aggs, SELECTIVITY[sel]))
-    ex = GpuQueryExecutor(q, gs)
-    try:
-        st = ex.stats()["plan"]
-        assert st["strategy"] == "lds" and st["lane_major"] == 1, st
-        got = ex.run()
-    finally:
-        ex.close()
-    assert_same(got, oracle.run_query(q, segs), DOUBLE_REL)
+    want = oracle.run_query(q, segs)
+    for flags in (L.PA_QF_NO_DENSE_GROUP, 0):
+        ex = GpuQueryExecutor(q, gs, flags=flags)
+        try:
+            st = ex.stats()["plan"]
+            if flags:
+                assert st["strategy"] == "lds" and st["lane_major"] == 1, st
+            got = ex.run()
+        finally:
+            ex.close()
+        assert_same(got, want, DOUBLE_REL)
 
 
 @pytest.mark.parametrize("sel", ["1pct", "30pct", "all"])
-@pytest.mark.parametrize("flags", [0, L.PA_QF_LAZY_POST])
+@pytest.mark.parametrize("flags", [L.PA_QF_NO_DENSE_GROUP, L.PA_QF_LAZY_POST])
 def test_lds_group_by_dictionary_metrics(lane_segments, sel, flags):
-    """Filter + GROUP BY over dictionary metrics on the LDS strategy, with the post-filter columns staged with the filter
-    column or read per matching doc from HBM (PA_QF_LAZY_POST)."""
+    """Filter + GROUP BY over dictionary metrics on the LDS strategy (PA_QF_NO_DENSE_GROUP: not the dense GROUP BY
+    kernel), with the post-filter columns staged with the filter column or read per matching doc from HBM
+    (PA_QF_LAZY_POST)."""
     segs, gs = lane_segments
     q = parse_sql("SELECT g, COUNT(*), SUM(dl), MIN(dd), MAX(dl), SUM(dd) FROM t WHERE day < %d GROUP BY g LIMIT 1000"
                   % SELECTIVITY[sel])
