@@ -1988,8 +1988,11 @@ int plan_kernels(pa_query* q, Prep& P, TilePlan& plan, TilePlan& count_plan) {
         ins = std::max(ins, n);
         img_dw = std::max(img_dw, dw);
       }
+      int nvalue = 0;
+      for (int a = 0; a < s.num_aggs; ++a) nvalue += s.aggs[a].type != PA_AGG_COUNT;
       for (int st : {STRAT_GDENSE_RS12, STRAT_GDENSE_RS8}) {
         if (ins > gd_rs_dmax(st)) continue;
+        if (st == STRAT_GDENSE_RS12 && (s.num_group_by > kGdRs12MaxGb || nvalue > kGdRs12MaxAgg)) continue;
         const size_t lds = P.gd_lds + (size_t)scan_waves(st) * img_dw * 4;
         if (lds > kLdsBudget) continue;
         int resident = 0;

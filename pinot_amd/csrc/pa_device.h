@@ -314,6 +314,7 @@ struct DevQuery {
 // lgkmcnt wait, which also waits for every LDS operation in flight).
 constexpr int kGdMaxGb = 3;    // group-by columns
 constexpr int kGdMaxAgg = 6;   // non-COUNT aggregations
+constexpr int kGdRs12MaxGb = 2, kGdRs12MaxAgg = 2;  // STRAT_GDENSE_RS12: at most this many (its VGPR budget)
 // (gd_plans holds 128 dwords per segment: the GdSegPlan, then the GdRsPlan of the register-staged variants)
 struct GdSegPlan {
   int32_t ngb, nagg, rpl, pad;           // 0..3

@@ -46,15 +46,18 @@ __device__ __forceinline__ uint32_t gd_decode(const lds_u32_t* region, uint32_t 
 // last bit at 64 nb i + (lane nb + nb - 1), and 64 nb i is a multiple of 32: the two stream words holding the value sit
 // at a lane constant plus 8 nb i bytes, and the alignbit shift is a lane constant. A decode is then one v_mad (address),
 // one ds_read2_b32 and alignbit + and. Raw columns: 4 or 8 bytes per doc, stride 256 / 512 bytes per step.
+// MG / MA: the group-by columns / non-COUNT aggregations a kernel variant handles at most (fewer: fewer VGPRs)
+template <int MG = kGdMaxGb, int MA = kGdMaxAgg>
 struct GdLane {
-  uint32_t ga[kGdMaxGb], gs[kGdMaxGb];    // group-by column j: LDS address of step 0's word pair, alignbit shift
-  uint32_t va[kGdMaxAgg], vs[kGdMaxAgg];  // aggregation k: the same for its column (raw: the value's address)
+  uint32_t ga[MG], gs[MG];    // group-by column j: LDS address of step 0's word pair, alignbit shift
+  uint32_t va[MA], vs[MA];    // aggregation k: the same for its column (raw: the value's address)
 };
 
-__device__ __forceinline__ void gd_lane_setup(uint32_t gt, uint32_t img, int lane, GdLane& L) {
+template <int MG, int MA>
+__device__ __forceinline__ void gd_lane_setup(uint32_t gt, uint32_t img, int lane, GdLane<MG, MA>& L) {
   const int ngb = (int)rl(gt, 0), na = (int)rl(gt, 1);
 #pragma unroll
-  for (int j = 0; j < kGdMaxGb; ++j) {
+  for (int j = 0; j < MG; ++j) {
     if (j >= ngb) break;
     const uint32_t nb = rl(gt, 5 + 6 * j);
     const uint32_t c = (uint32_t)lane * nb + nb - 1u;
@@ -62,7 +65,7 @@ __device__ __forceinline__ void gd_lane_setup(uint32_t gt, uint32_t img, int lan
     L.gs[j] = (~c) & 31u;
   }
 #pragma unroll
-  for (int k = 0; k < kGdMaxAgg; ++k) {
+  for (int k = 0; k < MA; ++k) {
     if (k >= na) break;
     const int vsrc = (int)rl(gt, 22 + 6 * k);
     const uint32_t reg = img + 4u * rl(gt, 24 + 6 * k);
@@ -99,8 +102,8 @@ __device__ __forceinline__ void gd_dec(uint32_t a, uint32_t sh, uint32_t nb, con
 // is an LDS read. errs counts matching docs whose key fell outside the LDS box (cannot happen when the planner's box is
 // right; the query then reports an error).
 // BOX (the key box is the filter, gd_box_tile): errs counts the docs inside the box instead (numDocsScanned).
-template <int N, bool BOX = false>
-__device__ __forceinline__ void gd_batch(uint32_t gt, const GdLane& L, const uint32_t (&st)[N], const bool (&on_in)[N],
+template <int N, bool BOX = false, int MG = kGdMaxGb, int MA = kGdMaxAgg>
+__device__ __forceinline__ void gd_batch(uint32_t gt, const GdLane<MG, MA>& L, const uint32_t (&st)[N], const bool (&on_in)[N],
                                          uint32_t r, uint32_t base, uint32_t& errs) {
   const int ngb = (int)rl(gt, 0), na = (int)rl(gt, 1);
   const uint32_t rpl = rl(gt, 2);
@@ -113,7 +116,7 @@ __device__ __forceinline__ void gd_batch(uint32_t gt, const GdLane& L, const uin
     on[k] = on_in[k];
   }
 #pragma unroll
-  for (int j = 0; j < kGdMaxGb; ++j) {
+  for (int j = 0; j < MG; ++j) {
     if (j >= ngb) break;
     const int o = 4 + 6 * j;
     uint32_t id[N];
@@ -153,7 +156,7 @@ __device__ __forceinline__ void gd_batch(uint32_t gt, const GdLane& L, const uin
       if (on[k]) __hip_atomic_fetch_add(cnt + idx[k], 1u, WG_RLX);
   }
 #pragma unroll
-  for (int g = 0; g < kGdMaxAgg; ++g) {
+  for (int g = 0; g < MA; ++g) {
     if (g >= na) break;
     const int o = 22 + 6 * g;
     const int vs = (int)rl(gt, o), op = (int)rl(gt, o + 1);
@@ -247,9 +250,9 @@ __device__ __forceinline__ void gd_batch(uint32_t gt, const GdLane& L, const uin
 // The matching docs of one tile, step-major match bits s (bit i <=> doc 64 i + lane): every lane walks its own set bits,
 // KB per batch, so a batch is productive on every lane until the lanes run out of matches (max popcount over the
 // lanes batches: ~23 of 32 steps at 50 % density, ~7 at 10 %).
+template <int KB = 4, int MG = kGdMaxGb, int MA = kGdMaxAgg>
 __device__ __forceinline__ void gd_walk(uint32_t gt, uint32_t img, uint32_t s, int lane, uint32_t base, uint32_t& errs) {
-  constexpr int KB = 4;
-  GdLane L;
+  GdLane<MG, MA> L;
   gd_lane_setup(gt, img, lane, L);
   const uint32_t r = (uint32_t)lane & ((1u << rl(gt, 2)) - 1u);
 #pragma unroll 1
@@ -262,16 +265,17 @@ __device__ __forceinline__ void gd_walk(uint32_t gt, uint32_t img, uint32_t s, i
       st[k] = on[k] ? (uint32_t)__builtin_ctz(s) : 0u;
       s &= s - 1u;
     }
-    gd_batch<KB>(gt, L, st, on, r, base, errs);
+    gd_batch<KB, false, MG, MA>(gt, L, st, on, r, base, errs);
   }
 }
 
 // The filter is exactly the key box (GdSegPlan::box: unit DICT_RANGE clauses on group-by columns): every valid doc of a
 // step-major tile goes through gd_batch, whose box check is the filter, KB steps per batch at compile-time step offsets
 // — no filter evaluation, no walk. Returns the lane's docs inside the box.
+template <int MG = kGdMaxGb, int MA = kGdMaxAgg>
 __device__ __forceinline__ uint32_t gd_box_tile(uint32_t gt, uint32_t img, uint32_t valid, int lane, uint32_t base) {
   constexpr int KB = 4;
-  GdLane L;
+  GdLane<MG, MA> L;
   gd_lane_setup(gt, img, lane, L);
   const uint32_t r = (uint32_t)lane & ((1u << rl(gt, 2)) - 1u);
   uint32_t inbox = 0;
@@ -284,7 +288,7 @@ __device__ __forceinline__ uint32_t gd_box_tile(uint32_t gt, uint32_t img, uint3
       st[k] = (uint32_t)(s0 + k);
       on[k] = (valid >> (s0 + k)) & 1u;
     }
-    gd_batch<KB, true>(gt, L, st, on, r, base, inbox);
+    gd_batch<KB, true, MG, MA>(gt, L, st, on, r, base, inbox);
   }
   return inbox;
 }
@@ -332,6 +336,9 @@ __device__ __forceinline__ uint32_t gd_tile(uint32_t gt, uint32_t pp, int64_t wt
 }
 
 // Step-major 1024-doc tiles: filter by leaf_bits (bit i of lane l <=> doc 64 i + l) straight into the walk's order.
+// KB: docs per lane per walk batch (the 12-wave register-staged variant walks 2 at a time: at 4 its tile ring no longer
+// fits the 170 VGPRs of 3 waves per SIMD and a ring slot spills, each refill then waiting for its own load)
+template <int KB = 4, int MG = kGdMaxGb, int MA = kGdMaxAgg>
 __device__ __forceinline__ uint32_t gd_tile_sm(uint32_t gt, const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg,
                                                int64_t wt, const uint32_t* img_ptr, uint32_t img, int lane,
                                                uint32_t base, uint32_t& errs) {
@@ -350,7 +357,7 @@ __device__ __forceinline__ uint32_t gd_tile_sm(uint32_t gt, const DevQuery* __re
     const int64_t n = rem > lane ? (rem - lane + kWave - 1) / kWave : 0;
     m = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
   }
-  if (rl(gt, kGdBoxDword)) return gd_box_tile(gt, img, m, lane, base);
+  if (rl(gt, kGdBoxDword)) return gd_box_tile<MG, MA>(gt, img, m, lane, base);
   uint32_t clause = 0;
   const int neager = cq->num_eager;
   for (int li = 0; li < neager; ++li) {
@@ -365,7 +372,7 @@ __device__ __forceinline__ uint32_t gd_tile_sm(uint32_t gt, const DevQuery* __re
   const uint32_t mine = (uint32_t)__builtin_popcount(m);
   if (__ballot(mine != 0) == 0) return 0;
   if (rl(gt, 3) & 1) return mine;  // measurement only: filter only
-  gd_walk(gt, img, m, lane, base, errs);
+  gd_walk<KB, MG, MA>(gt, img, m, lane, base, errs);
   return mine;
 }
 
@@ -690,7 +697,10 @@ __device__ __forceinline__ void rs_step(CQ* q, const DevQuery* __restrict__ q_in
   }
   rs_store<DM>(pc.rp, img, lane, cur);
   // (a wave-uniform segment pointer: its descriptor fields are scalar loads, which do not wait for the ring's loads)
-  matched += gd_tile_sm(pc.gt, q_in, uniform_ptr(segs + pc.si), pc.t - pc.first, img_ptr, img, lane, base, errs);
+  // (the 12-wave variant: at most 2 group-by columns and 2 value aggregations, so its tile ring fits the 170 VGPRs of
+  // 3 waves per SIMD; with the general limits a ring slot spilled and each refill waited for its own load)
+  matched += gd_tile_sm<4, (DM <= 4 ? kGdRs12MaxGb : kGdMaxGb), (DM <= 4 ? kGdRs12MaxAgg : kGdMaxAgg)>(
+      pc.gt, q_in, uniform_ptr(segs + pc.si), pc.t - pc.first, img_ptr, img, lane, base, errs);
   pc.t += wpw;
 }
 

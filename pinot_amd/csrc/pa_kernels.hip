@@ -1724,7 +1724,9 @@ hipError_t launch_leap_search(const DevQuery* q, const DevSeg* segs, int64_t sli
   const size_t lds = (size_t)(slices + 1) * 4;  // (alloc_leaps keeps slices within kLeapMaxSlices)
   hipError_t e = hipFuncSetAttribute((const void*)leap_search_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(leap_search_kernel, dim3(256), dim3(kLeapThreads), lds, s, q, segs);
+  // 512 workgroups of 16 waves: two per CU, 8192 waves (a listed doc's two searches are a dependent chain of loads:
+  // the list is spread over as many waves as fit; 256 workgroups measured 52 us, twice the docs per wave)
+  hipLaunchKernelGGL(leap_search_kernel, dim3(512), dim3(kLeapThreads), lds, s, q, segs);
   return hipGetLastError();
 }
 
