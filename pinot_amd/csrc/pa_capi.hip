@@ -667,6 +667,7 @@ struct Prep {
   size_t gd_lds = 0;                       // LDS bytes of the accumulators + tables (the ring follows)
   int gd_rp_log2 = 0, gd_nkeys = 0, gd_tables = 0;
   bool gd_box = false;                     // the key box is exactly the filter (pa_gdense.h gd_box_tile)
+  std::vector<int> gd_lut, gd_lut_words;   // per literal: LDS byte offset of its shared DICT_SET bitmap (-1: HBM)
   int gd_lo[PA_MAX_GROUP_BY] = {0}, gd_span[PA_MAX_GROUP_BY] = {0}, gd_ls[PA_MAX_GROUP_BY] = {0};
   int gd_tab[PA_MAX_GROUP_BY] = {0}, gd_tab_n[PA_MAX_GROUP_BY] = {0};
   std::vector<int> gd_vs, gd_op, gd_acc, gd_tab_a, gd_tab_an;
@@ -1182,6 +1183,22 @@ int plan_gdense(pa_query* q, Prep& P) {
     P.gd_op[a] = op;
     row[a] = op == GOP_SUM_L ? 16 : (op == GOP_MIN_U || op == GOP_MAX_U) ? 4 : 8;
   }
+  // DICT_SET bitmaps identical in every segment go to LDS too (their per-doc reads would otherwise be global loads
+  // in the tile loop, each waiting for every tile in flight: vmcnt counts in order), when they fit
+  P.gd_lut.assign(q->literals.size(), -1);
+  P.gd_lut_words.assign(q->literals.size(), 0);
+  std::vector<size_t> lutb(q->literals.size(), 0);
+  size_t lut_bytes = 0;
+  for (size_t li = 0; li < q->literals.size(); ++li) {
+    const int leaf = q->literals[li].leaf;
+    if (s.leaves[leaf].kind != PA_LEAF_DICT_SET) continue;
+    bool same = true;
+    for (int si = 1; si < q->nseg && same; ++si) same = q->luts[si][leaf] == q->luts[0][leaf];
+    if (!same || q->luts[0][leaf].empty()) continue;
+    P.gd_lut_words[li] = (int)q->luts[0][leaf].size();
+    lutb[li] = ((size_t)P.gd_lut_words[li] * 4 + 15) & ~(size_t)15;
+    lut_bytes += lutb[li];
+  }
   // LDS: replicated accumulators + tables + a ring of at least 2 tile images per wave (kGdWaves waves); replicas
   // 256 / keys (a wave's 64 lanes spread over >= 4 addresses per key), fewer while that does not fit
   auto acc_bytes = [&](int rpl) {
@@ -1193,7 +1210,14 @@ int plan_gdense(pa_query* q, Prep& P) {
   const size_t ring_min = (size_t)kGdWaves * 2 * (size_t)max_img_dw * 4;
   int rpl = 0;
   while (rpl < 5 && ((int64_t)1 << (rpl + 1)) * nkeys <= 256) ++rpl;
-  while (rpl > 0 && acc_bytes(rpl) + tab_bytes + ring_min > kLdsBudget) --rpl;
+  while (rpl > 0 && acc_bytes(rpl) + tab_bytes + lut_bytes + ring_min > kLdsBudget) --rpl;
+  if (lut_bytes && acc_bytes(rpl) + tab_bytes + lut_bytes + ring_min > kLdsBudget) {  // (the bitmaps stay in HBM)
+    lut_bytes = 0;
+    std::fill(lutb.begin(), lutb.end(), 0);
+    std::fill(P.gd_lut_words.begin(), P.gd_lut_words.end(), 0);
+    while (rpl < 5 && ((int64_t)1 << (rpl + 1)) * nkeys <= 256 && acc_bytes(rpl + 1) + tab_bytes + ring_min <= kLdsBudget)
+      ++rpl;
+  }
   if (acc_bytes(rpl) + tab_bytes + ring_min > kLdsBudget) return PA_OK;
   P.gd_rp_log2 = rpl;
   // layout: counts, per-aggregation accumulators, key tables, value tables
@@ -1213,6 +1237,12 @@ int plan_gdense(pa_query* q, Prep& P) {
     if (!atab[a]) continue;
     P.gd_tab_a[a] = (int)off;
     off += atab[a];
+  }
+  for (size_t li = 0; li < q->literals.size(); ++li) {
+    if (!lutb[li]) continue;
+    P.gd_lut[li] = (int)off;
+    off += lutb[li];
+    P.gd_tables = 1;
   }
   P.gd_lds = off;
   P.gdense = true;
@@ -2181,6 +2211,7 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
   h.has_mv = q->has_mv;
   h.gb_mv = std::max(-1, mv_group_component(q));
   h.count_skip_gb = -1;
+  for (int li = 0; li < PA_MAX_LEAVES; ++li) h.gd_lut[li] = -1;
   h.xcd_major = (P.dense || is_gdense(q->strategy)) ? 1 : 0;
   h.lds_count_off = 0;
   h.lds_acc_bytes = (q->strategy == STRAT_LDS || is_gdense(q->strategy) || is_lane(q->strategy))
@@ -2237,6 +2268,10 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
     h.gd_rp_log2 = P.gd_rp_log2;
     h.gd_nkeys = P.gd_nkeys;
     h.gd_tables = P.gd_tables;
+    for (size_t li = 0; li < q->literals.size() && li < (size_t)PA_MAX_LEAVES; ++li) {
+      h.gd_lut[li] = li < P.gd_lut.size() ? P.gd_lut[li] : -1;
+      h.gd_lut_words[li] = li < P.gd_lut_words.size() ? P.gd_lut_words[li] : 0;
+    }
     for (int j = 0; j < s.num_group_by; ++j) {
       h.gd_lo[j] = P.gd_lo[j];
       h.gd_span[j] = P.gd_span[j];

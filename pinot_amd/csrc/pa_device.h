@@ -300,6 +300,10 @@ struct DevQuery {
   int32_t gd_tab_n[PA_MAX_GROUP_BY]; // key table entries (largest segment cardinality)
   int32_t gd_tables;                 // some key or value table is loaded per segment
   int32_t gd_pad;
+  // DICT_SET literals whose dictId bitmap is the same in every segment: LDS byte offset of the bitmap (-1: read from
+  // HBM — a global load in the tile loop waits for every tile in flight), and its words
+  int32_t gd_lut[PA_MAX_LEAVES];
+  int32_t gd_lut_words[PA_MAX_LEAVES];
   const uint32_t* gd_plans;          // [num_segments][64]: GdSegPlan of every segment
   // fused execution statistics (PA_QF_FILTER_STATS, leap_tile + leap_search_kernel): 1 = literal 0 (eager, E) and
   // literal 1 (lazy, Z) are the two scan leaves of an AND

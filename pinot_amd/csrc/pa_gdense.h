@@ -269,6 +269,30 @@ __device__ __forceinline__ void gd_walk(uint32_t gt, uint32_t img, uint32_t s, i
   }
 }
 
+// A DICT_SET leaf whose dictId bitmap sits in LDS (gd_lut): bit i of lane l <=> doc 64 i + l of the step-major tile
+// (leaf_bits' decode, the bitmap read with ds_read instead of a global load that would wait for the tile ring).
+template <int STEPS, class LeafT>
+__device__ __forceinline__ uint32_t gd_leaf_set_lds(const LeafT& L, uint32_t img, int lane, uint32_t lut_addr) {
+  const int nb = L.nbits;
+  const uint32_t mask = nbits_mask(nb);
+  const uint32_t e1 = (uint32_t)lane * (uint32_t)nb + (uint32_t)(nb - 1);
+  const uint32_t sh = (~e1) & 31u;
+  const int step = 2 * nb;
+  // (address-space-3 pointers: a generic one would be a flat load, counted in vmcnt too)
+  const lds_u32_t* p = lds_at<const lds_u32_t>(img + 4u * (uint32_t)(L.lds_off + (int)(e1 >> 5)));
+  const lds_u32_t* lut = lds_at<const lds_u32_t>(lut_addr);
+  uint32_t id[STEPS];
+#pragma unroll
+  for (int i = 0; i < STEPS; ++i) id[i] = __builtin_amdgcn_alignbit(p[i * step - 1], p[i * step], sh) & mask;
+  uint32_t w[STEPS];
+#pragma unroll
+  for (int i = 0; i < STEPS; ++i) w[i] = lut[id[i] >> 5];
+  uint32_t bits = 0;
+#pragma unroll
+  for (int i = 0; i < STEPS; ++i) bits |= ((w[i] >> (id[i] & 31u)) & 1u) << i;
+  return L.negate ? ~bits : bits;
+}
+
 // The filter is exactly the key box (GdSegPlan::box: unit DICT_RANGE clauses on group-by columns): every valid doc of a
 // step-major tile goes through gd_batch, whose box check is the filter, KB steps per batch at compile-time step offsets
 // — no filter evaluation, no walk. Returns the lane's docs inside the box.
@@ -362,7 +386,9 @@ __device__ __forceinline__ uint32_t gd_tile_sm(uint32_t gt, const DevQuery* __re
   const int neager = cq->num_eager;
   for (int li = 0; li < neager; ++li) {
     const auto& L = cs->leaves[li];
-    clause |= leaf_bits<ST>(L, img_ptr, doc_base, lane);
+    const int lut = cq->gd_lut[li];
+    if (lut >= 0) clause |= gd_leaf_set_lds<ST>(L, img, lane, base + (uint32_t)lut);
+    else clause |= leaf_bits<ST>(L, img_ptr, doc_base, lane);
     if (L.clause_end) {
       m &= clause;
       clause = 0;
@@ -386,6 +412,13 @@ __device__ __forceinline__ bool gd_tables_differ(CQ* q, CSegT* a, CSegT* b) {
 }
 
 __device__ void gd_load_tables(CQ* q, CSegT* cs, unsigned char* lds, int tid, int nthreads) {
+  for (int li = 0; li < q->num_eager; ++li) {  // shared DICT_SET bitmaps (the same in every segment)
+    const int off = q->gd_lut[li];
+    if (off < 0) continue;
+    uint32_t* t = (uint32_t*)(lds + off);
+    const uint32_t* src = cs->leaves[li].lut;
+    for (int i = tid; i < q->gd_lut_words[li]; i += nthreads) t[i] = gp(src)[i];
+  }
   for (int j = 0; j < q->num_gb; ++j) {
     const int tab = q->gd_tab[j];
     if (tab < 0) continue;
