@@ -45,6 +45,7 @@ def optimize_filter(f, schema):
 
 # ------------------------------------------------------------------ FlattenAndOrFilterOptimizer
 def flatten(f):
+    """FlattenAndOrFilterOptimizer.optimize (:43-64): only AND / OR nodes, recursively through AND / OR operands."""
     if isinstance(f, (Q.And, Q.Or)):
         kids = []
         for c in f.children:
@@ -54,9 +55,7 @@ def flatten(f):
             else:
                 kids.append(c)
         return type(f)(tuple(kids))
-    if isinstance(f, Q.Not):
-        return Q.Not(flatten(f.child))
-    return f
+    return f  # a NOT (and anything else) is returned as it is: its operand is not flattened (:48-51)
 
 
 # ------------------------------------------------------------------ BaseAndOrBooleanFilterOptimizer
@@ -129,13 +128,23 @@ def _eq_or_in(column, vals):
     return Q.EqPredicate(column, vals[0]) if len(vals) == 1 else Q.InPredicate(column, tuple(vals))
 
 
+def _or_child(c):
+    """An AND / NOT operand of an OR: its own operands optimized (MergeEqInFilterOptimizer.java:61-63), so a NOT is
+    recursed into only here, as an OR's child."""
+    if isinstance(c, Q.Not):
+        return Q.Not(merge_eq_in(c.child))
+    return merge_eq_in(c)
+
+
 def merge_eq_in(f):
+    """MergeEqInFilterOptimizer.optimize (:46-140): OR nodes merge their EQ / IN operands per column, AND nodes recurse
+    into their operands, an IN node alone is de-duplicated; a NOT at the top or under an AND is returned as it is."""
     if isinstance(f, Q.Or):
         values, order, kids = {}, [], []
         recreate = False
         for c in f.children:
             if isinstance(c, (Q.And, Q.Not)):
-                kids.append(merge_eq_in(c))
+                kids.append(_or_child(c))
             elif isinstance(c, (Q.EqPredicate, Q.InPredicate)):
                 vals = _eq_in_values(c)
                 if isinstance(c, Q.InPredicate):
@@ -152,14 +161,12 @@ def merge_eq_in(f):
             else:
                 kids.append(c)
         if not recreate:
-            return Q.Or(tuple(merge_eq_in(c) if isinstance(c, (Q.And, Q.Not)) else c for c in f.children))
+            return Q.Or(tuple(_or_child(c) if isinstance(c, (Q.And, Q.Not)) else c for c in f.children))
         if not kids and len(values) == 1:
             return _eq_or_in(order[0], values[order[0]])
         return Q.Or(tuple(kids + [_eq_or_in(col, values[col]) for col in order]))
     if isinstance(f, Q.And):
         return Q.And(tuple(merge_eq_in(c) for c in f.children))
-    if isinstance(f, Q.Not):
-        return Q.Not(merge_eq_in(f.child))
     if isinstance(f, Q.InPredicate):
         uniq = _dedup(list(f.values))
         if len(uniq) == 1 or len(uniq) != len(f.values):
@@ -172,93 +179,130 @@ def _is_int_text(text):
     return _num(text) is not None and all(ch not in text for ch in ".eE")
 
 
-def _f32(x):
+def _literal(text):
+    """(kind, value) of a numeric literal as the reference's SQL compiler types it (RequestUtils.java:108-121): an exact
+    integer -> INT (int range) or LONG (BigDecimal.longValue: the low 64 bits), anything else -> DOUBLE (the
+    BigDecimal's correctly rounded double). (None, None) for a non-numeric literal."""
+    d = _num(text)
+    if d is None or not d.is_finite():
+        return None, None
+    if _is_int_text(text):
+        i = int(d)
+        if INT_MIN <= i <= INT_MAX:
+            return "INT", i
+        i &= (1 << 64) - 1
+        return "LONG", i - (1 << 64) if i > LONG_MAX else i
+    return "DOUBLE", float(d)
+
+
+def _bd(x):
+    """BigDecimal.valueOf: a long exactly, a double through Double.toString (the shortest repr that round-trips, as
+    Python's repr and JDK >= 19's Double.toString give it)."""
+    return Decimal(x) if isinstance(x, int) else Decimal(repr(float(x)))
+
+
+def _f32_of_long(v):
+    """(float) of a Java long: one IEEE rounding (numpy's int64 -> float32 cast), widened to double."""
+    return float(np.float32(np.int64(v)))
+
+
+def _f32_of_double(x):
     with np.errstate(over="ignore"):
-        return Decimal(float(np.float32(float(x))))
+        return float(np.float32(x))
+
+
+def _cast_int(x, lo, hi):
+    """(int) / (long) of a Java double: NaN -> 0, truncation toward zero, saturating at the type's bounds."""
+    if x != x:
+        return 0
+    if x >= hi:
+        return hi
+    if x <= lo:
+        return lo
+    return int(x)
+
+
+def _cmp(a, b):
+    return (a > b) - (a < b)
 
 
 def _numerical_child(f, schema):
+    """NumericalFilterOptimizer.optimizeChild: only on a single-value numeric column (getDataType returns null for a
+    multi-value one, :370-376), with a numeric literal."""
+    dt, sv = schema.get(getattr(f, "column", None), (None, True))
+    if dt not in NUMERIC or not sv:
+        return f
     if isinstance(f, (Q.EqPredicate, Q.NotEqPredicate)):
-        return _numerical_eq(f, schema)
+        return _numerical_eq(f, dt)
     if isinstance(f, Q.RangePredicate) and ((f.lower == Q.UNBOUNDED) != (f.upper == Q.UNBOUNDED)):
-        return _numerical_range(f, schema)
+        return _numerical_range(f, dt)
     return f
 
 
-def _numerical_eq(f, schema):
-    dt = schema.get(f.column, (None,))[0]
-    v = _num(str(f.value))
-    if dt not in NUMERIC or v is None:
-        return f
-    neq = isinstance(f, Q.NotEqPredicate)
-    const = TRUE if neq else FALSE
-    if _is_int_text(str(f.value)):
-        if INT_MIN <= v <= INT_MAX:
-            return f  # INT literal: converted on the server
+def _numerical_eq(f, dt):
+    """rewriteEqualsExpression (NumericalFilterOptimizer.java:96-185)."""
+    kind, v = _literal(str(f.value))
+    const = TRUE if isinstance(f, Q.NotEqPredicate) else FALSE
+    if kind == "LONG":
         if dt == "INT":
-            return const  # LONG literal outside INT
-        if dt == "FLOAT" and _f32(v) != v:
-            return const
-        if dt == "DOUBLE" and Decimal(float(v)) != v:
-            return const
-        return f
-    if dt == "INT":
-        if Decimal(int(v)) != v or not INT_MIN <= int(v) <= INT_MAX:
-            return const
-        return type(f)(f.column, str(int(v)))
-    if dt == "LONG":
-        if Decimal(int(v)) != v or not LONG_MIN <= int(v) <= LONG_MAX:
-            return const
-        return type(f)(f.column, str(int(v)))
+            return const  # (int) of a long outside INT differs from it
+        if dt in ("FLOAT", "DOUBLE"):
+            conv = _f32_of_long(v) if dt == "FLOAT" else float(v)
+            if _bd(v) != _bd(conv):
+                return const  # lossy conversion
+            return type(f)(f.column, repr(conv))
+    elif kind == "DOUBLE":
+        if dt == "INT":
+            conv = _cast_int(v, INT_MIN, INT_MAX)
+            if conv != v:
+                return const
+            return type(f)(f.column, str(conv))
+        if dt == "LONG":
+            conv = _cast_int(v, LONG_MIN, LONG_MAX)
+            if _bd(v) != _bd(conv):
+                return const
+            return type(f)(f.column, str(conv))
     return f
 
 
-def _numerical_range(f, schema):
-    dt = schema.get(f.column, (None,))[0]
+def _numerical_range(f, dt):
+    """rewriteRangeExpression + rewriteRangeOperator (NumericalFilterOptimizer.java:187-360)."""
     lower_side = f.lower != Q.UNBOUNDED  # col > v / col >= v
-    text = str(f.lower if lower_side else f.upper)
-    v = _num(text)
-    if dt not in NUMERIC or v is None:
-        return f
+    kind, v = _literal(str(f.lower if lower_side else f.upper))
     greater_true = TRUE if lower_side else FALSE  # the literal lies below every value of the type
     less_true = FALSE if lower_side else TRUE     # the literal lies above every value of the type
 
-    def rewritten(conv, cmp):
+    def rewritten(conv_text, cmp):
         # rewriteRangeOperator: literal > converted: "> / >=" -> ">", "< / <=" -> "<="; literal < converted: "> / >="
         # -> ">=", "< / <=" -> "<"
         if lower_side:
             incl = f.lower_inclusive if cmp == 0 else cmp < 0
-            return Q.RangePredicate(f.column, conv, incl, Q.UNBOUNDED, False)
+            return Q.RangePredicate(f.column, conv_text, incl, Q.UNBOUNDED, False)
         incl = f.upper_inclusive if cmp == 0 else cmp > 0
-        return Q.RangePredicate(f.column, Q.UNBOUNDED, False, conv, incl)
+        return Q.RangePredicate(f.column, Q.UNBOUNDED, False, conv_text, incl)
 
-    if _is_int_text(text):
-        if INT_MIN <= v <= INT_MAX:
-            return f
+    if kind == "LONG":
         if dt == "INT":
             return less_true if v > INT_MAX else greater_true
         if dt in ("FLOAT", "DOUBLE"):
-            conv = _f32(v) if dt == "FLOAT" else Decimal(float(v))
-            cmp = (v > conv) - (v < conv)
-            return rewritten(repr(float(conv)), cmp)
-        return f
-    if dt in ("INT", "LONG"):
-        lo, hi = (INT_MIN, INT_MAX) if dt == "INT" else (LONG_MIN, LONG_MAX)
-        conv = int(v)  # (int) / (long) cast: truncation toward zero, saturating
-        conv = max(lo, min(hi, conv))
-        cmp = (v > conv) - (v < conv)
-        if cmp > 0 and conv == hi:
-            return less_true
-        if cmp < 0 and conv == lo:
-            return greater_true
-        return rewritten(str(conv), cmp)
-    if dt == "FLOAT":
-        with np.errstate(over="ignore"):
-            c = float(np.float32(float(v)))
-        if c == float("inf"):
-            return less_true
-        if c == float("-inf"):
-            return greater_true
+            conv = _f32_of_long(v) if dt == "FLOAT" else float(v)
+            return rewritten(repr(conv), _cmp(_bd(v), _bd(conv)))
+    elif kind == "DOUBLE":
+        if dt in ("INT", "LONG"):
+            lo, hi = (INT_MIN, INT_MAX) if dt == "INT" else (LONG_MIN, LONG_MAX)
+            conv = _cast_int(v, lo, hi)
+            cmp = _cmp(v, conv) if dt == "INT" else _cmp(_bd(v), _bd(conv))  # Double.compare / BigDecimal.compareTo
+            if cmp > 0 and conv == hi:
+                return less_true
+            if cmp < 0 and conv == lo:
+                return greater_true
+            return rewritten(str(conv), cmp)
+        if dt == "FLOAT":
+            c = _f32_of_double(v)
+            if c == float("inf"):
+                return less_true
+            if c == float("-inf"):
+                return greater_true
     return f
 
 
@@ -268,8 +312,12 @@ def _typed(text, dt):
     if text == Q.UNBOUNDED:
         return None
     if dt in ("INT", "LONG"):
-        d = Decimal(str(text))
-        return int(d)
+        # Integer.valueOf / Long.valueOf of the literal text: a fractional or exponent text ("1.5", "3.0", "1e3") is
+        # a NumberFormatException in the reference, which fails the query
+        if not _is_int_text(str(text)):
+            raise ValueError("range bound %r of an %s column is not an integer (the reference's MergeRangeFilterOptimizer "
+                             "rejects it: NumberFormatException)" % (text, dt))
+        return int(Decimal(str(text)))
     if dt == "FLOAT":
         with np.errstate(over="ignore"):
             return float(np.float32(float(text)))

@@ -110,3 +110,60 @@ def test_merged_range_is_one_scan_in_the_statistics():
     in_two = FS.entries_scanned_in_filter(raw, seg, np.asarray([v >= 10, v <= 40]))
     assert in_one == n  # one scan driven to EOF reads every entry once
     assert in_two > n
+
+
+SCHEMA_MV = dict(SCHEMA, mvIntColumn=("INT", False))
+
+
+@pytest.mark.parametrize("where,expected", [
+    # FlattenAndOrFilterOptimizer returns a NOT as it is; MergeEqInFilterOptimizer recurses into a NOT only as an OR's
+    # operand (FlattenAndOrFilterOptimizer.java:48-51, MergeEqInFilterOptimizer.java:61-63, :117)
+    ("NOT (intColumn = 1 OR intColumn = 2)", "NOT (intColumn = 1 OR intColumn = 2)"),
+    ("longColumn > 3 AND NOT (intColumn = 1 OR intColumn = 2)", "longColumn > 3 AND NOT (intColumn = 1 OR intColumn = 2)"),
+    ("longColumn = 3 OR NOT (intColumn = 1 OR intColumn = 2)", "longColumn = 3 OR NOT (intColumn IN (1, 2))"),
+    ("NOT (intColumn IN (1, 1))", "NOT (intColumn IN (1, 1))"),
+    ("longColumn = 3 OR NOT (intColumn IN (1, 1))", "longColumn = 3 OR NOT (intColumn = 1)"),
+    # numerical rewrites skip multi-value columns (getDataType returns null for them, NumericalFilterOptimizer.java:370)
+    ("mvIntColumn = 5000000000", "mvIntColumn = 5000000000"),
+    ("mvIntColumn > 5.5", "mvIntColumn > 5.5"),
+    # a DOUBLE literal is compared as the double the SQL compiler made of it (RequestUtils.java:121)
+    ("intColumn = 3.00000000000000001", "intColumn = 3"),
+    ("longColumn >= 1.00000000000000001", "longColumn >= 1"),
+    ("longColumn = 5.0", "longColumn = 5"),
+])
+def test_not_and_numerical_semantics(where, expected):
+    got = optimize_filter(Q.parse_filter(where), SCHEMA_MV)
+    exp = Q.parse_filter(expected)
+    assert _canon(got) == _canon(exp), (where, got)
+
+
+def _canon(f):
+    """Structure-preserving form (unlike _norm, nested NOT / AND / OR nodes and IN duplicates stay as they are)."""
+    if isinstance(f, (Q.And, Q.Or)):
+        return (type(f).__name__, tuple(sorted(repr(_canon(c)) for c in f.children)))
+    if isinstance(f, Q.Not):
+        return ("Not", _canon(f.child))
+    if isinstance(f, (Q.InPredicate, Q.NotInPredicate)):
+        return (type(f).__name__, f.column, tuple(sorted(_lit(v) for v in f.values)))
+    if isinstance(f, (Q.EqPredicate, Q.NotEqPredicate)):
+        return (type(f).__name__, f.column, _lit(f.value))
+    if isinstance(f, Q.RangePredicate):
+        return ("Range", f.column, _lit(f.lower), f.lower_inclusive, _lit(f.upper), f.upper_inclusive)
+    return f
+
+
+@pytest.mark.parametrize("where", [
+    "intColumn >= 1 AND intColumn BETWEEN 1.5 AND 10",
+    "intColumn BETWEEN -1.5 AND 3 AND intColumn > -1",
+    "longColumn BETWEEN 2.0 AND 5 AND doubleColumn = 1",
+])
+def test_fractional_range_bound_of_an_integer_column_fails(where):
+    """MergeRangeFilterOptimizer converts every range operand of an AND with Integer.valueOf / Long.valueOf of the
+    literal text (getComparable, :134): a fractional bound fails the query instead of merging to a wrong range."""
+    with pytest.raises(ValueError, match="not an integer"):
+        optimize_filter(Q.parse_filter(where), SCHEMA)
+
+
+def test_integral_range_bounds_still_merge():
+    got = optimize_filter(Q.parse_filter("intColumn >= 1 AND intColumn BETWEEN 2 AND 10"), SCHEMA)
+    assert isinstance(got, Q.RangePredicate) and (got.lower, got.lower_inclusive, got.upper) == ("2", True, "10")
