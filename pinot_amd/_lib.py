@@ -28,6 +28,9 @@ PA_QF_WG_SHIFT = 12
 PA_QF_DEBUG_STREAM_ONLY = 1 << 16
 PA_QF_NO_LANE_MAJOR = 1 << 17
 PA_QF_NO_REG_STAGE = 1 << 18
+PA_QF_NO_GDENSE_LM = 1 << 15
+PA_QF_NO_GD_PACK = 1 << 3
+PA_QF_GD_DRAIN_EACH_TILE = 1 << 2
 PA_QF_NO_BOX_FILTER = 1 << 19
 PA_QF_BOX_FILTER = 1 << 20
 PA_QF_NO_PARTITION = 1 << 21
@@ -52,6 +55,7 @@ EXPORTED = [
     "pa_segment_add_raw_column", "pa_segment_num_docs", "pa_segment_device_bytes", "pa_segment_destroy",
     "pa_query_create", "pa_query_bind_segment", "pa_query_bind_value_remap", "pa_query_prepare", "pa_query_num_keys",
     "pa_query_execute", "pa_query_reset", "pa_query_scan", "pa_query_num_eager_literals", "pa_query_lane_major",
+    "pa_query_dense_packed",
     "pa_query_accumulator_bytes", "pa_query_set_accumulator_buffer", "pa_query_num_sections", "pa_query_section",
     "pa_query_fetch", "pa_query_matched_docs", "pa_query_key_layout", "pa_query_limit_trimming",
     "pa_query_num_groups_limit_reached", "pa_query_stats", "pa_query_leaf_bitmap_words", "pa_query_leaf_bitmaps",
@@ -132,6 +136,7 @@ def _declare(lib):
         "pa_query_scan": (ctypes.c_int, [vp, vp]),
         "pa_query_num_eager_literals": (i32, [vp]),
         "pa_query_lane_major": (i32, [vp]),
+        "pa_query_dense_packed": (i32, [vp]),
         "pa_query_accumulator_bytes": (u64, [vp]),
         "pa_query_set_accumulator_buffer": (ctypes.c_int, [vp, vp, u64]),
         "pa_query_num_sections": (i32, [vp]),

@@ -517,6 +517,7 @@ struct pa_query {
   DevBuf fetch_blocks, fetch_stage;  // large-key fetch: per-block counts / compacted rows
   void* fetch_host = nullptr;        // pinned copy of the compacted rows
   int lane_major = 0;
+  int dense_packed = 0;  // STRAT_GDENSE_LM*: packed accumulation (GdLmPlan)
   int has_mv = 0;
   bool hashed = false;           // packed 64-bit keys through a global open-addressing table
   int key_words = 1;             // hashed: 2 = two-word keys ([k0, k1, state] per slot)
@@ -673,6 +674,13 @@ struct Prep {
   std::vector<int> gd_vs, gd_op, gd_acc, gd_tab_a, gd_tab_an;
   std::vector<int64_t> gd_base, gd_step;
   std::vector<std::vector<const void*>> gd_src;  // [seg][agg] device dictionary behind the LDS value table
+  // lane-major walk, packed accumulation (GdLmPlan): possible (COUNT + SUM terms fit), the term bits and, for a value
+  // table turned into offsets (GVS_T32U), the offsets' base; chosen when the lane-major variant is
+  bool gd_pk_ok = false, gd_packed = false;
+  int gd_pk_c = 0;                         // bits of each field beyond its term (the drain bound)
+  std::vector<int> gd_pk_w;                // per aggregation: term bits
+  std::vector<char> gd_pk_t32u;            // per aggregation: the value table becomes uint32 offsets from gd_pk_base
+  std::vector<int64_t> gd_pk_base;
 };
 
 // Filter: CNF, clause order (most selective first), eager/lazy split, column slots of the leaves.
@@ -1182,6 +1190,59 @@ int plan_gdense(pa_query* q, Prep& P) {
     P.gd_vs[a] = vs;
     P.gd_op[a] = op;
     row[a] = op == GOP_SUM_L ? 16 : (op == GOP_MIN_U || op == GOP_MAX_U) ? 4 : 8;
+  }
+  // Packed accumulation for the lane-major walk: COUNT and every aggregation a SUM whose per-doc term is a small
+  // non-negative integer — the dictId of an affine dictionary (GVS_ID), or the value minus the smallest value of every
+  // segment's dictionary (a value table of uint32 offsets, GVS_T32U). Fields: each term w_a + c bits, COUNT c bits
+  // (the top), c as large as 64 bits allow; a field then holds 2^c - 1 docs' terms, so the waves drain every
+  // (2^c - 1) / 1024 tiles (c >= 11).
+  P.gd_pk_ok = false;
+  P.gd_pk_w.assign(na, 0);
+  P.gd_pk_t32u.assign(na, 0);
+  P.gd_pk_base.assign(na, 0);
+  if (!(s.flags & PA_QF_NO_GD_PACK)) {
+    bool ok = true;
+    int wsum = 0, nsum = 0;
+    for (int a = 0; a < na && ok; ++a) {
+      const int t = s.aggs[a].type;
+      if (t == PA_AGG_COUNT) continue;
+      if (t != PA_AGG_SUM || P.gd_op[a] != GOP_SUM_I || kind[a] != COL_SV_DICT) {
+        ok = false;
+        break;
+      }
+      int w = 0;
+      if (P.gd_vs[a] == GVS_ID) {
+        int32_t card = 1;
+        for (int si = 0; si < q->nseg; ++si) card = std::max(card, q->segs[si]->cols.at(s.aggs[a].column_id)->cardinality);
+        while (w < 32 && (int64_t(1) << w) < (int64_t)card) ++w;
+      } else if (P.gd_vs[a] == GVS_T32 || P.gd_vs[a] == GVS_T64) {
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        for (int si = 0; si < q->nseg; ++si)
+          for (uint64_t x : q->segs[si]->cols.at(s.aggs[a].column_id)->hvals) {
+            lo = std::min(lo, (int64_t)x);
+            hi = std::max(hi, (int64_t)x);
+          }
+        if (lo > hi || (__int128)hi - (__int128)lo >= ((__int128)1 << 32)) {
+          ok = false;
+          break;
+        }
+        const uint64_t span = (uint64_t)(hi - lo);
+        while (w < 32 && (span >> w) != 0) ++w;
+        P.gd_pk_t32u[a] = 1;
+        P.gd_pk_base[a] = lo;
+      } else {
+        ok = false;
+        break;
+      }
+      P.gd_pk_w[a] = w;
+      wsum += w;
+      ++nsum;
+    }
+    const int c = (64 - wsum) / (1 + nsum);
+    if (ok && c >= 11) {
+      P.gd_pk_ok = true;
+      P.gd_pk_c = std::min(c, 31);
+    }
   }
   // DICT_SET bitmaps identical in every segment go to LDS too (their per-doc reads would otherwise be global loads
   // in the tile loop, each waiting for every tile in flight: vmcnt counts in order), when they fit
@@ -1999,9 +2060,52 @@ int plan_kernels(pa_query* q, Prep& P, TilePlan& plan, TilePlan& count_plan) {
           best_strat = st;
         }
       }
+    // lane-major walk over the LDS-DMA ring (gdl_tile) whenever its ring of two 1024-doc images per wave fits: the most
+    // resident waves (16- or 8-wave workgroups); every staged dictionary column has 1..31 bits (the unpacker switch)
+    // (and every DICT_SET bitmap in LDS: gdl_leaf reads no HBM in the tile loop)
+    bool lm_walk = !(s.flags & (PA_QF_NO_GDENSE_LM | PA_QF_NO_LANE_MAJOR)) && q->num_eager <= kGdLmLeaves;
+    for (int li = 0; li < q->num_eager && lm_walk; ++li)
+      if (s.leaves[q->literals[li].leaf].kind == PA_LEAF_DICT_SET && (li >= (int)P.gd_lut.size() || P.gd_lut[li] < 0))
+        lm_walk = false;
+    for (const DevSeg& d : q->hsegs)
+      for (int k = 0; k < d.num_staged && lm_walk; ++k) {
+        const int nb = d.stage[k].nbits;
+        lm_walk = (nb >= 1 && nb <= 31) || nb == 32 || nb == 64;
+      }
+    size_t lm_acc = P.gd_lds;
+    bool lm_pk = false;
+    if (lm_walk) {
+      TilePlan lmb;
+      int lm_strat = -1;
+      double lm_score = -1;
+      for (int st : {STRAT_GDENSE_LM16, STRAT_GDENSE_LM8})
+        for (int pk : {1, 0}) {
+          if (pk && !P.gd_pk_ok) continue;
+          // packed accumulation: the waves' private rows (nkeys u64 each) follow the accumulators and tables; worth
+          // more than twice the resident waves (one atomic per matching doc instead of one per aggregation)
+          const size_t acc_b = (P.gd_lds + (pk ? (size_t)scan_waves(st) * (size_t)P.gd_nkeys * 8 : 0) + 15) & ~(size_t)15;
+          const TilePlan t = plan_tiles(q, q->hsegs, st, false, acc_b, true);
+          if (t.score < 0) continue;
+          const double sc = t.score + (pk ? 2.5e7 : 0.0);
+          if (sc > lm_score) {
+            lm_score = sc;
+            lmb = t;
+            lm_strat = st;
+            lm_acc = acc_b;
+            lm_pk = pk != 0;
+          }
+        }
+      if (lmb.score >= 0) {
+        best = lmb;
+        best_lm = false;
+        best_strat = lm_strat;
+      } else {
+        lm_walk = false;
+      }
+    }
     // register-staged tiles (more bytes in flight than the LDS ring beside large tables) when every segment shares the
     // LDS tables and a tile's load instructions fit a variant's register ring
-    bool shared = true;
+    bool shared = !lm_walk;
     for (int si = 1; si < q->nseg && shared; ++si) {
       for (int j = 0; j < s.num_group_by; ++j)
         shared = shared && (P.gd_tab[j] < 0 || q->hsegs[si].remap[j] == q->hsegs[0].remap[j]);
@@ -2042,6 +2146,18 @@ int plan_kernels(pa_query* q, Prep& P, TilePlan& plan, TilePlan& count_plan) {
       plan = best;
       q->strategy = best_strat;
       P.lds_acc = P.gd_lds;
+      if (is_gdense_lm(best_strat)) {
+        P.lds_acc = lm_acc;
+        if (lm_pk) {  // packed: tables of values become offsets from the values' minimum
+          P.gd_packed = true;
+          for (int a = 0; a < s.num_aggs; ++a)
+            if (P.gd_pk_t32u[a]) {
+              P.gd_vs[a] = GVS_T32U;
+              P.gd_base[a] = P.gd_pk_base[a];
+              P.gd_step[a] = 1;
+            }
+        }
+      }
     }
   }
   // Aggregation-only over single-value columns (configs[0]'s COUNT(*), SUM(m) WHERE ...): running totals in every lane's
@@ -2219,13 +2335,26 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
                         ? (uint32_t)P.lds_acc : 0;
   if (is_gdense(q->strategy)) {
     // per-segment parameter tables (GdSegPlan): the query's key box and LDS layout + the segment's staged regions
-    q->gdplans.assign((size_t)std::max(1, q->nseg) * 128, 0u);
+    q->gdplans.assign((size_t)std::max(1, q->nseg) * kGdPlanDw, 0u);
     for (int si = 0; si < q->nseg; ++si) {
-      GdSegPlan& g = *(GdSegPlan*)&q->gdplans[(size_t)si * 128];
+      GdSegPlan& g = *(GdSegPlan*)&q->gdplans[(size_t)si * kGdPlanDw];
       const DevSeg& d = q->hsegs[si];
       // register-staged variants: the tile's load instructions (stage_tile's order: columns, then 64-chunk groups)
-      GdRsPlan& rp = *(GdRsPlan*)&q->gdplans[(size_t)si * 128 + 64];
-      for (int k = 0; k < d.num_staged; ++k) {
+      GdRsPlan& rp = *(GdRsPlan*)&q->gdplans[(size_t)si * kGdPlanDw + 64];
+      if (is_gdense_lm(q->strategy)) {  // the lane-major walk's DMA issue table takes the same dwords
+        GdLmIssue& li = *(GdLmIssue*)&q->gdplans[(size_t)si * kGdPlanDw + 64];
+        li.ncols = d.num_staged;
+        for (int k = 0; k < d.num_staged; ++k) {
+          const int nb = d.stage[k].nbits;
+          const uint64_t src = (uint64_t)(uintptr_t)d.stage[k].words;
+          li.col[k].src_lo = (uint32_t)src;
+          li.col[k].src_hi = (uint32_t)(src >> 32);
+          li.col[k].stride = (uint32_t)(2 * kGdSmSteps * nb * 4);
+          li.col[k].chunks = (uint32_t)((kGdSmSteps / 2) * nb);
+          li.col[k].dst = (uint32_t)(4 * d.stage[k].lds_off);
+        }
+      }
+      for (int k = 0; k < d.num_staged && !is_gdense_lm(q->strategy); ++k) {
         const int nb = d.stage[k].nbits;
         const int chunks = (kGdSmSteps / 2) * nb;
         for (int c0 = 0; c0 < chunks && rp.ins < kGdRsMaxIns; c0 += 64) {
@@ -2265,6 +2394,44 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
         ++k;
       }
       g.nagg = k;
+      if (is_gdense_lm(q->strategy)) {
+        GdLmPlan& lp = *(GdLmPlan*)&q->gdplans[(size_t)si * kGdPlanDw + 128];
+        lp.nleaves = q->num_eager;
+        lp.num_docs = d.num_docs;
+        // the group key from the filter's unpack: one group-by column, read by a DICT_RANGE leaf
+        lp.key_leaf = -1;
+        for (int li = 0; li < q->num_eager && li < kGdLmLeaves && s.num_group_by == 1; ++li)
+          if (d.leaves[li].kind == PA_LEAF_DICT_RANGE && s.leaves[q->literals[li].leaf].column_id == s.group_by_columns[0] &&
+              d.leaves[li].lds_off == d.cols[P.gb_slot[0]].lds_off) {
+            lp.key_leaf = li;
+            break;
+          }
+        for (int li = 0; li < q->num_eager && li < kGdLmLeaves; ++li) {
+          const DevLeaf& L = d.leaves[li];
+          lp.lf[li].code = (uint32_t)L.kind | (L.negate ? 0x100u : 0u) | (L.clause_end ? 0x200u : 0u) |
+                           ((uint32_t)L.nbits << 16);
+          lp.lf[li].region = (uint32_t)(4 * L.lds_off);
+          lp.lf[li].lo_t = (uint32_t)L.lo;
+          lp.lf[li].hi_t = (uint32_t)L.span;
+          lp.lf[li].lut_lds = li < (int)P.gd_lut.size() ? P.gd_lut[li] : -1;
+          const uint64_t lut = (uint64_t)(uintptr_t)L.lut;
+          lp.lf[li].lut_lo = (uint32_t)lut;
+          lp.lf[li].lut_hi = (uint32_t)(lut >> 32);
+        }
+        if (P.gd_packed) {
+          lp.packed = 1;
+          int off = 0, kk = 0;
+          for (int a = 0; a < s.num_aggs; ++a) {
+            if (s.aggs[a].type == PA_AGG_COUNT) continue;
+            lp.pk_off[kk++] = off;
+            off += P.gd_pk_w[a] + P.gd_pk_c;
+          }
+          lp.pk_cnt = off;
+          lp.pk_drain = ((1 << P.gd_pk_c) - 1) >> 10;  // tiles of <= 1024 docs each
+          if (s.flags & PA_QF_GD_DRAIN_EACH_TILE) lp.pk_drain = 1;
+          lp.pk_base = (int32_t)P.gd_lds;  // (the waves' rows follow the accumulators and tables)
+        }
+      }
     }
     h.gd_rp_log2 = P.gd_rp_log2;
     h.gd_nkeys = P.gd_nkeys;
@@ -2658,6 +2825,7 @@ int pa_query_prepare(pa_query* q) {
   apply_layout(q->hsegs, plan.steps, nslots, (int)q->literals.size(), dummy, &q->staged_bytes, &total_tiles);
   q->num_tiles = (uint64_t)total_tiles;
   q->lane_major = P.lm ? 1 : 0;
+  q->dense_packed = P.gd_packed ? 1 : 0;
   q->plan_ring = plan.ring;
   q->plan_wg = plan.wg_per_cu;
   fill_devquery(q, P, plan, total_tiles);
@@ -3329,6 +3497,7 @@ int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t*
 int32_t pa_query_num_eager_literals(const pa_query* q) { return q && q->prepared ? q->num_eager : -1; }
 
 int32_t pa_query_lane_major(const pa_query* q) { return q && q->prepared ? q->lane_major : -1; }
+int32_t pa_query_dense_packed(const pa_query* q) { return q && q->prepared ? q->dense_packed : -1; }
 
 int32_t pa_query_column_staged(const pa_query* q, int32_t column_id) {
   if (!q || !q->prepared || q->nseg == 0) return -1;

@@ -51,15 +51,19 @@ enum Strategy : int32_t {
   // 3 tiles of <= 12 instructions
   STRAT_GDENSE_RS12 = 11, STRAT_GDENSE_RS8 = 12,
   // the count pass of a query grouping by a multi-value column (one record per (doc, value) pair)
-  STRAT_PCOUNT_MV = 13
+  STRAT_PCOUNT_MV = 13,
+  // STRAT_GDENSE over the LDS-DMA ring with the lane-major walk (gdl_tile): 8- / 16-wave workgroups
+  STRAT_GDENSE_LM8 = 14, STRAT_GDENSE_LM16 = 15
 };
 __host__ __device__ constexpr bool is_pcount(int s) { return s == STRAT_PCOUNT || s == STRAT_PCOUNT_MV; }
 // STRAT_GDENSE: 4-wave workgroups; STRAT_GDENSE8 / STRAT_GDENSE12: the same kernel with 8- / 12-wave workgroups (2 / 3
 // waves per SIMD when one workgroup fits a CU, e.g. beside a 64 KiB value table: the walk's LDS round trips and VALU
 // issue overlap across waves; 12 waves: step-major tiles only)
 __host__ __device__ constexpr bool is_gdense(int s) {
-  return s == STRAT_GDENSE || s == STRAT_GDENSE8 || s == STRAT_GDENSE12 || s == STRAT_GDENSE_RS12 || s == STRAT_GDENSE_RS8;
+  return s == STRAT_GDENSE || s == STRAT_GDENSE8 || s == STRAT_GDENSE12 || s == STRAT_GDENSE_RS12 || s == STRAT_GDENSE_RS8 ||
+         s == STRAT_GDENSE_LM8 || s == STRAT_GDENSE_LM16;
 }
+__host__ __device__ constexpr bool is_gdense_lm(int s) { return s == STRAT_GDENSE_LM8 || s == STRAT_GDENSE_LM16; }
 __host__ __device__ constexpr bool is_gdense_rs(int s) { return s == STRAT_GDENSE_RS12 || s == STRAT_GDENSE_RS8; }
 // register ring of the register-staged variants: tiles in flight + 1, wave instructions per tile at most
 __host__ __device__ constexpr int gd_rs_ring(int s) { return s == STRAT_GDENSE_RS12 ? 4 : 3; }
@@ -73,7 +77,8 @@ enum GdVs : int32_t {
   GVS_RI32 = 4,  // staged raw INT
   GVS_RF32 = 5,  // staged raw FLOAT
   GVS_RI64 = 6,  // staged raw LONG
-  GVS_RF64 = 7   // staged raw DOUBLE
+  GVS_RF64 = 7,  // staged raw DOUBLE
+  GVS_T32U = 8   // per-segment LDS table of uint32 offsets from gd_base (value = gd_base + entry; packed SUMs, GdLmPlan)
 };
 __host__ __device__ constexpr bool gvs_float(int vs) { return vs == GVS_TF || vs == GVS_RF32 || vs == GVS_RF64; }
 enum GdOp : int32_t {
@@ -111,8 +116,9 @@ __host__ __device__ constexpr bool pemit_mv(int s) { return is_pemit(s) && (s - 
 __host__ __device__ constexpr bool part_mv(int s) { return s == STRAT_PCOUNT_MV || pemit_mv(s); }
 __host__ __device__ constexpr int scan_waves(int s) {
   return is_pemit(s) && pemit_big(s) ? kEmitBigWaves
-                                       : (s == STRAT_GDENSE8 || s == STRAT_GDENSE_RS8) ? 2 * kGdWaves
-                                       : (s == STRAT_GDENSE12 || s == STRAT_GDENSE_RS12) ? 3 * kGdWaves : kWavesPerWG;
+                                       : (s == STRAT_GDENSE8 || s == STRAT_GDENSE_RS8 || s == STRAT_GDENSE_LM8) ? 2 * kGdWaves
+                                       : (s == STRAT_GDENSE12 || s == STRAT_GDENSE_RS12) ? 3 * kGdWaves
+                                       : s == STRAT_GDENSE_LM16 ? 4 * kGdWaves : kWavesPerWG;
 }
 // V record formats (word 0 always holds the key's offset inside its partition, key & ((1 << kshift_v) - 1)):
 //   V_FMT_KEY: COUNT only, one word;  V_FMT_ID: one word, | value id << kshift_v (the value column's table-wide value
@@ -319,7 +325,9 @@ struct DevQuery {
 constexpr int kGdMaxGb = 3;    // group-by columns
 constexpr int kGdMaxAgg = 6;   // non-COUNT aggregations
 constexpr int kGdRs12MaxGb = 2, kGdRs12MaxAgg = 2;  // STRAT_GDENSE_RS12: at most this many (its VGPR budget)
-// (gd_plans holds 128 dwords per segment: the GdSegPlan, then the GdRsPlan of the register-staged variants)
+// (gd_plans holds kGdPlanDw dwords per segment: the GdSegPlan, the GdRsPlan of the register-staged variants or the
+// GdLmIssue of the lane-major ones, then the GdLmPlan of the lane-major ones)
+constexpr int kGdPlanDw = 192;
 struct GdSegPlan {
   int32_t ngb, nagg, rpl, pad;           // 0..3
   struct {                               // 4 + 6j
@@ -351,6 +359,50 @@ struct GdRsPlan {
   int32_t pad1[2];
 };
 static_assert(sizeof(GdRsPlan) == 256, "one dword per lane");
+// Lane-major dense walk (STRAT_GDENSE_LM*): the LDS-DMA of one 1024-doc tile of the segment's staged columns, read
+// from one VGPR (lane k holds dword k) with v_readlane, so issuing a tile needs no descriptor load (a vector load's
+// vmcnt wait would wait for every DMA in flight; a scalar load's lgkmcnt wait for the LDS atomics in flight).
+struct GdLmIssue {
+  int32_t ncols;                         // 0
+  struct {                               // 1 + 5c
+    uint32_t src_lo, src_hi;             // the column's stream (tile 0's first chunk)
+    uint32_t stride;                     // bytes per tile
+    uint32_t chunks;                     // 16-byte chunks per tile
+    uint32_t dst;                        // byte offset of the column's region in the tile image
+  } col[kMaxSlots];
+  int32_t pad1[3];
+};
+static_assert(sizeof(GdLmIssue) == 256, "one dword per lane");
+
+// Lane-major dense walk: the per-segment parameters its tile loop reads (one VGPR, v_readlane; no scalar load, whose
+// lgkmcnt wait would also wait for the LDS atomics in flight). Packed accumulation: when COUNT and every SUM's per-doc
+// term (a dictId of an affine dictionary, or an offset from gd_base through a GVS_T32U table) fit one 64-bit word
+// together, a matching doc is ONE ds_add_u64 into its wave's private packed row [key] (term a at bit pk_off[a], COUNT
+// in the top bits from pk_cnt): a field of c bits holds 2^c - 1 docs' terms, so each wave drains its packed rows into
+// the workgroup's accumulators every pk_drain tiles (at most 1024 docs each).
+constexpr int kGdLmLeaves = 6;
+struct GdLmPlan {
+  int32_t nleaves;                       // 0: eager leaves (every literal)
+  int32_t num_docs;                      // 1
+  int32_t packed;                        // 2: 1 = packed accumulation
+  int32_t pk_cnt;                        // 3: bit offset of the COUNT field (the top field)
+  int32_t pk_drain;                      // 4: tiles between drains
+  int32_t pk_base;                       // 5: LDS byte offset of wave 0's packed rows (nkeys u64 per wave)
+  int32_t pk_off[kGdMaxAgg];             // 6..11: bit offset of non-COUNT aggregation k's field
+  int32_t key_leaf;                      // 12: the eager leaf on the (single) group-by column: its unpacked values are
+                                         //     the key's (no second unpack), -1: none
+  int32_t pad0[3];                       // 13..15
+  struct {                               // 16 + 7l
+    uint32_t code;                       // kind | negate << 8 | clause_end << 9 | nbits << 16
+    uint32_t region;                     // byte offset of the column's region in the tile image
+    uint32_t lo_t, hi_t;                 // DICT_RANGE bounds, MSB-aligned (leaf_bits)
+    int32_t lut_lds;                     // DICT_SET: LDS byte offset of the bitmap, -1: in HBM
+    uint32_t lut_lo, lut_hi;             // DICT_SET bitmap in HBM
+  } lf[kGdLmLeaves];
+  int32_t pad1[6];
+};
+static_assert(sizeof(GdLmPlan) == 256, "one dword per lane");
+
 // part_agg_kernel variant: -1 generic, else sum kind (0 none, 1 + AccSrc) | MIN << 2 | MAX << 3
 constexpr int kVkGeneric = -1;
 __host__ __device__ constexpr int vk_code(int sum_kind, bool mn, bool mx) { return sum_kind | (mn ? 4 : 0) | (mx ? 8 : 0); }

@@ -402,6 +402,423 @@ __device__ __forceinline__ uint32_t gd_tile_sm(uint32_t gt, const DevQuery* __re
   return mine;
 }
 
+// ---------------------------------------------------------------- lane-major walk (STRAT_GDENSE_LM8 / LM16)
+// The image of a 1024-doc tile is the step-major one (stage_tile<kGdSmSteps>: each column's 1024 nb-bit values as one
+// contiguous stream), but lane l takes docs [16 l, 16 l + 16): its 16 values of an nb-bit column are the stream bits
+// [16 l nb, 16 (l + 1) nb), i.e. nb / 2 + 1 words read once (ds_read_b32, conflict-free for odd nb, 2-way for nb = 2
+// mod 4) and unpacked with constant shifts (a switch on nb selects the unpacker). Against the step-major walk's ds_read2
+// per doc and column (plus its ds_bpermute transpose and set-bit walk), a column costs 1/32 of a read per doc, and every
+// value the accumulation needs is already in the lane's registers: a matching doc costs only its LDS atomics, issued
+// under a per-doc EXEC mask for docs i = 0..15 in turn.
+constexpr int kGdlDocs = 16;  // docs per lane of a 1024-doc tile
+
+// The lane's 16 values of an NB-bit column region (word 0 = the tile's first stream word), MSB-aligned: value i in
+// the top NB bits of v[i] (junk below). The lane's bits start at 16 lane NB, a word boundary or (odd NB, odd lane) 16
+// bits into a word: the words are read from one word earlier on word boundaries and realigned with ONE alignbit each
+// (shift 0 or 16), then unpacked with constant shifts.
+template <int NB>
+__device__ __forceinline__ void gdl_top(uint32_t region, int lane, uint32_t (&v)[kGdlDocs]) {
+  constexpr int K = (kGdlDocs * NB + 31) / 32 + 1;  // words holding the lane's 16 values (+1: the unpack's window)
+  // (an opaque copy of the lane id per call: otherwise the compiler computes every unpacker case's lane offset ahead
+  // of the switch, ~5 instructions per case on every tile)
+  uint32_t ln = (uint32_t)lane;
+  asm volatile("" : "+v"(ln));
+  const uint32_t bit0 = __umul24(ln, (uint32_t)(kGdlDocs * NB));
+  uint32_t w[K];
+  if constexpr ((kGdlDocs * NB) % 32 != 0) {  // odd NB
+    const uint32_t sh = bit0 & 16u;
+    const lds_u32_t* p = lds_at<const lds_u32_t>(region + 4u * ((bit0 >> 5) - 1u + (sh >> 4)));
+    uint32_t r[K + 1];
+#pragma unroll
+    for (int j = 0; j <= K; ++j) r[j] = p[j];
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = __builtin_amdgcn_alignbit(r[j], r[j + 1], sh);
+  } else {
+    const lds_u32_t* p = lds_at<const lds_u32_t>(region + 4u * (bit0 >> 5));
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = p[j];
+  }
+#pragma unroll
+  for (int i = 0; i < kGdlDocs; ++i) {
+    const int s = i * NB, j = s >> 5, o = s & 31;
+    v[i] = (o + NB <= 32) ? (w[j] << o) : __builtin_amdgcn_alignbit(w[j], w[j + 1], 32 - o);
+  }
+}
+
+#define PA_GDL_NB_CASES(X)                                                                                          \
+  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20)   \
+  X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31)
+
+// dictIds of the lane's 16 docs (nb wave-uniform, 1..31)
+__device__ __forceinline__ void gdl_ids(int nb, uint32_t region, int lane, uint32_t (&id)[kGdlDocs]) {
+  switch (nb) {
+#define PA_GDL_IDS(N)                                                \
+  case N: {                                                          \
+    gdl_top<N>(region, lane, id);                                    \
+    _Pragma("unroll") for (int i = 0; i < kGdlDocs; ++i) id[i] >>= 32 - N; \
+  } break;
+    PA_GDL_NB_CASES(PA_GDL_IDS)
+#undef PA_GDL_IDS
+    default:
+#pragma unroll
+      for (int i = 0; i < kGdlDocs; ++i) id[i] = 0;
+      break;
+  }
+}
+
+// Match bits of one DICT_RANGE / DICT_SET leaf over the lane's 16 docs (bit i <=> doc 16 lane + i), before negation.
+// DICT_RANGE bounds MSB-aligned by the host (leaf_bits): 3 VALU per doc; a DICT_SET bitmap in LDS: the word by the
+// dictId's high bits, the bit by v_bfe, 5 VALU + one LDS read per doc (the bitmap is always in LDS: a global load in
+// the tile loop would make the compiler's vmcnt waits cover the DMA in flight — the planner keeps such queries off the
+// lane-major walk). keep_it: the unpacked values also go to `keep` (the group key is this leaf's column).
+template <int NB>
+__device__ __forceinline__ uint32_t gdl_leaf(int kind, uint32_t region, int lane, uint32_t lo_t, uint32_t hi_t,
+                                             uint32_t lut_lds, bool keep_it, uint32_t (&keep)[kGdlDocs]) {
+  uint32_t t[kGdlDocs];
+  gdl_top<NB>(region, lane, t);
+  if (keep_it) {
+#pragma unroll
+    for (int i = 0; i < kGdlDocs; ++i) keep[i] = t[i];
+  }
+  if (kind == PA_LEAF_DICT_RANGE) {
+    uint32_t nm = 0;
+#pragma unroll
+    for (int i = kGdlDocs - 1; i >= 0; --i) {
+      uint32_t u;
+      asm("v_sub_u32_e64 %[u], %[t], %[lo]\n\t"
+          "v_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
+          "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
+          : [nm] "+v"(nm), [u] "=&v"(u)
+          : [t] "v"(t[i]), [lo] "s"(lo_t), [hi] "s"(hi_t)
+          : "vcc");
+    }
+    return ~nm & 0xffffu;
+  }
+  uint32_t id[kGdlDocs], w[kGdlDocs];
+#pragma unroll
+  for (int i = 0; i < kGdlDocs; ++i) {
+    id[i] = t[i] >> (32 - NB);
+    w[i] = *lds_at<const lds_u32_t>(lut_lds + 4u * (id[i] >> 5));
+  }
+  uint32_t bits = 0;
+#pragma unroll
+  for (int i = 0; i < kGdlDocs; ++i) bits |= __builtin_amdgcn_ubfe(w[i], id[i], 1) << i;
+  return bits;
+}
+
+__device__ __forceinline__ uint32_t gdl_leaf_any(int nb, int kind, uint32_t region, int lane, uint32_t lo_t,
+                                                 uint32_t hi_t, uint32_t lut_lds, bool keep_it,
+                                                 uint32_t (&keep)[kGdlDocs]) {
+  switch (nb) {
+#define PA_GDL_LEAF(N) \
+  case N: return gdl_leaf<N>(kind, region, lane, lo_t, hi_t, lut_lds, keep_it, keep);
+    PA_GDL_NB_CASES(PA_GDL_LEAF)
+#undef PA_GDL_LEAF
+    default: return 0;
+  }
+}
+
+// The lane's 16 values of a staged raw column (4 or 8 bytes each, 16-byte aligned region): 4 / 8 ds_read_b128
+__device__ __forceinline__ void gdl_raw32(uint32_t region, int lane, uint32_t (&v)[kGdlDocs]) {
+  const lds_u32x4_t* p = lds_at<const lds_u32x4_t>(region + 64u * (uint32_t)lane);
+  u32x4 r[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r[k] = p[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[4 * k] = r[k].x;
+    v[4 * k + 1] = r[k].y;
+    v[4 * k + 2] = r[k].z;
+    v[4 * k + 3] = r[k].w;
+  }
+}
+__device__ __forceinline__ void gdl_raw64(uint32_t region, int lane, uint64_t (&v)[kGdlDocs]) {
+  const lds_u32x4_t* p = lds_at<const lds_u32x4_t>(region + 128u * (uint32_t)lane);
+  u32x4 r[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = p[k];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    v[2 * k] = ((uint64_t)r[k].y << 32) | r[k].x;
+    v[2 * k + 1] = ((uint64_t)r[k].w << 32) | r[k].z;
+  }
+}
+
+// LDS-DMA of one 1024-doc tile from the segment's GdLmIssue (VGPR ip), padded to exactly D instructions (the padding
+// re-reads the first column's first chunk into the image's guard words).
+__device__ __forceinline__ void gdl_stage(uint32_t ip, int64_t wt, uint32_t img, int lane, const int D) {
+  const int nc = (int)rl(ip, 0);
+  int issued = 0;
+  for (int c = 0; c < nc; ++c) {
+    const uint32_t b = 1u + 5u * (uint32_t)c;
+    const uint64_t src = (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)ip, b + 1) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)ip, b)) +
+                         (uint64_t)wt * (uint32_t)__builtin_amdgcn_readlane((int)ip, b + 2);
+    const int chunks = __builtin_amdgcn_readlane((int)ip, b + 3);
+    const uint32_t dst = img + (uint32_t)__builtin_amdgcn_readlane((int)ip, b + 4);
+    for (int c0 = 0; c0 < chunks; c0 += 64) {
+      if (c0 + lane < chunks) dma16((const void*)(src + 16ull * (uint64_t)(c0 + lane)), dst + 16u * (uint32_t)c0);
+      ++issued;
+    }
+  }
+  const uint64_t src0 = ((uint64_t)rl(ip, 2) << 32) | rl(ip, 1);
+  for (; issued < D; ++issued)
+    if (lane == 0) dma16((const void*)src0, img);
+}
+
+// Drain of a wave's packed rows (GdLmPlan) into the workgroup's accumulators: every non-zero row is read, zeroed and
+// split into its fields (COUNT -> the count array, SUM term a -> the aggregation's u64 sums, replica 0).
+__device__ __forceinline__ void gdl_drain(uint32_t gt, uint32_t lp, uint32_t rows, int nkeys, int lane, uint32_t base) {
+  const int na = (int)rl(gt, 1);
+  const uint32_t rpl = rl(gt, 2), off_c = rl(lp, 3);
+  lds_u64_t* row = lds_at<lds_u64_t>(rows);
+  for (int k = lane; k < nkeys; k += kWave) {
+    const uint64_t x = row[k];
+    if (x == 0) continue;
+    row[k] = 0;
+    const uint32_t idx = (uint32_t)k << rpl;
+    __hip_atomic_fetch_add(lds_at<lds_u32_t>(base) + idx, (uint32_t)(x >> off_c), WG_RLX);
+    for (int g = 0; g < na; ++g) {
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)lp, 6 + g);
+      const uint32_t hi = g + 1 < na ? (uint32_t)__builtin_amdgcn_readlane((int)lp, 7 + g) : off_c;
+      const uint64_t f = (x >> lo) & ((hi - lo) >= 64 ? ~0ull : ((1ull << (hi - lo)) - 1ull));
+      __hip_atomic_fetch_add(lds_at<lds_u64_t>(base + (uint32_t)__builtin_amdgcn_readlane((int)gt, 26 + 6 * g)) + idx, f,
+                             WG_RLX);
+    }
+  }
+}
+
+// One 1024-doc tile, lane-major: filter (or the key box), keys, then the LDS updates of the lane's matching docs —
+// packed (one ds_add_u64 per doc into the wave's row, GdLmPlan) or per aggregation (the lane's 16 values, then one
+// atomic per matching doc). Every parameter comes from the segment's plan VGPRs gt (GdSegPlan) and lp (GdLmPlan).
+// Returns the lane's docs counted in numDocsScanned.
+template <int MG = kGdMaxGb, int MA = kGdMaxAgg>
+__device__ __forceinline__ uint32_t gdl_tile(uint32_t gt, uint32_t lp, int64_t wt, uint32_t img, int lane,
+                                             uint32_t base, uint32_t rows, uint32_t& errs) {
+  constexpr int ND = kGdlDocs;
+  const uint32_t dbg = rl(gt, 3);  // measurement only (PA_DEBUG_EMIT): 32 stream only, 1 filter only, 2 no atomics
+  if (dbg & 32) return 0;
+  const int64_t rem = (int64_t)(int32_t)rl(lp, 1) - wt * (kGdSmSteps * kWave);
+  uint32_t m = 0xffffu;
+  if (rem < kGdSmSteps * kWave) {
+    const int64_t n = rem - ND * lane;
+    m = n >= ND ? 0xffffu : (n <= 0 ? 0u : ((1u << n) - 1u));
+  }
+  const bool box = rl(gt, kGdBoxDword) != 0;
+  const int key_leaf = box ? -1 : (int)rl(lp, 12);
+  uint32_t kt[ND];  // key_leaf >= 0: that leaf's unpacked values (MSB-aligned) = group-by column 0's
+  if (!box) {
+    uint32_t clause = 0;
+    const int nl = (int)rl(lp, 0);
+    for (int li = 0; li < nl; ++li) {
+      const uint32_t b = 16u + 7u * (uint32_t)li;
+      const uint32_t code = (uint32_t)__builtin_amdgcn_readlane((int)lp, b);
+      const int lut_lds = __builtin_amdgcn_readlane((int)lp, b + 4);
+      uint32_t bits = gdl_leaf_any((int)(code >> 16), (int)(code & 0xffu),
+                                   img + (uint32_t)__builtin_amdgcn_readlane((int)lp, b + 1), lane,
+                                   (uint32_t)__builtin_amdgcn_readlane((int)lp, b + 2),
+                                   (uint32_t)__builtin_amdgcn_readlane((int)lp, b + 3), base + (uint32_t)lut_lds,
+                                   li == key_leaf, kt);
+      if (code & 0x100u) bits = ~bits & 0xffffu;
+      clause |= bits;
+      if (code & 0x200u) {
+        m &= clause;
+        clause = 0;
+        if (__ballot(m != 0) == 0) return 0;
+      }
+    }
+  }
+  if (__ballot(m != 0) == 0) return 0;
+  if (dbg & 1) return (uint32_t)__builtin_popcount(m);
+  // group keys: component j = key table entry (per-segment remap into the box, < 0 outside) or dictId - lo (< span)
+  const int ngb = (int)rl(gt, 0), na = (int)rl(gt, 1);
+  uint32_t key[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) key[i] = 0u;
+  uint32_t on = m;
+#pragma unroll
+  for (int j = 0; j < MG; ++j) {
+    if (j >= ngb) break;
+    const int o = 4 + 6 * j;
+    uint32_t id[ND];
+    if (j == 0 && key_leaf >= 0) {
+      const uint32_t shr = 32u - rl(gt, o + 1);
+#pragma unroll
+      for (int i = 0; i < ND; ++i) id[i] = kt[i] >> shr;
+    } else {
+      gdl_ids((int)rl(gt, o + 1), img + 4u * rl(gt, o), lane, id);
+    }
+    const int tab = (int)rl(gt, o + 2);
+    if (tab >= 0) {
+      const lds_i32_t* t = lds_at<const lds_i32_t>(base + (uint32_t)tab);
+      int32_t e[ND];
+#pragma unroll
+      for (int i = 0; i < ND; ++i) e[i] = t[id[i]];
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        on &= ~((e[i] < 0 ? 1u : 0u) << i);
+        key[i] += (uint32_t)e[i];
+      }
+    } else {
+      const uint32_t lo = rl(gt, o + 3), span = rl(gt, o + 4), ls = rl(gt, o + 5);
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        const uint32_t c0 = id[i] - lo;
+        on &= ~((c0 < span ? 0u : 1u) << i);
+        key[i] += c0 * ls;
+      }
+    }
+  }
+  uint32_t mine;
+  if (box) {
+    mine = (uint32_t)__builtin_popcount(on);  // the box is the filter: numDocsScanned = the docs inside it
+  } else {
+    mine = (uint32_t)__builtin_popcount(m);
+    errs += (uint32_t)__builtin_popcount(m & ~on);  // (the planner's box holds every match: none expected)
+  }
+  if (dbg & 2) {
+#pragma unroll
+    for (int i = 0; i < ND; ++i) asm volatile("" ::"v"(key[i]), "v"(on));
+    return mine;
+  }
+  if (rl(lp, 2)) {
+    // packed: one word per doc, COUNT + every SUM term at its field; the fields of one doc's word do not overlap, so
+    // the word is built with ORs, 32 bits at a time (a term below bit 32 also spills into the high word)
+    uint32_t plo[ND], phi[ND];
+    const uint32_t oc = rl(lp, 3);
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      plo[i] = oc < 32 ? 1u << oc : 0u;
+      phi[i] = oc < 32 ? 0u : 1u << (oc - 32);
+    }
+#pragma unroll 1
+    for (int g = 0; g < MA; ++g) {
+      if (g >= na) break;
+      const int o = 22 + 6 * g;
+      uint32_t id[ND];
+      gdl_ids((int)rl(gt, o + 3), img + 4u * rl(gt, o + 2), lane, id);
+      if ((int)rl(gt, o) == GVS_T32U) {
+        const lds_u32_t* t = lds_at<const lds_u32_t>(base + rl(gt, o + 5));
+#pragma unroll
+        for (int i = 0; i < ND; ++i) id[i] = t[id[i]];
+      }
+      const uint32_t sh = (uint32_t)__builtin_amdgcn_readlane((int)lp, 6 + g);
+      if (sh >= 32) {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) phi[i] |= id[i] << (sh - 32);
+      } else if (sh == 0) {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) plo[i] |= id[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+          plo[i] |= id[i] << sh;
+          phi[i] |= __builtin_amdgcn_alignbit(0u, id[i], 32u - sh);
+        }
+      }
+    }
+    lds_u64_t* row = lds_at<lds_u64_t>(rows);
+#pragma unroll
+    for (int i = 0; i < ND; ++i)
+      if ((on >> i) & 1u) __hip_atomic_fetch_add(row + key[i], ((uint64_t)phi[i] << 32) | plo[i], WG_RLX);
+    return mine;
+  }
+  const uint32_t rpl = rl(gt, 2);
+  const uint32_t r = (uint32_t)lane & ((1u << rpl) - 1u);
+#pragma unroll
+  for (int i = 0; i < ND; ++i) key[i] = (key[i] << rpl) | r;  // (from here on: the accumulator index)
+  {
+    lds_u32_t* cnt = lds_at<lds_u32_t>(base);
+#pragma unroll
+    for (int i = 0; i < ND; ++i)
+      if ((on >> i) & 1u) __hip_atomic_fetch_add(cnt + key[i], 1u, WG_RLX);
+  }
+#pragma unroll 1
+  for (int g = 0; g < MA; ++g) {
+    if (g >= na) break;
+    const int o = 22 + 6 * g;
+    const int vs = (int)rl(gt, o), op = (int)rl(gt, o + 1);
+    const uint32_t reg = img + 4u * rl(gt, o + 2);
+    const uint32_t acc = base + rl(gt, o + 4);
+    // v[i]: the value as an int64, or a double's bits (float sources)
+    uint64_t v[ND];
+    if (vs <= GVS_TF || vs == GVS_T32U) {  // dictionary column: dictId from the staged stream, value from the LDS table
+      uint32_t id[ND];
+      gdl_ids((int)rl(gt, o + 3), reg, lane, id);
+      const uint32_t tab = base + rl(gt, o + 5);
+      if (vs == GVS_ID) {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) v[i] = id[i];
+      } else if (vs == GVS_T32) {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) v[i] = (uint64_t)(int64_t)lds_at<const lds_i32_t>(tab)[id[i]];
+      } else if (vs == GVS_T32U) {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) v[i] = lds_at<const lds_u32_t>(tab)[id[i]];
+      } else {  // GVS_T64 / GVS_TF: 8-byte entries
+#pragma unroll
+        for (int i = 0; i < ND; ++i) v[i] = lds_at<const lds_u64_t>(tab)[id[i]];
+      }
+    } else if (vs == GVS_RI32 || vs == GVS_RF32) {
+      uint32_t w[ND];
+      gdl_raw32(reg, lane, w);
+#pragma unroll
+      for (int i = 0; i < ND; ++i)
+        v[i] = vs == GVS_RI32 ? (uint64_t)(int64_t)(int32_t)w[i]
+                              : __builtin_bit_cast(uint64_t, (double)__builtin_bit_cast(float, w[i]));
+    } else {
+      gdl_raw64(reg, lane, v);
+    }
+    const bool fl = gvs_float(vs);
+    switch (op) {
+      case GOP_SUM_I:
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+          if ((on >> i) & 1u) __hip_atomic_fetch_add(lds_at<lds_u64_t>(acc) + key[i], v[i], WG_RLX);
+        break;
+      case GOP_SUM_L:
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+          if (!((on >> i) & 1u)) continue;
+          __hip_atomic_fetch_add(lds_at<lds_u64_t>(acc) + 2 * key[i], (uint64_t)(uint32_t)v[i], WG_RLX);
+          __hip_atomic_fetch_add(lds_at<lds_u64_t>(acc) + 2 * key[i] + 1, (uint64_t)((int64_t)v[i] >> 32), WG_RLX);
+        }
+        break;
+      case GOP_SUM_F:
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+          if ((on >> i) & 1u)
+            __hip_atomic_fetch_add(lds_at<lds_f64_t>(acc) + key[i], __builtin_bit_cast(double, v[i]), WG_RLX);
+        break;
+      case GOP_MIN_I:
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+          if ((on >> i) & 1u)
+            __hip_atomic_fetch_min(lds_at<lds_i64_t>(acc) + key[i],
+                                   fl ? f64_order_encode(__builtin_bit_cast(double, v[i])) : (int64_t)v[i], WG_RLX);
+        break;
+      case GOP_MAX_I:
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+          if ((on >> i) & 1u)
+            __hip_atomic_fetch_max(lds_at<lds_i64_t>(acc) + key[i],
+                                   fl ? f64_order_encode(__builtin_bit_cast(double, v[i])) : (int64_t)v[i], WG_RLX);
+        break;
+      case GOP_MIN_U:
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+          if ((on >> i) & 1u) __hip_atomic_fetch_min(lds_at<lds_u32_t>(acc) + key[i], (uint32_t)v[i], WG_RLX);
+        break;
+      default:  // GOP_MAX_U
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+          if ((on >> i) & 1u) __hip_atomic_fetch_max(lds_at<lds_u32_t>(acc) + key[i], (uint32_t)v[i], WG_RLX);
+        break;
+    }
+  }
+  return mine;
+}
+
 // Per-segment LDS tables: key tables of the group-by columns that have them and value tables of the aggregations.
 __device__ __forceinline__ bool gd_tables_differ(CQ* q, CSegT* a, CSegT* b) {
   for (int j = 0; j < q->num_gb; ++j)
@@ -450,6 +867,10 @@ __device__ void gd_load_tables(CQ* q, CSegT* cs, unsigned char* lds, int tid, in
       if (vs == GVS_T64) {
         int64_t* t = (int64_t*)(lds + tab);
         for (int i = tid; i < n; i += nthreads) t[i] = i < card ? gp(src)[i] : 0;
+      } else if (vs == GVS_T32U) {  // offsets from the smallest value of every segment's dictionary
+        uint32_t* t = (uint32_t*)(lds + tab);
+        const int64_t b = q->aggs[a].gd_base;
+        for (int i = tid; i < n; i += nthreads) t[i] = i < card ? (uint32_t)(gp(src)[i] - b) : 0u;
       } else {
         int32_t* t = (int32_t*)(lds + tab);
         for (int i = tid; i < n; i += nthreads) t[i] = i < card ? (int32_t)gp(src)[i] : 0;
@@ -505,7 +926,9 @@ __device__ void gd_flush(const DevQuery* __restrict__ q, const DevSeg* __restric
           if (A.gd_op == GOP_SUM_I) {
             int64_t s = 0;
             for (int r = 0; r < rp; ++r) s += ((const int64_t*)p)[kl * rp + r];
-            tot = A.gd_vs == GVS_ID ? (__int128)A.gd_base * (__int128)c + (__int128)A.gd_step * (__int128)s : (__int128)s;
+            tot = (A.gd_vs == GVS_ID || A.gd_vs == GVS_T32U)
+                      ? (__int128)A.gd_base * (__int128)c + (__int128)A.gd_step * (__int128)s
+                      : (__int128)s;
           } else {
             int64_t lo = 0, hi = 0;
             for (int r = 0; r < rp; ++r) {
@@ -555,7 +978,8 @@ __device__ void gd_flush(const DevQuery* __restrict__ q, const DevSeg* __restric
 }
 
 // The kernel. LDS: [accumulators | tables] (q->lds_acc_bytes) then each wave's ring of q->ring tile images.
-// LM = 1: lane-major 2048-doc tiles (per-segment plan tables); LM = 0: step-major 1024-doc tiles.
+// LM = 1: lane-major 2048-doc tiles (per-segment plan tables); LM = 0: step-major 1024-doc tiles; LM = 2: the same
+// 1024-doc images walked lane-major (gdl_tile).
 template <int WPW, int LM>
 __global__ void __launch_bounds__(WPW * kWave, 1) gdense_kernel(const DevQuery* __restrict__ q_in,
                                                                 const DevSeg* __restrict__ segs,
@@ -578,22 +1002,35 @@ __global__ void __launch_bounds__(WPW * kWave, 1) gdense_kernel(const DevQuery* 
   const int64_t lb = q->xcd_major ? xcd_major_block(blockIdx.x, G) : (int64_t)blockIdx.x;
   const int64_t t0 = lb * T / G, t1 = (lb + 1) * T / G;
   uint32_t matched = 0, errs = 0;
+  // LM == 2: the segment's GdSegPlan / GdLmPlan, the wave's packed rows, tiles between drains (0: not packed)
+  uint32_t gt_cur = 0, lp = 0, rows = 0, pk_drain = 0, since = 0;
   if (t0 < t1) {  // (workgroup-uniform)
     const int nseg = q->num_segments;
     // issue side: this wave's tiles t0 + wave + WPW k, LDS-DMA into its ring, R - 1 tiles ahead
     int64_t ti = t0 + wave;
     int isi = find_segment(segs, nseg, t0);
     int64_t ifirst = segs[isi].first_wtile, iend = ifirst + segs[isi].num_wtiles;
-    uint32_t ip = LM ? ((const uint32_t*)(plans + isi))[lane] : 0u;
+    uint32_t ip = LM == 1 ? ((const uint32_t*)(plans + isi))[lane] : 0u;
+    if (LM == 2) {
+      ip = gp(q->gd_plans)[(int64_t)isi * kGdPlanDw + 64 + lane];  // GdLmIssue
+      // (a use right here makes the compiler wait for this load here, once per segment, and not at the next merge
+      // point after a tile's DMA issue, where its vmcnt(0) would wait for the DMA too)
+      asm volatile("" ::"v"(ip));
+    }
     int islot = 0;
     auto issue_next = [&]() {
       while (ti >= iend) {
         ++isi;
         ifirst = segs[isi].first_wtile;
         iend = ifirst + segs[isi].num_wtiles;
-        if (LM) ip = ((const uint32_t*)(plans + isi))[lane];
+        if (LM == 1) ip = ((const uint32_t*)(plans + isi))[lane];
+        if (LM == 2) {
+          ip = gp(q->gd_plans)[(int64_t)isi * kGdPlanDw + 64 + lane];
+          asm volatile("" ::"v"(ip));
+        }
       }
-      if constexpr (LM) stage_tile_lm(ip, ti - ifirst, ring_lds + 4u * (uint32_t)(islot * img_dw), lane, D);
+      if constexpr (LM == 1) stage_tile_lm(ip, ti - ifirst, ring_lds + 4u * (uint32_t)(islot * img_dw), lane, D);
+      else if constexpr (LM == 2) gdl_stage(ip, ti - ifirst, ring_lds + 4u * (uint32_t)(islot * img_dw), lane, D);
       else stage_tile<kGdSmSteps>(segs + isi, ti - ifirst, ring + islot * img_dw, lane, D);
       ti += WPW;
       islot = islot + 1 == R ? 0 : islot + 1;
@@ -611,19 +1048,41 @@ __global__ void __launch_bounds__(WPW * kWave, 1) gdense_kernel(const DevQuery* 
       }
       const int64_t sfirst = cs->first_wtile;
       const int64_t send = min(t1, sfirst + (int64_t)cs->num_wtiles);
-      const uint32_t pp = LM ? ((const uint32_t*)(plans + s))[lane] : 0u;
-      const uint32_t gt = gp(q->gd_plans)[(int64_t)s * 128 + lane];  // this segment's GdSegPlan, one dword per lane
+      const uint32_t pp = LM == 1 ? ((const uint32_t*)(plans + s))[lane] : 0u;
+      const uint32_t gt = gp(q->gd_plans)[(int64_t)s * kGdPlanDw + lane];  // this segment's GdSegPlan, one dword per lane
+      asm volatile("" ::"v"(gt));  // (waited for here, once per segment: see ip)
+      gt_cur = gt;
+      if (LM == 2) {
+        lp = gp(q->gd_plans)[(int64_t)s * kGdPlanDw + 128 + lane];  // GdLmPlan
+        asm volatile("" ::"v"(lp));
+        pk_drain = rl(lp, 2) ? rl(lp, 4) : 0u;
+        rows = base + rl(lp, 5) + (uint32_t)wave * (uint32_t)q->gd_nkeys * 8u;
+      }
       for (; t < send; t += WPW) {
         uint32_t slot_off = (uint32_t)(pslot * img_dw);
-        wait_tile((int)((ti - t) / WPW - 1), D, slot_off);  // tile t has landed (its younger tiles may still fly)
-        if (ti < t1) issue_next();
-        if constexpr (LM) matched += gd_tile(gt, pp, t - sfirst, ring_lds + 4u * slot_off, lane, base, errs);
+        if (LM == 2 && (rl(gt, 3) & 64)) {  // measurement only (PA_DEBUG_EMIT 64): no DMA, compute on stale images
+          ti = t1;
+        } else {
+          wait_tile((int)((ti - t) / WPW - 1), D, slot_off);  // tile t has landed (its younger tiles may still fly)
+          if (ti < t1) issue_next();
+        }
+        if constexpr (LM == 1) matched += gd_tile(gt, pp, t - sfirst, ring_lds + 4u * slot_off, lane, base, errs);
+        else if constexpr (LM == 2) {
+          matched += gdl_tile(gt, lp, t - sfirst, ring_lds + 4u * slot_off, lane, base, rows, errs);
+          if (pk_drain && ++since == pk_drain) {  // (packed rows: drained before a field can overflow)
+            gdl_drain(gt, lp, rows, q->gd_nkeys, lane, base);
+            since = 0;
+          }
+        }
         else matched += gd_tile_sm(gt, q_in, segs + s, t - sfirst, ring + slot_off, ring_lds + 4u * slot_off, lane, base, errs);
         pslot = pslot + 1 == R ? 0 : pslot + 1;
       }
     }
   }
   __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // vmcnt(0): no DMA left in flight
+  if constexpr (LM == 2) {
+    if (pk_drain) gdl_drain(gt_cur, lp, rows, q->gd_nkeys, lane, base);
+  }
   const int64_t wm = wave_sum_i64((int64_t)matched);
   const int64_t we = wave_sum_i64((int64_t)errs);
   if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)wm, RLX);
@@ -685,7 +1144,7 @@ __device__ __forceinline__ void rs_issue_next(CQ* q, const DevSeg* __restrict__ 
       CSegT* sg = (CSegT*)(uintptr_t)uniform_ptr(segs + c.si);
       c.first = sg->first_wtile;
       c.end = c.first + sg->num_wtiles;
-      c.rp = gp(q->gd_plans)[(int64_t)c.si * 128 + 64 + lane];
+      c.rp = gp(q->gd_plans)[(int64_t)c.si * kGdPlanDw + 64 + lane];
     }
     rs_issue<DM>(c.rp, c.ti - c.first, lane, r);
   }
@@ -725,8 +1184,8 @@ __device__ __forceinline__ void rs_step(CQ* q, const DevQuery* __restrict__ q_in
     CSegT* sg = (CSegT*)(uintptr_t)uniform_ptr(segs + pc.si);
     pc.first = sg->first_wtile;
     pc.end = pc.first + sg->num_wtiles;
-    pc.gt = gp(q->gd_plans)[(int64_t)pc.si * 128 + lane];
-    pc.rp = gp(q->gd_plans)[(int64_t)pc.si * 128 + 64 + lane];
+    pc.gt = gp(q->gd_plans)[(int64_t)pc.si * kGdPlanDw + lane];
+    pc.rp = gp(q->gd_plans)[(int64_t)pc.si * kGdPlanDw + 64 + lane];
   }
   rs_store<DM>(pc.rp, img, lane, cur);
   // (a wave-uniform segment pointer: its descriptor fields are scalar loads, which do not wait for the ring's loads)
@@ -765,11 +1224,11 @@ __global__ void __launch_bounds__(WPW * kWave, 1) gdense_rs_kernel(const DevQuer
     int64_t ti = t0 + wave;
     int isi = find_segment(segs, nseg, t0);
     int64_t ifirst = segs[isi].first_wtile, iend = ifirst + segs[isi].num_wtiles;
-    uint32_t rpi = gp(q->gd_plans)[(int64_t)isi * 128 + 64 + lane];
+    uint32_t rpi = gp(q->gd_plans)[(int64_t)isi * kGdPlanDw + 64 + lane];
     int64_t t = ti;
     int psi = isi;
     int64_t pfirst = ifirst, pend = iend;
-    uint32_t gt = gp(q->gd_plans)[(int64_t)psi * 128 + lane], rpp = rpi;
+    uint32_t gt = gp(q->gd_plans)[(int64_t)psi * kGdPlanDw + lane], rpp = rpi;
     RsRing<RS, DM> ring;
     RsCursor ic{ti, isi, ifirst, iend, rpi};
     RsProc pc{t, psi, pfirst, pend, gt, rpp};

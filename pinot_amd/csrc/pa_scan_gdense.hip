@@ -13,6 +13,8 @@ const void* scan_fn_gdense(int strategy, int lm) {
     return (const void*)gdense_rs_kernel<3 * kGdWaves, gd_rs_ring(STRAT_GDENSE_RS12), gd_rs_dmax(STRAT_GDENSE_RS12)>;
   if (strategy == STRAT_GDENSE_RS8 && !lm)
     return (const void*)gdense_rs_kernel<2 * kGdWaves, gd_rs_ring(STRAT_GDENSE_RS8), gd_rs_dmax(STRAT_GDENSE_RS8)>;
+  if (strategy == STRAT_GDENSE_LM8 && !lm) return (const void*)gdense_kernel<2 * kGdWaves, 2>;
+  if (strategy == STRAT_GDENSE_LM16 && !lm) return (const void*)gdense_kernel<4 * kGdWaves, 2>;
   return nullptr;
 }
 

@@ -501,10 +501,14 @@ class GpuQueryExecutor:
         L.check(L.lib().pa_query_plan(self.handle, *[ctypes.byref(v) for v in vals]), "plan")
         names = ("strategy", "steps", "dma_slots", "ring", "wg_per_cu", "grid", "lds_bytes")
         out["plan"] = {n: v.value for n, v in zip(names, vals)}
+        code = out["plan"]["strategy"]
         out["plan"]["strategy"] = {0: "lds", 1: "global", 2: "partitioned", 4: "lane", 5: "lane", 6: "lane", 7: "lane",
-                                    8: "lds_dense", 9: "lds_dense", 10: "lds_dense", 11: "lds_dense", 12: "lds_dense"}[out["plan"]["strategy"]]
+                                    8: "lds_dense", 9: "lds_dense", 10: "lds_dense", 11: "lds_dense", 12: "lds_dense",
+                                    14: "lds_dense", 15: "lds_dense"}[code]
+        out["plan"]["variant"] = STRATEGY_VARIANTS.get(code, str(code))
         out["plan"]["eager_literals"] = int(L.lib().pa_query_num_eager_literals(self.handle))
         out["plan"]["lane_major"] = int(L.lib().pa_query_lane_major(self.handle))
+        out["plan"]["dense_packed"] = int(L.lib().pa_query_dense_packed(self.handle))
         out["plan"]["limit_trimming"] = int(L.lib().pa_query_limit_trimming(self.handle))
         return out
 
@@ -710,6 +714,12 @@ class GpuQueryExecutor:
             self.close()
         except Exception:
             pass
+
+
+# the kernel variant behind each pa_query_plan strategy code (pa_device.h Strategy)
+STRATEGY_VARIANTS = {0: "lds", 1: "global", 2: "partitioned", 4: "lane", 5: "lane_cnt", 6: "lane_raw", 7: "lane_dict",
+                     8: "gdense4", 9: "gdense8", 10: "gdense12", 11: "gdense_rs12", 12: "gdense_rs8", 14: "gdense_lm8",
+                     15: "gdense_lm16"}
 
 
 def _has_comparison(f):

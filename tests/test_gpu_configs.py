@@ -146,6 +146,39 @@ def test_configs1_wide_in_list(adanalytics):
     assert len(got.groups) == 8 and got.num_docs_scanned > 1000
 
 
+@pytest.fixture(scope="module")
+def adanalytics3():
+    """Three bench.py segments (2M docs each) sharing their dictionaries, as the bench's 100 segments do."""
+    segs = [BENCH.make_segment(2000 + i, 2_000_000) for i in range(3)]
+    gs = [GpuSegment(s) for s in segs]
+    yield segs, gs
+    for g in gs:
+        g.close()
+
+
+# the dense GROUP BY kernel variant the bench's secondary lines run (pa_query_plan; engine.STRATEGY_VARIANTS)
+BENCH_SECONDARY_VARIANT = "gdense_lm8"
+
+
+@pytest.mark.parametrize("n_ids,frac", [(17476, 0.1), (87381, 0.5)])
+def test_configs1_secondary_lines(adanalytics3, n_ids, frac):
+    """bench.py's secondary lines at their plan: the accountId IN list widened to 10 % / 50 % of the docs (a 2^17-bit
+    bitmap held in LDS), the 384-day key box, two dictionary SUMs over segments that share dictionaries."""
+    segs, gs = adanalytics3
+    q = parse_sql(BENCH.secondary_query(n_ids))
+    ex = GpuQueryExecutor(q, gs)
+    try:
+        p = _plan(ex)
+        assert p["strategy"] == "lds_dense" and p["variant"] == BENCH_SECONDARY_VARIANT, p
+        got = ex.run()
+    finally:
+        ex.close()
+    exp = oracle.run_query(q, segs)
+    assert_same(got, exp)
+    assert len(got.groups) == 384
+    assert got.num_docs_scanned / sum(s.num_docs for s in segs) == pytest.approx(frac, abs=0.01)
+
+
 # ------------------------------------------------------------------ configs[2]
 @pytest.fixture(scope="module")
 def highcard():

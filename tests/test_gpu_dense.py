@@ -169,3 +169,45 @@ def test_dense_box_filter(own_dicts, shared_dict, dicts, flags):
         q = parse_sql(sql)
         got = _run(q, gs, flags=flags, expect_dense=None)
         assert_same(got, oracle.run_query(q, segs), DOUBLE_REL)
+
+
+PACKABLE = (
+    # COUNT + two SUMs whose terms fit one word: dl's values as offsets from their minimum (negative values), da's
+    # dictIds (affine shared dictionary) or offsets (own dictionaries)
+    "SELECT g, COUNT(*), SUM(dl), SUM(da) FROM t WHERE day < 1200 GROUP BY g LIMIT 1000",
+    "SELECT h, w, SUM(dl) FROM t WHERE w BETWEEN 10 AND 25 AND day >= 100 GROUP BY h, w",
+    "SELECT g, COUNT(*) FROM t WHERE day < 2000 GROUP BY g LIMIT 1000",
+    "SELECT day, SUM(da) FROM t WHERE day BETWEEN 1500 AND 2500 GROUP BY day LIMIT 2000",
+)
+NOT_PACKABLE = (
+    "SELECT g, SUM(dw), SUM(da) FROM t WHERE day < 1200 GROUP BY g LIMIT 1000",   # dw spans 2^41: no field fits
+    "SELECT g, COUNT(*), MIN(dl), SUM(rs) FROM t WHERE day < 3000 GROUP BY g LIMIT 1000",
+)
+
+
+@pytest.mark.parametrize("flags", [0, L.PA_QF_GD_DRAIN_EACH_TILE, L.PA_QF_NO_GD_PACK, L.PA_QF_NO_GDENSE_LM])
+@pytest.mark.parametrize("dicts", ["own", "shared"])
+def test_dense_lane_major_walk(own_dicts, shared_dict, dicts, flags):
+    """The lane-major walk (STRAT_GDENSE_LM*: each lane unpacks its 16 docs of every column) with packed accumulation
+    (one word per matching doc: COUNT + SUM terms, drained per wave; drained after every tile to exercise the drain),
+    with one atomic per aggregation, and the step-major kernels (PA_QF_NO_GDENSE_LM): identical to the oracle."""
+    segs, gs = own_dicts if dicts == "own" else shared_dict
+    lm = not (flags & L.PA_QF_NO_GDENSE_LM)
+    packed_runs = 0
+    for sql, packable in [(x, True) for x in PACKABLE] + [(x, False) for x in NOT_PACKABLE]:
+        q = parse_sql(sql)
+        ex = GpuQueryExecutor(q, gs, flags=flags)
+        try:
+            st = ex.stats()["plan"]
+            assert st["strategy"] == "lds_dense", (sql, st)
+            assert st["variant"].startswith("gdense_lm") == lm, (sql, st)
+            # (a packable query runs unpacked when the waves' packed rows do not fit LDS beside its tables)
+            if not (lm and packable and not (flags & L.PA_QF_NO_GD_PACK)):
+                assert st["dense_packed"] == 0, (sql, st)
+            packed_runs += st["dense_packed"]
+            got = ex.run()
+        finally:
+            ex.close()
+        assert_same(got, oracle.run_query(q, segs), DOUBLE_REL)
+    if lm and not (flags & L.PA_QF_NO_GD_PACK):
+        assert packed_runs >= 2

@@ -68,7 +68,7 @@ __device__ __forceinline__ void unpack(uint32_t region, int lane, uint32_t (&v)[
   }
 }
 
-template <int TD, int W, int MODE>
+template <int TD, int W, int MODE, int ORDER = 0>
 __global__ void __launch_bounds__(W * 64, 1) proto(const uint32_t* c0, const uint32_t* c1, const uint32_t* c2,
                                                    const uint32_t* c3, int64_t ntiles, uint32_t lo_t, uint32_t hi_t,
                                                    uint32_t* out) {
@@ -87,9 +87,18 @@ __global__ void __launch_bounds__(W * 64, 1) proto(const uint32_t* c0, const uin
   for (int i = tid; i < 3 * NK; i += W * 64) accw[i] = 0;
   __syncthreads();
   const uint32_t accb = lds_addr(accw), lutb = lds_addr(lut);
+  // ORDER 0: each wave its own contiguous range; 1: the workgroup's range, waves interleaved (t0 + wave + W k);
+  // 2: as 1 with XCD-major workgroup ranges
   const int64_t WT = (int64_t)gridDim.x * W;
   const int64_t gw = (int64_t)blockIdx.x * W + wave;
-  const int64_t t0 = gw * ntiles / WT, t1 = (gw + 1) * ntiles / WT;
+  int64_t t0 = gw * ntiles / WT, t1 = (gw + 1) * ntiles / WT, tstep = 1;
+  if (ORDER) {
+    const int64_t G = gridDim.x, b = blockIdx.x;
+    const int64_t lb = ORDER == 2 ? (b % 8) * (G / 8) + b / 8 : b;
+    t0 = lb * ntiles / G + wave;
+    t1 = (lb + 1) * ntiles / G;
+    tstep = W;
+  }
   const uint32_t* cols[4] = {c0, c1, c2, c3};
   uint32_t acc = 0, matched = 0;
   int64_t ti = t0;
@@ -108,12 +117,13 @@ __global__ void __launch_bounds__(W * 64, 1) proto(const uint32_t* c0, const uin
     }
     islot = islot + 1 == R ? 0 : islot + 1;
   };
-  if (ti < t1) issue(ti++);
+  if (ti < t1) { issue(ti); ti += tstep; }
   int pslot = 0;
-  for (int64_t t = t0; t < t1; ++t) {
+  for (int64_t t = t0; t < t1; t += tstep) {
     if (ti < t1) {
       vm_wait<0>();
-      issue(ti++);
+      issue(ti);
+      ti += tstep;
     } else {
       vm_wait<0>();
     }
@@ -187,12 +197,12 @@ __global__ void __launch_bounds__(W * 64, 1) proto(const uint32_t* c0, const uin
   if (lane == 0) atomicAdd(out + 1, matched);
 }
 
-template <int TD, int W, int MODE>
+template <int TD, int W, int MODE, int ORDER = 0>
 void run(uint32_t* const* cols, int64_t docs, uint32_t lo_t, uint32_t hi_t, uint32_t* out, int ncu) {
   constexpr int IMG = img_dw<TD>();
   const size_t lds = 4u * (4096 + 2 * 3 * 384 + (size_t)W * 2 * IMG);
   const int64_t ntiles = docs / (64 * TD);
-  auto k = proto<TD, W, MODE>;
+  auto k = proto<TD, W, MODE, ORDER>;
   CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
@@ -211,7 +221,7 @@ void run(uint32_t* const* cols, int64_t docs, uint32_t lo_t, uint32_t hi_t, uint
   uint32_t h[2];
   CHECK(hipMemcpy(h, out, 8, hipMemcpyDeviceToHost));
   const double bytes = (double)docs * 50 / 8;
-  printf("TD %2d W %d mode %d: %.3f ms  %.2f TB/s  frac %.3f  matched/launch %.3f  lds %zu\n", TD, W, MODE, ms,
+  printf("TD %2d W %d mode %d order %d: %.3f ms  %.2f TB/s  frac %.3f  matched/launch %.3f  lds %zu\n", TD, W, MODE, ORDER, ms,
          bytes / (ms * 1e-3) / 1e12, bytes / (ms * 1e-3) / 8e12, h[1] / (double)reps / docs, lds);
   fflush(stdout);
 }
@@ -238,17 +248,14 @@ int main(int argc, char** argv) {
   // day range: ids [64, 448) of 512, MSB-aligned compare (v - lo) <= hi - lo
   const uint32_t lo_t = 64u << (32 - NB0), hi_t = (447u << (32 - NB0)) - lo_t + ((1u << (32 - NB0)) - 1u);
   printf("ncu %d docs %lld\n", ncu, (long long)docs);
-  run<32, 4, 0>(cols, docs, lo_t, hi_t, out, ncu);
-  run<32, 4, 1>(cols, docs, lo_t, hi_t, out, ncu);
-  run<32, 4, 2>(cols, docs, lo_t, hi_t, out, ncu);
-  run<32, 4, 5>(cols, docs, lo_t, hi_t, out, ncu);
-  run<32, 4, 3>(cols, docs, lo_t, hi_t, out, ncu);
-  run<32, 4, 4>(cols, docs, lo_t, hi_t, out, ncu);
   run<16, 8, 0>(cols, docs, lo_t, hi_t, out, ncu);
-  run<16, 8, 1>(cols, docs, lo_t, hi_t, out, ncu);
   run<16, 8, 2>(cols, docs, lo_t, hi_t, out, ncu);
-  run<16, 8, 5>(cols, docs, lo_t, hi_t, out, ncu);
-  run<16, 8, 3>(cols, docs, lo_t, hi_t, out, ncu);
   run<16, 8, 4>(cols, docs, lo_t, hi_t, out, ncu);
+  run<16, 8, 0, 1>(cols, docs, lo_t, hi_t, out, ncu);
+  run<16, 8, 2, 1>(cols, docs, lo_t, hi_t, out, ncu);
+  run<16, 8, 4, 1>(cols, docs, lo_t, hi_t, out, ncu);
+  run<16, 8, 0, 2>(cols, docs, lo_t, hi_t, out, ncu);
+  run<16, 8, 2, 2>(cols, docs, lo_t, hi_t, out, ncu);
+  run<16, 8, 4, 2>(cols, docs, lo_t, hi_t, out, ncu);
   return 0;
 }
