@@ -194,6 +194,7 @@ typedef struct {
 #define PA_QF_WG_SHIFT 12             /* bits 12..14: workgroups per CU (1..4) */
 #define PA_QF_NO_GDENSE_LM (1 << 15)      /* dense GROUP BY kernel: the step-major walk (ds_read2 per doc and column) instead
                                              of the lane-major one (each lane unpacks its 16 docs of every column) */
+#define PA_QF_NO_JIT (1u << 31)          /* never the query-shape specialised dense kernel (gdl_jit.hip); also PA_NO_JIT=1 */
 #define PA_QF_GD_DRAIN_EACH_TILE (1 << 2) /* testing: packed dense accumulation drains each wave's rows after every tile */
 #define PA_QF_NO_GD_PACK (1 << 3)         /* dense GROUP BY, lane-major walk: one LDS atomic per aggregation and matching doc
                                              instead of one packed word (COUNT + SUM terms) per matching doc */
@@ -396,7 +397,8 @@ int32_t pa_query_num_eager_literals(const pa_query* q);
 /* 1 if the lane-major scan kernel was chosen (lane l owns docs [32l, 32l+32) of a tile), 0 step-major, <0 error. */
 int32_t pa_query_lane_major(const pa_query* q);
 /* 1 if the dense GROUP BY kernel accumulates packed words (COUNT + every SUM term in one 64-bit LDS atomic per matching
- * doc, drained per wave into the workgroup's accumulators), 0 if not, <0 error. */
+ * doc, drained per wave into the workgroup's accumulators), 2 if it does so in the kernel specialised to the query's
+ * shape (compiled by hiprtc at prepare), 0 if not, <0 error. */
 int32_t pa_query_dense_packed(const pa_query* q);
 int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t* dma_slots, int32_t* ring,
                   int32_t* wg_per_cu, int32_t* grid, int32_t* lds_bytes);

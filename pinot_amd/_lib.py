@@ -31,6 +31,7 @@ PA_QF_NO_REG_STAGE = 1 << 18
 PA_QF_NO_GDENSE_LM = 1 << 15
 PA_QF_NO_GD_PACK = 1 << 3
 PA_QF_GD_DRAIN_EACH_TILE = 1 << 2
+PA_QF_NO_JIT = -(1 << 31)  # bit 31 of the int32 flags word
 PA_QF_NO_BOX_FILTER = 1 << 19
 PA_QF_BOX_FILTER = 1 << 20
 PA_QF_NO_PARTITION = 1 << 21

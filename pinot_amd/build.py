@@ -17,13 +17,25 @@ def _stale():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [__file__]
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS + ["gdl_jit.hip"]] + [__file__]
     return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _jit_source():
+    """gdl_jit.hip as a C++ raw string literal (pa_capi.hip compiles it at query prepare with hiprtc)."""
+    src = open(os.path.join(CSRC, "gdl_jit.hip")).read()
+    assert ")JITSRC" not in src
+    out = os.path.join(CSRC, "gdl_jit_src.inc")
+    text = 'R"JITSRC(' + src + ')JITSRC"\n'
+    if not os.path.exists(out) or open(out).read() != text:
+        with open(out, "w") as f:
+            f.write(text)
 
 
 def build(force=False, verbose=False):
     if not force and not _stale():
         return LIB
+    _jit_source()
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     # one object per source, compiled in parallel (each translation unit holds its own kernels), then one link
     objs, procs = [], []
@@ -36,7 +48,7 @@ def build(force=False, verbose=False):
         objs.append(obj)
     if any(p.wait() != 0 for p in procs):
         raise RuntimeError("hipcc failed")
-    cmd = [hipcc] + FLAGS + objs + ["-o", LIB + ".tmp"]
+    cmd = [hipcc] + FLAGS + objs + ["-lhiprtc", "-o", LIB + ".tmp"]
     subprocess.run(cmd, check=True)
     for o in objs:
         os.remove(o)

@@ -1,0 +1,416 @@
+// The lane-major dense filter + GROUP BY kernel specialised to one query shape (STRAT_GDENSE_LM8 with packed
+// accumulation), compiled at pa_query_prepare by hiprtc with the shape as macros (pa_capi.hip jit_*). Same algorithm
+// as pa_gdense.h gdl_tile + gdl_packed_accumulate + gdl_drain + gd_flush, with every column width, image offset,
+// leaf kind, field offset and loop bound a compile-time constant: no switch on bit widths, no parameter reads in the
+// tile loop, the DMA of a tile is straight-line scalar code. Self-contained (hiprtc's built-in HIP headers only).
+//
+// Reference semantics: GroupByOperator -> DefaultGroupByExecutor.process (DefaultGroupByExecutor.java:131-158),
+// DictionaryBasedGroupKeyGenerator (one group-by column, :254-340), SumAggregationFunction.aggregateGroupBySV (:207)
+// and CountAggregationFunction, ScanBasedFilterOperator over dictId ranges / dictId sets (SVScanDocIdIterator.java:203).
+//
+// Shape macros (all integers; lists as {a, b, ...}):
+//   JIT_W  waves per workgroup         JIT_IMG  dwords of one tile image      JIT_NC  staged columns
+//   JIT_NB {bits per column}           JIT_OFF  {byte offset of each column's region in the image}
+//   JIT_NL eager leaves, JIT_LK {0 = DICT_RANGE, 1 = DICT_SET}, JIT_LC {column}, JIT_LN {negate},
+//          JIT_LE {closes a CNF clause}, JIT_LUT {LDS byte offset of the DICT_SET bitmap}
+//   JIT_KC the group-by column, JIT_KL the leaf whose unpack it reuses (-1: none), JIT_KIB the filter implies the box
+//   JIT_NA SUM aggregations, JIT_AC {column}, JIT_AT {LDS byte offset of a GVS_T32U table, -1: the dictId itself},
+//          JIT_AS {bit offset of the field}, JIT_OC bit offset of the COUNT field
+//   JIT_DRAIN tiles between drains of a wave's packed rows
+//   JIT_L_SUM {LDS byte offset of each SUM's accumulators}, JIT_L_ROWS, JIT_L_RING (LDS byte offsets)
+typedef unsigned int u32;
+typedef unsigned long long u64;
+typedef long long i64;
+typedef __attribute__((address_space(3))) u32 l32;
+typedef __attribute__((address_space(3))) u64 l64;
+
+constexpr int W = JIT_W, NC = JIT_NC, NL = JIT_NL, NA = JIT_NA, ND = 16, IMG = JIT_IMG;
+constexpr int NLA = NL > 0 ? NL : 1, NAA = NA > 0 ? NA : 1;
+constexpr int kNB[NC] = JIT_NB;
+constexpr int kOFF[NC] = JIT_OFF;
+constexpr int kLK[NLA] = JIT_LK;
+constexpr int kLC[NLA] = JIT_LC;
+constexpr int kLN[NLA] = JIT_LN;
+constexpr int kLE[NLA] = JIT_LE;
+constexpr int kLUT[NLA] = JIT_LUT;
+constexpr int kAC[NAA] = JIT_AC;
+constexpr int kAT[NAA] = JIT_AT;
+constexpr int kAS[NAA] = JIT_AS;
+constexpr int kLSUM[NAA] = JIT_L_SUM;
+
+// (fixed-size arrays: the host (pa_capi.hip JitSegH / JitArgsH) writes the same layout for every shape)
+constexpr int kJitMax = 6;
+static_assert(NC <= kJitMax && NL <= kJitMax && NA <= kJitMax, "shape beyond the JIT descriptors");
+struct JitSeg {          // one bound segment (read with scalar loads at segment switches only)
+  u64 src[kJitMax];      // column streams, past the guard words
+  i64 first_tile;        // first 1024-doc tile in the query's tile space
+  int num_docs, num_tiles;
+  u32 lo_t[kJitMax], hi_t[kJitMax];  // DICT_RANGE leaves: MSB-aligned bounds in this segment's dictId space
+};
+struct JitArgs {
+  i64 total_tiles;
+  int nseg, nkeys, key_lo, key_span, xcd_major, pad;
+  i64 key_stride;                 // table-wide key of LDS key k: (k + key_lo) * key_stride
+  unsigned long long* matched;    // [0] numDocsScanned, [3] matches outside the key box (planner error)
+  unsigned long long* count;      // table-wide COUNT accumulators
+  i64* sum[kJitMax];              // table-wide SUM accumulators (int64, or lo/hi pairs: sum_long)
+  int sum_long[kJitMax];
+  i64 base[kJitMax], step[kJitMax];  // value = base + step * term
+  const u32* lut[kJitMax];        // shared DICT_SET bitmaps
+  int lut_words[kJitMax];
+  const i64* tab[kJitMax];        // GVS_T32U: the shared dictionary (values - base go to LDS)
+  int tab_n[kJitMax];
+};
+typedef const __attribute__((address_space(4))) JitArgs CA;
+typedef const __attribute__((address_space(4))) JitSeg CS;
+
+__device__ __forceinline__ u32 lds_addr(const void* p) { return (u32)(unsigned long)(const l32*)p; }
+template <class T>
+__device__ __forceinline__ T* at(u32 a) { return (T*)(unsigned long)a; }
+
+template <int N>
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// LDS-DMA with a scalar base: lane l copies 16 bytes at sbase + voff to dst + 16 l (mask: the taking-part lanes)
+__device__ __forceinline__ void dma16(u32 voff, u64 sbase, u32 dst) {
+  u32 keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(dst));
+}
+__device__ __forceinline__ void dma16m(u32 voff, u64 sbase, u32 dst, u64 mask) {
+  u32 keep;
+  u64 save;
+  asm volatile(
+      "s_mov_b64 %1, exec\n\ts_mov_b64 exec, %5\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
+      : "=&s"(keep), "=&s"(save) : "v"(voff), "s"(sbase), "s"(dst), "s"(mask));
+}
+
+template <int C>
+__device__ __forceinline__ void dma_cols(CS* sg, i64 wt, u32 img, u32 voff) {
+  if constexpr (C < NC) {
+    constexpr int CH = 8 * kNB[C];  // 16-byte chunks of a 1024-doc tile
+    const u64 src = sg->src[C] + (u64)wt * (u64)(128 * kNB[C]);
+    const u32 dst = img + (u32)kOFF[C];
+#pragma unroll
+    for (int k = 0; k < CH / 64; ++k) dma16(voff, src + 1024u * k, dst + 1024u * k);
+    if constexpr (CH % 64) dma16m(voff, src + 1024u * (CH / 64), dst + 1024u * (CH / 64), (1ull << (CH % 64)) - 1ull);
+    dma_cols<C + 1>(sg, wt, img, voff);
+  }
+}
+
+// The lane's 16 values of column C (MSB-aligned: value i in the top NB bits of v[i])
+template <int C>
+__device__ __forceinline__ void top(u32 img, int lane, u32 (&v)[ND]) {
+  constexpr int NB = kNB[C];
+  constexpr int K = (ND * NB + 31) / 32 + 1;
+  const u32 region = img + (u32)kOFF[C];
+  const u32 bit0 = (u32)lane * (u32)(ND * NB);
+  u32 w[K];
+  if constexpr ((ND * NB) % 32 != 0) {  // odd NB: odd lanes start 16 bits into a word
+    const u32 sh = bit0 & 16u;
+    const l32* p = at<const l32>(region + 4u * ((bit0 >> 5) - 1u + (sh >> 4)));
+    u32 r[K + 1];
+#pragma unroll
+    for (int j = 0; j <= K; ++j) r[j] = p[j];
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = __builtin_amdgcn_alignbit(r[j], r[j + 1], sh);
+  } else {
+    const l32* p = at<const l32>(region + 4u * (bit0 >> 5));
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = p[j];
+  }
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+    const int s = i * NB, j = s >> 5, o = s & 31;
+    v[i] = (o + NB <= 32) ? (w[j] << o) : __builtin_amdgcn_alignbit(w[j], w[j + 1], 32 - o);
+  }
+}
+
+// dictIds of column C (one v_bfe per id, two ops when it straddles words)
+template <int C>
+__device__ __forceinline__ void ids(u32 img, int lane, u32 (&v)[ND]) {
+  constexpr int NB = kNB[C];
+  constexpr int K = (ND * NB + 31) / 32 + 1;
+  const u32 region = img + (u32)kOFF[C];
+  const u32 bit0 = (u32)lane * (u32)(ND * NB);
+  u32 w[K];
+  if constexpr ((ND * NB) % 32 != 0) {
+    const u32 sh = bit0 & 16u;
+    const l32* p = at<const l32>(region + 4u * ((bit0 >> 5) - 1u + (sh >> 4)));
+    u32 r[K + 1];
+#pragma unroll
+    for (int j = 0; j <= K; ++j) r[j] = p[j];
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = __builtin_amdgcn_alignbit(r[j], r[j + 1], sh);
+  } else {
+    const l32* p = at<const l32>(region + 4u * (bit0 >> 5));
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = p[j];
+  }
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+    const int s = i * NB, j = s >> 5, o = s & 31;
+    if (o + NB <= 32) v[i] = __builtin_amdgcn_ubfe(w[j], 32 - o - NB, NB);
+    else v[i] = __builtin_amdgcn_alignbit(w[j], w[j + 1], 32 - o) >> (32 - NB);
+  }
+}
+
+// MSB-aligned range test of 16 values: non-matches as borrow bits (lo <= v < lo + span <=> t - lo' <= hi')
+__device__ __forceinline__ u32 range_nm(const u32 (&t)[ND], u32 lo_t, u32 hi_t) {
+  u32 nm = 0;
+#pragma unroll
+  for (int i = ND - 1; i >= 0; --i) {
+    u32 u;
+    asm("v_sub_u32_e64 %[u], %[t], %[lo]\n\tv_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
+        "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
+        : [nm] "+v"(nm), [u] "=&v"(u) : [t] "v"(t[i]), [lo] "s"(lo_t), [hi] "s"(hi_t) : "vcc");
+  }
+  return nm;
+}
+
+// eager leaves L.. in order (CNF clauses closed by kLE); false when no doc of the wave's tile can match any more
+template <int L>
+__device__ __forceinline__ bool leaves(CS* sg, u32 img, int lane, u32 base, u32& m, u32& clause, u32 (&kt)[ND]) {
+  if constexpr (L < NL) {
+    u32 t[ND];
+    top<kLC[L]>(img, lane, t);
+    if constexpr (L == JIT_KL) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) kt[i] = t[i];
+    }
+    u32 bits;
+    if constexpr (kLK[L] == 0) {
+      bits = ~range_nm(t, sg->lo_t[L], sg->hi_t[L]) & 0xffffu;
+    } else {
+      constexpr int NB = kNB[kLC[L]];
+      u32 id[ND], w[ND];
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        id[i] = t[i] >> (32 - NB);
+        w[i] = *at<const l32>(base + (u32)kLUT[L] + 4u * (id[i] >> 5));
+      }
+      bits = 0;
+#pragma unroll
+      for (int i = 0; i < ND; ++i) bits |= __builtin_amdgcn_ubfe(w[i], id[i], 1) << i;
+    }
+    if constexpr (kLN[L]) bits = ~bits & 0xffffu;
+    clause |= bits;
+    if constexpr (kLE[L] != 0) {
+      m &= clause;
+      clause = 0;
+      if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return false;
+    }
+    return leaves<L + 1>(sg, img, lane, base, m, clause, kt);
+  }
+  return true;
+}
+
+// packed words of the lane's docs: COUNT + the SUM terms, ORed into their fields 32 bits at a time
+template <int A>
+__device__ __forceinline__ void terms(u32 img, int lane, u32 base, u32 (&plo)[ND], u32 (&phi)[ND]) {
+  if constexpr (A < NA) {
+    u32 id[ND];
+    ids<kAC[A]>(img, lane, id);
+    if constexpr (kAT[A] >= 0) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) id[i] = *at<const l32>(base + (u32)kAT[A] + 4u * id[i]);
+    }
+    constexpr int SH = kAS[A];
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      if constexpr (SH >= 32) {
+        phi[i] |= id[i] << (SH - 32);
+      } else if constexpr (SH == 0) {
+        plo[i] |= id[i];
+      } else {
+        plo[i] |= id[i] << SH;
+        phi[i] |= id[i] >> (32 - SH);
+      }
+    }
+    terms<A + 1>(img, lane, base, plo, phi);
+  }
+}
+
+// one 1024-doc tile: returns the lane's docs counted in numDocsScanned
+__device__ __forceinline__ u32 tile(CA* A, CS* sg, i64 wt, u32 img, int lane, u32 base, u32 rows, u32& errs) {
+  const i64 rem = (i64)sg->num_docs - wt * 1024;
+  u32 m = 0xffffu;
+  if (rem < 1024) {
+    const i64 n = rem - ND * lane;
+    m = n >= ND ? 0xffffu : (n <= 0 ? 0u : ((1u << n) - 1u));
+  }
+  u32 clause = 0, kt[ND];
+  if (!leaves<0>(sg, img, lane, base, m, clause, kt)) return 0;
+  if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return 0;
+  constexpr int NBK = kNB[JIT_KC];
+  u32 id[ND];
+  if constexpr (JIT_KL >= 0) {
+#pragma unroll
+    for (int i = 0; i < ND; ++i) id[i] = kt[i] >> (32 - NBK);
+  } else {
+    ids<JIT_KC>(img, lane, id);
+  }
+  const u32 klo = (u32)A->key_lo;
+  u32 on = m;
+  if constexpr (!JIT_KIB) {
+    u32 nm = 0;
+#pragma unroll
+    for (int i = ND - 1; i >= 0; --i) {
+      u32 u;
+      asm("v_sub_u32_e64 %[u], %[t], %[lo]\n\tv_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
+          "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
+          : [nm] "+v"(nm), [u] "=&v"(u) : [t] "v"(id[i]), [lo] "s"(klo), [hi] "s"((u32)A->key_span - 1u) : "vcc");
+    }
+    on &= ~nm;
+    errs += (u32)__builtin_popcount(m & ~on);
+  }
+  const u32 abase = rows - 8u * klo;
+  u32 plo[ND], phi[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+    plo[i] = JIT_OC < 32 ? (1u << (JIT_OC & 31)) : 0u;
+    phi[i] = JIT_OC < 32 ? 0u : (1u << ((JIT_OC - 32) & 31));
+  }
+  terms<0>(img, lane, base, plo, phi);
+#pragma unroll
+  for (int i = 0; i < ND; ++i)
+    if ((on >> i) & 1u)
+      __hip_atomic_fetch_add(at<l64>(abase + (id[i] << 3)), ((u64)phi[i] << 32) | plo[i], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+  return (u32)__builtin_popcount(m);
+}
+
+// a wave's packed rows -> the workgroup's COUNT / SUM accumulators (row zeroed)
+__device__ __forceinline__ void drain(u32 rows, int nkeys, int lane, u32 base) {
+  l64* row = at<l64>(rows);
+  for (int k = lane; k < nkeys; k += 64) {
+    const u64 x = row[k];
+    if (x == 0) continue;
+    row[k] = 0;
+    __hip_atomic_fetch_add(at<l32>(base) + k, (u32)(x >> JIT_OC), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      const int lo = kAS[a], hi = a + 1 < NA ? kAS[a + 1 < NA ? a + 1 : a] : JIT_OC;
+      const u64 f = (x >> lo) & ((hi - lo) >= 64 ? ~0ull : ((1ull << (hi - lo)) - 1ull));
+      __hip_atomic_fetch_add(at<l64>(base + (u32)kLSUM[a]) + k, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+}
+
+__device__ __forceinline__ int find_segment(CS* segs, int nseg, i64 t) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (segs[mid].first_tile <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a_in, const JitSeg* s_in) {
+  CA* A = (CA*)(unsigned long)a_in;
+  CS* S = (CS*)(unsigned long)s_in;
+  extern __shared__ __attribute__((aligned(16))) u32 smem[];
+  const u32 base = lds_addr(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nkeys = A->nkeys;
+  // LDS: counts, sums, bitmaps, tables, the waves' packed rows, the ring
+  for (int i = tid; i < nkeys; i += W * 64) smem[i] = 0u;
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+    for (int i = tid; i < nkeys; i += W * 64) at<l64>(base + (u32)kLSUM[a])[i] = 0ull;
+  for (int i = tid; i < W * nkeys; i += W * 64) at<l64>(base + (u32)JIT_L_ROWS)[i] = 0ull;
+#pragma unroll
+  for (int l = 0; l < NL; ++l)
+    if (kLK[l] == 1)
+      for (int i = tid; i < A->lut_words[l]; i += W * 64)
+        at<l32>(base + (u32)kLUT[l])[i] = ((const __attribute__((address_space(1))) u32*)A->lut[l])[i];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+    if (kAT[a] >= 0)
+      for (int i = tid; i < A->tab_n[a]; i += W * 64)
+        at<l32>(base + (u32)kAT[a])[i] =
+            (u32)(((const __attribute__((address_space(1))) i64*)A->tab[a])[i] - A->base[a]);
+  __syncthreads();
+  const i64 T = A->total_tiles, G = gridDim.x;
+  const i64 b = blockIdx.x;
+  const i64 lb = A->xcd_major ? (b % 8) * (G / 8) + (b % 8 < G % 8 ? b % 8 : G % 8) + b / 8 : b;
+  const i64 t0 = lb * T / G, t1 = (lb + 1) * T / G;
+  const u32 rows = base + (u32)JIT_L_ROWS + (u32)wave * (u32)nkeys * 8u;
+  const u32 ring = base + (u32)JIT_L_RING + (u32)wave * 2u * (u32)IMG * 4u;
+  const u32 voff = 16u * (u32)lane;
+  u32 matched = 0, errs = 0;
+  if (t0 < t1) {
+    const int nseg = A->nseg;
+    int isi = find_segment(S, nseg, t0 + wave);
+    int psi = isi;
+    i64 ifirst = S[isi].first_tile, iend = ifirst + S[isi].num_tiles;
+    i64 pfirst = ifirst, pend = iend;
+    i64 ti = t0 + wave;
+    if (ti < t1) {
+      while (ti >= iend) {
+        ++isi;
+        ifirst = S[isi].first_tile;
+        iend = ifirst + S[isi].num_tiles;
+      }
+      dma_cols<0>(S + isi, ti - ifirst, ring, voff);
+    }
+    ti += W;
+    int slot = 0, since = 0;
+    for (i64 t = t0 + wave; t < t1; t += W) {
+      vm_wait<0>();  // tile t has landed (two images: it was the one in flight)
+      if (ti < t1) {
+        while (ti >= iend) {
+          ++isi;
+          ifirst = S[isi].first_tile;
+          iend = ifirst + S[isi].num_tiles;
+        }
+        dma_cols<0>(S + isi, ti - ifirst, ring + (u32)(slot ^ 1) * (u32)IMG * 4u, voff);
+      }
+      ti += W;
+      while (t >= pend) {
+        ++psi;
+        pfirst = S[psi].first_tile;
+        pend = pfirst + S[psi].num_tiles;
+      }
+      matched += tile(A, S + psi, t - pfirst, ring + (u32)slot * (u32)IMG * 4u, lane, base, rows, errs);
+      if (++since == JIT_DRAIN) {
+        drain(rows, nkeys, lane, base);
+        since = 0;
+      }
+      slot ^= 1;
+    }
+  }
+  vm_wait<0>();
+  drain(rows, nkeys, lane, base);
+  u64 wm = matched, we = errs;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    wm += __shfl_xor(wm, o);
+    we += __shfl_xor(we, o);
+  }
+  if (lane == 0 && wm) __hip_atomic_fetch_add(A->matched, wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0 && we) __hip_atomic_fetch_add(A->matched + 3, we, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  // flush: one global update per non-empty key and aggregation (gd_flush for one group-by column)
+  for (int kl = tid; kl < nkeys; kl += W * 64) {
+    const u64 c = smem[kl];
+    if (c == 0) continue;
+    const i64 key = ((i64)kl + A->key_lo) * A->key_stride;
+    __hip_atomic_fetch_add(A->count + key, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      const u64 s = at<l64>(base + (u32)kLSUM[a])[kl];
+      const __int128 tot = (__int128)A->base[a] * (__int128)c + (__int128)A->step[a] * (__int128)s;
+      unsigned long long* acc = (unsigned long long*)A->sum[a];
+      if (A->sum_long[a]) {
+        __hip_atomic_fetch_add(acc + 2 * key, (u64)tot & 0xffffffffull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(acc + 2 * key + 1, (u64)(i64)(tot >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        __hip_atomic_fetch_add(acc + key, (u64)(i64)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}

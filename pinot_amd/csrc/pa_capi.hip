@@ -2,6 +2,7 @@
 // slots, staging, accumulator layout, strategy) and result fetch. No CPU fallback: every query runs the
 // HIP kernels; errors surface as negative return codes + pa_last_error().
 #include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -518,6 +519,10 @@ struct pa_query {
   void* fetch_host = nullptr;        // pinned copy of the compacted rows
   int lane_major = 0;
   int dense_packed = 0;  // STRAT_GDENSE_LM*: packed accumulation (GdLmPlan)
+  // the dense kernel specialised to this query's shape (gdl_jit.hip, compiled by hiprtc): null = the generic kernel
+  hipFunction_t jit_fn = nullptr;
+  int jit_waves = 0, jit_grid = 0, jit_lds = 0;
+  DevBuf jit_args, jit_segs;
   int has_mv = 0;
   bool hashed = false;           // packed 64-bit keys through a global open-addressing table
   int key_words = 1;             // hashed: 2 = two-word keys ([k0, k1, state] per slot)
@@ -587,6 +592,8 @@ struct pa_query {
     dev_free(merge_buf);
     dev_free(lim_admit);
     dev_free(dgdplans);
+    dev_free(jit_args);
+    dev_free(jit_segs);
     if (host_acc) (void)hipHostFree(host_acc);
     dev_free(fetch_blocks);
     dev_free(fetch_stage);
@@ -2064,6 +2071,7 @@ int plan_kernels(pa_query* q, Prep& P, TilePlan& plan, TilePlan& count_plan) {
     // resident waves (16- or 8-wave workgroups); every staged dictionary column has 1..31 bits (the unpacker switch)
     // (and every DICT_SET bitmap in LDS: gdl_leaf reads no HBM in the tile loop)
     bool lm_walk = !(s.flags & (PA_QF_NO_GDENSE_LM | PA_QF_NO_LANE_MAJOR)) && q->num_eager <= kGdLmLeaves;
+    for (const DevSeg& d : q->hsegs) lm_walk = lm_walk && d.num_staged <= kGdlMaxCols;
     for (int li = 0; li < q->num_eager && lm_walk; ++li)
       if (s.leaves[q->literals[li].leaf].kind == PA_LEAF_DICT_SET && (li >= (int)P.gd_lut.size() || P.gd_lut[li] < 0))
         lm_walk = false;
@@ -2404,6 +2412,14 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
           if (d.leaves[li].kind == PA_LEAF_DICT_RANGE && s.leaves[q->literals[li].leaf].column_id == s.group_by_columns[0] &&
               d.leaves[li].lds_off == d.cols[P.gb_slot[0]].lds_off) {
             lp.key_leaf = li;
+            // the box check is implied when this leaf is a unit clause (not negated) whose dictId range, without a
+            // remap, is exactly the box's component
+            const bool unit = q->clause_end[li] && (li == 0 || q->clause_end[li - 1]);
+            const pa_leaf_params& pr = q->leaf_params[si][q->literals[li].leaf];
+            const int64_t card = d.cols[P.gb_slot[0]].card;
+            const int64_t rlo = std::max<int64_t>(0, pr.lo), rhi = std::min<int64_t>(pr.hi, card);
+            lp.key_in_box = unit && !d.leaves[li].negate && P.gd_tab[0] < 0 && rlo == P.gd_lo[0] &&
+                            rhi - rlo == P.gd_span[0];
             break;
           }
         for (int li = 0; li < q->num_eager && li < kGdLmLeaves; ++li) {
@@ -2435,6 +2451,7 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
     }
     h.gd_rp_log2 = P.gd_rp_log2;
     h.gd_nkeys = P.gd_nkeys;
+    h.gd_pk_base = P.gd_packed ? (int32_t)P.gd_lds : 0;
     h.gd_tables = P.gd_tables;
     for (size_t li = 0; li < q->literals.size() && li < (size_t)PA_MAX_LEAVES; ++li) {
       h.gd_lut[li] = li < P.gd_lut.size() ? P.gd_lut[li] : -1;
@@ -2794,6 +2811,258 @@ static int alloc_leaps(pa_query* q, const Prep& P) {
   return PA_OK;
 }
 
+// ---------------------------------------------------------------- query-shape specialisation (gdl_jit.hip)
+// The lane-major dense kernel with packed accumulation, compiled per query shape by hiprtc: every column width, image
+// offset, leaf kind and field offset becomes a constant (no bit-width switch, no parameter reads, no DMA loop in the
+// tile loop). Compiled once per shape and device and cached for the process; the generic kernel runs when the shape
+// is outside the specialised form (or PA_QF_NO_JIT / PA_NO_JIT), or hiprtc fails.
+static const char* kGdlJitSrc =
+#include "gdl_jit_src.inc"
+    ;
+
+struct JitSegH {  // == gdl_jit.hip JitSeg
+  uint64_t src[6];
+  int64_t first_tile;
+  int32_t num_docs, num_tiles;
+  uint32_t lo_t[6], hi_t[6];
+};
+struct JitArgsH {  // == gdl_jit.hip JitArgs
+  int64_t total_tiles;
+  int32_t nseg, nkeys, key_lo, key_span, xcd_major, pad;
+  int64_t key_stride;
+  unsigned long long* matched;
+  unsigned long long* count;
+  int64_t* sum[6];
+  int32_t sum_long[6];
+  int64_t base[6], step[6];
+  const uint32_t* lut[6];
+  int32_t lut_words[6];
+  const int64_t* tab[6];
+  int32_t tab_n[6];
+};
+
+namespace {
+std::mutex g_jit_mu;
+struct JitEntry {
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr;
+};
+std::map<std::string, JitEntry> g_jit_cache;  // (device, compile options) -> loaded kernel
+
+std::string int_list(const std::vector<int>& v) {
+  std::string r = "{";
+  for (size_t i = 0; i < v.size(); ++i) r += (i ? "," : "") + std::to_string(v[i]);
+  return r + "}";
+}
+
+hipFunction_t jit_compile(const std::vector<std::string>& defs) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::string key = std::to_string(dev);
+  for (const std::string& d : defs) key += " " + d;
+  std::lock_guard<std::mutex> g(g_jit_mu);
+  auto it = g_jit_cache.find(key);
+  if (it != g_jit_cache.end()) return it->second.fn;
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, kGdlJitSrc, "gdl_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) return nullptr;
+  std::vector<std::string> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+  for (const std::string& d : defs) opts.push_back(d);
+  std::vector<const char*> o;
+  for (const std::string& x : opts) o.push_back(x.c_str());
+  hipFunction_t fn = nullptr;
+  if (hiprtcCompileProgram(prog, (int)o.size(), o.data()) == HIPRTC_SUCCESS) {
+    size_t n = 0;
+    if (hiprtcGetCodeSize(prog, &n) == HIPRTC_SUCCESS && n) {
+      std::vector<char> code(n);
+      JitEntry e;
+      if (hiprtcGetCode(prog, code.data()) == HIPRTC_SUCCESS && hipModuleLoadData(&e.mod, code.data()) == hipSuccess &&
+          hipModuleGetFunction(&e.fn, e.mod, "gdl_jit") == hipSuccess) {
+        fn = e.fn;
+        g_jit_cache[key] = e;
+      }
+    }
+  } else if (std::getenv("PA_JIT_LOG")) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::vector<char> log(n + 1, 0);
+    hiprtcGetProgramLog(prog, log.data());
+    std::fprintf(stderr, "pinot_amd: gdl_jit compile failed:\n%s\n", log.data());
+  }
+  hiprtcDestroyProgram(&prog);
+  return fn;
+}
+}  // namespace
+
+// The JIT args' accumulator pointers (the block can move: pa_query_set_accumulator_buffer)
+void jit_fill_pointers(pa_query* q, JitArgsH& a) {
+  const pa_query_spec& s = q->spec;
+  a.matched = q->hq.matched_docs;
+  a.count = q->hq.count;
+  int k = 0;
+  for (int i = 0; i < s.num_aggs; ++i) {
+    if (s.aggs[i].type == PA_AGG_COUNT) continue;
+    a.sum[k] = q->hq.aggs[i].acc_i64;
+    a.sum_long[k] = q->hq.aggs[i].src == SRC_LONG ? 1 : 0;
+    ++k;
+  }
+}
+
+int jit_plan(pa_query* q, const Prep& P, int cus) {
+  q->jit_fn = nullptr;
+  const pa_query_spec& s = q->spec;
+  if (!is_gdense_lm(q->strategy) || !P.gd_packed || P.gd_box || q->hq.leap_mode || q->nseg == 0) return PA_OK;
+  if ((s.flags & PA_QF_NO_JIT) || std::getenv("PA_NO_JIT") || std::getenv("PA_DEBUG_EMIT")) return PA_OK;
+  if (s.num_group_by != 1 || P.gd_tab[0] >= 0 || q->num_eager > 6) return PA_OK;
+  const DevSeg& d0 = q->hsegs[0];
+  const int nc = d0.num_staged;
+  if (nc < 1 || nc > 6) return PA_OK;
+  for (const DevSeg& d : q->hsegs) {
+    if (d.num_staged != nc) return PA_OK;
+    for (int k = 0; k < nc; ++k)
+      if (d.stage[k].nbits != d0.stage[k].nbits || d.stage[k].lds_off != d0.stage[k].lds_off || d.stage[k].nbits < 1 ||
+          d.stage[k].nbits > 31)
+        return PA_OK;
+  }
+  auto col_of = [&](int lds_off) {
+    for (int k = 0; k < nc; ++k)
+      if (d0.stage[k].lds_off == lds_off) return k;
+    return -1;
+  };
+  auto lmp = [&](int si) -> const GdLmPlan& { return *(const GdLmPlan*)&q->gdplans[(size_t)si * kGdPlanDw + 128]; };
+  for (int si = 1; si < q->nseg; ++si)
+    if (lmp(si).key_leaf != lmp(0).key_leaf || lmp(si).key_in_box != lmp(0).key_in_box) return PA_OK;
+  const int nkeys = P.gd_nkeys;
+  auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  // LDS: counts, sums, bitmaps, tables, then (per wave count) rows and ring
+  size_t off = al16((size_t)nkeys * 4);
+  std::vector<int> lsum;
+  std::vector<int> ac, at, as;
+  JitArgsH a;
+  std::memset(&a, 0, sizeof(a));
+  int k = 0;
+  for (int i = 0; i < s.num_aggs; ++i) {
+    if (s.aggs[i].type == PA_AGG_COUNT) continue;
+    if (P.gd_op[i] != GOP_SUM_I || (P.gd_vs[i] != GVS_ID && P.gd_vs[i] != GVS_T32U)) return PA_OK;
+    for (int si = 1; si < q->nseg; ++si)
+      if (P.gd_vs[i] == GVS_T32U && P.gd_src[si][i] != P.gd_src[0][i]) return PA_OK;
+    const int c = col_of(d0.cols[P.agg_slot[i]].lds_off);
+    if (c < 0) return PA_OK;
+    lsum.push_back((int)off);
+    off += al16((size_t)nkeys * 8);
+    ac.push_back(c);
+    as.push_back(lmp(0).pk_off[k]);
+    a.base[k] = P.gd_base[i];
+    a.step[k] = P.gd_step[i];
+    ++k;
+  }
+  const int na = k;
+  std::vector<int> lk, lc, ln, le, lut;
+  for (int li = 0; li < q->num_eager; ++li) {
+    const DevLeaf& L = d0.leaves[li];
+    for (const DevSeg& d : q->hsegs)
+      if (d.leaves[li].negate != L.negate || d.leaves[li].kind != L.kind) return PA_OK;
+    if (L.kind != PA_LEAF_DICT_RANGE && L.kind != PA_LEAF_DICT_SET) return PA_OK;
+    const int c = col_of(L.lds_off);
+    if (c < 0) return PA_OK;
+    lk.push_back(L.kind == PA_LEAF_DICT_SET ? 1 : 0);
+    lc.push_back(c);
+    ln.push_back(L.negate ? 1 : 0);
+    le.push_back(L.clause_end ? 1 : 0);
+    if (L.kind == PA_LEAF_DICT_SET) {
+      if (li >= (int)P.gd_lut.size() || P.gd_lut[li] < 0) return PA_OK;
+      lut.push_back((int)off);
+      a.lut[li] = L.lut;
+      a.lut_words[li] = P.gd_lut_words[li];
+      off += al16((size_t)P.gd_lut_words[li] * 4);
+    } else {
+      lut.push_back(0);
+    }
+  }
+  k = 0;
+  for (int i = 0; i < s.num_aggs; ++i) {
+    if (s.aggs[i].type == PA_AGG_COUNT) continue;
+    if (P.gd_vs[i] == GVS_T32U) {
+      at.push_back((int)off);
+      a.tab[k] = (const int64_t*)P.gd_src[0][i];
+      a.tab_n[k] = P.gd_tab_an[i];
+      off += al16((size_t)P.gd_tab_an[i] * 4);
+    } else {
+      at.push_back(-1);
+    }
+    ++k;
+  }
+  const int kc = col_of(d0.cols[P.gb_slot[0]].lds_off);
+  if (kc < 0) return PA_OK;
+  const size_t img_b = (size_t)q->hq.image_dwords_max * 4;
+  int w = 0;
+  for (int cand : {16, 8})
+    if (al16(off + (size_t)cand * nkeys * 8) + (size_t)cand * 2 * img_b <= kLdsBudget) {
+      w = cand;
+      break;
+    }
+  if (!w) return PA_OK;
+  const size_t rows = off;
+  const size_t ring = al16(off + (size_t)w * nkeys * 8);
+  const size_t lds = ring + (size_t)w * 2 * img_b;
+  auto pad6 = [](std::vector<int> v) {
+    if (v.empty()) v.push_back(0);
+    return v;
+  };
+  std::vector<int> nb, coff;
+  for (int c = 0; c < nc; ++c) {
+    nb.push_back(d0.stage[c].nbits);
+    coff.push_back(4 * d0.stage[c].lds_off);
+  }
+  const GdLmPlan& L0 = lmp(0);
+  std::vector<std::string> defs = {
+      "-DJIT_W=" + std::to_string(w), "-DJIT_IMG=" + std::to_string(q->hq.image_dwords_max),
+      "-DJIT_NC=" + std::to_string(nc), "-DJIT_NB=" + int_list(nb), "-DJIT_OFF=" + int_list(coff),
+      "-DJIT_NL=" + std::to_string(q->num_eager), "-DJIT_LK=" + int_list(pad6(lk)), "-DJIT_LC=" + int_list(pad6(lc)),
+      "-DJIT_LN=" + int_list(pad6(ln)), "-DJIT_LE=" + int_list(pad6(le)), "-DJIT_LUT=" + int_list(pad6(lut)),
+      "-DJIT_KC=" + std::to_string(kc), "-DJIT_KL=" + std::to_string(L0.key_leaf),
+      "-DJIT_KIB=" + std::to_string(L0.key_in_box ? 1 : 0), "-DJIT_NA=" + std::to_string(na),
+      "-DJIT_AC=" + int_list(pad6(ac)), "-DJIT_AT=" + int_list(pad6(at)), "-DJIT_AS=" + int_list(pad6(as)),
+      "-DJIT_OC=" + std::to_string(L0.pk_cnt), "-DJIT_DRAIN=" + std::to_string(std::max(1, L0.pk_drain)),
+      "-DJIT_L_SUM=" + int_list(pad6(lsum)), "-DJIT_L_ROWS=" + std::to_string(rows),
+      "-DJIT_L_RING=" + std::to_string(ring)};
+  hipFunction_t fn = jit_compile(defs);
+  if (!fn) return PA_OK;
+  (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  // descriptors
+  a.total_tiles = q->hq.total_wtiles;
+  a.nseg = q->nseg;
+  a.nkeys = nkeys;
+  a.key_lo = P.gd_lo[0];
+  a.key_span = P.gd_span[0];
+  a.xcd_major = 1;
+  a.key_stride = q->hq.gb_stride[0];
+  jit_fill_pointers(q, a);
+  std::vector<JitSegH> js(q->nseg);
+  for (int si = 0; si < q->nseg; ++si) {
+    const DevSeg& d = q->hsegs[si];
+    JitSegH& j = js[si];
+    std::memset(&j, 0, sizeof(j));
+    for (int c = 0; c < nc; ++c) j.src[c] = (uint64_t)(uintptr_t)d.stage[c].words;
+    j.first_tile = d.first_wtile;
+    j.num_docs = d.num_docs;
+    j.num_tiles = d.num_wtiles;
+    for (int li = 0; li < q->num_eager; ++li) {
+      j.lo_t[li] = (uint32_t)d.leaves[li].lo;
+      j.hi_t[li] = (uint32_t)d.leaves[li].span;
+    }
+  }
+  int rc = dev_alloc(q->jit_args, sizeof(JitArgsH));
+  if (!rc) rc = dev_alloc(q->jit_segs, sizeof(JitSegH) * js.size());
+  if (rc) return rc;
+  PA_HIP(hipMemcpy(q->jit_args.p, &a, sizeof(a), hipMemcpyHostToDevice));
+  PA_HIP(hipMemcpy(q->jit_segs.p, js.data(), sizeof(JitSegH) * js.size(), hipMemcpyHostToDevice));
+  q->jit_fn = fn;
+  q->jit_waves = w;
+  q->jit_lds = (int)lds;
+  q->jit_grid = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (q->hq.total_wtiles + w - 1) / w));
+  return PA_OK;
+}
+
 int pa_query_prepare(pa_query* q) {
   if (!q) return fail(PA_EINVAL, "null query");
   if (q->prepared) return PA_OK;
@@ -2892,6 +3161,8 @@ int pa_query_prepare(pa_query* q) {
   if (rc) return rc;
   rc = upload_descriptors(q);
   if (rc) return rc;
+  rc = jit_plan(q, P, cus);
+  if (rc) return rc;
   PA_HIP(hipDeviceSynchronize());
   q->prepared = true;
   return PA_OK;
@@ -2957,6 +3228,14 @@ int pa_query_scan(pa_query* q, void* stream) {
     a->used = true;
     return PA_OK;
   }
+  if (q->jit_fn) {  // the query-shape specialised dense kernel
+    void* pa = q->jit_args.p;
+    void* ps = q->jit_segs.p;
+    void* params[] = {&pa, &ps};
+    PA_HIP(hipModuleLaunchKernel(q->jit_fn, q->jit_grid, 1, 1, q->jit_waves * kWave, 1, 1, q->jit_lds, st, params,
+                                 nullptr));
+    return PA_OK;
+  }
   PartScratch none{};
   PA_HIP(launch_scan(q->strategy, q->steps, q->lane_major, q->grid, q->lds_bytes, (const DevQuery*)q->dq.p,
                      (const DevSeg*)q->dsegs.p, (const LmSegPlan*)q->dplans.p, none, st));
@@ -2995,6 +3274,12 @@ int pa_query_set_accumulator_buffer(pa_query* q, void* device_buffer, uint64_t b
   relocate(q->hq);
   if (q->limit_mode) q->limit.reached = q->hq.matched_docs + 2;
   PA_HIP(hipMemcpy(q->dq.p, &q->hq, sizeof(DevQuery), hipMemcpyHostToDevice));
+  if (q->jit_fn) {
+    JitArgsH a;
+    PA_HIP(hipMemcpy(&a, q->jit_args.p, sizeof(a), hipMemcpyDeviceToHost));
+    jit_fill_pointers(q, a);
+    PA_HIP(hipMemcpy(q->jit_args.p, &a, sizeof(a), hipMemcpyHostToDevice));
+  }
   if (q->partitioned) {
     relocate(q->hq_count);
     PA_HIP(hipMemcpy(q->dq_count.p, &q->hq_count, sizeof(DevQuery), hipMemcpyHostToDevice));
@@ -3497,7 +3782,9 @@ int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t*
 int32_t pa_query_num_eager_literals(const pa_query* q) { return q && q->prepared ? q->num_eager : -1; }
 
 int32_t pa_query_lane_major(const pa_query* q) { return q && q->prepared ? q->lane_major : -1; }
-int32_t pa_query_dense_packed(const pa_query* q) { return q && q->prepared ? q->dense_packed : -1; }
+int32_t pa_query_dense_packed(const pa_query* q) {
+  return q && q->prepared ? (q->dense_packed ? (q->jit_fn ? 2 : 1) : 0) : -1;
+}
 
 int32_t pa_query_column_staged(const pa_query* q, int32_t column_id) {
   if (!q || !q->prepared || q->nseg == 0) return -1;

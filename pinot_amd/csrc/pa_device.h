@@ -305,7 +305,8 @@ struct DevQuery {
                                      // gd_ls[j], -1 outside the box), or -1: component = dictId - gd_lo[j]
   int32_t gd_tab_n[PA_MAX_GROUP_BY]; // key table entries (largest segment cardinality)
   int32_t gd_tables;                 // some key or value table is loaded per segment
-  int32_t gd_pad;
+  int32_t gd_pk_base;                // lane-major walk, packed: LDS byte offset of the waves' packed rows (which end at
+                                     // lds_acc_bytes), 0 = not packed
   // DICT_SET literals whose dictId bitmap is the same in every segment: LDS byte offset of the bitmap (-1: read from
   // HBM — a global load in the tile loop waits for every tile in flight), and its words
   int32_t gd_lut[PA_MAX_LEAVES];
@@ -381,6 +382,7 @@ static_assert(sizeof(GdLmIssue) == 256, "one dword per lane");
 // in the top bits from pk_cnt): a field of c bits holds 2^c - 1 docs' terms, so each wave drains its packed rows into
 // the workgroup's accumulators every pk_drain tiles (at most 1024 docs each).
 constexpr int kGdLmLeaves = 6;
+constexpr int kGdlMaxCols = 6;  // staged columns of a lane-major walk query (its DMA descriptors live in SGPRs)
 struct GdLmPlan {
   int32_t nleaves;                       // 0: eager leaves (every literal)
   int32_t num_docs;                      // 1
@@ -391,7 +393,8 @@ struct GdLmPlan {
   int32_t pk_off[kGdMaxAgg];             // 6..11: bit offset of non-COUNT aggregation k's field
   int32_t key_leaf;                      // 12: the eager leaf on the (single) group-by column: its unpacked values are
                                          //     the key's (no second unpack), -1: none
-  int32_t pad0[3];                       // 13..15
+  int32_t key_in_box;                    // 13: key_leaf's range is exactly the key box (the filter implies the box)
+  int32_t pad0[2];                       // 14..15
   struct {                               // 16 + 7l
     uint32_t code;                       // kind | negate << 8 | clause_end << 9 | nbits << 16
     uint32_t region;                     // byte offset of the column's region in the tile image

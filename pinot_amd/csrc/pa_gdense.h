@@ -449,13 +449,42 @@ __device__ __forceinline__ void gdl_top(uint32_t region, int lane, uint32_t (&v)
   X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20)   \
   X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31)
 
+// The lane's 16 dictIds of an NB-bit column region: gdl_top's words, each id by one v_bfe_u32 (two ops when it
+// straddles two words)
+template <int NB>
+__device__ __forceinline__ void gdl_idv(uint32_t region, int lane, uint32_t (&v)[kGdlDocs]) {
+  constexpr int K = (kGdlDocs * NB + 31) / 32 + 1;
+  uint32_t ln = (uint32_t)lane;
+  asm volatile("" : "+v"(ln));
+  const uint32_t bit0 = __umul24(ln, (uint32_t)(kGdlDocs * NB));
+  uint32_t w[K];
+  if constexpr ((kGdlDocs * NB) % 32 != 0) {
+    const uint32_t sh = bit0 & 16u;
+    const lds_u32_t* p = lds_at<const lds_u32_t>(region + 4u * ((bit0 >> 5) - 1u + (sh >> 4)));
+    uint32_t r[K + 1];
+#pragma unroll
+    for (int j = 0; j <= K; ++j) r[j] = p[j];
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = __builtin_amdgcn_alignbit(r[j], r[j + 1], sh);
+  } else {
+    const lds_u32_t* p = lds_at<const lds_u32_t>(region + 4u * (bit0 >> 5));
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = p[j];
+  }
+#pragma unroll
+  for (int i = 0; i < kGdlDocs; ++i) {
+    const int s = i * NB, j = s >> 5, o = s & 31;
+    if (o + NB <= 32) v[i] = __builtin_amdgcn_ubfe(w[j], 32 - o - NB, NB);
+    else v[i] = __builtin_amdgcn_alignbit(w[j], w[j + 1], 32 - o) >> (32 - NB);
+  }
+}
+
 // dictIds of the lane's 16 docs (nb wave-uniform, 1..31)
 __device__ __forceinline__ void gdl_ids(int nb, uint32_t region, int lane, uint32_t (&id)[kGdlDocs]) {
   switch (nb) {
 #define PA_GDL_IDS(N)                                                \
   case N: {                                                          \
-    gdl_top<N>(region, lane, id);                                    \
-    _Pragma("unroll") for (int i = 0; i < kGdlDocs; ++i) id[i] >>= 32 - N; \
+    gdl_idv<N>(region, lane, id);                                    \
   } break;
     PA_GDL_NB_CASES(PA_GDL_IDS)
 #undef PA_GDL_IDS
@@ -544,6 +573,77 @@ __device__ __forceinline__ void gdl_raw64(uint32_t region, int lane, uint64_t (&
   }
 }
 
+// One LDS-DMA wave instruction with a scalar base address (global_load_lds_dwordx4 vaddr = 32-bit lane offset, saddr):
+// lane l copies the 16 bytes at sbase + voff_l to dst + 16 l. `mask` (a partial instruction): the lanes that take part.
+__device__ __forceinline__ void dma16s(uint32_t voff, uint64_t sbase, uint32_t dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(dst));
+}
+__device__ __forceinline__ void dma16s_masked(uint32_t voff, uint64_t sbase, uint32_t dst, uint64_t mask) {
+  uint32_t keep;
+  uint64_t save;
+  asm volatile(
+      "s_mov_b64 %1, exec\n\t"
+      "s_mov_b64 exec, %5\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %3\n\t"
+      "s_mov_b32 m0, %0\n\t"
+      "s_mov_b64 exec, %1"
+      : "=&s"(keep), "=&s"(save)
+      : "v"(voff), "s"(sbase), "s"(dst), "s"(mask));
+}
+
+// The lane-major walk's DMA descriptors of one segment, wave-uniform (SGPRs, read once per segment from the GdLmIssue
+// VGPR): per staged column the tile-0 source, bytes per tile, 16-byte chunks per tile and LDS destination. Issuing a
+// tile is then scalar arithmetic and one instruction per 1 KiB, no descriptor read and no per-lane address math.
+struct GdlDma {
+  int nc;
+  uint64_t src[kGdlMaxCols];
+  uint32_t stride[kGdlMaxCols], chunks[kGdlMaxCols], dst[kGdlMaxCols];
+};
+
+__device__ __forceinline__ void gdl_dma_load(uint32_t ip, GdlDma& d) {
+  d.nc = (int)rl(ip, 0);
+#pragma unroll
+  for (int c = 0; c < kGdlMaxCols; ++c) {
+    d.src[c] = ((uint64_t)rl(ip, 2 + 5 * c) << 32) | rl(ip, 1 + 5 * c);
+    d.stride[c] = rl(ip, 3 + 5 * c);
+    d.chunks[c] = rl(ip, 4 + 5 * c);
+    d.dst[c] = rl(ip, 5 + 5 * c);
+  }
+}
+
+// One 1024-doc tile: every column's chunks, exactly D instructions (dummies re-read column 0's first chunk into the
+// image's leading guard words)
+__device__ __forceinline__ void gdl_dma_issue(const GdlDma& d, int64_t wt, uint32_t img, uint32_t voff, int lane,
+                                              const int D) {
+  int issued = 0;
+#pragma unroll
+  for (int c = 0; c < kGdlMaxCols; ++c) {
+    if (c >= d.nc) break;
+    const uint64_t base = d.src[c] + (uint64_t)wt * d.stride[c];
+    const uint32_t dst = img + d.dst[c];
+    const int chunks = (int)d.chunks[c];
+    int c0 = 0;
+    for (; c0 + 64 <= chunks; c0 += 64, ++issued) dma16s(voff, base + 16u * (uint32_t)c0, dst + 16u * (uint32_t)c0);
+    if (c0 < chunks) {
+      dma16s_masked(voff, base + 16u * (uint32_t)c0, dst + 16u * (uint32_t)c0, (1ull << (chunks - c0)) - 1ull);
+      ++issued;
+    }
+  }
+  for (; issued < D; ++issued) dma16s_masked(voff, d.src[0], img, 1ull);
+  (void)lane;
+}
+
 // LDS-DMA of one 1024-doc tile from the segment's GdLmIssue (VGPR ip), padded to exactly D instructions (the padding
 // re-reads the first column's first chunk into the image's guard words).
 __device__ __forceinline__ void gdl_stage(uint32_t ip, int64_t wt, uint32_t img, int lane, const int D) {
@@ -564,6 +664,52 @@ __device__ __forceinline__ void gdl_stage(uint32_t ip, int64_t wt, uint32_t img,
   const uint64_t src0 = ((uint64_t)rl(ip, 2) << 32) | rl(ip, 1);
   for (; issued < D; ++issued)
     if (lane == 0) dma16((const void*)src0, img);
+}
+
+// Packed accumulation of the lane's matching docs (bits of `on`) into their rows (LDS byte addresses `addr`): one word
+// per doc, COUNT + every SUM term at its field. The fields of one doc's word do not overlap, so the word is built with
+// ORs, 32 bits at a time (a term below bit 32 also spills into the high word).
+template <int MA>
+__device__ __forceinline__ void gdl_packed_accumulate(uint32_t gt, uint32_t lp, uint32_t img, int lane, uint32_t base,
+                                                      uint32_t on, const uint32_t (&addr)[kGdlDocs]) {
+  constexpr int ND = kGdlDocs;
+  const int na = (int)rl(gt, 1);
+  uint32_t plo[ND], phi[ND];
+  const uint32_t oc = rl(lp, 3);
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+    plo[i] = oc < 32 ? 1u << oc : 0u;
+    phi[i] = oc < 32 ? 0u : 1u << (oc - 32);
+  }
+#pragma unroll 1
+  for (int g = 0; g < MA; ++g) {
+    if (g >= na) break;
+    const int o = 22 + 6 * g;
+    uint32_t id[ND];
+    gdl_ids((int)rl(gt, o + 3), img + 4u * rl(gt, o + 2), lane, id);
+    if ((int)rl(gt, o) == GVS_T32U) {
+      const lds_u32_t* t = lds_at<const lds_u32_t>(base + rl(gt, o + 5));
+#pragma unroll
+      for (int i = 0; i < ND; ++i) id[i] = t[id[i]];
+    }
+    const uint32_t sh = (uint32_t)__builtin_amdgcn_readlane((int)lp, 6 + g);
+    if (sh >= 32) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) phi[i] |= id[i] << (sh - 32);
+    } else if (sh == 0) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) plo[i] |= id[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        plo[i] |= id[i] << sh;
+        phi[i] |= __builtin_amdgcn_alignbit(0u, id[i], 32u - sh);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < ND; ++i)
+    if ((on >> i) & 1u) __hip_atomic_fetch_add(lds_at<lds_u64_t>(addr[i]), ((uint64_t)phi[i] << 32) | plo[i], WG_RLX);
 }
 
 // Drain of a wave's packed rows (GdLmPlan) into the workgroup's accumulators: every non-zero row is read, zeroed and
@@ -630,8 +776,52 @@ __device__ __forceinline__ uint32_t gdl_tile(uint32_t gt, uint32_t lp, int64_t w
   }
   if (__ballot(m != 0) == 0) return 0;
   if (dbg & 1) return (uint32_t)__builtin_popcount(m);
-  // group keys: component j = key table entry (per-segment remap into the box, < 0 outside) or dictId - lo (< span)
   const int ngb = (int)rl(gt, 0), na = (int)rl(gt, 1);
+  if (rl(lp, 2) && ngb == 1 && (int)rl(gt, 6) < 0) {
+    // packed, one group-by column without a key table: the doc's packed-row address straight from its dictId
+    // (rows + 8 (id - lo)), the box check only where the filter does not imply it (GdLmPlan key_in_box)
+    const uint32_t nb = rl(gt, 5), lo = rl(gt, 7), span = rl(gt, 8);
+    uint32_t id[ND];
+    if (key_leaf >= 0) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) id[i] = kt[i] >> (32u - nb);
+    } else {
+      gdl_ids((int)nb, img + 4u * rl(gt, 4), lane, id);
+    }
+    uint32_t on = m;
+    if (!rl(lp, 13)) {
+      uint32_t nm = 0;  // (not in the box: non-matches as in gdl_leaf's range, then cleared from the matches)
+#pragma unroll
+      for (int i = ND - 1; i >= 0; --i) {
+        uint32_t u;
+        asm("v_sub_u32_e64 %[u], %[t], %[lo]\n\t"
+            "v_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
+            "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
+            : [nm] "+v"(nm), [u] "=&v"(u)
+            : [t] "v"(id[i]), [lo] "s"(lo), [hi] "s"(span - 1u)
+            : "vcc");
+      }
+      on &= ~nm;
+    }
+    uint32_t mine;
+    if (box) {
+      mine = (uint32_t)__builtin_popcount(on);
+    } else {
+      mine = (uint32_t)__builtin_popcount(m);
+      errs += (uint32_t)__builtin_popcount(m & ~on);
+    }
+    if (dbg & 2) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) asm volatile("" ::"v"(id[i]), "v"(on));
+      return mine;
+    }
+    const uint32_t abase = rows - 8u * lo;
+#pragma unroll
+    for (int i = 0; i < ND; ++i) id[i] = abase + (id[i] << 3);  // (from here on: the row's LDS address)
+    gdl_packed_accumulate<MA>(gt, lp, img, lane, base, on, id);
+    return mine;
+  }
+  // group keys: component j = key table entry (per-segment remap into the box, < 0 outside) or dictId - lo (< span)
   uint32_t key[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) key[i] = 0u;
@@ -682,45 +872,9 @@ __device__ __forceinline__ uint32_t gdl_tile(uint32_t gt, uint32_t lp, int64_t w
     return mine;
   }
   if (rl(lp, 2)) {
-    // packed: one word per doc, COUNT + every SUM term at its field; the fields of one doc's word do not overlap, so
-    // the word is built with ORs, 32 bits at a time (a term below bit 32 also spills into the high word)
-    uint32_t plo[ND], phi[ND];
-    const uint32_t oc = rl(lp, 3);
 #pragma unroll
-    for (int i = 0; i < ND; ++i) {
-      plo[i] = oc < 32 ? 1u << oc : 0u;
-      phi[i] = oc < 32 ? 0u : 1u << (oc - 32);
-    }
-#pragma unroll 1
-    for (int g = 0; g < MA; ++g) {
-      if (g >= na) break;
-      const int o = 22 + 6 * g;
-      uint32_t id[ND];
-      gdl_ids((int)rl(gt, o + 3), img + 4u * rl(gt, o + 2), lane, id);
-      if ((int)rl(gt, o) == GVS_T32U) {
-        const lds_u32_t* t = lds_at<const lds_u32_t>(base + rl(gt, o + 5));
-#pragma unroll
-        for (int i = 0; i < ND; ++i) id[i] = t[id[i]];
-      }
-      const uint32_t sh = (uint32_t)__builtin_amdgcn_readlane((int)lp, 6 + g);
-      if (sh >= 32) {
-#pragma unroll
-        for (int i = 0; i < ND; ++i) phi[i] |= id[i] << (sh - 32);
-      } else if (sh == 0) {
-#pragma unroll
-        for (int i = 0; i < ND; ++i) plo[i] |= id[i];
-      } else {
-#pragma unroll
-        for (int i = 0; i < ND; ++i) {
-          plo[i] |= id[i] << sh;
-          phi[i] |= __builtin_amdgcn_alignbit(0u, id[i], 32u - sh);
-        }
-      }
-    }
-    lds_u64_t* row = lds_at<lds_u64_t>(rows);
-#pragma unroll
-    for (int i = 0; i < ND; ++i)
-      if ((on >> i) & 1u) __hip_atomic_fetch_add(row + key[i], ((uint64_t)phi[i] << 32) | plo[i], WG_RLX);
+    for (int i = 0; i < ND; ++i) key[i] = rows + (key[i] << 3);
+    gdl_packed_accumulate<MA>(gt, lp, img, lane, base, on, key);
     return mine;
   }
   const uint32_t rpl = rl(gt, 2);
@@ -880,6 +1034,9 @@ __device__ void gd_load_tables(CQ* q, CSegT* cs, unsigned char* lds, int tid, in
 }
 
 __device__ void gd_init(CQ* q, unsigned char* lds, int tid, int nthreads) {
+  if (q->gd_pk_base > 0)  // the waves' packed rows (lane-major walk)
+    for (uint32_t i = (uint32_t)q->gd_pk_base / 4u + (uint32_t)tid; i < q->lds_acc_bytes / 4u; i += (uint32_t)nthreads)
+      ((uint32_t*)lds)[i] = 0u;
   const int64_t n = (int64_t)q->gd_nkeys << q->gd_rp_log2;
   uint32_t* cnt = (uint32_t*)lds;
   for (int64_t i = tid; i < n; i += nthreads) cnt[i] = 0u;
@@ -1011,11 +1168,15 @@ __global__ void __launch_bounds__(WPW * kWave, 1) gdense_kernel(const DevQuery* 
     int isi = find_segment(segs, nseg, t0);
     int64_t ifirst = segs[isi].first_wtile, iend = ifirst + segs[isi].num_wtiles;
     uint32_t ip = LM == 1 ? ((const uint32_t*)(plans + isi))[lane] : 0u;
+    GdlDma dd;  // LM == 2: the issue segment's DMA descriptors (SGPRs)
+    dd.nc = 0;
+    const uint32_t voff = 16u * (uint32_t)lane;
     if (LM == 2) {
       ip = gp(q->gd_plans)[(int64_t)isi * kGdPlanDw + 64 + lane];  // GdLmIssue
       // (a use right here makes the compiler wait for this load here, once per segment, and not at the next merge
       // point after a tile's DMA issue, where its vmcnt(0) would wait for the DMA too)
       asm volatile("" ::"v"(ip));
+      gdl_dma_load(ip, dd);
     }
     int islot = 0;
     auto issue_next = [&]() {
@@ -1027,10 +1188,11 @@ __global__ void __launch_bounds__(WPW * kWave, 1) gdense_kernel(const DevQuery* 
         if (LM == 2) {
           ip = gp(q->gd_plans)[(int64_t)isi * kGdPlanDw + 64 + lane];
           asm volatile("" ::"v"(ip));
+          gdl_dma_load(ip, dd);
         }
       }
       if constexpr (LM == 1) stage_tile_lm(ip, ti - ifirst, ring_lds + 4u * (uint32_t)(islot * img_dw), lane, D);
-      else if constexpr (LM == 2) gdl_stage(ip, ti - ifirst, ring_lds + 4u * (uint32_t)(islot * img_dw), lane, D);
+      else if constexpr (LM == 2) gdl_dma_issue(dd, ti - ifirst, ring_lds + 4u * (uint32_t)(islot * img_dw), voff, lane, D);
       else stage_tile<kGdSmSteps>(segs + isi, ti - ifirst, ring + islot * img_dw, lane, D);
       ti += WPW;
       islot = islot + 1 == R ? 0 : islot + 1;
@@ -1063,7 +1225,8 @@ __global__ void __launch_bounds__(WPW * kWave, 1) gdense_kernel(const DevQuery* 
         if (LM == 2 && (rl(gt, 3) & 64)) {  // measurement only (PA_DEBUG_EMIT 64): no DMA, compute on stale images
           ti = t1;
         } else {
-          wait_tile((int)((ti - t) / WPW - 1), D, slot_off);  // tile t has landed (its younger tiles may still fly)
+          if (LM == 2 && R == 2) vm_wait<0>();  // (two images: the one tile in flight is this one)
+          else wait_tile((int)((ti - t) / WPW - 1), D, slot_off);  // tile t has landed (younger tiles may still fly)
           if (ti < t1) issue_next();
         }
         if constexpr (LM == 1) matched += gd_tile(gt, pp, t - sfirst, ring_lds + 4u * slot_off, lane, base, errs);

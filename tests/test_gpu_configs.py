@@ -157,7 +157,7 @@ def adanalytics3():
 
 
 # the dense GROUP BY kernel variant the bench's secondary lines run (pa_query_plan; engine.STRATEGY_VARIANTS)
-BENCH_SECONDARY_VARIANT = "gdense_lm8"
+BENCH_SECONDARY_VARIANT = "gdense_lm8"  # (dense_packed 2: the query-shape specialised kernel)
 
 
 @pytest.mark.parametrize("n_ids,frac", [(17476, 0.1), (87381, 0.5)])
