@@ -225,6 +225,24 @@ def main():
 
     # scan-kernel-only timing (per-launch duration = elapsed / steps, the figure rocprofv3 --stats averages)
     kernel_ms = kernel_time(ex, args.steps)
+    multi = None
+    if distributed:
+        # per-rank evidence for a scaling record: each rank's scan time, the merge's time (the RCCL collective of the
+        # partial aggregates alone, back to back) and the ranks the process group holds
+        torch.cuda.synchronize()
+        ma, mb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ma.record(stream)
+        for _ in range(args.steps):
+            dacc.reduce(dst=0)
+        mb.record(stream)
+        torch.cuda.synchronize()
+        merge_ms = ma.elapsed_time(mb) / args.steps
+        per = torch.tensor([kernel_ms, merge_ms], dtype=torch.float64, device=device)
+        allr = [torch.zeros_like(per) for _ in range(world)]
+        dist.all_gather(allr, per)
+        multi = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                 "kernel_ms_per_rank": [float(x[0].item()) for x in allr],
+                 "merge_ms_per_rank": [float(x[1].item()) for x in allr]}
 
     if distributed:
         dist.barrier()
@@ -315,6 +333,8 @@ def main():
             "cpu_baseline": cpu,
             "secondary": secondary,
         }
+        if multi is not None:
+            out["multi_gpu"] = multi
         print(json.dumps(out), flush=True)
     ex.close()
     for g in gsegs:

@@ -287,6 +287,75 @@ class TableLayout:
 from .query import DISTINCT_SET_FUNCTIONS as DISTINCT_FUNCTIONS, query_columns  # noqa: E402
 
 
+def _encode_record(rec):
+    """A rank's layout record as bytes without pickling: a JSON header (scalars, lists, and per array its dtype, shape
+    and byte range; string dictionaries as JSON lists) followed by the numeric arrays' raw bytes."""
+    import json
+    blobs, off = [], 0
+
+    def enc(v):
+        nonlocal off
+        if isinstance(v, np.ndarray):
+            if v.dtype.kind in "USO":
+                return {"strs": [str(x) for x in v.tolist()]}
+            a = np.ascontiguousarray(v)
+            blobs.append(a.tobytes())
+            d = {"dtype": a.dtype.str, "shape": list(a.shape), "off": off, "n": a.nbytes}
+            off += a.nbytes
+            return {"array": d}
+        if isinstance(v, dict):
+            return {"dict": {k: enc(x) for k, x in v.items()}}
+        if isinstance(v, (list, tuple)):
+            return {"list": [enc(x) for x in v]}
+        if isinstance(v, (bool, np.bool_)):
+            return {"v": bool(v)}
+        if isinstance(v, (int, np.integer)):
+            return {"v": int(v)}
+        return {"v": v}
+
+    head = json.dumps(enc(rec)).encode()
+    return len(head).to_bytes(8, "little") + head + b"".join(blobs)
+
+
+def _decode_record(buf):
+    import json
+    hl = int.from_bytes(buf[:8], "little")
+    head = json.loads(buf[8:8 + hl].decode())
+    body = buf[8 + hl:]
+
+    def dec(v):
+        if "array" in v:
+            a = v["array"]
+            return np.frombuffer(body[a["off"]:a["off"] + a["n"]], dtype=np.dtype(a["dtype"])).reshape(a["shape"]).copy()
+        if "strs" in v:
+            return np.asarray(v["strs"], dtype=object)
+        if "dict" in v:
+            return {k: dec(x) for k, x in v["dict"].items()}
+        if "list" in v:
+            return [dec(x) for x in v["list"]]
+        return v["v"]
+
+    return dec(head)
+
+
+def all_gather_records(rec, group=None):
+    """Every rank's record (dicts / lists / scalars / numpy arrays) on every rank, through two tensor all-gathers (byte
+    lengths, then the padded byte images) on the group's backend device: no pickles cross the wire."""
+    world = dist.get_world_size(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    data = _encode_record(rec)
+    n = torch.tensor([len(data)], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    cap = int(max(int(x.item()) for x in ns))
+    mine = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    if len(data):
+        mine[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    outs = [torch.zeros(cap, dtype=torch.uint8, device=dev) for _ in range(world)]
+    dist.all_gather(outs, mine, group=group)
+    return [_decode_record(bytes(o[:int(k.item())].cpu().numpy().tobytes())) for o, k in zip(outs, ns)]
+
+
 def table_layout(query, segments, group=None):
     """Everything the ranks of one multi-GPU query must agree on before building their executors, in one all-gather:
     the table-wide dictionary of every dictionary-encoded group-by column (the union over all ranks' segments: the
@@ -311,9 +380,7 @@ def table_layout(query, segments, group=None):
             ds = [s.column(a.column).dictionary for s in segments if s.column(a.column).has_dictionary]
             if ds:
                 local["vals"][a.column] = np.unique(np.concatenate(ds))
-    world = dist.get_world_size(group)
-    gathered = [None] * world
-    dist.all_gather_object(gathered, local, group=group)
+    gathered = all_gather_records(local, group)
     out = TableLayout()
     for name in query.group_by:
         parts = [g["dicts"][name] for g in gathered if name in g["dicts"]]

@@ -1,4 +1,5 @@
 """Host-side logic of the hot path's callers (no GPU): predicate literal parsing and HyperLogLog estimates."""
+import os
 import numpy as np
 import pytest
 
@@ -47,3 +48,22 @@ def test_fractional_bound_on_int_column_is_refused():
     q = parse_sql("SELECT COUNT(*) FROM t WHERE m >= 1.5")
     with pytest.raises(ValueError):
         P.dictionary_leaf(q.filter, seg.column("m"))
+
+
+def test_build_rebuilds_when_any_header_changes(monkeypatch):
+    """build() recompiles when any header under csrc/ (pa_keys.h included) or the JIT kernel source is newer than the
+    library (pinot_amd/build.py _stale): HEADERS is globbed, so a new header is covered without an edit."""
+    from pinot_amd import build as B
+    assert "pa_keys.h" in B.HEADERS and "pa_gdense.h" in B.HEADERS
+    lib_t = 1_000_000.0
+    real_exists = os.path.exists
+
+    def mtime(newer):
+        return lambda p: lib_t if p == B.LIB else (lib_t + 10 if p.endswith(newer) else lib_t - 10)
+
+    monkeypatch.setattr(os.path, "exists", lambda p: True if p == B.LIB else real_exists(p))
+    monkeypatch.setattr(os.path, "getmtime", mtime("no-such-file"))
+    assert not B._stale()
+    for name in ("pa_keys.h", "pa_device.h", "gdl_jit.hip", "pinot_amd.h"):
+        monkeypatch.setattr(os.path, "getmtime", mtime(name))
+        assert B._stale(), name

@@ -636,3 +636,19 @@ def test_gloo_hashed_merge_of_two_word_keys():
         assert docs.tolist() == [10 + r, 0, 0, 0]
         seen += share
     assert sorted(seen) == sorted(exp) and len(exp) == 20 + 20 * world
+
+
+def test_layout_records_round_trip_without_pickle():
+    """table_layout's per-rank record crosses ranks as tensor bytes (JSON header + raw arrays), not pickles: numeric and
+    string dictionaries, nested dicts, lists and scalars survive the round trip."""
+    from pinot_amd.parallel import _decode_record, _encode_record
+    rec = {"dicts": {"d": np.array([3, 1, 2], dtype=np.int64), "s": np.array(["b", "a"], dtype=object)},
+           "vals": {"f": np.array([1.5, -2.0])}, "wide": ["m"], "hb": 12345678901,
+           "schema": {"d": ("INT", True, True)}}
+    out = _decode_record(_encode_record(rec))
+    np.testing.assert_array_equal(out["dicts"]["d"], rec["dicts"]["d"])
+    assert out["dicts"]["d"].dtype == np.int64
+    assert list(out["dicts"]["s"]) == ["b", "a"]
+    np.testing.assert_array_equal(out["vals"]["f"], rec["vals"]["f"])
+    assert out["wide"] == ["m"] and out["hb"] == 12345678901 and tuple(out["schema"]["d"]) == ("INT", True, True)
+    assert b"\x80\x04" not in _encode_record(rec)[:2]  # (not a pickle stream)
