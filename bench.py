@@ -152,6 +152,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=16, help="segments in the CPU baseline sample (0 = skip)")
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--no-secondary", action="store_true", help="skip the widened-IN-list secondary lines")
+    ap.add_argument("--secondary", default="all", help="run only this secondary line (sel_10pct | sel_50pct)")
     args = ap.parse_args()
 
     import torch
@@ -164,7 +165,19 @@ def main():
     distributed = world > 1 or "RANK" in os.environ
     if distributed:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        # RCCL prints its version banner on stdout when the first communicator comes up: send it to stderr, so that
+        # stdout holds only the JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("nccl", device_id=device)
+            dist.barrier()
+            torch.cuda.synchronize()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
     from pinot_amd import parse_sql
     from pinot_amd.engine import GpuQueryExecutor, GpuSegment
@@ -264,6 +277,8 @@ def main():
     if not args.no_secondary:
         from pinot_amd import _lib as L
         for name, n_ids in SECONDARY:
+            if args.secondary not in ("all", name):
+                continue
             sql = secondary_query(n_ids)
             e2 = GpuQueryExecutor(parse_sql(sql), gsegs, flags=args.flags, **kw)
             for _ in range(args.warmup):
@@ -282,6 +297,7 @@ def main():
                 "groups": len(r2.groups) if r2 is not None else None,
                 "roofline": {"bound": "hbm", "achieved": algo / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": algo,
+                             "traffic": load_traffic("adanalytics_in_list_" + name, args.docs, len(gsegs)),
                              "plan": st2["plan"]}})
             e2.close()
 
