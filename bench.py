@@ -50,6 +50,11 @@ def secondary_query(n_ids):
             "AND accountId IN (%s) GROUP BY daysSinceEpoch TOP 100" % (DAY_RANGE + (",".join(map(str, ids)),)))
 
 
+def L_lib():
+    from pinot_amd import _lib
+    return _lib.lib()
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -217,7 +222,20 @@ def main():
         if dacc is not None:
             dacc.reduce(dst=0)
         if rank == 0:
-            return ex.fetch(sptr)
+            return ex.fetch(sptr, execution_stats=False)
+        return None
+
+    def step_with_stats():
+        """The same step plus the DataTable execution statistics every results block carries (BaseResultsBlock.java:194):
+        each rank (server) counts numEntriesScannedInFilter of its own segments after its scan."""
+        ex.execute(sptr)
+        in_filter, _ = ex.execution_stats(sptr, docs_total=0)
+        if dacc is not None:
+            dacc.reduce(dst=0)
+        if rank == 0:
+            r = ex.fetch(sptr, execution_stats=False)
+            r.num_entries_scanned_in_filter = in_filter
+            return r
         return None
 
     for _ in range(args.warmup):
@@ -267,10 +285,23 @@ def main():
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # the stats-inclusive step, timed the same way
+    for _ in range(max(1, args.warmup)):
+        sres = step_with_stats()
     if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        sres = step_with_stats()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed_stats = time.perf_counter() - t1
+    if distributed:
+        t = torch.tensor([elapsed, elapsed_stats], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, elapsed_stats = float(t[0].item()), float(t[1].item())
 
     # secondary lines: the same segments under the widened IN lists (kernel time, roofline on the same byte model)
     secondary = []
@@ -347,6 +378,12 @@ def main():
                 "plan": st["plan"],
             },
             "cpu_baseline": cpu,
+            # the same step with the execution statistics (numEntriesScannedInFilter of every segment: the scan's own
+            # leap counts for this two-scan AND, pa_query_execution_stats)
+            "stats_step": {"ms_per_step": elapsed_stats * 1e3 / args.steps,
+                           "vs_plain_step": elapsed_stats / elapsed,
+                           "num_entries_scanned_in_filter_rank0": sres.num_entries_scanned_in_filter,
+                           "fused": int(L_lib().pa_query_leap_leaf(ex.handle)) >= 0},
             "secondary": secondary,
         }
         if multi is not None:

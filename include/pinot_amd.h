@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define PA_ABI_VERSION 2
+#define PA_ABI_VERSION 3
 
 /* limits of one query shape */
 #define PA_MAX_LEAVES 16
@@ -219,8 +219,9 @@ typedef struct {
 #define PA_QF_NO_DENSE_GROUP (1 << 29)    /* filter + GROUP BY over a small key space: the LDS strategy (post-filter
                                              columns per matching doc from HBM) instead of the dense group-by kernel
                                              (every column staged, value dictionaries and remaps in LDS) */
-#define PA_QF_FILTER_STATS (1 << 30)      /* the scan also counts what the execution statistics of an AND of two scan
-                                             leaves need (pa_query_leap_leaf / pa_query_leap_counts) */
+#define PA_QF_NO_FILTER_STATS (1 << 30)   /* the scan does NOT count what the execution statistics of an AND of two scan
+                                             leaves need (by default it does wherever that fused count applies:
+                                             pa_query_leap_leaf / pa_query_leap_counts / pa_query_execution_stats) */
 #define PA_QF_PART_SHIFT 22              /* bits 22..23: LDS per partition of the partitioned aggregation (0 = auto,
                                              1 = 64 KiB, 2 = 96 KiB, 3 = 144 KiB): larger partitions = fewer record
                                              write fronts per XCD */
@@ -354,7 +355,47 @@ int pa_query_filter_counts(pa_query* q, int32_t num_requests, const int32_t* seg
  * pa_query_leap_counts writes out[3 s .. 3 s + 2] = (matched docs, leaps, 1 if the segment's counts are unavailable:
  * a neighbour search of the fused count gave up) for every bound segment s of the last scan (synchronises `stream`). */
 int32_t pa_query_leap_leaf(const pa_query* q);
-int pa_query_leap_counts(const pa_query* q, int64_t* out, void* stream);
+int pa_query_leap_counts(pa_query* q, int64_t* out, void* stream);
+
+/* Execution statistics of the DataTable (BaseResultsBlock.java:194 puts them in every results block):
+ * numEntriesScannedInFilter / numEntriesScannedPostFilter of the bound segments after the last scan.
+ *
+ * The host passes the filter operator tree the reference builds for each segment (FilterPlanNode +
+ * FilterOperatorUtils.getLeafFilterOperator / getAndFilterOperator / getOrFilterOperator: leaf operator choice from the
+ * segment's indexes, constant children removed, AND children in reorderAndFilterChildOperators order), as pa_filter_op
+ * nodes in pre-order; ops[tree_root[t] ..] is tree t. segment_tree[s] = the tree of bound segment s, or
+ * PA_STATS_NON_SCAN (AggregationPlanNode's non-scan plans: neither count), PA_STATS_HOST (the host accounts for the
+ * segment itself). The library derives what the reference's iterators read when the projection drives the tree's
+ * iterator to the end (SVScanDocIdIterator / MVScanDocIdIterator next, advance and applyAnd; AndDocIdSet's merge of index
+ * children; AndDocIdIterator's leap-frog, OrDocIdIterator, NotDocIdIterator) — constants, popcounts of applyAnd chains
+ * and leap-frogs counted on the GPU over the segments' leaf bitmaps (pa_stats.hip) — or, when the scan counted a
+ * two-scan AND itself (PA_QF_NO_FILTER_STATS unset), those counts.
+ * out[0] = numEntriesScannedInFilter over the segments the library covered, out[1] = numEntriesScannedPostFilter =
+ * (docs_scanned - docs of PA_STATS_NON_SCAN segments) x projected_columns (docs_scanned: numDocsScanned of the scan,
+ * < 0 = the one the last pa_query_fetch read), out[2] = segments whose count ran on the GPU. segment_in_filter[s]
+ * (optional, host int64[num_segments]) = segment s's numEntriesScannedInFilter, or -1 for a segment the host must
+ * account for (PA_STATS_HOST, or a tree shape outside the engine: a NOT child of a leap-frogging AND, an AND or NOT
+ * child of an OR child of one). Synchronises `stream`. */
+#define PA_FOP_EMPTY 0     /* EmptyFilterOperator */
+#define PA_FOP_MATCH_ALL 1 /* MatchAllFilterOperator */
+#define PA_FOP_SORTED 2    /* SortedIndexBasedFilterOperator (prog: its doc set) */
+#define PA_FOP_BITMAP 3    /* BitmapBasedFilterOperator / RangeIndexBasedFilterOperator (exact) */
+#define PA_FOP_SCAN 4      /* ScanBasedFilterOperator; mv_column >= 0: over that multi-value column */
+#define PA_FOP_AND 5
+#define PA_FOP_OR 6
+#define PA_FOP_NOT 7
+#define PA_STATS_NON_SCAN (-1)
+#define PA_STATS_HOST (-2)
+typedef struct {
+  int32_t kind;          /* PA_FOP_* */
+  int32_t num_children;  /* AND / OR: >= 2, NOT: 1, leaves: 0; the children follow in pre-order */
+  int32_t mv_column;     /* PA_FOP_SCAN: column id of a multi-value column (-1: single-value) */
+  int32_t prog_len;      /* leaves: the operator's doc set as a postfix program over the query's filter leaves */
+  int32_t prog[PA_BIT_PROG_MAX];  /* (pa_bitmap_counts tokens) */
+} pa_filter_op;
+int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* ops, int32_t num_trees,
+                             const int32_t* tree_root, const int32_t* segment_tree, int32_t projected_columns,
+                             int64_t docs_scanned, int64_t* out, int64_t* segment_in_filter, void* stream);
 
 /* Cross-GPU merge of hashed key spaces (parallel.merge_hashed_sections around one all-to-all). A row is one slot of
  * every per-key accumulator section (the numDocsScanned counters excluded) in section order: pa_query_row_bytes(q)

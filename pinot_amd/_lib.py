@@ -42,12 +42,14 @@ PA_QF_NO_LANE_ACC = 1 << 26
 PA_QF_NO_LANE_HIST = 1 << 27
 PA_QF_LAZY_POST = 1 << 28
 PA_QF_NO_DENSE_GROUP = 1 << 29
-PA_QF_FILTER_STATS = 1 << 30
+PA_QF_NO_FILTER_STATS = 1 << 30
+PA_FOP_EMPTY, PA_FOP_MATCH_ALL, PA_FOP_SORTED, PA_FOP_BITMAP, PA_FOP_SCAN, PA_FOP_AND, PA_FOP_OR, PA_FOP_NOT = range(8)
+PA_STATS_NON_SCAN, PA_STATS_HOST = -1, -2
 PA_BIT_AND, PA_BIT_OR, PA_BIT_NOT = -1, -2, -3
 PA_BIT_PROG_MAX = 64
 PA_ACC_COUNT_U64, PA_ACC_SUM_I64, PA_ACC_SUM_F64, PA_ACC_MIN_I64, PA_ACC_MAX_I64, PA_ACC_HLL_U8, \
     PA_ACC_SUM_I64X2, PA_ACC_DOCS_U64, PA_ACC_KEYS_I64, PA_ACC_PRESENCE_U8 = range(10)
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # every symbol declared in include/pinot_amd.h
 EXPORTED = [
@@ -62,6 +64,7 @@ EXPORTED = [
     "pa_query_num_groups_limit_reached", "pa_query_stats", "pa_query_leaf_bitmap_words", "pa_query_leaf_bitmaps",
     "pa_bitmap_counts_scratch_bytes", "pa_bitmap_counts", "pa_query_filter_counts",
     "pa_query_plan", "pa_query_column_staged", "pa_query_leap_leaf", "pa_query_leap_counts",
+    "pa_query_execution_stats",
     "pa_query_row_bytes", "pa_query_pack_rows", "pa_query_merge_rows", "pa_query_key_words", "pa_query_destroy",
 ]
 
@@ -157,6 +160,7 @@ def _declare(lib):
         "pa_query_column_staged": (i32, [vp, i32]),
         "pa_query_leap_leaf": (i32, [vp]),
         "pa_query_leap_counts": (ctypes.c_int, [vp, vp, vp]),
+        "pa_query_execution_stats": (ctypes.c_int, [vp, i32, vp, i32, vp, vp, i32, i64, vp, vp, vp]),
         "pa_query_row_bytes": (i64, [vp]),
         "pa_query_key_words": (i32, [vp]),
         "pa_query_pack_rows": (ctypes.c_int, [vp, i32, vp, vp, vp]),

@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libpinot_amd.so")
-SOURCES = ["pa_scan_part_a.hip", "pa_scan_part_b.hip", "pa_scan_part_mv.hip", "pa_scan_std.hip", "pa_scan_lane.hip", "pa_scan_gdense.hip", "pa_kernels.hip", "pa_merge.hip", "pa_capi.hip"]
+SOURCES = ["pa_scan_part_a.hip", "pa_scan_part_b.hip", "pa_scan_part_mv.hip", "pa_scan_std.hip", "pa_scan_lane.hip", "pa_scan_gdense.hip", "pa_kernels.hip", "pa_merge.hip", "pa_stats.hip", "pa_capi.hip"]
 # every header under csrc/ (globbed, so a new one is covered without an edit here) and the public C-ABI header
 HEADERS = sorted(f for f in os.listdir(CSRC) if f.endswith(".h")) + [os.path.join("..", "..", "include", "pinot_amd.h")]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-munsafe-fp-atomics", "-std=c++17",

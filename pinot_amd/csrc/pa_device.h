@@ -312,7 +312,7 @@ struct DevQuery {
   int32_t gd_lut[PA_MAX_LEAVES];
   int32_t gd_lut_words[PA_MAX_LEAVES];
   const uint32_t* gd_plans;          // [num_segments][64]: GdSegPlan of every segment
-  // fused execution statistics (PA_QF_FILTER_STATS, leap_tile + leap_search_kernel): 1 = literal 0 (eager, E) and
+  // fused execution statistics (default unless PA_QF_NO_FILTER_STATS, leap_tile + leap_search_kernel): 1 = literal 0 (eager, E) and
   // literal 1 (lazy, Z) are the two scan leaves of an AND
   int32_t leap_mode;
   int32_t pad_leap;

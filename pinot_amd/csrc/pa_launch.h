@@ -131,6 +131,43 @@ hipError_t launch_merge_rows(const RowDesc& d, const unsigned char* rows, int64_
 // fused execution statistics: the neighbour searches of the E docs the scan listed (DevQuery::leap_mode)
 hipError_t launch_leap_search(const DevQuery* q, const DevSeg* segs, int64_t slices, hipStream_t s);
 constexpr int64_t kLeapMaxSlices = 16384;  // fused statistics: list slices (scan waves) the search kernel scans in LDS
+// Execution statistics engine (pa_stats.hip): element masks (postfix programs over one segment's leaf bitmaps),
+// popcounts / value counts of masks, and leap-frogs of AndDocIdIterator over element masks
+constexpr int kStatMaskWordsPerThread = 4;
+constexpr int kLfMaxK = 8;      // children of one leap-frogging AND
+constexpr int kLfMaxSub = 8;    // scan / index children of its OR children, together
+constexpr int64_t kLfChunkDocs = 2048;
+enum : int32_t { LF_DOCS = 0, LF_SCAN = 1, LF_OR = 2 };
+struct StatMaskJob {  // workgroups [first_block, + stat_mask_blocks(words))
+  const uint32_t* bm;  // leaf l at bm + l * words
+  uint32_t* out;
+  int64_t words, num_docs, first_block;
+  int32_t tok_off, len;  // the program at toks[tok_off .. + len)
+};
+struct StatCountJob {
+  const uint32_t* mask;
+  const int32_t* wt;  // multi-value column: offsets[num_docs + 1] (a doc counts its values); nullptr: docs
+  unsigned long long* out;
+  int64_t words, first_block;
+};
+struct LfJob {
+  int32_t K, nsub;
+  int32_t kind[kLfMaxK];                        // LF_DOCS, LF_SCAN, LF_OR
+  int32_t sub_first[kLfMaxK], sub_count[kLfMaxK];  // LF_OR: its children at [sub_first, + sub_count)
+  int32_t sub_kind[kLfMaxSub];                  // LF_DOCS or LF_SCAN
+  int32_t cell_words, pad;                      // 4 + 2 nsub
+  const uint32_t* emask[kLfMaxK];
+  const int32_t* ewt[kLfMaxK];                  // multi-value scan: value offsets; nullptr: one entry per doc
+  const uint32_t* smask[kLfMaxSub];
+  const int32_t* swt[kLfMaxSub];
+  int64_t num_docs, nchunks, first_lane;        // lanes [first_lane, + nchunks (K + 1)) of lf_chunk_kernel
+  uint32_t* cells;                              // [nchunks][K + 1][cell_words]
+  unsigned long long* out;                      // [0] entries read, [1] read after the last match, [2] matches
+};
+int64_t stat_mask_blocks(int64_t words);
+hipError_t launch_stat_masks(const StatMaskJob* jobs, int nj, int64_t blocks, const int32_t* toks, hipStream_t s);
+hipError_t launch_stat_counts(const StatCountJob* jobs, int nj, int64_t blocks, hipStream_t s);
+hipError_t launch_leapfrogs(const LfJob* jobs, int nj, int64_t lanes, hipStream_t s);
 hipError_t set_scan_lds_limit(int strategy, int steps, int lm, int bytes);
 hipError_t scan_occupancy(int strategy, int steps, int lm, int lds_bytes, int* blocks_per_cu);
 hipError_t launch_scan(int strategy, int steps, int lm, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs,

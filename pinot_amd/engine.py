@@ -606,8 +606,8 @@ class GpuQueryExecutor:
 
     def fused_leap_counts(self, stream=None):
         """(E leaf, Z leaf, int64[segments, 3]) when the last scan counted the execution statistics of its two-leaf AND
-        itself (flags PA_QF_FILTER_STATS, pa_query_leap_counts: per segment matched docs, leaps of AndDocIdIterator(A = Z,
-        B = E), gave-up flag), else None. Synchronises `stream`."""
+        itself (the default where it applies; PA_QF_NO_FILTER_STATS turns it off. pa_query_leap_counts: per segment
+        matched docs, leaps of AndDocIdIterator(A = Z, B = E), gave-up flag), else None. Synchronises `stream`."""
         lib = L.lib()
         if self.handle is None or not self.segs or not getattr(self, "_scanned", False):
             return None
@@ -619,22 +619,39 @@ class GpuQueryExecutor:
         return e, 1 - e, out
 
     def execution_stats(self, stream=None, docs_total=None):
-        """(numEntriesScannedInFilter, numEntriesScannedPostFilter) of this server's segments: the reference's
-        operator accounting (filter_stats.py), closed forms over counts the GPU takes from its leaf bitmaps
-        (pa_bitmap_counts), the iterator replay over host bitmaps only for operator trees without one."""
+        """(numEntriesScannedInFilter, numEntriesScannedPostFilter) of this server's segments after the last scan: the
+        reference's operator accounting counted by the library (pa_query_execution_stats) over the operator trees this
+        host builds per segment (filter_stats.operator_trees = FilterOperatorUtils). Segments whose tree the engine
+        does not express (filter_stats "device path") replay the iterators on the host over GPU leaf bitmaps;
+        self.stats_replayed_segments counts them. docs_total: numDocsScanned of the scan (default: the last fetch's)."""
         from . import filter_stats as FS
-        if self.match_none:
+        self.stats_replayed_segments = self.stats_gpu_segments = 0
+        if self.match_none or self.handle is None or not self.segs:
             return 0, 0  # EmptyFilterOperator: no entry read, no doc projected
-        if docs_total is None:  # numDocsScanned of the last fetch (< 0: none yet)
-            docs_total = int(L.lib().pa_query_matched_docs(self.handle))
-        if getattr(self, "_stats_plan", None) is None:  # the operator trees of this prepared query, planned once
-            self._stats_plan = FS.plan_stats(self.query, self.segs, getattr(self, "leaf_params", None))
-        return FS.server_stats_device(self.query, self.segs, self, stream, docs_total if docs_total >= 0 else None,
-                                      self._stats_plan)
+        if getattr(self, "_stats_trees", None) is None:  # the operator trees of this prepared query, built once
+            self._stats_trees = FS.operator_trees(self.query, self.segs, getattr(self, "leaf_params", None),
+                                                  self.gsegs[0].column_ids)
+        ops, roots, seg_tree = self._stats_trees
+        out = np.zeros(3, dtype=np.int64)
+        per = np.zeros(len(self.segs), dtype=np.int64)
+        L.check(L.lib().pa_query_execution_stats(
+            self.handle, len(ops), ops.ctypes.data, len(roots), roots.ctypes.data, seg_tree.ctypes.data,
+            FS.projected_columns(self.query), -1 if docs_total is None else int(docs_total), out.ctypes.data,
+            per.ctypes.data, stream), "pa_query_execution_stats")
+        in_filter, post = int(out[0]), int(out[1])
+        self.stats_gpu_segments = int(out[2])  # segments whose statistics took a GPU pass (not the scan's own counts)
+        host = np.flatnonzero(per < 0).tolist()
+        if host:
+            self.stats_replayed_segments = len(host)
+            hi, _ = FS.server_stats(self.query, [self.segs[i] for i in host],
+                                    lambda i: self.leaf_bitmaps(host[i], stream))
+            in_filter += hi
+        return in_filter, post
 
-    def fetch(self, stream=None, execution_stats=False) -> IntermediateResult:
-        """execution_stats=True also fills numEntriesScannedInFilter / PostFilter (one leaf-bitmap pass and a few
-        count kernels per segment on the GPU, one synchronisation: execution_stats)."""
+    def fetch(self, stream=None, execution_stats=True) -> IntermediateResult:
+        """The results block of the last scan. Like the reference's results blocks (BaseResultsBlock.java:194) it carries
+        the execution statistics — numEntriesScannedInFilter / PostFilter from pa_query_execution_stats, after the groups
+        (execution_stats): execution_stats=False leaves them 0."""
         lib = L.lib()
         q = self.query
         if self.handle is None:

@@ -335,7 +335,9 @@ def _leaf_op(pred, seg, mask, index_info, lf=None):
         # segment here is taken to have; FilterOperatorUtils.java:127-130)
         return _Op("bitmap", LOW, mask)
     weights = None if sv else col.mv_lengths(seg.num_docs)
-    return _Op("scan", SCAN_P + (0 if sv else 50), mask, weights=weights)
+    op = _Op("scan", SCAN_P + (0 if sv else 50), mask, weights=weights)
+    op.column = pred.column
+    return op
 
 
 def _build(f, seg, cursor, index_info):
@@ -497,19 +499,14 @@ def server_stats(query, segments, leaf_bitmaps):
     return in_filter, post
 
 
-# ------------------------------------------------------------------ device path: closed forms over GPU counts
-# The iterator replay above is O(matching docs) on the host. The projection's iteration has closed forms for the
-# operator trees queries usually have, whose inputs are counts over the leaf bitmaps that the GPU computes without
-# moving the bitmaps (pa_bitmap_counts):
-#   * a scan iterator driven by next() to EOF reads every entry: num_docs (SV), the column's value count (MV);
-#     OR / NOT children are driven by next() to EOF too, so their costs add (NOT calls its child's next() once past
-#     EOF: free for every iterator but a leap-frogging AND);
-#   * AND with index-based children (AndDocIdSet.java:92-140): each SV scan child's applyAnd reads the docs that survive
-#     the index children and the scan children before it: popcounts of AND chains;
-#   * AND of two SV scan iterators leap-frogged by AndDocIdIterator: every advance(t) reads [t, next match of the
-#     advancing iterator], so the reads telescope to num_docs - matches + advance calls - 1, and the advance calls are
-#     2 per match + 1 + the leaps (pa_bitmap_counts): num_docs + popcount(A & B) + leaps.
-# Other shapes (an AND leap-frogging an OR / NOT / a third iterator, MV applyAnd) keep the host replay.
+# ------------------------------------------------------------------ device path: pa_query_execution_stats
+# The replay above is O(matching docs) on the host. The library counts the same entries on the GPU from the operator
+# trees this host builds (pa_query_execution_stats: constants for scans driven to EOF, popcounts of AndDocIdSet's
+# applyAnd chains, AndDocIdIterator leap-frogs simulated per 2048-doc chunk and chained per segment, NotDocIdIterator's
+# re-run of a leap-frog's last chain; pa_stats.hip). The replay stays for the shapes outside that engine: a NOT child of
+# a leap-frogging AND (NotDocIdIterator mixes next() batches and advance() on its child), an AND or NOT child of an OR
+# child of one, a NOT over a leap-frog with an OR child (the re-run after the end starts from the OR children's cached
+# answers), raw IN lists longer than a bitmap program, and inexact (v1) range indexes.
 class _Unsupported(Exception):
     pass
 
@@ -552,84 +549,6 @@ class _RpnCursor(_LeafCursor):
         return lf if isinstance(lf, DictLeaf) else None
 
 
-def _and_prog(progs):
-    out = list(progs[0])
-    for p in progs[1:]:
-        out += list(p) + [L.PA_BIT_AND]
-    return out
-
-
-class _Terms:
-    """A count as constant + sum of coef * (request field); requests are (program A, program B) of one segment."""
-
-    def __init__(self, const=0):
-        self.const, self.terms = const, []
-
-    def add(self, other):
-        self.const += other.const
-        self.terms += other.terms
-        return self
-
-    def request(self, reqs, si, a, b, field, coef=1):
-        if len(a) > L.PA_BIT_PROG_MAX or len(b) > L.PA_BIT_PROG_MAX:
-            raise _Unsupported("bitmap program too long")
-        key = (si, tuple(a), tuple(b))
-        if key not in reqs:
-            reqs[key] = len(reqs)
-        self.terms.append((reqs[key], field, coef))
-        return self
-
-    def value(self, counts):
-        v = self.const
-        for r, f, c in self.terms:
-            x = int(counts[r, f])
-            if x < 0:
-                raise RuntimeError("internal: count field %d of request %d not computed" % (f, r))
-            v += x * c
-        return v
-
-
-def _cost_next(op, seg, si, reqs):
-    """numEntriesScannedInFilter of op's iterator driven by next() to EOF, as _Terms."""
-    n = seg.num_docs
-    if op.kind in ("empty", "all", "sorted", "bitmap"):
-        return _Terms(0)
-    if op.kind == "scan":
-        return _Terms(n if op.weights is None else int(np.sum(op.weights, dtype=np.int64)))
-    if op.kind == "not":
-        c = op.children[0]
-        if c.kind == "and" and not any(k.kind in ("sorted", "bitmap") for k in c.children):
-            # NotDocIdIterator.next() calls its child's next() once more after EOF: an AndDocIdIterator re-runs its
-            # last leap-frog chain then (no closed form kept for that tail)
-            raise _Unsupported("NOT over a leap-frogging AND")
-        return _cost_next(c, seg, si, reqs)
-    if op.kind == "or":
-        t = _Terms(0)
-        for c in op.children:
-            t.add(_cost_next(c, seg, si, reqs))
-        return t
-    # AND: the iterator construction of _iterator / AndDocIdSet
-    kids = op.children
-    index = [c for c in kids if c.kind == "sorted"] + [c for c in kids if c.kind == "bitmap"]
-    scans = [c for c in kids if c.kind == "scan"]
-    rest = [c for c in kids if c.kind not in ("sorted", "bitmap", "scan")]
-    if (index and scans) or len(index) > 1:
-        if rest:
-            raise _Unsupported("AND leap-frogs a merged index set with other iterators")
-        t = _Terms(0)
-        docs = _and_prog([c.mask for c in index])
-        for s in scans:
-            if s.weights is not None:
-                raise _Unsupported("MV applyAnd")
-            t.request(reqs, si, docs, [], 0)
-            docs = _and_prog([docs, s.mask])
-        return t
-    if len(kids) == 2 and all(c.kind == "scan" and c.weights is None for c in kids):
-        return _Terms(n).request(reqs, si, kids[0].mask, kids[1].mask, 2).request(reqs, si, kids[0].mask,
-                                                                                    kids[1].mask, 3)
-    raise _Unsupported("AND leap-frogging other than two SV scans")
-
-
 def _filter_columns(f):
     if isinstance(f, (Q.And, Q.Or)):
         return set().union(*[_filter_columns(c) for c in f.children])
@@ -640,261 +559,84 @@ def _filter_columns(f):
 
 def _tree_signature(seg, fcols, params):
     """Everything _build reads from a segment (the bound leaf parameters, each filter column's dictionary size,
-    sortedness and indexes), or None when the tree must be built per segment (no bound parameters; MV columns, whose
-    scan costs are per-doc value counts). Segments with equal signatures share one operator tree, so this key must list
-    EVERY segment attribute _build / _leaf_op read (index_info included): a new per-segment input of the leaf operator
-    choice goes here too, or trees leak across segments."""
+    sortedness, indexes and single-/multi-value), or None when the tree must be built per segment (no bound
+    parameters). Segments with equal signatures share one operator tree, so this key must list EVERY segment attribute
+    _build / _leaf_op read (index_info included): a new per-segment input of the leaf operator choice goes here too, or
+    trees leak across segments."""
     if params is None:
         return None
     cols = []
     for name in fcols:
         c = seg.column(name)
-        if not c.single_value:
-            return None
-        cols.append((c.has_dictionary, c.cardinality if c.has_dictionary else 0, bool(c.is_sorted),
-                     bool(getattr(c, "inverted_index", False)), bool(getattr(c, "range_index", False)),
-                     bool(getattr(c, "range_index_exact", True))))
+        cols.append((bool(c.single_value), c.has_dictionary, c.cardinality if c.has_dictionary else 0,
+                     bool(c.is_sorted), bool(getattr(c, "inverted_index", False)),
+                     bool(getattr(c, "range_index", False)), bool(getattr(c, "range_index_exact", True))))
     leaves = tuple((p.kind, p.lo, p.hi, bool(p.negate), None if p.ids is None else len(np.unique(p.ids)))
                    if isinstance(p, DictLeaf) else None for p in params)
     return leaves, tuple(cols)
 
 
-class _StatsPlan:
-    """The per-segment operator trees of one query over one segment set, reduced to what the statistics need: per
-    segment None (non-scan plan), "host" (replay) or (in-filter _Terms, docs program, constant docs _Terms), the
-    requests of the in-filter terms, and — built on first use — the full request set with the docs requests and the
-    terms as flat arrays (one numpy gather evaluates every segment). GpuQueryExecutor keeps it across executions of
-    its prepared query (the trees depend on the query and the segments, not on a scan's results)."""
-
-    def __init__(self, ncols, plans, reqs):
-        self.ncols, self.plans, self.reqs = ncols, plans, reqs
-        self.full = None
-        self.fused_cache = {}  # fused_counts' classification of the full request set
-
-    def constant_value(self):
-        """in-filter entries when every segment's filter cost is a constant (no request at all), else None."""
-        if self.reqs or not all(p is not None and p != "host" for p in self.plans):
-            return None
-        return sum(p[0].value(None) for p in self.plans)
-
-    def flat(self):
-        if self.full is None:
-            reqs = dict(self.reqs)
-            plans = list(self.plans)
-            for si, p in enumerate(plans):
-                if isinstance(p, tuple):
-                    try:
-                        plans[si] = (p[0], p[2] if p[1] is None else _Terms(0).request(reqs, si, p[1], [], 0))
-                    except _Unsupported:
-                        plans[si] = "host"
-            const_in = const_docs = 0
-            ti, td = [], []
-            for p in plans:
-                if p is None or p == "host":
-                    continue
-                const_in += p[0].const
-                const_docs += p[1].const
-                ti += p[0].terms
-                td += p[1].terms
-            arr = lambda t: (np.array([x[0] for x in t], dtype=np.int64), np.array([x[1] for x in t], dtype=np.int64),
-                             np.array([x[2] for x in t], dtype=np.int64))
-            host = [si for si, p in enumerate(plans) if p == "host"]
-            self.full = (reqs, const_in, arr(ti), const_docs, arr(td), host)
-        return self.full
-
-    def fused_form(self, e, z, nseg):
-        """The statistics as linear forms of the counts the scan took itself (fused_counts' per-segment matched docs m
-        and leaps l): in_filter = const_in + A.m + B.l, post = (const_docs + C.m) x ncols — or None when some request
-        is not one the scan covers (then fused_counts + the closed forms run). Cached per (E leaf, Z leaf)."""
-        key = ("form", e, z)
-        if key not in self.fused_cache:
-            reqs, const_in, (ri, fi, ci), const_docs, (rd, fd, cd), host = self.flat()
-            form = None
-            if not host and self.reqs:  # (no request: a constant-cost filter, server_stats_closed_form's shortcut)
-                row = {}  # request row -> (segment, kind): 0 the AND request, 1 the whole-filter request
-                ok = True
-                for (si, a, b), r in reqs.items():
-                    if a == (z,) and b == (e,):
-                        row[r] = (si, 0)
-                    elif not b and a in ((z, e, L.PA_BIT_AND), (e, z, L.PA_BIT_AND)):
-                        row[r] = (si, 1)
-                    else:
-                        ok = False
-                A, B, C = (np.zeros(nseg, dtype=np.int64) for _ in range(3))
-                for rows, fields, coef, dst in ((ri, fi, ci, "in"), (rd, fd, cd, "docs")):
-                    for r, f, c in zip(rows.tolist(), fields.tolist(), coef.tolist()):
-                        si, kind = row.get(r, (None, None))
-                        if si is None:
-                            ok = False
-                        elif kind == 0 and f == 2:  # popcount(A & B) = the segment's matched docs
-                            (A if dst == "in" else C)[si] += c
-                        elif kind == 0 and f == 3 and dst == "in":  # leaps
-                            B[si] += c
-                        elif kind == 1 and f == 0:  # the whole filter's popcount = matched docs
-                            (A if dst == "in" else C)[si] += c
-                        else:
-                            ok = False
-                if ok:
-                    form = (int(const_in), A, B, int(const_docs), C)
-            self.fused_cache[key] = form
-        return self.fused_cache[key]
+OP_WORDS = 4 + L.PA_BIT_PROG_MAX  # int32 words of one pa_filter_op
+_FOP = {"empty": L.PA_FOP_EMPTY, "all": L.PA_FOP_MATCH_ALL, "sorted": L.PA_FOP_SORTED, "bitmap": L.PA_FOP_BITMAP,
+        "scan": L.PA_FOP_SCAN, "and": L.PA_FOP_AND, "or": L.PA_FOP_OR, "not": L.PA_FOP_NOT}
 
 
-def plan_stats(query, segments, leaf_params=None):
-    """_StatsPlan of `query` over `segments` (server_stats_closed_form's planning half)."""
-    ncols = projected_columns(query)
+def _encode(op, rows, column_ids):
+    """op in pre-order as pa_filter_op rows (int32[OP_WORDS] each)."""
+    r = np.zeros(OP_WORDS, dtype=np.int32)
+    r[0] = _FOP[op.kind]
+    r[1] = len(op.children)
+    r[2] = -1
+    if op.kind == "scan" and op.weights is not None:
+        r[2] = column_ids[op.column]
+    if op.kind in ("sorted", "bitmap", "scan"):
+        if len(op.mask) > L.PA_BIT_PROG_MAX:
+            raise _Unsupported("doc-set program too long")
+        r[3] = len(op.mask)
+        r[4:4 + len(op.mask)] = op.mask
+    rows.append(r)
+    for c in op.children:
+        _encode(c, rows, column_ids)
+
+
+def operator_trees(query, segments, leaf_params=None, column_ids=None):
+    """The reference's filter operator tree of every segment (FilterPlanNode + FilterOperatorUtils: _build), encoded for
+    pa_query_execution_stats: (ops int32[num_ops, OP_WORDS], tree_root int32[trees], segment_tree int32[segments]) —
+    segment_tree[i] a tree index, PA_STATS_NON_SCAN (AggregationPlanNode's non-scan plans) or PA_STATS_HOST (a leaf the
+    engine cannot express: the host replays that segment). Segments with equal trees share one."""
     filt = query.filter
-    reqs = {}
-    plans = []  # per segment: None (non-scan plan), "host", or (in_filter _Terms, docs program, constant docs _Terms)
     flat = _flatten(filt) if filt is not None else None
     fcols = sorted(_filter_columns(filt)) if filt is not None else []
-    trees = {}  # operator tree + docs program per segment signature (segments of a table usually share one)
+    rows, roots, seg_tree = [], [], []
+    by_bytes, by_sig = {}, {}
+
+    def add(op):
+        enc = []
+        _encode(op, enc, column_ids or {})
+        key = np.stack(enc).tobytes()
+        if key not in by_bytes:
+            by_bytes[key] = len(roots)
+            roots.append(len(rows))
+            rows.extend(enc)
+        return by_bytes[key]
+
     for si, seg in enumerate(segments):
-        if filt is None:
-            plans.append(None if non_scan_plan(query, seg, True) else (_Terms(0), None, _Terms(seg.num_docs)))
-            continue
         try:
-            params = None if leaf_params is None else leaf_params[si]
-            key = _tree_signature(seg, fcols, params)
-            if key is None or key not in trees:
-                tree = (_build(flat, seg, _RpnCursor(seg, params), segment_index_info(seg)),
-                        _rpn(expand_raw_in(filt, seg), 0))
-                if key is not None:
-                    trees[key] = tree
-            else:
-                tree = trees[key]
-            op, docs_prog = tree
-            if non_scan_plan(query, seg, op.kind == "all"):
-                plans.append(None)
+            if filt is None:
+                seg_tree.append(L.PA_STATS_NON_SCAN if non_scan_plan(query, seg, True) else add(_Op("all")))
                 continue
-            cost = _Terms(0) if op.kind in ("empty", "all") else _cost_next(op, seg, si, reqs)
-            plans.append((cost, docs_prog, None))
+            params = None if leaf_params is None else leaf_params[si]
+            sig = _tree_signature(seg, fcols, params)
+            if sig is not None and sig in by_sig:
+                seg_tree.append(by_sig[sig])
+                continue
+            op = _build(flat, seg, _RpnCursor(seg, params), segment_index_info(seg))
+            t = L.PA_STATS_NON_SCAN if non_scan_plan(query, seg, op.kind == "all") else add(op)
+            if sig is not None:
+                by_sig[sig] = t
+            seg_tree.append(t)
         except _Unsupported:
-            plans.append("host")
-    return _StatsPlan(ncols, plans, reqs)
-
-
-def server_stats_closed_form(query, segments, counts_fn, leaf_bitmaps, leaf_params=None, docs_total=None, plan=None):
-    """server_stats through the closed forms above. counts_fn(reqs) -> int64[len(reqs), 4]: for every request
-    (segment index, program A, program B) -> row, pa_bitmap_counts' four counts. Segments without a closed form replay
-    the iterators over leaf_bitmaps(i) (host bitmaps, as server_stats). leaf_params[i]: segment i's bound leaf
-    parameters in leaf order (GpuQueryExecutor.leaf_params), reused instead of re-matching the dictionaries.
-    docs_total: the scan's numDocsScanned over these segments, if known. When every segment's filter cost is a constant
-    (a scan driven to EOF reads every entry; OR / NOT of scans; index-served operators read none) the post-filter count
-    is docs_total x projected columns and counts_fn is never called: no pass over the filter columns.
-    plan: a _StatsPlan of this query and these segments (plan_stats) to reuse; built here when None."""
-    if plan is None:
-        plan = plan_stats(query, segments, leaf_params)
-    if docs_total is not None:
-        c = plan.constant_value()
-        if c is not None:
-            return c, int(docs_total) * plan.ncols
-    reqs, const_in, (ri, fi, ci), const_docs, (rd, fd, cd), host = plan.flat()
-    counts = counts_fn(reqs) if reqs else np.zeros((0, 4), dtype=np.int64)
-    vi, vd = counts[ri, fi], counts[rd, fd]
-    if (vi < 0).any() or (vd < 0).any():
-        raise RuntimeError("internal: a count the closed forms need was not computed")
-    in_filter = const_in + _exact_dot(vi, ci)
-    post = (const_docs + _exact_dot(vd, cd)) * plan.ncols
-    if host:
-        hi, hp = server_stats(query, [segments[si] for si in host], lambda i: leaf_bitmaps(host[i]))
-        in_filter += hi
-        post += hp
-    return in_filter, post
-
-
-def _exact_dot(v, c):
-    """sum(v * c) as a Python int: int64 arithmetic when the magnitude bound keeps it exact, else object arithmetic."""
-    if not len(v):
-        return 0
-    if float(np.abs(v).max()) * float(np.abs(c).sum()) < 2.0 ** 62:
-        return int(np.dot(v.astype(np.int64), c.astype(np.int64)))
-    return int(np.dot(v.astype(object), c.astype(object)))
-
-
-def device_counts(executor, segments, reqs, stream=None):
-    """pa_bitmap_counts' four counts for every request (segment index, program A, program B): one
-    pa_query_filter_counts call (leaf bitmaps of every requested segment, then the count kernels, one launch each)."""
-    n = len(reqs)
-    pm = L.PA_BIT_PROG_MAX
-    segs = np.zeros(n, dtype=np.int32)
-    progs = np.zeros((n, 2, pm), dtype=np.int32)
-    lens = np.zeros((n, 2), dtype=np.int32)
-    for (si, a, b), r in reqs.items():
-        segs[r] = si
-        progs[r, 0, :len(a)] = a
-        progs[r, 1, :len(b)] = b
-        lens[r] = (len(a), len(b))
-    out = np.zeros((n, 4), dtype=np.int64)
-    L.check(L.lib().pa_query_filter_counts(executor.handle, n, segs.ctypes.data, progs.ctypes.data, lens.ctypes.data,
-                                           out.ctypes.data, stream), "pa_query_filter_counts")
-    return out
-
-
-def fused_counts(reqs, fused, fallback, cache=None):
-    """counts_fn rows from the counts the scan took itself (GpuQueryExecutor.fused_leap_counts: E leaf, Z leaf, per
-    segment matched docs / leaps / gave-up): the AND request (A = [Z], B = [E]) gets popcount(A & B) = the segment's
-    matched docs and the leaps, the post-filter request (the whole filter, no B) its popcount = the matched docs. Other
-    requests, and segments whose fused count gave up, go to fallback(reqs) (device_counts). Unknown fields are -1.
-    cache: a dict kept with the requests (their classification is the same for every execution)."""
-    e, z, arr = fused
-    cls = None if cache is None else cache.get((e, z))
-    if cls is None:
-        rows = {0: [], 1: []}  # 0: AND requests, 1: whole-filter requests -> (row, segment)
-        other = []
-        for key, r in reqs.items():
-            si, a, b = key
-            if a == (z,) and b == (e,):
-                rows[0].append((r, si))
-            elif not b and a in ((z, e, L.PA_BIT_AND), (e, z, L.PA_BIT_AND)):
-                rows[1].append((r, si))
-            else:
-                other.append(key)
-        cls = tuple(np.array(rows[k], dtype=np.int64).reshape(-1, 2) for k in (0, 1)) + (other,)
-        if cache is not None:
-            cache[(e, z)] = cls
-    and_rs, doc_rs, other = cls
-    out = np.full((len(reqs), 4), -1, dtype=np.int64)
-    rest = list(other)
-    inv = None
-    for rs, fields in ((and_rs, (2, 3)), (doc_rs, (0,))):
-        if not len(rs):
-            continue
-        ok = arr[rs[:, 1], 2] == 0
-        r, sg = rs[ok, 0], rs[ok, 1]
-        if fields == (2, 3):
-            out[r, 2], out[r, 3] = arr[sg, 0], arr[sg, 1]
-        else:
-            out[r, 0] = arr[sg, 0]
-        if not ok.all():  # (gave-up segments: from leaf bitmaps)
-            if inv is None:
-                inv = {v: k for k, v in reqs.items()}
-            rest += [inv[int(x)] for x in rs[~ok, 0]]
-    if rest:
-        sub_reqs = {key: i for i, key in enumerate(rest)}
-        sub = fallback(sub_reqs)
-        for key, r2 in sub_reqs.items():
-            out[reqs[key]] = sub[r2]
-    return out
-
-
-def server_stats_device(query, segments, executor, stream=None, docs_total=None, plan=None):
-    """server_stats with the counts computed on the GPU (device_counts); same results. docs_total: the executor's
-    numDocsScanned of its last scan (server_stats_closed_form: constant-cost filters then need no GPU pass). When the
-    scan counted the statistics of its two-leaf AND itself (PA_QF_FILTER_STATS: fused_counts), no extra GPU pass runs
-    for the segments it covered."""
-    fz = executor.fused_leap_counts(stream) if hasattr(executor, "fused_leap_counts") else None
-    if fz is not None and plan is not None:
-        # every request covered by the scan's own counts: two dot products (no request table, no gathers)
-        e, z, arr = fz
-        form = plan.fused_form(e, z, len(segments))
-        if form is not None and not arr[:, 2].any():
-            const_in, A, B, const_docs, C = form
-            m, lp = arr[:, 0], arr[:, 1]
-            return const_in + int(A @ m + B @ lp), (const_docs + int(C @ m)) * plan.ncols
-
-    def counts(reqs):
-        dev = lambda rq: device_counts(executor, segments, rq, stream)
-        return dev(reqs) if fz is None else fused_counts(reqs, fz, dev, None if plan is None else plan.fused_cache)
-    return server_stats_closed_form(query, segments, counts, lambda si: executor.leaf_bitmaps(si, stream),
-                                    getattr(executor, "leaf_params", None), docs_total, plan)
+            seg_tree.append(L.PA_STATS_HOST)
+    ops = np.stack(rows) if rows else np.zeros((1, OP_WORDS), dtype=np.int32)
+    return (np.ascontiguousarray(ops, dtype=np.int32), np.asarray(roots, dtype=np.int32),
+            np.asarray(seg_tree, dtype=np.int32))

@@ -162,7 +162,7 @@ def test_post_filter_rules(golden_segment):
         assert post == docs * cols, sql
 
 
-# ---------------------------------------------------------------- closed forms (filter_stats.server_stats_closed_form)
+# ---------------------------------------------------------------- the GPU statistics engine (pa_query_execution_stats)
 def _np_prog(prog, masks, n):
     from pinot_amd import _lib as L
     st = []
@@ -184,19 +184,6 @@ def np_leaps(a, b):
     seq = lab[lab != 0]
     prev = np.concatenate([[3], seq[:-1]])
     return int(np.sum(((seq == 1) & (prev == 3)) | ((seq != 3) & (prev != 3) & (seq != prev))))
-
-
-def np_counts(masks_of, segments):
-    """counts_fn of server_stats_closed_form emulated with numpy over host leaf masks (test-side pa_bitmap_counts)."""
-    def fn(reqs):
-        out = np.zeros((len(reqs), 4), dtype=np.int64)
-        for (si, a, b), r in reqs.items():
-            m, n = masks_of(si), segments[si].num_docs
-            A = _np_prog(a, m, n)
-            B = _np_prog(b, m, n) if b else np.zeros(n, dtype=bool)
-            out[r] = [A.sum(), B.sum(), (A & B).sum(), np_leaps(A, B) if b else 0]
-        return out
-    return fn
 
 
 def test_leap_count_closed_form_matches_and_iterator():
@@ -221,36 +208,54 @@ CLOSED_FORM_WHERES = [
     "s BETWEEN 10 AND 20 AND a < 50 AND b > 30", "c = 4 AND a >= 10", "c IN (1, 2) AND s < 30 AND a < 60",
     "NOT (c = 3 AND a < 20)", "NOT (a < 10 OR b < 20)", "a IN (1, 5, 7) AND b NOT IN (3, 4)",
     "s = 7", "c IN (1, 2, 3)", "a < 1000 AND s = 7",
+    # the shapes the host used to replay: leap-frogs of more than two scans, an AND with an OR child, an OR of scans
+    # under an AND with an index leaf, NOT of a leap-frogging AND
+    "a < 30 AND b < 30 AND c < 10 AND s > 3 AND a > 2", "a < 50 AND (b < 10 OR s = 3)",
+    "(a < 10 OR b < 10) AND c = 3", "NOT (a < 10 AND b < 20)",
+    "a < 60 AND b < 70 AND c < 12", "a < 50 AND (b < 10 OR c < 3)", "(a < 10 OR b < 10) AND (a > 50 OR c = 3)",
+    "a < 50 AND (b < 10 OR (s = 3 AND a > 20))",
+    "(a < 20 AND b < 30) OR (c = 2 AND a > 70) OR NOT (b < 50 AND a > 10)", "NOT (a < 95 AND b < 95 AND c < 19)",
 ]
-HOST_WHERES = ["a < 30 AND b < 30 AND c < 10 AND s > 3 AND a > 2", "a < 50 AND (b < 10 OR s = 3)",
-               "(a < 10 OR b < 10) AND c = 3", "NOT (a < 10 AND b < 20)"]
+# outside the engine (documented in filter_stats "device path"): the host replays these segments
+HOST_WHERES = ["a < 50 AND NOT (b < 10 OR c = 2)", "a < 50 AND (b < 10 OR NOT c = 3)",
+               "NOT (a < 10 AND (b < 20 OR c = 1))"]
+# (the same lists, by name, for the GPU test)
+ENGINE_WHERES = CLOSED_FORM_WHERES
+
+
+def _model_stats(q, segs, masks, chunk, params=None):
+    import stats_model as M
+    ops, roots, seg_tree = FS.operator_trees(q, segs, params, {})
+    msegs = [M.Seg(s.num_docs, masks[i]) for i, s in enumerate(segs)]
+    docs = sum(int(FS.filter_mask(q.filter, s, masks[i]).sum()) if q.filter is not None else s.num_docs
+               for i, s in enumerate(segs))
+    return M.execution_stats(ops, roots, seg_tree, msegs, FS.projected_columns(q), docs, chunk)
 
 
 @pytest.mark.parametrize("where", CLOSED_FORM_WHERES + HOST_WHERES)
-def test_closed_form_matches_replay(where):
-    """server_stats_closed_form (counts emulated with numpy) = server_stats (iterator replay), and the closed form is
-    taken for every shape in CLOSED_FORM_WHERES (the replay is never asked for)."""
-    segs = [_seg(3000, 3), _seg(4097, 4)]
-    for sql in ("SELECT COUNT(*) FROM t WHERE " + where, "SELECT SUM(a), MAX(b) FROM t WHERE " + where,
-                "SELECT c, SUM(a) FROM t WHERE %s GROUP BY c" % where):
+def test_engine_model_matches_replay(where):
+    """The statistics engine's algorithm (tests/stats_model.py: the operator-tree reduction of pa_capi.hip and the
+    chunked leap-frog of pa_stats.hip, restated on the CPU with small chunks so the chunk boundaries and the chaining
+    are exercised) = the iterator replay, per segment; the replay is needed only for the HOST_WHERES shapes."""
+    segs = [_seg(3000, 3), _seg(4097, 4), _seg(257, 5)]
+    for sql in ("SELECT COUNT(*) FROM t WHERE " + where, "SELECT c, SUM(a) FROM t WHERE %s GROUP BY c" % where):
         q = parse_sql(sql)
         masks = [leaf_masks(q, s) for s in segs]
-        want = FS.server_stats(q, segs, lambda si: masks[si])
+        want_per = [FS.server_stats(q, [s], lambda si, i=i: masks[i]) for i, s in enumerate(segs)]
+        for chunk in (64, 5, 2048):
+            in_f, post, per = _model_stats(q, segs, masks, chunk)
+            for i in range(len(segs)):
+                if per[i] < 0:
+                    assert where in HOST_WHERES, "engine expected for " + where
+                else:
+                    assert per[i] == want_per[i][0], (sql, chunk, i)
+            assert post == sum(w[1] for w in want_per), sql
+            if where in HOST_WHERES:
+                assert any(p < 0 for p in per), where
 
-        def host(si):
-            assert where in HOST_WHERES, "closed form expected for " + where
-            return masks[si]
-        got = FS.server_stats_closed_form(q, segs, np_counts(lambda si: masks[si], segs), host)
-        assert got == want, sql
-        # with the executor's bound leaf parameters: operator trees shared by segments of one signature
-        params = [[P.dictionary_leaf(pred, s.column(pred.column)) for pred in _leaves(q, s)] for s in segs]
-        got = FS.server_stats_closed_form(q, segs + segs, np_counts(lambda si: masks[si % 2], segs + segs),
-                                          lambda si: host(si % 2), params + params)
-        assert got == tuple(2 * x for x in want), sql
 
-
-def test_closed_form_golden_statistics(golden_spec, golden_segment):
-    """The golden statistics through the closed forms (numpy-emulated counts)."""
+def test_engine_model_golden_statistics(golden_spec, golden_segment):
+    """The golden statistics' numEntriesScannedInFilter through the engine's algorithm (CPU model)."""
     bad = []
     for case in golden_spec["cases"]:
         if case["stats"] is None:
@@ -258,11 +263,59 @@ def test_closed_form_golden_statistics(golden_spec, golden_segment):
         q = parse_sql(case["sql"])
         segs = [golden_segment] * golden_spec["segments_per_server"]
         masks = leaf_masks(q, golden_segment)
-        got = FS.server_stats_closed_form(q, segs, np_counts(lambda si: masks, segs), lambda si: masks)
+        got = _model_stats(q, segs, [masks] * len(segs), 2048)
         want = FS.server_stats(q, segs, lambda si: masks)
-        if got != want:
-            bad.append((case["sql"][:80], got, want))
+        if (got[0], got[1]) != want or min(got[2]) < 0:
+            bad.append((case["sql"][:80], got[:2], want))
     assert not bad, bad
+
+
+def test_leapfrog_model_on_random_masks():
+    """The chunked leap-frog (per chunk and entry state, chained) = AndDocIdIterator over the same iterators, for random
+    masks of many densities, 2..5 children, scan / index / OR-of-scans children, and several chunk sizes."""
+    import stats_model as M
+    rng = np.random.default_rng(17)
+    for trial in range(120):
+        n = int(rng.integers(1, 700))
+        k = int(rng.integers(2, 6))
+        nleaf = k + 3
+        leaves = rng.random((nleaf, n)) < (rng.random(nleaf) ** 2)[:, None]
+        if trial % 5 == 0:
+            leaves[:, -1] = True
+        seg = M.Seg(n, leaves)
+        el, its = [], []
+        nxt = 0
+        for j in range(k):
+            kind = int(rng.integers(0, 3)) if j else 1
+            if kind == 2:  # an OR of two scans and an index doc set
+                subs = [(M.LF_SCAN, [nxt], -1), (M.LF_SCAN, [nxt + 1], -1), (M.LF_DOCS, [nxt + 2], -1)]
+                prog = [nxt, nxt + 1, L.PA_BIT_OR, nxt + 2, L.PA_BIT_OR]
+                el.append((M.LF_OR, prog, -1, subs))
+                its.append(FS._OrIt([FS._ScanIt(leaves[nxt]), FS._ScanIt(leaves[nxt + 1]),
+                                     FS._DocsIt(np.flatnonzero(leaves[nxt + 2]), "bitmap")]))
+                nxt += 3
+            else:
+                el.append((M.LF_SCAN if kind == 1 else M.LF_DOCS, [nxt], -1, []))
+                its.append(FS._ScanIt(leaves[nxt]) if kind == 1 else FS._DocsIt(np.flatnonzero(leaves[nxt]), "bitmap"))
+                nxt += 1
+            if nxt + 3 > nleaf:
+                break
+        if len(el) < 2:
+            continue
+        scans = []
+        for it in its:
+            if isinstance(it, FS._ScanIt):
+                scans.append(it)
+            elif isinstance(it, FS._OrIt):
+                scans += [x for x in it.its if isinstance(x, FS._ScanIt)]
+        ai = FS._AndIt(its)
+        matches = 0
+        while ai.next() != FS.EOF:
+            matches += 1
+        want = sum(x.entries for x in scans)
+        for chunk in (3, 32, 64, 1000):
+            got, _, m = M.leapfrog(el, False, seg, chunk)
+            assert (got, m) == (want, matches), (trial, chunk)
 
 
 def _word_leaps(a, b, prev):
@@ -301,9 +354,10 @@ def test_constant_time_word_leaps_match_the_sequence_rule():
 
 def test_operator_trees_not_shared_across_index_configurations():
     """segments with the same data and dictionaries but different indexes on a filter column (none, an
-    exact range index, an inverted index, an inexact v1 range index) must not share an operator tree in the closed-form
-    planner (_tree_signature lists every index attribute _leaf_op reads): each gets its own accounting, equal to its
-    own replay. An EQ on an inexact range index scans (RangeIndexBasedFilterOperator.canEvaluate needs isExact)."""
+    exact range index, an inverted index, an inexact v1 range index) must not share an operator tree
+    (filter_stats._tree_signature lists every index attribute _leaf_op reads): each gets its own tree, and its
+    accounting equals its own replay. An EQ on an inexact range index scans (RangeIndexBasedFilterOperator.canEvaluate
+    needs isExact)."""
     from pinot_amd.segment import create_segment
     rng = np.random.default_rng(21)
     n = 4000
@@ -317,82 +371,53 @@ def test_operator_trees_not_shared_across_index_configurations():
     q = parse_sql("SELECT c, SUM(b) FROM t WHERE a = 5 AND b < 50 GROUP BY c")
     masks = [leaf_masks(q, s) for s in segs]
     params = [[P.dictionary_leaf(pred, s.column(pred.column)) for pred in _leaves(q, s)] for s in segs]
-    got = FS.server_stats_closed_form(q, segs, np_counts(lambda si: masks[si], segs), lambda si: masks[si], params)
-    assert got == FS.server_stats(q, segs, lambda si: masks[si])
-    per = [FS.server_stats_closed_form(q, [s], np_counts(lambda si: masks[i], [s]), lambda si: masks[i], [params[i]])
-           for i, s in enumerate(segs)]
-    assert per[0] == per[3] != per[1] == per[2]  # scan vs index-served EQ
+    ops, roots, seg_tree = FS.operator_trees(q, segs, params, {})
+    assert seg_tree[0] == seg_tree[3] != seg_tree[1] == seg_tree[2]  # scan vs index-served EQ
+    got = _model_stats(q, segs, masks, 64, params)
+    assert (got[0], got[1]) == FS.server_stats(q, segs, lambda si: masks[si])
+    per = [FS.server_stats(q, [s], lambda si, i=i: masks[i])[0] for i, s in enumerate(segs)]
+    assert got[2] == per
 
 
 @pytest.mark.parametrize("where", ["a < 50", "NOT a < 50", "a < 10 OR b < 10", "s = 7", "c IN (1, 2, 3)",
                                    "NOT (a < 10 OR b < 20)"])
-def test_constant_cost_filters_need_no_counts(where):
-    """A filter whose entries are a constant (every scan driven to EOF reads all docs; index-served operators none):
-    given the scan's numDocsScanned the closed form never asks for counts, so the statistics cost no pass over the
-    filter columns (configs[0]'s day BETWEEN a AND b)."""
+def test_constant_cost_filters_need_no_gpu_pass(where):
+    """A filter whose entries are a constant (every scan driven to EOF reads all docs; index-served operators none)
+    reduces to a constant: no applyAnd count and no leap-frog, so the statistics cost no pass over the filter columns
+    (configs[0]'s day BETWEEN a AND b)."""
+    import stats_model as M
     segs = [_seg(3000, 3), _seg(4097, 4)]
-
-    def boom(*_):
-        raise AssertionError("counts requested for a constant-cost filter")
     for sql in ("SELECT COUNT(*), SUM(a) FROM t WHERE " + where, "SELECT c, SUM(a) FROM t WHERE %s GROUP BY c" % where):
         q = parse_sql(sql)
-        masks = [leaf_masks(q, s) for s in segs]
-        want = FS.server_stats(q, segs, lambda si: masks[si])
-        docs = sum(int(FS.filter_mask(q.filter, s, masks[i]).sum()) for i, s in enumerate(segs))
-        assert FS.server_stats_closed_form(q, segs, boom, boom, docs_total=docs) == want, sql
+        ops, roots, seg_tree = FS.operator_trees(q, segs, None, {})
+        for si, s in enumerate(segs):
+            counts, leaps = [], []
+            v = M._cost_next(ops, int(roots[seg_tree[si]]), M.Seg(s.num_docs, leaf_masks(q, s)), counts, leaps, False)
+            assert not counts and not leaps, sql
+            assert v == FS.server_stats(q, [s], lambda _: leaf_masks(q, s))[0], sql
 
 
-def test_fused_counts_serve_only_their_requests():
-    """filter_stats.fused_counts: the AND request (A = [Z], B = [E]) and the whole-filter popcount come from the scan's
-    per-segment counts; other requests and gave-up segments from the fallback."""
-    AND = L.PA_BIT_AND
-    arr = np.array([[10, 4, 0], [3, 1, 1]], dtype=np.int64)
-    reqs = {(0, (1,), (0,)): 0, (0, (1, 0, AND), ()): 1, (1, (1,), (0,)): 2, (0, (0,), (1,)): 3}
-    asked = []
-
-    def fallback(rest):
-        asked.append(sorted(rest))
-        return np.array([[100 + r, 0, 0, 0] for r in range(len(rest))], dtype=np.int64)
-
-    out = FS.fused_counts(reqs, (0, 1, arr), fallback)
-    assert out[0].tolist() == [-1, -1, 10, 4]
-    assert out[1].tolist() == [10, -1, -1, -1]
-    assert asked == [sorted([(1, (1,), (0,)), (0, (0,), (1,))])]
-    assert out[2][0] >= 100 and out[3][0] >= 100
-
-
-def test_fused_linear_form_equals_the_closed_forms(monkeypatch):
-    """server_stats_device's fast path (the statistics as linear forms of the scan's per-segment matched docs and
-    leaps, _StatsPlan.fused_form) gives what fused_counts + the closed forms give; a gave-up segment leaves it for the
-    general path (which asks the device counts for that segment)."""
-    segs = [_seg(4000, 11), _seg(3000, 12), _seg(5000, 13)]
-    q = parse_sql("SELECT COUNT(*), SUM(b) FROM t WHERE a < 20 AND b = 7")
-    plan = FS.plan_stats(q, segs)
-    reqs = plan.flat()[0]
-    e, z = None, None
-    for (si, a, b) in reqs:  # the two-leaf AND's request names the leaves: A = [Z], B = [E]
-        if len(a) == 1 and len(b) == 1:
-            z, e = a[0], b[0]
-    assert e is not None
-    rng = np.random.default_rng(5)
-    arr = np.stack([rng.integers(0, 500, 3), rng.integers(0, 900, 3), np.zeros(3, dtype=np.int64)], axis=1)
-
-    class Ex:
-        handle = None
-
-        def fused_leap_counts(self, stream=None):
-            return e, z, arr
-
-    def no_fallback(rq):
-        raise AssertionError(rq)
-
-    want = FS.server_stats_closed_form(q, segs, lambda rq: FS.fused_counts(rq, (e, z, arr), no_fallback), None, None,
-                                       777, plan)
-    assert plan.fused_form(e, z, len(segs)) is not None
-    assert FS.server_stats_device(q, segs, Ex(), None, 777, plan) == want
-    arr[1, 2] = 1  # segment 1 gave up
-    asked = []
-    monkeypatch.setattr(FS, "device_counts", lambda ex, sg, rq, st=None: asked.append(sorted(rq)) or
-                        np.zeros((len(rq), 4), dtype=np.int64))
-    FS.server_stats_device(q, segs, Ex(), None, 777, plan)
-    assert asked and all(k[0] == 1 for k in asked[0])
+def test_operator_tree_encoding():
+    """operator_trees: pre-order pa_filter_op rows (kind, children, multi-value column, program), AND children in the
+    reference's priority order (sorted index, inverted index, scans), constant leaves folded, one tree per signature."""
+    segs = [_seg(3000, 3), _seg(3000, 3)]
+    q = parse_sql("SELECT COUNT(*) FROM t WHERE a < 50 AND (b < 10 OR c = 3) AND s = 7")
+    ops, roots, seg_tree = FS.operator_trees(q, segs, None, {})
+    assert list(seg_tree) == [0, 0] and list(roots) == [0]
+    kinds = [int(r[0]) for r in ops]
+    assert kinds[0] == L.PA_FOP_AND and ops[0][1] == 3
+    # s = 7 on the sorted column first (HIGH), then the OR (OR_P 400), then the scan of a (SCAN_P 500)
+    assert kinds[1] == L.PA_FOP_SORTED and kinds[2] == L.PA_FOP_OR and kinds[5] == L.PA_FOP_SCAN
+    assert kinds[3:5] == [L.PA_FOP_SCAN, L.PA_FOP_BITMAP]
+    assert all(r[2] == -1 for r in ops)
+    for r in ops:
+        if r[0] in (L.PA_FOP_SORTED, L.PA_FOP_BITMAP, L.PA_FOP_SCAN):
+            assert r[3] == 1 and 0 <= r[4] < 4
+    q = parse_sql("SELECT COUNT(*) FROM t WHERE a > 1000 OR c = 2")  # always-false leaf folds: one bitmap leaf
+    ops, roots, seg_tree = FS.operator_trees(q, segs, None, {})
+    assert [int(r[0]) for r in ops] == [L.PA_FOP_BITMAP]
+    q = parse_sql("SELECT SUM(a) FROM t")  # no filter: a match-all tree (the projection reads every doc)
+    ops, roots, seg_tree = FS.operator_trees(q, segs, None, {})
+    assert [int(r[0]) for r in ops] == [L.PA_FOP_MATCH_ALL]
+    q = parse_sql("SELECT MAX(a) FROM t")  # non-scan plan
+    assert list(FS.operator_trees(q, segs, None, {})[2]) == [L.PA_STATS_NON_SCAN] * 2

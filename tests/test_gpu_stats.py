@@ -1,10 +1,12 @@
-"""Execution statistics on the GPU (pa_bitmap_counts + filter_stats closed forms) against the host iterator replay.
+"""Execution statistics on the GPU (pa_query_execution_stats: pa_stats.hip's masks, counts and chunked leap-frogs;
+the scan's fused counts) against the host iterator replay.
 
 pa_bitmap_counts is checked against a numpy restatement of its four counts on random leaf bitmaps (one word to
 multi-workgroup sizes, densities down to a few set bits so the cross-workgroup label carry is exercised); the
-executor's execution_stats() (closed forms over those counts) against filter_stats.server_stats (the replay of the
-reference's iterators, SVScanDocIdIterator / AndDocIdIterator / OrDocIdIterator / NotDocIdIterator) over the same
-GPU leaf bitmaps. Bit-exact integers."""
+executor's execution_stats() against filter_stats.server_stats (the replay of the reference's iterators,
+SVScanDocIdIterator / MVScanDocIdIterator / AndDocIdIterator / OrDocIdIterator / NotDocIdIterator) over the same GPU
+leaf bitmaps, per filter shape, with the replay asserted unused for every shape the engine covers. Bit-exact
+integers."""
 import ctypes
 
 import numpy as np
@@ -16,7 +18,7 @@ from pinot_amd import filter_stats as FS
 from pinot_amd import parse_sql
 from pinot_amd.engine import GpuQueryExecutor, GpuSegment
 from pinot_amd.segment import create_segment
-from test_filter_stats import CLOSED_FORM_WHERES, HOST_WHERES, _np_prog, np_leaps
+from test_filter_stats import ENGINE_WHERES, HOST_WHERES, _np_prog, np_leaps
 
 pytestmark = pytest.mark.gpu
 
@@ -72,26 +74,67 @@ def _segment(seed, n):
                           no_dictionary_columns=("r",))
 
 
+def _stats_and_replay(ex):
+    """(engine statistics, host replay) after a scan + fetch of the executor (the fetch fills the statistics)."""
+    res = ex.run()
+    got = (res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter)
+    assert got == ex.execution_stats()  # (a second evaluation over the same scan)
+    # (the executor holds the reference's rewritten filter: optimizer.py)
+    want = FS.server_stats(ex.query, ex.segs, lambda si: ex.leaf_bitmaps(si))
+    return got, want
+
+
 def test_execution_stats_device_vs_replay():
-    """Every shape of test_filter_stats' closed-form list (and the replay-only shapes) over 3 segments of up to 200K
-    docs: the executor's statistics = the host replay over the same GPU bitmaps."""
+    """Every filter shape of test_filter_stats (the engine's list and the host-replayed ones) over 3 segments of up to
+    200K docs (the leap-frogs cross many 2048-doc chunks): the statistics the fetch fills = the host replay over the
+    same GPU bitmaps, and no segment is replayed for the engine's shapes."""
     segs = [_segment(1, 200_003), _segment(2, 70_000), _segment(3, 1025)]
     gs = [GpuSegment(s) for s in segs]
     try:
         # (+ a raw column: per-doc leaf path; a 20-bit dictionary: wide lane-major decode)
-        for where in CLOSED_FORM_WHERES + HOST_WHERES + ["r < 1000 AND a < 50", "r BETWEEN 10 AND 20 OR b = 3",
-                                                          "w < 300000 AND b < 40", "w IN (5, 77, 1000) OR a = 1",
-                                                          "r IN (3, 5, 7, 4000) AND b < 50", "NOT r IN (3, 5) AND a < 9"]:
+        extra = ["r < 1000 AND a < 50", "r BETWEEN 10 AND 20 OR b = 3", "w < 300000 AND b < 40",
+                 "w IN (5, 77, 1000) OR a = 1", "r IN (3, 5, 7, 4000) AND b < 50",
+                 "w < 600000 AND (a < 5 OR r < 200) AND b > 20", "NOT (w < 900000 AND r > 40 AND b < 90)"]
+        host = HOST_WHERES + ["NOT r IN (3, 5) AND a < 9"]  # (a NOT child of a leap-frogging AND: replayed)
+        for where in ENGINE_WHERES + extra + host:
             for sql in ("SELECT COUNT(*) FROM t WHERE " + where, "SELECT c, SUM(a) FROM t WHERE %s GROUP BY c" % where):
-                q = parse_sql(sql)
-                ex = GpuQueryExecutor(q, gs)
+                ex = GpuQueryExecutor(parse_sql(sql), gs)
                 try:
-                    got = ex.execution_stats()
-                    # (the executor holds the reference's rewritten filter: optimizer.py)
-                    want = FS.server_stats(ex.query, ex.segs, lambda si: ex.leaf_bitmaps(si))
+                    got, want = _stats_and_replay(ex)
+                    replayed = ex.stats_replayed_segments
                 finally:
                     ex.close()
                 assert got == want, sql
+                if where not in host:
+                    assert replayed == 0, sql
+    finally:
+        for g in gs:
+            g.close()
+
+
+def test_execution_stats_multi_value_scans():
+    """Multi-value scans read every value of a doc (MVScanDocIdIterator): in applyAnd chains (value counts of the
+    surviving docs) and in leap-frogs (the values of the docs between target and answer) = the host replay."""
+    rng = np.random.default_rng(8)
+    segs = []
+    for i, n in enumerate((150_001, 4099)):
+        data = {"c": rng.integers(0, 20, n).astype(np.int32), "a": rng.integers(0, 100, n).astype(np.int32),
+                "s": np.sort(rng.integers(0, 40, n)).astype(np.int32),
+                "tags": [rng.integers(0, 300, int(k)).astype(np.int32) for k in rng.integers(1, 6, n)]}
+        segs.append(create_segment("mv%d" % i, data, {k: "INT" for k in data}, inverted_index_columns=("c",),
+                                   multi_value_columns=("tags",)))
+    gs = [GpuSegment(s) for s in segs]
+    try:
+        for where in ("tags IN (3, 5, 7) AND a < 50", "s < 20 AND tags < 100", "c = 3 AND tags > 250",
+                      "tags < 30 OR a < 5", "a < 40 AND (tags = 7 OR a > 90)", "NOT (tags < 200 AND a < 70)",
+                      "tags < 150 AND a < 60 AND c < 15"):
+            ex = GpuQueryExecutor(parse_sql("SELECT c, SUM(a) FROM t WHERE %s GROUP BY c" % where), gs)
+            try:
+                got, want = _stats_and_replay(ex)
+                assert ex.stats_replayed_segments == 0, where
+            finally:
+                ex.close()
+            assert got == want, where
     finally:
         for g in gs:
             g.close()
@@ -109,8 +152,8 @@ def test_merged_range_is_one_scan_on_the_gpu():
         ex = GpuQueryExecutor(q, gs)
         try:
             assert isinstance(ex.query.filter, type(q.filter.children[0]))  # one RANGE predicate
-            in_filter, post = ex.execution_stats()
             res = ex.run()
+            in_filter, post = ex.execution_stats()
         finally:
             ex.close()
         total = sum(s.num_docs for s in segs)
@@ -139,11 +182,11 @@ def _sparse_segment(seed, n, e_docs):
     return create_segment("sp%d" % seed, data, {k: "INT" for k in data})
 
 
-def test_fused_execution_stats_match_the_replay(monkeypatch):
-    """PA_QF_FILTER_STATS: the scan counts the leaps of `z-leaf AND e-leaf` itself (E = the sparse eager e leaf, found
-    by neighbour searches from each E doc); the statistics equal the host replay, and no leaf-bitmap pass runs when
-    every search finished. A sparse A leaf (y) makes searches give up: those segments fall back to the bitmap counts,
-    with the same result. With E first in the reference's AND order the fused counts do not apply (fallback)."""
+def test_fused_execution_stats_match_the_replay():
+    """The scan counts the leaps of `z-leaf AND e-leaf` itself by default (E = the sparse eager e leaf, found by
+    neighbour searches from each E doc); the statistics equal the host replay, and no GPU statistics pass runs when
+    every search finished. A sparse A leaf (y) makes searches give up: those segments take the statistics engine, with
+    the same result. With E first in the reference's AND order the fused counts do not apply (engine)."""
     n0 = 300_007
     # (segments large enough that e's dictionary keeps e = 7 below 1 / 256 of the docs, which makes the planner
     # evaluate the z clause lazily: the fused count's precondition)
@@ -155,27 +198,22 @@ def test_fused_execution_stats_match_the_replay(monkeypatch):
                  ("z = 5 AND e = 7", True), ("y = 17 AND e = 7", False), ("e = 7 AND z < 2", False)]
         for where, fused_only in cases:
             for sql in ("SELECT COUNT(*) FROM t WHERE " + where, "SELECT z, SUM(m) FROM t WHERE %s GROUP BY z" % where):
-                q = parse_sql(sql)
-                ex = GpuQueryExecutor(q, gs, flags=L.PA_QF_FILTER_STATS)
-                try:
-                    ex.execute()
-                    fz = ex.fused_leap_counts()
-                    assert fz is not None, sql  # (a sparse E: the scan counted)
-                    if fused_only:
-                        called = []
-                        orig = FS.device_counts
-                        monkeypatch.setattr(FS, "device_counts", lambda *a, **k: called.append(1) or orig(*a, **k))
-                        got = ex.execution_stats()
-                        monkeypatch.setattr(FS, "device_counts", orig)
-                        assert not called, sql
-                    else:
-                        got = ex.execution_stats()
-                    want = FS.server_stats(ex.query, ex.segs, lambda si: ex.leaf_bitmaps(si))
-                    res = ex.fetch()
-                    assert fz[2][:, 0].sum() == res.num_docs_scanned
-                finally:
-                    ex.close()
-                assert got == want, sql
+                for flags in (0, L.PA_QF_NO_FILTER_STATS):
+                    ex = GpuQueryExecutor(parse_sql(sql), gs, flags=flags)
+                    try:
+                        ex.execute()
+                        fz = ex.fused_leap_counts()
+                        assert (fz is not None) == (flags == 0), sql  # (a sparse E: the scan counted by default)
+                        res = ex.fetch()
+                        got = (res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter)
+                        if fused_only and flags == 0:
+                            assert ex.stats_gpu_segments == 0, sql
+                        want = FS.server_stats(ex.query, ex.segs, lambda si: ex.leaf_bitmaps(si))
+                        if fz is not None:
+                            assert fz[2][:, 0].sum() == res.num_docs_scanned
+                    finally:
+                        ex.close()
+                    assert got == want, (sql, flags)
     finally:
         for g in gs:
             g.close()
@@ -190,13 +228,15 @@ def test_fused_statistics_on_the_steady_state_tile_loop():
     gs = [GpuSegment(s) for s in segs]
     try:
         q = parse_sql("SELECT COUNT(*) FROM t WHERE z < 8 AND e = 7")
-        flags = L.PA_QF_FILTER_STATS | (2 << L.PA_QF_RING_SHIFT) | (1 << L.PA_QF_WG_SHIFT)
+        flags = (2 << L.PA_QF_RING_SHIFT) | (1 << L.PA_QF_WG_SHIFT)
         ex = GpuQueryExecutor(q, gs, flags=flags)
         try:
             ex.execute()
             fz = ex.fused_leap_counts()
             assert fz is not None and not fz[2][:, 2].any()
-            got = ex.execution_stats()
+            res = ex.fetch()
+            got = (res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter)
+            assert ex.stats_gpu_segments == 0
             want = FS.server_stats(ex.query, ex.segs, lambda si: ex.leaf_bitmaps(si))
         finally:
             ex.close()

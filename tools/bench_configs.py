@@ -235,7 +235,7 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
         def extra_flags(vs_, tag_):
             return dict((t_, f_) for f_, t_ in vs_)[tag_]
         for extra, tag in vs:
-            ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags | extra)
+            ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags | extra | (L.PA_QF_NO_FILTER_STATS if exec_stats else 0))
             ex.execute(sp)
             torch.cuda.synchronize()
             ex.reset(sp)
@@ -249,6 +249,7 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
             ex.execute(sp)
             torch.cuda.synchronize()  # fetch_ms = compaction + copies (+ host decode of small blocks) only
             ex.fetch_arrays(sp, pooled=True)  # (first use grows the process's pinned output pool)
+            ex.fetch(sp, execution_stats=False)  # (numDocsScanned of this scan)
             t1 = time.perf_counter()
             keys, counts, outs = ex.fetch_arrays(sp, pooled=True)
             fetch_ms = (time.perf_counter() - t1) * 1e3
@@ -270,17 +271,17 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
             if cpu_sample:
                 extra["cpu_baseline"] = cpu_port_baseline(sql, host)
             if exec_stats:
-                # numEntriesScannedInFilter / PostFilter of every segment: (a) the plain executor (leaf bitmaps +
-                # counts on the GPU when the closed forms need counts, filter_stats.server_stats_device); (b) a
-                # PA_QF_FILTER_STATS executor, whose scan counts the two-leaf AND's leaps itself (fused_counts): its
-                # scan time and the host closed form after it, against the plain scan (ms)
+                # numEntriesScannedInFilter / PostFilter of every segment: (a) an executor whose scan does not count
+                # (PA_QF_NO_FILTER_STATS: pa_query_execution_stats' GPU engine over leaf bitmaps); (b) the default
+                # executor, whose scan counts a two-leaf AND's leaps itself where that applies: its scan time and the
+                # statistics call after it, against the plain scan (ms)
                 from pinot_amd import filter_stats as FS
                 docs_total = int(L.lib().pa_query_matched_docs(ex.handle))
                 ex.execution_stats(sp, docs_total)  # (warms the allocator)
                 t3 = time.perf_counter()
                 in_f, post = ex.execution_stats(sp, docs_total)
                 plain_ms = (time.perf_counter() - t3) * 1e3
-                fx = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags | extra_flags(vs, tag) | L.PA_QF_FILTER_STATS)
+                fx = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags | extra_flags(vs, tag))
                 fx.execute(sp)
                 torch.cuda.synchronize()
                 fx.reset(sp)

@@ -248,8 +248,17 @@ int main(int argc, char** argv) {
   // day range: ids [64, 448) of 512, MSB-aligned compare (v - lo) <= hi - lo
   const uint32_t lo_t = 64u << (32 - NB0), hi_t = (447u << (32 - NB0)) - lo_t + ((1u << (32 - NB0)) - 1u);
   printf("ncu %d docs %lld\n", ncu, (long long)docs);
+  if (argc > 2) {  // one mode only (profiling): ./mc_probe DOCS MODE
+    const int m = atoi(argv[2]);
+    if (m == 0) run<16, 8, 0>(cols, docs, lo_t, hi_t, out, ncu);
+    if (m == 2) run<16, 8, 2>(cols, docs, lo_t, hi_t, out, ncu);
+    if (m == 3) run<16, 8, 3>(cols, docs, lo_t, hi_t, out, ncu);
+    if (m == 4) run<16, 8, 4>(cols, docs, lo_t, hi_t, out, ncu);
+    return 0;
+  }
   run<16, 8, 0>(cols, docs, lo_t, hi_t, out, ncu);
   run<16, 8, 2>(cols, docs, lo_t, hi_t, out, ncu);
+  run<16, 8, 3>(cols, docs, lo_t, hi_t, out, ncu);
   run<16, 8, 4>(cols, docs, lo_t, hi_t, out, ncu);
   run<16, 8, 0, 1>(cols, docs, lo_t, hi_t, out, ncu);
   run<16, 8, 2, 1>(cols, docs, lo_t, hi_t, out, ncu);
