@@ -181,6 +181,8 @@ typedef struct {
   int64_t hash_keys_bound; /* hashed key spaces: the table holds at least 2 x this many keys (0 = size from the bound
                               segments alone). A multi-GPU query passes the largest per-rank bound of all ranks so every
                               rank's table can hold its share of the cross-GPU merge (parallel.table_layout) */
+  int32_t flags2; /* PA_QF2_* */
+  int32_t reserved2;
 } pa_query_spec;
 
 #define PA_QF_STAGE_ALL 1  /* stage post-filter columns through LDS even when a filter exists */
@@ -222,6 +224,8 @@ typedef struct {
 #define PA_QF_NO_FILTER_STATS (1 << 30)   /* the scan does NOT count what the execution statistics of an AND of two scan
                                              leaves need (by default it does wherever that fused count applies:
                                              pa_query_leap_leaf / pa_query_leap_counts / pa_query_execution_stats) */
+#define PA_QF2_NO_COUNT_FREE 1         /* partitioned V-only plans: the count + emit passes even where the count-free
+                                           emit (pve_jit.hip, pa_query_count_free_emit) applies */
 #define PA_QF_PART_SHIFT 22              /* bits 22..23: LDS per partition of the partitioned aggregation (0 = auto,
                                              1 = 64 KiB, 2 = 96 KiB, 3 = 144 KiB): larger partitions = fewer record
                                              write fronts per XCD */
@@ -372,7 +376,7 @@ int pa_query_leap_counts(pa_query* q, int64_t* out, void* stream);
  * two-scan AND itself (PA_QF_NO_FILTER_STATS unset), those counts.
  * out[0] = numEntriesScannedInFilter over the segments the library covered, out[1] = numEntriesScannedPostFilter =
  * (docs_scanned - docs of PA_STATS_NON_SCAN segments) x projected_columns (docs_scanned: numDocsScanned of the scan,
- * < 0 = the one the last pa_query_fetch read), out[2] = segments whose count ran on the GPU. segment_in_filter[s]
+ * < 0 = the last scan's own counter), out[2] = segments whose count ran on the GPU. segment_in_filter[s]
  * (optional, host int64[num_segments]) = segment s's numEntriesScannedInFilter, or -1 for a segment the host must
  * account for (PA_STATS_HOST, or a tree shape outside the engine: a NOT child of a leap-frogging AND, an AND or NOT
  * child of an OR child of one). Synchronises `stream`. */
@@ -441,6 +445,9 @@ int32_t pa_query_lane_major(const pa_query* q);
  * doc, drained per wave into the workgroup's accumulators), 2 if it does so in the kernel specialised to the query's
  * shape (compiled by hiprtc at prepare), 0 if not, <0 error. */
 int32_t pa_query_dense_packed(const pa_query* q);
+/* 1 when the partitioned plan runs the count-free V emit (each workgroup writes whole record chunks into its own
+ * region; pass C reads every partition through its chunk list: no count pass), 0 otherwise, <0 if not prepared. */
+int32_t pa_query_count_free_emit(const pa_query* q);
 int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t* dma_slots, int32_t* ring,
                   int32_t* wg_per_cu, int32_t* grid, int32_t* lds_bytes);
 

@@ -31,7 +31,7 @@ PA_QF_NO_REG_STAGE = 1 << 18
 PA_QF_NO_GDENSE_LM = 1 << 15
 PA_QF_NO_GD_PACK = 1 << 3
 PA_QF_GD_DRAIN_EACH_TILE = 1 << 2
-PA_QF_NO_JIT = -(1 << 31)  # bit 31 of the int32 flags word
+PA_QF_NO_JIT = 1 << 31  # bit 31 of the int32 flags word (engine converts to int32)
 PA_QF_NO_BOX_FILTER = 1 << 19
 PA_QF_BOX_FILTER = 1 << 20
 PA_QF_NO_PARTITION = 1 << 21
@@ -43,6 +43,7 @@ PA_QF_NO_LANE_HIST = 1 << 27
 PA_QF_LAZY_POST = 1 << 28
 PA_QF_NO_DENSE_GROUP = 1 << 29
 PA_QF_NO_FILTER_STATS = 1 << 30
+PA_QF2_NO_COUNT_FREE = 1 << 32  # (engine flags: bits 32.. go to pa_query_spec.flags2)
 PA_FOP_EMPTY, PA_FOP_MATCH_ALL, PA_FOP_SORTED, PA_FOP_BITMAP, PA_FOP_SCAN, PA_FOP_AND, PA_FOP_OR, PA_FOP_NOT = range(8)
 PA_STATS_NON_SCAN, PA_STATS_HOST = -1, -2
 PA_BIT_AND, PA_BIT_OR, PA_BIT_NOT = -1, -2, -3
@@ -58,7 +59,7 @@ EXPORTED = [
     "pa_segment_add_raw_column", "pa_segment_num_docs", "pa_segment_device_bytes", "pa_segment_destroy",
     "pa_query_create", "pa_query_bind_segment", "pa_query_bind_value_remap", "pa_query_prepare", "pa_query_num_keys",
     "pa_query_execute", "pa_query_reset", "pa_query_scan", "pa_query_num_eager_literals", "pa_query_lane_major",
-    "pa_query_dense_packed",
+    "pa_query_dense_packed", "pa_query_count_free_emit",
     "pa_query_accumulator_bytes", "pa_query_set_accumulator_buffer", "pa_query_num_sections", "pa_query_section",
     "pa_query_fetch", "pa_query_matched_docs", "pa_query_key_layout", "pa_query_limit_trimming",
     "pa_query_num_groups_limit_reached", "pa_query_stats", "pa_query_leaf_bitmap_words", "pa_query_leaf_bitmaps",
@@ -99,6 +100,8 @@ class QuerySpec(ctypes.Structure):
         ("flags", ctypes.c_int32),
         ("num_groups_limit", ctypes.c_int32),
         ("hash_keys_bound", ctypes.c_int64),
+        ("flags2", ctypes.c_int32),
+        ("reserved2", ctypes.c_int32),
     ]
 
 
@@ -141,6 +144,7 @@ def _declare(lib):
         "pa_query_num_eager_literals": (i32, [vp]),
         "pa_query_lane_major": (i32, [vp]),
         "pa_query_dense_packed": (i32, [vp]),
+        "pa_query_count_free_emit": (i32, [vp]),
         "pa_query_accumulator_bytes": (u64, [vp]),
         "pa_query_set_accumulator_buffer": (ctypes.c_int, [vp, vp, u64]),
         "pa_query_num_sections": (i32, [vp]),

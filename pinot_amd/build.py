@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libpinot_amd.so")
-SOURCES = ["pa_scan_part_a.hip", "pa_scan_part_b.hip", "pa_scan_part_mv.hip", "pa_scan_std.hip", "pa_scan_lane.hip", "pa_scan_gdense.hip", "pa_kernels.hip", "pa_merge.hip", "pa_stats.hip", "pa_capi.hip"]
+SOURCES = ["pa_scan_part_a.hip", "pa_scan_part_b.hip", "pa_scan_part_mv.hip", "pa_scan_std.hip", "pa_scan_lane.hip", "pa_scan_gdense.hip", "pa_kernels.hip", "pa_merge.hip", "pa_stats.hip", "pa_pve.hip", "pa_capi.hip"]
 # every header under csrc/ (globbed, so a new one is covered without an edit here) and the public C-ABI header
 HEADERS = sorted(f for f in os.listdir(CSRC) if f.endswith(".h")) + [os.path.join("..", "..", "include", "pinot_amd.h")]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-munsafe-fp-atomics", "-std=c++17",
@@ -17,19 +17,23 @@ def _stale():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS + ["gdl_jit.hip"]] + [__file__]
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS + JIT_SOURCES] + [__file__]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+JIT_SOURCES = ["gdl_jit.hip", "pve_jit.hip"]
+
+
 def _jit_source():
-    """gdl_jit.hip as a C++ raw string literal (pa_capi.hip compiles it at query prepare with hiprtc)."""
-    src = open(os.path.join(CSRC, "gdl_jit.hip")).read()
-    assert ")JITSRC" not in src
-    out = os.path.join(CSRC, "gdl_jit_src.inc")
-    text = 'R"JITSRC(' + src + ')JITSRC"\n'
-    if not os.path.exists(out) or open(out).read() != text:
-        with open(out, "w") as f:
-            f.write(text)
+    """The JIT kernels' sources as C++ raw string literals (pa_capi.hip compiles them at query prepare with hiprtc)."""
+    for name in JIT_SOURCES:
+        src = open(os.path.join(CSRC, name)).read()
+        assert ")JITSRC" not in src
+        out = os.path.join(CSRC, name.replace(".hip", "_src.inc"))
+        text = 'R"JITSRC(' + src + ')JITSRC"\n'
+        if not os.path.exists(out) or open(out).read() != text:
+            with open(out, "w") as f:
+                f.write(text)
 
 
 def build(force=False, verbose=False):

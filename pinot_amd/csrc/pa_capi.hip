@@ -523,6 +523,12 @@ struct pa_query {
   hipFunction_t jit_fn = nullptr;
   int jit_waves = 0, jit_grid = 0, jit_lds = 0;
   DevBuf jit_args, jit_segs;
+  // the partitioned path's V emit without a count pass (pve_jit.hip + pa_pve.hip): null = count + emit passes
+  hipFunction_t pve_fn = nullptr;
+  int pve_waves = 0, pve_grid = 0, pve_lds = 0, pve_bs = 0;
+  int64_t pve_chunks = 0;  // chunk slots per workgroup
+  DevBuf pve_args, pve_segs, pve_buf;
+  size_t pve_o_table = 0, pve_o_hist = 0, pve_o_used = 0, pve_o_off = 0, pve_o_base = 0, pve_o_index = 0;
   int has_mv = 0;
   bool hashed = false;           // packed 64-bit keys through a global open-addressing table
   int key_words = 1;             // hashed: 2 = two-word keys ([k0, k1, state] per slot)
@@ -566,6 +572,7 @@ struct pa_query {
   DevBuf leap_buf;  // fused statistics (default; PA_QF_NO_FILTER_STATS turns them off): per segment (matched docs, leaps, gave up)
   int leap_leaf = -1;  // the eager leaf (spec order) when the scan counts the leaps
   bool leap_searched = true;  // the last scan's E-doc list has been searched (leap_search_kernel)
+  bool scanned_since_fetch = false;  // last_matched predates the last scan
   int64_t leap_slices = 0;
   std::vector<LmSegPlan> hplans;
   std::vector<uint32_t> gdplans;  // STRAT_GDENSE: per-segment parameter tables (GdSegPlan + GdRsPlan, 128 dwords)
@@ -595,6 +602,9 @@ struct pa_query {
     dev_free(dgdplans);
     dev_free(jit_args);
     dev_free(jit_segs);
+    dev_free(pve_args);
+    dev_free(pve_segs);
+    dev_free(pve_buf);
     if (host_acc) (void)hipHostFree(host_acc);
     dev_free(fetch_blocks);
     dev_free(fetch_stage);
@@ -2856,16 +2866,17 @@ std::string int_list(const std::vector<int>& v) {
   return r + "}";
 }
 
-hipFunction_t jit_compile(const std::vector<std::string>& defs) {
+hipFunction_t jit_compile(const std::vector<std::string>& defs, const char* src = kGdlJitSrc,
+                          const char* name = "gdl_jit") {
   int dev = 0;
   (void)hipGetDevice(&dev);
-  std::string key = std::to_string(dev);
+  std::string key = std::to_string(dev) + " " + name;
   for (const std::string& d : defs) key += " " + d;
   std::lock_guard<std::mutex> g(g_jit_mu);
   auto it = g_jit_cache.find(key);
   if (it != g_jit_cache.end()) return it->second.fn;
   hiprtcProgram prog;
-  if (hiprtcCreateProgram(&prog, kGdlJitSrc, "gdl_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) return nullptr;
+  if (hiprtcCreateProgram(&prog, src, name, 0, nullptr, nullptr) != HIPRTC_SUCCESS) return nullptr;
   std::vector<std::string> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
   for (const std::string& d : defs) opts.push_back(d);
   std::vector<const char*> o;
@@ -2877,7 +2888,7 @@ hipFunction_t jit_compile(const std::vector<std::string>& defs) {
       std::vector<char> code(n);
       JitEntry e;
       if (hiprtcGetCode(prog, code.data()) == HIPRTC_SUCCESS && hipModuleLoadData(&e.mod, code.data()) == hipSuccess &&
-          hipModuleGetFunction(&e.fn, e.mod, "gdl_jit") == hipSuccess) {
+          hipModuleGetFunction(&e.fn, e.mod, name) == hipSuccess) {
         fn = e.fn;
         g_jit_cache[key] = e;
       }
@@ -2887,7 +2898,7 @@ hipFunction_t jit_compile(const std::vector<std::string>& defs) {
     hiprtcGetProgramLogSize(prog, &n);
     std::vector<char> log(n + 1, 0);
     hiprtcGetProgramLog(prog, log.data());
-    std::fprintf(stderr, "pinot_amd: gdl_jit compile failed:\n%s\n", log.data());
+    std::fprintf(stderr, "pinot_amd: %s compile failed:\n%s\n", name, log.data());
   }
   hiprtcDestroyProgram(&prog);
   return fn;
@@ -3064,6 +3075,190 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
   return PA_OK;
 }
 
+// ---------------------------------------------------------------- count-free partitioned V emit (pve_jit.hip)
+// The emit pass of a V-only partitioned plan with one-word records (V_FMT_ID / V_FMT_KEY), dictionary group-by and
+// value columns whose segments share the table-wide dictionaries (no remaps), DICT_RANGE filter leaves on staged
+// columns and pass C's specialised variant: compiled per shape by hiprtc; each workgroup writes whole chunks of BS
+// records into its own region, so no count pass runs (pa_query_scan: pve kernel, chunk lists, pass C).
+static const char* kPveJitSrc =
+#include "pve_jit_src.inc"
+    ;
+
+struct PveSegH {  // == pve_jit.hip PveSeg
+  uint64_t src[6];
+  int64_t first_tile;
+  int32_t num_docs, num_tiles;
+  uint32_t lo_t[6], hi_t[6];
+};
+struct PveArgsH {  // == pve_jit.hip PveArgs
+  int64_t total_tiles;
+  int32_t nseg, xcd_major;
+  int64_t chunks_per_wg;
+  uint32_t* recs;
+  uint32_t* table;
+  uint32_t* hist;
+  uint32_t* used;
+  unsigned long long* matched;
+};
+
+static void pve_fill_pointers(pa_query* q, PveArgsH& a) {
+  char* b = (char*)q->pve_buf.p;
+  a.recs = (uint32_t*)b;
+  a.table = (uint32_t*)(b + q->pve_o_table);
+  a.hist = (uint32_t*)(b + q->pve_o_hist);
+  a.used = (uint32_t*)(b + q->pve_o_used);
+  a.matched = q->hq.matched_docs;
+}
+
+int pve_plan(pa_query* q, const Prep& P, int cus) {
+  q->pve_fn = nullptr;
+  const pa_query_spec& s = q->spec;
+  const DevQuery& h = q->hq;
+  if (!q->partitioned || q->split_emit || h.hll_agg >= 0 || q->limit_mode || q->limit_walk || q->hashed) return PA_OK;
+  if ((s.flags & PA_QF_NO_JIT) || (s.flags2 & PA_QF2_NO_COUNT_FREE) || std::getenv("PA_NO_JIT") || std::getenv("PA_DEBUG_EMIT"))
+    return PA_OK;
+  if ((h.v_fmt != V_FMT_ID && h.v_fmt != V_FMT_KEY) || h.rec_words_v != 1 || q->part_vk == kVkGeneric) return PA_OK;
+  if (q->nseg == 0 || s.num_group_by < 1 || s.num_group_by > 4 || q->num_eager != (int)q->literals.size() ||
+      q->num_eager > 6 || h.pv > 4096 || h.kshift_v < 1)
+    return PA_OK;
+  const DevSeg& d0 = q->hsegs[0];
+  const int nc = d0.num_staged;
+  if (nc < 1 || nc > 6) return PA_OK;
+  for (const DevSeg& d : q->hsegs) {
+    if (d.num_staged != nc || d.vremap) return PA_OK;
+    for (int j = 0; j < s.num_group_by; ++j)
+      if (d.remap[j]) return PA_OK;
+    for (int k = 0; k < nc; ++k)
+      if (d.stage[k].nbits != d0.stage[k].nbits || d.stage[k].lds_off != d0.stage[k].lds_off || d.stage[k].nbits < 1 ||
+          d.stage[k].nbits > 31)
+        return PA_OK;
+  }
+  auto col_of = [&](int lds_off) {
+    for (int k = 0; k < nc; ++k)
+      if (d0.stage[k].lds_off == lds_off) return k;
+    return -1;
+  };
+  std::vector<int> lc, ln, le, gc, gs;
+  for (int li = 0; li < q->num_eager; ++li) {
+    const DevLeaf& L = d0.leaves[li];
+    for (const DevSeg& d : q->hsegs)
+      if (d.leaves[li].negate != L.negate || d.leaves[li].kind != L.kind) return PA_OK;
+    if (L.kind != PA_LEAF_DICT_RANGE) return PA_OK;
+    const int c = col_of(L.lds_off);
+    if (c < 0) return PA_OK;
+    lc.push_back(c);
+    ln.push_back(L.negate ? 1 : 0);
+    le.push_back(L.clause_end ? 1 : 0);
+  }
+  for (int j = 0; j < s.num_group_by; ++j) {
+    const int c = col_of(d0.cols[P.gb_slot[j]].lds_off);
+    if (c < 0 || h.gb_stride[j] <= 0 || h.gb_stride[j] > 0xffffffffll) return PA_OK;
+    gc.push_back(c);
+    gs.push_back((int)(uint32_t)h.gb_stride[j]);
+  }
+  int vc = -1;
+  if (h.v_fmt == V_FMT_ID) {
+    if (h.emit_val_agg < 0) return PA_OK;
+    vc = col_of(d0.cols[P.agg_slot[h.emit_val_agg]].lds_off);
+    if (vc < 0) return PA_OK;
+  }
+  if ((uint64_t)q->num_keys > 0xffffffffull) return PA_OK;
+  // LDS: per-partition state (cnt, done, chunks), the chunk counter, the bins, then each wave's two tile images
+  const int Pv = h.pv, bs = 32;
+  auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const size_t l_bins = al16((size_t)(3 * Pv + 1) * 4);
+  const size_t l_ring = al16(l_bins + (size_t)Pv * bs * 4);
+  const size_t img_b = (size_t)h.image_dwords_max * 4;
+  int w = 0;
+  for (int cand : {16, 12, 8, 4})
+    if (l_ring + (size_t)cand * 2 * img_b <= kLdsBudget) {
+      w = cand;
+      break;
+    }
+  if (!w) return PA_OK;
+  const size_t lds = l_ring + (size_t)w * 2 * img_b;
+  std::vector<int> nb, coff;
+  for (int c = 0; c < nc; ++c) {
+    nb.push_back(d0.stage[c].nbits);
+    coff.push_back(4 * d0.stage[c].lds_off);
+  }
+  auto pad1 = [](std::vector<int> v) {
+    if (v.empty()) v.push_back(0);
+    return v;
+  };
+  std::vector<std::string> gsv;
+  std::string gss = "{";
+  for (size_t j = 0; j < gs.size(); ++j) gss += (j ? "," : "") + std::to_string((uint32_t)gs[j]) + "u";
+  gss += "}";
+  std::vector<std::string> defs = {
+      "-DPVE_W=" + std::to_string(w), "-DPVE_IMG=" + std::to_string(h.image_dwords_max),
+      "-DPVE_NC=" + std::to_string(nc), "-DPVE_NB=" + int_list(nb), "-DPVE_OFF=" + int_list(coff),
+      "-DPVE_NL=" + std::to_string(q->num_eager), "-DPVE_LC=" + int_list(pad1(lc)), "-DPVE_LN=" + int_list(pad1(ln)),
+      "-DPVE_LE=" + int_list(pad1(le)), "-DPVE_NG=" + std::to_string(s.num_group_by), "-DPVE_GC=" + int_list(gc),
+      "-DPVE_GS=" + gss, "-DPVE_VC=" + std::to_string(vc), "-DPVE_KS=" + std::to_string(h.kshift_v),
+      "-DPVE_P=" + std::to_string(Pv), "-DPVE_BS=" + std::to_string(bs), "-DPVE_L_BINS=" + std::to_string(l_bins),
+      "-DPVE_L_RING=" + std::to_string(l_ring)};
+  hipFunction_t fn = jit_compile(defs, kPveJitSrc, "pve_jit");
+  if (!fn) return PA_OK;
+  (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  // one workgroup per CU; a workgroup's region holds its docs' records in whole chunks plus one partial chunk per
+  // partition
+  const int64_t T = h.total_wtiles;
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (T + w - 1) / w));
+  const int64_t tiles_per_wg = (T + G - 1) / G;
+  const int64_t C = (tiles_per_wg * 1024 + bs - 1) / bs + Pv;
+  if (C >= (int64_t(1) << 20) || (int64_t)G * C >= (int64_t(1) << 32)) return PA_OK;  // (table ranks, chunk ids)
+  const size_t o_table = al16((size_t)G * C * bs * 4);
+  const size_t o_hist = al16(o_table + (size_t)G * C * 4);
+  const size_t o_used = al16(o_hist + (size_t)G * Pv * 4);
+  const size_t o_off = al16(o_used + (size_t)G * 4);
+  const size_t o_base = al16(o_off + (size_t)G * Pv * 4);
+  const size_t o_index = al16(o_base + (size_t)(Pv + 1) * 8);
+  const size_t total = o_index + (size_t)G * C * 4;
+  int rc = dev_alloc(q->pve_buf, total);
+  if (rc) return rc;
+  q->pve_o_table = o_table;
+  q->pve_o_hist = o_hist;
+  q->pve_o_used = o_used;
+  q->pve_o_off = o_off;
+  q->pve_o_base = o_base;
+  q->pve_o_index = o_index;
+  PveArgsH a;
+  std::memset(&a, 0, sizeof(a));
+  a.total_tiles = T;
+  a.nseg = q->nseg;
+  a.xcd_major = 1;
+  a.chunks_per_wg = C;
+  pve_fill_pointers(q, a);
+  std::vector<PveSegH> js(q->nseg);
+  for (int si = 0; si < q->nseg; ++si) {
+    const DevSeg& d = q->hsegs[si];
+    PveSegH& j = js[si];
+    std::memset(&j, 0, sizeof(j));
+    for (int c = 0; c < nc; ++c) j.src[c] = (uint64_t)(uintptr_t)d.stage[c].words;
+    j.first_tile = d.first_wtile;
+    j.num_docs = d.num_docs;
+    j.num_tiles = d.num_wtiles;
+    for (int li = 0; li < q->num_eager; ++li) {
+      j.lo_t[li] = (uint32_t)d.leaves[li].lo;
+      j.hi_t[li] = (uint32_t)d.leaves[li].span;
+    }
+  }
+  rc = dev_alloc(q->pve_args, sizeof(PveArgsH));
+  if (!rc) rc = dev_alloc(q->pve_segs, sizeof(PveSegH) * js.size());
+  if (rc) return rc;
+  PA_HIP(hipMemcpy(q->pve_args.p, &a, sizeof(a), hipMemcpyHostToDevice));
+  PA_HIP(hipMemcpy(q->pve_segs.p, js.data(), sizeof(PveSegH) * js.size(), hipMemcpyHostToDevice));
+  q->pve_fn = fn;
+  q->pve_waves = w;
+  q->pve_grid = G;
+  q->pve_lds = (int)lds;
+  q->pve_bs = bs;
+  q->pve_chunks = C;
+  PLAN_LOG("pve: W %d grid %d lds %zu C %lld P %d", w, G, lds, (long long)C, Pv);
+  return PA_OK;
+}
+
 int pa_query_prepare(pa_query* q) {
   if (!q) return fail(PA_EINVAL, "null query");
   if (q->prepared) return PA_OK;
@@ -3164,6 +3359,8 @@ int pa_query_prepare(pa_query* q) {
   if (rc) return rc;
   rc = jit_plan(q, P, cus);
   if (rc) return rc;
+  rc = pve_plan(q, P, cus);
+  if (rc) return rc;
   PA_HIP(hipDeviceSynchronize());
   q->prepared = true;
   return PA_OK;
@@ -3186,6 +3383,7 @@ int pa_query_reset(pa_query* q, void* stream) {
 
 int pa_query_scan(pa_query* q, void* stream) {
   if (!q || !q->prepared) return fail(PA_EINVAL, "query not prepared");
+  q->scanned_since_fetch = true;
   if (q->num_tiles == 0) return PA_OK;
   hipStream_t st = (hipStream_t)stream;
   if (q->limit_walk) {  // admitted keys of every segment where the limit can bind, before any pass tests them
@@ -3205,6 +3403,25 @@ int pa_query_scan(pa_query* q, void* stream) {
     PA_HIP(launch_limit_passes(dq, ds, F, q->limit_grid, 0, st));
     PA_HIP(launch_limit_passes(dq, ds, F, q->limit_grid, 1, st));
     PA_HIP(launch_limit_passes(dq, ds, F, q->limit_grid, 2, st));
+    return PA_OK;
+  }
+  if (q->pve_fn) {  // the count-free emit: records in per-workgroup chunks, the partitions' chunk lists, pass C
+    void* pa = q->pve_args.p;
+    void* psg = q->pve_segs.p;
+    void* params[] = {&pa, &psg};
+    PA_HIP(hipModuleLaunchKernel(q->pve_fn, q->pve_grid, 1, 1, q->pve_waves * kWave, 1, 1, q->pve_lds, st, params,
+                                 nullptr));
+    char* b = (char*)q->pve_buf.p;
+    PA_HIP(launch_pve_lists((const uint32_t*)(b + q->pve_o_hist), (uint32_t*)(b + q->pve_o_off),
+                            (uint64_t*)(b + q->pve_o_base), (const uint32_t*)(b + q->pve_o_table),
+                            (const uint32_t*)(b + q->pve_o_used), (uint32_t*)(b + q->pve_o_index), q->pve_grid,
+                            q->hq.pv, q->pve_chunks, q->pve_bs, st));
+    PartScratch ps{};
+    ps.base = (uint64_t*)(b + q->pve_o_base);
+    ps.recs_v = (uint32_t*)b;
+    ps.chunk_index = (const uint32_t*)(b + q->pve_o_index);
+    ps.chunk_shift = __builtin_ctz((unsigned)q->pve_bs);
+    PA_HIP(launch_part_agg(q->part_vk, (const DevQuery*)q->dq.p, ps, q->hq.pv, q->part_lds_c, st));
     return PA_OK;
   }
   if (q->partitioned) {  // count pass, range offsets, emit pass into the partitions, per-partition aggregation
@@ -3279,6 +3496,12 @@ int pa_query_set_accumulator_buffer(pa_query* q, void* device_buffer, uint64_t b
     PA_HIP(hipMemcpy(&a, q->jit_args.p, sizeof(a), hipMemcpyDeviceToHost));
     jit_fill_pointers(q, a);
     PA_HIP(hipMemcpy(q->jit_args.p, &a, sizeof(a), hipMemcpyHostToDevice));
+  }
+  if (q->pve_fn) {
+    PveArgsH a;
+    PA_HIP(hipMemcpy(&a, q->pve_args.p, sizeof(a), hipMemcpyDeviceToHost));
+    pve_fill_pointers(q, a);
+    PA_HIP(hipMemcpy(q->pve_args.p, &a, sizeof(a), hipMemcpyHostToDevice));
   }
   if (q->partitioned) {
     relocate(q->hq_count);
@@ -3384,6 +3607,7 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
     const uint64_t* docs = (const uint64_t*)hsec((int)q->sections.size() - 1);
     q->last_matched = (int64_t)docs[0];
     q->last_reached = (int64_t)docs[2];
+    q->scanned_since_fetch = false;
     if (docs[1]) return fail(PA_EUNSUPPORTED, "group-key table overflow (more distinct groups than slots)");
     if (docs[3]) return fail(PA_EHIP, "internal: partitioned passes disagree on record counts");
     const uint64_t* hc = (const uint64_t*)hsec(0);
@@ -3419,6 +3643,7 @@ int64_t pa_query_fetch(pa_query* q, void* stream, int64_t capacity, int64_t* out
   PA_HIP(hipStreamSynchronize(st));
   q->last_matched = (int64_t)md[0];
   q->last_reached = (int64_t)md[2];
+  q->scanned_since_fetch = false;
   if (md[1]) return fail(PA_EUNSUPPORTED, "group-key table overflow (more distinct groups than slots)");
   if (md[3]) return fail(PA_EHIP, "internal: partitioned passes disagree on record counts");
   const int64_t m = (int64_t)total;
@@ -3782,6 +4007,7 @@ int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t*
 int32_t pa_query_num_eager_literals(const pa_query* q) { return q && q->prepared ? q->num_eager : -1; }
 
 int32_t pa_query_lane_major(const pa_query* q) { return q && q->prepared ? q->lane_major : -1; }
+int32_t pa_query_count_free_emit(const pa_query* q) { return q && q->prepared ? (q->pve_fn ? 1 : 0) : -1; }
 int32_t pa_query_dense_packed(const pa_query* q) {
   return q && q->prepared ? (q->dense_packed ? (q->jit_fn ? 2 : 1) : 0) : -1;
 }
@@ -4210,8 +4436,13 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
     if (rc) return rc;
   }
   hipStream_t st = (hipStream_t)stream;
-  if (docs_scanned < 0) docs_scanned = q->last_matched;
-  if (docs_scanned < 0) return fail(PA_EINVAL, "execution stats: no numDocsScanned (fetch the scan first)");
+  if (docs_scanned < 0 && !q->scanned_since_fetch) docs_scanned = q->last_matched;
+  if (docs_scanned < 0) {  // numDocsScanned of the last scan, from its counter (no fetch since the scan)
+    unsigned long long d = 0;
+    PA_HIP(hipMemcpyAsync(&d, q->sections.back().ptr, 8, hipMemcpyDeviceToHost, st));
+    PA_HIP(hipStreamSynchronize(st));
+    docs_scanned = (int64_t)d;
+  }
   // the scan's own counts of a two-scan AND (fused statistics)
   std::vector<int64_t> fused;
   if (q->leap_leaf >= 0) {

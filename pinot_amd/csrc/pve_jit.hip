@@ -1,0 +1,360 @@
+// The partitioned aggregation's V emit pass without a count pass, specialised to one query shape (configs[2]-like:
+// dictionary group-by columns, one dictionary value column or none, DICT_RANGE filter leaves), compiled at
+// pa_query_prepare by hiprtc with the shape as macros (pa_capi.hip pve_*). Self-contained (hiprtc built-ins only).
+//
+// Reference semantics: DictionaryBasedGroupKeyGenerator raw keys (DictionaryBasedGroupKeyGenerator.java:254-340) over
+// the table-wide key space, the records feeding pass C's SUM / MIN / MAX / COUNT (part_agg_v_fast), the filter as
+// ScanBasedFilterOperator over dictId ranges (SVScanDocIdIterator.java:203).
+//
+// Each workgroup walks its tile range lane-major (lane l: docs [16 l, 16 l + 16) of a 1024-doc tile, unpacked from its
+// own words of the tile image — no per-doc LDS gather), builds one-word records (key offset in its partition | value id
+// << kshift) and puts them into per-partition LDS bins of BS records (claim a slot, write it, count it written; the lane
+// that completes a bin stores it). A full bin goes to the next free BS-record chunk of the workgroup's own region in the
+// record stream (an LDS counter: no count pass, no global atomic), and the chunk table records (partition, rank of the
+// chunk among the workgroup's chunks of that partition). At the end the partial bins leave as chunks padded with
+// sentinels, and the workgroup writes its chunks per partition; pa_pve.hip then lays out every partition's chunk list
+// and pass C reads records through it.
+//
+// Shape macros (lists as {a, b, ...}):
+//   PVE_W waves per workgroup   PVE_IMG dwords of one tile image   PVE_NC staged columns
+//   PVE_NB {bits per column}    PVE_OFF {byte offset of each column's region in the image}
+//   PVE_NL filter leaves (DICT_RANGE), PVE_LC {column}, PVE_LN {negate}, PVE_LE {closes a CNF clause}
+//   PVE_NG group-by columns, PVE_GC {column}, PVE_GS {key stride}
+//   PVE_VC the value column (-1: none)   PVE_KS key bits inside a partition   PVE_P partitions   PVE_BS bin records
+//   PVE_L_BINS, PVE_L_RING LDS byte offsets (state at 0: cnt[P], done[P], chunks[P], next)
+typedef unsigned int u32;
+typedef unsigned long long u64;
+typedef long long i64;
+typedef __attribute__((address_space(3))) u32 l32;
+
+constexpr int W = PVE_W, NC = PVE_NC, NL = PVE_NL, NG = PVE_NG, ND = 16, IMG = PVE_IMG;
+constexpr int NLA = NL > 0 ? NL : 1;
+constexpr int kNB[NC] = PVE_NB;
+constexpr int kOFF[NC] = PVE_OFF;
+constexpr int kLC[NLA] = PVE_LC;
+constexpr int kLN[NLA] = PVE_LN;
+constexpr int kLE[NLA] = PVE_LE;
+constexpr int kGC[NG] = PVE_GC;
+constexpr u32 kGS[NG] = PVE_GS;
+constexpr int VC = PVE_VC, KS = PVE_KS, P = PVE_P, BS = PVE_BS;
+constexpr u32 kSentinel = 0xffffffffu;
+
+constexpr int kJitMax = 6;
+static_assert(NC <= kJitMax && NL <= kJitMax && NG <= 4, "shape beyond the JIT descriptors");
+static_assert(BS % 4 == 0, "bins are whole 16-byte units");
+struct PveSeg {          // one bound segment (scalar loads at segment switches only)
+  u64 src[kJitMax];      // column streams, past the guard words
+  i64 first_tile;        // first 1024-doc tile in the query's tile space
+  int num_docs, num_tiles;
+  u32 lo_t[kJitMax], hi_t[kJitMax];  // DICT_RANGE leaves: MSB-aligned bounds in this segment's dictId space
+};
+struct PveArgs {
+  i64 total_tiles;
+  int nseg, xcd_major;
+  i64 chunks_per_wg;             // C: chunk slots of a workgroup's region
+  u32* recs;                     // record stream: workgroup g's chunks at [g C BS, (g + 1) C BS)
+  u32* table;                    // [G][C]: partition | rank << 12 of every chunk
+  u32* hist;                     // [G][P]: chunks per (workgroup, partition)
+  u32* used;                     // [G]: chunks a workgroup filled
+  unsigned long long* matched;   // [0] numDocsScanned, [3] region overflow (must stay 0)
+};
+typedef const __attribute__((address_space(4))) PveArgs CA;
+typedef const __attribute__((address_space(4))) PveSeg CS;
+
+__device__ __forceinline__ u32 lds_addr(const void* p) { return (u32)(unsigned long)(const l32*)p; }
+template <class T>
+__device__ __forceinline__ T* at(u32 a) { return (T*)(unsigned long)a; }
+
+template <int N>
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+__device__ __forceinline__ void dma16(u32 voff, u64 sbase, u32 dst) {
+  u32 keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(dst));
+}
+__device__ __forceinline__ void dma16m(u32 voff, u64 sbase, u32 dst, u64 mask) {
+  u32 keep;
+  u64 save;
+  asm volatile(
+      "s_mov_b64 %1, exec\n\ts_mov_b64 exec, %5\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
+      : "=&s"(keep), "=&s"(save) : "v"(voff), "s"(sbase), "s"(dst), "s"(mask));
+}
+
+template <int C>
+__device__ __forceinline__ void dma_cols(CS* sg, i64 wt, u32 img, u32 voff) {
+  if constexpr (C < NC) {
+    constexpr int CH = 8 * kNB[C];  // 16-byte chunks of a 1024-doc tile
+    const u64 src = sg->src[C] + (u64)wt * (u64)(128 * kNB[C]);
+    const u32 dst = img + (u32)kOFF[C];
+#pragma unroll
+    for (int k = 0; k < CH / 64; ++k) dma16(voff, src + 1024u * k, dst + 1024u * k);
+    if constexpr (CH % 64) dma16m(voff, src + 1024u * (CH / 64), dst + 1024u * (CH / 64), (1ull << (CH % 64)) - 1ull);
+    dma_cols<C + 1>(sg, wt, img, voff);
+  }
+}
+
+// the lane's 16 words of column C, MSB-aligned (top) or as dictIds
+template <int C, bool TOP>
+__device__ __forceinline__ void unpack(u32 img, int lane, u32 (&v)[ND]) {
+  constexpr int NB = kNB[C];
+  constexpr int K = (ND * NB + 31) / 32 + 1;
+  const u32 region = img + (u32)kOFF[C];
+  const u32 bit0 = (u32)lane * (u32)(ND * NB);
+  u32 w[K];
+  if constexpr ((ND * NB) % 32 != 0) {  // odd NB: odd lanes start 16 bits into a word
+    const u32 sh = bit0 & 16u;
+    const l32* p = at<const l32>(region + 4u * ((bit0 >> 5) - 1u + (sh >> 4)));
+    u32 r[K + 1];
+#pragma unroll
+    for (int j = 0; j <= K; ++j) r[j] = p[j];
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = __builtin_amdgcn_alignbit(r[j], r[j + 1], sh);
+  } else {
+    const l32* p = at<const l32>(region + 4u * (bit0 >> 5));
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = p[j];
+  }
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+    const int s = i * NB, j = s >> 5, o = s & 31;
+    if constexpr (TOP) {
+      v[i] = (o + NB <= 32) ? (w[j] << o) : __builtin_amdgcn_alignbit(w[j], w[j + 1], 32 - o);
+    } else {
+      if (o + NB <= 32) v[i] = __builtin_amdgcn_ubfe(w[j], 32 - o - NB, NB);
+      else v[i] = __builtin_amdgcn_alignbit(w[j], w[j + 1], 32 - o) >> (32 - NB);
+    }
+  }
+}
+
+__device__ __forceinline__ u32 range_nm(const u32 (&t)[ND], u32 lo_t, u32 hi_t) {
+  u32 nm = 0;
+#pragma unroll
+  for (int i = ND - 1; i >= 0; --i) {
+    u32 u;
+    asm("v_sub_u32_e64 %[u], %[t], %[lo]\n\tv_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
+        "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
+        : [nm] "+v"(nm), [u] "=&v"(u) : [t] "v"(t[i]), [lo] "s"(lo_t), [hi] "s"(hi_t) : "vcc");
+  }
+  return nm;
+}
+
+template <int L>
+__device__ __forceinline__ bool leaves(CS* sg, u32 img, int lane, u32& m, u32& clause) {
+  if constexpr (L < NL) {
+    u32 t[ND];
+    unpack<kLC[L], true>(img, lane, t);
+    u32 bits = ~range_nm(t, sg->lo_t[L], sg->hi_t[L]) & 0xffffu;
+    if constexpr (kLN[L]) bits = ~bits & 0xffffu;
+    clause |= bits;
+    if constexpr (kLE[L] != 0) {
+      m &= clause;
+      clause = 0;
+      if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return false;
+    }
+    return leaves<L + 1>(sg, img, lane, m, clause);
+  }
+  return true;
+}
+
+template <int G>
+__device__ __forceinline__ void keys(u32 img, int lane, u32 (&key)[ND]) {
+  if constexpr (G < NG) {
+    u32 id[ND];
+    unpack<kGC[G], false>(img, lane, id);
+#pragma unroll
+    for (int i = 0; i < ND; ++i) key[i] += id[i] * kGS[G];
+    keys<G + 1>(img, lane, key);
+  }
+}
+
+struct Bins {
+  u32 cnt, done, chunks, next, bins;
+  u32* recs;
+  u32* table;
+  i64 region, C;
+  unsigned long long* err;
+};
+
+// store bin p as the workgroup's next chunk (one lane): the bin's BS records, then the chunk's table entry
+__device__ __forceinline__ void flush_bin(const Bins& B, u32 p) {
+  const u32 c = __hip_atomic_fetch_add(at<l32>(B.next), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const u32 r = __hip_atomic_fetch_add(at<l32>(B.chunks) + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+  const __attribute__((address_space(3))) u32x4* src = at<const __attribute__((address_space(3))) u32x4>(B.bins + p * (u32)BS * 4u);
+  if ((i64)c < B.C) {
+    __attribute__((address_space(1))) u32x4* dst =
+        (__attribute__((address_space(1))) u32x4*)(B.recs + (B.region + (i64)c) * BS);
+    u32x4 v[BS / 4];
+#pragma unroll
+    for (int k = 0; k < BS / 4; ++k) v[k] = src[k];
+#pragma unroll
+    for (int k = 0; k < BS / 4; ++k) __builtin_nontemporal_store(v[k], dst + k);
+    ((__attribute__((address_space(1))) u32*)B.table)[B.region + (i64)c] = p | (r << 12);
+  } else {
+    __hip_atomic_fetch_add(B.err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (the bin is read before it restarts: LDS runs one wave's ops in order)
+  at<l32>(B.done)[p] = 0u;
+  at<l32>(B.cnt)[p] = 0u;
+}
+
+// the lane's matching docs (bits of m) into their partitions' bins, 8 at a time: claim, write, count written; a lane
+// that completes a bin flushes it; a record whose bin was full claims again after the flushes
+__device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], const u32 (&val)[ND]) {
+#pragma unroll
+  for (int h = 0; h < ND; h += 8) {
+    bool pend[8];
+    u32 pp[8], rr[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      pend[i] = (m >> (h + i)) & 1u;
+      pp[i] = key[h + i] >> KS;
+      rr[i] = (key[h + i] & ((1u << KS) - 1u)) | (VC >= 0 ? (val[h + i] << KS) : 0u);
+    }
+    for (int round = 0;; ++round) {
+      u32 s[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        s[i] = pend[i] ? __hip_atomic_fetch_add(at<l32>(B.cnt) + pp[i], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                       : 0xffffffffu;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (s[i] < (u32)BS) at<l32>(B.bins)[pp[i] * (u32)BS + s[i]] = rr[i];
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      bool full[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        full[i] = s[i] < (u32)BS &&
+                  __hip_atomic_fetch_add(at<l32>(B.done) + pp[i], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
+                      (u32)BS - 1u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (full[i]) flush_bin(B, pp[i]);
+      bool any = false;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        pend[i] = pend[i] && s[i] >= (u32)BS;
+        any |= pend[i];
+      }
+      if (__builtin_amdgcn_ballot_w64(any) == 0) break;
+      if (round > 0) __builtin_amdgcn_s_sleep(2);
+    }
+  }
+}
+
+// one 1024-doc tile: returns the lane's docs counted in numDocsScanned
+__device__ __forceinline__ u32 tile(const Bins& B, CS* sg, i64 wt, u32 img, int lane) {
+  const i64 rem = (i64)sg->num_docs - wt * 1024;
+  u32 m = 0xffffu;
+  if (rem < 1024) {
+    const i64 n = rem - ND * lane;
+    m = n >= ND ? 0xffffu : (n <= 0 ? 0u : ((1u << n) - 1u));
+  }
+  u32 clause = 0;
+  if (!leaves<0>(sg, img, lane, m, clause)) return 0;
+  if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return 0;
+  u32 key[ND], val[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) key[i] = val[i] = 0u;
+  keys<0>(img, lane, key);
+  if constexpr (VC >= 0) unpack<(VC >= 0 ? VC : 0), false>(img, lane, val);
+  put(B, m, key, val);
+  return (u32)__builtin_popcount(m);
+}
+
+__device__ __forceinline__ int find_segment(CS* segs, int nseg, i64 t) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (segs[mid].first_tile <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a_in, const PveSeg* s_in) {
+  CA* A = (CA*)(unsigned long)a_in;
+  CS* S = (CS*)(unsigned long)s_in;
+  extern __shared__ __attribute__((aligned(16))) u32 smem[];
+  const u32 base = lds_addr(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const i64 T = A->total_tiles, G = gridDim.x;
+  const i64 b = blockIdx.x;
+  const i64 lb = A->xcd_major ? (b % 8) * (G / 8) + (b % 8 < G % 8 ? b % 8 : G % 8) + b / 8 : b;
+  Bins B;
+  B.cnt = base;
+  B.done = base + 4u * P;
+  B.chunks = base + 8u * P;
+  B.next = base + 12u * P;
+  B.bins = base + (u32)PVE_L_BINS;
+  B.recs = A->recs;
+  B.table = A->table;
+  B.C = A->chunks_per_wg;
+  B.region = lb * B.C;
+  B.err = A->matched + 3;
+  for (int i = tid; i < 3 * P + 1; i += W * 64) smem[i] = 0u;
+  __syncthreads();
+  const i64 t0 = lb * T / G, t1 = (lb + 1) * T / G;
+  const u32 ring = base + (u32)PVE_L_RING + (u32)wave * 2u * (u32)IMG * 4u;
+  const u32 voff = 16u * (u32)lane;
+  u32 matched = 0;
+  if (t0 < t1) {
+    const int nseg = A->nseg;
+    int isi = find_segment(S, nseg, t0 + wave);
+    int psi = isi;
+    i64 ifirst = S[isi].first_tile, iend = ifirst + S[isi].num_tiles;
+    i64 pfirst = ifirst, pend = iend;
+    i64 ti = t0 + wave;
+    if (ti < t1) {
+      while (ti >= iend) {
+        ++isi;
+        ifirst = S[isi].first_tile;
+        iend = ifirst + S[isi].num_tiles;
+      }
+      dma_cols<0>(S + isi, ti - ifirst, ring, voff);
+    }
+    ti += W;
+    int slot = 0;
+    for (i64 t = t0 + wave; t < t1; t += W) {
+      vm_wait<0>();  // tile t has landed (and the previous tile's chunk stores have left)
+      if (ti < t1) {
+        while (ti >= iend) {
+          ++isi;
+          ifirst = S[isi].first_tile;
+          iend = ifirst + S[isi].num_tiles;
+        }
+        dma_cols<0>(S + isi, ti - ifirst, ring + (u32)(slot ^ 1) * (u32)IMG * 4u, voff);
+      }
+      ti += W;
+      while (t >= pend) {
+        ++psi;
+        pfirst = S[psi].first_tile;
+        pend = pfirst + S[psi].num_tiles;
+      }
+      matched += tile(B, S + psi, t - pfirst, ring + (u32)slot * (u32)IMG * 4u, lane);
+      slot ^= 1;
+    }
+  }
+  vm_wait<0>();
+  u64 wm = matched;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) wm += __shfl_xor(wm, o);
+  if (lane == 0 && wm) __hip_atomic_fetch_add(A->matched, wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  // the partial bins, padded with sentinels, as chunks; then this workgroup's chunks per partition
+  for (int p = tid; p < P; p += W * 64) {
+    const u32 n = at<l32>(B.cnt)[p];
+    if (n == 0) continue;
+    for (u32 k = n; k < (u32)BS; ++k) at<l32>(B.bins)[(u32)p * (u32)BS + k] = kSentinel;
+    flush_bin(B, (u32)p);
+  }
+  __syncthreads();
+  for (int p = tid; p < P; p += W * 64) A->hist[lb * P + p] = at<l32>(B.chunks)[p];
+  if (tid == 0) {
+    const u32 n = *at<l32>(B.next);
+    A->used[lb] = (i64)n < B.C ? n : (u32)B.C;
+  }
+}

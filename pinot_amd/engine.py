@@ -406,7 +406,8 @@ class GpuQueryExecutor:
                 else:
                     rm.append(np.searchsorted(gd, d).astype(np.int32))
             self.remaps.append(rm)
-        spec.flags = self.flags
+        spec.flags = ((self.flags & 0xffffffff) ^ 0x80000000) - 0x80000000  # (int32: PA_QF_NO_JIT is bit 31)
+        spec.flags2 = (self.flags >> 32) & 0x7fffffff if self.flags >= 0 else 0
         spec.hash_keys_bound = self.hash_keys_bound
 
         # numGroupsLimit (DictionaryBasedGroupKeyGenerator._globalGroupIdUpperBound): the per-segment first-seen group
@@ -509,6 +510,7 @@ class GpuQueryExecutor:
         out["plan"]["eager_literals"] = int(L.lib().pa_query_num_eager_literals(self.handle))
         out["plan"]["lane_major"] = int(L.lib().pa_query_lane_major(self.handle))
         out["plan"]["dense_packed"] = int(L.lib().pa_query_dense_packed(self.handle))
+        out["plan"]["count_free_emit"] = int(L.lib().pa_query_count_free_emit(self.handle))
         out["plan"]["limit_trimming"] = int(L.lib().pa_query_limit_trimming(self.handle))
         return out
 
@@ -623,7 +625,8 @@ class GpuQueryExecutor:
         reference's operator accounting counted by the library (pa_query_execution_stats) over the operator trees this
         host builds per segment (filter_stats.operator_trees = FilterOperatorUtils). Segments whose tree the engine
         does not express (filter_stats "device path") replay the iterators on the host over GPU leaf bitmaps;
-        self.stats_replayed_segments counts them. docs_total: numDocsScanned of the scan (default: the last fetch's)."""
+        self.stats_replayed_segments counts them. docs_total: numDocsScanned of the scan (default: the last scan's own
+        counter, so a call after execute() without a fetch is not stale)."""
         from . import filter_stats as FS
         self.stats_replayed_segments = self.stats_gpu_segments = 0
         if self.match_none or self.handle is None or not self.segs:

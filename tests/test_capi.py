@@ -33,7 +33,7 @@ def test_struct_layout_matches_header():
     assert ctypes.sizeof(L.LeafSpec) == 8
     assert ctypes.sizeof(L.AggSpec) == 24
     assert ctypes.sizeof(L.LeafParams) == 56
-    assert ctypes.sizeof(L.QuerySpec) == 840
+    assert ctypes.sizeof(L.QuerySpec) == 848  # (+ flags2, reserved2)
 
 
 def test_product_path_does_not_import_oracle():

@@ -76,9 +76,11 @@ def _segment(seed, n):
 
 def _stats_and_replay(ex):
     """(engine statistics, host replay) after a scan + fetch of the executor (the fetch fills the statistics)."""
-    res = ex.run()
+    ex.execute()
+    early = ex.execution_stats()  # before the fetch: numDocsScanned from the scan's own counter
+    res = ex.fetch()
     got = (res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter)
-    assert got == ex.execution_stats()  # (a second evaluation over the same scan)
+    assert got == early == ex.execution_stats()  # (evaluated again over the same scan)
     # (the executor holds the reference's rewritten filter: optimizer.py)
     want = FS.server_stats(ex.query, ex.segs, lambda si: ex.leaf_bitmaps(si))
     return got, want
