@@ -528,7 +528,7 @@ struct pa_query {
   int pve_waves = 0, pve_grid = 0, pve_lds = 0, pve_bs = 0;
   int64_t pve_chunks = 0;  // chunk slots per workgroup
   DevBuf pve_args, pve_segs, pve_buf;
-  size_t pve_o_table = 0, pve_o_hist = 0, pve_o_used = 0, pve_o_off = 0, pve_o_base = 0, pve_o_index = 0;
+  size_t pve_o_table = 0, pve_o_hist = 0, pve_o_used = 0, pve_o_off = 0, pve_o_base = 0, pve_o_index = 0, pve_o_tot = 0;
   int has_mv = 0;
   bool hashed = false;           // packed 64-bit keys through a global open-addressing table
   int key_words = 1;             // hashed: 2 = two-word keys ([k0, k1, state] per slot)
@@ -3115,7 +3115,8 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
   const pa_query_spec& s = q->spec;
   const DevQuery& h = q->hq;
   if (!q->partitioned || q->split_emit || h.hll_agg >= 0 || q->limit_mode || q->limit_walk || q->hashed) return PA_OK;
-  if ((s.flags & PA_QF_NO_JIT) || (s.flags2 & PA_QF2_NO_COUNT_FREE) || std::getenv("PA_NO_JIT") || std::getenv("PA_DEBUG_EMIT"))
+  if ((s.flags & PA_QF_NO_JIT) || (s.flags2 & PA_QF2_NO_COUNT_FREE) || std::getenv("PA_NO_JIT") ||
+      (std::getenv("PA_DEBUG_EMIT") && !std::getenv("PA_PVE_DBG")))
     return PA_OK;
   if ((h.v_fmt != V_FMT_ID && h.v_fmt != V_FMT_KEY) || h.rec_words_v != 1 || q->part_vk == kVkGeneric) return PA_OK;
   if (q->nseg == 0 || s.num_group_by < 1 || s.num_group_by > 4 || q->num_eager != (int)q->literals.size() ||
@@ -3164,9 +3165,12 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
   }
   if ((uint64_t)q->num_keys > 0xffffffffull) return PA_OK;
   // LDS: per-partition state (cnt, done, chunks), the chunk counter, the bins, then each wave's two tile images
-  const int Pv = h.pv, bs = 32;
+  // bins of 32 records (128 bytes), chunks of 4 bins (512-byte runs for pass C: longer runs measured no faster there,
+  // and every (workgroup, partition) pads its last chunk; PA_PVE_SC: measurement override)
+  const int Pv = h.pv, bs = 32, sc = std::getenv("PA_PVE_SC") ? std::atoi(std::getenv("PA_PVE_SC")) : 4;
+  if (sc < 1 || sc > 64 || (sc & (sc - 1))) return PA_OK;
   auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  const size_t l_bins = al16((size_t)(3 * Pv + 1) * 4);
+  const size_t l_bins = al16((size_t)(5 * Pv + 1) * 4);
   const size_t l_ring = al16(l_bins + (size_t)Pv * bs * 4);
   const size_t img_b = (size_t)h.image_dwords_max * 4;
   int w = 0;
@@ -3196,8 +3200,11 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
       "-DPVE_NL=" + std::to_string(q->num_eager), "-DPVE_LC=" + int_list(pad1(lc)), "-DPVE_LN=" + int_list(pad1(ln)),
       "-DPVE_LE=" + int_list(pad1(le)), "-DPVE_NG=" + std::to_string(s.num_group_by), "-DPVE_GC=" + int_list(gc),
       "-DPVE_GS=" + gss, "-DPVE_VC=" + std::to_string(vc), "-DPVE_KS=" + std::to_string(h.kshift_v),
-      "-DPVE_P=" + std::to_string(Pv), "-DPVE_BS=" + std::to_string(bs), "-DPVE_L_BINS=" + std::to_string(l_bins),
+      "-DPVE_P=" + std::to_string(Pv), "-DPVE_BS=" + std::to_string(bs), "-DPVE_SC=" + std::to_string(sc),
+      "-DPVE_L_BINS=" + std::to_string(l_bins),
       "-DPVE_L_RING=" + std::to_string(l_ring)};
+  if (const char* dbg = std::getenv("PA_PVE_DBG")) defs.push_back(std::string("-DPVE_DBG=") + dbg);  // (measurement)
+  if (const char* pb = std::getenv("PA_PVE_PB")) defs.push_back(std::string("-DPVE_PB=") + pb);      // (measurement)
   hipFunction_t fn = jit_compile(defs, kPveJitSrc, "pve_jit");
   if (!fn) return PA_OK;
   (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -3206,15 +3213,17 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
   const int64_t T = h.total_wtiles;
   const int G = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (T + w - 1) / w));
   const int64_t tiles_per_wg = (T + G - 1) / G;
-  const int64_t C = (tiles_per_wg * 1024 + bs - 1) / bs + Pv;
+  const int64_t cr = (int64_t)bs * sc;  // records per chunk
+  const int64_t C = (tiles_per_wg * 1024 + cr - 1) / cr + Pv;
   if (C >= (int64_t(1) << 20) || (int64_t)G * C >= (int64_t(1) << 32)) return PA_OK;  // (table ranks, chunk ids)
-  const size_t o_table = al16((size_t)G * C * bs * 4);
+  const size_t o_table = al16((size_t)G * C * cr * 4);
   const size_t o_hist = al16(o_table + (size_t)G * C * 4);
   const size_t o_used = al16(o_hist + (size_t)G * Pv * 4);
   const size_t o_off = al16(o_used + (size_t)G * 4);
   const size_t o_base = al16(o_off + (size_t)G * Pv * 4);
   const size_t o_index = al16(o_base + (size_t)(Pv + 1) * 8);
-  const size_t total = o_index + (size_t)G * C * 4;
+  const size_t o_tot = al16(o_index + (size_t)G * C * 4);
+  const size_t total = o_tot + (size_t)Pv * 4;
   int rc = dev_alloc(q->pve_buf, total);
   if (rc) return rc;
   q->pve_o_table = o_table;
@@ -3223,6 +3232,7 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
   q->pve_o_off = o_off;
   q->pve_o_base = o_base;
   q->pve_o_index = o_index;
+  q->pve_o_tot = o_tot;
   PveArgsH a;
   std::memset(&a, 0, sizeof(a));
   a.total_tiles = T;
@@ -3253,7 +3263,7 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
   q->pve_waves = w;
   q->pve_grid = G;
   q->pve_lds = (int)lds;
-  q->pve_bs = bs;
+  q->pve_bs = (int)cr;
   q->pve_chunks = C;
   PLAN_LOG("pve: W %d grid %d lds %zu C %lld P %d", w, G, lds, (long long)C, Pv);
   return PA_OK;
@@ -3414,8 +3424,8 @@ int pa_query_scan(pa_query* q, void* stream) {
     char* b = (char*)q->pve_buf.p;
     PA_HIP(launch_pve_lists((const uint32_t*)(b + q->pve_o_hist), (uint32_t*)(b + q->pve_o_off),
                             (uint64_t*)(b + q->pve_o_base), (const uint32_t*)(b + q->pve_o_table),
-                            (const uint32_t*)(b + q->pve_o_used), (uint32_t*)(b + q->pve_o_index), q->pve_grid,
-                            q->hq.pv, q->pve_chunks, q->pve_bs, st));
+                            (const uint32_t*)(b + q->pve_o_used), (uint32_t*)(b + q->pve_o_index),
+                            (uint32_t*)(b + q->pve_o_tot), q->pve_grid, q->hq.pv, q->pve_chunks, q->pve_bs, st));
     PartScratch ps{};
     ps.base = (uint64_t*)(b + q->pve_o_base);
     ps.recs_v = (uint32_t*)b;

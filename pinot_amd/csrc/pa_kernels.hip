@@ -1410,6 +1410,19 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   const int64_t vbase = q->v_base, vstep = q->v_step;
   constexpr int kB = 16;  // records per thread in flight
   const uint64_t span = (uint64_t)kB * kPartAggThreads;
+  // chunked records (count-free emit): the chunk ids of a batch are loaded one batch ahead, so a record load never
+  // waits for its index load
+  const AS1 uint32_t* cix = ps.chunk_index ? gp(ps.chunk_index) : nullptr;
+  const int csh = (int)ps.chunk_shift;
+  const uint64_t cmask = cix ? (1ull << csh) - 1ull : 0ull;
+  uint32_t cid[kB];
+  if (cix) {
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const uint64_t ri = r0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
+      cid[j] = ri < r1 ? cix[ri >> csh] : 0u;
+    }
+  }
   for (uint64_t b0 = r0; b0 < r1; b0 += span) {
     uint32_t w0[kB], w1[kB], w2[kB];
 #pragma unroll
@@ -1418,13 +1431,18 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
       w0[j] = kSentinel;
       w1[j] = w2[j] = 0u;
       if (ri < r1) {
-        const uint64_t pi = ps.chunk_index ? ((uint64_t)gp(ps.chunk_index)[ri >> ps.chunk_shift] << ps.chunk_shift) |
-                                                 (ri & ((1ull << ps.chunk_shift) - 1ull))
-                                           : ri;
+        const uint64_t pi = cix ? ((uint64_t)cid[j] << csh) | (ri & cmask) : ri;
         const AS1 uint32_t* rec = recs + pi * (uint64_t)W;
         w0[j] = __builtin_nontemporal_load(rec);
         if (fmt == V_FMT_32 || fmt == V_FMT_64) w1[j] = __builtin_nontemporal_load(rec + 1);
         if (fmt == V_FMT_64) w2[j] = __builtin_nontemporal_load(rec + 2);
+      }
+    }
+    if (cix) {
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        const uint64_t ri = b0 + span + (uint64_t)j * kPartAggThreads + threadIdx.x;
+        cid[j] = ri < r1 ? cix[ri >> csh] : 0u;
       }
     }
     int64_t iv[kB];

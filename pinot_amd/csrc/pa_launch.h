@@ -170,7 +170,8 @@ hipError_t launch_stat_counts(const StatCountJob* jobs, int nj, int64_t blocks, 
 hipError_t launch_leapfrogs(const LfJob* jobs, int nj, int64_t lanes, hipStream_t s);
 // count-free partitioned emit (pa_pve.hip): per-partition chunk lists from the emit workgroups' chunk tables
 hipError_t launch_pve_lists(const uint32_t* hist, uint32_t* off, uint64_t* base, const uint32_t* table,
-                            const uint32_t* used, uint32_t* index, int G, int P, int64_t C, int bs, hipStream_t s);
+                            const uint32_t* used, uint32_t* index, uint32_t* tot, int G, int P, int64_t C, int cr,
+                            hipStream_t s);
 hipError_t set_scan_lds_limit(int strategy, int steps, int lm, int bytes);
 hipError_t scan_occupancy(int strategy, int steps, int lm, int lds_bytes, int* blocks_per_cu);
 hipError_t launch_scan(int strategy, int steps, int lm, int grid, int lds_bytes, const DevQuery* q, const DevSeg* segs,

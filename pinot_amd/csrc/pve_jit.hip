@@ -21,7 +21,8 @@
 //   PVE_NL filter leaves (DICT_RANGE), PVE_LC {column}, PVE_LN {negate}, PVE_LE {closes a CNF clause}
 //   PVE_NG group-by columns, PVE_GC {column}, PVE_GS {key stride}
 //   PVE_VC the value column (-1: none)   PVE_KS key bits inside a partition   PVE_P partitions   PVE_BS bin records
-//   PVE_L_BINS, PVE_L_RING LDS byte offsets (state at 0: cnt[P], done[P], chunks[P], next)
+//   PVE_SC bins per chunk (a chunk is SC x BS consecutive records of one partition: pass C reads long runs)
+//   PVE_L_BINS, PVE_L_RING LDS byte offsets (state at 0: cnt[P], done[P], chunks[P], cur[P], fill[P], next)
 typedef unsigned int u32;
 typedef unsigned long long u64;
 typedef long long i64;
@@ -36,8 +37,14 @@ constexpr int kLN[NLA] = PVE_LN;
 constexpr int kLE[NLA] = PVE_LE;
 constexpr int kGC[NG] = PVE_GC;
 constexpr u32 kGS[NG] = PVE_GS;
-constexpr int VC = PVE_VC, KS = PVE_KS, P = PVE_P, BS = PVE_BS;
+constexpr int VC = PVE_VC, KS = PVE_KS, P = PVE_P, BS = PVE_BS, SC = PVE_SC;
 constexpr u32 kSentinel = 0xffffffffu;
+#ifndef PVE_PB
+#define PVE_PB 4  // records per lane per put round
+#endif
+#ifndef PVE_DBG
+#define PVE_DBG 0  // measurement only (PA_PVE_DBG): 1 = records built but not put, 2 = full bins not stored
+#endif
 
 constexpr int kJitMax = 6;
 static_assert(NC <= kJitMax && NL <= kJitMax && NG <= 4, "shape beyond the JIT descriptors");
@@ -52,7 +59,7 @@ struct PveArgs {
   i64 total_tiles;
   int nseg, xcd_major;
   i64 chunks_per_wg;             // C: chunk slots of a workgroup's region
-  u32* recs;                     // record stream: workgroup g's chunks at [g C BS, (g + 1) C BS)
+  u32* recs;                     // record stream: workgroup g's chunks at [g C SC BS, (g + 1) C SC BS)
   u32* table;                    // [G][C]: partition | rank << 12 of every chunk
   u32* hist;                     // [G][P]: chunks per (workgroup, partition)
   u32* used;                     // [G]: chunks a workgroup filled
@@ -170,71 +177,134 @@ __device__ __forceinline__ void keys(u32 img, int lane, u32 (&key)[ND]) {
 }
 
 struct Bins {
-  u32 cnt, done, chunks, next, bins;
+  u32 cnt, done, chunks, cur, fill, next, bins;
   u32* recs;
   u32* table;
   i64 region, C;
   unsigned long long* err;
 };
 
-// store bin p as the workgroup's next chunk (one lane): the bin's BS records, then the chunk's table entry
-__device__ __forceinline__ void flush_bin(const Bins& B, u32 p) {
-  const u32 c = __hip_atomic_fetch_add(at<l32>(B.next), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  const u32 r = __hip_atomic_fetch_add(at<l32>(B.chunks) + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-  const __attribute__((address_space(3))) u32x4* src = at<const __attribute__((address_space(3))) u32x4>(B.bins + p * (u32)BS * 4u);
-  if ((i64)c < B.C) {
-    __attribute__((address_space(1))) u32x4* dst =
-        (__attribute__((address_space(1))) u32x4*)(B.recs + (B.region + (i64)c) * BS);
-    u32x4 v[BS / 4];
-#pragma unroll
-    for (int k = 0; k < BS / 4; ++k) v[k] = src[k];
-#pragma unroll
-    for (int k = 0; k < BS / 4; ++k) __builtin_nontemporal_store(v[k], dst + k);
-    ((__attribute__((address_space(1))) u32*)B.table)[B.region + (i64)c] = p | (r << 12);
+// the chunk slot of bin p's next flush (one lane per bin): the partition's current chunk of this workgroup, a new one
+// every SC bins (its table entry = partition | its rank among the workgroup's chunks of that partition). One bin per
+// partition, flushed once full: the partition's chunk state has one writer at a time. Returns the record offset.
+__device__ __forceinline__ i64 bin_slot(const Bins& B, u32 p) {
+  const u32 f = at<l32>(B.fill)[p];
+  u32 c;
+  if (f == 0) {
+    c = __hip_atomic_fetch_add(at<l32>(B.next), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const u32 r = at<l32>(B.chunks)[p];
+    at<l32>(B.chunks)[p] = r + 1u;
+    at<l32>(B.cur)[p] = c;
+    if ((i64)c < B.C) ((__attribute__((address_space(1))) u32*)B.table)[B.region + (i64)c] = p | (r << 12);
   } else {
-    __hip_atomic_fetch_add(B.err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c = at<l32>(B.cur)[p];
   }
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (the bin is read before it restarts: LDS runs one wave's ops in order)
+  at<l32>(B.fill)[p] = f + 1u == (u32)SC ? 0u : f + 1u;
+  if ((i64)c >= B.C) {
+    __hip_atomic_fetch_add(B.err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return -1;
+  }
+  return ((B.region + (i64)c) * SC + f) * BS;
+}
+
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+
+// Every bin the wave completed (full[i] of its lanes) leaves together: eight lanes per bin (16 bytes each, so one store
+// instruction writes eight whole bins), the group's first lane takes the chunk slot and restarts the bin after the copy.
+__device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE_PB], const u32 (&pp)[PVE_PB], int lane) {
+  u64 fm[PVE_PB];
+  u64 any = 0;
+#pragma unroll
+  for (int i = 0; i < PVE_PB; ++i) {
+    fm[i] = __builtin_amdgcn_ballot_w64(full[i]);
+    any |= fm[i];
+  }
+  if (any == 0) return;
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  const int grp = lane >> 3, sub = lane & 7;
+  u32 mine = 0xffffffffu;
+  int g = 0;
+  auto round = [&]() {
+    const bool on = grp < g;
+    i64 at_rec = -1;
+    if (on && sub == 0) at_rec = bin_slot(B, mine);
+    const int leader = lane & ~7;
+    const i64 dst_rec = ((i64)__builtin_amdgcn_ds_bpermute(leader << 2, (int)(u32)at_rec) & 0xffffffffll) |
+                        ((i64)__builtin_amdgcn_ds_bpermute(leader << 2, (int)(u32)((u64)at_rec >> 32)) << 32);
+    if (on && dst_rec >= 0 && PVE_DBG != 2) {
+      const u32x4 v = *at<const __attribute__((address_space(3))) u32x4>(B.bins + mine * (u32)BS * 4u + 16u * (u32)sub);
+      __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4*)(B.recs + dst_rec) + sub);
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (the bin is read before it restarts: LDS runs one wave's ops in order)
+    if (on && sub == 0) {
+      at<l32>(B.done)[mine] = 0u;
+      at<l32>(B.cnt)[mine] = 0u;
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    g = 0;
+    mine = 0xffffffffu;
+  };
+#pragma unroll
+  for (int i = 0; i < PVE_PB; ++i) {
+    u64 m = fm[i];
+    while (m) {
+      const int l = __builtin_ctzll(m);
+      m &= m - 1;
+      const u32 p = (u32)__builtin_amdgcn_readlane((int)pp[i], l);
+      if (grp == g) mine = p;
+      if (++g == 8) round();
+    }
+  }
+  if (g) round();
+}
+
+// the end of the pass: bin p (one thread) as a chunk slot, copied by that thread
+__device__ __forceinline__ void flush_one(const Bins& B, u32 p) {
+  const i64 dst_rec = bin_slot(B, p);
+  if (dst_rec >= 0) {
+    const __attribute__((address_space(3))) u32x4* src =
+        at<const __attribute__((address_space(3))) u32x4>(B.bins + p * (u32)BS * 4u);
+    __attribute__((address_space(1))) u32x4* dst = (__attribute__((address_space(1))) u32x4*)(B.recs + dst_rec);
+    for (int k = 0; k < BS / 4; ++k) __builtin_nontemporal_store(src[k], dst + k);
+  }
   at<l32>(B.done)[p] = 0u;
   at<l32>(B.cnt)[p] = 0u;
 }
 
 // the lane's matching docs (bits of m) into their partitions' bins, 8 at a time: claim, write, count written; a lane
 // that completes a bin flushes it; a record whose bin was full claims again after the flushes
-__device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], const u32 (&val)[ND]) {
+__device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], const u32 (&val)[ND], int lane) {
+  constexpr int PB = PVE_PB;
 #pragma unroll
-  for (int h = 0; h < ND; h += 8) {
-    bool pend[8];
-    u32 pp[8], rr[8];
+  for (int h = 0; h < ND; h += PB) {
+    bool pend[PB];
+    u32 pp[PB], rr[PB];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < PB; ++i) {
       pend[i] = (m >> (h + i)) & 1u;
       pp[i] = key[h + i] >> KS;
       rr[i] = (key[h + i] & ((1u << KS) - 1u)) | (VC >= 0 ? (val[h + i] << KS) : 0u);
     }
     for (int round = 0;; ++round) {
-      u32 s[8];
+      u32 s[PB];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < PB; ++i)
         s[i] = pend[i] ? __hip_atomic_fetch_add(at<l32>(B.cnt) + pp[i], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
                        : 0xffffffffu;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < PB; ++i)
         if (s[i] < (u32)BS) at<l32>(B.bins)[pp[i] * (u32)BS + s[i]] = rr[i];
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      bool full[8];
+      bool full[PB];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < PB; ++i)
         full[i] = s[i] < (u32)BS &&
                   __hip_atomic_fetch_add(at<l32>(B.done) + pp[i], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
                       (u32)BS - 1u;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (full[i]) flush_bin(B, pp[i]);
+      flush_full(B, full, pp, lane);
       bool any = false;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < PB; ++i) {
         pend[i] = pend[i] && s[i] >= (u32)BS;
         any |= pend[i];
       }
@@ -260,7 +330,14 @@ __device__ __forceinline__ u32 tile(const Bins& B, CS* sg, i64 wt, u32 img, int 
   for (int i = 0; i < ND; ++i) key[i] = val[i] = 0u;
   keys<0>(img, lane, key);
   if constexpr (VC >= 0) unpack<(VC >= 0 ? VC : 0), false>(img, lane, val);
-  put(B, m, key, val);
+  if constexpr (PVE_DBG == 1) {
+    u32 x = 0;
+#pragma unroll
+    for (int i = 0; i < ND; ++i) x ^= key[i] + val[i];
+    if (x == 0x9e3779b9u) *at<l32>(B.next) = x;  // (keeps the records live)
+    return (u32)__builtin_popcount(m);
+  }
+  put(B, m, key, val, lane);
   return (u32)__builtin_popcount(m);
 }
 
@@ -288,14 +365,16 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
   B.cnt = base;
   B.done = base + 4u * P;
   B.chunks = base + 8u * P;
-  B.next = base + 12u * P;
+  B.cur = base + 12u * P;
+  B.fill = base + 16u * P;
+  B.next = base + 20u * P;
   B.bins = base + (u32)PVE_L_BINS;
   B.recs = A->recs;
   B.table = A->table;
   B.C = A->chunks_per_wg;
   B.region = lb * B.C;
   B.err = A->matched + 3;
-  for (int i = tid; i < 3 * P + 1; i += W * 64) smem[i] = 0u;
+  for (int i = tid; i < 5 * P + 1; i += W * 64) smem[i] = 0u;
   __syncthreads();
   const i64 t0 = lb * T / G, t1 = (lb + 1) * T / G;
   const u32 ring = base + (u32)PVE_L_RING + (u32)wave * 2u * (u32)IMG * 4u;
@@ -349,9 +428,20 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
     const u32 n = at<l32>(B.cnt)[p];
     if (n == 0) continue;
     for (u32 k = n; k < (u32)BS; ++k) at<l32>(B.bins)[(u32)p * (u32)BS + k] = kSentinel;
-    flush_bin(B, (u32)p);
+    flush_one(B, (u32)p);
   }
   __syncthreads();
+  // the unfilled bins of each partition's last chunk: sentinel records (pass C skips them)
+  for (int p = tid; p < P; p += W * 64) {
+    const u32 f = at<l32>(B.fill)[p];
+    if (f == 0) continue;
+    const u32 c = at<l32>(B.cur)[p];
+    if ((i64)c >= B.C) continue;
+    __attribute__((address_space(1))) u32x4* dst =
+        (__attribute__((address_space(1))) u32x4*)(B.recs + ((B.region + (i64)c) * SC + f) * BS);
+    const u32x4 sv = {kSentinel, kSentinel, kSentinel, kSentinel};
+    for (u32 k = 0; k < ((u32)SC - f) * (u32)BS / 4u; ++k) __builtin_nontemporal_store(sv, dst + k);
+  }
   for (int p = tid; p < P; p += W * 64) A->hist[lb * P + p] = at<l32>(B.chunks)[p];
   if (tid == 0) {
     const u32 n = *at<l32>(B.next);
