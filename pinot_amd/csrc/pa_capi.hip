@@ -4518,11 +4518,19 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
   struct CountReq { int si, mask; int32_t mv; };
   struct LeapReq { int si; const Leap* lp; };
   std::vector<CountReq> creq;
-  std::vector<LeapReq> lreq;
+  std::vector<LeapReq> lreq, breq;  // breq: two single-value scans leap-frogged (closed form over label counts)
+  std::vector<char> seg_bm(q->nseg, 0);
   for (int si = 0; si < q->nseg; ++si) {
     if (state[si] != 0) continue;
     for (const auto& c : plans[si].counts) creq.push_back(CountReq{si, mask_of(si, c.first), c.second});
     for (const Leap& lp : plans[si].leaps) {
+      if (lp.el.size() == 2 && !lp.tail && lp.el[0].kind == LF_SCAN && lp.el[1].kind == LF_SCAN && lp.el[0].mv < 0 &&
+          lp.el[1].mv < 0 && (int)lp.el[0].prog.size() <= kBitProgMax && (int)lp.el[1].prog.size() <= kBitProgMax) {
+        // AndDocIdIterator over two SVScanDocIdIterators reads num_docs + |A & B| + leaps (pa_kernels.hip word_leaps)
+        breq.push_back(LeapReq{si, &lp});
+        seg_bm[si] = 1;
+        continue;
+      }
       for (const Elem& e : lp.el) {
         mask_of(si, e.prog);
         for (const Elem& s : e.subs) mask_of(si, s.prog);
@@ -4530,18 +4538,38 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
       lreq.push_back(LeapReq{si, &lp});
     }
   }
+  for (const auto& m : masks) seg_bm[m.first] = 1;
   int gpu_segs = 0;
-  if (!masks.empty()) {
+  if (!masks.empty() || !breq.empty()) {
     for (int l = 0; l < nl; ++l)
       if (leaf_lit[l] < 0) return fail(PA_EUNSUPPORTED, "filter leaf " + std::to_string(l) + " has no literal in the plan");
     std::vector<int64_t> bm_off(q->nseg, -1);
     size_t bm_words = 0;
-    for (const auto& m : masks)
-      if (bm_off[m.first] < 0) {
-        bm_off[m.first] = (int64_t)bm_words;
-        bm_words += (size_t)nl * (size_t)leaf_words(q->segs[m.first]->num_docs);
+    for (int si = 0; si < q->nseg; ++si)
+      if (seg_bm[si]) {
+        bm_off[si] = (int64_t)bm_words;
+        bm_words += (size_t)nl * (size_t)leaf_words(q->segs[si]->num_docs);
         ++gpu_segs;
       }
+    // the two-scan leap-frogs: pa_bitmap_counts' jobs (programs A, B over the segment's leaf bitmaps)
+    std::vector<BitJob> bjobs(breq.size());
+    std::vector<int32_t> btok(breq.size() * 2 * kBitProgMax, 0);
+    std::vector<size_t> bsc(breq.size());
+    size_t bsc_words = 0;
+    int64_t bblocks = 0;
+    for (size_t r = 0; r < breq.size(); ++r) {
+      const Leap& lp = *breq[r].lp;
+      const int64_t n = q->segs[breq[r].si]->num_docs, words = leaf_words(n);
+      int32_t* t = btok.data() + r * 2 * kBitProgMax;
+      const int la = (int)lp.el[0].prog.size(), lb = (int)lp.el[1].prog.size();
+      std::copy(lp.el[0].prog.begin(), lp.el[0].prog.end(), t);
+      std::copy(lp.el[1].prog.begin(), lp.el[1].prog.end(), t + kBitProgMax);
+      bsc[r] = bsc_words;
+      bsc_words += (size_t)bit_count_scratch_words(words) + 2;
+      bjobs[r] = make_bit_job(nullptr, words, n, bblocks, nullptr, la, lb, nullptr, nullptr);
+      renumber_leaves(bjobs[r], t);
+      bblocks += bjobs[r].nb;
+    }
     std::vector<int64_t> mk_off(masks.size());
     size_t mk_words = 0;
     std::vector<int32_t> toks;
@@ -4612,11 +4640,15 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
         lblocks += leaf_bitmap_blocks(n);
       }
     }
-    const size_t nres = creq.size() + 3 * lreq.size();
+    const size_t nres = creq.size() + 3 * lreq.size() + 4 * breq.size();
     const size_t o_bm = 0, o_mk = align256(4 * bm_words), o_cells = o_mk + align256(4 * mk_words),
                  o_res = o_cells + align256(4 * std::max<size_t>(1, cell_words)),
-                 o_mj = o_res + align256(8 * std::max<size_t>(1, nres)),
-                 o_cj = o_mj + align256(sizeof(StatMaskJob) * mjobs.size()),
+                 o_bsc = o_res + align256(8 * std::max<size_t>(1, nres)),
+                 o_bj = o_bsc + align256(4 * std::max<size_t>(1, bsc_words)),
+                 o_btok = o_bj + align256(sizeof(BitJob) * std::max<size_t>(1, bjobs.size())),
+                 o_btab = o_btok + align256(4 * std::max<size_t>(1, btok.size())),
+                 o_mj = o_btab + align256(4 * (size_t)std::max<int64_t>(1, bblocks)),
+                 o_cj = o_mj + align256(sizeof(StatMaskJob) * std::max<size_t>(1, mjobs.size())),
                  o_lj = o_cj + align256(sizeof(StatCountJob) * std::max<size_t>(1, cjobs.size())),
                  o_fj = o_lj + align256(sizeof(LfJob) * std::max<size_t>(1, ljobs.size())),
                  o_tok = o_fj + align256(sizeof(LeafJob) * std::max<size_t>(1, leafjobs.size())),
@@ -4660,14 +4692,28 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
       j.out = res + creq.size() + 3 * r;
     }
     for (LeafJob& lj : leafjobs) lj.out = (uint32_t*)(base + o_bm) + (intptr_t)lj.out;
-    PA_HIP(hipMemcpyAsync(base + o_mj, mjobs.data(), sizeof(StatMaskJob) * mjobs.size(), hipMemcpyHostToDevice, st));
+    const size_t bres = creq.size() + 3 * lreq.size();
+    for (size_t r = 0; r < breq.size(); ++r) {
+      BitJob& j = bjobs[r];
+      j.bm = bm + bm_off[breq[r].si];
+      j.tok = (const int32_t*)(base + o_btok) + r * 2 * kBitProgMax;
+      j.scratch = (uint32_t*)(base + o_bsc) + bsc[r];
+      j.part = (unsigned long long*)(((uintptr_t)(j.scratch + 2 * j.nb) + 7) & ~(uintptr_t)7);
+      j.out = res + bres + 4 * r;
+    }
+    if (!mjobs.empty())
+      PA_HIP(hipMemcpyAsync(base + o_mj, mjobs.data(), sizeof(StatMaskJob) * mjobs.size(), hipMemcpyHostToDevice, st));
+    if (!bjobs.empty()) {
+      PA_HIP(hipMemcpyAsync(base + o_bj, bjobs.data(), sizeof(BitJob) * bjobs.size(), hipMemcpyHostToDevice, st));
+      PA_HIP(hipMemcpyAsync(base + o_btok, btok.data(), 4 * btok.size(), hipMemcpyHostToDevice, st));
+    }
     if (!cjobs.empty())
       PA_HIP(hipMemcpyAsync(base + o_cj, cjobs.data(), sizeof(StatCountJob) * cjobs.size(), hipMemcpyHostToDevice, st));
     if (!ljobs.empty())
       PA_HIP(hipMemcpyAsync(base + o_lj, ljobs.data(), sizeof(LfJob) * ljobs.size(), hipMemcpyHostToDevice, st));
     if (!leafjobs.empty())
       PA_HIP(hipMemcpyAsync(base + o_fj, leafjobs.data(), sizeof(LeafJob) * leafjobs.size(), hipMemcpyHostToDevice, st));
-    PA_HIP(hipMemcpyAsync(base + o_tok, toks.data(), 4 * toks.size(), hipMemcpyHostToDevice, st));
+    if (!toks.empty()) PA_HIP(hipMemcpyAsync(base + o_tok, toks.data(), 4 * toks.size(), hipMemcpyHostToDevice, st));
     PA_HIP(hipMemsetAsync(res, 0, 8 * std::max<size_t>(1, nres), st));
     if (!leafjobs.empty())
       PA_HIP(launch_leaf_bitmaps_batch((const LeafJob*)(base + o_fj), (int)leafjobs.size(), lblocks, st));
@@ -4675,12 +4721,16 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
                              (const int32_t*)(base + o_tok), st));
     PA_HIP(launch_stat_counts((const StatCountJob*)(base + o_cj), (int)cjobs.size(), cblocks, st));
     PA_HIP(launch_leapfrogs((const LfJob*)(base + o_lj), (int)ljobs.size(), lanes, st));
+    PA_HIP(launch_bit_counts_batch((const BitJob*)(base + o_bj), (int)bjobs.size(), bblocks, true,
+                                   (int32_t*)(base + o_btab), st));
     std::vector<int64_t> h(std::max<size_t>(1, nres));
     PA_HIP(hipMemcpyAsync(h.data(), res, 8 * h.size(), hipMemcpyDeviceToHost, st));
     PA_HIP(hipStreamSynchronize(st));
     for (size_t r = 0; r < creq.size(); ++r) seg_in[creq[r].si] += h[r];
     for (size_t r = 0; r < lreq.size(); ++r)
       seg_in[lreq[r].si] += h[creq.size() + 3 * r] + (lreq[r].lp->tail ? h[creq.size() + 3 * r + 1] : 0);
+    for (size_t r = 0; r < breq.size(); ++r)
+      seg_in[breq[r].si] += (int64_t)q->segs[breq[r].si]->num_docs + h[bres + 4 * r + 2] + h[bres + 4 * r + 3];
   }
   int64_t in_filter = 0;
   for (int si = 0; si < q->nseg; ++si) {
