@@ -3122,57 +3122,64 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
   if (q->nseg == 0 || s.num_group_by < 1 || s.num_group_by > 4 || q->num_eager != (int)q->literals.size() ||
       q->num_eager > 6 || h.pv > 4096 || h.kshift_v < 1)
     return PA_OK;
-  const DevSeg& d0 = q->hsegs[0];
-  const int nc = d0.num_staged;
-  if (nc < 1 || nc > 6) return PA_OK;
-  for (const DevSeg& d : q->hsegs) {
-    if (d.num_staged != nc || d.vremap) return PA_OK;
-    for (int j = 0; j < s.num_group_by; ++j)
-      if (d.remap[j]) return PA_OK;
-    for (int k = 0; k < nc; ++k)
-      if (d.stage[k].nbits != d0.stage[k].nbits || d.stage[k].lds_off != d0.stage[k].lds_off || d.stage[k].nbits < 1 ||
-          d.stage[k].nbits > 31)
-        return PA_OK;
-  }
-  auto col_of = [&](int lds_off) {
-    for (int k = 0; k < nc; ++k)
-      if (d0.stage[k].lds_off == lds_off) return k;
-    return -1;
+  // the columns the kernel stages (its own 1024-doc tile image, whatever the planner staged for the count + emit
+  // passes): the filter leaves', the group-by columns, the value column — dictionary-encoded SV in every segment
+  std::vector<int> slots;
+  auto col_of = [&](int slot) {
+    for (size_t k = 0; k < slots.size(); ++k)
+      if (slots[k] == slot) return (int)k;
+    slots.push_back(slot);
+    return (int)slots.size() - 1;
   };
+  const DevSeg& d0 = q->hsegs[0];
   std::vector<int> lc, ln, le, gc, gs;
   for (int li = 0; li < q->num_eager; ++li) {
     const DevLeaf& L = d0.leaves[li];
     for (const DevSeg& d : q->hsegs)
-      if (d.leaves[li].negate != L.negate || d.leaves[li].kind != L.kind) return PA_OK;
+      if (d.leaves[li].negate != L.negate || d.leaves[li].kind != L.kind || d.leaves[li].slot != L.slot) return PA_OK;
     if (L.kind != PA_LEAF_DICT_RANGE) return PA_OK;
-    const int c = col_of(L.lds_off);
-    if (c < 0) return PA_OK;
-    lc.push_back(c);
+    lc.push_back(col_of(L.slot));
     ln.push_back(L.negate ? 1 : 0);
     le.push_back(L.clause_end ? 1 : 0);
   }
   for (int j = 0; j < s.num_group_by; ++j) {
-    const int c = col_of(d0.cols[P.gb_slot[j]].lds_off);
-    if (c < 0 || h.gb_stride[j] <= 0 || h.gb_stride[j] > 0xffffffffll) return PA_OK;
-    gc.push_back(c);
+    if (h.gb_stride[j] <= 0 || h.gb_stride[j] > 0xffffffffll) return PA_OK;
+    gc.push_back(col_of(P.gb_slot[j]));
     gs.push_back((int)(uint32_t)h.gb_stride[j]);
   }
   int vc = -1;
   if (h.v_fmt == V_FMT_ID) {
     if (h.emit_val_agg < 0) return PA_OK;
-    vc = col_of(d0.cols[P.agg_slot[h.emit_val_agg]].lds_off);
-    if (vc < 0) return PA_OK;
+    vc = col_of(P.agg_slot[h.emit_val_agg]);
+  }
+  const int nc = (int)slots.size();
+  if (nc < 1 || nc > 6) return PA_OK;
+  for (const DevSeg& d : q->hsegs) {
+    if (d.vremap) return PA_OK;
+    for (int j = 0; j < s.num_group_by; ++j)
+      if (d.remap[j]) return PA_OK;
+    for (int k = 0; k < nc; ++k) {
+      const DevCol& c = d.cols[slots[k]];
+      if (c.kind != COL_SV_DICT || !c.words || c.nbits < 1 || c.nbits > 31 || c.nbits != d0.cols[slots[k]].nbits)
+        return PA_OK;
+    }
   }
   if ((uint64_t)q->num_keys > 0xffffffffull) return PA_OK;
-  // LDS: per-partition state (cnt, done, chunks), the chunk counter, the bins, then each wave's two tile images
-  // bins of 32 records (128 bytes), chunks of 4 bins (512-byte runs for pass C: longer runs measured no faster there,
-  // and every (workgroup, partition) pads its last chunk; PA_PVE_SC: measurement override)
+  // tile image: a 16-byte guard, then per column its 1024 docs' bits (128 nb bytes) and a 16-byte guard
+  std::vector<int> nb, coff;
+  size_t img_bytes = 16;
+  for (int k = 0; k < nc; ++k) {
+    nb.push_back(d0.cols[slots[k]].nbits);
+    coff.push_back((int)img_bytes);
+    img_bytes += 128 * (size_t)nb.back() + 16;
+  }
+  const int img_dw = (int)(img_bytes / 4);
   const int Pv = h.pv, bs = 32, sc = std::getenv("PA_PVE_SC") ? std::atoi(std::getenv("PA_PVE_SC")) : 4;
   if (sc < 1 || sc > 64 || (sc & (sc - 1))) return PA_OK;
   auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
   const size_t l_bins = al16((size_t)(5 * Pv + 1) * 4);
   const size_t l_ring = al16(l_bins + (size_t)Pv * bs * 4);
-  const size_t img_b = (size_t)h.image_dwords_max * 4;
+  const size_t img_b = img_bytes;
   int w = 0;
   for (int cand : {16, 12, 8, 4})
     if (l_ring + (size_t)cand * 2 * img_b <= kLdsBudget) {
@@ -3181,11 +3188,6 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
     }
   if (!w) return PA_OK;
   const size_t lds = l_ring + (size_t)w * 2 * img_b;
-  std::vector<int> nb, coff;
-  for (int c = 0; c < nc; ++c) {
-    nb.push_back(d0.stage[c].nbits);
-    coff.push_back(4 * d0.stage[c].lds_off);
-  }
   auto pad1 = [](std::vector<int> v) {
     if (v.empty()) v.push_back(0);
     return v;
@@ -3195,7 +3197,7 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
   for (size_t j = 0; j < gs.size(); ++j) gss += (j ? "," : "") + std::to_string((uint32_t)gs[j]) + "u";
   gss += "}";
   std::vector<std::string> defs = {
-      "-DPVE_W=" + std::to_string(w), "-DPVE_IMG=" + std::to_string(h.image_dwords_max),
+      "-DPVE_W=" + std::to_string(w), "-DPVE_IMG=" + std::to_string(img_dw),
       "-DPVE_NC=" + std::to_string(nc), "-DPVE_NB=" + int_list(nb), "-DPVE_OFF=" + int_list(coff),
       "-DPVE_NL=" + std::to_string(q->num_eager), "-DPVE_LC=" + int_list(pad1(lc)), "-DPVE_LN=" + int_list(pad1(ln)),
       "-DPVE_LE=" + int_list(pad1(le)), "-DPVE_NG=" + std::to_string(s.num_group_by), "-DPVE_GC=" + int_list(gc),
@@ -3210,7 +3212,9 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
   (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   // one workgroup per CU; a workgroup's region holds its docs' records in whole chunks plus one partial chunk per
   // partition
-  const int64_t T = h.total_wtiles;
+  std::vector<int64_t> first(q->nseg + 1, 0);  // 1024-doc tiles of the kernel's own schedule
+  for (int si = 0; si < q->nseg; ++si) first[si + 1] = first[si] + (q->hsegs[si].num_docs + 1023) / 1024;
+  const int64_t T = first[q->nseg];
   const int G = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (T + w - 1) / w));
   const int64_t tiles_per_wg = (T + G - 1) / G;
   const int64_t cr = (int64_t)bs * sc;  // records per chunk
@@ -3245,10 +3249,10 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
     const DevSeg& d = q->hsegs[si];
     PveSegH& j = js[si];
     std::memset(&j, 0, sizeof(j));
-    for (int c = 0; c < nc; ++c) j.src[c] = (uint64_t)(uintptr_t)d.stage[c].words;
-    j.first_tile = d.first_wtile;
+    for (int c = 0; c < nc; ++c) j.src[c] = (uint64_t)(uintptr_t)d.cols[slots[c]].words;
+    j.first_tile = first[si];
     j.num_docs = d.num_docs;
-    j.num_tiles = d.num_wtiles;
+    j.num_tiles = (int32_t)(first[si + 1] - first[si]);
     for (int li = 0; li < q->num_eager; ++li) {
       j.lo_t[li] = (uint32_t)d.leaves[li].lo;
       j.hi_t[li] = (uint32_t)d.leaves[li].span;
