@@ -3165,17 +3165,33 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
     }
   }
   if ((uint64_t)q->num_keys > 0xffffffffull) return PA_OK;
-  // tile image: a 16-byte guard, then per column its 1024 docs' bits (128 nb bytes) and a 16-byte guard
+  // tile image of nd docs per lane (64 nd per tile): a 16-byte guard, then per column its tile's bits (8 nd nb bytes)
+  // and a 16-byte guard. 16 docs per lane unless 8 leave room for more resident waves (PA_PVE_ND: measurement)
+  const int Pv0 = h.pv;
+  const size_t l_ring0 = ((((size_t)(5 * Pv0 + 1) * 4 + 15) & ~(size_t)15) + (size_t)Pv0 * 32 * 4 + 15) & ~(size_t)15;
+  auto image_bytes = [&](int nd) {
+    size_t b = 16;
+    for (int k = 0; k < nc; ++k) b += (size_t)8 * nd * d0.cols[slots[k]].nbits + 16;
+    return b;
+  };
+  auto waves_for = [&](int nd) {
+    for (int cand : {16, 12, 8, 4})
+      if (l_ring0 + (size_t)cand * 2 * image_bytes(nd) <= kLdsBudget) return cand;
+    return 0;
+  };
+  int nd = waves_for(8) > waves_for(16) ? 8 : 16;
+  if (const char* e = std::getenv("PA_PVE_ND")) nd = std::atoi(e) == 8 ? 8 : 16;
   std::vector<int> nb, coff;
   size_t img_bytes = 16;
   for (int k = 0; k < nc; ++k) {
     nb.push_back(d0.cols[slots[k]].nbits);
     coff.push_back((int)img_bytes);
-    img_bytes += 128 * (size_t)nb.back() + 16;
+    img_bytes += (size_t)8 * nd * nb.back() + 16;
   }
   const int img_dw = (int)(img_bytes / 4);
+  const int td = 64 * nd;
   const int Pv = h.pv, bs = 32, sc = std::getenv("PA_PVE_SC") ? std::atoi(std::getenv("PA_PVE_SC")) : 4;
-  if (sc < 1 || sc > 64 || (sc & (sc - 1))) return PA_OK;
+  if (sc < 1 || sc > 16 || (sc & (sc - 1))) return PA_OK;  // (bins - 1 of a chunk: 4 bits of its list entry)
   auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
   const size_t l_bins = al16((size_t)(5 * Pv + 1) * 4);
   const size_t l_ring = al16(l_bins + (size_t)Pv * bs * 4);
@@ -3197,7 +3213,7 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
   for (size_t j = 0; j < gs.size(); ++j) gss += (j ? "," : "") + std::to_string((uint32_t)gs[j]) + "u";
   gss += "}";
   std::vector<std::string> defs = {
-      "-DPVE_W=" + std::to_string(w), "-DPVE_IMG=" + std::to_string(img_dw),
+      "-DPVE_W=" + std::to_string(w), "-DPVE_IMG=" + std::to_string(img_dw), "-DPVE_ND=" + std::to_string(nd),
       "-DPVE_NC=" + std::to_string(nc), "-DPVE_NB=" + int_list(nb), "-DPVE_OFF=" + int_list(coff),
       "-DPVE_NL=" + std::to_string(q->num_eager), "-DPVE_LC=" + int_list(pad1(lc)), "-DPVE_LN=" + int_list(pad1(ln)),
       "-DPVE_LE=" + int_list(pad1(le)), "-DPVE_NG=" + std::to_string(s.num_group_by), "-DPVE_GC=" + int_list(gc),
@@ -3213,13 +3229,13 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
   // one workgroup per CU; a workgroup's region holds its docs' records in whole chunks plus one partial chunk per
   // partition
   std::vector<int64_t> first(q->nseg + 1, 0);  // 1024-doc tiles of the kernel's own schedule
-  for (int si = 0; si < q->nseg; ++si) first[si + 1] = first[si] + (q->hsegs[si].num_docs + 1023) / 1024;
+  for (int si = 0; si < q->nseg; ++si) first[si + 1] = first[si] + (q->hsegs[si].num_docs + td - 1) / td;
   const int64_t T = first[q->nseg];
   const int G = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (T + w - 1) / w));
   const int64_t tiles_per_wg = (T + G - 1) / G;
   const int64_t cr = (int64_t)bs * sc;  // records per chunk
-  const int64_t C = (tiles_per_wg * 1024 + cr - 1) / cr + Pv;
-  if (C >= (int64_t(1) << 20) || (int64_t)G * C >= (int64_t(1) << 32)) return PA_OK;  // (table ranks, chunk ids)
+  const int64_t C = (tiles_per_wg * td + cr - 1) / cr + Pv;
+  if (C >= (int64_t(1) << 16) || (int64_t)G * C >= (int64_t(1) << 28)) return PA_OK;  // (table ranks, chunk ids)
   const size_t o_table = al16((size_t)G * C * cr * 4);
   const size_t o_hist = al16(o_table + (size_t)G * C * 4);
   const size_t o_used = al16(o_hist + (size_t)G * Pv * 4);
@@ -3269,7 +3285,7 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
   q->pve_lds = (int)lds;
   q->pve_bs = (int)cr;
   q->pve_chunks = C;
-  PLAN_LOG("pve: W %d grid %d lds %zu C %lld P %d", w, G, lds, (long long)C, Pv);
+  PLAN_LOG("pve: W %d nd %d grid %d lds %zu C %lld P %d", w, nd, G, lds, (long long)C, Pv);
   return PA_OK;
 }
 
@@ -3435,6 +3451,7 @@ int pa_query_scan(pa_query* q, void* stream) {
     ps.recs_v = (uint32_t*)b;
     ps.chunk_index = (const uint32_t*)(b + q->pve_o_index);
     ps.chunk_shift = __builtin_ctz((unsigned)q->pve_bs);
+    ps.chunk_bin_shift = 5;  // (32-record bins)
     PA_HIP(launch_part_agg(q->part_vk, (const DevQuery*)q->dq.p, ps, q->hq.pv, q->part_lds_c, st));
     return PA_OK;
   }

@@ -417,11 +417,12 @@ struct PartScratch {
   uint64_t* base;    // [P + 2] first record of every partition: V at [0, pv], H at [pv + 1, P + 1] (stream-relative)
   uint32_t* recs_v;  // V records, partition-major, rec_words_v words each
   uint32_t* recs_h;  // H records, partition-major, one word each
-  // count-free emit (pve_jit.hip): V record i of the partitions' concatenation is record i & (2^chunk_shift - 1) of chunk
-  // chunk_index[i >> chunk_shift] (chunk c = records [c << chunk_shift, (c + 1) << chunk_shift) of recs_v); nullptr:
-  // the records are contiguous
+  // count-free emit (pve_jit.hip): V record i of the partitions' concatenation is record i & (2^chunk_shift - 1) of the
+  // chunk whose entry is chunk_index[i >> chunk_shift]: chunk id (bits 0..27: records [id << chunk_shift, ..) of
+  // recs_v) | (bins written - 1) << 28 (bins of 2^chunk_bin_shift records; the rest of the chunk is not read).
+  // nullptr: the records are contiguous
   const uint32_t* chunk_index;
-  int64_t chunk_shift;
+  int32_t chunk_shift, chunk_bin_shift;
 };
 
 // Per-segment table of the lane-major scan kernel (scan_lm_kernel): 64 dwords, loaded at segment entry into ONE

@@ -1410,8 +1410,8 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   const int64_t vbase = q->v_base, vstep = q->v_step;
   constexpr int kB = 16;  // records per thread in flight
   const uint64_t span = (uint64_t)kB * kPartAggThreads;
-  // chunked records (count-free emit): the chunk ids of a batch are loaded one batch ahead, so a record load never
-  // waits for its index load
+  // chunked records (count-free emit): the chunk entries of a batch are loaded one batch ahead, so a record load never
+  // waits for its entry load (vector loads: a scalar load's wait would also wait for the LDS atomics in flight)
   const AS1 uint32_t* cix = ps.chunk_index ? gp(ps.chunk_index) : nullptr;
   const int csh = (int)ps.chunk_shift;
   const uint64_t cmask = cix ? (1ull << csh) - 1ull : 0ull;
@@ -1431,9 +1431,11 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
       w0[j] = kSentinel;
       w1[j] = w2[j] = 0u;
       if (ri < r1) {
-        const uint64_t pi = cix ? ((uint64_t)cid[j] << csh) | (ri & cmask) : ri;
+        const uint64_t pi = cix ? ((uint64_t)(cid[j] & 0x0fffffffu) << csh) | (ri & cmask) : ri;
+        // (a partition's last chunk per workgroup holds (cid >> 28) + 1 bins)
+        const bool in = !cix || (uint32_t)(ri & cmask) < (((cid[j] >> 28) + 1u) << ps.chunk_bin_shift);
         const AS1 uint32_t* rec = recs + pi * (uint64_t)W;
-        w0[j] = __builtin_nontemporal_load(rec);
+        if (in) w0[j] = __builtin_nontemporal_load(rec);
         if (fmt == V_FMT_32 || fmt == V_FMT_64) w1[j] = __builtin_nontemporal_load(rec + 1);
         if (fmt == V_FMT_64) w2[j] = __builtin_nontemporal_load(rec + 2);
       }

@@ -1,5 +1,6 @@
 // Count-free partitioned emit (pve_jit.hip): the per-partition chunk lists pass C reads. Each emit workgroup g wrote
-// its chunks (cr records each) into its own region with a table entry (partition | rank << 12) per chunk and its chunk
+// its chunks (cr records each) into its own region with a table entry (partition | (bins - 1) << 12 | rank << 16) per
+// chunk and its chunk
 // count per partition (hist[g][p]). pve_offsets_kernel: per partition the exclusive scan over the workgroups (off) and
 // its total; pve_base_kernel: every partition's first list entry (base, in records = chunks x cr, the unit of pass C's
 // ranges); pve_scatter_kernel: every chunk's id into its partition's list at base + off + rank.
@@ -65,8 +66,8 @@ __global__ void __launch_bounds__(256) pve_scatter_kernel(const uint32_t* __rest
   const uint32_t n = used[g];
   for (uint32_t c = threadIdx.x; c < n; c += blockDim.x) {
     const uint32_t e = table[g * C + c];
-    const uint32_t p = e & 0xfffu, r = e >> 12;
-    index[base[p] / (uint64_t)bs + off[g * P + p] + r] = (uint32_t)(g * C + c);
+    const uint32_t p = e & 0xfffu, r = e >> 16;
+    index[base[p] / (uint64_t)bs + off[g * P + p] + r] = (uint32_t)(g * C + c) | (((e >> 12) & 15u) << 28);
   }
 }
 

@@ -28,7 +28,12 @@ typedef unsigned long long u64;
 typedef long long i64;
 typedef __attribute__((address_space(3))) u32 l32;
 
-constexpr int W = PVE_W, NC = PVE_NC, NL = PVE_NL, NG = PVE_NG, ND = 16, IMG = PVE_IMG;
+#ifndef PVE_ND
+#define PVE_ND 16
+#endif
+constexpr int W = PVE_W, NC = PVE_NC, NL = PVE_NL, NG = PVE_NG, ND = PVE_ND, IMG = PVE_IMG;
+constexpr int TD = 64 * ND;  // docs per tile (lane l: docs [ND l, ND l + ND))
+static_assert(ND == 8 || ND == 16, "8 or 16 docs per lane");
 constexpr int NLA = NL > 0 ? NL : 1;
 constexpr int kNB[NC] = PVE_NB;
 constexpr int kOFF[NC] = PVE_OFF;
@@ -51,7 +56,7 @@ static_assert(NC <= kJitMax && NL <= kJitMax && NG <= 4, "shape beyond the JIT d
 static_assert(BS % 4 == 0, "bins are whole 16-byte units");
 struct PveSeg {          // one bound segment (scalar loads at segment switches only)
   u64 src[kJitMax];      // column streams, past the guard words
-  i64 first_tile;        // first 1024-doc tile in the query's tile space
+  i64 first_tile;        // first TD-doc tile in the query's tile space
   int num_docs, num_tiles;
   u32 lo_t[kJitMax], hi_t[kJitMax];  // DICT_RANGE leaves: MSB-aligned bounds in this segment's dictId space
 };
@@ -60,7 +65,7 @@ struct PveArgs {
   int nseg, xcd_major;
   i64 chunks_per_wg;             // C: chunk slots of a workgroup's region
   u32* recs;                     // record stream: workgroup g's chunks at [g C SC BS, (g + 1) C SC BS)
-  u32* table;                    // [G][C]: partition | rank << 12 of every chunk
+  u32* table;                    // [G][C]: partition | (bins - 1) << 12 | rank << 16 of every chunk
   u32* hist;                     // [G][P]: chunks per (workgroup, partition)
   u32* used;                     // [G]: chunks a workgroup filled
   unsigned long long* matched;   // [0] numDocsScanned, [3] region overflow (must stay 0)
@@ -92,8 +97,8 @@ __device__ __forceinline__ void dma16m(u32 voff, u64 sbase, u32 dst, u64 mask) {
 template <int C>
 __device__ __forceinline__ void dma_cols(CS* sg, i64 wt, u32 img, u32 voff) {
   if constexpr (C < NC) {
-    constexpr int CH = 8 * kNB[C];  // 16-byte chunks of a 1024-doc tile
-    const u64 src = sg->src[C] + (u64)wt * (u64)(128 * kNB[C]);
+    constexpr int CH = ND * kNB[C] / 2;  // 16-byte chunks of a tile (TD nb / 128)
+    const u64 src = sg->src[C] + (u64)wt * (u64)(8 * ND * kNB[C]);
     const u32 dst = img + (u32)kOFF[C];
 #pragma unroll
     for (int k = 0; k < CH / 64; ++k) dma16(voff, src + 1024u * k, dst + 1024u * k);
@@ -102,7 +107,8 @@ __device__ __forceinline__ void dma_cols(CS* sg, i64 wt, u32 img, u32 voff) {
   }
 }
 
-// the lane's 16 words of column C, MSB-aligned (top) or as dictIds
+// the lane's ND values of column C, MSB-aligned (top) or as dictIds. The lane's bits start sh bits into a word: its
+// words are read from one word earlier when sh == 0 so that alignbit by (32 - sh) & 31 realigns every case
 template <int C, bool TOP>
 __device__ __forceinline__ void unpack(u32 img, int lane, u32 (&v)[ND]) {
   constexpr int NB = kNB[C];
@@ -110,14 +116,14 @@ __device__ __forceinline__ void unpack(u32 img, int lane, u32 (&v)[ND]) {
   const u32 region = img + (u32)kOFF[C];
   const u32 bit0 = (u32)lane * (u32)(ND * NB);
   u32 w[K];
-  if constexpr ((ND * NB) % 32 != 0) {  // odd NB: odd lanes start 16 bits into a word
-    const u32 sh = bit0 & 16u;
-    const l32* p = at<const l32>(region + 4u * ((bit0 >> 5) - 1u + (sh >> 4)));
+  if constexpr ((ND * NB) % 32 != 0) {
+    const u32 sh = bit0 & 31u;
+    const l32* p = at<const l32>(region + 4u * ((bit0 >> 5) - (sh == 0u ? 1u : 0u)));
     u32 r[K + 1];
 #pragma unroll
     for (int j = 0; j <= K; ++j) r[j] = p[j];
 #pragma unroll
-    for (int j = 0; j < K; ++j) w[j] = __builtin_amdgcn_alignbit(r[j], r[j + 1], sh);
+    for (int j = 0; j < K; ++j) w[j] = __builtin_amdgcn_alignbit(r[j], r[j + 1], (32u - sh) & 31u);
   } else {
     const l32* p = at<const l32>(region + 4u * (bit0 >> 5));
 #pragma unroll
@@ -152,8 +158,9 @@ __device__ __forceinline__ bool leaves(CS* sg, u32 img, int lane, u32& m, u32& c
   if constexpr (L < NL) {
     u32 t[ND];
     unpack<kLC[L], true>(img, lane, t);
-    u32 bits = ~range_nm(t, sg->lo_t[L], sg->hi_t[L]) & 0xffffu;
-    if constexpr (kLN[L]) bits = ~bits & 0xffffu;
+    constexpr u32 kAll = (1u << ND) - 1u;
+    u32 bits = ~range_nm(t, sg->lo_t[L], sg->hi_t[L]) & kAll;
+    if constexpr (kLN[L]) bits = ~bits & kAll;
     clause |= bits;
     if constexpr (kLE[L] != 0) {
       m &= clause;
@@ -195,7 +202,8 @@ __device__ __forceinline__ i64 bin_slot(const Bins& B, u32 p) {
     const u32 r = at<l32>(B.chunks)[p];
     at<l32>(B.chunks)[p] = r + 1u;
     at<l32>(B.cur)[p] = c;
-    if ((i64)c < B.C) ((__attribute__((address_space(1))) u32*)B.table)[B.region + (i64)c] = p | (r << 12);
+    if ((i64)c < B.C)  // (written full; a partition's last chunk is rewritten with its bins at the end)
+      ((__attribute__((address_space(1))) u32*)B.table)[B.region + (i64)c] = p | ((u32)(SC - 1) << 12) | (r << 16);
   } else {
     c = at<l32>(B.cur)[p];
   }
@@ -316,11 +324,12 @@ __device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], 
 
 // one 1024-doc tile: returns the lane's docs counted in numDocsScanned
 __device__ __forceinline__ u32 tile(const Bins& B, CS* sg, i64 wt, u32 img, int lane) {
-  const i64 rem = (i64)sg->num_docs - wt * 1024;
-  u32 m = 0xffffu;
-  if (rem < 1024) {
+  constexpr u32 kAll = (1u << ND) - 1u;
+  const i64 rem = (i64)sg->num_docs - wt * TD;
+  u32 m = kAll;
+  if (rem < TD) {
     const i64 n = rem - ND * lane;
-    m = n >= ND ? 0xffffu : (n <= 0 ? 0u : ((1u << n) - 1u));
+    m = n >= ND ? kAll : (n <= 0 ? 0u : ((1u << n) - 1u));
   }
   u32 clause = 0;
   if (!leaves<0>(sg, img, lane, m, clause)) return 0;
@@ -431,16 +440,14 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
     flush_one(B, (u32)p);
   }
   __syncthreads();
-  // the unfilled bins of each partition's last chunk: sentinel records (pass C skips them)
+  // each partition's last chunk: its table entry with the bins written (pass C reads no further)
   for (int p = tid; p < P; p += W * 64) {
     const u32 f = at<l32>(B.fill)[p];
     if (f == 0) continue;
     const u32 c = at<l32>(B.cur)[p];
     if ((i64)c >= B.C) continue;
-    __attribute__((address_space(1))) u32x4* dst =
-        (__attribute__((address_space(1))) u32x4*)(B.recs + ((B.region + (i64)c) * SC + f) * BS);
-    const u32x4 sv = {kSentinel, kSentinel, kSentinel, kSentinel};
-    for (u32 k = 0; k < ((u32)SC - f) * (u32)BS / 4u; ++k) __builtin_nontemporal_store(sv, dst + k);
+    ((__attribute__((address_space(1))) u32*)B.table)[B.region + (i64)c] =
+        (u32)p | ((f - 1u) << 12) | ((at<l32>(B.chunks)[p] - 1u) << 16);
   }
   for (int p = tid; p < P; p += W * 64) A->hist[lb * P + p] = at<l32>(B.chunks)[p];
   if (tid == 0) {
