@@ -3089,6 +3089,7 @@ struct PveSegH {  // == pve_jit.hip PveSeg
   int64_t first_tile;
   int32_t num_docs, num_tiles;
   uint32_t lo_t[6], hi_t[6];
+  uint64_t admit;
 };
 struct PveArgsH {  // == pve_jit.hip PveArgs
   int64_t total_tiles;
@@ -3114,7 +3115,8 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
   q->pve_fn = nullptr;
   const pa_query_spec& s = q->spec;
   const DevQuery& h = q->hq;
-  if (!q->partitioned || q->split_emit || h.hll_agg >= 0 || q->limit_mode || q->limit_walk || q->hashed) return PA_OK;
+  if (!q->partitioned || q->split_emit || h.hll_agg >= 0 || q->limit_mode || q->hashed) return PA_OK;
+  if (q->limit_walk && h.gb_mv >= 0) return PA_OK;
   if ((s.flags & PA_QF_NO_JIT) || (s.flags2 & PA_QF2_NO_COUNT_FREE) || std::getenv("PA_NO_JIT") ||
       (std::getenv("PA_DEBUG_EMIT") && !std::getenv("PA_PVE_DBG")))
     return PA_OK;
@@ -3219,7 +3221,7 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
       "-DPVE_LE=" + int_list(pad1(le)), "-DPVE_NG=" + std::to_string(s.num_group_by), "-DPVE_GC=" + int_list(gc),
       "-DPVE_GS=" + gss, "-DPVE_VC=" + std::to_string(vc), "-DPVE_KS=" + std::to_string(h.kshift_v),
       "-DPVE_P=" + std::to_string(Pv), "-DPVE_BS=" + std::to_string(bs), "-DPVE_SC=" + std::to_string(sc),
-      "-DPVE_L_BINS=" + std::to_string(l_bins),
+      "-DPVE_L_BINS=" + std::to_string(l_bins), "-DPVE_ADMIT=" + std::to_string(q->limit_walk ? 1 : 0),
       "-DPVE_L_RING=" + std::to_string(l_ring)};
   if (const char* dbg = std::getenv("PA_PVE_DBG")) defs.push_back(std::string("-DPVE_DBG=") + dbg);  // (measurement)
   if (const char* pb = std::getenv("PA_PVE_PB")) defs.push_back(std::string("-DPVE_PB=") + pb);      // (measurement)
@@ -3273,6 +3275,7 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
       j.lo_t[li] = (uint32_t)d.leaves[li].lo;
       j.hi_t[li] = (uint32_t)d.leaves[li].span;
     }
+    j.admit = (uint64_t)(uintptr_t)d.admit;
   }
   rc = dev_alloc(q->pve_args, sizeof(PveArgsH));
   if (!rc) rc = dev_alloc(q->pve_segs, sizeof(PveSegH) * js.size());

@@ -47,6 +47,9 @@ constexpr u32 kSentinel = 0xffffffffu;
 #ifndef PVE_PB
 #define PVE_PB 4  // records per lane per put round
 #endif
+#ifndef PVE_ADMIT
+#define PVE_ADMIT 0  // numGroupsLimit walk form: a record is put only when the segment's bitmap admits its key
+#endif
 #ifndef PVE_DBG
 #define PVE_DBG 0  // measurement only (PA_PVE_DBG): 1 = records built but not put, 2 = full bins not stored
 #endif
@@ -59,6 +62,7 @@ struct PveSeg {          // one bound segment (scalar loads at segment switches 
   i64 first_tile;        // first TD-doc tile in the query's tile space
   int num_docs, num_tiles;
   u32 lo_t[kJitMax], hi_t[kJitMax];  // DICT_RANGE leaves: MSB-aligned bounds in this segment's dictId space
+  u64 admit;             // PVE_ADMIT: the segment's admitted-key bitmap (limit_walk_kernel; 0 = every key)
 };
 struct PveArgs {
   i64 total_tiles;
@@ -322,8 +326,10 @@ __device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], 
   }
 }
 
-// one 1024-doc tile: returns the lane's docs counted in numDocsScanned
-__device__ __forceinline__ u32 tile(const Bins& B, CS* sg, i64 wt, u32 img, int lane) {
+// one tile: returns the lane's docs counted in numDocsScanned. issue() sends the next tile's DMA: here, after the
+// admission loads have been waited for (PVE_ADMIT: a wait for them would otherwise also wait for that DMA)
+template <class Issue>
+__device__ __forceinline__ u32 tile(const Bins& B, CS* sg, i64 wt, u32 img, int lane, Issue&& issue) {
   constexpr u32 kAll = (1u << ND) - 1u;
   const i64 rem = (i64)sg->num_docs - wt * TD;
   u32 m = kAll;
@@ -332,22 +338,37 @@ __device__ __forceinline__ u32 tile(const Bins& B, CS* sg, i64 wt, u32 img, int 
     m = n >= ND ? kAll : (n <= 0 ? 0u : ((1u << n) - 1u));
   }
   u32 clause = 0;
-  if (!leaves<0>(sg, img, lane, m, clause)) return 0;
-  if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return 0;
+  if (!leaves<0>(sg, img, lane, m, clause) || __builtin_amdgcn_ballot_w64(m != 0) == 0) {
+    if constexpr (PVE_ADMIT) issue();
+    return 0;
+  }
   u32 key[ND], val[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) key[i] = val[i] = 0u;
   keys<0>(img, lane, key);
   if constexpr (VC >= 0) unpack<(VC >= 0 ? VC : 0), false>(img, lane, val);
+  const u32 scanned = (u32)__builtin_popcount(m);  // (numDocsScanned: every doc the filter kept, admitted or not)
+  if constexpr (PVE_ADMIT) {
+    const __attribute__((address_space(1))) u32* adm = (const __attribute__((address_space(1))) u32*)sg->admit;
+    if (adm) {
+      u32 w[ND];
+#pragma unroll
+      for (int i = 0; i < ND; ++i) w[i] = ((m >> i) & 1u) ? adm[key[i] >> 5] : 0u;
+#pragma unroll
+      for (int i = 0; i < ND; ++i)
+        if (!((w[i] >> (key[i] & 31u)) & 1u)) m &= ~(1u << i);
+    }
+    issue();
+  }
   if constexpr (PVE_DBG == 1) {
     u32 x = 0;
 #pragma unroll
     for (int i = 0; i < ND; ++i) x ^= key[i] + val[i];
     if (x == 0x9e3779b9u) *at<l32>(B.next) = x;  // (keeps the records live)
-    return (u32)__builtin_popcount(m);
+    return scanned;
   }
   put(B, m, key, val, lane);
-  return (u32)__builtin_popcount(m);
+  return scanned;
 }
 
 __device__ __forceinline__ int find_segment(CS* segs, int nseg, i64 t) {
@@ -408,21 +429,24 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
     int slot = 0;
     for (i64 t = t0 + wave; t < t1; t += W) {
       vm_wait<0>();  // tile t has landed (and the previous tile's chunk stores have left)
-      if (ti < t1) {
-        while (ti >= iend) {
-          ++isi;
-          ifirst = S[isi].first_tile;
-          iend = ifirst + S[isi].num_tiles;
+      auto issue = [&]() {
+        if (ti < t1) {
+          while (ti >= iend) {
+            ++isi;
+            ifirst = S[isi].first_tile;
+            iend = ifirst + S[isi].num_tiles;
+          }
+          dma_cols<0>(S + isi, ti - ifirst, ring + (u32)(slot ^ 1) * (u32)IMG * 4u, voff);
         }
-        dma_cols<0>(S + isi, ti - ifirst, ring + (u32)(slot ^ 1) * (u32)IMG * 4u, voff);
-      }
-      ti += W;
+        ti += W;
+      };
+      if constexpr (!PVE_ADMIT) issue();
       while (t >= pend) {
         ++psi;
         pfirst = S[psi].first_tile;
         pend = pfirst + S[psi].num_tiles;
       }
-      matched += tile(B, S + psi, t - pfirst, ring + (u32)slot * (u32)IMG * 4u, lane);
+      matched += tile(B, S + psi, t - pfirst, ring + (u32)slot * (u32)IMG * 4u, lane, issue);
       slot ^= 1;
     }
   }

@@ -194,7 +194,8 @@ def highcard():
 def test_configs2_high_cardinality_group_by(highcard, variant, count_free):
     """configs[2] (GROUP BY d1, d2 over ~1M keys, SUM / MIN / MAX) on the partitioned path against the oracle: with the
     count-free emit (pve_jit.hip: whole record chunks per workgroup, partitions read through chunk lists) where it
-    applies (untrimmed, filtered), and with the count + emit passes (PA_QF2_NO_COUNT_FREE)."""
+    applies (untrimmed, filtered, and the default numGroupsLimit: the walk form's admitted-key bitmaps checked per record),
+    and with the count + emit passes (PA_QF2_NO_COUNT_FREE)."""
     segs, gs = highcard
     sql = {"untrimmed": "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000 "
                         "OPTION(numGroupsLimit=2000000)",
@@ -207,8 +208,7 @@ def test_configs2_high_cardinality_group_by(highcard, variant, count_free):
         p = _plan(ex)
         assert p["strategy"] == "partitioned", p
         assert p["limit_trimming"] == (2 if variant == "default_limit" else 0), p
-        # (numGroupsLimit's admission runs in the count pass: no count-free emit under the default limit)
-        assert p["count_free_emit"] == (1 if count_free and variant != "default_limit" else 0), p
+        assert p["count_free_emit"] == (1 if count_free else 0), p
         ex.execute()
         n = _compare_arrays(ex, q, segs)
     finally:
