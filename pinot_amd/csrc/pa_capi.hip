@@ -2812,6 +2812,17 @@ static int alloc_leaps(pa_query* q, const Prep& P) {
     q->leap_leaf = -1;
     return PA_OK;
   }
+  // a wave keeps its first entries in LDS past its tile ring when the workgroups per CU still fit
+  q->hq.leap_lds_cap = 0;
+  {
+    const int wpw = scan_waves(q->strategy);
+    const int want = (int)std::min<int64_t>(cap, 128);
+    const size_t extra = (size_t)wpw * want * 8;
+    if (q->plan_wg > 0 && ((size_t)q->lds_bytes + extra) * (size_t)q->plan_wg <= kLdsBudget) {
+      q->hq.leap_lds_cap = want;
+      q->lds_bytes += (int)extra;
+    }
+  }
   const size_t words = (size_t)std::max(1, q->nseg) * 3 + 1 + (size_t)slices + (size_t)slices * (size_t)cap;
   int rc = dev_alloc(q->leap_buf, words * sizeof(unsigned long long));
   if (rc) return rc;

@@ -315,7 +315,7 @@ struct DevQuery {
   // fused execution statistics (default unless PA_QF_NO_FILTER_STATS, leap_tile + leap_search_kernel): 1 = literal 0 (eager, E) and
   // literal 1 (lazy, Z) are the two scan leaves of an AND
   int32_t leap_mode;
-  int32_t pad_leap;
+  int32_t leap_lds_cap;           // list entries a wave keeps in LDS (after its tile ring) before writing to leap_out
   unsigned long long* leap_out;  // (layout: pa_scan.h "fused execution statistics")
   int64_t leap_cap;              // list entries per scan wave (E docs)
   int64_t leap_slices;           // scan waves (grid x waves per workgroup): one list slice each

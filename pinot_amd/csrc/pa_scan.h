@@ -881,8 +881,9 @@ __device__ __forceinline__ void leap_add(const DevQuery* __restrict__ q, int seg
 // The E docs of one tile (e: eager clause bits, f: those that also matched the lazy clause) into the list, and the
 // tile's matched docs into the segment's counter. LM: doc of bit i of lane l = 32 l + i, else 64 i + l.
 template <int LM>
-__device__ __noinline__ void leap_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int64_t doc_base,
-                                       uint32_t e, uint32_t f, int lane, uint32_t slice, uint32_t& listed) {
+__device__ __forceinline__ void leap_tile(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int64_t doc_base,
+                                       uint32_t e, uint32_t f, int lane, uint32_t slice, uint32_t& listed,
+                                       uint32_t lds_base) {
   const uint32_t mine = (uint32_t)__builtin_popcount(e);
   uint32_t incl = mine;
 #pragma unroll
@@ -902,12 +903,17 @@ __device__ __noinline__ void leap_tile(const DevQuery* __restrict__ q, const Dev
   } else {
     AS1 unsigned long long* list =
         gp(q->leap_out) + 3 * nseg + 1 + (int64_t)q->leap_slices + (int64_t)slice * (int64_t)cap;
+    const uint32_t lcap = (uint32_t)q->leap_lds_cap;
+    lds_u64_t* lds_list = (lds_u64_t*)(uintptr_t)lds_base;
     uint32_t pos = listed + (incl - mine);
     while (e) {
       const int i = __builtin_ctz(e);
       e &= e - 1u;
       const int64_t doc = doc_base + (LM ? 32 * lane + i : kWave * i + lane);
-      list[pos++] = ((uint64_t)si << 40) | ((uint64_t)doc << 1) | ((f >> i) & 1u);
+      const uint64_t ent = ((uint64_t)si << 40) | ((uint64_t)doc << 1) | ((f >> i) & 1u);
+      if (pos < lcap) lds_list[pos] = ent;
+      else list[pos] = ent;
+      ++pos;
     }
   }
   listed += total;
@@ -1999,8 +2005,10 @@ struct LaneAcc {
   uint32_t id;     // LDS byte address of aggregation 0's dictId slot of this thread
   uint32_t astr;   // bytes between aggregations' pair slots (16 * WGS); dictId slots: astr / 4
   uint32_t idm;    // bit a: aggregation a's dictId was updated in the current segment run
-  // fused execution statistics: this wave's slice of the E-doc list and the entries written so far
-  uint32_t leap_slice, leap_n;
+  // fused execution statistics: this wave's slice of the E-doc list, the entries listed so far, and the LDS byte
+  // address of the wave's first leap_lds_cap entries (a global store in the tile loop would make the next tile's
+  // counted DMA wait longer: vmcnt counts stores too)
+  uint32_t leap_slice, leap_n, leap_lds;
 };
 typedef __attribute__((address_space(3))) int64_t lds_i64_t;
 __device__ __forceinline__ void la_get(const LaneAcc& la, int a, int64_t& r0, int64_t& r1) {
@@ -2494,7 +2502,7 @@ __device__ __forceinline__ uint32_t tile_survivors(const DevQuery* __restrict__ 
       if (!ok) m &= ~bit;
     }
     if constexpr (!is_pcount(STRAT) && !is_pemit(STRAT))
-      if (q->leap_mode) leap_tile<LM>(q, seg, doc_base, eager, m, lane, la.leap_slice, la.leap_n);
+      if (q->leap_mode) leap_tile<LM>(q, seg, doc_base, eager, m, lane, la.leap_slice, la.leap_n, la.leap_lds);
     if (__ballot(m != 0) == 0) return 0;
   }
   const uint32_t scanned = m;  // numDocsScanned counts every doc the filter kept, admitted or not
@@ -2856,6 +2864,8 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
   LaneAcc la;
   la.leap_slice = (uint32_t)((q->xcd_major ? xcd_major_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x) * WPW + wave);
   la.leap_n = 0u;
+  la.leap_lds = lds_addr(smem + acc_dwords + (uint32_t)WPW * (uint32_t)q->ring * (uint32_t)img_dw) +
+                (uint32_t)wave * (uint32_t)q->leap_lds_cap * 8u;
   if constexpr (is_lane(STRAT) && STRAT != STRAT_LANE_CNT) lane_acc_init(q, la, smem, WGS);
   if constexpr (STRAT == STRAT_LANE_DICT) {  // the dictId histograms of SUMs over a shared dictionary
     for (int a = 0; a < q->num_aggs; ++a) {
@@ -2990,8 +3000,15 @@ __global__ void __launch_bounds__(scan_waves(STRAT) * kWave, emit_v_wide(STRAT) 
   }
 
   if constexpr (!is_pcount(STRAT) && !is_pemit(STRAT))
-    if (q->leap_mode && lane == 0)  // (every wave: the search kernel reads every slice's count)
-      gp(q->leap_out)[3 * (int64_t)q->num_segments + 1 + la.leap_slice] = la.leap_n;
+    if (q->leap_mode) {
+      // the entries kept in LDS to the wave's slice, then its count (every wave: the search kernel reads every count)
+      const uint32_t nl = min(la.leap_n, (uint32_t)q->leap_lds_cap);
+      AS1 unsigned long long* list = gp(q->leap_out) + 3 * (int64_t)q->num_segments + 1 + (int64_t)q->leap_slices +
+                                     (int64_t)la.leap_slice * (int64_t)q->leap_cap;
+      const lds_u64_t* ll = (const lds_u64_t*)(uintptr_t)la.leap_lds;
+      for (uint32_t k = (uint32_t)lane; k < nl; k += kWave) list[k] = ll[k];
+      if (lane == 0) gp(q->leap_out)[3 * (int64_t)q->num_segments + 1 + la.leap_slice] = la.leap_n;
+    }
   if (!is_pemit(STRAT)) {  // (the partitioned count pass counts numDocsScanned; its emit pass sees the same docs)
     const int64_t wm = wave_sum_i64((int64_t)matched);
     if (lane == 0 && wm != 0) __hip_atomic_fetch_add(gp(q->matched_docs), (unsigned long long)wm, RLX);
