@@ -473,16 +473,19 @@ class GpuQueryExecutor:
             return
         L.check(L.lib().pa_query_execute(self.handle, stream), "pa_query_execute")
         self._scanned = True
+        self.merged_stats = None
 
     def reset(self, stream=None):
         L.check(L.lib().pa_query_reset(self.handle, stream), "pa_query_reset")
         self._scanned = False
+        self.merged_stats = None
 
     def scan(self, stream=None):
         if not self.segs or self.match_none:
             return
         L.check(L.lib().pa_query_scan(self.handle, stream), "pa_query_scan")
         self._scanned = True
+        self.merged_stats = None
 
     def sections(self):
         """[(kind, device_ptr, num_elements)] accumulator sections (for the cross-GPU reduce)."""
@@ -664,7 +667,14 @@ class GpuQueryExecutor:
         res = IntermediateResult(list(q.aggregations), list(q.group_by))
         res.num_total_docs = sum(s.num_docs for s in self.all_segs)
         res.num_docs_scanned = int(lib.pa_query_matched_docs(self.handle))
-        if execution_stats:
+        merged = getattr(self, "merged_stats", None)
+        if merged is not None:
+            # numDocsScanned was summed across GPUs (parallel.DistributedAccumulators.reduce): this rank's segments
+            # cannot recount the statistics against it; the reduce summed every rank's own pair before its collective
+            # (reduce(execution_stats=True)), or left (0, 0)
+            if execution_stats:
+                res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter = merged
+        elif execution_stats:
             res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter = self.execution_stats(
                 stream, res.num_docs_scanned)
         key_cols = [kc.tolist() for kc in self.key_values(keys)]

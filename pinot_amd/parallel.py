@@ -503,6 +503,7 @@ class DistributedAccumulators:
         # the library now reads and writes this torch-owned block: the executor keeps it alive for as long as it lives
         # (pa_query_set_accumulator_buffer: the caller owns the block and must outlive the query)
         executor._acc_owner = self.buf
+        self.executor = executor
         runs = section_runs([(kind, ptr - self.base + pad, n) for kind, ptr, n in executor.sections()])
         self.views = [(kind, self.buf[a:b].view(dt)) for kind, dt, a, b in runs]
         self.num_keys = int(executor.num_keys)
@@ -515,20 +516,34 @@ class DistributedAccumulators:
             off = ptr - self.base + pad
             self.per_key.append((kind, self.buf[off:off + n * es].view(dt)))
 
-    def reduce(self, dst=0, all_reduce=False):
+    def reduce(self, dst=0, all_reduce=False, execution_stats=False, group=None):
+        """Element-wise merge onto rank `dst` (every rank with all_reduce). numDocsScanned is summed too, so the merged
+        results block's execution statistics are every rank's own pair summed before the collective
+        (execution_stats=True: one extra 16-byte all-reduce and a host sync per query); without it the merged
+        block carries (0, 0) — the timed bench steps, which fetch without statistics anyway."""
+        ex = self.executor
+        if execution_stats:
+            local = torch.tensor(list(ex.execution_stats()), dtype=torch.int64, device=self.buf.device)
+            if dist.is_initialized():
+                dist.all_reduce(local, group=group)
+            stats = tuple(int(v) for v in local.tolist())
+        else:
+            stats = (0, 0)
         reduce_sections(self.views, dst=dst, all_reduce=all_reduce)
+        if all_reduce or not dist.is_initialized() or dist.get_rank() == dst:
+            ex.merged_stats = stats
 
     def reduce_scatter(self, group=None):
         """Large direct key spaces: every rank ends up holding the merged rows of its own key range
         (reduce_scatter_sections), so each rank's fetch returns its share of the groups. Returns the range (lo, hi)."""
         return reduce_scatter_sections(self.per_key, self.num_keys, group)
 
-    def merge(self, dst=0, group=None, scatter_keys=1 << 20):
+    def merge(self, dst=0, group=None, scatter_keys=1 << 20, execution_stats=False):
         """The cross-GPU merge this key space wants: key spaces of at least `scatter_keys` keys reduce-scatter (every
         rank then fetches its share: returns True), smaller ones reduce onto rank `dst`, the one rank that fetches
         (returns False)."""
         if self.num_keys >= scatter_keys:
             self.reduce_scatter(group)
             return True
-        self.reduce(dst=dst)
+        self.reduce(dst=dst, execution_stats=execution_stats, group=group)
         return False

@@ -248,3 +248,33 @@ def test_reduce_scatter_merge_path(rccl_world1):
         ex.close()
         for g in gsegs:
             g.close()
+
+
+def test_reduce_execution_stats(rccl_world1):
+    """numDocsScanned is summed by the element-wise reduce, so the merged block's execution statistics are the ranks'
+    own pairs summed before the collective (reduce(execution_stats=True)); a plain reduce leaves (0, 0) rather than
+    recounting this rank's segments against the merged counter, and the next execute() returns to local counting."""
+    q = parse_sql("SELECT d1, COUNT(*), SUM(m) FROM t WHERE m > 0 AND d2 < 5 GROUP BY d1 LIMIT 10000")
+    segs = [make_segment(840 + i, n, COLS) for i, n in enumerate((12007, 4001))]
+    gsegs = [GpuSegment(s) for s in segs]
+    ex = GpuQueryExecutor(q, gsegs)
+    try:
+        acc = DistributedAccumulators(ex, torch.device("cuda", 0))
+        ex.execute()
+        before = ex.fetch()
+        local = (before.num_entries_scanned_in_filter, before.num_entries_scanned_post_filter)
+        assert local[0] > 0 and local[1] > 0
+        acc.reduce(dst=0, execution_stats=True)  # world size 1: the sum is this rank's own pair
+        got = ex.fetch()
+        assert (got.num_entries_scanned_in_filter, got.num_entries_scanned_post_filter) == local
+        ex.execute()
+        acc.reduce(dst=0)
+        got = ex.fetch()
+        assert (got.num_entries_scanned_in_filter, got.num_entries_scanned_post_filter) == (0, 0)
+        ex.execute()
+        again = ex.fetch()
+        assert (again.num_entries_scanned_in_filter, again.num_entries_scanned_post_filter) == local
+    finally:
+        ex.close()
+        for g in gsegs:
+            g.close()
