@@ -254,7 +254,7 @@ def test_reduce_execution_stats(rccl_world1):
     """numDocsScanned is summed by the element-wise reduce, so the merged block's execution statistics are the ranks'
     own pairs summed before the collective (reduce(execution_stats=True)); a plain reduce leaves (0, 0) rather than
     recounting this rank's segments against the merged counter, and the next execute() returns to local counting."""
-    q = parse_sql("SELECT d1, COUNT(*), SUM(m) FROM t WHERE m > 0 AND d2 < 5 GROUP BY d1 LIMIT 10000")
+    q = parse_sql("SELECT d1, COUNT(*), SUM(m) FROM t WHERE m > 1000 AND d1 < 30 GROUP BY d1 LIMIT 10000")
     segs = [make_segment(840 + i, n, COLS) for i, n in enumerate((12007, 4001))]
     gsegs = [GpuSegment(s) for s in segs]
     ex = GpuQueryExecutor(q, gsegs)
