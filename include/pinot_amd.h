@@ -224,8 +224,8 @@ typedef struct {
 #define PA_QF_NO_FILTER_STATS (1 << 30)   /* the scan does NOT count what the execution statistics of an AND of two scan
                                              leaves need (by default it does wherever that fused count applies:
                                              pa_query_leap_leaf / pa_query_leap_counts / pa_query_execution_stats) */
-#define PA_QF2_NO_COUNT_FREE 1         /* partitioned V-only plans: the count + emit passes even where the count-free
-                                           emit (pve_jit.hip, pa_query_count_free_emit) applies */
+#define PA_QF2_NO_COUNT_FREE 1         /* partitioned plans: the count + emit passes even where the count-free emit
+                                           (pve_jit.hip, pa_query_count_free_emit) applies */
 #define PA_QF_PART_SHIFT 22              /* bits 22..23: LDS per partition of the partitioned aggregation (0 = auto,
                                              1 = 64 KiB, 2 = 96 KiB, 3 = 144 KiB): larger partitions = fewer record
                                              write fronts per XCD */
@@ -446,7 +446,8 @@ int32_t pa_query_lane_major(const pa_query* q);
  * shape (compiled by hiprtc at prepare), 0 if not, <0 error. */
 int32_t pa_query_dense_packed(const pa_query* q);
 /* 1 when the partitioned plan runs the count-free V emit (each workgroup writes whole record chunks into its own
- * region; pass C reads every partition through its chunk list: no count pass), 0 otherwise, <0 if not prepared. */
+ * region; pass C reads every partition through its chunk list: no count pass), 2 when it also runs the count-free H
+ * emit (DISTINCTCOUNTHLLMV next to the V stream), 0 otherwise, <0 if not prepared. */
 int32_t pa_query_count_free_emit(const pa_query* q);
 int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t* dma_slots, int32_t* ring,
                   int32_t* wg_per_cu, int32_t* grid, int32_t* lds_bytes);

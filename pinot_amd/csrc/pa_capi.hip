@@ -524,11 +524,14 @@ struct pa_query {
   int jit_waves = 0, jit_grid = 0, jit_lds = 0;
   DevBuf jit_args, jit_segs;
   // the partitioned path's V emit without a count pass (pve_jit.hip + pa_pve.hip): null = count + emit passes
-  hipFunction_t pve_fn = nullptr;
-  int pve_waves = 0, pve_grid = 0, pve_lds = 0, pve_bs = 0;
-  int64_t pve_chunks = 0;  // chunk slots per workgroup
-  DevBuf pve_args, pve_segs, pve_buf;
-  size_t pve_o_table = 0, pve_o_hist = 0, pve_o_used = 0, pve_o_off = 0, pve_o_base = 0, pve_o_index = 0, pve_o_tot = 0;
+  // one per record stream: pve (V), pvh (H records of a DISTINCTCOUNTHLLMV next to a V stream)
+  struct PveStream {
+    hipFunction_t fn = nullptr;
+    int waves = 0, grid = 0, lds = 0, cr = 0, parts = 0, bin_shift = 5;  // cr: records per chunk (pass C's unit)
+    int64_t chunks = 0;                                                  // chunk slots per workgroup
+    DevBuf args, segs, buf;
+    size_t o_table = 0, o_hist = 0, o_used = 0, o_off = 0, o_base = 0, o_index = 0, o_tot = 0;
+  } pve, pvh;
   int has_mv = 0;
   bool hashed = false;           // packed 64-bit keys through a global open-addressing table
   int key_words = 1;             // hashed: 2 = two-word keys ([k0, k1, state] per slot)
@@ -602,9 +605,11 @@ struct pa_query {
     dev_free(dgdplans);
     dev_free(jit_args);
     dev_free(jit_segs);
-    dev_free(pve_args);
-    dev_free(pve_segs);
-    dev_free(pve_buf);
+    for (PveStream* p : {&pve, &pvh}) {
+      dev_free(p->args);
+      dev_free(p->segs);
+      dev_free(p->buf);
+    }
     if (host_acc) (void)hipHostFree(host_acc);
     dev_free(fetch_blocks);
     dev_free(fetch_stage);
@@ -3101,6 +3106,7 @@ struct PveSegH {  // == pve_jit.hip PveSeg
   int32_t num_docs, num_tiles;
   uint32_t lo_t[6], hi_t[6];
   uint64_t admit;
+  uint64_t raw, mv_off, mv_words, hlut;
 };
 struct PveArgsH {  // == pve_jit.hip PveArgs
   int64_t total_tiles;
@@ -3113,30 +3119,27 @@ struct PveArgsH {  // == pve_jit.hip PveArgs
   unsigned long long* matched;
 };
 
-static void pve_fill_pointers(pa_query* q, PveArgsH& a) {
-  char* b = (char*)q->pve_buf.p;
+static void pve_fill_pointers(const pa_query::PveStream& st, unsigned long long* matched, PveArgsH& a) {
+  char* b = (char*)st.buf.p;
   a.recs = (uint32_t*)b;
-  a.table = (uint32_t*)(b + q->pve_o_table);
-  a.hist = (uint32_t*)(b + q->pve_o_hist);
-  a.used = (uint32_t*)(b + q->pve_o_used);
-  a.matched = q->hq.matched_docs;
+  a.table = (uint32_t*)(b + st.o_table);
+  a.hist = (uint32_t*)(b + st.o_hist);
+  a.used = (uint32_t*)(b + st.o_used);
+  a.matched = matched;
 }
 
-int pve_plan(pa_query* q, const Prep& P, int cus) {
-  q->pve_fn = nullptr;
+// One record stream's kernel and buffers. V (hmode false): a record per matching doc, rw words (1: key offset | value
+// id, 2 / 3: key offset + the raw 32 / 64-bit value staged from a raw column of rawb bytes per doc). H: a record per
+// value of the DISTINCTCOUNTHLLMV column. base_parts: partitions the V stream's base array holds room for (Pv + 1 +
+// Ph + 1 when both streams run: pass C reads the H bases at base[pv + 1 ..]). Leaves S.fn null when the shape does not
+// fit (the count + emit passes run).
+static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, int rawb, int64_t base_entries,
+                      pa_query::PveStream& S) {
+  S.fn = nullptr;
   const pa_query_spec& s = q->spec;
   const DevQuery& h = q->hq;
-  if (!q->partitioned || q->split_emit || h.hll_agg >= 0 || q->limit_mode || q->hashed) return PA_OK;
-  if (q->limit_walk && h.gb_mv >= 0) return PA_OK;
-  if ((s.flags & PA_QF_NO_JIT) || (s.flags2 & PA_QF2_NO_COUNT_FREE) || std::getenv("PA_NO_JIT") ||
-      (std::getenv("PA_DEBUG_EMIT") && !std::getenv("PA_PVE_DBG")))
-    return PA_OK;
-  if ((h.v_fmt != V_FMT_ID && h.v_fmt != V_FMT_KEY) || h.rec_words_v != 1 || q->part_vk == kVkGeneric) return PA_OK;
-  if (q->nseg == 0 || s.num_group_by < 1 || s.num_group_by > 4 || q->num_eager != (int)q->literals.size() ||
-      q->num_eager > 6 || h.pv > 4096 || h.kshift_v < 1)
-    return PA_OK;
-  // the columns the kernel stages (its own 1024-doc tile image, whatever the planner staged for the count + emit
-  // passes): the filter leaves', the group-by columns, the value column — dictionary-encoded SV in every segment
+  // the columns the kernel stages (its own tile image, whatever the planner staged for the count + emit passes): the
+  // filter leaves', the group-by columns, the V stream's value-id column — dictionary-encoded SV in every segment
   std::vector<int> slots;
   auto col_of = [&](int slot) {
     for (size_t k = 0; k < slots.size(); ++k)
@@ -3160,14 +3163,25 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
     gc.push_back(col_of(P.gb_slot[j]));
     gs.push_back((int)(uint32_t)h.gb_stride[j]);
   }
-  int vc = -1;
-  if (h.v_fmt == V_FMT_ID) {
+  int vc = -1, rslot = -1, mslot = -1, hnb = 1, lg = 0;
+  if (!hmode && h.v_fmt == V_FMT_ID) {
     if (h.emit_val_agg < 0) return PA_OK;
     vc = col_of(P.agg_slot[h.emit_val_agg]);
   }
+  if (!hmode && rawb) {
+    if (h.emit_val_agg < 0) return PA_OK;
+    rslot = P.agg_slot[h.emit_val_agg];
+  }
+  if (hmode) {
+    mslot = P.agg_slot[h.hll_agg];
+    hnb = d0.cols[mslot].nbits;
+    lg = h.aggs[h.hll_agg].log2m;
+  }
   const int nc = (int)slots.size();
   if (nc < 1 || nc > 6) return PA_OK;
-  for (const DevSeg& d : q->hsegs) {
+  int max_values = 1;
+  for (int si = 0; si < q->nseg; ++si) {
+    const DevSeg& d = q->hsegs[si];
     if (d.vremap) return PA_OK;
     for (int j = 0; j < s.num_group_by; ++j)
       if (d.remap[j]) return PA_OK;
@@ -3176,24 +3190,48 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
       if (c.kind != COL_SV_DICT || !c.words || c.nbits < 1 || c.nbits > 31 || c.nbits != d0.cols[slots[k]].nbits)
         return PA_OK;
     }
+    if (rslot >= 0) {
+      const DevCol& c = d.cols[rslot];
+      if (c.kind != COL_SV_RAW || !c.raw) return PA_OK;
+      if (rawb == 4 ? c.vtype != PA_INT : (c.vtype != PA_LONG && c.vtype != PA_DOUBLE)) return PA_OK;
+    }
+    if (hmode) {
+      const DevCol& c = d.cols[mslot];
+      if (c.kind != COL_MV_DICT || !c.words || !c.mv_off || c.nbits != hnb || hnb < 1 || hnb > 31 ||
+          !d.hll_lut[h.hll_agg])
+        return PA_OK;
+      max_values = std::max(max_values, q->segs[si]->cols.at(s.aggs[h.hll_agg].column_id)->max_values);
+    }
   }
   if ((uint64_t)q->num_keys > 0xffffffffull) return PA_OK;
+  const int Pn = hmode ? h.num_parts - h.pv : h.pv;
+  const int ks = hmode ? h.kshift_h : h.kshift_v;
+  if (Pn < 1 || Pn > 4096 || ks < 1) return PA_OK;
   // tile image of nd docs per lane (64 nd per tile): a 16-byte guard, then per column its tile's bits (8 nd nb bytes)
-  // and a 16-byte guard. 16 docs per lane unless 8 leave room for more resident waves (PA_PVE_ND: measurement)
-  const int Pv0 = h.pv;
-  const size_t l_ring0 = ((((size_t)(5 * Pv0 + 1) * 4 + 15) & ~(size_t)15) + (size_t)Pv0 * 32 * 4 + 15) & ~(size_t)15;
+  // and a 16-byte guard, then the raw values (64 nd rawb bytes). 16 docs per lane unless 8 leave room for more
+  // resident waves (PA_PVE_ND: measurement); 32-record bins unless 16 do (H: many partitions)
+  auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
   auto image_bytes = [&](int nd) {
     size_t b = 16;
     for (int k = 0; k < nc; ++k) b += (size_t)8 * nd * d0.cols[slots[k]].nbits + 16;
-    return b;
+    return b + (size_t)64 * nd * rawb;
   };
-  auto waves_for = [&](int nd) {
+  auto lds_ring = [&](int bs) { return al16(al16((size_t)(5 * Pn + 1) * 4) + (size_t)Pn * bs * rw * 4); };
+  auto waves_for = [&](int nd, int bs) {
     for (int cand : {16, 12, 8, 4})
-      if (l_ring0 + (size_t)cand * 2 * image_bytes(nd) <= kLdsBudget) return cand;
+      if (lds_ring(bs) + (size_t)cand * 2 * image_bytes(nd) <= kLdsBudget) return cand;
     return 0;
   };
-  int nd = waves_for(8) > waves_for(16) ? 8 : 16;
+  // H: 8 docs per lane (a lane's run of MV values is half as long: the value loads of a wave spread over fewer cache
+  // lines; measured 3.97 vs 4.8 ms on configs[4]); bins of 16 records when 32 cost resident waves (H only: the V
+  // stream's three-word records measured slower with 16-record bins and more waves, 1.70 vs 1.33 ms)
+  int bs = 32;
+  if (hmode && waves_for(8, 32) < 16 && waves_for(8, 16) > waves_for(8, 32)) bs = 16;
+  int nd = hmode ? 8 : (waves_for(8, bs) > waves_for(16, bs) ? 8 : 16);
   if (const char* e = std::getenv("PA_PVE_ND")) nd = std::atoi(e) == 8 ? 8 : 16;
+  if (const char* e = std::getenv("PA_PVE_BS")) bs = std::atoi(e) == 16 ? 16 : 32;  // (measurement)
+  const int w = waves_for(nd, bs);
+  if (!w) return PA_OK;
   std::vector<int> nb, coff;
   size_t img_bytes = 16;
   for (int k = 0; k < nc; ++k) {
@@ -3201,27 +3239,31 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
     coff.push_back((int)img_bytes);
     img_bytes += (size_t)8 * nd * nb.back() + 16;
   }
+  const size_t raw_off = img_bytes;
+  img_bytes += (size_t)64 * nd * rawb;
   const int img_dw = (int)(img_bytes / 4);
   const int td = 64 * nd;
-  const int Pv = h.pv, bs = 32, sc = std::getenv("PA_PVE_SC") ? std::atoi(std::getenv("PA_PVE_SC")) : 4;
+  const size_t l_bins = al16((size_t)(5 * Pn + 1) * 4);
+  const size_t l_ring = lds_ring(bs);
+  const size_t lds = l_ring + (size_t)w * 2 * img_bytes;
+  // one workgroup per CU; a workgroup's region holds its docs' records (H: at most max_values per doc) in whole chunks
+  // plus one partial chunk per partition; chunks of sc bins, more when the region would need 2^16 chunks
+  std::vector<int64_t> first(q->nseg + 1, 0);  // the kernel's own tiles of td docs
+  for (int si = 0; si < q->nseg; ++si) first[si + 1] = first[si] + (q->hsegs[si].num_docs + td - 1) / td;
+  const int64_t T = first[q->nseg];
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (T + w - 1) / w));
+  const int64_t recs_per_wg = (T + G - 1) / G * td * (int64_t)max_values;
+  int sc = std::getenv("PA_PVE_SC") ? std::atoi(std::getenv("PA_PVE_SC")) : 4;
   if (sc < 1 || sc > 16 || (sc & (sc - 1))) return PA_OK;  // (bins - 1 of a chunk: 4 bits of its list entry)
-  auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  const size_t l_bins = al16((size_t)(5 * Pv + 1) * 4);
-  const size_t l_ring = al16(l_bins + (size_t)Pv * bs * 4);
-  const size_t img_b = img_bytes;
-  int w = 0;
-  for (int cand : {16, 12, 8, 4})
-    if (l_ring + (size_t)cand * 2 * img_b <= kLdsBudget) {
-      w = cand;
-      break;
-    }
-  if (!w) return PA_OK;
-  const size_t lds = l_ring + (size_t)w * 2 * img_b;
+  auto chunks_for = [&](int c) { return (recs_per_wg + (int64_t)bs * c - 1) / ((int64_t)bs * c) + Pn; };
+  while (sc < 16 && chunks_for(sc) >= (int64_t(1) << 16)) sc *= 2;
+  const int64_t cr = (int64_t)bs * sc;  // records per chunk
+  const int64_t C = chunks_for(sc);
+  if (C >= (int64_t(1) << 16) || (int64_t)G * C >= (int64_t(1) << 28)) return PA_OK;  // (table ranks, chunk ids)
   auto pad1 = [](std::vector<int> v) {
     if (v.empty()) v.push_back(0);
     return v;
   };
-  std::vector<std::string> gsv;
   std::string gss = "{";
   for (size_t j = 0; j < gs.size(); ++j) gss += (j ? "," : "") + std::to_string((uint32_t)gs[j]) + "u";
   gss += "}";
@@ -3230,49 +3272,41 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
       "-DPVE_NC=" + std::to_string(nc), "-DPVE_NB=" + int_list(nb), "-DPVE_OFF=" + int_list(coff),
       "-DPVE_NL=" + std::to_string(q->num_eager), "-DPVE_LC=" + int_list(pad1(lc)), "-DPVE_LN=" + int_list(pad1(ln)),
       "-DPVE_LE=" + int_list(pad1(le)), "-DPVE_NG=" + std::to_string(s.num_group_by), "-DPVE_GC=" + int_list(gc),
-      "-DPVE_GS=" + gss, "-DPVE_VC=" + std::to_string(vc), "-DPVE_KS=" + std::to_string(h.kshift_v),
-      "-DPVE_P=" + std::to_string(Pv), "-DPVE_BS=" + std::to_string(bs), "-DPVE_SC=" + std::to_string(sc),
+      "-DPVE_GS=" + gss, "-DPVE_VC=" + std::to_string(vc), "-DPVE_KS=" + std::to_string(ks),
+      "-DPVE_P=" + std::to_string(Pn), "-DPVE_BS=" + std::to_string(bs), "-DPVE_SC=" + std::to_string(sc),
       "-DPVE_L_BINS=" + std::to_string(l_bins), "-DPVE_ADMIT=" + std::to_string(q->limit_walk ? 1 : 0),
-      "-DPVE_L_RING=" + std::to_string(l_ring)};
+      "-DPVE_L_RING=" + std::to_string(l_ring), "-DPVE_RW=" + std::to_string(rw),
+      "-DPVE_RAWB=" + std::to_string(rawb), "-DPVE_RAWOFF=" + std::to_string(raw_off),
+      "-DPVE_H=" + std::to_string(hmode ? 1 : 0), "-DPVE_HNB=" + std::to_string(hnb), "-DPVE_LG=" + std::to_string(lg)};
   if (const char* dbg = std::getenv("PA_PVE_DBG")) defs.push_back(std::string("-DPVE_DBG=") + dbg);  // (measurement)
   if (const char* pb = std::getenv("PA_PVE_PB")) defs.push_back(std::string("-DPVE_PB=") + pb);      // (measurement)
   hipFunction_t fn = jit_compile(defs, kPveJitSrc, "pve_jit");
   if (!fn) return PA_OK;
   (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  // one workgroup per CU; a workgroup's region holds its docs' records in whole chunks plus one partial chunk per
-  // partition
-  std::vector<int64_t> first(q->nseg + 1, 0);  // 1024-doc tiles of the kernel's own schedule
-  for (int si = 0; si < q->nseg; ++si) first[si + 1] = first[si] + (q->hsegs[si].num_docs + td - 1) / td;
-  const int64_t T = first[q->nseg];
-  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (T + w - 1) / w));
-  const int64_t tiles_per_wg = (T + G - 1) / G;
-  const int64_t cr = (int64_t)bs * sc;  // records per chunk
-  const int64_t C = (tiles_per_wg * td + cr - 1) / cr + Pv;
-  if (C >= (int64_t(1) << 16) || (int64_t)G * C >= (int64_t(1) << 28)) return PA_OK;  // (table ranks, chunk ids)
-  const size_t o_table = al16((size_t)G * C * cr * 4);
+  const size_t o_table = al16((size_t)G * C * cr * rw * 4);
   const size_t o_hist = al16(o_table + (size_t)G * C * 4);
-  const size_t o_used = al16(o_hist + (size_t)G * Pv * 4);
+  const size_t o_used = al16(o_hist + (size_t)G * Pn * 4);
   const size_t o_off = al16(o_used + (size_t)G * 4);
-  const size_t o_base = al16(o_off + (size_t)G * Pv * 4);
-  const size_t o_index = al16(o_base + (size_t)(Pv + 1) * 8);
+  const size_t o_base = al16(o_off + (size_t)G * Pn * 4);
+  const size_t o_index = al16(o_base + (size_t)std::max<int64_t>(base_entries, Pn + 1) * 8);
   const size_t o_tot = al16(o_index + (size_t)G * C * 4);
-  const size_t total = o_tot + (size_t)Pv * 4;
-  int rc = dev_alloc(q->pve_buf, total);
+  const size_t total = o_tot + (size_t)Pn * 4;
+  int rc = dev_alloc(S.buf, total);
   if (rc) return rc;
-  q->pve_o_table = o_table;
-  q->pve_o_hist = o_hist;
-  q->pve_o_used = o_used;
-  q->pve_o_off = o_off;
-  q->pve_o_base = o_base;
-  q->pve_o_index = o_index;
-  q->pve_o_tot = o_tot;
+  S.o_table = o_table;
+  S.o_hist = o_hist;
+  S.o_used = o_used;
+  S.o_off = o_off;
+  S.o_base = o_base;
+  S.o_index = o_index;
+  S.o_tot = o_tot;
   PveArgsH a;
   std::memset(&a, 0, sizeof(a));
   a.total_tiles = T;
   a.nseg = q->nseg;
   a.xcd_major = 1;
   a.chunks_per_wg = C;
-  pve_fill_pointers(q, a);
+  pve_fill_pointers(S, q->hq.matched_docs, a);
   std::vector<PveSegH> js(q->nseg);
   for (int si = 0; si < q->nseg; ++si) {
     const DevSeg& d = q->hsegs[si];
@@ -3287,20 +3321,61 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
       j.hi_t[li] = (uint32_t)d.leaves[li].span;
     }
     j.admit = (uint64_t)(uintptr_t)d.admit;
+    if (rslot >= 0) j.raw = (uint64_t)(uintptr_t)d.cols[rslot].raw;
+    if (hmode) {
+      j.mv_off = (uint64_t)(uintptr_t)d.cols[mslot].mv_off;
+      j.mv_words = (uint64_t)(uintptr_t)d.cols[mslot].words;
+      j.hlut = (uint64_t)(uintptr_t)d.hll_lut[h.hll_agg];
+    }
   }
-  rc = dev_alloc(q->pve_args, sizeof(PveArgsH));
-  if (!rc) rc = dev_alloc(q->pve_segs, sizeof(PveSegH) * js.size());
+  rc = dev_alloc(S.args, sizeof(PveArgsH));
+  if (!rc) rc = dev_alloc(S.segs, sizeof(PveSegH) * js.size());
   if (rc) return rc;
-  PA_HIP(hipMemcpy(q->pve_args.p, &a, sizeof(a), hipMemcpyHostToDevice));
-  PA_HIP(hipMemcpy(q->pve_segs.p, js.data(), sizeof(PveSegH) * js.size(), hipMemcpyHostToDevice));
-  q->pve_fn = fn;
-  q->pve_waves = w;
-  q->pve_grid = G;
-  q->pve_lds = (int)lds;
-  q->pve_bs = (int)cr;
-  q->pve_chunks = C;
-  PLAN_LOG("pve: W %d nd %d grid %d lds %zu C %lld P %d", w, nd, G, lds, (long long)C, Pv);
+  PA_HIP(hipMemcpy(S.args.p, &a, sizeof(a), hipMemcpyHostToDevice));
+  PA_HIP(hipMemcpy(S.segs.p, js.data(), sizeof(PveSegH) * js.size(), hipMemcpyHostToDevice));
+  S.fn = fn;
+  S.waves = w;
+  S.grid = G;
+  S.lds = (int)lds;
+  S.cr = (int)cr;
+  S.parts = Pn;
+  S.bin_shift = __builtin_ctz((unsigned)bs);
+  S.chunks = C;
+  PLAN_LOG("pve %s: W %d nd %d bs %d sc %d grid %d lds %zu C %lld P %d", hmode ? "H" : "V", w, nd, bs, sc, G, lds,
+           (long long)C, Pn);
   return PA_OK;
+}
+
+int pve_plan(pa_query* q, const Prep& P, int cus) {
+  q->pve.fn = q->pvh.fn = nullptr;
+  const pa_query_spec& s = q->spec;
+  const DevQuery& h = q->hq;
+  if (!q->partitioned || q->limit_mode || q->hashed) return PA_OK;
+  if (q->limit_walk && h.gb_mv >= 0) return PA_OK;
+  if ((s.flags & PA_QF_NO_JIT) || (s.flags2 & PA_QF2_NO_COUNT_FREE) || std::getenv("PA_NO_JIT") ||
+      (std::getenv("PA_DEBUG_EMIT") && !std::getenv("PA_PVE_DBG")))
+    return PA_OK;
+  // both streams (DISTINCTCOUNTHLLMV next to a V stream): two launches, COUNT from the V records
+  const bool hstream = h.hll_agg >= 0;
+  if (hstream && (!q->split_emit || h.h_first || h.gb_mv >= 0)) return PA_OK;
+  if (!hstream && q->split_emit) return PA_OK;
+  int rw = 1, rawb = 0;
+  if (h.v_fmt == V_FMT_32 || h.v_fmt == V_FMT_64) {  // raw value columns only (dictionary values: V_FMT_ID)
+    rw = h.v_fmt == V_FMT_32 ? 2 : 3;
+    rawb = h.v_fmt == V_FMT_32 ? 4 : 8;
+  } else if (h.v_fmt != V_FMT_ID && h.v_fmt != V_FMT_KEY) {
+    return PA_OK;
+  }
+  if (h.rec_words_v != rw || q->part_vk == kVkGeneric) return PA_OK;
+  if (q->nseg == 0 || s.num_group_by < 1 || s.num_group_by > 4 || q->num_eager != (int)q->literals.size() ||
+      q->num_eager > 6 || h.pv > 4096 || h.kshift_v < 1)
+    return PA_OK;
+  const int64_t base_entries = (int64_t)h.pv + 1 + (hstream ? (int64_t)(h.num_parts - h.pv) + 1 : 0);
+  int rc = pve_stream(q, P, cus, false, rw, rawb, base_entries, q->pve);
+  if (rc || !q->pve.fn || !hstream) return rc;
+  rc = pve_stream(q, P, cus, true, 1, 0, 0, q->pvh);
+  if (rc || !q->pvh.fn) q->pve.fn = nullptr;  // (both streams or neither: the count pass serves both)
+  return rc;
 }
 
 int pa_query_prepare(pa_query* q) {
@@ -3449,24 +3524,37 @@ int pa_query_scan(pa_query* q, void* stream) {
     PA_HIP(launch_limit_passes(dq, ds, F, q->limit_grid, 2, st));
     return PA_OK;
   }
-  if (q->pve_fn) {  // the count-free emit: records in per-workgroup chunks, the partitions' chunk lists, pass C
-    void* pa = q->pve_args.p;
-    void* psg = q->pve_segs.p;
-    void* params[] = {&pa, &psg};
-    PA_HIP(hipModuleLaunchKernel(q->pve_fn, q->pve_grid, 1, 1, q->pve_waves * kWave, 1, 1, q->pve_lds, st, params,
-                                 nullptr));
-    char* b = (char*)q->pve_buf.p;
-    PA_HIP(launch_pve_lists((const uint32_t*)(b + q->pve_o_hist), (uint32_t*)(b + q->pve_o_off),
-                            (uint64_t*)(b + q->pve_o_base), (const uint32_t*)(b + q->pve_o_table),
-                            (const uint32_t*)(b + q->pve_o_used), (uint32_t*)(b + q->pve_o_index),
-                            (uint32_t*)(b + q->pve_o_tot), q->pve_grid, q->hq.pv, q->pve_chunks, q->pve_bs, st));
+  if (q->pve.fn) {  // the count-free emit: records in per-workgroup chunks, the partitions' chunk lists, pass C
     PartScratch ps{};
-    ps.base = (uint64_t*)(b + q->pve_o_base);
-    ps.recs_v = (uint32_t*)b;
-    ps.chunk_index = (const uint32_t*)(b + q->pve_o_index);
-    ps.chunk_shift = __builtin_ctz((unsigned)q->pve_bs);
-    ps.chunk_bin_shift = 5;  // (32-record bins)
-    PA_HIP(launch_part_agg(q->part_vk, (const DevQuery*)q->dq.p, ps, q->hq.pv, q->part_lds_c, st));
+    char* vb = (char*)q->pve.buf.p;
+    ps.base = (uint64_t*)(vb + q->pve.o_base);
+    for (pa_query::PveStream* S : {&q->pve, &q->pvh}) {
+      if (!S->fn) continue;
+      void* pa = S->args.p;
+      void* psg = S->segs.p;
+      void* params[] = {&pa, &psg};
+      PA_HIP(hipModuleLaunchKernel(S->fn, S->grid, 1, 1, S->waves * kWave, 1, 1, S->lds, st, params, nullptr));
+      char* b = (char*)S->buf.p;
+      // (the H partitions' bases follow the V partitions' in the V buffer's base array: base[pv + 1 ..])
+      uint64_t* base = S == &q->pve ? ps.base : ps.base + q->hq.pv + 1;
+      PA_HIP(launch_pve_lists((const uint32_t*)(b + S->o_hist), (uint32_t*)(b + S->o_off), base,
+                              (const uint32_t*)(b + S->o_table), (const uint32_t*)(b + S->o_used),
+                              (uint32_t*)(b + S->o_index), (uint32_t*)(b + S->o_tot), S->grid, S->parts, S->chunks,
+                              S->cr, st));
+      if (S == &q->pve) {
+        ps.recs_v = (uint32_t*)b;
+        ps.chunk_index = (const uint32_t*)(b + S->o_index);
+        ps.chunk_shift = __builtin_ctz((unsigned)S->cr);
+        ps.chunk_bin_shift = S->bin_shift;
+      } else {
+        ps.recs_h = (uint32_t*)b;
+        ps.chunk_index_h = (const uint32_t*)(b + S->o_index);
+        ps.chunk_shift_h = __builtin_ctz((unsigned)S->cr);
+        ps.chunk_bin_shift_h = S->bin_shift;
+      }
+    }
+    PA_HIP(launch_part_agg(q->part_vk, (const DevQuery*)q->dq.p, ps, q->pvh.fn ? q->hq.num_parts : q->hq.pv,
+                           q->part_lds_c, st));
     return PA_OK;
   }
   if (q->partitioned) {  // count pass, range offsets, emit pass into the partitions, per-partition aggregation
@@ -3542,11 +3630,12 @@ int pa_query_set_accumulator_buffer(pa_query* q, void* device_buffer, uint64_t b
     jit_fill_pointers(q, a);
     PA_HIP(hipMemcpy(q->jit_args.p, &a, sizeof(a), hipMemcpyHostToDevice));
   }
-  if (q->pve_fn) {
+  for (pa_query::PveStream* S : {&q->pve, &q->pvh}) {
+    if (!S->fn) continue;
     PveArgsH a;
-    PA_HIP(hipMemcpy(&a, q->pve_args.p, sizeof(a), hipMemcpyDeviceToHost));
-    pve_fill_pointers(q, a);
-    PA_HIP(hipMemcpy(q->pve_args.p, &a, sizeof(a), hipMemcpyHostToDevice));
+    PA_HIP(hipMemcpy(&a, S->args.p, sizeof(a), hipMemcpyDeviceToHost));
+    pve_fill_pointers(*S, q->hq.matched_docs, a);
+    PA_HIP(hipMemcpy(S->args.p, &a, sizeof(a), hipMemcpyHostToDevice));
   }
   if (q->partitioned) {
     relocate(q->hq_count);
@@ -4052,7 +4141,7 @@ int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t*
 int32_t pa_query_num_eager_literals(const pa_query* q) { return q && q->prepared ? q->num_eager : -1; }
 
 int32_t pa_query_lane_major(const pa_query* q) { return q && q->prepared ? q->lane_major : -1; }
-int32_t pa_query_count_free_emit(const pa_query* q) { return q && q->prepared ? (q->pve_fn ? 1 : 0) : -1; }
+int32_t pa_query_count_free_emit(const pa_query* q) { return q && q->prepared ? (q->pve.fn ? (q->pvh.fn ? 2 : 1) : 0) : -1; }
 int32_t pa_query_dense_packed(const pa_query* q) {
   return q && q->prepared ? (q->dense_packed ? (q->jit_fn ? 2 : 1) : 0) : -1;
 }

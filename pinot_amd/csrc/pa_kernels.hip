@@ -1424,22 +1424,35 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
     }
   }
   for (uint64_t b0 = r0; b0 < r1; b0 += span) {
+    // every address first (the chunk entries were loaded a batch ago), then the loads back to back without a branch
+    // per load (a branch per load makes each wait for the one before it); an absent record reads record 0 (always
+    // allocated) and becomes a sentinel
     uint32_t w0[kB], w1[kB], w2[kB];
+    uint64_t pa[kB];
+    bool ok[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       const uint64_t ri = b0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
-      w0[j] = kSentinel;
-      w1[j] = w2[j] = 0u;
-      if (ri < r1) {
-        const uint64_t pi = cix ? ((uint64_t)(cid[j] & 0x0fffffffu) << csh) | (ri & cmask) : ri;
-        // (a partition's last chunk per workgroup holds (cid >> 28) + 1 bins)
-        const bool in = !cix || (uint32_t)(ri & cmask) < (((cid[j] >> 28) + 1u) << ps.chunk_bin_shift);
-        const AS1 uint32_t* rec = recs + pi * (uint64_t)W;
-        if (in) w0[j] = __builtin_nontemporal_load(rec);
-        if (fmt == V_FMT_32 || fmt == V_FMT_64) w1[j] = __builtin_nontemporal_load(rec + 1);
-        if (fmt == V_FMT_64) w2[j] = __builtin_nontemporal_load(rec + 2);
-      }
+      const uint64_t pi = cix ? ((uint64_t)(cid[j] & 0x0fffffffu) << csh) | (ri & cmask) : ri;
+      // (a partition's last chunk per workgroup holds (cid >> 28) + 1 bins)
+      ok[j] = ri < r1 && (!cix || (uint32_t)(ri & cmask) < (((cid[j] >> 28) + 1u) << ps.chunk_bin_shift));
+      pa[j] = ok[j] ? pi * (uint64_t)W : 0ull;
     }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) w0[j] = __builtin_nontemporal_load(recs + pa[j]);
+#pragma unroll
+    for (int j = 0; j < kB; ++j) w1[j] = w2[j] = 0u;
+    if (fmt == V_FMT_32 || fmt == V_FMT_64) {
+#pragma unroll
+      for (int j = 0; j < kB; ++j) w1[j] = __builtin_nontemporal_load(recs + pa[j] + 1);
+    }
+    if (fmt == V_FMT_64) {
+#pragma unroll
+      for (int j = 0; j < kB; ++j) w2[j] = __builtin_nontemporal_load(recs + pa[j] + 2);
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j)
+      if (!ok[j]) w0[j] = kSentinel;
     if (cix) {
 #pragma unroll
       for (int j = 0; j < kB; ++j) {
@@ -1548,12 +1561,41 @@ __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps
   const uint32_t rmask = (1u << lg) - 1u;
   constexpr int kB = 8;
   const uint64_t span = (uint64_t)kB * kPartAggThreads;
+  // chunked records (count-free emit): as part_agg_v_fast, the chunk entries one batch ahead
+  const AS1 uint32_t* cix = ps.chunk_index_h ? gp(ps.chunk_index_h) : nullptr;
+  const int csh = (int)ps.chunk_shift_h;
+  const uint64_t cmask = cix ? (1ull << csh) - 1ull : 0ull;
+  uint32_t cid[kB];
+  if (cix) {
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const uint64_t ri = r0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
+      cid[j] = ri < r1 ? cix[ri >> csh] : 0u;
+    }
+  }
   for (uint64_t b0 = r0; b0 < r1; b0 += span) {
+    // (as part_agg_v_fast: every address, then the loads without a branch per load; an absent record reads record 0)
     uint32_t w[kB];
+    uint64_t pa[kB];
+    bool ok[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       const uint64_t ri = b0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
-      w[j] = ri < r1 ? __builtin_nontemporal_load(recs + ri) : kSentinel;
+      const uint64_t pi = cix ? ((uint64_t)(cid[j] & 0x0fffffffu) << csh) | (ri & cmask) : ri;
+      ok[j] = ri < r1 && (!cix || (uint32_t)(ri & cmask) < (((cid[j] >> 28) + 1u) << ps.chunk_bin_shift_h));
+      pa[j] = ok[j] ? pi : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) w[j] = __builtin_nontemporal_load(recs + pa[j]);
+#pragma unroll
+    for (int j = 0; j < kB; ++j)
+      if (!ok[j]) w[j] = kSentinel;
+    if (cix) {
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        const uint64_t ri = b0 + span + (uint64_t)j * kPartAggThreads + threadIdx.x;
+        cid[j] = ri < r1 ? cix[ri >> csh] : 0u;
+      }
     }
     // Byte max by compare-and-swap, in phases over the kB records (each phase one run of independent LDS operations,
     // one wait): read every target word, try every needed swap once, then retry the few that lost a race.

@@ -53,6 +53,27 @@ constexpr u32 kSentinel = 0xffffffffu;
 #ifndef PVE_DBG
 #define PVE_DBG 0  // measurement only (PA_PVE_DBG): 1 = records built but not put, 2 = full bins not stored
 #endif
+#ifndef PVE_RW
+#define PVE_RW 1  // words per record: 1 (key offset | value id), 2 (+ a raw 32-bit value), 3 (+ a raw 64-bit value)
+#endif
+#ifndef PVE_RAWB
+#define PVE_RAWB 0  // bytes per doc of the raw value column staged at PVE_RAWOFF (0: none; 4 with PVE_RW 2, 8 with 3)
+#endif
+#ifndef PVE_RAWOFF
+#define PVE_RAWOFF 0
+#endif
+#ifndef PVE_H
+#define PVE_H 0  // the H stream: one record per value of the DISTINCTCOUNTHLLMV column (PVE_HNB bits per dictId,
+#endif           // PVE_LG = log2m): key offset << (LG + 6) | register << 6 | rank << 1
+#ifndef PVE_HNB
+#define PVE_HNB 1
+#endif
+#ifndef PVE_LG
+#define PVE_LG 0
+#endif
+constexpr int RW = PVE_RW, RAWB = PVE_RAWB, HNB = PVE_HNB, LG = PVE_LG;
+static_assert(RW >= 1 && RW <= 3 && (RAWB == 0 || RAWB == 4 * (RW - 1)), "record words and the raw column agree");
+static_assert(!PVE_H || (RW == 1 && PVE_VC < 0 && RAWB == 0), "the H stream has one-word records");
 
 constexpr int kJitMax = 6;
 static_assert(NC <= kJitMax && NL <= kJitMax && NG <= 4, "shape beyond the JIT descriptors");
@@ -63,6 +84,10 @@ struct PveSeg {          // one bound segment (scalar loads at segment switches 
   int num_docs, num_tiles;
   u32 lo_t[kJitMax], hi_t[kJitMax];  // DICT_RANGE leaves: MSB-aligned bounds in this segment's dictId space
   u64 admit;             // PVE_ADMIT: the segment's admitted-key bitmap (limit_walk_kernel; 0 = every key)
+  u64 raw;               // PVE_RAWB: the raw value column (padded to whole 2048-doc tiles)
+  u64 mv_off;            // PVE_H: int32 value offset of every doc [num_docs + 1]
+  u64 mv_words;          // PVE_H: the MV column's value stream (byte-swapped words, past the guard words)
+  u64 hlut;              // PVE_H: dictId -> register << 8 | rank
 };
 struct PveArgs {
   i64 total_tiles;
@@ -108,6 +133,12 @@ __device__ __forceinline__ void dma_cols(CS* sg, i64 wt, u32 img, u32 voff) {
     for (int k = 0; k < CH / 64; ++k) dma16(voff, src + 1024u * k, dst + 1024u * k);
     if constexpr (CH % 64) dma16m(voff, src + 1024u * (CH / 64), dst + 1024u * (CH / 64), (1ull << (CH % 64)) - 1ull);
     dma_cols<C + 1>(sg, wt, img, voff);
+  } else if constexpr (RAWB > 0) {
+    constexpr int CH = TD * RAWB / 16;  // (a multiple of 64: whole wave instructions)
+    const u64 src = sg->raw + (u64)wt * (u64)(TD * RAWB);
+    const u32 dst = img + (u32)PVE_RAWOFF;
+#pragma unroll
+    for (int k = 0; k < CH / 64; ++k) dma16(voff, src + 1024u * k, dst + 1024u * k);
   }
 }
 
@@ -220,9 +251,11 @@ __device__ __forceinline__ i64 bin_slot(const Bins& B, u32 p) {
 }
 
 typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kPieces = BS * RW / 4;  // 16-byte pieces of a bin
 
-// Every bin the wave completed (full[i] of its lanes) leaves together: eight lanes per bin (16 bytes each, so one store
-// instruction writes eight whole bins), the group's first lane takes the chunk slot and restarts the bin after the copy.
+// Every bin the wave completed (full[i] of its lanes) leaves together: eight lanes per bin (16 bytes each per store
+// instruction: a 32-record one-word bin is one instruction for eight bins), the group's first lane takes the chunk slot
+// and restarts the bin after the copy.
 __device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE_PB], const u32 (&pp)[PVE_PB], int lane) {
   u64 fm[PVE_PB];
   u64 any = 0;
@@ -244,8 +277,13 @@ __device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE
     const i64 dst_rec = ((i64)__builtin_amdgcn_ds_bpermute(leader << 2, (int)(u32)at_rec) & 0xffffffffll) |
                         ((i64)__builtin_amdgcn_ds_bpermute(leader << 2, (int)(u32)((u64)at_rec >> 32)) << 32);
     if (on && dst_rec >= 0 && PVE_DBG != 2) {
-      const u32x4 v = *at<const __attribute__((address_space(3))) u32x4>(B.bins + mine * (u32)BS * 4u + 16u * (u32)sub);
-      __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4*)(B.recs + dst_rec) + sub);
+#pragma unroll
+      for (int k = 0; k < kPieces; k += 8) {
+        if (kPieces % 8 != 0 && sub + k >= kPieces) break;
+        const u32x4 v = *at<const __attribute__((address_space(3))) u32x4>(B.bins + mine * (u32)(BS * RW) * 4u +
+                                                                             16u * (u32)(sub + k));
+        __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4*)(B.recs + dst_rec * RW) + sub + k);
+      }
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (the bin is read before it restarts: LDS runs one wave's ops in order)
     if (on && sub == 0) {
@@ -275,28 +313,20 @@ __device__ __forceinline__ void flush_one(const Bins& B, u32 p) {
   const i64 dst_rec = bin_slot(B, p);
   if (dst_rec >= 0) {
     const __attribute__((address_space(3))) u32x4* src =
-        at<const __attribute__((address_space(3))) u32x4>(B.bins + p * (u32)BS * 4u);
-    __attribute__((address_space(1))) u32x4* dst = (__attribute__((address_space(1))) u32x4*)(B.recs + dst_rec);
-    for (int k = 0; k < BS / 4; ++k) __builtin_nontemporal_store(src[k], dst + k);
+        at<const __attribute__((address_space(3))) u32x4>(B.bins + p * (u32)(BS * RW) * 4u);
+    __attribute__((address_space(1))) u32x4* dst = (__attribute__((address_space(1))) u32x4*)(B.recs + dst_rec * RW);
+    for (int k = 0; k < kPieces; ++k) __builtin_nontemporal_store(src[k], dst + k);
   }
   at<l32>(B.done)[p] = 0u;
   at<l32>(B.cnt)[p] = 0u;
 }
 
-// the lane's matching docs (bits of m) into their partitions' bins, 8 at a time: claim, write, count written; a lane
+// PB records of the lane (pend[i]: record i exists) into their partitions' bins: claim, write, count written; a lane
 // that completes a bin flushes it; a record whose bin was full claims again after the flushes
-__device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], const u32 (&val)[ND], int lane) {
-  constexpr int PB = PVE_PB;
-#pragma unroll
-  for (int h = 0; h < ND; h += PB) {
-    bool pend[PB];
-    u32 pp[PB], rr[PB];
-#pragma unroll
-    for (int i = 0; i < PB; ++i) {
-      pend[i] = (m >> (h + i)) & 1u;
-      pp[i] = key[h + i] >> KS;
-      rr[i] = (key[h + i] & ((1u << KS) - 1u)) | (VC >= 0 ? (val[h + i] << KS) : 0u);
-    }
+constexpr int PB = PVE_PB;
+__device__ __forceinline__ void put_round(const Bins& B, bool (&pend)[PB], const u32 (&pp)[PB], const u32 (&rr)[PB][RW],
+                                          int lane) {
+  {
     for (int round = 0;; ++round) {
       u32 s[PB];
 #pragma unroll
@@ -305,7 +335,9 @@ __device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], 
                        : 0xffffffffu;
 #pragma unroll
       for (int i = 0; i < PB; ++i)
-        if (s[i] < (u32)BS) at<l32>(B.bins)[pp[i] * (u32)BS + s[i]] = rr[i];
+        if (s[i] < (u32)BS)
+#pragma unroll
+          for (int k = 0; k < RW; ++k) at<l32>(B.bins)[(pp[i] * (u32)BS + s[i]) * (u32)RW + (u32)k] = rr[i][k];
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       bool full[PB];
 #pragma unroll
@@ -326,6 +358,86 @@ __device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], 
   }
 }
 
+// the V stream: the lane's matching docs (bits of m), PB at a time
+__device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], const u32 (&val)[ND][RW], int lane) {
+#pragma unroll
+  for (int h = 0; h < ND; h += PB) {
+    bool pend[PB];
+    u32 pp[PB], rr[PB][RW];
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      pend[i] = (m >> (h + i)) & 1u;
+      pp[i] = key[h + i] >> KS;
+      rr[i][0] = (key[h + i] & ((1u << KS) - 1u)) | (VC >= 0 ? (val[h + i][0] << KS) : 0u);
+#pragma unroll
+      for (int k = 1; k < RW; ++k) rr[i][k] = val[h + i][k];
+    }
+    put_round(B, pend, pp, rr, lane);
+  }
+}
+
+// The H stream: one record per value of the lane's matching docs, PB values per round. The lane's values are one run
+// [o[first match], o[last match + 1]) of the MV stream; a value's doc is the last doc whose first value is not past it
+// (unrolled compares: no dynamically indexed registers); values of unmatched docs inside the run are skipped.
+__device__ __forceinline__ void put_values(const Bins& B, CS* sg, i64 wt, u32 m, const u32 (&key)[ND], int lane) {
+  if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return;
+  const __attribute__((address_space(1))) int* off = (const __attribute__((address_space(1))) int*)sg->mv_off;
+  const __attribute__((address_space(1))) u32* words = (const __attribute__((address_space(1))) u32*)sg->mv_words;
+  const __attribute__((address_space(1))) u32* lut = (const __attribute__((address_space(1))) u32*)sg->hlut;
+  const i64 d0 = wt * TD + (i64)ND * lane, nd = sg->num_docs;
+  int o[ND + 1];
+#pragma unroll
+  for (int i = 0; i <= ND; ++i) o[i] = m ? off[d0 + i < nd ? d0 + i : nd] : 0;
+  int s = 0, e = 0;
+  if (m) {
+    const int f = __builtin_ctz(m), l = 31 - __builtin_clz(m);
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      if (i == f) s = o[i];
+      if (i == l) e = o[i + 1];
+    }
+  }
+  constexpr u32 kmask = (1u << KS) - 1u;
+  for (int v0 = s;; v0 += PB) {
+    bool pend[PB];
+    u32 pp[PB], rr[PB][RW], k[PB], wa[PB], wb[PB], sh[PB];
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int v = v0 + j;
+      u32 kk = key[0];
+      bool mm = m & 1u;
+#pragma unroll
+      for (int i = 1; i < ND; ++i)
+        if (v >= o[i]) {
+          kk = key[i];
+          mm = (m >> i) & 1u;
+        }
+      pend[j] = v < e && mm;
+      k[j] = kk;
+      const u64 bit = (u64)(u32)v * (u64)HNB;
+      sh[j] = (u32)bit & 31u;
+      wa[j] = wb[j] = 0u;
+      if (pend[j]) {
+        wa[j] = words[bit >> 5];
+        wb[j] = words[(bit >> 5) + 1];
+      }
+    }
+    u32 hv[PB];
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const u32 x = sh[j] ? __builtin_amdgcn_alignbit(wa[j], wb[j], 32u - sh[j]) : wa[j];
+      hv[j] = pend[j] ? lut[x >> (32 - HNB)] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      pp[j] = k[j] >> KS;
+      rr[j][0] = ((k[j] & kmask) << (LG + 6)) | ((hv[j] >> 8) << 6) | ((hv[j] & 0xffu) << 1);
+    }
+    if constexpr (PVE_DBG != 1) put_round(B, pend, pp, rr, lane);
+    if (__builtin_amdgcn_ballot_w64(v0 + PB < e) == 0) break;
+  }
+}
+
 // one tile: returns the lane's docs counted in numDocsScanned. issue() sends the next tile's DMA: here, after the
 // admission loads have been waited for (PVE_ADMIT: a wait for them would otherwise also wait for that DMA)
 template <class Issue>
@@ -342,11 +454,37 @@ __device__ __forceinline__ u32 tile(const Bins& B, CS* sg, i64 wt, u32 img, int 
     if constexpr (PVE_ADMIT) issue();
     return 0;
   }
-  u32 key[ND], val[ND];
+  u32 key[ND], val[ND][RW];
 #pragma unroll
-  for (int i = 0; i < ND; ++i) key[i] = val[i] = 0u;
+  for (int i = 0; i < ND; ++i) {
+    key[i] = 0u;
+#pragma unroll
+    for (int k = 0; k < RW; ++k) val[i][k] = 0u;
+  }
   keys<0>(img, lane, key);
-  if constexpr (VC >= 0) unpack<(VC >= 0 ? VC : 0), false>(img, lane, val);
+  if constexpr (VC >= 0) {
+    u32 id[ND];
+    unpack<(VC >= 0 ? VC : 0), false>(img, lane, id);
+#pragma unroll
+    for (int i = 0; i < ND; ++i) val[i][0] = id[i];
+  }
+  if constexpr (RAWB > 0) {  // the lane's ND raw values: ND RAWB consecutive bytes of the staged tile
+    const __attribute__((address_space(3))) u32x4* r =
+        at<const __attribute__((address_space(3))) u32x4>(img + (u32)PVE_RAWOFF + (u32)lane * (u32)(ND * RAWB));
+    u32 w[ND * (RAWB > 0 ? RAWB : 4) / 4];
+#pragma unroll
+    for (int k = 0; k < ND * RAWB / 16; ++k) {
+      const u32x4 x = r[k];
+      w[4 * k] = x.x;
+      w[4 * k + 1] = x.y;
+      w[4 * k + 2] = x.z;
+      w[4 * k + 3] = x.w;
+    }
+#pragma unroll
+    for (int i = 0; i < ND; ++i)
+#pragma unroll
+      for (int k = 1; k < RW; ++k) val[i][k] = w[i * (RW - 1) + k - 1];
+  }
   const u32 scanned = (u32)__builtin_popcount(m);  // (numDocsScanned: every doc the filter kept, admitted or not)
   if constexpr (PVE_ADMIT) {
     const __attribute__((address_space(1))) u32* adm = (const __attribute__((address_space(1))) u32*)sg->admit;
@@ -363,11 +501,16 @@ __device__ __forceinline__ u32 tile(const Bins& B, CS* sg, i64 wt, u32 img, int 
   if constexpr (PVE_DBG == 1) {
     u32 x = 0;
 #pragma unroll
-    for (int i = 0; i < ND; ++i) x ^= key[i] + val[i];
+    for (int i = 0; i < ND; ++i) x ^= key[i] + val[i][RW - 1];
     if (x == 0x9e3779b9u) *at<l32>(B.next) = x;  // (keeps the records live)
     return scanned;
   }
-  put(B, m, key, val, lane);
+  if constexpr (PVE_H) {
+    put_values(B, sg, wt, m, key, lane);
+    return 0u;  // (numDocsScanned: counted by the V stream's launch)
+  } else {
+    put(B, m, key, val, lane);
+  }
   return scanned;
 }
 
@@ -460,7 +603,7 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
   for (int p = tid; p < P; p += W * 64) {
     const u32 n = at<l32>(B.cnt)[p];
     if (n == 0) continue;
-    for (u32 k = n; k < (u32)BS; ++k) at<l32>(B.bins)[(u32)p * (u32)BS + k] = kSentinel;
+    for (u32 k = n; k < (u32)BS; ++k) at<l32>(B.bins)[((u32)p * (u32)BS + k) * (u32)RW] = kSentinel;
     flush_one(B, (u32)p);
   }
   __syncthreads();

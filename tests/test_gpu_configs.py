@@ -246,24 +246,47 @@ def star():
         g.close()
 
 
-@pytest.mark.parametrize("variant", ["untrimmed", "default_limit"])
-def test_configs4_star_query(star, variant):
+@pytest.mark.parametrize("count_free", [True, False])
+@pytest.mark.parametrize("variant", ["untrimmed", "default_limit", "filtered"])
+def test_configs4_star_query(star, variant, count_free):
+    """configs[4] (raw DOUBLE SUM + DISTINCTCOUNTHLLMV over 262144 keys) on the partitioned path against the oracle: with
+    the count-free emit of both record streams where it applies (pve_jit.hip: V records of key offset + the raw value,
+    H records per MV value, each stream in whole chunks per workgroup read through chunk lists; the default
+    numGroupsLimit's admitted-key bitmaps checked per record) and with the count + emit passes."""
     segs, gs = star
     assert segs[0].column("tags").cardinality == 4096 and not segs[0].column("r").has_dictionary
-    opt = " OPTION(numGroupsLimit=1000000)" if variant == "untrimmed" else ""
-    q = parse_sql("SELECT d1, d2, d3, d4, COUNT(*), SUM(r), DISTINCTCOUNTHLLMV(tags) FROM t GROUP BY d1, d2, d3, d4 "
-                  "LIMIT 1000000" + opt)
-    ex = GpuQueryExecutor(q, gs)
+    opt = "" if variant == "default_limit" else " OPTION(numGroupsLimit=1000000)"
+    where = " WHERE d4 <> 5 AND d3 < 40" if variant == "filtered" else ""
+    q = parse_sql("SELECT d1, d2, d3, d4, COUNT(*), SUM(r), DISTINCTCOUNTHLLMV(tags) FROM t" + where +
+                  " GROUP BY d1, d2, d3, d4 LIMIT 1000000" + opt)
+    ex = GpuQueryExecutor(q, gs, flags=0 if count_free else L.PA_QF2_NO_COUNT_FREE)
     try:
         p = _plan(ex)
         assert ex.num_keys == 16 * 32 * 64 * 8
         assert p["strategy"] == "partitioned", p
-        assert p["limit_trimming"] == (0 if variant == "untrimmed" else 2), p
+        assert p["limit_trimming"] == (2 if variant == "default_limit" else 0), p
+        assert p["count_free_emit"] == (2 if count_free else 0), p
         ex.execute()
         n = _compare_arrays(ex, q, segs, rel=DOUBLE_REL)
     finally:
         ex.close()
     assert n > 250_000 if variant == "untrimmed" else n <= 200_000
+
+
+def test_configs4_hll_only_keeps_count_pass(star):
+    """DISTINCTCOUNTHLLMV without a V stream (COUNT from the H records' first-value flags) keeps the count + emit
+    passes."""
+    segs, gs = star
+    q = parse_sql("SELECT d1, d2, d3, d4, DISTINCTCOUNTHLLMV(tags) FROM t GROUP BY d1, d2, d3, d4 LIMIT 1000000 "
+                  "OPTION(numGroupsLimit=1000000)")
+    ex = GpuQueryExecutor(q, gs)
+    try:
+        p = _plan(ex)
+        assert p["strategy"] == "partitioned" and p["count_free_emit"] == 0, p
+        ex.execute()
+        _compare_arrays(ex, q, segs, rel=DOUBLE_REL)
+    finally:
+        ex.close()
 
 
 # ------------------------------------------------------------------ configs[3]
