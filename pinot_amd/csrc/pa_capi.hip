@@ -3217,16 +3217,21 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
     return b + (size_t)64 * nd * rawb;
   };
   auto lds_ring = [&](int bs) { return al16(al16((size_t)(5 * Pn + 1) * 4) + (size_t)Pn * bs * rw * 4); };
+  // H: a wave's buffer for one tile's MV value words (stage_values: at most max_values values per doc, whole 16-byte
+  // chunks from a 16-byte aligned start, one word of look-ahead)
+  auto val_bytes = [&](int nd) {
+    return hmode ? (size_t)16 * (((size_t)max_values * 64 * nd * hnb / 32 + 9 + 3) / 4) : (size_t)0;
+  };
   auto waves_for = [&](int nd, int bs) {
     for (int cand : {16, 12, 8, 4})
-      if (lds_ring(bs) + (size_t)cand * 2 * image_bytes(nd) <= kLdsBudget) return cand;
+      if (lds_ring(bs) + (size_t)cand * (2 * image_bytes(nd) + val_bytes(nd)) <= kLdsBudget) return cand;
     return 0;
   };
-  // H: 8 docs per lane (a lane's run of MV values is half as long: the value loads of a wave spread over fewer cache
-  // lines; measured 3.97 vs 4.8 ms on configs[4]); bins of 16 records when 32 cost resident waves (H only: the V
-  // stream's three-word records measured slower with 16-record bins and more waves, 1.70 vs 1.33 ms)
+  // H: 8 docs per lane (a lane's run of MV values is half as long: measured 3.97 vs 4.8 ms on configs[4]); 32-record
+  // bins (16-record bins for more resident waves measured slower on both streams: V 1.70 vs 1.33 ms at 12 vs 8 waves,
+  // H 4.37 vs 3.97 ms at 16 vs 12 waves), 16 only when 32 leave fewer than 4 waves
   int bs = 32;
-  if (hmode && waves_for(8, 32) < 16 && waves_for(8, 16) > waves_for(8, 32)) bs = 16;
+  if (waves_for(8, 32) < 4 && waves_for(8, 16) > waves_for(8, 32)) bs = 16;
   int nd = hmode ? 8 : (waves_for(8, bs) > waves_for(16, bs) ? 8 : 16);
   if (const char* e = std::getenv("PA_PVE_ND")) nd = std::atoi(e) == 8 ? 8 : 16;
   if (const char* e = std::getenv("PA_PVE_BS")) bs = std::atoi(e) == 16 ? 16 : 32;  // (measurement)
@@ -3245,7 +3250,9 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   const int td = 64 * nd;
   const size_t l_bins = al16((size_t)(5 * Pn + 1) * 4);
   const size_t l_ring = lds_ring(bs);
-  const size_t lds = l_ring + (size_t)w * 2 * img_bytes;
+  const size_t l_val = l_ring + (size_t)w * 2 * img_bytes;
+  const size_t vbytes = val_bytes(nd);
+  const size_t lds = l_val + (size_t)w * vbytes;
   // one workgroup per CU; a workgroup's region holds its docs' records (H: at most max_values per doc) in whole chunks
   // plus one partial chunk per partition; chunks of sc bins, more when the region would need 2^16 chunks
   std::vector<int64_t> first(q->nseg + 1, 0);  // the kernel's own tiles of td docs
@@ -3277,7 +3284,8 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
       "-DPVE_L_BINS=" + std::to_string(l_bins), "-DPVE_ADMIT=" + std::to_string(q->limit_walk ? 1 : 0),
       "-DPVE_L_RING=" + std::to_string(l_ring), "-DPVE_RW=" + std::to_string(rw),
       "-DPVE_RAWB=" + std::to_string(rawb), "-DPVE_RAWOFF=" + std::to_string(raw_off),
-      "-DPVE_H=" + std::to_string(hmode ? 1 : 0), "-DPVE_HNB=" + std::to_string(hnb), "-DPVE_LG=" + std::to_string(lg)};
+      "-DPVE_H=" + std::to_string(hmode ? 1 : 0), "-DPVE_HNB=" + std::to_string(hnb), "-DPVE_LG=" + std::to_string(lg),
+      "-DPVE_L_VAL=" + std::to_string(l_val), "-DPVE_VAL_B=" + std::to_string(vbytes)};
   if (const char* dbg = std::getenv("PA_PVE_DBG")) defs.push_back(std::string("-DPVE_DBG=") + dbg);  // (measurement)
   if (const char* pb = std::getenv("PA_PVE_PB")) defs.push_back(std::string("-DPVE_PB=") + pb);      // (measurement)
   hipFunction_t fn = jit_compile(defs, kPveJitSrc, "pve_jit");

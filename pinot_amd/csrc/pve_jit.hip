@@ -23,6 +23,8 @@
 //   PVE_VC the value column (-1: none)   PVE_KS key bits inside a partition   PVE_P partitions   PVE_BS bin records
 //   PVE_SC bins per chunk (a chunk is SC x BS consecutive records of one partition: pass C reads long runs)
 //   PVE_L_BINS, PVE_L_RING LDS byte offsets (state at 0: cnt[P], done[P], chunks[P], cur[P], fill[P], next)
+//   PVE_RW record words, PVE_RAWB / PVE_RAWOFF the staged raw value column, PVE_H the H stream (PVE_HNB, PVE_LG,
+//   PVE_L_VAL / PVE_VAL_B: per-wave LDS buffers of the tile's MV value words)
 typedef unsigned int u32;
 typedef unsigned long long u64;
 typedef long long i64;
@@ -67,6 +69,12 @@ constexpr u32 kSentinel = 0xffffffffu;
 #endif           // PVE_LG = log2m): key offset << (LG + 6) | register << 6 | rank << 1
 #ifndef PVE_HNB
 #define PVE_HNB 1
+#endif
+#ifndef PVE_L_VAL
+#define PVE_L_VAL 0  // H: LDS byte offset of the waves' value buffers, PVE_VAL_B bytes each
+#endif
+#ifndef PVE_VAL_B
+#define PVE_VAL_B 0
 #endif
 #ifndef PVE_LG
 #define PVE_LG 0
@@ -122,6 +130,14 @@ __device__ __forceinline__ void dma16m(u32 voff, u64 sbase, u32 dst, u64 mask) {
       "global_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
       : "=&s"(keep), "=&s"(save) : "v"(voff), "s"(sbase), "s"(dst), "s"(mask));
 }
+
+// wave DMA instructions of one tile image (dma_cols)
+constexpr int dma_instrs() {
+  int n = 0;
+  for (int c = 0; c < NC; ++c) n += (ND * kNB[c] / 2 + 63) / 64;
+  return n + TD * RAWB / 16 / 64;
+}
+constexpr int kDmaImg = dma_instrs();
 
 template <int C>
 __device__ __forceinline__ void dma_cols(CS* sg, i64 wt, u32 img, u32 voff) {
@@ -379,10 +395,33 @@ __device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], 
 // The H stream: one record per value of the lane's matching docs, PB values per round. The lane's values are one run
 // [o[first match], o[last match + 1]) of the MV stream; a value's doc is the last doc whose first value is not past it
 // (unrolled compares: no dynamically indexed registers); values of unmatched docs inside the run are skipped.
-__device__ __forceinline__ void put_values(const Bins& B, CS* sg, i64 wt, u32 m, const u32 (&key)[ND], int lane) {
+// H: the tile's MV value words [first value's word & ~3, last value's word + 2) into the wave's value buffer (LDS DMA,
+// whole 16-byte chunks: the stream has guard words on both sides); returns the first word staged
+__device__ __forceinline__ u32 stage_values(CS* sg, i64 wt, u32 vbuf, u32 voff) {
+  const int* off = (const int*)sg->mv_off;
+  const i64 d0 = wt * TD, nd = sg->num_docs;
+  const i64 d1 = d0 + TD < nd ? d0 + TD : nd;
+  const u32 S = (u32)__builtin_amdgcn_readfirstlane(off[d0]), E = (u32)__builtin_amdgcn_readfirstlane(off[d1]);
+  const u32 w0 = (u32)(((u64)S * (u64)HNB) >> 5) & ~3u;
+  const u32 w1 = (u32)(((u64)E * (u64)HNB) >> 5) + 2u;
+  const u32 n16 = (w1 - w0 + 3u) >> 2;
+  const u64 src = sg->mv_words + (u64)w0 * 4u;
+  for (u32 k = 0; 64u * k < n16; ++k) {
+    const u32 rem = n16 - 64u * k;
+    if (rem >= 64u) dma16(voff, src + 1024u * k, vbuf + 1024u * k);
+    else dma16m(voff, src + 1024u * k, vbuf + 1024u * k, (1ull << rem) - 1ull);
+  }
+  return w0;
+}
+
+__device__ __forceinline__ void put_values(const Bins& B, CS* sg, i64 wt, u32 m, const u32 (&key)[ND], int lane,
+                                           u32 vbuf, u32 vb0, bool nxt) {
   if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return;
+  // the value words have landed (the next tile's image DMA, issued after them, may still be in flight)
+  if (nxt) vm_wait<kDmaImg>();
+  else vm_wait<0>();
   const __attribute__((address_space(1))) int* off = (const __attribute__((address_space(1))) int*)sg->mv_off;
-  const __attribute__((address_space(1))) u32* words = (const __attribute__((address_space(1))) u32*)sg->mv_words;
+  const l32* words = at<const l32>(vbuf);
   const __attribute__((address_space(1))) u32* lut = (const __attribute__((address_space(1))) u32*)sg->hlut;
   const i64 d0 = wt * TD + (i64)ND * lane, nd = sg->num_docs;
   int o[ND + 1];
@@ -418,8 +457,9 @@ __device__ __forceinline__ void put_values(const Bins& B, CS* sg, i64 wt, u32 m,
       sh[j] = (u32)bit & 31u;
       wa[j] = wb[j] = 0u;
       if (pend[j]) {
-        wa[j] = words[bit >> 5];
-        wb[j] = words[(bit >> 5) + 1];
+        const u32 rel = (u32)(bit >> 5) - vb0;
+        wa[j] = words[rel];
+        wb[j] = words[rel + 1u];
       }
     }
     u32 hv[PB];
@@ -441,7 +481,8 @@ __device__ __forceinline__ void put_values(const Bins& B, CS* sg, i64 wt, u32 m,
 // one tile: returns the lane's docs counted in numDocsScanned. issue() sends the next tile's DMA: here, after the
 // admission loads have been waited for (PVE_ADMIT: a wait for them would otherwise also wait for that DMA)
 template <class Issue>
-__device__ __forceinline__ u32 tile(const Bins& B, CS* sg, i64 wt, u32 img, int lane, Issue&& issue) {
+__device__ __forceinline__ u32 tile(const Bins& B, CS* sg, i64 wt, u32 img, int lane, Issue&& issue, u32 vbuf, u32 vb0,
+                                    bool nxt) {
   constexpr u32 kAll = (1u << ND) - 1u;
   const i64 rem = (i64)sg->num_docs - wt * TD;
   u32 m = kAll;
@@ -506,7 +547,7 @@ __device__ __forceinline__ u32 tile(const Bins& B, CS* sg, i64 wt, u32 img, int 
     return scanned;
   }
   if constexpr (PVE_H) {
-    put_values(B, sg, wt, m, key, lane);
+    put_values(B, sg, wt, m, key, lane, vbuf, vb0, nxt);
     return 0u;  // (numDocsScanned: counted by the V stream's launch)
   } else {
     put(B, m, key, val, lane);
@@ -552,6 +593,7 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
   const i64 t0 = lb * T / G, t1 = (lb + 1) * T / G;
   const u32 ring = base + (u32)PVE_L_RING + (u32)wave * 2u * (u32)IMG * 4u;
   const u32 voff = 16u * (u32)lane;
+  const u32 vbuf = base + (u32)PVE_L_VAL + (u32)wave * (u32)PVE_VAL_B;  // H: the wave's MV value words
   u32 matched = 0;
   if (t0 < t1) {
     const int nseg = A->nseg;
@@ -583,13 +625,16 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
         }
         ti += W;
       };
-      if constexpr (!PVE_ADMIT) issue();
       while (t >= pend) {
         ++psi;
         pfirst = S[psi].first_tile;
         pend = pfirst + S[psi].num_tiles;
       }
-      matched += tile(B, S + psi, t - pfirst, ring + (u32)slot * (u32)IMG * 4u, lane, issue);
+      u32 vb0 = 0;
+      if constexpr (PVE_H) vb0 = stage_values(S + psi, t - pfirst, vbuf, voff);  // (before the next image's DMA)
+      const bool nxt = ti < t1;
+      if constexpr (!PVE_ADMIT) issue();
+      matched += tile(B, S + psi, t - pfirst, ring + (u32)slot * (u32)IMG * 4u, lane, issue, vbuf, vb0, nxt);
       slot ^= 1;
     }
   }
