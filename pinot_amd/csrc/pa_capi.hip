@@ -3265,6 +3265,7 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   auto chunks_for = [&](int c) { return (recs_per_wg + (int64_t)bs * c - 1) / ((int64_t)bs * c) + Pn; };
   while (sc < 16 && chunks_for(sc) >= (int64_t(1) << 16)) sc *= 2;
   const int64_t cr = (int64_t)bs * sc;  // records per chunk
+  if (cr < 64) return PA_OK;             // (pass C: a wave's 64 records of one slot lie in one chunk)
   const int64_t C = chunks_for(sc);
   if (C >= (int64_t(1) << 16) || (int64_t)G * C >= (int64_t(1) << 28)) return PA_OK;  // (table ranks, chunk ids)
   auto pad1 = [](std::vector<int> v) {

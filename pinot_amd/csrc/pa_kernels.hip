@@ -1411,19 +1411,22 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   constexpr int kB = 16;  // records per thread in flight
   const uint64_t span = (uint64_t)kB * kPartAggThreads;
   // chunked records (count-free emit): the chunk entries of a batch are loaded one batch ahead, so a record load never
-  // waits for its entry load (vector loads: a scalar load's wait would also wait for the LDS atomics in flight)
+  // waits for its entry load (vector loads: a scalar load's wait would also wait for the LDS atomics in flight). A
+  // wave's 64 records of one slot j lie in one chunk (chunks are >= 64 records, partition bases whole chunks), so
+  // lane j < kB loads slot j's entry — one load per batch, not one per record — and slot j reads it back uniform
   const AS1 uint32_t* cix = ps.chunk_index ? gp(ps.chunk_index) : nullptr;
   const int csh = (int)ps.chunk_shift;
   const uint64_t cmask = cix ? (1ull << csh) - 1ull : 0ull;
-  uint32_t cid[kB];
-  if (cix) {
-#pragma unroll
-    for (int j = 0; j < kB; ++j) {
-      const uint64_t ri = r0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
-      cid[j] = ri < r1 ? cix[ri >> csh] : 0u;
-    }
-  }
+  const uint32_t ln = threadIdx.x & 63u, wofs = threadIdx.x & ~63u;
+  auto load_cids = [&](uint64_t b) -> uint32_t {
+    const uint64_t ri = b + (uint64_t)ln * kPartAggThreads + wofs;
+    return (ln < (uint32_t)kB && ri < r1) ? cix[ri >> csh] : 0u;
+  };
+  uint32_t cidv = cix ? load_cids(r0) : 0u;
   for (uint64_t b0 = r0; b0 < r1; b0 += span) {
+    uint32_t cid[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) cid[j] = (uint32_t)__builtin_amdgcn_readlane((int)cidv, j);
     // every address first (the chunk entries were loaded a batch ago), then the loads back to back without a branch
     // per load (a branch per load makes each wait for the one before it); an absent record reads record 0 (always
     // allocated) and becomes a sentinel
@@ -1453,13 +1456,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
 #pragma unroll
     for (int j = 0; j < kB; ++j)
       if (!ok[j]) w0[j] = kSentinel;
-    if (cix) {
-#pragma unroll
-      for (int j = 0; j < kB; ++j) {
-        const uint64_t ri = b0 + span + (uint64_t)j * kPartAggThreads + threadIdx.x;
-        cid[j] = ri < r1 ? cix[ri >> csh] : 0u;
-      }
-    }
+    if (cix) cidv = load_cids(b0 + span);
     int64_t iv[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
@@ -1565,15 +1562,16 @@ __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps
   const AS1 uint32_t* cix = ps.chunk_index_h ? gp(ps.chunk_index_h) : nullptr;
   const int csh = (int)ps.chunk_shift_h;
   const uint64_t cmask = cix ? (1ull << csh) - 1ull : 0ull;
-  uint32_t cid[kB];
-  if (cix) {
-#pragma unroll
-    for (int j = 0; j < kB; ++j) {
-      const uint64_t ri = r0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
-      cid[j] = ri < r1 ? cix[ri >> csh] : 0u;
-    }
-  }
+  const uint32_t ln = threadIdx.x & 63u, wofs = threadIdx.x & ~63u;
+  auto load_cids = [&](uint64_t b) -> uint32_t {
+    const uint64_t ri = b + (uint64_t)ln * kPartAggThreads + wofs;
+    return (ln < (uint32_t)kB && ri < r1) ? cix[ri >> csh] : 0u;
+  };
+  uint32_t cidv = cix ? load_cids(r0) : 0u;
   for (uint64_t b0 = r0; b0 < r1; b0 += span) {
+    uint32_t cid[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) cid[j] = (uint32_t)__builtin_amdgcn_readlane((int)cidv, j);
     // (as part_agg_v_fast: every address, then the loads without a branch per load; an absent record reads record 0)
     uint32_t w[kB];
     uint64_t pa[kB];
@@ -1590,13 +1588,7 @@ __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps
 #pragma unroll
     for (int j = 0; j < kB; ++j)
       if (!ok[j]) w[j] = kSentinel;
-    if (cix) {
-#pragma unroll
-      for (int j = 0; j < kB; ++j) {
-        const uint64_t ri = b0 + span + (uint64_t)j * kPartAggThreads + threadIdx.x;
-        cid[j] = ri < r1 ? cix[ri >> csh] : 0u;
-      }
-    }
+    if (cix) cidv = load_cids(b0 + span);
     // Byte max by compare-and-swap, in phases over the kB records (each phase one run of independent LDS operations,
     // one wait): read every target word, try every needed swap once, then retry the few that lost a race.
     uint32_t rk[kB], sh[kB], old[kB];
