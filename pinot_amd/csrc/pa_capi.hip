@@ -3229,9 +3229,9 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   };
   // H: 8 docs per lane (a lane's run of MV values is half as long: measured 3.97 vs 4.8 ms on configs[4]); 32-record
   // bins (16-record bins for more resident waves measured slower on both streams: V 1.70 vs 1.33 ms at 12 vs 8 waves,
-  // H 4.37 vs 3.97 ms at 16 vs 12 waves), 16 only when 32 leave fewer than 4 waves
+  // H 4.37 vs 3.97 ms at 16 vs 12 waves), 16 only when 32 leave fewer than 8 waves
   int bs = 32;
-  if (waves_for(8, 32) < 4 && waves_for(8, 16) > waves_for(8, 32)) bs = 16;
+  if (waves_for(8, 32) < 8 && waves_for(8, 16) > waves_for(8, 32)) bs = 16;
   int nd = hmode ? 8 : (waves_for(8, bs) > waves_for(16, bs) ? 8 : 16);
   if (const char* e = std::getenv("PA_PVE_ND")) nd = std::atoi(e) == 8 ? 8 : 16;
   if (const char* e = std::getenv("PA_PVE_BS")) bs = std::atoi(e) == 16 ? 16 : 32;  // (measurement)

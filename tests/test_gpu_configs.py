@@ -342,3 +342,45 @@ def test_configs3_two_rank_merge_and_rccl_reduce(adanalytics):
     exp = oracle.run_query(q, [seg0, seg1])
     assert_same(got, exp)
     assert len(got.groups) == 101 and got.num_docs_scanned > 10_000
+
+
+def test_configs4_count_free_relocated_accumulators(star):
+    """configs[4] on the count-free emit with the accumulator block moved into a torch buffer (what the cross-GPU
+    reduce does, parallel.DistributedAccumulators under a world-size-1 RCCL group): both streams' kernels write through
+    the relocated numDocsScanned counter and pass C into the new block."""
+    import torch
+    import torch.distributed as dist
+    from pinot_amd.parallel import DistributedAccumulators
+    segs, gs = star
+    q = parse_sql("SELECT d1, d2, d3, d4, COUNT(*), SUM(r), DISTINCTCOUNTHLLMV(tags) FROM t WHERE d2 < 20 "
+                  "GROUP BY d1, d2, d3, d4 LIMIT 1000000 OPTION(numGroupsLimit=1000000)")
+    dist.init_process_group("nccl", rank=0, world_size=1, init_method="tcp://127.0.0.1:%d" % _port(),
+                            device_id=torch.device("cuda", 0))
+    ex = GpuQueryExecutor(q, gs)
+    try:
+        assert _plan(ex)["count_free_emit"] == 2
+        acc = DistributedAccumulators(ex, torch.device("cuda", 0))
+        ex.execute()
+        acc.reduce(dst=0)
+        torch.cuda.synchronize()
+        _compare_arrays(ex, q, segs, rel=DOUBLE_REL)
+    finally:
+        ex.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("agg", ["SUM(r)", "MIN(r), MAX(r)"])
+def test_configs4_raw_value_stream_count_free(star, agg):
+    """The V stream alone with a raw DOUBLE value (three-word records: key offset + the value's 64 bits, the raw column
+    staged by the count-free emit's DMA ring) against the oracle."""
+    segs, gs = star
+    q = parse_sql("SELECT d1, d2, d3, d4, COUNT(*), %s FROM t WHERE d3 >= 7 GROUP BY d1, d2, d3, d4 LIMIT 1000000 "
+                  "OPTION(numGroupsLimit=1000000)" % agg)
+    ex = GpuQueryExecutor(q, gs)
+    try:
+        p = _plan(ex)
+        assert p["strategy"] == "partitioned" and p["count_free_emit"] == 1, p
+        ex.execute()
+        _compare_arrays(ex, q, segs, rel=DOUBLE_REL)
+    finally:
+        ex.close()
