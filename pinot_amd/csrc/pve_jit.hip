@@ -55,6 +55,9 @@ constexpr u32 kSentinel = 0xffffffffu;
 #ifndef PVE_DBG
 #define PVE_DBG 0  // measurement only (PA_PVE_DBG): 1 = records built but not put, 2 = full bins not stored
 #endif
+#ifndef PVE_DONE_RTN
+#define PVE_DONE_RTN 0  // measurement (PA_PVE_DONE_RTN): the written count's returned value decides a bin is full
+#endif
 #ifndef PVE_RW
 #define PVE_RW 1  // words per record: 1 (key offset | value id), 2 (+ a raw 32-bit value), 3 (+ a raw 64-bit value)
 #endif
@@ -356,11 +359,35 @@ __device__ __forceinline__ void put_round(const Bins& B, bool (&pend)[PB], const
           for (int k = 0; k < RW; ++k) at<l32>(B.bins)[(pp[i] * (u32)BS + s[i]) * (u32)RW + (u32)k] = rr[i][k];
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       bool full[PB];
+#if PVE_DONE_RTN
 #pragma unroll
       for (int i = 0; i < PB; ++i)
         full[i] = s[i] < (u32)BS &&
                   __hip_atomic_fetch_add(at<l32>(B.done) + pp[i], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
                       (u32)BS - 1u;
+#else
+      // written counts without a returned value (no round trip per round): the lane that claimed a bin's last slot
+      // waits until every slot of the bin is written (LDS runs each wave's operations in order, so a writer's count
+      // follows its record), then flushes it
+#pragma unroll
+      for (int i = 0; i < PB; ++i)
+        if (s[i] < (u32)BS)
+          (void)__hip_atomic_fetch_add(at<l32>(B.done) + pp[i], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      bool anyfull = false;
+#pragma unroll
+      for (int i = 0; i < PB; ++i) {
+        full[i] = s[i] == (u32)BS - 1u;
+        anyfull |= full[i];
+      }
+      if (__builtin_amdgcn_ballot_w64(anyfull) != 0) {
+#pragma unroll
+        for (int i = 0; i < PB; ++i)
+          if (full[i])
+            while (__hip_atomic_load(at<l32>(B.done) + pp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) !=
+                   (u32)BS)
+              __builtin_amdgcn_s_sleep(1);
+      }
+#endif
       flush_full(B, full, pp, lane);
       bool any = false;
 #pragma unroll
