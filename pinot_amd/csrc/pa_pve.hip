@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(1024) pve_base_kernel(const uint32_t* __restri
   if (threadIdx.x == 0) base[P] = run * (uint64_t)cr;
 }
 
-__global__ void __launch_bounds__(256) pve_scatter_kernel(const uint32_t* __restrict__ table,
+__global__ void __launch_bounds__(1024) pve_scatter_kernel(const uint32_t* __restrict__ table,
                                                           const uint32_t* __restrict__ used,
                                                           const uint32_t* __restrict__ off,
                                                           const uint64_t* __restrict__ base, uint32_t* __restrict__ index,
@@ -80,7 +80,7 @@ hipError_t launch_pve_lists(const uint32_t* hist, uint32_t* off, uint64_t* base,
   pve_base_kernel<<<1, 1024, 0, s>>>(tot, base, P, cr);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  pve_scatter_kernel<<<G, 256, 0, s>>>(table, used, off, base, index, C, P, cr);
+  pve_scatter_kernel<<<G, 1024, 0, s>>>(table, used, off, base, index, C, P, cr);
   return hipGetLastError();
 }
 
