@@ -44,6 +44,37 @@ DAY_RANGE = (17532, 17915)
 SECONDARY = (("sel_10pct", 17476), ("sel_50pct", 87381))
 
 
+# Own-dictionary lines: the same columns where every segment built its own dictionaries (SegmentDictionaryCreator.java:104,
+# one per segment), as in a time-partitioned table: a 4-day slice of daysSinceEpoch (2 bits), a random half of the 2^17
+# accounts (16 bits), clicks a run of 1024 values and impressions 16384 values of step 3, each from a per-segment
+# offset. The day range covers every segment's slice; the IN list keeps a tenth / half of the docs.
+OWN_DAYS = 4
+OWN_SECONDARY = (("sel_10pct_own_dicts", 13107), ("sel_50pct_own_dicts", 65536))
+
+
+def make_segment_own(seed, docs, index):
+    from pinot_amd.segment import segment_from_dict_ids
+    rng = np.random.default_rng(seed)
+    accts = np.sort(rng.choice(COLUMNS["accountId"][2](), size=1 << 16, replace=False))
+    d0 = DAY_RANGE[0] + OWN_DAYS * index
+    dicts = {"daysSinceEpoch": ("INT", np.arange(d0, d0 + OWN_DAYS, dtype=np.int64)),
+             "accountId": ("INT", accts),
+             "clicks": ("LONG", np.arange(1024, dtype=np.int64) + (index * 37) % 500),
+             "impressions": ("LONG", (np.arange(1 << 14, dtype=np.int64) + (index * 101) % 2000) * 3)}
+    specs = {}
+    for name, (dt, d) in dicts.items():
+        nb = int(len(d) - 1).bit_length()  # (every cardinality a power of two: uniform dictIds = random bytes)
+        specs[name] = (dt, d, np.frombuffer(rng.bytes((docs * nb + 7) // 8), dtype=np.uint8))
+    return segment_from_dict_ids("AdAnalyticsOwn_%d" % seed, docs, specs)
+
+
+def secondary_query_own(n_ids, num_segments):
+    ids = np.sort(np.random.default_rng(4243).choice(COLUMNS["accountId"][2](), size=n_ids, replace=False))
+    return ("SELECT sum(clicks), sum(impressions) FROM AdAnalyticsTable WHERE daysSinceEpoch BETWEEN %d AND %d "
+            "AND accountId IN (%s) GROUP BY daysSinceEpoch TOP 1000" % (
+                DAY_RANGE[0], DAY_RANGE[0] + OWN_DAYS * num_segments - 1, ",".join(map(str, ids))))
+
+
 def secondary_query(n_ids):
     ids = np.sort(np.random.default_rng(4242).choice(COLUMNS["accountId"][2](), size=n_ids, replace=False))
     return ("SELECT sum(clicks), sum(impressions) FROM AdAnalyticsTable WHERE daysSinceEpoch BETWEEN %d AND %d "
@@ -147,6 +178,37 @@ def cpu_baseline(query, host_segments, min_wall_s=1.0):
                 passes, len(host_segments), host_segments[0].num_docs, cores, dt)}
 
 
+def oracle_check(q, gsegs, host_segments, sptr):
+    """A line's own result checked outside the timed region: the same query over the host sample's segments (the first
+    len(host_segments) of the rank's set, whose forward indexes the host kept) on the GPU, against the oracle's
+    server-level result of those segments (one oracle task per segment, merged by group key: COUNT and SUM add).
+    Bar as in tests/: bit-exact group keys, COUNT, numDocsScanned and LONG SUMs (all below 2^53 here)."""
+    import oracle
+    from concurrent.futures import ThreadPoolExecutor
+    from pinot_amd.engine import GpuQueryExecutor
+    assert all(a.function in ("COUNT", "SUM") for a in q.aggregations)
+    ex = GpuQueryExecutor(q, gsegs[:len(host_segments)])
+    try:
+        plan = ex.stats()["plan"]
+        got = ex.run(sptr)
+    finally:
+        ex.close()
+    with ThreadPoolExecutor(max(1, min(16, len(host_segments)))) as tp:
+        parts = list(tp.map(lambda s: oracle.run_query(q, [s]), host_segments))
+    groups, scanned = {}, 0
+    for r in parts:
+        scanned += r.num_docs_scanned
+        for k, v in r.groups.items():
+            groups[k] = [a + b for a, b in zip(groups[k], v)] if k in groups else list(v)
+    ok = got.num_docs_scanned == scanned and set(got.groups) == set(groups) and all(
+        list(got.groups[k]) == list(v) for k, v in groups.items())
+    if not ok:
+        log("oracle check FAILED: %d vs %d docs, %d vs %d groups" % (got.num_docs_scanned, scanned, len(got.groups),
+                                                                    len(groups)))
+    return {"checked": bool(ok), "check_segments": len(host_segments), "check_docs": scanned,
+            "check_groups": len(groups), "check_plan": plan["variant"], "check_dense_packed": plan["dense_packed"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,7 +219,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=16, help="segments in the CPU baseline sample (0 = skip)")
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--no-secondary", action="store_true", help="skip the widened-IN-list secondary lines")
-    ap.add_argument("--secondary", default="all", help="run only this secondary line (sel_10pct | sel_50pct)")
+    ap.add_argument("--secondary", default="all",
+                    help="run only this secondary line (sel_10pct | sel_50pct | sel_10pct_own_dicts | sel_50pct_own_dicts)")
     args = ap.parse_args()
 
     import torch
@@ -305,13 +368,33 @@ def main():
 
     # secondary lines: the same segments under the widened IN lists (kernel time, roofline on the same byte model)
     secondary = []
+    own = {}  # the own-dictionary segment set, built for its lines only
+
+    def own_segments():
+        if not own:
+            t = time.perf_counter()
+            own["g"], own["host"] = [], []
+            for i in mine:
+                seg = make_segment_own(5000 + i, args.docs, i)
+                own["g"].append(GpuSegment(seg, column_ids=cids, device=local))
+                if rank == 0 and len(own["host"]) < args.cpu_sample:
+                    own["host"].append(seg)
+                else:
+                    for c in seg.columns.values():
+                        c.fwd_bytes = None
+            own["kw"] = table_layout(q, [g.segment for g in own["g"]]).executor_kwargs() if distributed else {}
+            log("rank %d: own-dictionary segments resident, %.1f s" % (rank, time.perf_counter() - t))
+        return own["g"], own["host"], own["kw"]
+
     if not args.no_secondary:
         from pinot_amd import _lib as L
-        for name, n_ids in SECONDARY:
+        lines = [(n, k, False) for n, k in SECONDARY] + [(n, k, True) for n, k in OWN_SECONDARY]
+        for name, n_ids, own_dicts in lines:
             if args.secondary not in ("all", name):
                 continue
-            sql = secondary_query(n_ids)
-            e2 = GpuQueryExecutor(parse_sql(sql), gsegs, flags=args.flags, **kw)
+            sql = secondary_query_own(n_ids, args.segments * world) if own_dicts else secondary_query(n_ids)
+            lsegs, lhost, lkw = own_segments() if own_dicts else (gsegs, host_sample, kw)
+            e2 = GpuQueryExecutor(parse_sql(sql), lsegs, flags=args.flags, **lkw)
             for _ in range(args.warmup):
                 e2.execute(sptr)
             torch.cuda.synchronize()
@@ -323,14 +406,17 @@ def main():
             st2 = e2.stats()
             secondary.append({
                 "workload": "adanalytics_in_list_" + name, "matched_fraction": matched / st2["num_docs"],
-                "query": sql[:sql.index("IN (") + 4] + "... %d account ids) GROUP BY daysSinceEpoch TOP 100" % n_ids,
+                "query": sql[:sql.index("IN (") + 4] + "... %d account ids) GROUP BY daysSinceEpoch" % n_ids,
+                "own_dictionaries": own_dicts,
                 "kernel_ms": ms, "rows_per_s": st2["num_docs"] / (ms * 1e-3),
                 "groups": len(r2.groups) if r2 is not None else None,
                 "roofline": {"bound": "hbm", "achieved": algo / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": algo,
-                             "traffic": load_traffic("adanalytics_in_list_" + name, args.docs, len(gsegs)),
+                             "traffic": load_traffic("adanalytics_in_list_" + name, args.docs, len(lsegs)),
                              "plan": st2["plan"]}})
             e2.close()
+            if rank == 0 and lhost:
+                secondary[-1].update(oracle_check(parse_sql(sql), lsegs, lhost, sptr))
 
     st = ex.stats()
     rows_per_gpu = st["num_docs"]
@@ -390,7 +476,7 @@ def main():
             out["multi_gpu"] = multi
         print(json.dumps(out), flush=True)
     ex.close()
-    for g in gsegs:
+    for g in gsegs + own.get("g", []):
         g.close()
     if distributed:
         dist.destroy_process_group()

@@ -1,66 +1,69 @@
-// The lane-major dense filter + GROUP BY kernel specialised to one query shape (STRAT_GDENSE_LM8 with packed
-// accumulation), compiled at pa_query_prepare by hiprtc with the shape as macros (pa_capi.hip jit_*). Same algorithm
-// as pa_gdense.h gdl_tile + gdl_packed_accumulate + gdl_drain + gd_flush, with every column width, image offset,
-// leaf kind, field offset and loop bound a compile-time constant: no switch on bit widths, no parameter reads in the
-// tile loop, the DMA of a tile is straight-line scalar code. Self-contained (hiprtc's built-in HIP headers only).
+// The lane-major dense filter + GROUP BY kernel specialised to one query shape (packed accumulation), compiled at
+// pa_query_prepare by hiprtc with the shape as macros (pa_jit.hip jit_plan). Same algorithm as pa_gdense.h gdl_tile +
+// gdl_packed_accumulate + gdl_drain + gd_flush, with every column width, image offset, leaf kind, field offset and
+// loop bound a compile-time constant: no switch on bit widths, no parameter reads in the tile loop, the DMA of a tile
+// is straight-line scalar code. Self-contained (hiprtc's built-in HIP headers; pa_jit_abi.h is pasted in by build.py).
+//
+// Segments with their own dictionaries (every segment builds its own: SegmentDictionaryCreator.java:104, read through
+// DictionaryBasedGroupKeyGenerator.java:122) take the same kernel:
+//  * column widths per segment: each distinct width tuple is a class (JIT_NCLS <= 4), the tile body and its DMA are
+//    instantiated per class and a segment switch picks one (a scalar branch);
+//  * the group key: a segment whose dictionary is a contiguous run of the table dictionary (time partitions) shifts its
+//    box by an offset (JitSeg.key_lo); otherwise every segment reads a dictId -> table key table (JIT_KTAB);
+//  * DICT_SET bitmaps, value tables and key tables that differ per segment live in LDS table slots: a workgroup's tile
+//    range spans at most JIT_NSLOT segments, whose tables it loads when it starts; tables every segment shares sit in
+//    one shared area;
+//  * SUMs over per-segment arithmetic dictionaries with one common step add the segment's dictId offset (JitSeg.aoff);
+//  * a leaf negated in some segments only (an empty range becomes NOT(full range)) XORs the segment's bit (JIT_LN 2).
 //
 // Reference semantics: GroupByOperator -> DefaultGroupByExecutor.process (DefaultGroupByExecutor.java:131-158),
 // DictionaryBasedGroupKeyGenerator (one group-by column, :254-340), SumAggregationFunction.aggregateGroupBySV (:207)
 // and CountAggregationFunction, ScanBasedFilterOperator over dictId ranges / dictId sets (SVScanDocIdIterator.java:203).
 //
 // Shape macros (all integers; lists as {a, b, ...}):
-//   JIT_W  waves per workgroup         JIT_IMG  dwords of one tile image      JIT_NC  staged columns
-//   JIT_NB {bits per column}           JIT_OFF  {byte offset of each column's region in the image}
-//   JIT_NL eager leaves, JIT_LK {0 = DICT_RANGE, 1 = DICT_SET}, JIT_LC {column}, JIT_LN {negate},
-//          JIT_LE {closes a CNF clause}, JIT_LUT {LDS byte offset of the DICT_SET bitmap}
-//   JIT_KC the group-by column, JIT_KL the leaf whose unpack it reuses (-1: none), JIT_KIB the filter implies the box
-//   JIT_NA SUM aggregations, JIT_AC {column}, JIT_AT {LDS byte offset of a GVS_T32U table, -1: the dictId itself},
-//          JIT_AS {bit offset of the field}, JIT_OC bit offset of the COUNT field
+//   JIT_W waves per workgroup, JIT_ND docs per lane (a tile is 64 JIT_ND docs), JIT_IMG dwords of one tile image,
+//   JIT_NC staged columns, JIT_NCLS width classes, JIT_NB {{bits per column} per class},
+//   JIT_OFF {{byte offset of each column's region in the image} per class}
+//   JIT_NL eager leaves, JIT_LK {0 = DICT_RANGE, 1 = DICT_SET}, JIT_LC {column}, JIT_LN {0, 1 = negate, 2 = per segment},
+//          JIT_LE {closes a CNF clause}, JIT_LUT {LDS byte offset of the DICT_SET bitmap}, JIT_LUTS {1: in the slot}
+//   JIT_KC the group-by column, JIT_KL the leaf whose unpack it reuses (-1: none), JIT_KIB the filter implies the box,
+//          JIT_KTAB slot byte offset of the group-key table (-1: affine keys)
+//   JIT_NA SUM aggregations, JIT_AC {column}, JIT_AT {LDS byte offset of a value table, -1: the dictId itself},
+//          JIT_ATS {1: table in the slot}, JIT_AO {1: + the segment's dictId offset}, JIT_AS {bit offset of the field},
+//          JIT_OC bit offset of the COUNT field
 //   JIT_DRAIN tiles between drains of a wave's packed rows
-//   JIT_L_SUM {LDS byte offset of each SUM's accumulators}, JIT_L_ROWS, JIT_L_RING (LDS byte offsets)
+//   JIT_L_SUM {LDS byte offset of each SUM's accumulators}, JIT_L_SLOT / JIT_SLOT_B / JIT_NSLOT the table slots,
+//   JIT_L_ROWS, JIT_L_RING (LDS byte offsets)
 typedef unsigned int u32;
 typedef unsigned long long u64;
 typedef long long i64;
 typedef __attribute__((address_space(3))) u32 l32;
 typedef __attribute__((address_space(3))) u64 l64;
 
-constexpr int W = JIT_W, NC = JIT_NC, NL = JIT_NL, NA = JIT_NA, ND = 16, IMG = JIT_IMG;
+#include "pa_jit_abi.h"
+
+constexpr int W = JIT_W, NC = JIT_NC, NL = JIT_NL, NA = JIT_NA, ND = JIT_ND, IMG = JIT_IMG, NCLS = JIT_NCLS;
+constexpr int TD = 64 * ND;                // docs per tile (lane l: docs [ND l, ND l + ND))
+constexpr u32 FULL = (1u << ND) - 1u;      // the lane's match word of a whole tile
+static_assert(ND == 8 || ND == 16, "8 or 16 docs per lane");
+static_assert(NCLS >= 1 && NCLS <= 4, "1..4 width classes");
 constexpr int NLA = NL > 0 ? NL : 1, NAA = NA > 0 ? NA : 1;
-constexpr int kNB[NC] = JIT_NB;
-constexpr int kOFF[NC] = JIT_OFF;
+constexpr int kNB[NCLS][NC] = JIT_NB;
+constexpr int kOFF[NCLS][NC] = JIT_OFF;
 constexpr int kLK[NLA] = JIT_LK;
 constexpr int kLC[NLA] = JIT_LC;
 constexpr int kLN[NLA] = JIT_LN;
 constexpr int kLE[NLA] = JIT_LE;
 constexpr int kLUT[NLA] = JIT_LUT;
+constexpr int kLUTS[NLA] = JIT_LUTS;
 constexpr int kAC[NAA] = JIT_AC;
 constexpr int kAT[NAA] = JIT_AT;
+constexpr int kATS[NAA] = JIT_ATS;
+constexpr int kAO[NAA] = JIT_AO;
 constexpr int kAS[NAA] = JIT_AS;
 constexpr int kLSUM[NAA] = JIT_L_SUM;
-
-// (fixed-size arrays: the host (pa_capi.hip JitSegH / JitArgsH) writes the same layout for every shape)
-constexpr int kJitMax = 6;
 static_assert(NC <= kJitMax && NL <= kJitMax && NA <= kJitMax, "shape beyond the JIT descriptors");
-struct JitSeg {          // one bound segment (read with scalar loads at segment switches only)
-  u64 src[kJitMax];      // column streams, past the guard words
-  i64 first_tile;        // first 1024-doc tile in the query's tile space
-  int num_docs, num_tiles;
-  u32 lo_t[kJitMax], hi_t[kJitMax];  // DICT_RANGE leaves: MSB-aligned bounds in this segment's dictId space
-};
-struct JitArgs {
-  i64 total_tiles;
-  int nseg, nkeys, key_lo, key_span, xcd_major, pad;
-  i64 key_stride;                 // table-wide key of LDS key k: (k + key_lo) * key_stride
-  unsigned long long* matched;    // [0] numDocsScanned, [3] matches outside the key box (planner error)
-  unsigned long long* count;      // table-wide COUNT accumulators
-  i64* sum[kJitMax];              // table-wide SUM accumulators (int64, or lo/hi pairs: sum_long)
-  int sum_long[kJitMax];
-  i64 base[kJitMax], step[kJitMax];  // value = base + step * term
-  const u32* lut[kJitMax];        // shared DICT_SET bitmaps
-  int lut_words[kJitMax];
-  const i64* tab[kJitMax];        // GVS_T32U: the shared dictionary (values - base go to LDS)
-  int tab_n[kJitMax];
-};
+
 typedef const __attribute__((address_space(4))) JitArgs CA;
 typedef const __attribute__((address_space(4))) JitSeg CS;
 
@@ -86,40 +89,58 @@ __device__ __forceinline__ void dma16m(u32 voff, u64 sbase, u32 dst, u64 mask) {
       : "=&s"(keep), "=&s"(save) : "v"(voff), "s"(sbase), "s"(dst), "s"(mask));
 }
 
-template <int C>
+// tile wt of every column of class K: 8 ND nb bytes per column, as 16-byte chunks
+template <int K, int C>
 __device__ __forceinline__ void dma_cols(CS* sg, i64 wt, u32 img, u32 voff) {
   if constexpr (C < NC) {
-    constexpr int CH = 8 * kNB[C];  // 16-byte chunks of a 1024-doc tile
-    const u64 src = sg->src[C] + (u64)wt * (u64)(128 * kNB[C]);
-    const u32 dst = img + (u32)kOFF[C];
+    constexpr int NB = kNB[K][C];
+    constexpr int CH = ND * NB / 2;  // 16-byte chunks of a tile
+    const u64 src = sg->src[C] + (u64)wt * (u64)(8 * ND * NB);
+    const u32 dst = img + (u32)kOFF[K][C];
 #pragma unroll
     for (int k = 0; k < CH / 64; ++k) dma16(voff, src + 1024u * k, dst + 1024u * k);
     if constexpr (CH % 64) dma16m(voff, src + 1024u * (CH / 64), dst + 1024u * (CH / 64), (1ull << (CH % 64)) - 1ull);
-    dma_cols<C + 1>(sg, wt, img, voff);
+    dma_cols<K, C + 1>(sg, wt, img, voff);
+  }
+}
+template <int K>
+__device__ __forceinline__ void dma_tile(int cls, CS* sg, i64 wt, u32 img, u32 voff) {
+  if constexpr (K + 1 < NCLS) {
+    if (cls == K) dma_cols<K, 0>(sg, wt, img, voff);
+    else dma_tile<K + 1>(cls, sg, wt, img, voff);
+  } else {
+    dma_cols<K, 0>(sg, wt, img, voff);
   }
 }
 
-// The lane's 16 values of column C (MSB-aligned: value i in the top NB bits of v[i])
-template <int C>
-__device__ __forceinline__ void top(u32 img, int lane, u32 (&v)[ND]) {
-  constexpr int NB = kNB[C];
+// The lane's ND values of an NB-bit column from its region of the image, as whole 32-bit windows: w[j] holds the
+// stream bits [bit0 + 32 j, bit0 + 32 j + 32) (MSB first), bit0 = the lane's first bit
+template <int NB>
+__device__ __forceinline__ void lane_words(u32 region, int lane, u32 (&w)[(ND * NB + 31) / 32 + 1]) {
   constexpr int K = (ND * NB + 31) / 32 + 1;
-  const u32 region = img + (u32)kOFF[C];
   const u32 bit0 = (u32)lane * (u32)(ND * NB);
-  u32 w[K];
-  if constexpr ((ND * NB) % 32 != 0) {  // odd NB: odd lanes start 16 bits into a word
-    const u32 sh = bit0 & 16u;
-    const l32* p = at<const l32>(region + 4u * ((bit0 >> 5) - 1u + (sh >> 4)));
+  if constexpr ((ND * NB) % 32 != 0) {  // the lane starts inside a word: windows through alignbit
+    const u32 sh = bit0 & 31u;
+    const u32 lo_shift = (32u - sh) & 31u;  // sh 0: the word itself (alignbit by 0 of the next pair)
+    const l32* p = at<const l32>(region + 4u * ((bit0 >> 5) - 1u + (sh != 0u ? 1u : 0u)));
     u32 r[K + 1];
 #pragma unroll
     for (int j = 0; j <= K; ++j) r[j] = p[j];
 #pragma unroll
-    for (int j = 0; j < K; ++j) w[j] = __builtin_amdgcn_alignbit(r[j], r[j + 1], sh);
+    for (int j = 0; j < K; ++j) w[j] = __builtin_amdgcn_alignbit(r[j], r[j + 1], lo_shift);
   } else {
     const l32* p = at<const l32>(region + 4u * (bit0 >> 5));
 #pragma unroll
     for (int j = 0; j < K; ++j) w[j] = p[j];
   }
+}
+
+// The lane's ND values of column C (class K), MSB-aligned: value i in the top NB bits of v[i]
+template <int K, int C>
+__device__ __forceinline__ void top(u32 img, int lane, u32 (&v)[ND]) {
+  constexpr int NB = kNB[K][C];
+  u32 w[(ND * NB + 31) / 32 + 1];
+  lane_words<NB>(img + (u32)kOFF[K][C], lane, w);
 #pragma unroll
   for (int i = 0; i < ND; ++i) {
     const int s = i * NB, j = s >> 5, o = s & 31;
@@ -128,26 +149,11 @@ __device__ __forceinline__ void top(u32 img, int lane, u32 (&v)[ND]) {
 }
 
 // dictIds of column C (one v_bfe per id, two ops when it straddles words)
-template <int C>
+template <int K, int C>
 __device__ __forceinline__ void ids(u32 img, int lane, u32 (&v)[ND]) {
-  constexpr int NB = kNB[C];
-  constexpr int K = (ND * NB + 31) / 32 + 1;
-  const u32 region = img + (u32)kOFF[C];
-  const u32 bit0 = (u32)lane * (u32)(ND * NB);
-  u32 w[K];
-  if constexpr ((ND * NB) % 32 != 0) {
-    const u32 sh = bit0 & 16u;
-    const l32* p = at<const l32>(region + 4u * ((bit0 >> 5) - 1u + (sh >> 4)));
-    u32 r[K + 1];
-#pragma unroll
-    for (int j = 0; j <= K; ++j) r[j] = p[j];
-#pragma unroll
-    for (int j = 0; j < K; ++j) w[j] = __builtin_amdgcn_alignbit(r[j], r[j + 1], sh);
-  } else {
-    const l32* p = at<const l32>(region + 4u * (bit0 >> 5));
-#pragma unroll
-    for (int j = 0; j < K; ++j) w[j] = p[j];
-  }
+  constexpr int NB = kNB[K][C];
+  u32 w[(ND * NB + 31) / 32 + 1];
+  lane_words<NB>(img + (u32)kOFF[K][C], lane, w);
 #pragma unroll
   for (int i = 0; i < ND; ++i) {
     const int s = i * NB, j = s >> 5, o = s & 31;
@@ -156,7 +162,7 @@ __device__ __forceinline__ void ids(u32 img, int lane, u32 (&v)[ND]) {
   }
 }
 
-// MSB-aligned range test of 16 values: non-matches as borrow bits (lo <= v < lo + span <=> t - lo' <= hi')
+// MSB-aligned range test of ND values: non-matches as borrow bits (lo <= v < lo + span <=> t - lo' <= hi')
 __device__ __forceinline__ u32 range_nm(const u32 (&t)[ND], u32 lo_t, u32 hi_t) {
   u32 nm = 0;
 #pragma unroll
@@ -170,51 +176,60 @@ __device__ __forceinline__ u32 range_nm(const u32 (&t)[ND], u32 lo_t, u32 hi_t) 
 }
 
 // eager leaves L.. in order (CNF clauses closed by kLE); false when no doc of the wave's tile can match any more
-template <int L>
-__device__ __forceinline__ bool leaves(CS* sg, u32 img, int lane, u32 base, u32& m, u32& clause, u32 (&kt)[ND]) {
+template <int K, int L>
+__device__ __forceinline__ bool leaves(CS* sg, u32 img, int lane, u32 base, u32 tb, u32& m, u32& clause,
+                                       u32 (&kt)[ND]) {
   if constexpr (L < NL) {
     u32 t[ND];
-    top<kLC[L]>(img, lane, t);
+    top<K, kLC[L]>(img, lane, t);
     if constexpr (L == JIT_KL) {
 #pragma unroll
       for (int i = 0; i < ND; ++i) kt[i] = t[i];
     }
     u32 bits;
     if constexpr (kLK[L] == 0) {
-      bits = ~range_nm(t, sg->lo_t[L], sg->hi_t[L]) & 0xffffu;
+      bits = ~range_nm(t, sg->lo_t[L], sg->hi_t[L]) & FULL;
     } else {
-      constexpr int NB = kNB[kLC[L]];
+      constexpr int NB = kNB[K][kLC[L]];
+      const u32 lb = (kLUTS[L] ? tb : base) + (u32)kLUT[L];
       u32 id[ND], w[ND];
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
         id[i] = t[i] >> (32 - NB);
-        w[i] = *at<const l32>(base + (u32)kLUT[L] + 4u * (id[i] >> 5));
+        w[i] = *at<const l32>(lb + 4u * (id[i] >> 5));
       }
       bits = 0;
 #pragma unroll
       for (int i = 0; i < ND; ++i) bits |= __builtin_amdgcn_ubfe(w[i], id[i], 1) << i;
     }
-    if constexpr (kLN[L]) bits = ~bits & 0xffffu;
+    if constexpr (kLN[L] == 1) bits = ~bits & FULL;
+    if constexpr (kLN[L] == 2) bits ^= (0u - ((sg->neg >> L) & 1u)) & FULL;
     clause |= bits;
     if constexpr (kLE[L] != 0) {
       m &= clause;
       clause = 0;
       if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return false;
     }
-    return leaves<L + 1>(sg, img, lane, base, m, clause, kt);
+    return leaves<K, L + 1>(sg, img, lane, base, tb, m, clause, kt);
   }
   return true;
 }
 
 // packed words of the lane's docs: COUNT + the SUM terms, ORed into their fields 32 bits at a time
-template <int A>
-__device__ __forceinline__ void terms(u32 img, int lane, u32 base, u32 (&plo)[ND], u32 (&phi)[ND]) {
+template <int K, int A>
+__device__ __forceinline__ void terms(CS* sg, u32 img, int lane, u32 base, u32 tb, u32 (&plo)[ND], u32 (&phi)[ND]) {
   if constexpr (A < NA) {
     u32 id[ND];
-    ids<kAC[A]>(img, lane, id);
+    ids<K, kAC[A]>(img, lane, id);
     if constexpr (kAT[A] >= 0) {
+      const u32 ab = (kATS[A] ? tb : base) + (u32)kAT[A];
 #pragma unroll
-      for (int i = 0; i < ND; ++i) id[i] = *at<const l32>(base + (u32)kAT[A] + 4u * id[i]);
+      for (int i = 0; i < ND; ++i) id[i] = *at<const l32>(ab + 4u * id[i]);
+    }
+    if constexpr (kAO[A]) {
+      const u32 ao = (u32)sg->aoff[A];
+#pragma unroll
+      for (int i = 0; i < ND; ++i) id[i] += ao;
     }
     constexpr int SH = kAS[A];
 #pragma unroll
@@ -228,30 +243,36 @@ __device__ __forceinline__ void terms(u32 img, int lane, u32 base, u32 (&plo)[ND
         phi[i] |= id[i] >> (32 - SH);
       }
     }
-    terms<A + 1>(img, lane, base, plo, phi);
+    terms<K, A + 1>(sg, img, lane, base, tb, plo, phi);
   }
 }
 
-// one 1024-doc tile: returns the lane's docs counted in numDocsScanned
-__device__ __forceinline__ u32 tile(CA* A, CS* sg, i64 wt, u32 img, int lane, u32 base, u32 rows, u32& errs) {
-  const i64 rem = (i64)sg->num_docs - wt * 1024;
-  u32 m = 0xffffu;
-  if (rem < 1024) {
+// one tile of class K: returns the lane's docs counted in numDocsScanned
+template <int K>
+__device__ __forceinline__ u32 tile(CS* sg, i64 wt, u32 img, int lane, u32 base, u32 tb, u32 rows, u32 span_m1,
+                                    u32& errs) {
+  const i64 rem = (i64)sg->num_docs - wt * TD;
+  u32 m = FULL;
+  if (rem < TD) {
     const i64 n = rem - ND * lane;
-    m = n >= ND ? 0xffffu : (n <= 0 ? 0u : ((1u << n) - 1u));
+    m = n >= ND ? FULL : (n <= 0 ? 0u : ((1u << n) - 1u));
   }
   u32 clause = 0, kt[ND];
-  if (!leaves<0>(sg, img, lane, base, m, clause, kt)) return 0;
+  if (!leaves<K, 0>(sg, img, lane, base, tb, m, clause, kt)) return 0;
   if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return 0;
-  constexpr int NBK = kNB[JIT_KC];
+  constexpr int NBK = kNB[K][JIT_KC];
   u32 id[ND];
   if constexpr (JIT_KL >= 0) {
 #pragma unroll
     for (int i = 0; i < ND; ++i) id[i] = kt[i] >> (32 - NBK);
   } else {
-    ids<JIT_KC>(img, lane, id);
+    ids<K, JIT_KC>(img, lane, id);
   }
-  const u32 klo = (u32)A->key_lo;
+  if constexpr (JIT_KTAB >= 0) {  // dictId -> table key id
+#pragma unroll
+    for (int i = 0; i < ND; ++i) id[i] = *at<const l32>(tb + (u32)JIT_KTAB + 4u * id[i]);
+  }
+  const u32 klo = (u32)sg->key_lo;
   u32 on = m;
   if constexpr (!JIT_KIB) {
     u32 nm = 0;
@@ -260,7 +281,7 @@ __device__ __forceinline__ u32 tile(CA* A, CS* sg, i64 wt, u32 img, int lane, u3
       u32 u;
       asm("v_sub_u32_e64 %[u], %[t], %[lo]\n\tv_sub_co_u32_e32 %[u], vcc, %[hi], %[u]\n\t"
           "v_addc_co_u32_e32 %[nm], vcc, %[nm], %[nm], vcc"
-          : [nm] "+v"(nm), [u] "=&v"(u) : [t] "v"(id[i]), [lo] "s"(klo), [hi] "s"((u32)A->key_span - 1u) : "vcc");
+          : [nm] "+v"(nm), [u] "=&v"(u) : [t] "v"(id[i]), [lo] "s"(klo), [hi] "s"(span_m1) : "vcc");
     }
     on &= ~nm;
     errs += (u32)__builtin_popcount(m & ~on);
@@ -272,13 +293,23 @@ __device__ __forceinline__ u32 tile(CA* A, CS* sg, i64 wt, u32 img, int lane, u3
     plo[i] = JIT_OC < 32 ? (1u << (JIT_OC & 31)) : 0u;
     phi[i] = JIT_OC < 32 ? 0u : (1u << ((JIT_OC - 32) & 31));
   }
-  terms<0>(img, lane, base, plo, phi);
+  terms<K, 0>(sg, img, lane, base, tb, plo, phi);
 #pragma unroll
   for (int i = 0; i < ND; ++i)
     if ((on >> i) & 1u)
       __hip_atomic_fetch_add(at<l64>(abase + (id[i] << 3)), ((u64)phi[i] << 32) | plo[i], __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
   return (u32)__builtin_popcount(m);
+}
+template <int K>
+__device__ __forceinline__ u32 tile_any(int cls, CS* sg, i64 wt, u32 img, int lane, u32 base, u32 tb, u32 rows,
+                                        u32 span_m1, u32& errs) {
+  if constexpr (K + 1 < NCLS) {
+    if (cls == K) return tile<K>(sg, wt, img, lane, base, tb, rows, span_m1, errs);
+    return tile_any<K + 1>(cls, sg, wt, img, lane, base, tb, rows, span_m1, errs);
+  } else {
+    return tile<K>(sg, wt, img, lane, base, tb, rows, span_m1, errs);
+  }
 }
 
 // a wave's packed rows -> the workgroup's COUNT / SUM accumulators (row zeroed)
@@ -308,6 +339,24 @@ __device__ __forceinline__ int find_segment(CS* segs, int nseg, i64 t) {
   return lo;
 }
 
+// one segment's tables into an LDS area (slot = its per-segment tables, else the shared ones)
+__device__ __forceinline__ void load_tables(CA* A, CS* sg, u32 dst, bool slot, int tid) {
+  typedef const __attribute__((address_space(1))) u32 g32;
+  typedef const __attribute__((address_space(1))) i64 g64;
+#pragma unroll
+  for (int l = 0; l < NL; ++l)
+    if (kLK[l] == 1 && (kLUTS[l] != 0) == slot)
+      for (int i = tid; i < sg->lut_words[l]; i += W * 64) at<l32>(dst + (u32)kLUT[l])[i] = ((g32*)sg->lut[l])[i];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+    if (kAT[a] >= 0 && (kATS[a] != 0) == slot)
+      for (int i = tid; i < sg->tab_n[a]; i += W * 64)
+        at<l32>(dst + (u32)kAT[a])[i] = (u32)(((g64*)sg->tab[a])[i] - A->base[a]);
+  if (JIT_KTAB >= 0 && slot)
+    for (int i = tid; i < sg->ktab_n; i += W * 64)
+      at<l32>(dst + (u32)(JIT_KTAB >= 0 ? JIT_KTAB : 0))[i] = ((g32*)sg->ktab)[i];
+}
+
 extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a_in, const JitSeg* s_in) {
   CA* A = (CA*)(unsigned long)a_in;
   CS* S = (CS*)(unsigned long)s_in;
@@ -316,46 +365,48 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nkeys = A->nkeys;
-  // LDS: counts, sums, bitmaps, tables, the waves' packed rows, the ring
+  // LDS: counts, sums, shared tables, table slots, the waves' packed rows, the ring
   for (int i = tid; i < nkeys; i += W * 64) smem[i] = 0u;
 #pragma unroll
   for (int a = 0; a < NA; ++a)
     for (int i = tid; i < nkeys; i += W * 64) at<l64>(base + (u32)kLSUM[a])[i] = 0ull;
   for (int i = tid; i < W * nkeys; i += W * 64) at<l64>(base + (u32)JIT_L_ROWS)[i] = 0ull;
-#pragma unroll
-  for (int l = 0; l < NL; ++l)
-    if (kLK[l] == 1)
-      for (int i = tid; i < A->lut_words[l]; i += W * 64)
-        at<l32>(base + (u32)kLUT[l])[i] = ((const __attribute__((address_space(1))) u32*)A->lut[l])[i];
-#pragma unroll
-  for (int a = 0; a < NA; ++a)
-    if (kAT[a] >= 0)
-      for (int i = tid; i < A->tab_n[a]; i += W * 64)
-        at<l32>(base + (u32)kAT[a])[i] =
-            (u32)(((const __attribute__((address_space(1))) i64*)A->tab[a])[i] - A->base[a]);
-  __syncthreads();
   const i64 T = A->total_tiles, G = gridDim.x;
   const i64 b = blockIdx.x;
   const i64 lb = A->xcd_major ? (b % 8) * (G / 8) + (b % 8 < G % 8 ? b % 8 : G % 8) + b / 8 : b;
   const i64 t0 = lb * T / G, t1 = (lb + 1) * T / G;
+  const int nseg = A->nseg;
+  // the segments this workgroup's tiles cover: their tables into the slots (the planner sized JIT_NSLOT for them)
+  const int s_first = t0 < t1 ? find_segment(S, nseg, t0) : 0;
+  load_tables(A, S + s_first, base, false, tid);
+#pragma unroll
+  for (int k = 0; k < JIT_NSLOT; ++k) {
+    const int si = s_first + k;
+    if (t0 < t1 && si < nseg && S[si].first_tile < t1)
+      load_tables(A, S + si, base + (u32)JIT_L_SLOT + (u32)(k * JIT_SLOT_B), true, tid);
+  }
+  __syncthreads();
   const u32 rows = base + (u32)JIT_L_ROWS + (u32)wave * (u32)nkeys * 8u;
   const u32 ring = base + (u32)JIT_L_RING + (u32)wave * 2u * (u32)IMG * 4u;
   const u32 voff = 16u * (u32)lane;
+  const u32 span_m1 = (u32)A->key_span - 1u;
   u32 matched = 0, errs = 0;
   if (t0 < t1) {
-    const int nseg = A->nseg;
     int isi = find_segment(S, nseg, t0 + wave);
     int psi = isi;
     i64 ifirst = S[isi].first_tile, iend = ifirst + S[isi].num_tiles;
     i64 pfirst = ifirst, pend = iend;
+    int icls = S[isi].cls, pcls = icls;
+    u32 tb = base + (u32)JIT_L_SLOT + (u32)((psi - s_first) * JIT_SLOT_B);
     i64 ti = t0 + wave;
     if (ti < t1) {
       while (ti >= iend) {
         ++isi;
         ifirst = S[isi].first_tile;
         iend = ifirst + S[isi].num_tiles;
+        icls = S[isi].cls;
       }
-      dma_cols<0>(S + isi, ti - ifirst, ring, voff);
+      dma_tile<0>(icls, S + isi, ti - ifirst, ring, voff);
     }
     ti += W;
     int slot = 0, since = 0;
@@ -366,16 +417,20 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
           ++isi;
           ifirst = S[isi].first_tile;
           iend = ifirst + S[isi].num_tiles;
+          icls = S[isi].cls;
         }
-        dma_cols<0>(S + isi, ti - ifirst, ring + (u32)(slot ^ 1) * (u32)IMG * 4u, voff);
+        dma_tile<0>(icls, S + isi, ti - ifirst, ring + (u32)(slot ^ 1) * (u32)IMG * 4u, voff);
       }
       ti += W;
       while (t >= pend) {
         ++psi;
         pfirst = S[psi].first_tile;
         pend = pfirst + S[psi].num_tiles;
+        pcls = S[psi].cls;
+        tb = base + (u32)JIT_L_SLOT + (u32)((psi - s_first) * JIT_SLOT_B);
       }
-      matched += tile(A, S + psi, t - pfirst, ring + (u32)slot * (u32)IMG * 4u, lane, base, rows, errs);
+      matched += tile_any<0>(pcls, S + psi, t - pfirst, ring + (u32)slot * (u32)IMG * 4u, lane, base, tb, rows,
+                             span_m1, errs);
       if (++since == JIT_DRAIN) {
         drain(rows, nkeys, lane, base);
         since = 0;

@@ -30,6 +30,8 @@ typedef unsigned long long u64;
 typedef long long i64;
 typedef __attribute__((address_space(3))) u32 l32;
 
+#include "pa_jit_abi.h"  // PveSeg, PveArgs (one definition with the host)
+
 #ifndef PVE_ND
 #define PVE_ND 16
 #endif
@@ -86,30 +88,8 @@ constexpr int RW = PVE_RW, RAWB = PVE_RAWB, HNB = PVE_HNB, LG = PVE_LG;
 static_assert(RW >= 1 && RW <= 3 && (RAWB == 0 || RAWB == 4 * (RW - 1)), "record words and the raw column agree");
 static_assert(!PVE_H || (RW == 1 && PVE_VC < 0 && RAWB == 0), "the H stream has one-word records");
 
-constexpr int kJitMax = 6;
-static_assert(NC <= kJitMax && NL <= kJitMax && NG <= 4, "shape beyond the JIT descriptors");
+static_assert(NC <= kJitMax && NL <= kJitMax && NG <= kJitMaxGb, "shape beyond the JIT descriptors");
 static_assert(BS % 4 == 0, "bins are whole 16-byte units");
-struct PveSeg {          // one bound segment (scalar loads at segment switches only)
-  u64 src[kJitMax];      // column streams, past the guard words
-  i64 first_tile;        // first TD-doc tile in the query's tile space
-  int num_docs, num_tiles;
-  u32 lo_t[kJitMax], hi_t[kJitMax];  // DICT_RANGE leaves: MSB-aligned bounds in this segment's dictId space
-  u64 admit;             // PVE_ADMIT: the segment's admitted-key bitmap (limit_walk_kernel; 0 = every key)
-  u64 raw;               // PVE_RAWB: the raw value column (padded to whole 2048-doc tiles)
-  u64 mv_off;            // PVE_H: int32 value offset of every doc [num_docs + 1]
-  u64 mv_words;          // PVE_H: the MV column's value stream (byte-swapped words, past the guard words)
-  u64 hlut;              // PVE_H: dictId -> register << 8 | rank
-};
-struct PveArgs {
-  i64 total_tiles;
-  int nseg, xcd_major;
-  i64 chunks_per_wg;             // C: chunk slots of a workgroup's region
-  u32* recs;                     // record stream: workgroup g's chunks at [g C SC BS, (g + 1) C SC BS)
-  u32* table;                    // [G][C]: partition | (bins - 1) << 12 | rank << 16 of every chunk
-  u32* hist;                     // [G][P]: chunks per (workgroup, partition)
-  u32* used;                     // [G]: chunks a workgroup filled
-  unsigned long long* matched;   // [0] numDocsScanned, [3] region overflow (must stay 0)
-};
 typedef const __attribute__((address_space(4))) PveArgs CA;
 typedef const __attribute__((address_space(4))) PveSeg CS;
 

@@ -148,8 +148,10 @@ def test_configs1_wide_in_list(adanalytics):
 
 @pytest.fixture(scope="module")
 def adanalytics3():
-    """Three bench.py segments (2M docs each) sharing their dictionaries, as the bench's 100 segments do."""
-    segs = [BENCH.make_segment(2000 + i, 2_000_000) for i in range(3)]
+    """Three bench.py segments of the bench's own size (10M docs each) sharing their dictionaries, as the bench's 100
+    segments do: 29,298 1024-doc tiles, so every wave of the packed-row kernel runs past JIT_DRAIN tiles and its
+    mid-loop drain fires, as it does at the bench's 1B docs."""
+    segs = [BENCH.make_segment(2000 + i, 10_000_000) for i in range(3)]
     gs = [GpuSegment(s) for s in segs]
     yield segs, gs
     for g in gs:
@@ -160,22 +162,58 @@ def adanalytics3():
 BENCH_SECONDARY_VARIANT = "gdense_lm8"  # (dense_packed 2: the query-shape specialised kernel)
 
 
+@pytest.mark.parametrize("drain", [0, L.PA_QF_GD_DRAIN_EACH_TILE])
 @pytest.mark.parametrize("n_ids,frac", [(17476, 0.1), (87381, 0.5)])
-def test_configs1_secondary_lines(adanalytics3, n_ids, frac):
+def test_configs1_secondary_lines(adanalytics3, n_ids, frac, drain):
     """bench.py's secondary lines at their plan: the accountId IN list widened to 10 % / 50 % of the docs (a 2^17-bit
-    bitmap held in LDS), the 384-day key box, two dictionary SUMs over segments that share dictionaries."""
+    bitmap held in LDS), the 384-day key box, two dictionary SUMs over segments that share dictionaries, on the
+    query-shape specialised kernel (dense_packed 2: gdl_jit.hip) at the bench's own drain period and with a drain after
+    every tile."""
     segs, gs = adanalytics3
     q = parse_sql(BENCH.secondary_query(n_ids))
-    ex = GpuQueryExecutor(q, gs)
+    ex = GpuQueryExecutor(q, gs, flags=drain)
     try:
         p = _plan(ex)
         assert p["strategy"] == "lds_dense" and p["variant"] == BENCH_SECONDARY_VARIANT, p
+        assert p["dense_packed"] == 2, p  # the JIT compiled and loaded (not the generic packed kernel)
         got = ex.run()
     finally:
         ex.close()
     exp = oracle.run_query(q, segs)
     assert_same(got, exp)
     assert len(got.groups) == 384
+    assert got.num_docs_scanned / sum(s.num_docs for s in segs) == pytest.approx(frac, abs=0.01)
+
+
+@pytest.fixture(scope="module")
+def adanalytics_own():
+    """Three of bench.py's own-dictionary segments (4M docs each): 4-day time partitions, a random half of the accounts,
+    per-segment clicks / impressions value runs."""
+    segs = [BENCH.make_segment_own(6000 + i, 4_000_000, i) for i in range(3)]
+    gs = [GpuSegment(s) for s in segs]
+    yield segs, gs
+    for g in gs:
+        g.close()
+
+
+@pytest.mark.parametrize("drain", [0, L.PA_QF_GD_DRAIN_EACH_TILE])
+@pytest.mark.parametrize("n_ids,frac", [(13107, 0.1), (65536, 0.5)])
+def test_configs1_own_dictionary_lines(adanalytics_own, n_ids, frac, drain):
+    """bench.py's own-dictionary secondary lines at their plan: every segment's own dictionaries (per-segment accountId
+    IN bitmaps in LDS table slots, day keys shifted per partition, SUM terms offset per segment) on the query-shape
+    specialised kernel, at the packed rows' own drain period and drained after every tile."""
+    segs, gs = adanalytics_own
+    q = parse_sql(BENCH.secondary_query_own(n_ids, len(segs)))
+    ex = GpuQueryExecutor(q, gs, flags=drain)
+    try:
+        p = _plan(ex)
+        assert p["strategy"] == "lds_dense" and p["dense_packed"] == 2, p
+        got = ex.run()
+    finally:
+        ex.close()
+    exp = oracle.run_query(q, segs)
+    assert_same(got, exp)
+    assert len(got.groups) == BENCH.OWN_DAYS * len(segs)
     assert got.num_docs_scanned / sum(s.num_docs for s in segs) == pytest.approx(frac, abs=0.01)
 
 
