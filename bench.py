@@ -283,7 +283,7 @@ def main():
     def step():
         ex.execute(sptr)
         if dacc is not None:
-            dacc.reduce(dst=0)
+            dacc.reduce(dst=0, execution_stats=False)
         if rank == 0:
             return ex.fetch(sptr, execution_stats=False)
         return None
@@ -294,7 +294,7 @@ def main():
         ex.execute(sptr)
         in_filter, _ = ex.execution_stats(sptr, docs_total=0)
         if dacc is not None:
-            dacc.reduce(dst=0)
+            dacc.reduce(dst=0, execution_stats=False)
         if rank == 0:
             r = ex.fetch(sptr, execution_stats=False)
             r.num_entries_scanned_in_filter = in_filter
@@ -327,7 +327,7 @@ def main():
         ma, mb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ma.record(stream)
         for _ in range(args.steps):
-            dacc.reduce(dst=0)
+            dacc.reduce(dst=0, execution_stats=False)
         mb.record(stream)
         torch.cuda.synchronize()
         merge_ms = ma.elapsed_time(mb) / args.steps

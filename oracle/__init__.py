@@ -548,16 +548,34 @@ def run_query_arrays(query, segments):
     per-group Python objects of run_query cost more than the scan). Every segment must share one dictionary per
     group-by column, so the oracle's raw key (column 0 least significant) IS the GPU's table-wide key. Returns a dict:
     keys (ascending int64), counts (int64), accs (one array per oracle accumulator, in `oaggs` order: float64[n], or
-    uint8[n, 2^log2m] HLL registers), oaggs, amap, matched (numDocsScanned) and limit_reached."""
+    uint8[n, 2^log2m] HLL registers), oaggs, amap, matched (numDocsScanned) and limit_reached. Segments with their own
+    dictionaries: each segment's raw key is decomposed over its own cardinalities and recomposed over the table-wide
+    dictionaries (the sorted union of the segments' values, as the GPU's key space is), so keys are table-wide keys."""
     for c in query.group_by:
-        d0 = segments[0].column(c).dictionary
-        if not all(s.column(c).dictionary is d0 or np.array_equal(s.column(c).dictionary, d0) for s in segments):
-            raise ValueError("run_query_arrays: segments must share the dictionary of group-by column %s" % c)
+        if not all(s.column(c).has_dictionary for s in segments):
+            raise ValueError("run_query_arrays: group-by column %s needs a dictionary in every segment" % c)
+    tables = []
+    for c in query.group_by:
+        ds = [s.column(c).dictionary for s in segments]
+        same = all(d is ds[0] or (len(d) == len(ds[0]) and np.array_equal(d, ds[0])) for d in ds)
+        tables.append(ds[0] if same else np.unique(np.concatenate(ds)))
     raws = [_run_segment_raw(query, s) for s in segments]
     oaggs, amap = raws[0].oaggs, raws[0].amap
     if any(k[0] == "DISTINCTCOUNT" for k in oaggs):
         raise ValueError("run_query_arrays: DISTINCTCOUNT is compared through run_query")
-    seg_keys = [r.keys[:r.n] if query.group_by else np.zeros(r.n, np.int64) for r in raws]
+
+    def table_keys(r, seg):
+        raw = r.keys[:r.n].astype(np.int64)
+        out = np.zeros(r.n, np.int64)
+        stride = 1
+        for c, gd in zip(query.group_by, tables):
+            d = seg.column(c).dictionary
+            comp = raw % len(d)
+            raw = raw // len(d)
+            out += (comp if d is gd else np.searchsorted(gd, d)[comp]) * stride
+            stride *= len(gd)
+        return out
+    seg_keys = [table_keys(r, s) if query.group_by else np.zeros(r.n, np.int64) for r, s in zip(raws, segments)]
     uniq = np.unique(np.concatenate(seg_keys)) if seg_keys else np.zeros(0, np.int64)
     if not query.group_by:
         uniq = np.zeros(1, np.int64)

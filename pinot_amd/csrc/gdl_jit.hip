@@ -31,7 +31,7 @@
 //   JIT_NA SUM aggregations, JIT_AC {column}, JIT_AT {LDS byte offset of a value table, -1: the dictId itself},
 //          JIT_ATS {1: table in the slot}, JIT_AO {1: + the segment's dictId offset}, JIT_AS {bit offset of the field},
 //          JIT_OC bit offset of the COUNT field
-//   JIT_DRAIN tiles between drains of a wave's packed rows
+//   JIT_DRAIN tiles between drains of a wave's packed rows, JIT_RS waves sharing one set of rows
 //   JIT_L_SUM {LDS byte offset of each SUM's accumulators}, JIT_L_SLOT / JIT_SLOT_B / JIT_NSLOT the table slots,
 //   JIT_L_ROWS, JIT_L_RING (LDS byte offsets)
 typedef unsigned int u32;
@@ -42,7 +42,14 @@ typedef __attribute__((address_space(3))) u64 l64;
 
 #include "pa_jit_abi.h"
 
+#ifndef JIT_RS
+#define JIT_RS 1  // waves sharing one set of packed rows (2: half the rows' LDS, drained by atomic exchange)
+#endif
+#ifndef JIT_DBG
+#define JIT_DBG 0  // measurement only (PA_GDL_DBG; results invalid): 1 = stream the tiles only, 2 = + the filter
+#endif
 constexpr int W = JIT_W, NC = JIT_NC, NL = JIT_NL, NA = JIT_NA, ND = JIT_ND, IMG = JIT_IMG, NCLS = JIT_NCLS;
+static_assert(JIT_RS == 1 || JIT_RS == 2, "rows shared by 1 or 2 waves");
 constexpr int TD = 64 * ND;                // docs per tile (lane l: docs [ND l, ND l + ND))
 constexpr u32 FULL = (1u << ND) - 1u;      // the lane's match word of a whole tile
 static_assert(ND == 8 || ND == 16, "8 or 16 docs per lane");
@@ -251,6 +258,7 @@ __device__ __forceinline__ void terms(CS* sg, u32 img, int lane, u32 base, u32 t
 template <int K>
 __device__ __forceinline__ u32 tile(CS* sg, i64 wt, u32 img, int lane, u32 base, u32 tb, u32 rows, u32 span_m1,
                                     u32& errs) {
+  if constexpr (JIT_DBG == 1) return 0;
   const i64 rem = (i64)sg->num_docs - wt * TD;
   u32 m = FULL;
   if (rem < TD) {
@@ -260,6 +268,7 @@ __device__ __forceinline__ u32 tile(CS* sg, i64 wt, u32 img, int lane, u32 base,
   u32 clause = 0, kt[ND];
   if (!leaves<K, 0>(sg, img, lane, base, tb, m, clause, kt)) return 0;
   if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return 0;
+  if constexpr (JIT_DBG == 2) return (u32)__builtin_popcount(m);
   constexpr int NBK = kNB[K][JIT_KC];
   u32 id[ND];
   if constexpr (JIT_KL >= 0) {
@@ -312,13 +321,15 @@ __device__ __forceinline__ u32 tile_any(int cls, CS* sg, i64 wt, u32 img, int la
   }
 }
 
-// a wave's packed rows -> the workgroup's COUNT / SUM accumulators (row zeroed)
+// a wave's packed rows -> the workgroup's COUNT / SUM accumulators (row zeroed; rows shared by two waves are taken by
+// atomic exchange, the other wave may be adding to them)
 __device__ __forceinline__ void drain(u32 rows, int nkeys, int lane, u32 base) {
   l64* row = at<l64>(rows);
   for (int k = lane; k < nkeys; k += 64) {
-    const u64 x = row[k];
+    u64 x = row[k];
     if (x == 0) continue;
-    row[k] = 0;
+    if constexpr (JIT_RS > 1) x = __hip_atomic_exchange(row + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else row[k] = 0;
     __hip_atomic_fetch_add(at<l32>(base) + k, (u32)(x >> JIT_OC), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
@@ -370,7 +381,7 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
 #pragma unroll
   for (int a = 0; a < NA; ++a)
     for (int i = tid; i < nkeys; i += W * 64) at<l64>(base + (u32)kLSUM[a])[i] = 0ull;
-  for (int i = tid; i < W * nkeys; i += W * 64) at<l64>(base + (u32)JIT_L_ROWS)[i] = 0ull;
+  for (int i = tid; i < (W / JIT_RS) * nkeys; i += W * 64) at<l64>(base + (u32)JIT_L_ROWS)[i] = 0ull;
   const i64 T = A->total_tiles, G = gridDim.x;
   const i64 b = blockIdx.x;
   const i64 lb = A->xcd_major ? (b % 8) * (G / 8) + (b % 8 < G % 8 ? b % 8 : G % 8) + b / 8 : b;
@@ -386,7 +397,7 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
       load_tables(A, S + si, base + (u32)JIT_L_SLOT + (u32)(k * JIT_SLOT_B), true, tid);
   }
   __syncthreads();
-  const u32 rows = base + (u32)JIT_L_ROWS + (u32)wave * (u32)nkeys * 8u;
+  const u32 rows = base + (u32)JIT_L_ROWS + (u32)(wave / JIT_RS) * (u32)nkeys * 8u;
   const u32 ring = base + (u32)JIT_L_RING + (u32)wave * 2u * (u32)IMG * 4u;
   const u32 voff = 16u * (u32)lane;
   const u32 span_m1 = (u32)A->key_span - 1u;

@@ -226,6 +226,7 @@ int pa_query_scan(pa_query* q, void* stream) {
     return PA_OK;
   }
   if (q->pve.fn) {  // the count-free emit: records in per-workgroup chunks, the partitions' chunk lists, pass C
+    if (q->part_vk == kVkGeneric) return fail(PA_EINVAL, "internal: chunk lists need a specialised pass C");
     PartScratch ps{};
     char* vb = (char*)q->pve.buf.p;
     ps.base = (uint64_t*)(vb + q->pve.o_base);

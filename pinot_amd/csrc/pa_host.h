@@ -8,6 +8,7 @@
 #include <hip/hiprtc.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -196,6 +197,7 @@ struct pa_query {
   std::vector<std::vector<std::vector<int32_t>>> remaps;       // [seg][gb]
   std::vector<std::vector<char>> has_remap;
   std::vector<std::vector<std::vector<int32_t>>> vremaps;      // [seg][agg] DISTINCTCOUNT value remaps (empty = identity)
+  std::vector<std::vector<int32_t>> vremap_host;               // [seg] host copy of DevSeg::vremap (value_dictionary)
   bool prepared = false;
 
   // plan

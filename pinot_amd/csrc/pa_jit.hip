@@ -215,7 +215,7 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
     koff[k] = rm.empty() ? 0 : rm[0];
   }
   // the group key from a DICT_RANGE leaf's unpack; the box check implied when that leaf is a unit clause whose range,
-  // shifted into the table's key ids, is exactly the box in every segment
+  // shifted into the table's key ids, lies inside the box in every segment (a matching doc's key is then in the box)
   int kl = -1;
   for (int li = 0; li < nl; ++li)
     if (lk[li] == 0 && lc[li] == kc) {
@@ -227,7 +227,7 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
     const pa_leaf_params& p = q->leaf_params[inc[k]][q->literals[kl].leaf];
     const int64_t card = q->hsegs[inc[k]].cols[cols[kc]].card;
     const int64_t rlo = std::max<int64_t>(0, p.lo), rhi = std::min<int64_t>(p.hi, card);
-    kib = rlo + koff[k] == klo && rhi - rlo == kspan;
+    kib = rhi > rlo && rlo + koff[k] >= klo && rhi + koff[k] <= klo + kspan;
   }
   // SUM terms: dictIds of arithmetic dictionaries with one common step (each segment's offset into the term space), else
   // value tables (values - the smallest value)
@@ -333,24 +333,27 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
     so += al16((size_t)kcard * 4);
   }
   const size_t l_slot = off, slot_b = al16(so);
-  // waves and docs per lane: the most resident waves, then the larger tile (PA_GDL_W / PA_GDL_ND: measurement)
-  std::vector<std::pair<int, int>> cands = {{16, 16}, {16, 8}, {8, 16}, {8, 8}};
-  if (const char* e = std::getenv("PA_GDL_W")) {
-    const int w = std::atoi(e);
-    cands.erase(std::remove_if(cands.begin(), cands.end(), [&](const std::pair<int, int>& c) { return c.first != w; }),
-                cands.end());
-  }
-  if (const char* e = std::getenv("PA_GDL_ND")) {
-    const int nd = std::atoi(e);
-    cands.erase(std::remove_if(cands.begin(), cands.end(), [&](const std::pair<int, int>& c) { return c.second != nd; }),
-                cands.end());
-  }
-  int W = 0, ND = 0, nslot = 0, G = 0, img_dw = 0;
+  // waves, docs per lane and waves per set of packed rows: the most resident waves, then the larger tile, then private
+  // rows (PA_GDL_W / PA_GDL_ND / PA_GDL_RS: measurement)
+  struct Cand {
+    int w, nd, rs;
+  };
+  std::vector<Cand> cands = {{16, 16, 1}, {16, 8, 1}, {8, 16, 1}, {8, 8, 1}, {16, 16, 2}, {16, 8, 2}};
+  auto keep_only = [&](const char* env, int Cand::*f) {
+    if (const char* e = std::getenv(env)) {
+      const int v = std::atoi(e);
+      cands.erase(std::remove_if(cands.begin(), cands.end(), [&](const Cand& c) { return c.*f != v; }), cands.end());
+    }
+  };
+  keep_only("PA_GDL_W", &Cand::w);
+  keep_only("PA_GDL_ND", &Cand::nd);
+  keep_only("PA_GDL_RS", &Cand::rs);
+  int W = 0, ND = 0, RS = 1, nslot = 0, G = 0, img_dw = 0;
   size_t lds = 0, l_rows = 0, l_ring = 0;
   std::vector<int64_t> first(ni + 1, 0);
   std::vector<std::vector<int>> coff;
-  for (const auto& cd : cands) {
-    const int w = cd.first, nd = cd.second, td = 64 * nd;
+  for (const Cand& cd : cands) {
+    const int w = cd.w, nd = cd.nd, td = 64 * nd;
     std::vector<int64_t> f(ni + 1, 0);
     for (int k = 0; k < ni; ++k) f[k + 1] = f[k] + (q->hsegs[inc[k]].num_docs + td - 1) / td;
     const int64_t T = f[ni];
@@ -378,11 +381,12 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
       idw = std::max(idw, (int)(al16(b) / 4));
     }
     const size_t rows = al16(l_slot + (size_t)ns * slot_b);
-    const size_t ring = al16(rows + (size_t)w * nkeys * 8);
+    const size_t ring = al16(rows + (size_t)(w / cd.rs) * nkeys * 8);
     const size_t total = ring + (size_t)w * 2 * idw * 4;
     if (total > kLdsBudget) continue;
     W = w;
     ND = nd;
+    RS = cd.rs;
     nslot = ns;
     G = g;
     img_dw = idw;
@@ -401,7 +405,8 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
     as[k] = oc;
     oc += sums[k].w + cbits;
   }
-  int drain = (int)std::max<uint64_t>(1, ((uint64_t(1) << cbits) - 1) / (uint64_t)(64 * ND));
+  // (rows shared by RS waves: between two drains of a set, each of its waves ran at most its own drain period)
+  int drain = (int)std::max<uint64_t>(1, ((uint64_t(1) << cbits) - 1) / (uint64_t)(64 * ND) / (uint64_t)RS);
   if (s.flags & PA_QF_GD_DRAIN_EACH_TILE) drain = 1;
   auto list = [](const std::vector<int>& v) {
     std::string r = "{";
@@ -431,7 +436,8 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
       "-DJIT_OC=" + std::to_string(oc), "-DJIT_DRAIN=" + std::to_string(drain), "-DJIT_L_SUM=" + list(lsum),
       "-DJIT_L_SLOT=" + std::to_string(l_slot), "-DJIT_SLOT_B=" + std::to_string(slot_b),
       "-DJIT_NSLOT=" + std::to_string(nslot), "-DJIT_L_ROWS=" + std::to_string(l_rows),
-      "-DJIT_L_RING=" + std::to_string(l_ring)};
+      "-DJIT_L_RING=" + std::to_string(l_ring), "-DJIT_RS=" + std::to_string(RS)};
+  if (const char* dbg = std::getenv("PA_GDL_DBG")) defs.push_back(std::string("-DJIT_DBG=") + dbg);  // (measurement)
   hipFunction_t fn = jit_compile(defs);
   if (!fn) return PA_OK;
   (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -509,8 +515,8 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
   q->jit_classes = (int)classes.size();
   q->jit_slots = nslot;
   q->jit_cols = cols;
-  PLAN_LOG("gdl_jit: W %d ND %d classes %zu slots %d (%zu B) segments %d/%d ktab %d kib %d lds %zu", W, ND,
-           classes.size(), nslot, slot_b, ni, q->nseg, (int)ktab, (int)kib, lds);
+  PLAN_LOG("gdl_jit: W %d ND %d RS %d classes %zu slots %d (%zu B) segments %d/%d ktab %d kib %d lds %zu drain %d", W,
+           ND, RS, classes.size(), nslot, slot_b, ni, q->nseg, (int)ktab, (int)kib, lds, drain);
   return PA_OK;
 }
 
@@ -585,11 +591,29 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   const int nc = (int)slots.size();
   if (nc < 1 || nc > 6) return PA_OK;
   int max_values = 1;
+  // segments with their own dictionaries: each group-by column's and the value column's dictionary must be a contiguous
+  // run of the table-wide one (time partitions, shifted windows), so one offset per segment maps its dictIds
+  std::vector<std::array<int32_t, kJitMaxGb>> koff(q->nseg);
+  std::vector<int32_t> voff(q->nseg, 0);
+  bool any_koff = false, any_voff = false;
+  auto run_start = [](const std::vector<int32_t>& rm, int32_t* start) {
+    for (size_t i = 0; i < rm.size(); ++i)
+      if (rm[i] != rm[0] + (int32_t)i) return false;
+    *start = rm.empty() ? 0 : rm[0];
+    return true;
+  };
   for (int si = 0; si < q->nseg; ++si) {
     const DevSeg& d = q->hsegs[si];
-    if (d.vremap) return PA_OK;
-    for (int j = 0; j < s.num_group_by; ++j)
-      if (d.remap[j]) return PA_OK;
+    koff[si].fill(0);
+    for (int j = 0; j < s.num_group_by; ++j) {
+      if (!d.remap[j]) continue;
+      if (!q->has_remap[si][j] || !run_start(q->remaps[si][j], &koff[si][j])) return PA_OK;
+      any_koff |= koff[si][j] != 0;
+    }
+    if (d.vremap && vc >= 0) {  // (the value ids of the V records; the H stream carries none)
+      if (si >= (int)q->vremap_host.size() || !run_start(q->vremap_host[si], &voff[si])) return PA_OK;
+      any_voff |= voff[si] != 0;
+    }
     for (int k = 0; k < nc; ++k) {
       const DevCol& c = d.cols[slots[k]];
       if (c.kind != COL_SV_DICT || !c.words || c.nbits < 1 || c.nbits > 31 || c.nbits != d0.cols[slots[k]].nbits)
@@ -692,7 +716,8 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
       "-DPVE_L_RING=" + std::to_string(l_ring), "-DPVE_RW=" + std::to_string(rw),
       "-DPVE_RAWB=" + std::to_string(rawb), "-DPVE_RAWOFF=" + std::to_string(raw_off),
       "-DPVE_H=" + std::to_string(hmode ? 1 : 0), "-DPVE_HNB=" + std::to_string(hnb), "-DPVE_LG=" + std::to_string(lg),
-      "-DPVE_L_VAL=" + std::to_string(l_val), "-DPVE_VAL_B=" + std::to_string(vbytes)};
+      "-DPVE_L_VAL=" + std::to_string(l_val), "-DPVE_VAL_B=" + std::to_string(vbytes),
+      "-DPVE_KOFF=" + std::to_string(any_koff ? 1 : 0), "-DPVE_VOFF=" + std::to_string(any_voff ? 1 : 0)};
   if (const char* dbg = std::getenv("PA_PVE_DBG")) defs.push_back(std::string("-DPVE_DBG=") + dbg);  // (measurement)
   if (const char* pb = std::getenv("PA_PVE_PB")) defs.push_back(std::string("-DPVE_PB=") + pb);      // (measurement)
   if (std::getenv("PA_PVE_DONE_RTN")) defs.push_back("-DPVE_DONE_RTN=1");                            // (measurement)
@@ -737,6 +762,8 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
       j.hi_t[li] = (uint32_t)d.leaves[li].span;
     }
     j.admit = (uint64_t)(uintptr_t)d.admit;
+    for (int g = 0; g < s.num_group_by; ++g) j.koff[g] = koff[si][g];
+    j.voff = voff[si];
     if (rslot >= 0) j.raw = (uint64_t)(uintptr_t)d.cols[rslot].raw;
     if (hmode) {
       j.mv_off = (uint64_t)(uintptr_t)d.cols[mslot].mv_off;

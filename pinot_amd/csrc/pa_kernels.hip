@@ -1300,10 +1300,9 @@ __device__ void part_agg_v(const DevQuery* __restrict__ q, const PartScratch& ps
       w0[j] = kSentinel;
       w1[j] = w2[j] = 0u;
       if (ri < r1) {
-        const uint64_t pi = ps.chunk_index ? ((uint64_t)gp(ps.chunk_index)[ri >> ps.chunk_shift] << ps.chunk_shift) |
-                                                 (ri & ((1ull << ps.chunk_shift) - 1ull))
-                                           : ri;
-        const AS1 uint32_t* rec = recs + pi * (uint64_t)W;
+        // (contiguous partition ranges only: the count-free emit's chunk lists feed the specialised variants, never this
+        // one — pve_plan refuses kVkGeneric, so ps.chunk_index is null here)
+        const AS1 uint32_t* rec = recs + ri * (uint64_t)W;
         w0[j] = __builtin_nontemporal_load(rec);
         if (fmt == V_FMT_32 || fmt == V_FMT_64) w1[j] = __builtin_nontemporal_load(rec + 1);
         if (fmt == V_FMT_64) w2[j] = __builtin_nontemporal_load(rec + 2);

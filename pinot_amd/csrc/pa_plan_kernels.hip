@@ -91,6 +91,7 @@ int value_dictionary(pa_query* q, const Prep& P, int a, const uint64_t** vdict) 
     same = same && (c == c0 || (c->dict_hash == c0->dict_hash && c->hvals == c0->hvals));
   }
   for (int si = 0; si < q->nseg; ++si) q->hsegs[si].vremap = nullptr;
+  q->vremap_host.assign(q->nseg, {});
   q->hq.v_affine = 0;
   q->hq.v_maxabs = 0;
   if (same) {
@@ -138,6 +139,7 @@ int value_dictionary(pa_query* q, const Prep& P, int a, const uint64_t** vdict) 
     void* rp = nullptr;
     if (upload_owned(q, rm.data(), rm.size() * 4, &rp)) return -2;
     q->hsegs[si].vremap = (const int32_t*)rp;
+    q->vremap_host[si] = std::move(rm);
   }
   (void)P;
   return std::max(1, 64 - __builtin_clzll((unsigned long long)std::max<size_t>(1, uni.size() - 1)));
@@ -864,7 +866,7 @@ void fill_devquery(pa_query* q, const Prep& P, const TilePlan& plan, int64_t tot
             off += P.gd_pk_w[a] + P.gd_pk_c;
           }
           lp.pk_cnt = off;
-          lp.pk_drain = ((1 << P.gd_pk_c) - 1) >> 10;  // tiles of <= 1024 docs each
+          lp.pk_drain = (int32_t)(((uint64_t(1) << P.gd_pk_c) - 1) >> 10);  // tiles of <= 1024 docs each
           if (s.flags & PA_QF_GD_DRAIN_EACH_TILE) lp.pk_drain = 1;
           lp.pk_base = (int32_t)P.gd_lds;  // (the waves' rows follow the accumulators and tables)
         }

@@ -25,6 +25,8 @@
 //   PVE_L_BINS, PVE_L_RING LDS byte offsets (state at 0: cnt[P], done[P], chunks[P], cur[P], fill[P], next)
 //   PVE_RW record words, PVE_RAWB / PVE_RAWOFF the staged raw value column, PVE_H the H stream (PVE_HNB, PVE_LG,
 //   PVE_L_VAL / PVE_VAL_B: per-wave LDS buffers of the tile's MV value words)
+//   PVE_KOFF / PVE_VOFF segments with their own dictionaries, each a contiguous run of the table-wide dictionary: the
+//   segment's offsets into the table key ids / value ids (PveSeg.koff, voff)
 typedef unsigned int u32;
 typedef unsigned long long u64;
 typedef long long i64;
@@ -83,6 +85,12 @@ constexpr u32 kSentinel = 0xffffffffu;
 #endif
 #ifndef PVE_LG
 #define PVE_LG 0
+#endif
+#ifndef PVE_KOFF
+#define PVE_KOFF 0  // segments with their own dictionaries: table key id of component j = dictId + PveSeg.koff[j]
+#endif
+#ifndef PVE_VOFF
+#define PVE_VOFF 0  // the value column's table-wide value id = dictId + PveSeg.voff
 #endif
 constexpr int RW = PVE_RW, RAWB = PVE_RAWB, HNB = PVE_HNB, LG = PVE_LG;
 static_assert(RW >= 1 && RW <= 3 && (RAWB == 0 || RAWB == 4 * (RW - 1)), "record words and the raw column agree");
@@ -517,11 +525,19 @@ __device__ __forceinline__ u32 tile(const Bins& B, CS* sg, i64 wt, u32 img, int 
     for (int k = 0; k < RW; ++k) val[i][k] = 0u;
   }
   keys<0>(img, lane, key);
+  if constexpr (PVE_KOFF) {  // each component's run of the table dictionary: one offset per segment
+    u32 kadd = 0;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) kadd += (u32)sg->koff[g] * kGS[g];
+#pragma unroll
+    for (int i = 0; i < ND; ++i) key[i] += kadd;
+  }
   if constexpr (VC >= 0) {
     u32 id[ND];
     unpack<(VC >= 0 ? VC : 0), false>(img, lane, id);
+    const u32 vadd = PVE_VOFF ? (u32)sg->voff : 0u;
 #pragma unroll
-    for (int i = 0; i < ND; ++i) val[i][0] = id[i];
+    for (int i = 0; i < ND; ++i) val[i][0] = id[i] + vadd;
   }
   if constexpr (RAWB > 0) {  // the lane's ND raw values: ND RAWB consecutive bytes of the staged tile
     const __attribute__((address_space(3))) u32x4* r =

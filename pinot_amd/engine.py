@@ -671,8 +671,11 @@ class GpuQueryExecutor:
         if merged is not None:
             # numDocsScanned was summed across GPUs (parallel.DistributedAccumulators.reduce): this rank's segments
             # cannot recount the statistics against it; the reduce summed every rank's own pair before its collective
-            # (reduce(execution_stats=True)), or left (0, 0)
+            # (reduce(execution_stats=True), the default), or gathered none (NO_MERGED_STATS)
             if execution_stats:
+                if isinstance(merged, str):  # (parallel.NO_MERGED_STATS)
+                    raise L.PinotAmdError("the merged block has no execution statistics: reduce(execution_stats=True), "
+                                          "or fetch(execution_stats=False)")
                 res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter = merged
         elif execution_stats:
             res.num_entries_scanned_in_filter, res.num_entries_scanned_post_filter = self.execution_stats(

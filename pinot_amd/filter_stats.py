@@ -627,14 +627,20 @@ def operator_trees(query, segments, leaf_params=None, column_ids=None):
                 continue
             params = None if leaf_params is None else leaf_params[si]
             sig = _tree_signature(seg, fcols, params)
-            if sig is not None and sig in by_sig:
-                seg_tree.append(by_sig[sig])
+            # the tree (and its encoded index) is shared per filter signature; the non-scan plan choice is made per
+            # segment, as AggregationPlanNode.isFitForNonScanBasedPlan is per IndexSegment (it reads the aggregation
+            # columns, which the signature does not cover)
+            entry = by_sig.get(sig) if sig is not None else None
+            if entry is None:
+                entry = [_build(flat, seg, _RpnCursor(seg, params), segment_index_info(seg)), None]
+                if sig is not None:
+                    by_sig[sig] = entry
+            if non_scan_plan(query, seg, entry[0].kind == "all"):
+                seg_tree.append(L.PA_STATS_NON_SCAN)
                 continue
-            op = _build(flat, seg, _RpnCursor(seg, params), segment_index_info(seg))
-            t = L.PA_STATS_NON_SCAN if non_scan_plan(query, seg, op.kind == "all") else add(op)
-            if sig is not None:
-                by_sig[sig] = t
-            seg_tree.append(t)
+            if entry[1] is None:
+                entry[1] = add(entry[0])
+            seg_tree.append(entry[1])
         except _Unsupported:
             seg_tree.append(L.PA_STATS_HOST)
     ops = np.stack(rows) if rows else np.zeros((1, OP_WORDS), dtype=np.int32)

@@ -55,6 +55,10 @@ def shard_segments(num_segments, rank, world_size):
     return list(range(start, start + per + (1 if rank < extra else 0)))
 
 
+# DistributedAccumulators.reduce(execution_stats=False): the merged block carries no execution statistics
+NO_MERGED_STATS = "no merged execution statistics"
+
+
 def reduce_sections(views, dst=0, group=None, all_reduce=False):
     """views: [(section kind, tensor)] -> reduced in place on `dst` (or everywhere)."""
     for kind, t in views:
@@ -516,11 +520,12 @@ class DistributedAccumulators:
             off = ptr - self.base + pad
             self.per_key.append((kind, self.buf[off:off + n * es].view(dt)))
 
-    def reduce(self, dst=0, all_reduce=False, execution_stats=False, group=None):
-        """Element-wise merge onto rank `dst` (every rank with all_reduce). numDocsScanned is summed too, so the merged
-        results block's execution statistics are every rank's own pair summed before the collective
-        (execution_stats=True: one extra 16-byte all-reduce and a host sync per query); without it the merged
-        block carries (0, 0) — the timed bench steps, which fetch without statistics anyway."""
+    def reduce(self, dst=0, all_reduce=False, execution_stats=True, group=None):
+        """Element-wise merge onto rank `dst` (every rank with all_reduce; `dst` is a global rank, as torch.distributed's
+        reduce takes it, also under a subgroup). numDocsScanned is summed too, so the merged results block's execution
+        statistics are every rank's own pair summed before the collective (one extra 16-byte all-reduce and a host sync
+        per query). execution_stats=False skips that (the timed bench steps, which fetch without statistics): the merged
+        block then has no statistics, and a fetch that asks for them raises instead of returning (0, 0)."""
         ex = self.executor
         if execution_stats:
             local = torch.tensor(list(ex.execution_stats()), dtype=torch.int64, device=self.buf.device)
@@ -528,8 +533,8 @@ class DistributedAccumulators:
                 dist.all_reduce(local, group=group)
             stats = tuple(int(v) for v in local.tolist())
         else:
-            stats = (0, 0)
-        reduce_sections(self.views, dst=dst, all_reduce=all_reduce)
+            stats = NO_MERGED_STATS
+        reduce_sections(self.views, dst=dst, group=group, all_reduce=all_reduce)
         if all_reduce or not dist.is_initialized() or dist.get_rank() == dst:
             ex.merged_stats = stats
 
@@ -538,7 +543,7 @@ class DistributedAccumulators:
         (reduce_scatter_sections), so each rank's fetch returns its share of the groups. Returns the range (lo, hi)."""
         return reduce_scatter_sections(self.per_key, self.num_keys, group)
 
-    def merge(self, dst=0, group=None, scatter_keys=1 << 20, execution_stats=False):
+    def merge(self, dst=0, group=None, scatter_keys=1 << 20, execution_stats=True):
         """The cross-GPU merge this key space wants: key spaces of at least `scatter_keys` keys reduce-scatter (every
         rank then fetches its share: returns True), smaller ones reduce onto rank `dst`, the one rank that fetches
         (returns False)."""

@@ -421,3 +421,28 @@ def test_operator_tree_encoding():
     assert [int(r[0]) for r in ops] == [L.PA_FOP_MATCH_ALL]
     q = parse_sql("SELECT MAX(a) FROM t")  # non-scan plan
     assert list(FS.operator_trees(q, segs, None, {})[2]) == [L.PA_STATS_NON_SCAN] * 2
+
+
+def test_non_scan_plan_chosen_per_segment_with_shared_trees():
+    """segments sharing a filter signature share one operator tree, but the non-scan plan is chosen per
+    segment (AggregationPlanNode.isFitForNonScanBasedPlan reads each IndexSegment's aggregation columns): with the
+    aggregated column dictionary-encoded in one segment and raw in the other, only the first takes the non-scan plan,
+    and each segment's accounting equals its own replay."""
+    from pinot_amd.segment import create_segment
+    rng = np.random.default_rng(5)
+    n = 3000
+    data = {"a": rng.integers(0, 60, n).astype(np.int32), "b": rng.integers(0, 100, n).astype(np.int32)}
+    types = {"a": "INT", "b": "INT"}
+    segs = [create_segment("dict", data, types), create_segment("raw", data, types, no_dictionary_columns=("b",))]
+    q = parse_sql("SELECT DISTINCTCOUNT(b) FROM t WHERE a < 1000")  # (a match-all filter: every a < 60)
+    params = [[P.dictionary_leaf(pred, s.column(pred.column)) for pred in _leaves(q, s)] for s in segs]
+    ops, roots, seg_tree = FS.operator_trees(q, segs, params, {})
+    assert seg_tree[0] == L.PA_STATS_NON_SCAN and seg_tree[1] >= 0
+    for order in (segs, segs[::-1]):  # (whichever segment builds the shared tree first)
+        pr = [params[segs.index(s)] for s in order]
+        st = FS.operator_trees(q, order, pr, {})[2]
+        assert [t == L.PA_STATS_NON_SCAN for t in st] == [s.name == "dict" for s in order]
+        for s, t in zip(order, st):
+            masks = leaf_masks(q, s)
+            exp = FS.server_stats(q, [s], lambda _: masks)
+            assert (exp == (0, 0)) == (t == L.PA_STATS_NON_SCAN)

@@ -257,6 +257,40 @@ def test_configs2_high_cardinality_group_by(highcard, variant, count_free):
         assert n <= 2 * 100_000
 
 
+@pytest.fixture(scope="module")
+def highcard_own():
+    segs = [CFG.highcard_own_segment(201 + i, 1_500_000) for i in range(2)]
+    gs = [GpuSegment(s) for s in segs]
+    yield segs, gs
+    for g in gs:
+        g.close()
+
+
+@pytest.mark.parametrize("count_free", [True, False])
+@pytest.mark.parametrize("variant", ["untrimmed", "default_limit", "filtered"])
+def test_configs2_own_dictionaries(highcard_own, variant, count_free):
+    """configs[2] over segments that built their own dictionaries (d1 / d2 / m shifted runs of the table-wide
+    dictionaries): the count-free emit maps each segment's dictIds by its key and value id offsets (pve_jit.hip
+    PVE_KOFF / PVE_VOFF); the count + emit passes through the remap tables. Table-wide keys against the oracle's."""
+    segs, gs = highcard_own
+    assert not np.array_equal(segs[0].column("d1").dictionary, segs[1].column("d1").dictionary)
+    sql = {"untrimmed": "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000 "
+                        "OPTION(numGroupsLimit=2000000)",
+           "default_limit": "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000",
+           "filtered": "SELECT d1, d2, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t WHERE m < 6554 GROUP BY d1, d2 "
+                       "LIMIT 2000000 OPTION(numGroupsLimit=2000000)"}[variant]
+    q = parse_sql(sql)
+    ex = GpuQueryExecutor(q, gs, flags=0 if count_free else L.PA_QF2_NO_COUNT_FREE)
+    try:
+        p = _plan(ex)
+        assert p["strategy"] == "partitioned", p
+        assert p["count_free_emit"] == (1 if count_free else 0), p
+        ex.execute()
+        _compare_arrays(ex, q, segs)
+    finally:
+        ex.close()
+
+
 def test_configs2_non_affine_values():
     """configs[2] with a non-arithmetic value dictionary (pass C looks every SUM value up)."""
     segs = [CFG.highcard_rd_segment(300, 2_000_000)]

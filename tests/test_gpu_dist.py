@@ -252,8 +252,9 @@ def test_reduce_scatter_merge_path(rccl_world1):
 
 def test_reduce_execution_stats(rccl_world1):
     """numDocsScanned is summed by the element-wise reduce, so the merged block's execution statistics are the ranks'
-    own pairs summed before the collective (reduce(execution_stats=True)); a plain reduce leaves (0, 0) rather than
-    recounting this rank's segments against the merged counter, and the next execute() returns to local counting."""
+    own pairs summed before the collective (reduce(execution_stats=True), the default); a reduce without them
+    (execution_stats=False) makes a statistics fetch raise rather than recount this rank's segments against the merged
+    counter or return (0, 0), and the next execute() returns to local counting.""" 
     q = parse_sql("SELECT d1, COUNT(*), SUM(m) FROM t WHERE m > 1000 AND d1 < 30 GROUP BY d1 LIMIT 10000")
     segs = [make_segment(840 + i, n, COLS) for i, n in enumerate((12007, 4001))]
     gsegs = [GpuSegment(s) for s in segs]
@@ -268,8 +269,14 @@ def test_reduce_execution_stats(rccl_world1):
         got = ex.fetch()
         assert (got.num_entries_scanned_in_filter, got.num_entries_scanned_post_filter) == local
         ex.execute()
-        acc.reduce(dst=0)
+        acc.reduce(dst=0)  # (the default gathers the statistics too)
         got = ex.fetch()
+        assert (got.num_entries_scanned_in_filter, got.num_entries_scanned_post_filter) == local
+        ex.execute()
+        acc.reduce(dst=0, execution_stats=False)
+        with pytest.raises(L.PinotAmdError):
+            ex.fetch()  # (no statistics were gathered: no silent (0, 0))
+        got = ex.fetch(execution_stats=False)
         assert (got.num_entries_scanned_in_filter, got.num_entries_scanned_post_filter) == (0, 0)
         ex.execute()
         again = ex.fetch()
