@@ -13,7 +13,8 @@
 //  * DICT_SET bitmaps, value tables and key tables that differ per segment live in LDS table slots: a workgroup's tile
 //    range spans at most JIT_NSLOT segments, whose tables it loads when it starts; tables every segment shares sit in
 //    one shared area;
-//  * SUMs over per-segment arithmetic dictionaries with one common step add the segment's dictId offset (JitSeg.aoff);
+//  * SUMs over per-segment arithmetic dictionaries with one common step: the rows pack bare dictIds and the drain adds
+//    the segment's dictId offset x count (JitSeg.aoff; rows drained at every segment switch);
 //  * a leaf negated in some segments only (an empty range becomes NOT(full range)) XORs the segment's bit (JIT_LN 2).
 //
 // Reference semantics: GroupByOperator -> DefaultGroupByExecutor.process (DefaultGroupByExecutor.java:131-158),
@@ -29,7 +30,8 @@
 //   JIT_KC the group-by column, JIT_KL the leaf whose unpack it reuses (-1: none), JIT_KIB the filter implies the box,
 //          JIT_KTAB slot byte offset of the group-key table (-1: affine keys)
 //   JIT_NA SUM aggregations, JIT_AC {column}, JIT_AT {LDS byte offset of a value table, -1: the dictId itself},
-//          JIT_ATS {1: table in the slot}, JIT_AO {1: + the segment's dictId offset}, JIT_AS {bit offset of the field},
+//          JIT_ATS {1: table in the slot}, JIT_AO {1: + the segment's dictId offset, folded in at the drain},
+//          JIT_AS {bit offset of the field},
 //          JIT_OC bit offset of the COUNT field
 //   JIT_DRAIN tiles between drains of a wave's packed rows, JIT_RS waves sharing one set of rows
 //   JIT_L_SUM {LDS byte offset of each SUM's accumulators}, JIT_L_SLOT / JIT_SLOT_B / JIT_NSLOT the table slots,
@@ -233,11 +235,6 @@ __device__ __forceinline__ void terms(CS* sg, u32 img, int lane, u32 base, u32 t
 #pragma unroll
       for (int i = 0; i < ND; ++i) id[i] = *at<const l32>(ab + 4u * id[i]);
     }
-    if constexpr (kAO[A]) {
-      const u32 ao = (u32)sg->aoff[A];
-#pragma unroll
-      for (int i = 0; i < ND; ++i) id[i] += ao;
-    }
     constexpr int SH = kAS[A];
 #pragma unroll
     for (int i = 0; i < ND; ++i) {
@@ -322,23 +319,36 @@ __device__ __forceinline__ u32 tile_any(int cls, CS* sg, i64 wt, u32 img, int la
 }
 
 // a wave's packed rows -> the workgroup's COUNT / SUM accumulators (row zeroed; rows shared by two waves are taken by
-// atomic exchange, the other wave may be adding to them)
-__device__ __forceinline__ void drain(u32 rows, int nkeys, int lane, u32 base) {
+// atomic exchange, the other wave may be adding to them). A SUM over per-segment arithmetic dictionaries (kAO) packs
+// bare dictIds: the rows hold one segment's docs at a time (drained at every segment switch), so the segment's dictId
+// offset enters here once per key, as offset x count.
+__device__ __forceinline__ void drain(u32 rows, int nkeys, int lane, u32 base, CS* sg) {
   l64* row = at<l64>(rows);
+  u64 ao[NAA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) ao[a] = kAO[a] ? (u64)(u32)sg->aoff[a] : 0ull;
   for (int k = lane; k < nkeys; k += 64) {
     u64 x = row[k];
     if (x == 0) continue;
     if constexpr (JIT_RS > 1) x = __hip_atomic_exchange(row + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     else row[k] = 0;
-    __hip_atomic_fetch_add(at<l32>(base) + k, (u32)(x >> JIT_OC), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const u32 cnt = (u32)(x >> JIT_OC);
+    __hip_atomic_fetch_add(at<l32>(base) + k, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
       const int lo = kAS[a], hi = a + 1 < NA ? kAS[a + 1 < NA ? a + 1 : a] : JIT_OC;
-      const u64 f = (x >> lo) & ((hi - lo) >= 64 ? ~0ull : ((1ull << (hi - lo)) - 1ull));
+      u64 f = (x >> lo) & ((hi - lo) >= 64 ? ~0ull : ((1ull << (hi - lo)) - 1ull));
+      if (kAO[a]) f += ao[a] * (u64)cnt;
       __hip_atomic_fetch_add(at<l64>(base + (u32)kLSUM[a]) + k, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
 }
+constexpr bool kAnyAO = [] {
+  for (int a = 0; a < NA; ++a)
+    if (kAO[a]) return true;
+  return false;
+}();
+static_assert(!kAnyAO || JIT_RS == 1, "per-segment offsets need private rows (one segment's docs in them at a time)");
 
 __device__ __forceinline__ int find_segment(CS* segs, int nseg, i64 t) {
   int lo = 0, hi = nseg - 1;
@@ -434,6 +444,10 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
       }
       ti += W;
       while (t >= pend) {
+        if constexpr (kAnyAO) {  // (the rows hold the segment's docs only: its offsets are folded in here)
+          drain(rows, nkeys, lane, base, S + psi);
+          since = 0;
+        }
         ++psi;
         pfirst = S[psi].first_tile;
         pend = pfirst + S[psi].num_tiles;
@@ -443,14 +457,14 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
       matched += tile_any<0>(pcls, S + psi, t - pfirst, ring + (u32)slot * (u32)IMG * 4u, lane, base, tb, rows,
                              span_m1, errs);
       if (++since == JIT_DRAIN) {
-        drain(rows, nkeys, lane, base);
+        drain(rows, nkeys, lane, base, S + psi);
         since = 0;
       }
       slot ^= 1;
     }
+    vm_wait<0>();
+    drain(rows, nkeys, lane, base, S + psi);
   }
-  vm_wait<0>();
-  drain(rows, nkeys, lane, base);
   u64 wm = matched, we = errs;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {

@@ -276,8 +276,9 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
         J.table = false;
         J.base = (int64_t)mn;
         J.step = step;
-        J.w = bits_for((uint64_t)top);
         for (int64_t o : J.aoff) J.offs |= o != 0;
+        // (per-segment offsets are folded in at the drain: the rows pack bare dictIds)
+        J.w = J.offs ? bits_for((uint64_t)std::max(1, J.max_card) - 1) : bits_for((uint64_t)top);
         continue;
       }
     }
@@ -348,6 +349,10 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
   keep_only("PA_GDL_W", &Cand::w);
   keep_only("PA_GDL_ND", &Cand::nd);
   keep_only("PA_GDL_RS", &Cand::rs);
+  bool any_offs = false;  // (per-segment SUM offsets are folded in at the drain: one segment per private row set)
+  for (const JitSum& J : sums) any_offs |= !J.table && J.offs;
+  if (any_offs)
+    cands.erase(std::remove_if(cands.begin(), cands.end(), [](const Cand& c) { return c.rs != 1; }), cands.end());
   int W = 0, ND = 0, RS = 1, nslot = 0, G = 0, img_dw = 0;
   size_t lds = 0, l_rows = 0, l_ring = 0;
   std::vector<int64_t> first(ni + 1, 0);

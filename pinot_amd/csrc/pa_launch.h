@@ -164,6 +164,25 @@ struct LfJob {
   uint32_t* cells;                              // [nchunks][K + 1][cell_words]
   unsigned long long* out;                      // [0] entries read, [1] read after the last match, [2] matches
 };
+// The filter shapes the reduction above does not express (a NOT child of a leap-frogging AND, an AND or NOT under an
+// OR inside a leap-frog, a NOT over a leap-frog with an OR child): the segment's iterator tree replayed on the GPU, one
+// thread per segment, over the element masks (stat_replay_kernel): the reference's iterators restated node by node.
+constexpr int kRpMaxNodes = 24;
+constexpr int kRpMaxDepth = 6;
+enum : int32_t { RP_EMPTY = 0, RP_ALL = 1, RP_DOCS = 2, RP_SCAN = 3, RP_AND = 4, RP_OR = 5, RP_NOT = 6 };
+struct RpNode {
+  int32_t kind, nchild, first, depth;  // children: RpJob::kids[first .. first + nchild), depth below the root
+  const uint32_t* mask;                // RP_DOCS / RP_SCAN: the doc set
+  const int32_t* wt;                   // RP_SCAN over a multi-value column: value offsets (nullptr: one entry per doc)
+};
+struct RpJob {
+  int64_t num_docs;
+  int32_t nnodes, root;
+  int32_t kids[kRpMaxNodes];
+  RpNode node[kRpMaxNodes];
+  unsigned long long* out;             // entries the scan iterators read (UINT64_MAX: the step budget ran out)
+};
+hipError_t launch_stat_replay(const RpJob* jobs, int nj, hipStream_t s);
 int64_t stat_mask_blocks(int64_t words);
 hipError_t launch_stat_masks(const StatMaskJob* jobs, int nj, int64_t blocks, const int32_t* toks, hipStream_t s);
 hipError_t launch_stat_counts(const StatCountJob* jobs, int nj, int64_t blocks, hipStream_t s);

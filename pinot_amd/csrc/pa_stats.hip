@@ -345,4 +345,262 @@ hipError_t launch_leapfrogs(const LfJob* jobs, int nj, int64_t lanes, hipStream_
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- iterator replay (the shapes the reduction leaves out)
+// One thread per segment drives the reference's iterators over the element masks exactly as the projection does
+// (DocIdSetOperator: next() until EOF), counting the entries the scan iterators read:
+//   RP_DOCS  SortedDocIdIterator / BitmapDocIdIterator (and the merged doc sets AndDocIdSet / OrDocIdSet build): no reads
+//   RP_SCAN  SVScanDocIdIterator.java:76-142: next() reads 256-doc batches, advance(t) reads from t to the next match;
+//            MVScanDocIdIterator.java:61-110: doc by doc, every value of a doc
+//   RP_AND   AndDocIdIterator.java:39-73   RP_OR  OrDocIdIterator.java:50-109   RP_NOT  NotDocIdIterator.java:36-66
+// The host built the tree the way the reference's BlockDocIdSet.iterator() calls do (AndDocIdSet's applyAnd merges are
+// counted there, as popcounts). Node state lives in the thread's private arrays; calls nest at most kRpMaxDepth deep
+// (a template per depth: no recursion).
+namespace {
+constexpr int64_t kRpEof = -1;
+constexpr int kRpBatch = 256;  // BlockDocIdIterator.OPTIMAL_ITERATOR_BATCH_SIZE
+
+struct RpCtx {
+  const RpJob* J;
+  int64_t n;
+  int64_t a[kRpMaxNodes], b[kRpMaxNodes], c[kRpMaxNodes];  // per-node iterator state (kind-specific)
+  int64_t nd[kRpMaxNodes];                                 // an OR child's cached answer
+  bool live[kRpMaxNodes];                                  // an OR child not yet exhausted
+  unsigned long long ent;
+};
+
+// smallest set bit of m in [t, e), or e
+__device__ __forceinline__ int64_t rp_next_set(const uint32_t* __restrict__ m, int64_t t, int64_t e) {
+  if (t >= e) return e;
+  int64_t w = t >> 5;
+  uint32_t bits = m[w] & (0xffffffffu << (t & 31));
+  const int64_t wend = (e + 31) >> 5;
+  while (bits == 0u) {
+    if (++w >= wend) return e;
+    bits = m[w];
+  }
+  const int64_t d = (w << 5) + __builtin_ctz(bits);
+  return d < e ? d : e;
+}
+
+__device__ __forceinline__ void rp_read(RpCtx& x, const RpNode& nd, int64_t lo, int64_t hi) {
+  x.ent += nd.wt ? (unsigned long long)(nd.wt[hi] - nd.wt[lo]) : (unsigned long long)(hi - lo);
+}
+
+// SVScanDocIdIterator / MVScanDocIdIterator reading from `start` to its next match (advance; MV next)
+__device__ __forceinline__ int64_t rp_scan_from(RpCtx& x, int i, int64_t start) {
+  const RpNode& nd = x.J->node[i];
+  const int64_t n = x.n;
+  const int64_t d = rp_next_set(nd.mask, start, n);
+  if (d < n) {
+    rp_read(x, nd, start, d + 1);
+    x.a[i] = d + 1;
+    return d;
+  }
+  if (start < n) rp_read(x, nd, start, n);
+  x.a[i] = start > n ? start : n;
+  return kRpEof;
+}
+
+template <int D> __device__ int64_t rp_next(RpCtx& x, int i);
+template <int D> __device__ int64_t rp_adv(RpCtx& x, int i, int64_t t);
+
+template <int D>
+__device__ __forceinline__ int64_t rp_next_child(RpCtx& x, int k) {
+  if constexpr (D + 1 < kRpMaxDepth) return rp_next<D + 1>(x, k);
+  else return kRpEof;  // (the host limits the depth)
+}
+template <int D>
+__device__ __forceinline__ int64_t rp_adv_child(RpCtx& x, int k, int64_t t) {
+  if constexpr (D + 1 < kRpMaxDepth) return rp_adv<D + 1>(x, k, t);
+  else return kRpEof;
+}
+
+template <int D>
+__device__ int64_t rp_next(RpCtx& x, int i) {
+  const RpNode& nd = x.J->node[i];
+  const int64_t n = x.n;
+  switch (nd.kind) {
+    case RP_DOCS: {
+      const int64_t d = rp_next_set(nd.mask, x.a[i], n);
+      x.a[i] = d < n ? d + 1 : n;
+      return d < n ? d : kRpEof;
+    }
+    case RP_ALL:
+      return x.a[i] < n ? x.a[i]++ : kRpEof;
+    case RP_SCAN: {
+      if (nd.wt) return rp_scan_from(x, i, x.a[i]);
+      // a = next doc to read, [b, c) the current batch (its matches not yet returned from b on)
+      while (true) {
+        if (x.b[i] < x.c[i]) {
+          const int64_t d = rp_next_set(nd.mask, x.b[i], x.c[i]);
+          if (d < x.c[i]) {
+            x.b[i] = d + 1;
+            return d;
+          }
+          x.b[i] = x.c[i];
+        }
+        const int64_t limit = n - x.a[i] < kRpBatch ? n - x.a[i] : kRpBatch;
+        if (limit <= 0) return kRpEof;
+        x.ent += (unsigned long long)limit;
+        x.b[i] = x.a[i];
+        x.c[i] = x.a[i] + limit;
+        x.a[i] += limit;
+      }
+    }
+    case RP_AND: {
+      int64_t mx = x.a[i];
+      int mi = -1, idx = 0;
+      while (idx < nd.nchild) {
+        if (idx == mi) {
+          ++idx;
+          continue;
+        }
+        const int64_t d = rp_adv_child<D>(x, x.J->kids[nd.first + idx], mx);
+        if (d == kRpEof) return kRpEof;
+        if (d == mx) {
+          ++idx;
+        } else {
+          mx = d;
+          mi = idx;
+          idx = 0;
+        }
+      }
+      x.a[i] = mx + 1;
+      return mx;
+    }
+    case RP_OR: {
+      int64_t best = kRpEof;
+      for (int j = 0; j < nd.nchild; ++j) {
+        const int k = x.J->kids[nd.first + j];
+        if (!x.live[k]) continue;
+        int64_t d = x.nd[k];
+        if (d == x.a[i]) {
+          d = rp_next_child<D>(x, k);
+          x.nd[k] = d;
+          if (d == kRpEof) {
+            x.live[k] = false;
+            continue;
+          }
+        }
+        best = best == kRpEof || d < best ? d : best;
+      }
+      if (best != kRpEof) x.a[i] = best;
+      return best;
+    }
+    case RP_NOT: {
+      const int k = x.J->kids[nd.first];
+      while (x.a[i] == x.b[i]) {
+        ++x.a[i];
+        const int64_t c = rp_next_child<D>(x, k);
+        x.b[i] = c == kRpEof ? n : c;
+      }
+      if (x.a[i] >= n) return kRpEof;
+      return x.a[i]++;
+    }
+    default:
+      return kRpEof;
+  }
+}
+
+template <int D>
+__device__ int64_t rp_adv(RpCtx& x, int i, int64_t t) {
+  const RpNode& nd = x.J->node[i];
+  const int64_t n = x.n;
+  switch (nd.kind) {
+    case RP_DOCS: {
+      const int64_t d = rp_next_set(nd.mask, t, n);
+      x.a[i] = d < n ? d + 1 : n;
+      return d < n ? d : kRpEof;
+    }
+    case RP_ALL:
+      x.a[i] = t;
+      return rp_next<D>(x, i);
+    case RP_SCAN:
+      x.b[i] = x.c[i] = 0;  // (the batch is dropped)
+      return rp_scan_from(x, i, t);
+    case RP_AND:
+      x.a[i] = t;
+      return rp_next<D>(x, i);
+    case RP_OR: {
+      int64_t best = kRpEof;
+      for (int j = 0; j < nd.nchild; ++j) {
+        const int k = x.J->kids[nd.first + j];
+        if (!x.live[k]) continue;
+        int64_t d = x.nd[k];
+        if (d < t) {
+          d = rp_adv_child<D>(x, k, t);
+          x.nd[k] = d;
+          if (d == kRpEof) {
+            x.live[k] = false;
+            continue;
+          }
+        }
+        best = best == kRpEof || d < best ? d : best;
+      }
+      if (best != kRpEof) x.a[i] = best;
+      return best;
+    }
+    case RP_NOT: {
+      x.a[i] = t;
+      if (t > x.b[i]) {
+        const int64_t c = rp_adv_child<D>(x, x.J->kids[nd.first], t);
+        x.b[i] = c == kRpEof ? n : c;
+      }
+      return rp_next<D>(x, i);
+    }
+    default:
+      return kRpEof;
+  }
+}
+
+// NotDocIdIterator's constructor: its child's first next()
+template <int D>
+__device__ void rp_construct_not(RpCtx& x, int i, int depth) {
+  if constexpr (D < kRpMaxDepth) {
+    if (depth != D) {
+      rp_construct_not<D + 1>(x, i, depth);
+      return;
+    }
+    const int64_t c = rp_next_child<D>(x, x.J->kids[x.J->node[i].first]);
+    x.a[i] = 0;
+    x.b[i] = c == kRpEof ? x.n : c;
+  }
+}
+}  // namespace
+
+__global__ void __launch_bounds__(64) stat_replay_kernel(const RpJob* __restrict__ jobs, int nj) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nj) return;
+  RpCtx x;
+  x.J = jobs + j;
+  x.n = x.J->num_docs;
+  x.ent = 0;
+  for (int i = 0; i < kRpMaxNodes; ++i) {
+    x.a[i] = x.b[i] = x.c[i] = 0;
+    x.nd[i] = -1;
+    x.live[i] = true;
+  }
+  // every OR's cached answers start below doc 0 (OrDocIdIterator: _nextDocIds = -1, _previousDocId = -1)
+  for (int i = 0; i < x.J->nnodes; ++i)
+    if (x.J->node[i].kind == RP_OR) x.a[i] = -1;
+  // iterator construction, children before parents (reverse pre-order): each NOT reads its child's first answer
+  for (int i = x.J->nnodes - 1; i >= 0; --i)
+    if (x.J->node[i].kind == RP_NOT) rp_construct_not<0>(x, i, x.J->node[i].depth);
+  // the projection: next() until EOF; every call returns a larger doc, so n + 1 calls end it (a bound every thread
+  // reaches whatever the tree)
+  bool done = false;
+  for (int64_t it = 0; it <= x.n + 1; ++it)
+    if (rp_next<0>(x, x.J->root) == kRpEof) {
+      done = true;
+      break;
+    }
+  *x.J->out = done ? x.ent : ~0ull;
+}
+
+hipError_t launch_stat_replay(const RpJob* jobs, int nj, hipStream_t s) {
+  if (nj == 0) return hipSuccess;
+  stat_replay_kernel<<<(unsigned)((nj + 63) / 64), 64, 0, s>>>(jobs, nj);
+  return hipGetLastError();
+}
+
 }  // namespace pa

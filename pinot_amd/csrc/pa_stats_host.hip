@@ -503,6 +503,134 @@ int64_t cost_next(const Ctx& x, int i, bool tail) {
   throw Unsupported{};
 }
 
+// ---------------------------------------------------------------- iterator replay (stat_replay_kernel)
+// The filter shapes the reduction above leaves out are replayed on the GPU, iterator by iterator. The host builds the
+// iterator tree BlockDocIdSet.iterator() builds (filter_stats._iterator restated): AndDocIdSet's merge of index children
+// and applyAnd over its scan children (counted here, as popcounts), OrDocIdSet's merge of sorted children.
+struct RNode {
+  int32_t kind = RP_EMPTY;
+  bool sorted = false;        // RP_DOCS of a sorted index (the only kind OrDocIdSet merges)
+  std::vector<int32_t> prog;  // RP_DOCS / RP_SCAN: the doc set
+  int32_t mv = -1;            // RP_SCAN over a multi-value column
+  std::vector<int> kids;
+};
+struct Replay {
+  std::vector<RNode> nodes;
+  int root = -1;
+};
+
+int replay_build(const Ctx& x, int i, Replay& R) {
+  const pa_filter_op& o = x.ops[i];
+  auto add = [&](RNode n) {
+    if (R.nodes.size() >= 4 * (size_t)kRpMaxNodes) throw Unsupported{};
+    R.nodes.push_back(std::move(n));
+    return (int)R.nodes.size() - 1;
+  };
+  RNode n;
+  switch (o.kind) {
+    case PA_FOP_EMPTY:
+      n.kind = RP_EMPTY;
+      return add(n);
+    case PA_FOP_MATCH_ALL:
+      n.kind = RP_ALL;
+      return add(n);
+    case PA_FOP_SORTED:
+    case PA_FOP_BITMAP:
+      n.kind = RP_DOCS;
+      n.sorted = o.kind == PA_FOP_SORTED;
+      n.prog = prog_of(o);
+      return add(n);
+    case PA_FOP_SCAN:
+      n.kind = RP_SCAN;
+      n.prog = prog_of(o);
+      if (o.mv_column >= 0) {
+        mv_col(x, o.mv_column);
+        n.mv = o.mv_column;
+      }
+      return add(n);
+    case PA_FOP_NOT: {
+      const int c = replay_build(x, i + 1, R);
+      n.kind = RP_NOT;
+      n.kids = {c};
+      return add(n);
+    }
+    default:
+      break;
+  }
+  std::vector<int> its;
+  for (int k : children(x, i)) its.push_back(replay_build(x, k, R));
+  auto docs = [&](int k) { return R.nodes[k].kind == RP_DOCS; };
+  if (o.kind == PA_FOP_OR) {
+    // OrDocIdSet.java:63-127: more than one index child merge into one doc set; the reference collects only the sorted
+    // ones (its bitmap-based list stays empty), and a bitmap-based child is then neither merged nor kept
+    std::vector<int> srt, rest;
+    for (int k : its) {
+      if (docs(k) && R.nodes[k].sorted) srt.push_back(k);
+      if (!docs(k)) rest.push_back(k);
+    }
+    if (srt.size() > 1) {
+      RNode m;
+      m.kind = RP_DOCS;
+      for (int k : srt) m.prog = prog_join(m.prog, R.nodes[k].prog, PA_BIT_OR);
+      const int mi = add(m);
+      if (rest.empty()) return mi;
+      n.kids = {mi};
+      n.kids.insert(n.kids.end(), rest.begin(), rest.end());
+    } else {
+      n.kids = its;
+    }
+    n.kind = RP_OR;
+    return add(n);
+  }
+  // AndDocIdSet.java:72-186: index children intersect, each scan child applyAnd-reads the survivors in order
+  std::vector<int> idx, scans, rest;
+  for (int k : its) {
+    if (docs(k)) idx.push_back(k);
+    else if (R.nodes[k].kind == RP_SCAN) scans.push_back(k);
+    else rest.push_back(k);
+  }
+  if ((!idx.empty() && !scans.empty()) || idx.size() > 1) {
+    std::vector<int32_t> D;
+    for (int k : idx) D = prog_join(D, R.nodes[k].prog, PA_BIT_AND);
+    for (int k : scans) {
+      x.P->counts.push_back({D, R.nodes[k].mv});
+      D = prog_join(D, R.nodes[k].prog, PA_BIT_AND);
+    }
+    RNode m;
+    m.kind = RP_DOCS;
+    m.prog = D;
+    const int mi = add(m);
+    if (rest.empty()) return mi;
+    n.kids = {mi};
+    n.kids.insert(n.kids.end(), rest.begin(), rest.end());
+  } else {
+    n.kids = its;
+  }
+  n.kind = RP_AND;
+  return add(n);
+}
+
+// the reachable tree in pre-order (a node before its children), as the kernel reads it; the programs per node
+struct ReplayFlat {
+  std::vector<RNode> nodes;  // kids renumbered
+  std::vector<int32_t> depth;
+};
+ReplayFlat replay_flatten(const Replay& R) {
+  ReplayFlat F;
+  std::function<int(int, int)> emit = [&](int r, int d) -> int {
+    if (d >= kRpMaxDepth || F.nodes.size() >= (size_t)kRpMaxNodes) throw Unsupported{};
+    const int me = (int)F.nodes.size();
+    F.nodes.push_back(R.nodes[r]);
+    F.depth.push_back(d);
+    std::vector<int> ch;
+    for (int c : R.nodes[r].kids) ch.push_back(emit(c, d + 1));
+    F.nodes[me].kids = ch;
+    return me;
+  };
+  emit(R.root, 0);
+  return F;
+}
+
 int check_tree(const pa_filter_op* ops, int nops, int root, int num_leaves) {
   const int end = extent(ops, nops, root);
   if (end < 0) return fail(PA_EINVAL, "execution stats: malformed operator tree");
@@ -556,7 +684,8 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
     if (rc) return rc;
   }
   std::vector<Plan> plans(q->nseg);
-  std::vector<int> state(q->nseg, 0);  // 0: plan, 1: constant known (fused / non-scan), -1: host
+  std::vector<int> state(q->nseg, 0);  // 0: plan, 1: constant known (fused / non-scan), 2: GPU replay, -1: host
+  std::vector<std::pair<int, ReplayFlat>> replays;
   std::vector<int64_t> seg_in(q->nseg, 0);
   int64_t non_scan_docs = 0;
   for (int si = 0; si < q->nseg; ++si) {
@@ -589,8 +718,18 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
     try {
       seg_in[si] = cost_next(x, root, false);
     } catch (const Unsupported&) {
+      // outside the reduction: the iterator tree replayed on the GPU (stat_replay_kernel), else on the host
       plans[si] = Plan{};
-      state[si] = -1;
+      seg_in[si] = 0;
+      try {
+        Replay R;
+        R.root = replay_build(x, root, R);
+        replays.push_back({si, replay_flatten(R)});
+        state[si] = 2;
+      } catch (const Unsupported&) {
+        plans[si] = Plan{};
+        state[si] = -1;
+      }
     }
   }
   // GPU work: leaf bitmaps of the segments with counts or leap-frogs, their element masks, the counts, the leap-frogs
@@ -615,8 +754,11 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
   std::vector<CountReq> creq;
   std::vector<LeapReq> lreq, breq;  // breq: two single-value scans leap-frogged (closed form over label counts)
   std::vector<char> seg_bm(q->nseg, 0);
+  for (const auto& rp : replays)
+    for (const RNode& nd : rp.second.nodes)
+      if (nd.kind == RP_DOCS || nd.kind == RP_SCAN) mask_of(rp.first, nd.prog);
   for (int si = 0; si < q->nseg; ++si) {
-    if (state[si] != 0) continue;
+    if (state[si] != 0 && state[si] != 2) continue;
     for (const auto& c : plans[si].counts) creq.push_back(CountReq{si, mask_of(si, c.first), c.second});
     for (const Leap& lp : plans[si].leaps) {
       if (lp.el.size() == 2 && !lp.tail && lp.el[0].kind == LF_SCAN && lp.el[1].kind == LF_SCAN && lp.el[0].mv < 0 &&
@@ -635,7 +777,7 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
   }
   for (const auto& m : masks) seg_bm[m.first] = 1;
   int gpu_segs = 0;
-  if (!masks.empty() || !breq.empty()) {
+  if (!masks.empty() || !breq.empty() || !replays.empty()) {
     for (int l = 0; l < nl; ++l)
       if (leaf_lit[l] < 0) return fail(PA_EUNSUPPORTED, "filter leaf " + std::to_string(l) + " has no literal in the plan");
     std::vector<int64_t> bm_off(q->nseg, -1);
@@ -735,7 +877,7 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
         lblocks += leaf_bitmap_blocks(n);
       }
     }
-    const size_t nres = creq.size() + 3 * lreq.size() + 4 * breq.size();
+    const size_t nres = creq.size() + 3 * lreq.size() + 4 * breq.size() + replays.size();
     const size_t o_bm = 0, o_mk = align256(4 * bm_words), o_cells = o_mk + align256(4 * mk_words),
                  o_res = o_cells + align256(4 * std::max<size_t>(1, cell_words)),
                  o_bsc = o_res + align256(8 * std::max<size_t>(1, nres)),
@@ -747,7 +889,8 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
                  o_lj = o_cj + align256(sizeof(StatCountJob) * std::max<size_t>(1, cjobs.size())),
                  o_fj = o_lj + align256(sizeof(LfJob) * std::max<size_t>(1, ljobs.size())),
                  o_tok = o_fj + align256(sizeof(LeafJob) * std::max<size_t>(1, leafjobs.size())),
-                 total = o_tok + 4 * std::max<size_t>(1, toks.size());
+                 o_rp = o_tok + align256(4 * std::max<size_t>(1, toks.size())),
+                 total = o_rp + sizeof(RpJob) * std::max<size_t>(1, replays.size());
     if (q->stat_buf.n < total) {
       dev_free(q->stat_buf);
       int rc = dev_alloc(q->stat_buf, total);
@@ -787,6 +930,32 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
       j.out = res + creq.size() + 3 * r;
     }
     for (LeafJob& lj : leafjobs) lj.out = (uint32_t*)(base + o_bm) + (intptr_t)lj.out;
+    const size_t rres = creq.size() + 3 * lreq.size() + 4 * breq.size();
+    std::vector<RpJob> rjobs(replays.size());
+    for (size_t r = 0; r < replays.size(); ++r) {
+      const int si = replays[r].first;
+      const ReplayFlat& F = replays[r].second;
+      RpJob& j = rjobs[r];
+      std::memset(&j, 0, sizeof(j));
+      j.num_docs = q->segs[si]->num_docs;
+      j.nnodes = (int32_t)F.nodes.size();
+      j.root = 0;
+      int nk = 0;
+      for (size_t i = 0; i < F.nodes.size(); ++i) {
+        const RNode& nd = F.nodes[i];
+        RpNode& o = j.node[i];
+        o.kind = nd.kind;
+        o.depth = F.depth[i];
+        o.first = nk;
+        o.nchild = (int32_t)nd.kids.size();
+        for (int c : nd.kids) j.kids[nk++] = c;
+        if (nd.kind == RP_DOCS || nd.kind == RP_SCAN) o.mask = mk + mk_off[mask_id.at(std::make_pair(si, nd.prog))];
+        if (nd.mv >= 0) o.wt = (const int32_t*)q->segs[si]->cols.at(nd.mv)->mv_off.p;
+      }
+      j.out = res + rres + r;
+    }
+    if (!rjobs.empty())
+      PA_HIP(hipMemcpyAsync(base + o_rp, rjobs.data(), sizeof(RpJob) * rjobs.size(), hipMemcpyHostToDevice, st));
     const size_t bres = creq.size() + 3 * lreq.size();
     for (size_t r = 0; r < breq.size(); ++r) {
       BitJob& j = bjobs[r];
@@ -818,6 +987,7 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
     PA_HIP(launch_leapfrogs((const LfJob*)(base + o_lj), (int)ljobs.size(), lanes, st));
     PA_HIP(launch_bit_counts_batch((const BitJob*)(base + o_bj), (int)bjobs.size(), bblocks, true,
                                    (int32_t*)(base + o_btab), st));
+    PA_HIP(launch_stat_replay((const RpJob*)(base + o_rp), (int)rjobs.size(), st));
     std::vector<int64_t> h(std::max<size_t>(1, nres));
     PA_HIP(hipMemcpyAsync(h.data(), res, 8 * h.size(), hipMemcpyDeviceToHost, st));
     PA_HIP(hipStreamSynchronize(st));
@@ -826,6 +996,10 @@ int pa_query_execution_stats(pa_query* q, int32_t num_ops, const pa_filter_op* o
       seg_in[lreq[r].si] += h[creq.size() + 3 * r] + (lreq[r].lp->tail ? h[creq.size() + 3 * r + 1] : 0);
     for (size_t r = 0; r < breq.size(); ++r)
       seg_in[breq[r].si] += (int64_t)q->segs[breq[r].si]->num_docs + h[bres + 4 * r + 2] + h[bres + 4 * r + 3];
+    for (size_t r = 0; r < replays.size(); ++r) {
+      if ((uint64_t)h[rres + r] == ~0ull) return fail(PA_EHIP, "execution stats: iterator replay did not finish");
+      seg_in[replays[r].first] += h[rres + r];
+    }
   }
   int64_t in_filter = 0;
   for (int si = 0; si < q->nseg; ++si) {

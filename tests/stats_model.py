@@ -275,8 +275,229 @@ def leapfrog(el, tail_wanted, seg, chunk=64):
     return cost, tl, matched
 
 
-def execution_stats(ops, roots, seg_tree, segs, ncols, docs_scanned, chunk=64):
-    """(in filter, post filter, per-segment in filter with -1 for host-replayed segments)."""
+# ------------------------------------------------------------------ iterator replay (pa_stats.hip stat_replay_kernel)
+RP_EMPTY, RP_ALL, RP_DOCS, RP_SCAN, RP_AND, RP_OR, RP_NOT = range(7)
+RP_MAX_NODES, RP_MAX_DEPTH = 24, 6
+EOF_ = -1
+
+
+def replay_build(ops, i, seg, counts, nodes):
+    """pa_stats_host.hip replay_build: the iterator tree BlockDocIdSet.iterator() builds, applyAnd reads into counts.
+    nodes: list of [kind, sorted, prog, mv, kids]; returns the node index."""
+    o = ops[i]
+    kd = o[0]
+
+    def add(n):
+        if len(nodes) >= 4 * RP_MAX_NODES:
+            raise Unsupported("replay tree too large")
+        nodes.append(n)
+        return len(nodes) - 1
+    if kd == L.PA_FOP_EMPTY:
+        return add([RP_EMPTY, False, [], -1, []])
+    if kd == L.PA_FOP_MATCH_ALL:
+        return add([RP_ALL, False, [], -1, []])
+    if kd in (L.PA_FOP_SORTED, L.PA_FOP_BITMAP):
+        return add([RP_DOCS, kd == L.PA_FOP_SORTED, _prog(o), -1, []])
+    if kd == L.PA_FOP_SCAN:
+        return add([RP_SCAN, False, _prog(o), _mv(seg, o[2]) if o[2] >= 0 else -1, []])
+    if kd == L.PA_FOP_NOT:
+        c = replay_build(ops, i + 1, seg, counts, nodes)
+        return add([RP_NOT, False, [], -1, [c]])
+    its = [replay_build(ops, k, seg, counts, nodes) for k in _children(ops, i)]
+    docs = [k for k in its if nodes[k][0] == RP_DOCS]
+    if kd == L.PA_FOP_OR:
+        srt = [k for k in docs if nodes[k][1]]
+        rest = [k for k in its if nodes[k][0] != RP_DOCS]
+        if len(srt) > 1:  # (OrDocIdSet: bitmap-based children neither merged nor kept, as the reference)
+            prog = []
+            for k in srt:
+                prog = _join(prog, nodes[k][2], L.PA_BIT_OR)
+            m = add([RP_DOCS, False, prog, -1, []])
+            return m if not rest else add([RP_OR, False, [], -1, [m] + rest])
+        return add([RP_OR, False, [], -1, its])
+    scans = [k for k in its if nodes[k][0] == RP_SCAN]
+    rest = [k for k in its if nodes[k][0] not in (RP_DOCS, RP_SCAN)]
+    if (docs and scans) or len(docs) > 1:
+        D = []
+        for k in docs:
+            D = _join(D, nodes[k][2], L.PA_BIT_AND)
+        for k in scans:
+            counts.append((D, nodes[k][3]))
+            D = _join(D, nodes[k][2], L.PA_BIT_AND)
+        m = add([RP_DOCS, False, D, -1, []])
+        return m if not rest else add([RP_AND, False, [], -1, [m] + rest])
+    return add([RP_AND, False, [], -1, its])
+
+
+def replay_flatten(nodes, root):
+    """Pre-order reachable tree, depth- and size-limited as the kernel's job."""
+    out, depth = [], []
+
+    def emit(r, d):
+        if d >= RP_MAX_DEPTH or len(out) >= RP_MAX_NODES:
+            raise Unsupported("replay tree too deep / large")
+        me = len(out)
+        out.append(list(nodes[r]))
+        depth.append(d)
+        out[me][4] = [emit(c, d + 1) for c in nodes[r][4]]
+        return me
+    emit(root, 0)
+    return out, depth
+
+
+def replay(flat, depth, seg):
+    """stat_replay_kernel restated: the projection's next() until EOF over the node machine; entries read."""
+    n = seg.n
+    masks = [eval_prog(nd[2], seg.leaves, n) if nd[0] in (RP_DOCS, RP_SCAN) else None for nd in flat]
+    wts = [np.concatenate([[0], np.cumsum(seg.weights[nd[3]])]) if nd[0] == RP_SCAN and nd[3] >= 0 else None
+           for nd in flat]
+    N = len(flat)
+    a, b, c = [0] * N, [0] * N, [0] * N
+    nd_, live = [-1] * N, [True] * N
+    ent = [0]
+
+    def next_set(m, t, e):
+        if t >= e:
+            return e
+        z = np.flatnonzero(m[t:e])
+        return t + int(z[0]) if len(z) else e
+
+    def read(i, lo, hi):
+        ent[0] += int(wts[i][hi] - wts[i][lo]) if wts[i] is not None else hi - lo
+
+    def scan_from(i, start):
+        d = next_set(masks[i], start, n)
+        if d < n:
+            read(i, start, d + 1)
+            a[i] = d + 1
+            return d
+        if start < n:
+            read(i, start, n)
+        a[i] = max(start, n)
+        return EOF_
+
+    def nxt(i):
+        k = flat[i][0]
+        if k == RP_DOCS:
+            d = next_set(masks[i], a[i], n)
+            a[i] = d + 1 if d < n else n
+            return d if d < n else EOF_
+        if k == RP_ALL:
+            if a[i] < n:
+                a[i] += 1
+                return a[i] - 1
+            return EOF_
+        if k == RP_SCAN:
+            if wts[i] is not None:
+                return scan_from(i, a[i])
+            while True:
+                if b[i] < c[i]:
+                    d = next_set(masks[i], b[i], c[i])
+                    if d < c[i]:
+                        b[i] = d + 1
+                        return d
+                    b[i] = c[i]
+                limit = min(n - a[i], 256)
+                if limit <= 0:
+                    return EOF_
+                ent[0] += limit
+                b[i], c[i] = a[i], a[i] + limit
+                a[i] += limit
+        if k == RP_AND:
+            kids = flat[i][4]
+            mx, mi, idx = a[i], -1, 0
+            while idx < len(kids):
+                if idx == mi:
+                    idx += 1
+                    continue
+                d = adv(kids[idx], mx)
+                if d == EOF_:
+                    return EOF_
+                if d == mx:
+                    idx += 1
+                else:
+                    mx, mi, idx = d, idx, 0
+            a[i] = mx + 1
+            return mx
+        if k == RP_OR:
+            best = EOF_
+            for kk in flat[i][4]:
+                if not live[kk]:
+                    continue
+                d = nd_[kk]
+                if d == a[i]:
+                    d = nxt(kk)
+                    nd_[kk] = d
+                    if d == EOF_:
+                        live[kk] = False
+                        continue
+                best = d if best == EOF_ or d < best else best
+            if best != EOF_:
+                a[i] = best
+            return best
+        if k == RP_NOT:
+            kk = flat[i][4][0]
+            while a[i] == b[i]:
+                a[i] += 1
+                d = nxt(kk)
+                b[i] = n if d == EOF_ else d
+            if a[i] >= n:
+                return EOF_
+            a[i] += 1
+            return a[i] - 1
+        return EOF_
+
+    def adv(i, t):
+        k = flat[i][0]
+        if k == RP_DOCS:
+            d = next_set(masks[i], t, n)
+            a[i] = d + 1 if d < n else n
+            return d if d < n else EOF_
+        if k in (RP_ALL, RP_AND):
+            a[i] = t
+            return nxt(i)
+        if k == RP_SCAN:
+            b[i] = c[i] = 0
+            return scan_from(i, t)
+        if k == RP_OR:
+            best = EOF_
+            for kk in flat[i][4]:
+                if not live[kk]:
+                    continue
+                d = nd_[kk]
+                if d < t:
+                    d = adv(kk, t)
+                    nd_[kk] = d
+                    if d == EOF_:
+                        live[kk] = False
+                        continue
+                best = d if best == EOF_ or d < best else best
+            if best != EOF_:
+                a[i] = best
+            return best
+        if k == RP_NOT:
+            a[i] = t
+            if t > b[i]:
+                d = adv(flat[i][4][0], t)
+                b[i] = n if d == EOF_ else d
+            return nxt(i)
+        return EOF_
+
+    for i in range(N):
+        if flat[i][0] == RP_OR:
+            a[i] = -1
+    for i in reversed(range(N)):
+        if flat[i][0] == RP_NOT:
+            d = nxt(flat[i][4][0])
+            a[i], b[i] = 0, n if d == EOF_ else d
+    while nxt(0) != EOF_:
+        pass
+    return ent[0]
+
+
+def execution_stats(ops, roots, seg_tree, segs, ncols, docs_scanned, chunk=64, replayed=None):
+    """(in filter, post filter, per-segment in filter with -1 for host-replayed segments). Segments outside the
+    reduction are replayed iterator by iterator (stat_replay_kernel); replayed (a list) collects their indices."""
     per = []
     non_scan = 0
     for si, seg in enumerate(segs):
@@ -292,8 +513,17 @@ def execution_stats(ops, roots, seg_tree, segs, ncols, docs_scanned, chunk=64):
         try:
             v = _cost_next(ops, int(roots[t]), seg, counts, leaps, False)
         except Unsupported:
-            per.append(-1)
-            continue
+            counts, leaps = [], []
+            try:
+                nodes = []
+                root = replay_build(ops, int(roots[t]), seg, counts, nodes)
+                flat, depth = replay_flatten(nodes, root)
+                v = replay(flat, depth, seg)
+            except Unsupported:
+                per.append(-1)
+                continue
+            if replayed is not None:
+                replayed.append(si)
         for prog, mv in counts:
             m = eval_prog(prog, seg.leaves, seg.n)
             v += int(seg.weights[mv][m].sum()) if mv >= 0 else int(m.sum())

@@ -217,41 +217,44 @@ CLOSED_FORM_WHERES = [
     "(a < 20 AND b < 30) OR (c = 2 AND a > 70) OR NOT (b < 50 AND a > 10)", "NOT (a < 95 AND b < 95 AND c < 19)",
 ]
 # outside the engine (documented in filter_stats "device path"): the host replays these segments
-HOST_WHERES = ["a < 50 AND NOT (b < 10 OR c = 2)", "a < 50 AND (b < 10 OR NOT c = 3)",
-               "NOT (a < 10 AND (b < 20 OR c = 1))"]
+# the shapes outside the reduction (a NOT child of a leap-frogging AND, an AND / NOT under an OR inside a leap-frog, a
+# NOT over a leap-frog with an OR child): the GPU iterator replay counts them (stat_replay_kernel)
+REPLAY_WHERES = ["a < 50 AND NOT (b < 10 OR c = 2)", "a < 50 AND (b < 10 OR NOT c = 3)",
+                 "NOT (a < 10 AND (b < 20 OR c = 1))", "NOT a IN (3, 5) AND b < 9",
+                 "a < 60 AND (c = 3 OR (a > 7 AND b > 70))", "NOT (b > 40) AND (a < 30 OR NOT c = 1)"]
+HOST_WHERES = REPLAY_WHERES  # (former name)
 # (the same lists, by name, for the GPU test)
 ENGINE_WHERES = CLOSED_FORM_WHERES
 
 
-def _model_stats(q, segs, masks, chunk, params=None):
+def _model_stats(q, segs, masks, chunk, params=None, replayed=None):
     import stats_model as M
     ops, roots, seg_tree = FS.operator_trees(q, segs, params, {})
     msegs = [M.Seg(s.num_docs, masks[i]) for i, s in enumerate(segs)]
     docs = sum(int(FS.filter_mask(q.filter, s, masks[i]).sum()) if q.filter is not None else s.num_docs
                for i, s in enumerate(segs))
-    return M.execution_stats(ops, roots, seg_tree, msegs, FS.projected_columns(q), docs, chunk)
+    return M.execution_stats(ops, roots, seg_tree, msegs, FS.projected_columns(q), docs, chunk, replayed)
 
 
-@pytest.mark.parametrize("where", CLOSED_FORM_WHERES + HOST_WHERES)
+@pytest.mark.parametrize("where", CLOSED_FORM_WHERES + REPLAY_WHERES)
 def test_engine_model_matches_replay(where):
-    """The statistics engine's algorithm (tests/stats_model.py: the operator-tree reduction of pa_capi.hip and the
+    """The statistics engine's algorithm (tests/stats_model.py: the operator-tree reduction of pa_stats_host.hip, the
     chunked leap-frog of pa_stats.hip, restated on the CPU with small chunks so the chunk boundaries and the chaining
-    are exercised) = the iterator replay, per segment; the replay is needed only for the HOST_WHERES shapes."""
+    are exercised, and the GPU iterator replay of the shapes outside the reduction: the REPLAY_WHERES) = the host's
+    iterator replay (filter_stats.server_stats), per segment; no segment is left to the host."""
     segs = [_seg(3000, 3), _seg(4097, 4), _seg(257, 5)]
     for sql in ("SELECT COUNT(*) FROM t WHERE " + where, "SELECT c, SUM(a) FROM t WHERE %s GROUP BY c" % where):
         q = parse_sql(sql)
         masks = [leaf_masks(q, s) for s in segs]
         want_per = [FS.server_stats(q, [s], lambda si, i=i: masks[i]) for i, s in enumerate(segs)]
         for chunk in (64, 5, 2048):
-            in_f, post, per = _model_stats(q, segs, masks, chunk)
+            replayed = []
+            in_f, post, per = _model_stats(q, segs, masks, chunk, replayed=replayed)
             for i in range(len(segs)):
-                if per[i] < 0:
-                    assert where in HOST_WHERES, "engine expected for " + where
-                else:
-                    assert per[i] == want_per[i][0], (sql, chunk, i)
+                assert per[i] >= 0, (sql, i)
+                assert per[i] == want_per[i][0], (sql, chunk, i)
             assert post == sum(w[1] for w in want_per), sql
-            if where in HOST_WHERES:
-                assert any(p < 0 for p in per), where
+            assert bool(replayed) == (where in REPLAY_WHERES), (where, replayed)
 
 
 def test_engine_model_golden_statistics(golden_spec, golden_segment):

@@ -90,6 +90,7 @@ QUERIES = (
 @pytest.mark.parametrize("nd", ["16", "8"])
 @pytest.mark.parametrize("flags", [0, L.PA_QF_GD_DRAIN_EACH_TILE])
 def test_own_dictionaries_on_the_specialised_kernel(partitions, monkeypatch, nd, flags):
+    """Every QUERIES shape with 16 or 8 docs per lane."""
     segs, gs = partitions
     monkeypatch.setenv("PA_GDL_ND", nd)
     for sql in QUERIES:

@@ -18,7 +18,7 @@ from pinot_amd import filter_stats as FS
 from pinot_amd import parse_sql
 from pinot_amd.engine import GpuQueryExecutor, GpuSegment
 from pinot_amd.segment import create_segment
-from test_filter_stats import ENGINE_WHERES, HOST_WHERES, _np_prog, np_leaps
+from test_filter_stats import ENGINE_WHERES, REPLAY_WHERES, _np_prog, np_leaps
 
 pytestmark = pytest.mark.gpu
 
@@ -87,9 +87,10 @@ def _stats_and_replay(ex):
 
 
 def test_execution_stats_device_vs_replay():
-    """Every filter shape of test_filter_stats (the engine's list and the host-replayed ones) over 3 segments of up to
-    200K docs (the leap-frogs cross many 2048-doc chunks): the statistics the fetch fills = the host replay over the
-    same GPU bitmaps, and no segment is replayed for the engine's shapes."""
+    """Every filter shape of test_filter_stats over 3 segments of up to 200K docs (the leap-frogs cross many 2048-doc
+    chunks): the statistics the fetch fills = the host replay over the same GPU bitmaps, and the host replay is never
+    used — the shapes outside the reduction (REPLAY_WHERES, a NOT child of a leap-frogging AND) are replayed iterator by
+    iterator on the GPU (stat_replay_kernel)."""
     segs = [_segment(1, 200_003), _segment(2, 70_000), _segment(3, 1025)]
     gs = [GpuSegment(s) for s in segs]
     try:
@@ -97,8 +98,8 @@ def test_execution_stats_device_vs_replay():
         extra = ["r < 1000 AND a < 50", "r BETWEEN 10 AND 20 OR b = 3", "w < 300000 AND b < 40",
                  "w IN (5, 77, 1000) OR a = 1", "r IN (3, 5, 7, 4000) AND b < 50",
                  "w < 600000 AND (a < 5 OR r < 200) AND b > 20", "NOT (w < 900000 AND r > 40 AND b < 90)"]
-        host = HOST_WHERES + ["NOT r IN (3, 5) AND a < 9"]  # (a NOT child of a leap-frogging AND: replayed)
-        for where in ENGINE_WHERES + extra + host:
+        replay = REPLAY_WHERES + ["NOT r IN (3, 5) AND a < 9", "w < 500000 AND NOT (r < 100 OR b > 60)"]
+        for where in ENGINE_WHERES + extra + replay:
             for sql in ("SELECT COUNT(*) FROM t WHERE " + where, "SELECT c, SUM(a) FROM t WHERE %s GROUP BY c" % where):
                 ex = GpuQueryExecutor(parse_sql(sql), gs)
                 try:
@@ -107,8 +108,7 @@ def test_execution_stats_device_vs_replay():
                 finally:
                     ex.close()
                 assert got == want, sql
-                if where not in host:
-                    assert replayed == 0, sql
+                assert replayed == 0, sql
     finally:
         for g in gs:
             g.close()

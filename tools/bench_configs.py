@@ -43,6 +43,17 @@ def highcard_segment(seed, docs):
         "m": sv_spec(rng, docs, 1 << 16, "LONG")})
 
 
+def highcard_own_segment(seed, docs):
+    """configs[2] where every segment built its own dictionaries (SegmentDictionaryCreator.java:104): d1 / d2 runs of 1024
+    values starting at a per-segment shift (0..7) of the table-wide 1031-value dictionaries (~1.06M keys), m 65536
+    values from a per-segment offset (the table-wide value dictionary is their union)."""
+    from pinot_amd.segment import segment_from_dict_ids
+    rng = np.random.default_rng(seed)
+    return segment_from_dict_ids("hco%d" % seed, docs, {
+        "d1": sv_spec(rng, docs, 1024, base=1000 + seed % 8), "d2": sv_spec(rng, docs, 1024, base=5000 + (3 * seed) % 8),
+        "m": sv_spec(rng, docs, 1 << 16, "LONG", base=(611 * seed) % 4096)})
+
+
 def highcard_rd_segment(seed, docs):
     """configs[2] with a non-arithmetic value dictionary: m's 65536 values are sorted random distinct longs, so pass C
     looks every SUM value up in the dictionary (the affine shortcut does not apply)."""
@@ -147,6 +158,14 @@ WORKLOADS = {
         ("sum_only", "SELECT d1, d2, SUM(m) FROM t GROUP BY d1, d2 LIMIT 2000000 "
                      "OPTION(numGroupsLimit=2000000)", 0),
         # the default numGroupsLimit (100000 < 1M keys): first-seen trimming per segment (a11)
+        ("default_limit", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000", 0),
+    ]),
+    # configs[2] over segments with their own dictionaries (count-free emit: per-segment key / value id offsets)
+    "highcard_own": (highcard_own_segment, [
+        ("all_docs", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000 "
+                     "OPTION(numGroupsLimit=2000000)", 0),
+        ("filtered_10pct", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t WHERE m < 6554 GROUP BY d1, d2 "
+                           "LIMIT 2000000 OPTION(numGroupsLimit=2000000)", 0),
         ("default_limit", "SELECT d1, d2, SUM(m), MIN(m), MAX(m) FROM t GROUP BY d1, d2 LIMIT 2000000", 0),
     ]),
     "highcard_rd": (highcard_rd_segment, [
