@@ -9,7 +9,9 @@
 //  * column widths per segment: each distinct width tuple is a class (JIT_NCLS <= 4), the tile body and its DMA are
 //    instantiated per class and a segment switch picks one (a scalar branch);
 //  * the group key: a segment whose dictionary is a contiguous run of the table dictionary (time partitions) shifts its
-//    box by an offset (JitSeg.key_lo); otherwise every segment reads a dictId -> table key table (JIT_KTAB);
+//    box by an offset; otherwise every segment reads a dictId -> table key table (JIT_KTAB). The packed rows are
+//    indexed by the segment's local keys (JitSeg lbase / lspan / gofs), replicated JIT_RR times when few keys per segment
+//    leave room (a time partition's handful of days: no same-address atomics), and drained at segment switches;
 //  * DICT_SET bitmaps, value tables and key tables that differ per segment live in LDS table slots: a workgroup's tile
 //    range spans at most JIT_NSLOT segments, whose tables it loads when it starts; tables every segment shares sit in
 //    one shared area;
@@ -33,7 +35,8 @@
 //          JIT_ATS {1: table in the slot}, JIT_AO {1: + the segment's dictId offset, folded in at the drain},
 //          JIT_AS {bit offset of the field},
 //          JIT_OC bit offset of the COUNT field
-//   JIT_DRAIN tiles between drains of a wave's packed rows, JIT_RS waves sharing one set of rows
+//   JIT_DRAIN tiles between drains of a wave's packed rows, JIT_RS waves sharing one set of rows, JIT_RR replicas of
+//   JIT_LMAX rows, JIT_SEGDRAIN drains at segment switches
 //   JIT_L_SUM {LDS byte offset of each SUM's accumulators}, JIT_L_SLOT / JIT_SLOT_B / JIT_NSLOT the table slots,
 //   JIT_L_ROWS, JIT_L_RING (LDS byte offsets)
 typedef unsigned int u32;
@@ -47,11 +50,23 @@ typedef __attribute__((address_space(3))) u64 l64;
 #ifndef JIT_RS
 #define JIT_RS 1  // waves sharing one set of packed rows (2: half the rows' LDS, drained by atomic exchange)
 #endif
+#ifndef JIT_RR
+#define JIT_RR 1  // replicas of each row: lane l updates replica l % JIT_RR (few keys per segment: no same-address atomics)
+#endif
+#ifndef JIT_LMAX
+#define JIT_LMAX 1  // rows (keys) per replica: the largest number of box keys one segment holds
+#endif
+#ifndef JIT_SEGDRAIN
+#define JIT_SEGDRAIN 0  // the rows are drained at every segment switch (their local keys / offsets change there)
+#endif
 #ifndef JIT_DBG
 #define JIT_DBG 0  // measurement only (PA_GDL_DBG; results invalid): 1 = stream the tiles only, 2 = + the filter
 #endif
 constexpr int W = JIT_W, NC = JIT_NC, NL = JIT_NL, NA = JIT_NA, ND = JIT_ND, IMG = JIT_IMG, NCLS = JIT_NCLS;
 static_assert(JIT_RS == 1 || JIT_RS == 2, "rows shared by 1 or 2 waves");
+static_assert(JIT_RR >= 1 && JIT_RR <= 64 && (JIT_RR & (JIT_RR - 1)) == 0, "1..64 row replicas, a power of two");
+constexpr int kRRLog = JIT_RR >= 64 ? 6 : JIT_RR >= 32 ? 5 : JIT_RR >= 16 ? 4 : JIT_RR >= 8 ? 3 : JIT_RR >= 4 ? 2
+                                                                                      : JIT_RR >= 2 ? 1 : 0;
 constexpr int TD = 64 * ND;                // docs per tile (lane l: docs [ND l, ND l + ND))
 constexpr u32 FULL = (1u << ND) - 1u;      // the lane's match word of a whole tile
 static_assert(ND == 8 || ND == 16, "8 or 16 docs per lane");
@@ -253,8 +268,7 @@ __device__ __forceinline__ void terms(CS* sg, u32 img, int lane, u32 base, u32 t
 
 // one tile of class K: returns the lane's docs counted in numDocsScanned
 template <int K>
-__device__ __forceinline__ u32 tile(CS* sg, i64 wt, u32 img, int lane, u32 base, u32 tb, u32 rows, u32 span_m1,
-                                    u32& errs) {
+__device__ __forceinline__ u32 tile(CS* sg, i64 wt, u32 img, int lane, u32 base, u32 tb, u32 rows, u32& errs) {
   if constexpr (JIT_DBG == 1) return 0;
   const i64 rem = (i64)sg->num_docs - wt * TD;
   u32 m = FULL;
@@ -278,7 +292,8 @@ __device__ __forceinline__ u32 tile(CS* sg, i64 wt, u32 img, int lane, u32 base,
 #pragma unroll
     for (int i = 0; i < ND; ++i) id[i] = *at<const l32>(tb + (u32)JIT_KTAB + 4u * id[i]);
   }
-  const u32 klo = (u32)sg->key_lo;
+  // the segment's local key = key - lbase, kept when below lspan (the box check); row entry local * JIT_RR + replica
+  const u32 klo = (u32)sg->lbase, span_m1 = (u32)sg->lspan - 1u;
   u32 on = m;
   if constexpr (!JIT_KIB) {
     u32 nm = 0;
@@ -292,7 +307,7 @@ __device__ __forceinline__ u32 tile(CS* sg, i64 wt, u32 img, int lane, u32 base,
     on &= ~nm;
     errs += (u32)__builtin_popcount(m & ~on);
   }
-  const u32 abase = rows - 8u * klo;
+  const u32 abase = rows + 8u * ((u32)lane & (u32)(JIT_RR - 1)) - (klo << (3 + kRRLog));
   u32 plo[ND], phi[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) {
@@ -303,43 +318,64 @@ __device__ __forceinline__ u32 tile(CS* sg, i64 wt, u32 img, int lane, u32 base,
 #pragma unroll
   for (int i = 0; i < ND; ++i)
     if ((on >> i) & 1u)
-      __hip_atomic_fetch_add(at<l64>(abase + (id[i] << 3)), ((u64)phi[i] << 32) | plo[i], __ATOMIC_RELAXED,
+      __hip_atomic_fetch_add(at<l64>(abase + (id[i] << (3 + kRRLog))), ((u64)phi[i] << 32) | plo[i], __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
   return (u32)__builtin_popcount(m);
 }
 template <int K>
 __device__ __forceinline__ u32 tile_any(int cls, CS* sg, i64 wt, u32 img, int lane, u32 base, u32 tb, u32 rows,
-                                        u32 span_m1, u32& errs) {
+                                        u32& errs) {
   if constexpr (K + 1 < NCLS) {
-    if (cls == K) return tile<K>(sg, wt, img, lane, base, tb, rows, span_m1, errs);
-    return tile_any<K + 1>(cls, sg, wt, img, lane, base, tb, rows, span_m1, errs);
+    if (cls == K) return tile<K>(sg, wt, img, lane, base, tb, rows, errs);
+    return tile_any<K + 1>(cls, sg, wt, img, lane, base, tb, rows, errs);
   } else {
-    return tile<K>(sg, wt, img, lane, base, tb, rows, span_m1, errs);
+    return tile<K>(sg, wt, img, lane, base, tb, rows, errs);
   }
 }
 
-// a wave's packed rows -> the workgroup's COUNT / SUM accumulators (row zeroed; rows shared by two waves are taken by
-// atomic exchange, the other wave may be adding to them). A SUM over per-segment arithmetic dictionaries (kAO) packs
-// bare dictIds: the rows hold one segment's docs at a time (drained at every segment switch), so the segment's dictId
-// offset enters here once per key, as offset x count.
-__device__ __forceinline__ void drain(u32 rows, int nkeys, int lane, u32 base, CS* sg) {
+// a wave's packed rows -> the workgroup's COUNT / SUM accumulators (rows zeroed; rows shared by two waves are taken by
+// atomic exchange, the other wave may be adding to them). Entry e = local key (e / JIT_RR) x replica: the replicas of a
+// key lie in aligned groups of lanes, unpacked one by one (fields of different replicas cannot be added packed) and
+// reduced across the group before one atomic per key goes to the box accumulators at gofs + local key. A SUM over
+// per-segment arithmetic dictionaries (kAO) packs bare dictIds: the rows hold one segment's docs at a time (drained at
+// every segment switch), so the segment's dictId offset enters here as offset x count.
+__device__ __forceinline__ void drain(u32 rows, int lane, u32 base, CS* sg) {
   l64* row = at<l64>(rows);
   u64 ao[NAA];
 #pragma unroll
   for (int a = 0; a < NA; ++a) ao[a] = kAO[a] ? (u64)(u32)sg->aoff[a] : 0ull;
-  for (int k = lane; k < nkeys; k += 64) {
-    u64 x = row[k];
-    if (x == 0) continue;
-    if constexpr (JIT_RS > 1) x = __hip_atomic_exchange(row + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    else row[k] = 0;
-    const u32 cnt = (u32)(x >> JIT_OC);
-    __hip_atomic_fetch_add(at<l32>(base) + k, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int ne = sg->lspan << kRRLog;
+  const int gofs = sg->gofs;
+  for (int e0 = 0; e0 < ne; e0 += 64) {
+    const int e = e0 + lane;
+    u64 x = 0;
+    if (e < ne) {
+      x = row[e];
+      if (x != 0) {
+        if constexpr (JIT_RS > 1) x = __hip_atomic_exchange(row + e, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else row[e] = 0;
+      }
+    }
+    u64 cnt = x >> JIT_OC;
+    u64 f[NAA];
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
       const int lo = kAS[a], hi = a + 1 < NA ? kAS[a + 1 < NA ? a + 1 : a] : JIT_OC;
-      u64 f = (x >> lo) & ((hi - lo) >= 64 ? ~0ull : ((1ull << (hi - lo)) - 1ull));
-      if (kAO[a]) f += ao[a] * (u64)cnt;
-      __hip_atomic_fetch_add(at<l64>(base + (u32)kLSUM[a]) + k, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      f[a] = (x >> lo) & ((hi - lo) >= 64 ? ~0ull : ((1ull << (hi - lo)) - 1ull));
+      if (kAO[a]) f[a] += ao[a] * cnt;
+    }
+#pragma unroll
+    for (int o = 1; o < JIT_RR; o <<= 1) {
+      cnt += __shfl_xor(cnt, o);
+#pragma unroll
+      for (int a = 0; a < NA; ++a) f[a] += __shfl_xor(f[a], o);
+    }
+    if ((lane & (JIT_RR - 1)) == 0 && cnt != 0) {
+      const int k = gofs + (e >> kRRLog);
+      __hip_atomic_fetch_add(at<l32>(base) + k, (u32)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+        __hip_atomic_fetch_add(at<l64>(base + (u32)kLSUM[a]) + k, f[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
 }
@@ -348,7 +384,7 @@ constexpr bool kAnyAO = [] {
     if (kAO[a]) return true;
   return false;
 }();
-static_assert(!kAnyAO || JIT_RS == 1, "per-segment offsets need private rows (one segment's docs in them at a time)");
+static_assert(!kAnyAO || (JIT_RS == 1 && JIT_SEGDRAIN), "per-segment offsets need private rows drained per segment");
 
 __device__ __forceinline__ int find_segment(CS* segs, int nseg, i64 t) {
   int lo = 0, hi = nseg - 1;
@@ -391,7 +427,7 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
 #pragma unroll
   for (int a = 0; a < NA; ++a)
     for (int i = tid; i < nkeys; i += W * 64) at<l64>(base + (u32)kLSUM[a])[i] = 0ull;
-  for (int i = tid; i < (W / JIT_RS) * nkeys; i += W * 64) at<l64>(base + (u32)JIT_L_ROWS)[i] = 0ull;
+  for (int i = tid; i < (W / JIT_RS) * JIT_LMAX * JIT_RR; i += W * 64) at<l64>(base + (u32)JIT_L_ROWS)[i] = 0ull;
   const i64 T = A->total_tiles, G = gridDim.x;
   const i64 b = blockIdx.x;
   const i64 lb = A->xcd_major ? (b % 8) * (G / 8) + (b % 8 < G % 8 ? b % 8 : G % 8) + b / 8 : b;
@@ -407,10 +443,9 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
       load_tables(A, S + si, base + (u32)JIT_L_SLOT + (u32)(k * JIT_SLOT_B), true, tid);
   }
   __syncthreads();
-  const u32 rows = base + (u32)JIT_L_ROWS + (u32)(wave / JIT_RS) * (u32)nkeys * 8u;
+  const u32 rows = base + (u32)JIT_L_ROWS + (u32)(wave / JIT_RS) * (u32)(JIT_LMAX * JIT_RR) * 8u;
   const u32 ring = base + (u32)JIT_L_RING + (u32)wave * 2u * (u32)IMG * 4u;
   const u32 voff = 16u * (u32)lane;
-  const u32 span_m1 = (u32)A->key_span - 1u;
   u32 matched = 0, errs = 0;
   if (t0 < t1) {
     int isi = find_segment(S, nseg, t0 + wave);
@@ -444,8 +479,8 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
       }
       ti += W;
       while (t >= pend) {
-        if constexpr (kAnyAO) {  // (the rows hold the segment's docs only: its offsets are folded in here)
-          drain(rows, nkeys, lane, base, S + psi);
+        if constexpr (JIT_SEGDRAIN) {  // (the rows hold the segment's local keys only)
+          drain(rows, lane, base, S + psi);
           since = 0;
         }
         ++psi;
@@ -454,16 +489,15 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
         pcls = S[psi].cls;
         tb = base + (u32)JIT_L_SLOT + (u32)((psi - s_first) * JIT_SLOT_B);
       }
-      matched += tile_any<0>(pcls, S + psi, t - pfirst, ring + (u32)slot * (u32)IMG * 4u, lane, base, tb, rows,
-                             span_m1, errs);
+      matched += tile_any<0>(pcls, S + psi, t - pfirst, ring + (u32)slot * (u32)IMG * 4u, lane, base, tb, rows, errs);
       if (++since == JIT_DRAIN) {
-        drain(rows, nkeys, lane, base, S + psi);
+        drain(rows, lane, base, S + psi);
         since = 0;
       }
       slot ^= 1;
     }
     vm_wait<0>();
-    drain(rows, nkeys, lane, base, S + psi);
+    drain(rows, lane, base, S + psi);
   }
   u64 wm = matched, we = errs;
 #pragma unroll

@@ -351,9 +351,29 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
   keep_only("PA_GDL_RS", &Cand::rs);
   bool any_offs = false;  // (per-segment SUM offsets are folded in at the drain: one segment per private row set)
   for (const JitSum& J : sums) any_offs |= !J.table && J.offs;
-  if (any_offs)
+  // the packed rows are indexed by each segment's local keys: its keys inside the box, [lbase, lbase + lspan) of its
+  // own dictIds (affine keys) or of the table keys (remap table); box index = local key + gofs
+  std::vector<int> lbase(ni), lspan(ni), gofs(ni);
+  int lmax = 1;
+  bool segdrain = any_offs;
+  for (int k = 0; k < ni; ++k) {
+    if (ktab) {
+      lbase[k] = (int)klo;
+      lspan[k] = (int)kspan;
+      gofs[k] = 0;
+    } else {
+      const int64_t card = q->hsegs[inc[k]].cols[cols[kc]].card;
+      const int64_t lo = std::max<int64_t>(0, klo - koff[k]), hi = std::min<int64_t>(card, klo + kspan - koff[k]);
+      lbase[k] = (int)lo;
+      lspan[k] = (int)std::max<int64_t>(1, hi - lo);
+      gofs[k] = (int)(lo + koff[k] - klo);
+    }
+    lmax = std::max(lmax, lspan[k]);
+    segdrain |= lbase[k] != lbase[0] || gofs[k] != gofs[0];
+  }
+  if (any_offs || segdrain)
     cands.erase(std::remove_if(cands.begin(), cands.end(), [](const Cand& c) { return c.rs != 1; }), cands.end());
-  int W = 0, ND = 0, RS = 1, nslot = 0, G = 0, img_dw = 0;
+  int W = 0, ND = 0, RS = 1, RR = 1, nslot = 0, G = 0, img_dw = 0;
   size_t lds = 0, l_rows = 0, l_ring = 0;
   std::vector<int64_t> first(ni + 1, 0);
   std::vector<std::vector<int>> coff;
@@ -386,9 +406,17 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
       idw = std::max(idw, (int)(al16(b) / 4));
     }
     const size_t rows = al16(l_slot + (size_t)ns * slot_b);
-    const size_t ring = al16(rows + (size_t)(w / cd.rs) * nkeys * 8);
-    const size_t total = ring + (size_t)w * 2 * idw * 4;
+    const size_t ring_img = (size_t)w * 2 * idw * 4;
+    // row replicas: as many as fit (up to one per lane), so the lanes of a wave hitting a segment's few keys update
+    // different words (PA_GDL_RR: measurement)
+    int rr = 64;
+    if (const char* e = std::getenv("PA_GDL_RR")) rr = std::max(1, std::min(64, std::atoi(e)));
+    while (rr > 1 && al16(rows + (size_t)(w / cd.rs) * lmax * rr * 8) + ring_img > kLdsBudget) rr >>= 1;
+    while (rr > 1 && (rr & (rr - 1))) rr &= rr - 1;
+    const size_t ring = al16(rows + (size_t)(w / cd.rs) * lmax * rr * 8);
+    const size_t total = ring + ring_img;
     if (total > kLdsBudget) continue;
+    RR = rr;
     W = w;
     ND = nd;
     RS = cd.rs;
@@ -410,8 +438,10 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
     as[k] = oc;
     oc += sums[k].w + cbits;
   }
-  // (rows shared by RS waves: between two drains of a set, each of its waves ran at most its own drain period)
-  int drain = (int)std::max<uint64_t>(1, ((uint64_t(1) << cbits) - 1) / (uint64_t)(64 * ND) / (uint64_t)RS);
+  // (a row replica takes the docs of 64 / RR lanes, ND each per tile; rows shared by RS waves: between two drains of a
+  // set, each of its waves ran at most its own drain period)
+  int drain = (int)std::max<uint64_t>(
+      1, ((uint64_t(1) << cbits) - 1) / (uint64_t)((64 / RR) * ND) / (uint64_t)RS);
   if (s.flags & PA_QF_GD_DRAIN_EACH_TILE) drain = 1;
   auto list = [](const std::vector<int>& v) {
     std::string r = "{";
@@ -441,7 +471,8 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
       "-DJIT_OC=" + std::to_string(oc), "-DJIT_DRAIN=" + std::to_string(drain), "-DJIT_L_SUM=" + list(lsum),
       "-DJIT_L_SLOT=" + std::to_string(l_slot), "-DJIT_SLOT_B=" + std::to_string(slot_b),
       "-DJIT_NSLOT=" + std::to_string(nslot), "-DJIT_L_ROWS=" + std::to_string(l_rows),
-      "-DJIT_L_RING=" + std::to_string(l_ring), "-DJIT_RS=" + std::to_string(RS)};
+      "-DJIT_L_RING=" + std::to_string(l_ring), "-DJIT_RS=" + std::to_string(RS), "-DJIT_RR=" + std::to_string(RR),
+      "-DJIT_LMAX=" + std::to_string(lmax), "-DJIT_SEGDRAIN=" + std::to_string(segdrain ? 1 : 0)};
   if (const char* dbg = std::getenv("PA_GDL_DBG")) defs.push_back(std::string("-DJIT_DBG=") + dbg);  // (measurement)
   hipFunction_t fn = jit_compile(defs);
   if (!fn) return PA_OK;
@@ -481,7 +512,9 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
     }
     j.neg = negmask[k];
     j.cls = seg_cls[k];
-    j.key_lo = (int)(klo - (ktab ? 0 : koff[k]));
+    j.lbase = lbase[k];
+    j.lspan = lspan[k];
+    j.gofs = gofs[k];
     if (ktab) {
       const int card = (int)d.cols[cols[kc]].card;
       if (d.remap[0]) {
@@ -520,8 +553,10 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
   q->jit_classes = (int)classes.size();
   q->jit_slots = nslot;
   q->jit_cols = cols;
-  PLAN_LOG("gdl_jit: W %d ND %d RS %d classes %zu slots %d (%zu B) segments %d/%d ktab %d kib %d lds %zu drain %d", W,
-           ND, RS, classes.size(), nslot, slot_b, ni, q->nseg, (int)ktab, (int)kib, lds, drain);
+  PLAN_LOG("gdl_jit: W %d ND %d RS %d RR %d lmax %d segdrain %d classes %zu slots %d (%zu B) segments %d/%d ktab %d "
+           "kib %d lds %zu drain %d",
+           W, ND, RS, RR, lmax, (int)segdrain, classes.size(), nslot, slot_b, ni, q->nseg, (int)ktab, (int)kib, lds,
+           drain);
   return PA_OK;
 }
 

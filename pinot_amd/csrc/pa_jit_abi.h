@@ -17,8 +17,9 @@ struct JitSeg {
   int num_docs, num_tiles;
   unsigned int lo_t[kJitMax], hi_t[kJitMax];  // DICT_RANGE leaves: MSB-aligned bounds in this segment's dictId space
   int cls;                              // width class (the column widths of JIT_NB[cls])
-  int key_lo;                           // the key box's first key in this segment's key space: table key - key_off
-                                        // (affine group key), or the table key itself (through the remap table)
+  int lbase, lspan;                     // the segment's keys in the box: [lbase, lbase + lspan) in its own key space
+                                        // (dictIds of an affine group key, table keys through the remap table)
+  int gofs;                             // box index of local key 0 (lbase + key offset - the box start)
   int aoff[kJitMax];                    // per SUM over an affine dictionary: dictId offset into the term space
   unsigned long long ktab;              // group key remap (dictId -> table key id, int32[ktab_n]); 0: affine
   unsigned long long lut[kJitMax];      // DICT_SET bitmaps (uint32 words)
@@ -31,14 +32,14 @@ struct JitSeg {
 struct JitArgs {
   long long total_tiles;
   int nseg, nkeys, key_lo, key_span, xcd_major, pad;
-  long long key_stride;                 // table-wide key of LDS key k: (k + key_lo) * key_stride
+  long long key_stride;                 // table-wide key of box index k: (k + key_lo) * key_stride
   unsigned long long* matched;          // [0] numDocsScanned, [3] matches outside the key box (planner error)
   unsigned long long* count;            // table-wide COUNT accumulators
   long long* sum[kJitMax];              // table-wide SUM accumulators (int64, or lo/hi pairs: sum_long)
   int sum_long[kJitMax];
   long long base[kJitMax], step[kJitMax];  // value = base + step * term
 };
-static_assert(sizeof(JitSeg) == 48 + 8 + 8 + 48 + 8 + 24 + 8 + 48 + 48 + 24 + 24 + 8, "JitSeg layout");
+static_assert(sizeof(JitSeg) == 48 + 8 + 8 + 48 + 16 + 24 + 8 + 48 + 48 + 24 + 24 + 8, "JitSeg layout");
 static_assert(sizeof(JitArgs) == 8 + 24 + 8 + 8 + 8 + 48 + 24 + 48 + 48, "JitArgs layout");
 
 // ---------------------------------------------------------------- pve_jit.hip (count-free partitioned emit)

@@ -11,6 +11,7 @@ construction. The cases drive each per-segment mechanism of the kernel:
   * SUMs over per-segment arithmetic dictionaries (a dictId offset per segment) and over value tables,
   * a leaf negated in some segments only (an empty range becomes NOT(full range); NOT EQUALS of a value some segments
     lack), and segments a unit clause empties (left out of the kernel's tiles),
+  * packed rows indexed by each segment's local keys, replicated per lane (PA_GDL_RR) and drained at segment switches,
   * 16 or 8 docs per lane (PA_GDL_ND), drained after every tile (PA_QF_GD_DRAIN_EACH_TILE).
 Bars: bit-exact COUNT, LONG SUM, group keys, numDocsScanned.
 """
@@ -87,12 +88,15 @@ QUERIES = (
 )
 
 
+@pytest.mark.parametrize("rr", ["64", "1"])
 @pytest.mark.parametrize("nd", ["16", "8"])
 @pytest.mark.parametrize("flags", [0, L.PA_QF_GD_DRAIN_EACH_TILE])
-def test_own_dictionaries_on_the_specialised_kernel(partitions, monkeypatch, nd, flags):
-    """Every QUERIES shape with 16 or 8 docs per lane."""
+def test_own_dictionaries_on_the_specialised_kernel(partitions, monkeypatch, nd, flags, rr):
+    """Every QUERIES shape with 16 or 8 docs per lane, the packed rows replicated per lane (as many replicas as fit, up
+    to 64) or not."""
     segs, gs = partitions
     monkeypatch.setenv("PA_GDL_ND", nd)
+    monkeypatch.setenv("PA_GDL_RR", rr)
     for sql in QUERIES:
         q = parse_sql(sql)
         ex = GpuQueryExecutor(q, gs, flags=flags)

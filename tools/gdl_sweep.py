@@ -26,8 +26,10 @@ SETTINGS = [
     ("w16_nd8_rs2", {"PA_GDL_W": "16", "PA_GDL_ND": "8", "PA_GDL_RS": "2"}),
     ("w8_nd8", {"PA_GDL_W": "8", "PA_GDL_ND": "8", "PA_GDL_RS": "1"}),
     ("w8_nd16_rs2", {"PA_GDL_W": "8", "PA_GDL_ND": "16", "PA_GDL_RS": "2"}),
+    ("rr1", {"PA_GDL_RR": "1"}),
+    ("w16_nd8", {"PA_GDL_W": "16", "PA_GDL_ND": "8", "PA_GDL_RS": "1"}),
 ]
-KNOBS = ("PA_GDL_W", "PA_GDL_ND", "PA_GDL_RS", "PA_GDL_DBG")
+KNOBS = ("PA_GDL_W", "PA_GDL_ND", "PA_GDL_RS", "PA_GDL_DBG", "PA_GDL_RR")
 
 
 def main():
