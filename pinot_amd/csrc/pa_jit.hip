@@ -116,8 +116,67 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
   if (s.flags & (PA_QF_NO_DENSE_GROUP | PA_QF_FORCE_GLOBAL | PA_QF_FORCE_LDS | PA_QF_LAZY_POST | PA_QF_NO_LANE_MAJOR |
                  PA_QF_STEPS16 | PA_QF_DEBUG_STREAM_ONLY | PA_QF_NO_GDENSE_LM | PA_QF_NO_GD_PACK))
     return PA_OK;
-  const int nl = (int)q->literals.size();
-  if (q->num_eager != nl || nl > kJitMax) return PA_OK;
+  const int nl_all = (int)q->literals.size();
+  if (q->num_eager != nl_all) return PA_OK;
+  for (int li = 0; li < nl_all; ++li) {
+    const int kind = s.leaves[q->literals[li].leaf].kind;
+    if (kind != PA_LEAF_DICT_RANGE && kind != PA_LEAF_DICT_SET) return PA_OK;
+  }
+  // a literal's standing in one segment: 1 = every doc matches (the range covers the segment's dictionary, the set holds
+  // every dictId, or the negation of an empty one), -1 = no doc matches, 0 = depends on the doc
+  auto literal_in = [&](int si, int li) {
+    const Literal lit = q->literals[li];
+    const pa_leaf_params& p = q->leaf_params[si][lit.leaf];
+    const bool neg = (p.negate != 0) != lit.neg;
+    const int64_t card = q->segs[si]->cols.at(s.leaves[lit.leaf].column_id)->cardinality;
+    bool all = false, none = false;
+    if (s.leaves[lit.leaf].kind == PA_LEAF_DICT_RANGE) {
+      const int64_t lo = std::max<int64_t>(0, p.lo), hi = std::min<int64_t>(p.hi, card);
+      none = hi <= lo;
+      all = lo == 0 && hi >= card;
+    } else {
+      const std::vector<uint32_t>& lut = q->luts[si][lit.leaf];
+      int64_t n = 0;
+      for (int64_t w = 0; w < (card + 31) / 32 && (size_t)w < lut.size(); ++w) {
+        const int64_t left = card - 32 * w;
+        n += __builtin_popcount(lut[w] & (left >= 32 ? 0xffffffffu : ((1u << left) - 1u)));
+      }
+      none = n == 0;
+      all = n == card;
+    }
+    if (neg) std::swap(all, none);
+    return all ? 1 : (none ? -1 : 0);
+  };
+  // segments a unit clause provably empties (a day range outside a time partition, an IN list none of whose values the
+  // segment holds) match no doc: they stay out of the kernel's tiles (numDocsScanned 0 there)
+  std::vector<int> inc;  // included segments
+  for (int si = 0; si < q->nseg; ++si) {
+    bool empty = false;
+    for (int li = 0; li < nl_all && !empty; ++li)
+      empty = q->clause_end[li] && (li == 0 || q->clause_end[li - 1]) && literal_in(si, li) < 0;
+    if (!empty) inc.push_back(si);
+  }
+  if (inc.empty()) return PA_OK;  // (nothing to scan: the generic plan's launch finds no match either)
+  const int ni = (int)inc.size();
+  // clauses every included segment satisfies whatever the doc (a literal of it matching every doc there: a day range
+  // covering each time partition) are left out of the kernel: they cannot filter, and their unpack and compares cost
+  // VALU per doc
+  std::vector<int> lit;  // the kernel's leaves: indices into q->literals
+  for (int c0 = 0; c0 < nl_all;) {
+    int c1 = c0;
+    while (!q->clause_end[c1]) ++c1;
+    bool always = true;
+    for (int k = 0; k < ni && always; ++k) {
+      bool sat = false;
+      for (int li = c0; li <= c1 && !sat; ++li) sat = literal_in(inc[k], li) > 0;
+      always = sat;
+    }
+    if (!always)
+      for (int li = c0; li <= c1; ++li) lit.push_back(li);
+    c0 = c1 + 1;
+  }
+  const int nl = (int)lit.size();
+  if (nl > kJitMax) return PA_OK;
   // the kernel's columns: the leaves', the group-by column, the SUMs'
   std::vector<int> cols;
   auto col_of = [&](int slot) {
@@ -128,11 +187,10 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
   };
   std::vector<int> lk(nl), lc(nl), le(nl);
   for (int li = 0; li < nl; ++li) {
-    const int kind = s.leaves[q->literals[li].leaf].kind;
-    if (kind != PA_LEAF_DICT_RANGE && kind != PA_LEAF_DICT_SET) return PA_OK;
-    lk[li] = kind == PA_LEAF_DICT_SET ? 1 : 0;
-    lc[li] = col_of(P.leaf_slot[q->literals[li].leaf]);
-    le[li] = q->clause_end[li] ? 1 : 0;
+    const Literal& L = q->literals[lit[li]];
+    lk[li] = s.leaves[L.leaf].kind == PA_LEAF_DICT_SET ? 1 : 0;
+    lc[li] = col_of(P.leaf_slot[L.leaf]);
+    le[li] = q->clause_end[lit[li]] ? 1 : 0;
   }
   const int kc = col_of(P.gb_slot[0]);
   std::vector<int> sum_aggs;
@@ -158,43 +216,20 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
       if ((c->vtype != PA_INT && c->vtype != PA_LONG) || c->hvals.size() != (size_t)c->cardinality || !c->dict.p)
         return PA_OK;
     }
-  // segments a unit clause provably empties (a day range outside a time partition, an IN list none of whose values the
-  // segment holds) match no doc: they stay out of the kernel's tiles (numDocsScanned 0 there)
-  auto unit_empty = [&](int si, int li) {
-    if (!q->clause_end[li] || (li > 0 && !q->clause_end[li - 1])) return false;
-    const Literal lit = q->literals[li];
-    const pa_leaf_params& p = q->leaf_params[si][lit.leaf];
-    if ((p.negate != 0) != lit.neg) return false;
-    if (lk[li] == 0) {
-      const int64_t card = q->hsegs[si].cols[cols[lc[li]]].card;
-      return std::min<int64_t>(p.hi, card) <= std::max<int64_t>(0, p.lo);
-    }
-    for (uint32_t w : q->luts[si][lit.leaf])
-      if (w) return false;
-    return true;
-  };
-  std::vector<int> inc;  // included segments
-  for (int si = 0; si < q->nseg; ++si) {
-    bool empty = false;
-    for (int li = 0; li < nl && !empty; ++li) empty = unit_empty(si, li);
-    if (!empty) inc.push_back(si);
-  }
-  if (inc.empty()) return PA_OK;  // (nothing to scan: the generic plan's launch finds no match either)
-  const int ni = (int)inc.size();
   // leaves: negation per segment, DICT_SET bitmaps shared or per segment
   std::vector<int> ln(nl, 0), luts_slot(nl, 0), lut_words(nl, 0);
   std::vector<uint32_t> negmask(ni, 0);
   for (int li = 0; li < nl; ++li) {
     bool any = false, all = true;
     for (int k = 0; k < ni; ++k) {
-      const bool n = q->hsegs[inc[k]].leaves[li].negate != 0;
+      const bool n = q->hsegs[inc[k]].leaves[lit[li]].negate != 0;
       any |= n;
       all &= n;
       if (n) negmask[k] |= 1u << li;
     }
     ln[li] = all ? 1 : (any ? 2 : 0);
     if (lk[li]) {
-      const int leaf = q->literals[li].leaf;
+      const int leaf = q->literals[lit[li]].leaf;
       for (int k = 0; k < ni; ++k) {
         lut_words[li] = std::max(lut_words[li], (int)q->luts[inc[k]][leaf].size());
         if (q->luts[inc[k]][leaf] != q->luts[inc[0]][leaf]) luts_slot[li] = 1;
@@ -214,20 +249,26 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
     for (size_t i = 0; i < rm.size() && !ktab; ++i) ktab = rm[i] != rm[0] + (int32_t)i;
     koff[k] = rm.empty() ? 0 : rm[0];
   }
-  // the group key from a DICT_RANGE leaf's unpack; the box check implied when that leaf is a unit clause whose range,
-  // shifted into the table's key ids, lies inside the box in every segment (a matching doc's key is then in the box)
+  // the group key from a DICT_RANGE leaf's unpack; the box check implied in a segment when that leaf is a unit clause
+  // whose range, shifted into the table's key ids, lies inside the box, or when the segment's whole dictionary does (a
+  // matching doc's key is then in the box) — in every segment
   int kl = -1;
   for (int li = 0; li < nl; ++li)
     if (lk[li] == 0 && lc[li] == kc) {
       kl = li;
       break;
     }
-  bool kib = kl >= 0 && !ktab && ln[kl] == 0 && q->clause_end[kl] && (kl == 0 || q->clause_end[kl - 1]);
+  const bool kl_unit = kl >= 0 && ln[kl] == 0 && q->clause_end[lit[kl]] && (kl == 0 || q->clause_end[lit[kl] - 1]);
+  bool kib = !ktab;
   for (int k = 0; k < ni && kib; ++k) {
-    const pa_leaf_params& p = q->leaf_params[inc[k]][q->literals[kl].leaf];
     const int64_t card = q->hsegs[inc[k]].cols[cols[kc]].card;
-    const int64_t rlo = std::max<int64_t>(0, p.lo), rhi = std::min<int64_t>(p.hi, card);
-    kib = rhi > rlo && rlo + koff[k] >= klo && rhi + koff[k] <= klo + kspan;
+    int64_t rlo = 0, rhi = card;
+    if (kl_unit) {
+      const pa_leaf_params& p = q->leaf_params[inc[k]][q->literals[lit[kl]].leaf];
+      rlo = std::max<int64_t>(0, p.lo);
+      rhi = std::min<int64_t>(p.hi, card);
+    }
+    kib = (rhi > rlo && rlo + koff[k] >= klo && rhi + koff[k] <= klo + kspan) || (koff[k] >= klo && card + koff[k] <= klo + kspan);
   }
   // SUM terms: dictIds of arithmetic dictionaries with one common step (each segment's offset into the term space), else
   // value tables (values - the smallest value)
@@ -503,11 +544,11 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
     j.num_docs = d.num_docs;
     j.num_tiles = (int)(first[k + 1] - first[k]);
     for (int li = 0; li < nl; ++li) {
-      j.lo_t[li] = (uint32_t)d.leaves[li].lo;
-      j.hi_t[li] = (uint32_t)d.leaves[li].span;
+      j.lo_t[li] = (uint32_t)d.leaves[lit[li]].lo;
+      j.hi_t[li] = (uint32_t)d.leaves[lit[li]].span;
       if (lk[li]) {
-        j.lut[li] = (unsigned long long)(uintptr_t)d.leaves[li].lut;
-        j.lut_words[li] = (int)q->luts[si][q->literals[li].leaf].size();
+        j.lut[li] = (unsigned long long)(uintptr_t)d.leaves[lit[li]].lut;
+        j.lut_words[li] = (int)q->luts[si][q->literals[lit[li]].leaf].size();
       }
     }
     j.neg = negmask[k];

@@ -242,7 +242,7 @@ SUM_FUNCTIONS = ("SUM", "AVG", "SUMMV", "AVGMV")
 def wide_sum_columns_local(query, segments):
     """Columns of this rank's segments whose SUM needs the 64-bit accumulator (PA_AGGF_WIDE_SUM): LONG columns that are
     hold a value outside int32, raw or in the dictionary (the library picks SUM_I64 for all-int32 columns, SUM_I64X2
-    else: pa_capi.hip pa_segment_add_raw_column / upload_dict)."""
+    else: pa_segment.hip pa_segment_add_raw_column / upload_dict)."""
     out = set()
     for a in query.aggregations:
         if a.function not in SUM_FUNCTIONS or a.column in out:
@@ -259,7 +259,7 @@ def wide_sum_columns_local(query, segments):
 
 
 def hash_keys_bound_local(query, segments):
-    """The hashed key space's key bound of these segments (pa_capi.hip plan_key_space): every doc a key, or twice the
+    """The hashed key space's key bound of these segments (pa_plan.hip plan_key_space): every doc a key, or twice the
     values of a multi-value group-by column."""
     b = 0
     for s in segments:

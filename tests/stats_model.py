@@ -1,4 +1,4 @@
-"""CPU model of pa_query_execution_stats (pa_capi.hip `stats` + pa_stats.hip), for tests: the same reduction of an
+"""CPU model of pa_query_execution_stats (pa_stats_host.hip `stats` + pa_stats.hip), for tests: the same reduction of an
 encoded operator tree (filter_stats.operator_trees rows) to constants, applyAnd counts and leap-frogs, and the same
 chunked leap-frog (per chunk and entry state, then chained per segment) with a small chunk size, so the algorithm is
 checked against the iterator replay (filter_stats.server_stats) on the CPU. Not product code."""

@@ -43,3 +43,21 @@ def test_product_path_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 text = open(os.path.join(dirpath, f)).read()
                 assert "import oracle" not in text and "from oracle" not in text and "liboracle" not in text, f
+
+
+def test_jit_descriptors_have_one_definition():
+    """The hiprtc kernels' descriptors (JitSeg, JitArgs, PveSeg, PveArgs) have one definition, pa_jit_abi.h, with its
+    layout static_asserts: the host includes it and build.py pastes it into the kernels' source strings, so no kernel
+    source defines a copy of its own (round 5 kept hand-mirrored host structs)."""
+    from pinot_amd import build
+    csrc = os.path.join(ROOT, "pinot_amd", "csrc")
+    abi = open(os.path.join(csrc, build.JIT_ABI)).read()
+    assert "static_assert(sizeof(JitSeg)" in abi and "static_assert(sizeof(PveSeg)" in abi
+    for name in build.JIT_SOURCES:
+        raw = open(os.path.join(csrc, name)).read()
+        assert '#include "%s"' % build.JIT_ABI in raw, name
+        for st in ("struct JitSeg", "struct JitArgs", "struct PveSeg", "struct PveArgs"):
+            assert st not in raw, (name, st)
+        text = build.jit_source_text(name)
+        assert abi.replace("#pragma once\n", "") in text and '#include "' not in text, name
+    assert '#include "%s"' % build.JIT_ABI in open(os.path.join(csrc, "pa_host.h")).read()

@@ -67,3 +67,30 @@ def test_build_rebuilds_when_any_header_changes(monkeypatch):
     for name in ("pa_keys.h", "pa_device.h", "gdl_jit.hip", "pinot_amd.h"):
         monkeypatch.setattr(os.path, "getmtime", mtime(name))
         assert B._stale(), name
+
+
+def test_build_covers_every_source_and_rebuilds_objects_by_includes(monkeypatch):
+    """Every .hip translation unit under csrc/ (the JIT kernels aside: hiprtc compiles them) is in build.SOURCES, the
+    library is stale when any of them is newer, and an object is rebuilt exactly when its source or a header it includes
+    (recursively) is newer (build._stale_objs): a host-only header such as pa_host.h rebuilds the host units, not the
+    scan kernels."""
+    from pinot_amd import build as B
+    units = sorted(f for f in os.listdir(B.CSRC) if f.endswith(".hip") and f not in B.JIT_SOURCES)
+    assert units == sorted(B.SOURCES)
+    for name in ("pa_plan.hip", "pa_jit.hip", "pa_stats_host.hip", "pa_fetch.hip", "pa_segment.hip"):
+        assert name in B.SOURCES
+    deps = {s: {os.path.basename(d) for d in B._deps(os.path.join(B.CSRC, s))} for s in B.SOURCES}
+    assert "pa_host.h" in deps["pa_capi.hip"] and "pa_jit_abi.h" in deps["pa_jit.hip"]
+    assert "pa_host.h" not in deps["pa_scan_std.hip"] and "pa_scan.h" in deps["pa_scan_std.hip"]
+    t0 = 1_000_000.0
+    real_exists = os.path.exists
+
+    def mtime(newer):
+        return lambda p: t0 + 10 if os.path.basename(p) == newer else t0
+
+    monkeypatch.setattr(os.path, "exists", lambda p: True if p.endswith(".o") or p == B.LIB else real_exists(p))
+    monkeypatch.setattr(os.path, "getmtime", mtime("pa_host.h"))
+    stale = set(B._stale_objs())
+    assert stale == {s for s in B.SOURCES if "pa_host.h" in deps[s]} and "pa_scan_std.hip" not in stale
+    monkeypatch.setattr(os.path, "getmtime", mtime("pa_plan.hip"))
+    assert B._stale_objs() == ["pa_plan.hip"]

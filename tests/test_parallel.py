@@ -113,7 +113,7 @@ def test_shard_segments_partition(n, world):
 
 
 def _block_layout(secs):
-    """pa_capi.hip accumulator block: sections at 256-byte aligned offsets (gaps zero, as pa_query_reset leaves them)."""
+    """pa_plan.hip plan_accumulators block: sections at 256-byte aligned offsets (gaps zero, as pa_query_reset leaves them)."""
     offs, total = [], 0
     for k, a in secs:
         offs.append(total)
