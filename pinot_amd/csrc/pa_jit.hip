@@ -802,6 +802,7 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   if (const char* dbg = std::getenv("PA_PVE_DBG")) defs.push_back(std::string("-DPVE_DBG=") + dbg);  // (measurement)
   if (const char* pb = std::getenv("PA_PVE_PB")) defs.push_back(std::string("-DPVE_PB=") + pb);      // (measurement)
   if (std::getenv("PA_PVE_DONE_RTN")) defs.push_back("-DPVE_DONE_RTN=1");                            // (measurement)
+  if (const char* e = std::getenv("PA_PVE_SENT")) defs.push_back(std::string("-DPVE_SENT=") + e);    // (measurement)
   hipFunction_t fn = jit_compile(defs, kPveJitSrc, "pve_jit");
   if (!fn) return PA_OK;
   (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

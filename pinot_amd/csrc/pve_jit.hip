@@ -62,6 +62,9 @@ constexpr u32 kSentinel = 0xffffffffu;
 #ifndef PVE_DONE_RTN
 #define PVE_DONE_RTN 0  // measurement (PA_PVE_DONE_RTN): the written count's returned value decides a bin is full
 #endif
+#ifndef PVE_SENT
+#define PVE_SENT 0  // no written count: empty bin slots hold the sentinel, the claimer of a bin's last slot waits until
+#endif          // none does (word 0 of a record written last), the flusher restores the sentinels before reopening
 #ifndef PVE_RW
 #define PVE_RW 1  // words per record: 1 (key offset | value id), 2 (+ a raw 32-bit value), 3 (+ a raw 64-bit value)
 #endif
@@ -293,6 +296,18 @@ __device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE
       }
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (the bin is read before it restarts: LDS runs one wave's ops in order)
+    if constexpr (PVE_SENT) {  // every slot back to the sentinel before the bin reopens
+      if (on) {
+        u32x4 z;
+        z.x = z.y = z.z = z.w = kSentinel;
+#pragma unroll
+        for (int k = 0; k < kPieces; k += 8) {
+          if (kPieces % 8 != 0 && sub + k >= kPieces) break;
+          *at<__attribute__((address_space(3))) u32x4>(B.bins + mine * (u32)(BS * RW) * 4u + 16u * (u32)(sub + k)) = z;
+        }
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
     if (on && sub == 0) {
       at<l32>(B.done)[mine] = 0u;
       at<l32>(B.cnt)[mine] = 0u;
@@ -344,10 +359,29 @@ __device__ __forceinline__ void put_round(const Bins& B, bool (&pend)[PB], const
       for (int i = 0; i < PB; ++i)
         if (s[i] < (u32)BS)
 #pragma unroll
-          for (int k = 0; k < RW; ++k) at<l32>(B.bins)[(pp[i] * (u32)BS + s[i]) * (u32)RW + (u32)k] = rr[i][k];
+          for (int k = RW - 1; k >= 0; --k)  // (word 0 last: PVE_SENT reads it as "written")
+            at<l32>(B.bins)[(pp[i] * (u32)BS + s[i]) * (u32)RW + (u32)k] = rr[i][k];
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       bool full[PB];
-#if PVE_DONE_RTN
+#if PVE_SENT
+      bool anyfull = false;
+#pragma unroll
+      for (int i = 0; i < PB; ++i) {
+        full[i] = s[i] == (u32)BS - 1u;
+        anyfull |= full[i];
+      }
+      if (__builtin_amdgcn_ballot_w64(anyfull) != 0) {
+#pragma unroll
+        for (int i = 0; i < PB; ++i)
+          if (full[i])
+            for (u32 k = 0; k < (u32)BS;)  // the bin's slots, until each holds a record
+              if (__hip_atomic_load(at<l32>(B.bins) + (pp[i] * (u32)BS + k) * (u32)RW, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_WORKGROUP) == kSentinel)
+                __builtin_amdgcn_s_sleep(1);
+              else
+                ++k;
+      }
+#elif PVE_DONE_RTN
 #pragma unroll
       for (int i = 0; i < PB; ++i)
         full[i] = s[i] < (u32)BS &&
@@ -619,6 +653,8 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
   B.region = lb * B.C;
   B.err = A->matched + 3;
   for (int i = tid; i < 5 * P + 1; i += W * 64) smem[i] = 0u;
+  if constexpr (PVE_SENT)
+    for (int i = tid; i < P * BS * RW; i += W * 64) at<l32>(B.bins)[i] = kSentinel;
   __syncthreads();
   const i64 t0 = lb * T / G, t1 = (lb + 1) * T / G;
   const u32 ring = base + (u32)PVE_L_RING + (u32)wave * 2u * (u32)IMG * 4u;
