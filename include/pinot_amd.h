@@ -449,6 +449,10 @@ int32_t pa_query_dense_packed(const pa_query* q);
  * region; pass C reads every partition through its chunk list: no count pass), 2 when it also runs the count-free H
  * emit (DISTINCTCOUNTHLLMV next to the V stream), 0 otherwise, <0 if not prepared. */
 int32_t pa_query_count_free_emit(const pa_query* q);
+/* Keys per partition of the partitioned plan's V stream (a power of two, or under the count-free emit any count that
+ * spreads the key space over whole rounds of pass C's workgroups), 0 when the plan is not partitioned, <0 if not
+ * prepared. */
+int32_t pa_query_partition_keys(const pa_query* q);
 int pa_query_plan(const pa_query* q, int32_t* strategy, int32_t* steps, int32_t* dma_slots, int32_t* ring,
                   int32_t* wg_per_cu, int32_t* grid, int32_t* lds_bytes);
 

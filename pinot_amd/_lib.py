@@ -59,7 +59,7 @@ EXPORTED = [
     "pa_segment_add_raw_column", "pa_segment_num_docs", "pa_segment_device_bytes", "pa_segment_destroy",
     "pa_query_create", "pa_query_bind_segment", "pa_query_bind_value_remap", "pa_query_prepare", "pa_query_num_keys",
     "pa_query_execute", "pa_query_reset", "pa_query_scan", "pa_query_num_eager_literals", "pa_query_lane_major",
-    "pa_query_dense_packed", "pa_query_count_free_emit",
+    "pa_query_dense_packed", "pa_query_count_free_emit", "pa_query_partition_keys",
     "pa_query_accumulator_bytes", "pa_query_set_accumulator_buffer", "pa_query_num_sections", "pa_query_section",
     "pa_query_fetch", "pa_query_matched_docs", "pa_query_key_layout", "pa_query_limit_trimming",
     "pa_query_num_groups_limit_reached", "pa_query_stats", "pa_query_leaf_bitmap_words", "pa_query_leaf_bitmaps",
@@ -145,6 +145,7 @@ def _declare(lib):
         "pa_query_lane_major": (i32, [vp]),
         "pa_query_dense_packed": (i32, [vp]),
         "pa_query_count_free_emit": (i32, [vp]),
+        "pa_query_partition_keys": (i32, [vp]),
         "pa_query_accumulator_bytes": (u64, [vp]),
         "pa_query_set_accumulator_buffer": (ctypes.c_int, [vp, vp, u64]),
         "pa_query_num_sections": (i32, [vp]),

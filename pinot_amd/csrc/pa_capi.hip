@@ -396,6 +396,11 @@ int32_t pa_query_num_eager_literals(const pa_query* q) { return q && q->prepared
 
 int32_t pa_query_lane_major(const pa_query* q) { return q && q->prepared ? q->lane_major : -1; }
 int32_t pa_query_count_free_emit(const pa_query* q) { return q && q->prepared ? (q->pve.fn ? (q->pvh.fn ? 2 : 1) : 0) : -1; }
+int32_t pa_query_partition_keys(const pa_query* q) {
+  if (!q || !q->prepared) return -1;
+  if (!q->partitioned || q->hq.pv == 0) return 0;
+  return q->hq.part_kr_v ? q->hq.part_kr_v : (int32_t)1 << q->hq.kshift_v;
+}
 int32_t pa_query_dense_packed(const pa_query* q) {
   return q && q->prepared ? (q->jit_fn ? 2 : (q->dense_packed ? 1 : 0)) : -1;
 }

@@ -253,7 +253,9 @@ struct DevQuery {
   int32_t pv;                // V partitions (0: no V stream)
   int32_t kshift_v;          // V partition of key k: k >> kshift_v
   int32_t kshift_h;          // H partition of key k: k >> kshift_h
-  int32_t v_fmt;             // VFormat
+  int32_t part_kr_v;         // 0, or (count-free emit) V partition p = keys [p part_kr_v, (p + 1) part_kr_v), part_kr_v
+                             // <= 1 << kshift_v (the record's key offset still takes kshift_v bits)
+  int32_t v_fmt;            // VFormat
   int32_t rec_words_v;       // words per V record (1..kMaxVWords)
   int32_t bs_v, bs_h;        // records per LDS bin (a full bin = one store burst of whole 16-byte units)
   int32_t h_first;           // H records carry the first-value-of-the-doc flag (no V stream: COUNT comes from H)

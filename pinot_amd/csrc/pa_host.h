@@ -253,6 +253,7 @@ struct pa_query {
   DevBuf dq_count, dsegs_count;
   int count_lds = 0, count_ring = 0, part_lds_c = 0;
   int part_vk = -1;     // part_agg_kernel variant (vk_code, kVkGeneric)
+  int v_id_bits = 0;    // V_FMT_ID: bits of a table-wide value id (a record holds it above the key offset)
   int emit_strat = 0;   // the emit kernel variant (pemit_strat)
   // both streams: the emit pass runs as two launches (V records, then H records), each with only its own bins in LDS
   // (more resident workgroups than one kernel holding both): the H launch's descriptor, variant and plan

@@ -798,11 +798,11 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
       "-DPVE_RAWB=" + std::to_string(rawb), "-DPVE_RAWOFF=" + std::to_string(raw_off),
       "-DPVE_H=" + std::to_string(hmode ? 1 : 0), "-DPVE_HNB=" + std::to_string(hnb), "-DPVE_LG=" + std::to_string(lg),
       "-DPVE_L_VAL=" + std::to_string(l_val), "-DPVE_VAL_B=" + std::to_string(vbytes),
-      "-DPVE_KOFF=" + std::to_string(any_koff ? 1 : 0), "-DPVE_VOFF=" + std::to_string(any_voff ? 1 : 0)};
+      "-DPVE_KOFF=" + std::to_string(any_koff ? 1 : 0), "-DPVE_VOFF=" + std::to_string(any_voff ? 1 : 0),
+      "-DPVE_KR=" + std::to_string(hmode ? 0 : h.part_kr_v)};
   if (const char* dbg = std::getenv("PA_PVE_DBG")) defs.push_back(std::string("-DPVE_DBG=") + dbg);  // (measurement)
   if (const char* pb = std::getenv("PA_PVE_PB")) defs.push_back(std::string("-DPVE_PB=") + pb);      // (measurement)
   if (std::getenv("PA_PVE_DONE_RTN")) defs.push_back("-DPVE_DONE_RTN=1");                            // (measurement)
-  if (const char* e = std::getenv("PA_PVE_SENT")) defs.push_back(std::string("-DPVE_SENT=") + e);    // (measurement)
   hipFunction_t fn = jit_compile(defs, kPveJitSrc, "pve_jit");
   if (!fn) return PA_OK;
   (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -871,6 +871,49 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   return PA_OK;
 }
 
+// Pass C runs one workgroup per V partition, one per CU (its LDS accumulators): a partition count just past a whole
+// number of rounds leaves a round of a few full partitions at the end (configs[2] over segments with their own
+// dictionaries: 1031 x 1025 keys, 259 partitions of 4096 keys on 256 CUs, pass C 839 vs 488 us for 256). The count-free
+// emit divides a key by a constant, so its partitions need not hold a power of two keys: ceil(K / (rounds x CUs)) keys
+// each, in as few rounds as pass C's LDS allows. The record keeps the key offset in ceil(log2) bits. Returns whether
+// the V partitions changed (q->hq and pass C's LDS layout rewritten).
+static bool pve_repartition(pa_query* q, const Prep& P, int cus) {
+  DevQuery& h = q->hq;
+  const pa_query_spec& s = q->spec;
+  if (h.hll_agg >= 0 || h.pv <= cus || std::getenv("PA_PVE_POW2")) return false;  // (PA_PVE_POW2: measurement)
+  size_t per_key = 4;  // pass C's LDS per key: u32 count, then each aggregation's slot
+  for (int a = 0; a < s.num_aggs; ++a) {
+    const int t = s.aggs[a].type;
+    if (t == PA_AGG_COUNT || t == PA_AGG_DISTINCTCOUNTHLL) continue;
+    per_key += (t == PA_AGG_SUM && P.agg_src[a] == SRC_LONG) ? 16 : 8;
+  }
+  // (the whole LDS unless the query asked for a smaller pass C, PA_QF_PART_SHIFT)
+  const int choice = (s.flags >> PA_QF_PART_SHIFT) & 3;
+  const size_t budget = choice ? kPartLdsChoices[choice] : kLdsBudget;
+  const int64_t K = q->num_keys, rounds = (h.pv + cus - 1) / cus;
+  for (int64_t r = 1; r < rounds; ++r) {
+    const int64_t kr = (K + r * cus - 1) / (r * cus);
+    if (kr < 2 || kr >= (int64_t(1) << 30) || (size_t)kr * per_key + 16 > budget) continue;
+    const int ks = 64 - __builtin_clzll((unsigned long long)(kr - 1));
+    if (h.v_fmt == V_FMT_ID && q->v_id_bits + ks > 31) continue;
+    const int32_t pv = (int32_t)((K + kr - 1) / kr);
+    h.pv = h.num_parts = h.part_hi = pv;
+    h.kshift_v = ks;
+    h.part_kr_v = (int32_t)kr;
+    size_t lv = ((size_t)kr * 4 + 15) & ~(size_t)15;  // (as plan_partitioned: counts, then the accumulators)
+    for (int a = 0; a < s.num_aggs; ++a) {
+      const int t = s.aggs[a].type;
+      if (t == PA_AGG_COUNT || t == PA_AGG_DISTINCTCOUNTHLL) continue;
+      h.aggs[a].lds_off = (int32_t)lv;
+      lv += (size_t)kr * ((t == PA_AGG_SUM && P.agg_src[a] == SRC_LONG) ? 16 : 8);
+    }
+    q->part_lds_c = (int)lv;
+    PLAN_LOG("pve: V partitions of %lld keys (%d partitions, pass C lds %zu)", (long long)kr, pv, lv);
+    return true;
+  }
+  return false;
+}
+
 int pve_plan(pa_query* q, const Prep& P, int cus) {
   q->pve.fn = q->pvh.fn = nullptr;
   const pa_query_spec& s = q->spec;
@@ -895,8 +938,20 @@ int pve_plan(pa_query* q, const Prep& P, int cus) {
   if (q->nseg == 0 || s.num_group_by < 1 || s.num_group_by > 4 || q->num_eager != (int)q->literals.size() ||
       q->num_eager > 6 || h.pv > 4096 || h.kshift_v < 1)
     return PA_OK;
+  const DevQuery saved = q->hq;
+  const int saved_lds_c = q->part_lds_c;
+  const bool repart = !hstream && pve_repartition(q, P, cus);
   const int64_t base_entries = (int64_t)h.pv + 1 + (hstream ? (int64_t)(h.num_parts - h.pv) + 1 : 0);
   int rc = pve_stream(q, P, cus, false, rw, rawb, base_entries, q->pve);
+  if (repart) {
+    if (rc || !q->pve.fn) {  // (the generic emit runs power-of-two partitions)
+      q->hq = saved;
+      q->part_lds_c = saved_lds_c;
+    } else {
+      PA_HIP(hipMemcpy(q->dq.p, &q->hq, sizeof(DevQuery), hipMemcpyHostToDevice));
+      PA_HIP(set_part_agg_lds_limit(q->part_vk, q->part_lds_c));
+    }
+  }
   if (rc || !q->pve.fn || !hstream) return rc;
   rc = pve_stream(q, P, cus, true, 1, 0, 0, q->pvh);
   if (rc || !q->pvh.fn) q->pve.fn = nullptr;  // (both streams or neither: the count pass serves both)

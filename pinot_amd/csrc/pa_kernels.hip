@@ -1286,7 +1286,7 @@ __device__ void part_agg_v(const DevQuery* __restrict__ q, const PartScratch& ps
   const uint64_t r0 = gp(ps.base)[p], r1 = gp(ps.base)[p + 1];
   const int W = q->rec_words_v;
   const int fmt = q->v_fmt;
-  const uint32_t kmask = (uint32_t)(KR - 1);
+  const uint32_t kmask = (1u << ks) - 1u;  // (the key offset's bits: KR need not be a power of two)
   const AS1 uint32_t* recs = gp((const uint32_t*)ps.recs_v);
   const AS1 uint64_t* vdict = gp(q->vdict);
   // 8 records per thread in flight: every load of the batch first, then the LDS updates
@@ -1370,8 +1370,8 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   constexpr int SK = VK & 3;
   constexpr bool MN = (VK & 4) != 0, MX = (VK & 8) != 0;
   const int ks = q->kshift_v;
-  const int64_t KR = int64_t(1) << ks;
-  const int64_t kbase = (int64_t)p << ks;
+  const int64_t KR = q->part_kr_v ? (int64_t)q->part_kr_v : int64_t(1) << ks;  // (part_kr_v: count-free emit)
+  const int64_t kbase = (int64_t)p * KR;
   const int64_t nk = min(KR, q->num_keys - kbase);
   const int fmt = q->v_fmt;
   const bool ids = fmt == V_FMT_ID && q->v_id_order != 0;  // MIN/MAX on value ids
@@ -1402,7 +1402,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   // 64-bit SUM in one int64 per key when this partition's records cannot overflow it
   const bool narrow = SK == 1 + SRC_LONG && fmt == V_FMT_ID && q->v_maxabs > 0 &&
                       (r1 - r0) < ((uint64_t)1 << 62) / q->v_maxabs;
-  const uint32_t kmask = (uint32_t)(KR - 1);
+  const uint32_t kmask = (1u << ks) - 1u;  // (the key offset's bits: KR need not be a power of two)
   const AS1 uint32_t* recs = gp((const uint32_t*)ps.recs_v);
   const AS1 uint64_t* vdict = gp(q->vdict);
   const bool aff = q->v_affine != 0;

@@ -399,6 +399,8 @@ bool plan_partitions(pa_query* q, Prep& P, TilePlan& emit_plan, TilePlan& count_
                    ? vk_code(h.vop_sum >= 0 ? 1 + P.agg_src[h.vop_sum] : 0, h.vop_min >= 0, h.vop_max >= 0)
                    : kVkGeneric;
   h.v_id_order = (fmt == V_FMT_ID && sorted_ids) ? 1 : 0;
+  h.part_kr_v = 0;
+  q->v_id_bits = fmt == V_FMT_ID ? vbits : 0;
 
   h.vdict = vdict;
   size_t o = 0;

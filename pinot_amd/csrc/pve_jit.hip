@@ -21,6 +21,7 @@
 //   PVE_NL filter leaves (DICT_RANGE), PVE_LC {column}, PVE_LN {negate}, PVE_LE {closes a CNF clause}
 //   PVE_NG group-by columns, PVE_GC {column}, PVE_GS {key stride}
 //   PVE_VC the value column (-1: none)   PVE_KS key bits inside a partition   PVE_P partitions   PVE_BS bin records
+//   PVE_KR keys per V partition when not 1 << PVE_KS (0: 1 << PVE_KS; else partition = key / PVE_KR, a constant divisor)
 //   PVE_SC bins per chunk (a chunk is SC x BS consecutive records of one partition: pass C reads long runs)
 //   PVE_L_BINS, PVE_L_RING LDS byte offsets (state at 0: cnt[P], done[P], chunks[P], cur[P], fill[P], next)
 //   PVE_RW record words, PVE_RAWB / PVE_RAWOFF the staged raw value column, PVE_H the H stream (PVE_HNB, PVE_LG,
@@ -49,6 +50,11 @@ constexpr int kLE[NLA] = PVE_LE;
 constexpr int kGC[NG] = PVE_GC;
 constexpr u32 kGS[NG] = PVE_GS;
 constexpr int VC = PVE_VC, KS = PVE_KS, P = PVE_P, BS = PVE_BS, SC = PVE_SC;
+#ifndef PVE_KR
+#define PVE_KR 0
+#endif
+constexpr u32 KR = PVE_KR, KRD = KR ? KR : 1u;
+static_assert(KR <= (1u << KS), "a partition's key offsets fit KS bits");
 constexpr u32 kSentinel = 0xffffffffu;
 #ifndef PVE_PB
 #define PVE_PB 4  // records per lane per put round
@@ -62,9 +68,6 @@ constexpr u32 kSentinel = 0xffffffffu;
 #ifndef PVE_DONE_RTN
 #define PVE_DONE_RTN 0  // measurement (PA_PVE_DONE_RTN): the written count's returned value decides a bin is full
 #endif
-#ifndef PVE_SENT
-#define PVE_SENT 0  // no written count: empty bin slots hold the sentinel, the claimer of a bin's last slot waits until
-#endif          // none does (word 0 of a record written last), the flusher restores the sentinels before reopening
 #ifndef PVE_RW
 #define PVE_RW 1  // words per record: 1 (key offset | value id), 2 (+ a raw 32-bit value), 3 (+ a raw 64-bit value)
 #endif
@@ -296,18 +299,6 @@ __device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE
       }
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (the bin is read before it restarts: LDS runs one wave's ops in order)
-    if constexpr (PVE_SENT) {  // every slot back to the sentinel before the bin reopens
-      if (on) {
-        u32x4 z;
-        z.x = z.y = z.z = z.w = kSentinel;
-#pragma unroll
-        for (int k = 0; k < kPieces; k += 8) {
-          if (kPieces % 8 != 0 && sub + k >= kPieces) break;
-          *at<__attribute__((address_space(3))) u32x4>(B.bins + mine * (u32)(BS * RW) * 4u + 16u * (u32)(sub + k)) = z;
-        }
-      }
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    }
     if (on && sub == 0) {
       at<l32>(B.done)[mine] = 0u;
       at<l32>(B.cnt)[mine] = 0u;
@@ -359,29 +350,10 @@ __device__ __forceinline__ void put_round(const Bins& B, bool (&pend)[PB], const
       for (int i = 0; i < PB; ++i)
         if (s[i] < (u32)BS)
 #pragma unroll
-          for (int k = RW - 1; k >= 0; --k)  // (word 0 last: PVE_SENT reads it as "written")
-            at<l32>(B.bins)[(pp[i] * (u32)BS + s[i]) * (u32)RW + (u32)k] = rr[i][k];
+          for (int k = 0; k < RW; ++k) at<l32>(B.bins)[(pp[i] * (u32)BS + s[i]) * (u32)RW + (u32)k] = rr[i][k];
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       bool full[PB];
-#if PVE_SENT
-      bool anyfull = false;
-#pragma unroll
-      for (int i = 0; i < PB; ++i) {
-        full[i] = s[i] == (u32)BS - 1u;
-        anyfull |= full[i];
-      }
-      if (__builtin_amdgcn_ballot_w64(anyfull) != 0) {
-#pragma unroll
-        for (int i = 0; i < PB; ++i)
-          if (full[i])
-            for (u32 k = 0; k < (u32)BS;)  // the bin's slots, until each holds a record
-              if (__hip_atomic_load(at<l32>(B.bins) + (pp[i] * (u32)BS + k) * (u32)RW, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_WORKGROUP) == kSentinel)
-                __builtin_amdgcn_s_sleep(1);
-              else
-                ++k;
-      }
-#elif PVE_DONE_RTN
+#if PVE_DONE_RTN
 #pragma unroll
       for (int i = 0; i < PB; ++i)
         full[i] = s[i] < (u32)BS &&
@@ -432,8 +404,8 @@ __device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], 
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
       pend[i] = (m >> (h + i)) & 1u;
-      pp[i] = key[h + i] >> KS;
-      rr[i][0] = (key[h + i] & ((1u << KS) - 1u)) | (VC >= 0 ? (val[h + i][0] << KS) : 0u);
+      pp[i] = KR ? key[h + i] / KRD : key[h + i] >> KS;
+      rr[i][0] = (KR ? key[h + i] - pp[i] * KR : key[h + i] & ((1u << KS) - 1u)) | (VC >= 0 ? (val[h + i][0] << KS) : 0u);
 #pragma unroll
       for (int k = 1; k < RW; ++k) rr[i][k] = val[h + i][k];
     }
@@ -653,8 +625,6 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
   B.region = lb * B.C;
   B.err = A->matched + 3;
   for (int i = tid; i < 5 * P + 1; i += W * 64) smem[i] = 0u;
-  if constexpr (PVE_SENT)
-    for (int i = tid; i < P * BS * RW; i += W * 64) at<l32>(B.bins)[i] = kSentinel;
   __syncthreads();
   const i64 t0 = lb * T / G, t1 = (lb + 1) * T / G;
   const u32 ring = base + (u32)PVE_L_RING + (u32)wave * 2u * (u32)IMG * 4u;

@@ -514,6 +514,7 @@ class GpuQueryExecutor:
         out["plan"]["lane_major"] = int(L.lib().pa_query_lane_major(self.handle))
         out["plan"]["dense_packed"] = int(L.lib().pa_query_dense_packed(self.handle))
         out["plan"]["count_free_emit"] = int(L.lib().pa_query_count_free_emit(self.handle))
+        out["plan"]["partition_keys"] = int(L.lib().pa_query_partition_keys(self.handle))
         out["plan"]["limit_trimming"] = int(L.lib().pa_query_limit_trimming(self.handle))
         return out
 

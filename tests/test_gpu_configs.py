@@ -19,6 +19,7 @@ import socket
 
 import numpy as np
 import pytest
+import torch
 
 import oracle
 from pinot_amd import _lib as L
@@ -285,6 +286,10 @@ def test_configs2_own_dictionaries(highcard_own, variant, count_free):
         p = _plan(ex)
         assert p["strategy"] == "partitioned", p
         assert p["count_free_emit"] == (1 if count_free else 0), p
+        # (about 1025 x 1027 keys: 257 partitions of 4096 keys, or under the count-free emit one per CU: pve_repartition)
+        nk = int(L.lib().pa_query_num_keys(ex.handle))
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        assert nk > 256 * 4096 and p["partition_keys"] == (-(-nk // cus) if count_free else 4096), (nk, p)
         ex.execute()
         _compare_arrays(ex, q, segs)
     finally:
