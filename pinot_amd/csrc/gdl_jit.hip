@@ -60,9 +60,14 @@ typedef __attribute__((address_space(3))) u64 l64;
 #define JIT_SEGDRAIN 0  // the rows are drained at every segment switch (their local keys / offsets change there)
 #endif
 #ifndef JIT_DBG
-#define JIT_DBG 0  // measurement only (PA_GDL_DBG; results invalid): 1 = stream the tiles only, 2 = + the filter
+#define JIT_DBG 0  // measurement only (PA_GDL_DBG; results invalid): 1 = stream the tiles only, 2 = + the filter,
+#endif             // 3 = + keys and packed terms (no row atomics)
+#ifndef JIT_RING
+#define JIT_RING 2  // tile images per wave: JIT_RING - 1 tiles in flight while one is walked
 #endif
 constexpr int W = JIT_W, NC = JIT_NC, NL = JIT_NL, NA = JIT_NA, ND = JIT_ND, IMG = JIT_IMG, NCLS = JIT_NCLS;
+constexpr int R = JIT_RING;
+static_assert(R >= 2 && R <= 4, "2..4 tile images per wave");
 static_assert(JIT_RS == 1 || JIT_RS == 2, "rows shared by 1 or 2 waves");
 static_assert(JIT_RR >= 1 && JIT_RR <= 64 && (JIT_RR & (JIT_RR - 1)) == 0, "1..64 row replicas, a power of two");
 constexpr int kRRLog = JIT_RR >= 64 ? 6 : JIT_RR >= 32 ? 5 : JIT_RR >= 16 ? 4 : JIT_RR >= 8 ? 3 : JIT_RR >= 4 ? 2
@@ -127,6 +132,23 @@ __device__ __forceinline__ void dma_cols(CS* sg, i64 wt, u32 img, u32 voff) {
     dma_cols<K, C + 1>(sg, wt, img, voff);
   }
 }
+// wave DMA instructions of one tile of class K, and the fewest over the classes (a wait for "every tile but the
+// R - 2 youngest" counts that many per younger tile: a class with more only makes the wait conservative)
+template <int K>
+constexpr int dma_instrs() {
+  int n = 0;
+  for (int c = 0; c < NC; ++c) n += (ND * kNB[K][c] / 2 + 63) / 64;
+  return n;
+}
+constexpr int dma_min() {
+  int n = dma_instrs<0>();
+  if (NCLS > 1 && dma_instrs<(NCLS > 1 ? 1 : 0)>() < n) n = dma_instrs<(NCLS > 1 ? 1 : 0)>();
+  if (NCLS > 2 && dma_instrs<(NCLS > 2 ? 2 : 0)>() < n) n = dma_instrs<(NCLS > 2 ? 2 : 0)>();
+  if (NCLS > 3 && dma_instrs<(NCLS > 3 ? 3 : 0)>() < n) n = dma_instrs<(NCLS > 3 ? 3 : 0)>();
+  return n;
+}
+constexpr int kDmaMin = dma_min();
+
 template <int K>
 __device__ __forceinline__ void dma_tile(int cls, CS* sg, i64 wt, u32 img, u32 voff) {
   if constexpr (K + 1 < NCLS) {
@@ -280,6 +302,18 @@ __device__ __forceinline__ u32 tile(CS* sg, i64 wt, u32 img, int lane, u32 base,
   if (!leaves<K, 0>(sg, img, lane, base, tb, m, clause, kt)) return 0;
   if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return 0;
   if constexpr (JIT_DBG == 2) return (u32)__builtin_popcount(m);
+  if constexpr (JIT_DBG == 3) {  // (measurement: keys and terms built and kept live, no row atomics)
+    u32 id[ND], plo[ND], phi[ND];
+    ids<K, JIT_KC>(img, lane, id);
+#pragma unroll
+    for (int i = 0; i < ND; ++i) plo[i] = phi[i] = 0u;
+    terms<K, 0>(sg, img, lane, base, tb, plo, phi);
+    u32 x = 0;
+#pragma unroll
+    for (int i = 0; i < ND; ++i) x ^= ((m >> i) & 1u) ? id[i] + plo[i] + phi[i] : 0u;
+    if (x == 0x9e3779b9u) *at<l32>(rows) = x;
+    return (u32)__builtin_popcount(m);
+  }
   constexpr int NBK = kNB[K][JIT_KC];
   u32 id[ND];
   if constexpr (JIT_KL >= 0) {
@@ -444,7 +478,7 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
   }
   __syncthreads();
   const u32 rows = base + (u32)JIT_L_ROWS + (u32)(wave / JIT_RS) * (u32)(JIT_LMAX * JIT_RR) * 8u;
-  const u32 ring = base + (u32)JIT_L_RING + (u32)wave * 2u * (u32)IMG * 4u;
+  const u32 ring = base + (u32)JIT_L_RING + (u32)wave * (u32)R * (u32)IMG * 4u;
   const u32 voff = 16u * (u32)lane;
   u32 matched = 0, errs = 0;
   if (t0 < t1) {
@@ -455,19 +489,7 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
     int icls = S[isi].cls, pcls = icls;
     u32 tb = base + (u32)JIT_L_SLOT + (u32)((psi - s_first) * JIT_SLOT_B);
     i64 ti = t0 + wave;
-    if (ti < t1) {
-      while (ti >= iend) {
-        ++isi;
-        ifirst = S[isi].first_tile;
-        iend = ifirst + S[isi].num_tiles;
-        icls = S[isi].cls;
-      }
-      dma_tile<0>(icls, S + isi, ti - ifirst, ring, voff);
-    }
-    ti += W;
-    int slot = 0, since = 0;
-    for (i64 t = t0 + wave; t < t1; t += W) {
-      vm_wait<0>();  // tile t has landed (two images: it was the one in flight)
+    auto issue = [&](int to) {  // the wave's next tile into image slot `to`
       if (ti < t1) {
         while (ti >= iend) {
           ++isi;
@@ -475,9 +497,18 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
           iend = ifirst + S[isi].num_tiles;
           icls = S[isi].cls;
         }
-        dma_tile<0>(icls, S + isi, ti - ifirst, ring + (u32)(slot ^ 1) * (u32)IMG * 4u, voff);
+        dma_tile<0>(icls, S + isi, ti - ifirst, ring + (u32)to * (u32)IMG * 4u, voff);
       }
       ti += W;
+    };
+#pragma unroll
+    for (int k = 0; k + 1 < R; ++k) issue(k);
+    int slot = 0, since = 0;
+    for (i64 t = t0 + wave; t < t1; t += W) {
+      // tile t has landed: the R - 2 tiles after it may stay in flight when they were all issued
+      if (R > 2 && t + (i64)(R - 2) * W < t1) vm_wait<(R > 2 ? (R - 2) * kDmaMin : 0)>();
+      else vm_wait<0>();
+      issue(slot == 0 ? R - 1 : slot - 1);  // (the image walked last)
       while (t >= pend) {
         if constexpr (JIT_SEGDRAIN) {  // (the rows hold the segment's local keys only)
           drain(rows, lane, base, S + psi);
@@ -494,7 +525,7 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) gdl_jit(const JitArgs* a
         drain(rows, lane, base, S + psi);
         since = 0;
       }
-      slot ^= 1;
+      slot = slot + 1 == R ? 0 : slot + 1;
     }
     vm_wait<0>();
     drain(rows, lane, base, S + psi);

@@ -414,6 +414,9 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
   }
   if (any_offs || segdrain)
     cands.erase(std::remove_if(cands.begin(), cands.end(), [](const Cand& c) { return c.rs != 1; }), cands.end());
+  // tile images per wave (PA_GDL_RING: measurement): RING - 1 tiles in flight while one is walked
+  int ring_n = 2;
+  if (const char* e = std::getenv("PA_GDL_RING")) ring_n = std::max(2, std::min(4, std::atoi(e)));
   int W = 0, ND = 0, RS = 1, RR = 1, nslot = 0, G = 0, img_dw = 0;
   size_t lds = 0, l_rows = 0, l_ring = 0;
   std::vector<int64_t> first(ni + 1, 0);
@@ -447,7 +450,7 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
       idw = std::max(idw, (int)(al16(b) / 4));
     }
     const size_t rows = al16(l_slot + (size_t)ns * slot_b);
-    const size_t ring_img = (size_t)w * 2 * idw * 4;
+    const size_t ring_img = (size_t)w * ring_n * idw * 4;
     // row replicas: as many as fit (up to one per lane), so the lanes of a wave hitting a segment's few keys update
     // different words (PA_GDL_RR: measurement)
     int rr = 64;
@@ -513,7 +516,8 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
       "-DJIT_L_SLOT=" + std::to_string(l_slot), "-DJIT_SLOT_B=" + std::to_string(slot_b),
       "-DJIT_NSLOT=" + std::to_string(nslot), "-DJIT_L_ROWS=" + std::to_string(l_rows),
       "-DJIT_L_RING=" + std::to_string(l_ring), "-DJIT_RS=" + std::to_string(RS), "-DJIT_RR=" + std::to_string(RR),
-      "-DJIT_LMAX=" + std::to_string(lmax), "-DJIT_SEGDRAIN=" + std::to_string(segdrain ? 1 : 0)};
+      "-DJIT_LMAX=" + std::to_string(lmax), "-DJIT_SEGDRAIN=" + std::to_string(segdrain ? 1 : 0),
+      "-DJIT_RING=" + std::to_string(ring_n)};
   if (const char* dbg = std::getenv("PA_GDL_DBG")) defs.push_back(std::string("-DJIT_DBG=") + dbg);  // (measurement)
   hipFunction_t fn = jit_compile(defs);
   if (!fn) return PA_OK;
@@ -594,10 +598,10 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
   q->jit_classes = (int)classes.size();
   q->jit_slots = nslot;
   q->jit_cols = cols;
-  PLAN_LOG("gdl_jit: W %d ND %d RS %d RR %d lmax %d segdrain %d classes %zu slots %d (%zu B) segments %d/%d ktab %d "
-           "kib %d lds %zu drain %d",
-           W, ND, RS, RR, lmax, (int)segdrain, classes.size(), nslot, slot_b, ni, q->nseg, (int)ktab, (int)kib, lds,
-           drain);
+  PLAN_LOG("gdl_jit: W %d ND %d RS %d RR %d ring %d lmax %d segdrain %d classes %zu slots %d (%zu B) segments %d/%d "
+           "ktab %d kib %d lds %zu drain %d",
+           W, ND, RS, RR, ring_n, lmax, (int)segdrain, classes.size(), nslot, slot_b, ni, q->nseg, (int)ktab, (int)kib,
+           lds, drain);
   return PA_OK;
 }
 
@@ -732,9 +736,13 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   auto val_bytes = [&](int nd) {
     return hmode ? (size_t)16 * (((size_t)max_values * 64 * nd * hnb / 32 + 9 + 3) / 4) : (size_t)0;
   };
+  // tile images per wave (PA_PVE_RING: measurement; the H stream and admission loads keep two)
+  int rn = 2;
+  if (const char* e = std::getenv("PA_PVE_RING")) rn = std::max(2, std::min(4, std::atoi(e)));
+  if (hmode || q->limit_walk) rn = 2;
   auto waves_for = [&](int nd, int bs) {
     for (int cand : {16, 12, 8, 4})
-      if (lds_ring(bs) + (size_t)cand * (2 * image_bytes(nd) + val_bytes(nd)) <= kLdsBudget) return cand;
+      if (lds_ring(bs) + (size_t)cand * (rn * image_bytes(nd) + val_bytes(nd)) <= kLdsBudget) return cand;
     return 0;
   };
   // H: 8 docs per lane (a lane's run of MV values is half as long: measured 3.97 vs 4.8 ms on configs[4]); 32-record
@@ -760,7 +768,7 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   const int td = 64 * nd;
   const size_t l_bins = al16((size_t)(5 * Pn + 1) * 4);
   const size_t l_ring = lds_ring(bs);
-  const size_t l_val = l_ring + (size_t)w * 2 * img_bytes;
+  const size_t l_val = l_ring + (size_t)w * rn * img_bytes;
   const size_t vbytes = val_bytes(nd);
   const size_t lds = l_val + (size_t)w * vbytes;
   // one workgroup per CU; a workgroup's region holds its docs' records (H: at most max_values per doc) in whole chunks
@@ -799,7 +807,7 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
       "-DPVE_H=" + std::to_string(hmode ? 1 : 0), "-DPVE_HNB=" + std::to_string(hnb), "-DPVE_LG=" + std::to_string(lg),
       "-DPVE_L_VAL=" + std::to_string(l_val), "-DPVE_VAL_B=" + std::to_string(vbytes),
       "-DPVE_KOFF=" + std::to_string(any_koff ? 1 : 0), "-DPVE_VOFF=" + std::to_string(any_voff ? 1 : 0),
-      "-DPVE_KR=" + std::to_string(hmode ? 0 : h.part_kr_v)};
+      "-DPVE_KR=" + std::to_string(hmode ? 0 : h.part_kr_v), "-DPVE_RING=" + std::to_string(rn)};
   if (const char* dbg = std::getenv("PA_PVE_DBG")) defs.push_back(std::string("-DPVE_DBG=") + dbg);  // (measurement)
   if (const char* pb = std::getenv("PA_PVE_PB")) defs.push_back(std::string("-DPVE_PB=") + pb);      // (measurement)
   if (std::getenv("PA_PVE_DONE_RTN")) defs.push_back("-DPVE_DONE_RTN=1");                            // (measurement)

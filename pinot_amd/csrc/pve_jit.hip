@@ -98,7 +98,13 @@ constexpr u32 kSentinel = 0xffffffffu;
 #ifndef PVE_VOFF
 #define PVE_VOFF 0  // the value column's table-wide value id = dictId + PveSeg.voff
 #endif
+#ifndef PVE_RING
+#define PVE_RING 2  // tile images per wave (V streams without admission loads: RING - 1 tiles in flight)
+#endif
 constexpr int RW = PVE_RW, RAWB = PVE_RAWB, HNB = PVE_HNB, LG = PVE_LG;
+// (the H stream's value words and the admission bitmap loads are waited for with the image DMA counted in: two images)
+constexpr int R = (PVE_H || PVE_ADMIT) ? 2 : PVE_RING;
+static_assert(R >= 2 && R <= 4, "2..4 tile images per wave");
 static_assert(RW >= 1 && RW <= 3 && (RAWB == 0 || RAWB == 4 * (RW - 1)), "record words and the raw column agree");
 static_assert(!PVE_H || (RW == 1 && PVE_VC < 0 && RAWB == 0), "the H stream has one-word records");
 
@@ -627,7 +633,7 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
   for (int i = tid; i < 5 * P + 1; i += W * 64) smem[i] = 0u;
   __syncthreads();
   const i64 t0 = lb * T / G, t1 = (lb + 1) * T / G;
-  const u32 ring = base + (u32)PVE_L_RING + (u32)wave * 2u * (u32)IMG * 4u;
+  const u32 ring = base + (u32)PVE_L_RING + (u32)wave * (u32)R * (u32)IMG * 4u;
   const u32 voff = 16u * (u32)lane;
   const u32 vbuf = base + (u32)PVE_L_VAL + (u32)wave * (u32)PVE_VAL_B;  // H: the wave's MV value words
   u32 matched = 0;
@@ -638,29 +644,27 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
     i64 ifirst = S[isi].first_tile, iend = ifirst + S[isi].num_tiles;
     i64 pfirst = ifirst, pend = iend;
     i64 ti = t0 + wave;
-    if (ti < t1) {
-      while (ti >= iend) {
-        ++isi;
-        ifirst = S[isi].first_tile;
-        iend = ifirst + S[isi].num_tiles;
+    auto issue_to = [&](int to) {  // the wave's next tile into image slot `to`
+      if (ti < t1) {
+        while (ti >= iend) {
+          ++isi;
+          ifirst = S[isi].first_tile;
+          iend = ifirst + S[isi].num_tiles;
+        }
+        dma_cols<0>(S + isi, ti - ifirst, ring + (u32)to * (u32)IMG * 4u, voff);
       }
-      dma_cols<0>(S + isi, ti - ifirst, ring, voff);
-    }
-    ti += W;
+      ti += W;
+    };
+#pragma unroll
+    for (int k = 0; k + 1 < R; ++k) issue_to(k);
     int slot = 0;
     for (i64 t = t0 + wave; t < t1; t += W) {
-      vm_wait<0>();  // tile t has landed (and the previous tile's chunk stores have left)
-      auto issue = [&]() {
-        if (ti < t1) {
-          while (ti >= iend) {
-            ++isi;
-            ifirst = S[isi].first_tile;
-            iend = ifirst + S[isi].num_tiles;
-          }
-          dma_cols<0>(S + isi, ti - ifirst, ring + (u32)(slot ^ 1) * (u32)IMG * 4u, voff);
-        }
-        ti += W;
-      };
+      // tile t has landed (the R - 2 tiles after it may stay in flight when they were all issued; the chunk stores of
+      // the tiles before it are younger than their DMA and only make the count conservative)
+      if (R > 2 && t + (i64)(R - 2) * W < t1) vm_wait<(R > 2 ? (R - 2) * kDmaImg : 0)>();
+      else vm_wait<0>();
+      const int to = slot == 0 ? R - 1 : slot - 1;  // (the image walked last)
+      auto issue = [&]() { issue_to(to); };
       while (t >= pend) {
         ++psi;
         pfirst = S[psi].first_tile;
@@ -671,7 +675,7 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
       const bool nxt = ti < t1;
       if constexpr (!PVE_ADMIT) issue();
       matched += tile(B, S + psi, t - pfirst, ring + (u32)slot * (u32)IMG * 4u, lane, issue, vbuf, vb0, nxt);
-      slot ^= 1;
+      slot = slot + 1 == R ? 0 : slot + 1;
     }
   }
   vm_wait<0>();

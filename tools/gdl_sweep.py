@@ -1,7 +1,8 @@
 """Measurement of the query-shape specialised dense kernel (gdl_jit.hip) on bench.py's secondary lines: one segment set
 built once, then every knob setting (environment variables read at query prepare) timed with HIP events around
 back-to-back scans. Settings: default plan; waves / docs per lane / rows shared by two waves (PA_GDL_W, PA_GDL_ND,
-PA_GDL_RS); the decomposition stream-only / + filter (PA_GDL_DBG=1 / 2: results invalid, not checked). Every other
+PA_GDL_RS), tile images per wave (PA_GDL_RING); the decomposition stream-only / + filter / + keys and terms without
+the row atomics (PA_GDL_DBG=1 / 2 / 3: results invalid, not checked). Every other
 setting's groups must equal the default plan's.
 
 python tools/gdl_sweep.py [--segments 100] [--docs 10000000] [--own] [--lines sel_10pct,sel_50pct] [--reps 10]
@@ -28,8 +29,15 @@ SETTINGS = [
     ("w8_nd16_rs2", {"PA_GDL_W": "8", "PA_GDL_ND": "16", "PA_GDL_RS": "2"}),
     ("rr1", {"PA_GDL_RR": "1"}),
     ("w16_nd8", {"PA_GDL_W": "16", "PA_GDL_ND": "8", "PA_GDL_RS": "1"}),
+    ("walk_no_atomics", {"PA_GDL_DBG": "3"}),
+    ("ring3", {"PA_GDL_RING": "3"}),
+    ("ring4", {"PA_GDL_RING": "4"}),
+    ("ring3_w8_nd8", {"PA_GDL_RING": "3", "PA_GDL_W": "8", "PA_GDL_ND": "8"}),
+    ("ring3_w8_nd16", {"PA_GDL_RING": "3", "PA_GDL_W": "8", "PA_GDL_ND": "16"}),
+    ("ring3_w16_nd8", {"PA_GDL_RING": "3", "PA_GDL_W": "16", "PA_GDL_ND": "8"}),
+    ("ring3_rr1", {"PA_GDL_RING": "3", "PA_GDL_RR": "1"}),
 ]
-KNOBS = ("PA_GDL_W", "PA_GDL_ND", "PA_GDL_RS", "PA_GDL_DBG", "PA_GDL_RR")
+KNOBS = ("PA_GDL_W", "PA_GDL_ND", "PA_GDL_RS", "PA_GDL_DBG", "PA_GDL_RR", "PA_GDL_RING")
 
 
 def main():
