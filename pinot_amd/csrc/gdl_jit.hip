@@ -181,48 +181,12 @@ __device__ __forceinline__ void lane_words(u32 region, int lane, u32 (&w)[(ND * 
   }
 }
 
-// The lane's words of every staged column, read at the start of the tile (JIT_HOIST: one LDS round trip for the
-// filter and the walk's columns instead of one per use; the reads stay in flight while earlier results are used)
-#ifndef JIT_HOIST
-#define JIT_HOIST 1
-#endif
-constexpr int kw_max() {  // the most words a lane's window of one column takes, over every class and column
-  int m = 1;
-  for (int k = 0; k < NCLS; ++k)
-    for (int c = 0; c < NC; ++c) m = (ND * kNB[k][c] + 31) / 32 + 1 > m ? (ND * kNB[k][c] + 31) / 32 + 1 : m;
-  return m;
-}
-constexpr int KWMAX = kw_max();
-struct Words {
-  u32 w[NC][KWMAX];
-};
-template <int K, int C>
-__device__ __forceinline__ void load_words(u32 img, int lane, Words& wd) {
-  if constexpr (C < NC) {
-    constexpr int NB = kNB[K][C];
-    u32 w[(ND * NB + 31) / 32 + 1];
-    lane_words<NB>(img + (u32)kOFF[K][C], lane, w);
-#pragma unroll
-    for (int j = 0; j < (ND * NB + 31) / 32 + 1; ++j) wd.w[C][j] = w[j];
-    load_words<K, C + 1>(img, lane, wd);
-  }
-}
-template <int K, int C>
-__device__ __forceinline__ void col_words(u32 img, int lane, const Words& wd, u32 (&w)[(ND * kNB[K][C] + 31) / 32 + 1]) {
-  if constexpr (JIT_HOIST) {
-#pragma unroll
-    for (int j = 0; j < (ND * kNB[K][C] + 31) / 32 + 1; ++j) w[j] = wd.w[C][j];
-  } else {
-    lane_words<kNB[K][C]>(img + (u32)kOFF[K][C], lane, w);
-  }
-}
-
 // The lane's ND values of column C (class K), MSB-aligned: value i in the top NB bits of v[i]
 template <int K, int C>
-__device__ __forceinline__ void top(u32 img, int lane, const Words& wd, u32 (&v)[ND]) {
+__device__ __forceinline__ void top(u32 img, int lane, u32 (&v)[ND]) {
   constexpr int NB = kNB[K][C];
   u32 w[(ND * NB + 31) / 32 + 1];
-  col_words<K, C>(img, lane, wd, w);
+  lane_words<NB>(img + (u32)kOFF[K][C], lane, w);
 #pragma unroll
   for (int i = 0; i < ND; ++i) {
     const int s = i * NB, j = s >> 5, o = s & 31;
@@ -232,10 +196,10 @@ __device__ __forceinline__ void top(u32 img, int lane, const Words& wd, u32 (&v)
 
 // dictIds of column C (one v_bfe per id, two ops when it straddles words)
 template <int K, int C>
-__device__ __forceinline__ void ids(u32 img, int lane, const Words& wd, u32 (&v)[ND]) {
+__device__ __forceinline__ void ids(u32 img, int lane, u32 (&v)[ND]) {
   constexpr int NB = kNB[K][C];
   u32 w[(ND * NB + 31) / 32 + 1];
-  col_words<K, C>(img, lane, wd, w);
+  lane_words<NB>(img + (u32)kOFF[K][C], lane, w);
 #pragma unroll
   for (int i = 0; i < ND; ++i) {
     const int s = i * NB, j = s >> 5, o = s & 31;
@@ -259,11 +223,11 @@ __device__ __forceinline__ u32 range_nm(const u32 (&t)[ND], u32 lo_t, u32 hi_t) 
 
 // eager leaves L.. in order (CNF clauses closed by kLE); false when no doc of the wave's tile can match any more
 template <int K, int L>
-__device__ __forceinline__ bool leaves(CS* sg, u32 img, int lane, const Words& wd, u32 base, u32 tb, u32& m,
-                                       u32& clause, u32 (&kt)[ND]) {
+__device__ __forceinline__ bool leaves(CS* sg, u32 img, int lane, u32 base, u32 tb, u32& m, u32& clause,
+                                       u32 (&kt)[ND]) {
   if constexpr (L < NL) {
     u32 t[ND];
-    top<K, kLC[L]>(img, lane, wd, t);
+    top<K, kLC[L]>(img, lane, t);
     if constexpr (L == JIT_KL) {
 #pragma unroll
       for (int i = 0; i < ND; ++i) kt[i] = t[i];
@@ -292,18 +256,17 @@ __device__ __forceinline__ bool leaves(CS* sg, u32 img, int lane, const Words& w
       clause = 0;
       if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return false;
     }
-    return leaves<K, L + 1>(sg, img, lane, wd, base, tb, m, clause, kt);
+    return leaves<K, L + 1>(sg, img, lane, base, tb, m, clause, kt);
   }
   return true;
 }
 
 // packed words of the lane's docs: COUNT + the SUM terms, ORed into their fields 32 bits at a time
 template <int K, int A>
-__device__ __forceinline__ void terms(CS* sg, u32 img, int lane, const Words& wd, u32 base, u32 tb, u32 (&plo)[ND],
-                                      u32 (&phi)[ND]) {
+__device__ __forceinline__ void terms(CS* sg, u32 img, int lane, u32 base, u32 tb, u32 (&plo)[ND], u32 (&phi)[ND]) {
   if constexpr (A < NA) {
     u32 id[ND];
-    ids<K, kAC[A]>(img, lane, wd, id);
+    ids<K, kAC[A]>(img, lane, id);
     if constexpr (kAT[A] >= 0) {
       const u32 ab = (kATS[A] ? tb : base) + (u32)kAT[A];
 #pragma unroll
@@ -321,7 +284,7 @@ __device__ __forceinline__ void terms(CS* sg, u32 img, int lane, const Words& wd
         phi[i] |= id[i] >> (32 - SH);
       }
     }
-    terms<K, A + 1>(sg, img, lane, wd, base, tb, plo, phi);
+    terms<K, A + 1>(sg, img, lane, base, tb, plo, phi);
   }
 }
 
@@ -335,27 +298,16 @@ __device__ __forceinline__ u32 tile(CS* sg, i64 wt, u32 img, int lane, u32 base,
     const i64 n = rem - ND * lane;
     m = n >= ND ? FULL : (n <= 0 ? 0u : ((1u << n) - 1u));
   }
-  Words wd;
-  if constexpr (JIT_HOIST) {
-    load_words<K, 0>(img, lane, wd);
-    // (the words are materialised here, before the filter's branches: otherwise the compiler sinks each column's reads
-    // to its first use, one LDS round trip per use)
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-      for (int j = 0; j < KWMAX; ++j)
-        if (j < (ND * kNB[K][c] + 31) / 32 + 1) asm volatile("" : "+v"(wd.w[c][j]));
-  }
   u32 clause = 0, kt[ND];
-  if (!leaves<K, 0>(sg, img, lane, wd, base, tb, m, clause, kt)) return 0;
+  if (!leaves<K, 0>(sg, img, lane, base, tb, m, clause, kt)) return 0;
   if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return 0;
   if constexpr (JIT_DBG == 2) return (u32)__builtin_popcount(m);
   if constexpr (JIT_DBG == 3) {  // (measurement: keys and terms built and kept live, no row atomics)
     u32 id[ND], plo[ND], phi[ND];
-    ids<K, JIT_KC>(img, lane, wd, id);
+    ids<K, JIT_KC>(img, lane, id);
 #pragma unroll
     for (int i = 0; i < ND; ++i) plo[i] = phi[i] = 0u;
-    terms<K, 0>(sg, img, lane, wd, base, tb, plo, phi);
+    terms<K, 0>(sg, img, lane, base, tb, plo, phi);
     u32 x = 0;
 #pragma unroll
     for (int i = 0; i < ND; ++i) x ^= ((m >> i) & 1u) ? id[i] + plo[i] + phi[i] : 0u;
@@ -368,7 +320,7 @@ __device__ __forceinline__ u32 tile(CS* sg, i64 wt, u32 img, int lane, u32 base,
 #pragma unroll
     for (int i = 0; i < ND; ++i) id[i] = kt[i] >> (32 - NBK);
   } else {
-    ids<K, JIT_KC>(img, lane, wd, id);
+    ids<K, JIT_KC>(img, lane, id);
   }
   if constexpr (JIT_KTAB >= 0) {  // dictId -> table key id
 #pragma unroll
@@ -396,7 +348,7 @@ __device__ __forceinline__ u32 tile(CS* sg, i64 wt, u32 img, int lane, u32 base,
     plo[i] = JIT_OC < 32 ? (1u << (JIT_OC & 31)) : 0u;
     phi[i] = JIT_OC < 32 ? 0u : (1u << ((JIT_OC - 32) & 31));
   }
-  terms<K, 0>(sg, img, lane, wd, base, tb, plo, phi);
+  terms<K, 0>(sg, img, lane, base, tb, plo, phi);
 #pragma unroll
   for (int i = 0; i < ND; ++i)
     if ((on >> i) & 1u)

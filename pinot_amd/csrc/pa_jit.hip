@@ -519,7 +519,6 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
       "-DJIT_LMAX=" + std::to_string(lmax), "-DJIT_SEGDRAIN=" + std::to_string(segdrain ? 1 : 0),
       "-DJIT_RING=" + std::to_string(ring_n)};
   if (const char* dbg = std::getenv("PA_GDL_DBG")) defs.push_back(std::string("-DJIT_DBG=") + dbg);  // (measurement)
-  if (const char* h = std::getenv("PA_GDL_HOIST")) defs.push_back(std::string("-DJIT_HOIST=") + h);  // (measurement)
   hipFunction_t fn = jit_compile(defs);
   if (!fn) return PA_OK;
   (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -731,11 +730,7 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
     for (int k = 0; k < nc; ++k) b += (size_t)8 * nd * d0.cols[slots[k]].nbits + 16;
     return b + (size_t)64 * nd * rawb;
   };
-  // double-buffered bins (PA_PVE_DB: measurement): two bins and two written counts per partition
-  const int dbuf = std::getenv("PA_PVE_DB") ? 2 : 1;
-  auto lds_ring = [&](int bs) {
-    return al16(al16((size_t)((4 + dbuf) * Pn + 1) * 4) + (size_t)dbuf * Pn * bs * rw * 4);
-  };
+  auto lds_ring = [&](int bs) { return al16(al16((size_t)(5 * Pn + 1) * 4) + (size_t)Pn * bs * rw * 4); };
   // H: a wave's buffer for one tile's MV value words (stage_values: at most max_values values per doc, whole 16-byte
   // chunks from a 16-byte aligned start, one word of look-ahead)
   auto val_bytes = [&](int nd) {
@@ -771,7 +766,7 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   img_bytes += (size_t)64 * nd * rawb;
   const int img_dw = (int)(img_bytes / 4);
   const int td = 64 * nd;
-  const size_t l_bins = al16((size_t)((4 + dbuf) * Pn + 1) * 4);
+  const size_t l_bins = al16((size_t)(5 * Pn + 1) * 4);
   const size_t l_ring = lds_ring(bs);
   const size_t l_val = l_ring + (size_t)w * rn * img_bytes;
   const size_t vbytes = val_bytes(nd);
@@ -812,7 +807,7 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
       "-DPVE_H=" + std::to_string(hmode ? 1 : 0), "-DPVE_HNB=" + std::to_string(hnb), "-DPVE_LG=" + std::to_string(lg),
       "-DPVE_L_VAL=" + std::to_string(l_val), "-DPVE_VAL_B=" + std::to_string(vbytes),
       "-DPVE_KOFF=" + std::to_string(any_koff ? 1 : 0), "-DPVE_VOFF=" + std::to_string(any_voff ? 1 : 0),
-      "-DPVE_KR=" + std::to_string(hmode ? 0 : h.part_kr_v), "-DPVE_RING=" + std::to_string(rn), "-DPVE_DB=" + std::to_string(dbuf - 1)};
+      "-DPVE_KR=" + std::to_string(hmode ? 0 : h.part_kr_v), "-DPVE_RING=" + std::to_string(rn)};
   if (const char* dbg = std::getenv("PA_PVE_DBG")) defs.push_back(std::string("-DPVE_DBG=") + dbg);  // (measurement)
   if (const char* pb = std::getenv("PA_PVE_PB")) defs.push_back(std::string("-DPVE_PB=") + pb);      // (measurement)
   if (std::getenv("PA_PVE_DONE_RTN")) defs.push_back("-DPVE_DONE_RTN=1");                            // (measurement)

@@ -98,9 +98,6 @@ constexpr u32 kSentinel = 0xffffffffu;
 #ifndef PVE_VOFF
 #define PVE_VOFF 0  // the value column's table-wide value id = dictId + PveSeg.voff
 #endif
-#ifndef PVE_DB
-#define PVE_DB 0  // double-buffered bins: two per partition, claims never fail (see put_round)
-#endif
 #ifndef PVE_RING
 #define PVE_RING 2  // tile images per wave (V streams without admission loads: RING - 1 tiles in flight)
 #endif
@@ -278,8 +275,7 @@ constexpr int kPieces = BS * RW / 4;  // 16-byte pieces of a bin
 // Every bin the wave completed (full[i] of its lanes) leaves together: eight lanes per bin (16 bytes each per store
 // instruction: a 32-record one-word bin is one instruction for eight bins), the group's first lane takes the chunk slot
 // and restarts the bin after the copy.
-__device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE_PB], const u32 (&pp)[PVE_PB],
-                                           const u32 (&bb)[PVE_PB], int lane) {
+__device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE_PB], const u32 (&pp)[PVE_PB], int lane) {
   u64 fm[PVE_PB];
   u64 any = 0;
 #pragma unroll
@@ -290,7 +286,7 @@ __device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE
   if (any == 0) return;
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   const int grp = lane >> 3, sub = lane & 7;
-  u32 mine = 0xffffffffu, mbin = 0xffffffffu;  // (the group's partition and its bin buffer)
+  u32 mine = 0xffffffffu;
   int g = 0;
   auto round = [&]() {
     const bool on = grp < g;
@@ -303,24 +299,19 @@ __device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE
 #pragma unroll
       for (int k = 0; k < kPieces; k += 8) {
         if (kPieces % 8 != 0 && sub + k >= kPieces) break;
-        const u32x4 v = *at<const __attribute__((address_space(3))) u32x4>(B.bins + mbin * (u32)(BS * RW) * 4u +
+        const u32x4 v = *at<const __attribute__((address_space(3))) u32x4>(B.bins + mine * (u32)(BS * RW) * 4u +
                                                                              16u * (u32)(sub + k));
         __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4*)(B.recs + dst_rec * RW) + sub + k);
       }
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (the bin is read before it restarts: LDS runs one wave's ops in order)
     if (on && sub == 0) {
-      at<l32>(B.done)[mbin] = 0u;
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      if constexpr (PVE_DB)  // (the bin is free again: one more bin of the partition released, BS claims retired)
-        (void)__hip_atomic_fetch_add(at<l32>(B.cnt) + mine, 0x10000u - (u32)BS, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_WORKGROUP);
-      else
-        at<l32>(B.cnt)[mine] = 0u;
+      at<l32>(B.done)[mine] = 0u;
+      at<l32>(B.cnt)[mine] = 0u;
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     g = 0;
-    mine = mbin = 0xffffffffu;
+    mine = 0xffffffffu;
   };
 #pragma unroll
   for (int i = 0; i < PVE_PB; ++i) {
@@ -329,11 +320,7 @@ __device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE
       const int l = __builtin_ctzll(m);
       m &= m - 1;
       const u32 p = (u32)__builtin_amdgcn_readlane((int)pp[i], l);
-      const u32 q = (u32)__builtin_amdgcn_readlane((int)bb[i], l);
-      if (grp == g) {
-        mine = p;
-        mbin = q;
-      }
+      if (grp == g) mine = p;
       if (++g == 8) round();
     }
   }
@@ -341,98 +328,21 @@ __device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE
 }
 
 // the end of the pass: bin p (one thread) as a chunk slot, copied by that thread
-__device__ __forceinline__ void flush_one(const Bins& B, u32 p, u32 bin) {
+__device__ __forceinline__ void flush_one(const Bins& B, u32 p) {
   const i64 dst_rec = bin_slot(B, p);
   if (dst_rec >= 0) {
     const __attribute__((address_space(3))) u32x4* src =
-        at<const __attribute__((address_space(3))) u32x4>(B.bins + bin * (u32)(BS * RW) * 4u);
+        at<const __attribute__((address_space(3))) u32x4>(B.bins + p * (u32)(BS * RW) * 4u);
     __attribute__((address_space(1))) u32x4* dst = (__attribute__((address_space(1))) u32x4*)(B.recs + dst_rec * RW);
     for (int k = 0; k < kPieces; ++k) __builtin_nontemporal_store(src[k], dst + k);
   }
+  at<l32>(B.done)[p] = 0u;
+  at<l32>(B.cnt)[p] = 0u;
 }
 
 // PB records of the lane (pend[i]: record i exists) into their partitions' bins: claim, write, count written; a lane
 // that completes a bin flushes it; a record whose bin was full claims again after the flushes
 constexpr int PB = PVE_PB;
-#if PVE_DB
-// Double-buffered bins: partition p has two bin buffers and one claim word (bins released << 16 | claims outstanding).
-// A claim (one returning LDS atomic) reads both halves at once: the record's bin is n = released + outstanding / BS,
-// its buffer n & 1, its slot outstanding % BS; it never fails. The claimer of a bin's last slot releases the bin once
-// every slot is written and the partition's earlier bins are released (so the partition's chunk state keeps one writer
-// and the two buffers alternate): copy out, reset its written count, add 2^16 - BS to the claim word. A claim two bins
-// ahead of the last release (the buffer still holds bin n - 2) waits for that release before it writes. Every wait is
-// for an older bin, and each wave's loop serves whichever of its records and releases is ready, so none waits on itself.
-__device__ __forceinline__ void put_round(const Bins& B, bool (&pend)[PB], const u32 (&pp)[PB], const u32 (&rr)[PB][RW],
-                                          int lane) {
-  static_assert(!PVE_DONE_RTN, "double-buffered bins count writes without a returned value");
-  u32 bb[PB], nn[PB], ss[PB];
-  bool wr[PB], fl[PB];
-#pragma unroll
-  for (int i = 0; i < PB; ++i) {
-    const u32 old = pend[i] ? __hip_atomic_fetch_add(at<l32>(B.cnt) + pp[i], 1u, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP)
-                            : 0u;
-    const u32 o = old & 0xffffu, k = o / (u32)BS;
-    nn[i] = ((old >> 16) + k) & 0xffffu;
-    ss[i] = o % (u32)BS;
-    bb[i] = pp[i] * 2u + (nn[i] & 1u);
-    wr[i] = pend[i];
-    fl[i] = false;
-    pend[i] = pend[i] && k >= 2u;  // (laps: waits below)
-  }
-#pragma unroll
-  for (int i = 0; i < PB; ++i)
-    if (wr[i] && !pend[i]) {
-#pragma unroll
-      for (int k = 0; k < RW; ++k) at<l32>(B.bins)[(bb[i] * (u32)BS + ss[i]) * (u32)RW + (u32)k] = rr[i][k];
-    }
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#pragma unroll
-  for (int i = 0; i < PB; ++i)
-    if (wr[i] && !pend[i]) {
-      (void)__hip_atomic_fetch_add(at<l32>(B.done) + bb[i], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      fl[i] = ss[i] == (u32)BS - 1u;
-    }
-  for (int it = 0;; ++it) {
-    bool any = false;
-    // lapped records whose buffer's previous bin is released
-#pragma unroll
-    for (int i = 0; i < PB; ++i) {
-      if (!pend[i]) continue;
-      const u32 rel = __hip_atomic_load(at<l32>(B.cnt) + pp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> 16;
-      if (((rel - (nn[i] - 1u)) & 0xffffu) >= 0x8000u) {
-        any = true;
-        continue;
-      }
-#pragma unroll
-      for (int k = 0; k < RW; ++k) at<l32>(B.bins)[(bb[i] * (u32)BS + ss[i]) * (u32)RW + (u32)k] = rr[i][k];
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      (void)__hip_atomic_fetch_add(at<l32>(B.done) + bb[i], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      pend[i] = false;
-      fl[i] = ss[i] == (u32)BS - 1u;
-    }
-    // completed bins whose writes have all landed and whose partition released the bin before
-    bool ready[PB];
-#pragma unroll
-    for (int i = 0; i < PB; ++i) {
-      ready[i] = false;
-      if (!fl[i]) continue;
-      const u32 d = __hip_atomic_load(at<l32>(B.done) + bb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const u32 rel = __hip_atomic_load(at<l32>(B.cnt) + pp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> 16;
-      ready[i] = d == (u32)BS && rel == nn[i];
-      fl[i] = !ready[i];
-      any |= fl[i];
-    }
-    flush_full(B, ready, pp, bb, lane);
-    if (__builtin_amdgcn_ballot_w64(any) == 0) break;
-    if (it > (1 << 20)) {  // (a protocol fault, not a wait: reported as an overflow, the pass ends instead of hanging)
-      if (lane == 0) __hip_atomic_fetch_add(B.err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-    if (it > 0) __builtin_amdgcn_s_sleep(1);
-  }
-}
-#else
 __device__ __forceinline__ void put_round(const Bins& B, bool (&pend)[PB], const u32 (&pp)[PB], const u32 (&rr)[PB][RW],
                                           int lane) {
   {
@@ -478,7 +388,7 @@ __device__ __forceinline__ void put_round(const Bins& B, bool (&pend)[PB], const
               __builtin_amdgcn_s_sleep(1);
       }
 #endif
-      flush_full(B, full, pp, pp, lane);
+      flush_full(B, full, pp, lane);
       bool any = false;
 #pragma unroll
       for (int i = 0; i < PB; ++i) {
@@ -490,7 +400,6 @@ __device__ __forceinline__ void put_round(const Bins& B, bool (&pend)[PB], const
     }
   }
 }
-#endif
 
 // the V stream: the lane's matching docs (bits of m), PB at a time
 __device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], const u32 (&val)[ND][RW], int lane) {
@@ -709,20 +618,19 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
   const i64 b = blockIdx.x;
   const i64 lb = A->xcd_major ? (b % 8) * (G / 8) + (b % 8 < G % 8 ? b % 8 : G % 8) + b / 8 : b;
   Bins B;
-  constexpr u32 ND2 = PVE_DB ? 2u : 1u;  // written counts: one per bin buffer
   B.cnt = base;
   B.done = base + 4u * P;
-  B.chunks = base + 4u * (1u + ND2) * P;
-  B.cur = B.chunks + 4u * P;
-  B.fill = B.cur + 4u * P;
-  B.next = B.fill + 4u * P;
+  B.chunks = base + 8u * P;
+  B.cur = base + 12u * P;
+  B.fill = base + 16u * P;
+  B.next = base + 20u * P;
   B.bins = base + (u32)PVE_L_BINS;
   B.recs = A->recs;
   B.table = A->table;
   B.C = A->chunks_per_wg;
   B.region = lb * B.C;
   B.err = A->matched + 3;
-  for (int i = tid; i < (int)(4u + ND2) * P + 1; i += W * 64) smem[i] = 0u;
+  for (int i = tid; i < 5 * P + 1; i += W * 64) smem[i] = 0u;
   __syncthreads();
   const i64 t0 = lb * T / G, t1 = (lb + 1) * T / G;
   const u32 ring = base + (u32)PVE_L_RING + (u32)wave * (u32)R * (u32)IMG * 4u;
@@ -778,12 +686,10 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
   __syncthreads();
   // the partial bins, padded with sentinels, as chunks; then this workgroup's chunks per partition
   for (int p = tid; p < P; p += W * 64) {
-    const u32 w = at<l32>(B.cnt)[p];
-    const u32 n = w & 0xffffu;  // (every full bin has been released: the current one holds n < BS records)
+    const u32 n = at<l32>(B.cnt)[p];
     if (n == 0) continue;
-    const u32 bin = PVE_DB ? (u32)p * 2u + ((w >> 16) & 1u) : (u32)p;
-    for (u32 k = n; k < (u32)BS; ++k) at<l32>(B.bins)[(bin * (u32)BS + k) * (u32)RW] = kSentinel;
-    flush_one(B, (u32)p, bin);
+    for (u32 k = n; k < (u32)BS; ++k) at<l32>(B.bins)[((u32)p * (u32)BS + k) * (u32)RW] = kSentinel;
+    flush_one(B, (u32)p);
   }
   __syncthreads();
   // each partition's last chunk: its table entry with the bins written (pass C reads no further)
