@@ -1585,6 +1585,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   }
 }
 
+template <bool NEW>
 __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps, int ph, unsigned char* lds) {
   const DevAgg& H = q->aggs[q->hll_agg];
   const int lg = H.log2m;
@@ -1619,19 +1620,42 @@ __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps
     uint32_t cid[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) cid[j] = (uint32_t)__builtin_amdgcn_readlane((int)cidv, j);
-    // (as part_agg_v_fast: every address, then the loads without a branch per load; an absent record reads record 0)
+    // (as part_agg_v_fast: every address, then the loads without a branch per load; an absent record reads record 0;
+    // NEW: the wave's first record of slot j and the count readable from it are wave-uniform)
     uint32_t w[kB];
-    uint64_t pa[kB];
     bool ok[kB];
+    if constexpr (NEW) {
+      const uint32_t wofs_s = (uint32_t)__builtin_amdgcn_readfirstlane((int)wofs);
+      const AS1 uint32_t* pw[kB];
 #pragma unroll
-    for (int j = 0; j < kB; ++j) {
-      const uint64_t ri = b0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
-      const uint64_t pi = cix ? ((uint64_t)(cid[j] & 0x0fffffffu) << csh) | (ri & cmask) : ri;
-      ok[j] = ri < r1 && (!cix || (uint32_t)(ri & cmask) < (((cid[j] >> 28) + 1u) << ps.chunk_bin_shift_h));
-      pa[j] = ok[j] ? pi : 0ull;
+      for (int j = 0; j < kB; ++j) {
+        const uint64_t u = b0 + (uint64_t)j * kPartAggThreads + wofs_s;
+        uint64_t rec0 = u;
+        uint64_t lim = r1 > u ? r1 - u : 0ull;
+        if (cix) {
+          const uint32_t inch = (uint32_t)(u & cmask);
+          rec0 = ((uint64_t)(cid[j] & 0x0fffffffu) << csh) | inch;
+          const uint32_t bound = ((cid[j] >> 28) + 1u) << ps.chunk_bin_shift_h;
+          lim = min(lim, (uint64_t)(bound > inch ? bound - inch : 0u));
+        }
+        if (lim == 0) rec0 = 0;
+        pw[j] = recs + rec0;
+        ok[j] = (uint64_t)ln < lim;
+      }
+#pragma unroll
+      for (int j = 0; j < kB; ++j) w[j] = __builtin_nontemporal_load(pw[j] + (ok[j] ? ln : 0u));
+    } else {
+      uint64_t pa[kB];
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        const uint64_t ri = b0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
+        const uint64_t pi = cix ? ((uint64_t)(cid[j] & 0x0fffffffu) << csh) | (ri & cmask) : ri;
+        ok[j] = ri < r1 && (!cix || (uint32_t)(ri & cmask) < (((cid[j] >> 28) + 1u) << ps.chunk_bin_shift_h));
+        pa[j] = ok[j] ? pi : 0ull;
+      }
+#pragma unroll
+      for (int j = 0; j < kB; ++j) w[j] = __builtin_nontemporal_load(recs + pa[j]);
     }
-#pragma unroll
-    for (int j = 0; j < kB; ++j) w[j] = __builtin_nontemporal_load(recs + pa[j]);
 #pragma unroll
     for (int j = 0; j < kB; ++j)
       if (!ok[j]) w[j] = kSentinel;
@@ -1691,8 +1715,10 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
     if constexpr (VK == kVkGeneric) part_agg_v(q, ps, (int)blockIdx.x, (unsigned char*)smem);
     else if (ps.flags & 1) part_agg_v_fast<VK, false>(q, ps, (int)blockIdx.x, (unsigned char*)smem);  // (measurement)
     else part_agg_v_fast<VK, true>(q, ps, (int)blockIdx.x, (unsigned char*)smem);
+  } else if (ps.flags & 1) {  // (measurement)
+    part_agg_h<false>(q, ps, (int)blockIdx.x - q->pv, (unsigned char*)smem);
   } else {
-    part_agg_h(q, ps, (int)blockIdx.x - q->pv, (unsigned char*)smem);
+    part_agg_h<true>(q, ps, (int)blockIdx.x - q->pv, (unsigned char*)smem);
   }
 }
 
