@@ -1365,7 +1365,7 @@ __device__ void part_agg_v(const DevQuery* __restrict__ q, const PartScratch& ps
 // read once into registers, the record loop is straight-line. V_FMT_ID records with value ids in value order keep
 // MIN/MAX as 32-bit ids (the value is looked up once per key at the store), so the per-record dictionary gather is
 // only needed by SUM.
-template <int VK, bool NEW>
+template <int VK>
 __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratch& ps, int p, unsigned char* lds) {
   constexpr int SK = VK & 3;
   constexpr bool MN = (VK & 4) != 0, MX = (VK & 8) != 0;
@@ -1422,53 +1422,16 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
     return (ln < (uint32_t)kB && ri < r1) ? cix[ri >> csh] : 0u;
   };
   uint32_t cidv = cix ? load_cids(r0) : 0u;
-  // NEW: a wave's 64 records of slot j are consecutive in one chunk (or in the contiguous stream), so their first
-  // record's address and the count readable from it are wave-uniform (scalar math); a lane adds only its 32-bit offset.
-  // A SUM over an affine dictionary accumulates value ids; the store forms base x count + step x (sum of ids).
-  const bool sid = NEW && (SK == 1 + SRC_LONG || SK == 1 + SRC_INT) && fmt == V_FMT_ID && aff;
-  const uint32_t wofs_s = (uint32_t)__builtin_amdgcn_readfirstlane((int)wofs);
   for (uint64_t b0 = r0; b0 < r1; b0 += span) {
     uint32_t cid[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) cid[j] = (uint32_t)__builtin_amdgcn_readlane((int)cidv, j);
-    uint32_t w0[kB], w1[kB], w2[kB];
-    bool ok[kB];
-    if constexpr (NEW) {
-      const AS1 uint32_t* pw[kB];
-      uint32_t lo[kB];
-#pragma unroll
-      for (int j = 0; j < kB; ++j) {
-        const uint64_t u = b0 + (uint64_t)j * kPartAggThreads + wofs_s;
-        uint64_t rec0 = u;
-        uint64_t lim = r1 > u ? r1 - u : 0ull;
-        if (cix) {
-          const uint32_t inch = (uint32_t)(u & cmask);
-          rec0 = ((uint64_t)(cid[j] & 0x0fffffffu) << csh) | inch;
-          const uint32_t bound = ((cid[j] >> 28) + 1u) << ps.chunk_bin_shift;  // (records written in the chunk)
-          lim = min(lim, (uint64_t)(bound > inch ? bound - inch : 0u));
-        }
-        if (lim == 0) rec0 = 0;  // (the wave reads record 0, always allocated, and drops it)
-        pw[j] = recs + rec0 * (uint64_t)W;
-        ok[j] = (uint64_t)ln < lim;
-        lo[j] = ok[j] ? ln * (uint32_t)W : 0u;
-      }
-#pragma unroll
-      for (int j = 0; j < kB; ++j) w0[j] = __builtin_nontemporal_load(pw[j] + lo[j]);
-#pragma unroll
-      for (int j = 0; j < kB; ++j) w1[j] = w2[j] = 0u;
-      if (fmt == V_FMT_32 || fmt == V_FMT_64) {
-#pragma unroll
-        for (int j = 0; j < kB; ++j) w1[j] = __builtin_nontemporal_load(pw[j] + lo[j] + 1);
-      }
-      if (fmt == V_FMT_64) {
-#pragma unroll
-        for (int j = 0; j < kB; ++j) w2[j] = __builtin_nontemporal_load(pw[j] + lo[j] + 2);
-      }
-    } else {
     // every address first (the chunk entries were loaded a batch ago), then the loads back to back without a branch
     // per load (a branch per load makes each wait for the one before it); an absent record reads record 0 (always
     // allocated) and becomes a sentinel
+    uint32_t w0[kB], w1[kB], w2[kB];
     uint64_t pa[kB];
+    bool ok[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       const uint64_t ri = b0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
@@ -1489,7 +1452,6 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
 #pragma unroll
       for (int j = 0; j < kB; ++j) w2[j] = __builtin_nontemporal_load(recs + pa[j] + 2);
     }
-    }
 #pragma unroll
     for (int j = 0; j < kB; ++j)
       if (!ok[j]) w0[j] = kSentinel;
@@ -1500,8 +1462,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
       iv[j] = 0;
       if (w0[j] == kSentinel) continue;
       if (fmt == V_FMT_ID) {
-        if (sid) iv[j] = (int64_t)(w0[j] >> ks);
-        else if (SK || !ids) iv[j] = aff ? vbase + vstep * (int64_t)(w0[j] >> ks) : (int64_t)vdict[w0[j] >> ks];
+        if (SK || !ids) iv[j] = aff ? vbase + vstep * (int64_t)(w0[j] >> ks) : (int64_t)vdict[w0[j] >> ks];
       } else if (fmt == V_FMT_32) {
         iv[j] = (int64_t)(int32_t)w1[j];
       } else if (fmt == V_FMT_64) {
@@ -1516,7 +1477,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
       if (SK == 1 + SRC_INT) {
         __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + lk, (uint64_t)iv[j], WG_RLX);
       } else if (SK == 1 + SRC_LONG) {
-        if (narrow || sid) {
+        if (narrow) {
           __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + 2 * lk, (uint64_t)iv[j], WG_RLX);
         } else {
           __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + 2 * lk, (uint64_t)(uint32_t)iv[j], WG_RLX);
@@ -1551,16 +1512,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
     const int64_t k = kbase + lk;
     const uint32_t c = cnt[lk];
     gc[k] = c;
-    if (sid) {  // base x count + step x (sum of value ids), exact
-      const uint64_t si = ((const lds_u64_t*)lds_ptr(lds + off_s))[SK == 1 + SRC_LONG ? 2 * lk : lk];
-      const __int128 S = (__int128)vbase * (__int128)c + (__int128)vstep * (__int128)si;
-      if (SK == 1 + SRC_LONG) {
-        gs[2 * k] = (int64_t)(uint32_t)(uint64_t)S;
-        gs[2 * k + 1] = (int64_t)(S >> 32);
-      } else {
-        gs[k] = (int64_t)S;
-      }
-    } else if (SK == 1 + SRC_LONG) {
+    if (SK == 1 + SRC_LONG) {
       const int64_t lo = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[2 * lk];
       const int64_t hi = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[2 * lk + 1];
       // (narrow: lo holds the whole sum S; the pair is (S mod 2^32, S >> 32), the same total)
@@ -1585,7 +1537,6 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   }
 }
 
-template <bool NEW>
 __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps, int ph, unsigned char* lds) {
   const DevAgg& H = q->aggs[q->hll_agg];
   const int lg = H.log2m;
@@ -1620,42 +1571,19 @@ __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps
     uint32_t cid[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) cid[j] = (uint32_t)__builtin_amdgcn_readlane((int)cidv, j);
-    // (as part_agg_v_fast: every address, then the loads without a branch per load; an absent record reads record 0;
-    // NEW: the wave's first record of slot j and the count readable from it are wave-uniform)
+    // (as part_agg_v_fast: every address, then the loads without a branch per load; an absent record reads record 0)
     uint32_t w[kB];
+    uint64_t pa[kB];
     bool ok[kB];
-    if constexpr (NEW) {
-      const uint32_t wofs_s = (uint32_t)__builtin_amdgcn_readfirstlane((int)wofs);
-      const AS1 uint32_t* pw[kB];
 #pragma unroll
-      for (int j = 0; j < kB; ++j) {
-        const uint64_t u = b0 + (uint64_t)j * kPartAggThreads + wofs_s;
-        uint64_t rec0 = u;
-        uint64_t lim = r1 > u ? r1 - u : 0ull;
-        if (cix) {
-          const uint32_t inch = (uint32_t)(u & cmask);
-          rec0 = ((uint64_t)(cid[j] & 0x0fffffffu) << csh) | inch;
-          const uint32_t bound = ((cid[j] >> 28) + 1u) << ps.chunk_bin_shift_h;
-          lim = min(lim, (uint64_t)(bound > inch ? bound - inch : 0u));
-        }
-        if (lim == 0) rec0 = 0;
-        pw[j] = recs + rec0;
-        ok[j] = (uint64_t)ln < lim;
-      }
-#pragma unroll
-      for (int j = 0; j < kB; ++j) w[j] = __builtin_nontemporal_load(pw[j] + (ok[j] ? ln : 0u));
-    } else {
-      uint64_t pa[kB];
-#pragma unroll
-      for (int j = 0; j < kB; ++j) {
-        const uint64_t ri = b0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
-        const uint64_t pi = cix ? ((uint64_t)(cid[j] & 0x0fffffffu) << csh) | (ri & cmask) : ri;
-        ok[j] = ri < r1 && (!cix || (uint32_t)(ri & cmask) < (((cid[j] >> 28) + 1u) << ps.chunk_bin_shift_h));
-        pa[j] = ok[j] ? pi : 0ull;
-      }
-#pragma unroll
-      for (int j = 0; j < kB; ++j) w[j] = __builtin_nontemporal_load(recs + pa[j]);
+    for (int j = 0; j < kB; ++j) {
+      const uint64_t ri = b0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
+      const uint64_t pi = cix ? ((uint64_t)(cid[j] & 0x0fffffffu) << csh) | (ri & cmask) : ri;
+      ok[j] = ri < r1 && (!cix || (uint32_t)(ri & cmask) < (((cid[j] >> 28) + 1u) << ps.chunk_bin_shift_h));
+      pa[j] = ok[j] ? pi : 0ull;
     }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) w[j] = __builtin_nontemporal_load(recs + pa[j]);
 #pragma unroll
     for (int j = 0; j < kB; ++j)
       if (!ok[j]) w[j] = kSentinel;
@@ -1713,12 +1641,9 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   if ((int)blockIdx.x < q->pv) {
     if constexpr (VK == kVkGeneric) part_agg_v(q, ps, (int)blockIdx.x, (unsigned char*)smem);
-    else if (ps.flags & 1) part_agg_v_fast<VK, false>(q, ps, (int)blockIdx.x, (unsigned char*)smem);  // (measurement)
-    else part_agg_v_fast<VK, true>(q, ps, (int)blockIdx.x, (unsigned char*)smem);
-  } else if (ps.flags & 1) {  // (measurement)
-    part_agg_h<false>(q, ps, (int)blockIdx.x - q->pv, (unsigned char*)smem);
+    else part_agg_v_fast<VK>(q, ps, (int)blockIdx.x, (unsigned char*)smem);
   } else {
-    part_agg_h<true>(q, ps, (int)blockIdx.x - q->pv, (unsigned char*)smem);
+    part_agg_h(q, ps, (int)blockIdx.x - q->pv, (unsigned char*)smem);
   }
 }
 
