@@ -1421,15 +1421,20 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
     const uint64_t ri = b + (uint64_t)ln * kPartAggThreads + wofs;
     return (ln < (uint32_t)kB && ri < r1) ? cix[ri >> csh] : 0u;
   };
+  // A batch = kB records per thread. issue(): addresses (the chunk entries were loaded a batch ago), then the loads back
+  // to back without a branch per load (a branch per load makes each wait for the one before it; an absent record reads
+  // record 0, always allocated, and becomes a sentinel), then the next batch's chunk entries. process(): the LDS
+  // updates. Two register batches alternate, so one batch's loads are in flight while the other's updates run
+  // (PA_PASSC_SERIAL: one batch at a time, measurement).
+  struct Batch {
+    uint32_t w0[kB], w1[kB], w2[kB];
+    uint32_t okm;  // (record j exists: bit j; tested in process(), so issue() never waits for its loads)
+  };
   uint32_t cidv = cix ? load_cids(r0) : 0u;
-  for (uint64_t b0 = r0; b0 < r1; b0 += span) {
+  auto issue = [&](uint64_t b0, Batch& B) {
     uint32_t cid[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) cid[j] = (uint32_t)__builtin_amdgcn_readlane((int)cidv, j);
-    // every address first (the chunk entries were loaded a batch ago), then the loads back to back without a branch
-    // per load (a branch per load makes each wait for the one before it); an absent record reads record 0 (always
-    // allocated) and becomes a sentinel
-    uint32_t w0[kB], w1[kB], w2[kB];
     uint64_t pa[kB];
     bool ok[kB];
 #pragma unroll
@@ -1441,38 +1446,43 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
       pa[j] = ok[j] ? pi * (uint64_t)W : 0ull;
     }
 #pragma unroll
-    for (int j = 0; j < kB; ++j) w0[j] = __builtin_nontemporal_load(recs + pa[j]);
+    for (int j = 0; j < kB; ++j) B.w0[j] = __builtin_nontemporal_load(recs + pa[j]);
 #pragma unroll
-    for (int j = 0; j < kB; ++j) w1[j] = w2[j] = 0u;
+    for (int j = 0; j < kB; ++j) B.w1[j] = B.w2[j] = 0u;
     if (fmt == V_FMT_32 || fmt == V_FMT_64) {
 #pragma unroll
-      for (int j = 0; j < kB; ++j) w1[j] = __builtin_nontemporal_load(recs + pa[j] + 1);
+      for (int j = 0; j < kB; ++j) B.w1[j] = __builtin_nontemporal_load(recs + pa[j] + 1);
     }
     if (fmt == V_FMT_64) {
 #pragma unroll
-      for (int j = 0; j < kB; ++j) w2[j] = __builtin_nontemporal_load(recs + pa[j] + 2);
+      for (int j = 0; j < kB; ++j) B.w2[j] = __builtin_nontemporal_load(recs + pa[j] + 2);
     }
+    B.okm = 0u;
+#pragma unroll
+    for (int j = 0; j < kB; ++j) B.okm |= ok[j] ? 1u << j : 0u;
+    if (cix) cidv = load_cids(b0 + span);
+  };
+  auto process = [&](Batch& B) {
+    int64_t iv[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j)
-      if (!ok[j]) w0[j] = kSentinel;
-    if (cix) cidv = load_cids(b0 + span);
-    int64_t iv[kB];
+      if (!((B.okm >> j) & 1u)) B.w0[j] = kSentinel;
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       iv[j] = 0;
-      if (w0[j] == kSentinel) continue;
+      if (B.w0[j] == kSentinel) continue;
       if (fmt == V_FMT_ID) {
-        if (SK || !ids) iv[j] = aff ? vbase + vstep * (int64_t)(w0[j] >> ks) : (int64_t)vdict[w0[j] >> ks];
+        if (SK || !ids) iv[j] = aff ? vbase + vstep * (int64_t)(B.w0[j] >> ks) : (int64_t)vdict[B.w0[j] >> ks];
       } else if (fmt == V_FMT_32) {
-        iv[j] = (int64_t)(int32_t)w1[j];
+        iv[j] = (int64_t)(int32_t)B.w1[j];
       } else if (fmt == V_FMT_64) {
-        iv[j] = (int64_t)(((uint64_t)w2[j] << 32) | w1[j]);
+        iv[j] = (int64_t)(((uint64_t)B.w2[j] << 32) | B.w1[j]);
       }
     }
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
-      if (w0[j] == kSentinel) continue;
-      const uint32_t lk = w0[j] & kmask;
+      if (B.w0[j] == kSentinel) continue;
+      const uint32_t lk = B.w0[j] & kmask;
       __hip_atomic_fetch_add(cnt + lk, 1u, WG_RLX);
       if (SK == 1 + SRC_INT) {
         __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + lk, (uint64_t)iv[j], WG_RLX);
@@ -1487,7 +1497,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
         atomicAdd((double*)(lds + off_s) + lk, __builtin_bit_cast(double, iv[j]));
       }
       if (ids) {
-        const uint32_t id = w0[j] >> ks;
+        const uint32_t id = B.w0[j] >> ks;
         if (MN) __hip_atomic_fetch_min(lds_ptr(lds + off_mn) + lk, id, WG_RLX);
         if (MX) __hip_atomic_fetch_max(lds_ptr(lds + off_mx) + lk, id, WG_RLX);
       } else {
@@ -1500,6 +1510,25 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
           __hip_atomic_fetch_max((__attribute__((address_space(3))) int64_t*)lds_ptr(lds + off_mx) + lk, e, WG_RLX);
         }
       }
+    }
+  };
+  Batch X, Y;
+  if (ps.flags & 2) {  // (measurement: one batch at a time)
+    for (uint64_t b0 = r0; b0 < r1; b0 += span) {
+      issue(b0, X);
+      process(X);
+    }
+  } else if (r0 < r1) {
+    issue(r0, X);
+    for (uint64_t b0 = r0;; b0 += 2 * span) {
+      const bool more = b0 + span < r1;
+      if (more) issue(b0 + span, Y);
+      process(X);
+      if (!more) break;
+      const bool more2 = b0 + 2 * span < r1;
+      if (more2) issue(b0 + 2 * span, X);
+      process(Y);
+      if (!more2) break;
     }
   }
   __syncthreads();
