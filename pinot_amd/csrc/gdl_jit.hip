@@ -38,7 +38,7 @@
 //   JIT_DRAIN tiles between drains of a wave's packed rows, JIT_RS waves sharing one set of rows, JIT_RR replicas of
 //   JIT_LMAX rows, JIT_SEGDRAIN drains at segment switches
 //   JIT_L_SUM {LDS byte offset of each SUM's accumulators}, JIT_L_SLOT / JIT_SLOT_B / JIT_NSLOT the table slots,
-//   JIT_L_ROWS, JIT_L_RING, JIT_L_SPARE (LDS byte offsets; the spare rows: JIT_NOBR)
+//   JIT_L_ROWS, JIT_L_RING (LDS byte offsets)
 typedef unsigned int u32;
 typedef unsigned long long u64;
 typedef long long i64;
@@ -103,39 +103,19 @@ __device__ __forceinline__ T* at(u32 a) { return (T*)(unsigned long)a; }
 template <int N>
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-#ifndef JIT_M0
-#define JIT_M0 0  // 1: the DMA's LDS address goes in as an m0 operand (the compiler sets m0; no save / restore)
-#endif
-#ifndef JIT_L_SPARE
-#define JIT_L_SPARE 0
-#endif
-#ifndef JIT_NOBR
-#define JIT_NOBR 0  // 1: every doc slot's row atomic runs on all lanes, a lane without a match adding to its own spare row
-#endif
-
 // LDS-DMA with a scalar base: lane l copies 16 bytes at sbase + voff to dst + 16 l (mask: the taking-part lanes)
 __device__ __forceinline__ void dma16(u32 voff, u64 sbase, u32 dst) {
-  if constexpr (JIT_M0) {
-    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "{m0}"(dst));
-  } else {
-    u32 keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(dst));
-  }
+  u32 keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(dst));
 }
 __device__ __forceinline__ void dma16m(u32 voff, u64 sbase, u32 dst, u64 mask) {
+  u32 keep;
   u64 save;
-  if constexpr (JIT_M0) {
-    asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 exec, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
-                 "s_mov_b64 exec, %0"
-                 : "=&s"(save) : "v"(voff), "s"(sbase), "s"(mask), "{m0}"(dst));
-  } else {
-    u32 keep;
-    asm volatile(
-        "s_mov_b64 %1, exec\n\ts_mov_b64 exec, %5\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
-        : "=&s"(keep), "=&s"(save) : "v"(voff), "s"(sbase), "s"(dst), "s"(mask));
-  }
+  asm volatile(
+      "s_mov_b64 %1, exec\n\ts_mov_b64 exec, %5\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
+      : "=&s"(keep), "=&s"(save) : "v"(voff), "s"(sbase), "s"(dst), "s"(mask));
 }
 
 // tile wt of every column of class K: 8 ND nb bytes per column, as 16-byte chunks
@@ -369,19 +349,11 @@ __device__ __forceinline__ u32 tile(CS* sg, i64 wt, u32 img, int lane, u32 base,
     phi[i] = JIT_OC < 32 ? 0u : (1u << ((JIT_OC - 32) & 31));
   }
   terms<K, 0>(sg, img, lane, base, tb, plo, phi);
-  if constexpr (JIT_NOBR) {  // (no exec-mask branch per doc slot: a lane without a match adds to its spare row)
-    const u32 spare = base + (u32)JIT_L_SPARE + 8u * (u32)lane;
 #pragma unroll
-    for (int i = 0; i < ND; ++i)
-      __hip_atomic_fetch_add(at<l64>(((on >> i) & 1u) ? abase + (id[i] << (3 + kRRLog)) : spare),
-                             ((u64)phi[i] << 32) | plo[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  } else {
-#pragma unroll
-    for (int i = 0; i < ND; ++i)
-      if ((on >> i) & 1u)
-        __hip_atomic_fetch_add(at<l64>(abase + (id[i] << (3 + kRRLog))), ((u64)phi[i] << 32) | plo[i],
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
+  for (int i = 0; i < ND; ++i)
+    if ((on >> i) & 1u)
+      __hip_atomic_fetch_add(at<l64>(abase + (id[i] << (3 + kRRLog))), ((u64)phi[i] << 32) | plo[i], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
   return (u32)__builtin_popcount(m);
 }
 template <int K>

@@ -1,7 +1,6 @@
 // Host side of the C-ABI (include/pinot_amd.h): segment residency, query planning (CNF filter, column
 // slots, staging, accumulator layout, strategy) and result fetch. No CPU fallback: every query runs the
 // HIP kernels; errors surface as negative return codes + pa_last_error().
-#include <cstdlib>
 #include "pa_host.h"
 
 extern "C" {
@@ -229,7 +228,6 @@ int pa_query_scan(pa_query* q, void* stream) {
   if (q->pve.fn) {  // the count-free emit: records in per-workgroup chunks, the partitions' chunk lists, pass C
     if (q->part_vk == kVkGeneric) return fail(PA_EINVAL, "internal: chunk lists need a specialised pass C");
     PartScratch ps{};
-    ps.flags = std::getenv("PA_PASSC_SERIAL") ? 2 : 0;  // (measurement)
     char* vb = (char*)q->pve.buf.p;
     ps.base = (uint64_t*)(vb + q->pve.o_base);
     for (pa_query::PveStream* S : {&q->pve, &q->pvh}) {
@@ -267,8 +265,7 @@ int pa_query_scan(pa_query* q, void* stream) {
     int rc = arena_grow(a, q->sc_bytes);
     if (rc) return rc;
     if (a->used && a->last_stream != st) PA_HIP(hipStreamWaitEvent(st, a->last, 0));
-    PartScratch ps = scratch_of(q, a->p);
-    ps.flags = std::getenv("PA_PASSC_SERIAL") ? 2 : 0;  // (measurement)
+    const PartScratch ps = scratch_of(q, a->p);
     const LmSegPlan* plans = (const LmSegPlan*)q->dplans.p;
     PA_HIP(launch_scan(q->count_strat, q->steps, 0, q->grid * q->count_k, q->count_lds, (const DevQuery*)q->dq_count.p,
                        (const DevSeg*)q->dsegs_count.p, plans, ps, st));

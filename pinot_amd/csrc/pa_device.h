@@ -427,7 +427,6 @@ struct PartScratch {
   int32_t chunk_shift, chunk_bin_shift;
   const uint32_t* chunk_index_h;  // the same for the H records (recs_h), relative to base[pv + 1]
   int32_t chunk_shift_h, chunk_bin_shift_h;
-  int32_t flags;  // measurement only: 2 = pass C loads and updates one batch at a time (PA_PASSC_SERIAL)
 };
 
 // Per-segment table of the lane-major scan kernel (scan_lm_kernel): 64 dwords, loaded at segment entry into ONE

@@ -417,10 +417,6 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
   // tile images per wave (PA_GDL_RING: measurement): RING - 1 tiles in flight while one is walked
   int ring_n = 2;
   if (const char* e = std::getenv("PA_GDL_RING")) ring_n = std::max(2, std::min(4, std::atoi(e)));
-  // branch-free row atomics (PA_GDL_NOBR: measurement): one spare row per lane after the ring; the DMA's LDS address as
-  // an m0 operand (PA_GDL_M0: measurement)
-  const bool nobr = std::getenv("PA_GDL_NOBR") != nullptr;
-  const size_t spare_b = nobr ? 64 * 8 : 0;
   int W = 0, ND = 0, RS = 1, RR = 1, nslot = 0, G = 0, img_dw = 0;
   size_t lds = 0, l_rows = 0, l_ring = 0;
   std::vector<int64_t> first(ni + 1, 0);
@@ -459,10 +455,10 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
     // different words (PA_GDL_RR: measurement)
     int rr = 64;
     if (const char* e = std::getenv("PA_GDL_RR")) rr = std::max(1, std::min(64, std::atoi(e)));
-    while (rr > 1 && al16(rows + (size_t)(w / cd.rs) * lmax * rr * 8) + ring_img + spare_b > kLdsBudget) rr >>= 1;
+    while (rr > 1 && al16(rows + (size_t)(w / cd.rs) * lmax * rr * 8) + ring_img > kLdsBudget) rr >>= 1;
     while (rr > 1 && (rr & (rr - 1))) rr &= rr - 1;
     const size_t ring = al16(rows + (size_t)(w / cd.rs) * lmax * rr * 8);
-    const size_t total = ring + ring_img + spare_b;
+    const size_t total = ring + ring_img;
     if (total > kLdsBudget) continue;
     RR = rr;
     W = w;
@@ -521,9 +517,7 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
       "-DJIT_NSLOT=" + std::to_string(nslot), "-DJIT_L_ROWS=" + std::to_string(l_rows),
       "-DJIT_L_RING=" + std::to_string(l_ring), "-DJIT_RS=" + std::to_string(RS), "-DJIT_RR=" + std::to_string(RR),
       "-DJIT_LMAX=" + std::to_string(lmax), "-DJIT_SEGDRAIN=" + std::to_string(segdrain ? 1 : 0),
-      "-DJIT_RING=" + std::to_string(ring_n), "-DJIT_NOBR=" + std::to_string(nobr ? 1 : 0),
-      "-DJIT_L_SPARE=" + std::to_string(lds - spare_b)};
-  if (std::getenv("PA_GDL_M0")) defs.push_back("-DJIT_M0=1");
+      "-DJIT_RING=" + std::to_string(ring_n)};
   if (const char* dbg = std::getenv("PA_GDL_DBG")) defs.push_back(std::string("-DJIT_DBG=") + dbg);  // (measurement)
   hipFunction_t fn = jit_compile(defs);
   if (!fn) return PA_OK;

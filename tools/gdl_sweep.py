@@ -30,9 +30,6 @@ SETTINGS = [
     ("rr1", {"PA_GDL_RR": "1"}),
     ("w16_nd8", {"PA_GDL_W": "16", "PA_GDL_ND": "8", "PA_GDL_RS": "1"}),
     ("walk_no_atomics", {"PA_GDL_DBG": "3"}),
-    ("nobr", {"PA_GDL_NOBR": "1"}),
-    ("m0", {"PA_GDL_M0": "1"}),
-    ("nobr_m0", {"PA_GDL_NOBR": "1", "PA_GDL_M0": "1"}),
     ("ring3", {"PA_GDL_RING": "3"}),
     ("ring4", {"PA_GDL_RING": "4"}),
     ("ring3_w8_nd8", {"PA_GDL_RING": "3", "PA_GDL_W": "8", "PA_GDL_ND": "8"}),
@@ -40,7 +37,7 @@ SETTINGS = [
     ("ring3_w16_nd8", {"PA_GDL_RING": "3", "PA_GDL_W": "16", "PA_GDL_ND": "8"}),
     ("ring3_rr1", {"PA_GDL_RING": "3", "PA_GDL_RR": "1"}),
 ]
-KNOBS = ("PA_GDL_W", "PA_GDL_ND", "PA_GDL_RS", "PA_GDL_DBG", "PA_GDL_RR", "PA_GDL_RING", "PA_GDL_NOBR", "PA_GDL_M0")
+KNOBS = ("PA_GDL_W", "PA_GDL_ND", "PA_GDL_RS", "PA_GDL_DBG", "PA_GDL_RR", "PA_GDL_RING")
 
 
 def main():
