@@ -380,7 +380,8 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
   struct Cand {
     int w, nd, rs;
   };
-  std::vector<Cand> cands = {{16, 16, 1}, {16, 8, 1}, {8, 16, 1}, {8, 8, 1}, {16, 16, 2}, {16, 8, 2}};
+  std::vector<Cand> cands = {{16, 16, 1}, {16, 8, 1}, {8, 16, 1}, {8, 8, 1}, {16, 16, 2}, {16, 8, 2}, {12, 16, 1},
+                             {12, 8, 1}};
   auto keep_only = [&](const char* env, int Cand::*f) {
     if (const char* e = std::getenv(env)) {
       const int v = std::atoi(e);

@@ -30,6 +30,10 @@ SETTINGS = [
     ("rr1", {"PA_GDL_RR": "1"}),
     ("w16_nd8", {"PA_GDL_W": "16", "PA_GDL_ND": "8", "PA_GDL_RS": "1"}),
     ("walk_no_atomics", {"PA_GDL_DBG": "3"}),
+    ("w12_nd8", {"PA_GDL_W": "12", "PA_GDL_ND": "8", "PA_GDL_RS": "1"}),
+    ("w12_nd16", {"PA_GDL_W": "12", "PA_GDL_ND": "16", "PA_GDL_RS": "1"}),
+    ("w8_nd8_pin", {"PA_GDL_W": "8", "PA_GDL_ND": "8", "PA_GDL_RS": "1"}),
+    ("w16_nd16", {"PA_GDL_W": "16", "PA_GDL_ND": "16", "PA_GDL_RS": "1"}),
     ("ring3", {"PA_GDL_RING": "3"}),
     ("ring4", {"PA_GDL_RING": "4"}),
     ("ring3_w8_nd8", {"PA_GDL_RING": "3", "PA_GDL_W": "8", "PA_GDL_ND": "8"}),
