@@ -1487,11 +1487,13 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
       if (SK == 1 + SRC_INT) {
         __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + lk, (uint64_t)iv[j], WG_RLX);
       } else if (SK == 1 + SRC_LONG) {
+        // (low and high partial sums in two arrays of 8-byte slots: interleaved 16-byte slots left a u64 atomic's
+        // 16 lanes only 8 bank pairs)
         if (narrow) {
-          __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + 2 * lk, (uint64_t)iv[j], WG_RLX);
+          __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + lk, (uint64_t)iv[j], WG_RLX);
         } else {
-          __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + 2 * lk, (uint64_t)(uint32_t)iv[j], WG_RLX);
-          __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + 2 * lk + 1, (uint64_t)(iv[j] >> 32), WG_RLX);
+          __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + lk, (uint64_t)(uint32_t)iv[j], WG_RLX);
+          __hip_atomic_fetch_add((lds_u64_t*)lds_ptr(lds + off_s) + KR + lk, (uint64_t)(iv[j] >> 32), WG_RLX);
         }
       } else if (SK == 1 + SRC_DOUBLE) {
         atomicAdd((double*)(lds + off_s) + lk, __builtin_bit_cast(double, iv[j]));
@@ -1537,8 +1539,8 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
     const uint32_t c = cnt[lk];
     gc[k] = c;
     if (SK == 1 + SRC_LONG) {
-      const int64_t lo = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[2 * lk];
-      const int64_t hi = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[2 * lk + 1];
+      const int64_t lo = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[lk];
+      const int64_t hi = (int64_t)((const lds_u64_t*)lds_ptr(lds + off_s))[KR + lk];
       // (narrow: lo holds the whole sum S; the pair is (S mod 2^32, S >> 32), the same total)
       gs[2 * k] = narrow ? (int64_t)(uint32_t)lo : lo;
       gs[2 * k + 1] = narrow ? (lo >> 32) : hi;
