@@ -380,8 +380,10 @@ int jit_plan(pa_query* q, const Prep& P, int cus) {
   struct Cand {
     int w, nd, rs;
   };
-  std::vector<Cand> cands = {{16, 16, 1}, {16, 8, 1}, {8, 16, 1}, {8, 8, 1}, {16, 16, 2}, {16, 8, 2}, {12, 16, 1},
-                             {12, 8, 1}};
+  // (12 waves of 1024-doc tiles beat 16 of 512-doc tiles: own-dictionary secondary lines 1.130 / 1.159 vs 1.158 / 1.206
+  // ms; 8 waves of 1024-doc tiles beat 12 of 512: shared 1.391 vs 1.425 ms; 12 of 512 beat 8 of 512: 1.425 vs 1.594 ms)
+  std::vector<Cand> cands = {{16, 16, 1}, {12, 16, 1}, {16, 8, 1}, {8, 16, 1}, {12, 8, 1}, {8, 8, 1}, {16, 16, 2},
+                             {16, 8, 2}};
   auto keep_only = [&](const char* env, int Cand::*f) {
     if (const char* e = std::getenv(env)) {
       const int v = std::atoi(e);
