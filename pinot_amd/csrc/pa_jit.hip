@@ -743,9 +743,12 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   int rn = 2;
   if (const char* e = std::getenv("PA_PVE_RING")) rn = std::max(2, std::min(4, std::atoi(e)));
   if (hmode || q->limit_walk) rn = 2;
+  // compacted put rounds (PA_PVE_Q: measurement): a queue of 512 records (partition + record words) per wave
+  const bool pq = std::getenv("PA_PVE_Q") != nullptr;
+  const size_t qbytes = pq ? (size_t)4 * 512 * (rw + 1) : 0;
   auto waves_for = [&](int nd, int bs) {
     for (int cand : {16, 12, 8, 4})
-      if (lds_ring(bs) + (size_t)cand * (rn * image_bytes(nd) + val_bytes(nd)) <= kLdsBudget) return cand;
+      if (lds_ring(bs) + (size_t)cand * (rn * image_bytes(nd) + val_bytes(nd) + qbytes) <= kLdsBudget) return cand;
     return 0;
   };
   // H: 8 docs per lane (a lane's run of MV values is half as long: measured 3.97 vs 4.8 ms on configs[4]); 32-record
@@ -773,7 +776,8 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   const size_t l_ring = lds_ring(bs);
   const size_t l_val = l_ring + (size_t)w * rn * img_bytes;
   const size_t vbytes = val_bytes(nd);
-  const size_t lds = l_val + (size_t)w * vbytes;
+  const size_t l_q = l_val + (size_t)w * vbytes;
+  const size_t lds = l_q + (size_t)w * qbytes;
   // one workgroup per CU; a workgroup's region holds its docs' records (H: at most max_values per doc) in whole chunks
   // plus one partial chunk per partition; chunks of sc bins, more when the region would need 2^16 chunks
   std::vector<int64_t> first(q->nseg + 1, 0);  // the kernel's own tiles of td docs
@@ -810,7 +814,8 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
       "-DPVE_H=" + std::to_string(hmode ? 1 : 0), "-DPVE_HNB=" + std::to_string(hnb), "-DPVE_LG=" + std::to_string(lg),
       "-DPVE_L_VAL=" + std::to_string(l_val), "-DPVE_VAL_B=" + std::to_string(vbytes),
       "-DPVE_KOFF=" + std::to_string(any_koff ? 1 : 0), "-DPVE_VOFF=" + std::to_string(any_voff ? 1 : 0),
-      "-DPVE_KR=" + std::to_string(hmode ? 0 : h.part_kr_v), "-DPVE_RING=" + std::to_string(rn)};
+      "-DPVE_KR=" + std::to_string(hmode ? 0 : h.part_kr_v), "-DPVE_RING=" + std::to_string(rn), "-DPVE_Q=" + std::to_string(pq ? 1 : 0),
+      "-DPVE_L_Q=" + std::to_string(l_q)};
   if (const char* dbg = std::getenv("PA_PVE_DBG")) defs.push_back(std::string("-DPVE_DBG=") + dbg);  // (measurement)
   if (const char* pb = std::getenv("PA_PVE_PB")) defs.push_back(std::string("-DPVE_PB=") + pb);      // (measurement)
   if (std::getenv("PA_PVE_DONE_RTN")) defs.push_back("-DPVE_DONE_RTN=1");                            // (measurement)

@@ -98,6 +98,12 @@ constexpr u32 kSentinel = 0xffffffffu;
 #ifndef PVE_VOFF
 #define PVE_VOFF 0  // the value column's table-wide value id = dictId + PveSeg.voff
 #endif
+#ifndef PVE_Q
+#define PVE_Q 0  // compacted put rounds: a wave queues its records in LDS, each put round takes 64 PB of them
+#endif
+#ifndef PVE_L_Q
+#define PVE_L_Q 0  // LDS byte offset of the waves' queues (PVE_QB bytes each)
+#endif
 #ifndef PVE_RING
 #define PVE_RING 2  // tile images per wave (V streams without admission loads: RING - 1 tiles in flight)
 #endif
@@ -239,6 +245,8 @@ __device__ __forceinline__ void keys(u32 img, int lane, u32 (&key)[ND]) {
 
 struct Bins {
   u32 cnt, done, chunks, cur, fill, next, bins;
+  u32 q;                      // PVE_Q: the wave's queue (partitions [kQN], then RW record-word arrays [kQN])
+  mutable u32 qhead, qtail;   // (wave-uniform record counters of the queue)
   u32* recs;
   u32* table;
   i64 region, C;
@@ -401,6 +409,57 @@ __device__ __forceinline__ void put_round(const Bins& B, bool (&pend)[PB], const
   }
 }
 
+// Compacted put rounds (PVE_Q): a lane's records join the wave's queue in LDS (positions by ballot prefix counts), and
+// a put round runs only when the queue holds 64 PB records, every lane taking PB consecutive ones; the rest waits for
+// the next tile (the wave's last records go at the end of its tiles). A put round then carries 64 PB records whatever
+// the filter kept or however unevenly the lanes' MV value runs are spread.
+constexpr u32 kQN = 512;  // queue entries: < 64 PB left + 64 PB pushed
+static_assert(!PVE_Q || 128 * PB <= (int)kQN, "queue too small for the put round");
+__device__ __forceinline__ void q_push(const Bins& B, const bool (&pend)[PB], const u32 (&pp)[PB],
+                                       const u32 (&rr)[PB][RW]) {
+  u32 n = B.qtail;
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const u64 b = __builtin_amdgcn_ballot_w64(pend[i]);
+    if (pend[i]) {
+      const u32 pos = (n + __builtin_amdgcn_mbcnt_hi((u32)(b >> 32), __builtin_amdgcn_mbcnt_lo((u32)b, 0u))) & (kQN - 1);
+      at<l32>(B.q)[pos] = pp[i];
+#pragma unroll
+      for (int k = 0; k < RW; ++k) at<l32>(B.q + 4u * kQN * (u32)(k + 1))[pos] = rr[i][k];
+    }
+    n += (u32)__builtin_popcountll(b);
+  }
+  B.qtail = n;
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (a wave's LDS operations run in order: the round's reads see these)
+}
+__device__ __forceinline__ void q_drain(const Bins& B, int lane, bool all) {
+  while (B.qtail - B.qhead >= 64u * (u32)PB || (all && B.qtail != B.qhead)) {
+    bool pend[PB];
+    u32 pp[PB], rr[PB][RW];
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const u32 idx = B.qhead + (u32)lane * (u32)PB + (u32)i;
+      pend[i] = idx - B.qhead < B.qtail - B.qhead;
+      const u32 pos = idx & (kQN - 1);
+      pp[i] = pend[i] ? at<const l32>(B.q)[pos] : 0u;
+#pragma unroll
+      for (int k = 0; k < RW; ++k) rr[i][k] = pend[i] ? at<const l32>(B.q + 4u * kQN * (u32)(k + 1))[pos] : 0u;
+    }
+    const u32 take = B.qtail - B.qhead < 64u * (u32)PB ? B.qtail - B.qhead : 64u * (u32)PB;
+    B.qhead += take;
+    put_round(B, pend, pp, rr, lane);
+  }
+}
+__device__ __forceinline__ void put_any(const Bins& B, bool (&pend)[PB], const u32 (&pp)[PB], const u32 (&rr)[PB][RW],
+                                        int lane) {
+  if constexpr (PVE_Q) {
+    q_push(B, pend, pp, rr);
+    q_drain(B, lane, false);
+  } else {
+    put_round(B, pend, pp, rr, lane);
+  }
+}
+
 // the V stream: the lane's matching docs (bits of m), PB at a time
 __device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], const u32 (&val)[ND][RW], int lane) {
 #pragma unroll
@@ -415,7 +474,7 @@ __device__ __forceinline__ void put(const Bins& B, u32 m, const u32 (&key)[ND], 
 #pragma unroll
       for (int k = 1; k < RW; ++k) rr[i][k] = val[h + i][k];
     }
-    put_round(B, pend, pp, rr, lane);
+    put_any(B, pend, pp, rr, lane);
   }
 }
 
@@ -501,7 +560,7 @@ __device__ __forceinline__ void put_values(const Bins& B, CS* sg, i64 wt, u32 m,
       rr[j][0] = ((k[j] & kmask) << (LG + 6)) | ((hv[j] >> 8) << 6) | ((hv[j] & 0xffu) << 1);
     }
     if constexpr (PVE_DBG != 1) {
-      put_round(B, pend, pp, rr, lane);
+      put_any(B, pend, pp, rr, lane);
     } else {  // (measurement: records built, kept live, not put)
       u32 x = 0;
 #pragma unroll
@@ -630,6 +689,8 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
   B.C = A->chunks_per_wg;
   B.region = lb * B.C;
   B.err = A->matched + 3;
+  B.q = base + (u32)PVE_L_Q + (u32)wave * 4u * kQN * (u32)(RW + 1);
+  B.qhead = B.qtail = 0u;
   for (int i = tid; i < 5 * P + 1; i += W * 64) smem[i] = 0u;
   __syncthreads();
   const i64 t0 = lb * T / G, t1 = (lb + 1) * T / G;
@@ -678,6 +739,7 @@ extern "C" __global__ void __launch_bounds__(W * 64, 1) pve_jit(const PveArgs* a
       slot = slot + 1 == R ? 0 : slot + 1;
     }
   }
+  if constexpr (PVE_Q) q_drain(B, lane, true);  // (the wave's last queued records)
   vm_wait<0>();
   u64 wm = matched;
 #pragma unroll
