@@ -743,8 +743,12 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   int rn = 2;
   if (const char* e = std::getenv("PA_PVE_RING")) rn = std::max(2, std::min(4, std::atoi(e)));
   if (hmode || q->limit_walk) rn = 2;
-  // compacted put rounds (PA_PVE_Q: measurement): a queue of 512 records (partition + record words) per wave
-  const bool pq = std::getenv("PA_PVE_Q") != nullptr;
+  // compacted put rounds: a queue of 512 records (partition + record words) per wave, for a V stream whose filter is
+  // expected to keep less than half the docs (configs[2] 10 %: 0.409 vs 0.496 ms per 200M docs; on every doc it costs
+  // resident waves: 1.38 vs 1.20 ms, and the H stream's uneven MV runs gain nothing: 5.26 vs 3.89 ms). PA_PVE_Q=0 / 1
+  // forces it (measurement)
+  bool pq = !hmode && P.has_filter && P.post_density < 0.5 * (double)kWTileDocs;
+  if (const char* e = std::getenv("PA_PVE_Q")) pq = std::atoi(e) != 0;
   const size_t qbytes = pq ? (size_t)4 * 512 * (rw + 1) : 0;
   auto waves_for = [&](int nd, int bs) {
     for (int cand : {16, 12, 8, 4})
@@ -882,7 +886,8 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   S.parts = Pn;
   S.bin_shift = __builtin_ctz((unsigned)bs);
   S.chunks = C;
-  PLAN_LOG("pve %s: W %d nd %d bs %d sc %d grid %d lds %zu C %lld P %d", hmode ? "H" : "V", w, nd, bs, sc, G, lds,
+  PLAN_LOG("pve %s: W %d nd %d bs %d sc %d queue %d grid %d lds %zu C %lld P %d", hmode ? "H" : "V", w, nd, bs, sc,
+           (int)pq, G, lds,
            (long long)C, Pn);
   return PA_OK;
 }
