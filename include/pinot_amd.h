@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define PA_ABI_VERSION 3
+#define PA_ABI_VERSION 4
 
 /* limits of one query shape */
 #define PA_MAX_LEAVES 16
@@ -82,6 +82,8 @@ extern "C" {
 #define PA_LEAF_RAW_RANGE 2  /* ilo<=v<=ihi (INT/LONG) or dlo<=v<=dhi (FLOAT/DOUBLE) on a raw column       */
 #define PA_LEAF_MV_DICT_RANGE 3 /* MV column: any value with lo <= dictId < hi (MVScanDocIdIterator)      */
 #define PA_LEAF_MV_DICT_SET 4   /* MV column: any value whose bit is set in lut                            */
+#define PA_LEAF_RAW_SET 5       /* raw column: v is one of the leaf's num_values values (IN / NOT IN on a no-dictionary
+                                   column: RawValueBasedInPredicateEvaluatorFactory.java's value sets), any list size */
 
 /* postfix filter program opcodes; PA_OP_LEAF carries the leaf index in bits 8..15 */
 #define PA_OP_LEAF 0
@@ -238,6 +240,9 @@ typedef struct {
   const uint32_t* lut;  /* DICT_SET: host bitmap, ceil(cardinality/32) words, bit (id&31) of word id>>5 */
   int64_t ilo, ihi;     /* RAW_RANGE on INT/LONG, inclusive */
   double dlo, dhi;      /* RAW_RANGE on FLOAT/DOUBLE, inclusive */
+  const void* values;   /* RAW_SET: host int64_t[num_values] (INT/LONG column) or double[num_values] (FLOAT/DOUBLE:
+                           the stored float widened), strictly ascending; copied at bind */
+  int64_t num_values;
 } pa_leaf_params;
 
 typedef struct pa_query pa_query;

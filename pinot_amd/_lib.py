@@ -14,7 +14,7 @@ PA_MAX_GROUP_BY = 8
 PA_MAX_AGGS = 16
 
 PA_INT, PA_LONG, PA_FLOAT, PA_DOUBLE, PA_STRING, PA_BYTES = range(6)
-PA_LEAF_DICT_RANGE, PA_LEAF_DICT_SET, PA_LEAF_RAW_RANGE, PA_LEAF_MV_DICT_RANGE, PA_LEAF_MV_DICT_SET = range(5)
+PA_LEAF_DICT_RANGE, PA_LEAF_DICT_SET, PA_LEAF_RAW_RANGE, PA_LEAF_MV_DICT_RANGE, PA_LEAF_MV_DICT_SET, PA_LEAF_RAW_SET = range(6)
 PA_OP_LEAF, PA_OP_AND, PA_OP_OR, PA_OP_NOT = range(4)
 PA_AGG_COUNT, PA_AGG_SUM, PA_AGG_MIN, PA_AGG_MAX, PA_AGG_DISTINCTCOUNTHLL, PA_AGG_COUNT_MV, PA_AGG_DISTINCTCOUNT = range(7)
 PA_QF_STAGE_ALL = 1
@@ -50,7 +50,7 @@ PA_BIT_AND, PA_BIT_OR, PA_BIT_NOT = -1, -2, -3
 PA_BIT_PROG_MAX = 64
 PA_ACC_COUNT_U64, PA_ACC_SUM_I64, PA_ACC_SUM_F64, PA_ACC_MIN_I64, PA_ACC_MAX_I64, PA_ACC_HLL_U8, \
     PA_ACC_SUM_I64X2, PA_ACC_DOCS_U64, PA_ACC_KEYS_I64, PA_ACC_PRESENCE_U8 = range(10)
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # every symbol declared in include/pinot_amd.h
 EXPORTED = [
@@ -111,6 +111,7 @@ class LeafParams(ctypes.Structure):
         ("lut", ctypes.POINTER(ctypes.c_uint32)),
         ("ilo", ctypes.c_int64), ("ihi", ctypes.c_int64),
         ("dlo", ctypes.c_double), ("dhi", ctypes.c_double),
+        ("values", ctypes.c_void_p), ("num_values", ctypes.c_int64),
     ]
 
 

@@ -44,6 +44,20 @@ int pa_query_bind_segment(pa_query* q, int32_t index, const pa_segment* seg, con
       if (!leaf_params[l].lut) return fail(PA_EINVAL, "DICT_SET leaf without lut");
       const size_t words = ((size_t)it->second->cardinality + 31) / 32;
       q->luts[index][l].assign(leaf_params[l].lut, leaf_params[l].lut + words);
+    } else if (kind == PA_LEAF_RAW_SET) {  // (the values, 8 bytes each, kept as word pairs)
+      auto it = seg->cols.find(s.leaves[l].column_id);
+      if (it == seg->cols.end()) return fail(PA_EINVAL, "leaf column missing in segment");
+      const int64_t n = leaf_params[l].num_values;
+      if (n < 0 || n > (int64_t(1) << 30) || (n > 0 && !leaf_params[l].values))
+        return fail(PA_EINVAL, "RAW_SET leaf: bad value list");
+      const bool integral = it->second->vtype == PA_INT || it->second->vtype == PA_LONG;
+      const int64_t* vi = (const int64_t*)leaf_params[l].values;
+      const double* vd = (const double*)leaf_params[l].values;
+      for (int64_t i = 1; i < n; ++i)
+        if (integral ? !(vi[i - 1] < vi[i]) : !(vd[i - 1] < vd[i]))
+          return fail(PA_EINVAL, "RAW_SET leaf: values must be strictly ascending");
+      const uint32_t* w = (const uint32_t*)leaf_params[l].values;
+      q->luts[index][l].assign(w, w + 2 * n);
     }
   }
   q->remaps[index].assign(s.num_group_by, {});

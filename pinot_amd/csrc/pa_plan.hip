@@ -817,7 +817,7 @@ int build_segments(pa_query* q, Prep& P) {
         if (dc.kind != COL_SV_DICT) return fail(PA_EINVAL, "dictionary leaf on a non-dictionary column");
       } else if (L.kind == PA_LEAF_MV_DICT_RANGE || L.kind == PA_LEAF_MV_DICT_SET) {
         if (dc.kind != COL_MV_DICT) return fail(PA_EINVAL, "multi-value leaf on a single-value column");
-      } else if (L.kind == PA_LEAF_RAW_RANGE) {
+      } else if (L.kind == PA_LEAF_RAW_RANGE || L.kind == PA_LEAF_RAW_SET) {
         if (dc.kind != COL_SV_RAW) return fail(PA_EINVAL, "raw leaf on a non-raw column");
       }
       if (L.kind == PA_LEAF_DICT_RANGE) {
@@ -845,6 +845,22 @@ int build_segments(pa_query* q, Prep& P) {
         rc = upload_owned(q, lut.data(), lut.size() * 4, &dp);
         if (rc) return rc;
         L.lut = (const uint32_t*)dp;
+      } else if (L.kind == PA_LEAF_RAW_SET) {
+        // the sorted values (binary search per doc); the first and last bound the search. An empty set matches no
+        // doc: an empty range
+        const auto& w = q->luts[si][lit.leaf];
+        const int64_t n = (int64_t)w.size() / 2;
+        void* dp = nullptr;
+        rc = upload_owned(q, w.data(), std::max<size_t>(w.size(), 2) * 4, &dp);
+        if (rc) return rc;
+        L.lut = (const uint32_t*)dp;
+        L.span = (int32_t)n;
+        const int64_t* vi = (const int64_t*)w.data();
+        const double* vd = (const double*)w.data();
+        L.ilo = n ? vi[0] : 1;
+        L.ihi = n ? vi[n - 1] : 0;
+        L.dlo = n ? vd[0] : 1.0;
+        L.dhi = n ? vd[n - 1] : 0.0;
       } else {
         L.ilo = p.ilo;
         L.ihi = p.ihi;

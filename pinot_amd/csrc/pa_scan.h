@@ -681,6 +681,33 @@ __device__ void accumulate_doc_mv(const DevQuery* __restrict__ q, const DevSeg* 
   }
 }
 
+// RAW_SET membership (RawValueBasedInPredicateEvaluatorFactory's value sets): the set's first / last value bound it,
+// then a binary search of the sorted values (a few L2-resident loads per doc)
+template <class LeafT>
+__device__ __forceinline__ bool raw_set_has(const LeafT& L, int64_t x) {
+  if (x < L.ilo || x > L.ihi) return false;
+  const AS1 int64_t* v = gp((const int64_t*)L.lut);
+  int32_t b = 0, n = L.span;
+  while (n > 1) {
+    const int32_t h = n >> 1;
+    b = v[b + h] <= x ? b + h : b;
+    n -= h;
+  }
+  return v[b] == x;
+}
+template <class LeafT>
+__device__ __forceinline__ bool raw_set_has(const LeafT& L, double x) {
+  if (!(x >= L.dlo && x <= L.dhi)) return false;
+  const AS1 double* v = gp((const double*)L.lut);
+  int32_t b = 0, n = L.span;
+  while (n > 1) {
+    const int32_t h = n >> 1;
+    b = v[b + h] <= x ? b + h : b;
+    n -= h;
+  }
+  return v[b] == x;
+}
+
 // Match word of one leaf over a whole wave tile: bit i of lane l <=> doc 64*i + l of the tile matches.
 // Leaf parameters are loaded once per tile; the 32 decodes are independent, so the LDS reads pipeline.
 template <int STEPS, class LeafT = DevLeaf>
@@ -744,6 +771,18 @@ __device__ __forceinline__ uint32_t leaf_bits(const LeafT& L, const uint32_t* im
         }
       }
     }  // filter columns are always staged (pa_query_prepare), so there is no lazy filter-decode path
+  } else if (L.kind == PA_LEAF_RAW_SET) {  // coalesced loads of the raw values, a set lookup each
+    const int64_t d0 = doc_base + lane;
+    for (int i = 0; i < STEPS; ++i) {
+      bool m;
+      switch (L.vtype) {
+        case PA_INT: m = raw_set_has(L, (int64_t)gp((const int32_t*)L.raw)[d0 + i * kWave]); break;
+        case PA_LONG: m = raw_set_has(L, gp((const int64_t*)L.raw)[d0 + i * kWave]); break;
+        case PA_FLOAT: m = raw_set_has(L, (double)gp((const float*)L.raw)[d0 + i * kWave]); break;
+        default: m = raw_set_has(L, gp((const double*)L.raw)[d0 + i * kWave]); break;
+      }
+      bits |= (uint32_t)m << i;
+    }
   } else {  // PA_LEAF_RAW_RANGE: coalesced loads of the raw values
     const int64_t d0 = doc_base + lane;
     switch (L.vtype) {
@@ -818,6 +857,13 @@ __device__ __forceinline__ bool leaf_match_doc(const DevLeaf& L, int64_t doc) {
       m = (id - lo) < span;
     } else {
       m = (gp(L.lut)[id >> 5] >> (id & 31u)) & 1u;
+    }
+  } else if (L.kind == PA_LEAF_RAW_SET) {
+    switch (L.vtype) {
+      case PA_INT: m = raw_set_has(L, (int64_t)gp((const int32_t*)L.raw)[doc]); break;
+      case PA_LONG: m = raw_set_has(L, gp((const int64_t*)L.raw)[doc]); break;
+      case PA_FLOAT: m = raw_set_has(L, (double)gp((const float*)L.raw)[doc]); break;
+      default: m = raw_set_has(L, gp((const double*)L.raw)[doc]); break;
     }
   } else {
     switch (L.vtype) {

@@ -338,7 +338,7 @@ class GpuQueryExecutor:
                 spec.aggs[i].num_values = len(vd)
 
         # filter
-        filt = P.expand_raw_in(q.filter, seg0) if q.filter is not None else None
+        filt = q.filter
         leaves, ops = [], []
         if filt is not None:
             _flatten_filter(filt, leaves, ops)
@@ -437,6 +437,11 @@ class GpuQueryExecutor:
                     lp.ilo = max(min(int(p.ilo), P.LONG_MAX), P.LONG_MIN)
                     lp.ihi = max(min(int(p.ihi), P.LONG_MAX), P.LONG_MIN)
                     lp.dlo, lp.dhi = float(p.dlo), float(p.dhi)
+                    if p.kind == L.PA_LEAF_RAW_SET:
+                        vals = np.ascontiguousarray(p.values)
+                        self._keep.append(vals)
+                        lp.values = vals.ctypes.data if len(vals) else None
+                        lp.num_values = len(vals)
             rms = (ctypes.c_void_p * max(1, len(q.group_by)))()
             for j, rm in enumerate(self.remaps[si]):
                 if rm is not None:

@@ -30,7 +30,7 @@ import numpy as np
 
 from . import _lib as L
 from . import query as Q
-from .predicate import DictLeaf, dictionary_leaf, expand_raw_in
+from .predicate import DictLeaf, dictionary_leaf
 
 EOF = -1
 BATCH = 256  # BlockDocIdIterator.OPTIMAL_ITERATOR_BATCH_SIZE
@@ -285,16 +285,15 @@ def _eval(f, bitmaps, start):
 
 
 class _LeafCursor:
-    """Walks the reference's (unexpanded) predicates in the engine's leaf order: a raw IN / NOT IN became an OR of
-    equality leaves on the GPU (predicate.expand_raw_in); its doc mask is rebuilt from those leaves."""
+    """Walks the reference's predicates in the engine's leaf order (one leaf per predicate: a raw IN / NOT IN is one
+    RAW_SET leaf)."""
 
     def __init__(self, bitmaps, segment):
         self.bitmaps, self.segment, self.k = bitmaps, segment, 0
 
     def take(self, pred):
-        sub = expand_raw_in(pred, self.segment)
-        m = _eval(sub, self.bitmaps, self.k)
-        self.k += _count_leaves(sub)
+        m = self.bitmaps[self.k]
+        self.k += 1
         return m
 
     def param(self):
@@ -424,7 +423,7 @@ def segment_index_info(segment):
 def entries_scanned_in_filter(filt, segment, bitmaps, index_info=None):
     """numEntriesScannedInFilter of one segment when the projection iterates the filter to the end.
     filt: the query's filter tree (None = no filter); bitmaps: bool[leaves, num_docs] in the engine's leaf order
-    (predicate.expand_raw_in + the engine's flattening); index_info(column) -> (inverted index, range index, range index
+    (the engine's flattening); index_info(column) -> (inverted index, range index, range index
     exact)."""
     if filt is None:
         return 0
@@ -441,7 +440,7 @@ def entries_scanned_in_filter(filt, segment, bitmaps, index_info=None):
 
 def filter_mask(filt, segment, bitmaps):
     """The filter's doc mask of one segment from the leaf bitmaps (numDocsScanned per segment)."""
-    return _eval(expand_raw_in(filt, segment), bitmaps, 0)
+    return _eval(filt, bitmaps, 0)
 
 
 def filter_is_match_all(filt, segment, bitmaps, index_info=None):
@@ -506,7 +505,7 @@ def server_stats(query, segments, leaf_bitmaps):
 # re-run of a leap-frog's last chain; pa_stats.hip). The replay stays for the shapes outside that engine: a NOT child of
 # a leap-frogging AND (NotDocIdIterator mixes next() batches and advance() on its child), an AND or NOT child of an OR
 # child of one, a NOT over a leap-frog with an OR child (the re-run after the end starts from the OR children's cached
-# answers), raw IN lists longer than a bitmap program, and inexact (v1) range indexes.
+# answers), and inexact (v1) range indexes.
 class _Unsupported(Exception):
     pass
 
@@ -534,11 +533,9 @@ class _RpnCursor(_LeafCursor):
         self.params, self.last = params, None
 
     def take(self, pred):
-        sub = expand_raw_in(pred, self.segment)
-        p = _rpn(sub, self.k)
-        n = _count_leaves(sub)
-        self.last = self.k if n == 1 else None
-        self.k += n
+        p = [self.k]
+        self.last = self.k
+        self.k += 1
         return p
 
     def param(self):

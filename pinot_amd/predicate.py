@@ -17,7 +17,7 @@ from typing import Optional
 import numpy as np
 
 from . import query as Q
-from ._lib import PA_LEAF_DICT_RANGE, PA_LEAF_DICT_SET, PA_LEAF_RAW_RANGE
+from ._lib import PA_LEAF_DICT_RANGE, PA_LEAF_DICT_SET, PA_LEAF_RAW_RANGE, PA_LEAF_RAW_SET
 
 INT_MIN, INT_MAX = -(1 << 31), (1 << 31) - 1
 LONG_MIN, LONG_MAX = -(1 << 63), (1 << 63) - 1
@@ -74,6 +74,7 @@ class RawLeaf:
     dhi: float = np.inf
     negate: bool = False
     kind: int = PA_LEAF_RAW_RANGE
+    values: object = None  # RAW_SET: int64 (INT/LONG) or float64 (FLOAT/DOUBLE) sorted unique values
 
 
 def _ids_leaf(ids, negate):
@@ -124,10 +125,19 @@ def dictionary_leaf(pred, column) -> DictLeaf:
 
 
 def raw_leaf(pred, column) -> RawLeaf:
-    """Inclusive bounds for a raw-value range/eq predicate (Int/Long/Float/DoubleRawValueBased evaluators)."""
+    """Inclusive bounds for a raw-value range/eq predicate (Int/Long/Float/DoubleRawValueBased evaluators); an IN /
+    NOT IN list is one RAW_SET leaf of its stored values, sorted and unique (RawValueBasedInPredicateEvaluatorFactory.java:
+    the values parsed with the column type's parse into a set; FLOAT values as the stored float, widened)."""
     dt = column.data_type
     integral = dt in ("INT", "LONG")
     lo_min, hi_max = (INT_MIN, INT_MAX) if dt == "INT" else (LONG_MIN, LONG_MAX)
+    if isinstance(pred, (Q.InPredicate, Q.NotInPredicate)):
+        vals = [stored_value(v, dt) for v in pred.values]
+        arr = (np.unique(np.asarray(vals, dtype=np.int64)) if integral else
+               np.unique(np.asarray([float(v) for v in vals], dtype=np.float64)))
+        if not integral:
+            arr = arr[~np.isnan(arr)]
+        return RawLeaf(negate=isinstance(pred, Q.NotInPredicate), kind=PA_LEAF_RAW_SET, values=arr)
     if isinstance(pred, (Q.EqPredicate, Q.NotEqPredicate)):
         v = stored_value(pred.value, dt)
         neg = isinstance(pred, Q.NotEqPredicate)
@@ -154,18 +164,3 @@ def raw_leaf(pred, column) -> RawLeaf:
     raise TypeError("unsupported raw predicate %r" % (pred,))
 
 
-def expand_raw_in(f, segment):
-    """IN / NOT IN on raw columns -> OR of equality leaves (each a RAW_RANGE [v, v])."""
-    if f is None:
-        return None
-    if isinstance(f, Q.And):
-        return Q.And(tuple(expand_raw_in(c, segment) for c in f.children))
-    if isinstance(f, Q.Or):
-        return Q.Or(tuple(expand_raw_in(c, segment) for c in f.children))
-    if isinstance(f, Q.Not):
-        return Q.Not(expand_raw_in(f.child, segment))
-    col = segment.column(f.column)
-    if not col.has_dictionary and isinstance(f, (Q.InPredicate, Q.NotInPredicate)):
-        ors = Q.Or(tuple(Q.EqPredicate(f.column, v) for v in f.values))
-        return Q.Not(ors) if isinstance(f, Q.NotInPredicate) else ors
-    return f

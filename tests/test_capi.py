@@ -32,7 +32,7 @@ def test_struct_layout_matches_header():
     # pa_query_spec: 4 + 16*8 + 4 + 48*4 + 4 + 8*4 (+4 pad) + 8*8 + 4 (+4 pad) + 16*24 + 4 + 4
     assert ctypes.sizeof(L.LeafSpec) == 8
     assert ctypes.sizeof(L.AggSpec) == 24
-    assert ctypes.sizeof(L.LeafParams) == 56
+    assert ctypes.sizeof(L.LeafParams) == 72  # (+ RAW_SET values, num_values: ABI 4)
     assert ctypes.sizeof(L.QuerySpec) == 848  # (+ flags2, reserved2)
 
 

@@ -17,11 +17,11 @@ from pinot_amd.engine import _flatten_filter
 
 
 def leaf_masks(query, seg):
-    """bool[leaves, docs] in the engine's leaf order (expand_raw_in + postfix flattening), evaluated with numpy."""
+    """bool[leaves, docs] in the engine's leaf order (postfix flattening), evaluated with numpy."""
     if query.filter is None:
         return None
     leaves, ops = [], []
-    _flatten_filter(P.expand_raw_in(query.filter, seg), leaves, ops)
+    _flatten_filter(query.filter, leaves, ops)
     out = np.zeros((len(leaves), seg.num_docs), dtype=bool)
     for i, pred in enumerate(leaves):
         col = seg.column(pred.column)
@@ -141,7 +141,7 @@ def test_range_index_serves_eq_but_not_in():
 
 def _leaves(q, seg):
     leaves, ops = [], []
-    _flatten_filter(P.expand_raw_in(q.filter, seg), leaves, ops)
+    _flatten_filter(q.filter, leaves, ops)
     return leaves
 
 
