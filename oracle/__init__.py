@@ -164,6 +164,13 @@ def _dict_match(pred, col):
         i = index_of(_parse(pred.value, dt))
         if i >= 0:
             m[i] = 0
+    elif isinstance(pred, Q.RegexpLikePredicate):
+        # DictionaryBasedRegexpLikePredicateEvaluator.applySV: Matcher.find() on the dictionary value
+        # (RegexpLikePredicateEvaluatorFactory.java), restated with re.search
+        import re
+        rx = re.compile(pred.pattern)
+        for i, v in enumerate(values):
+            m[i] = 1 if rx.search(str(v)) else 0
     elif isinstance(pred, Q.InPredicate):
         for v in pred.values:
             i = index_of(_parse(v, dt))

@@ -160,7 +160,7 @@ typedef struct {
 
 typedef struct {
   int32_t num_ops;
-  const int32_t* ops;       /* postfix, OQ_LEAF | leaf << 8 */
+  const int32_t* ops;       /* postfix, OQ_LEAF | leaf << 8 (leaf index: the upper 24 bits) */
   int32_t num_leaves;
   const oracle_leaf* leaves;
   int32_t num_gb;
@@ -245,7 +245,7 @@ static int filter_match(const mv_cursor* mc, const oracle_query* q, const oracle
   int sp = 0;
   for (int i = 0; i < q->num_ops; ++i) {
     const int op = q->ops[i] & 0xff;
-    if (op == OQ_LEAF) st[sp++] = leaf_match(mc, &q->leaves[(q->ops[i] >> 8) & 0xff], cols, doc);
+    if (op == OQ_LEAF) st[sp++] = leaf_match(mc, &q->leaves[((uint32_t)q->ops[i] >> 8) & 0xffffffu], cols, doc);
     else if (op == OQ_NOT) st[sp - 1] = !st[sp - 1];
     else {
       const int b = st[--sp];

@@ -305,6 +305,13 @@ def _leaf_op(pred, seg, mask, index_info, lf=None):
     has it already (the executor's bound leaf parameters)."""
     col = seg.column(pred.column)
     sv = col.single_value
+    if isinstance(pred, Q.RegexpLikePredicate):
+        # DictionaryBasedRegexpLikePredicateEvaluator never sets _alwaysTrue / _alwaysFalse, and without an FST index
+        # FilterOperatorUtils.java:108-117 picks the scan whatever the column's sorted / inverted index
+        weights = None if sv else col.mv_lengths(seg.num_docs)
+        op = _Op("scan", SCAN_P + (0 if sv else 50), mask, weights=weights)
+        op.column = pred.column
+        return op
     if col.has_dictionary:
         # dictionary-based predicate evaluators: always false with no matching dictId, always true with all of them
         if lf is None:

@@ -121,6 +121,14 @@ def dictionary_leaf(pred, column) -> DictLeaf:
         if end < start:
             end = start
         return DictLeaf(PA_LEAF_DICT_RANGE, start, end)
+    if isinstance(pred, Q.RegexpLikePredicate):
+        # DictionaryBasedRegexpLikePredicateEvaluator (RegexpLikePredicateEvaluatorFactory.java): STRING / JSON
+        # dictionaries only, applySV(dictId) = the pattern found in the value (Matcher.find(); Python's re.search on
+        # the patterns both regex dialects read alike). Resolved once per segment to the matching dictIds
+        if dt not in ("STRING", "JSON"):
+            raise ValueError("REGEXP_LIKE: unsupported data type %s" % dt)
+        rx = re.compile(pred.pattern)
+        return _ids_leaf([i for i, v in enumerate(column.dictionary) if rx.search(str(v))], False)
     raise TypeError("unsupported predicate %r" % (pred,))
 
 

@@ -5,7 +5,8 @@ parser for the SQL subset the reference's query tests use on this path:
   [LIMIT n] [OPTION(k=v, ...)]
 
 filter: AND / OR / NOT / ( ) over  col = v | col != v | col <> v | col < v | col <= v | col > v | col >= v |
-        col BETWEEN a AND b | col IN (...) | col NOT IN (...)
+        col BETWEEN a AND b | col IN (...) | col NOT IN (...) | REGEXP_LIKE(col, 'regex') | col [NOT] LIKE 'pattern'
+REGEXP_LIKE / LIKE become RegexpLikePredicate as in RequestContextUtils.java:231-236 (LIKE through likeToRegexpLike).
 Comparison predicates become RangePredicate exactly as the reference's RequestContextUtils does
 (pinot-common/.../request/context/RequestContextUtils.java: >, >=, <, <=, BETWEEN -> RANGE).
 Aggregations: COUNT(*), SUM, MIN, MAX, AVG, MINMAXRANGE, DISTINCTCOUNT, DISTINCTSUM, DISTINCTAVG, DISTINCTCOUNTHLL(col[, log2m]) and their *MV
@@ -56,6 +57,48 @@ class RangePredicate:
 
 
 @dataclass(frozen=True)
+class RegexpLikePredicate:
+    """REGEXP_LIKE(col, pattern): a value matches when the pattern is found in it (Matcher.find(),
+    RegexpLikePredicateEvaluatorFactory.java); LIKE arrives converted by like_to_regexp."""
+    column: str
+    pattern: str
+
+
+def like_to_regexp(like):
+    """RegexpPatternConverterUtils.likeToRegexpLike, restated from its test vectors (RegexpPatternConverterUtilsTest.java):
+    leading / trailing '%' runs drop the '^' / '$' anchor, '%' -> '.*', '_' -> '.', a backslash escapes the next
+    character (a trailing lone backslash is a literal one), regex metacharacters are escaped."""
+    n = len(like)
+    start, end = 0, n
+    while start < end and like[start] == "%":
+        start += 1
+    while end > start and like[end - 1] == "%" and not (end - 2 >= start and like[end - 2] == "\\"):
+        end -= 1
+    out = ["^"] if start == 0 else []
+    i = start
+    while i < end:
+        c = like[i]
+        if c == "\\":
+            if i + 1 < end:
+                out.append("\\" + like[i + 1])
+                i += 2
+                continue
+            out.append("\\\\")
+        elif c == "%":
+            out.append(".*")
+        elif c == "_":
+            out.append(".")
+        elif c in ".^$*+?()[]{}|":
+            out.append("\\" + c)
+        else:
+            out.append(c)
+        i += 1
+    if end == n:
+        out.append("$")
+    return "".join(out)
+
+
+@dataclass(frozen=True)
 class And:
     children: Tuple
 
@@ -86,7 +129,7 @@ class Comparison:
     rhs: Tuple
 
 
-PREDICATES = (EqPredicate, NotEqPredicate, InPredicate, NotInPredicate, RangePredicate)
+PREDICATES = (EqPredicate, NotEqPredicate, InPredicate, NotInPredicate, RangePredicate, RegexpLikePredicate)
 
 
 # AggregationFunctionType names the hot path runs: single-value functions and their multi-value (*MV) forms, which
@@ -296,6 +339,13 @@ class _Parser:
                 raise ValueError("expected a literal or column at %r" % (rhs,))
             self.i += 1
             return Comparison(lhs, "=" if op[1] == "=" else "!=", (rhs[0], rhs[1]))
+        if tok[0] == "id" and tok[1].upper() == "REGEXP_LIKE" and nxt == ("op", "("):
+            self.i += 2
+            col = self.ident()
+            self.expect_op(",")
+            pat = self.literal()
+            self.expect_op(")")
+            return RegexpLikePredicate(col, str(pat))
         col = self.ident()
         if self.kw("BETWEEN"):
             lo = self.literal()
@@ -303,6 +353,9 @@ class _Parser:
             hi = self.literal()
             return RangePredicate(col, lo, True, hi, True)
         negate = self.kw("NOT")
+        if self.kw("LIKE"):
+            f = RegexpLikePredicate(col, like_to_regexp(str(self.literal())))
+            return Not(f) if negate else f
         if self.kw("IN"):
             self.expect_op("(")
             vals = [self.literal()]
@@ -311,7 +364,7 @@ class _Parser:
             self.expect_op(")")
             return NotInPredicate(col, tuple(vals)) if negate else InPredicate(col, tuple(vals))
         if negate:
-            raise ValueError("NOT must be followed by IN here")
+            raise ValueError("NOT must be followed by IN or LIKE here")
         tok = self.peek()
         if tok[0] != "op":
             raise ValueError("expected comparison at %r" % (tok,))

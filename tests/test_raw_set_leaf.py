@@ -47,3 +47,16 @@ def test_raw_set_matches_the_oracle():
             lf = P.raw_leaf(q.filter, seg.column(col))
             m = np.isin(vals.astype(np.float64) if col in ("rf", "rd") else vals.astype(np.int64), lf.values)
             assert int((~m if neg else m).sum()) == oracle.run_query(q, [seg]).row[0], (col, neg)
+
+
+def test_oracle_evaluates_lists_past_256_values():
+    """The oracle expands a raw IN list into one equality leaf per value (its restatement of the reference's per-value
+    set test); its postfix ops carry the leaf index in 24 bits (8 bits wrapped past 256 values)."""
+    seg = _seg()
+    vals = np.unique(seg.column("ri").raw_values)
+    lits = ", ".join(str(int(v)) for v in vals[::2]) + ", " + ", ".join(str(10_000 + i) for i in range(300))
+    q = parse_sql("SELECT COUNT(*) FROM t WHERE ri IN (%s)" % lits)
+    lf = P.raw_leaf(q.filter, seg.column("ri"))
+    assert len(lf.values) > 256
+    want = int(np.isin(seg.column("ri").raw_values.astype(np.int64), lf.values).sum())
+    assert oracle.run_query(q, [seg]).num_docs_scanned == want
