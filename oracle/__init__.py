@@ -266,6 +266,7 @@ _AGG = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "DISTINCTCOUNTHLL": 4, "COUNTM
 _ORACLE_FNS = {"SUM": ("SUM",), "AVG": ("SUM",), "MIN": ("MIN",), "MAX": ("MAX",),
                "DISTINCTCOUNTHLL": ("DISTINCTCOUNTHLL",), "SUMMV": ("SUM",), "MINMV": ("MIN",), "MAXMV": ("MAX",),
                "DISTINCTCOUNTHLLMV": ("DISTINCTCOUNTHLL",), "COUNTMV": ("COUNTMV",), "AVGMV": ("SUM", "COUNTMV"),
+               "DISTINCTCOUNTRAWHLL": ("DISTINCTCOUNTHLL",), "DISTINCTCOUNTRAWHLLMV": ("DISTINCTCOUNTHLL",),
                "COUNT": ("COUNT",), "MINMAXRANGE": ("MIN", "MAX"), "MINMAXRANGEMV": ("MIN", "MAX"),
                "DISTINCTCOUNT": ("DISTINCTCOUNT",), "DISTINCTCOUNTMV": ("DISTINCTCOUNT",),
                "DISTINCTSUM": ("DISTINCTCOUNT",), "DISTINCTSUMMV": ("DISTINCTCOUNT",),
@@ -292,7 +293,7 @@ def _run_segment_raw(query, segment):
         virt[c] = np.unique(segment.column(c).raw_values, return_inverse=True)
     ocols = (OCol * max(1, len(cols_order) + len(virt)))()
     keep = []
-    hll_cols = {a.column for a in query.aggregations if a.function in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV")}
+    hll_cols = {a.column for a in query.aggregations if a.function in Q.HLL_FUNCTIONS}
     for name, i in cidx.items():
         col = segment.column(name)
         oc = ocols[i]
@@ -486,6 +487,7 @@ def _constant_filters(query, segments):
 def run_query(query, segments):
     """Server-level intermediate result for a segment set, merged by key value in segment order."""
     query = _constant_filters(query, segments)
+    from pinot_amd import query as Q  # query model only (data classes)
     from pinot_amd.engine import AvgPair, IntermediateResult, MinMaxRangePair
     from pinot_amd.hll import HyperLogLog
     merged = {}
@@ -534,7 +536,7 @@ def run_query(query, segments):
                 vals.append(AvgPair(row[ai[0]], int(row[ai[1]])))
             elif a.function == "COUNTMV":
                 vals.append(int(row[ai]))
-            elif a.function in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV"):
+            elif a.function in Q.HLL_FUNCTIONS:
                 vals.append(HyperLogLog(a.log2m, row[ai] if isinstance(row[ai], np.ndarray) else None))
             elif a.function in ("MINMAXRANGE", "MINMAXRANGEMV"):
                 vals.append(MinMaxRangePair(row[ai[0]], row[ai[1]]))

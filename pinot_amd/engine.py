@@ -302,7 +302,7 @@ class GpuQueryExecutor:
                 self.agg_map.append(acc_index((L.PA_AGG_MIN, ids[a.column], 0)))
             elif fn in ("MAX", "MAXMV"):
                 self.agg_map.append(acc_index((L.PA_AGG_MAX, ids[a.column], 0)))
-            elif fn in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV"):
+            elif fn in Q.HLL_FUNCTIONS:
                 self.agg_map.append(acc_index((L.PA_AGG_DISTINCTCOUNTHLL, ids[a.column], a.log2m)))
             elif fn in ("MINMAXRANGE", "MINMAXRANGEMV"):
                 # MinMaxRangePair(min, max): the MIN and MAX accumulators of the column
@@ -697,7 +697,7 @@ class GpuQueryExecutor:
                 cols.append([AvgPair(s_, int(c_)) for s_, c_ in zip(outs[pi[0]].tolist(), outs[pi[1]].tolist())])
             elif a.function == "COUNTMV":
                 cols.append([int(v) for v in outs[pi].tolist()])
-            elif a.function in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV"):
+            elif a.function in Q.HLL_FUNCTIONS:
                 log2m = self.pa_aggs[pi][2]
                 regs = outs[pi].reshape(n, 1 << log2m)
                 cols.append([HyperLogLog(log2m, regs[r]) for r in range(n)])
@@ -731,7 +731,7 @@ class GpuQueryExecutor:
                 row.append({"COUNT": 0, "SUM": 0.0, "MIN": float("inf"), "MAX": float("-inf")}.get(fn) if fn in
                            ("COUNT", "SUM", "MIN", "MAX") else
                            AvgPair(0.0, 0) if fn == "AVG" else
-                           HyperLogLog(a.log2m) if fn == "DISTINCTCOUNTHLL" else
+                           HyperLogLog(a.log2m) if fn in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTRAWHLL") else
                            MinMaxRangePair(float("inf"), float("-inf")) if fn == "MINMAXRANGE" else set())
             res.row = row
         return res

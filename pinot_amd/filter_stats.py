@@ -459,7 +459,7 @@ def filter_is_match_all(filt, segment, bitmaps, index_info=None):
 
 # AggregationPlanNode.java:49-53
 DICTIONARY_BASED = {"MIN", "MINMV", "MAX", "MAXMV", "MINMAXRANGE", "MINMAXRANGEMV", "DISTINCTCOUNT", "DISTINCTCOUNTMV",
-                    "DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV", "DISTINCTSUM", "DISTINCTAVG", "DISTINCTSUMMV",
+                    "DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV", "DISTINCTCOUNTRAWHLL", "DISTINCTCOUNTRAWHLLMV", "DISTINCTSUM", "DISTINCTAVG", "DISTINCTSUMMV",
                     "DISTINCTAVGMV"}
 METADATA_BASED = {"COUNT", "MIN", "MINMV", "MAX", "MAXMV", "MINMAXRANGE", "MINMAXRANGEMV"}
 

@@ -9,7 +9,7 @@ filter: AND / OR / NOT / ( ) over  col = v | col != v | col <> v | col < v | col
 REGEXP_LIKE / LIKE become RegexpLikePredicate as in RequestContextUtils.java:231-236 (LIKE through likeToRegexpLike).
 Comparison predicates become RangePredicate exactly as the reference's RequestContextUtils does
 (pinot-common/.../request/context/RequestContextUtils.java: >, >=, <, <=, BETWEEN -> RANGE).
-Aggregations: COUNT(*), SUM, MIN, MAX, AVG, MINMAXRANGE, DISTINCTCOUNT, DISTINCTSUM, DISTINCTAVG, DISTINCTCOUNTHLL(col[, log2m]) and their *MV
+Aggregations: COUNT(*), SUM, MIN, MAX, AVG, MINMAXRANGE, DISTINCTCOUNT, DISTINCTSUM, DISTINCTAVG, DISTINCTCOUNTHLL(col[, log2m]), DISTINCTCOUNTRAWHLL(col[, log2m]) and their *MV
 forms.
 """
 import re
@@ -134,14 +134,21 @@ PREDICATES = (EqPredicate, NotEqPredicate, InPredicate, NotInPredicate, RangePre
 
 # AggregationFunctionType names the hot path runs: single-value functions and their multi-value (*MV) forms, which
 # aggregate every value of a multi-value column (SumMVAggregationFunction, CountMVAggregationFunction, ...)
-SUPPORTED_FUNCTIONS = ("SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNTHLL", "MINMAXRANGE", "DISTINCTCOUNT",
+SUPPORTED_FUNCTIONS = ("SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNTHLL", "DISTINCTCOUNTRAWHLL", "MINMAXRANGE", "DISTINCTCOUNT",
                        "DISTINCTSUM", "DISTINCTAVG",
-                       "COUNTMV", "SUMMV", "MINMV", "MAXMV", "AVGMV", "DISTINCTCOUNTHLLMV", "MINMAXRANGEMV",
+                       "COUNTMV", "SUMMV", "MINMV", "MAXMV", "AVGMV", "DISTINCTCOUNTHLLMV", "DISTINCTCOUNTRAWHLLMV",
+                       "MINMAXRANGEMV",
                        "DISTINCTCOUNTMV", "DISTINCTSUMMV", "DISTINCTAVGMV")
 # BaseDistinctAggregateAggregationFunction subclasses: the intermediate result is the set of distinct values (one
 # presence accumulator on the GPU); they differ only in extractFinalResult (size / sum / average)
 DISTINCT_SET_FUNCTIONS = ("DISTINCTCOUNT", "DISTINCTSUM", "DISTINCTAVG", "DISTINCTCOUNTMV", "DISTINCTSUMMV",
                           "DISTINCTAVGMV")
+
+
+# HyperLogLog functions: one register set per group (DistinctCountHLLAggregationFunction); the RAW forms differ only in
+# the final result, the serialized registers (DistinctCountRawHLLAggregationFunction: SerializedHLL.toString, the hex
+# of HyperLogLog.getBytes)
+HLL_FUNCTIONS = ("DISTINCTCOUNTHLL", "DISTINCTCOUNTHLLMV", "DISTINCTCOUNTRAWHLL", "DISTINCTCOUNTRAWHLLMV")
 
 
 def base_function(fn):

@@ -26,7 +26,7 @@ def merge_value(fn, a, b):
         return max(a, b)
     if fn == "AVG":
         return AvgPair(a.sum + b.sum, a.count + b.count)
-    if fn == "DISTINCTCOUNTHLL":
+    if fn in ("DISTINCTCOUNTHLL", "DISTINCTCOUNTRAWHLL"):
         return HyperLogLog(a.log2m, a.registers).add_all(b)
     if fn == "MINMAXRANGE":  # MinMaxRangePair.apply
         return MinMaxRangePair(min(a.min, b.min), max(a.max, b.max))
@@ -41,6 +41,8 @@ def final_value(fn, v):
         return v.sum / v.count if v.count else -math.inf
     if fn == "DISTINCTCOUNTHLL":
         return v.cardinality()
+    if fn == "DISTINCTCOUNTRAWHLL":
+        return SerializedHLL(v)
     if fn == "MINMAXRANGE":  # MinMaxRangeAggregationFunction.extractFinalResult: max - min
         return v.max - v.min
     if fn == "DISTINCTCOUNT":  # DistinctCountAggregationFunction.extractFinalResult: the set's size
@@ -83,6 +85,20 @@ def merge_intermediate(results):
     return out
 
 
+class SerializedHLL(str):
+    """DISTINCTCOUNTRAWHLL's final result (SerializedHLL.java): the string is BytesUtils.toHexString of
+    HyperLogLog.getBytes(); ORDER BY compares cardinalities (compareTo)."""
+
+    def __new__(cls, hll):
+        s = str.__new__(cls, hll.to_bytes().hex())
+        s.cardinality = hll.cardinality()
+        return s
+
+
+def _sort_value(v):
+    return v.cardinality if isinstance(v, SerializedHLL) else v
+
+
 def _order_key_fn(query):
     """Comparator over (key, final values) following ORDER BY; ties broken by group key for determinism."""
     items = []
@@ -100,8 +116,8 @@ def _order_key_fn(query):
 
     def cmp(x, y):
         for kind, idx, asc in items:
-            a = x[1][idx] if kind == "agg" else x[0][idx]
-            b = y[1][idx] if kind == "agg" else y[0][idx]
+            a = _sort_value(x[1][idx]) if kind == "agg" else x[0][idx]
+            b = _sort_value(y[1][idx]) if kind == "agg" else y[0][idx]
             if a != b:
                 c = -1 if a < b else 1
                 return c if asc else -c

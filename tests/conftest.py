@@ -33,6 +33,16 @@ def golden_segment(golden_spec):
                           inverted_index_columns=("column6", "column7", "column11", "column17", "column18"))
 
 
+def golden_rows(got, case):
+    """A golden case's result rows as the reference's test compares them: with "extract": "hll_cardinality" each value
+    is a serialized HyperLogLog (DISTINCTCOUNTRAWHLL's hex string) whose cardinality is compared
+    (InterSegmentAggregationSingleValueQueriesTest.testDistinctCountRawHLL's cardinalityExtractor)."""
+    if case.get("extract") != "hll_cardinality":
+        return got
+    from pinot_amd.hll import HyperLogLog
+    return [[HyperLogLog.from_bytes(bytes.fromhex(v)).cardinality() for v in row] for row in got]
+
+
 def rows_match(got, expected, delta):
     if len(got) != len(expected):
         return False

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import oracle
-from conftest import rows_match
+from conftest import golden_rows, rows_match
 from pinot_amd import _lib as L
 from pinot_amd import parse_sql
 from pinot_amd.engine import AvgPair, GpuQueryExecutor, GpuSegment, MinMaxRangePair
@@ -88,7 +88,7 @@ def test_golden_cases_gpu(golden_spec, golden_segment):
             assert_same(server, exp)
             broker = merge_intermediate([server_trim(server, q)] * 2)
             got = final_result_table(broker, q)
-            if case["rows"] is not None and not rows_match(got, case["rows"], case["delta"]):
+            if case["rows"] is not None and not rows_match(golden_rows(got, case), case["rows"], case["delta"]):
                 failures.append((case["source"], got[:3], case["rows"][:3]))
             if "limit_reached" in case and broker.num_groups_limit_reached != case["limit_reached"]:
                 failures.append((case["source"], "numGroupsLimitReached", broker.num_groups_limit_reached))

@@ -9,7 +9,7 @@ import pytest
 import oracle
 from pinot_amd import parse_sql
 from pinot_amd.reduce import final_result_table, merge_intermediate, server_trim
-from conftest import rows_match
+from conftest import golden_rows, rows_match
 
 
 def _broker(query, segment, servers=2, per_server=2):
@@ -23,7 +23,7 @@ def test_golden_cases(golden_spec, golden_segment):
     for case in golden_spec["cases"]:
         q = parse_sql(case["sql"])
         got, merged = _broker(q, golden_segment)
-        if case["rows"] is not None and not rows_match(got, case["rows"], case["delta"]):
+        if case["rows"] is not None and not rows_match(golden_rows(got, case), case["rows"], case["delta"]):
             failures.append((case["source"], case["sql"], got[:5], case["rows"][:5]))
         # BrokerResponseNative.isNumGroupsLimitReached: OR over the servers' DataTable metadata
         if "limit_reached" in case and merged.num_groups_limit_reached != case["limit_reached"]:
