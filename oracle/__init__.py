@@ -270,7 +270,32 @@ _ORACLE_FNS = {"SUM": ("SUM",), "AVG": ("SUM",), "MIN": ("MIN",), "MAX": ("MAX",
                "COUNT": ("COUNT",), "MINMAXRANGE": ("MIN", "MAX"), "MINMAXRANGEMV": ("MIN", "MAX"),
                "DISTINCTCOUNT": ("DISTINCTCOUNT",), "DISTINCTCOUNTMV": ("DISTINCTCOUNT",),
                "DISTINCTSUM": ("DISTINCTCOUNT",), "DISTINCTSUMMV": ("DISTINCTCOUNT",),
-               "DISTINCTAVG": ("DISTINCTCOUNT",), "DISTINCTAVGMV": ("DISTINCTCOUNT",)}
+               "DISTINCTAVG": ("DISTINCTCOUNT",), "DISTINCTAVGMV": ("DISTINCTCOUNT",),
+               "DISTINCTCOUNTBITMAP": ("DISTINCTCOUNT",), "DISTINCTCOUNTBITMAPMV": ("DISTINCTCOUNT",)}
+
+
+def _java_hash(v, dt):
+    """Object.hashCode of a stored value as DistinctCountBitmapAggregationFunction.convertToValueBitmap
+    (DistinctCountBitmapAggregationFunction.java:410-446) adds it: Integer (the value), Long ((int)(v ^ v >>> 32)),
+    Float (floatToIntBits), Double (doubleToLongBits folded like Long), String (s[0]*31^(n-1) + ... over UTF-16 units)."""
+    import struct
+    if dt == "INT":
+        h = int(v)
+    elif dt == "LONG":
+        x = int(v) % (1 << 64)
+        h = x ^ (x >> 32)
+    elif dt == "FLOAT":
+        h = 0x7FC00000 if v != v else struct.unpack("<I", struct.pack("<f", float(v)))[0]
+    elif dt == "DOUBLE":
+        x = 0x7FF8000000000000 if v != v else struct.unpack("<Q", struct.pack("<d", float(v)))[0]
+        h = x ^ (x >> 32)
+    else:
+        h = 0
+        u = str(v).encode("utf-16-le")
+        for i in range(0, len(u), 2):
+            h = (h * 31 + (u[i] | (u[i + 1] << 8))) % (1 << 32)
+    h %= 1 << 32
+    return h - (1 << 32) if h >= 1 << 31 else h
 
 
 def _pack_msb(ids, nb):
@@ -540,6 +565,9 @@ def run_query(query, segments):
                 vals.append(HyperLogLog(a.log2m, row[ai] if isinstance(row[ai], np.ndarray) else None))
             elif a.function in ("MINMAXRANGE", "MINMAXRANGEMV"):
                 vals.append(MinMaxRangePair(row[ai[0]], row[ai[1]]))
+            elif a.function in ("DISTINCTCOUNTBITMAP", "DISTINCTCOUNTBITMAPMV"):
+                dt = segments[0].column(a.column).data_type
+                vals.append({_java_hash(x, dt) for x in row[ai]})
             elif a.function in ("DISTINCTCOUNT", "DISTINCTCOUNTMV", "DISTINCTSUM", "DISTINCTSUMMV", "DISTINCTAVG",
                                 "DISTINCTAVGMV"):
                 vals.append(set(row[ai]))

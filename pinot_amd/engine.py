@@ -23,6 +23,7 @@ from . import _lib as L
 from . import predicate as P
 from . import query as Q
 from .hll import HyperLogLog, hash_value
+from .java_hash import java_hash_code
 from .optimizer import optimize_filter
 from .segment import Segment
 
@@ -707,7 +708,12 @@ class GpuQueryExecutor:
                 # the value set of BaseDistinctAggregateAggregationFunction (DISTINCTCOUNT / DISTINCTSUM / DISTINCTAVG)
                 vd = self.value_dicts[pi]
                 pres = outs[pi].reshape(n, self._presence_stride(pi))[:, :len(vd)]
-                cols.append([set(vd[np.flatnonzero(pres[r])].tolist()) for r in range(n)])
+                if a.function in Q.BITMAP_FUNCTIONS:  # (DISTINCTCOUNTBITMAP: the values' Java hash codes)
+                    dt = self.segs[0].column(a.column).data_type
+                    hc = np.array([java_hash_code(v, dt) for v in vd.tolist()], dtype=np.int64)
+                    cols.append([set(hc[np.flatnonzero(pres[r])].tolist()) for r in range(n)])
+                else:
+                    cols.append([set(vd[np.flatnonzero(pres[r])].tolist()) for r in range(n)])
             else:
                 cols.append(outs[pi].tolist())
         rows = list(zip(*cols)) if cols else [()] * n

@@ -135,15 +135,21 @@ PREDICATES = (EqPredicate, NotEqPredicate, InPredicate, NotInPredicate, RangePre
 # AggregationFunctionType names the hot path runs: single-value functions and their multi-value (*MV) forms, which
 # aggregate every value of a multi-value column (SumMVAggregationFunction, CountMVAggregationFunction, ...)
 SUPPORTED_FUNCTIONS = ("SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNTHLL", "DISTINCTCOUNTRAWHLL", "MINMAXRANGE", "DISTINCTCOUNT",
+                       "DISTINCTCOUNTBITMAP", "DISTINCTCOUNTBITMAPMV",
                        "DISTINCTSUM", "DISTINCTAVG",
                        "COUNTMV", "SUMMV", "MINMV", "MAXMV", "AVGMV", "DISTINCTCOUNTHLLMV", "DISTINCTCOUNTRAWHLLMV",
                        "MINMAXRANGEMV",
                        "DISTINCTCOUNTMV", "DISTINCTSUMMV", "DISTINCTAVGMV")
 # BaseDistinctAggregateAggregationFunction subclasses: the intermediate result is the set of distinct values (one
 # presence accumulator on the GPU); they differ only in extractFinalResult (size / sum / average)
-DISTINCT_SET_FUNCTIONS = ("DISTINCTCOUNT", "DISTINCTSUM", "DISTINCTAVG", "DISTINCTCOUNTMV", "DISTINCTSUMMV",
+DISTINCT_SET_FUNCTIONS = ("DISTINCTCOUNT", "DISTINCTSUM", "DISTINCTAVG", "DISTINCTCOUNTBITMAP", "DISTINCTCOUNTMV",
+                          "DISTINCTCOUNTBITMAPMV", "DISTINCTSUMMV",
                           "DISTINCTAVGMV")
 
+
+# DistinctCountBitmapAggregationFunction: the same value presence per group, reported as the set of the values' Java
+# hash codes (its RoaringBitmap: java_hash.py), so equal hash codes count once
+BITMAP_FUNCTIONS = ("DISTINCTCOUNTBITMAP", "DISTINCTCOUNTBITMAPMV")
 
 # HyperLogLog functions: one register set per group (DistinctCountHLLAggregationFunction); the RAW forms differ only in
 # the final result, the serialized registers (DistinctCountRawHLLAggregationFunction: SerializedHLL.toString, the hex

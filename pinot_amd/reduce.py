@@ -30,7 +30,8 @@ def merge_value(fn, a, b):
         return HyperLogLog(a.log2m, a.registers).add_all(b)
     if fn == "MINMAXRANGE":  # MinMaxRangePair.apply
         return MinMaxRangePair(min(a.min, b.min), max(a.max, b.max))
-    if fn in ("DISTINCTCOUNT", "DISTINCTSUM", "DISTINCTAVG"):  # BaseDistinctAggregateAggregationFunction.merge: union
+    if fn in ("DISTINCTCOUNT", "DISTINCTSUM", "DISTINCTAVG", "DISTINCTCOUNTBITMAP"):
+        # BaseDistinctAggregateAggregationFunction.merge: union (DISTINCTCOUNTBITMAP: RoaringBitmap.or)
         return set(a) | set(b)
     raise ValueError(fn)
 
@@ -45,7 +46,7 @@ def final_value(fn, v):
         return SerializedHLL(v)
     if fn == "MINMAXRANGE":  # MinMaxRangeAggregationFunction.extractFinalResult: max - min
         return v.max - v.min
-    if fn == "DISTINCTCOUNT":  # DistinctCountAggregationFunction.extractFinalResult: the set's size
+    if fn in ("DISTINCTCOUNT", "DISTINCTCOUNTBITMAP"):  # extractFinalResult: the set's size / the bitmap's cardinality
         return len(v)
     if fn in ("DISTINCTSUM", "DISTINCTAVG"):
         # DistinctSumAggregationFunction / DistinctAvgAggregationFunction.extractFinalResult: a double sum over the set
