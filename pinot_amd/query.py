@@ -297,7 +297,13 @@ class _Parser:
     def aggregation(self):
         fn = self.ident().upper()
         self.expect_op("(")
-        if fn == "COUNT":
+        if self.kw("DISTINCT"):
+            # CalciteSqlParser.java:761-772: COUNT / SUM / AVG (DISTINCT x) -> DISTINCTCOUNT / DISTINCTSUM / DISTINCTAVG,
+            # any other aggregation on DISTINCT is refused
+            if fn not in ("COUNT", "SUM", "AVG"):
+                raise ValueError("Function '%s' on DISTINCT is not supported." % fn)
+            fn = "DISTINCT" + fn
+        elif fn == "COUNT":
             self.expect_op("*")
             self.expect_op(")")
             return Aggregation("COUNT")

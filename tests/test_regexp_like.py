@@ -84,3 +84,13 @@ def test_statistics_take_the_scan_operator(sorted_col, pattern):
     seg = _seg(sorted_col=sorted_col)
     op = FS._leaf_op(Q.RegexpLikePredicate("s", pattern), seg, None, lambda c: (False, False, True))
     assert op.kind == "scan"
+
+
+def test_distinct_quantifier_rewrites():
+    """CalciteSqlParser.java:761-772: COUNT / SUM / AVG (DISTINCT x) are DISTINCTCOUNT / DISTINCTSUM / DISTINCTAVG; any
+    other aggregation on DISTINCT is refused."""
+    q = parse_sql("SELECT COUNT(DISTINCT a), SUM(DISTINCT b), AVG(DISTINCT c), COUNT(*) FROM t GROUP BY d")
+    assert [(a.function, a.column) for a in q.aggregations] == [("DISTINCTCOUNT", "a"), ("DISTINCTSUM", "b"),
+                                                               ("DISTINCTAVG", "c"), ("COUNT", None)]
+    with pytest.raises(ValueError):
+        parse_sql("SELECT MAX(DISTINCT a) FROM t")
