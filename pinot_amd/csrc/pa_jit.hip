@@ -735,10 +735,17 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   };
   auto lds_ring = [&](int bs) { return al16(al16((size_t)(5 * Pn + 1) * 4) + (size_t)Pn * bs * rw * 4); };
   // H: a wave's buffer for one tile's MV value words (stage_values: at most max_values values per doc, whole 16-byte
-  // chunks from a 16-byte aligned start, one word of look-ahead)
+  // chunks from a 16-byte aligned start, one word of look-ahead; the run rounds read a window of up to 9 words)
   auto val_bytes = [&](int nd) {
-    return hmode ? (size_t)16 * (((size_t)max_values * 64 * nd * hnb / 32 + 9 + 3) / 4) : (size_t)0;
+    return hmode ? (size_t)16 * (((size_t)max_values * 64 * nd * hnb / 32 + 17 + 3) / 4) : (size_t)0;
   };
+  // H run rounds: one claim per run of up to hb values of one doc (its values share the doc's key); hb = the column's
+  // most values per doc up to 8, so a run is normally a whole doc. PA_PVE_HRUN=0 keeps one claim per value
+  // (measurement), PA_PVE_HB sets the run length
+  bool hrun = true;
+  if (const char* e = std::getenv("PA_PVE_HRUN")) hrun = std::atoi(e) != 0;
+  int hb = (int)std::max<int64_t>(1, std::min<int64_t>(8, max_values));
+  if (const char* e = std::getenv("PA_PVE_HB")) hb = std::max(1, std::min(8, std::atoi(e)));
   // tile images per wave (PA_PVE_RING: measurement; the H stream and admission loads keep two)
   int rn = 2;
   if (const char* e = std::getenv("PA_PVE_RING")) rn = std::max(2, std::min(4, std::atoi(e)));
@@ -819,7 +826,8 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
       "-DPVE_L_VAL=" + std::to_string(l_val), "-DPVE_VAL_B=" + std::to_string(vbytes),
       "-DPVE_KOFF=" + std::to_string(any_koff ? 1 : 0), "-DPVE_VOFF=" + std::to_string(any_voff ? 1 : 0),
       "-DPVE_KR=" + std::to_string(hmode ? 0 : h.part_kr_v), "-DPVE_RING=" + std::to_string(rn), "-DPVE_Q=" + std::to_string(pq ? 1 : 0),
-      "-DPVE_L_Q=" + std::to_string(l_q)};
+      "-DPVE_L_Q=" + std::to_string(l_q), "-DPVE_HRUN=" + std::to_string(hmode && hrun ? 1 : 0),
+      "-DPVE_HB=" + std::to_string(hb)};
   if (const char* dbg = std::getenv("PA_PVE_DBG")) defs.push_back(std::string("-DPVE_DBG=") + dbg);  // (measurement)
   if (const char* pb = std::getenv("PA_PVE_PB")) defs.push_back(std::string("-DPVE_PB=") + pb);      // (measurement)
   if (std::getenv("PA_PVE_DONE_RTN")) defs.push_back("-DPVE_DONE_RTN=1");                            // (measurement)
@@ -886,8 +894,8 @@ static int pve_stream(pa_query* q, const Prep& P, int cus, bool hmode, int rw, i
   S.parts = Pn;
   S.bin_shift = __builtin_ctz((unsigned)bs);
   S.chunks = C;
-  PLAN_LOG("pve %s: W %d nd %d bs %d sc %d queue %d grid %d lds %zu C %lld P %d", hmode ? "H" : "V", w, nd, bs, sc,
-           (int)pq, G, lds,
+  PLAN_LOG("pve %s: W %d nd %d bs %d sc %d queue %d runs %d grid %d lds %zu C %lld P %d", hmode ? "H" : "V", w, nd, bs,
+           sc, (int)pq, hmode && hrun ? hb : 0, G, lds,
            (long long)C, Pn);
   return PA_OK;
 }

@@ -225,20 +225,51 @@ __global__ void __launch_bounds__(256) limit_agg_kernel(const DevQuery* __restri
 // so one workgroup per segment walks it in docId order with the key set as an LDS bitmap, instead of a first-position
 // pass over every doc: rounds of kWalkRound docs mark their keys with LDS atomicOr (the old bit tells "new": the
 // number of distinct new keys of a round is exact in any order); the round in which the count reaches L is undone and
-// replayed by one wave in docId order (64 docs at a time, duplicates inside a step resolved by lane order), stopping
-// at the L-th distinct key. The bitmap is then the segment's admitted keys (admitted_docs tests it in the scan).
+// replayed in docId order (64 docs a step, each step by the wave whose registers hold its keys, duplicates inside a
+// step resolved by lane order), stopping at the L-th distinct key. The bitmap is then the segment's admitted keys (admitted_docs tests it in the scan).
 constexpr int kWalkThreads = 1024;
 constexpr int kWalkPerThread = 8;
 constexpr int kWalkRound = kWalkThreads * kWalkPerThread;
 constexpr uint32_t kNoKey = 0xffffffffu;
 
-__device__ __forceinline__ uint32_t walk_key(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int64_t doc) {
-  if (doc >= seg->num_docs || !doc_passes(q, seg, doc)) return kNoKey;
-  uint32_t key = 0;
-  for (int j = 0; j < q->num_gb; ++j)
-    key += (uint32_t)gb_component<true>(seg->cols[q->gb_slot[j]], seg->remap[j], nullptr, 0, doc) *
-           (uint32_t)q->gb_stride[j];
-  return key;
+// The keys of a thread's kWalkPerThread docs of a round (doc0 + k kWalkThreads): columns outer, docs inner, so a
+// dictionary column's loads for every doc issue back to back (one HBM latency per column and per remap, not one per
+// doc and column)
+__device__ __forceinline__ void walk_keys(const DevQuery* __restrict__ q, const DevSeg* __restrict__ seg, int64_t doc0,
+                                          uint32_t (&key)[kWalkPerThread]) {
+  const int64_t nd = seg->num_docs;
+  int64_t doc[kWalkPerThread];
+  bool pass[kWalkPerThread];
+#pragma unroll
+  for (int k = 0; k < kWalkPerThread; ++k) {
+    const int64_t d = doc0 + (int64_t)k * kWalkThreads;
+    pass[k] = d < nd && doc_passes(q, seg, d);
+    doc[k] = d < nd ? d : (nd > 0 ? nd - 1 : 0);  // (a doc past the end reads the last one's words: no key taken)
+    key[k] = 0u;
+  }
+  for (int j = 0; j < q->num_gb; ++j) {
+    const DevCol& c = seg->cols[q->gb_slot[j]];
+    const int32_t* rm = seg->remap[j];
+    const uint32_t stride = (uint32_t)q->gb_stride[j];
+    if (c.kind == COL_SV_DICT) {
+      uint32_t id[kWalkPerThread];
+#pragma unroll
+      for (int k = 0; k < kWalkPerThread; ++k) id[k] = decode_global(c.words, doc[k], c.nbits);
+      if (rm != nullptr) {
+#pragma unroll
+        for (int k = 0; k < kWalkPerThread; ++k) id[k] = (uint32_t)gp(rm)[id[k]];
+      }
+#pragma unroll
+      for (int k = 0; k < kWalkPerThread; ++k) key[k] += id[k] * stride;
+    } else {
+#pragma unroll
+      for (int k = 0; k < kWalkPerThread; ++k)
+        key[k] += (uint32_t)gb_component<true>(c, rm, nullptr, 0, doc[k]) * stride;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kWalkPerThread; ++k)
+    if (!pass[k]) key[k] = kNoKey;
 }
 
 // G: the bitmap is the segment's admit bitmap in HBM (zeroed by the host; key spaces beyond kWalkMaxWords * 32 keys),
@@ -248,6 +279,8 @@ __global__ void __launch_bounds__(kWalkThreads) limit_walk_kernel(const DevQuery
                                                                    const DevSeg* __restrict__ segs, int64_t words) {
   extern __shared__ uint32_t lds_seen[];
   __shared__ uint32_t round_new[2];  // by round parity: a round resets its counter while the last one may be read
+  __shared__ int64_t relay_cnt;      // the replay's running count of distinct keys, step to step
+  __shared__ int relay_done;
   const DevSeg* seg = segs + blockIdx.x;
   uint32_t* adm = (uint32_t*)seg->admit;
   if (adm == nullptr) return;  // (workgroup-uniform) the limit cannot bind in this segment
@@ -264,8 +297,7 @@ __global__ void __launch_bounds__(kWalkThreads) limit_walk_kernel(const DevQuery
   for (int64_t d0 = 0; d0 < nd && !reached; d0 += kWalkRound, par ^= 1) {
     if (tid == 0) round_new[par] = 0u;
     uint32_t key[kWalkPerThread];
-#pragma unroll
-    for (int k = 0; k < kWalkPerThread; ++k) key[k] = walk_key(q, seg, d0 + (int64_t)k * kWalkThreads + tid);
+    walk_keys(q, seg, d0 + tid, key);
     __syncthreads();
     uint32_t mine = 0;  // bit k: this thread's doc k brought a key new to the bitmap
 #pragma unroll
@@ -284,14 +316,30 @@ __global__ void __launch_bounds__(kWalkThreads) limit_walk_kernel(const DevQuery
       cnt += rn;
       continue;
     }
-    // the L-th distinct key appears in this round: undo its marks, replay it in docId order with one wave
+    // the L-th distinct key appears in this round: undo its marks, replay it in docId order, 64 docs per step. The
+    // round's keys stay in the registers that computed them (doc d0 + k * kWalkThreads + tid), so step s (docs
+    // d0 + 64 s ..) is replayed by the wave holding them (wave s % waves, its key[s / waves]) and the running count
+    // passes from step to step through LDS, one barrier per step (a single replaying wave re-read every key from HBM,
+    // one dependent load per step)
 #pragma unroll
     for (int k = 0; k < kWalkPerThread; ++k)
       if ((mine >> k) & 1u) atomicAnd(seen + (key[k] >> 5), ~(1u << (key[k] & 31u)));
+    if (tid == 0) {
+      relay_cnt = cnt;
+      relay_done = 0;
+    }
     __syncthreads();
-    if (tid < kWave) {
-      for (int64_t b = d0; b < d0 + kWalkRound && b < nd; b += kWave) {
-        const uint32_t k0 = walk_key(q, seg, b + lane);
+    constexpr int kWaves = kWalkThreads / kWave;
+    const int wave = tid / kWave;
+    for (int st = 0; st < kWalkRound / kWave; ++st) {
+      const int64_t b = d0 + (int64_t)st * kWave;
+      if (b >= nd) break;  // (workgroup-uniform)
+      if (wave == st % kWaves) {
+        uint32_t k0 = kNoKey;
+#pragma unroll
+        for (int k = 0; k < kWalkPerThread; ++k)
+          if (k == st / kWaves) k0 = key[k];
+        const int64_t c0 = relay_cnt;
         // (an atomic load: in HBM the bitmap's lines may sit stale in this CU's L1 after the atomics at L2)
         bool cand = k0 != kNoKey &&
                     !((__hip_atomic_load(seen + (k0 >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (k0 & 31u)) & 1u);
@@ -308,8 +356,8 @@ __global__ void __launch_bounds__(kWalkThreads) limit_walk_kernel(const DevQuery
         const uint64_t nm = __ballot(nw);
         const int64_t c = __builtin_popcountll(nm);
         uint64_t take = nm;
-        if (cnt + c >= L) {  // keep the first L - cnt new keys of this step
-          int64_t need = L - cnt;
+        if (c0 + c >= L) {  // keep the first L - c0 new keys of this step
+          int64_t need = L - c0;
           uint64_t t = 0, r = nm;
           while (need-- > 0) {
             const uint64_t low = r & (~r + 1);
@@ -319,10 +367,15 @@ __global__ void __launch_bounds__(kWalkThreads) limit_walk_kernel(const DevQuery
           take = t;
         }
         if ((take >> lane) & 1ull) atomicOr(seen + (k0 >> 5), 1u << (k0 & 31u));
-        cnt += __builtin_popcountll(take);
-        if (cnt >= L) break;
+        if (lane == 0) {
+          relay_cnt = c0 + __builtin_popcountll(take);
+          relay_done = c0 + __builtin_popcountll(take) >= L ? 1 : 0;
+        }
       }
+      __syncthreads();
+      if (relay_done) break;  // (read after the barrier: workgroup-uniform)
     }
+    cnt = relay_cnt;
     reached = true;
     __syncthreads();
   }

@@ -26,6 +26,7 @@
 //   PVE_L_BINS, PVE_L_RING LDS byte offsets (state at 0: cnt[P], done[P], chunks[P], cur[P], fill[P], next)
 //   PVE_RW record words, PVE_RAWB / PVE_RAWOFF the staged raw value column, PVE_H the H stream (PVE_HNB, PVE_LG,
 //   PVE_L_VAL / PVE_VAL_B: per-wave LDS buffers of the tile's MV value words)
+//   PVE_HRUN / PVE_HB the H stream's run rounds: one claim per run of up to PVE_HB values of one doc
 //   PVE_KOFF / PVE_VOFF segments with their own dictionaries, each a contiguous run of the table-wide dictionary: the
 //   segment's offsets into the table key ids / value ids (PveSeg.koff, voff)
 typedef unsigned int u32;
@@ -103,6 +104,12 @@ constexpr u32 kSentinel = 0xffffffffu;
 #endif
 #ifndef PVE_L_Q
 #define PVE_L_Q 0  // LDS byte offset of the waves' queues (PVE_QB bytes each)
+#endif
+#ifndef PVE_HRUN
+#define PVE_HRUN 0  // H: one claim per run of up to PVE_HB values of one doc (they share the doc's key, so its partition)
+#endif
+#ifndef PVE_HB
+#define PVE_HB 4
 #endif
 #ifndef PVE_RING
 #define PVE_RING 2  // tile images per wave (V streams without admission loads: RING - 1 tiles in flight)
@@ -283,7 +290,10 @@ constexpr int kPieces = BS * RW / 4;  // 16-byte pieces of a bin
 // Every bin the wave completed (full[i] of its lanes) leaves together: eight lanes per bin (16 bytes each per store
 // instruction: a 32-record one-word bin is one instruction for eight bins), the group's first lane takes the chunk slot
 // and restarts the bin after the copy.
-__device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE_PB], const u32 (&pp)[PVE_PB], int lane) {
+// keep: lanes whose record-0 bin is restarted by the lane itself (PVE_HRUN: the claim's records past the bin's end
+// go into the new bin first)
+__device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE_PB], const u32 (&pp)[PVE_PB], int lane,
+                                           u64 keep = 0) {
   u64 fm[PVE_PB];
   u64 any = 0;
 #pragma unroll
@@ -295,6 +305,7 @@ __device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   const int grp = lane >> 3, sub = lane & 7;
   u32 mine = 0xffffffffu;
+  bool mkeep = false;
   int g = 0;
   auto round = [&]() {
     const bool on = grp < g;
@@ -313,13 +324,14 @@ __device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE
       }
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (the bin is read before it restarts: LDS runs one wave's ops in order)
-    if (on && sub == 0) {
+    if (on && sub == 0 && !mkeep) {
       at<l32>(B.done)[mine] = 0u;
       at<l32>(B.cnt)[mine] = 0u;
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     g = 0;
     mine = 0xffffffffu;
+    mkeep = false;
   };
 #pragma unroll
   for (int i = 0; i < PVE_PB; ++i) {
@@ -328,7 +340,10 @@ __device__ __forceinline__ void flush_full(const Bins& B, const bool (&full)[PVE
       const int l = __builtin_ctzll(m);
       m &= m - 1;
       const u32 p = (u32)__builtin_amdgcn_readlane((int)pp[i], l);
-      if (grp == g) mine = p;
+      if (grp == g) {
+        mine = p;
+        mkeep = i == 0 && ((keep >> l) & 1ull);
+      }
       if (++g == 8) round();
     }
   }
@@ -571,6 +586,127 @@ __device__ __forceinline__ void put_values(const Bins& B, CS* sg, i64 wt, u32 m,
   }
 }
 
+// The H stream by runs (PVE_HRUN): a lane walks its values in doc order, each round taking up to HB values of its
+// current doc (one partition: they share the doc's key) with ONE claim of as many slots (and one written count),
+// instead of one claim per value. A claim that runs past the bin's end belongs to the lane holding the bin's last
+// slot: it writes what fits, flushes the bin when every slot is written, then puts the rest into the restarted bin
+// itself (slots 0.., written count and claim counter set to that many: the other lanes' claims keep failing until the
+// counter drops below BS). A claim that finds the bin full is retried next round. The values' words come from one
+// window of NWIN words read once per round.
+constexpr int HB = PVE_HB;
+constexpr int NWIN = ((31 + (HB - 1) * HNB) >> 5) + 2;
+__device__ __forceinline__ void put_values_run(const Bins& B, CS* sg, i64 wt, u32 m, const u32 (&key)[ND], int lane,
+                                               u32 vbuf, u32 vb0, bool nxt) {
+  if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return;
+  if (nxt) vm_wait<kDmaImg>();
+  else vm_wait<0>();
+  const __attribute__((address_space(1))) int* off = (const __attribute__((address_space(1))) int*)sg->mv_off;
+  const l32* words = at<const l32>(vbuf);
+  const __attribute__((address_space(1))) u32* lut = (const __attribute__((address_space(1))) u32*)sg->hlut;
+  const i64 d0 = wt * TD + (i64)ND * lane, nd = sg->num_docs;
+  int o[ND + 1];
+#pragma unroll
+  for (int i = 0; i <= ND; ++i) o[i] = m ? off[d0 + i < nd ? d0 + i : nd] : 0;
+  int v = 0, e = 0;
+  if (m) {
+    const int f = __builtin_ctz(m), l = 31 - __builtin_clz(m);
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      if (i == f) v = o[i];
+      if (i == l) e = o[i + 1];
+    }
+  }
+  constexpr u32 kmask = (1u << KS) - 1u;
+  while (__builtin_amdgcn_ballot_w64(v < e) != 0) {
+    // the lane's current doc: the last one whose first value is not past v
+    u32 kk = key[0];
+    bool mm = m & 1u;
+    int end = o[1];
+#pragma unroll
+    for (int i = 1; i < ND; ++i)
+      if (v >= o[i]) {
+        kk = key[i];
+        mm = (m >> i) & 1u;
+        end = o[i + 1];
+      }
+    const int avail = v < e ? end - v : 0;
+    const u32 n = mm ? (u32)(avail < HB ? avail : HB) : 0u;
+    const u32 p = kk >> KS;
+    u32 rec[HB];
+    if (n) {
+      const u64 bit0 = (u64)(u32)v * (u64)HNB;
+      const u32 w0 = (u32)(bit0 >> 5) - vb0, sh = (u32)bit0 & 31u;
+      u32 win[NWIN];
+#pragma unroll
+      for (int k = 0; k < NWIN; ++k) win[k] = words[w0 + (u32)k];
+      u32 hv[HB];
+#pragma unroll
+      for (int j = 0; j < HB; ++j) {
+        const u32 q = sh + (u32)(j * HNB), wi = q >> 5, s2 = q & 31u;
+        u32 wa = win[0], wb = win[1];
+#pragma unroll
+        for (int k = 1; k + 1 < NWIN; ++k)
+          if (wi == (u32)k) {
+            wa = win[k];
+            wb = win[k + 1];
+          }
+        const u32 x = s2 ? __builtin_amdgcn_alignbit(wa, wb, 32u - s2) : wa;
+        hv[j] = (u32)j < n ? lut[x >> (32 - HNB)] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < HB; ++j) rec[j] = ((kk & kmask) << (LG + 6)) | ((hv[j] >> 8) << 6) | ((hv[j] & 0xffu) << 1);
+    }
+    if constexpr (PVE_DBG == 1) {  // (measurement: records built, kept live, not put)
+      u32 x = 0;
+#pragma unroll
+      for (int j = 0; j < HB; ++j) x ^= (u32)j < n ? rec[j] + p : 0u;
+      if (x == 0x9e3779b9u) *at<l32>(B.next) = x;
+      v = n ? v + (int)n : (v < e ? end : v);
+      continue;
+    }
+    const u32 s = n ? __hip_atomic_fetch_add(at<l32>(B.cnt) + p, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                    : 0xffffffffu;
+    const u32 w = s < (u32)BS ? ((u32)BS - s < n ? (u32)BS - s : n) : 0u;
+#pragma unroll
+    for (int j = 0; j < HB; ++j)
+      if ((u32)j < w) at<l32>(B.bins)[p * (u32)BS + s + (u32)j] = rec[j];
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (w) (void)__hip_atomic_fetch_add(at<l32>(B.done) + p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // the claimer of the bin's last slot waits until every slot is written (a writer's count follows its record)
+    const bool closer = w && s + n >= (u32)BS;
+    const u32 carry = closer ? s + n - (u32)BS : 0u;
+    if (__builtin_amdgcn_ballot_w64(closer) != 0) {
+      if (closer)
+        while (__hip_atomic_load(at<l32>(B.done) + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (u32)BS)
+          __builtin_amdgcn_s_sleep(1);
+      bool full[PVE_PB];
+      u32 pp[PVE_PB];
+#pragma unroll
+      for (int i = 0; i < PVE_PB; ++i) {
+        full[i] = i == 0 && closer;
+        pp[i] = p;
+      }
+      flush_full(B, full, pp, lane, __builtin_amdgcn_ballot_w64(carry != 0));
+      if (carry) {  // the rest of the claim starts the restarted bin (the copy's reads came first: one wave, in order)
+#pragma unroll
+        for (int j = 0; j < HB; ++j)
+          if ((u32)j >= w && (u32)j < n) at<l32>(B.bins)[p * (u32)BS + (u32)j - w] = rec[j];
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        at<l32>(B.done)[p] = carry;
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        at<l32>(B.cnt)[p] = carry;
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+    // advance: past the claimed values, past an unmatched doc, or stay (the bin was full: claim again)
+    if (n) {
+      if (w) v += (int)n;
+    } else if (v < e) {
+      v = end;
+    }
+  }
+}
+
 // one tile: returns the lane's docs counted in numDocsScanned. issue() sends the next tile's DMA: here, after the
 // admission loads have been waited for (PVE_ADMIT: a wait for them would otherwise also wait for that DMA)
 template <class Issue>
@@ -647,7 +783,10 @@ __device__ __forceinline__ u32 tile(const Bins& B, CS* sg, i64 wt, u32 img, int 
     if (x == 0x9e3779b9u) *at<l32>(B.next) = x;  // (keeps the records live)
     return scanned;
   }
-  if constexpr (PVE_H) {
+  if constexpr (PVE_H && PVE_HRUN) {
+    put_values_run(B, sg, wt, m, key, lane, vbuf, vb0, nxt);
+    return 0u;
+  } else if constexpr (PVE_H) {
     put_values(B, sg, wt, m, key, lane, vbuf, vb0, nxt);
     return 0u;  // (numDocsScanned: counted by the V stream's launch)
   } else {
