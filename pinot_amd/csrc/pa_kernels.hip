@@ -1616,6 +1616,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   }
 }
 
+template <int NT = kPartAggThreads>
 __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps, int ph, unsigned char* lds) {
   const DevAgg& H = q->aggs[q->hll_agg];
   const int lg = H.log2m;
@@ -1626,23 +1627,23 @@ __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps
   const bool first = q->h_first != 0;
   uint32_t* regw = (uint32_t*)lds;                      // KR << lg one-byte registers, as words
   uint32_t* cnt = (uint32_t*)(lds + ((size_t)KR << lg));  // first-value counts (h_first)
-  for (int64_t k = threadIdx.x; k < (KR << lg) / 4; k += kPartAggThreads) regw[k] = 0u;
+  for (int64_t k = threadIdx.x; k < (KR << lg) / 4; k += NT) regw[k] = 0u;
   if (first)
-    for (int64_t k = threadIdx.x; k < KR; k += kPartAggThreads) cnt[k] = 0u;
+    for (int64_t k = threadIdx.x; k < KR; k += NT) cnt[k] = 0u;
   __syncthreads();
   const int pv = q->pv;
   const uint64_t r0 = gp(ps.base)[pv + 1 + ph], r1 = gp(ps.base)[pv + 2 + ph];
   const AS1 uint32_t* recs = gp((const uint32_t*)ps.recs_h);
   const uint32_t rmask = (1u << lg) - 1u;
   constexpr int kB = 8;
-  const uint64_t span = (uint64_t)kB * kPartAggThreads;
+  const uint64_t span = (uint64_t)kB * NT;
   // chunked records (count-free emit): as part_agg_v_fast, the chunk entries one batch ahead
   const AS1 uint32_t* cix = ps.chunk_index_h ? gp(ps.chunk_index_h) : nullptr;
   const int csh = (int)ps.chunk_shift_h;
   const uint64_t cmask = cix ? (1ull << csh) - 1ull : 0ull;
   const uint32_t ln = threadIdx.x & 63u, wofs = threadIdx.x & ~63u;
   auto load_cids = [&](uint64_t b) -> uint32_t {
-    const uint64_t ri = b + (uint64_t)ln * kPartAggThreads + wofs;
+    const uint64_t ri = b + (uint64_t)ln * NT + wofs;
     return (ln < (uint32_t)kB && ri < r1) ? cix[ri >> csh] : 0u;
   };
   uint32_t cidv = cix ? load_cids(r0) : 0u;
@@ -1656,7 +1657,7 @@ __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps
     bool ok[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
-      const uint64_t ri = b0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
+      const uint64_t ri = b0 + (uint64_t)j * NT + threadIdx.x;
       const uint64_t pi = cix ? ((uint64_t)(cid[j] & 0x0fffffffu) << csh) | (ri & cmask) : ri;
       ok[j] = ri < r1 && (!cix || (uint32_t)(ri & cmask) < (((cid[j] >> 28) + 1u) << ps.chunk_bin_shift_h));
       pa[j] = ok[j] ? pi : 0ull;
@@ -1710,9 +1711,9 @@ __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps
   // the partition's registers (16-byte stores: 2^lg >= 16 bytes per key) and, without a V stream, its counts
   AS1 u32x4* g = (AS1 u32x4*)(H.acc_hll + ((size_t)kbase << lg));
   const u32x4* l = (const u32x4*)lds;
-  for (int64_t i = threadIdx.x; i < (nk << lg) / 16; i += kPartAggThreads) g[i] = l[i];
+  for (int64_t i = threadIdx.x; i < (nk << lg) / 16; i += NT) g[i] = l[i];
   if (first)
-    for (int64_t lk = threadIdx.x; lk < nk; lk += kPartAggThreads) gp(q->count)[kbase + lk] = cnt[lk];
+    for (int64_t lk = threadIdx.x; lk < nk; lk += NT) gp(q->count)[kbase + lk] = cnt[lk];
 }
 
 template <int VK>
@@ -1724,6 +1725,21 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
   } else {
     part_agg_h(q, ps, (int)blockIdx.x - q->pv, (unsigned char*)smem);
   }
+}
+
+// H partitions alone, 16 waves per workgroup: a partition's registers fill the LDS (one workgroup per CU), and with 8
+// waves each wave's record loads and LDS round trips sat exposed (the V variants' registers do not fit 16 waves)
+constexpr int kPartAggHThreads = 1024;
+__global__ void __launch_bounds__(kPartAggHThreads) part_agg_h_kernel(const DevQuery* __restrict__ q, PartScratch ps) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  part_agg_h<kPartAggHThreads>(q, ps, (int)blockIdx.x, (unsigned char*)smem);
+}
+static bool part_agg_h_split() {
+  static const bool on = [] {
+    const char* e = std::getenv("PA_PASSC_H_SPLIT");  // (measurement: 0 = H partitions in the V launch, 8 waves)
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
 }
 
 template <int VK>
@@ -1747,12 +1763,23 @@ hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G,
 }
 
 hipError_t set_part_agg_lds_limit(int vk, int lds_bytes) {
+  hipError_t e = hipFuncSetAttribute((const void*)part_agg_h_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  if (e != hipSuccess) return e;
   return hipFuncSetAttribute(part_agg_variant(vk), hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
 }
 
-hipError_t launch_part_agg(int vk, const DevQuery* q, const PartScratch& ps, int P, int lds_bytes, hipStream_t s) {
+// pv: the V partitions (workgroups [0, pv) of the launch); the H partitions [pv, P) go to their own launch
+hipError_t launch_part_agg(int vk, const DevQuery* q, const PartScratch& ps, int P, int pv, int lds_bytes,
+                           hipStream_t s) {
   void* args[] = {(void*)&q, (void*)&ps};
-  return hipLaunchKernel(part_agg_variant(vk), dim3(P), dim3(kPartAggThreads), args, (size_t)lds_bytes, s);
+  if (!part_agg_h_split() || pv >= P)
+    return hipLaunchKernel(part_agg_variant(vk), dim3(P), dim3(kPartAggThreads), args, (size_t)lds_bytes, s);
+  if (pv > 0) {
+    hipError_t e = hipLaunchKernel(part_agg_variant(vk), dim3(pv), dim3(kPartAggThreads), args, (size_t)lds_bytes, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipLaunchKernel((const void*)part_agg_h_kernel, dim3(P - pv), dim3(kPartAggHThreads), args, (size_t)lds_bytes,
+                         s);
 }
 
 static int grid_for(int64_t n, int block) {
