@@ -40,6 +40,7 @@ SETTINGS = [
     ("ring3_w8_nd16", {"PA_GDL_RING": "3", "PA_GDL_W": "8", "PA_GDL_ND": "16"}),
     ("ring3_w16_nd8", {"PA_GDL_RING": "3", "PA_GDL_W": "16", "PA_GDL_ND": "8"}),
     ("ring3_rr1", {"PA_GDL_RING": "3", "PA_GDL_RR": "1"}),
+    ("default_b", {}),
 ]
 KNOBS = ("PA_GDL_W", "PA_GDL_ND", "PA_GDL_RS", "PA_GDL_DBG", "PA_GDL_RR", "PA_GDL_RING")
 
