@@ -270,7 +270,7 @@ int pa_query_scan(pa_query* q, void* stream) {
       }
     }
     PA_HIP(launch_part_agg(q->part_vk, (const DevQuery*)q->dq.p, ps, q->pvh.fn ? q->hq.num_parts : q->hq.pv,
-                           q->hq.pv, q->part_lds_c, st));
+                           q->hq.pv, q->hq.v_fmt <= V_FMT_ID, q->part_lds_c, st));
     return PA_OK;
   }
   if (q->partitioned) {  // count pass, range offsets, emit pass into the partitions, per-partition aggregation
@@ -289,7 +289,8 @@ int pa_query_scan(pa_query* q, void* stream) {
     if (q->split_emit)
       PA_HIP(launch_scan(q->emit_h_strat, q->steps, 0, q->grid, q->emit_h_lds, (const DevQuery*)q->dq_h.p,
                          (const DevSeg*)q->dsegs.p, plans, ps, st));
-    PA_HIP(launch_part_agg(q->part_vk, (const DevQuery*)q->dq.p, ps, q->hq.num_parts, q->hq.pv, q->part_lds_c, st));
+    PA_HIP(launch_part_agg(q->part_vk, (const DevQuery*)q->dq.p, ps, q->hq.num_parts, q->hq.pv, q->hq.v_fmt <= V_FMT_ID,
+                           q->part_lds_c, st));
     PA_HIP(hipEventRecord(a->last, st));
     a->last_stream = st;
     a->used = true;

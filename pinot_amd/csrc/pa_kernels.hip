@@ -1418,7 +1418,7 @@ __device__ void part_agg_v(const DevQuery* __restrict__ q, const PartScratch& ps
 // read once into registers, the record loop is straight-line. V_FMT_ID records with value ids in value order keep
 // MIN/MAX as 32-bit ids (the value is looked up once per key at the store), so the per-record dictionary gather is
 // only needed by SUM.
-template <int VK>
+template <int VK, int NT = kPartAggThreads>
 __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratch& ps, int p, unsigned char* lds) {
   constexpr int SK = VK & 3;
   constexpr bool MN = (VK & 4) != 0, MX = (VK & 8) != 0;
@@ -1435,7 +1435,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   const uint32_t off_mx = MX ? (uint32_t)q->aggs[amx].lds_off : 0u;
   const bool dbl_mn = MN && q->aggs[amn].src == SRC_DOUBLE, dbl_mx = MX && q->aggs[amx].src == SRC_DOUBLE;
   lds_u32_t* cnt = lds_ptr(lds);
-  for (int64_t k = threadIdx.x; k < KR; k += kPartAggThreads) {
+  for (int64_t k = threadIdx.x; k < KR; k += NT) {
     cnt[k] = 0u;
     if (SK) {
       ((lds_u64_t*)lds_ptr(lds + off_s))[k] = 0ull;
@@ -1461,7 +1461,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   const bool aff = q->v_affine != 0;
   const int64_t vbase = q->v_base, vstep = q->v_step;
   constexpr int kB = 16;  // records per thread in flight
-  const uint64_t span = (uint64_t)kB * kPartAggThreads;
+  const uint64_t span = (uint64_t)kB * NT;
   // chunked records (count-free emit): the chunk entries of a batch are loaded one batch ahead, so a record load never
   // waits for its entry load (vector loads: a scalar load's wait would also wait for the LDS atomics in flight). A
   // wave's 64 records of one slot j lie in one chunk (chunks are >= 64 records, partition bases whole chunks), so
@@ -1471,7 +1471,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   const uint64_t cmask = cix ? (1ull << csh) - 1ull : 0ull;
   const uint32_t ln = threadIdx.x & 63u, wofs = threadIdx.x & ~63u;
   auto load_cids = [&](uint64_t b) -> uint32_t {
-    const uint64_t ri = b + (uint64_t)ln * kPartAggThreads + wofs;
+    const uint64_t ri = b + (uint64_t)ln * NT + wofs;
     return (ln < (uint32_t)kB && ri < r1) ? cix[ri >> csh] : 0u;
   };
   // A batch = kB records per thread. issue(): addresses (the chunk entries were loaded a batch ago), then the loads back
@@ -1492,7 +1492,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
     bool ok[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
-      const uint64_t ri = b0 + (uint64_t)j * kPartAggThreads + threadIdx.x;
+      const uint64_t ri = b0 + (uint64_t)j * NT + threadIdx.x;
       const uint64_t pi = cix ? ((uint64_t)(cid[j] & 0x0fffffffu) << csh) | (ri & cmask) : ri;
       // (a partition's last chunk per workgroup holds (cid >> 28) + 1 bins)
       ok[j] = ri < r1 && (!cix || (uint32_t)(ri & cmask) < (((cid[j] >> 28) + 1u) << ps.chunk_bin_shift));
@@ -1568,7 +1568,12 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
     }
   };
   Batch X, Y;
-  if (r0 < r1) {
+  if constexpr (NT > kPartAggThreads) {  // 16 waves hide the loads themselves: one register batch
+    for (uint64_t b0 = r0; b0 < r1; b0 += span) {
+      issue(b0, X);
+      process(X);
+    }
+  } else if (r0 < r1) {
     issue(r0, X);
     for (uint64_t b0 = r0;; b0 += 2 * span) {
       const bool more = b0 + span < r1;
@@ -1587,7 +1592,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   AS1 int64_t* gs = SK ? gp(q->aggs[as].acc_i64) : nullptr;
   AS1 int64_t* gmn = MN ? gp(q->aggs[amn].acc_i64) : nullptr;
   AS1 int64_t* gmx = MX ? gp(q->aggs[amx].acc_i64) : nullptr;
-  for (int64_t lk = threadIdx.x; lk < nk; lk += kPartAggThreads) {
+  for (int64_t lk = threadIdx.x; lk < nk; lk += NT) {
     const int64_t k = kbase + lk;
     const uint32_t c = cnt[lk];
     gc[k] = c;
@@ -1734,6 +1739,30 @@ __global__ void __launch_bounds__(kPartAggHThreads) part_agg_h_kernel(const DevQ
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   part_agg_h<kPartAggHThreads>(q, ps, (int)blockIdx.x, (unsigned char*)smem);
 }
+// V partitions at 16 waves per workgroup, one register batch per wave: for one-word records (configs[2]: pass C 505 ->
+// 364 us, the all-docs line 1.185 -> 1.069 ms); 3-word raw-value records stay at 8 waves with two batches (configs[4]:
+// 775 vs 735 us). PA_PASSC_V16=0 / 1 forces it (measurement)
+template <int VK>
+__global__ void __launch_bounds__(kPartAggHThreads) part_agg_v16_kernel(const DevQuery* __restrict__ q, PartScratch ps) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  part_agg_v_fast<VK, kPartAggHThreads>(q, ps, (int)blockIdx.x, (unsigned char*)smem);
+}
+static bool part_agg_v16(bool one_word) {
+  static const int force = [] {
+    const char* e = std::getenv("PA_PASSC_V16");
+    return e == nullptr ? -1 : (std::atoi(e) != 0 ? 1 : 0);
+  }();
+  return force < 0 ? one_word : force != 0;
+}
+static const void* part_agg_v16_variant(int vk) {
+  switch (vk) {
+#define PA_VK(c) case c: return (const void*)part_agg_v16_kernel<c>;
+    PA_VK(0) PA_VK(1) PA_VK(2) PA_VK(3) PA_VK(4) PA_VK(5) PA_VK(6) PA_VK(7)
+    PA_VK(8) PA_VK(9) PA_VK(10) PA_VK(11) PA_VK(12) PA_VK(13) PA_VK(14) PA_VK(15)
+#undef PA_VK
+    default: return nullptr;
+  }
+}
 static bool part_agg_h_split() {
   static const bool on = [] {
     const char* e = std::getenv("PA_PASSC_H_SPLIT");  // (measurement: 0 = H partitions in the V launch, 8 waves)
@@ -1765,19 +1794,28 @@ hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G,
 hipError_t set_part_agg_lds_limit(int vk, int lds_bytes) {
   hipError_t e = hipFuncSetAttribute((const void*)part_agg_h_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
   if (e != hipSuccess) return e;
+  if (const void* f = part_agg_v16_variant(vk)) {
+    e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    if (e != hipSuccess) return e;
+  }
   return hipFuncSetAttribute(part_agg_variant(vk), hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
 }
 
-// pv: the V partitions (workgroups [0, pv) of the launch); the H partitions [pv, P) go to their own launch
-hipError_t launch_part_agg(int vk, const DevQuery* q, const PartScratch& ps, int P, int pv, int lds_bytes,
-                           hipStream_t s) {
+// pv: the V partitions (workgroups [0, pv) of the launch); the H partitions [pv, P) go to their own launch. one_word:
+// the V records are one word (key offset | value id)
+hipError_t launch_part_agg(int vk, const DevQuery* q, const PartScratch& ps, int P, int pv, bool one_word,
+                           int lds_bytes, hipStream_t s) {
   void* args[] = {(void*)&q, (void*)&ps};
-  if (!part_agg_h_split() || pv >= P)
+  const bool v16 = part_agg_v16(one_word) && part_agg_v16_variant(vk) != nullptr;
+  if (!part_agg_h_split() || (pv >= P && !v16))
     return hipLaunchKernel(part_agg_variant(vk), dim3(P), dim3(kPartAggThreads), args, (size_t)lds_bytes, s);
   if (pv > 0) {
-    hipError_t e = hipLaunchKernel(part_agg_variant(vk), dim3(pv), dim3(kPartAggThreads), args, (size_t)lds_bytes, s);
+    hipError_t e = v16 ? hipLaunchKernel(part_agg_v16_variant(vk), dim3(pv), dim3(kPartAggHThreads), args,
+                                         (size_t)lds_bytes, s)
+                       : hipLaunchKernel(part_agg_variant(vk), dim3(pv), dim3(kPartAggThreads), args, (size_t)lds_bytes, s);
     if (e != hipSuccess) return e;
   }
+  if (pv >= P) return hipSuccess;
   return hipLaunchKernel((const void*)part_agg_h_kernel, dim3(P - pv), dim3(kPartAggHThreads), args, (size_t)lds_bytes,
                          s);
 }

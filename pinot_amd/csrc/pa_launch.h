@@ -100,8 +100,8 @@ hipError_t launch_gather(const void* src, int esize, int64_t per, const int64_t*
 hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G, int k, hipStream_t s);
 // vk: the pass-C variant of the V stream (vk_code / kVkGeneric)
 hipError_t set_part_agg_lds_limit(int vk, int lds_bytes);
-hipError_t launch_part_agg(int vk, const DevQuery* q, const PartScratch& ps, int P, int pv, int lds_bytes,
-                           hipStream_t s);
+hipError_t launch_part_agg(int vk, const DevQuery* q, const PartScratch& ps, int P, int pv, bool one_word,
+                           int lds_bytes, hipStream_t s);
 // Cross-GPU merge of hashed key spaces (pa_merge.hip): a row is every per-key section's elements of one slot
 enum RowOp : int32_t { ROW_ADD_U64 = 0, ROW_ADD_F64 = 1, ROW_MIN_I64 = 2, ROW_MAX_I64 = 3, ROW_MAX_U8 = 4, ROW_KEY = 5 };
 constexpr int kMaxRowSecs = PA_MAX_AGGS + 2;
