@@ -274,9 +274,14 @@ __device__ __forceinline__ void walk_keys(const DevQuery* __restrict__ q, const 
 
 // G: the bitmap is the segment's admit bitmap in HBM (zeroed by the host; key spaces beyond kWalkMaxWords * 32 keys),
 // else an LDS copy written out at the end.
+// tlog: log2 of the replay's first-lane table (LDS words after the bitmap; 0: none). A step's candidate lanes take
+// atomicMin(lane) on their key's slot: a lane whose slot holds a lane with the same key knows the key's first lane (it
+// or a lower one) with no compare against the other lanes; only when the slot's lane has another key (two keys in one
+// slot) do the candidates compare against every candidate lane.
 template <bool G>
 __global__ void __launch_bounds__(kWalkThreads) limit_walk_kernel(const DevQuery* __restrict__ q,
-                                                                   const DevSeg* __restrict__ segs, int64_t words) {
+                                                                   const DevSeg* __restrict__ segs, int64_t words,
+                                                                   int tlog) {
   extern __shared__ uint32_t lds_seen[];
   __shared__ uint32_t round_new[2];  // by round parity: a round resets its counter while the last one may be read
   __shared__ int64_t relay_cnt;      // the replay's running count of distinct keys, step to step
@@ -288,6 +293,8 @@ __global__ void __launch_bounds__(kWalkThreads) limit_walk_kernel(const DevQuery
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   if (!G)
     for (int64_t w = tid; w < words; w += kWalkThreads) seen[w] = 0u;
+  uint32_t* tab = lds_seen + (G ? 0 : words);
+  for (int w = tid; w < (tlog ? 1 << tlog : 0); w += kWalkThreads) tab[w] = 0xffffffffu;
   const int64_t L = q->num_groups_limit;
   const int64_t nd = seg->num_docs;
   int64_t cnt = 0;  // distinct keys before the current round
@@ -345,12 +352,27 @@ __global__ void __launch_bounds__(kWalkThreads) limit_walk_kernel(const DevQuery
                     !((__hip_atomic_load(seen + (k0 >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (k0 & 31u)) & 1u);
         // a key new to the bitmap counts at its first lane only
         uint64_t cm = __ballot(cand);
-        bool dup = false;
-        while (cm) {
-          const int j = __builtin_ctzll(cm);
-          cm &= cm - 1;
-          const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)k0, j);
-          dup |= j < lane && kj == k0;
+        bool dup = false, unres = cand;
+        if (tlog) {
+          const uint32_t slot = (k0 * 0x9e3779b1u) >> (32 - tlog);
+          if (cand) atomicMin(tab + slot, (uint32_t)lane);
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (one wave: its LDS operations run in order)
+          const uint32_t w = cand ? tab[slot] : 0u;
+          const uint32_t kw = (uint32_t)__shfl((int)k0, (int)w, kWave);
+          unres = cand && kw != k0;
+          dup = cand && kw == k0 && w != (uint32_t)lane;
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          if (cand) tab[slot] = 0xffffffffu;
+        }
+        if (__ballot(unres) != 0) {
+          bool d2 = false;
+          while (cm) {
+            const int j = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)k0, j);
+            d2 |= j < lane && kj == k0;
+          }
+          if (unres) dup = d2;
         }
         const bool nw = cand && !dup;
         const uint64_t nm = __ballot(nw);
@@ -527,15 +549,33 @@ hipError_t launch_limit_walk(const DevQuery* q, const DevSeg* segs, int nseg, in
     limit_walk_mv_kernel<<<nseg, kWalkThreads, lds, s>>>(q, segs, words);
     return hipGetLastError();
   }
+  // the replay's first-lane table: up to 4096 words in what the bitmap leaves of the LDS (PA_WALK_TAB=0: none,
+  // measurement)
+  static const bool use_tab = [] {
+    const char* e = std::getenv("PA_WALK_TAB");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  auto tlog_for = [&](size_t used) {
+    int t = 0;
+    if (use_tab)
+      for (int l = 12; l >= 6 && !t; --l)
+        if (used + ((size_t)4 << l) + 64 <= (size_t)kWalkMaxWords * 4 + 3840) t = l;
+    return t;
+  };
   if (words > kWalkMaxWords) {
-    limit_walk_kernel<true><<<nseg, kWalkThreads, 0, s>>>(q, segs, words);
+    const int tl = tlog_for(0);
+    hipError_t e = hipFuncSetAttribute((const void*)limit_walk_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)((size_t)4 << tl));
+    if (e != hipSuccess) return e;
+    limit_walk_kernel<true><<<nseg, kWalkThreads, tl ? (size_t)4 << tl : 0, s>>>(q, segs, words, tl);
     return hipGetLastError();
   }
-  const size_t lds = (size_t)words * 4;
+  const int tl = tlog_for((size_t)words * 4);
+  const size_t lds = (size_t)words * 4 + (tl ? (size_t)4 << tl : 0);
   hipError_t e = hipFuncSetAttribute((const void*)limit_walk_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
-  limit_walk_kernel<false><<<nseg, kWalkThreads, lds, s>>>(q, segs, words);
+  limit_walk_kernel<false><<<nseg, kWalkThreads, lds, s>>>(q, segs, words, tl);
   return hipGetLastError();
 }
 
@@ -1621,7 +1661,7 @@ __device__ void part_agg_v_fast(const DevQuery* __restrict__ q, const PartScratc
   }
 }
 
-template <int NT = kPartAggThreads>
+template <int NT = kPartAggThreads, int KB = 8>
 __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps, int ph, unsigned char* lds) {
   const DevAgg& H = q->aggs[q->hll_agg];
   const int lg = H.log2m;
@@ -1640,7 +1680,7 @@ __device__ void part_agg_h(const DevQuery* __restrict__ q, const PartScratch& ps
   const uint64_t r0 = gp(ps.base)[pv + 1 + ph], r1 = gp(ps.base)[pv + 2 + ph];
   const AS1 uint32_t* recs = gp((const uint32_t*)ps.recs_h);
   const uint32_t rmask = (1u << lg) - 1u;
-  constexpr int kB = 8;
+  constexpr int kB = KB;
   const uint64_t span = (uint64_t)kB * NT;
   // chunked records (count-free emit): as part_agg_v_fast, the chunk entries one batch ahead
   const AS1 uint32_t* cix = ps.chunk_index_h ? gp(ps.chunk_index_h) : nullptr;
@@ -1735,9 +1775,17 @@ __global__ void __launch_bounds__(kPartAggThreads) part_agg_kernel(const DevQuer
 // H partitions alone, 16 waves per workgroup: a partition's registers fill the LDS (one workgroup per CU), and with 8
 // waves each wave's record loads and LDS round trips sat exposed (the V variants' registers do not fit 16 waves)
 constexpr int kPartAggHThreads = 1024;
+template <int KB>
 __global__ void __launch_bounds__(kPartAggHThreads) part_agg_h_kernel(const DevQuery* __restrict__ q, PartScratch ps) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  part_agg_h<kPartAggHThreads>(q, ps, (int)blockIdx.x, (unsigned char*)smem);
+  part_agg_h<kPartAggHThreads, KB>(q, ps, (int)blockIdx.x, (unsigned char*)smem);
+}
+static const void* part_agg_h_fn() {  // 16 records per thread in flight (8: 990 vs 960 us on configs[4]; PA_PASSC_HKB)
+  static const bool b16 = [] {
+    const char* e = std::getenv("PA_PASSC_HKB");
+    return e == nullptr || std::atoi(e) != 8;
+  }();
+  return b16 ? (const void*)part_agg_h_kernel<16> : (const void*)part_agg_h_kernel<8>;
 }
 // V partitions at 16 waves per workgroup, one register batch per wave: for one-word records (configs[2]: pass C 505 ->
 // 364 us, the all-docs line 1.185 -> 1.069 ms); 3-word raw-value records stay at 8 waves with two batches (configs[4]:
@@ -1792,7 +1840,7 @@ hipError_t launch_part_offsets(const DevQuery* hq, const PartScratch& ps, int G,
 }
 
 hipError_t set_part_agg_lds_limit(int vk, int lds_bytes) {
-  hipError_t e = hipFuncSetAttribute((const void*)part_agg_h_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  hipError_t e = hipFuncSetAttribute(part_agg_h_fn(), hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
   if (e != hipSuccess) return e;
   if (const void* f = part_agg_v16_variant(vk)) {
     e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
@@ -1816,8 +1864,7 @@ hipError_t launch_part_agg(int vk, const DevQuery* q, const PartScratch& ps, int
     if (e != hipSuccess) return e;
   }
   if (pv >= P) return hipSuccess;
-  return hipLaunchKernel((const void*)part_agg_h_kernel, dim3(P - pv), dim3(kPartAggHThreads), args, (size_t)lds_bytes,
-                         s);
+  return hipLaunchKernel(part_agg_h_fn(), dim3(P - pv), dim3(kPartAggHThreads), args, (size_t)lds_bytes, s);
 }
 
 static int grid_for(int64_t n, int block) {

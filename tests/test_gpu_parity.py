@@ -553,6 +553,19 @@ def test_num_groups_limit_walk_every_strategy(flags):
     assert got.num_groups_limit_reached
 
 
+@pytest.mark.parametrize("limit", [5, 50, 119])
+def test_num_groups_limit_walk_small_key_space(limit):
+    """A key space of 120 keys (10 x 12) under a binding limit: nearly every 64-doc replay step of the walk holds the same
+    key in several lanes (the replay's first-lane table resolves them; two keys in one table slot fall back to comparing
+    every lane); same first-seen groups as the oracle on both trimming paths."""
+    cols = {"k1": ("INT", 10), "k2": ("LONG", 12), "m": ("LONG", 500)}
+    segs = [make_segment(760 + i, n, cols) for i, n in enumerate((20000, 3001))]
+    for flags, mode in LIMIT_PATHS:
+        got, exp = _limit_run("SELECT k1, k2, COUNT(*), SUM(m) FROM t GROUP BY k1, k2 LIMIT 100000000 "
+                              "OPTION(numGroupsLimit=%d)" % limit, segs, mode, flags=flags)
+        assert got.num_groups_limit_reached
+
+
 def test_num_groups_limit_walk_hbm_bitmap():
     """Key spaces beyond the walk's LDS bitmap (1.28M keys: 1500 x 1000 here) keep the admitted-key bitmap in HBM
     (limit_walk_kernel<true>); same first-seen groups as the oracle."""
