@@ -212,8 +212,10 @@ def oracle_check(q, gsegs, host_segments, sptr):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # (20 warmup steps, ~10 ms of scans: with 3 the first timed launches still ran at the clocks of the idle setup
+    # phase, ~4 % slower than the same plan measured warm by tools/sweep.py)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--segments", type=int, default=100, help="segments per GPU")
     ap.add_argument("--docs", type=int, default=10_000_000, help="docs per segment")
     ap.add_argument("--cpu-sample", type=int, default=16, help="segments in the CPU baseline sample (0 = skip)")

@@ -437,16 +437,19 @@ __device__ __forceinline__ uint32_t walk_mv_key(const DevQuery* __restrict__ q, 
 }
 
 __global__ void __launch_bounds__(kWalkThreads) limit_walk_mv_kernel(const DevQuery* __restrict__ q,
-                                                                      const DevSeg* __restrict__ segs, int64_t words) {
+                                                                      const DevSeg* __restrict__ segs, int64_t words,
+                                                                      int tlog) {
   extern __shared__ uint32_t lds_walk[];
   __shared__ uint32_t round_new[2];
   uint32_t* seen = lds_walk;
   uint32_t* snap = lds_walk + words;
+  uint32_t* tab = lds_walk + 2 * words;  // the replay's first-lane table (as limit_walk_kernel; tlog 0: none)
   const DevSeg* seg = segs + blockIdx.x;
   uint32_t* adm = (uint32_t*)seg->admit;
   if (adm == nullptr) return;  // (workgroup-uniform)
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   for (int64_t w = tid; w < words; w += kWalkThreads) seen[w] = 0u;
+  for (int w = tid; w < (tlog ? 1 << tlog : 0); w += kWalkThreads) tab[w] = 0xffffffffu;
   const int64_t L = q->num_groups_limit;
   const int64_t nd = seg->num_docs;
   int64_t cnt = 0;
@@ -508,12 +511,27 @@ __global__ void __launch_bounds__(kWalkThreads) limit_walk_mv_kernel(const DevQu
           const bool cand = act && !((seen[k0 >> 5] >> (k0 & 31u)) & 1u);
           // a key new to the bitmap counts at its first record only
           uint64_t cm = __ballot(cand);
-          bool dup = false;
-          while (cm) {
-            const int j = __builtin_ctzll(cm);
-            cm &= cm - 1;
-            const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)k0, j);
-            dup |= j < lane && kj == k0;
+          bool dup = false, unres = cand;
+          if (tlog) {
+            const uint32_t slot = (k0 * 0x9e3779b1u) >> (32 - tlog);
+            if (cand) atomicMin(tab + slot, (uint32_t)lane);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            const uint32_t w = cand ? tab[slot] : 0u;
+            const uint32_t kw = (uint32_t)__shfl((int)k0, (int)w, kWave);
+            unres = cand && kw != k0;
+            dup = cand && kw == k0 && w != (uint32_t)lane;
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            if (cand) tab[slot] = 0xffffffffu;
+          }
+          if (__ballot(unres) != 0) {
+            bool d2 = false;
+            while (cm) {
+              const int j = __builtin_ctzll(cm);
+              cm &= cm - 1;
+              const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)k0, j);
+              d2 |= j < lane && kj == k0;
+            }
+            if (unres) dup = d2;
           }
           const bool nw = cand && !dup;
           const uint64_t nm = __ballot(nw);
@@ -541,14 +559,6 @@ __global__ void __launch_bounds__(kWalkThreads) limit_walk_mv_kernel(const DevQu
 }
 
 hipError_t launch_limit_walk(const DevQuery* q, const DevSeg* segs, int nseg, int64_t words, bool mv, hipStream_t s) {
-  if (mv) {  // (the planner keeps 2 * words within kWalkMaxWords)
-    const size_t lds = (size_t)words * 8;
-    hipError_t e = hipFuncSetAttribute((const void*)limit_walk_mv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
-    if (e != hipSuccess) return e;
-    limit_walk_mv_kernel<<<nseg, kWalkThreads, lds, s>>>(q, segs, words);
-    return hipGetLastError();
-  }
   // the replay's first-lane table: up to 4096 words in what the bitmap leaves of the LDS (PA_WALK_TAB=0: none,
   // measurement)
   static const bool use_tab = [] {
@@ -562,6 +572,15 @@ hipError_t launch_limit_walk(const DevQuery* q, const DevSeg* segs, int nseg, in
         if (used + ((size_t)4 << l) + 64 <= (size_t)kWalkMaxWords * 4 + 3840) t = l;
     return t;
   };
+  if (mv) {  // (the planner keeps 2 * words within kWalkMaxWords)
+    const int tl = tlog_for((size_t)words * 8);
+    const size_t lds = (size_t)words * 8 + (tl ? (size_t)4 << tl : 0);
+    hipError_t e = hipFuncSetAttribute((const void*)limit_walk_mv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    limit_walk_mv_kernel<<<nseg, kWalkThreads, lds, s>>>(q, segs, words, tl);
+    return hipGetLastError();
+  }
   if (words > kWalkMaxWords) {
     const int tl = tlog_for(0);
     hipError_t e = hipFuncSetAttribute((const void*)limit_walk_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,

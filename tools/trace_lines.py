@@ -9,7 +9,7 @@ import json
 import sys
 
 
-def main(trace, bench, out, prefix="gdl_jit", per_line=24):
+def main(trace, bench, out, prefix="gdl_jit", per_line=71):  # (bench.py defaults: 20 warmup + 50 steps + 1)
     per_line = int(per_line)
     rows = [r for r in csv.DictReader(open(trace)) if r["Kernel_Name"].startswith(prefix)]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
