@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--lines", default=None)
     ap.add_argument("--settings", default=None, help="comma-separated setting names")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--warm", type=int, default=0, help="untimed scans before the timed ones (clocks at steady state)")
     args = ap.parse_args()
     spec = importlib.util.spec_from_file_location("bench_main", os.path.join(ROOT, "bench.py"))
     B = importlib.util.module_from_spec(spec)
@@ -90,6 +91,8 @@ def main():
                 plan = ex.stats()["plan"]
                 ex.execute(sp)
                 torch.cuda.synchronize()
+                for _ in range(args.warm):
+                    ex.scan(sp)
                 ex.reset(sp)
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record(stream)
