@@ -219,7 +219,8 @@ def _bench():
     return _BENCH[0]
 
 
-def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None, cpu_sample=0, exec_stats=False):
+def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None, cpu_sample=0, exec_stats=False,
+        warm=0):
     import torch
     from pinot_amd import parse_sql
     from pinot_amd import _lib as L
@@ -256,6 +257,8 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
         for extra, tag in vs:
             ex = GpuQueryExecutor(parse_sql(sql), gsegs, flags=flags | extra | (L.PA_QF_NO_FILTER_STATS if exec_stats else 0))
             ex.execute(sp)
+            for _ in range(warm):  # (untimed: the clocks reach their steady state)
+                ex.scan(sp)
             torch.cuda.synchronize()
             ex.reset(sp)
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -341,6 +344,7 @@ def main():
     ap.add_argument("--segments", type=int, default=20)
     ap.add_argument("--docs", type=int, default=10_000_000)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--warm", type=int, default=0, help="untimed scans before each line's timed ones")
     ap.add_argument("--plan", default=None, help="only this plan name (e.g. all_docs)")
     ap.add_argument("--no-stepmajor", action="store_true", help="skip the forced step-major variants")
     ap.add_argument("--sweep-part", action="store_true",
@@ -359,7 +363,7 @@ def main():
     torch.cuda.set_device(0)
     for w in (WORKLOADS if args.workload == "all" else [args.workload]):
         run(w, args.segments, args.docs, args.reps, args.plan, args.no_stepmajor, variants, args.cpu_sample,
-            args.exec_stats)
+            args.exec_stats, args.warm)
 
 
 if __name__ == "__main__":
