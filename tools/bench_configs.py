@@ -196,6 +196,38 @@ WORKLOADS = {
 }
 
 
+CHECK_LINES = ("all_docs", "filtered_10pct", "default_limit")
+
+
+def oracle_check(ex, q, host_segs, sp):
+    """The full-size line's result (every segment of the run) against the oracle's server-level result of the same
+    segments, outside the timed region (--check; test infrastructure, as bench.py's oracle_check): keys, counts,
+    numDocsScanned, numGroupsLimitReached and every aggregation bit-exact (tests/test_gpu_configs.py _compare_arrays)."""
+    import numpy as np
+    import oracle
+    from pinot_amd import _lib as L
+    ex.execute(sp)
+    keys, counts, outs = ex.fetch_arrays(sp)
+    t0 = time.perf_counter()
+    exp = oracle.run_query_arrays(q, host_segs)
+    res = {"docs": int(sum(s.num_docs for s in host_segs)), "groups": int(len(exp["keys"])),
+           "oracle_s": round(time.perf_counter() - t0, 1)}
+    try:
+        assert int(L.lib().pa_query_matched_docs(ex.handle)) == exp["matched"], "numDocsScanned"
+        assert (int(L.lib().pa_query_num_groups_limit_reached(ex.handle)) > 0) == exp["limit_reached"], "limit"
+        np.testing.assert_array_equal(keys, exp["keys"])
+        np.testing.assert_array_equal(counts, exp["counts"])
+        for a, gi, oi in zip(q.aggregations, ex.agg_map, exp["amap"]):
+            if a.function != "COUNT":
+                got, want = outs[gi], exp["accs"][oi]
+                np.testing.assert_array_equal(got.reshape(want.shape), want, err_msg=a.function)
+        res["checked"] = True
+    except AssertionError as e:
+        res["checked"] = False
+        res["error"] = str(e)[:300]
+    return res
+
+
 def cpu_port_baseline(sql, host_segs):
     """bench.py's cpu_baseline (the C oracle port, one segment per thread) over the kept host segments."""
     import importlib.util
@@ -220,7 +252,7 @@ def _bench():
 
 
 def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None, cpu_sample=0, exec_stats=False,
-        warm=0):
+        warm=0, check=False):
     import torch
     from pinot_amd import parse_sql
     from pinot_amd import _lib as L
@@ -233,7 +265,7 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
         if cids is None:
             cids = {n: j for j, n in enumerate(sorted(seg.columns))}
         gsegs.append(GpuSegment(seg, column_ids=cids, device=0))
-        if len(host) < cpu_sample:
+        if check or len(host) < cpu_sample:
             host.append(seg)  # (kept whole for the CPU baseline)
             continue
         for c in seg.columns.values():  # HBM holds the data now; keep only the dictionaries
@@ -283,6 +315,9 @@ def run(workload, nseg, docs, reps, only=None, no_stepmajor=False, variants=None
             e2e_ms = (time.perf_counter() - t2) * 1e3 / 3
             st = ex.stats()
             extra = {}
+            if check and name in CHECK_LINES:
+                extra["check"] = oracle_check(ex, parse_sql(sql), host, sp)
+                log("%s %s%s: oracle check %s" % (workload, name, tag, extra["check"]))
             # roofline of the fused scan on the byte model every line shares (bench.algorithmic_bytes): staged columns
             # whole, columns read per surviving doc (and multi-value offsets / values) at 64-byte-sector granularity
             matched = int(L.lib().pa_query_matched_docs(ex.handle))
@@ -345,6 +380,8 @@ def main():
     ap.add_argument("--docs", type=int, default=10_000_000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--warm", type=int, default=0, help="untimed scans before each line's timed ones")
+    ap.add_argument("--check", action="store_true",
+                    help="keep every segment on the host and check the full-size results against the oracle")
     ap.add_argument("--plan", default=None, help="only this plan name (e.g. all_docs)")
     ap.add_argument("--no-stepmajor", action="store_true", help="skip the forced step-major variants")
     ap.add_argument("--sweep-part", action="store_true",
@@ -363,7 +400,7 @@ def main():
     torch.cuda.set_device(0)
     for w in (WORKLOADS if args.workload == "all" else [args.workload]):
         run(w, args.segments, args.docs, args.reps, args.plan, args.no_stepmajor, variants, args.cpu_sample,
-            args.exec_stats, args.warm)
+            args.exec_stats, args.warm, args.check)
 
 
 if __name__ == "__main__":
