@@ -10,5 +10,5 @@ import json
 for l in open('$out/$1.jsonl'):
     d=json.loads(l); print('$1', d['plan_name'], d['kernel_ms'], d['groups'], d.get('check'))"
 }
-run highcard "" && run star "" && run highcard_own "--plan all_docs"
+run ${1:-star} "${2:-}"
 echo all_ok
